@@ -1,0 +1,267 @@
+"""ORACLE -- CPU parity checker for the mplib_amd batched collide path.
+
+TEST INFRASTRUCTURE ONLY.  Only ``tests/``, ``__graft_entry__.smoke()`` and the
+``cpu_baseline`` leg of ``bench.py`` may import this package.  The shipped
+product (``mplib_amd``) never imports, links or executes anything under
+``oracle/``; it fails loudly when its HIP library is missing instead.
+
+* ``oracle/model.py``          -- independent URDF/SRDF/STL -> model restatement
+* ``oracle/collide_oracle.c``  -- C restatement of the FK + FCL/libccd MPR +
+                                  PlanningWorld pair loops (built into
+                                  ``oracle/build/liboracle.so`` by ``make -C oracle``)
+
+Parity status (see DESIGN.md section "Oracle"): the reference (KolinGuo/MPlib
+0.1.1) ships no golden vectors for this path and its third-party arithmetic
+(FCL 0.7.0, libccd 2.1, pinocchio 2.6.21, Eigen 3.4.0) is absent from this
+image, so the restatement is pinned by the reference's own known answers
+(examples/detect_collision.py:25,31), the Panda model facts in SURVEY.md 8(a),
+and -- for sin/cos -- bit-for-bit agreement with the host libm.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import model as M
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "build", "liboracle.so")
+_lib = None
+
+
+def build(force: bool = False) -> str:
+    """Compile the C restatement (gcc -O2 -ffp-contract=off)."""
+    src = os.path.join(_HERE, "collide_oracle.c")
+    if force or not os.path.exists(_LIB_PATH) or os.path.getmtime(_LIB_PATH) < os.path.getmtime(src):
+        subprocess.check_call(["make", "-s", "-C", _HERE])
+    return _LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        build()
+        _lib = ctypes.CDLL(_LIB_PATH)
+        _lib.orc_collide_batch.restype = ctypes.c_int
+        _lib.orc_fk_batch.restype = ctypes.c_int
+        _lib.orc_collide_pair.restype = ctypes.c_int
+    return _lib
+
+
+_IP = ctypes.POINTER(ctypes.c_int)
+_DP = ctypes.POINTER(ctypes.c_double)
+
+
+class _World(ctypes.Structure):
+    _fields_ = [
+        ("nj", ctypes.c_int), ("nq_pin", ctypes.c_int),
+        ("jtype", _IP), ("jparent", _IP), ("jidx_q", _IP),
+        ("jaxis", _DP), ("jplace", _DP),
+        ("n_user_joints", ctypes.c_int), ("user_joint", _IP),
+        ("nq_user", ctypes.c_int), ("qpos_template", _DP),
+        ("dof", ctypes.c_int), ("mg_index", _IP),
+        ("n_links", ctypes.c_int), ("link_parent", _IP), ("link_place", _DP),
+        ("n_geom", ctypes.c_int), ("geom_type", _IP), ("geom_vstart", _IP), ("geom_nv", _IP),
+        ("geom_param", _DP), ("geom_interior", _DP), ("verts", _DP),
+        ("n_obj", ctypes.c_int), ("obj_link", _IP), ("obj_geom", _IP), ("obj_origin", _DP),
+        ("n_att", ctypes.c_int), ("att_link", _IP), ("att_geom", _IP), ("att_pose", _DP),
+        ("n_scene", ctypes.c_int), ("scene_geom", _IP), ("scene_tf", _DP),
+        ("n_pairs", ctypes.c_int),
+        ("pa_kind", _IP), ("pa_idx", _IP), ("pb_kind", _IP), ("pb_idx", _IP), ("p_allowed", _IP),
+    ]
+
+
+class Stats(ctypes.Structure):
+    _fields_ = [("support_calls", ctypes.c_longlong), ("vertex_dots", ctypes.c_longlong),
+                ("refine_iters", ctypes.c_longlong), ("mpr_runs", ctypes.c_longlong)]
+
+
+def _se3_flat(T) -> List[float]:
+    return list(T[0]) + list(T[1])
+
+
+def pose7_to_se3(pose) -> tuple:
+    """``posevec_to_transform`` / CollisionObject(p, wxyz) (src/math_utils.cpp:12-18)."""
+    p = pose[:3]
+    w, x, y, z = pose[3:7]
+    return (M.quat_to_mat(float(w), float(x), float(y), float(z)), [float(v) for v in p])
+
+
+KIND_ROBOT, KIND_ATTACHED, KIND_SCENE = 0, 1, 2
+
+
+class OracleWorld:
+    """A PlanningWorld with one planned articulation, static scene objects,
+    attached bodies and an allowed-collision set, evaluated on the CPU.
+
+    Pair-table order follows ``PlanningWorldTpl::selfCollide`` then
+    ``collideWithOthers`` (src/planning_world.cpp:277-481); each pair keeps the
+    reference's (o1, o2) argument order for ``fcl::collide``.
+    """
+
+    def __init__(self, art: M.Articulation, scene: Sequence[Tuple[str, object, tuple]] = (),
+                 attached: Sequence[Tuple[str, int, object, tuple]] = (),
+                 allowed: Sequence[Tuple[str, str]] = ()):
+        self.art = art
+        self.scene = list(scene)          # (name, geom, SE3)
+        self.attached = list(attached)    # (name, user link index, geom, SE3 pose)
+        self.allowed = {frozenset(p) for p in allowed}
+        self._build()
+
+    # ------------------------------------------------------------------
+    def _geom_index(self, g, geoms, verts) -> int:
+        for i, gg in enumerate(geoms):
+            if gg is g:
+                return i
+        geoms.append(g)
+        return len(geoms) - 1
+
+    def _build(self):
+        art = self.art
+        pin = art.pin
+        geoms: List[object] = []
+        obj_geom = [self._geom_index(o.geom, geoms, None) for o in art.objects]
+        att_geom = [self._geom_index(a[2], geoms, None) for a in self.attached]
+        scene_geom = [self._geom_index(s[1], geoms, None) for s in self.scene]
+        gtype, gvstart, gnv, gparam, ginterior, verts = [], [], [], [], [], []
+        nverts = 0
+        for g in geoms:
+            if isinstance(g, M.ConvexGeom):
+                gtype.append(M.GEOM_CONVEX)
+                gvstart.append(nverts)
+                gnv.append(len(g.vertices))
+                nverts += len(g.vertices)
+                verts.append(np.asarray(g.vertices, dtype=np.float64).reshape(-1))
+                gparam += [0.0] * 4
+                ginterior += g.interior
+            elif isinstance(g, M.BoxGeom):
+                gtype.append(M.GEOM_BOX)
+                gvstart.append(0)
+                gnv.append(0)
+                gparam += [float(g.side[0]), float(g.side[1]), float(g.side[2]), 0.0]
+                ginterior += [0.0] * 3
+            else:
+                raise TypeError(f"oracle: unsupported geometry {type(g)}")
+        names = [o.link for o in art.objects]
+        pairs = []  # (ka, ia, kb, ib, name1, name2)
+        for a, b in art.pairs:
+            pairs.append((KIND_ROBOT, a, KIND_ROBOT, b, names[a], names[b]))
+        for k, att in enumerate(self.attached):
+            for i in range(len(art.objects)):
+                pairs.append((KIND_ATTACHED, k, KIND_ROBOT, i, names[i], att[0]))
+        for k in range(len(self.attached)):
+            for k2 in range(k):
+                pairs.append((KIND_ATTACHED, k, KIND_ATTACHED, k2, self.attached[k][0], self.attached[k2][0]))
+        self.n_self_pairs = len(pairs)
+        for s, sc in enumerate(self.scene):
+            for i in range(len(art.objects)):
+                pairs.append((KIND_ROBOT, i, KIND_SCENE, s, names[i], sc[0]))
+        for k, att in enumerate(self.attached):
+            for s, sc in enumerate(self.scene):
+                pairs.append((KIND_ATTACHED, k, KIND_SCENE, s, att[0], sc[0]))
+        self.pairs = pairs
+        self.W = max(1, (len(pairs) + 31) // 32)
+        allowed = [1 if frozenset((p[4], p[5])) in self.allowed else 0 for p in pairs]
+
+        nj = len(pin.joints) - 1
+        J = pin.joints[1:]
+        self._keep = []
+
+        def ia(x):
+            a = np.ascontiguousarray(np.asarray(x, dtype=np.int32).reshape(-1) if len(x) else np.zeros(1, np.int32))
+            self._keep.append(a)
+            return a.ctypes.data_as(_IP)
+
+        def da(x):
+            a = np.ascontiguousarray(np.asarray(x, dtype=np.float64).reshape(-1) if len(x) else np.zeros(1))
+            self._keep.append(a)
+            return a.ctypes.data_as(_DP)
+
+        mg = art.move_group_qpos_index()
+        w = _World()
+        w.nj = nj
+        w.nq_pin = pin.nq
+        w.jtype = ia([j.jtype for j in J])
+        w.jparent = ia([j.parent for j in J])
+        w.jidx_q = ia([j.idx_q for j in J])
+        w.jaxis = da([c for j in J for c in j.axis])
+        w.jplace = da([c for j in J for c in _se3_flat(j.placement)])
+        w.n_user_joints = len(art.user_joints)
+        w.user_joint = ia(art.user_joints)
+        w.nq_user = art.nv
+        w.qpos_template = da(art.current_qpos)
+        w.dof = len(mg)
+        w.mg_index = ia(mg)
+        frames = [pin.frames[f] for f in art.link_frames]
+        w.n_links = len(frames)
+        w.link_parent = ia([f.parent for f in frames])
+        w.link_place = da([c for f in frames for c in _se3_flat(f.placement)])
+        w.n_geom = len(geoms)
+        w.geom_type = ia(gtype)
+        w.geom_vstart = ia(gvstart)
+        w.geom_nv = ia(gnv)
+        w.geom_param = da(gparam)
+        w.geom_interior = da(ginterior)
+        w.verts = da(np.concatenate(verts) if verts else [])
+        w.n_obj = len(art.objects)
+        w.obj_link = ia(art.obj_user_link)
+        w.obj_geom = ia(obj_geom)
+        w.obj_origin = da([c for o in art.objects for c in _se3_flat(o.origin)])
+        w.n_att = len(self.attached)
+        w.att_link = ia([a[1] for a in self.attached])
+        w.att_geom = ia(att_geom)
+        w.att_pose = da([c for a in self.attached for c in _se3_flat(a[3])])
+        w.n_scene = len(self.scene)
+        w.scene_geom = ia(scene_geom)
+        w.scene_tf = da([c for s in self.scene for c in _se3_flat(s[2])])
+        w.n_pairs = len(pairs)
+        w.pa_kind = ia([p[0] for p in pairs])
+        w.pa_idx = ia([p[1] for p in pairs])
+        w.pb_kind = ia([p[2] for p in pairs])
+        w.pb_idx = ia([p[3] for p in pairs])
+        w.p_allowed = ia(allowed)
+        self._w = w
+        self.geoms = geoms
+        self.dof = len(mg)
+
+    # ------------------------------------------------------------------
+    def collide_batch(self, q: np.ndarray, nthreads: int = 1, want_stats: bool = False):
+        q = np.ascontiguousarray(q, dtype=np.float64).reshape(-1, self.dof)
+        n = q.shape[0]
+        flags = np.zeros(n, dtype=np.uint8)
+        masks = np.zeros((n, self.W), dtype=np.uint32)
+        st = Stats()
+        rc = lib().orc_collide_batch(ctypes.byref(self._w), q.ctypes.data_as(_DP), ctypes.c_long(n),
+                                     flags.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)),
+                                     masks.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)),
+                                     ctypes.c_int(self.W), ctypes.c_int(nthreads), ctypes.byref(st))
+        if rc != 0:
+            raise RuntimeError("orc_collide_batch failed")
+        if want_stats:
+            return flags, masks, {k: getattr(st, k) for k, _ in Stats._fields_}
+        return flags, masks
+
+    def fk_batch(self, q: np.ndarray):
+        q = np.ascontiguousarray(q, dtype=np.float64).reshape(-1, self.dof)
+        n = q.shape[0]
+        poses = np.zeros((n, self._w.n_links, 7))
+        objT = np.zeros((n, self._w.n_obj, 12))
+        rc = lib().orc_fk_batch(ctypes.byref(self._w), q.ctypes.data_as(_DP), ctypes.c_long(n),
+                                poses.ctypes.data_as(_DP), objT.ctypes.data_as(_DP))
+        if rc != 0:
+            raise RuntimeError("orc_fk_batch failed")
+        return poses, objT
+
+    def pair_names(self) -> List[Tuple[str, str]]:
+        return [(p[4], p[5]) for p in self.pairs]
+
+    def decode(self, mask_row) -> List[Tuple[str, str]]:
+        out = []
+        for p, pr in enumerate(self.pairs):
+            if (int(mask_row[p >> 5]) >> (p & 31)) & 1:
+                out.append((pr[4], pr[5]))
+        return out

@@ -1,0 +1,745 @@
+/*
+ * ORACLE (test infrastructure only) -- CPU restatement of MPlib's
+ * PlanningWorld::collide() hot path.  Only tests/, __graft_entry__.smoke()
+ * and bench.py's cpu_baseline leg may load this library; the shipped product
+ * (mplib_amd) never links or calls it.
+ *
+ * Built with gcc -O2 -ffp-contract=off (no fused multiply-add anywhere), like
+ * the reference (CMakeLists.txt:4-6: -O3, no -march => no FMA on x86-64).
+ * sin/cos come from the host libm, exactly as pinocchio's SINCOS does.
+ *
+ * Structure deliberately mirrors the reference and its third-party
+ * dependencies so the restatement can be audited line by line:
+ *   - qposUser2Pinocchio           src/pinocchio_model.cpp:499-525
+ *   - pinocchio::forwardKinematics [ext pinocchio 2.6.21 kinematics.hxx]
+ *       oMi[i] = oMi[parent] * (jointPlacements[i] * M_i(q))
+ *   - getLinkPose                  src/pinocchio_model.cpp:277-312
+ *   - ArticulatedModel::setQpos    src/articulated_model.cpp:101-127
+ *   - FCLModel::updateCollisionObjects src/fcl_model.cpp:139-148
+ *   - AttachedBody::getGlobalPose  src/attached_body.h:48-51
+ *   - fcl::collide -> GJKSolver_libccd::shapeIntersect -> GJKCollide
+ *       -> ccdMPRIntersect          [ext FCL 0.7.0 gjk_libccd-inl.h,
+ *                                    libccd 2.1 src/mpr.c, ccd/vec3.h, ccd/quat.h]
+ *   - PlanningWorld::selfCollide / collideWithOthers / filterCollisions
+ *                                  src/planning_world.cpp:265-481
+ * Eigen 3.4.0 conversions: quaternionbase_assign_impl (matrix->quat),
+ * QuaternionBase::toRotationMatrix (quat->matrix), lazy 3x3 products
+ * ((a0 b0 + a1 b1) + a2 b2).
+ *
+ * Parity status: the reference ships no golden vectors for this path
+ * (SURVEY.md section 4); this restatement is pinned by the two
+ * examples/detect_collision.py known answers and by the Panda model facts,
+ * and its sin/cos agree bit-for-bit with the host libm by construction.
+ */
+#include <float.h>
+#include <math.h>
+#include <pthread.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+typedef double real;
+#define CCD_EPS DBL_EPSILON
+#define CCD_REAL_MAX DBL_MAX
+
+/* ---------------------------------------------------------------- world */
+enum { GEOM_CONVEX = 0, GEOM_BOX = 1, GEOM_SPHERE = 2, GEOM_CAPSULE = 3, GEOM_CYLINDER = 4 };
+enum { JT_RX, JT_RY, JT_RZ, JT_RU, JT_PX, JT_PY, JT_PZ, JT_PU, JT_RUBX, JT_RUBY, JT_RUBZ, JT_RUBU };
+enum { KIND_ROBOT = 0, KIND_ATTACHED = 1, KIND_SCENE = 2 };
+
+typedef struct {
+    /* pinocchio joints 1..nj stored at [0..nj-1] */
+    int nj, nq_pin;
+    const int *jtype, *jparent, *jidx_q;
+    const double *jaxis, *jplace; /* [nj*3], [nj*12] R row-major + p */
+    /* user joints (setJointOrder) */
+    int n_user_joints;
+    const int *user_joint; /* pinocchio joint index (0 = universe) */
+    int nq_user;           /* length of the full user qpos (= nv) */
+    const double *qpos_template; /* current_qpos_ [nq_user] */
+    int dof;
+    const int *mg_index;   /* move-group dof -> user qpos slot [dof] */
+    /* user links (setLinkOrder) */
+    int n_links;
+    const int *link_parent;     /* frame.parent joint (0 = universe) */
+    const double *link_place;   /* [n_links*12] frame.placement */
+    /* geometry */
+    int n_geom;
+    const int *geom_type, *geom_vstart, *geom_nv;
+    const double *geom_param;    /* [n_geom*4] */
+    const double *geom_interior; /* [n_geom*3] */
+    const double *verts;         /* [*3] */
+    /* robot collision objects */
+    int n_obj;
+    const int *obj_link, *obj_geom;
+    const double *obj_origin; /* [n_obj*12] */
+    /* attached bodies */
+    int n_att;
+    const int *att_link, *att_geom;
+    const double *att_pose; /* [n_att*12] */
+    /* scene objects */
+    int n_scene;
+    const int *scene_geom;
+    const double *scene_tf; /* [n_scene*12] */
+    /* pair table */
+    int n_pairs;
+    const int *pa_kind, *pa_idx, *pb_kind, *pb_idx, *p_allowed;
+} orc_world;
+
+typedef struct {
+    long long support_calls;
+    long long vertex_dots;
+    long long refine_iters;
+    long long mpr_runs;
+} orc_stats;
+
+/* ----------------------------------------------------------- SE3 / Eigen */
+static void mat3_mul(const real *a, const real *b, real *out) {
+    real r[9];
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j)
+            r[3 * i + j] = (a[3 * i] * b[j] + a[3 * i + 1] * b[3 + j]) + a[3 * i + 2] * b[6 + j];
+    memcpy(out, r, sizeof r);
+}
+
+/* C = A * B for SE3 stored as R[9] row-major followed by p[3]. */
+static void se3_mul(const real *A, const real *B, real *C) {
+    real R[9], p[3];
+    mat3_mul(A, B, R);
+    for (int i = 0; i < 3; ++i)
+        p[i] = ((A[3 * i] * B[9] + A[3 * i + 1] * B[10]) + A[3 * i + 2] * B[11]) + A[9 + i];
+    memcpy(C, R, sizeof R);
+    memcpy(C + 9, p, sizeof p);
+}
+
+static void se3_identity(real *T) {
+    memset(T, 0, 12 * sizeof(real));
+    T[0] = T[4] = T[8] = 1.0;
+}
+
+/* Eigen QuaternionBase::toRotationMatrix; q = (w, x, y, z) */
+static void quat_to_mat(real w, real x, real y, real z, real *m) {
+    const real tx = 2.0 * x, ty = 2.0 * y, tz = 2.0 * z;
+    const real twx = tx * w, twy = ty * w, twz = tz * w;
+    const real txx = tx * x, txy = ty * x, txz = tz * x;
+    const real tyy = ty * y, tyz = tz * y, tzz = tz * z;
+    m[0] = 1.0 - (tyy + tzz); m[1] = txy - twz;         m[2] = txz + twy;
+    m[3] = txy + twz;         m[4] = 1.0 - (txx + tzz); m[5] = tyz - twx;
+    m[6] = txz - twy;         m[7] = tyz + twx;         m[8] = 1.0 - (txx + tyy);
+}
+
+/* Eigen quaternionbase_assign_impl<Matrix3,3,3>; out q = (w, x, y, z) */
+static void mat_to_quat(const real *m, real *q) {
+#define C(i, j) m[3 * (i) + (j)]
+    real t = (C(0, 0) + C(1, 1)) + C(2, 2);
+    real xyz[3];
+    if (t > 0.0) {
+        t = sqrt(t + 1.0);
+        q[0] = 0.5 * t;
+        t = 0.5 / t;
+        xyz[0] = (C(2, 1) - C(1, 2)) * t;
+        xyz[1] = (C(0, 2) - C(2, 0)) * t;
+        xyz[2] = (C(1, 0) - C(0, 1)) * t;
+    } else {
+        int i = 0;
+        if (C(1, 1) > C(0, 0)) i = 1;
+        if (C(2, 2) > C(i, i)) i = 2;
+        int j = (i + 1) % 3, k = (j + 1) % 3;
+        t = sqrt(((C(i, i) - C(j, j)) - C(k, k)) + 1.0);
+        xyz[i] = 0.5 * t;
+        t = 0.5 / t;
+        q[0] = (C(k, j) - C(j, k)) * t;
+        xyz[j] = (C(j, i) + C(i, j)) * t;
+        xyz[k] = (C(k, i) + C(i, k)) * t;
+    }
+    q[1] = xyz[0]; q[2] = xyz[1]; q[3] = xyz[2];
+#undef C
+}
+
+/* ------------------------------------------------------------ kinematics */
+/* pinocchio::toRotationMatrix(axis, cos, sin) [ext pinocchio 2.6.21 math/rotation.hpp] */
+static void axis_rot(const real *ax, real c, real s, real *R) {
+    real sa[3] = {s * ax[0], s * ax[1], s * ax[2]};
+    real c1 = 1.0 - c;
+    real ca[3] = {c1 * ax[0], c1 * ax[1], c1 * ax[2]};
+    real tmp;
+    tmp = ca[0] * ax[1]; R[1] = tmp - sa[2]; R[3] = tmp + sa[2];
+    tmp = ca[0] * ax[2]; R[2] = tmp + sa[1]; R[6] = tmp - sa[1];
+    tmp = ca[1] * ax[2]; R[5] = tmp - sa[0]; R[7] = tmp + sa[0];
+    R[0] = ca[0] * ax[0] + c; R[4] = ca[1] * ax[1] + c; R[8] = ca[2] * ax[2] + c;
+}
+
+/* joint motion M_i(q) as a plain SE3 (pinocchio JointModel*::calc) */
+static void joint_motion(int type, const real *axis, const real *qj, real *M) {
+    se3_identity(M);
+    real c, s;
+    switch (type) {
+    case JT_RX: case JT_RY: case JT_RZ: case JT_RU:
+        s = sin(qj[0]);
+        c = cos(qj[0]);
+        break;
+    case JT_RUBX: case JT_RUBY: case JT_RUBZ: case JT_RUBU:
+        c = qj[0];
+        s = qj[1];
+        break;
+    default:
+        c = s = 0.0;
+    }
+    switch (type) {
+    case JT_RX: case JT_RUBX:
+        M[4] = c; M[5] = -s; M[7] = s; M[8] = c; break;
+    case JT_RY: case JT_RUBY:
+        M[0] = c; M[2] = s; M[6] = -s; M[8] = c; break;
+    case JT_RZ: case JT_RUBZ:
+        M[0] = c; M[1] = -s; M[3] = s; M[4] = c; break;
+    case JT_RU: case JT_RUBU:
+        axis_rot(axis, c, s, M); break;
+    case JT_PX: M[9] = qj[0]; break;
+    case JT_PY: M[10] = qj[0]; break;
+    case JT_PZ: M[11] = qj[0]; break;
+    case JT_PU:
+        M[9] = axis[0] * qj[0]; M[10] = axis[1] * qj[0]; M[11] = axis[2] * qj[0]; break;
+    }
+}
+
+/* full user qpos from move-group dof values (ArticulatedModel::setQpos, full=false) */
+static void user_qpos(const orc_world *w, const real *q, real *qu) {
+    memcpy(qu, w->qpos_template, (size_t)w->nq_user * sizeof(real));
+    for (int d = 0; d < w->dof; ++d) qu[w->mg_index[d]] = q[d];
+}
+
+/* qposUser2Pinocchio (src/pinocchio_model.cpp:499-525) */
+static void user_to_pin(const orc_world *w, const real *qu, real *qp) {
+    int count = 0;
+    for (int u = 0; u < w->n_user_joints; ++u) {
+        int j = w->user_joint[u];
+        if (j == 0) continue; /* universe: nq = nv = 0 */
+        int start = w->jidx_q[j - 1];
+        int t = w->jtype[j - 1];
+        if (t >= JT_RUBX) {
+            qp[start] = cos(qu[count]);
+            qp[start + 1] = sin(qu[count]);
+        } else {
+            qp[start] = qu[count];
+        }
+        count += 1;
+    }
+}
+
+/* forwardKinematics + getLinkPose + setQpos re-matrix.
+ * out link_T[n_links*12] (matrix form used by FCL), link_pose7 optional
+ * [n_links*7] (p xyz, q wxyz) as returned by getLinkPose. */
+static void fk_links(const orc_world *w, const real *q, real *oMi, real *link_T, real *link_pose7) {
+    real qu[64], qp[64];
+    user_qpos(w, q, qu);
+    user_to_pin(w, qu, qp);
+    se3_identity(oMi); /* oMi[0] = universe */
+    for (int j = 1; j <= w->nj; ++j) {
+        real M[12], li[12];
+        joint_motion(w->jtype[j - 1], w->jaxis + 3 * (j - 1), qp + w->jidx_q[j - 1], M);
+        se3_mul(w->jplace + 12 * (j - 1), M, li);
+        int par = w->jparent[j - 1];
+        if (par > 0)
+            se3_mul(oMi + 12 * par, li, oMi + 12 * j);
+        else
+            memcpy(oMi + 12 * j, li, sizeof li);
+    }
+    for (int l = 0; l < w->n_links; ++l) {
+        real L[12], quat[4];
+        se3_mul(oMi + 12 * w->link_parent[l], w->link_place + 12 * l, L);
+        mat_to_quat(L, quat);
+        if (link_pose7) {
+            real *o = link_pose7 + 7 * l;
+            o[0] = L[9]; o[1] = L[10]; o[2] = L[11];
+            o[3] = quat[0]; o[4] = quat[1]; o[5] = quat[2]; o[6] = quat[3];
+        }
+        real *T = link_T + 12 * l;
+        quat_to_mat(quat[0], quat[1], quat[2], quat[3], T);
+        T[9] = L[9]; T[10] = L[10]; T[11] = L[11];
+    }
+}
+
+/* -------------------------------------------------------------- libccd */
+typedef struct { real v[3]; } ccd_vec3_t;
+typedef struct { real q[4]; } ccd_quat_t; /* x y z w */
+typedef struct { ccd_vec3_t v, v1, v2; } ccd_support_t;
+typedef struct { ccd_support_t ps[4]; int last; } ccd_simplex_t;
+
+static int ccdIsZero(real val) { return fabs(val) < CCD_EPS; }
+static int ccdEq(real _a, real _b) {
+    real ab = fabs(_a - _b);
+    if (fabs(ab) < CCD_EPS) return 1;
+    real a = fabs(_a), b = fabs(_b);
+    if (b > a) return ab < CCD_EPS * b;
+    return ab < CCD_EPS * a;
+}
+static void ccdVec3Set(ccd_vec3_t *v, real x, real y, real z) { v->v[0] = x; v->v[1] = y; v->v[2] = z; }
+static void ccdVec3Copy(ccd_vec3_t *a, const ccd_vec3_t *b) { *a = *b; }
+static void ccdVec3Sub2(ccd_vec3_t *d, const ccd_vec3_t *v, const ccd_vec3_t *w) {
+    d->v[0] = v->v[0] - w->v[0]; d->v[1] = v->v[1] - w->v[1]; d->v[2] = v->v[2] - w->v[2];
+}
+static void ccdVec3Add(ccd_vec3_t *v, const ccd_vec3_t *w) {
+    v->v[0] += w->v[0]; v->v[1] += w->v[1]; v->v[2] += w->v[2];
+}
+static void ccdVec3Scale(ccd_vec3_t *d, real k) { d->v[0] *= k; d->v[1] *= k; d->v[2] *= k; }
+static real ccdVec3Dot(const ccd_vec3_t *a, const ccd_vec3_t *b) {
+    real dot = a->v[0] * b->v[0];
+    dot += a->v[1] * b->v[1];
+    dot += a->v[2] * b->v[2];
+    return dot;
+}
+static real ccdVec3Len2(const ccd_vec3_t *v) { return ccdVec3Dot(v, v); }
+static void ccdVec3Normalize(ccd_vec3_t *d) {
+    real k = 1.0 / sqrt(ccdVec3Len2(d));
+    ccdVec3Scale(d, k);
+}
+static void ccdVec3Cross(ccd_vec3_t *d, const ccd_vec3_t *a, const ccd_vec3_t *b) {
+    d->v[0] = (a->v[1] * b->v[2]) - (a->v[2] * b->v[1]);
+    d->v[1] = (a->v[2] * b->v[0]) - (a->v[0] * b->v[2]);
+    d->v[2] = (a->v[0] * b->v[1]) - (a->v[1] * b->v[0]);
+}
+static int ccdVec3Eq(const ccd_vec3_t *a, const ccd_vec3_t *b) {
+    return ccdEq(a->v[0], b->v[0]) && ccdEq(a->v[1], b->v[1]) && ccdEq(a->v[2], b->v[2]);
+}
+static void ccdQuatRotVec(ccd_vec3_t *v, const ccd_quat_t *q) {
+    real vx = v->v[0], vy = v->v[1], vz = v->v[2];
+    real w = q->q[3], x = q->q[0], y = q->q[1], z = q->q[2];
+    real c1x = y * vz - z * vy + w * vx;
+    real c1y = z * vx - x * vz + w * vy;
+    real c1z = x * vy - y * vx + w * vz;
+    real c2x = y * c1z - z * c1y;
+    real c2y = z * c1x - x * c1z;
+    real c2z = x * c1y - y * c1x;
+    ccdVec3Set(v, vx + 2 * c2x, vy + 2 * c2y, vz + 2 * c2z);
+}
+static int ccdQuatInvert2(ccd_quat_t *dest, const ccd_quat_t *src) {
+    *dest = *src;
+    real len2 = dest->q[0] * dest->q[0];
+    len2 += dest->q[1] * dest->q[1];
+    len2 += dest->q[2] * dest->q[2];
+    len2 += dest->q[3] * dest->q[3];
+    if (len2 < CCD_EPS) return -1;
+    len2 = 1.0 / len2;
+    dest->q[0] = -dest->q[0] * len2;
+    dest->q[1] = -dest->q[1] * len2;
+    dest->q[2] = -dest->q[2] * len2;
+    dest->q[3] = dest->q[3] * len2;
+    return 0;
+}
+
+static const ccd_vec3_t ccd_vec3_origin = {{0.0, 0.0, 0.0}};
+
+/* ------------------------------------------------- FCL GJK objects (0.7.0) */
+typedef struct {
+    ccd_vec3_t pos;
+    ccd_quat_t rot, rot_inv;
+    int type;
+    const real *verts; /* convex */
+    int nv;
+    const real *interior;
+    real dim[3];       /* box half sizes */
+    real radius, height; /* sphere / capsule / cylinder */
+    orc_stats *stats;
+} gjk_obj;
+
+/* shapeToGJK: Quaternion q(tf.linear()); pos = T; rot = (x,y,z,w); rot_inv */
+static void shape_to_gjk(const real *T, gjk_obj *o) {
+    real q[4];
+    mat_to_quat(T, q);
+    ccdVec3Set(&o->pos, T[9], T[10], T[11]);
+    o->rot.q[0] = q[1]; o->rot.q[1] = q[2]; o->rot.q[2] = q[3]; o->rot.q[3] = q[0];
+    ccdQuatInvert2(&o->rot_inv, &o->rot);
+}
+
+static void support_convex(const gjk_obj *c, const ccd_vec3_t *dir_, ccd_vec3_t *v) {
+    ccd_vec3_t dir;
+    ccdVec3Copy(&dir, dir_);
+    ccdQuatRotVec(&dir, &c->rot_inv);
+    /* Convex::findExtremeVertex: argmax of dir . vertex, first maximum wins */
+    const real *p = c->verts;
+    real maxdot = -CCD_REAL_MAX;
+    int best = 0;
+    for (int i = 0; i < c->nv; ++i) {
+        real dot = (dir.v[0] * p[3 * i] + dir.v[1] * p[3 * i + 1]) + dir.v[2] * p[3 * i + 2];
+        if (dot > maxdot) { maxdot = dot; best = i; }
+    }
+    if (c->stats) c->stats->vertex_dots += c->nv;
+    ccdVec3Set(v, p[3 * best], p[3 * best + 1], p[3 * best + 2]);
+    ccdQuatRotVec(v, &c->rot);
+    ccdVec3Add(v, &c->pos);
+}
+
+static void support_box(const gjk_obj *o, const ccd_vec3_t *dir_, ccd_vec3_t *v) {
+    ccd_vec3_t dir;
+    ccdVec3Copy(&dir, dir_);
+    ccdQuatRotVec(&dir, &o->rot_inv);
+    ccdVec3Set(v, (dir.v[0] >= 0 ? 1.0 : -1.0) * o->dim[0],
+                  (dir.v[1] >= 0 ? 1.0 : -1.0) * o->dim[1],
+                  (dir.v[2] >= 0 ? 1.0 : -1.0) * o->dim[2]);
+    ccdQuatRotVec(v, &o->rot);
+    ccdVec3Add(v, &o->pos);
+}
+
+static void support_sphere(const gjk_obj *s, const ccd_vec3_t *dir_, ccd_vec3_t *v) {
+    ccd_vec3_t dir;
+    ccdVec3Copy(&dir, dir_);
+    ccdQuatRotVec(&dir, &s->rot_inv);
+    ccdVec3Copy(v, &dir);
+    ccdVec3Scale(v, s->radius);
+    ccdVec3Scale(v, 1.0 / sqrt(ccdVec3Len2(&dir)));
+    ccdQuatRotVec(v, &s->rot);
+    ccdVec3Add(v, &s->pos);
+}
+
+static void support_capsule(const gjk_obj *o, const ccd_vec3_t *dir_, ccd_vec3_t *v) {
+    ccd_vec3_t dir, pos1, pos2;
+    ccdVec3Copy(&dir, dir_);
+    ccdQuatRotVec(&dir, &o->rot_inv);
+    ccdVec3Set(&pos1, 0.0, 0.0, o->height);
+    ccdVec3Set(&pos2, 0.0, 0.0, -o->height);
+    ccdVec3Copy(v, &dir);
+    ccdVec3Normalize(v);
+    ccdVec3Scale(v, o->radius);
+    ccdVec3Add(&pos1, v);
+    ccdVec3Add(&pos2, v);
+    if (dir.v[2] > 0) ccdVec3Copy(v, &pos1);
+    else ccdVec3Copy(v, &pos2);
+    ccdQuatRotVec(v, &o->rot);
+    ccdVec3Add(v, &o->pos);
+}
+
+static void support_cylinder(const gjk_obj *c, const ccd_vec3_t *dir_, ccd_vec3_t *v) {
+    ccd_vec3_t dir;
+    real zdist, rad;
+    ccdVec3Copy(&dir, dir_);
+    ccdQuatRotVec(&dir, &c->rot_inv);
+    zdist = dir.v[0] * dir.v[0] + dir.v[1] * dir.v[1];
+    zdist = sqrt(zdist);
+    if (ccdIsZero(zdist))
+        ccdVec3Set(v, 0.0, 0.0, (dir.v[2] > 0 ? 1.0 : -1.0) * c->height);
+    else {
+        rad = c->radius / zdist;
+        ccdVec3Set(v, rad * dir.v[0], rad * dir.v[1], (dir.v[2] > 0 ? 1.0 : -1.0) * c->height);
+    }
+    ccdQuatRotVec(v, &c->rot);
+    ccdVec3Add(v, &c->pos);
+}
+
+static void gjk_support(const gjk_obj *o, const ccd_vec3_t *dir, ccd_vec3_t *v) {
+    switch (o->type) {
+    case GEOM_CONVEX: support_convex(o, dir, v); break;
+    case GEOM_BOX: support_box(o, dir, v); break;
+    case GEOM_SPHERE: support_sphere(o, dir, v); break;
+    case GEOM_CAPSULE: support_capsule(o, dir, v); break;
+    default: support_cylinder(o, dir, v); break;
+    }
+}
+
+static void gjk_center(const gjk_obj *o, ccd_vec3_t *c) {
+    if (o->type == GEOM_CONVEX) { /* centerConvex */
+        ccdVec3Set(c, o->interior[0], o->interior[1], o->interior[2]);
+        ccdQuatRotVec(c, &o->rot);
+        ccdVec3Add(c, &o->pos);
+    } else { /* centerShape */
+        ccdVec3Copy(c, &o->pos);
+    }
+}
+
+/* ------------------------------------------------ libccd 2.1 mpr.c */
+#define SP(s, i) (&(s)->ps[i])
+
+static void ccd_support(const gjk_obj *o1, const gjk_obj *o2, const ccd_vec3_t *_dir, ccd_support_t *supp) {
+    ccd_vec3_t dir;
+    ccdVec3Copy(&dir, _dir);
+    gjk_support(o1, &dir, &supp->v1);
+    ccdVec3Scale(&dir, -1.0);
+    gjk_support(o2, &dir, &supp->v2);
+    ccdVec3Sub2(&supp->v, &supp->v1, &supp->v2);
+    if (o1->stats) o1->stats->support_calls++;
+}
+
+static void find_origin(const gjk_obj *o1, const gjk_obj *o2, ccd_support_t *center) {
+    gjk_center(o1, &center->v1);
+    gjk_center(o2, &center->v2);
+    ccdVec3Sub2(&center->v, &center->v1, &center->v2);
+}
+
+static int discover_portal(const gjk_obj *o1, const gjk_obj *o2, ccd_simplex_t *portal) {
+    ccd_vec3_t dir, va, vb;
+    real dot;
+    int cont;
+    find_origin(o1, o2, SP(portal, 0));
+    portal->last = 0;
+    if (ccdVec3Eq(&SP(portal, 0)->v, &ccd_vec3_origin)) {
+        ccdVec3Set(&va, CCD_EPS * 10.0, 0.0, 0.0);
+        ccdVec3Add(&SP(portal, 0)->v, &va);
+    }
+    ccdVec3Copy(&dir, &SP(portal, 0)->v);
+    ccdVec3Scale(&dir, -1.0);
+    ccdVec3Normalize(&dir);
+    ccd_support(o1, o2, &dir, SP(portal, 1));
+    portal->last = 1;
+    dot = ccdVec3Dot(&SP(portal, 1)->v, &dir);
+    if (ccdIsZero(dot) || dot < 0.0) return -1;
+
+    ccdVec3Cross(&dir, &SP(portal, 0)->v, &SP(portal, 1)->v);
+    if (ccdIsZero(ccdVec3Len2(&dir))) {
+        if (ccdVec3Eq(&SP(portal, 1)->v, &ccd_vec3_origin)) return 1;
+        return 2;
+    }
+    ccdVec3Normalize(&dir);
+    ccd_support(o1, o2, &dir, SP(portal, 2));
+    dot = ccdVec3Dot(&SP(portal, 2)->v, &dir);
+    if (ccdIsZero(dot) || dot < 0.0) return -1;
+    portal->last = 2;
+
+    ccdVec3Sub2(&va, &SP(portal, 1)->v, &SP(portal, 0)->v);
+    ccdVec3Sub2(&vb, &SP(portal, 2)->v, &SP(portal, 0)->v);
+    ccdVec3Cross(&dir, &va, &vb);
+    ccdVec3Normalize(&dir);
+    dot = ccdVec3Dot(&dir, &SP(portal, 0)->v);
+    if (dot > 0.0) {
+        ccd_support_t tmp = *SP(portal, 1);
+        *SP(portal, 1) = *SP(portal, 2);
+        *SP(portal, 2) = tmp;
+        ccdVec3Scale(&dir, -1.0);
+    }
+    while (portal->last < 3) {
+        ccd_support(o1, o2, &dir, SP(portal, 3));
+        dot = ccdVec3Dot(&SP(portal, 3)->v, &dir);
+        if (ccdIsZero(dot) || dot < 0.0) return -1;
+        cont = 0;
+        ccdVec3Cross(&va, &SP(portal, 1)->v, &SP(portal, 3)->v);
+        dot = ccdVec3Dot(&va, &SP(portal, 0)->v);
+        if (dot < 0.0 && !ccdIsZero(dot)) {
+            *SP(portal, 2) = *SP(portal, 3);
+            cont = 1;
+        }
+        if (!cont) {
+            ccdVec3Cross(&va, &SP(portal, 3)->v, &SP(portal, 2)->v);
+            dot = ccdVec3Dot(&va, &SP(portal, 0)->v);
+            if (dot < 0.0 && !ccdIsZero(dot)) {
+                *SP(portal, 1) = *SP(portal, 3);
+                cont = 1;
+            }
+        }
+        if (cont) {
+            ccdVec3Sub2(&va, &SP(portal, 1)->v, &SP(portal, 0)->v);
+            ccdVec3Sub2(&vb, &SP(portal, 2)->v, &SP(portal, 0)->v);
+            ccdVec3Cross(&dir, &va, &vb);
+            ccdVec3Normalize(&dir);
+        } else {
+            portal->last = 3;
+        }
+    }
+    return 0;
+}
+
+static void portal_dir(const ccd_simplex_t *portal, ccd_vec3_t *dir) {
+    ccd_vec3_t v2v1, v3v1;
+    ccdVec3Sub2(&v2v1, &portal->ps[2].v, &portal->ps[1].v);
+    ccdVec3Sub2(&v3v1, &portal->ps[3].v, &portal->ps[1].v);
+    ccdVec3Cross(dir, &v2v1, &v3v1);
+    ccdVec3Normalize(dir);
+}
+
+static int portal_encapsules_origin(const ccd_simplex_t *portal, const ccd_vec3_t *dir) {
+    real dot = ccdVec3Dot(dir, &portal->ps[1].v);
+    return ccdIsZero(dot) || dot > 0.0;
+}
+
+static int portal_reach_tolerance(const ccd_simplex_t *portal, const ccd_support_t *v4,
+                                  const ccd_vec3_t *dir, real tol) {
+    real dv1 = ccdVec3Dot(&portal->ps[1].v, dir);
+    real dv2 = ccdVec3Dot(&portal->ps[2].v, dir);
+    real dv3 = ccdVec3Dot(&portal->ps[3].v, dir);
+    real dv4 = ccdVec3Dot(&v4->v, dir);
+    real dot1 = dv4 - dv1, dot2 = dv4 - dv2, dot3 = dv4 - dv3;
+    dot1 = fmin(dot1, dot2);
+    dot1 = fmin(dot1, dot3);
+    return ccdEq(dot1, tol) || dot1 < tol;
+}
+
+static int portal_can_encapsule_origin(const ccd_support_t *v4, const ccd_vec3_t *dir) {
+    real dot = ccdVec3Dot(&v4->v, dir);
+    return ccdIsZero(dot) || dot > 0.0;
+}
+
+static void expand_portal(ccd_simplex_t *portal, const ccd_support_t *v4) {
+    real dot;
+    ccd_vec3_t v4v0;
+    ccdVec3Cross(&v4v0, &v4->v, &portal->ps[0].v);
+    dot = ccdVec3Dot(&portal->ps[1].v, &v4v0);
+    if (dot > 0.0) {
+        dot = ccdVec3Dot(&portal->ps[2].v, &v4v0);
+        if (dot > 0.0) portal->ps[1] = *v4;
+        else portal->ps[3] = *v4;
+    } else {
+        dot = ccdVec3Dot(&portal->ps[3].v, &v4v0);
+        if (dot > 0.0) portal->ps[2] = *v4;
+        else portal->ps[1] = *v4;
+    }
+}
+
+static int refine_portal(const gjk_obj *o1, const gjk_obj *o2, ccd_simplex_t *portal, real tol) {
+    ccd_vec3_t dir;
+    ccd_support_t v4;
+    for (;;) {
+        if (o1->stats) o1->stats->refine_iters++;
+        portal_dir(portal, &dir);
+        if (portal_encapsules_origin(portal, &dir)) return 0;
+        ccd_support(o1, o2, &dir, &v4);
+        if (!portal_can_encapsule_origin(&v4, &dir) || portal_reach_tolerance(portal, &v4, &dir, tol))
+            return -1;
+        expand_portal(portal, &v4);
+    }
+}
+
+/* ccdMPRIntersect */
+static int mpr_intersect(const gjk_obj *o1, const gjk_obj *o2, real tol) {
+    ccd_simplex_t portal;
+    if (o1->stats) o1->stats->mpr_runs++;
+    int res = discover_portal(o1, o2, &portal);
+    if (res < 0) return 0;
+    if (res > 0) return 1;
+    res = refine_portal(o1, o2, &portal, tol);
+    return res == 0 ? 1 : 0;
+}
+
+/* ------------------------------------------------------- world collide */
+static void make_obj(const orc_world *w, int geom, const real *T, gjk_obj *o, orc_stats *st) {
+    memset(o, 0, sizeof *o);
+    shape_to_gjk(T, o);
+    o->type = w->geom_type[geom];
+    o->stats = st;
+    const real *prm = w->geom_param + 4 * geom;
+    switch (o->type) {
+    case GEOM_CONVEX:
+        o->verts = w->verts + 3 * (size_t)w->geom_vstart[geom];
+        o->nv = w->geom_nv[geom];
+        o->interior = w->geom_interior + 3 * geom;
+        break;
+    case GEOM_BOX: /* boxToGJK: dim = side / 2 */
+        o->dim[0] = prm[0] / 2.0; o->dim[1] = prm[1] / 2.0; o->dim[2] = prm[2] / 2.0; break;
+    case GEOM_SPHERE: o->radius = prm[0]; break;
+    case GEOM_CAPSULE: o->radius = prm[0]; o->height = prm[1] / 2.0; break;
+    case GEOM_CYLINDER: o->radius = prm[0]; o->height = prm[1] / 2.0; break;
+    }
+}
+
+#define MAX_OBJ 512
+
+/* Per-configuration worker: FK + every pair + ACM filter (allowed pairs are
+ * evaluated by the reference and then dropped by filterCollisions; their
+ * narrow-phase result cannot influence the output, so they are skipped). */
+static int collide_one(const orc_world *w, const real *q, uint32_t *mask, int W, orc_stats *st,
+                       real *oMi, real *link_T, real *obj_T, real *att_T) {
+    fk_links(w, q, oMi, link_T, NULL);
+    for (int i = 0; i < w->n_obj; ++i)
+        se3_mul(link_T + 12 * w->obj_link[i], w->obj_origin + 12 * i, obj_T + 12 * i);
+    for (int i = 0; i < w->n_att; ++i)
+        se3_mul(link_T + 12 * w->att_link[i], w->att_pose + 12 * i, att_T + 12 * i);
+    memset(mask, 0, (size_t)W * sizeof(uint32_t));
+    int any = 0;
+    for (int p = 0; p < w->n_pairs; ++p) {
+        if (w->p_allowed[p]) continue;
+        gjk_obj a, b;
+        int ks[2] = {w->pa_kind[p], w->pb_kind[p]}, is[2] = {w->pa_idx[p], w->pb_idx[p]};
+        gjk_obj *objs[2] = {&a, &b};
+        for (int s = 0; s < 2; ++s) {
+            const real *T;
+            int g;
+            if (ks[s] == KIND_ROBOT) { T = obj_T + 12 * is[s]; g = w->obj_geom[is[s]]; }
+            else if (ks[s] == KIND_ATTACHED) { T = att_T + 12 * is[s]; g = w->att_geom[is[s]]; }
+            else { T = w->scene_tf + 12 * is[s]; g = w->scene_geom[is[s]]; }
+            make_obj(w, g, T, objs[s], st);
+        }
+        if (mpr_intersect(&a, &b, 1e-6)) {
+            mask[p >> 5] |= 1u << (p & 31);
+            any = 1;
+        }
+    }
+    return any;
+}
+
+typedef struct {
+    const orc_world *w;
+    const real *q;
+    long lo, hi;
+    uint8_t *flags;
+    uint32_t *masks;
+    int W;
+    orc_stats st;
+} job_t;
+
+static void *worker(void *arg) {
+    job_t *j = (job_t *)arg;
+    const orc_world *w = j->w;
+    real *oMi = malloc(sizeof(real) * 12 * (size_t)(w->nj + 1));
+    real *link_T = malloc(sizeof(real) * 12 * (size_t)(w->n_links + 1));
+    real *obj_T = malloc(sizeof(real) * 12 * (size_t)(w->n_obj + 1));
+    real *att_T = malloc(sizeof(real) * 12 * (size_t)(w->n_att + 1));
+    for (long i = j->lo; i < j->hi; ++i)
+        j->flags[i] = (uint8_t)collide_one(w, j->q + (size_t)i * w->dof, j->masks + (size_t)i * j->W, j->W,
+                                           &j->st, oMi, link_T, obj_T, att_T);
+    free(oMi); free(link_T); free(obj_T); free(att_T);
+    return NULL;
+}
+
+/* Batch entry point.  flags[n], masks[n*W]; stats (may be NULL) receives
+ * the summed instrumentation counters. */
+int orc_collide_batch(const orc_world *w, const double *q, long n, uint8_t *flags, uint32_t *masks, int W,
+                      int nthreads, orc_stats *stats) {
+    if (w->nq_user > 64 || w->nq_pin > 64) return -1;
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > 256) nthreads = 256;
+    job_t jobs[256];
+    pthread_t th[256];
+    long chunk = (n + nthreads - 1) / nthreads;
+    for (int t = 0; t < nthreads; ++t) {
+        jobs[t].w = w; jobs[t].q = q; jobs[t].flags = flags; jobs[t].masks = masks; jobs[t].W = W;
+        jobs[t].lo = t * chunk < n ? t * chunk : n;
+        jobs[t].hi = (t + 1) * chunk < n ? (t + 1) * chunk : n;
+        memset(&jobs[t].st, 0, sizeof(orc_stats));
+    }
+    if (nthreads == 1) worker(&jobs[0]);
+    else {
+        for (int t = 0; t < nthreads; ++t) pthread_create(&th[t], NULL, worker, &jobs[t]);
+        for (int t = 0; t < nthreads; ++t) pthread_join(th[t], NULL);
+    }
+    if (stats) {
+        memset(stats, 0, sizeof *stats);
+        for (int t = 0; t < nthreads; ++t) {
+            stats->support_calls += jobs[t].st.support_calls;
+            stats->vertex_dots += jobs[t].st.vertex_dots;
+            stats->refine_iters += jobs[t].st.refine_iters;
+            stats->mpr_runs += jobs[t].st.mpr_runs;
+        }
+    }
+    return 0;
+}
+
+/* FK entry point: link_pose7[n*n_links*7] (getLinkPose), obj_T[n*n_obj*12]
+ * (collision object transforms after updateCollisionObjects).  Either output
+ * may be NULL. */
+int orc_fk_batch(const orc_world *w, const double *q, long n, double *link_pose7, double *obj_T) {
+    if (w->nq_user > 64 || w->nq_pin > 64) return -1;
+    real *oMi = malloc(sizeof(real) * 12 * (size_t)(w->nj + 1));
+    real *link_T = malloc(sizeof(real) * 12 * (size_t)(w->n_links + 1));
+    for (long i = 0; i < n; ++i) {
+        fk_links(w, q + (size_t)i * w->dof, oMi, link_T, link_pose7 ? link_pose7 + (size_t)i * w->n_links * 7 : NULL);
+        if (obj_T)
+            for (int o = 0; o < w->n_obj; ++o)
+                se3_mul(link_T + 12 * w->obj_link[o], w->obj_origin + 12 * o, obj_T + ((size_t)i * w->n_obj + o) * 12);
+    }
+    free(oMi); free(link_T);
+    return 0;
+}
+
+/* Single-pair entry (fcl.collide(o1, o2) on two posed shapes). */
+int orc_collide_pair(const orc_world *w, int ga, const double *Ta, int gb, const double *Tb) {
+    gjk_obj a, b;
+    make_obj(w, ga, Ta, &a, NULL);
+    make_obj(w, gb, Tb, &b, NULL);
+    return mpr_intersect(&a, &b, 1e-6);
+}

@@ -1,0 +1,639 @@
+"""ORACLE (test infrastructure only) -- independent host-side model loader.
+
+This module is part of the CPU parity oracle.  Only ``tests/``,
+``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline`` leg may import
+it.  The shipped product (``mplib_amd``) never imports anything under
+``oracle/``.
+
+It restates, in plain Python floats (IEEE binary64, one rounding per operation,
+never fused), how MPlib turns a URDF/SRDF pair into the numbers the collision
+path uses:
+
+* urdfdom 4.0.0 tree building: ``child_links`` are appended while iterating
+  the joints in ``std::map`` (sorted-by-name) order; ``Rotation::setFromRPY`` +
+  ``normalize`` for every ``<origin rpy=...>``.  [ext: urdfdom_headers 1.1.1]
+* ``pose_to_se3`` / ``pose_to_transform``: quaternion -> Eigen
+  ``toRotationMatrix`` (reference ``src/urdf_utils.cpp:47-63``).
+* pinocchio 2.6.21 ``UrdfVisitor`` as driven by MPlib's own DFS
+  (``src/pinocchio_model.cpp:559-752``): joint placements are folded with the
+  parent body frame placement, fixed joints become frames, RX/RY/RZ vs
+  unaligned axes via ``isApprox``.  [ext: pinocchio 2.6.21]
+* ``FCLModelTpl::dfs_parse_tree`` / ``init`` (``src/fcl_model.cpp:196-294``):
+  collision object order, the self-collision pair rule (``:282-293``) and SRDF
+  removal (``:114-136``).
+* assimp 5.3.1 ASCII/binary STL import with ``JoinIdenticalVertices``
+  (first-occurrence vertex order) and its ``fast_atoreal_move`` float parser,
+  promoted float->double as ``dfs_build_mesh`` does
+  (``src/urdf_utils.cpp:82-133, 156-183``).  [ext: assimp 5.3.1]
+* FCL 0.7.0 ``Convex`` interior point = ``sum * (1.0 / n)``.  [ext: FCL 0.7.0]
+
+Parity status: these restatements are pinned only by the Panda fixture facts
+quoted in SURVEY.md section 8(a) (object count, pair list, per-hull vertex
+counts); the reference ships no numeric golden vectors.
+"""
+from __future__ import annotations
+
+import ctypes
+import ctypes.util
+import math
+import os
+import struct
+import xml.etree.ElementTree as ET
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+# ----------------------------------------------------------------------------
+# libm powf (assimp's exponent handling calls std::pow(float, float))
+# ----------------------------------------------------------------------------
+_libm = ctypes.CDLL(ctypes.util.find_library("m") or "libm.so.6")
+_libm.powf.restype = ctypes.c_float
+_libm.powf.argtypes = [ctypes.c_float, ctypes.c_float]
+
+
+def f32(x: float) -> float:
+    """Round a binary64 value to binary32 (round-to-nearest-even)."""
+    return float(np.float32(x))
+
+
+# ----------------------------------------------------------------------------
+# SE(3) helpers, row-major R (9) + p (3); exact Eigen/pinocchio op order
+# ----------------------------------------------------------------------------
+IDENT = ([1.0, 0.0, 0.0, 0.0, 1.0, 0.0, 0.0, 0.0, 1.0], [0.0, 0.0, 0.0])
+
+
+def mat3_mul(a: Sequence[float], b: Sequence[float]) -> List[float]:
+    """Eigen lazy 3x3 product: each entry ((a_i0 b_0j + a_i1 b_1j) + a_i2 b_2j)."""
+    out = [0.0] * 9
+    for i in range(3):
+        for j in range(3):
+            out[3 * i + j] = (a[3 * i] * b[j] + a[3 * i + 1] * b[3 + j]) + a[3 * i + 2] * b[6 + j]
+    return out
+
+
+def mat3_vec(a: Sequence[float], v: Sequence[float]) -> List[float]:
+    return [(a[3 * i] * v[0] + a[3 * i + 1] * v[1]) + a[3 * i + 2] * v[2] for i in range(3)]
+
+
+def se3_mul(A, B):
+    """pinocchio ``SE3::__mult__`` / Eigen Isometry product:
+    R = R1 R2, p = R1 p2 + p1 (addition order is commutative in IEEE)."""
+    R = mat3_mul(A[0], B[0])
+    Rp = mat3_vec(A[0], B[1])
+    return (R, [Rp[0] + A[1][0], Rp[1] + A[1][1], Rp[2] + A[1][2]])
+
+
+def quat_to_mat(w: float, x: float, y: float, z: float) -> List[float]:
+    """Eigen 3.4 ``QuaternionBase::toRotationMatrix``."""
+    tx, ty, tz = 2.0 * x, 2.0 * y, 2.0 * z
+    twx, twy, twz = tx * w, ty * w, tz * w
+    txx, txy, txz = tx * x, ty * x, tz * x
+    tyy, tyz, tzz = ty * y, tz * y, tz * z
+    return [1.0 - (tyy + tzz), txy - twz, txz + twy,
+            txy + twz, 1.0 - (txx + tzz), tyz - twx,
+            txz - twy, tyz + twx, 1.0 - (txx + tyy)]
+
+
+def mat_to_quat(m: Sequence[float]) -> Tuple[float, float, float, float]:
+    """Eigen 3.4 ``quaternionbase_assign_impl<Other,3,3>`` -> (w, x, y, z)."""
+    def c(i, j):
+        return m[3 * i + j]
+    t = (c(0, 0) + c(1, 1)) + c(2, 2)
+    q = [0.0, 0.0, 0.0]  # x y z
+    if t > 0.0:
+        t = math.sqrt(t + 1.0)
+        w = 0.5 * t
+        t = 0.5 / t
+        q[0] = (c(2, 1) - c(1, 2)) * t
+        q[1] = (c(0, 2) - c(2, 0)) * t
+        q[2] = (c(1, 0) - c(0, 1)) * t
+    else:
+        i = 0
+        if c(1, 1) > c(0, 0):
+            i = 1
+        if c(2, 2) > c(i, i):
+            i = 2
+        j = (i + 1) % 3
+        k = (j + 1) % 3
+        t = math.sqrt(((c(i, i) - c(j, j)) - c(k, k)) + 1.0)
+        q[i] = 0.5 * t
+        t = 0.5 / t
+        w = (c(k, j) - c(j, k)) * t
+        q[j] = (c(j, i) + c(i, j)) * t
+        q[k] = (c(k, i) + c(i, k)) * t
+    return (w, q[0], q[1], q[2])
+
+
+def rpy_to_quat(r: float, p: float, y: float) -> Tuple[float, float, float, float]:
+    """urdfdom ``Rotation::setFromRPY`` followed by ``normalize``; returns (x,y,z,w)."""
+    phi, the, psi = r / 2.0, p / 2.0, y / 2.0
+    sphi, cphi = math.sin(phi), math.cos(phi)
+    sthe, cthe = math.sin(the), math.cos(the)
+    spsi, cpsi = math.sin(psi), math.cos(psi)
+    x = sphi * cthe * cpsi - cphi * sthe * spsi
+    yy = cphi * sthe * cpsi + sphi * cthe * spsi
+    z = cphi * cthe * spsi - sphi * sthe * cpsi
+    w = cphi * cthe * cpsi + sphi * sthe * spsi
+    s = math.sqrt(x * x + yy * yy + z * z + w * w)
+    if s == 0.0:
+        return (0.0, 0.0, 0.0, 1.0)
+    return (x / s, yy / s, z / s, w / s)
+
+
+def _vec3(s: Optional[str], default=(0.0, 0.0, 0.0)) -> Tuple[float, float, float]:
+    if s is None:
+        return default
+    parts = s.split()
+    if len(parts) != 3:
+        raise ValueError(f"bad vector '{s}'")
+    return (float(parts[0]), float(parts[1]), float(parts[2]))
+
+
+@dataclass
+class Pose:
+    xyz: Tuple[float, float, float] = (0.0, 0.0, 0.0)
+    quat: Tuple[float, float, float, float] = (0.0, 0.0, 0.0, 1.0)  # x y z w
+
+    def se3(self):
+        x, y, z, w = self.quat
+        return (quat_to_mat(w, x, y, z), list(self.xyz))
+
+
+def _parse_origin(el) -> Pose:
+    if el is None:
+        return Pose()
+    xyz = _vec3(el.get("xyz"))
+    rpy = el.get("rpy")
+    quat = (0.0, 0.0, 0.0, 1.0)
+    if rpy is not None:
+        quat = rpy_to_quat(*_vec3(rpy))
+    return Pose(xyz, quat)
+
+
+# ----------------------------------------------------------------------------
+# URDF (urdfdom semantics)
+# ----------------------------------------------------------------------------
+@dataclass
+class Geometry:
+    kind: str                      # 'mesh' | 'box' | 'sphere' | 'cylinder'
+    filename: str = ""
+    scale: Tuple[float, float, float] = (1.0, 1.0, 1.0)
+    size: Tuple[float, float, float] = (0.0, 0.0, 0.0)
+    radius: float = 0.0
+    length: float = 0.0
+
+
+@dataclass
+class Link:
+    name: str
+    collisions: List[Tuple[Pose, Geometry]] = field(default_factory=list)
+    parent: Optional[str] = None
+    parent_joint: Optional[str] = None
+    children: List[str] = field(default_factory=list)
+
+
+@dataclass
+class Joint:
+    name: str
+    type: str
+    parent: str
+    child: str
+    origin: Pose
+    axis: Tuple[float, float, float]
+    lower: float = 0.0
+    upper: float = 0.0
+    has_limits: bool = False
+
+
+@dataclass
+class URDF:
+    links: Dict[str, Link]
+    joints: Dict[str, Joint]
+    root: str
+    directory: str
+
+
+def _parse_geometry(el) -> Geometry:
+    g = list(el)
+    if not g:
+        raise ValueError("empty geometry")
+    g = g[0]
+    if g.tag == "mesh":
+        return Geometry("mesh", filename=g.get("filename"), scale=_vec3(g.get("scale"), (1.0, 1.0, 1.0)))
+    if g.tag == "box":
+        return Geometry("box", size=_vec3(g.get("size")))
+    if g.tag == "sphere":
+        return Geometry("sphere", radius=float(g.get("radius")))
+    if g.tag == "cylinder":
+        return Geometry("cylinder", radius=float(g.get("radius")), length=float(g.get("length")))
+    raise ValueError(f"unknown geometry {g.tag}")
+
+
+def parse_urdf(path: str) -> URDF:
+    root_el = ET.parse(path).getroot()
+    links: Dict[str, Link] = {}
+    joints: Dict[str, Joint] = {}
+    for el in root_el.findall("link"):
+        ln = Link(el.get("name"))
+        for c in el.findall("collision"):
+            ln.collisions.append((_parse_origin(c.find("origin")), _parse_geometry(c.find("geometry"))))
+        links[ln.name] = ln
+    for el in root_el.findall("joint"):
+        lim = el.find("limit")
+        ax = el.find("axis")
+        j = Joint(
+            el.get("name"), el.get("type"), el.find("parent").get("link"), el.find("child").get("link"),
+            _parse_origin(el.find("origin")),
+            _vec3(ax.get("xyz")) if ax is not None else (1.0, 0.0, 0.0),
+        )
+        if lim is not None:
+            j.has_limits = True
+            j.lower = float(lim.get("lower", "0"))
+            j.upper = float(lim.get("upper", "0"))
+        joints[j.name] = j
+    # urdfdom initTree: iterate joints in std::map (byte-sorted) order
+    for jname in sorted(joints.keys(), key=lambda s: s.encode()):
+        j = joints[jname]
+        links[j.child].parent = j.parent
+        links[j.child].parent_joint = j.name
+        links[j.parent].children.append(j.child)
+    roots = [n for n, l in links.items() if l.parent is None]
+    if len(roots) != 1:
+        raise ValueError(f"URDF must have exactly one root, got {roots}")
+    return URDF(links, joints, roots[0], os.path.dirname(os.path.abspath(path)))
+
+
+# ----------------------------------------------------------------------------
+# assimp 5.3.1 STL import
+# ----------------------------------------------------------------------------
+_FAST_ATOF_TABLE = [0.0, 0.1, 0.01, 0.001, 0.0001, 0.00001, 0.000001, 0.0000001,
+                    0.00000001, 0.000000001, 0.0000000001, 0.00000000001,
+                    0.000000000001, 0.0000000000001, 0.00000000000001,
+                    0.000000000000001]
+
+
+def _strtoul10_64(s: str, i: int, max_digits: Optional[int] = None):
+    if i >= len(s) or not s[i].isdigit():
+        raise ValueError(f"cannot parse number at '{s[i:i+20]}'")
+    value = 0
+    cur = 0
+    while i < len(s) and s[i].isdigit():
+        value = value * 10 + (ord(s[i]) - 48)
+        i += 1
+        cur += 1
+        if max_digits is not None and cur == max_digits:
+            while i < len(s) and s[i].isdigit():
+                i += 1
+            return value, i, cur
+    return value, i, cur
+
+
+def assimp_atof(s: str) -> float:
+    """assimp ``fast_atoreal_move<float>`` (include/assimp/fast_atof.h)."""
+    i = 0
+    inv = s[0] == "-"
+    if inv or s[0] == "+":
+        i += 1
+    f = 0.0
+    if s[i] != ".":
+        v, i, _ = _strtoul10_64(s, i)
+        f = f32(float(v))
+    if i < len(s) and s[i] == "." and i + 1 < len(s) and s[i + 1].isdigit():
+        i += 1
+        v, i, diff = _strtoul10_64(s, i, 15)
+        pl = float(v) * _FAST_ATOF_TABLE[diff]
+        f = f32(f + f32(pl))
+    elif i < len(s) and s[i] == ".":
+        i += 1
+    if i < len(s) and s[i] in "eE":
+        i += 1
+        einv = s[i] == "-"
+        if einv or s[i] == "+":
+            i += 1
+        v, i, _ = _strtoul10_64(s, i)
+        e = f32(float(v))
+        if einv:
+            e = -e
+        f = f32(f * float(_libm.powf(10.0, e)))
+    if inv:
+        f = -f
+    return f
+
+
+def load_stl(path: str) -> Tuple[List[Tuple[float, float, float]], List[Tuple[int, int, int]]]:
+    """Unique vertices (binary32 values as float) in first-occurrence order and
+    triangles, as assimp's STL importer + JoinIdenticalVertices produce them."""
+    with open(path, "rb") as fh:
+        data = fh.read()
+    raw: List[Tuple[float, float, float]] = []
+    is_ascii = data[:5].lower() == b"solid" and b"facet" in data[:2048]
+    if is_ascii:
+        toks = data.decode("ascii", "replace").split()
+        k = 0
+        while k < len(toks):
+            if toks[k] == "vertex":
+                raw.append((assimp_atof(toks[k + 1]), assimp_atof(toks[k + 2]), assimp_atof(toks[k + 3])))
+                k += 4
+            else:
+                k += 1
+    else:
+        n = struct.unpack_from("<I", data, 80)[0]
+        off = 84
+        for _ in range(n):
+            vals = struct.unpack_from("<12f", data, off)
+            for t in range(3):
+                raw.append(tuple(float(v) for v in vals[3 + 3 * t: 6 + 3 * t]))
+            off += 50
+    if len(raw) % 3:
+        raise ValueError("STL vertex count not a multiple of 3")
+    index: Dict[Tuple[float, float, float], int] = {}
+    verts: List[Tuple[float, float, float]] = []
+    remap = []
+    for v in raw:
+        key = (v[0] + 0.0, v[1] + 0.0, v[2] + 0.0)  # -0 == +0 in assimp's comparison
+        if key not in index:
+            index[key] = len(verts)
+            verts.append(v)
+        remap.append(index[key])
+    tris = [(remap[3 * t], remap[3 * t + 1], remap[3 * t + 2]) for t in range(len(raw) // 3)]
+    return verts, tris
+
+
+# ----------------------------------------------------------------------------
+# geometry records (FCL semantics)
+# ----------------------------------------------------------------------------
+GEOM_CONVEX, GEOM_BOX, GEOM_SPHERE, GEOM_CAPSULE, GEOM_CYLINDER = 0, 1, 2, 3, 4
+
+
+@dataclass
+class ConvexGeom:
+    vertices: np.ndarray  # [n, 3] float64
+    faces: List[Tuple[int, int, int]]
+
+    @property
+    def interior(self) -> List[float]:
+        """FCL 0.7.0 Convex ctor: sum of vertices, times (1.0 / n)."""
+        s = [0.0, 0.0, 0.0]
+        for v in self.vertices.tolist():
+            s[0] += v[0]
+            s[1] += v[1]
+            s[2] += v[2]
+        inv = 1.0 / len(self.vertices)
+        return [s[0] * inv, s[1] * inv, s[2] * inv]
+
+
+@dataclass
+class BoxGeom:
+    side: Tuple[float, float, float]
+
+
+def load_convex_mesh(path: str, scale=(1.0, 1.0, 1.0)) -> ConvexGeom:
+    verts, tris = load_stl(path)
+    arr = np.array([[v[0] * scale[0], v[1] * scale[1], v[2] * scale[2]] for v in verts], dtype=np.float64)
+    return ConvexGeom(arr, tris)
+
+
+# ----------------------------------------------------------------------------
+# pinocchio-style kinematic model
+# ----------------------------------------------------------------------------
+# joint type codes shared with oracle/collide_oracle.c
+JT_RX, JT_RY, JT_RZ, JT_RU, JT_PX, JT_PY, JT_PZ, JT_PU, JT_RUBX, JT_RUBY, JT_RUBZ, JT_RUBU = range(12)
+_JT_NAMES = {JT_RX: "JointModelRX", JT_RY: "JointModelRY", JT_RZ: "JointModelRZ",
+             JT_RU: "JointModelRevoluteUnaligned", JT_PX: "JointModelPX", JT_PY: "JointModelPY",
+             JT_PZ: "JointModelPZ", JT_PU: "JointModelPrismaticUnaligned", JT_RUBX: "JointModelRUBX",
+             JT_RUBY: "JointModelRUBY", JT_RUBZ: "JointModelRUBZ",
+             JT_RUBU: "JointModelRevoluteUnboundedUnaligned"}
+
+
+def _is_approx(a, b, prec=1e-12) -> bool:
+    """Eigen ``isApprox``: ||a-b||^2 <= prec^2 * min(||a||^2, ||b||^2)."""
+    d = sum((a[i] - b[i]) ** 2 for i in range(3))
+    na = sum(x * x for x in a)
+    nb = sum(x * x for x in b)
+    return d <= prec * prec * min(na, nb)
+
+
+def _cartesian_axis(axis) -> int:
+    if _is_approx(axis, (1.0, 0.0, 0.0)):
+        return 0
+    if _is_approx(axis, (0.0, 1.0, 0.0)):
+        return 1
+    if _is_approx(axis, (0.0, 0.0, 1.0)):
+        return 2
+    return 3
+
+
+@dataclass
+class PinJoint:
+    name: str
+    jtype: int
+    parent: int
+    placement: tuple
+    axis: Tuple[float, float, float]
+    idx_q: int
+    nq: int
+    nv: int
+    lower: List[float]
+    upper: List[float]
+
+
+@dataclass
+class PinFrame:
+    name: str
+    ftype: str
+    parent: int
+    placement: tuple
+
+
+class PinModel:
+    """pinocchio ``Model`` as built by MPlib's ``dfs_parse_tree`` +
+    ``UrdfVisitor`` (reference ``src/pinocchio_model.cpp:559-752``)."""
+
+    def __init__(self, urdf: URDF):
+        self.joints: List[Optional[PinJoint]] = [None]  # index 0 = universe
+        self.names = ["universe"]
+        self.frames = [PinFrame("universe", "FIXED_JOINT", 0, IDENT)]
+        self.nq = 0
+        self.nv = 0
+        # addRootJoint -> addFixedJointAndBody(0, Identity, "root_joint", root)
+        self._add_fixed(0, IDENT, "root_joint", urdf.root)
+        self._dfs(urdf, urdf.root)
+
+    def body_frame(self, name: str) -> int:
+        for i, f in enumerate(self.frames):
+            if f.name == name and f.ftype == "BODY":
+                return i
+        raise KeyError(name)
+
+    def _add_fixed(self, parent_frame: int, jp, jname: str, body: str):
+        pf = self.frames[parent_frame]
+        placement = se3_mul(pf.placement, jp)
+        self.frames.append(PinFrame(jname, "FIXED_JOINT", pf.parent, placement))
+        self.frames.append(PinFrame(body, "BODY", pf.parent, placement))
+
+    def _dfs(self, urdf: URDF, link_name: str):
+        for child in urdf.links[link_name].children:
+            link = urdf.links[child]
+            j = urdf.joints[link.parent_joint]
+            parent_frame = self.body_frame(link_name)
+            jp = j.origin.se3()
+            if j.type == "fixed":
+                self._add_fixed(parent_frame, jp, j.name, child)
+            else:
+                pf = self.frames[parent_frame]
+                ax = _cartesian_axis(j.axis)
+                if j.type == "revolute":
+                    jt, nq, nv = (JT_RX, JT_RY, JT_RZ, JT_RU)[ax], 1, 1
+                    lo, hi = [j.lower], [j.upper]
+                elif j.type == "continuous":
+                    jt, nq, nv = (JT_RUBX, JT_RUBY, JT_RUBZ, JT_RUBU)[ax], 2, 1
+                    lo, hi = [-1.01, -1.01], [1.01, 1.01]
+                elif j.type == "prismatic":
+                    jt, nq, nv = (JT_PX, JT_PY, JT_PZ, JT_PU)[ax], 1, 1
+                    lo, hi = [j.lower], [j.upper]
+                else:
+                    raise ValueError(f"unsupported joint type {j.type}")
+                axis = tuple(j.axis)
+                if ax == 3:
+                    n = math.sqrt(axis[0] * axis[0] + axis[1] * axis[1] + axis[2] * axis[2])
+                    axis = (axis[0] / n, axis[1] / n, axis[2] / n)
+                idx = len(self.joints)
+                self.joints.append(PinJoint(j.name, jt, pf.parent, se3_mul(pf.placement, jp), axis,
+                                            self.nq, nq, nv, lo, hi))
+                self.names.append(j.name)
+                self.nq += nq
+                self.nv += nv
+                # addJointFrame (Identity) then appendBodyToJoint(Identity)
+                self.frames.append(PinFrame(j.name, "JOINT", idx, IDENT))
+                self.frames.append(PinFrame(child, "BODY", idx, se3_mul(IDENT, IDENT)))
+            self._dfs(urdf, child)
+
+    def link_names(self) -> List[str]:
+        return [f.name for f in self.frames if f.ftype == "BODY"]
+
+    def joint_type_name(self, j: int) -> str:
+        return _JT_NAMES[self.joints[j].jtype]
+
+    def supports(self, j: int) -> List[int]:
+        out = []
+        while j > 0:
+            out.append(j)
+            j = self.joints[j].parent
+        return [0] + out[::-1]
+
+
+# ----------------------------------------------------------------------------
+# articulated model (FCLModel + PinocchioModel + move group)
+# ----------------------------------------------------------------------------
+@dataclass
+class CollisionObj:
+    link: str
+    parent_link: str
+    origin: tuple          # SE3 collision origin -> link
+    geom: object           # ConvexGeom | BoxGeom
+
+
+class Articulation:
+    """``ArticulatedModelTpl`` construction (reference
+    ``src/articulated_model.cpp:15-36``) with ``convex=True``."""
+
+    def __init__(self, urdf_path: str, srdf_path: str = "", link_names=None, joint_names=None,
+                 convex: bool = True, move_group: Optional[str] = None):
+        self.urdf = parse_urdf(urdf_path)
+        self.pin = PinModel(self.urdf)
+        self.objects: List[CollisionObj] = []
+        self._fcl_dfs(self.urdf.root, "root's parent", convex)
+        self.user_link_names = list(link_names) if link_names else self.pin.link_names()
+        self.user_joint_names = list(joint_names) if joint_names else list(self.pin.names)
+        # pinocchio setLinkOrder / setJointOrder
+        self.link_frames = [self.pin.body_frame(n) for n in self.user_link_names]
+        self.user_joints = [self.pin.names.index(n) for n in self.user_joint_names]
+        # fcl setLinkOrder
+        self.obj_user_link = [self.user_link_names.index(o.link) for o in self.objects]
+        # pair rule (fcl_model.cpp:282-293)
+        self.pairs: List[Tuple[int, int]] = []
+        names = [o.link for o in self.objects]
+        parents = [o.parent_link for o in self.objects]
+        for i in range(len(self.objects)):
+            for j in range(i):
+                if names[i] != names[j] and parents[i] != names[j] and parents[j] != names[i]:
+                    self.pairs.append((j, i))
+        if srdf_path:
+            self.remove_pairs_from_srdf(srdf_path)
+        # user qpos layout (vidx_ / nvs_)
+        self.user_vidx, self.user_nv = [], []
+        v = 0
+        for j in self.user_joints:
+            nvj = self.pin.joints[j].nv if j > 0 else 0
+            self.user_vidx.append(v)
+            self.user_nv.append(nvj)
+            v += nvj
+        self.nv = v
+        self.current_qpos = [0.0] * self.pin.nv
+        self.set_move_group(move_group if move_group else self.user_link_names)
+
+    def _fcl_dfs(self, link_name: str, parent: str, convex: bool):
+        link = self.urdf.links[link_name]
+        for origin, geom in link.collisions:
+            if geom.kind == "mesh":
+                fn = geom.filename
+                if convex and ".convex.stl" not in fn:
+                    fn = fn + ".convex.stl"
+                if not convex:
+                    raise ValueError("oracle supports convex=True only")
+                g = load_convex_mesh(os.path.join(self.urdf.directory, fn), geom.scale)
+            elif geom.kind == "box":
+                g = BoxGeom(geom.size)
+            else:
+                raise ValueError(f"oracle: unsupported link geometry {geom.kind}")
+            self.objects.append(CollisionObj(link_name, parent, origin.se3(), g))
+        for child in link.children:
+            self._fcl_dfs(child, link_name, convex)
+
+    def remove_pairs_from_srdf(self, srdf_path: str):
+        root = ET.parse(srdf_path).getroot()
+        names = [o.link for o in self.objects]
+        for node in root:
+            if node.tag != "disable_collisions":
+                continue
+            l1, l2 = node.get("link1"), node.get("link2")
+            self.pairs = [(a, b) for (a, b) in self.pairs
+                          if not ((names[a] == l1 and names[b] == l2) or (names[a] == l2 and names[b] == l1))]
+
+    def set_move_group(self, end_effectors):
+        if isinstance(end_effectors, str):
+            end_effectors = [end_effectors]
+        js = set()
+        for ee in end_effectors:
+            f = self.pin.frames[self.pin.body_frame(ee)]
+            for j in self.pin.supports(f.parent):
+                if j in self.user_joints:
+                    js.add(self.user_joints.index(j))
+        self.move_group = sorted(js)
+        self.qpos_dim = sum(self.user_nv[i] for i in self.move_group)
+
+    # qpos helpers ---------------------------------------------------------
+    def move_group_qpos_index(self) -> List[int]:
+        out = []
+        for i in self.move_group:
+            out += list(range(self.user_vidx[i], self.user_vidx[i] + self.user_nv[i]))
+        return out
+
+    def joint_limits(self) -> np.ndarray:
+        """Per user joint [lo, hi] (``PinocchioModelTpl::getJointLimit``)."""
+        rows = []
+        for j in self.user_joints:
+            if j == 0:
+                continue
+            pj = self.pin.joints[j]
+            if pj.nq == 1:
+                rows.append([pj.lower[0], pj.upper[0]])
+            else:
+                rows.append([-3.14159265359, 3.14159265359])
+        return np.array(rows, dtype=np.float64)
+
+
+def srdf_pairs_panda(urdf_path: str, srdf_path: str) -> List[Tuple[str, str]]:
+    art = Articulation(urdf_path, srdf_path)
+    return [(art.objects[a].link, art.objects[b].link) for a, b in art.pairs]
