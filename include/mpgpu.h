@@ -1,0 +1,198 @@
+/*
+ * mpgpu.h -- C ABI of the MI355X batched state-validity checker.
+ *
+ * This is the drop-in boundary beneath MPlib's PlanningWorld::collide() /
+ * collideFull() and the OMPL isStateValid() inner loop.  Plain C, plain
+ * pointers and sizes, no C++ or torch types; every call returns an int
+ * status (0 = ok) and never throws.  The text of the last error on the
+ * calling thread is available from mpg_last_error().
+ *
+ * Reference interfaces replaced (KolinGuo/MPlib 0.1.1, paths relative to the
+ * reference root):
+ *   mpg_world_create     <- the mutable FCL/pinocchio state that
+ *                           PlanningWorldTpl (src/planning_world.h:52-312),
+ *                           ArticulatedModelTpl (src/articulated_model.cpp:15-36),
+ *                           FCLModelTpl::init (src/fcl_model.cpp:268-294) and
+ *                           AllowedCollisionMatrix (src/collision_matrix.h) hold,
+ *                           frozen into an immutable device snapshot.
+ *   mpg_collide_batch    <- N x { PlanningWorldTpl::setQposAll(q)
+ *                                 (src/planning_world.cpp:250-262);
+ *                                 PlanningWorldTpl::collideFull(CollisionRequest())
+ *                                 (src/planning_world.cpp:484-490) }
+ *                           flags[i]  == collide() (src/planning_world.h:248-250)
+ *                           pair_mask == which pairs collideFull() reports,
+ *                           after filterCollisions (src/planning_world.cpp:265-274).
+ *                           Also the OMPL ValidityCheckerTpl::isValid batch
+ *                           (src/ompl_planner.h:59-62): valid = !flags[i].
+ *   mpg_fk_batch         <- N x { PinocchioModelTpl::computeForwardKinematics
+ *                                 (src/pinocchio_model.cpp:272-274);
+ *                                 getLinkPose(i) for every user link
+ *                                 (src/pinocchio_model.cpp:277-312) }
+ *   mpg_world_destroy    <- shared_ptr release of the above.
+ *
+ * Memory: buffers are caller-owned.  With MPG_MEM_DEVICE every pointer is a
+ * device pointer on the world's device and the work is enqueued on `stream`
+ * (a hipStream_t, NULL = default stream) without synchronising.  With
+ * MPG_MEM_HOST the call copies through internal device staging buffers and
+ * returns after the results are back on the host.
+ *
+ * Threading: a world is immutable after creation; concurrent calls on one
+ * world from several host threads are allowed when each uses its own stream
+ * and MPG_MEM_DEVICE.  MPG_MEM_HOST calls on one world are serialised.
+ */
+#ifndef MPGPU_H
+#define MPGPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MPG_VERSION_MAJOR 0
+#define MPG_VERSION_MINOR 1
+
+/* status codes */
+#define MPG_OK 0
+#define MPG_E_INVALID 1     /* bad argument / descriptor                    */
+#define MPG_E_UNSUPPORTED 2 /* request or geometry pair not implemented     */
+#define MPG_E_HIP 3         /* HIP runtime error                            */
+#define MPG_E_NOMEM 4
+
+/* memory kinds for the batch calls */
+#define MPG_MEM_HOST 0
+#define MPG_MEM_DEVICE 1
+
+/* pinocchio joint models (pinocchio 2.6.21 JointCollectionDefault subset) */
+#define MPG_JOINT_RX 0
+#define MPG_JOINT_RY 1
+#define MPG_JOINT_RZ 2
+#define MPG_JOINT_REVOLUTE_UNALIGNED 3
+#define MPG_JOINT_PX 4
+#define MPG_JOINT_PY 5
+#define MPG_JOINT_PZ 6
+#define MPG_JOINT_PRISMATIC_UNALIGNED 7
+#define MPG_JOINT_RUBX 8  /* continuous joints: user value v -> (cos v, sin v) */
+#define MPG_JOINT_RUBY 9
+#define MPG_JOINT_RUBZ 10
+#define MPG_JOINT_RUB_UNALIGNED 11
+
+/* FCL geometry kinds supported on the device */
+#define MPG_GEOM_CONVEX 0   /* fcl::Convex   : param unused, vertices        */
+#define MPG_GEOM_BOX 1      /* fcl::Box      : param = side x, y, z          */
+#define MPG_GEOM_SPHERE 2   /* fcl::Sphere   : param = radius                */
+#define MPG_GEOM_CAPSULE 3  /* fcl::Capsule  : param = radius, lz            */
+#define MPG_GEOM_CYLINDER 4 /* fcl::Cylinder : param = radius, lz            */
+
+/*
+ * World descriptor.  SE3 values are 12 doubles: a row-major 3x3 rotation
+ * followed by the translation.  All arrays are read during
+ * mpg_world_create only.
+ */
+typedef struct mpg_world_desc {
+  /* --- kinematics: pinocchio joints 1..n_joints (universe omitted) ------- */
+  int32_t n_joints;
+  const int32_t *joint_type;     /* MPG_JOINT_*                               */
+  const int32_t *joint_parent;   /* parent joint, 0 = universe, else 1-based  */
+  const double *joint_axis;      /* [n_joints*3] (unaligned joints only)      */
+  const double *joint_placement; /* [n_joints*12] model.jointPlacements       */
+  /* joint value source: dof slot d >= 0 reads q[i*dof + d]; -1 uses
+   * joint_value_const (fixed, non-move-group joints keep current_qpos_,
+   * src/articulated_model.cpp:104-113).                                    */
+  const int32_t *joint_q_source; /* [n_joints]                             */
+  const double *joint_q_const;   /* [n_joints]                             */
+  int32_t dof;                   /* move-group dimension = row length of q */
+
+  /* --- user links (PinocchioModel::setLinkOrder) ---------------------------- */
+  int32_t n_links;
+  const int32_t *link_parent;     /* frame.parent joint (0 = universe)      */
+  const double *link_placement;   /* [n_links*12] frame.placement           */
+
+  /* --- geometry ------------------------------------------------------------- */
+  int32_t n_geoms;
+  const int32_t *geom_type;       /* MPG_GEOM_*                             */
+  const int32_t *geom_vertex_start;
+  const int32_t *geom_vertex_count;
+  const double *geom_param;       /* [n_geoms*4]                            */
+  int64_t n_vertices;
+  const double *vertices;         /* [n_vertices*3] Convex vertices, local  */
+
+  /* --- moving objects: robot collision objects then attached bodies -------- */
+  int32_t n_moving;
+  const int32_t *moving_link;     /* user link index                        */
+  const int32_t *moving_geom;
+  const double *moving_offset;    /* [n_moving*12] link -> object pose      */
+
+  /* --- static scene objects -------------------------------------------------- */
+  int32_t n_static;
+  const int32_t *static_geom;
+  const double *static_transform; /* [n_static*12] world pose               */
+
+  /* --- pairs, in output-bit order. Object ids: [0, n_moving) moving,
+   *     [n_moving, n_moving + n_static) static.  (pair_a[p], pair_b[p]) keeps
+   *     fcl::collide's (o1, o2) argument order.                              */
+  int32_t n_pairs;
+  const int32_t *pair_a;
+  const int32_t *pair_b;
+  const uint8_t *pair_allowed;    /* 1: ACM allows it (never reported)      */
+
+  /* --- CollisionRequest -------------------------------------------------------- */
+  double gjk_tolerance;           /* CollisionRequest::gjk_tolerance (1e-6) */
+} mpg_world_desc;
+
+typedef struct mpg_world mpg_world;
+
+typedef struct mpg_world_info {
+  int32_t n_pairs;
+  int32_t mask_words; /* uint32 words per configuration in pair_mask      */
+  int32_t dof;
+  int32_t n_links;
+  int32_t device;
+  int32_t block_size;
+  int64_t snapshot_bytes;
+} mpg_world_info;
+
+/* Build an immutable device snapshot of the world on `device`. */
+int mpg_world_create(const mpg_world_desc *desc, int device, mpg_world **out);
+int mpg_world_destroy(mpg_world *world);
+int mpg_world_get_info(const mpg_world *world, mpg_world_info *info);
+
+/*
+ * q:         [n*dof] row-major move-group joint values (float64).
+ * flags:     [n] 1 if the configuration collides (collide() == true).
+ * pair_mask: [n*mask_words] bit p of word p/32 set if pair p is reported by
+ *            collideFull(); may be NULL when only flags are wanted.
+ */
+int mpg_collide_batch(mpg_world *world, const double *q, int64_t n, uint8_t *flags,
+                      uint32_t *pair_mask, int mem, void *stream);
+
+/*
+ * Same pair evaluation as mpg_collide_batch, but the link poses are given
+ * directly instead of being computed from joint values:
+ * link_pose [n*n_links*7] = (px, py, pz, qw, qx, qy, qz) per user link.
+ * Replaces FCLModelTpl::updateCollisionObjects(vector<Vector7>)
+ * (src/fcl_model.cpp:151-167) followed by FCLModelTpl::collideFull
+ * (src/fcl_model.cpp:182-193).
+ */
+int mpg_collide_link_poses(mpg_world *world, const double *link_pose, int64_t n, uint8_t *flags,
+                           uint32_t *pair_mask, int mem, void *stream);
+
+/* link_pose: [n*n_links*7] = getLinkPose(l) -> (px, py, pz, qw, qx, qy, qz). */
+int mpg_fk_batch(mpg_world *world, const double *q, int64_t n, double *link_pose, int mem,
+                 void *stream);
+
+/* Diagnostics: the device sin/cos used by the FK (host buffers). */
+int mpg_debug_sincos(const double *x, int64_t n, double *s, double *c, int device);
+
+/* Synchronise the world's device (used after MPG_MEM_DEVICE calls). */
+int mpg_synchronize(int device);
+
+int mpg_device_count(int *count);
+const char *mpg_last_error(void);
+const char *mpg_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MPGPU_H */

@@ -1,0 +1,503 @@
+// pymp.cpp -- pybind11 module ``mplib_amd.pymp``: the reference's
+// ``mplib.pymp`` API surface (python/pybind.cpp:16-27 and the
+// python/pybind_*.hpp files it includes) for the components on the
+// collision/validity path, plus the batched entry points.  Every evaluation
+// goes to the HIP library (include/mpgpu.h); there is no CPU path.
+#include <pybind11/numpy.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include "host.hpp"
+
+namespace py = pybind11;
+using namespace mpgh;
+
+namespace {
+
+std::array<double, 4> quat_arg(const std::vector<double>& q) {
+  if (q.size() != 4) throw std::invalid_argument("quaternion must have 4 elements (w, x, y, z)");
+  return {q[0], q[1], q[2], q[3]};
+}
+Vec3 vec3_arg(const std::vector<double>& v) {
+  if (v.size() != 3) throw std::invalid_argument("expected 3 elements");
+  return {v[0], v[1], v[2]};
+}
+Vec7 vec7_arg(const std::vector<double>& v) {
+  if (v.size() != 7) throw std::invalid_argument("pose must have 7 elements (x, y, z, qw, qx, qy, qz)");
+  Vec7 o;
+  for (int i = 0; i < 7; ++i) o[i] = v[i];
+  return o;
+}
+py::array_t<double> mat3(const SE3& T) {
+  py::array_t<double> a({3, 3});
+  auto m = a.mutable_unchecked<2>();
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) m(i, j) = T.R[3 * i + j];
+  return a;
+}
+py::array_t<double> vec(const double* p, int n) {
+  py::array_t<double> a(n);
+  auto m = a.mutable_unchecked<1>();
+  for (int i = 0; i < n; ++i) m(i) = p[i];
+  return a;
+}
+
+// NotImplemented-style errors from the host become NotImplementedError.
+void translate_exceptions() {
+  py::register_exception_translator([](std::exception_ptr p) {
+    try {
+      if (p) std::rethrow_exception(p);
+    } catch (const std::logic_error& e) {
+      std::string m = e.what();
+      if (m.rfind("NotImplemented: ", 0) == 0) {
+        PyErr_SetString(PyExc_NotImplementedError, m.substr(16).c_str());
+        return;
+      }
+      if (dynamic_cast<const std::invalid_argument*>(&e)) {
+        PyErr_SetString(PyExc_ValueError, m.c_str());
+        return;
+      }
+      if (dynamic_cast<const std::out_of_range*>(&e)) {
+        PyErr_SetString(PyExc_IndexError, m.c_str());
+        return;
+      }
+      PyErr_SetString(PyExc_RuntimeError, m.c_str());
+    }
+  });
+}
+
+}  // namespace
+
+PYBIND11_MODULE(pymp, m_all) {
+  m_all.doc() = "mplib_amd.pymp -- MI355X-native MPlib collision/validity path";
+  translate_exceptions();
+  m_all.def("set_global_seed", &set_global_seed, py::arg("seed"));
+  m_all.def("device_version", []() { return std::string(mpg_version()); });
+
+  // ------------------------------------------------------------------ fcl
+  auto m = m_all.def_submodule("fcl");
+  py::class_<CollisionGeometry, std::shared_ptr<CollisionGeometry>>(m, "CollisionGeometry")
+      .def_readonly("kind", &CollisionGeometry::kind);
+  py::class_<Box, CollisionGeometry, std::shared_ptr<Box>>(m, "Box")
+      .def(py::init([](const std::vector<double>& s) { return std::make_shared<Box>(vec3_arg(s)); }), py::arg("side"))
+      .def(py::init([](double x, double y, double z) { return std::make_shared<Box>(Vec3{x, y, z}); }), py::arg("x"),
+           py::arg("y"), py::arg("z"))
+      .def_readwrite("side", &Box::side);
+  py::class_<Sphere, CollisionGeometry, std::shared_ptr<Sphere>>(m, "Sphere")
+      .def(py::init<double>(), py::arg("radius"))
+      .def_readwrite("radius", &Sphere::radius);
+  py::class_<Capsule, CollisionGeometry, std::shared_ptr<Capsule>>(m, "Capsule")
+      .def(py::init<double, double>(), py::arg("radius"), py::arg("lz"))
+      .def_readwrite("radius", &Capsule::radius)
+      .def_readwrite("lz", &Capsule::lz);
+  py::class_<Cylinder, CollisionGeometry, std::shared_ptr<Cylinder>>(m, "Cylinder")
+      .def(py::init<double, double>(), py::arg("radius"), py::arg("lz"))
+      .def_readwrite("radius", &Cylinder::radius)
+      .def_readwrite("lz", &Cylinder::lz);
+  py::class_<Convex, CollisionGeometry, std::shared_ptr<Convex>>(m, "Convex")
+      .def(py::init([](py::array_t<double, py::array::c_style | py::array::forcecast> v,
+                       py::array_t<int, py::array::c_style | py::array::forcecast> f, bool throw_if_invalid) {
+             (void)throw_if_invalid;
+             if (v.ndim() != 2 || v.shape(1) != 3) throw std::invalid_argument("vertices must be [N, 3]");
+             if (f.ndim() != 2 || f.shape(1) != 3) throw std::invalid_argument("faces must be [M, 3]");
+             std::vector<Vec3> vv;
+             auto a = v.unchecked<2>();
+             for (ssize_t i = 0; i < v.shape(0); ++i) vv.push_back({a(i, 0), a(i, 1), a(i, 2)});
+             std::vector<int> ff;
+             auto b = f.unchecked<2>();
+             for (ssize_t i = 0; i < f.shape(0); ++i) {
+               ff.push_back(3);
+               for (int k = 0; k < 3; ++k) {
+                 if (b(i, k) < 0 || b(i, k) >= (int)vv.size()) throw std::invalid_argument("face index out of range");
+                 ff.push_back(b(i, k));
+               }
+             }
+             return std::make_shared<Convex>(std::move(vv), (int)f.shape(0), std::move(ff));
+           }),
+           py::arg("vertices"), py::arg("faces"), py::arg("throw_if_invalid") = true)
+      .def("get_face_count", [](const Convex& c) { return c.num_faces; })
+      .def("get_faces", [](const Convex& c) { return c.faces; })
+      .def("get_vertices",
+           [](const Convex& c) {
+             py::array_t<double> a({(ssize_t)c.vertices.size(), (ssize_t)3});
+             auto x = a.mutable_unchecked<2>();
+             for (size_t i = 0; i < c.vertices.size(); ++i)
+               for (int k = 0; k < 3; ++k) x(i, k) = c.vertices[i][k];
+             return a;
+           })
+      .def("get_interior_point", [](const Convex& c) {
+        auto p = c.interior_point();
+        return vec(p.data(), 3);
+      });
+
+  py::class_<CollisionObject, std::shared_ptr<CollisionObject>>(m, "CollisionObject")
+      .def(py::init([](const GeomPtr& g, const std::vector<double>& p, const std::vector<double>& q) {
+             return std::make_shared<CollisionObject>(g, se3_from_pq(vec3_arg(p), quat_arg(q)));
+           }),
+           py::arg("collision_geometry"), py::arg("position") = std::vector<double>{0, 0, 0},
+           py::arg("quaternion") = std::vector<double>{1, 0, 0, 0})
+      .def("get_collision_geometry", [](const CollisionObject& o) { return o.geom; })
+      .def("get_translation", [](const CollisionObject& o) { return vec(o.tf.p, 3); })
+      .def("get_rotation", [](const CollisionObject& o) { return mat3(o.tf); })
+      .def("set_transformation",
+           [](CollisionObject& o, const std::vector<double>& pose) { o.set_transform(se3_from_pose7(vec7_arg(pose))); },
+           py::arg("pose"));
+
+  py::enum_<GJKSolverType>(m, "GJKSolverType")
+      .value("GST_LIBCCD", GST_LIBCCD)
+      .value("GST_INDEP", GST_INDEP)
+      .export_values();
+
+  py::class_<CollisionRequest, std::shared_ptr<CollisionRequest>>(m, "CollisionRequest")
+      .def(py::init([](size_t nmc, bool ec, size_t nmcs, bool ecost, bool uac, GJKSolverType t, double tol) {
+             CollisionRequest r;
+             r.num_max_contacts = nmc;
+             r.enable_contact = ec;
+             r.num_max_cost_sources = nmcs;
+             r.enable_cost = ecost;
+             r.use_approximate_cost = uac;
+             r.gjk_solver_type = t;
+             r.gjk_tolerance = tol;
+             return r;
+           }),
+           py::arg("num_max_contacts") = 1, py::arg("enable_contact") = false, py::arg("num_max_cost_sources") = 1,
+           py::arg("enable_cost") = false, py::arg("use_approximate_cost") = true,
+           py::arg("gjk_solver_type") = GST_LIBCCD, py::arg("gjk_tolerance") = 1e-6)
+      .def_readwrite("num_max_contacts", &CollisionRequest::num_max_contacts)
+      .def_readwrite("enable_contact", &CollisionRequest::enable_contact)
+      .def_readwrite("gjk_solver_type", &CollisionRequest::gjk_solver_type)
+      .def_readwrite("gjk_tolerance", &CollisionRequest::gjk_tolerance)
+      .def("isSatisfied", [](const CollisionRequest& r, const CollisionResult& res) {
+        return !r.enable_cost && res.num_contacts() >= r.num_max_contacts;
+      }, py::arg("result"));
+
+  py::class_<Contact, std::shared_ptr<Contact>>(m, "Contact")
+      .def(py::init<>())
+      .def_readonly("normal", &Contact::normal)
+      .def_readonly("pos", &Contact::pos)
+      .def_readonly("penetration_depth", &Contact::penetration_depth);
+
+  py::class_<CollisionResult, std::shared_ptr<CollisionResult>>(m, "CollisionResult")
+      .def(py::init<>())
+      .def("is_collision", &CollisionResult::is_collision)
+      .def("num_contacts", &CollisionResult::num_contacts)
+      .def("get_contacts", [](const CollisionResult& r) { return r.contacts; })
+      .def("get_contact", [](const CollisionResult& r, size_t i) { return r.contacts.at(i); }, py::arg("i"))
+      .def("clear", &CollisionResult::clear);
+
+  py::class_<FCLModel, std::shared_ptr<FCLModel>>(m, "FCLModel")
+      .def(py::init([](const std::string& urdf, bool verbose, bool convex) {
+             return FCLModel::from_file(urdf, verbose, convex);
+           }),
+           py::arg("urdf_filename"), py::arg("verbose") = true, py::arg("convex") = false)
+      .def_static("create_from_urdf_string", &FCLModel::from_urdf_string, py::arg("urdf_string"),
+                  py::arg("collision_links"), py::arg("verbose") = true)
+      .def("get_collision_pairs", &FCLModel::get_collision_pairs)
+      .def("get_collision_objects", &FCLModel::get_collision_objects)
+      .def("get_collision_link_names", &FCLModel::get_collision_link_names)
+      .def("set_link_order", &FCLModel::set_link_order, py::arg("names"))
+      .def("remove_collision_pairs_from_srdf", &FCLModel::remove_collision_pairs_from_srdf, py::arg("srdf_filename"))
+      .def("update_collision_objects",
+           [](FCLModel& f, const std::vector<std::vector<double>>& poses) {
+             std::vector<Vec7> p;
+             for (auto& v : poses) p.push_back(vec7_arg(v));
+             f.update_collision_objects(p);
+           },
+           py::arg("link_poses"))
+      .def("collide", &FCLModel::collide, py::arg("request") = CollisionRequest(),
+           py::call_guard<py::gil_scoped_release>())
+      .def("collide_full", &FCLModel::collide_full, py::arg("request") = CollisionRequest(),
+           py::call_guard<py::gil_scoped_release>())
+      .def("print_collision_pairs", &FCLModel::print_collision_pairs);
+
+  m.def("load_mesh_as_Convex",
+        [](const std::string& path, const std::vector<double>& scale) {
+          return load_mesh_as_convex(path, vec3_arg(scale));
+        },
+        py::arg("mesh_path"), py::arg("scale"));
+  m.def(
+      "collide",
+      [](const ObjPtr& o1, const ObjPtr& o2, const CollisionRequest& req) {
+        // fcl::collide(o1, o2): a two-object world evaluated on the device
+        req.check_supported();
+        DescBuilder d;
+        d.gjk_tolerance = req.gjk_tolerance;
+        d.link_parent.push_back(0);
+        SE3 I;
+        mpg::se3_identity(I);
+        push_se3(d.link_placement, I);
+        d.moving_link.push_back(0);
+        d.moving_geom.push_back(d.add_geometry(o1->geom.get()));
+        push_se3(d.moving_offset, o1->tf);
+        d.static_geom.push_back(d.add_geometry(o2->geom.get()));
+        push_se3(d.static_transform, o2->tf);
+        d.pair_a.push_back(0);
+        d.pair_b.push_back(1);
+        d.pair_allowed.push_back(0);
+        DeviceWorld w(d, default_device());
+        const double pose[7] = {0, 0, 0, 1, 0, 0, 0};
+        uint8_t flag = 0;
+        uint32_t mask = 0;
+        check_status(mpg_collide_link_poses(w.get(), pose, 1, &flag, &mask, MPG_MEM_HOST, nullptr),
+                     "mpg_collide_link_poses");
+        CollisionResult r;
+        if (flag) {
+          Contact c;
+          c.o1 = o1->geom;
+          c.o2 = o2->geom;
+          r.contacts.push_back(c);
+        }
+        return r;
+      },
+      py::arg("o1"), py::arg("o2"), py::arg("request") = CollisionRequest());
+
+  // ------------------------------------------------------------ pinocchio
+  auto mp = m_all.def_submodule("pinocchio");
+  py::class_<PinocchioModel, std::shared_ptr<PinocchioModel>>(mp, "PinocchioModel")
+      .def(py::init([](const std::string& urdf, const std::vector<double>& g, bool verbose) {
+             return PinocchioModel::from_file(urdf, vec3_arg(g), verbose);
+           }),
+           py::arg("urdf_filename"), py::arg("gravity") = std::vector<double>{0, 0, -9.81}, py::arg("verbose") = true)
+      .def_static("create_from_urdf_string",
+                  [](const std::string& urdf, const std::vector<double>& g, bool verbose) {
+                    return PinocchioModel::from_string(urdf, vec3_arg(g), verbose);
+                  },
+                  py::arg("urdf_string"), py::arg("gravity") = std::vector<double>{0, 0, -9.81},
+                  py::arg("verbose") = true)
+      .def("set_joint_order", &PinocchioModel::set_joint_order, py::arg("names"))
+      .def("set_link_order", &PinocchioModel::set_link_order, py::arg("names"))
+      .def("compute_forward_kinematics", &PinocchioModel::compute_forward_kinematics, py::arg("qpos"))
+      .def("get_link_pose",
+           [](const PinocchioModel& p, size_t i) {
+             auto v = p.get_link_pose(i);
+             return vec(v.data(), 7);
+           },
+           py::arg("index"))
+      .def("get_random_configuration", &PinocchioModel::get_random_configuration)
+      .def("get_joint_names", &PinocchioModel::get_joint_names, py::arg("user") = true)
+      .def("get_link_names", &PinocchioModel::get_link_names, py::arg("user") = true)
+      .def("get_leaf_links", &PinocchioModel::get_leaf_links)
+      .def("get_joint_dim", &PinocchioModel::get_joint_dim, py::arg("index"), py::arg("user") = true)
+      .def("get_joint_dims", &PinocchioModel::get_joint_dims, py::arg("user") = true)
+      .def("get_joint_id", &PinocchioModel::get_joint_id, py::arg("index"), py::arg("user") = true)
+      .def("get_joint_ids", &PinocchioModel::get_joint_ids, py::arg("user") = true)
+      .def("get_parents", &PinocchioModel::get_parents, py::arg("user") = true)
+      .def("get_joint_type", &PinocchioModel::get_joint_type, py::arg("index"), py::arg("user") = true)
+      .def("get_joint_types", &PinocchioModel::get_joint_types, py::arg("user") = true)
+      .def("get_joint_limit", &PinocchioModel::get_joint_limit, py::arg("index"), py::arg("user") = true)
+      .def("get_joint_limits", &PinocchioModel::get_joint_limits, py::arg("user") = true)
+      .def("get_chain_joint_name", &PinocchioModel::get_chain_joint_name, py::arg("end_effector"))
+      .def("get_chain_joint_index", &PinocchioModel::get_chain_joint_index, py::arg("end_effector"));
+
+  // ---------------------------------------------------------- articulation
+  auto ma = m_all.def_submodule("articulation");
+  py::class_<ArticulatedModel, std::shared_ptr<ArticulatedModel>>(ma, "ArticulatedModel")
+      .def(py::init([](const std::string& urdf, const std::string& srdf, const std::vector<double>& g,
+                       const std::vector<std::string>& joints, const std::vector<std::string>& links, bool verbose,
+                       bool convex) {
+             return ArticulatedModel::create(urdf, srdf, vec3_arg(g), joints, links, verbose, convex);
+           }),
+           py::arg("urdf_filename"), py::arg("srdf_filename"), py::arg("gravity") = std::vector<double>{0, 0, -9.81},
+           py::arg("joint_names") = std::vector<std::string>(), py::arg("link_names") = std::vector<std::string>(),
+           py::arg("verbose") = true, py::arg("convex") = false)
+      .def_static("create_from_urdf_string",
+                  [](const std::string& urdf, const std::string& srdf,
+                     const std::vector<std::pair<std::string, std::vector<ObjPtr>>>& links,
+                     const std::vector<double>& g, const std::vector<std::string>& joints,
+                     const std::vector<std::string>& lnames, bool verbose) {
+                    return ArticulatedModel::create_from_urdf_string(urdf, srdf, links, vec3_arg(g), joints, lnames,
+                                                                     verbose);
+                  },
+                  py::arg("urdf_string"), py::arg("srdf_string"), py::arg("collision_links"),
+                  py::arg("gravity") = std::vector<double>{0, 0, -9.81},
+                  py::arg("joint_names") = std::vector<std::string>(),
+                  py::arg("link_names") = std::vector<std::string>(), py::arg("verbose") = true)
+      .def("get_pinocchio_model", &ArticulatedModel::get_pinocchio_model)
+      .def("get_fcl_model", &ArticulatedModel::get_fcl_model)
+      .def("get_user_link_names", &ArticulatedModel::get_user_link_names)
+      .def("get_user_joint_names", &ArticulatedModel::get_user_joint_names)
+      .def("get_move_group_joint_indices", &ArticulatedModel::get_move_group_joint_indices)
+      .def("get_move_group_end_effectors", &ArticulatedModel::get_move_group_end_effectors)
+      .def("get_move_group_joint_names", &ArticulatedModel::get_move_group_joint_names)
+      .def("set_move_group",
+           [](ArticulatedModel& a, const std::string& ee) { a.set_move_group(std::vector<std::string>{ee}); },
+           py::arg("end_effector"))
+      .def("set_move_group",
+           [](ArticulatedModel& a, const std::vector<std::string>& ees) { a.set_move_group(ees); },
+           py::arg("end_effectors"))
+      .def("get_qpos", [](const ArticulatedModel& a) { return vec(a.get_qpos().data(), (int)a.get_qpos().size()); })
+      .def("set_qpos", &ArticulatedModel::set_qpos, py::arg("qpos"), py::arg("full") = false)
+      .def("get_qpos_dim", &ArticulatedModel::get_qpos_dim)
+      .def("update_SRDF", &ArticulatedModel::update_srdf, py::arg("SRDF"))
+      .def("get_name", &ArticulatedModel::get_name);
+
+  // ------------------------------------------------------ collision_matrix
+  auto mc = m_all.def_submodule("collision_matrix");
+  py::enum_<AllowedCollision>(mc, "AllowedCollision")
+      .value("NEVER", AllowedCollision::NEVER)
+      .value("ALWAYS", AllowedCollision::ALWAYS)
+      .value("CONDITIONAL", AllowedCollision::CONDITIONAL)
+      .export_values();
+  using ACM = AllowedCollisionMatrix;
+  using S = std::string;
+  using VS = std::vector<std::string>;
+  py::class_<ACM, std::shared_ptr<ACM>>(mc, "AllowedCollisionMatrix")
+      .def(py::init<>())
+      .def("get_entry", &ACM::get_entry, py::arg("name1"), py::arg("name2"))
+      .def("has_entry", py::overload_cast<const S&>(&ACM::has_entry, py::const_), py::arg("name"))
+      .def("has_entry", py::overload_cast<const S&, const S&>(&ACM::has_entry, py::const_), py::arg("name1"),
+           py::arg("name2"))
+      .def("set_entry", py::overload_cast<const S&, const S&, bool>(&ACM::set_entry), py::arg("name1"),
+           py::arg("name2"), py::arg("allowed"))
+      .def("set_entry", py::overload_cast<const S&, const VS&, bool>(&ACM::set_entry), py::arg("name"),
+           py::arg("other_names"), py::arg("allowed"))
+      .def("set_entry", py::overload_cast<const VS&, const VS&, bool>(&ACM::set_entry), py::arg("names1"),
+           py::arg("names2"), py::arg("allowed"))
+      .def("set_entry", py::overload_cast<const S&, bool>(&ACM::set_entry), py::arg("name"), py::arg("allowed"))
+      .def("set_entry", py::overload_cast<const VS&, bool>(&ACM::set_entry), py::arg("names"), py::arg("allowed"))
+      .def("set_entry", py::overload_cast<bool>(&ACM::set_entry), py::arg("allowed"))
+      .def("remove_entry", py::overload_cast<const S&, const S&>(&ACM::remove_entry), py::arg("name1"),
+           py::arg("name2"))
+      .def("remove_entry", py::overload_cast<const S&, const VS&>(&ACM::remove_entry), py::arg("name"),
+           py::arg("other_names"))
+      .def("remove_entry", py::overload_cast<const VS&, const VS&>(&ACM::remove_entry), py::arg("names1"),
+           py::arg("names2"))
+      .def("remove_entry", py::overload_cast<const S&>(&ACM::remove_entry), py::arg("name"))
+      .def("remove_entry", py::overload_cast<const VS&>(&ACM::remove_entry), py::arg("names"))
+      .def("__len__", &ACM::get_size)
+      .def("get_default_entry", &ACM::get_default_entry, py::arg("name"))
+      .def("has_default_entry", &ACM::has_default_entry, py::arg("name"))
+      .def("set_default_entry", py::overload_cast<const S&, bool>(&ACM::set_default_entry), py::arg("name"),
+           py::arg("allowed"))
+      .def("set_default_entry", py::overload_cast<const VS&, bool>(&ACM::set_default_entry), py::arg("names"),
+           py::arg("allowed"))
+      .def("remove_default_entry", py::overload_cast<const S&>(&ACM::remove_default_entry), py::arg("name"))
+      .def("remove_default_entry", py::overload_cast<const VS&>(&ACM::remove_default_entry), py::arg("names"))
+      .def("get_allowed_collision", &ACM::get_allowed_collision, py::arg("name1"), py::arg("name2"))
+      .def("clear", &ACM::clear)
+      .def("get_all_entry_names", &ACM::get_all_entry_names)
+      .def("__str__", &ACM::print);
+
+  // -------------------------------------------------------- planning_world
+  auto mw = m_all.def_submodule("planning_world");
+  py::class_<AttachedBody, std::shared_ptr<AttachedBody>>(mw, "AttachedBody")
+      .def("get_name", [](const AttachedBody& b) { return b.name; })
+      .def("get_object", [](const AttachedBody& b) { return b.object; })
+      .def("get_attached_articulation", [](const AttachedBody& b) { return b.articulation; })
+      .def("get_attached_link_id", [](const AttachedBody& b) { return b.link_id; })
+      .def("get_touch_links", [](const AttachedBody& b) { return b.touch_links; })
+      .def("set_touch_links", [](AttachedBody& b, const VS& t) { b.touch_links = t; });
+
+  py::class_<WorldCollisionResult, std::shared_ptr<WorldCollisionResult>>(mw, "WorldCollisionResult")
+      .def(py::init<>())
+      .def_readwrite("res", &WorldCollisionResult::res)
+      .def_readwrite("collision_type", &WorldCollisionResult::collision_type)
+      .def_readwrite("object_name1", &WorldCollisionResult::object_name1)
+      .def_readwrite("object_name2", &WorldCollisionResult::object_name2)
+      .def_readwrite("link_name1", &WorldCollisionResult::link_name1)
+      .def_readwrite("link_name2", &WorldCollisionResult::link_name2);
+
+  using PW = PlanningWorld;
+  py::class_<PW, std::shared_ptr<PW>>(mw, "PlanningWorld")
+      .def(py::init<const std::vector<ArtPtr>&, const VS&, const std::vector<ObjPtr>&, const VS&>(),
+           py::arg("articulations"), py::arg("articulation_names"),
+           py::arg("normal_objects") = std::vector<ObjPtr>(), py::arg("normal_object_names") = VS())
+      .def("get_articulation_names", &PW::get_articulation_names)
+      .def("get_planned_articulations", &PW::get_planned_articulations)
+      .def("get_articulation", &PW::get_articulation, py::arg("name"))
+      .def("has_articulation", &PW::has_articulation, py::arg("name"))
+      .def("add_articulation", &PW::add_articulation, py::arg("name"), py::arg("model"), py::arg("planned") = false)
+      .def("remove_articulation", &PW::remove_articulation, py::arg("name"))
+      .def("is_articulation_planned", &PW::is_articulation_planned, py::arg("name"))
+      .def("set_articulation_planned", &PW::set_articulation_planned, py::arg("name"), py::arg("planned"))
+      .def("get_normal_object_names", &PW::get_normal_object_names)
+      .def("get_normal_object", &PW::get_normal_object, py::arg("name"))
+      .def("has_normal_object", &PW::has_normal_object, py::arg("name"))
+      .def("add_normal_object", &PW::add_normal_object, py::arg("name"), py::arg("collision_object"))
+      .def("remove_normal_object", &PW::remove_normal_object, py::arg("name"))
+      .def("is_normal_object_attached", &PW::is_normal_object_attached, py::arg("name"))
+      .def("get_attached_object", &PW::get_attached_object, py::arg("name"))
+      .def("attach_object",
+           [](PW& w, const S& n, const S& art, int link, const std::vector<double>& pose, const VS& touch) {
+             w.attach_object(n, art, link, vec7_arg(pose), touch);
+           },
+           py::arg("name"), py::arg("art_name"), py::arg("link_id"), py::arg("pose"), py::arg("touch_links"))
+      .def("attach_object",
+           [](PW& w, const S& n, const S& art, int link, const std::vector<double>& pose) {
+             w.attach_object(n, art, link, vec7_arg(pose));
+           },
+           py::arg("name"), py::arg("art_name"), py::arg("link_id"), py::arg("pose"))
+      .def("attach_object",
+           [](PW& w, const S& n, const GeomPtr& g, const S& art, int link, const std::vector<double>& pose,
+              const VS& touch) { w.attach_object(n, g, art, link, vec7_arg(pose), touch); },
+           py::arg("name"), py::arg("p_geom"), py::arg("art_name"), py::arg("link_id"), py::arg("pose"),
+           py::arg("touch_links"))
+      .def("attach_object",
+           [](PW& w, const S& n, const GeomPtr& g, const S& art, int link, const std::vector<double>& pose) {
+             w.attach_object(n, g, art, link, vec7_arg(pose));
+           },
+           py::arg("name"), py::arg("p_geom"), py::arg("art_name"), py::arg("link_id"), py::arg("pose"))
+      .def("attach_sphere",
+           [](PW& w, double r, const S& art, int link, const std::vector<double>& pose) {
+             w.attach_sphere(r, art, link, vec7_arg(pose));
+           },
+           py::arg("radius"), py::arg("art_name"), py::arg("link_id"), py::arg("pose"))
+      .def("attach_box",
+           [](PW& w, const std::vector<double>& size, const S& art, int link, const std::vector<double>& pose) {
+             w.attach_box(vec3_arg(size), art, link, vec7_arg(pose));
+           },
+           py::arg("size"), py::arg("art_name"), py::arg("link_id"), py::arg("pose"))
+      .def("attach_mesh",
+           [](PW& w, const S& path, const S& art, int link, const std::vector<double>& pose) {
+             w.attach_mesh(path, art, link, vec7_arg(pose));
+           },
+           py::arg("mesh_path"), py::arg("art_name"), py::arg("link_id"), py::arg("pose"))
+      .def("detach_object", &PW::detach_object, py::arg("name"), py::arg("also_remove") = false)
+      .def("set_qpos", &PW::set_qpos, py::arg("name"), py::arg("qpos"))
+      .def("set_qpos_all", &PW::set_qpos_all, py::arg("state"))
+      .def("get_allowed_collision_matrix", &PW::get_allowed_collision_matrix)
+      .def("collide", &PW::collide, py::arg("request") = CollisionRequest())
+      .def("self_collide", &PW::self_collide, py::arg("request") = CollisionRequest())
+      .def("collide_with_others", &PW::collide_with_others, py::arg("request") = CollisionRequest())
+      .def("collide_full", &PW::collide_full, py::arg("request") = CollisionRequest())
+      // ---- batched validity (new; one device launch for N states) ----
+      .def("get_state_dim", &PW::state_dim)
+      .def("get_mask_words", &PW::mask_words)
+      .def("get_collision_pair_info",
+           [](PW& w) {
+             py::list out;
+             for (auto& p : w.pair_table())
+               out.append(py::make_tuple(p.collision_type, p.object_name1, p.object_name2, p.link_name1,
+                                         p.link_name2, p.allowed, p.self));
+             return out;
+           })
+      .def("collide_batch",
+           [](PW& w, py::array_t<double, py::array::c_style | py::array::forcecast> states) {
+             const int dim = w.state_dim();
+             if (states.ndim() != 2 || states.shape(1) != dim)
+               throw std::invalid_argument("states must be [N, " + std::to_string(dim) + "] float64");
+             const int64_t n = states.shape(0);
+             const int W = w.mask_words();
+             py::array_t<uint8_t> flags(n);
+             py::array_t<uint32_t> masks({(ssize_t)n, (ssize_t)W});
+             const double* q = states.data();
+             uint8_t* f = flags.mutable_data();
+             uint32_t* mk = masks.mutable_data();
+             {
+               py::gil_scoped_release rel;
+               w.collide_batch(q, n, f, mk);
+             }
+             return py::make_tuple(flags, masks);
+           },
+           py::arg("states"),
+           "Batched collide(): flags[i] = collide() at states[i]; bit p of masks[i] = pair p reported by "
+           "collide_full() (see get_collision_pair_info()).")
+      .def("collide_batch_device",
+           [](PW& w, uintptr_t q, int64_t n, uintptr_t flags, uintptr_t masks, uintptr_t stream) {
+             w.collide_batch_device(reinterpret_cast<const void*>(q), n, reinterpret_cast<void*>(flags),
+                                    reinterpret_cast<void*>(masks), reinterpret_cast<void*>(stream));
+           },
+           py::arg("states_ptr"), py::arg("n"), py::arg("flags_ptr"), py::arg("masks_ptr") = 0,
+           py::arg("stream") = 0,
+           "Enqueue the batched check on device buffers (float64 [n, dim], uint8 [n], uint32 [n, W]).");
+}

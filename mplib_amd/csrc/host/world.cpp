@@ -1,0 +1,587 @@
+// world.cpp -- AllowedCollisionMatrix and PlanningWorld.
+//
+// AllowedCollisionMatrix restates src/collision_matrix.cpp (entries + default
+// entries, getAllowedCollision = entry, else combined default entries).
+// PlanningWorld restates src/planning_world.cpp: the pair loops of
+// selfCollide (:277-369) and collideWithOthers (:372-481) become one pair
+// table, in the same (o1, o2) argument order, and filterCollisions (:265-274)
+// becomes a per-pair "allowed" bit resolved when the device snapshot is built.
+// The snapshot is rebuilt whenever the world, the ACM, an object pose, or a
+// constant joint value changes.
+#include <algorithm>
+#include <cmath>
+#include <cstdlib>
+#include <cstring>
+#include <set>
+#include <sstream>
+
+#include "host.hpp"
+
+namespace mpgh {
+
+// ===========================================================================
+// AllowedCollisionMatrix
+// ===========================================================================
+std::optional<AllowedCollision> AllowedCollisionMatrix::get_entry(const std::string& a, const std::string& b) const {
+  auto i = entries_.find(a);
+  if (i == entries_.end()) return std::nullopt;
+  auto j = i->second.find(b);
+  if (j == i->second.end()) return std::nullopt;
+  return j->second;
+}
+bool AllowedCollisionMatrix::has_entry(const std::string& a, const std::string& b) const {
+  auto i = entries_.find(a);
+  return i != entries_.end() && i->second.count(b) > 0;
+}
+void AllowedCollisionMatrix::set_entry(const std::string& a, const std::string& b, bool allowed) {
+  const auto v = allowed ? AllowedCollision::ALWAYS : AllowedCollision::NEVER;
+  entries_[a][b] = entries_[b][a] = v;
+  ++version_;
+}
+void AllowedCollisionMatrix::set_entry(const std::string& a, const std::vector<std::string>& others, bool allowed) {
+  for (auto& o : others)
+    if (o != a) set_entry(o, a, allowed);
+}
+void AllowedCollisionMatrix::set_entry(const std::vector<std::string>& a, const std::vector<std::string>& b,
+                                       bool allowed) {
+  for (auto& x : a) set_entry(x, b, allowed);
+}
+void AllowedCollisionMatrix::set_entry(const std::string& a, bool allowed) {
+  std::vector<std::string> keys;
+  for (auto& e : entries_) keys.push_back(e.first);
+  for (auto& k : keys)
+    if (k != a) set_entry(a, k, allowed);
+}
+void AllowedCollisionMatrix::set_entry(const std::vector<std::string>& a, bool allowed) {
+  for (auto& x : a) set_entry(x, allowed);
+}
+void AllowedCollisionMatrix::set_entry(bool allowed) {
+  const auto v = allowed ? AllowedCollision::ALWAYS : AllowedCollision::NEVER;
+  for (auto& e : entries_)
+    for (auto& f : e.second) f.second = v;
+  ++version_;
+}
+void AllowedCollisionMatrix::remove_entry(const std::string& a, const std::string& b) {
+  if (auto it = entries_.find(a); it != entries_.end())
+    if (it->second.erase(b) == 1 && it->second.empty()) entries_.erase(it);
+  if (auto it = entries_.find(b); it != entries_.end())
+    if (it->second.erase(a) == 1 && it->second.empty()) entries_.erase(it);
+  ++version_;
+}
+void AllowedCollisionMatrix::remove_entry(const std::string& a, const std::vector<std::string>& others) {
+  for (auto& o : others)
+    if (o != a) remove_entry(o, a);
+}
+void AllowedCollisionMatrix::remove_entry(const std::vector<std::string>& a, const std::vector<std::string>& b) {
+  for (auto& x : a) remove_entry(x, b);
+}
+void AllowedCollisionMatrix::remove_entry(const std::string& a) {
+  entries_.erase(a);
+  for (auto it = entries_.begin(); it != entries_.end();)
+    if (it->second.erase(a) == 1 && it->second.empty()) it = entries_.erase(it);
+    else ++it;
+  ++version_;
+}
+void AllowedCollisionMatrix::remove_entry(const std::vector<std::string>& a) {
+  for (auto& x : a) remove_entry(x);
+}
+std::optional<AllowedCollision> AllowedCollisionMatrix::get_default_entry(const std::string& a) const {
+  auto it = defaults_.find(a);
+  if (it == defaults_.end()) return std::nullopt;
+  return it->second;
+}
+void AllowedCollisionMatrix::set_default_entry(const std::string& a, bool allowed) {
+  defaults_[a] = allowed ? AllowedCollision::ALWAYS : AllowedCollision::NEVER;
+  ++version_;
+}
+void AllowedCollisionMatrix::set_default_entry(const std::vector<std::string>& a, bool allowed) {
+  for (auto& x : a) set_default_entry(x, allowed);
+}
+void AllowedCollisionMatrix::remove_default_entry(const std::string& a) {
+  defaults_.erase(a);
+  ++version_;
+}
+void AllowedCollisionMatrix::remove_default_entry(const std::vector<std::string>& a) {
+  for (auto& x : a) remove_default_entry(x);
+}
+std::optional<AllowedCollision> AllowedCollisionMatrix::default_pair(const std::string& a, const std::string& b) const {
+  auto t1 = get_default_entry(a), t2 = get_default_entry(b);
+  if (!t1 && !t2) return std::nullopt;
+  if (t1 && !t2) return t1;
+  if (!t1 && t2) return t2;
+  if (*t1 == AllowedCollision::NEVER || *t2 == AllowedCollision::NEVER) return AllowedCollision::NEVER;
+  if (*t1 == AllowedCollision::CONDITIONAL || *t2 == AllowedCollision::CONDITIONAL) return AllowedCollision::CONDITIONAL;
+  return AllowedCollision::ALWAYS;
+}
+std::optional<AllowedCollision> AllowedCollisionMatrix::get_allowed_collision(const std::string& a,
+                                                                              const std::string& b) const {
+  auto t = get_entry(a, b);
+  return t ? t : default_pair(a, b);
+}
+void AllowedCollisionMatrix::clear() {
+  entries_.clear();
+  defaults_.clear();
+  ++version_;
+}
+std::vector<std::string> AllowedCollisionMatrix::get_all_entry_names() const {
+  std::set<std::string> s;
+  for (auto& e : entries_) s.insert(e.first);
+  for (auto& d : defaults_) s.insert(d.first);
+  return std::vector<std::string>(s.begin(), s.end());
+}
+std::string AllowedCollisionMatrix::print() const {
+  auto names = get_all_entry_names();
+  std::ostringstream os;
+  for (auto& a : names) {
+    os << a << ": ";
+    for (auto& b : names) {
+      auto t = get_allowed_collision(a, b);
+      os << (!t ? '-' : *t == AllowedCollision::NEVER ? '0' : *t == AllowedCollision::ALWAYS ? '1' : '?');
+    }
+    os << "\n";
+  }
+  return os.str();
+}
+
+// ===========================================================================
+// PlanningWorld
+// ===========================================================================
+PlanningWorld::PlanningWorld(const std::vector<ArtPtr>& arts, const std::vector<std::string>& names,
+                             const std::vector<ObjPtr>& objs, const std::vector<std::string>& obj_names)
+    : acm_(std::make_shared<AllowedCollisionMatrix>()) {
+  if (arts.size() != names.size())
+    throw std::runtime_error("articulations and articulation_names should have the same size");
+  if (objs.size() != obj_names.size())
+    throw std::runtime_error("normal_objects and normal_object_names should have the same size");
+  for (size_t i = 0; i < arts.size(); ++i) {
+    arts[i]->set_name(names[i]);
+    arts_[names[i]] = arts[i];
+    planned_[names[i]] = arts[i];
+  }
+  for (size_t i = 0; i < objs.size(); ++i) add_normal_object(obj_names[i], objs[i]);
+}
+
+std::vector<std::string> PlanningWorld::get_articulation_names() const {
+  std::vector<std::string> out;
+  for (auto& kv : arts_) out.push_back(kv.first);
+  return out;
+}
+std::vector<ArtPtr> PlanningWorld::get_planned_articulations() const {
+  std::vector<ArtPtr> out;
+  for (auto& kv : planned_) out.push_back(kv.second);
+  return out;
+}
+ArtPtr PlanningWorld::get_articulation(const std::string& n) const {
+  auto it = arts_.find(n);
+  return it == arts_.end() ? nullptr : it->second;
+}
+void PlanningWorld::add_articulation(const std::string& n, const ArtPtr& a, bool planned) {
+  a->set_name(n);
+  arts_[n] = a;
+  set_articulation_planned(n, planned);
+  ++structure_version_;
+}
+bool PlanningWorld::remove_articulation(const std::string& n) {
+  auto it = arts_.find(n);
+  if (it == arts_.end()) return false;
+  auto links = it->second->get_user_link_names();
+  arts_.erase(it);
+  planned_.erase(n);
+  acm_->remove_entry(links);
+  acm_->remove_default_entry(links);
+  ++structure_version_;
+  return true;
+}
+void PlanningWorld::set_articulation_planned(const std::string& n, bool planned) {
+  auto art = arts_.at(n);
+  if (planned) planned_[n] = art;
+  else planned_.erase(n);
+  ++structure_version_;
+}
+std::vector<std::string> PlanningWorld::get_normal_object_names() const { return obj_insertion_; }
+ObjPtr PlanningWorld::get_normal_object(const std::string& n) const {
+  auto it = objs_.find(n);
+  return it == objs_.end() ? nullptr : it->second;
+}
+void PlanningWorld::add_normal_object(const std::string& n, const ObjPtr& o) {
+  if (!objs_.count(n)) obj_insertion_.push_back(n);
+  objs_[n] = o;
+  ++structure_version_;
+}
+bool PlanningWorld::remove_normal_object(const std::string& n) {
+  if (!objs_.erase(n)) return false;
+  obj_insertion_.erase(std::remove(obj_insertion_.begin(), obj_insertion_.end(), n), obj_insertion_.end());
+  if (attached_.erase(n))
+    attached_insertion_.erase(std::remove(attached_insertion_.begin(), attached_insertion_.end(), n),
+                              attached_insertion_.end());
+  acm_->remove_entry(n);
+  acm_->remove_default_entry(n);
+  ++structure_version_;
+  return true;
+}
+AttachedPtr PlanningWorld::get_attached_object(const std::string& n) const {
+  auto it = attached_.find(n);
+  return it == attached_.end() ? nullptr : it->second;
+}
+
+void PlanningWorld::attach_object(const std::string& n, const std::string& art, int link, const Vec7& pose,
+                                  const std::vector<std::string>& touch_links) {
+  auto obj = objs_.at(n);
+  auto a = planned_.at(art);
+  if (link < 0 || link >= (int)a->get_user_link_names().size()) throw std::out_of_range("link_id out of range");
+  auto body = std::make_shared<AttachedBody>(AttachedBody{n, obj, a, link, se3_from_pose7(pose), touch_links});
+  auto it = attached_.find(n);
+  if (it != attached_.end()) acm_->remove_entry(n, it->second->touch_links);
+  else attached_insertion_.push_back(n);
+  attached_[n] = body;
+  acm_->set_entry(n, touch_links, true);
+  ++structure_version_;
+}
+
+void PlanningWorld::attach_object(const std::string& n, const std::string& art, int link, const Vec7& pose) {
+  auto obj = objs_.at(n);
+  auto a = planned_.at(art);
+  if (link < 0 || link >= (int)a->get_user_link_names().size()) throw std::out_of_range("link_id out of range");
+  auto body = std::make_shared<AttachedBody>(AttachedBody{n, obj, a, link, se3_from_pose7(pose), {}});
+  auto it = attached_.find(n);
+  if (it != attached_.end()) {
+    body->touch_links = it->second->touch_links;
+    attached_[n] = body;
+    ++structure_version_;
+    return;
+  }
+  attached_insertion_.push_back(n);
+  attached_[n] = body;
+  ++structure_version_;
+  // touch_links = self links colliding with the object in the current state
+  std::vector<std::string> touch;
+  for (auto& c : self_collide())
+    if (c.link_name1 == n) touch.push_back(c.link_name2);
+    else if (c.link_name2 == n) touch.push_back(c.link_name1);
+  body->touch_links = touch;
+  acm_->set_entry(n, touch, true);
+}
+
+void PlanningWorld::attach_object(const std::string& n, const GeomPtr& g, const std::string& art, int link,
+                                  const Vec7& pose, const std::vector<std::string>& touch_links) {
+  remove_normal_object(n);
+  SE3 I;
+  mpg::se3_identity(I);
+  add_normal_object(n, std::make_shared<CollisionObject>(g, I));
+  attach_object(n, art, link, pose, touch_links);
+}
+void PlanningWorld::attach_object(const std::string& n, const GeomPtr& g, const std::string& art, int link,
+                                  const Vec7& pose) {
+  remove_normal_object(n);
+  SE3 I;
+  mpg::se3_identity(I);
+  add_normal_object(n, std::make_shared<CollisionObject>(g, I));
+  attach_object(n, art, link, pose);
+}
+void PlanningWorld::attach_sphere(double r, const std::string& art, int link, const Vec7& pose) {
+  attach_object(art + "_" + std::to_string(link) + "_sphere", std::make_shared<Sphere>(r), art, link, pose);
+}
+void PlanningWorld::attach_box(const Vec3& size, const std::string& art, int link, const Vec7& pose) {
+  attach_object(art + "_" + std::to_string(link) + "_box", std::make_shared<Box>(size), art, link, pose);
+}
+void PlanningWorld::attach_mesh(const std::string& path, const std::string& art, int link, const Vec7& pose) {
+  // reference loads the mesh as a BVH (non-convex) model
+  (void)path;
+  attach_object(art + "_" + std::to_string(link) + "_mesh", std::make_shared<UnsupportedGeometry>("BVHModel"), art,
+                link, pose);
+}
+bool PlanningWorld::detach_object(const std::string& n, bool also_remove) {
+  if (also_remove) {
+    if (objs_.erase(n))
+      obj_insertion_.erase(std::remove(obj_insertion_.begin(), obj_insertion_.end(), n), obj_insertion_.end());
+    acm_->remove_entry(n);
+    acm_->remove_default_entry(n);
+  }
+  auto it = attached_.find(n);
+  ++structure_version_;
+  if (it == attached_.end()) return false;
+  acm_->remove_entry(n, it->second->touch_links);
+  attached_.erase(it);
+  attached_insertion_.erase(std::remove(attached_insertion_.begin(), attached_insertion_.end(), n),
+                            attached_insertion_.end());
+  return true;
+}
+
+void PlanningWorld::set_qpos(const std::string& n, const std::vector<double>& q) const { arts_.at(n)->set_qpos(q); }
+
+void PlanningWorld::set_qpos_all(const std::vector<double>& state) const {
+  size_t i = 0;
+  for (auto& kv : planned_) {
+    const size_t n = kv.second->get_qpos_dim();
+    if (i + n > state.size()) throw std::runtime_error("State dimension is not correct");
+    kv.second->set_qpos(std::vector<double>(state.begin() + i, state.begin() + i + n));
+    i += n;
+  }
+  if (i != state.size()) throw std::runtime_error("State dimension is not correct");
+}
+
+std::vector<std::string> PlanningWorld::attached_order() const { return attached_insertion_; }
+
+std::vector<std::string> PlanningWorld::scene_order() const {
+  std::vector<std::string> out;
+  for (auto& n : obj_insertion_)
+    if (!attached_.count(n)) out.push_back(n);
+  return out;
+}
+
+// state = concatenated move-group qpos of the planned articulations (std::map order)
+std::vector<double> PlanningWorld::current_state() const {
+  std::vector<double> s;
+  for (auto& kv : planned_) {
+    auto& q = kv.second->get_qpos();
+    for (int slot : kv.second->move_group_slots()) s.push_back(q[slot]);
+  }
+  return s;
+}
+
+uint64_t PlanningWorld::snapshot_key(const CollisionRequest& r) const {
+  uint64_t h = 1469598103934665603ull;
+  auto mix = [&](uint64_t v) { h = (h ^ v) * 1099511628211ull; };
+  auto mixd = [&](double d) {
+    uint64_t u;
+    std::memcpy(&u, &d, 8);
+    mix(u);
+  };
+  mix(structure_version_);
+  mix(acm_->version());
+  mixd(r.gjk_tolerance);
+  for (auto& kv : arts_) {
+    mix(kv.second->structure_version());
+    mix(kv.second->get_fcl_model()->structure_version());
+    const bool planned = planned_.count(kv.first) > 0;
+    mix(planned);
+    // constants baked into the snapshot: non-move-group joints of planned
+    // articulations and every joint of unplanned ones
+    auto& q = kv.second->get_qpos();
+    std::vector<int> slots = planned ? kv.second->move_group_slots() : std::vector<int>();
+    for (size_t i = 0; i < q.size(); ++i)
+      if (std::find(slots.begin(), slots.end(), (int)i) == slots.end()) mixd(q[i]);
+  }
+  for (auto& n : obj_insertion_) mix(objs_.at(n)->version);
+  for (auto& n : attached_insertion_) mix((uint64_t)(uintptr_t)attached_.at(n).get());
+  return h;
+}
+
+void PlanningWorld::ensure_snapshot(const CollisionRequest& r, bool need_device) {
+  r.check_supported();
+  const uint64_t key = snapshot_key(r);
+  if (key == desc_key_) {
+    if (need_device && !world_) {
+      world_ = std::make_unique<DeviceWorld>(*desc_, default_device());
+      world_key_ = key;
+    }
+    return;
+  }
+  world_.reset();
+  world_key_ = ~0ull;
+  desc_ = std::make_unique<DescBuilder>();
+  DescBuilder& d = *desc_;
+  d.gjk_tolerance = r.gjk_tolerance;
+  pairs_.clear();
+  // ---- kinematic forest: planned articulations (map order), then unplanned
+  struct ArtInfo {
+    ArtPtr art;
+    int link_base;   // first user link index in the desc
+    int obj_base;    // first moving object id
+    bool planned;
+  };
+  std::vector<ArtInfo> infos;
+  int dof = 0;
+  auto add_art = [&](const ArtPtr& a, bool planned) {
+    auto pin = a->get_pinocchio_model();
+    const int joint_offset = (int)d.joint_type.size();
+    std::vector<int> user_slot = pin->pin_joint_user_slot();
+    auto& q = a->get_qpos();
+    std::vector<int> slots = planned ? a->move_group_slots() : std::vector<int>();
+    std::vector<int> src(user_slot.size(), -1);
+    std::vector<double> cst(user_slot.size(), 0.0);
+    for (size_t j = 0; j < user_slot.size(); ++j) {
+      const int s = user_slot[j];
+      if (s < 0) continue;
+      auto it = std::find(slots.begin(), slots.end(), s);
+      if (it != slots.end()) src[j] = dof + (int)(it - slots.begin());
+      else cst[j] = q[s];
+    }
+    const int link_base = (int)d.link_parent.size();
+    pin->fill_kinematics(d, joint_offset, src, cst);
+    if (planned) dof += (int)slots.size();
+    auto fcl = a->get_fcl_model();
+    const int obj_base = (int)d.moving_link.size();
+    const auto& objs = fcl->raw_objects();
+    for (size_t i = 0; i < objs.size(); ++i) {
+      d.moving_link.push_back(link_base + (int)fcl->get_collision_link_user_indices()[i]);
+      d.moving_geom.push_back(d.add_geometry(objs[i]->geom.get()));
+      push_se3(d.moving_offset, fcl->origins()[i]);
+    }
+    infos.push_back({a, link_base, obj_base, planned});
+  };
+  for (auto& kv : planned_) add_art(kv.second, true);
+  for (auto& kv : arts_)
+    if (!planned_.count(kv.first)) add_art(kv.second, false);
+  d.dof = dof;
+  state_dim_ = dof;
+  // attached bodies (moving objects on a planned articulation's link)
+  std::vector<std::string> att = attached_order();
+  std::map<std::string, int> att_id;
+  for (auto& n : att) {
+    auto& b = attached_.at(n);
+    int link_base = -1;
+    for (auto& inf : infos)
+      if (inf.art == b->articulation) link_base = inf.link_base;
+    if (link_base < 0) throw std::runtime_error("attached body " + n + " refers to an articulation not in the world");
+    att_id[n] = (int)d.moving_link.size();
+    d.moving_link.push_back(link_base + b->link_id);
+    d.moving_geom.push_back(d.add_geometry(b->object->geom.get()));
+    push_se3(d.moving_offset, b->pose);
+  }
+  const int n_moving = (int)d.moving_link.size();
+  // scene objects (static)
+  std::vector<std::string> scene = scene_order();
+  std::map<std::string, int> scene_id;
+  for (auto& n : scene) {
+    scene_id[n] = n_moving + (int)d.static_geom.size();
+    d.static_geom.push_back(d.add_geometry(objs_.at(n)->geom.get()));
+    push_se3(d.static_transform, objs_.at(n)->tf);
+  }
+  auto add_pair = [&](int a, int b, const char* type, const std::string& on1, const std::string& on2,
+                      const std::string& ln1, const std::string& ln2, bool self) {
+    auto t = acm_->get_allowed_collision(ln1, ln2);
+    const bool allowed = t && *t != AllowedCollision::NEVER;
+    pairs_.push_back({a, b, type, on1, on2, ln1, ln2, allowed, self});
+    d.pair_a.push_back(a);
+    d.pair_b.push_back(b);
+    d.pair_allowed.push_back(allowed ? 1 : 0);
+  };
+  // ---- selfCollide (planning_world.cpp:277-369)
+  for (size_t ai = 0; ai < infos.size(); ++ai) {
+    if (!infos[ai].planned) continue;
+    auto& A = infos[ai];
+    auto fcl = A.art->get_fcl_model();
+    auto& names = fcl->get_collision_link_names();
+    const std::string& an = A.art->get_name();
+    for (auto& p : fcl->get_collision_pairs())
+      add_pair(A.obj_base + (int)p.first, A.obj_base + (int)p.second, "self", an, an, names[p.first],
+               names[p.second], true);
+    for (size_t bi = 0; bi < ai; ++bi) {  // planned x planned (earlier in map order)
+      auto& B = infos[bi];
+      auto fcl2 = B.art->get_fcl_model();
+      auto& names2 = fcl2->get_collision_link_names();
+      for (size_t i = 0; i < names.size(); ++i)
+        for (size_t j = 0; j < names2.size(); ++j)
+          add_pair(A.obj_base + (int)i, B.obj_base + (int)j, "self_articulation", an, B.art->get_name(), names[i],
+                   names2[j], true);
+    }
+    for (auto& n : att)
+      for (size_t i = 0; i < names.size(); ++i)
+        add_pair(att_id[n], A.obj_base + (int)i, "self_attach", an, n, names[i], n, true);
+  }
+  for (size_t k = 0; k < att.size(); ++k)
+    for (size_t k2 = 0; k2 < k; ++k2)
+      add_pair(att_id[att[k]], att_id[att[k2]], "attach_attach", att[k], att[k2], att[k], att[k2], true);
+  // ---- collideWithOthers (planning_world.cpp:372-481)
+  for (auto& A : infos) {
+    if (!A.planned) continue;
+    auto fcl = A.art->get_fcl_model();
+    auto& names = fcl->get_collision_link_names();
+    const std::string& an = A.art->get_name();
+    for (auto& B : infos) {
+      if (B.planned) continue;
+      auto& names2 = B.art->get_fcl_model()->get_collision_link_names();
+      for (size_t i = 0; i < names.size(); ++i)
+        for (size_t j = 0; j < names2.size(); ++j)
+          add_pair(A.obj_base + (int)i, B.obj_base + (int)j, "articulation_articulation", an, B.art->get_name(),
+                   names[i], names2[j], false);
+    }
+    for (auto& s : scene)
+      for (size_t i = 0; i < names.size(); ++i)
+        add_pair(A.obj_base + (int)i, scene_id[s], "articulation_sceneobject", an, s, names[i], s, false);
+  }
+  for (auto& n : att) {
+    for (auto& B : infos) {
+      if (B.planned) continue;
+      auto& names2 = B.art->get_fcl_model()->get_collision_link_names();
+      for (size_t i = 0; i < names2.size(); ++i)
+        add_pair(att_id[n], B.obj_base + (int)i, "attach_articulation", n, B.art->get_name(), n, names2[i], false);
+    }
+    for (auto& s : scene) add_pair(att_id[n], scene_id[s], "attach_sceneobject", n, s, n, s, false);
+  }
+  desc_key_ = key;
+  tol_ = r.gjk_tolerance;
+  // validate the descriptor on the host even when no device is needed yet
+  if (need_device) {
+    world_ = std::make_unique<DeviceWorld>(d, default_device());
+    world_key_ = key;
+  }
+}
+
+std::vector<WorldCollisionResult> PlanningWorld::run_scalar(const CollisionRequest& r, bool self, bool others) {
+  ensure_snapshot(r);
+  std::vector<double> s = current_state();
+  uint8_t flag = 0;
+  std::vector<uint32_t> mask(world_->info().mask_words, 0);
+  check_status(mpg_collide_batch(world_->get(), s.data(), 1, &flag, mask.data(), MPG_MEM_HOST, nullptr),
+               "mpg_collide_batch");
+  std::vector<WorldCollisionResult> out;
+  for (size_t p = 0; p < pairs_.size(); ++p) {
+    const PairInfo& pi = pairs_[p];
+    if ((pi.self && !self) || (!pi.self && !others)) continue;
+    if ((mask[p >> 5] >> (p & 31)) & 1u) {
+      WorldCollisionResult w;
+      w.res.contacts.push_back(Contact{});
+      w.collision_type = pi.collision_type;
+      w.object_name1 = pi.object_name1;
+      w.object_name2 = pi.object_name2;
+      w.link_name1 = pi.link_name1;
+      w.link_name2 = pi.link_name2;
+      out.push_back(w);
+    }
+  }
+  return out;
+}
+
+bool PlanningWorld::collide(const CollisionRequest& r) { return !run_scalar(r, true, true).empty(); }
+std::vector<WorldCollisionResult> PlanningWorld::self_collide(const CollisionRequest& r) {
+  return run_scalar(r, true, false);
+}
+std::vector<WorldCollisionResult> PlanningWorld::collide_with_others(const CollisionRequest& r) {
+  return run_scalar(r, false, true);
+}
+std::vector<WorldCollisionResult> PlanningWorld::collide_full(const CollisionRequest& r) {
+  return run_scalar(r, true, true);
+}
+
+int PlanningWorld::state_dim() {
+  ensure_snapshot(CollisionRequest(), false);
+  return state_dim_;
+}
+const std::vector<PairInfo>& PlanningWorld::pair_table() {
+  ensure_snapshot(CollisionRequest(), false);
+  return pairs_;
+}
+int PlanningWorld::mask_words() {
+  ensure_snapshot(CollisionRequest(), false);
+  return std::max<int>(1, ((int)pairs_.size() + 31) / 32);
+}
+mpg_world* PlanningWorld::device_world() {
+  ensure_snapshot(CollisionRequest());
+  return world_->get();
+}
+void PlanningWorld::collide_batch(const double* q, int64_t n, uint8_t* flags, uint32_t* masks) {
+  ensure_snapshot(CollisionRequest());
+  check_status(mpg_collide_batch(world_->get(), q, n, flags, masks, MPG_MEM_HOST, nullptr), "mpg_collide_batch");
+}
+void PlanningWorld::collide_batch_device(const void* q, int64_t n, void* flags, void* masks, void* stream) {
+  ensure_snapshot(CollisionRequest());
+  check_status(mpg_collide_batch(world_->get(), static_cast<const double*>(q), n, static_cast<uint8_t*>(flags),
+                                 static_cast<uint32_t*>(masks), MPG_MEM_DEVICE, stream),
+               "mpg_collide_batch");
+}
+
+void set_global_seed(unsigned seed) { std::srand(seed); }
+
+}  // namespace mpgh

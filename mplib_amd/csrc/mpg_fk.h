@@ -1,0 +1,123 @@
+// mpg_fk.h -- device snapshot layout + forward kinematics shared by the HIP
+// kernels and the host-side self test (tests/test_host_fk.py compiles this
+// header with g++ -ffp-contract=off).
+//
+//   setQposAll/setQpos   src/planning_world.cpp:250-262, src/articulated_model.cpp:101-127
+//   forwardKinematics    [ext pinocchio 2.6.21]: oMi[i] = oMi[parent] * (jointPlacement_i * M_i(q))
+//   getLinkPose          src/pinocchio_model.cpp:277-312 (quaternion round trip)
+#pragma once
+#include "mpg_math.h"
+#include "../../include/mpgpu.h"
+
+namespace mpg {
+
+constexpr int kMaxJoints = 32;
+
+// per-geometry double record
+enum { G_PARAM = 0, G_INTERIOR = 4, G_OBB_C = 7, G_OBB_E = 10, G_RADIUS = 13, G_STRIDE = 14 };
+// per-static-object double record
+enum { S_ROT = 0, S_ROTINV = 4, S_POS = 8, S_OBBC = 11, S_R = 14, S_STRIDE = 23 };
+
+struct DevWorld {
+  int nj, dof, n_links, n_geoms, n_moving, n_static, n_pairs, W;
+  double mpr_tol, cull_margin;
+  const int* joint_type;      // [nj]
+  const int* joint_parent;    // [nj]
+  const int* joint_q_source;  // [nj]
+  const double* joint_q_const;
+  const double* joint_axis;   // [nj*3]
+  const double* joint_place;  // [nj*12]
+  const int* link_parent;     // [n_links]
+  const double* link_place;   // [n_links*12]
+  const int* geom_type;       // [n_geoms]
+  const int* geom_vstart;
+  const int* geom_nv;
+  const double* geom_rec;     // [n_geoms*G_STRIDE]
+  const double* verts;        // [nv*4] (x, y, z, 0)
+  const int* moving_link;     // [n_moving]
+  const int* moving_geom;
+  const double* moving_offset;  // [n_moving*12]
+  const int* static_geom;     // [n_static]
+  const double* static_rec;   // [n_static*S_STRIDE]
+  const int* pair_a;          // [n_pairs]
+  const int* pair_b;
+  const int* pair_allowed;
+};
+
+MPG_INLINE SE3 load_se3(const double* p) {
+  SE3 T;
+#pragma unroll
+  for (int i = 0; i < 9; ++i) T.R[i] = p[i];
+  T.p[0] = p[9];
+  T.p[1] = p[10];
+  T.p[2] = p[11];
+  return T;
+}
+
+// pinocchio JointModel*::calc as a plain SE3 (see oracle/collide_oracle.c)
+MPG_INLINE SE3 joint_motion(int type, const double* axis, double v) {
+  SE3 M;
+  se3_identity(M);
+  if (type <= MPG_JOINT_REVOLUTE_UNALIGNED || type >= MPG_JOINT_RUBX) {
+    const double s = mpg_sin(v);
+    const double c = mpg_cos(v);
+    const int t = (type >= MPG_JOINT_RUBX) ? type - MPG_JOINT_RUBX : type;
+    if (t == 0) {
+      M.R[4] = c; M.R[5] = -s; M.R[7] = s; M.R[8] = c;
+    } else if (t == 1) {
+      M.R[0] = c; M.R[2] = s; M.R[6] = -s; M.R[8] = c;
+    } else if (t == 2) {
+      M.R[0] = c; M.R[1] = -s; M.R[3] = s; M.R[4] = c;
+    } else {
+      axis_rot(axis, c, s, M.R);
+    }
+  } else if (type == MPG_JOINT_PX) {
+    M.p[0] = v;
+  } else if (type == MPG_JOINT_PY) {
+    M.p[1] = v;
+  } else if (type == MPG_JOINT_PZ) {
+    M.p[2] = v;
+  } else {  // prismatic unaligned: translation = axis * q
+    M.p[0] = axis[0] * v;
+    M.p[1] = axis[1] * v;
+    M.p[2] = axis[2] * v;
+  }
+  return M;
+}
+
+// Forward kinematics for one configuration; oMi in thread-private storage.
+struct FkState {
+  SE3 oMi[kMaxJoints + 1];
+};
+
+MPG_HD inline void forward_kinematics(const DevWorld& w, const double* __restrict__ qrow, FkState& st) {
+  se3_identity(st.oMi[0]);
+  for (int j = 1; j <= w.nj; ++j) {
+    const int src = w.joint_q_source[j - 1];
+    const double v = src >= 0 ? qrow[src] : w.joint_q_const[j - 1];
+    const SE3 M = joint_motion(w.joint_type[j - 1], w.joint_axis + 3 * (j - 1), v);
+    const SE3 li = se3_mul(load_se3(w.joint_place + 12 * (j - 1)), M);
+    const int par = w.joint_parent[j - 1];
+    st.oMi[j] = par > 0 ? se3_mul(st.oMi[par], li) : li;
+  }
+}
+
+// getLinkPose + ArticulatedModel::setQpos re-matrix: returns the link
+// Isometry FCL sees, plus the (p, wxyz) pose vector.
+MPG_INLINE SE3 link_transform(const DevWorld& w, const FkState& st, int l, double* pose7) {
+  const SE3 L = se3_mul(st.oMi[w.link_parent[l]], load_se3(w.link_place + 12 * l));
+  double qw, qxyz[3];
+  mat_to_quat(L.R, &qw, qxyz);
+  SE3 T;
+  quat_to_mat(qw, qxyz[0], qxyz[1], qxyz[2], T.R);
+  T.p[0] = L.p[0];
+  T.p[1] = L.p[1];
+  T.p[2] = L.p[2];
+  if (pose7) {
+    pose7[0] = L.p[0]; pose7[1] = L.p[1]; pose7[2] = L.p[2];
+    pose7[3] = qw; pose7[4] = qxyz[0]; pose7[5] = qxyz[1]; pose7[6] = qxyz[2];
+  }
+  return T;
+}
+
+}  // namespace mpg

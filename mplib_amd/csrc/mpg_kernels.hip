@@ -1,0 +1,841 @@
+// mpg_kernels.hip -- MI355X (gfx950) kernels and the C ABI of include/mpgpu.h.
+//
+// Hot path: one batched launch evaluates, per joint configuration,
+//   setQposAll(q) -> FK -> getLinkPose quaternion round trip -> collision
+//   object transforms (src/articulated_model.cpp:101-127,
+//   src/fcl_model.cpp:139-148), then every pair of the world's pair table
+//   with fcl::collide semantics for CollisionRequest() (GST_LIBCCD ->
+//   ccdMPRIntersect, FCL 0.7.0 / libccd 2.1), then the ACM filter
+//   (src/planning_world.cpp:265-274).
+//
+// Mapping (DESIGN.md "Kernel"): one lane = one configuration.  All lanes of a
+// wave walk the SAME pair at the same time, so geometry reads (hull vertices,
+// box sizes, static poses) are wave-uniform scalar loads, and the only
+// divergence is per-lane cull outcome / MPR iteration count.  Per-object GJK
+// state (quaternion + position, 7 doubles) lives in LDS as [object][7][lane]
+// so the pair loop can index objects dynamically without spilling.
+// A conservative broad phase (bounding sphere, then 15-axis OBB SAT, both
+// inflated by kCullMargin) skips pairs that are geometrically separated;
+// libccd MPR returns "no intersection" for every such pair, so results are
+// unchanged (see DESIGN.md "Broad phase soundness").
+//
+// All arithmetic is fp64 and compiled with -ffp-contract=off.
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cfloat>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/mpgpu.h"
+#include "mpg_math.h"
+#include "mpg_fk.h"
+
+using namespace mpg;
+
+namespace {
+
+constexpr double kCcdEps = DBL_EPSILON;
+constexpr double kCullMargin = 1e-5;  // metres; >> fp64 rounding at robot scale
+
+thread_local std::string g_last_error;
+
+int set_error(int code, const std::string& msg) {
+  g_last_error = msg;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                 \
+  do {                                                                                \
+    hipError_t _e = (expr);                                                           \
+    if (_e != hipSuccess)                                                             \
+      return set_error(MPG_E_HIP, std::string(#expr " failed: ") + hipGetErrorString(_e)); \
+  } while (0)
+
+// ---------------------------------------------------------------------------
+// device snapshot
+// ---------------------------------------------------------------------------
+
+
+
+// ---------------------------------------------------------------------------
+// FCL GJK objects + libccd MPR
+// ---------------------------------------------------------------------------
+struct GObj {
+  Q4 rot, rot_inv;
+  V3 pos;
+  int geom;
+  int type;
+};
+
+__device__ __forceinline__ V3 support(const DevWorld& w, const GObj& o, const V3& dir_world) {
+  const V3 dir = quat_rot(dir_world, o.rot_inv);
+  const double* rec = w.geom_rec + G_STRIDE * o.geom;
+  V3 v;
+  if (o.type == MPG_GEOM_CONVEX) {
+    // Convex::findExtremeVertex: argmax dir . vertex, first maximum wins.
+    const int vs = w.geom_vstart[o.geom];
+    const int nv = w.geom_nv[o.geom];
+    const double* __restrict__ P = w.verts + 4 * (size_t)vs;
+    double best = -DBL_MAX;
+    int bi = 0;
+    for (int i = 0; i < nv; ++i) {
+      const double d = (dir.x * P[4 * i] + dir.y * P[4 * i + 1]) + dir.z * P[4 * i + 2];
+      if (d > best) {
+        best = d;
+        bi = i;
+      }
+    }
+    v = v3(P[4 * bi], P[4 * bi + 1], P[4 * bi + 2]);
+  } else if (o.type == MPG_GEOM_BOX) {
+    const double hx = rec[G_PARAM + 0] / 2.0, hy = rec[G_PARAM + 1] / 2.0, hz = rec[G_PARAM + 2] / 2.0;
+    v = v3((dir.x >= 0 ? 1.0 : -1.0) * hx, (dir.y >= 0 ? 1.0 : -1.0) * hy, (dir.z >= 0 ? 1.0 : -1.0) * hz);
+  } else if (o.type == MPG_GEOM_SPHERE) {
+    const double r = rec[G_PARAM];
+    v = vscale(vscale(dir, r), 1.0 / std::sqrt(vdot(dir, dir)));
+  } else if (o.type == MPG_GEOM_CAPSULE) {
+    const double r = rec[G_PARAM], h = rec[G_PARAM + 1] / 2.0;
+    const V3 n = vscale(vnormalize(dir), r);
+    V3 p1 = v3(0.0, 0.0, h), p2 = v3(0.0, 0.0, -h);
+    p1 = vadd(p1, n);
+    p2 = vadd(p2, n);
+    v = dir.z > 0 ? p1 : p2;
+  } else {  // cylinder
+    const double r = rec[G_PARAM], h = rec[G_PARAM + 1] / 2.0;
+    double zdist = dir.x * dir.x + dir.y * dir.y;
+    zdist = std::sqrt(zdist);
+    if (std::fabs(zdist) < kCcdEps) {
+      v = v3(0.0, 0.0, (dir.z > 0 ? 1.0 : -1.0) * h);
+    } else {
+      const double rad = r / zdist;
+      v = v3(rad * dir.x, rad * dir.y, (dir.z > 0 ? 1.0 : -1.0) * h);
+    }
+  }
+  return vadd(quat_rot(v, o.rot), o.pos);
+}
+
+__device__ __forceinline__ V3 center(const DevWorld& w, const GObj& o) {
+  if (o.type == MPG_GEOM_CONVEX) {
+    const double* rec = w.geom_rec + G_STRIDE * o.geom;
+    return vadd(quat_rot(v3(rec[G_INTERIOR], rec[G_INTERIOR + 1], rec[G_INTERIOR + 2]), o.rot), o.pos);
+  }
+  return o.pos;
+}
+
+__device__ __forceinline__ bool is_zero(double v) { return std::fabs(v) < kCcdEps; }
+
+__device__ __forceinline__ bool ccd_eq(double _a, double _b) {
+  const double ab = std::fabs(_a - _b);
+  if (std::fabs(ab) < kCcdEps) return true;
+  const double a = std::fabs(_a), b = std::fabs(_b);
+  if (b > a) return ab < kCcdEps * b;
+  return ab < kCcdEps * a;
+}
+
+__device__ __forceinline__ bool vec_is_origin(const V3& v) {
+  return ccd_eq(v.x, 0.0) && ccd_eq(v.y, 0.0) && ccd_eq(v.z, 0.0);
+}
+
+__device__ __forceinline__ V3 msupport(const DevWorld& w, const GObj& a, const GObj& b, const V3& dir) {
+  const V3 s1 = support(w, a, dir);
+  const V3 s2 = support(w, b, vscale(dir, -1.0));
+  return vsub(s1, s2);
+}
+
+// libccd 2.1 ccdMPRIntersect (discoverPortal + refinePortal).
+__device__ bool mpr_intersect(const DevWorld& w, const GObj& A, const GObj& B) {
+  V3 v0 = vsub(center(w, A), center(w, B));
+  if (vec_is_origin(v0)) v0 = vadd(v0, v3(kCcdEps * 10.0, 0.0, 0.0));
+  V3 dir = vnormalize(vscale(v0, -1.0));
+  V3 v1 = msupport(w, A, B, dir);
+  double dot = vdot(v1, dir);
+  if (is_zero(dot) || dot < 0.0) return false;
+  dir = vcross(v0, v1);
+  if (is_zero(vdot(dir, dir))) return true;  // origin on v1 or on segment v0-v1
+  dir = vnormalize(dir);
+  V3 v2 = msupport(w, A, B, dir);
+  dot = vdot(v2, dir);
+  if (is_zero(dot) || dot < 0.0) return false;
+  {
+    const V3 va = vsub(v1, v0), vb = vsub(v2, v0);
+    dir = vnormalize(vcross(va, vb));
+  }
+  if (vdot(dir, v0) > 0.0) {
+    const V3 t = v1;
+    v1 = v2;
+    v2 = t;
+    dir = vscale(dir, -1.0);
+  }
+  V3 v3p;
+  for (;;) {
+    v3p = msupport(w, A, B, dir);
+    dot = vdot(v3p, dir);
+    if (is_zero(dot) || dot < 0.0) return false;
+    bool cont = false;
+    double d2 = vdot(vcross(v1, v3p), v0);
+    if (d2 < 0.0 && !is_zero(d2)) {
+      v2 = v3p;
+      cont = true;
+    }
+    if (!cont) {
+      d2 = vdot(vcross(v3p, v2), v0);
+      if (d2 < 0.0 && !is_zero(d2)) {
+        v1 = v3p;
+        cont = true;
+      }
+    }
+    if (!cont) break;
+    const V3 va = vsub(v1, v0), vb = vsub(v2, v0);
+    dir = vnormalize(vcross(va, vb));
+  }
+  // refinePortal (no iteration cap in libccd 2.1)
+  V3 p1 = v1, p2 = v2, p3 = v3p;
+  for (;;) {
+    dir = vnormalize(vcross(vsub(p2, p1), vsub(p3, p1)));
+    dot = vdot(dir, p1);
+    if (is_zero(dot) || dot > 0.0) return true;
+    const V3 v4 = msupport(w, A, B, dir);
+    const double dv4 = vdot(v4, dir);
+    if (!(is_zero(dv4) || dv4 > 0.0)) return false;
+    {
+      const double dv1 = vdot(p1, dir), dv2 = vdot(p2, dir), dv3 = vdot(p3, dir);
+      double d1 = dv4 - dv1;
+      const double dd2 = dv4 - dv2, dd3 = dv4 - dv3;
+      d1 = (d1 < dd2) ? d1 : dd2;  // CCD_FMIN
+      d1 = (d1 < dd3) ? d1 : dd3;
+      if (ccd_eq(d1, w.mpr_tol) || d1 < w.mpr_tol) return false;
+    }
+    const V3 v4v0 = vcross(v4, v0);
+    if (vdot(p1, v4v0) > 0.0) {
+      if (vdot(p2, v4v0) > 0.0) p1 = v4;
+      else p3 = v4;
+    } else {
+      if (vdot(p3, v4v0) > 0.0) p2 = v4;
+      else p1 = v4;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// conservative broad phase (sphere, then OBB separating-axis test)
+// ---------------------------------------------------------------------------
+struct WObb {
+  V3 c;
+  double R[9];  // columns = box axes in world
+  V3 e;
+  double r;
+};
+
+__device__ __forceinline__ WObb world_obb_moving(const DevWorld& w, const GObj& o) {
+  const double* rec = w.geom_rec + G_STRIDE * o.geom;
+  WObb b;
+  quat_to_mat(o.rot.w, o.rot.x, o.rot.y, o.rot.z, b.R);
+  const V3 lc = v3(rec[G_OBB_C], rec[G_OBB_C + 1], rec[G_OBB_C + 2]);
+  b.c = vadd(v3((b.R[0] * lc.x + b.R[1] * lc.y) + b.R[2] * lc.z, (b.R[3] * lc.x + b.R[4] * lc.y) + b.R[5] * lc.z,
+                (b.R[6] * lc.x + b.R[7] * lc.y) + b.R[8] * lc.z),
+             o.pos);
+  b.e = v3(rec[G_OBB_E], rec[G_OBB_E + 1], rec[G_OBB_E + 2]);
+  b.r = rec[G_RADIUS];
+  return b;
+}
+
+__device__ __forceinline__ bool obb_separated(const WObb& A, const WObb& B, double margin) {
+  const V3 d = vsub(B.c, A.c);
+  const double rr = A.r + B.r + margin;
+  if (vdot(d, d) > rr * rr) return true;
+  // Rm[i][j] = a_i . b_j (columns of R are the box axes)
+  double Rm[3][3], Ab[3][3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      Rm[i][j] = A.R[i] * B.R[j] + A.R[3 + i] * B.R[3 + j] + A.R[6 + i] * B.R[6 + j];
+      Ab[i][j] = std::fabs(Rm[i][j]) + 1e-12;
+    }
+  const double ea[3] = {A.e.x, A.e.y, A.e.z}, eb[3] = {B.e.x, B.e.y, B.e.z};
+  double t[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) t[i] = d.x * A.R[i] + d.y * A.R[3 + i] + d.z * A.R[6 + i];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const double rb = eb[0] * Ab[i][0] + eb[1] * Ab[i][1] + eb[2] * Ab[i][2];
+    if (std::fabs(t[i]) > ea[i] + rb + margin) return true;
+  }
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const double ra = ea[0] * Ab[0][j] + ea[1] * Ab[1][j] + ea[2] * Ab[2][j];
+    const double tb = t[0] * Rm[0][j] + t[1] * Rm[1][j] + t[2] * Rm[2][j];
+    if (std::fabs(tb) > ra + eb[j] + margin) return true;
+  }
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const int i1 = (i + 1) % 3, i2 = (i + 2) % 3;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const int j1 = (j + 1) % 3, j2 = (j + 2) % 3;
+      const double ra = ea[i1] * Ab[i2][j] + ea[i2] * Ab[i1][j];
+      const double rb = eb[j1] * Ab[i][j2] + eb[j2] * Ab[i][j1];
+      const double tl = t[i2] * Rm[i1][j] - t[i1] * Rm[i2][j];
+      if (std::fabs(tl) > ra + rb + margin) return true;
+    }
+  }
+  return false;
+}
+
+// ---------------------------------------------------------------------------
+// kernels
+// ---------------------------------------------------------------------------
+// Link Isometry from a (p, wxyz) pose vector (FCLModel::updateCollisionObjects,
+// src/fcl_model.cpp:151-167 / ArticulatedModel::setQpos re-matrix).
+__device__ __forceinline__ SE3 link_from_pose7(const double* p7) {
+  SE3 T;
+  quat_to_mat(p7[3], p7[4], p7[5], p7[6], T.R);
+  T.p[0] = p7[0];
+  T.p[1] = p7[1];
+  T.p[2] = p7[2];
+  return T;
+}
+
+template <int BLOCK, bool FROM_POSES>
+__global__ __launch_bounds__(BLOCK) void collide_kernel(DevWorld w, const double* __restrict__ q, long long n,
+                                                       uint8_t* __restrict__ flags, uint32_t* __restrict__ masks) {
+  extern __shared__ __attribute__((aligned(16))) double lds[];  // [n_moving][7][BLOCK]
+  const int tid = threadIdx.x;
+  const long long cfg = (long long)blockIdx.x * BLOCK + tid;
+  if (cfg >= n) return;
+
+  {
+    FkState st;
+    if (!FROM_POSES) forward_kinematics(w, q + cfg * w.dof, st);
+    for (int m = 0; m < w.n_moving; ++m) {
+      const int l = w.moving_link[m];
+      const SE3 L = FROM_POSES ? link_from_pose7(q + (cfg * w.n_links + l) * 7) : link_transform(w, st, l, nullptr);
+      const SE3 T = se3_mul(L, load_se3(w.moving_offset + 12 * m));
+      const Q4 r = gjk_rot_from_matrix(T.R);
+      double* slot = lds + (size_t)m * 7 * BLOCK + tid;
+      slot[0 * BLOCK] = r.x;
+      slot[1 * BLOCK] = r.y;
+      slot[2 * BLOCK] = r.z;
+      slot[3 * BLOCK] = r.w;
+      slot[4 * BLOCK] = T.p[0];
+      slot[5 * BLOCK] = T.p[1];
+      slot[6 * BLOCK] = T.p[2];
+    }
+  }
+
+  uint32_t word = 0;
+  int cur = 0;
+  bool any = false;
+  uint32_t* out = masks ? masks + cfg * w.W : nullptr;
+  for (int p = 0; p < w.n_pairs; ++p) {
+    if ((p >> 5) != cur) {
+      if (out) out[cur] = word;
+      any |= word != 0;
+      word = 0;
+      cur = p >> 5;
+    }
+    if (w.pair_allowed[p]) continue;
+    GObj o[2];
+    WObb box[2];
+    const int ids[2] = {w.pair_a[p], w.pair_b[p]};
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int id = ids[s];
+      if (id < w.n_moving) {
+        const double* slot = lds + (size_t)id * 7 * BLOCK + tid;
+        o[s].rot = Q4{slot[0], slot[BLOCK], slot[2 * BLOCK], slot[3 * BLOCK]};
+        o[s].pos = v3(slot[4 * BLOCK], slot[5 * BLOCK], slot[6 * BLOCK]);
+        o[s].geom = w.moving_geom[id];
+        o[s].rot_inv = quat_invert2(o[s].rot);
+        o[s].type = w.geom_type[o[s].geom];
+        box[s] = world_obb_moving(w, o[s]);
+      } else {
+        const int sid = id - w.n_moving;
+        const double* r = w.static_rec + S_STRIDE * sid;
+        o[s].rot = Q4{r[S_ROT], r[S_ROT + 1], r[S_ROT + 2], r[S_ROT + 3]};
+        o[s].rot_inv = Q4{r[S_ROTINV], r[S_ROTINV + 1], r[S_ROTINV + 2], r[S_ROTINV + 3]};
+        o[s].pos = v3(r[S_POS], r[S_POS + 1], r[S_POS + 2]);
+        o[s].geom = w.static_geom[sid];
+        o[s].type = w.geom_type[o[s].geom];
+        box[s].c = v3(r[S_OBBC], r[S_OBBC + 1], r[S_OBBC + 2]);
+#pragma unroll
+        for (int k = 0; k < 9; ++k) box[s].R[k] = r[S_R + k];
+        const double* g = w.geom_rec + G_STRIDE * o[s].geom;
+        box[s].e = v3(g[G_OBB_E], g[G_OBB_E + 1], g[G_OBB_E + 2]);
+        box[s].r = g[G_RADIUS];
+      }
+    }
+    if (obb_separated(box[0], box[1], w.cull_margin)) continue;
+    if (mpr_intersect(w, o[0], o[1])) word |= 1u << (p & 31);
+  }
+  if (out) out[cur] = word;
+  any |= word != 0;
+  flags[cfg] = any ? 1 : 0;
+}
+
+__global__ void fk_kernel(DevWorld w, const double* __restrict__ q, long long n, double* __restrict__ out) {
+  const long long cfg = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (cfg >= n) return;
+  FkState st;
+  forward_kinematics(w, q + cfg * w.dof, st);
+  for (int l = 0; l < w.n_links; ++l) link_transform(w, st, l, out + (cfg * w.n_links + l) * 7);
+}
+
+__global__ void sincos_kernel(const double* __restrict__ x, long long n, double* s, double* c) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  s[i] = mpg_sin(x[i]);
+  c[i] = mpg_cos(x[i]);
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// host side: snapshot build + C ABI
+// ---------------------------------------------------------------------------
+struct mpg_world {
+  int device = 0;
+  DevWorld dw{};
+  void* blob = nullptr;
+  size_t blob_bytes = 0;
+  int block = 128;
+  size_t lds_bytes = 0;
+  // staging for MPG_MEM_HOST
+  std::mutex host_mu;
+  double* d_q = nullptr;
+  uint8_t* d_flags = nullptr;
+  uint32_t* d_masks = nullptr;
+  double* d_out = nullptr;
+  size_t cap_cfg = 0;
+  size_t cap_out = 0;
+};
+
+namespace {
+
+struct BlobBuilder {
+  std::vector<char> bytes;
+  template <class T>
+  size_t add(const T* data, size_t count) {
+    size_t off = (bytes.size() + 15) & ~size_t(15);
+    bytes.resize(off + sizeof(T) * std::max<size_t>(count, 1), 0);
+    if (count) std::memcpy(bytes.data() + off, data, sizeof(T) * count);
+    return off;
+  }
+};
+
+bool finite_all(const double* p, size_t n) {
+  for (size_t i = 0; i < n; ++i)
+    if (!std::isfinite(p[i])) return false;
+  return true;
+}
+
+int validate(const mpg_world_desc* d) {
+  if (!d) return set_error(MPG_E_INVALID, "desc is NULL");
+  if (d->n_joints < 0 || d->n_joints > kMaxJoints) return set_error(MPG_E_INVALID, "n_joints out of range [0, 32]");
+  if (d->dof < 0) return set_error(MPG_E_INVALID, "dof < 0");
+  if (d->n_links < 0 || d->n_geoms < 0 || d->n_moving < 0 || d->n_static < 0 || d->n_pairs < 0)
+    return set_error(MPG_E_INVALID, "negative count");
+  for (int j = 0; j < d->n_joints; ++j) {
+    if (d->joint_type[j] < 0 || d->joint_type[j] > MPG_JOINT_RUB_UNALIGNED)
+      return set_error(MPG_E_INVALID, "bad joint type");
+    if (d->joint_parent[j] < 0 || d->joint_parent[j] > j)
+      return set_error(MPG_E_INVALID, "joint_parent must reference an earlier joint (0 = universe)");
+    if (d->joint_q_source[j] >= d->dof) return set_error(MPG_E_INVALID, "joint_q_source >= dof");
+  }
+  for (int l = 0; l < d->n_links; ++l)
+    if (d->link_parent[l] < 0 || d->link_parent[l] > d->n_joints) return set_error(MPG_E_INVALID, "bad link_parent");
+  for (int g = 0; g < d->n_geoms; ++g) {
+    const int t = d->geom_type[g];
+    if (t < MPG_GEOM_CONVEX || t > MPG_GEOM_CYLINDER) return set_error(MPG_E_UNSUPPORTED, "unsupported geometry type");
+    if (t == MPG_GEOM_CONVEX) {
+      if (d->geom_vertex_count[g] <= 0 || d->geom_vertex_start[g] < 0 ||
+          (int64_t)d->geom_vertex_start[g] + d->geom_vertex_count[g] > d->n_vertices)
+        return set_error(MPG_E_INVALID, "convex vertex range out of bounds");
+    }
+  }
+  for (int m = 0; m < d->n_moving; ++m) {
+    if (d->moving_link[m] < 0 || d->moving_link[m] >= d->n_links) return set_error(MPG_E_INVALID, "bad moving_link");
+    if (d->moving_geom[m] < 0 || d->moving_geom[m] >= d->n_geoms) return set_error(MPG_E_INVALID, "bad moving_geom");
+  }
+  for (int s = 0; s < d->n_static; ++s)
+    if (d->static_geom[s] < 0 || d->static_geom[s] >= d->n_geoms) return set_error(MPG_E_INVALID, "bad static_geom");
+  const int nobj = d->n_moving + d->n_static;
+  for (int p = 0; p < d->n_pairs; ++p) {
+    const int a = d->pair_a[p], b = d->pair_b[p];
+    if (a < 0 || a >= nobj || b < 0 || b >= nobj) return set_error(MPG_E_INVALID, "pair object id out of range");
+    if (a >= d->n_moving && b >= d->n_moving) return set_error(MPG_E_INVALID, "static-static pair");
+    const int ta = d->geom_type[a < d->n_moving ? d->moving_geom[a] : d->static_geom[a - d->n_moving]];
+    const int tb = d->geom_type[b < d->n_moving ? d->moving_geom[b] : d->static_geom[b - d->n_moving]];
+    // FCL 0.7.0 GJKSolver_libccd routes these pairs to closed-form tests, not
+    // MPR; they are not implemented on the device yet.
+    const bool sa = ta == MPG_GEOM_SPHERE, sb = tb == MPG_GEOM_SPHERE;
+    if ((sa && (sb || tb == MPG_GEOM_BOX || tb == MPG_GEOM_CAPSULE || tb == MPG_GEOM_CYLINDER)) ||
+        (sb && (ta == MPG_GEOM_BOX || ta == MPG_GEOM_CAPSULE || ta == MPG_GEOM_CYLINDER)) ||
+        (ta == MPG_GEOM_BOX && tb == MPG_GEOM_BOX) || (ta == MPG_GEOM_CAPSULE && tb == MPG_GEOM_CAPSULE))
+      return set_error(MPG_E_UNSUPPORTED,
+                       "pair uses an FCL closed-form narrow phase (sphere/box/capsule specialisation) "
+                       "that is not implemented on the device");
+  }
+  if (!finite_all(d->joint_placement, 12 * (size_t)d->n_joints) || !finite_all(d->link_placement, 12 * (size_t)d->n_links) ||
+      !finite_all(d->vertices, 3 * (size_t)d->n_vertices))
+    return set_error(MPG_E_INVALID, "non-finite value in descriptor");
+  if (!(d->gjk_tolerance > 0)) return set_error(MPG_E_INVALID, "gjk_tolerance must be > 0");
+  return MPG_OK;
+}
+
+void geom_record(const mpg_world_desc* d, int g, double* rec) {
+  for (int k = 0; k < G_STRIDE; ++k) rec[k] = 0.0;
+  for (int k = 0; k < 4; ++k) rec[G_PARAM + k] = d->geom_param[4 * g + k];
+  const int t = d->geom_type[g];
+  double lo[3], hi[3];
+  if (t == MPG_GEOM_CONVEX) {
+    const double* V = d->vertices + 3 * (size_t)d->geom_vertex_start[g];
+    const int nv = d->geom_vertex_count[g];
+    // FCL 0.7.0 Convex: interior point = (sum of vertices) * (1.0 / n)
+    double s[3] = {0.0, 0.0, 0.0};
+    for (int i = 0; i < nv; ++i) {
+      s[0] += V[3 * i];
+      s[1] += V[3 * i + 1];
+      s[2] += V[3 * i + 2];
+    }
+    const double inv = 1.0 / (double)nv;
+    for (int k = 0; k < 3; ++k) rec[G_INTERIOR + k] = s[k] * inv;
+    for (int k = 0; k < 3; ++k) lo[k] = hi[k] = V[k];
+    for (int i = 1; i < nv; ++i)
+      for (int k = 0; k < 3; ++k) {
+        lo[k] = std::min(lo[k], V[3 * i + k]);
+        hi[k] = std::max(hi[k], V[3 * i + k]);
+      }
+  } else if (t == MPG_GEOM_BOX) {
+    for (int k = 0; k < 3; ++k) {
+      hi[k] = d->geom_param[4 * g + k] / 2.0;
+      lo[k] = -hi[k];
+    }
+  } else if (t == MPG_GEOM_SPHERE) {
+    for (int k = 0; k < 3; ++k) {
+      hi[k] = d->geom_param[4 * g];
+      lo[k] = -hi[k];
+    }
+  } else {  // capsule / cylinder along z
+    const double r = d->geom_param[4 * g], hz = d->geom_param[4 * g + 1] / 2.0 + (t == MPG_GEOM_CAPSULE ? r : 0.0);
+    lo[0] = lo[1] = -r;
+    hi[0] = hi[1] = r;
+    lo[2] = -hz;
+    hi[2] = hz;
+  }
+  // local box, widened by a relative epsilon so rounding never shrinks it
+  double r2 = 0.0;
+  for (int k = 0; k < 3; ++k) {
+    const double c = 0.5 * (lo[k] + hi[k]);
+    const double e = 0.5 * (hi[k] - lo[k]);
+    rec[G_OBB_C + k] = c;
+    rec[G_OBB_E + k] = e * (1.0 + 1e-12) + 1e-12;
+    r2 += rec[G_OBB_E + k] * rec[G_OBB_E + k];
+  }
+  rec[G_RADIUS] = std::sqrt(r2) * (1.0 + 1e-12);
+}
+
+void static_record(const mpg_world_desc* d, int s, const double* geom_rec_all, double* rec) {
+  const double* T = d->static_transform + 12 * s;
+  const Q4 r = gjk_rot_from_matrix(T);
+  const Q4 ri = quat_invert2(r);
+  rec[S_ROT] = r.x; rec[S_ROT + 1] = r.y; rec[S_ROT + 2] = r.z; rec[S_ROT + 3] = r.w;
+  rec[S_ROTINV] = ri.x; rec[S_ROTINV + 1] = ri.y; rec[S_ROTINV + 2] = ri.z; rec[S_ROTINV + 3] = ri.w;
+  rec[S_POS] = T[9]; rec[S_POS + 1] = T[10]; rec[S_POS + 2] = T[11];
+  // broad-phase OBB from the same rotation MPR uses
+  double R[9];
+  quat_to_mat(r.w, r.x, r.y, r.z, R);
+  const double* g = geom_rec_all + G_STRIDE * d->static_geom[s];
+  for (int i = 0; i < 3; ++i)
+    rec[S_OBBC + i] = ((R[3 * i] * g[G_OBB_C] + R[3 * i + 1] * g[G_OBB_C + 1]) + R[3 * i + 2] * g[G_OBB_C + 2]) + T[9 + i];
+  for (int k = 0; k < 9; ++k) rec[S_R + k] = R[k];
+}
+
+int choose_block(int n_moving, size_t* lds) {
+  const size_t per_thread = (size_t)std::max(n_moving, 1) * 7 * sizeof(double);
+  // keep two workgroups resident per CU (160 KiB LDS) when possible
+  int block = 256;
+  while (block > 64 && per_thread * block > 80 * 1024) block /= 2;
+  *lds = per_thread * block;
+  if (*lds > 160 * 1024) return -1;
+  return block;
+}
+
+template <bool FROM_POSES>
+int launch_collide(mpg_world* w, const double* q, long long n, uint8_t* flags, uint32_t* masks, hipStream_t stream) {
+  if (n == 0) return MPG_OK;
+  const long long grid = (n + w->block - 1) / w->block;
+  if (grid > 0x7fffffffLL) return set_error(MPG_E_INVALID, "batch too large for one launch");
+  switch (w->block) {
+    case 256:
+      hipLaunchKernelGGL((collide_kernel<256, FROM_POSES>), dim3((unsigned)grid), dim3(256), w->lds_bytes, stream,
+                         w->dw, q, n, flags, masks);
+      break;
+    case 128:
+      hipLaunchKernelGGL((collide_kernel<128, FROM_POSES>), dim3((unsigned)grid), dim3(128), w->lds_bytes, stream,
+                         w->dw, q, n, flags, masks);
+      break;
+    default:
+      hipLaunchKernelGGL((collide_kernel<64, FROM_POSES>), dim3((unsigned)grid), dim3(64), w->lds_bytes, stream,
+                         w->dw, q, n, flags, masks);
+      break;
+  }
+  HIP_TRY(hipGetLastError());
+  return MPG_OK;
+}
+
+int ensure_staging(mpg_world* w, size_t ncfg, size_t nout) {
+  if (ncfg > w->cap_cfg) {
+    hipFree(w->d_q);
+    hipFree(w->d_flags);
+    hipFree(w->d_masks);
+    w->d_q = nullptr;
+    w->d_flags = nullptr;
+    w->d_masks = nullptr;
+    HIP_TRY(hipMalloc(&w->d_q, sizeof(double) * std::max<size_t>(1, ncfg * std::max(w->dw.dof, 1))));
+    HIP_TRY(hipMalloc(&w->d_flags, std::max<size_t>(1, ncfg)));
+    HIP_TRY(hipMalloc(&w->d_masks, sizeof(uint32_t) * std::max<size_t>(1, ncfg * w->dw.W)));
+    w->cap_cfg = ncfg;
+  }
+  if (nout > w->cap_out) {
+    hipFree(w->d_out);
+    w->d_out = nullptr;
+    HIP_TRY(hipMalloc(&w->d_out, sizeof(double) * nout));
+    w->cap_out = nout;
+  }
+  return MPG_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* mpg_last_error(void) { return g_last_error.c_str(); }
+
+const char* mpg_version(void) { return "mpgpu 0.1 (gfx950, fp64, libccd-MPR)"; }
+
+int mpg_device_count(int* count) {
+  if (!count) return set_error(MPG_E_INVALID, "count is NULL");
+  HIP_TRY(hipGetDeviceCount(count));
+  return MPG_OK;
+}
+
+int mpg_synchronize(int device) {
+  HIP_TRY(hipSetDevice(device));
+  HIP_TRY(hipDeviceSynchronize());
+  return MPG_OK;
+}
+
+int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
+  if (!out) return set_error(MPG_E_INVALID, "out is NULL");
+  *out = nullptr;
+  int rc = validate(d);
+  if (rc) return rc;
+  size_t lds = 0;
+  const int block = choose_block(d->n_moving, &lds);
+  if (block < 0) return set_error(MPG_E_UNSUPPORTED, "too many moving objects for the LDS budget (max 45)");
+  HIP_TRY(hipSetDevice(device));
+
+  std::vector<double> geom_rec((size_t)G_STRIDE * std::max(d->n_geoms, 1), 0.0);
+  for (int g = 0; g < d->n_geoms; ++g) geom_record(d, g, geom_rec.data() + (size_t)G_STRIDE * g);
+  std::vector<double> static_rec((size_t)S_STRIDE * std::max(d->n_static, 1), 0.0);
+  for (int s = 0; s < d->n_static; ++s) static_record(d, s, geom_rec.data(), static_rec.data() + (size_t)S_STRIDE * s);
+  std::vector<double> verts4((size_t)4 * std::max<int64_t>(d->n_vertices, 1), 0.0);
+  for (int64_t i = 0; i < d->n_vertices; ++i)
+    for (int k = 0; k < 3; ++k) verts4[4 * i + k] = d->vertices[3 * i + k];
+  std::vector<int> allowed(std::max(d->n_pairs, 1), 0);
+  for (int p = 0; p < d->n_pairs; ++p) allowed[p] = d->pair_allowed ? (d->pair_allowed[p] != 0) : 0;
+
+  BlobBuilder bb;
+  const size_t o_jt = bb.add(d->joint_type, d->n_joints);
+  const size_t o_jp = bb.add(d->joint_parent, d->n_joints);
+  const size_t o_jqs = bb.add(d->joint_q_source, d->n_joints);
+  const size_t o_jqc = bb.add(d->joint_q_const, d->n_joints);
+  const size_t o_ja = bb.add(d->joint_axis, 3 * (size_t)d->n_joints);
+  const size_t o_jpl = bb.add(d->joint_placement, 12 * (size_t)d->n_joints);
+  const size_t o_lp = bb.add(d->link_parent, d->n_links);
+  const size_t o_lpl = bb.add(d->link_placement, 12 * (size_t)d->n_links);
+  const size_t o_gt = bb.add(d->geom_type, d->n_geoms);
+  const size_t o_gvs = bb.add(d->geom_vertex_start, d->n_geoms);
+  const size_t o_gnv = bb.add(d->geom_vertex_count, d->n_geoms);
+  const size_t o_grec = bb.add(geom_rec.data(), geom_rec.size());
+  const size_t o_v = bb.add(verts4.data(), verts4.size());
+  const size_t o_ml = bb.add(d->moving_link, d->n_moving);
+  const size_t o_mg = bb.add(d->moving_geom, d->n_moving);
+  const size_t o_mo = bb.add(d->moving_offset, 12 * (size_t)d->n_moving);
+  const size_t o_sg = bb.add(d->static_geom, d->n_static);
+  const size_t o_srec = bb.add(static_rec.data(), static_rec.size());
+  const size_t o_pa = bb.add(d->pair_a, d->n_pairs);
+  const size_t o_pb = bb.add(d->pair_b, d->n_pairs);
+  const size_t o_al = bb.add(allowed.data(), allowed.size());
+
+  mpg_world* w = new mpg_world();
+  w->device = device;
+  w->block = block;
+  w->lds_bytes = lds;
+  w->blob_bytes = bb.bytes.size();
+  hipError_t e = hipMalloc(&w->blob, w->blob_bytes);
+  if (e != hipSuccess) {
+    delete w;
+    return set_error(MPG_E_HIP, std::string("hipMalloc(snapshot): ") + hipGetErrorString(e));
+  }
+  e = hipMemcpy(w->blob, bb.bytes.data(), w->blob_bytes, hipMemcpyHostToDevice);
+  if (e != hipSuccess) {
+    hipFree(w->blob);
+    delete w;
+    return set_error(MPG_E_HIP, std::string("hipMemcpy(snapshot): ") + hipGetErrorString(e));
+  }
+  char* base = static_cast<char*>(w->blob);
+  DevWorld& dw = w->dw;
+  dw.nj = d->n_joints;
+  dw.dof = d->dof;
+  dw.n_links = d->n_links;
+  dw.n_geoms = d->n_geoms;
+  dw.n_moving = d->n_moving;
+  dw.n_static = d->n_static;
+  dw.n_pairs = d->n_pairs;
+  dw.W = std::max(1, (d->n_pairs + 31) / 32);
+  dw.mpr_tol = d->gjk_tolerance;
+  dw.cull_margin = kCullMargin;
+  dw.joint_type = reinterpret_cast<const int*>(base + o_jt);
+  dw.joint_parent = reinterpret_cast<const int*>(base + o_jp);
+  dw.joint_q_source = reinterpret_cast<const int*>(base + o_jqs);
+  dw.joint_q_const = reinterpret_cast<const double*>(base + o_jqc);
+  dw.joint_axis = reinterpret_cast<const double*>(base + o_ja);
+  dw.joint_place = reinterpret_cast<const double*>(base + o_jpl);
+  dw.link_parent = reinterpret_cast<const int*>(base + o_lp);
+  dw.link_place = reinterpret_cast<const double*>(base + o_lpl);
+  dw.geom_type = reinterpret_cast<const int*>(base + o_gt);
+  dw.geom_vstart = reinterpret_cast<const int*>(base + o_gvs);
+  dw.geom_nv = reinterpret_cast<const int*>(base + o_gnv);
+  dw.geom_rec = reinterpret_cast<const double*>(base + o_grec);
+  dw.verts = reinterpret_cast<const double*>(base + o_v);
+  dw.moving_link = reinterpret_cast<const int*>(base + o_ml);
+  dw.moving_geom = reinterpret_cast<const int*>(base + o_mg);
+  dw.moving_offset = reinterpret_cast<const double*>(base + o_mo);
+  dw.static_geom = reinterpret_cast<const int*>(base + o_sg);
+  dw.static_rec = reinterpret_cast<const double*>(base + o_srec);
+  dw.pair_a = reinterpret_cast<const int*>(base + o_pa);
+  dw.pair_b = reinterpret_cast<const int*>(base + o_pb);
+  dw.pair_allowed = reinterpret_cast<const int*>(base + o_al);
+  *out = w;
+  return MPG_OK;
+}
+
+int mpg_world_destroy(mpg_world* w) {
+  if (!w) return MPG_OK;
+  hipSetDevice(w->device);
+  hipFree(w->blob);
+  hipFree(w->d_q);
+  hipFree(w->d_flags);
+  hipFree(w->d_masks);
+  hipFree(w->d_out);
+  delete w;
+  return MPG_OK;
+}
+
+int mpg_world_get_info(const mpg_world* w, mpg_world_info* info) {
+  if (!w || !info) return set_error(MPG_E_INVALID, "NULL argument");
+  info->n_pairs = w->dw.n_pairs;
+  info->mask_words = w->dw.W;
+  info->dof = w->dw.dof;
+  info->n_links = w->dw.n_links;
+  info->device = w->device;
+  info->block_size = w->block;
+  info->snapshot_bytes = (int64_t)w->blob_bytes;
+  return MPG_OK;
+}
+
+}  // extern "C"
+
+namespace {
+template <bool FROM_POSES>
+int collide_common(mpg_world* w, const double* q, int64_t n, uint8_t* flags, uint32_t* pair_mask, int mem,
+                   void* stream) {
+  if (!w) return set_error(MPG_E_INVALID, "world is NULL");
+  if (n < 0) return set_error(MPG_E_INVALID, "n < 0");
+  if (n > 0 && (!q || !flags)) return set_error(MPG_E_INVALID, "input/flags is NULL");
+  HIP_TRY(hipSetDevice(w->device));
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (mem == MPG_MEM_DEVICE) return launch_collide<FROM_POSES>(w, q, n, flags, pair_mask, s);
+  if (mem != MPG_MEM_HOST) return set_error(MPG_E_INVALID, "bad mem kind");
+  const size_t row = FROM_POSES ? (size_t)w->dw.n_links * 7 : (size_t)w->dw.dof;
+  std::lock_guard<std::mutex> lk(w->host_mu);
+  int rc = ensure_staging(w, (size_t)n, std::max<size_t>(1, (size_t)n * row));
+  if (rc) return rc;
+  if (n == 0) return MPG_OK;
+  double* din = FROM_POSES ? w->d_out : w->d_q;
+  if (row) HIP_TRY(hipMemcpyAsync(din, q, sizeof(double) * n * row, hipMemcpyHostToDevice, s));
+  rc = launch_collide<FROM_POSES>(w, din, n, w->d_flags, w->d_masks, s);
+  if (rc) return rc;
+  HIP_TRY(hipMemcpyAsync(flags, w->d_flags, n, hipMemcpyDeviceToHost, s));
+  if (pair_mask)
+    HIP_TRY(hipMemcpyAsync(pair_mask, w->d_masks, sizeof(uint32_t) * n * w->dw.W, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  return MPG_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int mpg_collide_batch(mpg_world* w, const double* q, int64_t n, uint8_t* flags, uint32_t* pair_mask, int mem,
+                      void* stream) {
+  return collide_common<false>(w, q, n, flags, pair_mask, mem, stream);
+}
+
+int mpg_collide_link_poses(mpg_world* w, const double* link_pose, int64_t n, uint8_t* flags, uint32_t* pair_mask,
+                           int mem, void* stream) {
+  return collide_common<true>(w, link_pose, n, flags, pair_mask, mem, stream);
+}
+
+int mpg_fk_batch(mpg_world* w, const double* q, int64_t n, double* link_pose, int mem, void* stream) {
+  if (!w) return set_error(MPG_E_INVALID, "world is NULL");
+  if (n < 0) return set_error(MPG_E_INVALID, "n < 0");
+  if (n > 0 && (!q || !link_pose)) return set_error(MPG_E_INVALID, "q/link_pose is NULL");
+  HIP_TRY(hipSetDevice(w->device));
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const size_t nout = (size_t)n * w->dw.n_links * 7;
+  const unsigned grid = (unsigned)((n + 127) / 128);
+  if (mem == MPG_MEM_DEVICE) {
+    if (n) hipLaunchKernelGGL(fk_kernel, dim3(grid), dim3(128), 0, s, w->dw, q, (long long)n, link_pose);
+    HIP_TRY(hipGetLastError());
+    return MPG_OK;
+  }
+  if (mem != MPG_MEM_HOST) return set_error(MPG_E_INVALID, "bad mem kind");
+  std::lock_guard<std::mutex> lk(w->host_mu);
+  int rc = ensure_staging(w, (size_t)n, std::max<size_t>(nout, 1));
+  if (rc) return rc;
+  if (n == 0) return MPG_OK;
+  HIP_TRY(hipMemcpyAsync(w->d_q, q, sizeof(double) * n * w->dw.dof, hipMemcpyHostToDevice, s));
+  hipLaunchKernelGGL(fk_kernel, dim3(grid), dim3(128), 0, s, w->dw, w->d_q, (long long)n, w->d_out);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpyAsync(link_pose, w->d_out, sizeof(double) * nout, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  return MPG_OK;
+}
+
+int mpg_debug_sincos(const double* x, int64_t n, double* s, double* c, int device) {
+  if (n < 0 || (n > 0 && (!x || !s || !c))) return set_error(MPG_E_INVALID, "bad arguments");
+  if (n == 0) return MPG_OK;
+  HIP_TRY(hipSetDevice(device));
+  double *dx = nullptr, *ds = nullptr, *dc = nullptr;
+  HIP_TRY(hipMalloc(&dx, sizeof(double) * n));
+  HIP_TRY(hipMalloc(&ds, sizeof(double) * n));
+  HIP_TRY(hipMalloc(&dc, sizeof(double) * n));
+  HIP_TRY(hipMemcpy(dx, x, sizeof(double) * n, hipMemcpyHostToDevice));
+  hipLaunchKernelGGL(sincos_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, 0, dx, (long long)n, ds, dc);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpy(s, ds, sizeof(double) * n, hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(c, dc, sizeof(double) * n, hipMemcpyDeviceToHost));
+  hipFree(dx);
+  hipFree(ds);
+  hipFree(dc);
+  return MPG_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,344 @@
+// mpg_math.h -- fp64 arithmetic shared by the HIP kernels and the host-side
+// snapshot builder.  Every function reproduces the operation ORDER of the
+// library the reference calls, with no implicit fused multiply-add (all
+// translation units are compiled with -ffp-contract=off; fused steps are
+// written explicitly with mpg_fma where the reference's binary fuses them).
+//
+//   * mpg_sin<kFma> / mpg_cos<kFma>: glibc 2.35 sysdeps/ieee754/dbl-64/s_sin.c.
+//     kFma = false is the generic build, which is what glibc's sincos() runs
+//     on every x86-64 host (sincos has no FMA ifunc variant).  pinocchio's
+//     SINCOS (forwardKinematics, pinocchio_model.cpp:272-274) and
+//     qposUser2Pinocchio's cos/sin pair (:515-516) both end in sincos(): GCC
+//     folds sin(a);cos(a) into one sincos() call.  kFma = true reproduces the
+//     standalone sin()/cos() __sin_fma/__cos_fma variants selected on
+//     FMA+AVX2 hosts.  Both verified bit-exact against the host libm by
+//     tests/test_sincos.py.
+//   * Eigen 3.4 quaternion <-> matrix conversions and lazy 3x3 products
+//     (pinocchio_model.cpp:299, articulated_model.cpp:119-124,
+//     fcl_model.cpp:139-148, FCL shapeToGJK).
+//   * libccd 2.1 ccdQuatRotVec / ccdQuatInvert2 / vec3 helpers.
+#pragma once
+
+#include <cstdint>
+#include <cstring>
+#include <cmath>
+
+#include "mpg_sincostab.h"
+
+#if defined(__HIPCC__)
+#define MPG_HD __host__ __device__
+#define MPG_INLINE __host__ __device__ __forceinline__
+#else
+#define MPG_HD
+#define MPG_INLINE inline
+#endif
+
+namespace mpg {
+
+constexpr double kSinCosTab[440] = MPG_SINCOSTAB_INIT;
+
+// glibc's FMA build fuses where GCC -mfma contracts; the generic build rounds
+// the product first.
+template <bool kFma>
+MPG_INLINE double mpg_fma(double a, double b, double c) {
+  if constexpr (kFma) return __builtin_fma(a, b, c);
+  else return a * b + c;
+}
+
+MPG_INLINE uint32_t hi_word(double d) {
+  uint64_t u;
+  std::memcpy(&u, &d, 8);
+  return (uint32_t)(u >> 32);
+}
+MPG_INLINE int32_t lo_word(double d) {
+  uint64_t u;
+  std::memcpy(&u, &d, 8);
+  return (int32_t)(uint32_t)u;
+}
+
+// --------------------------------------------------------------------------
+// glibc dbl-64 sin/cos.  Constants: sysdeps/ieee754/dbl-64/usncs.h and
+// s_sin.c.  kFma: contraction pattern of GCC -mfma -ffp-contract=fast on that
+// code (the __sin_fma/__cos_fma ifunc variants); !kFma: the generic build.
+// --------------------------------------------------------------------------
+namespace sc {
+constexpr double sn3 = -1.66666666666664880952546298448555E-01;
+constexpr double sn5 = 8.33333214285722277379541354343671E-03;
+constexpr double cs2 = 4.99999999999999999999950396842453E-01;
+constexpr double cs4 = -4.16666666666664434524222570944589E-02;
+constexpr double cs6 = 1.38888874007937613028114285595617E-03;
+constexpr double s1 = -0x1.5555555555555p-3;
+constexpr double s2 = 0x1.1111111110ECEp-7;
+constexpr double s3 = -0x1.a01a019db08b8p-13;
+constexpr double s4 = 0x1.71de27b9a7ed9p-19;
+constexpr double s5 = -0x1.addffc2fcdf59p-26;
+constexpr double big = 0x1.8p45;
+constexpr double hp0 = 0x1.921FB54442D18p0;
+constexpr double hp1 = 0x1.1A62633145C07p-54;
+constexpr double mp1 = 0x1.921FB58000000p0;
+constexpr double mp2 = -0x1.DDE973C000000p-27;
+constexpr double pp3 = -0x1.CB3B398000000p-55;
+constexpr double pp4 = -0x1.d747f23e32ed7p-83;
+constexpr double hpinv = 0x1.45F306DC9C883p-1;
+constexpr double toint = 0x1.8p52;
+}  // namespace sc
+
+template <bool kFma = false>
+MPG_INLINE double taylor_sin(double xx, double a, double da) {
+  using namespace sc;
+  double p = mpg_fma<kFma>(mpg_fma<kFma>(mpg_fma<kFma>(mpg_fma<kFma>(s5, xx, s4), xx, s3), xx, s2), xx, s1);
+  double m2 = 0.5 * da;
+  double in = mpg_fma<kFma>(p, a, -m2);
+  double t = mpg_fma<kFma>(in, xx, da);
+  return a + t;
+}
+
+template <bool kFma = false>
+MPG_INLINE double do_cos(double x, double dx) {
+  using namespace sc;
+  if (x < 0) dx = -dx;
+  double u = big + std::fabs(x);
+  x = std::fabs(x) - (u - big) + dx;
+  double xx = x * x;
+  double s = mpg_fma<kFma>(x * xx, mpg_fma<kFma>(xx, sn5, sn3), x);
+  double c = xx * mpg_fma<kFma>(xx, mpg_fma<kFma>(xx, cs6, cs4), cs2);
+  int k = lo_word(u) << 2;
+  double sn = kSinCosTab[k], ssn = kSinCosTab[k + 1], cs = kSinCosTab[k + 2], ccs = kSinCosTab[k + 3];
+  double cor = mpg_fma<kFma>(-sn, s, mpg_fma<kFma>(-cs, c, mpg_fma<kFma>(-s, ssn, ccs)));
+  return cs + cor;
+}
+
+template <bool kFma = false>
+MPG_INLINE double do_sin(double x, double dx) {
+  using namespace sc;
+  double xold = x;
+  if (std::fabs(x) < 0.126) return taylor_sin<kFma>(x * x, x, dx);
+  if (x <= 0) dx = -dx;
+  double u = big + std::fabs(x);
+  x = std::fabs(x) - (u - big);
+  double xx = x * x;
+  double s = x + mpg_fma<kFma>(x * xx, mpg_fma<kFma>(xx, sn5, sn3), dx);
+  double c = mpg_fma<kFma>(x, dx, xx * mpg_fma<kFma>(xx, mpg_fma<kFma>(xx, cs6, cs4), cs2));
+  int k = lo_word(u) << 2;
+  double sn = kSinCosTab[k], ssn = kSinCosTab[k + 1], cs = kSinCosTab[k + 2], ccs = kSinCosTab[k + 3];
+  double cor = mpg_fma<kFma>(cs, s, mpg_fma<kFma>(-sn, c, mpg_fma<kFma>(s, ccs, ssn)));
+  return std::copysign(sn + cor, xold);
+}
+
+template <bool kFma = false>
+MPG_INLINE int reduce_sincos(double x, double* a, double* da) {
+  using namespace sc;
+  double t = mpg_fma<kFma>(x, hpinv, toint);
+  double xn = t - toint;
+  double y = mpg_fma<kFma>(-xn, mp2, mpg_fma<kFma>(-xn, mp1, x));
+  int n = lo_word(t) & 3;
+  double t2 = mpg_fma<kFma>(-xn, pp3, y);
+  double db = mpg_fma<kFma>(-xn, pp3, y - t2);
+  double b = mpg_fma<kFma>(-xn, pp4, t2);
+  db += mpg_fma<kFma>(-xn, pp4, t2 - b);
+  *a = b;
+  *da = db;
+  return n;
+}
+
+template <bool kFma = false>
+MPG_INLINE double do_sincos(double a, double da, int n) {
+  double r = (n & 1) ? do_cos<kFma>(a, da) : do_sin<kFma>(a, da);
+  return (n & 2) ? -r : r;
+}
+
+// Valid for |x| < 105414350 (glibc's reduce_sincos range); larger arguments
+// return NaN and are rejected by the host before launch.
+template <bool kFma = false>
+MPG_INLINE double mpg_sin(double x) {
+  using namespace sc;
+  uint32_t k = hi_word(x) & 0x7fffffffu;
+  if (k < 0x3e500000u) return x;
+  if (k < 0x3feb6000u) return do_sin<kFma>(x, 0);
+  if (k < 0x400368fdu) {
+    double t = hp0 - std::fabs(x);
+    return std::copysign(do_cos<kFma>(t, hp1), x);
+  }
+  if (k < 0x419921FBu) {
+    double a, da;
+    int n = reduce_sincos<kFma>(x, &a, &da);
+    return do_sincos<kFma>(a, da, n);
+  }
+  return x - x + NAN;
+}
+
+template <bool kFma = false>
+MPG_INLINE double mpg_cos(double x) {
+  using namespace sc;
+  uint32_t k = hi_word(x) & 0x7fffffffu;
+  if (k < 0x3e400000u) return 1.0;
+  if (k < 0x3feb6000u) return do_cos<kFma>(x, 0);
+  if (k < 0x400368fdu) {
+    double y = hp0 - std::fabs(x);
+    double a = y + hp1;
+    double da = (y - a) + hp1;
+    return do_sin<kFma>(a, da);
+  }
+  if (k < 0x419921FBu) {
+    double a, da;
+    int n = reduce_sincos<kFma>(x, &a, &da);
+    return do_sincos<kFma>(a, da, n + 1);
+  }
+  return x - x + NAN;
+}
+
+// --------------------------------------------------------------------------
+// SE(3) as R[9] (row-major) + p[3]
+// --------------------------------------------------------------------------
+struct SE3 {
+  double R[9];
+  double p[3];
+};
+
+MPG_INLINE void se3_identity(SE3& T) {
+  for (int i = 0; i < 9; ++i) T.R[i] = (i % 4 == 0) ? 1.0 : 0.0;
+  T.p[0] = T.p[1] = T.p[2] = 0.0;
+}
+
+// pinocchio SE3::__mult__ / Eigen Isometry product: R = A.R B.R entries
+// ((a_i0 b_0j + a_i1 b_1j) + a_i2 b_2j); p = A.R B.p + A.p.
+MPG_INLINE SE3 se3_mul(const SE3& A, const SE3& B) {
+  SE3 C;
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+      C.R[3 * i + j] = (A.R[3 * i] * B.R[j] + A.R[3 * i + 1] * B.R[3 + j]) + A.R[3 * i + 2] * B.R[6 + j];
+    C.p[i] = ((A.R[3 * i] * B.p[0] + A.R[3 * i + 1] * B.p[1]) + A.R[3 * i + 2] * B.p[2]) + A.p[i];
+  }
+  return C;
+}
+
+// Eigen QuaternionBase::toRotationMatrix, q = (w, x, y, z)
+MPG_INLINE void quat_to_mat(double w, double x, double y, double z, double* m) {
+  const double tx = 2.0 * x, ty = 2.0 * y, tz = 2.0 * z;
+  const double twx = tx * w, twy = ty * w, twz = tz * w;
+  const double txx = tx * x, txy = ty * x, txz = tz * x;
+  const double tyy = ty * y, tyz = tz * y, tzz = tz * z;
+  m[0] = 1.0 - (tyy + tzz);
+  m[1] = txy - twz;
+  m[2] = txz + twy;
+  m[3] = txy + twz;
+  m[4] = 1.0 - (txx + tzz);
+  m[5] = tyz - twx;
+  m[6] = txz - twy;
+  m[7] = tyz + twx;
+  m[8] = 1.0 - (txx + tyy);
+}
+
+// Eigen quaternionbase_assign_impl<Matrix3,3,3>; out (w, x, y, z)
+MPG_INLINE void mat_to_quat(const double* m, double* w_out, double* xyz) {
+  double t = (m[0] + m[4]) + m[8];
+  if (t > 0.0) {
+    t = std::sqrt(t + 1.0);
+    *w_out = 0.5 * t;
+    t = 0.5 / t;
+    xyz[0] = (m[7] - m[5]) * t;
+    xyz[1] = (m[2] - m[6]) * t;
+    xyz[2] = (m[3] - m[1]) * t;
+  } else {
+    int i = 0;
+    if (m[4] > m[0]) i = 1;
+    if (m[8] > m[3 * i + i]) i = 2;
+    int j = (i + 1) % 3, k = (j + 1) % 3;
+    t = std::sqrt(((m[3 * i + i] - m[3 * j + j]) - m[3 * k + k]) + 1.0);
+    double qi = 0.5 * t;
+    t = 0.5 / t;
+    double w = (m[3 * k + j] - m[3 * j + k]) * t;
+    double qj = (m[3 * j + i] + m[3 * i + j]) * t;
+    double qk = (m[3 * k + i] + m[3 * i + k]) * t;
+    *w_out = w;
+    // branch-free scatter keeps the arrays in registers on the GPU
+    xyz[0] = (i == 0) ? qi : (j == 0) ? qj : qk;
+    xyz[1] = (i == 1) ? qi : (j == 1) ? qj : qk;
+    xyz[2] = (i == 2) ? qi : (j == 2) ? qj : qk;
+  }
+}
+
+// pinocchio::toRotationMatrix(axis, cos, sin) for unaligned revolute joints
+MPG_INLINE void axis_rot(const double* ax, double c, double s, double* R) {
+  double sa0 = s * ax[0], sa1 = s * ax[1], sa2 = s * ax[2];
+  double c1 = 1.0 - c;
+  double ca0 = c1 * ax[0], ca1 = c1 * ax[1], ca2 = c1 * ax[2];
+  double tmp;
+  tmp = ca0 * ax[1];
+  R[1] = tmp - sa2;
+  R[3] = tmp + sa2;
+  tmp = ca0 * ax[2];
+  R[2] = tmp + sa1;
+  R[6] = tmp - sa1;
+  tmp = ca1 * ax[2];
+  R[5] = tmp - sa0;
+  R[7] = tmp + sa0;
+  R[0] = ca0 * ax[0] + c;
+  R[4] = ca1 * ax[1] + c;
+  R[8] = ca2 * ax[2] + c;
+}
+
+// --------------------------------------------------------------------------
+// libccd 2.1 vec3 / quat (ccd/vec3.h, ccd/quat.h)
+// --------------------------------------------------------------------------
+struct V3 {
+  double x, y, z;
+};
+
+MPG_INLINE V3 v3(double x, double y, double z) { return V3{x, y, z}; }
+MPG_INLINE V3 vsub(const V3& a, const V3& b) { return V3{a.x - b.x, a.y - b.y, a.z - b.z}; }
+MPG_INLINE V3 vadd(const V3& a, const V3& b) { return V3{a.x + b.x, a.y + b.y, a.z + b.z}; }
+MPG_INLINE V3 vscale(const V3& a, double k) { return V3{a.x * k, a.y * k, a.z * k}; }
+MPG_INLINE double vdot(const V3& a, const V3& b) {
+  double d = a.x * b.x;
+  d += a.y * b.y;
+  d += a.z * b.z;
+  return d;
+}
+MPG_INLINE V3 vcross(const V3& a, const V3& b) {
+  return V3{(a.y * b.z) - (a.z * b.y), (a.z * b.x) - (a.x * b.z), (a.x * b.y) - (a.y * b.x)};
+}
+MPG_INLINE V3 vnormalize(const V3& d) {
+  double k = 1.0 / std::sqrt(vdot(d, d));
+  return vscale(d, k);
+}
+
+// quaternion stored (x, y, z, w) as libccd does
+struct Q4 {
+  double x, y, z, w;
+};
+
+MPG_INLINE V3 quat_rot(const V3& v, const Q4& q) {
+  const double vx = v.x, vy = v.y, vz = v.z;
+  const double w = q.w, x = q.x, y = q.y, z = q.z;
+  const double c1x = y * vz - z * vy + w * vx;
+  const double c1y = z * vx - x * vz + w * vy;
+  const double c1z = x * vy - y * vx + w * vz;
+  const double c2x = y * c1z - z * c1y;
+  const double c2y = z * c1x - x * c1z;
+  const double c2z = x * c1y - y * c1x;
+  return V3{vx + 2 * c2x, vy + 2 * c2y, vz + 2 * c2z};
+}
+
+MPG_INLINE Q4 quat_invert2(const Q4& q) {
+  double len2 = q.x * q.x;
+  len2 += q.y * q.y;
+  len2 += q.z * q.z;
+  len2 += q.w * q.w;
+  // ccdQuatInvert returns -1 (leaving dest = src) when len2 < CCD_EPS; unit
+  // quaternions from Eigen never take that branch, kept for fidelity.
+  if (len2 < 2.220446049250313080847e-16) return q;
+  len2 = 1.0 / len2;
+  return Q4{-q.x * len2, -q.y * len2, -q.z * len2, q.w * len2};
+}
+
+// FCL shapeToGJK: Quaternion q(tf.linear()) -> rot (x,y,z,w)
+MPG_INLINE Q4 gjk_rot_from_matrix(const double* R) {
+  double w, xyz[3];
+  mat_to_quat(R, &w, xyz);
+  return Q4{xyz[0], xyz[1], xyz[2], w};
+}
+
+}  // namespace mpg

@@ -1,0 +1,89 @@
+"""The BASELINE.json benchmark worlds, built through the product API
+(``mplib_amd.pymp``) exactly as a user of the reference would build them.
+
+  cfg2  Panda self-collision (2^16 states, default_rng(0))
+  cfg3  Panda + 10 boxes: collision_avoidance.py:29-59 table/red/green/blue
+        (side = 2 x half_size) + 6 boxes from default_rng(1234);
+        ACM (panda_link0, table) = ALWAYS  (2^20 states, default_rng(1))
+  cfg4  Panda + 4 convex hulls (link3/link5/hand/link0 hulls at poses from
+        default_rng(4321))  (2^22 states sharded over GPUs, default_rng(2))
+
+States are uniform in the URDF joint limits (panda.urdf:37-157).
+"""
+from __future__ import annotations
+
+import os
+from typing import Tuple
+
+import numpy as np
+
+from . import pymp
+
+_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PANDA_DIR = os.path.join(_ROOT, "data", "panda")
+PANDA_LINKS = ["panda_link0", "panda_link1", "panda_link2", "panda_link3", "panda_link4", "panda_link5",
+               "panda_link6", "panda_link7", "panda_hand", "panda_leftfinger", "panda_rightfinger"]
+PANDA_JOINTS = ["panda_joint1", "panda_joint2", "panda_joint3", "panda_joint4", "panda_joint5", "panda_joint6",
+                "panda_joint7", "panda_finger_joint1", "panda_finger_joint2"]
+CFG_SEED = {2: 0, 3: 1, 4: 2}
+CFG_N = {2: 1 << 16, 3: 1 << 20, 4: 1 << 22}
+CFG_NAME = {2: "panda_self", 3: "panda_10boxes", 4: "panda_4convex"}
+
+
+def panda() -> "pymp.articulation.ArticulatedModel":
+    a = pymp.articulation.ArticulatedModel(os.path.join(PANDA_DIR, "panda.urdf"), os.path.join(PANDA_DIR, "panda.srdf"),
+                                           [0, 0, -9.81], PANDA_JOINTS, PANDA_LINKS, verbose=False, convex=True)
+    a.set_move_group("panda_hand")
+    return a
+
+
+def _boxes():
+    out = [("table", (0.8, 0.8, 0.05), (0.56, 0.0, -0.025)),
+           ("red_cube", (0.04, 0.04, 0.12), (0.7, 0.0, 0.06)),
+           ("green_cube", (0.08, 0.08, 0.01), (0.4, 0.3, 0.005)),
+           ("blue_cube", (0.1, 0.4, 0.2), (0.55, 0.0, 0.1))]
+    rng = np.random.default_rng(1234)
+    for k in range(6):
+        side = rng.uniform(0.02, 0.2, size=3)
+        c = rng.uniform([0.2, -0.5, 0.05], [0.8, 0.5, 0.8])
+        out.append((f"box{k}", tuple(float(s) for s in side), tuple(float(v) for v in c)))
+    return out
+
+
+def _hulls():
+    rng = np.random.default_rng(4321)
+    out = []
+    for k, name in enumerate(["link3", "link5", "hand", "link0"]):
+        pos = rng.uniform([0.3, -0.5, 0.0], [0.8, 0.5, 0.7])
+        q = rng.normal(size=4)
+        q /= np.linalg.norm(q)
+        out.append((f"hull{k}_panda_{name}", name, [float(v) for v in pos], [float(v) for v in q]))
+    return out
+
+
+def world(cfg: int):
+    """(PlanningWorld, ArticulatedModel) for a BASELINE config."""
+    art = panda()
+    w = pymp.planning_world.PlanningWorld([art], ["panda"], [], [])
+    if cfg == 3:
+        for name, side, pos in _boxes():
+            w.add_normal_object(name, pymp.fcl.CollisionObject(pymp.fcl.Box(list(side)), list(pos), [1, 0, 0, 0]))
+        w.get_allowed_collision_matrix().set_entry("panda_link0", "table", True)
+    elif cfg == 4:
+        mesh_dir = os.path.join(PANDA_DIR, "franka_description", "meshes", "collision")
+        for name, mesh, pos, quat in _hulls():
+            g = pymp.fcl.load_mesh_as_Convex(os.path.join(mesh_dir, mesh + ".stl.convex.stl"), [1, 1, 1])
+            w.add_normal_object(name, pymp.fcl.CollisionObject(g, pos, quat))
+    elif cfg != 2:
+        raise ValueError(f"unknown config {cfg}")
+    return w, art
+
+
+def joint_limits(art) -> np.ndarray:
+    lims = art.get_pinocchio_model().get_joint_limits()
+    return np.array([l[0] for l in lims[:7]], dtype=np.float64)
+
+
+def sample_states(art, n: int, seed: int) -> np.ndarray:
+    lim = joint_limits(art)
+    return np.random.default_rng(seed).uniform(lim[:, 0], lim[:, 1], size=(n, 7))

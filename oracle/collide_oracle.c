@@ -6,7 +6,8 @@
  *
  * Built with gcc -O2 -ffp-contract=off (no fused multiply-add anywhere), like
  * the reference (CMakeLists.txt:4-6: -O3, no -march => no FMA on x86-64).
- * sin/cos come from the host libm, exactly as pinocchio's SINCOS does.
+ * sin/cos come from the host libm's sincos(): pinocchio's SINCOS calls it on
+ * Linux, and GCC folds any sin(a); cos(a) pair into that one call anyway.
  *
  * Structure deliberately mirrors the reference and its third-party
  * dependencies so the restatement can be audited line by line:
@@ -31,6 +32,7 @@
  * examples/detect_collision.py known answers and by the Panda model facts,
  * and its sin/cos agree bit-for-bit with the host libm by construction.
  */
+#define _GNU_SOURCE
 #include <float.h>
 #include <math.h>
 #include <pthread.h>
@@ -175,8 +177,7 @@ static void joint_motion(int type, const real *axis, const real *qj, real *M) {
     real c, s;
     switch (type) {
     case JT_RX: case JT_RY: case JT_RZ: case JT_RU:
-        s = sin(qj[0]);
-        c = cos(qj[0]);
+        sincos(qj[0], &s, &c);
         break;
     case JT_RUBX: case JT_RUBY: case JT_RUBZ: case JT_RUBU:
         c = qj[0];
@@ -216,9 +217,11 @@ static void user_to_pin(const orc_world *w, const real *qu, real *qp) {
         if (j == 0) continue; /* universe: nq = nv = 0 */
         int start = w->jidx_q[j - 1];
         int t = w->jtype[j - 1];
-        if (t >= JT_RUBX) {
-            qp[start] = cos(qu[count]);
-            qp[start + 1] = sin(qu[count]);
+        if (t >= JT_RUBX) { /* std::cos; std::sin -> one sincos() after GCC folding */
+            double sv, cv;
+            sincos(qu[count], &sv, &cv);
+            qp[start] = cv;
+            qp[start + 1] = sv;
         } else {
             qp[start] = qu[count];
         }
@@ -555,8 +558,8 @@ static int portal_reach_tolerance(const ccd_simplex_t *portal, const ccd_support
     real dv3 = ccdVec3Dot(&portal->ps[3].v, dir);
     real dv4 = ccdVec3Dot(&v4->v, dir);
     real dot1 = dv4 - dv1, dot2 = dv4 - dv2, dot3 = dv4 - dv3;
-    dot1 = fmin(dot1, dot2);
-    dot1 = fmin(dot1, dot3);
+    dot1 = (dot1 < dot2) ? dot1 : dot2; /* CCD_FMIN */
+    dot1 = (dot1 < dot3) ? dot1 : dot3;
     return ccdEq(dot1, tol) || dot1 < tol;
 }
 

@@ -50,6 +50,15 @@ import numpy as np
 _libm = ctypes.CDLL(ctypes.util.find_library("m") or "libm.so.6")
 _libm.powf.restype = ctypes.c_float
 _libm.powf.argtypes = [ctypes.c_float, ctypes.c_float]
+_libm.sincos.restype = None
+_libm.sincos.argtypes = [ctypes.c_double, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]
+
+
+def sincos(x: float) -> Tuple[float, float]:
+    """glibc ``sincos``: what a GCC-built ``sin(a); cos(a)`` pair becomes."""
+    s, c = ctypes.c_double(), ctypes.c_double()
+    _libm.sincos(float(x), ctypes.byref(s), ctypes.byref(c))
+    return s.value, c.value
 
 
 def f32(x: float) -> float:
@@ -126,11 +135,13 @@ def mat_to_quat(m: Sequence[float]) -> Tuple[float, float, float, float]:
 
 
 def rpy_to_quat(r: float, p: float, y: float) -> Tuple[float, float, float, float]:
-    """urdfdom ``Rotation::setFromRPY`` followed by ``normalize``; returns (x,y,z,w)."""
+    """urdfdom ``Rotation::setFromRPY`` followed by ``normalize``; returns (x,y,z,w).
+    The sin/cos pairs of each half angle go through glibc ``sincos`` (GCC folds
+    urdfdom's ``sin(phi) ... cos(phi)`` into it)."""
     phi, the, psi = r / 2.0, p / 2.0, y / 2.0
-    sphi, cphi = math.sin(phi), math.cos(phi)
-    sthe, cthe = math.sin(the), math.cos(the)
-    spsi, cpsi = math.sin(psi), math.cos(psi)
+    sphi, cphi = sincos(phi)
+    sthe, cthe = sincos(the)
+    spsi, cpsi = sincos(psi)
     x = sphi * cthe * cpsi - cphi * sthe * spsi
     yy = cphi * sthe * cpsi + sphi * cthe * spsi
     z = cphi * cthe * spsi - sphi * sthe * cpsi

@@ -1,0 +1,18 @@
+"""Build tests/native/host_fk.cpp (product headers compiled for the host)."""
+import ctypes
+import os
+import subprocess
+import tempfile
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        out = os.path.join(tempfile.gettempdir(), "mplib_amd_host_fk_%d.so" % os.getuid())
+        src = os.path.join(_HERE, "host_fk.cpp")
+        subprocess.check_call(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-fPIC", "-shared", "-o", out, src])
+        _lib = ctypes.CDLL(out)
+    return _lib

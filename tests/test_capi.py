@@ -1,0 +1,72 @@
+"""CPU: the C-ABI library loads, exports every symbol include/mpgpu.h declares,
+and rejects malformed descriptors before touching a device."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+import worlds as Wd
+from mplib_amd import _capi as C
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared_symbols():
+    txt = open(os.path.join(ROOT, "include", "mpgpu.h")).read()
+    return sorted(set(re.findall(r"\b(mpg_[a-z_]+)\s*\(", txt)))
+
+
+def test_library_exports_header_symbols():
+    L = C.lib()
+    syms = declared_symbols()
+    assert "mpg_collide_batch" in syms and "mpg_world_create" in syms
+    for s in syms:
+        assert hasattr(L, s), s
+    assert set(syms) <= set(C.SIGNATURES), set(syms) - set(C.SIGNATURES)
+    assert C.lib().mpg_version().decode().startswith("mpgpu")
+
+
+def test_world_desc_layout_matches_header():
+    """ctypes WorldDesc mirrors mpg_world_desc field-for-field."""
+    txt = open(os.path.join(ROOT, "include", "mpgpu.h")).read()
+    body = txt[txt.index("typedef struct mpg_world_desc"):txt.index("} mpg_world_desc;")]
+    names = re.findall(r"\*?\s*([a-z_]+);", body)
+    assert names == [f[0] for f in C.WorldDesc._fields_]
+
+
+def _desc(ow, **over):
+    a = Wd.desc_arrays(ow)
+    a.update(over)
+    return a
+
+
+def _create(arrays):
+    from mplib_amd.batch import DeviceWorld
+    return DeviceWorld(arrays)
+
+
+@pytest.mark.parametrize("field,value,msg", [
+    ("joint_parent", [5, 0, 0, 0, 0, 0, 0, 0, 0], "joint_parent"),
+    ("moving_link", [99] * 11, "moving_link"),
+    ("pair_a", [500] * 129, "pair object id"),
+])
+def test_invalid_descriptor_rejected(field, value, msg):
+    ow = Wd.oracle_world(3)
+    with pytest.raises(ValueError, match=msg):
+        _create(_desc(ow, **{field: value}))
+
+
+def test_unsupported_pair_rejected():
+    """Box-box uses FCL's closed-form boxBox test, not MPR: refused, never approximated."""
+    ow = Wd.oracle_world(3)
+    a = _desc(ow)
+    # make a pair between two static boxes impossible -> use moving box instead
+    a["geom_type"] = list(a["geom_type"])
+    n_mov = len(a["moving_link"])
+    box_geom = a["static_geom"][0]
+    a["moving_geom"] = list(a["moving_geom"])
+    a["moving_geom"][0] = box_geom  # link0 is now a box; (link0, table) is box-box
+    with pytest.raises(NotImplementedError, match="closed-form"):
+        _create(a)
