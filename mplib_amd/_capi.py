@@ -83,6 +83,10 @@ def lib() -> ctypes.CDLL:
         if not os.path.exists(LIB_PATH):
             raise ImportError(f"mplib_amd: HIP library {LIB_PATH} is missing -- run `make -C mplib_amd` "
                               "(there is no CPU fallback)")
+        try:  # share torch's HIP runtime when torch is present (see mplib_amd/__init__.py)
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         L = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
             fn = getattr(L, name)
