@@ -42,6 +42,11 @@ struct DevWorld {
   const int* pair_a;          // [n_pairs]
   const int* pair_b;
   const int* pair_allowed;
+  // per user link: the joints from the root to link_parent[l] (1-based,
+  // root first) -- lets a thread rebuild one link's oMi without the others
+  const int* link_chain_start;  // [n_links]
+  const int* link_chain_len;    // [n_links]
+  const int* chain_joints;
 };
 
 MPG_INLINE SE3 load_se3(const double* p) {
@@ -102,10 +107,29 @@ MPG_HD inline void forward_kinematics(const DevWorld& w, const double* __restric
   }
 }
 
-// getLinkPose + ArticulatedModel::setQpos re-matrix: returns the link
-// Isometry FCL sees, plus the (p, wxyz) pose vector.
-MPG_INLINE SE3 link_transform(const DevWorld& w, const FkState& st, int l, double* pose7) {
-  const SE3 L = se3_mul(st.oMi[w.link_parent[l]], load_se3(w.link_place + 12 * l));
+// oMi[link_parent[l]] by folding liMi along the link's joint chain: the same
+// products, in the same order, as forward_kinematics (oMi[j] = oMi[parent] *
+// liMi[j], oMi[j] = liMi[j] when the parent is the universe), without storing
+// the other joints.
+MPG_INLINE SE3 chain_oMi(const DevWorld& w, const double* __restrict__ qrow, int l) {
+  const int cs = w.link_chain_start[l], cl = w.link_chain_len[l];
+  SE3 T;
+  se3_identity(T);
+  for (int k = 0; k < cl; ++k) {
+    const int j = w.chain_joints[cs + k];
+    const int src = w.joint_q_source[j - 1];
+    const double v = src >= 0 ? qrow[src] : w.joint_q_const[j - 1];
+    const SE3 M = joint_motion(w.joint_type[j - 1], w.joint_axis + 3 * (j - 1), v);
+    const SE3 li = se3_mul(load_se3(w.joint_place + 12 * (j - 1)), M);
+    T = k == 0 ? li : se3_mul(T, li);
+  }
+  return T;
+}
+
+// Quaternion round trip of getLinkPose (pinocchio_model.cpp:277-312) then the
+// re-matrix of ArticulatedModel::setQpos (articulated_model.cpp:119-124).
+MPG_INLINE SE3 link_from_oMi(const DevWorld& w, const SE3& oMi_parent, int l, double* pose7) {
+  const SE3 L = se3_mul(oMi_parent, load_se3(w.link_place + 12 * l));
   double qw, qxyz[3];
   mat_to_quat(L.R, &qw, qxyz);
   SE3 T;
@@ -118,6 +142,12 @@ MPG_INLINE SE3 link_transform(const DevWorld& w, const FkState& st, int l, doubl
     pose7[3] = qw; pose7[4] = qxyz[0]; pose7[5] = qxyz[1]; pose7[6] = qxyz[2];
   }
   return T;
+}
+
+// getLinkPose + ArticulatedModel::setQpos re-matrix: returns the link
+// Isometry FCL sees, plus the (p, wxyz) pose vector.
+MPG_INLINE SE3 link_transform(const DevWorld& w, const FkState& st, int l, double* pose7) {
+  return link_from_oMi(w, st.oMi[w.link_parent[l]], l, pose7);
 }
 
 }  // namespace mpg

@@ -28,6 +28,7 @@
 #include <cfloat>
 #include <cstdio>
 #include <cstring>
+#include <map>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -231,19 +232,6 @@ struct WObb {
   double r;
 };
 
-__device__ __forceinline__ WObb world_obb_moving(const DevWorld& w, const GObj& o) {
-  const double* rec = w.geom_rec + G_STRIDE * o.geom;
-  WObb b;
-  quat_to_mat(o.rot.w, o.rot.x, o.rot.y, o.rot.z, b.R);
-  const V3 lc = v3(rec[G_OBB_C], rec[G_OBB_C + 1], rec[G_OBB_C + 2]);
-  b.c = vadd(v3((b.R[0] * lc.x + b.R[1] * lc.y) + b.R[2] * lc.z, (b.R[3] * lc.x + b.R[4] * lc.y) + b.R[5] * lc.z,
-                (b.R[6] * lc.x + b.R[7] * lc.y) + b.R[8] * lc.z),
-             o.pos);
-  b.e = v3(rec[G_OBB_E], rec[G_OBB_E + 1], rec[G_OBB_E + 2]);
-  b.r = rec[G_RADIUS];
-  return b;
-}
-
 __device__ __forceinline__ bool obb_separated(const WObb& A, const WObb& B, double margin) {
   const V3 d = vsub(B.c, A.c);
   const double rr = A.r + B.r + margin;
@@ -301,46 +289,80 @@ __device__ __forceinline__ SE3 link_from_pose7(const double* p7) {
   return T;
 }
 
+// Moving object -> FCL GJK object (shapeToGJK on link pose * offset).
+template <bool FROM_POSES>
+__device__ __forceinline__ GObj moving_obj(const DevWorld& w, const double* __restrict__ in, long long cfg, int id) {
+  const int l = w.moving_link[id];
+  const SE3 L = FROM_POSES ? link_from_pose7(in + (cfg * w.n_links + l) * 7)
+                           : link_from_oMi(w, chain_oMi(w, in + cfg * w.dof, l), l, nullptr);
+  const SE3 T = se3_mul(L, load_se3(w.moving_offset + 12 * id));
+  GObj o;
+  o.rot = gjk_rot_from_matrix(T.R);
+  o.rot_inv = quat_invert2(o.rot);
+  o.pos = v3(T.p[0], T.p[1], T.p[2]);
+  o.geom = w.moving_geom[id];
+  o.type = w.geom_type[o.geom];
+  return o;
+}
+
+__device__ __forceinline__ GObj static_obj(const DevWorld& w, int sid) {
+  const double* r = w.static_rec + S_STRIDE * sid;
+  GObj o;
+  o.rot = Q4{r[S_ROT], r[S_ROT + 1], r[S_ROT + 2], r[S_ROT + 3]};
+  o.rot_inv = Q4{r[S_ROTINV], r[S_ROTINV + 1], r[S_ROTINV + 2], r[S_ROTINV + 3]};
+  o.pos = v3(r[S_POS], r[S_POS + 1], r[S_POS + 2]);
+  o.geom = w.static_geom[sid];
+  o.type = w.geom_type[o.geom];
+  return o;
+}
+
+__device__ __forceinline__ uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
+
+// ---------------------------------------------------------------------------
+// Phase A: one lane per configuration.  FK -> per-object broad-phase record in
+// LDS ([object][7][lane]: GJK quaternion xyzw + world OBB centre) -> every
+// pair's conservative cull.  Survivors are appended to the pair's candidate
+// list with one atomic per wave (ballot + mbcnt), so phase B sees each pair's
+// configurations contiguously.  Also zeroes this configuration's outputs.
+// ---------------------------------------------------------------------------
 template <int BLOCK, bool FROM_POSES>
-__global__ __launch_bounds__(BLOCK) void collide_kernel(DevWorld w, const double* __restrict__ q, long long n,
-                                                       uint8_t* __restrict__ flags, uint32_t* __restrict__ masks) {
-  extern __shared__ __attribute__((aligned(16))) double lds[];  // [n_moving][7][BLOCK]
+__global__ __launch_bounds__(BLOCK) void cull_kernel(DevWorld w, const double* __restrict__ in, long long n,
+                                                    uint8_t* __restrict__ flags, uint32_t* __restrict__ masks,
+                                                    uint32_t* __restrict__ counts, uint32_t* __restrict__ cand,
+                                                    long long cap) {
+  extern __shared__ __attribute__((aligned(16))) double lds[];
   const int tid = threadIdx.x;
   const long long cfg = (long long)blockIdx.x * BLOCK + tid;
-  if (cfg >= n) return;
-
+  const bool live = cfg < n;
+  const long long c = live ? cfg : n - 1;  // dead lanes shadow a valid row and never append
+  if (live) {
+    flags[cfg] = 0;
+    if (masks)
+      for (int k = 0; k < w.W; ++k) masks[cfg * w.W + k] = 0u;
+  }
   {
     FkState st;
-    if (!FROM_POSES) forward_kinematics(w, q + cfg * w.dof, st);
+    if (!FROM_POSES) forward_kinematics(w, in + c * w.dof, st);
     for (int m = 0; m < w.n_moving; ++m) {
       const int l = w.moving_link[m];
-      const SE3 L = FROM_POSES ? link_from_pose7(q + (cfg * w.n_links + l) * 7) : link_transform(w, st, l, nullptr);
+      const SE3 L = FROM_POSES ? link_from_pose7(in + (c * w.n_links + l) * 7) : link_transform(w, st, l, nullptr);
       const SE3 T = se3_mul(L, load_se3(w.moving_offset + 12 * m));
       const Q4 r = gjk_rot_from_matrix(T.R);
+      const double* rec = w.geom_rec + G_STRIDE * w.moving_geom[m];
       double* slot = lds + (size_t)m * 7 * BLOCK + tid;
       slot[0 * BLOCK] = r.x;
       slot[1 * BLOCK] = r.y;
       slot[2 * BLOCK] = r.z;
       slot[3 * BLOCK] = r.w;
-      slot[4 * BLOCK] = T.p[0];
-      slot[5 * BLOCK] = T.p[1];
-      slot[6 * BLOCK] = T.p[2];
+#pragma unroll
+      for (int i = 0; i < 3; ++i)
+        slot[(4 + i) * BLOCK] = ((T.R[3 * i] * rec[G_OBB_C] + T.R[3 * i + 1] * rec[G_OBB_C + 1]) +
+                                 T.R[3 * i + 2] * rec[G_OBB_C + 2]) + T.p[i];
     }
   }
-
-  uint32_t word = 0;
-  int cur = 0;
-  bool any = false;
-  uint32_t* out = masks ? masks + cfg * w.W : nullptr;
+  const uint32_t lane = lane_id();
   for (int p = 0; p < w.n_pairs; ++p) {
-    if ((p >> 5) != cur) {
-      if (out) out[cur] = word;
-      any |= word != 0;
-      word = 0;
-      cur = p >> 5;
-    }
-    if (w.pair_allowed[p]) continue;
-    GObj o[2];
+    if (w.pair_allowed[p]) continue;  // filterCollisions drops it whatever MPR says
     WObb box[2];
     const int ids[2] = {w.pair_a[p], w.pair_b[p]};
 #pragma unroll
@@ -348,34 +370,95 @@ __global__ __launch_bounds__(BLOCK) void collide_kernel(DevWorld w, const double
       const int id = ids[s];
       if (id < w.n_moving) {
         const double* slot = lds + (size_t)id * 7 * BLOCK + tid;
-        o[s].rot = Q4{slot[0], slot[BLOCK], slot[2 * BLOCK], slot[3 * BLOCK]};
-        o[s].pos = v3(slot[4 * BLOCK], slot[5 * BLOCK], slot[6 * BLOCK]);
-        o[s].geom = w.moving_geom[id];
-        o[s].rot_inv = quat_invert2(o[s].rot);
-        o[s].type = w.geom_type[o[s].geom];
-        box[s] = world_obb_moving(w, o[s]);
+        const double* g = w.geom_rec + G_STRIDE * w.moving_geom[id];
+        box[s].c = v3(slot[4 * BLOCK], slot[5 * BLOCK], slot[6 * BLOCK]);
+        box[s].e = v3(g[G_OBB_E], g[G_OBB_E + 1], g[G_OBB_E + 2]);
+        box[s].r = g[G_RADIUS];
       } else {
-        const int sid = id - w.n_moving;
-        const double* r = w.static_rec + S_STRIDE * sid;
-        o[s].rot = Q4{r[S_ROT], r[S_ROT + 1], r[S_ROT + 2], r[S_ROT + 3]};
-        o[s].rot_inv = Q4{r[S_ROTINV], r[S_ROTINV + 1], r[S_ROTINV + 2], r[S_ROTINV + 3]};
-        o[s].pos = v3(r[S_POS], r[S_POS + 1], r[S_POS + 2]);
-        o[s].geom = w.static_geom[sid];
-        o[s].type = w.geom_type[o[s].geom];
+        const double* r = w.static_rec + S_STRIDE * (id - w.n_moving);
+        const double* g = w.geom_rec + G_STRIDE * w.static_geom[id - w.n_moving];
         box[s].c = v3(r[S_OBBC], r[S_OBBC + 1], r[S_OBBC + 2]);
-#pragma unroll
-        for (int k = 0; k < 9; ++k) box[s].R[k] = r[S_R + k];
-        const double* g = w.geom_rec + G_STRIDE * o[s].geom;
         box[s].e = v3(g[G_OBB_E], g[G_OBB_E + 1], g[G_OBB_E + 2]);
         box[s].r = g[G_RADIUS];
       }
     }
-    if (obb_separated(box[0], box[1], w.cull_margin)) continue;
-    if (mpr_intersect(w, o[0], o[1])) word |= 1u << (p & 31);
+    bool keep = false;
+    const V3 d = vsub(box[1].c, box[0].c);
+    const double rr = box[0].r + box[1].r + w.cull_margin;
+    if (live && vdot(d, d) <= rr * rr) {  // bounding spheres overlap: run the 15-axis SAT
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const int id = ids[s];
+        if (id < w.n_moving) {
+          const double* slot = lds + (size_t)id * 7 * BLOCK + tid;
+          quat_to_mat(slot[3 * BLOCK], slot[0], slot[BLOCK], slot[2 * BLOCK], box[s].R);
+        } else {
+          const double* r = w.static_rec + S_STRIDE * (id - w.n_moving);
+#pragma unroll
+          for (int k = 0; k < 9; ++k) box[s].R[k] = r[S_R + k];
+        }
+      }
+      keep = !obb_separated(box[0], box[1], w.cull_margin);
+    }
+    const unsigned long long bal = __ballot(keep);
+    if (bal) {
+      uint32_t base = 0;
+      if (lane == 0) base = atomicAdd(&counts[p], (uint32_t)__popcll(bal));
+      base = __shfl(base, 0);
+      if (keep) {
+        const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+        cand[(long long)p * cap + base + rank] = (uint32_t)cfg;
+      }
+    }
   }
-  if (out) out[cur] = word;
-  any |= word != 0;
-  flags[cfg] = any ? 1 : 0;
+}
+
+// Exclusive scan of per-pair chunk counts (64 candidates per chunk).
+__global__ void chunk_scan_kernel(const uint32_t* __restrict__ counts, int n_pairs, uint32_t* __restrict__ prefix) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  uint32_t acc = 0;
+  for (int p = 0; p < n_pairs; ++p) {
+    prefix[p] = acc;
+    acc += (counts[p] + 63u) >> 6;
+  }
+  prefix[n_pairs] = acc;
+}
+
+// ---------------------------------------------------------------------------
+// Phase B: exact narrow phase.  Each wave takes 64 candidates of ONE pair, so
+// every lane scans the same hull (wave-uniform scalar loads of the vertices)
+// and only the MPR iteration count diverges.  Poses are rebuilt in fp64 from
+// the joint values (chain FK), bit-identical to phase A / the reference.
+// ---------------------------------------------------------------------------
+template <bool FROM_POSES>
+__global__ __launch_bounds__(256) void narrow_kernel(DevWorld w, const double* __restrict__ in,
+                                                    const uint32_t* __restrict__ counts,
+                                                    const uint32_t* __restrict__ prefix,
+                                                    const uint32_t* __restrict__ cand, long long cap,
+                                                    uint8_t* __restrict__ flags, uint32_t* __restrict__ masks) {
+  const uint32_t lane = lane_id();
+  const uint32_t wave = __builtin_amdgcn_readfirstlane((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+  const uint32_t n_waves = (gridDim.x * blockDim.x) >> 6;
+  const uint32_t total = prefix[w.n_pairs];
+  for (uint32_t ch = wave; ch < total; ch += n_waves) {
+    int lo = 0, hi = w.n_pairs;  // prefix[lo] <= ch < prefix[hi]
+    while (hi - lo > 1) {
+      const int mid = (lo + hi) >> 1;
+      if (prefix[mid] <= ch) lo = mid;
+      else hi = mid;
+    }
+    const int p = lo;
+    const uint32_t idx = (ch - prefix[p]) * 64u + lane;
+    if (idx >= counts[p]) continue;
+    const long long cfg = cand[(long long)p * cap + idx];
+    const int a = w.pair_a[p], b = w.pair_b[p];
+    const GObj A = a < w.n_moving ? moving_obj<FROM_POSES>(w, in, cfg, a) : static_obj(w, a - w.n_moving);
+    const GObj B = b < w.n_moving ? moving_obj<FROM_POSES>(w, in, cfg, b) : static_obj(w, b - w.n_moving);
+    if (mpr_intersect(w, A, B)) {
+      if (masks) atomicOr(&masks[cfg * w.W + (p >> 5)], 1u << (p & 31));
+      flags[cfg] = 1;
+    }
+  }
 }
 
 __global__ void fk_kernel(DevWorld w, const double* __restrict__ q, long long n, double* __restrict__ out) {
@@ -413,6 +496,17 @@ struct mpg_world {
   double* d_out = nullptr;
   size_t cap_cfg = 0;
   size_t cap_out = 0;
+  // phase A/B workspace, one per stream so concurrent streams never share it
+  struct Workspace {
+    uint32_t* counts = nullptr;  // [n_pairs]
+    uint32_t* prefix = nullptr;  // [n_pairs + 1]
+    uint32_t* cand = nullptr;    // [n_pairs * cap]
+    long long cap = 0;
+  };
+  std::mutex ws_mu;
+  std::map<hipStream_t, Workspace> ws;
+  long long max_chunk = 1 << 20;
+  int narrow_blocks = 1024;
 };
 
 namespace {
@@ -566,26 +660,63 @@ int choose_block(int n_moving, size_t* lds) {
   return block;
 }
 
-template <bool FROM_POSES>
-int launch_collide(mpg_world* w, const double* q, long long n, uint8_t* flags, uint32_t* masks, hipStream_t stream) {
-  if (n == 0) return MPG_OK;
-  const long long grid = (n + w->block - 1) / w->block;
-  if (grid > 0x7fffffffLL) return set_error(MPG_E_INVALID, "batch too large for one launch");
-  switch (w->block) {
-    case 256:
-      hipLaunchKernelGGL((collide_kernel<256, FROM_POSES>), dim3((unsigned)grid), dim3(256), w->lds_bytes, stream,
-                         w->dw, q, n, flags, masks);
-      break;
-    case 128:
-      hipLaunchKernelGGL((collide_kernel<128, FROM_POSES>), dim3((unsigned)grid), dim3(128), w->lds_bytes, stream,
-                         w->dw, q, n, flags, masks);
-      break;
-    default:
-      hipLaunchKernelGGL((collide_kernel<64, FROM_POSES>), dim3((unsigned)grid), dim3(64), w->lds_bytes, stream,
-                         w->dw, q, n, flags, masks);
-      break;
+int get_workspace(mpg_world* w, hipStream_t s, long long want, mpg_world::Workspace** out) {
+  std::lock_guard<std::mutex> lk(w->ws_mu);
+  auto& ws = w->ws[s];
+  const long long np = std::max(w->dw.n_pairs, 1);
+  if (ws.cap < want) {
+    if (ws.counts) HIP_TRY(hipFree(ws.counts));
+    if (ws.prefix) HIP_TRY(hipFree(ws.prefix));
+    if (ws.cand) HIP_TRY(hipFree(ws.cand));
+    ws = mpg_world::Workspace{};
+    HIP_TRY(hipMalloc(&ws.counts, sizeof(uint32_t) * np));
+    HIP_TRY(hipMalloc(&ws.prefix, sizeof(uint32_t) * (np + 1)));
+    HIP_TRY(hipMalloc(&ws.cand, sizeof(uint32_t) * np * want));
+    ws.cap = want;
   }
-  HIP_TRY(hipGetLastError());
+  *out = &ws;
+  return MPG_OK;
+}
+
+template <bool FROM_POSES>
+int launch_collide(mpg_world* w, const double* in, long long n, uint8_t* flags, uint32_t* masks, hipStream_t stream) {
+  if (n == 0) return MPG_OK;
+  const long long chunk = std::min<long long>(n, w->max_chunk);
+  mpg_world::Workspace* ws = nullptr;
+  int rc = get_workspace(w, stream, chunk, &ws);
+  if (rc) return rc;
+  const size_t row = FROM_POSES ? (size_t)w->dw.n_links * 7 : (size_t)w->dw.dof;
+  for (long long off = 0; off < n; off += chunk) {
+    const long long m = std::min(chunk, n - off);
+    const double* qin = in + off * row;
+    uint8_t* fl = flags + off;
+    uint32_t* mk = masks ? masks + off * w->dw.W : nullptr;
+    HIP_TRY(hipMemsetAsync(ws->counts, 0, sizeof(uint32_t) * std::max(w->dw.n_pairs, 1), stream));
+    const unsigned grid = (unsigned)((m + w->block - 1) / w->block);
+    switch (w->block) {
+      case 256:
+        hipLaunchKernelGGL((cull_kernel<256, FROM_POSES>), dim3(grid), dim3(256), w->lds_bytes, stream, w->dw, qin,
+                           m, fl, mk, ws->counts, ws->cand, ws->cap);
+        break;
+      case 128:
+        hipLaunchKernelGGL((cull_kernel<128, FROM_POSES>), dim3(grid), dim3(128), w->lds_bytes, stream, w->dw, qin,
+                           m, fl, mk, ws->counts, ws->cand, ws->cap);
+        break;
+      default:
+        hipLaunchKernelGGL((cull_kernel<64, FROM_POSES>), dim3(grid), dim3(64), w->lds_bytes, stream, w->dw, qin, m,
+                           fl, mk, ws->counts, ws->cand, ws->cap);
+        break;
+    }
+    HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(chunk_scan_kernel, dim3(1), dim3(64), 0, stream, ws->counts, w->dw.n_pairs, ws->prefix);
+    HIP_TRY(hipGetLastError());
+    // persistent narrow phase: enough waves to fill the chip, fewer for tiny batches
+    const long long want_waves = (m * std::max(w->dw.n_pairs, 1) + 63) / 64;
+    const unsigned nb = (unsigned)std::max<long long>(1, std::min<long long>(w->narrow_blocks, (want_waves + 3) / 4));
+    hipLaunchKernelGGL((narrow_kernel<FROM_POSES>), dim3(nb), dim3(256), 0, stream, w->dw, qin, ws->counts,
+                       ws->prefix, ws->cand, ws->cap, fl, mk);
+    HIP_TRY(hipGetLastError());
+  }
   return MPG_OK;
 }
 
@@ -648,6 +779,16 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
   std::vector<double> verts4((size_t)4 * std::max<int64_t>(d->n_vertices, 1), 0.0);
   for (int64_t i = 0; i < d->n_vertices; ++i)
     for (int k = 0; k < 3; ++k) verts4[4 * i + k] = d->vertices[3 * i + k];
+  // per link: joints from the root to link_parent (chain FK in phase B)
+  std::vector<int> chain_start, chain_len, chain_joints;
+  for (int l = 0; l < d->n_links; ++l) {
+    std::vector<int> c;
+    for (int j = d->link_parent[l]; j > 0; j = d->joint_parent[j - 1]) c.push_back(j);
+    std::reverse(c.begin(), c.end());
+    chain_start.push_back((int)chain_joints.size());
+    chain_len.push_back((int)c.size());
+    chain_joints.insert(chain_joints.end(), c.begin(), c.end());
+  }
   std::vector<int> allowed(std::max(d->n_pairs, 1), 0);
   for (int p = 0; p < d->n_pairs; ++p) allowed[p] = d->pair_allowed ? (d->pair_allowed[p] != 0) : 0;
 
@@ -673,6 +814,9 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
   const size_t o_pa = bb.add(d->pair_a, d->n_pairs);
   const size_t o_pb = bb.add(d->pair_b, d->n_pairs);
   const size_t o_al = bb.add(allowed.data(), allowed.size());
+  const size_t o_cs = bb.add(chain_start.data(), chain_start.size());
+  const size_t o_cl = bb.add(chain_len.data(), chain_len.size());
+  const size_t o_cj = bb.add(chain_joints.data(), chain_joints.size());
 
   mpg_world* w = new mpg_world();
   w->device = device;
@@ -723,6 +867,14 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
   dw.pair_a = reinterpret_cast<const int*>(base + o_pa);
   dw.pair_b = reinterpret_cast<const int*>(base + o_pb);
   dw.pair_allowed = reinterpret_cast<const int*>(base + o_al);
+  dw.link_chain_start = reinterpret_cast<const int*>(base + o_cs);
+  dw.link_chain_len = reinterpret_cast<const int*>(base + o_cl);
+  dw.chain_joints = reinterpret_cast<const int*>(base + o_cj);
+  int cus = 256;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0) cus = 256;
+  w->narrow_blocks = cus * 4;
+  // bound the candidate lists to 1 GiB: cap * n_pairs * 4 B
+  w->max_chunk = std::max<long long>(4096, std::min<long long>(1 << 20, (1ll << 28) / std::max(d->n_pairs, 1)));
   *out = w;
   return MPG_OK;
 }
@@ -735,6 +887,11 @@ int mpg_world_destroy(mpg_world* w) {
   hipFree(w->d_flags);
   hipFree(w->d_masks);
   hipFree(w->d_out);
+  for (auto& kv : w->ws) {
+    hipFree(kv.second.counts);
+    hipFree(kv.second.prefix);
+    hipFree(kv.second.cand);
+  }
   delete w;
   return MPG_OK;
 }
