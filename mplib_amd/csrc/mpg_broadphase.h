@@ -1,0 +1,368 @@
+// mpg_broadphase.h -- phase A of the batched collide(): a conservative fp32
+// broad phase that decides, per (configuration, pair), whether the exact fp64
+// narrow phase (FCL/libccd MPR, phase B) has to run at all.
+//
+// The reference has no broad phase for these pairs: PlanningWorld::collideFull
+// (src/planning_world.cpp:484-490) calls ::fcl::collide on every pair.  A pair
+// culled here is one whose bounding volumes are separated by more than
+// kBpMargin, so MPR would report "no intersection" for it; the output bits are
+// therefore identical to evaluating every pair.  Soundness budget (DESIGN.md
+// "Broad phase"): fp32 FK + record rounding is bounded by ~2e-5 m for a
+// 10-joint chain at 1.5 m reach (measured max 1e-6 m, tests/test_broadphase.py),
+// MPR's own tolerance is gjk_tolerance = 1e-6 m; kBpMargin = 1e-4 m covers
+// both with >= 5x headroom.
+//
+// Everything here compiles for the host too (tests/native/host_fk.cpp) so the
+// fp32-vs-fp64 pose error is checked on the CPU.
+#pragma once
+#include <cmath>
+#include <vector>
+
+#include "mpg_math.h"
+#include "../../include/mpgpu.h"
+
+namespace mpg {
+
+constexpr float kBpMargin = 1e-4f;  // metres
+
+// per moving object float record: local OBB centre, half extents, radius
+enum { BM_C = 0, BM_E = 3, BM_R = 6, BM_STRIDE = 8 };
+// per static object float record: world OBB centre, axes (R columns), extents
+enum { BS_C = 0, BS_R = 3, BS_E = 12, BS_STRIDE = 16 };
+
+// Read-only view of the broad-phase program (device snapshot or host vectors).
+struct BpView {
+  int nj, n_links, n_moving, n_static, n_saves;
+  const int* joint_type;      // [nj]
+  const int* joint_q_source;  // [nj]
+  const double* joint_q_const;
+  const int* jsrc;   // [nj] -1: parent is the universe, 0: previous joint, k>0: save slot k-1
+  const int* jsave;  // [nj] save slot or -1
+  const float* jaxis;   // [nj*3]
+  const float* jplace;  // [nj*12]
+  const int* link_start;  // [nj+2] links grouped by parent joint
+  const int* link_order;  // [n_links]
+  const float* lplace;    // [n_links*12]
+  const int* obj_start;   // [n_links+1] moving objects grouped by link
+  const int* obj_order;   // [n_moving]
+  const int* moving_link; // [n_moving]
+  const float* moff;      // [n_moving*12]
+  const float* mobj;      // [n_moving*BM_STRIDE]
+  const float* sobj;      // [n_static*BS_STRIDE]
+};
+
+struct F34 {
+  float R[9];  // row-major
+  float p[3];
+};
+
+MPG_INLINE F34 f34_load(const float* a) {
+  F34 T;
+#pragma unroll
+  for (int i = 0; i < 9; ++i) T.R[i] = a[i];
+  T.p[0] = a[9];
+  T.p[1] = a[10];
+  T.p[2] = a[11];
+  return T;
+}
+
+MPG_INLINE F34 f34_mul(const F34& A, const F34& B) {
+  F34 C;
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+      C.R[3 * i + j] = A.R[3 * i] * B.R[j] + A.R[3 * i + 1] * B.R[3 + j] + A.R[3 * i + 2] * B.R[6 + j];
+    C.p[i] = A.R[3 * i] * B.p[0] + A.R[3 * i + 1] * B.p[1] + A.R[3 * i + 2] * B.p[2] + A.p[i];
+  }
+  return C;
+}
+
+MPG_INLINE void f_quat_to_mat(float w, float x, float y, float z, float* m) {
+  const float tx = 2.f * x, ty = 2.f * y, tz = 2.f * z;
+  const float twx = tx * w, twy = ty * w, twz = tz * w;
+  const float txx = tx * x, txy = ty * x, txz = tz * x;
+  const float tyy = ty * y, tyz = tz * y, tzz = tz * z;
+  m[0] = 1.f - (tyy + tzz);
+  m[1] = txy - twz;
+  m[2] = txz + twy;
+  m[3] = txy + twz;
+  m[4] = 1.f - (txx + tzz);
+  m[5] = tyz - twx;
+  m[6] = txz - twy;
+  m[7] = tyz + twx;
+  m[8] = 1.f - (txx + tyy);
+}
+
+// rotation -> unit quaternion (x, y, z, w); Shepperd's method, branch-free selects
+MPG_INLINE void f_mat_to_quat(const float* m, float* q) {
+  const float t0 = m[0] + m[4] + m[8];
+  const float d0 = 1.f + t0, d1 = 1.f + m[0] - m[4] - m[8], d2 = 1.f - m[0] + m[4] - m[8],
+              d3 = 1.f - m[0] - m[4] + m[8];
+  int k = 0;
+  float best = d0;
+  if (d1 > best) { best = d1; k = 1; }
+  if (d2 > best) { best = d2; k = 2; }
+  if (d3 > best) { best = d3; k = 3; }
+  const float s = 0.5f / sqrtf(best);
+  const float h = 0.5f * sqrtf(best);
+  const float a = (m[7] - m[5]) * s, b = (m[2] - m[6]) * s, c = (m[3] - m[1]) * s;  // w*4 components
+  const float e = (m[1] + m[3]) * s, f = (m[2] + m[6]) * s, g = (m[5] + m[7]) * s;
+  // k = 0: w = h, (a, b, c); k = 1: x = h, w = a, y = e, z = f; ...
+  q[0] = k == 0 ? a : k == 1 ? h : k == 2 ? e : f;
+  q[1] = k == 0 ? b : k == 1 ? e : k == 2 ? h : g;
+  q[2] = k == 0 ? c : k == 1 ? f : k == 2 ? g : h;
+  q[3] = k == 0 ? h : k == 1 ? a : k == 2 ? b : c;
+}
+
+// revolute angles are reduced in fp64 before the fp32 sincos so large user
+// values (continuous joints) keep full fp32 accuracy
+MPG_INLINE F34 f_joint_motion(int type, const float* axis, double v) {
+  F34 M;
+#pragma unroll
+  for (int i = 0; i < 9; ++i) M.R[i] = (i % 4 == 0) ? 1.f : 0.f;
+  M.p[0] = M.p[1] = M.p[2] = 0.f;
+  if (type <= MPG_JOINT_REVOLUTE_UNALIGNED || type >= MPG_JOINT_RUBX) {
+    const double k = rint(v * 0.15915494309189535);
+    const float a = (float)(v - k * 6.283185307179586);
+    const float s = sinf(a), c = cosf(a);
+    const int t = (type >= MPG_JOINT_RUBX) ? type - MPG_JOINT_RUBX : type;
+    if (t == 0) {
+      M.R[4] = c; M.R[5] = -s; M.R[7] = s; M.R[8] = c;
+    } else if (t == 1) {
+      M.R[0] = c; M.R[2] = s; M.R[6] = -s; M.R[8] = c;
+    } else if (t == 2) {
+      M.R[0] = c; M.R[1] = -s; M.R[3] = s; M.R[4] = c;
+    } else {  // Rodrigues about a unit axis
+      const float x = axis[0], y = axis[1], z = axis[2], u = 1.f - c;
+      M.R[0] = c + x * x * u;     M.R[1] = x * y * u - z * s; M.R[2] = x * z * u + y * s;
+      M.R[3] = y * x * u + z * s; M.R[4] = c + y * y * u;     M.R[5] = y * z * u - x * s;
+      M.R[6] = z * x * u - y * s; M.R[7] = z * y * u + x * s; M.R[8] = c + z * z * u;
+    }
+  } else {
+    const float f = (float)v;
+    if (type == MPG_JOINT_PX) M.p[0] = f;
+    else if (type == MPG_JOINT_PY) M.p[1] = f;
+    else if (type == MPG_JOINT_PZ) M.p[2] = f;
+    else { M.p[0] = axis[0] * f; M.p[1] = axis[1] * f; M.p[2] = axis[2] * f; }
+  }
+  return M;
+}
+
+// fp32 FK over the whole tree; calls sink(m, T) with every moving object's
+// world transform (link pose * collision origin).  Joint frames that a later
+// non-consecutive child needs are spilled to `save` ([slot][12] x stride).
+template <class Sink>
+MPG_INLINE void bp_fk(const BpView& b, const double* __restrict__ qrow, float* save, int stride, Sink&& sink) {
+  F34 cur;
+  for (int j = 0; j <= b.nj; ++j) {
+    if (j > 0) {
+      const int jj = j - 1;
+      const int src = b.joint_q_source[jj];
+      const double v = src >= 0 ? qrow[src] : b.joint_q_const[jj];
+      const F34 li = f34_mul(f34_load(b.jplace + 12 * jj), f_joint_motion(b.joint_type[jj], b.jaxis + 3 * jj, v));
+      const int s = b.jsrc[jj];
+      if (s < 0) {
+        cur = li;
+      } else if (s == 0) {
+        cur = f34_mul(cur, li);
+      } else {
+        F34 P;
+        const float* sp = save + (size_t)(s - 1) * 12 * stride;
+#pragma unroll
+        for (int i = 0; i < 9; ++i) P.R[i] = sp[i * stride];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) P.p[i] = sp[(9 + i) * stride];
+        cur = f34_mul(P, li);
+      }
+      const int sv = b.jsave[jj];
+      if (sv >= 0) {
+        float* sp = save + (size_t)sv * 12 * stride;
+#pragma unroll
+        for (int i = 0; i < 9; ++i) sp[i * stride] = cur.R[i];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) sp[(9 + i) * stride] = cur.p[i];
+      }
+    }
+    for (int k = b.link_start[j]; k < b.link_start[j + 1]; ++k) {
+      const int l = b.link_order[k];
+      const F34 L = j == 0 ? f34_load(b.lplace + 12 * l) : f34_mul(cur, f34_load(b.lplace + 12 * l));
+      for (int o = b.obj_start[l]; o < b.obj_start[l + 1]; ++o) {
+        const int m = b.obj_order[o];
+        sink(m, f34_mul(L, f34_load(b.moff + 12 * m)));
+      }
+    }
+  }
+}
+
+// moving object transform from a given link pose (px, py, pz, qw, qx, qy, qz)
+MPG_INLINE F34 bp_from_pose7(const BpView& b, const double* p7, int m) {
+  F34 L;
+  f_quat_to_mat((float)p7[3], (float)p7[4], (float)p7[5], (float)p7[6], L.R);
+  L.p[0] = (float)p7[0];
+  L.p[1] = (float)p7[1];
+  L.p[2] = (float)p7[2];
+  return f34_mul(L, f34_load(b.moff + 12 * m));
+}
+
+struct FObb {
+  float c[3];
+  float R[9];  // row-major world rotation: column j = box axis j
+  float e[3];
+};
+
+// 15-axis separating-axis test with every bound widened by `margin`
+MPG_INLINE bool fobb_separated(const FObb& A, const FObb& B, float margin) {
+  const float d[3] = {B.c[0] - A.c[0], B.c[1] - A.c[1], B.c[2] - A.c[2]};
+  float Rm[3][3], Ab[3][3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      Rm[i][j] = A.R[i] * B.R[j] + A.R[3 + i] * B.R[3 + j] + A.R[6 + i] * B.R[6 + j];
+      Ab[i][j] = fabsf(Rm[i][j]) + 1e-6f;
+    }
+  float t[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) t[i] = d[0] * A.R[i] + d[1] * A.R[3 + i] + d[2] * A.R[6 + i];
+  bool sep = false;
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const float rb = B.e[0] * Ab[i][0] + B.e[1] * Ab[i][1] + B.e[2] * Ab[i][2];
+    sep |= fabsf(t[i]) > A.e[i] + rb + margin;
+  }
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const float ra = A.e[0] * Ab[0][j] + A.e[1] * Ab[1][j] + A.e[2] * Ab[2][j];
+    const float tb = t[0] * Rm[0][j] + t[1] * Rm[1][j] + t[2] * Rm[2][j];
+    sep |= fabsf(tb) > ra + B.e[j] + margin;
+  }
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const int i1 = (i + 1) % 3, i2 = (i + 2) % 3;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const int j1 = (j + 1) % 3, j2 = (j + 2) % 3;
+      const float ra = A.e[i1] * Ab[i2][j] + A.e[i2] * Ab[i1][j];
+      const float rb = B.e[j1] * Ab[i][j2] + B.e[j2] * Ab[i][j1];
+      const float tl = t[i2] * Rm[i1][j] - t[i1] * Rm[i2][j];
+      sep |= fabsf(tl) > ra + rb + margin;
+    }
+  }
+  return sep;
+}
+
+// moving-object bounding sphere vs static OBB
+MPG_INLINE bool fsphere_obb_separated(const float* c, float r, const float* sobj, float margin) {
+  const float d[3] = {c[0] - sobj[BS_C], c[1] - sobj[BS_C + 1], c[2] - sobj[BS_C + 2]};
+  float acc = 0.f;
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const float t = d[0] * sobj[BS_R + j] + d[1] * sobj[BS_R + 3 + j] + d[2] * sobj[BS_R + 6 + j];
+    const float ex = fmaxf(fabsf(t) - sobj[BS_E + j], 0.f);
+    acc += ex * ex;
+  }
+  const float rr = r + margin;
+  return acc > rr * rr;
+}
+
+// ---------------------------------------------------------------------------
+// host: build the program from a world descriptor + the per-geometry local
+// OBB records (centre, half extents, bounding radius about that centre)
+// ---------------------------------------------------------------------------
+struct BpProgram {
+  int n_saves = 0;
+  std::vector<int> jsrc, jsave, link_start, link_order, obj_start, obj_order;
+  std::vector<float> jaxis, jplace, lplace, moff, mobj, sobj;
+};
+
+inline float widen(double v) {  // |v| rounded away from zero, plus a hair
+  const float f = (float)std::fabs(v);
+  return std::nextafter(f, INFINITY) * (1.f + 1e-6f) + 1e-7f;
+}
+
+// obb[g*7] = local centre (3), half extents (3), radius about the centre
+inline void bp_build(const mpg_world_desc* d, const std::vector<double>& obb, BpProgram& P) {
+  const int nj = d->n_joints, nl = d->n_links, nm = d->n_moving, ns = d->n_static;
+  P.jsrc.assign(std::max(nj, 1), -1);
+  P.jsave.assign(std::max(nj, 1), -1);
+  std::vector<int> need_save(nj + 1, 0);
+  for (int j = 1; j <= nj; ++j) {
+    const int par = d->joint_parent[j - 1];
+    if (par > 0 && par != j - 1) need_save[par] = 1;
+  }
+  int slots = 0;
+  std::vector<int> slot_of(nj + 1, -1);
+  for (int j = 1; j <= nj; ++j)
+    if (need_save[j]) slot_of[j] = slots++;
+  P.n_saves = slots;
+  for (int j = 1; j <= nj; ++j) {
+    const int par = d->joint_parent[j - 1];
+    P.jsrc[j - 1] = par == 0 ? -1 : par == j - 1 ? 0 : slot_of[par] + 1;
+    P.jsave[j - 1] = slot_of[j];
+  }
+  for (int i = 0; i < 3 * nj; ++i) P.jaxis.push_back((float)d->joint_axis[i]);
+  for (int i = 0; i < 12 * nj; ++i) P.jplace.push_back((float)d->joint_placement[i]);
+  for (int i = 0; i < 12 * nl; ++i) P.lplace.push_back((float)d->link_placement[i]);
+  for (int i = 0; i < 12 * nm; ++i) P.moff.push_back((float)d->moving_offset[i]);
+  P.link_start.assign(nj + 2, 0);
+  for (int j = 0; j <= nj; ++j) {
+    P.link_start[j] = (int)P.link_order.size();
+    for (int l = 0; l < nl; ++l)
+      if (d->link_parent[l] == j) P.link_order.push_back(l);
+  }
+  P.link_start[nj + 1] = (int)P.link_order.size();
+  P.obj_start.assign(nl + 1, 0);
+  for (int l = 0; l < nl; ++l) {
+    P.obj_start[l] = (int)P.obj_order.size();
+    for (int m = 0; m < nm; ++m)
+      if (d->moving_link[m] == l) P.obj_order.push_back(m);
+  }
+  P.obj_start[nl] = (int)P.obj_order.size();
+  P.mobj.assign((size_t)BM_STRIDE * std::max(nm, 1), 0.f);
+  for (int m = 0; m < nm; ++m) {
+    const double* g = obb.data() + 7 * d->moving_geom[m];
+    float* r = P.mobj.data() + BM_STRIDE * m;
+    for (int k = 0; k < 3; ++k) r[BM_C + k] = (float)g[k];
+    for (int k = 0; k < 3; ++k) r[BM_E + k] = widen(g[3 + k]);
+    r[BM_R] = widen(g[6]);
+  }
+  P.sobj.assign((size_t)BS_STRIDE * std::max(ns, 1), 0.f);
+  for (int s = 0; s < ns; ++s) {
+    const double* T = d->static_transform + 12 * s;
+    const double* g = obb.data() + 7 * d->static_geom[s];
+    float* r = P.sobj.data() + BS_STRIDE * s;
+    for (int i = 0; i < 3; ++i)
+      r[BS_C + i] = (float)(T[3 * i] * g[0] + T[3 * i + 1] * g[1] + T[3 * i + 2] * g[2] + T[9 + i]);
+    for (int k = 0; k < 9; ++k) r[BS_R + k] = (float)T[k];
+    for (int k = 0; k < 3; ++k) r[BS_E + k] = widen(g[3 + k]);
+  }
+}
+
+inline BpView bp_view(const mpg_world_desc* d, const BpProgram& P) {
+  BpView b{};
+  b.nj = d->n_joints;
+  b.n_links = d->n_links;
+  b.n_moving = d->n_moving;
+  b.n_static = d->n_static;
+  b.n_saves = P.n_saves;
+  b.joint_type = d->joint_type;
+  b.joint_q_source = d->joint_q_source;
+  b.joint_q_const = d->joint_q_const;
+  b.jsrc = P.jsrc.data();
+  b.jsave = P.jsave.data();
+  b.jaxis = P.jaxis.data();
+  b.jplace = P.jplace.data();
+  b.link_start = P.link_start.data();
+  b.link_order = P.link_order.data();
+  b.lplace = P.lplace.data();
+  b.obj_start = P.obj_start.data();
+  b.obj_order = P.obj_order.data();
+  b.moving_link = d->moving_link;
+  b.moff = P.moff.data();
+  b.mobj = P.mobj.data();
+  b.sobj = P.sobj.data();
+  return b;
+}
+
+}  // namespace mpg

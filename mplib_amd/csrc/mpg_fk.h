@@ -7,6 +7,7 @@
 //   getLinkPose          src/pinocchio_model.cpp:277-312 (quaternion round trip)
 #pragma once
 #include "mpg_math.h"
+#include "mpg_broadphase.h"
 #include "../../include/mpgpu.h"
 
 namespace mpg {
@@ -20,7 +21,8 @@ enum { S_ROT = 0, S_ROTINV = 4, S_POS = 8, S_OBBC = 11, S_R = 14, S_STRIDE = 23 
 
 struct DevWorld {
   int nj, dof, n_links, n_geoms, n_moving, n_static, n_pairs, W;
-  double mpr_tol, cull_margin;
+  double mpr_tol;
+  int debug_mode;  // diagnostics only: 1 = broad-phase records only, 2 = no SAT stage
   const int* joint_type;      // [nj]
   const int* joint_parent;    // [nj]
   const int* joint_q_source;  // [nj]
@@ -47,6 +49,7 @@ struct DevWorld {
   const int* link_chain_start;  // [n_links]
   const int* link_chain_len;    // [n_links]
   const int* chain_joints;
+  BpView bp;  // fp32 broad-phase program (mpg_broadphase.h)
 };
 
 MPG_INLINE SE3 load_se3(const double* p) {

@@ -8,18 +8,20 @@
 //   ccdMPRIntersect, FCL 0.7.0 / libccd 2.1), then the ACM filter
 //   (src/planning_world.cpp:265-274).
 //
-// Mapping (DESIGN.md "Kernel"): one lane = one configuration.  All lanes of a
-// wave walk the SAME pair at the same time, so geometry reads (hull vertices,
-// box sizes, static poses) are wave-uniform scalar loads, and the only
-// divergence is per-lane cull outcome / MPR iteration count.  Per-object GJK
-// state (quaternion + position, 7 doubles) lives in LDS as [object][7][lane]
-// so the pair loop can index objects dynamically without spilling.
-// A conservative broad phase (bounding sphere, then 15-axis OBB SAT, both
-// inflated by kCullMargin) skips pairs that are geometrically separated;
-// libccd MPR returns "no intersection" for every such pair, so results are
-// unchanged (see DESIGN.md "Broad phase soundness").
+// Two phases per chunk of configurations (DESIGN.md "Kernels"):
+//   A  cull_kernel      lane per configuration: fp32 FK + conservative broad
+//                       phase (mpg_broadphase.h) -> survivor bits [word][cfg]
+//      tile_count / pair_scan / chunk_scan / scatter: bucket the survivors
+//                       into per-pair candidate lists (deterministic, no
+//                       global atomics)
+//   B  narrow_kernel    wave per 64 candidates of ONE pair: exact fp64 FK of
+//                       the two objects' chains + libccd MPR; hull reads are
+//                       wave-uniform scalar loads.
+// A pair culled in A is separated by more than kBpMargin, so MPR would say
+// "no intersection": the output bits equal evaluating every pair.
 //
-// All arithmetic is fp64 and compiled with -ffp-contract=off.
+// Everything that decides an output bit (phase B) is fp64 with
+// -ffp-contract=off, bit-identical to the reference's operation order.
 
 #include <hip/hip_runtime.h>
 
@@ -27,6 +29,7 @@
 #include <atomic>
 #include <cfloat>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -42,7 +45,6 @@ using namespace mpg;
 namespace {
 
 constexpr double kCcdEps = DBL_EPSILON;
-constexpr double kCullMargin = 1e-5;  // metres; >> fp64 rounding at robot scale
 
 thread_local std::string g_last_error;
 
@@ -223,59 +225,6 @@ __device__ bool mpr_intersect(const DevWorld& w, const GObj& A, const GObj& B) {
 }
 
 // ---------------------------------------------------------------------------
-// conservative broad phase (sphere, then OBB separating-axis test)
-// ---------------------------------------------------------------------------
-struct WObb {
-  V3 c;
-  double R[9];  // columns = box axes in world
-  V3 e;
-  double r;
-};
-
-__device__ __forceinline__ bool obb_separated(const WObb& A, const WObb& B, double margin) {
-  const V3 d = vsub(B.c, A.c);
-  const double rr = A.r + B.r + margin;
-  if (vdot(d, d) > rr * rr) return true;
-  // Rm[i][j] = a_i . b_j (columns of R are the box axes)
-  double Rm[3][3], Ab[3][3];
-#pragma unroll
-  for (int i = 0; i < 3; ++i)
-#pragma unroll
-    for (int j = 0; j < 3; ++j) {
-      Rm[i][j] = A.R[i] * B.R[j] + A.R[3 + i] * B.R[3 + j] + A.R[6 + i] * B.R[6 + j];
-      Ab[i][j] = std::fabs(Rm[i][j]) + 1e-12;
-    }
-  const double ea[3] = {A.e.x, A.e.y, A.e.z}, eb[3] = {B.e.x, B.e.y, B.e.z};
-  double t[3];
-#pragma unroll
-  for (int i = 0; i < 3; ++i) t[i] = d.x * A.R[i] + d.y * A.R[3 + i] + d.z * A.R[6 + i];
-#pragma unroll
-  for (int i = 0; i < 3; ++i) {
-    const double rb = eb[0] * Ab[i][0] + eb[1] * Ab[i][1] + eb[2] * Ab[i][2];
-    if (std::fabs(t[i]) > ea[i] + rb + margin) return true;
-  }
-#pragma unroll
-  for (int j = 0; j < 3; ++j) {
-    const double ra = ea[0] * Ab[0][j] + ea[1] * Ab[1][j] + ea[2] * Ab[2][j];
-    const double tb = t[0] * Rm[0][j] + t[1] * Rm[1][j] + t[2] * Rm[2][j];
-    if (std::fabs(tb) > ra + eb[j] + margin) return true;
-  }
-#pragma unroll
-  for (int i = 0; i < 3; ++i) {
-    const int i1 = (i + 1) % 3, i2 = (i + 2) % 3;
-#pragma unroll
-    for (int j = 0; j < 3; ++j) {
-      const int j1 = (j + 1) % 3, j2 = (j + 2) % 3;
-      const double ra = ea[i1] * Ab[i2][j] + ea[i2] * Ab[i1][j];
-      const double rb = eb[j1] * Ab[i][j2] + eb[j2] * Ab[i][j1];
-      const double tl = t[i2] * Rm[i1][j] - t[i1] * Rm[i2][j];
-      if (std::fabs(tl) > ra + rb + margin) return true;
-    }
-  }
-  return false;
-}
-
-// ---------------------------------------------------------------------------
 // kernels
 // ---------------------------------------------------------------------------
 // Link Isometry from a (p, wxyz) pose vector (FCLModel::updateCollisionObjects,
@@ -319,109 +268,228 @@ __device__ __forceinline__ GObj static_obj(const DevWorld& w, int sid) {
 __device__ __forceinline__ uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
 
 // ---------------------------------------------------------------------------
-// Phase A: one lane per configuration.  FK -> per-object broad-phase record in
-// LDS ([object][7][lane]: GJK quaternion xyzw + world OBB centre) -> every
-// pair's conservative cull.  Survivors are appended to the pair's candidate
-// list with one atomic per wave (ballot + mbcnt), so phase B sees each pair's
-// configurations contiguously.  Also zeroes this configuration's outputs.
+// Phase A: one lane per configuration (mpg_broadphase.h).
+//   1. fp32 FK over the tree -> per moving object a record in LDS
+//      ([object][7][lane]: rotation quaternion xyzw + world OBB centre);
+//   2. per pair a cheap bounding test (sphere-sphere for robot pairs,
+//      sphere-OBB against static objects);
+//   3. pairs that pass are queued per wave in LDS as (pair, lane) entries and
+//      the 15-axis OBB SAT runs 64 queued entries at a time with every lane
+//      busy -- the per-pair branch no longer makes the whole wave pay for one
+//      lane's survivor;
+//   4. SAT survivors set the configuration's bit in an LDS survivor word,
+//      written to surv[word][cfg] at the end (no global atomics).
+// Also zeroes this configuration's outputs for phase B.
 // ---------------------------------------------------------------------------
+constexpr int kQueue = 128;  // entries per wave: < 64 pending + <= 64 pushed
+
+__device__ __forceinline__ FObb bp_obb(const DevWorld& w, const float* __restrict__ rec, int id, int t, int block) {
+  FObb o;
+  if (id < w.n_moving) {
+    const float* r = rec + (size_t)id * 7 * block + t;
+    f_quat_to_mat(r[3 * block], r[0], r[block], r[2 * block], o.R);
+    o.c[0] = r[4 * block];
+    o.c[1] = r[5 * block];
+    o.c[2] = r[6 * block];
+    const float* g = w.bp.mobj + BM_STRIDE * id;
+    o.e[0] = g[BM_E];
+    o.e[1] = g[BM_E + 1];
+    o.e[2] = g[BM_E + 2];
+  } else {
+    const float* g = w.bp.sobj + BS_STRIDE * (id - w.n_moving);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) o.c[k] = g[BS_C + k];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) o.R[k] = g[BS_R + k];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) o.e[k] = g[BS_E + k];
+  }
+  return o;
+}
+
+template <int BLOCK>
+__device__ __forceinline__ void sat_drain(const DevWorld& w, const float* __restrict__ rec, uint32_t* survw,
+                                          const uint32_t* queue, uint32_t head, uint32_t cnt, int wbase,
+                                          uint32_t lane) {
+  __builtin_amdgcn_wave_barrier();
+  if (lane < cnt) {
+    const uint32_t e = queue[(head + lane) & (kQueue - 1)];
+    const int p = (int)(e >> 6), t = wbase + (int)(e & 63u);
+    const FObb A = bp_obb(w, rec, w.pair_a[p], t, BLOCK);
+    const FObb B = bp_obb(w, rec, w.pair_b[p], t, BLOCK);
+    if (!fobb_separated(A, B, kBpMargin)) atomicOr(&survw[(p >> 5) * BLOCK + t], 1u << (p & 31));
+  }
+  __builtin_amdgcn_wave_barrier();
+}
+
 template <int BLOCK, bool FROM_POSES>
 __global__ __launch_bounds__(BLOCK) void cull_kernel(DevWorld w, const double* __restrict__ in, long long n,
                                                     uint8_t* __restrict__ flags, uint32_t* __restrict__ masks,
-                                                    uint32_t* __restrict__ counts, uint32_t* __restrict__ cand,
-                                                    long long cap) {
-  extern __shared__ __attribute__((aligned(16))) double lds[];
+                                                    uint32_t* __restrict__ surv, long long cap) {
+  extern __shared__ __attribute__((aligned(16))) float lds_f[];
+  float* rec = lds_f;                                                    // [n_moving][7][BLOCK]
+  float* save = rec + (size_t)w.n_moving * 7 * BLOCK;                    // [n_saves][12][BLOCK]
+  uint32_t* survw = reinterpret_cast<uint32_t*>(save + (size_t)w.bp.n_saves * 12 * BLOCK);  // [W][BLOCK]
   const int tid = threadIdx.x;
+  uint32_t* queue = survw + (size_t)w.W * BLOCK + (tid >> 6) * kQueue;  // [BLOCK/64][kQueue]
+  const uint32_t lane = lane_id();
+  const int wbase = tid & ~63;
   const long long cfg = (long long)blockIdx.x * BLOCK + tid;
   const bool live = cfg < n;
-  const long long c = live ? cfg : n - 1;  // dead lanes shadow a valid row and never append
+  const long long c = live ? cfg : n - 1;  // dead lanes shadow a valid row and never queue
   if (live) {
     flags[cfg] = 0;
     if (masks)
       for (int k = 0; k < w.W; ++k) masks[cfg * w.W + k] = 0u;
   }
-  {
-    FkState st;
-    if (!FROM_POSES) forward_kinematics(w, in + c * w.dof, st);
-    for (int m = 0; m < w.n_moving; ++m) {
-      const int l = w.moving_link[m];
-      const SE3 L = FROM_POSES ? link_from_pose7(in + (c * w.n_links + l) * 7) : link_transform(w, st, l, nullptr);
-      const SE3 T = se3_mul(L, load_se3(w.moving_offset + 12 * m));
-      const Q4 r = gjk_rot_from_matrix(T.R);
-      const double* rec = w.geom_rec + G_STRIDE * w.moving_geom[m];
-      double* slot = lds + (size_t)m * 7 * BLOCK + tid;
-      slot[0 * BLOCK] = r.x;
-      slot[1 * BLOCK] = r.y;
-      slot[2 * BLOCK] = r.z;
-      slot[3 * BLOCK] = r.w;
+  for (int k = 0; k < w.W; ++k) survw[k * BLOCK + tid] = 0u;
+
+  auto put = [&](int m, const F34& T) {
+    float q[4];
+    f_mat_to_quat(T.R, q);
+    float* r = rec + (size_t)m * 7 * BLOCK + tid;
+    r[0] = q[0];
+    r[BLOCK] = q[1];
+    r[2 * BLOCK] = q[2];
+    r[3 * BLOCK] = q[3];
+    const float* g = w.bp.mobj + BM_STRIDE * m;
 #pragma unroll
-      for (int i = 0; i < 3; ++i)
-        slot[(4 + i) * BLOCK] = ((T.R[3 * i] * rec[G_OBB_C] + T.R[3 * i + 1] * rec[G_OBB_C + 1]) +
-                                 T.R[3 * i + 2] * rec[G_OBB_C + 2]) + T.p[i];
-    }
+    for (int i = 0; i < 3; ++i)
+      r[(4 + i) * BLOCK] = T.R[3 * i] * g[BM_C] + T.R[3 * i + 1] * g[BM_C + 1] + T.R[3 * i + 2] * g[BM_C + 2] + T.p[i];
+  };
+  if (FROM_POSES) {
+    for (int m = 0; m < w.n_moving; ++m) put(m, bp_from_pose7(w.bp, in + (c * w.n_links + w.moving_link[m]) * 7, m));
+  } else {
+    bp_fk(w.bp, in + c * w.dof, save + tid, BLOCK, put);
   }
-  const uint32_t lane = lane_id();
+  if (w.debug_mode == 1) {
+    if (live && rec[tid] == 12345.f) flags[cfg] = 2;  // keep the records alive
+    return;
+  }
+
+  uint32_t head = 0, tail = 0;  // wave-uniform queue cursors
   for (int p = 0; p < w.n_pairs; ++p) {
     if (w.pair_allowed[p]) continue;  // filterCollisions drops it whatever MPR says
-    WObb box[2];
-    const int ids[2] = {w.pair_a[p], w.pair_b[p]};
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const int id = ids[s];
-      if (id < w.n_moving) {
-        const double* slot = lds + (size_t)id * 7 * BLOCK + tid;
-        const double* g = w.geom_rec + G_STRIDE * w.moving_geom[id];
-        box[s].c = v3(slot[4 * BLOCK], slot[5 * BLOCK], slot[6 * BLOCK]);
-        box[s].e = v3(g[G_OBB_E], g[G_OBB_E + 1], g[G_OBB_E + 2]);
-        box[s].r = g[G_RADIUS];
-      } else {
-        const double* r = w.static_rec + S_STRIDE * (id - w.n_moving);
-        const double* g = w.geom_rec + G_STRIDE * w.static_geom[id - w.n_moving];
-        box[s].c = v3(r[S_OBBC], r[S_OBBC + 1], r[S_OBBC + 2]);
-        box[s].e = v3(g[G_OBB_E], g[G_OBB_E + 1], g[G_OBB_E + 2]);
-        box[s].r = g[G_RADIUS];
-      }
+    const int a = w.pair_a[p], b = w.pair_b[p];
+    bool keep;
+    if (a < w.n_moving && b < w.n_moving) {
+      const float* ra = rec + (size_t)a * 7 * BLOCK + tid;
+      const float* rb = rec + (size_t)b * 7 * BLOCK + tid;
+      const float dx = rb[4 * BLOCK] - ra[4 * BLOCK], dy = rb[5 * BLOCK] - ra[5 * BLOCK],
+                  dz = rb[6 * BLOCK] - ra[6 * BLOCK];
+      const float rr = w.bp.mobj[BM_STRIDE * a + BM_R] + w.bp.mobj[BM_STRIDE * b + BM_R] + kBpMargin;
+      keep = dx * dx + dy * dy + dz * dz <= rr * rr;
+    } else {
+      const int m = a < w.n_moving ? a : b, st = (a < w.n_moving ? b : a) - w.n_moving;
+      const float* rm = rec + (size_t)m * 7 * BLOCK + tid;
+      const float cm[3] = {rm[4 * BLOCK], rm[5 * BLOCK], rm[6 * BLOCK]};
+      keep = !fsphere_obb_separated(cm, w.bp.mobj[BM_STRIDE * m + BM_R], w.bp.sobj + BS_STRIDE * st, kBpMargin);
     }
-    bool keep = false;
-    const V3 d = vsub(box[1].c, box[0].c);
-    const double rr = box[0].r + box[1].r + w.cull_margin;
-    if (live && vdot(d, d) <= rr * rr) {  // bounding spheres overlap: run the 15-axis SAT
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        const int id = ids[s];
-        if (id < w.n_moving) {
-          const double* slot = lds + (size_t)id * 7 * BLOCK + tid;
-          quat_to_mat(slot[3 * BLOCK], slot[0], slot[BLOCK], slot[2 * BLOCK], box[s].R);
-        } else {
-          const double* r = w.static_rec + S_STRIDE * (id - w.n_moving);
-#pragma unroll
-          for (int k = 0; k < 9; ++k) box[s].R[k] = r[S_R + k];
-        }
-      }
-      keep = !obb_separated(box[0], box[1], w.cull_margin);
+    keep = keep && live;
+    if (w.debug_mode == 2) {
+      if (keep) survw[(p >> 5) * BLOCK + tid] |= 1u << (p & 31);
+      continue;
     }
     const unsigned long long bal = __ballot(keep);
     if (bal) {
-      uint32_t base = 0;
-      if (lane == 0) base = atomicAdd(&counts[p], (uint32_t)__popcll(bal));
-      base = __shfl(base, 0);
       if (keep) {
         const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
-        cand[(long long)p * cap + base + rank] = (uint32_t)cfg;
+        queue[(tail + rank) & (kQueue - 1)] = ((uint32_t)p << 6) | lane;
+      }
+      tail += (uint32_t)__popcll(bal);
+      if (tail - head >= 64) {
+        sat_drain<BLOCK>(w, rec, survw, queue, head, 64, wbase, lane);
+        head += 64;
       }
     }
   }
+  if (tail != head) sat_drain<BLOCK>(w, rec, survw, queue, head, tail - head, wbase, lane);
+  if (live)
+    for (int k = 0; k < w.W; ++k) surv[(long long)k * cap + cfg] = survw[k * BLOCK + tid];
 }
 
-// Exclusive scan of per-pair chunk counts (64 candidates per chunk).
-__global__ void chunk_scan_kernel(const uint32_t* __restrict__ counts, int n_pairs, uint32_t* __restrict__ prefix) {
+// ---------------------------------------------------------------------------
+// Deterministic bucketing of the survivor bits into per-pair candidate lists
+// (no global atomics): count per (pair, 64-config tile) -> per-pair scan ->
+// scatter.  Candidates of a pair end up contiguous and sorted by config.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void tile_count_kernel(const uint32_t* __restrict__ surv, long long n, long long cap,
+                                                        int n_pairs, int W, int n_tiles,
+                                                        uint32_t* __restrict__ cnt) {
+  const uint32_t lane = lane_id();
+  const long long wid = __builtin_amdgcn_readfirstlane((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+  if (wid >= (long long)n_tiles * W) return;
+  const int wd = (int)(wid / n_tiles), t = (int)(wid % n_tiles);
+  const long long cfg = (long long)t * 64 + lane;
+  const uint32_t x = cfg < n ? surv[(long long)wd * cap + cfg] : 0u;
+  const int nb = min(32, n_pairs - wd * 32);
+  for (int b = 0; b < nb; ++b) {
+    const unsigned long long bal = __ballot((x >> b) & 1u);
+    if (lane == (uint32_t)b) cnt[(long long)(wd * 32 + b) * n_tiles + t] = (uint32_t)__popcll(bal);
+  }
+}
+
+// one block per pair: exclusive scan of its tile counts (in place) + total
+__global__ __launch_bounds__(1024) void pair_scan_kernel(uint32_t* __restrict__ cnt, int n_tiles,
+                                                        uint32_t* __restrict__ seg_len) {
+  __shared__ uint32_t part[1024];
+  uint32_t* c = cnt + (long long)blockIdx.x * n_tiles;
+  const int per = (n_tiles + 1023) / 1024;
+  const int lo = threadIdx.x * per, hi = min(n_tiles, lo + per);
+  uint32_t sum = 0;
+  for (int i = lo; i < hi; ++i) sum += c[i];
+  part[threadIdx.x] = sum;
+  __syncthreads();
+  for (int off = 1; off < 1024; off <<= 1) {  // Hillis-Steele inclusive scan
+    const uint32_t v = threadIdx.x >= (unsigned)off ? part[threadIdx.x - off] : 0u;
+    __syncthreads();
+    part[threadIdx.x] += v;
+    __syncthreads();
+  }
+  uint32_t run = part[threadIdx.x] - sum;
+  for (int i = lo; i < hi; ++i) {
+    const uint32_t v = c[i];
+    c[i] = run;
+    run += v;
+  }
+  if (threadIdx.x == 1023) seg_len[blockIdx.x] = part[1023];
+}
+
+// segment starts + 64-candidate chunk prefix (n_pairs is small)
+__global__ void chunk_scan_kernel(const uint32_t* __restrict__ seg_len, int n_pairs, uint32_t* __restrict__ seg_start,
+                                  uint32_t* __restrict__ prefix) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  uint32_t acc = 0;
+  uint32_t acc = 0, start = 0;
   for (int p = 0; p < n_pairs; ++p) {
     prefix[p] = acc;
-    acc += (counts[p] + 63u) >> 6;
+    seg_start[p] = start;
+    acc += (seg_len[p] + 63u) >> 6;
+    start += seg_len[p];
   }
   prefix[n_pairs] = acc;
+}
+
+__global__ __launch_bounds__(256) void scatter_kernel(const uint32_t* __restrict__ surv, long long n, long long cap,
+                                                     int n_pairs, int W, int n_tiles,
+                                                     const uint32_t* __restrict__ off,
+                                                     const uint32_t* __restrict__ seg_start,
+                                                     uint32_t* __restrict__ cand) {
+  const uint32_t lane = lane_id();
+  const long long wid = __builtin_amdgcn_readfirstlane((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+  if (wid >= (long long)n_tiles * W) return;
+  const int wd = (int)(wid / n_tiles), t = (int)(wid % n_tiles);
+  const long long cfg = (long long)t * 64 + lane;
+  const uint32_t x = cfg < n ? surv[(long long)wd * cap + cfg] : 0u;
+  const int nb = min(32, n_pairs - wd * 32);
+  for (int b = 0; b < nb; ++b) {
+    const uint32_t bit = (x >> b) & 1u;
+    const unsigned long long bal = __ballot(bit);
+    if (bit) {
+      const int p = wd * 32 + b;
+      const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+      cand[seg_start[p] + off[(long long)p * n_tiles + t] + rank] = (uint32_t)cfg;
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -432,9 +500,10 @@ __global__ void chunk_scan_kernel(const uint32_t* __restrict__ counts, int n_pai
 // ---------------------------------------------------------------------------
 template <bool FROM_POSES>
 __global__ __launch_bounds__(256) void narrow_kernel(DevWorld w, const double* __restrict__ in,
-                                                    const uint32_t* __restrict__ counts,
+                                                    const uint32_t* __restrict__ seg_len,
+                                                    const uint32_t* __restrict__ seg_start,
                                                     const uint32_t* __restrict__ prefix,
-                                                    const uint32_t* __restrict__ cand, long long cap,
+                                                    const uint32_t* __restrict__ cand,
                                                     uint8_t* __restrict__ flags, uint32_t* __restrict__ masks) {
   const uint32_t lane = lane_id();
   const uint32_t wave = __builtin_amdgcn_readfirstlane((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
@@ -449,8 +518,8 @@ __global__ __launch_bounds__(256) void narrow_kernel(DevWorld w, const double* _
     }
     const int p = lo;
     const uint32_t idx = (ch - prefix[p]) * 64u + lane;
-    if (idx >= counts[p]) continue;
-    const long long cfg = cand[(long long)p * cap + idx];
+    if (idx >= seg_len[p]) continue;
+    const long long cfg = cand[seg_start[p] + idx];
     const int a = w.pair_a[p], b = w.pair_b[p];
     const GObj A = a < w.n_moving ? moving_obj<FROM_POSES>(w, in, cfg, a) : static_obj(w, a - w.n_moving);
     const GObj B = b < w.n_moving ? moving_obj<FROM_POSES>(w, in, cfg, b) : static_obj(w, b - w.n_moving);
@@ -498,9 +567,12 @@ struct mpg_world {
   size_t cap_out = 0;
   // phase A/B workspace, one per stream so concurrent streams never share it
   struct Workspace {
-    uint32_t* counts = nullptr;  // [n_pairs]
-    uint32_t* prefix = nullptr;  // [n_pairs + 1]
-    uint32_t* cand = nullptr;    // [n_pairs * cap]
+    uint32_t* surv = nullptr;       // [W * cap] survivor bits, word-major
+    uint32_t* cnt = nullptr;        // [n_pairs * n_tiles] tile counts -> offsets
+    uint32_t* seg_len = nullptr;    // [n_pairs]
+    uint32_t* seg_start = nullptr;  // [n_pairs]
+    uint32_t* prefix = nullptr;     // [n_pairs + 1] chunk prefix
+    uint32_t* cand = nullptr;       // [n_pairs * cap] worst case
     long long cap = 0;
   };
   std::mutex ws_mu;
@@ -631,7 +703,19 @@ void geom_record(const mpg_world_desc* d, int g, double* rec) {
     rec[G_OBB_E + k] = e * (1.0 + 1e-12) + 1e-12;
     r2 += rec[G_OBB_E + k] * rec[G_OBB_E + k];
   }
-  rec[G_RADIUS] = std::sqrt(r2) * (1.0 + 1e-12);
+  if (t == MPG_GEOM_CONVEX) {  // bounding sphere about the box centre: farthest vertex
+    const double* V = d->vertices + 3 * (size_t)d->geom_vertex_start[g];
+    r2 = 0.0;
+    for (int i = 0; i < d->geom_vertex_count[g]; ++i) {
+      double s2 = 0.0;
+      for (int k = 0; k < 3; ++k) {
+        const double dv = V[3 * i + k] - rec[G_OBB_C + k];
+        s2 += dv * dv;
+      }
+      r2 = std::max(r2, s2);
+    }
+  }
+  rec[G_RADIUS] = std::sqrt(r2) * (1.0 + 1e-12) + 1e-12;
 }
 
 void static_record(const mpg_world_desc* d, int s, const double* geom_rec_all, double* rec) {
@@ -650,14 +734,27 @@ void static_record(const mpg_world_desc* d, int s, const double* geom_rec_all, d
   for (int k = 0; k < 9; ++k) rec[S_R + k] = R[k];
 }
 
-int choose_block(int n_moving, size_t* lds) {
-  const size_t per_thread = (size_t)std::max(n_moving, 1) * 7 * sizeof(double);
-  // keep two workgroups resident per CU (160 KiB LDS) when possible
-  int block = 256;
-  while (block > 64 && per_thread * block > 80 * 1024) block /= 2;
-  *lds = per_thread * block;
-  if (*lds > 160 * 1024) return -1;
-  return block;
+// phase A LDS bytes per thread: records + FK save slots + survivor words + queue share
+size_t cull_lds_per_thread(int n_moving, int n_saves, int W) {
+  return (size_t)std::max(n_moving, 1) * 7 * sizeof(float) + (size_t)n_saves * 12 * sizeof(float) +
+         (size_t)W * sizeof(uint32_t) + (kQueue / 64) * sizeof(uint32_t);
+}
+
+// block size that keeps the most waves resident per CU (160 KiB of LDS),
+// ties to the larger block; -1 if even one wave does not fit
+int choose_block(size_t per_thread, size_t* lds) {
+  int best = -1, best_waves = 0;
+  for (int b : {256, 128, 64}) {
+    const size_t bytes = per_thread * b;
+    if (bytes > 160 * 1024) continue;
+    const int waves = std::min(32, (int)(160 * 1024 / bytes) * (b / 64));
+    if (waves > best_waves) {
+      best_waves = waves;
+      best = b;
+    }
+  }
+  if (best > 0) *lds = per_thread * best;
+  return best;
 }
 
 int get_workspace(mpg_world* w, hipStream_t s, long long want, mpg_world::Workspace** out) {
@@ -665,11 +762,14 @@ int get_workspace(mpg_world* w, hipStream_t s, long long want, mpg_world::Worksp
   auto& ws = w->ws[s];
   const long long np = std::max(w->dw.n_pairs, 1);
   if (ws.cap < want) {
-    if (ws.counts) HIP_TRY(hipFree(ws.counts));
-    if (ws.prefix) HIP_TRY(hipFree(ws.prefix));
-    if (ws.cand) HIP_TRY(hipFree(ws.cand));
+    for (uint32_t* p : {ws.surv, ws.cnt, ws.seg_len, ws.seg_start, ws.prefix, ws.cand})
+      if (p) HIP_TRY(hipFree(p));
     ws = mpg_world::Workspace{};
-    HIP_TRY(hipMalloc(&ws.counts, sizeof(uint32_t) * np));
+    const long long tiles = (want + 63) / 64;
+    HIP_TRY(hipMalloc(&ws.surv, sizeof(uint32_t) * w->dw.W * want));
+    HIP_TRY(hipMalloc(&ws.cnt, sizeof(uint32_t) * np * tiles));
+    HIP_TRY(hipMalloc(&ws.seg_len, sizeof(uint32_t) * np));
+    HIP_TRY(hipMalloc(&ws.seg_start, sizeof(uint32_t) * np));
     HIP_TRY(hipMalloc(&ws.prefix, sizeof(uint32_t) * (np + 1)));
     HIP_TRY(hipMalloc(&ws.cand, sizeof(uint32_t) * np * want));
     ws.cap = want;
@@ -691,30 +791,43 @@ int launch_collide(mpg_world* w, const double* in, long long n, uint8_t* flags, 
     const double* qin = in + off * row;
     uint8_t* fl = flags + off;
     uint32_t* mk = masks ? masks + off * w->dw.W : nullptr;
-    HIP_TRY(hipMemsetAsync(ws->counts, 0, sizeof(uint32_t) * std::max(w->dw.n_pairs, 1), stream));
     const unsigned grid = (unsigned)((m + w->block - 1) / w->block);
     switch (w->block) {
       case 256:
         hipLaunchKernelGGL((cull_kernel<256, FROM_POSES>), dim3(grid), dim3(256), w->lds_bytes, stream, w->dw, qin,
-                           m, fl, mk, ws->counts, ws->cand, ws->cap);
+                           m, fl, mk, ws->surv, ws->cap);
         break;
       case 128:
         hipLaunchKernelGGL((cull_kernel<128, FROM_POSES>), dim3(grid), dim3(128), w->lds_bytes, stream, w->dw, qin,
-                           m, fl, mk, ws->counts, ws->cand, ws->cap);
+                           m, fl, mk, ws->surv, ws->cap);
         break;
       default:
         hipLaunchKernelGGL((cull_kernel<64, FROM_POSES>), dim3(grid), dim3(64), w->lds_bytes, stream, w->dw, qin, m,
-                           fl, mk, ws->counts, ws->cand, ws->cap);
+                           fl, mk, ws->surv, ws->cap);
         break;
     }
     HIP_TRY(hipGetLastError());
-    hipLaunchKernelGGL(chunk_scan_kernel, dim3(1), dim3(64), 0, stream, ws->counts, w->dw.n_pairs, ws->prefix);
+    const int n_tiles = (int)((m + 63) / 64);
+    const long long tw = (long long)n_tiles * w->dw.W;  // one wave per (word, tile)
+    const unsigned gb = (unsigned)((tw + 3) / 4);
+    hipLaunchKernelGGL(tile_count_kernel, dim3(gb), dim3(256), 0, stream, ws->surv, m, ws->cap, w->dw.n_pairs,
+                       w->dw.W, n_tiles, ws->cnt);
+    HIP_TRY(hipGetLastError());
+    if (w->dw.n_pairs > 0) {
+      hipLaunchKernelGGL(pair_scan_kernel, dim3(w->dw.n_pairs), dim3(1024), 0, stream, ws->cnt, n_tiles, ws->seg_len);
+      HIP_TRY(hipGetLastError());
+    }
+    hipLaunchKernelGGL(chunk_scan_kernel, dim3(1), dim3(64), 0, stream, ws->seg_len, w->dw.n_pairs, ws->seg_start,
+                       ws->prefix);
+    HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(scatter_kernel, dim3(gb), dim3(256), 0, stream, ws->surv, m, ws->cap, w->dw.n_pairs, w->dw.W,
+                       n_tiles, ws->cnt, ws->seg_start, ws->cand);
     HIP_TRY(hipGetLastError());
     // persistent narrow phase: enough waves to fill the chip, fewer for tiny batches
     const long long want_waves = (m * std::max(w->dw.n_pairs, 1) + 63) / 64;
     const unsigned nb = (unsigned)std::max<long long>(1, std::min<long long>(w->narrow_blocks, (want_waves + 3) / 4));
-    hipLaunchKernelGGL((narrow_kernel<FROM_POSES>), dim3(nb), dim3(256), 0, stream, w->dw, qin, ws->counts,
-                       ws->prefix, ws->cand, ws->cap, fl, mk);
+    hipLaunchKernelGGL((narrow_kernel<FROM_POSES>), dim3(nb), dim3(256), 0, stream, w->dw, qin, ws->seg_len,
+                       ws->seg_start, ws->prefix, ws->cand, fl, mk);
     HIP_TRY(hipGetLastError());
   }
   return MPG_OK;
@@ -767,13 +880,23 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
   *out = nullptr;
   int rc = validate(d);
   if (rc) return rc;
-  size_t lds = 0;
-  const int block = choose_block(d->n_moving, &lds);
-  if (block < 0) return set_error(MPG_E_UNSUPPORTED, "too many moving objects for the LDS budget (max 45)");
-  HIP_TRY(hipSetDevice(device));
-
   std::vector<double> geom_rec((size_t)G_STRIDE * std::max(d->n_geoms, 1), 0.0);
   for (int g = 0; g < d->n_geoms; ++g) geom_record(d, g, geom_rec.data() + (size_t)G_STRIDE * g);
+  std::vector<double> obb((size_t)7 * std::max(d->n_geoms, 1), 0.0);
+  for (int g = 0; g < d->n_geoms; ++g) {
+    const double* r = geom_rec.data() + (size_t)G_STRIDE * g;
+    for (int k = 0; k < 3; ++k) obb[7 * g + k] = r[G_OBB_C + k];
+    for (int k = 0; k < 3; ++k) obb[7 * g + 3 + k] = r[G_OBB_E + k];
+    obb[7 * g + 6] = r[G_RADIUS];
+  }
+  BpProgram bpp;
+  bp_build(d, obb, bpp);
+  size_t lds = 0;
+  const int W = std::max(1, (d->n_pairs + 31) / 32);
+  const int block = choose_block(cull_lds_per_thread(d->n_moving, bpp.n_saves, W), &lds);
+  if (block < 0) return set_error(MPG_E_UNSUPPORTED, "world too large for the phase-A LDS budget");
+  HIP_TRY(hipSetDevice(device));
+
   std::vector<double> static_rec((size_t)S_STRIDE * std::max(d->n_static, 1), 0.0);
   for (int s = 0; s < d->n_static; ++s) static_record(d, s, geom_rec.data(), static_rec.data() + (size_t)S_STRIDE * s);
   std::vector<double> verts4((size_t)4 * std::max<int64_t>(d->n_vertices, 1), 0.0);
@@ -817,6 +940,18 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
   const size_t o_cs = bb.add(chain_start.data(), chain_start.size());
   const size_t o_cl = bb.add(chain_len.data(), chain_len.size());
   const size_t o_cj = bb.add(chain_joints.data(), chain_joints.size());
+  const size_t o_bjs = bb.add(bpp.jsrc.data(), bpp.jsrc.size());
+  const size_t o_bjv = bb.add(bpp.jsave.data(), bpp.jsave.size());
+  const size_t o_bja = bb.add(bpp.jaxis.data(), bpp.jaxis.size());
+  const size_t o_bjp = bb.add(bpp.jplace.data(), bpp.jplace.size());
+  const size_t o_bls = bb.add(bpp.link_start.data(), bpp.link_start.size());
+  const size_t o_blo = bb.add(bpp.link_order.data(), bpp.link_order.size());
+  const size_t o_blp = bb.add(bpp.lplace.data(), bpp.lplace.size());
+  const size_t o_bos = bb.add(bpp.obj_start.data(), bpp.obj_start.size());
+  const size_t o_boo = bb.add(bpp.obj_order.data(), bpp.obj_order.size());
+  const size_t o_bmo = bb.add(bpp.moff.data(), bpp.moff.size());
+  const size_t o_bmb = bb.add(bpp.mobj.data(), bpp.mobj.size());
+  const size_t o_bsb = bb.add(bpp.sobj.data(), bpp.sobj.size());
 
   mpg_world* w = new mpg_world();
   w->device = device;
@@ -843,9 +978,9 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
   dw.n_moving = d->n_moving;
   dw.n_static = d->n_static;
   dw.n_pairs = d->n_pairs;
-  dw.W = std::max(1, (d->n_pairs + 31) / 32);
+  dw.W = W;
   dw.mpr_tol = d->gjk_tolerance;
-  dw.cull_margin = kCullMargin;
+  dw.debug_mode = std::getenv("MPG_DEBUG_CULL") ? std::atoi(std::getenv("MPG_DEBUG_CULL")) : 0;
   dw.joint_type = reinterpret_cast<const int*>(base + o_jt);
   dw.joint_parent = reinterpret_cast<const int*>(base + o_jp);
   dw.joint_q_source = reinterpret_cast<const int*>(base + o_jqs);
@@ -870,6 +1005,30 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
   dw.link_chain_start = reinterpret_cast<const int*>(base + o_cs);
   dw.link_chain_len = reinterpret_cast<const int*>(base + o_cl);
   dw.chain_joints = reinterpret_cast<const int*>(base + o_cj);
+  auto I = [&](size_t o) { return reinterpret_cast<const int*>(base + o); };
+  auto F = [&](size_t o) { return reinterpret_cast<const float*>(base + o); };
+  BpView& bp = dw.bp;
+  bp.nj = d->n_joints;
+  bp.n_links = d->n_links;
+  bp.n_moving = d->n_moving;
+  bp.n_static = d->n_static;
+  bp.n_saves = bpp.n_saves;
+  bp.joint_type = dw.joint_type;
+  bp.joint_q_source = dw.joint_q_source;
+  bp.joint_q_const = dw.joint_q_const;
+  bp.jsrc = I(o_bjs);
+  bp.jsave = I(o_bjv);
+  bp.jaxis = F(o_bja);
+  bp.jplace = F(o_bjp);
+  bp.link_start = I(o_bls);
+  bp.link_order = I(o_blo);
+  bp.lplace = F(o_blp);
+  bp.obj_start = I(o_bos);
+  bp.obj_order = I(o_boo);
+  bp.moving_link = dw.moving_link;
+  bp.moff = F(o_bmo);
+  bp.mobj = F(o_bmb);
+  bp.sobj = F(o_bsb);
   int cus = 256;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0) cus = 256;
   w->narrow_blocks = cus * 4;
@@ -887,11 +1046,10 @@ int mpg_world_destroy(mpg_world* w) {
   hipFree(w->d_flags);
   hipFree(w->d_masks);
   hipFree(w->d_out);
-  for (auto& kv : w->ws) {
-    hipFree(kv.second.counts);
-    hipFree(kv.second.prefix);
-    hipFree(kv.second.cand);
-  }
+  for (auto& kv : w->ws)
+    for (uint32_t* p : {kv.second.surv, kv.second.cnt, kv.second.seg_len, kv.second.seg_start, kv.second.prefix,
+                        kv.second.cand})
+      hipFree(p);
   delete w;
   return MPG_OK;
 }

@@ -1,0 +1,77 @@
+"""CPU: the phase-A broad phase (mplib_amd/csrc/mpg_broadphase.h, the code the
+cull kernel runs, compiled for the host) stays far inside its safety margin.
+
+Phase A evaluates FK in fp32 and culls a pair only when its bounding volumes
+are separated by more than kBpMargin = 1e-4 m.  That is sound as long as the
+fp32 object poses deviate from the exact fp64 poses (the oracle's) by much
+less than the margin; this test measures the deviation on uniform, extreme
+and far-out-of-limit configurations.
+"""
+import ctypes
+
+import numpy as np
+
+import worlds as Wd
+from native.host_shim import lib
+
+MARGIN = 1e-4
+
+
+def bp_objects(d, q):
+    keep = []
+
+    def I(a):
+        a = np.ascontiguousarray(np.asarray(a, dtype=np.int32))
+        keep.append(a)
+        return a.ctypes.data_as(ctypes.c_void_p)
+
+    def F(a):
+        a = np.ascontiguousarray(np.asarray(a, dtype=np.float64))
+        keep.append(a)
+        return a.ctypes.data_as(ctypes.c_void_p)
+
+    nl = len(d["link_parent"])
+    nm = len(d["moving_link"])
+    out = np.zeros((len(q), nm, 12), dtype=np.float32)
+    rq = np.zeros((len(q), nm, 9), dtype=np.float32)
+    lib().host_bp_objects(len(d["joint_type"]), I(d["joint_type"]), I(d["joint_parent"]), I(d["joint_q_source"]),
+                          F(d["joint_q_const"]), F(d["joint_axis"]), F(d["joint_placement"]), int(d["dof"]), nl,
+                          I(d["link_parent"]), F(d["link_placement"]), nm, I(d["moving_link"]),
+                          F(d["moving_offset"]), F(q), ctypes.c_long(len(q)), out.ctypes.data_as(ctypes.c_void_p),
+                          rq.ctypes.data_as(ctypes.c_void_p))
+    return out, rq
+
+
+def _check(q):
+    ow = Wd.oracle_world(3)
+    d = Wd.desc_arrays(ow)
+    f32, rq = bp_objects(d, q)
+    _, objT = ow.fk_batch(q)
+    nm = f32.shape[1]
+    ref = objT[:, :nm]
+    dR = np.abs(f32[..., :9].astype(np.float64) - ref[..., :9]).max()
+    dRq = np.abs(rq.astype(np.float64) - ref[..., :9]).max()
+    dp = np.abs(f32[..., 9:].astype(np.float64) - ref[..., 9:]).max()
+    return dR, dRq, dp
+
+
+def test_fp32_poses_within_margin_uniform():
+    ow = Wd.oracle_world(3)
+    q = Wd.sample_q(ow.art, 50000, 11)
+    dR, dRq, dp = _check(q)
+    # position error bounds the centre error directly; a rotation error of dR
+    # moves a point at 0.3 m from the frame origin by <= 0.3*sqrt(3)*dR
+    assert dp < MARGIN / 20, dp
+    assert dR < 2e-5 and dRq < 2e-5, (dR, dRq)
+    assert dp + 0.3 * 3 ** 0.5 * dRq < MARGIN / 10
+
+
+def test_fp32_poses_within_margin_extreme():
+    ow = Wd.oracle_world(3)
+    rng = np.random.default_rng(12)
+    lim = np.array([[-2.8973, 2.8973], [-1.7628, 1.7628], [-2.8973, 2.8973], [-3.0718, -0.0698],
+                    [-2.8973, 2.8973], [-0.0175, 3.7525], [-2.8973, 2.8973]])
+    corners = lim[np.arange(7), rng.integers(0, 2, (4000, 7))]
+    far = rng.uniform(-60.0, 60.0, (4000, 7))
+    dR, dRq, dp = _check(np.concatenate([corners, far]))
+    assert dp < MARGIN / 20 and dR < 2e-5 and dRq < 2e-5, (dR, dRq, dp)
