@@ -33,22 +33,22 @@ enum { BS_C = 0, BS_R = 3, BS_E = 12, BS_STRIDE = 16 };
 // Read-only view of the broad-phase program (device snapshot or host vectors).
 struct BpView {
   int nj, n_links, n_moving, n_static, n_saves;
-  const int* joint_type;      // [nj]
-  const int* joint_q_source;  // [nj]
-  const double* joint_q_const;
-  const int* jsrc;   // [nj] -1: parent is the universe, 0: previous joint, k>0: save slot k-1
-  const int* jsave;  // [nj] save slot or -1
-  const float* jaxis;   // [nj*3]
-  const float* jplace;  // [nj*12]
-  const int* link_start;  // [nj+2] links grouped by parent joint
-  const int* link_order;  // [n_links]
-  const float* lplace;    // [n_links*12]
-  const int* obj_start;   // [n_links+1] moving objects grouped by link
-  const int* obj_order;   // [n_moving]
-  const int* moving_link; // [n_moving]
-  const float* moff;      // [n_moving*12]
-  const float* mobj;      // [n_moving*BM_STRIDE]
-  const float* sobj;      // [n_static*BS_STRIDE]
+  cptr<int> joint_type;      // [nj]
+  cptr<int> joint_q_source;  // [nj]
+  cptr<double> joint_q_const;
+  cptr<int> jsrc;   // [nj] -1: parent is the universe, 0: previous joint, k>0: save slot k-1
+  cptr<int> jsave;  // [nj] save slot or -1
+  cptr<float> jaxis;   // [nj*3]
+  cptr<float> jplace;  // [nj*12]
+  cptr<int> link_start;  // [nj+2] links grouped by parent joint
+  cptr<int> link_order;  // [n_links]
+  cptr<float> lplace;    // [n_links*12]
+  cptr<int> obj_start;   // [n_links+1] moving objects grouped by link
+  cptr<int> obj_order;   // [n_moving]
+  cptr<int> moving_link; // [n_moving]
+  cptr<float> moff;      // [n_moving*12]
+  cptr<float> mobj;      // [n_moving*BM_STRIDE]
+  cptr<float> sobj;      // [n_static*BS_STRIDE]
 };
 
 struct F34 {
@@ -56,7 +56,8 @@ struct F34 {
   float p[3];
 };
 
-MPG_INLINE F34 f34_load(const float* a) {
+template <class P>
+MPG_INLINE F34 f34_load(P a) {
   F34 T;
 #pragma unroll
   for (int i = 0; i < 9; ++i) T.R[i] = a[i];
@@ -117,7 +118,8 @@ MPG_INLINE void f_mat_to_quat(const float* m, float* q) {
 
 // revolute angles are reduced in fp64 before the fp32 sincos so large user
 // values (continuous joints) keep full fp32 accuracy
-MPG_INLINE F34 f_joint_motion(int type, const float* axis, double v) {
+template <class P>
+MPG_INLINE F34 f_joint_motion(int type, P axis, double v) {
   F34 M;
 #pragma unroll
   for (int i = 0; i < 9; ++i) M.R[i] = (i % 4 == 0) ? 1.f : 0.f;
@@ -253,7 +255,8 @@ MPG_INLINE bool fobb_separated(const FObb& A, const FObb& B, float margin) {
 }
 
 // moving-object bounding sphere vs static OBB
-MPG_INLINE bool fsphere_obb_separated(const float* c, float r, const float* sobj, float margin) {
+template <class P>
+MPG_INLINE bool fsphere_obb_separated(const float* c, float r, P sobj, float margin) {
   const float d[3] = {c[0] - sobj[BS_C], c[1] - sobj[BS_C + 1], c[2] - sobj[BS_C + 2]};
   float acc = 0.f;
 #pragma unroll
@@ -346,22 +349,22 @@ inline BpView bp_view(const mpg_world_desc* d, const BpProgram& P) {
   b.n_moving = d->n_moving;
   b.n_static = d->n_static;
   b.n_saves = P.n_saves;
-  b.joint_type = d->joint_type;
-  b.joint_q_source = d->joint_q_source;
-  b.joint_q_const = d->joint_q_const;
-  b.jsrc = P.jsrc.data();
-  b.jsave = P.jsave.data();
-  b.jaxis = P.jaxis.data();
-  b.jplace = P.jplace.data();
-  b.link_start = P.link_start.data();
-  b.link_order = P.link_order.data();
-  b.lplace = P.lplace.data();
-  b.obj_start = P.obj_start.data();
-  b.obj_order = P.obj_order.data();
-  b.moving_link = d->moving_link;
-  b.moff = P.moff.data();
-  b.mobj = P.mobj.data();
-  b.sobj = P.sobj.data();
+  b.joint_type = to_cptr<int>(d->joint_type);
+  b.joint_q_source = to_cptr<int>(d->joint_q_source);
+  b.joint_q_const = to_cptr<double>(d->joint_q_const);
+  b.jsrc = to_cptr<int>(P.jsrc.data());
+  b.jsave = to_cptr<int>(P.jsave.data());
+  b.jaxis = to_cptr<float>(P.jaxis.data());
+  b.jplace = to_cptr<float>(P.jplace.data());
+  b.link_start = to_cptr<int>(P.link_start.data());
+  b.link_order = to_cptr<int>(P.link_order.data());
+  b.lplace = to_cptr<float>(P.lplace.data());
+  b.obj_start = to_cptr<int>(P.obj_start.data());
+  b.obj_order = to_cptr<int>(P.obj_order.data());
+  b.moving_link = to_cptr<int>(d->moving_link);
+  b.moff = to_cptr<float>(P.moff.data());
+  b.mobj = to_cptr<float>(P.mobj.data());
+  b.sobj = to_cptr<float>(P.sobj.data());
   return b;
 }
 

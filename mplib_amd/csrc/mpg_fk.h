@@ -22,37 +22,40 @@ enum { S_ROT = 0, S_ROTINV = 4, S_POS = 8, S_OBBC = 11, S_R = 14, S_STRIDE = 23 
 struct DevWorld {
   int nj, dof, n_links, n_geoms, n_moving, n_static, n_pairs, W;
   double mpr_tol;
-  int debug_mode;  // diagnostics only: 1 = broad-phase records only, 2 = no SAT stage
-  const int* joint_type;      // [nj]
-  const int* joint_parent;    // [nj]
-  const int* joint_q_source;  // [nj]
-  const double* joint_q_const;
-  const double* joint_axis;   // [nj*3]
-  const double* joint_place;  // [nj*12]
-  const int* link_parent;     // [n_links]
-  const double* link_place;   // [n_links*12]
-  const int* geom_type;       // [n_geoms]
-  const int* geom_vstart;
-  const int* geom_nv;
-  const double* geom_rec;     // [n_geoms*G_STRIDE]
-  const double* verts;        // [nv*4] (x, y, z, 0)
-  const int* moving_link;     // [n_moving]
-  const int* moving_geom;
-  const double* moving_offset;  // [n_moving*12]
-  const int* static_geom;     // [n_static]
-  const double* static_rec;   // [n_static*S_STRIDE]
-  const int* pair_a;          // [n_pairs]
-  const int* pair_b;
-  const int* pair_allowed;
+  int debug_mode;  // diagnostics only: 1 = broad-phase records only, 2 = no SAT stage, 3 = no MPR
+  unsigned long long* stats;  // diagnostics only (MPG_STATS=1), else NULL
+  cptr<int> joint_type;      // [nj]
+  cptr<int> joint_parent;    // [nj]
+  cptr<int> joint_q_source;  // [nj]
+  cptr<double> joint_q_const;
+  cptr<double> joint_axis;   // [nj*3]
+  cptr<double> joint_place;  // [nj*12]
+  cptr<int> link_parent;     // [n_links]
+  cptr<double> link_place;   // [n_links*12]
+  cptr<int> geom_type;       // [n_geoms]
+  cptr<int> geom_gstart;     // [n_geoms] first 4-vertex group in `hull`
+  cptr<int> geom_ng;         // [n_geoms] number of groups
+  cptr<double> geom_rec;     // [n_geoms*G_STRIDE]
+  cptr<double> hull;         // AoSoA-4 vertex groups: x0..3 y0..3 z0..3
+  int hull_doubles;
+  cptr<int> moving_link;     // [n_moving]
+  cptr<int> moving_geom;
+  cptr<double> moving_offset;  // [n_moving*12]
+  cptr<int> static_geom;     // [n_static]
+  cptr<double> static_rec;   // [n_static*S_STRIDE]
+  cptr<int> pair_a;          // [n_pairs]
+  cptr<int> pair_b;
+  cptr<int> pair_allowed;
   // per user link: the joints from the root to link_parent[l] (1-based,
   // root first) -- lets a thread rebuild one link's oMi without the others
-  const int* link_chain_start;  // [n_links]
-  const int* link_chain_len;    // [n_links]
-  const int* chain_joints;
+  cptr<int> link_chain_start;  // [n_links]
+  cptr<int> link_chain_len;    // [n_links]
+  cptr<int> chain_joints;
   BpView bp;  // fp32 broad-phase program (mpg_broadphase.h)
 };
 
-MPG_INLINE SE3 load_se3(const double* p) {
+template <class P>
+MPG_INLINE SE3 load_se3(P p) {
   SE3 T;
 #pragma unroll
   for (int i = 0; i < 9; ++i) T.R[i] = p[i];
@@ -63,7 +66,8 @@ MPG_INLINE SE3 load_se3(const double* p) {
 }
 
 // pinocchio JointModel*::calc as a plain SE3 (see oracle/collide_oracle.c)
-MPG_INLINE SE3 joint_motion(int type, const double* axis, double v) {
+template <class P>
+MPG_INLINE SE3 joint_motion(int type, P axis, double v) {
   SE3 M;
   se3_identity(M);
   if (type <= MPG_JOINT_REVOLUTE_UNALIGNED || type >= MPG_JOINT_RUBX) {

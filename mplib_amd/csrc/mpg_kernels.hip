@@ -76,25 +76,35 @@ struct GObj {
   int type;
 };
 
-__device__ __forceinline__ V3 support(const DevWorld& w, const GObj& o, const V3& dir_world) {
+// HV: the hulls in AoSoA-4 layout (per group of 4 vertices: x0..3, y0..3,
+// z0..3), staged in LDS by the narrow kernel.  Hulls are padded to whole
+// groups with copies of their first vertex, which can never win the strict
+// '>' below, so the result equals the unpadded scan.
+__device__ __forceinline__ V3 support(const DevWorld& w, cptr<double> HV, const GObj& o,
+                                      const V3& dir_world) {
   const V3 dir = quat_rot(dir_world, o.rot_inv);
-  const double* rec = w.geom_rec + G_STRIDE * o.geom;
+  const cptr<double> rec = w.geom_rec + G_STRIDE * o.geom;
   V3 v;
   if (o.type == MPG_GEOM_CONVEX) {
     // Convex::findExtremeVertex: argmax dir . vertex, first maximum wins.
-    const int vs = w.geom_vstart[o.geom];
-    const int nv = w.geom_nv[o.geom];
-    const double* __restrict__ P = w.verts + 4 * (size_t)vs;
+    const cptr<double> P = HV + 12 * (size_t)w.geom_gstart[o.geom];
+    const int ng = w.geom_ng[o.geom];
     double best = -DBL_MAX;
     int bi = 0;
-    for (int i = 0; i < nv; ++i) {
-      const double d = (dir.x * P[4 * i] + dir.y * P[4 * i + 1]) + dir.z * P[4 * i + 2];
-      if (d > best) {
-        best = d;
-        bi = i;
-      }
+    for (int g = 0; g < ng; ++g) {
+      const cptr<double> G = P + 12 * g;
+      double dd[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) dd[k] = (dir.x * G[k] + dir.y * G[4 + k]) + dir.z * G[8 + k];
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (dd[k] > best) {
+          best = dd[k];
+          bi = 4 * g + k;
+        }
     }
-    v = v3(P[4 * bi], P[4 * bi + 1], P[4 * bi + 2]);
+    const cptr<double> B = P + 12 * (bi >> 2) + (bi & 3);
+    v = v3(B[0], B[4], B[8]);
   } else if (o.type == MPG_GEOM_BOX) {
     const double hx = rec[G_PARAM + 0] / 2.0, hy = rec[G_PARAM + 1] / 2.0, hz = rec[G_PARAM + 2] / 2.0;
     v = v3((dir.x >= 0 ? 1.0 : -1.0) * hx, (dir.y >= 0 ? 1.0 : -1.0) * hy, (dir.z >= 0 ? 1.0 : -1.0) * hz);
@@ -124,7 +134,7 @@ __device__ __forceinline__ V3 support(const DevWorld& w, const GObj& o, const V3
 
 __device__ __forceinline__ V3 center(const DevWorld& w, const GObj& o) {
   if (o.type == MPG_GEOM_CONVEX) {
-    const double* rec = w.geom_rec + G_STRIDE * o.geom;
+    const cptr<double> rec = w.geom_rec + G_STRIDE * o.geom;
     return vadd(quat_rot(v3(rec[G_INTERIOR], rec[G_INTERIOR + 1], rec[G_INTERIOR + 2]), o.rot), o.pos);
   }
   return o.pos;
@@ -144,24 +154,28 @@ __device__ __forceinline__ bool vec_is_origin(const V3& v) {
   return ccd_eq(v.x, 0.0) && ccd_eq(v.y, 0.0) && ccd_eq(v.z, 0.0);
 }
 
-__device__ __forceinline__ V3 msupport(const DevWorld& w, const GObj& a, const GObj& b, const V3& dir) {
-  const V3 s1 = support(w, a, dir);
-  const V3 s2 = support(w, b, vscale(dir, -1.0));
+__device__ __forceinline__ V3 msupport(const DevWorld& w, cptr<double> HV, const GObj& a,
+                                       const GObj& b, const V3& dir) {
+  const V3 s1 = support(w, HV, a, dir);
+  const V3 s2 = support(w, HV, b, vscale(dir, -1.0));
   return vsub(s1, s2);
 }
 
 // libccd 2.1 ccdMPRIntersect (discoverPortal + refinePortal).
-__device__ bool mpr_intersect(const DevWorld& w, const GObj& A, const GObj& B) {
+__device__ __forceinline__ bool mpr_intersect(const DevWorld& w, cptr<double> HV, const GObj& A,
+                                              const GObj& B, int& nsup) {
   V3 v0 = vsub(center(w, A), center(w, B));
   if (vec_is_origin(v0)) v0 = vadd(v0, v3(kCcdEps * 10.0, 0.0, 0.0));
   V3 dir = vnormalize(vscale(v0, -1.0));
-  V3 v1 = msupport(w, A, B, dir);
+  V3 v1 = msupport(w, HV, A, B, dir);
+  nsup = 1;
   double dot = vdot(v1, dir);
   if (is_zero(dot) || dot < 0.0) return false;
   dir = vcross(v0, v1);
   if (is_zero(vdot(dir, dir))) return true;  // origin on v1 or on segment v0-v1
   dir = vnormalize(dir);
-  V3 v2 = msupport(w, A, B, dir);
+  V3 v2 = msupport(w, HV, A, B, dir);
+  ++nsup;
   dot = vdot(v2, dir);
   if (is_zero(dot) || dot < 0.0) return false;
   {
@@ -176,7 +190,8 @@ __device__ bool mpr_intersect(const DevWorld& w, const GObj& A, const GObj& B) {
   }
   V3 v3p;
   for (;;) {
-    v3p = msupport(w, A, B, dir);
+    v3p = msupport(w, HV, A, B, dir);
+    ++nsup;
     dot = vdot(v3p, dir);
     if (is_zero(dot) || dot < 0.0) return false;
     bool cont = false;
@@ -202,7 +217,8 @@ __device__ bool mpr_intersect(const DevWorld& w, const GObj& A, const GObj& B) {
     dir = vnormalize(vcross(vsub(p2, p1), vsub(p3, p1)));
     dot = vdot(dir, p1);
     if (is_zero(dot) || dot > 0.0) return true;
-    const V3 v4 = msupport(w, A, B, dir);
+    const V3 v4 = msupport(w, HV, A, B, dir);
+    ++nsup;
     const double dv4 = vdot(v4, dir);
     if (!(is_zero(dv4) || dv4 > 0.0)) return false;
     {
@@ -255,7 +271,7 @@ __device__ __forceinline__ GObj moving_obj(const DevWorld& w, const double* __re
 }
 
 __device__ __forceinline__ GObj static_obj(const DevWorld& w, int sid) {
-  const double* r = w.static_rec + S_STRIDE * sid;
+  const cptr<double> r = w.static_rec + S_STRIDE * sid;
   GObj o;
   o.rot = Q4{r[S_ROT], r[S_ROT + 1], r[S_ROT + 2], r[S_ROT + 3]};
   o.rot_inv = Q4{r[S_ROTINV], r[S_ROTINV + 1], r[S_ROTINV + 2], r[S_ROTINV + 3]};
@@ -291,12 +307,12 @@ __device__ __forceinline__ FObb bp_obb(const DevWorld& w, const float* __restric
     o.c[0] = r[4 * block];
     o.c[1] = r[5 * block];
     o.c[2] = r[6 * block];
-    const float* g = w.bp.mobj + BM_STRIDE * id;
+    const cptr<float> g = w.bp.mobj + BM_STRIDE * id;
     o.e[0] = g[BM_E];
     o.e[1] = g[BM_E + 1];
     o.e[2] = g[BM_E + 2];
   } else {
-    const float* g = w.bp.sobj + BS_STRIDE * (id - w.n_moving);
+    const cptr<float> g = w.bp.sobj + BS_STRIDE * (id - w.n_moving);
 #pragma unroll
     for (int k = 0; k < 3; ++k) o.c[k] = g[BS_C + k];
 #pragma unroll
@@ -352,7 +368,7 @@ __global__ __launch_bounds__(BLOCK) void cull_kernel(DevWorld w, const double* _
     r[BLOCK] = q[1];
     r[2 * BLOCK] = q[2];
     r[3 * BLOCK] = q[3];
-    const float* g = w.bp.mobj + BM_STRIDE * m;
+    const cptr<float> g = w.bp.mobj + BM_STRIDE * m;
 #pragma unroll
     for (int i = 0; i < 3; ++i)
       r[(4 + i) * BLOCK] = T.R[3 * i] * g[BM_C] + T.R[3 * i + 1] * g[BM_C + 1] + T.R[3 * i + 2] * g[BM_C + 2] + T.p[i];
@@ -505,6 +521,9 @@ __global__ __launch_bounds__(256) void narrow_kernel(DevWorld w, const double* _
                                                     const uint32_t* __restrict__ prefix,
                                                     const uint32_t* __restrict__ cand,
                                                     uint8_t* __restrict__ flags, uint32_t* __restrict__ masks) {
+  // hull reads are wave-uniform: scalar loads through the constant cache
+  // (staging the hulls in LDS measured slower: +60 VGPRs, occupancy 4 -> 3)
+  const cptr<double> HV = w.hull;
   const uint32_t lane = lane_id();
   const uint32_t wave = __builtin_amdgcn_readfirstlane((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
   const uint32_t n_waves = (gridDim.x * blockDim.x) >> 6;
@@ -523,7 +542,18 @@ __global__ __launch_bounds__(256) void narrow_kernel(DevWorld w, const double* _
     const int a = w.pair_a[p], b = w.pair_b[p];
     const GObj A = a < w.n_moving ? moving_obj<FROM_POSES>(w, in, cfg, a) : static_obj(w, a - w.n_moving);
     const GObj B = b < w.n_moving ? moving_obj<FROM_POSES>(w, in, cfg, b) : static_obj(w, b - w.n_moving);
-    if (mpr_intersect(w, A, B)) {
+    int nsup = 0;
+#ifdef MPG_STATS
+    const bool hit = w.debug_mode == 3 ? (A.pos.x == 12345.0 && B.pos.x == 12345.0) : mpr_intersect(w, HV, A, B, nsup);
+    if (w.stats) {  // diagnostics build: candidates, support calls, hits
+      atomicAdd(&w.stats[0], 1ull);
+      atomicAdd(&w.stats[1], (unsigned long long)nsup);
+      if (hit) atomicAdd(&w.stats[2], 1ull);
+    }
+#else
+    const bool hit = mpr_intersect(w, HV, A, B, nsup);
+#endif
+    if (hit) {
       if (masks) atomicOr(&masks[cfg * w.W + (p >> 5)], 1u << (p & 31));
       flags[cfg] = 1;
     }
@@ -899,9 +929,23 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
 
   std::vector<double> static_rec((size_t)S_STRIDE * std::max(d->n_static, 1), 0.0);
   for (int s = 0; s < d->n_static; ++s) static_record(d, s, geom_rec.data(), static_rec.data() + (size_t)S_STRIDE * s);
-  std::vector<double> verts4((size_t)4 * std::max<int64_t>(d->n_vertices, 1), 0.0);
-  for (int64_t i = 0; i < d->n_vertices; ++i)
-    for (int k = 0; k < 3; ++k) verts4[4 * i + k] = d->vertices[3 * i + k];
+  // hulls in AoSoA-4 groups, padded with copies of the hull's first vertex
+  std::vector<int> gstart(std::max(d->n_geoms, 1), 0), ngroups(std::max(d->n_geoms, 1), 0);
+  std::vector<double> hull;
+  for (int g = 0; g < d->n_geoms; ++g) {
+    if (d->geom_type[g] != MPG_GEOM_CONVEX) continue;
+    const double* V = d->vertices + 3 * (size_t)d->geom_vertex_start[g];
+    const int nv = d->geom_vertex_count[g], ng = (nv + 3) / 4;
+    gstart[g] = (int)(hull.size() / 12);
+    ngroups[g] = ng;
+    for (int q = 0; q < ng; ++q)
+      for (int k = 0; k < 3; ++k)
+        for (int l = 0; l < 4; ++l) {
+          const int i = 4 * q + l < nv ? 4 * q + l : 0;
+          hull.push_back(V[3 * i + k]);
+        }
+  }
+  if (hull.empty()) hull.assign(12, 0.0);
   // per link: joints from the root to link_parent (chain FK in phase B)
   std::vector<int> chain_start, chain_len, chain_joints;
   for (int l = 0; l < d->n_links; ++l) {
@@ -925,10 +969,10 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
   const size_t o_lp = bb.add(d->link_parent, d->n_links);
   const size_t o_lpl = bb.add(d->link_placement, 12 * (size_t)d->n_links);
   const size_t o_gt = bb.add(d->geom_type, d->n_geoms);
-  const size_t o_gvs = bb.add(d->geom_vertex_start, d->n_geoms);
-  const size_t o_gnv = bb.add(d->geom_vertex_count, d->n_geoms);
+  const size_t o_gvs = bb.add(gstart.data(), gstart.size());
+  const size_t o_gnv = bb.add(ngroups.data(), ngroups.size());
   const size_t o_grec = bb.add(geom_rec.data(), geom_rec.size());
-  const size_t o_v = bb.add(verts4.data(), verts4.size());
+  const size_t o_v = bb.add(hull.data(), hull.size());
   const size_t o_ml = bb.add(d->moving_link, d->n_moving);
   const size_t o_mg = bb.add(d->moving_geom, d->n_moving);
   const size_t o_mo = bb.add(d->moving_offset, 12 * (size_t)d->n_moving);
@@ -981,32 +1025,38 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
   dw.W = W;
   dw.mpr_tol = d->gjk_tolerance;
   dw.debug_mode = std::getenv("MPG_DEBUG_CULL") ? std::atoi(std::getenv("MPG_DEBUG_CULL")) : 0;
-  dw.joint_type = reinterpret_cast<const int*>(base + o_jt);
-  dw.joint_parent = reinterpret_cast<const int*>(base + o_jp);
-  dw.joint_q_source = reinterpret_cast<const int*>(base + o_jqs);
-  dw.joint_q_const = reinterpret_cast<const double*>(base + o_jqc);
-  dw.joint_axis = reinterpret_cast<const double*>(base + o_ja);
-  dw.joint_place = reinterpret_cast<const double*>(base + o_jpl);
-  dw.link_parent = reinterpret_cast<const int*>(base + o_lp);
-  dw.link_place = reinterpret_cast<const double*>(base + o_lpl);
-  dw.geom_type = reinterpret_cast<const int*>(base + o_gt);
-  dw.geom_vstart = reinterpret_cast<const int*>(base + o_gvs);
-  dw.geom_nv = reinterpret_cast<const int*>(base + o_gnv);
-  dw.geom_rec = reinterpret_cast<const double*>(base + o_grec);
-  dw.verts = reinterpret_cast<const double*>(base + o_v);
-  dw.moving_link = reinterpret_cast<const int*>(base + o_ml);
-  dw.moving_geom = reinterpret_cast<const int*>(base + o_mg);
-  dw.moving_offset = reinterpret_cast<const double*>(base + o_mo);
-  dw.static_geom = reinterpret_cast<const int*>(base + o_sg);
-  dw.static_rec = reinterpret_cast<const double*>(base + o_srec);
-  dw.pair_a = reinterpret_cast<const int*>(base + o_pa);
-  dw.pair_b = reinterpret_cast<const int*>(base + o_pb);
-  dw.pair_allowed = reinterpret_cast<const int*>(base + o_al);
-  dw.link_chain_start = reinterpret_cast<const int*>(base + o_cs);
-  dw.link_chain_len = reinterpret_cast<const int*>(base + o_cl);
-  dw.chain_joints = reinterpret_cast<const int*>(base + o_cj);
-  auto I = [&](size_t o) { return reinterpret_cast<const int*>(base + o); };
-  auto F = [&](size_t o) { return reinterpret_cast<const float*>(base + o); };
+  dw.stats = nullptr;
+  if (std::getenv("MPG_STATS") && std::atoi(std::getenv("MPG_STATS")) > 0) {
+    HIP_TRY(hipMalloc(&dw.stats, 8 * sizeof(unsigned long long)));
+    HIP_TRY(hipMemset(dw.stats, 0, 8 * sizeof(unsigned long long)));
+  }
+  dw.joint_type = to_cptr<int>(base + o_jt);
+  dw.joint_parent = to_cptr<int>(base + o_jp);
+  dw.joint_q_source = to_cptr<int>(base + o_jqs);
+  dw.joint_q_const = to_cptr<double>(base + o_jqc);
+  dw.joint_axis = to_cptr<double>(base + o_ja);
+  dw.joint_place = to_cptr<double>(base + o_jpl);
+  dw.link_parent = to_cptr<int>(base + o_lp);
+  dw.link_place = to_cptr<double>(base + o_lpl);
+  dw.geom_type = to_cptr<int>(base + o_gt);
+  dw.geom_gstart = to_cptr<int>(base + o_gvs);
+  dw.geom_ng = to_cptr<int>(base + o_gnv);
+  dw.geom_rec = to_cptr<double>(base + o_grec);
+  dw.hull = to_cptr<double>(base + o_v);
+  dw.hull_doubles = (int)hull.size();
+  dw.moving_link = to_cptr<int>(base + o_ml);
+  dw.moving_geom = to_cptr<int>(base + o_mg);
+  dw.moving_offset = to_cptr<double>(base + o_mo);
+  dw.static_geom = to_cptr<int>(base + o_sg);
+  dw.static_rec = to_cptr<double>(base + o_srec);
+  dw.pair_a = to_cptr<int>(base + o_pa);
+  dw.pair_b = to_cptr<int>(base + o_pb);
+  dw.pair_allowed = to_cptr<int>(base + o_al);
+  dw.link_chain_start = to_cptr<int>(base + o_cs);
+  dw.link_chain_len = to_cptr<int>(base + o_cl);
+  dw.chain_joints = to_cptr<int>(base + o_cj);
+  auto I = [&](size_t o) { return to_cptr<int>(base + o); };
+  auto F = [&](size_t o) { return to_cptr<float>(base + o); };
   BpView& bp = dw.bp;
   bp.nj = d->n_joints;
   bp.n_links = d->n_links;
@@ -1041,6 +1091,14 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
 int mpg_world_destroy(mpg_world* w) {
   if (!w) return MPG_OK;
   hipSetDevice(w->device);
+  if (w->dw.stats) {
+    unsigned long long st[8];
+    hipDeviceSynchronize();
+    hipMemcpy(st, w->dw.stats, sizeof(st), hipMemcpyDeviceToHost);
+    std::fprintf(stderr, "[mpg stats] narrow candidates %llu, support calls %llu (%.2f/cand), hits %llu\n", st[0],
+                 st[1], st[0] ? (double)st[1] / st[0] : 0.0, st[2]);
+    hipFree(w->dw.stats);
+  }
   hipFree(w->blob);
   hipFree(w->d_q);
   hipFree(w->d_flags);

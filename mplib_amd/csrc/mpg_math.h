@@ -33,7 +33,23 @@
 #define MPG_INLINE inline
 #endif
 
+// Read-only snapshot arrays live in the constant address space on the device:
+// uniform reads of them become scalar (s_load) loads through the scalar cache
+// instead of vector loads that wait on the vector memory path.
+#if defined(__HIP_DEVICE_COMPILE__)
+#define MPG_CONST __attribute__((address_space(4)))
+#else
+#define MPG_CONST
+#endif
+
 namespace mpg {
+
+template <class T>
+using cptr = const T MPG_CONST*;
+template <class T>
+MPG_INLINE cptr<T> to_cptr(const void* p) {
+  return (cptr<T>)p;
+}
 
 constexpr double kSinCosTab[440] = MPG_SINCOSTAB_INIT;
 
@@ -231,6 +247,19 @@ MPG_INLINE void quat_to_mat(double w, double x, double y, double z, double* m) {
   m[8] = 1.0 - (txx + tyy);
 }
 
+// Eigen's non-positive-trace branch for a fixed largest diagonal index I
+template <int I>
+MPG_INLINE void mat_to_quat_diag(const double* m, double* w_out, double* xyz) {
+  constexpr int i = I, j = (I + 1) % 3, k = (j + 1) % 3;
+  double t = std::sqrt(((m[3 * i + i] - m[3 * j + j]) - m[3 * k + k]) + 1.0);
+  const double qi = 0.5 * t;
+  t = 0.5 / t;
+  *w_out = (m[3 * k + j] - m[3 * j + k]) * t;
+  xyz[i] = qi;
+  xyz[j] = (m[3 * j + i] + m[3 * i + j]) * t;
+  xyz[k] = (m[3 * k + i] + m[3 * i + k]) * t;
+}
+
 // Eigen quaternionbase_assign_impl<Matrix3,3,3>; out (w, x, y, z)
 MPG_INLINE void mat_to_quat(const double* m, double* w_out, double* xyz) {
   double t = (m[0] + m[4]) + m[8];
@@ -245,18 +274,10 @@ MPG_INLINE void mat_to_quat(const double* m, double* w_out, double* xyz) {
     int i = 0;
     if (m[4] > m[0]) i = 1;
     if (m[8] > m[3 * i + i]) i = 2;
-    int j = (i + 1) % 3, k = (j + 1) % 3;
-    t = std::sqrt(((m[3 * i + i] - m[3 * j + j]) - m[3 * k + k]) + 1.0);
-    double qi = 0.5 * t;
-    t = 0.5 / t;
-    double w = (m[3 * k + j] - m[3 * j + k]) * t;
-    double qj = (m[3 * j + i] + m[3 * i + j]) * t;
-    double qk = (m[3 * k + i] + m[3 * i + k]) * t;
-    *w_out = w;
-    // branch-free scatter keeps the arrays in registers on the GPU
-    xyz[0] = (i == 0) ? qi : (j == 0) ? qj : qk;
-    xyz[1] = (i == 1) ? qi : (j == 1) ? qj : qk;
-    xyz[2] = (i == 2) ? qi : (j == 2) ? qj : qk;
+    // constant indices per branch keep m[] in registers on the GPU
+    if (i == 0) mat_to_quat_diag<0>(m, w_out, xyz);
+    else if (i == 1) mat_to_quat_diag<1>(m, w_out, xyz);
+    else mat_to_quat_diag<2>(m, w_out, xyz);
   }
 }
 
