@@ -6,8 +6,9 @@ Panda 7-DoF + 10 boxes world (cfg3), 2^20 uniform-random configurations per
 GPU per step, weak scaling over 1/2/4/8 GPUs (one process per GPU).
 
 A step = one pass of the hot path (FK + all 129 pairs + ACM filter) over one
-2^20-configuration batch that is already resident in HBM: a single
-mpg_collide_batch launch writing flags[N] (u8) and pair_mask[N, 5] (u32).
+2^20-configuration batch that is already resident in HBM: one
+mpg_collide_batch call (cull -> bucket -> narrow kernels on one stream)
+writing flags[N] (u8) and pair_mask[N, 5] (u32).
 
 Usage:  python bench.py [--gpus N] [--steps K] [--warmup W] [--cpu-sample S]
         torchrun --nproc-per-node N bench.py --gpus N ...
@@ -27,6 +28,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+STAGES = ("cull", "bucket", "narrow")  # MPG_STAGE_* (include/mpgpu.h)
+KERNEL_NAME = {"cull": "cull_kernel", "bucket": "tile_count/pair_scan/chunk_scan/scatter", "narrow": "narrow_kernel"}
 FP64_VALU_PEAK_TFLOPS = 78.6  # MI355X spec (vector FP64; FMA counted as 2)
 
 
@@ -79,6 +82,8 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
+    w.profile_enable(True)  # HIP events around each device stage, on the launch stream
+    w.profile_read()
     starts = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
     ends = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
     if world > 1:
@@ -93,11 +98,19 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    kernel_ms = float(np.mean([s.elapsed_time(e) for s, e in zip(starts, ends)]))
+    step_ms = float(np.mean([s.elapsed_time(e) for s, e in zip(starts, ends)]))
+    prof = w.profile_read()
+    w.profile_enable(False)
+    # per-launch averages of each stage
+    st = {k: {"ms_per_launch": v[0] / max(v[1], 1), "launches_per_step": v[1] / args.steps,
+              "units_per_launch": v[2] / max(v[1], 1)} for k, v in prof.items()}
     if world > 1:
-        t = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device=q.device)
+        t = torch.tensor([elapsed, step_ms] + [st[k]["ms_per_launch"] for k in STAGES], dtype=torch.float64,
+                         device=q.device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, kernel_ms = float(t[0]), float(t[1])
+        elapsed, step_ms = float(t[0]), float(t[1])
+        for i, k in enumerate(STAGES):
+            st[k]["ms_per_launch"] = float(t[2 + i])
 
     gather_ms = None
     if args.gather and world > 1:
@@ -110,15 +123,22 @@ def main():
 
     total = n * world * args.steps
     value = total / elapsed
-    bytes_per_cfg = 8 * dim + 1 + 4 * W  # q read + flag + pair mask
-    achieved_gbps = bytes_per_cfg * n / (kernel_ms * 1e-3) / 1e9
+    # algorithmic bytes per unit (DESIGN.md "Roofline"):
+    #   cull:   per configuration  q row in + flag + pair-mask zeroing (8*dof + 1 + 4W)
+    #           + survivor words out (4W)
+    #   narrow: per candidate      candidate index + q row + mask word read-modify-write + flag
+    bytes_per_unit = {"cull": 8 * dim + 1 + 4 * W + 4 * W, "narrow": 4 + 8 * dim + 8 + 1,
+                      "bucket": 4 * W * 3 + 4 * (n_pairs + 1)}
+    dom = max(("cull", "narrow"), key=lambda k: st[k]["ms_per_launch"])
+    units = st[dom]["units_per_launch"]
+    achieved_gbps = bytes_per_unit[dom] * units / (st[dom]["ms_per_launch"] * 1e-3) / 1e9
     traffic = None
     pmc_file = os.path.join(ROOT, "profiles", f"pmc_cfg{cfg}.json")
     if os.path.exists(pmc_file):
         try:
-            traffic = json.load(open(pmc_file)).get("hbm_bytes_per_launch_per_config")
-            if traffic is not None:
-                traffic = traffic * n
+            pm = json.load(open(pmc_file))
+            if pm.get("configs_per_launch") == n and dom in pm.get("hbm_bytes_per_launch", {}):
+                traffic = pm["hbm_bytes_per_launch"][dom]
         except Exception:
             traffic = None
 
@@ -141,9 +161,14 @@ def main():
                                                                           "data-path collective)"},
         "roofline": {"bound": "hbm", "achieved": achieved_gbps, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": achieved_gbps / HBM_PEAK_GBPS, "traffic": traffic,
-                     "kernel": "collide_kernel<128,false>", "kernel_ms": kernel_ms,
-                     "algorithmic_bytes_per_config": bytes_per_cfg,
-                     "note": "fp64-VALU/latency bound; HBM fraction reported as mandated"},
+                     "kernel": KERNEL_NAME[dom], "kernel_ms": st[dom]["ms_per_launch"],
+                     "units_per_launch": units, "unit_kind": "configs" if dom == "cull" else "candidates",
+                     "algorithmic_bytes_per_unit": bytes_per_unit[dom],
+                     "note": "the path is fp32/fp64-VALU and latency bound, not HBM bound (DESIGN.md); "
+                             "HBM fraction reported as mandated"},
+        "stages": {k: {"ms_per_step": st[k]["ms_per_launch"] * st[k]["launches_per_step"],
+                       "units_per_launch": st[k]["units_per_launch"]} for k in STAGES},
+        "step_ms_events": step_ms,
     }
     if gather_ms is not None:
         result["gather_ms"] = gather_ms

@@ -182,6 +182,24 @@ int mpg_collide_link_poses(mpg_world *world, const double *link_pose, int64_t n,
 int mpg_fk_batch(mpg_world *world, const double *q, int64_t n, double *link_pose, int mem,
                  void *stream);
 
+/*
+ * Per-kernel timing with HIP events recorded on the launch stream (off by
+ * default; no cost when off).  mpg_profile_read synchronises the recorded
+ * events, writes the accumulated milliseconds, launch counts and work units
+ * of each stage since the last read (then resets them).  Units: configurations
+ * for CULL and BUCKET, narrow-phase (configuration, pair) candidates for
+ * NARROW.  Any output pointer may be NULL.
+ *   MPG_STAGE_CULL    phase A broad phase           (cull_kernel)
+ *   MPG_STAGE_BUCKET  survivor bucketing            (tile_count/pair_scan/chunk_scan/scatter)
+ *   MPG_STAGE_NARROW  phase B exact narrow phase    (narrow_kernel)
+ */
+#define MPG_STAGE_CULL 0
+#define MPG_STAGE_BUCKET 1
+#define MPG_STAGE_NARROW 2
+#define MPG_NUM_STAGES 3
+int mpg_profile_enable(mpg_world *world, int enable);
+int mpg_profile_read(mpg_world *world, double *ms, int64_t *launches, int64_t *units, int n_stages);
+
 /* Diagnostics: the device sin/cos used by the FK (host buffers). */
 int mpg_debug_sincos(const double *x, int64_t n, double *s, double *c, int device);
 

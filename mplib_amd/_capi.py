@@ -15,6 +15,7 @@ LIB_PATH = os.path.join(_HERE, "lib", "libmpgpu.so")
 
 MPG_OK, MPG_E_INVALID, MPG_E_UNSUPPORTED, MPG_E_HIP, MPG_E_NOMEM = 0, 1, 2, 3, 4
 MPG_MEM_HOST, MPG_MEM_DEVICE = 0, 1
+STAGES = ("cull", "bucket", "narrow")  # MPG_STAGE_* order
 
 (JOINT_RX, JOINT_RY, JOINT_RZ, JOINT_REVOLUTE_UNALIGNED, JOINT_PX, JOINT_PY, JOINT_PZ,
  JOINT_PRISMATIC_UNALIGNED, JOINT_RUBX, JOINT_RUBY, JOINT_RUBZ, JOINT_RUB_UNALIGNED) = range(12)
@@ -61,6 +62,9 @@ SIGNATURES = {
                                               ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]),
     "mpg_fk_batch": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p,
                                     ctypes.c_int, ctypes.c_void_p]),
+    "mpg_profile_enable": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    "mpg_profile_read": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double),
+                                        ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64), ctypes.c_int]),
     "mpg_debug_sincos": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p,
                                         ctypes.c_int]),
     "mpg_synchronize": (ctypes.c_int, [ctypes.c_int]),

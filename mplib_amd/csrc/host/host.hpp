@@ -508,6 +508,9 @@ class PlanningWorld {
   void collide_batch_device(const void* q, int64_t n, void* flags, void* masks, void* stream);
   int mask_words();
   mpg_world* device_world();  // rebuilds the snapshot if the world changed
+  void profile_enable(bool on);
+  struct StageTime { double ms; int64_t launches, units; };
+  std::vector<StageTime> profile_read();  // per MPG_STAGE_*
 
  private:
   std::vector<WorldCollisionResult> run_scalar(const CollisionRequest& r, bool self, bool others);

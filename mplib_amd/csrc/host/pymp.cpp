@@ -499,5 +499,17 @@ PYBIND11_MODULE(pymp, m_all) {
            },
            py::arg("states_ptr"), py::arg("n"), py::arg("flags_ptr"), py::arg("masks_ptr") = 0,
            py::arg("stream") = 0,
-           "Enqueue the batched check on device buffers (float64 [n, dim], uint8 [n], uint32 [n, W]).");
+           "Enqueue the batched check on device buffers (float64 [n, dim], uint8 [n], uint32 [n, W]).")
+      .def("profile_enable", &PW::profile_enable, py::arg("enable") = true,
+           "Record HIP events around each device stage of the batched check (diagnostics).")
+      .def("profile_read",
+           [](PW& w) {
+             static const char* names[MPG_NUM_STAGES] = {"cull", "bucket", "narrow"};
+             py::dict d;
+             auto v = w.profile_read();
+             for (int k = 0; k < MPG_NUM_STAGES; ++k) d[names[k]] = py::make_tuple(v[k].ms, v[k].launches, v[k].units);
+             return d;
+           },
+           "{stage: (milliseconds, launches, units)} accumulated since the last read; units are configurations "
+           "(cull, bucket) or narrow-phase candidates (narrow).");
 }

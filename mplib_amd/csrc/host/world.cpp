@@ -582,6 +582,16 @@ void PlanningWorld::collide_batch_device(const void* q, int64_t n, void* flags, 
                "mpg_collide_batch");
 }
 
+void PlanningWorld::profile_enable(bool on) { check_status(mpg_profile_enable(device_world(), on ? 1 : 0), "mpg_profile_enable"); }
+std::vector<PlanningWorld::StageTime> PlanningWorld::profile_read() {
+  double ms[MPG_NUM_STAGES];
+  int64_t n[MPG_NUM_STAGES], u[MPG_NUM_STAGES];
+  check_status(mpg_profile_read(device_world(), ms, n, u, MPG_NUM_STAGES), "mpg_profile_read");
+  std::vector<StageTime> out;
+  for (int k = 0; k < MPG_NUM_STAGES; ++k) out.push_back({ms[k], n[k], u[k]});
+  return out;
+}
+
 void set_global_seed(unsigned seed) { std::srand(seed); }
 
 }  // namespace mpgh

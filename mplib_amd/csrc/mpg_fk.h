@@ -52,6 +52,11 @@ struct DevWorld {
   cptr<int> link_chain_len;    // [n_links]
   cptr<int> chain_joints;
   BpView bp;  // fp32 broad-phase program (mpg_broadphase.h)
+  // phase-A pair schedule: entries [sched_start[m], sched_start[m+1]) are the
+  // non-allowed pairs whose lower moving object is m: (pair index, partner)
+  cptr<int> sched_start;  // [n_moving+1]
+  cptr<int> sched_pair;
+  cptr<int> sched_other;
 };
 
 template <class P>

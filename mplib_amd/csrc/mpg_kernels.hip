@@ -285,28 +285,33 @@ __device__ __forceinline__ uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi
 
 // ---------------------------------------------------------------------------
 // Phase A: one lane per configuration (mpg_broadphase.h).
-//   1. fp32 FK over the tree -> per moving object a record in LDS
-//      ([object][7][lane]: rotation quaternion xyzw + world OBB centre);
-//   2. per pair a cheap bounding test (sphere-sphere for robot pairs,
-//      sphere-OBB against static objects);
+//   1. fp32 FK over the tree -> per moving object its world OBB centre in LDS
+//      ([object][3][lane]) and its rotation quaternion in the workspace
+//      (rq[object][4][cfg], read back only by the SAT stage);
+//   2. pairs are walked grouped by their moving object (host-built schedule,
+//      ACM-allowed pairs dropped): the object's centre is loaded once, then
+//      a cheap bounding test per partner (sphere-OBB against static objects,
+//      sphere-sphere against moving ones);
 //   3. pairs that pass are queued per wave in LDS as (pair, lane) entries and
 //      the 15-axis OBB SAT runs 64 queued entries at a time with every lane
-//      busy -- the per-pair branch no longer makes the whole wave pay for one
-//      lane's survivor;
+//      busy -- one lane's survivor no longer makes the whole wave pay;
 //   4. SAT survivors set the configuration's bit in an LDS survivor word,
 //      written to surv[word][cfg] at the end (no global atomics).
 // Also zeroes this configuration's outputs for phase B.
 // ---------------------------------------------------------------------------
 constexpr int kQueue = 128;  // entries per wave: < 64 pending + <= 64 pushed
 
-__device__ __forceinline__ FObb bp_obb(const DevWorld& w, const float* __restrict__ rec, int id, int t, int block) {
+template <int BLOCK>
+__device__ __forceinline__ FObb bp_obb(const DevWorld& w, const float* __restrict__ cen, const float* __restrict__ rq,
+                                       long long cap, int id, int t, long long cfg) {
   FObb o;
   if (id < w.n_moving) {
-    const float* r = rec + (size_t)id * 7 * block + t;
-    f_quat_to_mat(r[3 * block], r[0], r[block], r[2 * block], o.R);
-    o.c[0] = r[4 * block];
-    o.c[1] = r[5 * block];
-    o.c[2] = r[6 * block];
+    const float* q = rq + (size_t)id * 4 * cap + cfg;
+    f_quat_to_mat(q[3 * cap], q[0], q[cap], q[2 * cap], o.R);
+    const float* c = cen + (size_t)id * 3 * BLOCK + t;
+    o.c[0] = c[0];
+    o.c[1] = c[BLOCK];
+    o.c[2] = c[2 * BLOCK];
     const cptr<float> g = w.bp.mobj + BM_STRIDE * id;
     o.e[0] = g[BM_E];
     o.e[1] = g[BM_E + 1];
@@ -324,15 +329,15 @@ __device__ __forceinline__ FObb bp_obb(const DevWorld& w, const float* __restric
 }
 
 template <int BLOCK>
-__device__ __forceinline__ void sat_drain(const DevWorld& w, const float* __restrict__ rec, uint32_t* survw,
-                                          const uint32_t* queue, uint32_t head, uint32_t cnt, int wbase,
-                                          uint32_t lane) {
+__device__ __forceinline__ void sat_drain(const DevWorld& w, const float* __restrict__ cen, const float* __restrict__ rq,
+                                          long long cap, long long cfg0, uint32_t* survw, const uint32_t* queue,
+                                          uint32_t head, uint32_t cnt, int wbase, uint32_t lane) {
   __builtin_amdgcn_wave_barrier();
   if (lane < cnt) {
     const uint32_t e = queue[(head + lane) & (kQueue - 1)];
     const int p = (int)(e >> 6), t = wbase + (int)(e & 63u);
-    const FObb A = bp_obb(w, rec, w.pair_a[p], t, BLOCK);
-    const FObb B = bp_obb(w, rec, w.pair_b[p], t, BLOCK);
+    const FObb A = bp_obb<BLOCK>(w, cen, rq, cap, w.pair_a[p], t, cfg0 + t);
+    const FObb B = bp_obb<BLOCK>(w, cen, rq, cap, w.pair_b[p], t, cfg0 + t);
     if (!fobb_separated(A, B, kBpMargin)) atomicOr(&survw[(p >> 5) * BLOCK + t], 1u << (p & 31));
   }
   __builtin_amdgcn_wave_barrier();
@@ -341,16 +346,18 @@ __device__ __forceinline__ void sat_drain(const DevWorld& w, const float* __rest
 template <int BLOCK, bool FROM_POSES>
 __global__ __launch_bounds__(BLOCK) void cull_kernel(DevWorld w, const double* __restrict__ in, long long n,
                                                     uint8_t* __restrict__ flags, uint32_t* __restrict__ masks,
-                                                    uint32_t* __restrict__ surv, long long cap) {
+                                                    uint32_t* __restrict__ surv, float* __restrict__ rq,
+                                                    long long cap) {
   extern __shared__ __attribute__((aligned(16))) float lds_f[];
-  float* rec = lds_f;                                                    // [n_moving][7][BLOCK]
-  float* save = rec + (size_t)w.n_moving * 7 * BLOCK;                    // [n_saves][12][BLOCK]
+  float* cen = lds_f;                                                    // [n_moving][3][BLOCK]
+  float* save = cen + (size_t)w.n_moving * 3 * BLOCK;                    // [n_saves][12][BLOCK]
   uint32_t* survw = reinterpret_cast<uint32_t*>(save + (size_t)w.bp.n_saves * 12 * BLOCK);  // [W][BLOCK]
   const int tid = threadIdx.x;
   uint32_t* queue = survw + (size_t)w.W * BLOCK + (tid >> 6) * kQueue;  // [BLOCK/64][kQueue]
   const uint32_t lane = lane_id();
   const int wbase = tid & ~63;
-  const long long cfg = (long long)blockIdx.x * BLOCK + tid;
+  const long long cfg0 = (long long)blockIdx.x * BLOCK;
+  const long long cfg = cfg0 + tid;
   const bool live = cfg < n;
   const long long c = live ? cfg : n - 1;  // dead lanes shadow a valid row and never queue
   if (live) {
@@ -363,15 +370,16 @@ __global__ __launch_bounds__(BLOCK) void cull_kernel(DevWorld w, const double* _
   auto put = [&](int m, const F34& T) {
     float q[4];
     f_mat_to_quat(T.R, q);
-    float* r = rec + (size_t)m * 7 * BLOCK + tid;
-    r[0] = q[0];
-    r[BLOCK] = q[1];
-    r[2 * BLOCK] = q[2];
-    r[3 * BLOCK] = q[3];
+    if (live) {
+      float* r = rq + (size_t)m * 4 * cap + cfg;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) r[k * cap] = q[k];
+    }
+    float* r = cen + (size_t)m * 3 * BLOCK + tid;
     const cptr<float> g = w.bp.mobj + BM_STRIDE * m;
 #pragma unroll
     for (int i = 0; i < 3; ++i)
-      r[(4 + i) * BLOCK] = T.R[3 * i] * g[BM_C] + T.R[3 * i + 1] * g[BM_C + 1] + T.R[3 * i + 2] * g[BM_C + 2] + T.p[i];
+      r[i * BLOCK] = T.R[3 * i] * g[BM_C] + T.R[3 * i + 1] * g[BM_C + 1] + T.R[3 * i + 2] * g[BM_C + 2] + T.p[i];
   };
   if (FROM_POSES) {
     for (int m = 0; m < w.n_moving; ++m) put(m, bp_from_pose7(w.bp, in + (c * w.n_links + w.moving_link[m]) * 7, m));
@@ -379,47 +387,49 @@ __global__ __launch_bounds__(BLOCK) void cull_kernel(DevWorld w, const double* _
     bp_fk(w.bp, in + c * w.dof, save + tid, BLOCK, put);
   }
   if (w.debug_mode == 1) {
-    if (live && rec[tid] == 12345.f) flags[cfg] = 2;  // keep the records alive
+    if (live && cen[tid] == 12345.f) flags[cfg] = 2;  // keep the records alive
     return;
   }
 
   uint32_t head = 0, tail = 0;  // wave-uniform queue cursors
-  for (int p = 0; p < w.n_pairs; ++p) {
-    if (w.pair_allowed[p]) continue;  // filterCollisions drops it whatever MPR says
-    const int a = w.pair_a[p], b = w.pair_b[p];
-    bool keep;
-    if (a < w.n_moving && b < w.n_moving) {
-      const float* ra = rec + (size_t)a * 7 * BLOCK + tid;
-      const float* rb = rec + (size_t)b * 7 * BLOCK + tid;
-      const float dx = rb[4 * BLOCK] - ra[4 * BLOCK], dy = rb[5 * BLOCK] - ra[5 * BLOCK],
-                  dz = rb[6 * BLOCK] - ra[6 * BLOCK];
-      const float rr = w.bp.mobj[BM_STRIDE * a + BM_R] + w.bp.mobj[BM_STRIDE * b + BM_R] + kBpMargin;
-      keep = dx * dx + dy * dy + dz * dz <= rr * rr;
-    } else {
-      const int m = a < w.n_moving ? a : b, st = (a < w.n_moving ? b : a) - w.n_moving;
-      const float* rm = rec + (size_t)m * 7 * BLOCK + tid;
-      const float cm[3] = {rm[4 * BLOCK], rm[5 * BLOCK], rm[6 * BLOCK]};
-      keep = !fsphere_obb_separated(cm, w.bp.mobj[BM_STRIDE * m + BM_R], w.bp.sobj + BS_STRIDE * st, kBpMargin);
-    }
-    keep = keep && live;
-    if (w.debug_mode == 2) {
-      if (keep) survw[(p >> 5) * BLOCK + tid] |= 1u << (p & 31);
-      continue;
-    }
-    const unsigned long long bal = __ballot(keep);
-    if (bal) {
-      if (keep) {
-        const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
-        queue[(tail + rank) & (kQueue - 1)] = ((uint32_t)p << 6) | lane;
+  for (int m = 0; m < w.n_moving; ++m) {
+    const int e0 = w.sched_start[m], e1 = w.sched_start[m + 1];
+    if (e0 == e1) continue;
+    const float* rm = cen + (size_t)m * 3 * BLOCK + tid;
+    const float cm[3] = {rm[0], rm[BLOCK], rm[2 * BLOCK]};
+    const float r_m = w.bp.mobj[BM_STRIDE * m + BM_R];
+    for (int e = e0; e < e1; ++e) {
+      const int p = w.sched_pair[e], o = w.sched_other[e];
+      bool keep;
+      if (o >= w.n_moving) {
+        keep = !fsphere_obb_separated(cm, r_m, w.bp.sobj + BS_STRIDE * (o - w.n_moving), kBpMargin);
+      } else {
+        const float* ro = cen + (size_t)o * 3 * BLOCK + tid;
+        const float dx = ro[0] - cm[0], dy = ro[BLOCK] - cm[1], dz = ro[2 * BLOCK] - cm[2];
+        const float rr = r_m + w.bp.mobj[BM_STRIDE * o + BM_R] + kBpMargin;
+        keep = dx * dx + dy * dy + dz * dz <= rr * rr;
       }
-      tail += (uint32_t)__popcll(bal);
-      if (tail - head >= 64) {
-        sat_drain<BLOCK>(w, rec, survw, queue, head, 64, wbase, lane);
-        head += 64;
+      keep = keep && live;
+      if (w.debug_mode == 2) {
+        if (keep) survw[(p >> 5) * BLOCK + tid] |= 1u << (p & 31);
+        continue;
+      }
+      const unsigned long long bal = __ballot(keep);
+      if (bal) {
+        if (keep) {
+          const uint32_t rank =
+              __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+          queue[(tail + rank) & (kQueue - 1)] = ((uint32_t)p << 6) | lane;
+        }
+        tail += (uint32_t)__popcll(bal);
+        if (tail - head >= 64) {
+          sat_drain<BLOCK>(w, cen, rq, cap, cfg0, survw, queue, head, 64, wbase, lane);
+          head += 64;
+        }
       }
     }
   }
-  if (tail != head) sat_drain<BLOCK>(w, rec, survw, queue, head, tail - head, wbase, lane);
+  if (tail != head) sat_drain<BLOCK>(w, cen, rq, cap, cfg0, survw, queue, head, tail - head, wbase, lane);
   if (live)
     for (int k = 0; k < w.W; ++k) surv[(long long)k * cap + cfg] = survw[k * BLOCK + tid];
 }
@@ -473,7 +483,7 @@ __global__ __launch_bounds__(1024) void pair_scan_kernel(uint32_t* __restrict__ 
 
 // segment starts + 64-candidate chunk prefix (n_pairs is small)
 __global__ void chunk_scan_kernel(const uint32_t* __restrict__ seg_len, int n_pairs, uint32_t* __restrict__ seg_start,
-                                  uint32_t* __restrict__ prefix) {
+                                  uint32_t* __restrict__ prefix, unsigned long long* units) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   uint32_t acc = 0, start = 0;
   for (int p = 0; p < n_pairs; ++p) {
@@ -483,6 +493,7 @@ __global__ void chunk_scan_kernel(const uint32_t* __restrict__ seg_len, int n_pa
     start += seg_len[p];
   }
   prefix[n_pairs] = acc;
+  if (units) atomicAdd(units, (unsigned long long)start);  // profiling: narrow-phase candidates
 }
 
 __global__ __launch_bounds__(256) void scatter_kernel(const uint32_t* __restrict__ surv, long long n, long long cap,
@@ -603,10 +614,24 @@ struct mpg_world {
     uint32_t* seg_start = nullptr;  // [n_pairs]
     uint32_t* prefix = nullptr;     // [n_pairs + 1] chunk prefix
     uint32_t* cand = nullptr;       // [n_pairs * cap] worst case
+    float* rq = nullptr;            // [n_moving * 4 * cap] phase-A rotations for the SAT stage
     long long cap = 0;
   };
   std::mutex ws_mu;
   std::map<hipStream_t, Workspace> ws;
+  // optional per-stage timing (mpg_profile_enable)
+  struct Mark {
+    int stage;
+    hipEvent_t a, b;
+  };
+  std::mutex prof_mu;
+  bool prof = false;
+  std::vector<Mark> marks;
+  std::vector<hipEvent_t> ev_pool;
+  double prof_ms[MPG_NUM_STAGES] = {0, 0, 0};
+  int64_t prof_n[MPG_NUM_STAGES] = {0, 0, 0};
+  int64_t prof_cfg = 0;                       // configurations launched while profiling
+  unsigned long long* prof_units = nullptr;   // device counter: narrow candidates
   long long max_chunk = 1 << 20;
   int narrow_blocks = 1024;
 };
@@ -766,7 +791,7 @@ void static_record(const mpg_world_desc* d, int s, const double* geom_rec_all, d
 
 // phase A LDS bytes per thread: records + FK save slots + survivor words + queue share
 size_t cull_lds_per_thread(int n_moving, int n_saves, int W) {
-  return (size_t)std::max(n_moving, 1) * 7 * sizeof(float) + (size_t)n_saves * 12 * sizeof(float) +
+  return (size_t)std::max(n_moving, 1) * 3 * sizeof(float) + (size_t)n_saves * 12 * sizeof(float) +
          (size_t)W * sizeof(uint32_t) + (kQueue / 64) * sizeof(uint32_t);
 }
 
@@ -794,6 +819,7 @@ int get_workspace(mpg_world* w, hipStream_t s, long long want, mpg_world::Worksp
   if (ws.cap < want) {
     for (uint32_t* p : {ws.surv, ws.cnt, ws.seg_len, ws.seg_start, ws.prefix, ws.cand})
       if (p) HIP_TRY(hipFree(p));
+    if (ws.rq) HIP_TRY(hipFree(ws.rq));
     ws = mpg_world::Workspace{};
     const long long tiles = (want + 63) / 64;
     HIP_TRY(hipMalloc(&ws.surv, sizeof(uint32_t) * w->dw.W * want));
@@ -802,11 +828,47 @@ int get_workspace(mpg_world* w, hipStream_t s, long long want, mpg_world::Worksp
     HIP_TRY(hipMalloc(&ws.seg_start, sizeof(uint32_t) * np));
     HIP_TRY(hipMalloc(&ws.prefix, sizeof(uint32_t) * (np + 1)));
     HIP_TRY(hipMalloc(&ws.cand, sizeof(uint32_t) * np * want));
+    HIP_TRY(hipMalloc(&ws.rq, sizeof(float) * 4 * std::max(w->dw.n_moving, 1) * want));
     ws.cap = want;
   }
   *out = &ws;
   return MPG_OK;
 }
+
+hipEvent_t prof_event(mpg_world* w) {
+  if (!w->ev_pool.empty()) {
+    hipEvent_t e = w->ev_pool.back();
+    w->ev_pool.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  if (hipEventCreate(&e) != hipSuccess) return nullptr;
+  return e;
+}
+
+// records the start of a stage on `stream` when profiling is on
+struct StageTimer {
+  mpg_world* w;
+  hipStream_t s;
+  int stage;
+  hipEvent_t a = nullptr;
+  StageTimer(mpg_world* w_, hipStream_t s_, int st) : w(w_), s(s_), stage(st) {
+    if (!w->prof) return;
+    std::lock_guard<std::mutex> lk(w->prof_mu);
+    a = prof_event(w);
+    if (a) hipEventRecord(a, s);
+  }
+  void stop() {
+    if (!a) return;
+    std::lock_guard<std::mutex> lk(w->prof_mu);
+    hipEvent_t b = prof_event(w);
+    if (!b) return;
+    hipEventRecord(b, s);
+    w->marks.push_back({stage, a, b});
+    a = nullptr;
+  }
+  ~StageTimer() { stop(); }
+};
 
 template <bool FROM_POSES>
 int launch_collide(mpg_world* w, const double* in, long long n, uint8_t* flags, uint32_t* masks, hipStream_t stream) {
@@ -822,21 +884,25 @@ int launch_collide(mpg_world* w, const double* in, long long n, uint8_t* flags, 
     uint8_t* fl = flags + off;
     uint32_t* mk = masks ? masks + off * w->dw.W : nullptr;
     const unsigned grid = (unsigned)((m + w->block - 1) / w->block);
+    StageTimer t_cull(w, stream, MPG_STAGE_CULL);
+    if (w->prof) w->prof_cfg += m;
     switch (w->block) {
       case 256:
         hipLaunchKernelGGL((cull_kernel<256, FROM_POSES>), dim3(grid), dim3(256), w->lds_bytes, stream, w->dw, qin,
-                           m, fl, mk, ws->surv, ws->cap);
+                           m, fl, mk, ws->surv, ws->rq, ws->cap);
         break;
       case 128:
         hipLaunchKernelGGL((cull_kernel<128, FROM_POSES>), dim3(grid), dim3(128), w->lds_bytes, stream, w->dw, qin,
-                           m, fl, mk, ws->surv, ws->cap);
+                           m, fl, mk, ws->surv, ws->rq, ws->cap);
         break;
       default:
         hipLaunchKernelGGL((cull_kernel<64, FROM_POSES>), dim3(grid), dim3(64), w->lds_bytes, stream, w->dw, qin, m,
-                           fl, mk, ws->surv, ws->cap);
+                           fl, mk, ws->surv, ws->rq, ws->cap);
         break;
     }
     HIP_TRY(hipGetLastError());
+    t_cull.stop();
+    StageTimer t_bucket(w, stream, MPG_STAGE_BUCKET);
     const int n_tiles = (int)((m + 63) / 64);
     const long long tw = (long long)n_tiles * w->dw.W;  // one wave per (word, tile)
     const unsigned gb = (unsigned)((tw + 3) / 4);
@@ -848,11 +914,13 @@ int launch_collide(mpg_world* w, const double* in, long long n, uint8_t* flags, 
       HIP_TRY(hipGetLastError());
     }
     hipLaunchKernelGGL(chunk_scan_kernel, dim3(1), dim3(64), 0, stream, ws->seg_len, w->dw.n_pairs, ws->seg_start,
-                       ws->prefix);
+                       ws->prefix, w->prof ? w->prof_units : nullptr);
     HIP_TRY(hipGetLastError());
     hipLaunchKernelGGL(scatter_kernel, dim3(gb), dim3(256), 0, stream, ws->surv, m, ws->cap, w->dw.n_pairs, w->dw.W,
                        n_tiles, ws->cnt, ws->seg_start, ws->cand);
     HIP_TRY(hipGetLastError());
+    t_bucket.stop();
+    StageTimer t_narrow(w, stream, MPG_STAGE_NARROW);
     // persistent narrow phase: enough waves to fill the chip, fewer for tiny batches
     const long long want_waves = (m * std::max(w->dw.n_pairs, 1) + 63) / 64;
     const unsigned nb = (unsigned)std::max<long long>(1, std::min<long long>(w->narrow_blocks, (want_waves + 3) / 4));
@@ -896,6 +964,52 @@ const char* mpg_version(void) { return "mpgpu 0.1 (gfx950, fp64, libccd-MPR)"; }
 int mpg_device_count(int* count) {
   if (!count) return set_error(MPG_E_INVALID, "count is NULL");
   HIP_TRY(hipGetDeviceCount(count));
+  return MPG_OK;
+}
+
+int mpg_profile_enable(mpg_world* w, int enable) {
+  if (!w) return set_error(MPG_E_INVALID, "world is NULL");
+  HIP_TRY(hipSetDevice(w->device));
+  std::lock_guard<std::mutex> lk(w->prof_mu);
+  if (enable && !w->prof_units) {
+    HIP_TRY(hipMalloc(&w->prof_units, sizeof(unsigned long long)));
+    HIP_TRY(hipMemset(w->prof_units, 0, sizeof(unsigned long long)));
+  }
+  w->prof = enable != 0;
+  return MPG_OK;
+}
+
+int mpg_profile_read(mpg_world* w, double* ms, int64_t* launches, int64_t* units, int n_stages) {
+  if (!w) return set_error(MPG_E_INVALID, "world is NULL");
+  HIP_TRY(hipSetDevice(w->device));
+  std::lock_guard<std::mutex> lk(w->prof_mu);
+  unsigned long long cand = 0;
+  if (w->prof_units) {
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpy(&cand, w->prof_units, sizeof(cand), hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemset(w->prof_units, 0, sizeof(cand)));
+  }
+  const int64_t u[MPG_NUM_STAGES] = {w->prof_cfg, w->prof_cfg, (int64_t)cand};
+  w->prof_cfg = 0;
+  for (auto& mk : w->marks) {
+    HIP_TRY(hipEventSynchronize(mk.b));
+    float t = 0.f;
+    HIP_TRY(hipEventElapsedTime(&t, mk.a, mk.b));
+    w->prof_ms[mk.stage] += t;
+    w->prof_n[mk.stage] += 1;
+    w->ev_pool.push_back(mk.a);
+    w->ev_pool.push_back(mk.b);
+  }
+  w->marks.clear();
+  for (int k = 0; k < MPG_NUM_STAGES; ++k) {
+    if (k < n_stages) {
+      if (ms) ms[k] = w->prof_ms[k];
+      if (launches) launches[k] = w->prof_n[k];
+      if (units) units[k] = u[k];
+    }
+    w->prof_ms[k] = 0.0;
+    w->prof_n[k] = 0;
+  }
   return MPG_OK;
 }
 
@@ -958,6 +1072,25 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
   }
   std::vector<int> allowed(std::max(d->n_pairs, 1), 0);
   for (int p = 0; p < d->n_pairs; ++p) allowed[p] = d->pair_allowed ? (d->pair_allowed[p] != 0) : 0;
+  // phase-A schedule: non-allowed pairs grouped by their lower moving object
+  std::vector<int> sched_start(d->n_moving + 1, 0), sched_pair, sched_other;
+  for (int m = 0; m < d->n_moving; ++m) {
+    sched_start[m] = (int)sched_pair.size();
+    for (int p = 0; p < d->n_pairs; ++p) {
+      if (allowed[p]) continue;
+      const int a = d->pair_a[p], b = d->pair_b[p];
+      const int lo = std::min(a, b), hi = std::max(a, b);  // static ids are >= n_moving
+      if (lo == m) {
+        sched_pair.push_back(p);
+        sched_other.push_back(hi);
+      }
+    }
+  }
+  sched_start[d->n_moving] = (int)sched_pair.size();
+  if (sched_pair.empty()) {
+    sched_pair.push_back(0);
+    sched_other.push_back(0);
+  }
 
   BlobBuilder bb;
   const size_t o_jt = bb.add(d->joint_type, d->n_joints);
@@ -984,6 +1117,9 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
   const size_t o_cs = bb.add(chain_start.data(), chain_start.size());
   const size_t o_cl = bb.add(chain_len.data(), chain_len.size());
   const size_t o_cj = bb.add(chain_joints.data(), chain_joints.size());
+  const size_t o_ss = bb.add(sched_start.data(), sched_start.size());
+  const size_t o_sp = bb.add(sched_pair.data(), sched_pair.size());
+  const size_t o_so = bb.add(sched_other.data(), sched_other.size());
   const size_t o_bjs = bb.add(bpp.jsrc.data(), bpp.jsrc.size());
   const size_t o_bjv = bb.add(bpp.jsave.data(), bpp.jsave.size());
   const size_t o_bja = bb.add(bpp.jaxis.data(), bpp.jaxis.size());
@@ -1056,6 +1192,9 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
   dw.link_chain_len = to_cptr<int>(base + o_cl);
   dw.chain_joints = to_cptr<int>(base + o_cj);
   auto I = [&](size_t o) { return to_cptr<int>(base + o); };
+  dw.sched_start = I(o_ss);
+  dw.sched_pair = I(o_sp);
+  dw.sched_other = I(o_so);
   auto F = [&](size_t o) { return to_cptr<float>(base + o); };
   BpView& bp = dw.bp;
   bp.nj = d->n_joints;
@@ -1104,10 +1243,19 @@ int mpg_world_destroy(mpg_world* w) {
   hipFree(w->d_flags);
   hipFree(w->d_masks);
   hipFree(w->d_out);
+  for (auto& mk : w->marks) {
+    hipEventDestroy(mk.a);
+    hipEventDestroy(mk.b);
+  }
+  for (hipEvent_t e : w->ev_pool) hipEventDestroy(e);
+  hipFree(w->prof_units);
   for (auto& kv : w->ws)
+  {
     for (uint32_t* p : {kv.second.surv, kv.second.cnt, kv.second.seg_len, kv.second.seg_start, kv.second.prefix,
                         kv.second.cand})
       hipFree(p);
+    hipFree(kv.second.rq);
+  }
   delete w;
   return MPG_OK;
 }
