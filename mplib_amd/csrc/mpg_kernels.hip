@@ -83,12 +83,15 @@ struct GObj {
 __device__ __forceinline__ V3 support(const DevWorld& w, cptr<double> HV, const GObj& o,
                                       const V3& dir_world) {
   const V3 dir = quat_rot(dir_world, o.rot_inv);
-  const cptr<double> rec = w.geom_rec + G_STRIDE * o.geom;
+  // the geometry is the same on every lane of the wave (one pair per wave):
+  // say so, so hull and parameter reads stay scalar loads
+  const int geom = __builtin_amdgcn_readfirstlane(o.geom), type = __builtin_amdgcn_readfirstlane(o.type);
+  const cptr<double> rec = w.geom_rec + G_STRIDE * geom;
   V3 v;
-  if (o.type == MPG_GEOM_CONVEX) {
+  if (type == MPG_GEOM_CONVEX) {
     // Convex::findExtremeVertex: argmax dir . vertex, first maximum wins.
-    const cptr<double> P = HV + 12 * (size_t)w.geom_gstart[o.geom];
-    const int ng = w.geom_ng[o.geom];
+    const cptr<double> P = HV + 12 * (size_t)w.geom_gstart[geom];
+    const int ng = w.geom_ng[geom];
     double best = -DBL_MAX;
     int bi = 0;
     for (int g = 0; g < ng; ++g) {
@@ -105,13 +108,13 @@ __device__ __forceinline__ V3 support(const DevWorld& w, cptr<double> HV, const 
     }
     const cptr<double> B = P + 12 * (bi >> 2) + (bi & 3);
     v = v3(B[0], B[4], B[8]);
-  } else if (o.type == MPG_GEOM_BOX) {
+  } else if (type == MPG_GEOM_BOX) {
     const double hx = rec[G_PARAM + 0] / 2.0, hy = rec[G_PARAM + 1] / 2.0, hz = rec[G_PARAM + 2] / 2.0;
     v = v3((dir.x >= 0 ? 1.0 : -1.0) * hx, (dir.y >= 0 ? 1.0 : -1.0) * hy, (dir.z >= 0 ? 1.0 : -1.0) * hz);
-  } else if (o.type == MPG_GEOM_SPHERE) {
+  } else if (type == MPG_GEOM_SPHERE) {
     const double r = rec[G_PARAM];
     v = vscale(vscale(dir, r), 1.0 / std::sqrt(vdot(dir, dir)));
-  } else if (o.type == MPG_GEOM_CAPSULE) {
+  } else if (type == MPG_GEOM_CAPSULE) {
     const double r = rec[G_PARAM], h = rec[G_PARAM + 1] / 2.0;
     const V3 n = vscale(vnormalize(dir), r);
     V3 p1 = v3(0.0, 0.0, h), p2 = v3(0.0, 0.0, -h);
@@ -133,8 +136,8 @@ __device__ __forceinline__ V3 support(const DevWorld& w, cptr<double> HV, const 
 }
 
 __device__ __forceinline__ V3 center(const DevWorld& w, const GObj& o) {
-  if (o.type == MPG_GEOM_CONVEX) {
-    const cptr<double> rec = w.geom_rec + G_STRIDE * o.geom;
+  if (__builtin_amdgcn_readfirstlane(o.type) == MPG_GEOM_CONVEX) {
+    const cptr<double> rec = w.geom_rec + G_STRIDE * __builtin_amdgcn_readfirstlane(o.geom);
     return vadd(quat_rot(v3(rec[G_INTERIOR], rec[G_INTERIOR + 1], rec[G_INTERIOR + 2]), o.rot), o.pos);
   }
   return o.pos;
@@ -159,85 +162,6 @@ __device__ __forceinline__ V3 msupport(const DevWorld& w, cptr<double> HV, const
   const V3 s1 = support(w, HV, a, dir);
   const V3 s2 = support(w, HV, b, vscale(dir, -1.0));
   return vsub(s1, s2);
-}
-
-// libccd 2.1 ccdMPRIntersect (discoverPortal + refinePortal).
-__device__ __forceinline__ bool mpr_intersect(const DevWorld& w, cptr<double> HV, const GObj& A,
-                                              const GObj& B, int& nsup) {
-  V3 v0 = vsub(center(w, A), center(w, B));
-  if (vec_is_origin(v0)) v0 = vadd(v0, v3(kCcdEps * 10.0, 0.0, 0.0));
-  V3 dir = vnormalize(vscale(v0, -1.0));
-  V3 v1 = msupport(w, HV, A, B, dir);
-  nsup = 1;
-  double dot = vdot(v1, dir);
-  if (is_zero(dot) || dot < 0.0) return false;
-  dir = vcross(v0, v1);
-  if (is_zero(vdot(dir, dir))) return true;  // origin on v1 or on segment v0-v1
-  dir = vnormalize(dir);
-  V3 v2 = msupport(w, HV, A, B, dir);
-  ++nsup;
-  dot = vdot(v2, dir);
-  if (is_zero(dot) || dot < 0.0) return false;
-  {
-    const V3 va = vsub(v1, v0), vb = vsub(v2, v0);
-    dir = vnormalize(vcross(va, vb));
-  }
-  if (vdot(dir, v0) > 0.0) {
-    const V3 t = v1;
-    v1 = v2;
-    v2 = t;
-    dir = vscale(dir, -1.0);
-  }
-  V3 v3p;
-  for (;;) {
-    v3p = msupport(w, HV, A, B, dir);
-    ++nsup;
-    dot = vdot(v3p, dir);
-    if (is_zero(dot) || dot < 0.0) return false;
-    bool cont = false;
-    double d2 = vdot(vcross(v1, v3p), v0);
-    if (d2 < 0.0 && !is_zero(d2)) {
-      v2 = v3p;
-      cont = true;
-    }
-    if (!cont) {
-      d2 = vdot(vcross(v3p, v2), v0);
-      if (d2 < 0.0 && !is_zero(d2)) {
-        v1 = v3p;
-        cont = true;
-      }
-    }
-    if (!cont) break;
-    const V3 va = vsub(v1, v0), vb = vsub(v2, v0);
-    dir = vnormalize(vcross(va, vb));
-  }
-  // refinePortal (no iteration cap in libccd 2.1)
-  V3 p1 = v1, p2 = v2, p3 = v3p;
-  for (;;) {
-    dir = vnormalize(vcross(vsub(p2, p1), vsub(p3, p1)));
-    dot = vdot(dir, p1);
-    if (is_zero(dot) || dot > 0.0) return true;
-    const V3 v4 = msupport(w, HV, A, B, dir);
-    ++nsup;
-    const double dv4 = vdot(v4, dir);
-    if (!(is_zero(dv4) || dv4 > 0.0)) return false;
-    {
-      const double dv1 = vdot(p1, dir), dv2 = vdot(p2, dir), dv3 = vdot(p3, dir);
-      double d1 = dv4 - dv1;
-      const double dd2 = dv4 - dv2, dd3 = dv4 - dv3;
-      d1 = (d1 < dd2) ? d1 : dd2;  // CCD_FMIN
-      d1 = (d1 < dd3) ? d1 : dd3;
-      if (ccd_eq(d1, w.mpr_tol) || d1 < w.mpr_tol) return false;
-    }
-    const V3 v4v0 = vcross(v4, v0);
-    if (vdot(p1, v4v0) > 0.0) {
-      if (vdot(p2, v4v0) > 0.0) p1 = v4;
-      else p3 = v4;
-    } else {
-      if (vdot(p3, v4v0) > 0.0) p2 = v4;
-      else p1 = v4;
-    }
-  }
 }
 
 // ---------------------------------------------------------------------------
@@ -299,7 +223,14 @@ __device__ __forceinline__ uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi
 //      written to surv[word][cfg] at the end (no global atomics).
 // Also zeroes this configuration's outputs for phase B.
 // ---------------------------------------------------------------------------
+#ifndef MPG_TASK
+#define MPG_TASK 128
+#endif
+#ifndef MPG_REFILL
+#define MPG_REFILL 32
+#endif
 constexpr int kQueue = 128;  // entries per wave: < 64 pending + <= 64 pushed
+constexpr uint32_t kTask = MPG_TASK;  // narrow phase: candidates of one pair per wave task
 
 template <int BLOCK>
 __device__ __forceinline__ FObb bp_obb(const DevWorld& w, const float* __restrict__ cen, const float* __restrict__ rq,
@@ -481,7 +412,7 @@ __global__ __launch_bounds__(1024) void pair_scan_kernel(uint32_t* __restrict__ 
   if (threadIdx.x == 1023) seg_len[blockIdx.x] = part[1023];
 }
 
-// segment starts + 64-candidate chunk prefix (n_pairs is small)
+// segment starts + prefix of narrow-phase tasks (kTask candidates of one pair)
 __global__ void chunk_scan_kernel(const uint32_t* __restrict__ seg_len, int n_pairs, uint32_t* __restrict__ seg_start,
                                   uint32_t* __restrict__ prefix, unsigned long long* units) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
@@ -489,10 +420,11 @@ __global__ void chunk_scan_kernel(const uint32_t* __restrict__ seg_len, int n_pa
   for (int p = 0; p < n_pairs; ++p) {
     prefix[p] = acc;
     seg_start[p] = start;
-    acc += (seg_len[p] + 63u) >> 6;
+    acc += (seg_len[p] + kTask - 1) / kTask;
     start += seg_len[p];
   }
   prefix[n_pairs] = acc;
+  prefix[n_pairs + 1] = 0;  // narrow-phase task counter
   if (units) atomicAdd(units, (unsigned long long)start);  // profiling: narrow-phase candidates
 }
 
@@ -525,48 +457,181 @@ __global__ __launch_bounds__(256) void scatter_kernel(const uint32_t* __restrict
 // and only the MPR iteration count diverges.  Poses are rebuilt in fp64 from
 // the joint values (chain FK), bit-identical to phase A / the reference.
 // ---------------------------------------------------------------------------
+// ---------------------------------------------------------------------------
+// Phase B: exact narrow phase (fp64, bit-identical to the reference).
+//
+// A wave takes a task of up to kTask candidates of ONE pair, so every lane
+// scans the same hull (wave-uniform scalar loads).  libccd's MPR is run as a
+// per-lane state machine whose every step is exactly one Minkowski support
+// call: all lanes step together through the (uniform) support scan and only
+// the cheap portal update diverges.  A lane that finishes takes the next
+// candidate of the task; refills are batched (>= 32 idle lanes, or none
+// active) so the fp64 chain FK of the refilled lanes runs at high lane
+// occupancy too.  Results: atomicOr into the pair mask, flag = 1.
+//
+// States follow ccdMPRIntersect (libccd 2.1 mpr.c): discoverPortal's v1, v2
+// and v3 support points (1, 2, 3), then refinePortal's v4 (4).
+// ---------------------------------------------------------------------------
+enum : int { MPR_DONE = 0, MPR_V1 = 1, MPR_V2 = 2, MPR_V3 = 3, MPR_V4 = 4 };
+
 template <bool FROM_POSES>
 __global__ __launch_bounds__(256) void narrow_kernel(DevWorld w, const double* __restrict__ in,
                                                     const uint32_t* __restrict__ seg_len,
                                                     const uint32_t* __restrict__ seg_start,
                                                     const uint32_t* __restrict__ prefix,
                                                     const uint32_t* __restrict__ cand,
-                                                    uint8_t* __restrict__ flags, uint32_t* __restrict__ masks) {
+                                                    uint8_t* __restrict__ flags, uint32_t* __restrict__ masks,
+                                                    uint32_t* __restrict__ task_ctr) {
   // hull reads are wave-uniform: scalar loads through the constant cache
   // (staging the hulls in LDS measured slower: +60 VGPRs, occupancy 4 -> 3)
   const cptr<double> HV = w.hull;
   const uint32_t lane = lane_id();
-  const uint32_t wave = __builtin_amdgcn_readfirstlane((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
-  const uint32_t n_waves = (gridDim.x * blockDim.x) >> 6;
   const uint32_t total = prefix[w.n_pairs];
-  for (uint32_t ch = wave; ch < total; ch += n_waves) {
-    int lo = 0, hi = w.n_pairs;  // prefix[lo] <= ch < prefix[hi]
+  for (;;) {
+    uint32_t tk = 0;  // dynamic task queue: waves that drew cheap tasks take more
+    if (lane == 0) tk = atomicAdd(task_ctr, 1u);
+    tk = __builtin_amdgcn_readfirstlane(tk);
+    if (tk >= total) break;
+    int lo = 0, hi = w.n_pairs;  // prefix[lo] <= tk < prefix[hi]
     while (hi - lo > 1) {
       const int mid = (lo + hi) >> 1;
-      if (prefix[mid] <= ch) lo = mid;
+      if (prefix[mid] <= tk) lo = mid;
       else hi = mid;
     }
     const int p = lo;
-    const uint32_t idx = (ch - prefix[p]) * 64u + lane;
-    if (idx >= seg_len[p]) continue;
-    const long long cfg = cand[seg_start[p] + idx];
+    const uint32_t t0 = (tk - prefix[p]) * kTask;
+    const uint32_t t1 = min(seg_len[p], t0 + kTask);
+    const uint32_t* __restrict__ cl = cand + seg_start[p];
     const int a = w.pair_a[p], b = w.pair_b[p];
-    const GObj A = a < w.n_moving ? moving_obj<FROM_POSES>(w, in, cfg, a) : static_obj(w, a - w.n_moving);
-    const GObj B = b < w.n_moving ? moving_obj<FROM_POSES>(w, in, cfg, b) : static_obj(w, b - w.n_moving);
-    int nsup = 0;
-#ifdef MPG_STATS
-    const bool hit = w.debug_mode == 3 ? (A.pos.x == 12345.0 && B.pos.x == 12345.0) : mpr_intersect(w, HV, A, B, nsup);
-    if (w.stats) {  // diagnostics build: candidates, support calls, hits
-      atomicAdd(&w.stats[0], 1ull);
-      atomicAdd(&w.stats[1], (unsigned long long)nsup);
-      if (hit) atomicAdd(&w.stats[2], 1ull);
-    }
-#else
-    const bool hit = mpr_intersect(w, HV, A, B, nsup);
-#endif
-    if (hit) {
-      if (masks) atomicOr(&masks[cfg * w.W + (p >> 5)], 1u << (p & 31));
-      flags[cfg] = 1;
+    const bool am = a < w.n_moving, bm = b < w.n_moving;
+    const uint32_t bit = 1u << (p & 31);
+    uint32_t next = t0;  // wave-uniform
+    int st = MPR_DONE;
+    long long cfg = 0;
+    GObj A, B;
+    if (!am) A = static_obj(w, a - w.n_moving);
+    if (!bm) B = static_obj(w, b - w.n_moving);
+    V3 v0, v1, v2, v3, dir;
+    for (;;) {
+      const unsigned long long idle = __ballot(st == MPR_DONE);
+      const uint32_t n_idle = (uint32_t)__popcll(idle);
+      if (next < t1 && (n_idle >= MPG_REFILL || n_idle == 64)) {  // batched refill
+        if (st == MPR_DONE) {
+          const uint32_t rank =
+              __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
+          const uint32_t idx = next + rank;
+          if (idx < t1) {
+            cfg = cl[idx];
+            if (am) A = moving_obj<FROM_POSES>(w, in, cfg, a);
+            if (bm) B = moving_obj<FROM_POSES>(w, in, cfg, b);
+            // findOrigin; discoverPortal's v0 and first direction
+            v0 = vsub(center(w, A), center(w, B));
+            if (vec_is_origin(v0)) v0 = vadd(v0, mpg::v3(kCcdEps * 10.0, 0.0, 0.0));
+            dir = vnormalize(vscale(v0, -1.0));
+            st = MPR_V1;
+          }
+        }
+        next = min(t1, next + n_idle);
+      }
+      if (__ballot(st != MPR_DONE) == 0) {
+        if (next >= t1) break;
+        continue;
+      }
+      if (st != MPR_DONE) {
+        const V3 s = msupport(w, HV, A, B, dir);
+        int res = 0;  // 1 = intersect, -1 = separated
+        if (st == MPR_V1) {
+          v1 = s;
+          const double dot = vdot(v1, dir);
+          if (is_zero(dot) || dot < 0.0) {
+            res = -1;
+          } else {
+            dir = vcross(v0, v1);
+            if (is_zero(vdot(dir, dir))) {
+              res = 1;  // origin on v1 or on segment v0-v1
+            } else {
+              dir = vnormalize(dir);
+              st = MPR_V2;
+            }
+          }
+        } else if (st == MPR_V2) {
+          v2 = s;
+          const double dot = vdot(v2, dir);
+          if (is_zero(dot) || dot < 0.0) {
+            res = -1;
+          } else {
+            dir = vnormalize(vcross(vsub(v1, v0), vsub(v2, v0)));
+            if (vdot(dir, v0) > 0.0) {
+              const V3 t = v1;
+              v1 = v2;
+              v2 = t;
+              dir = vscale(dir, -1.0);
+            }
+            st = MPR_V3;
+          }
+        } else if (st == MPR_V3) {
+          v3 = s;
+          const double dot = vdot(v3, dir);
+          if (is_zero(dot) || dot < 0.0) {
+            res = -1;
+          } else {
+            bool cont = false;
+            double d2 = vdot(vcross(v1, v3), v0);
+            if (d2 < 0.0 && !is_zero(d2)) {
+              v2 = v3;
+              cont = true;
+            }
+            if (!cont) {
+              d2 = vdot(vcross(v3, v2), v0);
+              if (d2 < 0.0 && !is_zero(d2)) {
+                v1 = v3;
+                cont = true;
+              }
+            }
+            if (cont) {
+              dir = vnormalize(vcross(vsub(v1, v0), vsub(v2, v0)));
+            } else {  // portal found: refinePortal with (v1, v2, v3)
+              dir = vnormalize(vcross(vsub(v2, v1), vsub(v3, v1)));
+              const double d = vdot(dir, v1);
+              if (is_zero(d) || d > 0.0) res = 1;
+              else st = MPR_V4;
+            }
+          }
+        } else {  // MPR_V4: expand the portal (v1, v2, v3) towards v4
+          const double dv4 = vdot(s, dir);
+          if (!(is_zero(dv4) || dv4 > 0.0)) {
+            res = -1;
+          } else {
+            const double dv1 = vdot(v1, dir), dv2 = vdot(v2, dir), dv3 = vdot(v3, dir);
+            double d1 = dv4 - dv1;
+            const double dd2 = dv4 - dv2, dd3 = dv4 - dv3;
+            d1 = (d1 < dd2) ? d1 : dd2;  // CCD_FMIN
+            d1 = (d1 < dd3) ? d1 : dd3;
+            if (ccd_eq(d1, w.mpr_tol) || d1 < w.mpr_tol) {
+              res = -1;
+            } else {
+              const V3 v4v0 = vcross(s, v0);
+              if (vdot(v1, v4v0) > 0.0) {
+                if (vdot(v2, v4v0) > 0.0) v1 = s;
+                else v3 = s;
+              } else {
+                if (vdot(v3, v4v0) > 0.0) v2 = s;
+                else v1 = s;
+              }
+              dir = vnormalize(vcross(vsub(v2, v1), vsub(v3, v1)));
+              const double d = vdot(dir, v1);
+              if (is_zero(d) || d > 0.0) res = 1;
+            }
+          }
+        }
+        if (res != 0) {
+          if (res > 0) {
+            if (masks) atomicOr(&masks[cfg * w.W + (p >> 5)], bit);
+            flags[cfg] = 1;
+          }
+          st = MPR_DONE;
+        }
+      }
     }
   }
 }
@@ -612,7 +677,7 @@ struct mpg_world {
     uint32_t* cnt = nullptr;        // [n_pairs * n_tiles] tile counts -> offsets
     uint32_t* seg_len = nullptr;    // [n_pairs]
     uint32_t* seg_start = nullptr;  // [n_pairs]
-    uint32_t* prefix = nullptr;     // [n_pairs + 1] chunk prefix
+    uint32_t* prefix = nullptr;     // [n_pairs + 2] task prefix + task counter
     uint32_t* cand = nullptr;       // [n_pairs * cap] worst case
     float* rq = nullptr;            // [n_moving * 4 * cap] phase-A rotations for the SAT stage
     long long cap = 0;
@@ -826,7 +891,7 @@ int get_workspace(mpg_world* w, hipStream_t s, long long want, mpg_world::Worksp
     HIP_TRY(hipMalloc(&ws.cnt, sizeof(uint32_t) * np * tiles));
     HIP_TRY(hipMalloc(&ws.seg_len, sizeof(uint32_t) * np));
     HIP_TRY(hipMalloc(&ws.seg_start, sizeof(uint32_t) * np));
-    HIP_TRY(hipMalloc(&ws.prefix, sizeof(uint32_t) * (np + 1)));
+    HIP_TRY(hipMalloc(&ws.prefix, sizeof(uint32_t) * (np + 2)));
     HIP_TRY(hipMalloc(&ws.cand, sizeof(uint32_t) * np * want));
     HIP_TRY(hipMalloc(&ws.rq, sizeof(float) * 4 * std::max(w->dw.n_moving, 1) * want));
     ws.cap = want;
@@ -922,10 +987,10 @@ int launch_collide(mpg_world* w, const double* in, long long n, uint8_t* flags, 
     t_bucket.stop();
     StageTimer t_narrow(w, stream, MPG_STAGE_NARROW);
     // persistent narrow phase: enough waves to fill the chip, fewer for tiny batches
-    const long long want_waves = (m * std::max(w->dw.n_pairs, 1) + 63) / 64;
+    const long long want_waves = (m * std::max(w->dw.n_pairs, 1) + kTask - 1) / kTask;
     const unsigned nb = (unsigned)std::max<long long>(1, std::min<long long>(w->narrow_blocks, (want_waves + 3) / 4));
     hipLaunchKernelGGL((narrow_kernel<FROM_POSES>), dim3(nb), dim3(256), 0, stream, w->dw, qin, ws->seg_len,
-                       ws->seg_start, ws->prefix, ws->cand, fl, mk);
+                       ws->seg_start, ws->prefix, ws->cand, fl, mk, ws->prefix + w->dw.n_pairs + 1);
     HIP_TRY(hipGetLastError());
   }
   return MPG_OK;
@@ -1220,7 +1285,11 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
   bp.sobj = F(o_bsb);
   int cus = 256;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0) cus = 256;
-  w->narrow_blocks = cus * 4;
+  // persistent narrow grid: exactly the resident workgroups
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, narrow_kernel<false>, 256, 0) != hipSuccess || per_cu <= 0)
+    per_cu = 2;
+  w->narrow_blocks = cus * per_cu;
   // bound the candidate lists to 1 GiB: cap * n_pairs * 4 B
   w->max_chunk = std::max<long long>(4096, std::min<long long>(1 << 20, (1ll << 28) / std::max(d->n_pairs, 1)));
   *out = w;
