@@ -15,7 +15,7 @@ namespace mpg {
 constexpr int kMaxJoints = 32;
 
 // per-geometry double record
-enum { G_PARAM = 0, G_INTERIOR = 4, G_OBB_C = 7, G_OBB_E = 10, G_RADIUS = 13, G_STRIDE = 14 };
+enum { G_PARAM = 0, G_INTERIOR = 4, G_OBB_C = 7, G_OBB_E = 10, G_RADIUS = 13, G_VMAX = 14, G_STRIDE = 15 };
 // per-static-object double record
 enum { S_ROT = 0, S_ROTINV = 4, S_POS = 8, S_OBBC = 11, S_R = 14, S_STRIDE = 23 };
 
@@ -37,6 +37,7 @@ struct DevWorld {
   cptr<int> geom_ng;         // [n_geoms] number of groups
   cptr<double> geom_rec;     // [n_geoms*G_STRIDE]
   cptr<double> hull;         // AoSoA-4 vertex groups: x0..3 y0..3 z0..3
+  cptr<float> hull32;        // the same groups in fp32, padding = NaN (support pre-pass)
   int hull_doubles;
   cptr<int> moving_link;     // [n_moving]
   cptr<int> moving_geom;
@@ -71,13 +72,21 @@ MPG_INLINE SE3 load_se3(P p) {
 }
 
 // pinocchio JointModel*::calc as a plain SE3 (see oracle/collide_oracle.c)
+MPG_INLINE bool joint_is_revolute(int type) { return type <= MPG_JOINT_REVOLUTE_UNALIGNED || type >= MPG_JOINT_RUBX; }
+
+// sc: optional precomputed (mpg_sin(v), mpg_cos(v)) for revolute joints
 template <class P>
-MPG_INLINE SE3 joint_motion(int type, P axis, double v) {
+MPG_INLINE SE3 joint_motion(int type, P axis, double v, const double* sc = nullptr) {
   SE3 M;
   se3_identity(M);
-  if (type <= MPG_JOINT_REVOLUTE_UNALIGNED || type >= MPG_JOINT_RUBX) {
-    const double s = mpg_sin(v);
-    const double c = mpg_cos(v);
+  if (joint_is_revolute(type)) {
+    double s, c;
+    if (sc) {
+      s = sc[0];
+      c = sc[1];
+    } else {
+      mpg_sincos(v, &s, &c);
+    }
     const int t = (type >= MPG_JOINT_RUBX) ? type - MPG_JOINT_RUBX : type;
     if (t == 0) {
       M.R[4] = c; M.R[5] = -s; M.R[7] = s; M.R[8] = c;
@@ -123,15 +132,20 @@ MPG_HD inline void forward_kinematics(const DevWorld& w, const double* __restric
 // products, in the same order, as forward_kinematics (oMi[j] = oMi[parent] *
 // liMi[j], oMi[j] = liMi[j] when the parent is the universe), without storing
 // the other joints.
-MPG_INLINE SE3 chain_oMi(const DevWorld& w, const double* __restrict__ qrow, int l) {
+// screw: optional [dof][2] exact (sin, cos) of the row's joint values
+// (computed once per configuration by phase A), used for revolute joints
+MPG_INLINE SE3 chain_oMi(const DevWorld& w, const double* __restrict__ qrow, int l,
+                         const double* __restrict__ screw = nullptr) {
   const int cs = w.link_chain_start[l], cl = w.link_chain_len[l];
   SE3 T;
   se3_identity(T);
   for (int k = 0; k < cl; ++k) {
     const int j = w.chain_joints[cs + k];
     const int src = w.joint_q_source[j - 1];
-    const double v = src >= 0 ? qrow[src] : w.joint_q_const[j - 1];
-    const SE3 M = joint_motion(w.joint_type[j - 1], w.joint_axis + 3 * (j - 1), v);
+    const int type = w.joint_type[j - 1];
+    const bool pre = screw && src >= 0 && joint_is_revolute(type);
+    const double v = pre ? 0.0 : src >= 0 ? qrow[src] : w.joint_q_const[j - 1];
+    const SE3 M = joint_motion(type, w.joint_axis + 3 * (j - 1), v, pre ? screw + 2 * src : nullptr);
     const SE3 li = se3_mul(load_se3(w.joint_place + 12 * (j - 1)), M);
     T = k == 0 ? li : se3_mul(T, li);
   }

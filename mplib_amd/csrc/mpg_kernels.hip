@@ -31,6 +31,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <limits>
 #include <map>
 #include <mutex>
 #include <string>
@@ -45,6 +46,10 @@ using namespace mpg;
 namespace {
 
 constexpr double kCcdEps = DBL_EPSILON;
+// bound on |fp32 dot - fp64 dot| per unit of |dir|_1 * max|coord|: input
+// rounding (2 u32), three rounded operations (3 u32) and the fp64 dot's own
+// rounding, with 3x headroom (u32 = 2^-24)
+constexpr double kSupE = 16.0 * 5.9604644775390625e-08;
 
 thread_local std::string g_last_error;
 
@@ -89,22 +94,47 @@ __device__ __forceinline__ V3 support(const DevWorld& w, cptr<double> HV, const 
   const cptr<double> rec = w.geom_rec + G_STRIDE * geom;
   V3 v;
   if (type == MPG_GEOM_CONVEX) {
-    // Convex::findExtremeVertex: argmax dir . vertex, first maximum wins.
-    const cptr<double> P = HV + 12 * (size_t)w.geom_gstart[geom];
-    const int ng = w.geom_ng[geom];
-    double best = -DBL_MAX;
+    // Convex::findExtremeVertex: argmax dir . vertex (fp64), first maximum wins.
+    // fp32 pre-pass: best and runner-up of the fp32 dot products.  Each fp32
+    // dot is within E = kSupE * |dir|_1 * max|coord| of the fp64 one, so a
+    // best/runner-up gap > 2E proves the fp32 winner is the unique fp64
+    // argmax; otherwise (near-ties, NaN directions) the exact fp64 scan runs.
+    const int g0 = w.geom_gstart[geom], ng = w.geom_ng[geom];
+    const cptr<float> F = w.hull32 + 12 * (size_t)g0;
+    const float fx = (float)dir.x, fy = (float)dir.y, fz = (float)dir.z;
+    float b1 = -FLT_MAX, b2 = -FLT_MAX;
     int bi = 0;
     for (int g = 0; g < ng; ++g) {
-      const cptr<double> G = P + 12 * g;
-      double dd[4];
+      const cptr<float> G = F + 12 * g;
 #pragma unroll
-      for (int k = 0; k < 4; ++k) dd[k] = (dir.x * G[k] + dir.y * G[4 + k]) + dir.z * G[8 + k];
-#pragma unroll
-      for (int k = 0; k < 4; ++k)
-        if (dd[k] > best) {
-          best = dd[k];
+      for (int k = 0; k < 4; ++k) {
+        const float d = fmaf(fz, G[8 + k], fmaf(fy, G[4 + k], fx * G[k]));
+        if (d > b1) {
+          b2 = b1;
+          b1 = d;
           bi = 4 * g + k;
+        } else {
+          b2 = fmaxf(b2, d);
         }
+      }
+    }
+    const double e2 = 2.0 * kSupE * (std::fabs(dir.x) + std::fabs(dir.y) + std::fabs(dir.z)) * rec[G_VMAX];
+    const cptr<double> P = HV + 12 * (size_t)g0;
+    if (!((double)b1 - (double)b2 > e2)) {
+      double best = -DBL_MAX;
+      bi = 0;
+      for (int g = 0; g < ng; ++g) {
+        const cptr<double> G = P + 12 * g;
+        double dd[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) dd[k] = (dir.x * G[k] + dir.y * G[4 + k]) + dir.z * G[8 + k];
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          if (dd[k] > best) {
+            best = dd[k];
+            bi = 4 * g + k;
+          }
+      }
     }
     const cptr<double> B = P + 12 * (bi >> 2) + (bi & 3);
     v = v3(B[0], B[4], B[8]);
@@ -180,10 +210,11 @@ __device__ __forceinline__ SE3 link_from_pose7(const double* p7) {
 
 // Moving object -> FCL GJK object (shapeToGJK on link pose * offset).
 template <bool FROM_POSES>
-__device__ __forceinline__ GObj moving_obj(const DevWorld& w, const double* __restrict__ in, long long cfg, int id) {
+__device__ __forceinline__ GObj moving_obj(const DevWorld& w, const double* __restrict__ in,
+                                           const double* __restrict__ sc, long long cfg, int id) {
   const int l = w.moving_link[id];
   const SE3 L = FROM_POSES ? link_from_pose7(in + (cfg * w.n_links + l) * 7)
-                           : link_from_oMi(w, chain_oMi(w, in + cfg * w.dof, l), l, nullptr);
+                           : link_from_oMi(w, chain_oMi(w, in + cfg * w.dof, l, sc + cfg * w.dof * 2), l, nullptr);
   const SE3 T = se3_mul(L, load_se3(w.moving_offset + 12 * id));
   GObj o;
   o.rot = gjk_rot_from_matrix(T.R);
@@ -278,7 +309,7 @@ template <int BLOCK, bool FROM_POSES>
 __global__ __launch_bounds__(BLOCK) void cull_kernel(DevWorld w, const double* __restrict__ in, long long n,
                                                     uint8_t* __restrict__ flags, uint32_t* __restrict__ masks,
                                                     uint32_t* __restrict__ surv, float* __restrict__ rq,
-                                                    long long cap) {
+                                                    double* __restrict__ sc, long long cap) {
   extern __shared__ __attribute__((aligned(16))) float lds_f[];
   float* cen = lds_f;                                                    // [n_moving][3][BLOCK]
   float* save = cen + (size_t)w.n_moving * 3 * BLOCK;                    // [n_saves][12][BLOCK]
@@ -316,6 +347,18 @@ __global__ __launch_bounds__(BLOCK) void cull_kernel(DevWorld w, const double* _
     for (int m = 0; m < w.n_moving; ++m) put(m, bp_from_pose7(w.bp, in + (c * w.n_links + w.moving_link[m]) * 7, m));
   } else {
     bp_fk(w.bp, in + c * w.dof, save + tid, BLOCK, put);
+    // exact fp64 sin/cos of every revolute move-group joint, once per
+    // configuration, for the narrow phase's chain FK (same values as the
+    // glibc sincos restatement it would otherwise run per candidate)
+    if (live)
+      for (int j = 0; j < w.nj; ++j) {
+        const int src = w.joint_q_source[j];
+        if (src < 0 || !joint_is_revolute(w.joint_type[j])) continue;
+        double sv, cv;
+        mpg_sincos(in[cfg * w.dof + src], &sv, &cv);
+        sc[(cfg * w.dof + src) * 2] = sv;
+        sc[(cfg * w.dof + src) * 2 + 1] = cv;
+      }
   }
   if (w.debug_mode == 1) {
     if (live && cen[tid] == 12345.f) flags[cfg] = 2;  // keep the records alive
@@ -481,7 +524,7 @@ __global__ __launch_bounds__(256) void narrow_kernel(DevWorld w, const double* _
                                                     const uint32_t* __restrict__ prefix,
                                                     const uint32_t* __restrict__ cand,
                                                     uint8_t* __restrict__ flags, uint32_t* __restrict__ masks,
-                                                    uint32_t* __restrict__ task_ctr) {
+                                                    uint32_t* __restrict__ task_ctr, const double* __restrict__ sc) {
   // hull reads are wave-uniform: scalar loads through the constant cache
   // (staging the hulls in LDS measured slower: +60 VGPRs, occupancy 4 -> 3)
   const cptr<double> HV = w.hull;
@@ -515,6 +558,9 @@ __global__ __launch_bounds__(256) void narrow_kernel(DevWorld w, const double* _
     for (;;) {
       const unsigned long long idle = __ballot(st == MPR_DONE);
       const uint32_t n_idle = (uint32_t)__popcll(idle);
+#ifdef MPG_STATS
+      const unsigned long long c0 = __builtin_amdgcn_s_memtime();
+#endif
       if (next < t1 && (n_idle >= MPG_REFILL || n_idle == 64)) {  // batched refill
         if (st == MPR_DONE) {
           const uint32_t rank =
@@ -522,8 +568,8 @@ __global__ __launch_bounds__(256) void narrow_kernel(DevWorld w, const double* _
           const uint32_t idx = next + rank;
           if (idx < t1) {
             cfg = cl[idx];
-            if (am) A = moving_obj<FROM_POSES>(w, in, cfg, a);
-            if (bm) B = moving_obj<FROM_POSES>(w, in, cfg, b);
+            if (am) A = moving_obj<FROM_POSES>(w, in, sc, cfg, a);
+            if (bm) B = moving_obj<FROM_POSES>(w, in, sc, cfg, b);
             // findOrigin; discoverPortal's v0 and first direction
             v0 = vsub(center(w, A), center(w, B));
             if (vec_is_origin(v0)) v0 = vadd(v0, mpg::v3(kCcdEps * 10.0, 0.0, 0.0));
@@ -533,12 +579,27 @@ __global__ __launch_bounds__(256) void narrow_kernel(DevWorld w, const double* _
         }
         next = min(t1, next + n_idle);
       }
+#ifdef MPG_STATS
+      const unsigned long long c1 = __builtin_amdgcn_s_memtime();
+      const unsigned long long n_act = (unsigned long long)__popcll(__ballot(st != MPR_DONE));
+      if (w.stats && lane_id() == 0) {
+        atomicAdd(&w.stats[3], c1 - c0);
+        atomicAdd(&w.stats[6], n_act);
+        atomicAdd(&w.stats[7], 1ull);
+      }
+#endif
       if (__ballot(st != MPR_DONE) == 0) {
         if (next >= t1) break;
         continue;
       }
+#ifdef MPG_STATS
+      unsigned long long c2 = 0;
+#endif
       if (st != MPR_DONE) {
         const V3 s = msupport(w, HV, A, B, dir);
+#ifdef MPG_STATS
+        c2 = __builtin_amdgcn_s_memtime();
+#endif
         int res = 0;  // 1 = intersect, -1 = separated
         if (st == MPR_V1) {
           v1 = s;
@@ -632,6 +693,21 @@ __global__ __launch_bounds__(256) void narrow_kernel(DevWorld w, const double* _
           st = MPR_DONE;
         }
       }
+#ifdef MPG_STATS
+      {
+        const unsigned long long c3 = __builtin_amdgcn_s_memtime();
+        unsigned long long c2m = c2 ? c2 : ~0ull;  // earliest support end over the active lanes
+        for (int off = 32; off > 0; off >>= 1) {
+          const unsigned long long o = ((unsigned long long)__shfl_xor((unsigned)(c2m >> 32), off) << 32) |
+                                       (unsigned)__shfl_xor((unsigned)c2m, off);
+          c2m = o < c2m ? o : c2m;
+        }
+        if (w.stats && lane_id() == 0 && c2m != ~0ull) {
+          atomicAdd(&w.stats[4], c2m - c1);
+          atomicAdd(&w.stats[5], c3 - c2m);
+        }
+      }
+#endif
     }
   }
 }
@@ -647,8 +723,7 @@ __global__ void fk_kernel(DevWorld w, const double* __restrict__ q, long long n,
 __global__ void sincos_kernel(const double* __restrict__ x, long long n, double* s, double* c) {
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  s[i] = mpg_sin(x[i]);
-  c[i] = mpg_cos(x[i]);
+  mpg_sincos(x[i], s + i, c + i);
 }
 
 }  // namespace
@@ -680,6 +755,7 @@ struct mpg_world {
     uint32_t* prefix = nullptr;     // [n_pairs + 2] task prefix + task counter
     uint32_t* cand = nullptr;       // [n_pairs * cap] worst case
     float* rq = nullptr;            // [n_moving * 4 * cap] phase-A rotations for the SAT stage
+    double* sc = nullptr;           // [cap * dof * 2] exact joint (sin, cos) for phase B
     long long cap = 0;
   };
   std::mutex ws_mu;
@@ -836,6 +912,12 @@ void geom_record(const mpg_world_desc* d, int g, double* rec) {
     }
   }
   rec[G_RADIUS] = std::sqrt(r2) * (1.0 + 1e-12) + 1e-12;
+  double vmax = 0.0;
+  if (t == MPG_GEOM_CONVEX) {
+    const double* V = d->vertices + 3 * (size_t)d->geom_vertex_start[g];
+    for (int i = 0; i < 3 * d->geom_vertex_count[g]; ++i) vmax = std::max(vmax, std::fabs(V[i]));
+  }
+  rec[G_VMAX] = vmax;
 }
 
 void static_record(const mpg_world_desc* d, int s, const double* geom_rec_all, double* rec) {
@@ -885,6 +967,7 @@ int get_workspace(mpg_world* w, hipStream_t s, long long want, mpg_world::Worksp
     for (uint32_t* p : {ws.surv, ws.cnt, ws.seg_len, ws.seg_start, ws.prefix, ws.cand})
       if (p) HIP_TRY(hipFree(p));
     if (ws.rq) HIP_TRY(hipFree(ws.rq));
+    if (ws.sc) HIP_TRY(hipFree(ws.sc));
     ws = mpg_world::Workspace{};
     const long long tiles = (want + 63) / 64;
     HIP_TRY(hipMalloc(&ws.surv, sizeof(uint32_t) * w->dw.W * want));
@@ -894,6 +977,7 @@ int get_workspace(mpg_world* w, hipStream_t s, long long want, mpg_world::Worksp
     HIP_TRY(hipMalloc(&ws.prefix, sizeof(uint32_t) * (np + 2)));
     HIP_TRY(hipMalloc(&ws.cand, sizeof(uint32_t) * np * want));
     HIP_TRY(hipMalloc(&ws.rq, sizeof(float) * 4 * std::max(w->dw.n_moving, 1) * want));
+    HIP_TRY(hipMalloc(&ws.sc, sizeof(double) * 2 * std::max(w->dw.dof, 1) * want));
     ws.cap = want;
   }
   *out = &ws;
@@ -954,15 +1038,15 @@ int launch_collide(mpg_world* w, const double* in, long long n, uint8_t* flags, 
     switch (w->block) {
       case 256:
         hipLaunchKernelGGL((cull_kernel<256, FROM_POSES>), dim3(grid), dim3(256), w->lds_bytes, stream, w->dw, qin,
-                           m, fl, mk, ws->surv, ws->rq, ws->cap);
+                           m, fl, mk, ws->surv, ws->rq, ws->sc, ws->cap);
         break;
       case 128:
         hipLaunchKernelGGL((cull_kernel<128, FROM_POSES>), dim3(grid), dim3(128), w->lds_bytes, stream, w->dw, qin,
-                           m, fl, mk, ws->surv, ws->rq, ws->cap);
+                           m, fl, mk, ws->surv, ws->rq, ws->sc, ws->cap);
         break;
       default:
         hipLaunchKernelGGL((cull_kernel<64, FROM_POSES>), dim3(grid), dim3(64), w->lds_bytes, stream, w->dw, qin, m,
-                           fl, mk, ws->surv, ws->rq, ws->cap);
+                           fl, mk, ws->surv, ws->rq, ws->sc, ws->cap);
         break;
     }
     HIP_TRY(hipGetLastError());
@@ -990,7 +1074,7 @@ int launch_collide(mpg_world* w, const double* in, long long n, uint8_t* flags, 
     const long long want_waves = (m * std::max(w->dw.n_pairs, 1) + kTask - 1) / kTask;
     const unsigned nb = (unsigned)std::max<long long>(1, std::min<long long>(w->narrow_blocks, (want_waves + 3) / 4));
     hipLaunchKernelGGL((narrow_kernel<FROM_POSES>), dim3(nb), dim3(256), 0, stream, w->dw, qin, ws->seg_len,
-                       ws->seg_start, ws->prefix, ws->cand, fl, mk, ws->prefix + w->dw.n_pairs + 1);
+                       ws->seg_start, ws->prefix, ws->cand, fl, mk, ws->prefix + w->dw.n_pairs + 1, ws->sc);
     HIP_TRY(hipGetLastError());
   }
   return MPG_OK;
@@ -1111,6 +1195,7 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
   // hulls in AoSoA-4 groups, padded with copies of the hull's first vertex
   std::vector<int> gstart(std::max(d->n_geoms, 1), 0), ngroups(std::max(d->n_geoms, 1), 0);
   std::vector<double> hull;
+  std::vector<float> hull32;
   for (int g = 0; g < d->n_geoms; ++g) {
     if (d->geom_type[g] != MPG_GEOM_CONVEX) continue;
     const double* V = d->vertices + 3 * (size_t)d->geom_vertex_start[g];
@@ -1122,9 +1207,13 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
         for (int l = 0; l < 4; ++l) {
           const int i = 4 * q + l < nv ? 4 * q + l : 0;
           hull.push_back(V[3 * i + k]);
+          hull32.push_back(4 * q + l < nv ? (float)V[3 * i + k] : std::numeric_limits<float>::quiet_NaN());
         }
   }
-  if (hull.empty()) hull.assign(12, 0.0);
+  if (hull.empty()) {
+    hull.assign(12, 0.0);
+    hull32.assign(12, 0.f);
+  }
   // per link: joints from the root to link_parent (chain FK in phase B)
   std::vector<int> chain_start, chain_len, chain_joints;
   for (int l = 0; l < d->n_links; ++l) {
@@ -1171,6 +1260,7 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
   const size_t o_gnv = bb.add(ngroups.data(), ngroups.size());
   const size_t o_grec = bb.add(geom_rec.data(), geom_rec.size());
   const size_t o_v = bb.add(hull.data(), hull.size());
+  const size_t o_v32 = bb.add(hull32.data(), hull32.size());
   const size_t o_ml = bb.add(d->moving_link, d->n_moving);
   const size_t o_mg = bb.add(d->moving_geom, d->n_moving);
   const size_t o_mo = bb.add(d->moving_offset, 12 * (size_t)d->n_moving);
@@ -1245,6 +1335,7 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
   dw.geom_rec = to_cptr<double>(base + o_grec);
   dw.hull = to_cptr<double>(base + o_v);
   dw.hull_doubles = (int)hull.size();
+  dw.hull32 = to_cptr<float>(base + o_v32);
   dw.moving_link = to_cptr<int>(base + o_ml);
   dw.moving_geom = to_cptr<int>(base + o_mg);
   dw.moving_offset = to_cptr<double>(base + o_mo);
@@ -1303,8 +1394,10 @@ int mpg_world_destroy(mpg_world* w) {
     unsigned long long st[8];
     hipDeviceSynchronize();
     hipMemcpy(st, w->dw.stats, sizeof(st), hipMemcpyDeviceToHost);
-    std::fprintf(stderr, "[mpg stats] narrow candidates %llu, support calls %llu (%.2f/cand), hits %llu\n", st[0],
-                 st[1], st[0] ? (double)st[1] / st[0] : 0.0, st[2]);
+    std::fprintf(stderr,
+                 "[mpg stats] narrow: refill %llu, support %llu, update %llu (memtime ticks, summed over waves); "
+                 "steps %llu, mean active lanes/step %.1f\n",
+                 st[3], st[4], st[5], st[7], st[7] ? (double)st[6] / st[7] : 0.0);
     hipFree(w->dw.stats);
   }
   hipFree(w->blob);
@@ -1324,6 +1417,7 @@ int mpg_world_destroy(mpg_world* w) {
                         kv.second.cand})
       hipFree(p);
     hipFree(kv.second.rq);
+    hipFree(kv.second.sc);
   }
   delete w;
   return MPG_OK;

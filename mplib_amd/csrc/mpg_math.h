@@ -203,6 +203,81 @@ MPG_INLINE double mpg_cos(double x) {
   return x - x + NAN;
 }
 
+// do_sin / do_cos with the table index clamped and do_sin's Taylor branch
+// turned into a select, so they can run on arguments of an unselected case
+// (the result is discarded) without divergence or out-of-range reads.
+MPG_INLINE double do_sin_sel(double x, double dx) {
+  using namespace sc;
+  const double xold = x;
+  const double rt = taylor_sin<false>(x * x, x, dx);
+  if (x <= 0) dx = -dx;
+  const double u = big + std::fabs(x);
+  x = std::fabs(x) - (u - big);
+  const double xx = x * x;
+  const double s = x + mpg_fma<false>(x * xx, mpg_fma<false>(xx, sn5, sn3), dx);
+  const double c = mpg_fma<false>(x, dx, xx * mpg_fma<false>(xx, mpg_fma<false>(xx, cs6, cs4), cs2));
+  int k = lo_word(u) << 2;
+  k = k < 0 ? 0 : k > 436 ? 436 : k;
+  const double sn = kSinCosTab[k], ssn = kSinCosTab[k + 1], cs = kSinCosTab[k + 2], ccs = kSinCosTab[k + 3];
+  const double cor = mpg_fma<false>(cs, s, mpg_fma<false>(-sn, c, mpg_fma<false>(s, ccs, ssn)));
+  return std::fabs(xold) < 0.126 ? rt : std::copysign(sn + cor, xold);
+}
+
+MPG_INLINE double do_cos_sel(double x, double dx) {
+  using namespace sc;
+  if (x < 0) dx = -dx;
+  const double u = big + std::fabs(x);
+  x = std::fabs(x) - (u - big) + dx;
+  const double xx = x * x;
+  const double s = mpg_fma<false>(x * xx, mpg_fma<false>(xx, sn5, sn3), x);
+  const double c = xx * mpg_fma<false>(xx, mpg_fma<false>(xx, cs6, cs4), cs2);
+  int k = lo_word(u) << 2;
+  k = k < 0 ? 0 : k > 436 ? 436 : k;
+  const double sn = kSinCosTab[k], ssn = kSinCosTab[k + 1], cs = kSinCosTab[k + 2], ccs = kSinCosTab[k + 3];
+  const double cor = mpg_fma<false>(-sn, s, mpg_fma<false>(-cs, c, mpg_fma<false>(-s, ssn, ccs)));
+  return cs + cor;
+}
+
+// glibc __sincos (generic build) with its case analysis turned into selects.
+// Every case of __sin/__cos (s_sin.c) ends in exactly one do_sin-kernel and
+// one do_cos-kernel evaluation for the pair, so both run once, on selected
+// arguments, and the outputs are picked/negated per case.  Bit-identical to
+// mpg_sin<false>/mpg_cos<false> (tests/test_sincos.py), without the per-lane
+// branch divergence of calling them separately.
+MPG_INLINE void mpg_sincos(double x, double* s_out, double* c_out) {
+  using namespace sc;
+  const uint32_t k = hi_word(x) & 0x7fffffffu;
+  const double ax = std::fabs(x);
+  const bool c1 = k < 0x3feb6000u, c2 = !c1 && k < 0x400368fdu, c3 = !c1 && !c2 && k < 0x419921FBu;
+  // case 2: sin = copysign(do_cos(t2, hp1), x); cos = do_sin(a2, da2)
+  const double t2 = hp0 - ax;
+  const double a2 = t2 + hp1;
+  const double da2 = (t2 - a2) + hp1;
+  // case 3: argument reduction
+  double a3, da3;
+  const int n = reduce_sincos<false>(c3 ? x : 0.0, &a3, &da3);
+  const double sa = c1 ? x : c2 ? a2 : a3, sda = c1 ? 0.0 : c2 ? da2 : da3;
+  const double ca = c1 ? x : c2 ? t2 : a3, cda = c1 ? 0.0 : c2 ? hp1 : da3;
+  const double rs = do_sin_sel(sa, sda);
+  const double rc = do_cos_sel(ca, cda);
+  double sv, cv;
+  if (c1) {
+    sv = k < 0x3e500000u ? x : rs;
+    cv = k < 0x3e400000u ? 1.0 : rc;
+  } else if (c2) {
+    sv = std::copysign(rc, x);
+    cv = rs;
+  } else if (c3) {
+    const double rsin = (n & 1) ? rc : rs, rcos = (n & 1) ? rs : rc;
+    sv = (n & 2) ? -rsin : rsin;
+    cv = ((n + 1) & 2) ? -rcos : rcos;
+  } else {
+    sv = cv = x - x + NAN;
+  }
+  *s_out = sv;
+  *c_out = cv;
+}
+
 // --------------------------------------------------------------------------
 // SE(3) as R[9] (row-major) + p[3]
 // --------------------------------------------------------------------------

@@ -49,7 +49,8 @@ int host_bp_objects(int nj, const int* jt, const int* jp, const int* jqs, const 
 }
 void host_sincos(const double* x, long n, double* s, double* c, int fma) {
   for (long i = 0; i < n; ++i) {
-    if (fma) { s[i] = mpg::mpg_sin<true>(x[i]); c[i] = mpg::mpg_cos<true>(x[i]); }
+    if (fma == 1) { s[i] = mpg::mpg_sin<true>(x[i]); c[i] = mpg::mpg_cos<true>(x[i]); }
+    else if (fma == 2) mpg::mpg_sincos(x[i], s + i, c + i);
     else { s[i] = mpg::mpg_sin<false>(x[i]); c[i] = mpg::mpg_cos<false>(x[i]); }
   }
 }
