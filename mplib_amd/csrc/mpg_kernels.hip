@@ -555,6 +555,9 @@ __global__ __launch_bounds__(256) void narrow_kernel(DevWorld w, const double* _
     if (!am) A = static_obj(w, a - w.n_moving);
     if (!bm) B = static_obj(w, b - w.n_moving);
     V3 v0, v1, v2, v3, dir;
+#ifdef MPG_STATS
+    int nsteps = 0;
+#endif
     for (;;) {
       const unsigned long long idle = __ballot(st == MPR_DONE);
       const uint32_t n_idle = (uint32_t)__popcll(idle);
@@ -575,6 +578,9 @@ __global__ __launch_bounds__(256) void narrow_kernel(DevWorld w, const double* _
             if (vec_is_origin(v0)) v0 = vadd(v0, mpg::v3(kCcdEps * 10.0, 0.0, 0.0));
             dir = vnormalize(vscale(v0, -1.0));
             st = MPR_V1;
+#ifdef MPG_STATS
+            nsteps = 0;
+#endif
           }
         }
         next = min(t1, next + n_idle);
@@ -597,6 +603,9 @@ __global__ __launch_bounds__(256) void narrow_kernel(DevWorld w, const double* _
 #endif
       if (st != MPR_DONE) {
         const V3 s = msupport(w, HV, A, B, dir);
+#ifdef MPG_STATS
+        ++nsteps;
+#endif
 #ifdef MPG_STATS
         c2 = __builtin_amdgcn_s_memtime();
 #endif
@@ -691,6 +700,12 @@ __global__ __launch_bounds__(256) void narrow_kernel(DevWorld w, const double* _
             flags[cfg] = 1;
           }
           st = MPR_DONE;
+#ifdef MPG_STATS
+          if (w.stats) {
+            atomicAdd(&w.stats[res > 0 ? 0 : 1], (unsigned long long)nsteps);
+            atomicAdd(&w.stats[res > 0 ? 2 : 8], 1ull);
+          }
+#endif
         }
       }
 #ifdef MPG_STATS
@@ -1318,8 +1333,8 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
   dw.debug_mode = std::getenv("MPG_DEBUG_CULL") ? std::atoi(std::getenv("MPG_DEBUG_CULL")) : 0;
   dw.stats = nullptr;
   if (std::getenv("MPG_STATS") && std::atoi(std::getenv("MPG_STATS")) > 0) {
-    HIP_TRY(hipMalloc(&dw.stats, 8 * sizeof(unsigned long long)));
-    HIP_TRY(hipMemset(dw.stats, 0, 8 * sizeof(unsigned long long)));
+    HIP_TRY(hipMalloc(&dw.stats, 10 * sizeof(unsigned long long)));
+    HIP_TRY(hipMemset(dw.stats, 0, 10 * sizeof(unsigned long long)));
   }
   dw.joint_type = to_cptr<int>(base + o_jt);
   dw.joint_parent = to_cptr<int>(base + o_jp);
@@ -1391,13 +1406,14 @@ int mpg_world_destroy(mpg_world* w) {
   if (!w) return MPG_OK;
   hipSetDevice(w->device);
   if (w->dw.stats) {
-    unsigned long long st[8];
+    unsigned long long st[10];
     hipDeviceSynchronize();
     hipMemcpy(st, w->dw.stats, sizeof(st), hipMemcpyDeviceToHost);
     std::fprintf(stderr,
                  "[mpg stats] narrow: refill %llu, support %llu, update %llu (memtime ticks, summed over waves); "
-                 "steps %llu, mean active lanes/step %.1f\n",
-                 st[3], st[4], st[5], st[7], st[7] ? (double)st[6] / st[7] : 0.0);
+                 "steps %llu, mean active lanes/step %.1f; hits %llu (%.2f supports each), misses %llu (%.2f)\n",
+                 st[3], st[4], st[5], st[7], st[7] ? (double)st[6] / st[7] : 0.0, st[2],
+                 st[2] ? (double)st[0] / st[2] : 0.0, st[8], st[8] ? (double)st[1] / st[8] : 0.0);
     hipFree(w->dw.stats);
   }
   hipFree(w->blob);
