@@ -1,0 +1,57 @@
+"""CPU: configuration sharding + gather over torch.distributed (gloo,
+world_size 2, 127.0.0.1), the same code path bench.py / multi-GPU callers use
+with RCCL.  The per-rank compute is the CPU oracle here (no GPU in this
+container); on the GPU box it is PlanningWorld.collide_batch."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+from mplib_amd.dist import shard_range
+
+
+def test_shard_range_covers_exactly():
+    for n in (0, 1, 7, 64, 1001):
+        for world in (1, 2, 3, 8):
+            spans = [shard_range(n, r, world) for r in range(world)]
+            assert sum(c for _, c in spans) == n
+            assert all(spans[i][0] + spans[i][1] == spans[i + 1][0] for i in range(world - 1))
+            assert max(c for _, c in spans) - min(c for _, c in spans) <= 1
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q, out_dir):
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    import torch.distributed as dist
+    import worlds as Wd
+    from mplib_amd.dist import collide_sharded
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    ow = Wd.oracle_world(3)
+    f, m, (s, c) = collide_sharded(lambda x: ow.collide_batch(x, nthreads=1), q)
+    np.savez(os.path.join(out_dir, f"r{rank}.npz"), flags=f, masks=m, start=s, count=c)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_collide_sharded_gloo_world2(tmp_path):
+    mp = pytest.importorskip("torch.multiprocessing")
+    import worlds as Wd
+    ow = Wd.oracle_world(3)
+    q = Wd.sample_q(ow.art, 1001, 31)  # odd size: ragged shards
+    mp.start_processes(_worker, args=(2, _free_port(), q, str(tmp_path)), nprocs=2, join=True, start_method="spawn")
+    fo, mo = ow.collide_batch(q, nthreads=4)
+    for r in range(2):
+        d = np.load(tmp_path / f"r{r}.npz")
+        np.testing.assert_array_equal(d["flags"], fo)
+        np.testing.assert_array_equal(d["masks"], mo)
+    assert int(np.load(tmp_path / "r0.npz")["count"]) == 501
