@@ -178,6 +178,24 @@ int mpg_collide_batch(mpg_world *world, const double *q, int64_t n, uint8_t *fla
 int mpg_collide_link_poses(mpg_world *world, const double *link_pose, int64_t n, uint8_t *flags,
                            uint32_t *pair_mask, int mem, void *stream);
 
+/*
+ * Batched motion validation: for each edge e, OMPL's
+ * DiscreteMotionValidator::checkMotion(q_from[e], q_to[e]) over MPlib's state
+ * space (src/ompl_planner.cpp:248-293: one RealVectorStateSpace(1) per
+ * prismatic/revolute joint, SO2StateSpace for continuous joints, weights 1):
+ *   segments[e] = max(1, ceil(distance / longest_valid_segment)),
+ *   states q(j/segments), j = 1..segments (the last is q_to itself; q_from is
+ *   assumed valid, as OMPL does), each checked with collide().
+ *   valid[e] = 1 if every state is collision-free;
+ *   first_invalid[e] = smallest colliding j, or -1 (checkMotion's lastValid).
+ * so2_mask: bit i set if move-group dof i is an SO2 subspace.  first_invalid
+ * and segments may be NULL.  Synchronises `stream` once (the state count
+ * sizes the work).
+ */
+int mpg_check_motion_batch(mpg_world *world, const double *q_from, const double *q_to, int64_t n,
+                           uint32_t so2_mask, double longest_valid_segment, uint8_t *valid,
+                           int32_t *first_invalid, int32_t *segments, int mem, void *stream);
+
 /* link_pose: [n*n_links*7] = getLinkPose(l) -> (px, py, pz, qw, qx, qy, qz). */
 int mpg_fk_batch(mpg_world *world, const double *q, int64_t n, double *link_pose, int mem,
                  void *stream);

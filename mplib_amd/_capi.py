@@ -60,6 +60,9 @@ SIGNATURES = {
                                          ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]),
     "mpg_collide_link_poses": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p,
                                               ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]),
+    "mpg_check_motion_batch": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
+                                              ctypes.c_uint32, ctypes.c_double, ctypes.c_void_p, ctypes.c_void_p,
+                                              ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]),
     "mpg_fk_batch": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p,
                                     ctypes.c_int, ctypes.c_void_p]),
     "mpg_profile_enable": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),

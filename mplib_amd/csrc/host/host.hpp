@@ -508,6 +508,15 @@ class PlanningWorld {
   void collide_batch_device(const void* q, int64_t n, void* flags, void* masks, void* stream);
   int mask_words();
   mpg_world* device_world();  // rebuilds the snapshot if the world changed
+  // batched OMPL motion validation over the planner's state space
+  // (src/ompl_planner.cpp:248-293): SO2 dofs and the space's maximum extent
+  struct MotionSpace {
+    uint32_t so2_mask = 0;
+    double max_extent = 0.0;
+  };
+  MotionSpace motion_space();
+  void check_motion_batch(const double* from, const double* to, int64_t n, double longest_valid_segment,
+                          uint8_t* valid, int32_t* first_invalid, int32_t* segments);
   void profile_enable(bool on);
   struct StageTime { double ms; int64_t launches, units; };
   std::vector<StageTime> profile_read();  // per MPG_STAGE_*

@@ -500,6 +500,39 @@ PYBIND11_MODULE(pymp, m_all) {
            py::arg("states_ptr"), py::arg("n"), py::arg("flags_ptr"), py::arg("masks_ptr") = 0,
            py::arg("stream") = 0,
            "Enqueue the batched check on device buffers (float64 [n, dim], uint8 [n], uint32 [n, W]).")
+      .def("check_motion_batch",
+           [](PW& w, py::array_t<double, py::array::c_style | py::array::forcecast> q_from,
+              py::array_t<double, py::array::c_style | py::array::forcecast> q_to, double fraction, double lvs) {
+             const int dim = w.state_dim();
+             if (q_from.ndim() != 2 || q_from.shape(1) != dim || q_to.ndim() != 2 || q_to.shape(1) != dim ||
+                 q_to.shape(0) != q_from.shape(0))
+               throw std::invalid_argument("q_from / q_to must both be [N, " + std::to_string(dim) + "] float64");
+             if (lvs <= 0.0) lvs = fraction * w.motion_space().max_extent;
+             const int64_t n = q_from.shape(0);
+             py::array_t<bool> valid(n);
+             py::array_t<int32_t> first(n), segs(n);
+             const double* a = q_from.data();
+             const double* b = q_to.data();
+             uint8_t* v = reinterpret_cast<uint8_t*>(valid.mutable_data());
+             int32_t* f = first.mutable_data();
+             int32_t* sg = segs.mutable_data();
+             {
+               py::gil_scoped_release rel;
+               w.check_motion_batch(a, b, n, lvs, v, f, sg);
+             }
+             return py::make_tuple(valid, first, segs);
+           },
+           py::arg("q_from"), py::arg("q_to"), py::arg("longest_valid_segment_fraction") = 0.01,
+           py::arg("longest_valid_segment") = 0.0,
+           "Batched OMPL DiscreteMotionValidator::checkMotion over the planner's state space: returns (valid[N], "
+           "first_invalid[N] (1-based state index along the edge, -1 if valid), segments[N]). The longest valid "
+           "segment defaults to fraction * the space's maximum extent, as OMPL's SpaceInformation does.")
+      .def("get_motion_space",
+           [](PW& w) {
+             auto ms = w.motion_space();
+             return py::make_tuple(ms.so2_mask, ms.max_extent);
+           },
+           "(so2_mask, maximum_extent) of the planner state space (src/ompl_planner.cpp:248-293).")
       .def("profile_enable", &PW::profile_enable, py::arg("enable") = true,
            "Record HIP events around each device stage of the batched check (diagnostics).")
       .def("profile_read",

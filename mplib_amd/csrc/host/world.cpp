@@ -582,6 +582,37 @@ void PlanningWorld::collide_batch_device(const void* q, int64_t n, void* flags, 
                "mpg_collide_batch");
 }
 
+PlanningWorld::MotionSpace PlanningWorld::motion_space() {
+  MotionSpace ms;
+  int slot = 0;
+  for (auto& kv : planned_) {  // std::map: the state layout of setQposAll
+    const auto& pin = kv.second->get_pinocchio_model();
+    for (size_t id : kv.second->get_move_group_joint_indices()) {
+      const PinJoint& pj = pin->joints()[pin->user_joints().at(id)];
+      if (pj.type >= MPG_JOINT_RUBX) {  // continuous joint: SO2StateSpace, extent pi
+        if (slot < 32) ms.so2_mask |= 1u << slot;
+        ms.max_extent += 1.0 * M_PI;
+        slot += 1;
+      } else {  // RealVectorStateSpace(nq), extent = |high - low|
+        double e2 = 0.0;
+        for (int k = 0; k < pj.nq; ++k) e2 += (pj.upper[k] - pj.lower[k]) * (pj.upper[k] - pj.lower[k]);
+        ms.max_extent += 1.0 * std::sqrt(e2);
+        slot += pj.nq;
+      }
+    }
+  }
+  return ms;
+}
+
+void PlanningWorld::check_motion_batch(const double* from, const double* to, int64_t n, double lvs, uint8_t* valid,
+                                       int32_t* first_invalid, int32_t* segments) {
+  ensure_snapshot(CollisionRequest());
+  const MotionSpace ms = motion_space();
+  check_status(mpg_check_motion_batch(world_->get(), from, to, n, ms.so2_mask, lvs, valid, first_invalid, segments,
+                                      MPG_MEM_HOST, nullptr),
+               "mpg_check_motion_batch");
+}
+
 void PlanningWorld::profile_enable(bool on) { check_status(mpg_profile_enable(device_world(), on ? 1 : 0), "mpg_profile_enable"); }
 std::vector<PlanningWorld::StageTime> PlanningWorld::profile_read() {
   double ms[MPG_NUM_STAGES];

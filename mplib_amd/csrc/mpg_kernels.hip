@@ -735,6 +735,89 @@ __global__ void fk_kernel(DevWorld w, const double* __restrict__ q, long long n,
   for (int l = 0; l < w.n_links; ++l) link_transform(w, st, l, out + (cfg * w.n_links + l) * 7);
 }
 
+// ---------------------------------------------------------------------------
+// Batched motion validation (OMPL DiscreteMotionValidator over the MPlib
+// compound state space, src/ompl_planner.cpp:248-293): per edge the segment
+// count, the interpolated states, then the per-edge reduction of their flags.
+// ---------------------------------------------------------------------------
+// ompl::base::SO2StateSpace::distance / RealVectorStateSpace(1)::distance,
+// summed with weight 1.0 by CompoundStateSpace::distance
+__device__ __forceinline__ double motion_distance(const double* a, const double* b, int dof, uint32_t so2) {
+  double d = 0.0;
+  for (int i = 0; i < dof; ++i) {
+    double di;
+    if ((so2 >> i) & 1u) {
+      di = std::fabs(a[i] - b[i]);
+      di = (di > M_PI) ? 2.0 * M_PI - di : di;
+    } else {
+      const double diff = a[i] - b[i];
+      di = std::sqrt(diff * diff);
+    }
+    d += 1.0 * di;
+  }
+  return d;
+}
+
+__global__ void motion_count_kernel(const double* __restrict__ from, const double* __restrict__ to, long long n,
+                                    int dof, uint32_t so2, double lvs, int32_t* __restrict__ segs) {
+  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  // StateSpace::validSegmentCount: factor 1 * (unsigned)ceil(distance / longestValidSegment)
+  const unsigned nd = (unsigned)std::ceil(motion_distance(from + e * dof, to + e * dof, dof, so2) / lvs);
+  segs[e] = (int32_t)(nd > 1u ? nd : 1u);  // states j/nd, j = 1..nd (s1 is assumed valid)
+}
+
+__global__ void motion_states_kernel(const double* __restrict__ from, const double* __restrict__ to, long long n,
+                                     int dof, uint32_t so2, const int32_t* __restrict__ segs,
+                                     const long long* __restrict__ offs, double* __restrict__ states) {
+  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  const double* a = from + e * dof;
+  const double* b = to + e * dof;
+  const int m = segs[e];
+  double* out = states + offs[e] * dof;
+  for (int j = 1; j <= m; ++j, out += dof) {
+    if (j == m) {  // checkMotion tests s2 itself
+      for (int i = 0; i < dof; ++i) out[i] = b[i];
+      continue;
+    }
+    const double t = (double)j / (double)m;
+    for (int i = 0; i < dof; ++i) {
+      if ((so2 >> i) & 1u) {  // SO2StateSpace::interpolate
+        double diff = b[i] - a[i];
+        double v;
+        if (std::fabs(diff) <= M_PI) {
+          v = a[i] + diff * t;
+        } else {
+          diff = diff > 0.0 ? 2.0 * M_PI - diff : -2.0 * M_PI - diff;
+          v = a[i] - diff * t;
+          if (v > M_PI) v -= 2.0 * M_PI;
+          else if (v < -M_PI) v += 2.0 * M_PI;
+        }
+        out[i] = v;
+      } else {  // RealVectorStateSpace::interpolate
+        out[i] = a[i] + (b[i] - a[i]) * t;
+      }
+    }
+  }
+}
+
+__global__ void motion_reduce_kernel(const uint8_t* __restrict__ flags, long long n, const int32_t* __restrict__ segs,
+                                     const long long* __restrict__ offs, uint8_t* __restrict__ valid,
+                                     int32_t* __restrict__ first_invalid) {
+  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  const uint8_t* f = flags + offs[e];
+  int bad = -1;
+  for (int j = 0; j < segs[e]; ++j)
+    if (f[j]) {
+      bad = j + 1;
+      break;
+    }
+  valid[e] = bad < 0 ? 1 : 0;
+  if (first_invalid) first_invalid[e] = bad;
+}
+
 __global__ void sincos_kernel(const double* __restrict__ x, long long n, double* s, double* c) {
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -780,6 +863,22 @@ struct mpg_world {
     int stage;
     hipEvent_t a, b;
   };
+  // batched motion validation buffers (grow-only)
+  struct Motion {
+    double* edges = nullptr;
+    size_t edges_cap = 0;
+    int32_t* segs = nullptr;
+    size_t segs_cap = 0;
+    long long* offs = nullptr;
+    size_t offs_cap = 0;
+    int32_t* out = nullptr;  // staging: first_invalid[n] then valid[n] bytes
+    size_t out_cap = 0;
+    double* states = nullptr;
+    size_t states_cap = 0;
+    uint8_t* flags = nullptr;
+    size_t flags_cap = 0;
+  } motion;
+  std::mutex motion_mu;
   std::mutex prof_mu;
   bool prof = false;
   std::vector<Mark> marks;
@@ -1426,6 +1525,12 @@ int mpg_world_destroy(mpg_world* w) {
     hipEventDestroy(mk.b);
   }
   for (hipEvent_t e : w->ev_pool) hipEventDestroy(e);
+  hipFree(w->motion.edges);
+  hipFree(w->motion.segs);
+  hipFree(w->motion.offs);
+  hipFree(w->motion.out);
+  hipFree(w->motion.states);
+  hipFree(w->motion.flags);
   hipFree(w->prof_units);
   for (auto& kv : w->ws)
   {
@@ -1491,6 +1596,81 @@ int mpg_collide_batch(mpg_world* w, const double* q, int64_t n, uint8_t* flags, 
 int mpg_collide_link_poses(mpg_world* w, const double* link_pose, int64_t n, uint8_t* flags, uint32_t* pair_mask,
                            int mem, void* stream) {
   return collide_common<true>(w, link_pose, n, flags, pair_mask, mem, stream);
+}
+
+int mpg_check_motion_batch(mpg_world* w, const double* q_from, const double* q_to, int64_t n, uint32_t so2_mask,
+                           double longest_valid_segment, uint8_t* valid, int32_t* first_invalid, int32_t* segments,
+                           int mem, void* stream) {
+  if (!w) return set_error(MPG_E_INVALID, "world is NULL");
+  if (n < 0) return set_error(MPG_E_INVALID, "n < 0");
+  if (n > 0 && (!q_from || !q_to || !valid)) return set_error(MPG_E_INVALID, "from/to/valid is NULL");
+  if (!(longest_valid_segment > 0.0)) return set_error(MPG_E_INVALID, "longest_valid_segment must be > 0");
+  if (mem != MPG_MEM_HOST && mem != MPG_MEM_DEVICE) return set_error(MPG_E_INVALID, "bad mem kind");
+  if (w->dw.dof > 32) return set_error(MPG_E_UNSUPPORTED, "motion validation supports dof <= 32");
+  if (n == 0) return MPG_OK;
+  HIP_TRY(hipSetDevice(w->device));
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  std::lock_guard<std::mutex> lk(w->motion_mu);
+  const int dof = w->dw.dof;
+  const size_t eb = sizeof(double) * (size_t)n * dof;
+  auto grow = [&](void** p, size_t& cap, size_t want) -> int {
+    if (cap >= want) return MPG_OK;
+    if (*p) HIP_TRY(hipFree(*p));
+    *p = nullptr;
+    HIP_TRY(hipMalloc(p, want));
+    cap = want;
+    return MPG_OK;
+  };
+  auto& M = w->motion;
+  int rc;
+  if ((rc = grow((void**)&M.edges, M.edges_cap, 2 * eb))) return rc;
+  if ((rc = grow((void**)&M.segs, M.segs_cap, sizeof(int32_t) * n))) return rc;
+  if ((rc = grow((void**)&M.offs, M.offs_cap, sizeof(long long) * n))) return rc;
+  if ((rc = grow((void**)&M.out, M.out_cap, (sizeof(int32_t) + 1) * n))) return rc;
+  const double* from = q_from;
+  const double* to = q_to;
+  if (mem == MPG_MEM_HOST) {
+    HIP_TRY(hipMemcpyAsync(M.edges, q_from, eb, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(M.edges + (size_t)n * dof, q_to, eb, hipMemcpyHostToDevice, s));
+    from = M.edges;
+    to = M.edges + (size_t)n * dof;
+  }
+  const unsigned grid = (unsigned)((n + 255) / 256);
+  hipLaunchKernelGGL(motion_count_kernel, dim3(grid), dim3(256), 0, s, from, to, (long long)n, dof, so2_mask,
+                     longest_valid_segment, M.segs);
+  HIP_TRY(hipGetLastError());
+  // the state count decides the allocation: one synchronisation per call
+  std::vector<int32_t> segs((size_t)n);
+  HIP_TRY(hipMemcpyAsync(segs.data(), M.segs, sizeof(int32_t) * n, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  std::vector<long long> offs((size_t)n);
+  long long total = 0;
+  for (int64_t e = 0; e < n; ++e) {
+    offs[e] = total;
+    total += segs[e];
+  }
+  HIP_TRY(hipMemcpyAsync(M.offs, offs.data(), sizeof(long long) * n, hipMemcpyHostToDevice, s));
+  if ((rc = grow((void**)&M.states, M.states_cap, sizeof(double) * (size_t)total * dof))) return rc;
+  if ((rc = grow((void**)&M.flags, M.flags_cap, (size_t)total))) return rc;
+  hipLaunchKernelGGL(motion_states_kernel, dim3(grid), dim3(256), 0, s, from, to, (long long)n, dof, so2_mask, M.segs,
+                     M.offs, M.states);
+  HIP_TRY(hipGetLastError());
+  rc = launch_collide<false>(w, M.states, total, M.flags, nullptr, s);
+  if (rc) return rc;
+  uint8_t* d_valid = mem == MPG_MEM_DEVICE ? valid : reinterpret_cast<uint8_t*>(M.out + n);
+  int32_t* d_first = first_invalid ? (mem == MPG_MEM_DEVICE ? first_invalid : M.out) : nullptr;
+  hipLaunchKernelGGL(motion_reduce_kernel, dim3(grid), dim3(256), 0, s, M.flags, (long long)n, M.segs, M.offs, d_valid,
+                     d_first);
+  HIP_TRY(hipGetLastError());
+  if (mem == MPG_MEM_HOST) {
+    HIP_TRY(hipMemcpyAsync(valid, d_valid, n, hipMemcpyDeviceToHost, s));
+    if (first_invalid) HIP_TRY(hipMemcpyAsync(first_invalid, d_first, sizeof(int32_t) * n, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    if (segments) std::memcpy(segments, segs.data(), sizeof(int32_t) * n);
+  } else if (segments) {
+    HIP_TRY(hipMemcpyAsync(segments, M.segs, sizeof(int32_t) * n, hipMemcpyDeviceToDevice, s));
+  }
+  return MPG_OK;
 }
 
 int mpg_fk_batch(mpg_world* w, const double* q, int64_t n, double* link_pose, int mem, void* stream) {

@@ -218,3 +218,52 @@ def test_fcl_collide_free_function():
         assert r == bool(ref)
         hits += r
     assert 0 < hits < 200
+
+
+# ------------------------------------------------------- batched motion validation
+def _motion_reference(q_from, q_to, lvs, ow_):
+    """OMPL DiscreteMotionValidator semantics restated in numpy (RealVector
+    subspaces, weights 1) + the CPU oracle for every generated state."""
+    segs, states, owner = [], [], []
+    for e in range(len(q_from)):
+        a, b = q_from[e], q_to[e]
+        d = 0.0
+        for i in range(len(a)):
+            diff = a[i] - b[i]
+            d += 1.0 * float(np.sqrt(diff * diff))
+        m = max(1, int(np.ceil(d / lvs)))
+        segs.append(m)
+        for j in range(1, m + 1):
+            states.append(b.copy() if j == m else a + (b - a) * (j / m))
+            owner.append(e)
+    flags, _ = ow_.collide_batch(np.array(states), nthreads=NTHREADS)
+    valid = np.ones(len(q_from), bool)
+    first = np.full(len(q_from), -1, np.int32)
+    owner = np.array(owner)
+    pos = 0
+    for e, m in enumerate(segs):
+        f = flags[pos:pos + m]
+        if f.any():
+            valid[e] = False
+            first[e] = int(np.argmax(f)) + 1
+        pos += m
+    return valid, first, np.array(segs, np.int32)
+
+
+def test_check_motion_batch_matches_oracle():
+    w, art = scenes.world(3)
+    rng = np.random.default_rng(17)
+    n = 600
+    q_from = scenes.sample_states(art, n, 71)
+    q_to = q_from + rng.normal(scale=rng.choice([0.02, 0.3, 1.0], size=(n, 1)), size=(n, 7))
+    lim = scenes.joint_limits(art)
+    q_to = np.clip(q_to, lim[:, 0], lim[:, 1])
+    q_to[:5] = q_from[:5]  # zero-length edges: only q_to is checked
+    so2, extent = w.get_motion_space()
+    assert so2 == 0 and abs(extent - float(np.sum(lim[:, 1] - lim[:, 0]))) < 1e-12
+    valid, first, segs = w.check_motion_batch(q_from, q_to)
+    rv, rf, rs = _motion_reference(q_from, q_to, 0.01 * extent, ow(3))
+    np.testing.assert_array_equal(segs, rs)
+    np.testing.assert_array_equal(valid, rv)
+    np.testing.assert_array_equal(first, rf)
+    assert 0 < valid.sum() < n
