@@ -35,6 +35,7 @@ struct DevWorld {
   cptr<int> geom_type;       // [n_geoms]
   cptr<int> geom_gstart;     // [n_geoms] first 4-vertex group in `hull`
   cptr<int> geom_ng;         // [n_geoms] number of groups
+  cptr<int> geom_nvert;      // [n_geoms] convex vertex count
   cptr<double> geom_rec;     // [n_geoms*G_STRIDE]
   cptr<double> hull;         // AoSoA-4 vertex groups: x0..3 y0..3 z0..3
   cptr<float> hull32;        // the same groups in fp32, padding = NaN (support pre-pass)

@@ -46,6 +46,7 @@ using namespace mpg;
 namespace {
 
 constexpr double kCcdEps = DBL_EPSILON;
+typedef float f2 __attribute__((ext_vector_type(2)));
 // bound on |fp32 dot - fp64 dot| per unit of |dir|_1 * max|coord|: input
 // rounding (2 u32), three rounded operations (3 u32) and the fp64 dot's own
 // rounding, with 3x headroom (u32 = 2^-24)
@@ -99,24 +100,33 @@ __device__ __forceinline__ V3 support(const DevWorld& w, cptr<double> HV, const 
     // dot is within E = kSupE * |dir|_1 * max|coord| of the fp64 one, so a
     // best/runner-up gap > 2E proves the fp32 winner is the unique fp64
     // argmax; otherwise (near-ties, NaN directions) the exact fp64 scan runs.
-    const int g0 = w.geom_gstart[geom], ng = w.geom_ng[geom];
+    const int g0 = w.geom_gstart[geom], ng = w.geom_ng[geom], nv = w.geom_nvert[geom];
     const cptr<float> F = w.hull32 + 12 * (size_t)g0;
     const float fx = (float)dir.x, fy = (float)dir.y, fz = (float)dir.z;
+    const f2 X = {fx, fx}, Y = {fy, fy}, Z = {fz, fz};
     float b1 = -FLT_MAX, b2 = -FLT_MAX;
     int bi = 0;
-    for (int g = 0; g < ng; ++g) {
+    // b2 <= b1 always: med3(b1, d, b2) is the new runner-up
+    auto upd = [&](float d, int idx) {
+      const bool gt = d > b1;
+      bi = gt ? idx : bi;
+      b2 = __builtin_amdgcn_fmed3f(b1, d, b2);
+      b1 = gt ? d : b1;
+    };
+    const int nfull = nv >> 2;
+#pragma unroll 2
+    for (int g = 0; g < nfull; ++g) {
       const cptr<float> G = F + 12 * g;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const float d = fmaf(fz, G[8 + k], fmaf(fy, G[4 + k], fx * G[k]));
-        if (d > b1) {
-          b2 = b1;
-          b1 = d;
-          bi = 4 * g + k;
-        } else {
-          b2 = fmaxf(b2, d);
-        }
-      }
+      const f2 d01 = __builtin_elementwise_fma(Z, f2{G[8], G[9]}, __builtin_elementwise_fma(Y, f2{G[4], G[5]}, X * f2{G[0], G[1]}));
+      const f2 d23 = __builtin_elementwise_fma(Z, f2{G[10], G[11]}, __builtin_elementwise_fma(Y, f2{G[6], G[7]}, X * f2{G[2], G[3]}));
+      upd(d01.x, 4 * g);
+      upd(d01.y, 4 * g + 1);
+      upd(d23.x, 4 * g + 2);
+      upd(d23.y, 4 * g + 3);
+    }
+    for (int k = 0; k < (nv & 3); ++k) {  // partial last group (uniform trip count)
+      const cptr<float> G = F + 12 * nfull;
+      upd(fmaf(fz, G[8 + k], fmaf(fy, G[4 + k], fx * G[k])), 4 * nfull + k);
     }
     const double e2 = 2.0 * kSupE * (std::fabs(dir.x) + std::fabs(dir.y) + std::fabs(dir.z)) * rec[G_VMAX];
     const cptr<double> P = HV + 12 * (size_t)g0;
@@ -1372,6 +1382,9 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
   const size_t o_gt = bb.add(d->geom_type, d->n_geoms);
   const size_t o_gvs = bb.add(gstart.data(), gstart.size());
   const size_t o_gnv = bb.add(ngroups.data(), ngroups.size());
+  std::vector<int> nvert(std::max(d->n_geoms, 1), 0);
+  for (int g = 0; g < d->n_geoms; ++g) nvert[g] = d->geom_type[g] == MPG_GEOM_CONVEX ? d->geom_vertex_count[g] : 0;
+  const size_t o_gnvt = bb.add(nvert.data(), nvert.size());
   const size_t o_grec = bb.add(geom_rec.data(), geom_rec.size());
   const size_t o_v = bb.add(hull.data(), hull.size());
   const size_t o_v32 = bb.add(hull32.data(), hull32.size());
@@ -1446,6 +1459,7 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
   dw.geom_type = to_cptr<int>(base + o_gt);
   dw.geom_gstart = to_cptr<int>(base + o_gvs);
   dw.geom_ng = to_cptr<int>(base + o_gnv);
+  dw.geom_nvert = to_cptr<int>(base + o_gnvt);
   dw.geom_rec = to_cptr<double>(base + o_grec);
   dw.hull = to_cptr<double>(base + o_v);
   dw.hull_doubles = (int)hull.size();
