@@ -620,71 +620,19 @@ __global__ __launch_bounds__(256) void narrow_kernel(DevWorld w, const double* _
         c2 = __builtin_amdgcn_s_memtime();
 #endif
         int res = 0;  // 1 = intersect, -1 = separated
-        if (st == MPR_V1) {
-          v1 = s;
-          const double dot = vdot(v1, dir);
-          if (is_zero(dot) || dot < 0.0) {
-            res = -1;
-          } else {
-            dir = vcross(v0, v1);
-            if (is_zero(vdot(dir, dir))) {
-              res = 1;  // origin on v1 or on segment v0-v1
-            } else {
-              dir = vnormalize(dir);
-              st = MPR_V2;
-            }
-          }
-        } else if (st == MPR_V2) {
-          v2 = s;
-          const double dot = vdot(v2, dir);
-          if (is_zero(dot) || dot < 0.0) {
-            res = -1;
-          } else {
-            dir = vnormalize(vcross(vsub(v1, v0), vsub(v2, v0)));
-            if (vdot(dir, v0) > 0.0) {
-              const V3 t = v1;
-              v1 = v2;
-              v2 = t;
-              dir = vscale(dir, -1.0);
-            }
-            st = MPR_V3;
-          }
-        } else if (st == MPR_V3) {
-          v3 = s;
-          const double dot = vdot(v3, dir);
-          if (is_zero(dot) || dot < 0.0) {
-            res = -1;
-          } else {
-            bool cont = false;
-            double d2 = vdot(vcross(v1, v3), v0);
-            if (d2 < 0.0 && !is_zero(d2)) {
-              v2 = v3;
-              cont = true;
-            }
-            if (!cont) {
-              d2 = vdot(vcross(v3, v2), v0);
-              if (d2 < 0.0 && !is_zero(d2)) {
-                v1 = v3;
-                cont = true;
-              }
-            }
-            if (cont) {
-              dir = vnormalize(vcross(vsub(v1, v0), vsub(v2, v0)));
-            } else {  // portal found: refinePortal with (v1, v2, v3)
-              dir = vnormalize(vcross(vsub(v2, v1), vsub(v3, v1)));
-              const double d = vdot(dir, v1);
-              if (is_zero(d) || d > 0.0) res = 1;
-              else st = MPR_V4;
-            }
-          }
-        } else {  // MPR_V4: expand the portal (v1, v2, v3) towards v4
-          const double dv4 = vdot(s, dir);
-          if (!(is_zero(dv4) || dv4 > 0.0)) {
+        // Every state ends in one new search direction dir = normalize(a x b);
+        // the states only pick (a, b), so the costly normalize (sqrt + divide)
+        // runs once per step for all lanes instead of once per state branch.
+        const double dsd = vdot(s, dir);
+        V3 ca, cb;
+        bool post_swap = false, post_encl = false;
+        if (st == MPR_V4) {  // refinePortal: expand the portal (v1, v2, v3) towards v4 = s
+          if (!(is_zero(dsd) || dsd > 0.0)) {
             res = -1;
           } else {
             const double dv1 = vdot(v1, dir), dv2 = vdot(v2, dir), dv3 = vdot(v3, dir);
-            double d1 = dv4 - dv1;
-            const double dd2 = dv4 - dv2, dd3 = dv4 - dv3;
+            double d1 = dsd - dv1;
+            const double dd2 = dsd - dv2, dd3 = dsd - dv3;
             d1 = (d1 < dd2) ? d1 : dd2;  // CCD_FMIN
             d1 = (d1 < dd3) ? d1 : dd3;
             if (ccd_eq(d1, w.mpr_tol) || d1 < w.mpr_tol) {
@@ -698,7 +646,64 @@ __global__ __launch_bounds__(256) void narrow_kernel(DevWorld w, const double* _
                 if (vdot(v3, v4v0) > 0.0) v2 = s;
                 else v1 = s;
               }
-              dir = vnormalize(vcross(vsub(v2, v1), vsub(v3, v1)));
+              ca = vsub(v2, v1);
+              cb = vsub(v3, v1);
+              post_encl = true;
+            }
+          }
+        } else if (is_zero(dsd) || dsd < 0.0) {  // discoverPortal: support not past the origin
+          res = -1;
+        } else if (st == MPR_V1) {
+          v1 = s;
+          ca = v0;
+          cb = v1;
+        } else if (st == MPR_V2) {
+          v2 = s;
+          ca = vsub(v1, v0);
+          cb = vsub(v2, v0);
+          post_swap = true;
+        } else {  // MPR_V3
+          v3 = s;
+          bool cont = false;
+          double d2 = vdot(vcross(v1, v3), v0);
+          if (d2 < 0.0 && !is_zero(d2)) {
+            v2 = v3;
+            cont = true;
+          }
+          if (!cont) {
+            d2 = vdot(vcross(v3, v2), v0);
+            if (d2 < 0.0 && !is_zero(d2)) {
+              v1 = v3;
+              cont = true;
+            }
+          }
+          if (cont) {
+            ca = vsub(v1, v0);
+            cb = vsub(v2, v0);
+          } else {  // portal found: refinePortal starts with (v1, v2, v3)
+            ca = vsub(v2, v1);
+            cb = vsub(v3, v1);
+            post_encl = true;
+            st = MPR_V4;
+          }
+        }
+        if (res == 0) {
+          const V3 cr = vcross(ca, cb);
+          if (st == MPR_V1 && is_zero(vdot(cr, cr))) {
+            res = 1;  // origin on v1 or on segment v0-v1
+          } else {
+            dir = vnormalize(cr);
+            if (st == MPR_V1) {
+              st = MPR_V2;
+            } else if (post_swap) {
+              if (vdot(dir, v0) > 0.0) {
+                const V3 t = v1;
+                v1 = v2;
+                v2 = t;
+                dir = vscale(dir, -1.0);
+              }
+              st = MPR_V3;
+            } else if (post_encl) {  // portalEncapsulesOrigin
               const double d = vdot(dir, v1);
               if (is_zero(d) || d > 0.0) res = 1;
             }
