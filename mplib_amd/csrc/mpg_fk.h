@@ -48,6 +48,8 @@ struct DevWorld {
   cptr<int> pair_a;          // [n_pairs]
   cptr<int> pair_b;
   cptr<int> pair_allowed;
+  cptr<int> pair_cf;          // [n_pairs] CF_* closed-form kind (0 = MPR)
+  cptr<double> static_T;      // [n_static*12] world transforms as given
   // per user link: the joints from the root to link_parent[l] (1-based,
   // root first) -- lets a thread rebuild one link's oMi without the others
   cptr<int> link_chain_start;  // [n_links]

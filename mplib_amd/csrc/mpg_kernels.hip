@@ -219,13 +219,22 @@ __device__ __forceinline__ SE3 link_from_pose7(const double* p7) {
 }
 
 // Moving object -> FCL GJK object (shapeToGJK on link pose * offset).
+// world transform of moving object `id` (link pose * collision origin) -- the
+// Isometry FCLModel::updateCollisionObjects hands to setTransform
 template <bool FROM_POSES>
-__device__ __forceinline__ GObj moving_obj(const DevWorld& w, const double* __restrict__ in,
-                                           const double* __restrict__ sc, long long cfg, int id) {
+__device__ __forceinline__ SE3 moving_tf(const DevWorld& w, const double* __restrict__ in,
+                                         const double* __restrict__ sc, long long cfg, int id) {
   const int l = w.moving_link[id];
   const SE3 L = FROM_POSES ? link_from_pose7(in + (cfg * w.n_links + l) * 7)
                            : link_from_oMi(w, chain_oMi(w, in + cfg * w.dof, l, sc + cfg * w.dof * 2), l, nullptr);
-  const SE3 T = se3_mul(L, load_se3(w.moving_offset + 12 * id));
+  return se3_mul(L, load_se3(w.moving_offset + 12 * id));
+}
+
+// Moving object -> FCL GJK object (shapeToGJK on link pose * offset).
+template <bool FROM_POSES>
+__device__ __forceinline__ GObj moving_obj(const DevWorld& w, const double* __restrict__ in,
+                                           const double* __restrict__ sc, long long cfg, int id) {
+  const SE3 T = moving_tf<FROM_POSES>(w, in, sc, cfg, id);
   GObj o;
   o.rot = gjk_rot_from_matrix(T.R);
   o.rot_inv = quat_invert2(o.rot);
@@ -233,6 +242,141 @@ __device__ __forceinline__ GObj moving_obj(const DevWorld& w, const double* __re
   o.geom = w.moving_geom[id];
   o.type = w.geom_type[o.geom];
   return o;
+}
+
+// ---------------------------------------------------------------------------
+// FCL 0.7.0 closed-form shape pairs (GJKSolver_libccd::shapeIntersect
+// specialisations, both argument orders), boolean part; same operation order
+// as the oracle (oracle/collide_oracle.c box_box_intersect & co.)
+// ---------------------------------------------------------------------------
+enum : int { CF_NONE = 0, CF_BOX_BOX = 1, CF_SPHERE_SPHERE = 2, CF_SPHERE_BOX = 3, CF_BOX_SPHERE = 4 };
+
+// detail::boxBox2 (box_box-inl.h, from ODE dBoxBox): return_code != 0
+__device__ __forceinline__ bool box_box_intersect(const double* side1, const SE3& T1, const double* side2,
+                                                  const SE3& T2) {
+  const double p[3] = {T2.p[0] - T1.p[0], T2.p[1] - T1.p[1], T2.p[2] - T1.p[2]};
+  double pp[3], A[3], B[3], R[3][3], Q[3][3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) pp[i] = (T1.R[i] * p[0] + T1.R[3 + i] * p[1]) + T1.R[6 + i] * p[2];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    A[i] = side1[i] * 0.5;
+    B[i] = side2[i] * 0.5;
+  }
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      R[i][j] = (T1.R[i] * T2.R[j] + T1.R[3 + i] * T2.R[3 + j]) + T1.R[6 + i] * T2.R[6 + j];
+      Q[i][j] = std::fabs(R[i][j]);
+    }
+  double s = -DBL_MAX, s2, tmp;
+  int code = 0;
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {  // axes u1, u2, u3
+    tmp = pp[i];
+    s2 = std::fabs(tmp) - (((Q[i][0] * B[0] + Q[i][1] * B[1]) + Q[i][2] * B[2]) + A[i]);
+    if (s2 > 0) return false;
+    if (s2 > s) {
+      s = s2;
+      code = 1 + i;
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {  // axes v1, v2, v3
+    tmp = (T2.R[j] * p[0] + T2.R[3 + j] * p[1]) + T2.R[6 + j] * p[2];
+    s2 = std::fabs(tmp) - (((Q[0][j] * A[0] + Q[1][j] * A[1]) + Q[2][j] * A[2]) + B[j]);
+    if (s2 > 0) return false;
+    if (s2 > s) {
+      s = s2;
+      code = 4 + j;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) Q[i][j] += 1.0e-6;  // ODE's edge-axis tolerance
+  const double eps = DBL_EPSILON, fudge = 1.05;
+  auto edge = [&](double t, double rad, double n0, double n1, double n2, int c) -> bool {
+    const double e2 = std::fabs(t) - rad;
+    if (e2 > eps) return true;
+    const double l = std::sqrt((n0 * n0 + n1 * n1) + n2 * n2);
+    if (l > eps) {
+      const double e3 = e2 / l;
+      if (e3 * fudge > s) {
+        s = e3;
+        code = c;
+      }
+    }
+    return false;
+  };
+  // u1 x (v1, v2, v3)
+  if (edge(pp[2] * R[1][0] - pp[1] * R[2][0], ((A[1] * Q[2][0] + A[2] * Q[1][0]) + B[1] * Q[0][2]) + B[2] * Q[0][1], 0,
+           -R[2][0], R[1][0], 7)) return false;
+  if (edge(pp[2] * R[1][1] - pp[1] * R[2][1], ((A[1] * Q[2][1] + A[2] * Q[1][1]) + B[0] * Q[0][2]) + B[2] * Q[0][0], 0,
+           -R[2][1], R[1][1], 8)) return false;
+  if (edge(pp[2] * R[1][2] - pp[1] * R[2][2], ((A[1] * Q[2][2] + A[2] * Q[1][2]) + B[0] * Q[0][1]) + B[1] * Q[0][0], 0,
+           -R[2][2], R[1][2], 9)) return false;
+  // u2 x (v1, v2, v3)
+  if (edge(pp[0] * R[2][0] - pp[2] * R[0][0], ((A[0] * Q[2][0] + A[2] * Q[0][0]) + B[1] * Q[1][2]) + B[2] * Q[1][1],
+           R[2][0], 0, -R[0][0], 10)) return false;
+  if (edge(pp[0] * R[2][1] - pp[2] * R[0][1], ((A[0] * Q[2][1] + A[2] * Q[0][1]) + B[0] * Q[1][2]) + B[2] * Q[1][0],
+           R[2][1], 0, -R[0][1], 11)) return false;
+  if (edge(pp[0] * R[2][2] - pp[2] * R[0][2], ((A[0] * Q[2][2] + A[2] * Q[0][2]) + B[0] * Q[1][1]) + B[1] * Q[1][0],
+           R[2][2], 0, -R[0][2], 12)) return false;
+  // u3 x (v1, v2, v3)
+  if (edge(pp[1] * R[0][0] - pp[0] * R[1][0], ((A[0] * Q[1][0] + A[1] * Q[0][0]) + B[1] * Q[2][2]) + B[2] * Q[2][1],
+           -R[1][0], R[0][0], 0, 13)) return false;
+  if (edge(pp[1] * R[0][1] - pp[0] * R[1][1], ((A[0] * Q[1][1] + A[1] * Q[0][1]) + B[0] * Q[2][2]) + B[2] * Q[2][0],
+           -R[1][1], R[0][1], 0, 14)) return false;
+  if (edge(pp[1] * R[0][2] - pp[0] * R[1][2], ((A[0] * Q[1][2] + A[1] * Q[0][2]) + B[0] * Q[2][1]) + B[1] * Q[2][0],
+           -R[1][2], R[0][2], 0, 15)) return false;
+  return code != 0;
+}
+
+// detail::sphereSphereIntersect
+__device__ __forceinline__ bool sphere_sphere_intersect(double r1, const SE3& T1, double r2, const SE3& T2) {
+  const double d0 = T2.p[0] - T1.p[0], d1 = T2.p[1] - T1.p[1], d2 = T2.p[2] - T1.p[2];
+  const double len = std::sqrt((d0 * d0 + d1 * d1) + d2 * d2);
+  return !(len > r1 + r2);
+}
+
+// detail::sphereBoxIntersect: X_BS = X_FB.inverse() * X_FS, nearestPointInBox
+__device__ __forceinline__ bool sphere_box_intersect(double r, const SE3& TS, const double* side, const SE3& TB) {
+  double c[3];
+  bool clamped = false;
+  double dd = 0.0;
+  double d[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const double inv_t = -((TB.R[i] * TB.p[0] + TB.R[3 + i] * TB.p[1]) + TB.R[6 + i] * TB.p[2]);
+    c[i] = ((TB.R[i] * TS.p[0] + TB.R[3 + i] * TS.p[1]) + TB.R[6 + i] * TS.p[2]) + inv_t;
+    const double h = side[i] / 2;
+    double nq = c[i];
+    if (c[i] < -h) {
+      clamped = true;
+      nq = -h;
+    }
+    if (c[i] > h) {
+      clamped = true;
+      nq = h;
+    }
+    d[i] = c[i] - nq;
+  }
+  dd = (d[0] * d[0] + d[1] * d[1]) + d[2] * d[2];
+  return !(clamped && dd > r * r);
+}
+
+__device__ __forceinline__ bool closed_form(int kind, const DevWorld& w, int ga, const SE3& TA, int gb,
+                                            const SE3& TB) {
+  const cptr<double> pa = w.geom_rec + G_STRIDE * ga + G_PARAM, pb = w.geom_rec + G_STRIDE * gb + G_PARAM;
+  const double sa[3] = {pa[0], pa[1], pa[2]}, sb[3] = {pb[0], pb[1], pb[2]};
+  switch (kind) {
+    case CF_BOX_BOX: return box_box_intersect(sa, TA, sb, TB);
+    case CF_SPHERE_SPHERE: return sphere_sphere_intersect(sa[0], TA, sb[0], TB);
+    case CF_SPHERE_BOX: return sphere_box_intersect(sa[0], TA, sb, TB);
+    default: return sphere_box_intersect(sb[0], TB, sa, TA);  // CF_BOX_SPHERE
+  }
 }
 
 __device__ __forceinline__ GObj static_obj(const DevWorld& w, int sid) {
@@ -558,6 +702,23 @@ __global__ __launch_bounds__(256) void narrow_kernel(DevWorld w, const double* _
     const int a = w.pair_a[p], b = w.pair_b[p];
     const bool am = a < w.n_moving, bm = b < w.n_moving;
     const uint32_t bit = 1u << (p & 31);
+    const int cf = w.pair_cf[p];
+    if (cf != CF_NONE) {  // closed-form pair: one test per candidate, no MPR
+      const int ga = am ? w.moving_geom[a] : w.static_geom[a - w.n_moving];
+      const int gb = bm ? w.moving_geom[b] : w.static_geom[b - w.n_moving];
+      for (uint32_t base = t0; base < t1; base += 64) {
+        const uint32_t idx = base + lane;
+        if (idx >= t1) continue;
+        const long long c = cl[idx];
+        const SE3 TA = am ? moving_tf<FROM_POSES>(w, in, sc, c, a) : load_se3(w.static_T + 12 * (a - w.n_moving));
+        const SE3 TB = bm ? moving_tf<FROM_POSES>(w, in, sc, c, b) : load_se3(w.static_T + 12 * (b - w.n_moving));
+        if (closed_form(cf, w, ga, TA, gb, TB)) {
+          if (masks) atomicOr(&masks[c * w.W + (p >> 5)], bit);
+          flags[c] = 1;
+        }
+      }
+      continue;
+    }
     uint32_t next = t0;  // wave-uniform
     int st = MPR_DONE;
     long long cfg = 0;
@@ -925,6 +1086,20 @@ bool finite_all(const double* p, size_t n) {
   return true;
 }
 
+int obj_geom_type(const mpg_world_desc* d, int id) {
+  return d->geom_type[id < d->n_moving ? d->moving_geom[id] : d->static_geom[id - d->n_moving]];
+}
+
+// FCL closed-form pair for (o1, o2) in fcl::collide argument order
+int closed_form_kind(const mpg_world_desc* d, int a, int b) {
+  const int ta = obj_geom_type(d, a), tb = obj_geom_type(d, b);
+  if (ta == MPG_GEOM_BOX && tb == MPG_GEOM_BOX) return CF_BOX_BOX;
+  if (ta == MPG_GEOM_SPHERE && tb == MPG_GEOM_SPHERE) return CF_SPHERE_SPHERE;
+  if (ta == MPG_GEOM_SPHERE && tb == MPG_GEOM_BOX) return CF_SPHERE_BOX;
+  if (ta == MPG_GEOM_BOX && tb == MPG_GEOM_SPHERE) return CF_BOX_SPHERE;
+  return CF_NONE;
+}
+
 int validate(const mpg_world_desc* d) {
   if (!d) return set_error(MPG_E_INVALID, "desc is NULL");
   if (d->n_joints < 0 || d->n_joints > kMaxJoints) return set_error(MPG_E_INVALID, "n_joints out of range [0, 32]");
@@ -964,12 +1139,15 @@ int validate(const mpg_world_desc* d) {
     const int tb = d->geom_type[b < d->n_moving ? d->moving_geom[b] : d->static_geom[b - d->n_moving]];
     // FCL 0.7.0 GJKSolver_libccd routes these pairs to closed-form tests, not
     // MPR; they are not implemented on the device yet.
+    // box-box, sphere-sphere and sphere-box run FCL's closed forms on the
+    // device; sphere-capsule / sphere-cylinder (and capsule-capsule, whose
+    // FCL 0.7 routing is unverified here) are not implemented yet
     const bool sa = ta == MPG_GEOM_SPHERE, sb = tb == MPG_GEOM_SPHERE;
-    if ((sa && (sb || tb == MPG_GEOM_BOX || tb == MPG_GEOM_CAPSULE || tb == MPG_GEOM_CYLINDER)) ||
-        (sb && (ta == MPG_GEOM_BOX || ta == MPG_GEOM_CAPSULE || ta == MPG_GEOM_CYLINDER)) ||
-        (ta == MPG_GEOM_BOX && tb == MPG_GEOM_BOX) || (ta == MPG_GEOM_CAPSULE && tb == MPG_GEOM_CAPSULE))
+    if ((sa && (tb == MPG_GEOM_CAPSULE || tb == MPG_GEOM_CYLINDER)) ||
+        (sb && (ta == MPG_GEOM_CAPSULE || ta == MPG_GEOM_CYLINDER)) ||
+        (ta == MPG_GEOM_CAPSULE && tb == MPG_GEOM_CAPSULE))
       return set_error(MPG_E_UNSUPPORTED,
-                       "pair uses an FCL closed-form narrow phase (sphere/box/capsule specialisation) "
+                       "pair uses an FCL closed-form narrow phase (sphere-capsule/cylinder or capsule-capsule) "
                        "that is not implemented on the device");
   }
   if (!finite_all(d->joint_placement, 12 * (size_t)d->n_joints) || !finite_all(d->link_placement, 12 * (size_t)d->n_links) ||
@@ -1355,6 +1533,8 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
   }
   std::vector<int> allowed(std::max(d->n_pairs, 1), 0);
   for (int p = 0; p < d->n_pairs; ++p) allowed[p] = d->pair_allowed ? (d->pair_allowed[p] != 0) : 0;
+  std::vector<int> pair_cf(std::max(d->n_pairs, 1), 0);
+  for (int p = 0; p < d->n_pairs; ++p) pair_cf[p] = closed_form_kind(d, d->pair_a[p], d->pair_b[p]);
   // phase-A schedule: non-allowed pairs grouped by their lower moving object
   std::vector<int> sched_start(d->n_moving + 1, 0), sched_pair, sched_other;
   for (int m = 0; m < d->n_moving; ++m) {
@@ -1401,6 +1581,8 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
   const size_t o_pa = bb.add(d->pair_a, d->n_pairs);
   const size_t o_pb = bb.add(d->pair_b, d->n_pairs);
   const size_t o_al = bb.add(allowed.data(), allowed.size());
+  const size_t o_cf = bb.add(pair_cf.data(), pair_cf.size());
+  const size_t o_sT = bb.add(d->static_transform, 12 * (size_t)d->n_static);
   const size_t o_cs = bb.add(chain_start.data(), chain_start.size());
   const size_t o_cl = bb.add(chain_len.data(), chain_len.size());
   const size_t o_cj = bb.add(chain_joints.data(), chain_joints.size());
@@ -1477,6 +1659,8 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
   dw.pair_a = to_cptr<int>(base + o_pa);
   dw.pair_b = to_cptr<int>(base + o_pb);
   dw.pair_allowed = to_cptr<int>(base + o_al);
+  dw.pair_cf = to_cptr<int>(base + o_cf);
+  dw.static_T = to_cptr<double>(base + o_sT);
   dw.link_chain_start = to_cptr<int>(base + o_cs);
   dw.link_chain_len = to_cptr<int>(base + o_cl);
   dw.chain_joints = to_cptr<int>(base + o_cj);

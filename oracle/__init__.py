@@ -144,6 +144,12 @@ class OracleWorld:
                 gnv.append(0)
                 gparam += [float(g.side[0]), float(g.side[1]), float(g.side[2]), 0.0]
                 ginterior += [0.0] * 3
+            elif isinstance(g, M.SphereGeom):
+                gtype.append(M.GEOM_SPHERE)
+                gvstart.append(0)
+                gnv.append(0)
+                gparam += [float(g.radius), 0.0, 0.0, 0.0]
+                ginterior += [0.0] * 3
             else:
                 raise TypeError(f"oracle: unsupported geometry {type(g)}")
         names = [o.link for o in art.objects]

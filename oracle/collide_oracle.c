@@ -609,6 +609,124 @@ static int mpr_intersect(const gjk_obj *o1, const gjk_obj *o2, real tol) {
     return res == 0 ? 1 : 0;
 }
 
+/* ------------------------------------------------ FCL closed-form pairs
+ * GJKSolver_libccd::shapeIntersect routes these shape pairs to closed forms
+ * instead of MPR (FCL 0.7.0 gjk_solver_libccd-inl.h specialisations;
+ * both argument orders).  Boolean results only (enable_contact = false).
+ * Transforms are the collision objects' Isometries (row-major R, t). */
+
+/* detail::boxBox2 (narrowphase/detail/primitive_shape_algorithm/box_box-inl.h,
+ * derived from ODE dBoxBox): return_code != 0.  Eigen evaluation order:
+ * dot products ((a0 b0 + a1 b1) + a2 b2), sums left to right. */
+static int box_box_intersect(const real *side1, const real *T1, const real *side2, const real *T2) {
+#define R1_(i, j) T1[3 * (i) + (j)]
+#define R2_(i, j) T2[3 * (i) + (j)]
+    const real p[3] = {T2[9] - T1[9], T2[10] - T1[10], T2[11] - T1[11]};
+    real pp[3], A[3], B[3], R[3][3], Q[3][3];
+    for (int i = 0; i < 3; ++i) pp[i] = (R1_(0, i) * p[0] + R1_(1, i) * p[1]) + R1_(2, i) * p[2];
+    for (int i = 0; i < 3; ++i) { A[i] = side1[i] * 0.5; B[i] = side2[i] * 0.5; }
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) {
+            R[i][j] = (R1_(0, i) * R2_(0, j) + R1_(1, i) * R2_(1, j)) + R1_(2, i) * R2_(2, j);
+            Q[i][j] = fabs(R[i][j]);
+        }
+    real s = -DBL_MAX, s2, tmp;
+    int code = 0;
+    /* separating axis = u1, u2, u3 */
+    for (int i = 0; i < 3; ++i) {
+        tmp = pp[i];
+        s2 = fabs(tmp) - (((Q[i][0] * B[0] + Q[i][1] * B[1]) + Q[i][2] * B[2]) + A[i]);
+        if (s2 > 0) return 0;
+        if (s2 > s) { s = s2; code = 1 + i; }
+    }
+    /* separating axis = v1, v2, v3 */
+    for (int j = 0; j < 3; ++j) {
+        tmp = (R2_(0, j) * p[0] + R2_(1, j) * p[1]) + R2_(2, j) * p[2];
+        s2 = fabs(tmp) - (((Q[0][j] * A[0] + Q[1][j] * A[1]) + Q[2][j] * A[2]) + B[j]);
+        if (s2 > 0) return 0;
+        if (s2 > s) { s = s2; code = 4 + j; }
+    }
+    /* ODE's tolerance for the edge-edge axes */
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) Q[i][j] += 1.0e-6;
+    const real eps = DBL_EPSILON, fudge = 1.05;
+    real n[3], l;
+#define EDGE(TMP, S2, N0, N1, N2, CODE)                           \
+    tmp = (TMP);                                                  \
+    s2 = fabs(tmp) - (S2);                                        \
+    if (s2 > eps) return 0;                                       \
+    n[0] = (N0); n[1] = (N1); n[2] = (N2);                        \
+    l = sqrt((n[0] * n[0] + n[1] * n[1]) + n[2] * n[2]);          \
+    if (l > eps) {                                                \
+        s2 /= l;                                                  \
+        if (s2 * fudge > s) { s = s2; code = (CODE); }            \
+    }
+    /* u1 x (v1, v2, v3) */
+    EDGE(pp[2] * R[1][0] - pp[1] * R[2][0], ((A[1] * Q[2][0] + A[2] * Q[1][0]) + B[1] * Q[0][2]) + B[2] * Q[0][1],
+         0, -R[2][0], R[1][0], 7)
+    EDGE(pp[2] * R[1][1] - pp[1] * R[2][1], ((A[1] * Q[2][1] + A[2] * Q[1][1]) + B[0] * Q[0][2]) + B[2] * Q[0][0],
+         0, -R[2][1], R[1][1], 8)
+    EDGE(pp[2] * R[1][2] - pp[1] * R[2][2], ((A[1] * Q[2][2] + A[2] * Q[1][2]) + B[0] * Q[0][1]) + B[1] * Q[0][0],
+         0, -R[2][2], R[1][2], 9)
+    /* u2 x (v1, v2, v3) */
+    EDGE(pp[0] * R[2][0] - pp[2] * R[0][0], ((A[0] * Q[2][0] + A[2] * Q[0][0]) + B[1] * Q[1][2]) + B[2] * Q[1][1],
+         R[2][0], 0, -R[0][0], 10)
+    EDGE(pp[0] * R[2][1] - pp[2] * R[0][1], ((A[0] * Q[2][1] + A[2] * Q[0][1]) + B[0] * Q[1][2]) + B[2] * Q[1][0],
+         R[2][1], 0, -R[0][1], 11)
+    EDGE(pp[0] * R[2][2] - pp[2] * R[0][2], ((A[0] * Q[2][2] + A[2] * Q[0][2]) + B[0] * Q[1][1]) + B[1] * Q[1][0],
+         R[2][2], 0, -R[0][2], 12)
+    /* u3 x (v1, v2, v3) */
+    EDGE(pp[1] * R[0][0] - pp[0] * R[1][0], ((A[0] * Q[1][0] + A[1] * Q[0][0]) + B[1] * Q[2][2]) + B[2] * Q[2][1],
+         -R[1][0], R[0][0], 0, 13)
+    EDGE(pp[1] * R[0][1] - pp[0] * R[1][1], ((A[0] * Q[1][1] + A[1] * Q[0][1]) + B[0] * Q[2][2]) + B[2] * Q[2][0],
+         -R[1][1], R[0][1], 0, 14)
+    EDGE(pp[1] * R[0][2] - pp[0] * R[1][2], ((A[0] * Q[1][2] + A[1] * Q[0][2]) + B[0] * Q[2][1]) + B[1] * Q[2][0],
+         -R[1][2], R[0][2], 0, 15)
+#undef EDGE
+#undef R1_
+#undef R2_
+    return code != 0;
+}
+
+/* detail::sphereSphereIntersect (sphere_sphere-inl.h) */
+static int sphere_sphere_intersect(real r1, const real *T1, real r2, const real *T2) {
+    const real d[3] = {T2[9] - T1[9], T2[10] - T1[10], T2[11] - T1[11]};
+    const real len = sqrt((d[0] * d[0] + d[1] * d[1]) + d[2] * d[2]);
+    return !(len > r1 + r2);
+}
+
+/* detail::sphereBoxIntersect (sphere_box-inl.h): sphere centre in the box
+ * frame X_BS = X_FB.inverse() * X_FS, nearestPointInBox clamp, squared
+ * distance against r^2. */
+static int sphere_box_intersect(real r, const real *TS, const real *side, const real *TB) {
+    real inv_t[3], c[3], nq[3];
+    for (int i = 0; i < 3; ++i)  /* inverse translation: -(R^T t) */
+        inv_t[i] = -((TB[i] * TB[9] + TB[3 + i] * TB[10]) + TB[6 + i] * TB[11]);
+    for (int i = 0; i < 3; ++i)
+        c[i] = ((TB[i] * TS[9] + TB[3 + i] * TS[10]) + TB[6 + i] * TS[11]) + inv_t[i];
+    int clamped = 0;
+    for (int i = 0; i < 3; ++i) {
+        const real h = side[i] / 2;
+        nq[i] = c[i];
+        if (c[i] < -h) { clamped = 1; nq[i] = -h; }
+        if (c[i] > h) { clamped = 1; nq[i] = h; }
+    }
+    const real d[3] = {c[0] - nq[0], c[1] - nq[1], c[2] - nq[2]};
+    if (clamped && ((d[0] * d[0] + d[1] * d[1]) + d[2] * d[2]) > r * r) return 0;
+    return 1;
+}
+
+/* 1/0 for a closed-form pair, -1 when the pair goes through MPR */
+static int closed_form_intersect(const orc_world *w, int ga, const real *Ta, int gb, const real *Tb) {
+    const int ta = w->geom_type[ga], tb = w->geom_type[gb];
+    const real *pa = w->geom_param + 4 * ga, *pb = w->geom_param + 4 * gb;
+    if (ta == GEOM_BOX && tb == GEOM_BOX) return box_box_intersect(pa, Ta, pb, Tb);
+    if (ta == GEOM_SPHERE && tb == GEOM_SPHERE) return sphere_sphere_intersect(pa[0], Ta, pb[0], Tb);
+    if (ta == GEOM_SPHERE && tb == GEOM_BOX) return sphere_box_intersect(pa[0], Ta, pb, Tb);
+    if (ta == GEOM_BOX && tb == GEOM_SPHERE) return sphere_box_intersect(pb[0], Tb, pa, Ta);
+    return -1;
+}
+
 /* ------------------------------------------------------- world collide */
 static void make_obj(const orc_world *w, int geom, const real *T, gjk_obj *o, orc_stats *st) {
     memset(o, 0, sizeof *o);
@@ -649,15 +767,19 @@ static int collide_one(const orc_world *w, const real *q, uint32_t *mask, int W,
         gjk_obj a, b;
         int ks[2] = {w->pa_kind[p], w->pb_kind[p]}, is[2] = {w->pa_idx[p], w->pb_idx[p]};
         gjk_obj *objs[2] = {&a, &b};
+        const real *Ts[2];
+        int gs[2];
         for (int s = 0; s < 2; ++s) {
-            const real *T;
-            int g;
-            if (ks[s] == KIND_ROBOT) { T = obj_T + 12 * is[s]; g = w->obj_geom[is[s]]; }
-            else if (ks[s] == KIND_ATTACHED) { T = att_T + 12 * is[s]; g = w->att_geom[is[s]]; }
-            else { T = w->scene_tf + 12 * is[s]; g = w->scene_geom[is[s]]; }
-            make_obj(w, g, T, objs[s], st);
+            if (ks[s] == KIND_ROBOT) { Ts[s] = obj_T + 12 * is[s]; gs[s] = w->obj_geom[is[s]]; }
+            else if (ks[s] == KIND_ATTACHED) { Ts[s] = att_T + 12 * is[s]; gs[s] = w->att_geom[is[s]]; }
+            else { Ts[s] = w->scene_tf + 12 * is[s]; gs[s] = w->scene_geom[is[s]]; }
         }
-        if (mpr_intersect(&a, &b, 1e-6)) {
+        int hit = closed_form_intersect(w, gs[0], Ts[0], gs[1], Ts[1]);
+        if (hit < 0) {
+            for (int s = 0; s < 2; ++s) make_obj(w, gs[s], Ts[s], objs[s], st);
+            hit = mpr_intersect(&a, &b, 1e-6);
+        }
+        if (hit) {
             mask[p >> 5] |= 1u << (p & 31);
             any = 1;
         }
@@ -741,6 +863,8 @@ int orc_fk_batch(const orc_world *w, const double *q, long n, double *link_pose7
 
 /* Single-pair entry (fcl.collide(o1, o2) on two posed shapes). */
 int orc_collide_pair(const orc_world *w, int ga, const double *Ta, int gb, const double *Tb) {
+    const int cf = closed_form_intersect(w, ga, Ta, gb, Tb);
+    if (cf >= 0) return cf;
     gjk_obj a, b;
     make_obj(w, ga, Ta, &a, NULL);
     make_obj(w, gb, Tb, &b, NULL);

@@ -399,6 +399,11 @@ class BoxGeom:
     side: Tuple[float, float, float]
 
 
+@dataclass
+class SphereGeom:
+    radius: float
+
+
 def load_convex_mesh(path: str, scale=(1.0, 1.0, 1.0)) -> ConvexGeom:
     verts, tris = load_stl(path)
     arr = np.array([[v[0] * scale[0], v[1] * scale[1], v[2] * scale[2]] for v in verts], dtype=np.float64)

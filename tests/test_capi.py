@@ -59,14 +59,17 @@ def test_invalid_descriptor_rejected(field, value, msg):
 
 
 def test_unsupported_pair_rejected():
-    """Box-box uses FCL's closed-form boxBox test, not MPR: refused, never approximated."""
+    """Capsule-capsule (and sphere-capsule/cylinder) would need FCL closed forms
+    the device does not implement: refused at world creation, never
+    approximated.  Box-box / sphere-sphere / sphere-box are implemented."""
     ow = Wd.oracle_world(3)
     a = _desc(ow)
-    # make a pair between two static boxes impossible -> use moving box instead
     a["geom_type"] = list(a["geom_type"])
-    n_mov = len(a["moving_link"])
-    box_geom = a["static_geom"][0]
+    a["geom_param"] = list(a["geom_param"])
+    cap = a["static_geom"][0]
+    a["geom_type"][cap] = 3  # MPG_GEOM_CAPSULE
+    a["geom_param"][4 * cap:4 * cap + 2] = [0.05, 0.2]
     a["moving_geom"] = list(a["moving_geom"])
-    a["moving_geom"][0] = box_geom  # link0 is now a box; (link0, table) is box-box
+    a["moving_geom"][0] = cap  # link0 is now a capsule; (link0, table) is capsule-capsule
     with pytest.raises(NotImplementedError, match="closed-form"):
         _create(a)

@@ -267,3 +267,63 @@ def test_check_motion_batch_matches_oracle():
     np.testing.assert_array_equal(valid, rv)
     np.testing.assert_array_equal(first, rf)
     assert 0 < valid.sum() < n
+
+
+# ------------------------------------------ FCL closed-form pairs (attached bodies)
+def _oracle_T(pose):
+    from oracle import model as M
+    return (M.quat_to_mat(*[float(v) for v in pose[3:]]), [float(v) for v in pose[:3]])
+
+
+def test_attached_box_in_box_scene_matches_oracle():
+    """collision_avoidance.py:87-90: a box attached to the hand in the box
+    scene -> Box-Box pairs take FCL's boxBox2 closed form, Box-Convex MPR."""
+    import oracle
+    from oracle import model as M
+    w, art = scenes.world(3)
+    pose = [0.0, 0.0, 0.14, 1.0, 0.0, 0.0, 0.0]
+    w.attach_object("held", pymp.fcl.Box([0.04, 0.04, 0.12]), "panda", 8, pose, ["panda_hand"])
+    base = ow(3)
+    o2 = oracle.OracleWorld(base.art, scene=base.scene,
+                            attached=[("held", 8, M.BoxGeom((0.04, 0.04, 0.12)), _oracle_T(pose))],
+                            allowed=[("panda_hand", "held"), ("panda_link0", "table")])
+    assert [(i[3], i[4]) for i in w.get_collision_pair_info()] == o2.pair_names()
+    q = Wd.sample_q(base.art, 30000, 18)
+    f, m = w.collide_batch(q)
+    fo, mo = o2.collide_batch(q, nthreads=NTHREADS)
+    np.testing.assert_array_equal(f, fo)
+    np.testing.assert_array_equal(m, mo)
+    held = [k for k, i in enumerate(w.get_collision_pair_info()) if i[3] == "held" or i[4] == "held"]
+    box_box = [k for k in held if w.get_collision_pair_info()[k][0] != "self"]
+    hits = [(mo[:, k >> 5] >> (k & 31)) & 1 for k in box_box]
+    assert sum(int(h.sum()) for h in hits) > 0  # the closed form is exercised with both outcomes
+
+
+def test_spheres_closed_forms_match_oracle():
+    """Sphere obstacles + an attached sphere: Sphere-Sphere and Sphere-Box
+    closed forms, Sphere-Convex MPR."""
+    import oracle
+    from oracle import model as M
+    w, art = scenes.world(3)
+    rng = np.random.default_rng(55)
+    spheres = []
+    for k in range(4):
+        c = rng.uniform([0.2, -0.4, 0.1], [0.7, 0.4, 0.7])
+        r = float(rng.uniform(0.05, 0.15))
+        w.add_normal_object(f"ball{k}", pymp.fcl.CollisionObject(pymp.fcl.Sphere(r), list(c), [1, 0, 0, 0]))
+        spheres.append((f"ball{k}", M.SphereGeom(r), _oracle_T(list(c) + [1.0, 0.0, 0.0, 0.0])))
+    pose = [0.0, 0.0, 0.12, 1.0, 0.0, 0.0, 0.0]
+    w.attach_object("orb", pymp.fcl.Sphere(0.05), "panda", 8, pose, ["panda_hand"])
+    base = ow(3)
+    o2 = oracle.OracleWorld(base.art, scene=list(base.scene) + spheres,
+                            attached=[("orb", 8, M.SphereGeom(0.05), _oracle_T(pose))],
+                            allowed=[("panda_hand", "orb"), ("panda_link0", "table")])
+    assert sorted((i[3], i[4]) for i in w.get_collision_pair_info()) == sorted(o2.pair_names())
+    order = {pn: k for k, pn in enumerate(o2.pair_names())}
+    perm = [order[(i[3], i[4])] for i in w.get_collision_pair_info()]
+    q = Wd.sample_q(base.art, 30000, 19)
+    f, m = w.collide_batch(q)
+    fo, mo = o2.collide_batch(q, nthreads=NTHREADS)
+    np.testing.assert_array_equal(f, fo)
+    bits = lambda M_, P: np.stack([(M_[:, p >> 5] >> (p & 31)) & 1 for p in P], 1)
+    np.testing.assert_array_equal(bits(m, range(len(perm))), bits(mo, perm))

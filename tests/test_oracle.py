@@ -92,3 +92,61 @@ def test_assimp_atof_semantics():
     v = M.assimp_atof("-0.031705923")
     assert v == float(np.float32(v))  # a binary32 value
     assert abs(v + 0.031705923) < 1e-8
+
+
+# ------------------------------------------------ FCL closed-form primitive pairs
+def _pair_world(geoms):
+    import oracle
+    from oracle import model as M
+    base = Wd.oracle_world(2)
+    eye = (list(M.quat_to_mat(1.0, 0.0, 0.0, 0.0)), [0.0, 0.0, 0.0])
+    w = oracle.OracleWorld(base.art, scene=[(f"g{i}", g, eye) for i, g in enumerate(geoms)])
+    idx = [next(i for i, gg in enumerate(w.geoms) if gg is g) for g in geoms]
+    return w, idx
+
+
+def _T(q=(1.0, 0.0, 0.0, 0.0), p=(0.0, 0.0, 0.0)):
+    from oracle import model as M
+    return np.array(list(M.quat_to_mat(*q)) + list(p), dtype=np.float64)
+
+
+def _collide(w, ga, Ta, gb, Tb):
+    import ctypes
+    import oracle
+    P = ctypes.POINTER(ctypes.c_double)
+    return oracle.lib().orc_collide_pair(ctypes.byref(w._w), ga, Ta.ctypes.data_as(P), gb, Tb.ctypes.data_as(P))
+
+
+def test_box_box_closed_form_known_answers():
+    """FCL boxBox2 (return_code != 0): face axes separate only for s2 > 0, so
+    touching boxes intersect; edge axes use ODE's 1e-6 fudge."""
+    from oracle import model as M
+    b1, b2 = M.BoxGeom((1.0, 1.0, 1.0)), M.BoxGeom((0.5, 2.0, 0.25))
+    w, (g1, g2) = _pair_world([b1, b2])
+    assert _collide(w, g1, _T(), g2, _T(p=(0.7, 0.0, 0.0))) == 1
+    assert _collide(w, g1, _T(), g2, _T(p=(0.75, 0.0, 0.0))) == 1       # touching faces: s2 == 0
+    assert _collide(w, g1, _T(), g2, _T(p=(0.7500001, 0.0, 0.0))) == 0
+    assert _collide(w, g1, _T(), g2, _T(p=(0.0, 1.4, 0.0))) == 1
+    assert _collide(w, g1, _T(), g2, _T(p=(0.0, 0.0, 0.63))) == 0
+    c, s = np.cos(np.pi / 8), np.sin(np.pi / 8)                          # 45 deg about z
+    q45 = (c, 0.0, 0.0, s)
+    # corner of the rotated unit box reaches 0.5*sqrt(2) along x
+    assert _collide(w, g1, _T(), g1, _T(q=q45, p=(1.2, 0.0, 0.0))) == 1
+    assert _collide(w, g1, _T(), g1, _T(q=q45, p=(1.22, 0.0, 0.0))) == 0
+    assert _collide(w, g2, _T(q=q45), g1, _T(p=(0.3, 0.3, 0.3))) == 1    # argument order swapped
+
+
+def test_sphere_closed_forms_known_answers():
+    from oracle import model as M
+    sp, sp2, bx = M.SphereGeom(0.1), M.SphereGeom(0.25), M.BoxGeom((0.4, 0.2, 1.0))
+    w, (gs, gs2, gb) = _pair_world([sp, sp2, bx])
+    assert _collide(w, gs, _T(), gs2, _T(p=(0.35, 0.0, 0.0))) == 1      # len == r1 + r2 touches
+    assert _collide(w, gs, _T(), gs2, _T(p=(0.3500001, 0.0, 0.0))) == 0
+    assert _collide(w, gs, _T(p=(0.0, 0.0, 0.0)), gb, _T()) == 1        # centre inside the box
+    assert _collide(w, gs, _T(p=(0.2999, 0.0, 0.0)), gb, _T()) == 1
+    assert _collide(w, gs, _T(p=(0.3001, 0.0, 0.0)), gb, _T()) == 0
+    assert _collide(w, gb, _T(), gs, _T(p=(0.0, 0.1999, 0.0))) == 1    # box first: same test
+    corner = 0.2 + 0.1 / np.sqrt(3) * 0.999
+    assert _collide(w, gs, _T(p=(corner, 0.1 + 0.1 / np.sqrt(3) * 0.999, 0.5 + 0.1 / np.sqrt(3) * 0.999)), gb,
+                    _T()) == 1
+    assert _collide(w, gs, _T(p=(0.2 + 0.06, 0.1 + 0.06, 0.5 + 0.06)), gb, _T()) == 0
