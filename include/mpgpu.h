@@ -196,6 +196,19 @@ int mpg_check_motion_batch(mpg_world *world, const double *q_from, const double 
                            uint32_t so2_mask, double longest_valid_segment, uint8_t *valid,
                            int32_t *first_invalid, int32_t *segments, int mem, void *stream);
 
+/*
+ * Batched distance: per configuration, PlanningWorldTpl::distanceSelf and
+ * distanceOthers (src/planning_world.cpp:493-720) over the pair table, whose
+ * first n_self_pairs entries form the self group: ACM-allowed pairs are
+ * skipped, each pair's fcl::distance (DistanceRequest(): -1 when the shapes
+ * penetrate) is compared with strict '<', so the first minimum wins.
+ * d_*: minimum distance (DBL_MAX if the group is empty), p_*: its pair
+ * index (-1 if none).  Distances are within 1e-5 of FCL's GJK (GJK run to
+ * 1e-12 relative convergence on the same support mappings).
+ */
+int mpg_distance_batch(mpg_world *world, const double *q, int64_t n, int32_t n_self_pairs, double *d_self,
+                       int32_t *p_self, double *d_others, int32_t *p_others, int mem, void *stream);
+
 /* link_pose: [n*n_links*7] = getLinkPose(l) -> (px, py, pz, qw, qx, qy, qz). */
 int mpg_fk_batch(mpg_world *world, const double *q, int64_t n, double *link_pose, int mem,
                  void *stream);

@@ -109,6 +109,21 @@ struct CollisionRequest {
   void check_supported() const;
 };
 
+// fcl::DistanceRequest / DistanceResult (python/pybind_fcl.hpp:306-325)
+struct DistanceRequest {
+  bool enable_nearest_points = false;
+  bool enable_signed_distance = false;
+  double rel_err = 0.0, abs_err = 0.0, distance_tolerance = 1e-6;
+  GJKSolverType gjk_solver_type = GST_LIBCCD;
+  // the device computes the plain (unsigned, -1 on penetration) GJK distance
+  void check_supported() const;
+};
+struct DistanceResult {
+  double min_distance = std::numeric_limits<double>::max();
+  std::array<Vec3, 2> nearest_points{};
+  void clear() { min_distance = std::numeric_limits<double>::max(); }
+};
+
 struct Contact {
   std::shared_ptr<CollisionGeometry> o1, o2;
   int b1 = -1, b2 = -1;
@@ -455,6 +470,12 @@ struct WorldCollisionResult {
   std::string collision_type, object_name1, object_name2, link_name1, link_name2;
 };
 
+struct WorldDistanceResult {  // src/planning_world.h:35-41
+  DistanceResult res;
+  double min_distance = std::numeric_limits<double>::max();
+  std::string distance_type, object_name1, object_name2, link_name1, link_name2;
+};
+
 struct PairInfo {
   int a, b;  // device object ids
   std::string collision_type, object_name1, object_name2, link_name1, link_name2;
@@ -500,6 +521,17 @@ class PlanningWorld {
   std::vector<WorldCollisionResult> self_collide(const CollisionRequest& r = CollisionRequest());
   std::vector<WorldCollisionResult> collide_with_others(const CollisionRequest& r = CollisionRequest());
   std::vector<WorldCollisionResult> collide_full(const CollisionRequest& r = CollisionRequest());
+
+  // distance (src/planning_world.cpp:493-720); distance() ignores its
+  // request like the reference's (planning_world.h:271-273)
+  double distance(const DistanceRequest& r = DistanceRequest());
+  WorldDistanceResult self_distance(const DistanceRequest& r = DistanceRequest());
+  WorldDistanceResult distance_with_others(const DistanceRequest& r = DistanceRequest());
+  WorldDistanceResult distance_full(const DistanceRequest& r = DistanceRequest());
+  // per configuration: (self group, others group) minimum and pair index
+  void distance_batch(const double* q, int64_t n, double* d_self, int32_t* p_self, double* d_others,
+                      int32_t* p_others);
+  int n_self_pairs();
 
   // batch API (one launch for N configurations)
   int state_dim();

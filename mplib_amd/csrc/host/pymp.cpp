@@ -177,6 +177,32 @@ PYBIND11_MODULE(pymp, m_all) {
       .def_readonly("pos", &Contact::pos)
       .def_readonly("penetration_depth", &Contact::penetration_depth);
 
+  py::class_<DistanceRequest, std::shared_ptr<DistanceRequest>>(m, "DistanceRequest")
+      .def(py::init([](bool np_, bool sd, double rel, double abs_, double tol, GJKSolverType t) {
+             DistanceRequest r;
+             r.enable_nearest_points = np_;
+             r.enable_signed_distance = sd;
+             r.rel_err = rel;
+             r.abs_err = abs_;
+             r.distance_tolerance = tol;
+             r.gjk_solver_type = t;
+             return r;
+           }),
+           py::arg("enable_nearest_points") = false, py::arg("enable_signed_distance") = false,
+           py::arg("rel_err") = 0.0, py::arg("abs_err") = 0.0, py::arg("distance_tolerance") = 1e-6,
+           py::arg("gjk_solver_type") = GST_LIBCCD)
+      .def("isSatisfied", [](const DistanceRequest&, const DistanceResult&) { return false; }, py::arg("result"));
+  py::class_<DistanceResult, std::shared_ptr<DistanceResult>>(m, "DistanceResult")
+      .def(py::init([](double d) {
+             DistanceResult r;
+             r.min_distance = d;
+             return r;
+           }),
+           py::arg("min_distance") = std::numeric_limits<double>::max())
+      .def_readonly("nearest_points", &DistanceResult::nearest_points)
+      .def_readonly("min_distance", &DistanceResult::min_distance)
+      .def("clear", &DistanceResult::clear);
+
   py::class_<CollisionResult, std::shared_ptr<CollisionResult>>(m, "CollisionResult")
       .def(py::init<>())
       .def("is_collision", &CollisionResult::is_collision)
@@ -250,6 +276,34 @@ PYBIND11_MODULE(pymp, m_all) {
         return r;
       },
       py::arg("o1"), py::arg("o2"), py::arg("request") = CollisionRequest());
+  m.def(
+      "distance",
+      [](const ObjPtr& o1, const ObjPtr& o2, const DistanceRequest& req) {
+        // fcl::distance(o1, o2): a two-object world evaluated on the device
+        req.check_supported();
+        DescBuilder d;
+        d.link_parent.push_back(0);
+        SE3 I;
+        mpg::se3_identity(I);
+        push_se3(d.link_placement, I);
+        d.moving_link.push_back(0);
+        d.moving_geom.push_back(d.add_geometry(o1->geom.get()));
+        push_se3(d.moving_offset, o1->tf);
+        d.static_geom.push_back(d.add_geometry(o2->geom.get()));
+        push_se3(d.static_transform, o2->tf);
+        d.pair_a.push_back(0);
+        d.pair_b.push_back(1);
+        d.pair_allowed.push_back(0);
+        DeviceWorld w(d, default_device());
+        double ds = 0, dd = 0;
+        int32_t ps = -1, po = -1;
+        check_status(mpg_distance_batch(w.get(), nullptr, 1, 0, &ds, &ps, &dd, &po, MPG_MEM_HOST, nullptr),
+                     "mpg_distance_batch");
+        DistanceResult r;
+        r.min_distance = dd;
+        return r;
+      },
+      py::arg("o1"), py::arg("o2"), py::arg("request") = DistanceRequest());
 
   // ------------------------------------------------------------ pinocchio
   auto mp = m_all.def_submodule("pinocchio");
@@ -396,6 +450,15 @@ PYBIND11_MODULE(pymp, m_all) {
       .def_readwrite("object_name2", &WorldCollisionResult::object_name2)
       .def_readwrite("link_name1", &WorldCollisionResult::link_name1)
       .def_readwrite("link_name2", &WorldCollisionResult::link_name2);
+  py::class_<WorldDistanceResult, std::shared_ptr<WorldDistanceResult>>(mw, "WorldDistanceResult")
+      .def(py::init<>())
+      .def_readwrite("res", &WorldDistanceResult::res)
+      .def_readwrite("min_distance", &WorldDistanceResult::min_distance)
+      .def_readwrite("distance_type", &WorldDistanceResult::distance_type)
+      .def_readwrite("object_name1", &WorldDistanceResult::object_name1)
+      .def_readwrite("object_name2", &WorldDistanceResult::object_name2)
+      .def_readwrite("link_name1", &WorldDistanceResult::link_name1)
+      .def_readwrite("link_name2", &WorldDistanceResult::link_name2);
 
   using PW = PlanningWorld;
   py::class_<PW, std::shared_ptr<PW>>(mw, "PlanningWorld")
@@ -460,6 +523,30 @@ PYBIND11_MODULE(pymp, m_all) {
       .def("self_collide", &PW::self_collide, py::arg("request") = CollisionRequest())
       .def("collide_with_others", &PW::collide_with_others, py::arg("request") = CollisionRequest())
       .def("collide_full", &PW::collide_full, py::arg("request") = CollisionRequest())
+      .def("distance", &PW::distance, py::arg("request") = DistanceRequest())
+      .def("self_distance", &PW::self_distance, py::arg("request") = DistanceRequest())
+      .def("distance_with_others", &PW::distance_with_others, py::arg("request") = DistanceRequest())
+      .def("distance_full", &PW::distance_full, py::arg("request") = DistanceRequest())
+      .def("distance_batch",
+           [](PW& w, py::array_t<double, py::array::c_style | py::array::forcecast> states) {
+             const int dim = w.state_dim();
+             if (states.ndim() != 2 || states.shape(1) != dim)
+               throw std::invalid_argument("states must be [N, " + std::to_string(dim) + "] float64");
+             const int64_t n = states.shape(0);
+             py::array_t<double> ds(n), dot(n);
+             py::array_t<int32_t> ps(n), po(n);
+             const double* q = states.data();
+             double *a = ds.mutable_data(), *b = dot.mutable_data();
+             int32_t *c = ps.mutable_data(), *d = po.mutable_data();
+             {
+               py::gil_scoped_release rel;
+               w.distance_batch(q, n, a, c, b, d);
+             }
+             return py::make_tuple(ds, ps, dot, po);
+           },
+           py::arg("states"),
+           "Batched self_distance / distance_with_others: (d_self[N], pair_self[N], d_others[N], pair_others[N]); "
+           "-1 = a penetrating pair, pair indices into get_collision_pair_info().")
       // ---- batched validity (new; one device launch for N states) ----
       .def("get_state_dim", &PW::state_dim)
       .def("get_mask_words", &PW::mask_words)

@@ -613,6 +613,75 @@ void PlanningWorld::check_motion_batch(const double* from, const double* to, int
                "mpg_check_motion_batch");
 }
 
+void DistanceRequest::check_supported() const {
+  if (enable_signed_distance)
+    throw std::logic_error("NotImplemented: DistanceRequest(enable_signed_distance=True) is not implemented on the device");
+  if (enable_nearest_points)
+    throw std::logic_error("NotImplemented: DistanceRequest(enable_nearest_points=True) is not implemented on the device");
+  if (gjk_solver_type != GST_LIBCCD)
+    throw std::logic_error("NotImplemented: only GJKSolverType.GST_LIBCCD is implemented on the device");
+}
+
+int PlanningWorld::n_self_pairs() {
+  ensure_snapshot(CollisionRequest(), false);
+  int n = 0;
+  while (n < (int)pairs_.size() && pairs_[n].self) ++n;
+  for (size_t p = n; p < pairs_.size(); ++p)
+    if (pairs_[p].self) throw std::logic_error("pair table: self pairs must lead");
+  return n;
+}
+
+void PlanningWorld::distance_batch(const double* q, int64_t n, double* d_self, int32_t* p_self, double* d_others,
+                                   int32_t* p_others) {
+  const int ns = n_self_pairs();
+  ensure_snapshot(CollisionRequest());
+  check_status(mpg_distance_batch(world_->get(), q, n, ns, d_self, p_self, d_others, p_others, MPG_MEM_HOST, nullptr),
+               "mpg_distance_batch");
+}
+
+namespace {
+WorldDistanceResult distance_result(double d, int p, const std::vector<PairInfo>& pairs) {
+  WorldDistanceResult r;
+  if (p < 0) return r;
+  const PairInfo& pi = pairs[p];
+  r.min_distance = d;
+  r.res.min_distance = d;
+  r.distance_type = pi.collision_type;
+  r.object_name1 = pi.object_name1;
+  r.object_name2 = pi.object_name2;
+  r.link_name1 = pi.link_name1;
+  r.link_name2 = pi.link_name2;
+  return r;
+}
+}  // namespace
+
+WorldDistanceResult PlanningWorld::self_distance(const DistanceRequest& r) {
+  r.check_supported();
+  std::vector<double> s = current_state();
+  double ds, dot;
+  int32_t ps, po;
+  distance_batch(s.data(), 1, &ds, &ps, &dot, &po);
+  return distance_result(ds, ps, pairs_);
+}
+WorldDistanceResult PlanningWorld::distance_with_others(const DistanceRequest& r) {
+  r.check_supported();
+  std::vector<double> s = current_state();
+  double ds, dot;
+  int32_t ps, po;
+  distance_batch(s.data(), 1, &ds, &ps, &dot, &po);
+  return distance_result(dot, po, pairs_);
+}
+WorldDistanceResult PlanningWorld::distance_full(const DistanceRequest& r) {
+  r.check_supported();
+  std::vector<double> s = current_state();
+  double ds, dot;
+  int32_t ps, po;
+  distance_batch(s.data(), 1, &ds, &ps, &dot, &po);
+  auto r1 = distance_result(ds, ps, pairs_), r2 = distance_result(dot, po, pairs_);
+  return r1.min_distance < r2.min_distance ? r1 : r2;  // planning_world.cpp:718-719
+}
+double PlanningWorld::distance(const DistanceRequest&) { return distance_full().min_distance; }
+
 void PlanningWorld::profile_enable(bool on) { check_status(mpg_profile_enable(device_world(), on ? 1 : 0), "mpg_profile_enable"); }
 std::vector<PlanningWorld::StageTime> PlanningWorld::profile_read() {
   double ms[MPG_NUM_STAGES];

@@ -903,6 +903,269 @@ __global__ __launch_bounds__(256) void narrow_kernel(DevWorld w, const double* _
   }
 }
 
+// ---------------------------------------------------------------------------
+// Batched distance (PlanningWorld::distanceSelf / distanceOthers,
+// src/planning_world.cpp:493-720): exact fp64 object poses once per
+// configuration (pose_kernel), then per configuration every non-allowed pair
+// in order with a bounding-sphere lower bound against the running minimum,
+// GJK distance on the FCL support mappings (-1 for penetrating pairs, as
+// fcl::distance with DistanceRequest() reports), strict '<' keeps the first
+// minimum.  Same algorithm as the oracle (oracle/collide_oracle.c
+// gjk_distance); the north star's bar vs FCL's GJK is 1e-5.
+// ---------------------------------------------------------------------------
+constexpr int kPoseStride = 12;  // rot xyzw, pos xyz, world OBB centre xyz, pad
+
+template <bool FROM_POSES>
+__global__ __launch_bounds__(128) void pose_kernel(DevWorld w, const double* __restrict__ in, long long n,
+                                                   double* __restrict__ poses, double* __restrict__ save64) {
+  const long long cfg = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (cfg >= n) return;
+  auto store = [&](int m, const SE3& T) {
+    const Q4 r = gjk_rot_from_matrix(T.R);
+    double* g = poses + ((size_t)m * kPoseStride) * n + cfg;  // [m][field][cfg]
+    g[0 * n] = r.x;
+    g[1 * n] = r.y;
+    g[2 * n] = r.z;
+    g[3 * n] = r.w;
+    g[4 * n] = T.p[0];
+    g[5 * n] = T.p[1];
+    g[6 * n] = T.p[2];
+    const cptr<double> gr = w.geom_rec + G_STRIDE * w.moving_geom[m];
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+      g[(7 + i) * n] = ((T.R[3 * i] * gr[G_OBB_C] + T.R[3 * i + 1] * gr[G_OBB_C + 1]) + T.R[3 * i + 2] * gr[G_OBB_C + 2]) +
+                       T.p[i];
+  };
+  if (FROM_POSES) {
+    for (int m = 0; m < w.n_moving; ++m)
+      store(m, se3_mul(link_from_pose7(in + (cfg * w.n_links + w.moving_link[m]) * 7), load_se3(w.moving_offset + 12 * m)));
+    return;
+  }
+  // oMi[j] = oMi[parent] * (jointPlacement_j * M_j(q)); branch frames spilled
+  const double* qrow = in + cfg * w.dof;
+  SE3 cur;
+  se3_identity(cur);
+  for (int j = 0; j <= w.nj; ++j) {
+    if (j > 0) {
+      const int jj = j - 1;
+      const int src = w.joint_q_source[jj];
+      const double v = src >= 0 ? qrow[src] : w.joint_q_const[jj];
+      const SE3 li = se3_mul(load_se3(w.joint_place + 12 * jj), joint_motion(w.joint_type[jj], w.joint_axis + 3 * jj, v));
+      const int sidx = w.bp.jsrc[jj];
+      if (sidx < 0) {
+        cur = li;
+      } else if (sidx > 0) {
+        SE3 P;
+        const double* sp = save64 + (size_t)(sidx - 1) * 12 * n + cfg;
+        for (int i = 0; i < 9; ++i) P.R[i] = sp[i * n];
+        for (int i = 0; i < 3; ++i) P.p[i] = sp[(9 + i) * n];
+        cur = se3_mul(P, li);
+      } else {
+        cur = se3_mul(cur, li);
+      }
+      const int sv = w.bp.jsave[jj];
+      if (sv >= 0) {
+        double* sp = save64 + (size_t)sv * 12 * n + cfg;
+        for (int i = 0; i < 9; ++i) sp[i * n] = cur.R[i];
+        for (int i = 0; i < 3; ++i) sp[(9 + i) * n] = cur.p[i];
+      }
+    }
+    for (int k = w.bp.link_start[j]; k < w.bp.link_start[j + 1]; ++k) {
+      const int l = w.bp.link_order[k];
+      const int o0 = w.bp.obj_start[l], o1 = w.bp.obj_start[l + 1];
+      if (o0 == o1) continue;
+      SE3 root;
+      se3_identity(root);
+      const SE3 L = link_from_oMi(w, j == 0 ? root : cur, l, nullptr);
+      for (int o = o0; o < o1; ++o) {
+        const int m = w.bp.obj_order[o];
+        store(m, se3_mul(L, load_se3(w.moving_offset + 12 * m)));
+      }
+    }
+  }
+}
+
+__device__ __forceinline__ double d3dot(const V3& a, const V3& b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+
+// closest point of triangle (a, b, c) to the origin (Ericson 5.1.5); keep
+// marks the vertices of the reached feature
+__device__ __forceinline__ V3 tri_closest(const V3& a, const V3& b, const V3& c, bool keep[3]) {
+  const V3 ab = vsub(b, a), ac = vsub(c, a);
+  const double d1 = -d3dot(ab, a), d2 = -d3dot(ac, a);
+  keep[0] = keep[1] = keep[2] = false;
+  if (d1 <= 0 && d2 <= 0) {
+    keep[0] = true;
+    return a;
+  }
+  const double d3 = -d3dot(ab, b), d4 = -d3dot(ac, b);
+  if (d3 >= 0 && d4 <= d3) {
+    keep[1] = true;
+    return b;
+  }
+  const double vc = d1 * d4 - d3 * d2;
+  if (vc <= 0 && d1 >= 0 && d3 <= 0) {
+    const double t = d1 / (d1 - d3);
+    keep[0] = keep[1] = true;
+    return V3{a.x + t * ab.x, a.y + t * ab.y, a.z + t * ab.z};
+  }
+  const double d5 = -d3dot(ab, c), d6 = -d3dot(ac, c);
+  if (d6 >= 0 && d5 <= d6) {
+    keep[2] = true;
+    return c;
+  }
+  const double vb = d5 * d2 - d1 * d6;
+  if (vb <= 0 && d2 >= 0 && d6 <= 0) {
+    const double t = d2 / (d2 - d6);
+    keep[0] = keep[2] = true;
+    return V3{a.x + t * ac.x, a.y + t * ac.y, a.z + t * ac.z};
+  }
+  const double va = d3 * d6 - d5 * d4;
+  if (va <= 0 && (d4 - d3) >= 0 && (d5 - d6) >= 0) {
+    const double t = (d4 - d3) / ((d4 - d3) + (d5 - d6));
+    const V3 bc = vsub(c, b);
+    keep[1] = keep[2] = true;
+    return V3{b.x + t * bc.x, b.y + t * bc.y, b.z + t * bc.z};
+  }
+  const double den = 1.0 / (va + vb + vc), t1 = vb * den, t2 = vc * den;
+  keep[0] = keep[1] = keep[2] = true;
+  return V3{a.x + ab.x * t1 + ac.x * t2, a.y + ab.y * t1 + ac.y * t2, a.z + ab.z * t1 + ac.z * t2};
+}
+
+// simplex P[0..n) -> closest point, reduced simplex; true if it encloses the origin
+__device__ __forceinline__ bool simplex_closest(V3 P[4], int& n, V3& v) {
+  if (n == 1) {
+    v = P[0];
+    return false;
+  }
+  if (n == 2) {
+    const V3 ab = vsub(P[1], P[0]);
+    const double den = d3dot(ab, ab), t = den > 0 ? -d3dot(P[0], ab) / den : 0.0;
+    if (t <= 0) {
+      v = P[0];
+      n = 1;
+    } else if (t >= 1) {
+      v = P[1];
+      P[0] = P[1];
+      n = 1;
+    } else {
+      v = V3{P[0].x + t * ab.x, P[0].y + t * ab.y, P[0].z + t * ab.z};
+    }
+    return false;
+  }
+  if (n == 3) {
+    bool keep[3];
+    v = tri_closest(P[0], P[1], P[2], keep);
+    int m = 0;
+    for (int k = 0; k < 3; ++k)
+      if (keep[k]) P[m++] = P[k];
+    n = m;
+    return false;
+  }
+  const int F[4][4] = {{0, 1, 2, 3}, {0, 2, 3, 1}, {0, 3, 1, 2}, {1, 3, 2, 0}};
+  double best = DBL_MAX;
+  V3 bv{0, 0, 0}, BP[3];
+  int bn = 0;
+  bool any = false;
+  for (int f = 0; f < 4; ++f) {
+    const V3 a = P[F[f][0]], b = P[F[f][1]], c = P[F[f][2]], d = P[F[f][3]];
+    const V3 nrm = vcross(vsub(b, a), vsub(c, a));
+    const double sp = -d3dot(a, nrm), sd = d3dot(vsub(d, a), nrm);
+    if (!(sp * sd < 0 || sd == 0.0)) continue;
+    any = true;
+    bool keep[3];
+    const V3 fv = tri_closest(a, b, c, keep);
+    const double dd = d3dot(fv, fv);
+    if (dd < best) {
+      best = dd;
+      bv = fv;
+      bn = 0;
+      const V3 abc[3] = {a, b, c};
+      for (int k = 0; k < 3; ++k)
+        if (keep[k]) BP[bn++] = abc[k];
+    }
+  }
+  if (!any) return true;
+  for (int k = 0; k < bn; ++k) P[k] = BP[k];
+  n = bn;
+  v = bv;
+  return false;
+}
+
+__device__ double gjk_distance(const DevWorld& w, cptr<double> HV, const GObj& A, const GObj& B) {
+  V3 v = vsub(center(w, A), center(w, B));
+  if (d3dot(v, v) == 0.0) v.x = 1e-12;
+  V3 P[4];
+  int n = 0;
+  for (int it = 0; it < 128; ++it) {
+    const V3 wv = msupport(w, HV, A, B, V3{-v.x, -v.y, -v.z});
+    const double vv = d3dot(v, v), vw = d3dot(v, wv);
+    if (n > 0 && vv - vw <= 1e-12 * vv) break;
+    bool dup = false;
+    for (int k = 0; k < n; ++k) dup |= (P[k].x == wv.x && P[k].y == wv.y && P[k].z == wv.z);
+    if (dup) break;
+    P[n++] = wv;
+    if (simplex_closest(P, n, v)) return -1.0;
+    const double nv = d3dot(v, v);
+    if (nv <= 1e-24) return -1.0;
+    if (n > 1 && nv >= vv) break;
+  }
+  return std::sqrt(d3dot(v, v));
+}
+
+__device__ __forceinline__ GObj pose_obj(const DevWorld& w, const double* __restrict__ poses, long long n, long long cfg,
+                                         int id, V3& c) {
+  if (id < w.n_moving) {
+    const double* g = poses + ((size_t)id * kPoseStride) * n + cfg;
+    GObj o;
+    o.rot = Q4{g[0], g[n], g[2 * n], g[3 * n]};
+    o.rot_inv = quat_invert2(o.rot);
+    o.pos = v3(g[4 * n], g[5 * n], g[6 * n]);
+    o.geom = w.moving_geom[id];
+    o.type = w.geom_type[o.geom];
+    c = v3(g[7 * n], g[8 * n], g[9 * n]);
+    return o;
+  }
+  const int sid = id - w.n_moving;
+  const cptr<double> r = w.static_rec + S_STRIDE * sid;
+  c = v3(r[S_OBBC], r[S_OBBC + 1], r[S_OBBC + 2]);
+  return static_obj(w, sid);
+}
+
+__global__ __launch_bounds__(128) void distance_kernel(DevWorld w, const double* __restrict__ poses, long long n,
+                                                       int n_self, double* __restrict__ d_self,
+                                                       int32_t* __restrict__ p_self, double* __restrict__ d_others,
+                                                       int32_t* __restrict__ p_others) {
+  const long long cfg0 = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool live = cfg0 < n;
+  const long long cfg = live ? cfg0 : n - 1;
+  const cptr<double> HV = w.hull;
+  double best[2] = {DBL_MAX, DBL_MAX};
+  int bp[2] = {-1, -1};
+  for (int p = 0; p < w.n_pairs; ++p) {
+    if (w.pair_allowed[p]) continue;  // ACM before distance (planning_world.cpp:509-510)
+    const int g = p < n_self ? 0 : 1;
+    const int a = w.pair_a[p], b = w.pair_b[p];
+    V3 ca, cb;
+    const GObj A = pose_obj(w, poses, n, cfg, a, ca);
+    const GObj B = pose_obj(w, poses, n, cfg, b, cb);
+    const double ra = w.geom_rec[G_STRIDE * A.geom + G_RADIUS], rb = w.geom_rec[G_STRIDE * B.geom + G_RADIUS];
+    const V3 dc = vsub(cb, ca);
+    // bounding spheres: the pair cannot beat the running minimum
+    const double lb = std::sqrt(d3dot(dc, dc)) - ra - rb - 1e-9;
+    if (!live || best[g] == -1.0 || lb >= best[g]) continue;
+    const double d = gjk_distance(w, HV, A, B);
+    if (d < best[g]) {
+      best[g] = d;
+      bp[g] = p;
+    }
+  }
+  if (!live) return;
+  d_self[cfg] = best[0];
+  p_self[cfg] = bp[0];
+  d_others[cfg] = best[1];
+  p_others[cfg] = bp[1];
+}
+
 __global__ void fk_kernel(DevWorld w, const double* __restrict__ q, long long n, double* __restrict__ out) {
   const long long cfg = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (cfg >= n) return;
@@ -1055,6 +1318,18 @@ struct mpg_world {
     size_t flags_cap = 0;
   } motion;
   std::mutex motion_mu;
+  // batched distance buffers (grow-only)
+  struct Dist {
+    double* poses = nullptr;
+    size_t poses_cap = 0;
+    double* save64 = nullptr;
+    size_t save_cap = 0;
+    double* q = nullptr;
+    size_t q_cap = 0;
+    char* out = nullptr;
+    size_t out_cap = 0;
+  } dist;
+  std::mutex dist_mu;
   std::mutex prof_mu;
   bool prof = false;
   std::vector<Mark> marks;
@@ -1728,6 +2003,10 @@ int mpg_world_destroy(mpg_world* w) {
     hipEventDestroy(mk.b);
   }
   for (hipEvent_t e : w->ev_pool) hipEventDestroy(e);
+  hipFree(w->dist.poses);
+  hipFree(w->dist.save64);
+  hipFree(w->dist.q);
+  hipFree(w->dist.out);
   hipFree(w->motion.edges);
   hipFree(w->motion.segs);
   hipFree(w->motion.offs);
@@ -1872,6 +2151,60 @@ int mpg_check_motion_batch(mpg_world* w, const double* q_from, const double* q_t
     if (segments) std::memcpy(segments, segs.data(), sizeof(int32_t) * n);
   } else if (segments) {
     HIP_TRY(hipMemcpyAsync(segments, M.segs, sizeof(int32_t) * n, hipMemcpyDeviceToDevice, s));
+  }
+  return MPG_OK;
+}
+
+int mpg_distance_batch(mpg_world* w, const double* q, int64_t n, int32_t n_self_pairs, double* d_self,
+                       int32_t* p_self, double* d_others, int32_t* p_others, int mem, void* stream) {
+  if (!w) return set_error(MPG_E_INVALID, "world is NULL");
+  if (n < 0) return set_error(MPG_E_INVALID, "n < 0");
+  if (n_self_pairs < 0 || n_self_pairs > w->dw.n_pairs) return set_error(MPG_E_INVALID, "bad n_self_pairs");
+  if (n > 0 && ((!q && w->dw.dof > 0) || !d_self || !p_self || !d_others || !p_others))
+    return set_error(MPG_E_INVALID, "NULL buffer");
+  if (mem != MPG_MEM_HOST && mem != MPG_MEM_DEVICE) return set_error(MPG_E_INVALID, "bad mem kind");
+  if (n == 0) return MPG_OK;
+  HIP_TRY(hipSetDevice(w->device));
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  std::lock_guard<std::mutex> lk(w->dist_mu);
+  auto grow = [&](void** p, size_t& cap, size_t want) -> int {
+    if (cap >= want) return MPG_OK;
+    if (*p) HIP_TRY(hipFree(*p));
+    *p = nullptr;
+    HIP_TRY(hipMalloc(p, want));
+    cap = want;
+    return MPG_OK;
+  };
+  auto& D = w->dist;
+  int rc;
+  const size_t nm = std::max(w->dw.n_moving, 1), ns = std::max(w->dw.bp.n_saves, 1);
+  if ((rc = grow((void**)&D.poses, D.poses_cap, sizeof(double) * kPoseStride * nm * n))) return rc;
+  if ((rc = grow((void**)&D.save64, D.save_cap, sizeof(double) * 12 * ns * n))) return rc;
+  const double* qin = q;
+  double *ds = d_self, *dd = d_others;
+  int32_t *ps = p_self, *po = p_others;
+  if (mem == MPG_MEM_HOST) {
+    if ((rc = grow((void**)&D.q, D.q_cap, sizeof(double) * std::max(w->dw.dof, 1) * n))) return rc;
+    if ((rc = grow((void**)&D.out, D.out_cap, (2 * sizeof(double) + 2 * sizeof(int32_t)) * n))) return rc;
+    if (w->dw.dof) HIP_TRY(hipMemcpyAsync(D.q, q, sizeof(double) * w->dw.dof * n, hipMemcpyHostToDevice, s));
+    qin = D.q;
+    ds = reinterpret_cast<double*>(D.out);
+    dd = ds + n;
+    ps = reinterpret_cast<int32_t*>(dd + n);
+    po = ps + n;
+  }
+  const unsigned grid = (unsigned)((n + 127) / 128);
+  hipLaunchKernelGGL((pose_kernel<false>), dim3(grid), dim3(128), 0, s, w->dw, qin, (long long)n, D.poses, D.save64);
+  HIP_TRY(hipGetLastError());
+  hipLaunchKernelGGL(distance_kernel, dim3(grid), dim3(128), 0, s, w->dw, D.poses, (long long)n, n_self_pairs, ds, ps,
+                     dd, po);
+  HIP_TRY(hipGetLastError());
+  if (mem == MPG_MEM_HOST) {
+    HIP_TRY(hipMemcpyAsync(d_self, ds, sizeof(double) * n, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(d_others, dd, sizeof(double) * n, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(p_self, ps, sizeof(int32_t) * n, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(p_others, po, sizeof(int32_t) * n, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
   }
   return MPG_OK;
 }

@@ -49,6 +49,8 @@ def lib():
         _lib.orc_collide_batch.restype = ctypes.c_int
         _lib.orc_fk_batch.restype = ctypes.c_int
         _lib.orc_collide_pair.restype = ctypes.c_int
+        _lib.orc_distance_pair.restype = ctypes.c_double
+        _lib.orc_distance_batch.restype = ctypes.c_int
     return _lib
 
 
@@ -261,6 +263,21 @@ class OracleWorld:
         if rc != 0:
             raise RuntimeError("orc_fk_batch failed")
         return poses, objT
+
+    def distance_batch(self, q: np.ndarray):
+        """PlanningWorld::distanceSelf / distanceOthers per configuration:
+        (d_self, pair_self, d_others, pair_others); -1 = penetrating pair,
+        DBL_MAX / -1 = empty group."""
+        q = np.ascontiguousarray(q, dtype=np.float64).reshape(-1, self.dof)
+        n = q.shape[0]
+        ds, do = np.zeros(n), np.zeros(n)
+        ps, po = np.zeros(n, np.int32), np.zeros(n, np.int32)
+        rc = lib().orc_distance_batch(ctypes.byref(self._w), q.ctypes.data_as(_DP), ctypes.c_long(n),
+                                      ctypes.c_int(self.n_self_pairs), ds.ctypes.data_as(_DP), ps.ctypes.data_as(_IP),
+                                      do.ctypes.data_as(_DP), po.ctypes.data_as(_IP))
+        if rc != 0:
+            raise RuntimeError("orc_distance_batch failed")
+        return ds, ps, do, po
 
     def pair_names(self) -> List[Tuple[str, str]]:
         return [(p[4], p[5]) for p in self.pairs]

@@ -727,6 +727,134 @@ static int closed_form_intersect(const orc_world *w, int ga, const real *Ta, int
     return -1;
 }
 
+/* ------------------------------------------------ GJK distance
+ * PlanningWorld::distance* (src/planning_world.cpp:493-720) calls
+ * fcl::distance -> GJKSolver_libccd::shapeDistance -> libccd GJK distance
+ * [ext FCL 0.7.0 / libccd 2.1], which returns -1 for penetrating shapes
+ * (DistanceRequest() has enable_signed_distance = false).  The north star
+ * asks for distances within 1e-5 of the CPU path, not bit equality: this is
+ * a plain GJK (Johnson sub-distance via Ericson's closest-point regions) run
+ * to 1e-12 relative convergence on the same FCL support mappings, so it
+ * lands on the true Euclidean distance; the device runs the same algorithm
+ * (mplib_amd/csrc/mpg_kernels.hip gjk_distance). */
+static double d3dot(const double *a, const double *b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
+static void d3sub(double *o, const double *a, const double *b) { o[0] = a[0] - b[0]; o[1] = a[1] - b[1]; o[2] = a[2] - b[2]; }
+static void d3cross(double *o, const double *a, const double *b) {
+    o[0] = a[1] * b[2] - a[2] * b[1]; o[1] = a[2] * b[0] - a[0] * b[2]; o[2] = a[0] * b[1] - a[1] * b[0];
+}
+
+/* closest point of triangle (a, b, c) to the origin; keep[] marks the
+ * vertices of the reached feature (Ericson, Real-Time Collision Detection 5.1.5) */
+static void tri_closest(const double *a, const double *b, const double *c, double *v, int keep[3]) {
+    double ab[3], ac[3], bc[3];
+    d3sub(ab, b, a); d3sub(ac, c, a);
+    const double d1 = -d3dot(ab, a), d2 = -d3dot(ac, a);
+    keep[0] = keep[1] = keep[2] = 0;
+    if (d1 <= 0 && d2 <= 0) { memcpy(v, a, 24); keep[0] = 1; return; }
+    const double d3 = -d3dot(ab, b), d4 = -d3dot(ac, b);
+    if (d3 >= 0 && d4 <= d3) { memcpy(v, b, 24); keep[1] = 1; return; }
+    const double vc = d1 * d4 - d3 * d2;
+    if (vc <= 0 && d1 >= 0 && d3 <= 0) {
+        const double t = d1 / (d1 - d3);
+        for (int i = 0; i < 3; ++i) v[i] = a[i] + t * ab[i];
+        keep[0] = keep[1] = 1; return;
+    }
+    const double d5 = -d3dot(ab, c), d6 = -d3dot(ac, c);
+    if (d6 >= 0 && d5 <= d6) { memcpy(v, c, 24); keep[2] = 1; return; }
+    const double vb = d5 * d2 - d1 * d6;
+    if (vb <= 0 && d2 >= 0 && d6 <= 0) {
+        const double t = d2 / (d2 - d6);
+        for (int i = 0; i < 3; ++i) v[i] = a[i] + t * ac[i];
+        keep[0] = keep[2] = 1; return;
+    }
+    const double va = d3 * d6 - d5 * d4;
+    if (va <= 0 && (d4 - d3) >= 0 && (d5 - d6) >= 0) {
+        const double t = (d4 - d3) / ((d4 - d3) + (d5 - d6));
+        d3sub(bc, c, b);
+        for (int i = 0; i < 3; ++i) v[i] = b[i] + t * bc[i];
+        keep[1] = keep[2] = 1; return;
+    }
+    const double den = 1.0 / (va + vb + vc), t1 = vb * den, t2 = vc * den;
+    for (int i = 0; i < 3; ++i) v[i] = a[i] + ab[i] * t1 + ac[i] * t2;
+    keep[0] = keep[1] = keep[2] = 1;
+}
+
+/* simplex P[0..n) -> closest point v, reduced simplex; 1 if it encloses the origin */
+static int simplex_closest(double P[4][3], int *n, double *v) {
+    if (*n == 1) { memcpy(v, P[0], 24); return 0; }
+    if (*n == 2) {
+        double ab[3];
+        d3sub(ab, P[1], P[0]);
+        const double den = d3dot(ab, ab), t = den > 0 ? -d3dot(P[0], ab) / den : 0.0;
+        if (t <= 0) { memcpy(v, P[0], 24); *n = 1; return 0; }
+        if (t >= 1) { memcpy(v, P[1], 24); memcpy(P[0], P[1], 24); *n = 1; return 0; }
+        for (int i = 0; i < 3; ++i) v[i] = P[0][i] + t * ab[i];
+        return 0;
+    }
+    if (*n == 3) {
+        int keep[3];
+        tri_closest(P[0], P[1], P[2], v, keep);
+        int m = 0;
+        for (int k = 0; k < 3; ++k) if (keep[k]) { if (m != k) memcpy(P[m], P[k], 24); ++m; }
+        *n = m;
+        return 0;
+    }
+    /* tetrahedron: faces whose plane separates the origin from the 4th vertex */
+    static const int F[4][4] = {{0, 1, 2, 3}, {0, 2, 3, 1}, {0, 3, 1, 2}, {1, 3, 2, 0}};
+    double best = DBL_MAX, bv[3] = {0, 0, 0}, BP[3][3];
+    int bn = -1, any = 0;
+    for (int f = 0; f < 4; ++f) {
+        const double *a = P[F[f][0]], *b = P[F[f][1]], *c = P[F[f][2]], *d = P[F[f][3]];
+        double ab[3], ac[3], nrm[3], ad[3];
+        d3sub(ab, b, a); d3sub(ac, c, a); d3cross(nrm, ab, ac); d3sub(ad, d, a);
+        const double sp = -d3dot(a, nrm), sd = d3dot(ad, nrm);
+        if (!(sp * sd < 0 || sd == 0.0)) continue;
+        any = 1;
+        double fv[3];
+        int keep[3];
+        tri_closest(a, b, c, fv, keep);
+        const double dd = d3dot(fv, fv);
+        if (dd < best) {
+            best = dd; memcpy(bv, fv, 24); bn = 0;
+            const double *abc[3] = {a, b, c};
+            for (int k = 0; k < 3; ++k) if (keep[k]) memcpy(BP[bn++], abc[k], 24);
+        }
+    }
+    if (!any) return 1;
+    for (int k = 0; k < bn; ++k) memcpy(P[k], BP[k], 24);
+    *n = bn;
+    memcpy(v, bv, 24);
+    return 0;
+}
+
+static double gjk_distance(const gjk_obj *o1, const gjk_obj *o2) {
+    ccd_vec3_t c1, c2;
+    gjk_center(o1, &c1);
+    gjk_center(o2, &c2);
+    double v[3] = {c1.v[0] - c2.v[0], c1.v[1] - c2.v[1], c1.v[2] - c2.v[2]};
+    if (d3dot(v, v) == 0.0) v[0] = 1e-12;
+    double P[4][3];
+    int n = 0;
+    for (int it = 0; it < 128; ++it) {
+        ccd_vec3_t dir;
+        ccd_support_t sp;
+        ccdVec3Set(&dir, -v[0], -v[1], -v[2]);
+        ccd_support(o1, o2, &dir, &sp);
+        const double w[3] = {sp.v.v[0], sp.v.v[1], sp.v.v[2]};
+        const double vv = d3dot(v, v), vw = d3dot(v, w);
+        if (n > 0 && vv - vw <= 1e-12 * vv) break;
+        int dup = 0;
+        for (int k = 0; k < n; ++k) dup |= (P[k][0] == w[0] && P[k][1] == w[1] && P[k][2] == w[2]);
+        if (dup) break;
+        memcpy(P[n++], w, 24);
+        if (simplex_closest(P, &n, v)) return -1.0;
+        const double nv = d3dot(v, v);
+        if (nv <= 1e-24) return -1.0;
+        if (n > 1 && nv >= vv) break;
+    }
+    return sqrt(d3dot(v, v));
+}
+
 /* ------------------------------------------------------- world collide */
 static void make_obj(const orc_world *w, int geom, const real *T, gjk_obj *o, orc_stats *st) {
     memset(o, 0, sizeof *o);
@@ -811,6 +939,46 @@ static void *worker(void *arg) {
     return NULL;
 }
 
+/* PlanningWorld::distanceSelf / distanceOthers per configuration: pairs
+ * [0, n_self) are the self group, the rest the others group; ACM-allowed
+ * pairs are skipped before any distance (src/planning_world.cpp:509-510);
+ * strict '<' keeps the first minimum.  best = DBL_MAX / pair -1 when a group
+ * has no pair. */
+int orc_distance_batch(const orc_world *w, const double *q, long n, int n_self, double *d_self, int *p_self,
+                       double *d_others, int *p_others) {
+    real *oMi = malloc(sizeof(real) * 12 * (size_t)(w->nj + 1));
+    real *link_T = malloc(sizeof(real) * 12 * (size_t)(w->n_links + 1));
+    real *obj_T = malloc(sizeof(real) * 12 * (size_t)(w->n_obj + 1));
+    real *att_T = malloc(sizeof(real) * 12 * (size_t)(w->n_att + 1));
+    for (long c = 0; c < n; ++c) {
+        fk_links(w, q + (size_t)c * w->dof, oMi, link_T, NULL);
+        for (int i = 0; i < w->n_obj; ++i) se3_mul(link_T + 12 * w->obj_link[i], w->obj_origin + 12 * i, obj_T + 12 * i);
+        for (int i = 0; i < w->n_att; ++i) se3_mul(link_T + 12 * w->att_link[i], w->att_pose + 12 * i, att_T + 12 * i);
+        double best[2] = {DBL_MAX, DBL_MAX};
+        int bp[2] = {-1, -1};
+        for (int p = 0; p < w->n_pairs; ++p) {
+            if (w->p_allowed[p]) continue;
+            const int g = p < n_self ? 0 : 1;
+            if (best[g] == -1.0) continue;  /* nothing is below -1 */
+            int ks[2] = {w->pa_kind[p], w->pb_kind[p]}, is[2] = {w->pa_idx[p], w->pb_idx[p]};
+            gjk_obj o[2];
+            for (int s = 0; s < 2; ++s) {
+                const real *T;
+                int gg;
+                if (ks[s] == KIND_ROBOT) { T = obj_T + 12 * is[s]; gg = w->obj_geom[is[s]]; }
+                else if (ks[s] == KIND_ATTACHED) { T = att_T + 12 * is[s]; gg = w->att_geom[is[s]]; }
+                else { T = w->scene_tf + 12 * is[s]; gg = w->scene_geom[is[s]]; }
+                make_obj(w, gg, T, &o[s], NULL);
+            }
+            const double d = gjk_distance(&o[0], &o[1]);
+            if (d < best[g]) { best[g] = d; bp[g] = p; }
+        }
+        d_self[c] = best[0]; p_self[c] = bp[0]; d_others[c] = best[1]; p_others[c] = bp[1];
+    }
+    free(oMi); free(link_T); free(obj_T); free(att_T);
+    return 0;
+}
+
 /* Batch entry point.  flags[n], masks[n*W]; stats (may be NULL) receives
  * the summed instrumentation counters. */
 int orc_collide_batch(const orc_world *w, const double *q, long n, uint8_t *flags, uint32_t *masks, int W,
@@ -862,6 +1030,13 @@ int orc_fk_batch(const orc_world *w, const double *q, long n, double *link_pose7
 }
 
 /* Single-pair entry (fcl.collide(o1, o2) on two posed shapes). */
+double orc_distance_pair(const orc_world *w, int ga, const double *Ta, int gb, const double *Tb) {
+    gjk_obj a, b;
+    make_obj(w, ga, Ta, &a, NULL);
+    make_obj(w, gb, Tb, &b, NULL);
+    return gjk_distance(&a, &b);
+}
+
 int orc_collide_pair(const orc_world *w, int ga, const double *Ta, int gb, const double *Tb) {
     const int cf = closed_form_intersect(w, ga, Ta, gb, Tb);
     if (cf >= 0) return cf;

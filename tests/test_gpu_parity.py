@@ -327,3 +327,47 @@ def test_spheres_closed_forms_match_oracle():
     np.testing.assert_array_equal(f, fo)
     bits = lambda M_, P: np.stack([(M_[:, p >> 5] >> (p & 31)) & 1 for p in P], 1)
     np.testing.assert_array_equal(bits(m, range(len(perm))), bits(mo, perm))
+
+
+# ------------------------------------------------------------------- distance
+@pytest.mark.parametrize("cfg", [3, 4])
+def test_distance_batch_matches_oracle(cfg):
+    """Batched distanceSelf/distanceOthers vs the oracle (same GJK restated):
+    |d_gpu - d_cpu| < 1e-9 (the north star's bar vs FCL is 1e-5), -1 exactly
+    on penetration, argmin pair equal."""
+    w, art = scenes.world(cfg)
+    q = scenes.sample_states(art, 4000, 90 + cfg)
+    ds, ps, do, po = w.distance_batch(q)
+    rs, rps, ro, rpo = ow(cfg).distance_batch(q)
+    for d, r in ((ds, rs), (do, ro)):
+        np.testing.assert_array_equal(d == -1.0, r == -1.0)
+        np.testing.assert_allclose(d, r, rtol=0, atol=1e-9)
+    assert (ps == rps).mean() > 0.999 and (po == rpo).mean() > 0.999
+    f, _ = w.collide_batch(q)
+    np.testing.assert_array_equal((ds == -1.0) | (do == -1.0), f.astype(bool))
+
+
+def test_scalar_distance_api():
+    w, art = scenes.world(3)
+    q = scenes.sample_states(art, 16, 5)
+    rs, rps, ro, rpo = ow(3).distance_batch(q)
+    names = [(i[3], i[4]) for i in w.get_collision_pair_info()]
+    for i in range(len(q)):
+        w.set_qpos_all(list(q[i]))
+        s, o, full = w.self_distance(), w.distance_with_others(), w.distance_full()
+        assert abs(s.min_distance - rs[i]) < 1e-9 and (s.link_name1, s.link_name2) == names[rps[i]]
+        assert abs(o.min_distance - ro[i]) < 1e-9 and (o.link_name1, o.link_name2) == names[rpo[i]]
+        assert s.distance_type == "self" and o.distance_type == "articulation_sceneobject"
+        assert full.min_distance == min(s.min_distance, o.min_distance) == w.distance()
+    with pytest.raises(NotImplementedError):
+        w.self_distance(pymp.fcl.DistanceRequest(enable_signed_distance=True))
+
+
+def test_fcl_distance_free_function():
+    a = pymp.fcl.CollisionObject(pymp.fcl.Box([1.0, 1.0, 1.0]), [0, 0, 0], [1, 0, 0, 0])
+    b = pymp.fcl.CollisionObject(pymp.fcl.Box([1.0, 1.0, 1.0]), [1.5, 1.5, 0.0], [1, 0, 0, 0])
+    assert abs(pymp.fcl.distance(a, b).min_distance - np.sqrt(0.5)) < 1e-9
+    c = pymp.fcl.CollisionObject(pymp.fcl.Sphere(0.25), [1.0, 0.0, 0.0], [1, 0, 0, 0])
+    assert abs(pymp.fcl.distance(c, a).min_distance - 0.25) < 1e-6
+    d = pymp.fcl.CollisionObject(pymp.fcl.Box([1.0, 1.0, 1.0]), [0.9, 0.2, 0.1], [1, 0, 0, 0])
+    assert pymp.fcl.distance(a, d).min_distance == -1.0

@@ -150,3 +150,76 @@ def test_sphere_closed_forms_known_answers():
     assert _collide(w, gs, _T(p=(corner, 0.1 + 0.1 / np.sqrt(3) * 0.999, 0.5 + 0.1 / np.sqrt(3) * 0.999)), gb,
                     _T()) == 1
     assert _collide(w, gs, _T(p=(0.2 + 0.06, 0.1 + 0.06, 0.5 + 0.06)), gb, _T()) == 0
+
+
+# ------------------------------------------------------------- GJK distance
+def _qp_distance(VA, VB):
+    """min |sum l_i a_i - sum m_j b_j| over the two simplices (SLSQP): an
+    independent reference for the polytope distance."""
+    from scipy.optimize import minimize
+    na, nb = len(VA), len(VB)
+
+    def f(x):
+        d = x[:na] @ VA - x[na:] @ VB
+        return d @ d
+
+    def g(x):
+        d = x[:na] @ VA - x[na:] @ VB
+        return np.concatenate([2 * VA @ d, -2 * VB @ d])
+
+    x0 = np.concatenate([np.full(na, 1 / na), np.full(nb, 1 / nb)])
+    cons = [{"type": "eq", "fun": lambda x: x[:na].sum() - 1}, {"type": "eq", "fun": lambda x: x[na:].sum() - 1}]
+    r = minimize(f, x0, jac=g, bounds=[(0, 1)] * (na + nb), constraints=cons, method="SLSQP",
+                 options={"ftol": 1e-16, "maxiter": 500})
+    return float(np.sqrt(max(r.fun, 0.0)))
+
+
+def test_gjk_distance_matches_qp():
+    import ctypes
+    import oracle
+    from oracle import model as M
+    rng = np.random.default_rng(8)
+    P = ctypes.POINTER(ctypes.c_double)
+    for trial in range(12):
+        A = rng.normal(size=(rng.integers(6, 20), 3)) * 0.1
+        B = rng.normal(size=(rng.integers(6, 20), 3)) * 0.1
+        gA, gB = M.ConvexGeom(A, []), M.ConvexGeom(B, [])
+        w, (ia, ib) = _pair_world([gA, gB])
+        off = rng.normal(size=3)
+        off *= (0.3 + 0.3 * rng.random()) / np.linalg.norm(off)
+        Ta, Tb = _T(), _T(p=tuple(off))
+        d = oracle.lib().orc_distance_pair(ctypes.byref(w._w), ia, Ta.ctypes.data_as(P), ib, Tb.ctypes.data_as(P))
+        ref = _qp_distance(A, B + off)
+        if ref < 1e-9:
+            assert d == -1.0
+        else:
+            assert abs(d - ref) < 1e-7, (trial, d, ref)
+
+
+def test_gjk_distance_primitives_known_answers():
+    import ctypes
+    import oracle
+    from oracle import model as M
+    P = ctypes.POINTER(ctypes.c_double)
+    b1, s1 = M.BoxGeom((1.0, 1.0, 1.0)), M.SphereGeom(0.25)
+    w, (gb, gs) = _pair_world([b1, s1])
+    dist = lambda ga, Ta, gb_, Tb: oracle.lib().orc_distance_pair(ctypes.byref(w._w), ga, Ta.ctypes.data_as(P), gb_,
+                                                                   Tb.ctypes.data_as(P))
+    assert abs(dist(gb, _T(), gb, _T(p=(1.7, 0.0, 0.0))) - 0.7) < 1e-9       # face-face
+    assert abs(dist(gb, _T(), gb, _T(p=(1.5, 1.5, 0.0))) - np.sqrt(0.5)) < 1e-9  # edge-edge
+    assert abs(dist(gs, _T(), gb, _T(p=(1.0, 0.0, 0.0))) - 0.25) < 1e-6      # sphere (curved support)
+    assert dist(gb, _T(), gb, _T(p=(0.9, 0.2, 0.1))) == -1.0                  # penetrating -> -1
+    assert dist(gs, _T(), gs, _T(p=(0.3, 0.3, 0.0))) == -1.0
+
+
+def test_distance_batch_semantics():
+    ow = Wd.oracle_world(3)
+    q = Wd.sample_q(ow.art, 300, 4)
+    ds, ps, do, po = ow.distance_batch(q)
+    f, _ = ow.collide_batch(q)
+    # a colliding configuration has a penetrating pair (-1) in one group
+    coll = (ds == -1.0) | (do == -1.0)
+    np.testing.assert_array_equal(coll, f.astype(bool))
+    assert ((ps >= 0) & (ps < ow.n_self_pairs)).all() and (po >= ow.n_self_pairs).all()
+    free = ~coll
+    assert (np.minimum(ds, do)[free] > 0).all()
