@@ -209,6 +209,22 @@ int mpg_check_motion_batch(mpg_world *world, const double *q_from, const double 
 int mpg_distance_batch(mpg_world *world, const double *q, int64_t n, int32_t n_self_pairs, double *d_self,
                        int32_t *p_self, double *d_others, int32_t *p_others, int mem, void *stream);
 
+/*
+ * Collide with contacts: CollisionRequest(enable_contact=True).  Same flags /
+ * pair_mask as mpg_collide_batch (input_kind MPG_INPUT_Q: q rows) or
+ * mpg_collide_link_poses (MPG_INPUT_LINK_POSES), plus, for every reported
+ * pair p of configuration i, libccd's MPR penetration (FCL GJKCollide ->
+ * ccdMPRPenetration, the one contact FCL reports for an MPR pair):
+ *   depth[i*P + p], normal[(i*P + p)*3 ..] (from object 1 to object 2),
+ *   pos[(i*P + p)*3 ..]; zeros for pairs not reported.  P = n_pairs.
+ * Worlds whose non-allowed pairs include FCL closed forms (box-box,
+ * sphere-sphere, sphere-box) return MPG_E_UNSUPPORTED.
+ */
+#define MPG_INPUT_Q 0
+#define MPG_INPUT_LINK_POSES 1
+int mpg_collide_contacts(mpg_world *world, const double *input, int64_t n, int input_kind, uint8_t *flags,
+                         uint32_t *pair_mask, double *depth, double *normal, double *pos, int mem, void *stream);
+
 /* link_pose: [n*n_links*7] = getLinkPose(l) -> (px, py, pz, qw, qx, qy, qz). */
 int mpg_fk_batch(mpg_world *world, const double *q, int64_t n, double *link_pose, int mem,
                  void *stream);

@@ -204,6 +204,9 @@ class DeviceWorld {
 };
 
 void check_status(int rc, const char* what);
+// copy pair p's contact (mpg_collide_contacts layout) into c
+void fill_contacts(const uint32_t* mask, size_t n_pairs, const std::vector<double>& depth,
+                   const std::vector<double>& normal, const std::vector<double>& pos, size_t p, Contact& c);
 int default_device();
 
 struct DescBuilder {
@@ -346,7 +349,9 @@ class FCLModel {
   FCLModel() = default;
   void dfs(const UrdfModel& urdf, const std::string& link, const std::string& parent, bool convex);
   void build_pairs_from_parents();
-  std::vector<uint32_t> run_pairs(const CollisionRequest& req) const;
+  // pair masks; with req.enable_contact also depth[P], normal[P*3], pos[P*3]
+  std::vector<uint32_t> run_pairs(const CollisionRequest& req, std::vector<double>* depth = nullptr,
+                                  std::vector<double>* normal = nullptr, std::vector<double>* pos = nullptr) const;
   std::vector<Vec7> current_link_poses() const;
 
   std::vector<ObjPtr> objects_;

@@ -322,14 +322,21 @@ std::shared_ptr<Convex> load_mesh_as_convex(const std::string& path, const Vec3&
 // ---------------------------------------------------------------------------
 void CollisionRequest::check_supported() const {
   if (num_max_contacts == 0) throw std::invalid_argument("CollisionRequest.num_max_contacts must be >= 1");
-  if (enable_contact)
-    throw std::logic_error(
-        "NotImplemented: enable_contact=True (libccd MPR penetration depth/normal) is not implemented on the "
-        "device yet");
   if (gjk_solver_type != GST_LIBCCD)
     throw std::logic_error("NotImplemented: only gjk_solver_type=GST_LIBCCD is implemented on the device");
   if (enable_cost) throw std::logic_error("NotImplemented: enable_cost=True is not implemented on the device");
   if (!(gjk_tolerance > 0)) throw std::invalid_argument("gjk_tolerance must be > 0");
+}
+
+void fill_contacts(const uint32_t* mask, size_t n_pairs, const std::vector<double>& depth,
+                   const std::vector<double>& normal, const std::vector<double>& pos, size_t p, Contact& c) {
+  (void)mask;
+  (void)n_pairs;
+  c.penetration_depth = depth[p];
+  for (int k = 0; k < 3; ++k) {
+    c.normal[k] = normal[3 * p + k];
+    c.pos[k] = pos[3 * p + k];
+  }
 }
 
 void check_status(int rc, const char* what) {

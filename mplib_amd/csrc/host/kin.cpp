@@ -488,7 +488,8 @@ const std::vector<ObjPtr>& FCLModel::get_collision_objects() const {
   return objects_;
 }
 
-std::vector<uint32_t> FCLModel::run_pairs(const CollisionRequest& req) const {
+std::vector<uint32_t> FCLModel::run_pairs(const CollisionRequest& req, std::vector<double>* depth,
+                                          std::vector<double>* normal, std::vector<double>* pos) const {
   req.check_supported();
   const uint64_t key = structure_version_ * 1000003ull + (uint64_t)std::llround(req.gjk_tolerance * 1e15);
   if (!world_ || world_key_ != key) {
@@ -517,6 +518,16 @@ std::vector<uint32_t> FCLModel::run_pairs(const CollisionRequest& req) const {
     for (int k = 0; k < 7; ++k) flat.push_back(poses[l][k]);
   uint8_t flag = 0;
   std::vector<uint32_t> mask(world_->info().mask_words, 0);
+  if (req.enable_contact && depth) {
+    const size_t P = pairs_.size();
+    depth->assign(std::max<size_t>(P, 1), 0.0);
+    normal->assign(3 * std::max<size_t>(P, 1), 0.0);
+    pos->assign(3 * std::max<size_t>(P, 1), 0.0);
+    check_status(mpg_collide_contacts(world_->get(), flat.data(), 1, MPG_INPUT_LINK_POSES, &flag, mask.data(),
+                                      depth->data(), normal->data(), pos->data(), MPG_MEM_HOST, nullptr),
+                 "mpg_collide_contacts");
+    return mask;
+  }
   check_status(mpg_collide_link_poses(world_->get(), flat.data(), 1, &flag, mask.data(), MPG_MEM_HOST, nullptr),
                "mpg_collide_link_poses");
   return mask;
@@ -530,13 +541,15 @@ bool FCLModel::collide(const CollisionRequest& req) const {
 }
 
 std::vector<CollisionResult> FCLModel::collide_full(const CollisionRequest& req) const {
-  auto m = run_pairs(req);
+  std::vector<double> depth, normal, pos;
+  auto m = run_pairs(req, &depth, &normal, &pos);
   std::vector<CollisionResult> out(pairs_.size());
   for (size_t p = 0; p < pairs_.size(); ++p)
     if ((m[p >> 5] >> (p & 31)) & 1u) {
       Contact c;
       c.o1 = objects_[pairs_[p].first]->geom;
       c.o2 = objects_[pairs_[p].second]->geom;
+      if (req.enable_contact) fill_contacts(m.data(), pairs_.size(), depth, normal, pos, p, c);
       out[p].contacts.push_back(c);
     }
   return out;

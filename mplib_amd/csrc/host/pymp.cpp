@@ -264,13 +264,26 @@ PYBIND11_MODULE(pymp, m_all) {
         const double pose[7] = {0, 0, 0, 1, 0, 0, 0};
         uint8_t flag = 0;
         uint32_t mask = 0;
-        check_status(mpg_collide_link_poses(w.get(), pose, 1, &flag, &mask, MPG_MEM_HOST, nullptr),
-                     "mpg_collide_link_poses");
+        double depth = 0, normal[3] = {0, 0, 0}, pos[3] = {0, 0, 0};
+        if (req.enable_contact)
+          check_status(mpg_collide_contacts(w.get(), pose, 1, MPG_INPUT_LINK_POSES, &flag, &mask, &depth, normal, pos,
+                                            MPG_MEM_HOST, nullptr),
+                       "mpg_collide_contacts");
+        else
+          check_status(mpg_collide_link_poses(w.get(), pose, 1, &flag, &mask, MPG_MEM_HOST, nullptr),
+                       "mpg_collide_link_poses");
         CollisionResult r;
         if (flag) {
           Contact c;
           c.o1 = o1->geom;
           c.o2 = o2->geom;
+          if (req.enable_contact) {
+            c.penetration_depth = depth;
+            for (int k = 0; k < 3; ++k) {
+              c.normal[k] = normal[k];
+              c.pos[k] = pos[k];
+            }
+          }
           r.contacts.push_back(c);
         }
         return r;

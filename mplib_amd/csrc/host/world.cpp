@@ -524,15 +524,28 @@ std::vector<WorldCollisionResult> PlanningWorld::run_scalar(const CollisionReque
   std::vector<double> s = current_state();
   uint8_t flag = 0;
   std::vector<uint32_t> mask(world_->info().mask_words, 0);
-  check_status(mpg_collide_batch(world_->get(), s.data(), 1, &flag, mask.data(), MPG_MEM_HOST, nullptr),
-               "mpg_collide_batch");
+  std::vector<double> depth, normal, pos;
+  if (r.enable_contact) {
+    const size_t P = std::max<size_t>(pairs_.size(), 1);
+    depth.assign(P, 0.0);
+    normal.assign(3 * P, 0.0);
+    pos.assign(3 * P, 0.0);
+    check_status(mpg_collide_contacts(world_->get(), s.data(), 1, MPG_INPUT_Q, &flag, mask.data(), depth.data(),
+                                      normal.data(), pos.data(), MPG_MEM_HOST, nullptr),
+                 "mpg_collide_contacts");
+  } else {
+    check_status(mpg_collide_batch(world_->get(), s.data(), 1, &flag, mask.data(), MPG_MEM_HOST, nullptr),
+                 "mpg_collide_batch");
+  }
   std::vector<WorldCollisionResult> out;
   for (size_t p = 0; p < pairs_.size(); ++p) {
     const PairInfo& pi = pairs_[p];
     if ((pi.self && !self) || (!pi.self && !others)) continue;
     if ((mask[p >> 5] >> (p & 31)) & 1u) {
       WorldCollisionResult w;
-      w.res.contacts.push_back(Contact{});
+      Contact c;
+      if (r.enable_contact) fill_contacts(mask.data(), pairs_.size(), depth, normal, pos, p, c);
+      w.res.contacts.push_back(c);
       w.collision_type = pi.collision_type;
       w.object_name1 = pi.object_name1;
       w.object_name2 = pi.object_name2;

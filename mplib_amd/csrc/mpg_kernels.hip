@@ -1166,6 +1166,250 @@ __global__ __launch_bounds__(128) void distance_kernel(DevWorld w, const double*
   p_others[cfg] = bp[1];
 }
 
+// ---------------------------------------------------------------------------
+// Contacts: CollisionRequest(enable_contact=True) -> FCL GJKCollide ->
+// libccd 2.1 ccdMPRPenetration (discoverPortal, refinePortal, findPenetr /
+// findPenetrTouch / findPenetrSegment, findPos; max_iterations 500), the same
+// restatement as oracle/collide_oracle.c mpr_penetration.  Runs after the
+// collide pipeline on the pairs it reported, one lane per candidate; the
+// portal keeps each vertex's per-object support points (v1, v2) for findPos.
+// ---------------------------------------------------------------------------
+struct SupP {
+  V3 v, v1, v2;
+};
+
+__device__ __forceinline__ SupP msupport3(const DevWorld& w, cptr<double> HV, const GObj& a, const GObj& b,
+                                          const V3& dir) {
+  SupP s;
+  s.v1 = support(w, HV, a, dir);
+  s.v2 = support(w, HV, b, vscale(dir, -1.0));
+  s.v = vsub(s.v1, s.v2);
+  return s;
+}
+
+__device__ __forceinline__ V3 portal_dir3(const SupP P[4]) {
+  return vnormalize(vcross(vsub(P[2].v, P[1].v), vsub(P[3].v, P[1].v)));
+}
+
+__device__ __forceinline__ bool reach_tol(const SupP P[4], const V3& v4, const V3& dir, double tol) {
+  const double dv1 = vdot(P[1].v, dir), dv2 = vdot(P[2].v, dir), dv3 = vdot(P[3].v, dir), dv4 = vdot(v4, dir);
+  double d1 = dv4 - dv1;
+  const double d2 = dv4 - dv2, d3 = dv4 - dv3;
+  d1 = (d1 < d2) ? d1 : d2;
+  d1 = (d1 < d3) ? d1 : d3;
+  return ccd_eq(d1, tol) || d1 < tol;
+}
+
+__device__ __forceinline__ void expand3(SupP P[4], const SupP& v4) {
+  const V3 v4v0 = vcross(v4.v, P[0].v);
+  if (vdot(P[1].v, v4v0) > 0.0) {
+    if (vdot(P[2].v, v4v0) > 0.0) P[1] = v4;
+    else P[3] = v4;
+  } else {
+    if (vdot(P[3].v, v4v0) > 0.0) P[2] = v4;
+    else P[1] = v4;
+  }
+}
+
+__device__ __forceinline__ double seg_dist2(const V3& x0, const V3& b, V3& wit) {
+  const V3 d = vsub(b, x0), a = x0;  // P = origin
+  double t = -1.0 * vdot(a, d);
+  t /= vdot(d, d);
+  if (t < 0.0 || is_zero(t)) {
+    wit = x0;
+  } else if (t > 1.0 || ccd_eq(t, 1.0)) {
+    wit = b;
+  } else {
+    wit = vadd(vscale(d, t), x0);
+  }
+  return vdot(wit, wit);
+}
+
+// ccdVec3PointTriDist2(origin, x0, B, C, witness)
+__device__ __forceinline__ double tri_dist2(const V3& x0, const V3& B, const V3& C, V3& wit) {
+  const V3 d1 = vsub(B, x0), d2 = vsub(C, x0), a = x0;
+  const double v = vdot(d1, d1), w_ = vdot(d2, d2), p = vdot(a, d1), q = vdot(a, d2), r = vdot(d1, d2);
+  const double d = w_ * v - r * r;
+  double s, t;
+  if (is_zero(d)) {
+    s = t = -1.0;
+  } else {
+    s = (q * r - w_ * p) / d;
+    t = (-s * r - q) / w_;
+  }
+  if ((is_zero(s) || s > 0.0) && (ccd_eq(s, 1.0) || s < 1.0) && (is_zero(t) || t > 0.0) && (ccd_eq(t, 1.0) || t < 1.0) &&
+      (ccd_eq(t + s, 1.0) || t + s < 1.0)) {
+    wit = vadd(vadd(x0, vscale(d1, s)), vscale(d2, t));
+    return vdot(wit, wit);
+  }
+  V3 w2;
+  double dist = seg_dist2(x0, B, wit);
+  double dist2 = seg_dist2(x0, C, w2);
+  if (dist2 < dist) {
+    dist = dist2;
+    wit = w2;
+  }
+  dist2 = seg_dist2(B, C, w2);
+  if (dist2 < dist) {
+    dist = dist2;
+    wit = w2;
+  }
+  return dist;
+}
+
+__device__ __forceinline__ V3 find_pos3(const SupP P[4]) {
+  const V3 dir = portal_dir3(P);
+  double b[4];
+  b[0] = vdot(vcross(P[1].v, P[2].v), P[3].v);
+  b[1] = vdot(vcross(P[3].v, P[2].v), P[0].v);
+  b[2] = vdot(vcross(P[0].v, P[1].v), P[3].v);
+  b[3] = vdot(vcross(P[2].v, P[1].v), P[0].v);
+  double sum = b[0] + b[1] + b[2] + b[3];
+  if (is_zero(sum) || sum < 0.0) {
+    b[0] = 0.0;
+    b[1] = vdot(vcross(P[2].v, P[3].v), dir);
+    b[2] = vdot(vcross(P[3].v, P[1].v), dir);
+    b[3] = vdot(vcross(P[1].v, P[2].v), dir);
+    sum = b[1] + b[2] + b[3];
+  }
+  const double inv = 1.0 / sum;
+  V3 p1{0, 0, 0}, p2{0, 0, 0};
+  for (int i = 0; i < 4; ++i) {
+    p1 = vadd(p1, vscale(P[i].v1, b[i]));
+    p2 = vadd(p2, vscale(P[i].v2, b[i]));
+  }
+  p1 = vscale(p1, inv);
+  p2 = vscale(p2, inv);
+  return vscale(vadd(p1, p2), 0.5);
+}
+
+// ccdMPRPenetration: true if penetrating (depth, dir, pos set)
+__device__ bool mpr_penetration(const DevWorld& w, cptr<double> HV, const GObj& A, const GObj& B, double& depth,
+                                V3& dir_out, V3& pos_out) {
+  SupP P[4];
+  P[0].v1 = center(w, A);
+  P[0].v2 = center(w, B);
+  P[0].v = vsub(P[0].v1, P[0].v2);
+  if (vec_is_origin(P[0].v)) P[0].v = vadd(P[0].v, mpg::v3(kCcdEps * 10.0, 0.0, 0.0));
+  V3 dir = vnormalize(vscale(P[0].v, -1.0));
+  P[1] = msupport3(w, HV, A, B, dir);
+  double dot = vdot(P[1].v, dir);
+  if (is_zero(dot) || dot < 0.0) return false;
+  dir = vcross(P[0].v, P[1].v);
+  if (is_zero(vdot(dir, dir))) {
+    pos_out = vscale(vadd(P[1].v1, P[1].v2), 0.5);
+    if (vec_is_origin(P[1].v)) {  // findPenetrTouch
+      depth = 0.0;
+      dir_out = mpg::v3(0.0, 0.0, 0.0);
+    } else {  // findPenetrSegment
+      dir_out = P[1].v;
+      depth = std::sqrt(vdot(dir_out, dir_out));
+      dir_out = vnormalize(dir_out);
+    }
+    return true;
+  }
+  dir = vnormalize(dir);
+  P[2] = msupport3(w, HV, A, B, dir);
+  dot = vdot(P[2].v, dir);
+  if (is_zero(dot) || dot < 0.0) return false;
+  dir = vnormalize(vcross(vsub(P[1].v, P[0].v), vsub(P[2].v, P[0].v)));
+  if (vdot(dir, P[0].v) > 0.0) {
+    const SupP t = P[1];
+    P[1] = P[2];
+    P[2] = t;
+    dir = vscale(dir, -1.0);
+  }
+  for (;;) {
+    P[3] = msupport3(w, HV, A, B, dir);
+    dot = vdot(P[3].v, dir);
+    if (is_zero(dot) || dot < 0.0) return false;
+    bool cont = false;
+    double d2 = vdot(vcross(P[1].v, P[3].v), P[0].v);
+    if (d2 < 0.0 && !is_zero(d2)) {
+      P[2] = P[3];
+      cont = true;
+    }
+    if (!cont) {
+      d2 = vdot(vcross(P[3].v, P[2].v), P[0].v);
+      if (d2 < 0.0 && !is_zero(d2)) {
+        P[1] = P[3];
+        cont = true;
+      }
+    }
+    if (!cont) break;
+    dir = vnormalize(vcross(vsub(P[1].v, P[0].v), vsub(P[2].v, P[0].v)));
+  }
+  // refinePortal
+  for (;;) {
+    dir = portal_dir3(P);
+    const double d = vdot(dir, P[1].v);
+    if (is_zero(d) || d > 0.0) break;
+    const SupP v4 = msupport3(w, HV, A, B, dir);
+    const double dv4 = vdot(v4.v, dir);
+    if (!(is_zero(dv4) || dv4 > 0.0) || reach_tol(P, v4.v, dir, w.mpr_tol)) return false;
+    expand3(P, v4);
+  }
+  // findPenetr
+  for (unsigned long it = 0;; ++it) {
+    dir = portal_dir3(P);
+    const SupP v4 = msupport3(w, HV, A, B, dir);
+    if (reach_tol(P, v4.v, dir, w.mpr_tol) || it > 500UL) {
+      V3 wit;
+      depth = std::sqrt(tri_dist2(P[1].v, P[2].v, P[3].v, wit));
+      dir_out = is_zero(depth) ? mpg::v3(0.0, 0.0, 0.0) : vnormalize(wit);
+      pos_out = find_pos3(P);
+      return true;
+    }
+    expand3(P, v4);
+  }
+}
+
+template <bool FROM_POSES>
+__global__ __launch_bounds__(256) void contact_kernel(DevWorld w, const double* __restrict__ in,
+                                                     const uint32_t* __restrict__ seg_len,
+                                                     const uint32_t* __restrict__ seg_start,
+                                                     const uint32_t* __restrict__ prefix,
+                                                     const uint32_t* __restrict__ cand,
+                                                     const uint32_t* __restrict__ masks, const double* __restrict__ sc,
+                                                     double* __restrict__ depth, double* __restrict__ normal,
+                                                     double* __restrict__ pos) {
+  const cptr<double> HV = w.hull;
+  const uint32_t lane = lane_id();
+  const uint32_t wave = __builtin_amdgcn_readfirstlane((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+  const uint32_t n_waves = (gridDim.x * blockDim.x) >> 6;
+  const uint32_t total = prefix[w.n_pairs];
+  for (uint32_t tk = wave; tk < total; tk += n_waves) {
+    int lo = 0, hi = w.n_pairs;
+    while (hi - lo > 1) {
+      const int mid = (lo + hi) >> 1;
+      if (prefix[mid] <= tk) lo = mid;
+      else hi = mid;
+    }
+    const int p = lo;
+    const uint32_t t0 = (tk - prefix[p]) * kTask, t1 = min(seg_len[p], t0 + kTask);
+    const int a = w.pair_a[p], b = w.pair_b[p];
+    for (uint32_t base = t0; base < t1; base += 64) {
+      const uint32_t idx = base + lane;
+      if (idx >= t1) continue;
+      const long long c = cand[seg_start[p] + idx];
+      if (!((masks[c * w.W + (p >> 5)] >> (p & 31)) & 1u)) continue;
+      const GObj A = a < w.n_moving ? moving_obj<FROM_POSES>(w, in, sc, c, a) : static_obj(w, a - w.n_moving);
+      const GObj B = b < w.n_moving ? moving_obj<FROM_POSES>(w, in, sc, c, b) : static_obj(w, b - w.n_moving);
+      double dp = 0.0;
+      V3 nd{0, 0, 0}, ps{0, 0, 0};
+      mpr_penetration(w, HV, A, B, dp, nd, ps);
+      const size_t k = (size_t)c * w.n_pairs + p;
+      depth[k] = dp;
+      normal[3 * k] = nd.x;
+      normal[3 * k + 1] = nd.y;
+      normal[3 * k + 2] = nd.z;
+      pos[3 * k] = ps.x;
+      pos[3 * k + 1] = ps.y;
+      pos[3 * k + 2] = ps.z;
+    }
+  }
+}
+
 __global__ void fk_kernel(DevWorld w, const double* __restrict__ q, long long n, double* __restrict__ out) {
   const long long cfg = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (cfg >= n) return;
@@ -1318,6 +1562,7 @@ struct mpg_world {
     size_t flags_cap = 0;
   } motion;
   std::mutex motion_mu;
+  bool has_closed_form = false;  // a non-allowed pair uses an FCL closed form
   // batched distance buffers (grow-only)
   struct Dist {
     double* poses = nullptr;
@@ -1601,8 +1846,13 @@ struct StageTimer {
   ~StageTimer() { stop(); }
 };
 
+struct ContactOut {
+  double *depth, *normal, *pos;  // [n*P], [n*P*3], [n*P*3]
+};
+
 template <bool FROM_POSES>
-int launch_collide(mpg_world* w, const double* in, long long n, uint8_t* flags, uint32_t* masks, hipStream_t stream) {
+int launch_collide(mpg_world* w, const double* in, long long n, uint8_t* flags, uint32_t* masks, hipStream_t stream,
+                   const ContactOut* co = nullptr) {
   if (n == 0) return MPG_OK;
   const long long chunk = std::min<long long>(n, w->max_chunk);
   mpg_world::Workspace* ws = nullptr;
@@ -1658,6 +1908,16 @@ int launch_collide(mpg_world* w, const double* in, long long n, uint8_t* flags, 
     hipLaunchKernelGGL((narrow_kernel<FROM_POSES>), dim3(nb), dim3(256), 0, stream, w->dw, qin, ws->seg_len,
                        ws->seg_start, ws->prefix, ws->cand, fl, mk, ws->prefix + w->dw.n_pairs + 1, ws->sc);
     HIP_TRY(hipGetLastError());
+    if (co) {  // penetration info of the reported pairs (enable_contact)
+      const size_t P = (size_t)w->dw.n_pairs;
+      HIP_TRY(hipMemsetAsync(co->depth + off * P, 0, sizeof(double) * m * P, stream));
+      HIP_TRY(hipMemsetAsync(co->normal + off * P * 3, 0, sizeof(double) * m * P * 3, stream));
+      HIP_TRY(hipMemsetAsync(co->pos + off * P * 3, 0, sizeof(double) * m * P * 3, stream));
+      hipLaunchKernelGGL((contact_kernel<FROM_POSES>), dim3(nb), dim3(256), 0, stream, w->dw, qin, ws->seg_len,
+                         ws->seg_start, ws->prefix, ws->cand, mk, ws->sc, co->depth + off * P, co->normal + off * P * 3,
+                         co->pos + off * P * 3);
+      HIP_TRY(hipGetLastError());
+    }
   }
   return MPG_OK;
 }
@@ -1935,6 +2195,7 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
   dw.pair_b = to_cptr<int>(base + o_pb);
   dw.pair_allowed = to_cptr<int>(base + o_al);
   dw.pair_cf = to_cptr<int>(base + o_cf);
+  for (int p = 0; p < d->n_pairs; ++p) w->has_closed_form |= pair_cf[p] != CF_NONE && !allowed[p];
   dw.static_T = to_cptr<double>(base + o_sT);
   dw.link_chain_start = to_cptr<int>(base + o_cs);
   dw.link_chain_len = to_cptr<int>(base + o_cl);
@@ -2207,6 +2468,65 @@ int mpg_distance_batch(mpg_world* w, const double* q, int64_t n, int32_t n_self_
     HIP_TRY(hipStreamSynchronize(s));
   }
   return MPG_OK;
+}
+
+int mpg_collide_contacts(mpg_world* w, const double* input, int64_t n, int input_kind, uint8_t* flags,
+                         uint32_t* pair_mask, double* depth, double* normal, double* pos, int mem, void* stream) {
+  if (!w) return set_error(MPG_E_INVALID, "world is NULL");
+  if (n < 0) return set_error(MPG_E_INVALID, "n < 0");
+  if (input_kind != MPG_INPUT_Q && input_kind != MPG_INPUT_LINK_POSES) return set_error(MPG_E_INVALID, "bad input_kind");
+  const bool poses = input_kind == MPG_INPUT_LINK_POSES;
+  const size_t row = poses ? (size_t)w->dw.n_links * 7 : (size_t)w->dw.dof;
+  if (n > 0 && ((!input && row > 0) || !flags || !pair_mask || !depth || !normal || !pos))
+    return set_error(MPG_E_INVALID, "NULL buffer");
+  if (mem != MPG_MEM_HOST && mem != MPG_MEM_DEVICE) return set_error(MPG_E_INVALID, "bad mem kind");
+  if (w->has_closed_form)
+    return set_error(MPG_E_UNSUPPORTED,
+                     "contacts for FCL closed-form pairs (box-box, sphere-sphere, sphere-box) are not implemented");
+  if (n == 0) return MPG_OK;
+  HIP_TRY(hipSetDevice(w->device));
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const size_t P = (size_t)w->dw.n_pairs, W = (size_t)w->dw.W;
+  if (mem == MPG_MEM_DEVICE) {
+    ContactOut co{depth, normal, pos};
+    return poses ? launch_collide<true>(w, input, n, flags, pair_mask, s, &co)
+                 : launch_collide<false>(w, input, n, flags, pair_mask, s, &co);
+  }
+  // host buffers: temporary device copies
+  double *d_in = nullptr, *d_out = nullptr;
+  uint8_t* d_fl = nullptr;
+  uint32_t* d_mk = nullptr;
+  auto cleanup = [&]() {
+    hipFree(d_in);
+    hipFree(d_out);
+    hipFree(d_fl);
+    hipFree(d_mk);
+  };
+  int rc = MPG_OK;
+  do {
+    if (hipMalloc(&d_in, sizeof(double) * std::max<size_t>(1, row * n)) != hipSuccess ||
+        hipMalloc(&d_out, sizeof(double) * 7 * P * n) != hipSuccess || hipMalloc(&d_fl, n) != hipSuccess ||
+        hipMalloc(&d_mk, sizeof(uint32_t) * W * n) != hipSuccess) {
+      rc = set_error(MPG_E_NOMEM, "contact staging buffers");
+      break;
+    }
+    if (row && hipMemcpyAsync(d_in, input, sizeof(double) * row * n, hipMemcpyHostToDevice, s) != hipSuccess) {
+      rc = set_error(MPG_E_HIP, "copy input");
+      break;
+    }
+    ContactOut co{d_out, d_out + P * n, d_out + 4 * P * n};
+    rc = poses ? launch_collide<true>(w, d_in, n, d_fl, d_mk, s, &co) : launch_collide<false>(w, d_in, n, d_fl, d_mk, s, &co);
+    if (rc) break;
+    if (hipMemcpyAsync(flags, d_fl, n, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipMemcpyAsync(pair_mask, d_mk, sizeof(uint32_t) * W * n, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipMemcpyAsync(depth, co.depth, sizeof(double) * P * n, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipMemcpyAsync(normal, co.normal, sizeof(double) * 3 * P * n, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipMemcpyAsync(pos, co.pos, sizeof(double) * 3 * P * n, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess)
+      rc = set_error(MPG_E_HIP, "copy contact results");
+  } while (false);
+  cleanup();
+  return rc;
 }
 
 int mpg_fk_batch(mpg_world* w, const double* q, int64_t n, double* link_pose, int mem, void* stream) {

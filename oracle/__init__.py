@@ -51,6 +51,8 @@ def lib():
         _lib.orc_collide_pair.restype = ctypes.c_int
         _lib.orc_distance_pair.restype = ctypes.c_double
         _lib.orc_distance_batch.restype = ctypes.c_int
+        _lib.orc_contact_pair.restype = ctypes.c_int
+        _lib.orc_contact_batch.restype = ctypes.c_int
     return _lib
 
 
@@ -278,6 +280,20 @@ class OracleWorld:
         if rc != 0:
             raise RuntimeError("orc_distance_batch failed")
         return ds, ps, do, po
+
+    def contact_batch(self, q: np.ndarray):
+        """fcl::collide with CollisionRequest(enable_contact=True) on every pair:
+        (hit[n, P], depth[n, P], normal[n, P, 3], pos[n, P, 3])."""
+        q = np.ascontiguousarray(q, dtype=np.float64).reshape(-1, self.dof)
+        n, P = q.shape[0], len(self.pairs)
+        hit = np.zeros((n, P), np.uint8)
+        depth = np.zeros((n, P))
+        normal = np.zeros((n, P, 3))
+        pos = np.zeros((n, P, 3))
+        lib().orc_contact_batch(ctypes.byref(self._w), q.ctypes.data_as(_DP), ctypes.c_long(n),
+                                hit.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), depth.ctypes.data_as(_DP),
+                                normal.ctypes.data_as(_DP), pos.ctypes.data_as(_DP))
+        return hit, depth, normal, pos
 
     def pair_names(self) -> List[Tuple[str, str]]:
         return [(p[4], p[5]) for p in self.pairs]

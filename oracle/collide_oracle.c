@@ -609,6 +609,159 @@ static int mpr_intersect(const gjk_obj *o1, const gjk_obj *o2, real tol) {
     return res == 0 ? 1 : 0;
 }
 
+/* ------------------------------------------------ libccd 2.1 ccdMPRPenetration
+ * (mpr.c findPenetr / findPenetrTouch / findPenetrSegment / findPos, vec3.c
+ * ccdVec3PointTriDist2 / __ccdVec3PointSegmentDist2), as FCL 0.7.0's
+ * GJKCollide runs it for CollisionRequest(enable_contact=True):
+ * max_iterations = 500 (GJKSolver_libccd::max_collision_iterations),
+ * mpr_tolerance = gjk_tolerance.  dir points from object 1 to object 2. */
+static real point_segment_dist2(const ccd_vec3_t *P, const ccd_vec3_t *x0, const ccd_vec3_t *b, ccd_vec3_t *witness) {
+    ccd_vec3_t d, a;
+    real t, dist;
+    ccdVec3Sub2(&d, b, x0);
+    ccdVec3Sub2(&a, x0, P);
+    t = -1.0 * ccdVec3Dot(&a, &d);
+    t /= ccdVec3Len2(&d);
+    if (t < 0.0 || ccdIsZero(t)) {
+        ccd_vec3_t e; ccdVec3Sub2(&e, x0, P); dist = ccdVec3Len2(&e);
+        ccdVec3Copy(witness, x0);
+    } else if (t > 1.0 || ccdEq(t, 1.0)) {
+        ccd_vec3_t e; ccdVec3Sub2(&e, b, P); dist = ccdVec3Len2(&e);
+        ccdVec3Copy(witness, b);
+    } else {
+        ccdVec3Copy(witness, &d);
+        ccdVec3Scale(witness, t);
+        ccdVec3Add(witness, x0);
+        ccd_vec3_t e; ccdVec3Sub2(&e, witness, P); dist = ccdVec3Len2(&e);
+    }
+    return dist;
+}
+
+static real point_tri_dist2(const ccd_vec3_t *P, const ccd_vec3_t *x0, const ccd_vec3_t *B, const ccd_vec3_t *C,
+                            ccd_vec3_t *witness) {
+    ccd_vec3_t d1, d2, a, witness2;
+    real u, v, w, p, q, r, d, s, t, dist, dist2;
+    ccdVec3Sub2(&d1, B, x0);
+    ccdVec3Sub2(&d2, C, x0);
+    ccdVec3Sub2(&a, x0, P);
+    u = ccdVec3Dot(&a, &a);
+    v = ccdVec3Dot(&d1, &d1);
+    w = ccdVec3Dot(&d2, &d2);
+    p = ccdVec3Dot(&a, &d1);
+    q = ccdVec3Dot(&a, &d2);
+    r = ccdVec3Dot(&d1, &d2);
+    (void)u;
+    d = w * v - r * r;
+    if (ccdIsZero(d)) {
+        s = t = -1.0;
+    } else {
+        s = (q * r - w * p) / d;
+        t = (-s * r - q) / w;
+    }
+    if ((ccdIsZero(s) || s > 0.0) && (ccdEq(s, 1.0) || s < 1.0) && (ccdIsZero(t) || t > 0.0) &&
+        (ccdEq(t, 1.0) || t < 1.0) && (ccdEq(t + s, 1.0) || t + s < 1.0)) {
+        ccdVec3Scale(&d1, s);
+        ccdVec3Scale(&d2, t);
+        ccdVec3Copy(witness, x0);
+        ccdVec3Add(witness, &d1);
+        ccdVec3Add(witness, &d2);
+        ccd_vec3_t e; ccdVec3Sub2(&e, witness, P); dist = ccdVec3Len2(&e);
+    } else {
+        dist = point_segment_dist2(P, x0, B, witness);
+        dist2 = point_segment_dist2(P, x0, C, &witness2);
+        if (dist2 < dist) { dist = dist2; ccdVec3Copy(witness, &witness2); }
+        dist2 = point_segment_dist2(P, B, C, &witness2);
+        if (dist2 < dist) { dist = dist2; ccdVec3Copy(witness, &witness2); }
+    }
+    return dist;
+}
+
+static void find_pos(const ccd_simplex_t *portal, ccd_vec3_t *pos) {
+    ccd_vec3_t dir, vec, p1, p2;
+    real b[4], sum, inv;
+    portal_dir(portal, &dir);
+    ccdVec3Cross(&vec, &portal->ps[1].v, &portal->ps[2].v);
+    b[0] = ccdVec3Dot(&vec, &portal->ps[3].v);
+    ccdVec3Cross(&vec, &portal->ps[3].v, &portal->ps[2].v);
+    b[1] = ccdVec3Dot(&vec, &portal->ps[0].v);
+    ccdVec3Cross(&vec, &portal->ps[0].v, &portal->ps[1].v);
+    b[2] = ccdVec3Dot(&vec, &portal->ps[3].v);
+    ccdVec3Cross(&vec, &portal->ps[2].v, &portal->ps[1].v);
+    b[3] = ccdVec3Dot(&vec, &portal->ps[0].v);
+    sum = b[0] + b[1] + b[2] + b[3];
+    if (ccdIsZero(sum) || sum < 0.0) {
+        b[0] = 0.0;
+        ccdVec3Cross(&vec, &portal->ps[2].v, &portal->ps[3].v);
+        b[1] = ccdVec3Dot(&vec, &dir);
+        ccdVec3Cross(&vec, &portal->ps[3].v, &portal->ps[1].v);
+        b[2] = ccdVec3Dot(&vec, &dir);
+        ccdVec3Cross(&vec, &portal->ps[1].v, &portal->ps[2].v);
+        b[3] = ccdVec3Dot(&vec, &dir);
+        sum = b[1] + b[2] + b[3];
+    }
+    inv = 1.0 / sum;
+    ccdVec3Set(&p1, 0.0, 0.0, 0.0);
+    ccdVec3Set(&p2, 0.0, 0.0, 0.0);
+    for (int i = 0; i < 4; ++i) {
+        ccdVec3Copy(&vec, &portal->ps[i].v1);
+        ccdVec3Scale(&vec, b[i]);
+        ccdVec3Add(&p1, &vec);
+        ccdVec3Copy(&vec, &portal->ps[i].v2);
+        ccdVec3Scale(&vec, b[i]);
+        ccdVec3Add(&p2, &vec);
+    }
+    ccdVec3Scale(&p1, inv);
+    ccdVec3Scale(&p2, inv);
+    ccdVec3Copy(pos, &p1);
+    ccdVec3Add(pos, &p2);
+    ccdVec3Scale(pos, 0.5);
+}
+
+/* 1 = penetrating (depth/dir/pos set), 0 = separated */
+static int mpr_penetration(const gjk_obj *o1, const gjk_obj *o2, real tol, real *depth, real dir_out[3],
+                           real pos_out[3]) {
+    ccd_simplex_t portal;
+    ccd_vec3_t dir, pos;
+    int res = discover_portal(o1, o2, &portal);
+    if (res < 0) return 0;
+    if (res == 1) { /* findPenetrTouch */
+        *depth = 0.0;
+        ccdVec3Set(&dir, 0.0, 0.0, 0.0);
+        ccdVec3Copy(&pos, &portal.ps[1].v1);
+        ccdVec3Add(&pos, &portal.ps[1].v2);
+        ccdVec3Scale(&pos, 0.5);
+    } else if (res == 2) { /* findPenetrSegment */
+        ccdVec3Copy(&pos, &portal.ps[1].v1);
+        ccdVec3Add(&pos, &portal.ps[1].v2);
+        ccdVec3Scale(&pos, 0.5);
+        ccdVec3Copy(&dir, &portal.ps[1].v);
+        *depth = sqrt(ccdVec3Len2(&dir));
+        ccdVec3Normalize(&dir);
+    } else {
+        if (refine_portal(o1, o2, &portal, tol) < 0) return 0;
+        /* findPenetr */
+        unsigned long iterations = 0;
+        ccd_support_t v4;
+        for (;;) {
+            portal_dir(&portal, &dir);
+            ccd_support(o1, o2, &dir, &v4);
+            if (portal_reach_tolerance(&portal, &v4, &dir, tol) || iterations > 500UL) {
+                ccd_vec3_t origin;
+                ccdVec3Set(&origin, 0.0, 0.0, 0.0);
+                *depth = sqrt(point_tri_dist2(&origin, &portal.ps[1].v, &portal.ps[2].v, &portal.ps[3].v, &dir));
+                if (ccdIsZero(*depth)) ccdVec3Set(&dir, 0.0, 0.0, 0.0);
+                else ccdVec3Normalize(&dir);
+                find_pos(&portal, &pos);
+                break;
+            }
+            expand_portal(&portal, &v4);
+            iterations++;
+        }
+    }
+    for (int i = 0; i < 3; ++i) { dir_out[i] = dir.v[i]; pos_out[i] = pos.v[i]; }
+    return 1;
+}
+
 /* ------------------------------------------------ FCL closed-form pairs
  * GJKSolver_libccd::shapeIntersect routes these shape pairs to closed forms
  * instead of MPR (FCL 0.7.0 gjk_solver_libccd-inl.h specialisations;
@@ -1030,6 +1183,50 @@ int orc_fk_batch(const orc_world *w, const double *q, long n, double *link_pose7
 }
 
 /* Single-pair entry (fcl.collide(o1, o2) on two posed shapes). */
+int orc_contact_pair(const orc_world *w, int ga, const double *Ta, int gb, const double *Tb, double *depth,
+                     double *normal, double *pos) {
+    gjk_obj a, b;
+    make_obj(w, ga, Ta, &a, NULL);
+    make_obj(w, gb, Tb, &b, NULL);
+    return mpr_penetration(&a, &b, 1e-6, depth, normal, pos);
+}
+
+/* every (configuration, pair): penetration of the pairs MPR reports
+ * (enable_contact): hit[n*P], depth[n*P], normal[n*P*3], pos[n*P*3] */
+int orc_contact_batch(const orc_world *w, const double *q, long n, uint8_t *hit, double *depth, double *normal,
+                      double *pos) {
+    real *oMi = malloc(sizeof(real) * 12 * (size_t)(w->nj + 1));
+    real *link_T = malloc(sizeof(real) * 12 * (size_t)(w->n_links + 1));
+    real *obj_T = malloc(sizeof(real) * 12 * (size_t)(w->n_obj + 1));
+    real *att_T = malloc(sizeof(real) * 12 * (size_t)(w->n_att + 1));
+    const int P = w->n_pairs;
+    for (long c = 0; c < n; ++c) {
+        fk_links(w, q + (size_t)c * w->dof, oMi, link_T, NULL);
+        for (int i = 0; i < w->n_obj; ++i) se3_mul(link_T + 12 * w->obj_link[i], w->obj_origin + 12 * i, obj_T + 12 * i);
+        for (int i = 0; i < w->n_att; ++i) se3_mul(link_T + 12 * w->att_link[i], w->att_pose + 12 * i, att_T + 12 * i);
+        for (int p = 0; p < P; ++p) {
+            const size_t k = (size_t)c * P + p;
+            hit[k] = 0;
+            depth[k] = 0.0;
+            for (int i = 0; i < 3; ++i) normal[3 * k + i] = pos[3 * k + i] = 0.0;
+            if (w->p_allowed[p]) continue;
+            int ks[2] = {w->pa_kind[p], w->pb_kind[p]}, is[2] = {w->pa_idx[p], w->pb_idx[p]};
+            gjk_obj o[2];
+            for (int s = 0; s < 2; ++s) {
+                const real *T;
+                int gg;
+                if (ks[s] == KIND_ROBOT) { T = obj_T + 12 * is[s]; gg = w->obj_geom[is[s]]; }
+                else if (ks[s] == KIND_ATTACHED) { T = att_T + 12 * is[s]; gg = w->att_geom[is[s]]; }
+                else { T = w->scene_tf + 12 * is[s]; gg = w->scene_geom[is[s]]; }
+                make_obj(w, gg, T, &o[s], NULL);
+            }
+            hit[k] = (uint8_t)mpr_penetration(&o[0], &o[1], 1e-6, depth + k, normal + 3 * k, pos + 3 * k);
+        }
+    }
+    free(oMi); free(link_T); free(obj_T); free(att_T);
+    return 0;
+}
+
 double orc_distance_pair(const orc_world *w, int ga, const double *Ta, int gb, const double *Tb) {
     gjk_obj a, b;
     make_obj(w, ga, Ta, &a, NULL);

@@ -94,7 +94,7 @@ def test_attached_body_pairs():
 def test_unsupported_requests_raise():
     w, _ = scenes.world(2)
     with pytest.raises(NotImplementedError):
-        w.collide(pymp.fcl.CollisionRequest(enable_contact=True))
+        w.collide(pymp.fcl.CollisionRequest(enable_cost=True))
     with pytest.raises(NotImplementedError):
         w.collide(pymp.fcl.CollisionRequest(gjk_solver_type=pymp.fcl.GJKSolverType.GST_INDEP))
 

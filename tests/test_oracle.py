@@ -223,3 +223,41 @@ def test_distance_batch_semantics():
     assert ((ps >= 0) & (ps < ow.n_self_pairs)).all() and (po >= ow.n_self_pairs).all()
     free = ~coll
     assert (np.minimum(ds, do)[free] > 0).all()
+
+
+# ------------------------------------------------------ MPR penetration (contacts)
+def test_mpr_penetration_box_box_known_answer():
+    """Two unit boxes overlapping by 0.1 along x: libccd's MPR penetration
+    converges to depth 0.1 along +x (object 1 -> object 2), contact point in
+    the overlap slab."""
+    import ctypes
+    import oracle
+    from oracle import model as M
+    P = ctypes.POINTER(ctypes.c_double)
+    hull = M.ConvexGeom(np.array([[x, y, z] for x in (-.5, .5) for y in (-.5, .5) for z in (-.5, .5)]), [])
+    w, (g,) = _pair_world([hull])
+    depth = ctypes.c_double()
+    nrm, pos = np.zeros(3), np.zeros(3)
+    r = oracle.lib().orc_contact_pair(ctypes.byref(w._w), g, _T().ctypes.data_as(P), g,
+                                      _T(p=(0.9, 0.02, 0.01)).ctypes.data_as(P), ctypes.byref(depth),
+                                      nrm.ctypes.data_as(P), pos.ctypes.data_as(P))
+    assert r == 1
+    assert abs(depth.value - 0.1) < 1e-6
+    np.testing.assert_allclose(nrm, [1.0, 0.0, 0.0], atol=1e-6)
+    assert 0.4 - 1e-9 <= pos[0] <= 0.5 + 1e-9
+    r = oracle.lib().orc_contact_pair(ctypes.byref(w._w), g, _T().ctypes.data_as(P), g,
+                                      _T(p=(1.1, 0.0, 0.0)).ctypes.data_as(P), ctypes.byref(depth),
+                                      nrm.ctypes.data_as(P), pos.ctypes.data_as(P))
+    assert r == 0
+
+
+def test_contact_batch_consistent_with_collide():
+    ow = Wd.oracle_world(3)
+    q = Wd.sample_q(ow.art, 200, 6)
+    hit, depth, normal, pos = ow.contact_batch(q)
+    _, masks = ow.collide_batch(q)
+    bits = np.stack([(masks[:, p >> 5] >> (p & 31)) & 1 for p in range(len(ow.pairs))], 1)
+    np.testing.assert_array_equal(hit, bits)  # same MPR discovery/refinement decides
+    nz = depth[hit == 1] > 0
+    np.testing.assert_allclose(np.linalg.norm(normal[hit == 1][nz], axis=1), 1.0, atol=1e-12)
+    assert (depth >= 0).all()
