@@ -39,7 +39,7 @@ def parse():
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--cfg", type=int, default=3, help="BASELINE config (2, 3 or 4)")
-    p.add_argument("--n", type=int, default=0, help="configs per GPU per step (default: BASELINE size)")
+    p.add_argument("--per-gpu", type=int, default=0, help="configs per GPU per step (default: BASELINE size)")
     p.add_argument("--cpu-sample", type=int, default=1 << 17,
                    help="configs timed on the CPU oracle for cpu_baseline (rank 0, N=1 only; 0 = skip)")
     p.add_argument("--cpu-threads", type=int, default=1)
@@ -55,15 +55,23 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # RCCL ("nccl") across GPUs; MPLIB_AMD_DIST_BACKEND=gloo rehearses the
+    # multi-rank flow with several ranks sharing one GPU (tests / 1-GPU boxes)
+    backend = os.environ.get("MPLIB_AMD_DIST_BACKEND", "nccl")
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
+    if backend != "nccl":
+        local = 0
     torch.cuda.set_device(local)
     os.environ["MPLIB_AMD_DEVICE"] = str(local)
 
     from mplib_amd import scenes
 
     cfg = args.cfg
-    n = args.n or (scenes.CFG_N[cfg] if cfg != 4 else (1 << 22) // max(world, 1))
+    n = args.per_gpu or (scenes.CFG_N[cfg] if cfg != 4 else (1 << 22) // max(world, 1))
     w, art = scenes.world(cfg)
     dim = w.get_state_dim()
     W = w.get_mask_words()
@@ -106,14 +114,14 @@ def main():
               "units_per_launch": v[2] / max(v[1], 1)} for k, v in prof.items()}
     if world > 1:
         t = torch.tensor([elapsed, step_ms] + [st[k]["ms_per_launch"] for k in STAGES], dtype=torch.float64,
-                         device=q.device)
+                         device=q.device if backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, step_ms = float(t[0]), float(t[1])
         for i, k in enumerate(STAGES):
             st[k]["ms_per_launch"] = float(t[2 + i])
 
     gather_ms = None
-    if args.gather and world > 1:
+    if args.gather and world > 1 and backend == "nccl":
         out = torch.empty(n * world, dtype=torch.uint8, device=q.device)
         torch.cuda.synchronize()
         g0 = time.perf_counter()

@@ -418,3 +418,58 @@ def test_contacts_scalar_api():
             assert abs(c.penetration_depth - rd[i, p]) < 1e-9
             np.testing.assert_allclose(c.normal, rn[i, p], atol=1e-9)
             np.testing.assert_allclose(c.pos, rp[i, p], atol=1e-9)
+
+
+# ------------------------------------------------------------ scale / streams
+def test_chunked_batch_across_workspace_chunks():
+    """Batches larger than one workspace chunk (2^20 configurations) run as
+    consecutive chunks on the stream; results stay bit-exact."""
+    w, art = scenes.world(2)
+    q = scenes.sample_states(art, (1 << 20) + 4097, 123)
+    f, m = w.collide_batch(q)
+    fo, mo = ow(2).collide_batch(q, nthreads=NTHREADS)
+    np.testing.assert_array_equal(f, fo)
+    np.testing.assert_array_equal(m, mo)
+
+
+def test_concurrent_streams_do_not_share_workspace():
+    torch = pytest.importorskip("torch")
+    d = dw(3)
+    qs = [Wd.sample_q(ow(3).art, 50000, 200 + k) for k in range(3)]
+    streams = [torch.cuda.Stream() for _ in qs]
+    outs = []
+    for q, s in zip(qs, streams):
+        qd = torch.from_numpy(q).cuda()
+        fd = torch.zeros(len(q), dtype=torch.uint8, device="cuda")
+        md = torch.zeros((len(q), d.mask_words), dtype=torch.int32, device="cuda")
+        d.collide_batch(qd, fd, md, stream=s.cuda_stream)
+        outs.append((qd, fd, md))
+    torch.cuda.synchronize()
+    for q, (_, fd, md) in zip(qs, outs):
+        fo, mo = ow(3).collide_batch(q, nthreads=NTHREADS)
+        np.testing.assert_array_equal(fd.cpu().numpy(), fo)
+        np.testing.assert_array_equal(md.cpu().numpy().view(np.uint32), mo)
+
+
+def test_bench_two_ranks_gloo_one_gpu():
+    """bench.py's multi-rank path (barrier, max over ranks, weak scaling) with
+    two ranks sharing this box's GPU over gloo."""
+    import json
+    import socket
+    import subprocess
+    import sys
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, MPLIB_AMD_DIST_BACKEND="gloo")
+    out = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                          "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(root, "bench.py"),
+                          "--gpus", "2", "--steps", "3", "--warmup", "1", "--per-gpu", "65536", "--cpu-sample", "0"],
+                         env=env, capture_output=True, text=True, timeout=600, cwd=root)
+    assert out.returncode == 0, out.stderr[-2000:]
+    line = [l for l in out.stdout.splitlines() if l.startswith("{")][-1]
+    r = json.loads(line)
+    assert r["n_gpus"] == 2 and r["scaling"] == "weak" and r["value"] > 0
+    assert r["config"]["configs_per_gpu"] == 65536
