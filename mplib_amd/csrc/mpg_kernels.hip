@@ -408,6 +408,9 @@ __device__ __forceinline__ uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi
 //      written to surv[word][cfg] at the end (no global atomics).
 // Also zeroes this configuration's outputs for phase B.
 // ---------------------------------------------------------------------------
+#ifndef MPG_NARROW_WAVES
+#define MPG_NARROW_WAVES
+#endif
 #ifndef MPG_TASK
 #define MPG_TASK 128
 #endif
@@ -466,8 +469,8 @@ __global__ __launch_bounds__(BLOCK) void cull_kernel(DevWorld w, const double* _
                                                     double* __restrict__ sc, long long cap) {
   extern __shared__ __attribute__((aligned(16))) float lds_f[];
   float* cen = lds_f;                                                    // [n_moving][3][BLOCK]
-  float* save = cen + (size_t)w.n_moving * 3 * BLOCK;                    // [n_saves][12][BLOCK]
-  uint32_t* survw = reinterpret_cast<uint32_t*>(save + (size_t)w.bp.n_saves * 12 * BLOCK);  // [W][BLOCK]
+  float* save = cen + (size_t)w.n_moving * 3 * BLOCK;  // [n_saves - kRegSaves][12][BLOCK]
+  uint32_t* survw = reinterpret_cast<uint32_t*>(save + (size_t)max(w.bp.n_saves - kRegSaves, 0) * 12 * BLOCK);  // [W][BLOCK]
   const int tid = threadIdx.x;
   uint32_t* queue = survw + (size_t)w.W * BLOCK + (tid >> 6) * kQueue;  // [BLOCK/64][kQueue]
   const uint32_t lane = lane_id();
@@ -671,8 +674,53 @@ __global__ __launch_bounds__(256) void scatter_kernel(const uint32_t* __restrict
 // ---------------------------------------------------------------------------
 enum : int { MPR_DONE = 0, MPR_V1 = 1, MPR_V2 = 2, MPR_V3 = 3, MPR_V4 = 4 };
 
+// FCL closed-form pairs (box-box, sphere-sphere, sphere-box) of the candidate
+// lists: one test per candidate.  A kernel of its own so the closed forms'
+// registers do not lower the MPR kernel's occupancy.
 template <bool FROM_POSES>
-__global__ __launch_bounds__(256) void narrow_kernel(DevWorld w, const double* __restrict__ in,
+__global__ __launch_bounds__(256) void closed_form_kernel(DevWorld w, const double* __restrict__ in,
+                                                         const uint32_t* __restrict__ seg_len,
+                                                         const uint32_t* __restrict__ seg_start,
+                                                         const uint32_t* __restrict__ prefix,
+                                                         const uint32_t* __restrict__ cand,
+                                                         uint8_t* __restrict__ flags, uint32_t* __restrict__ masks,
+                                                         const double* __restrict__ sc) {
+  const uint32_t lane = lane_id();
+  const uint32_t wave = __builtin_amdgcn_readfirstlane((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+  const uint32_t n_waves = (gridDim.x * blockDim.x) >> 6;
+  const uint32_t total = prefix[w.n_pairs];
+  for (uint32_t tk = wave; tk < total; tk += n_waves) {
+    int lo = 0, hi = w.n_pairs;
+    while (hi - lo > 1) {
+      const int mid = (lo + hi) >> 1;
+      if (prefix[mid] <= tk) lo = mid;
+      else hi = mid;
+    }
+    const int p = lo;
+    const int cf = w.pair_cf[p];
+    if (cf == CF_NONE) continue;
+    const uint32_t t0 = (tk - prefix[p]) * kTask, t1 = min(seg_len[p], t0 + kTask);
+    const int a = w.pair_a[p], b = w.pair_b[p];
+    const bool am = a < w.n_moving, bm = b < w.n_moving;
+    const int ga = am ? w.moving_geom[a] : w.static_geom[a - w.n_moving];
+    const int gb = bm ? w.moving_geom[b] : w.static_geom[b - w.n_moving];
+    const uint32_t* __restrict__ cl = cand + seg_start[p];
+    for (uint32_t base = t0; base < t1; base += 64) {
+      const uint32_t idx = base + lane;
+      if (idx >= t1) continue;
+      const long long c = cl[idx];
+      const SE3 TA = am ? moving_tf<FROM_POSES>(w, in, sc, c, a) : load_se3(w.static_T + 12 * (a - w.n_moving));
+      const SE3 TB = bm ? moving_tf<FROM_POSES>(w, in, sc, c, b) : load_se3(w.static_T + 12 * (b - w.n_moving));
+      if (closed_form(cf, w, ga, TA, gb, TB)) {
+        if (masks) atomicOr(&masks[c * w.W + (p >> 5)], 1u << (p & 31));
+        flags[c] = 1;
+      }
+    }
+  }
+}
+
+template <bool FROM_POSES>
+__global__ __launch_bounds__(256) MPG_NARROW_WAVES void narrow_kernel(DevWorld w, const double* __restrict__ in,
                                                     const uint32_t* __restrict__ seg_len,
                                                     const uint32_t* __restrict__ seg_start,
                                                     const uint32_t* __restrict__ prefix,
@@ -702,23 +750,7 @@ __global__ __launch_bounds__(256) void narrow_kernel(DevWorld w, const double* _
     const int a = w.pair_a[p], b = w.pair_b[p];
     const bool am = a < w.n_moving, bm = b < w.n_moving;
     const uint32_t bit = 1u << (p & 31);
-    const int cf = w.pair_cf[p];
-    if (cf != CF_NONE) {  // closed-form pair: one test per candidate, no MPR
-      const int ga = am ? w.moving_geom[a] : w.static_geom[a - w.n_moving];
-      const int gb = bm ? w.moving_geom[b] : w.static_geom[b - w.n_moving];
-      for (uint32_t base = t0; base < t1; base += 64) {
-        const uint32_t idx = base + lane;
-        if (idx >= t1) continue;
-        const long long c = cl[idx];
-        const SE3 TA = am ? moving_tf<FROM_POSES>(w, in, sc, c, a) : load_se3(w.static_T + 12 * (a - w.n_moving));
-        const SE3 TB = bm ? moving_tf<FROM_POSES>(w, in, sc, c, b) : load_se3(w.static_T + 12 * (b - w.n_moving));
-        if (closed_form(cf, w, ga, TA, gb, TB)) {
-          if (masks) atomicOr(&masks[c * w.W + (p >> 5)], bit);
-          flags[c] = 1;
-        }
-      }
-      continue;
-    }
+    if (w.pair_cf[p] != CF_NONE) continue;  // closed-form pairs: closed_form_kernel
     uint32_t next = t0;  // wave-uniform
     int st = MPR_DONE;
     long long cfg = 0;
@@ -1563,6 +1595,7 @@ struct mpg_world {
   } motion;
   std::mutex motion_mu;
   bool has_closed_form = false;  // a non-allowed pair uses an FCL closed form
+  bool any_closed_form = false;  // some pair (allowed or not) does
   // batched distance buffers (grow-only)
   struct Dist {
     double* poses = nullptr;
@@ -1765,7 +1798,7 @@ void static_record(const mpg_world_desc* d, int s, const double* geom_rec_all, d
 
 // phase A LDS bytes per thread: records + FK save slots + survivor words + queue share
 size_t cull_lds_per_thread(int n_moving, int n_saves, int W) {
-  return (size_t)std::max(n_moving, 1) * 3 * sizeof(float) + (size_t)n_saves * 12 * sizeof(float) +
+  return (size_t)std::max(n_moving, 1) * 3 * sizeof(float) + (size_t)std::max(n_saves - kRegSaves, 0) * 12 * sizeof(float) +
          (size_t)W * sizeof(uint32_t) + (kQueue / 64) * sizeof(uint32_t);
 }
 
@@ -1908,6 +1941,11 @@ int launch_collide(mpg_world* w, const double* in, long long n, uint8_t* flags, 
     hipLaunchKernelGGL((narrow_kernel<FROM_POSES>), dim3(nb), dim3(256), 0, stream, w->dw, qin, ws->seg_len,
                        ws->seg_start, ws->prefix, ws->cand, fl, mk, ws->prefix + w->dw.n_pairs + 1, ws->sc);
     HIP_TRY(hipGetLastError());
+    if (w->any_closed_form) {
+      hipLaunchKernelGGL((closed_form_kernel<FROM_POSES>), dim3(w->narrow_blocks), dim3(256), 0, stream, w->dw, qin,
+                         ws->seg_len, ws->seg_start, ws->prefix, ws->cand, fl, mk, ws->sc);
+      HIP_TRY(hipGetLastError());
+    }
     if (co) {  // penetration info of the reported pairs (enable_contact)
       const size_t P = (size_t)w->dw.n_pairs;
       HIP_TRY(hipMemsetAsync(co->depth + off * P, 0, sizeof(double) * m * P, stream));
@@ -2195,7 +2233,10 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
   dw.pair_b = to_cptr<int>(base + o_pb);
   dw.pair_allowed = to_cptr<int>(base + o_al);
   dw.pair_cf = to_cptr<int>(base + o_cf);
-  for (int p = 0; p < d->n_pairs; ++p) w->has_closed_form |= pair_cf[p] != CF_NONE && !allowed[p];
+  for (int p = 0; p < d->n_pairs; ++p) {
+    w->has_closed_form |= pair_cf[p] != CF_NONE && !allowed[p];
+    w->any_closed_form |= pair_cf[p] != CF_NONE;
+  }
   dw.static_T = to_cptr<double>(base + o_sT);
   dw.link_chain_start = to_cptr<int>(base + o_cs);
   dw.link_chain_len = to_cptr<int>(base + o_cl);
