@@ -153,10 +153,14 @@ MPG_INLINE F34 f_joint_motion(int type, P axis, double v) {
 
 // fp32 FK over the whole tree; calls sink(m, T) with every moving object's
 // world transform (link pose * collision origin).  Joint frames that a later
-// non-consecutive child needs are spilled to `save` ([slot][12] x stride).
+// non-consecutive child needs are kept in registers for the first
+// kRegSaves slots and spilled to `save` ([slot - kRegSaves][12] x stride)
+// beyond that.
+constexpr int kRegSaves = 2;
+
 template <class Sink>
 MPG_INLINE void bp_fk(const BpView& b, const double* __restrict__ qrow, float* save, int stride, Sink&& sink) {
-  F34 cur;
+  F34 cur, r0, r1;
   for (int j = 0; j <= b.nj; ++j) {
     if (j > 0) {
       const int jj = j - 1;
@@ -168,9 +172,13 @@ MPG_INLINE void bp_fk(const BpView& b, const double* __restrict__ qrow, float* s
         cur = li;
       } else if (s == 0) {
         cur = f34_mul(cur, li);
+      } else if (s == 1) {
+        cur = f34_mul(r0, li);
+      } else if (s == 2) {
+        cur = f34_mul(r1, li);
       } else {
         F34 P;
-        const float* sp = save + (size_t)(s - 1) * 12 * stride;
+        const float* sp = save + (size_t)(s - 1 - kRegSaves) * 12 * stride;
 #pragma unroll
         for (int i = 0; i < 9; ++i) P.R[i] = sp[i * stride];
 #pragma unroll
@@ -178,8 +186,12 @@ MPG_INLINE void bp_fk(const BpView& b, const double* __restrict__ qrow, float* s
         cur = f34_mul(P, li);
       }
       const int sv = b.jsave[jj];
-      if (sv >= 0) {
-        float* sp = save + (size_t)sv * 12 * stride;
+      if (sv == 0) {
+        r0 = cur;
+      } else if (sv == 1) {
+        r1 = cur;
+      } else if (sv >= kRegSaves) {
+        float* sp = save + (size_t)(sv - kRegSaves) * 12 * stride;
 #pragma unroll
         for (int i = 0; i < 9; ++i) sp[i * stride] = cur.R[i];
 #pragma unroll
