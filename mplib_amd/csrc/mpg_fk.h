@@ -8,6 +8,7 @@
 #pragma once
 #include "mpg_math.h"
 #include "mpg_broadphase.h"
+#include "mpg_hullcells.h"
 #include "../../include/mpgpu.h"
 
 namespace mpg {
@@ -38,8 +39,10 @@ struct DevWorld {
   cptr<int> geom_nvert;      // [n_geoms] convex vertex count
   cptr<double> geom_rec;     // [n_geoms*G_STRIDE]
   cptr<double> hull;         // AoSoA-4 vertex groups: x0..3 y0..3 z0..3
-  cptr<float> hull32;        // the same groups in fp32, padding = NaN (support pre-pass)
   int hull_doubles;
+  cptr<int> geom_cbase;      // [n_geoms] first cell_start entry of the hull's cell table, -1 = none
+  cptr<uint32_t> cell_start; // per hull kCellsPerHull + 1 offsets into cell_pts (mpg_hullcells.h)
+  cptr<double> cell_pts;     // candidate vertices per cell: x, y, z, 0
   cptr<int> moving_link;     // [n_moving]
   cptr<int> moving_geom;
   cptr<double> moving_offset;  // [n_moving*12]

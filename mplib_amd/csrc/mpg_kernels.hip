@@ -46,11 +46,6 @@ using namespace mpg;
 namespace {
 
 constexpr double kCcdEps = DBL_EPSILON;
-typedef float f2 __attribute__((ext_vector_type(2)));
-// bound on |fp32 dot - fp64 dot| per unit of |dir|_1 * max|coord|: input
-// rounding (2 u32), three rounded operations (3 u32) and the fp64 dot's own
-// rounding, with 3x headroom (u32 = 2^-24)
-constexpr double kSupE = 16.0 * 5.9604644775390625e-08;
 
 thread_local std::string g_last_error;
 
@@ -96,43 +91,31 @@ __device__ __forceinline__ V3 support(const DevWorld& w, cptr<double> HV, const 
   V3 v;
   if (type == MPG_GEOM_CONVEX) {
     // Convex::findExtremeVertex: argmax dir . vertex (fp64), first maximum wins.
-    // fp32 pre-pass: best and runner-up of the fp32 dot products.  Each fp32
-    // dot is within E = kSupE * |dir|_1 * max|coord| of the fp64 one, so a
-    // best/runner-up gap > 2E proves the fp32 winner is the unique fp64
-    // argmax; otherwise (near-ties, NaN directions) the exact fp64 scan runs.
-    const int g0 = w.geom_gstart[geom], ng = w.geom_ng[geom], nv = w.geom_nvert[geom];
-    const cptr<float> F = w.hull32 + 12 * (size_t)g0;
-    const float fx = (float)dir.x, fy = (float)dir.y, fz = (float)dir.z;
-    const f2 X = {fx, fx}, Y = {fy, fy}, Z = {fz, fz};
-    float b1 = -FLT_MAX, b2 = -FLT_MAX;
-    int bi = 0;
-    // b2 <= b1 always: med3(b1, d, b2) is the new runner-up
-    auto upd = [&](float d, int idx) {
-      const bool gt = d > b1;
-      bi = gt ? idx : bi;
-      b2 = __builtin_amdgcn_fmed3f(b1, d, b2);
-      b1 = gt ? d : b1;
-    };
-    const int nfull = nv >> 2;
-#pragma unroll 2
-    for (int g = 0; g < nfull; ++g) {
-      const cptr<float> G = F + 12 * g;
-      const f2 d01 = __builtin_elementwise_fma(Z, f2{G[8], G[9]}, __builtin_elementwise_fma(Y, f2{G[4], G[5]}, X * f2{G[0], G[1]}));
-      const f2 d23 = __builtin_elementwise_fma(Z, f2{G[10], G[11]}, __builtin_elementwise_fma(Y, f2{G[6], G[7]}, X * f2{G[2], G[3]}));
-      upd(d01.x, 4 * g);
-      upd(d01.y, 4 * g + 1);
-      upd(d23.x, 4 * g + 2);
-      upd(d23.y, 4 * g + 3);
-    }
-    for (int k = 0; k < (nv & 3); ++k) {  // partial last group (uniform trip count)
-      const cptr<float> G = F + 12 * nfull;
-      upd(fmaf(fz, G[8 + k], fmaf(fy, G[4 + k], fx * G[k])), 4 * nfull + k);
-    }
-    const double e2 = 2.0 * kSupE * (std::fabs(dir.x) + std::fabs(dir.y) + std::fabs(dir.z)) * rec[G_VMAX];
-    const cptr<double> P = HV + 12 * (size_t)g0;
-    if (!((double)b1 - (double)b2 > e2)) {
+    // Scan only the candidate list of dir's cell (mpg_hullcells.h: every
+    // vertex left out is strictly beaten in fp64 by a listed one, and the
+    // list is in vertex order, so the result is the full scan's).
+    const int cb = w.geom_cbase[geom];
+    const int c = cb >= 0 ? hull_cell(dir.x, dir.y, dir.z) : -1;
+    if (c >= 0) {
+      const uint32_t e0 = w.cell_start[cb + c], e1 = w.cell_start[cb + c + 1];
+      double best = -DBL_MAX, bx = 0.0, by = 0.0, bz = 0.0;
+      for (uint32_t e = e0; e < e1; ++e) {
+        const cptr<double> P = w.cell_pts + 4 * (size_t)e;
+        const double px = P[0], py = P[1], pz = P[2];
+        const double dd = (dir.x * px + dir.y * py) + dir.z * pz;
+        if (dd > best) {
+          best = dd;
+          bx = px;
+          by = py;
+          bz = pz;
+        }
+      }
+      v = v3(bx, by, bz);
+    } else {  // no cell (zero / non-finite / extreme direction): full scan
+      const int g0 = w.geom_gstart[geom], ng = w.geom_ng[geom];
+      const cptr<double> P = HV + 12 * (size_t)g0;
       double best = -DBL_MAX;
-      bi = 0;
+      int bi = 0;
       for (int g = 0; g < ng; ++g) {
         const cptr<double> G = P + 12 * g;
         double dd[4];
@@ -145,9 +128,9 @@ __device__ __forceinline__ V3 support(const DevWorld& w, cptr<double> HV, const 
             bi = 4 * g + k;
           }
       }
+      const cptr<double> B = P + 12 * (bi >> 2) + (bi & 3);
+      v = v3(B[0], B[4], B[8]);
     }
-    const cptr<double> B = P + 12 * (bi >> 2) + (bi & 3);
-    v = v3(B[0], B[4], B[8]);
   } else if (type == MPG_GEOM_BOX) {
     const double hx = rec[G_PARAM + 0] / 2.0, hy = rec[G_PARAM + 1] / 2.0, hz = rec[G_PARAM + 2] / 2.0;
     v = v3((dir.x >= 0 ? 1.0 : -1.0) * hx, (dir.y >= 0 ? 1.0 : -1.0) * hy, (dir.z >= 0 ? 1.0 : -1.0) * hz);
@@ -2075,9 +2058,15 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
   // hulls in AoSoA-4 groups, padded with copies of the hull's first vertex
   std::vector<int> gstart(std::max(d->n_geoms, 1), 0), ngroups(std::max(d->n_geoms, 1), 0);
   std::vector<double> hull;
-  std::vector<float> hull32;
+  std::vector<int> cbase(std::max(d->n_geoms, 1), -1);
+  std::vector<uint32_t> cell_start;
+  std::vector<double> cell_pts;
   for (int g = 0; g < d->n_geoms; ++g) {
     if (d->geom_type[g] != MPG_GEOM_CONVEX) continue;
+    const int cs0 = (int)cell_start.size();
+    if (build_hull_cells(d->vertices + 3 * (size_t)d->geom_vertex_start[g], d->geom_vertex_count[g], cell_start,
+                         cell_pts))
+      cbase[g] = cs0;
     const double* V = d->vertices + 3 * (size_t)d->geom_vertex_start[g];
     const int nv = d->geom_vertex_count[g], ng = (nv + 3) / 4;
     gstart[g] = (int)(hull.size() / 12);
@@ -2087,13 +2076,11 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
         for (int l = 0; l < 4; ++l) {
           const int i = 4 * q + l < nv ? 4 * q + l : 0;
           hull.push_back(V[3 * i + k]);
-          hull32.push_back(4 * q + l < nv ? (float)V[3 * i + k] : std::numeric_limits<float>::quiet_NaN());
         }
   }
-  if (hull.empty()) {
-    hull.assign(12, 0.0);
-    hull32.assign(12, 0.f);
-  }
+  if (hull.empty()) hull.assign(12, 0.0);
+  if (cell_start.empty()) cell_start.assign(1, 0u);
+  if (cell_pts.empty()) cell_pts.assign(4, 0.0);
   // per link: joints from the root to link_parent (chain FK in phase B)
   std::vector<int> chain_start, chain_len, chain_joints;
   for (int l = 0; l < d->n_links; ++l) {
@@ -2145,7 +2132,9 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
   const size_t o_gnvt = bb.add(nvert.data(), nvert.size());
   const size_t o_grec = bb.add(geom_rec.data(), geom_rec.size());
   const size_t o_v = bb.add(hull.data(), hull.size());
-  const size_t o_v32 = bb.add(hull32.data(), hull32.size());
+  const size_t o_cb = bb.add(cbase.data(), cbase.size());
+  const size_t o_cst = bb.add(cell_start.data(), cell_start.size());
+  const size_t o_cpt = bb.add(cell_pts.data(), cell_pts.size());
   const size_t o_ml = bb.add(d->moving_link, d->n_moving);
   const size_t o_mg = bb.add(d->moving_geom, d->n_moving);
   const size_t o_mo = bb.add(d->moving_offset, 12 * (size_t)d->n_moving);
@@ -2223,7 +2212,9 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
   dw.geom_rec = to_cptr<double>(base + o_grec);
   dw.hull = to_cptr<double>(base + o_v);
   dw.hull_doubles = (int)hull.size();
-  dw.hull32 = to_cptr<float>(base + o_v32);
+  dw.geom_cbase = to_cptr<int>(base + o_cb);
+  dw.cell_start = to_cptr<uint32_t>(base + o_cst);
+  dw.cell_pts = to_cptr<double>(base + o_cpt);
   dw.moving_link = to_cptr<int>(base + o_ml);
   dw.moving_geom = to_cptr<int>(base + o_mg);
   dw.moving_offset = to_cptr<double>(base + o_mo);

@@ -1,6 +1,8 @@
 // Test shim: compiles the product's FK/math headers (mplib_amd/csrc/mpg_fk.h)
 // for the host with g++ -ffp-contract=off so tests can compare them with the
 // oracle on a machine without a GPU.  Not part of the product.
+#include <cfloat>
+
 #include "../../mplib_amd/csrc/mpg_fk.h"
 
 extern "C" {
@@ -53,5 +55,56 @@ void host_sincos(const double* x, long n, double* s, double* c, int fma) {
     else if (fma == 2) mpg::mpg_sincos(x[i], s + i, c + i);
     else { s[i] = mpg::mpg_sin<false>(x[i]); c[i] = mpg::mpg_cos<false>(x[i]); }
   }
+}
+// Convex support through the direction-cell lists (mpg_hullcells.h) next to
+// the full first-maximum scan, for n directions; returns the number of
+// directions whose results differ, -1 when the hull has no cell table.
+// stats[0] = directions that used a cell, stats[1] = total list entries
+// scanned, stats[2] = longest list
+long host_hull_support(const double* V, int nv, const double* dirs, long n, double* full, double* cell,
+                       long* stats) {
+  std::vector<uint32_t> start;
+  std::vector<double> pts;
+  if (!mpg::build_hull_cells(V, nv, start, pts)) return -1;
+  long bad = 0;
+  stats[0] = stats[1] = stats[2] = 0;
+  for (long i = 0; i < n; ++i) {
+    const double* d = dirs + 3 * i;
+    double best = -DBL_MAX;
+    int bi = 0;
+    for (int k = 0; k < nv; ++k) {
+      const double dd = (d[0] * V[3 * k] + d[1] * V[3 * k + 1]) + d[2] * V[3 * k + 2];
+      if (dd > best) {
+        best = dd;
+        bi = k;
+      }
+    }
+    for (int j = 0; j < 3; ++j) full[3 * i + j] = V[3 * bi + j];
+    const int c = mpg::hull_cell(d[0], d[1], d[2]);
+    if (c < 0) {
+      for (int j = 0; j < 3; ++j) cell[3 * i + j] = full[3 * i + j];
+      continue;
+    }
+    const uint32_t e0 = start[c], e1 = start[c + 1];
+    stats[0] += 1;
+    stats[1] += e1 - e0;
+    stats[2] = std::max<long>(stats[2], e1 - e0);
+    double cb = -DBL_MAX, bx = 0, by = 0, bz = 0;
+    for (uint32_t e = e0; e < e1; ++e) {
+      const double* P = pts.data() + 4 * e;
+      const double dd = (d[0] * P[0] + d[1] * P[1]) + d[2] * P[2];
+      if (dd > cb) {
+        cb = dd;
+        bx = P[0];
+        by = P[1];
+        bz = P[2];
+      }
+    }
+    cell[3 * i] = bx;
+    cell[3 * i + 1] = by;
+    cell[3 * i + 2] = bz;
+    if (bx != full[3 * i] || by != full[3 * i + 1] || bz != full[3 * i + 2]) ++bad;
+  }
+  return bad;
 }
 }
