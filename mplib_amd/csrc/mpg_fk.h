@@ -40,9 +40,9 @@ struct DevWorld {
   cptr<double> geom_rec;     // [n_geoms*G_STRIDE]
   cptr<double> hull;         // AoSoA-4 vertex groups: x0..3 y0..3 z0..3
   int hull_doubles;
-  cptr<int> geom_cbase;      // [n_geoms] first cell_start entry of the hull's cell table, -1 = none
-  cptr<uint32_t> cell_start; // per hull kCellsPerHull + 1 offsets into cell_pts (mpg_hullcells.h)
-  cptr<double> cell_pts;     // candidate vertices per cell: x, y, z, 0
+  cptr<int> geom_cbase;      // [n_geoms] first cell record of the hull, -1 = none (full scan)
+  cptr<double> cell_rec;     // kCellsPerHull records of kCellRec doubles per hull (mpg_hullcells.h)
+  cptr<double> cell_ovf;     // list entries beyond the inline ones: x, y, z, 0
   cptr<int> moving_link;     // [n_moving]
   cptr<int> moving_geom;
   cptr<double> moving_offset;  // [n_moving*12]

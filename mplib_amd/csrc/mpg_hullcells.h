@@ -4,7 +4,7 @@
 // dir . vertex in fp64, first maximum wins).
 //
 // The sphere of directions is cut into 6 cube faces x K x K cells; each cell
-// is a polyhedral cone spanned by its 4 corner rays r_k (widened by 1e-6).  A
+// is a polyhedral cone spanned by its 4 corner rays r_k (widened by kCellWiden).  A
 // vertex w is left out of a cell's list only when one other vertex u beats it
 // on every corner ray by a margin: r_k.(u - w) > M_k.  Every direction d of
 // the cone is a non-negative combination of the r_k, so then
@@ -17,6 +17,7 @@
 // under/overflow) and hulls of extreme size have no cell: the caller runs the
 // full scan.
 #pragma once
+#include <cfloat>
 #include <cmath>
 #include <cstdint>
 #include <algorithm>
@@ -27,12 +28,18 @@ namespace mpg {
 
 constexpr int kCellK = 16;
 constexpr int kCellsPerHull = 6 * kCellK * kCellK;
-constexpr double kCellMin = 1e-100, kCellMax = 1e100;  // |dir| and max|coord| range with cells
+constexpr double kCellMin = 1e-30, kCellMax = 1e30;  // |dir| range with cells
+constexpr double kHullMin = 1e-100, kHullMax = 1e100;  // max|coord| range with cells
+constexpr double kCellWiden = 1e-5;  // cone widening: covers the fp32 cell arithmetic below
 
-// cell of direction (x, y, z), or -1 (no cell: full scan)
+// cell of direction (x, y, z), or -1 (no cell: full scan).  The range checks
+// are exact (fp64); the cell arithmetic is fp32: the ratios u/|m| are off by
+// at most a few 1e-7 (|ratio| <= 1), far inside the kCellWiden widening, so the
+// direction always lies in the widened cone of the cell returned.
 MPG_INLINE int hull_cell(double x, double y, double z) {
   const double ax = std::fabs(x), ay = std::fabs(y), az = std::fabs(z);
   if (!(ax <= kCellMax && ay <= kCellMax && az <= kCellMax)) return -1;  // also NaN
+  if (!(ax >= kCellMin || ay >= kCellMin || az >= kCellMin)) return -1;
   int f;
   double m, u, v;
   if (ax >= ay && ax >= az) {
@@ -42,10 +49,14 @@ MPG_INLINE int hull_cell(double x, double y, double z) {
   } else {
     f = 2; m = z; u = x; v = y;
   }
-  const double am = std::fabs(m);
-  if (!(am >= kCellMin)) return -1;
-  const double inv = 1.0 / am, h = 0.5 * kCellK;
-  int iu = (int)((u * inv + 1.0) * h), iv = (int)((v * inv + 1.0) * h);
+  const float am = (float)std::fabs(m);
+#if defined(__HIP_DEVICE_COMPILE__)
+  const float inv = __builtin_amdgcn_rcpf(am);
+#else
+  const float inv = 1.0f / am;
+#endif
+  const float h = 0.5f * kCellK;
+  int iu = (int)(((float)u * inv + 1.0f) * h), iv = (int)(((float)v * inv + 1.0f) * h);
   iu = iu < 0 ? 0 : (iu >= kCellK ? kCellK - 1 : iu);
   iv = iv < 0 ? 0 : (iv >= kCellK ? kCellK - 1 : iv);
   return ((2 * f + (m < 0.0 ? 1 : 0)) * kCellK + iu) * kCellK + iv;
@@ -58,8 +69,8 @@ MPG_INLINE int hull_cell(double x, double y, double z) {
 inline bool build_hull_cells(const double* V, int nv, std::vector<uint32_t>& start, std::vector<double>& pts) {
   double X = 0.0;
   for (int i = 0; i < 3 * nv; ++i) X = std::max(X, std::fabs(V[i]));
-  if (nv <= 0 || !(X >= kCellMin && X <= kCellMax)) return false;
-  const double delta = 1e-6, rel = 1e-9;
+  if (nv <= 0 || !(X >= kHullMin && X <= kHullMax)) return false;
+  const double delta = kCellWiden, rel = 1e-9;
   std::vector<double> P((size_t)nv * 4);
   std::vector<char> keep(nv);
   for (int f = 0; f < 3; ++f)
@@ -110,6 +121,69 @@ inline bool build_hull_cells(const double* V, int nv, std::vector<uint32_t>& sta
         }
   start.push_back((uint32_t)(pts.size() / 4));
   return true;
+}
+
+// Device layout: one 96-byte record per cell holding the first kCellInline
+// list entries inline (a short list is padded with its first entry, whose
+// equal dot product can never win the strict '>' again), then the entry count
+// and the offset of the remaining entries in an overflow array (x, y, z, 0
+// each).  A support is then one batch of loads for most cells.
+constexpr int kCellInline = 3;
+constexpr int kCellRec = 12;  // doubles per record: 3 x (x, y, z), count, offset, pad
+
+// (host) converts build_hull_cells lists [start[0], start[kCellsPerHull]) into
+// kCellsPerHull records appended to rec, their overflow entries to ovf
+inline void pack_cell_records(const uint32_t* start, const double* pts, std::vector<double>& rec,
+                              std::vector<double>& ovf) {
+  for (int c = 0; c < kCellsPerHull; ++c) {
+    const uint32_t s = start[c], n = start[c + 1] - start[c];
+    for (int k = 0; k < kCellInline; ++k) {
+      const uint32_t e = s + (k < (int)n ? k : 0);
+      for (int j = 0; j < 3; ++j) rec.push_back(pts[4 * e + j]);
+    }
+    const uint32_t off = (uint32_t)(ovf.size() / 4);
+    for (uint32_t e = s + kCellInline; e < s + n; ++e)
+      for (int j = 0; j < 4; ++j) ovf.push_back(pts[4 * e + j]);
+    rec.push_back((double)n);
+    rec.push_back((double)off);
+    rec.push_back(0.0);
+  }
+}
+
+// first maximum of dir . p over a cell record (and its overflow entries), in
+// the reference's dot order ((x*px + y*py) + z*pz)
+template <class PD>
+MPG_INLINE void cell_record_support(PD R, PD ovf, double x, double y, double z, double* out) {
+  double best = -DBL_MAX, bx = 0.0, by = 0.0, bz = 0.0;
+#pragma unroll
+  for (int k = 0; k < kCellInline; ++k) {
+    const double px = R[3 * k], py = R[3 * k + 1], pz = R[3 * k + 2];
+    const double dd = (x * px + y * py) + z * pz;
+    if (dd > best) {
+      best = dd;
+      bx = px;
+      by = py;
+      bz = pz;
+    }
+  }
+  const int n = (int)R[9];
+  if (n > kCellInline) {
+    const PD P0 = ovf + 4 * (size_t)R[10];
+    for (int k = 0; k < n - kCellInline; ++k) {
+      const PD P = P0 + 4 * k;
+      const double px = P[0], py = P[1], pz = P[2];
+      const double dd = (x * px + y * py) + z * pz;
+      if (dd > best) {
+        best = dd;
+        bx = px;
+        by = py;
+        bz = pz;
+      }
+    }
+  }
+  out[0] = bx;
+  out[1] = by;
+  out[2] = bz;
 }
 
 }  // namespace mpg

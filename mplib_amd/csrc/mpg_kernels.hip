@@ -77,60 +77,51 @@ struct GObj {
   int type;
 };
 
-// HV: the hulls in AoSoA-4 layout (per group of 4 vertices: x0..3, y0..3,
-// z0..3), staged in LDS by the narrow kernel.  Hulls are padded to whole
-// groups with copies of their first vertex, which can never win the strict
-// '>' below, so the result equals the unpadded scan.
-__device__ __forceinline__ V3 support(const DevWorld& w, cptr<double> HV, const GObj& o,
-                                      const V3& dir_world) {
-  const V3 dir = quat_rot(dir_world, o.rot_inv);
-  // the geometry is the same on every lane of the wave (one pair per wave):
-  // say so, so hull and parameter reads stay scalar loads
-  const int geom = __builtin_amdgcn_readfirstlane(o.geom), type = __builtin_amdgcn_readfirstlane(o.type);
+// Convex::findExtremeVertex over the whole hull: argmax dir . vertex (fp64),
+// first maximum wins.  HV: the hulls in AoSoA-4 layout (per group of 4
+// vertices: x0..3, y0..3, z0..3), padded to whole groups with copies of the
+// hull's first vertex, which can never win the strict '>', so the result
+// equals the unpadded scan.  Only for directions without a cell.
+__device__ __forceinline__ V3 convex_full_scan(const DevWorld& w, cptr<double> HV, int geom, const V3& dir) {
+  const int g0 = w.geom_gstart[geom], ng = w.geom_ng[geom];
+  const cptr<double> P = HV + 12 * (size_t)g0;
+  double best = -DBL_MAX;
+  int bi = 0;
+  for (int g = 0; g < ng; ++g) {
+    const cptr<double> G = P + 12 * g;
+    double dd[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) dd[k] = (dir.x * G[k] + dir.y * G[4 + k]) + dir.z * G[8 + k];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (dd[k] > best) {
+        best = dd[k];
+        bi = 4 * g + k;
+      }
+  }
+  const cptr<double> B = P + 12 * (bi >> 2) + (bi & 3);
+  return v3(B[0], B[4], B[8]);
+}
+
+// Convex support through the cell record of dir (mpg_hullcells.h: every
+// vertex left out of a cell's list is strictly beaten in fp64 by a listed one
+// and the list is in vertex order, so its first maximum is the full scan's).
+__device__ __forceinline__ V3 convex_support_local(const DevWorld& w, cptr<double> HV, int geom, const V3& d) {
+  const int cb = w.geom_cbase[geom];
+  const int c = cb >= 0 ? hull_cell(d.x, d.y, d.z) : -1;
+  if (c < 0) return convex_full_scan(w, HV, geom, d);
+  double p[3];
+  cell_record_support(w.cell_rec + kCellRec * (size_t)(cb + c), w.cell_ovf, d.x, d.y, d.z, p);
+  return v3(p[0], p[1], p[2]);
+}
+
+// support mapping of one shape in its own frame (FCL shapeToGJK supports:
+// supportConvex, supportBox, supportSphere, supportCap, supportCyl)
+__device__ __forceinline__ V3 support_local(const DevWorld& w, cptr<double> HV, int geom, int type, const V3& dir) {
   const cptr<double> rec = w.geom_rec + G_STRIDE * geom;
   V3 v;
   if (type == MPG_GEOM_CONVEX) {
-    // Convex::findExtremeVertex: argmax dir . vertex (fp64), first maximum wins.
-    // Scan only the candidate list of dir's cell (mpg_hullcells.h: every
-    // vertex left out is strictly beaten in fp64 by a listed one, and the
-    // list is in vertex order, so the result is the full scan's).
-    const int cb = w.geom_cbase[geom];
-    const int c = cb >= 0 ? hull_cell(dir.x, dir.y, dir.z) : -1;
-    if (c >= 0) {
-      const uint32_t e0 = w.cell_start[cb + c], e1 = w.cell_start[cb + c + 1];
-      double best = -DBL_MAX, bx = 0.0, by = 0.0, bz = 0.0;
-      for (uint32_t e = e0; e < e1; ++e) {
-        const cptr<double> P = w.cell_pts + 4 * (size_t)e;
-        const double px = P[0], py = P[1], pz = P[2];
-        const double dd = (dir.x * px + dir.y * py) + dir.z * pz;
-        if (dd > best) {
-          best = dd;
-          bx = px;
-          by = py;
-          bz = pz;
-        }
-      }
-      v = v3(bx, by, bz);
-    } else {  // no cell (zero / non-finite / extreme direction): full scan
-      const int g0 = w.geom_gstart[geom], ng = w.geom_ng[geom];
-      const cptr<double> P = HV + 12 * (size_t)g0;
-      double best = -DBL_MAX;
-      int bi = 0;
-      for (int g = 0; g < ng; ++g) {
-        const cptr<double> G = P + 12 * g;
-        double dd[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) dd[k] = (dir.x * G[k] + dir.y * G[4 + k]) + dir.z * G[8 + k];
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-          if (dd[k] > best) {
-            best = dd[k];
-            bi = 4 * g + k;
-          }
-      }
-      const cptr<double> B = P + 12 * (bi >> 2) + (bi & 3);
-      v = v3(B[0], B[4], B[8]);
-    }
+    v = convex_support_local(w, HV, geom, dir);
   } else if (type == MPG_GEOM_BOX) {
     const double hx = rec[G_PARAM + 0] / 2.0, hy = rec[G_PARAM + 1] / 2.0, hz = rec[G_PARAM + 2] / 2.0;
     v = v3((dir.x >= 0 ? 1.0 : -1.0) * hx, (dir.y >= 0 ? 1.0 : -1.0) * hy, (dir.z >= 0 ? 1.0 : -1.0) * hz);
@@ -155,7 +146,17 @@ __device__ __forceinline__ V3 support(const DevWorld& w, cptr<double> HV, const 
       v = v3(rad * dir.x, rad * dir.y, (dir.z > 0 ? 1.0 : -1.0) * h);
     }
   }
-  return vadd(quat_rot(v, o.rot), o.pos);
+  return v;
+}
+
+// libccd support of one GJK object: direction into the object frame
+// (ccdQuatRotVec with rot_inv), local support, back to the world frame.  The
+// geometry is the same on every lane of the wave (one pair per wave): say so,
+// so parameter reads stay scalar loads.
+__device__ __forceinline__ V3 support(const DevWorld& w, cptr<double> HV, const GObj& o, const V3& dir_world) {
+  const V3 dir = quat_rot(dir_world, o.rot_inv);
+  const int geom = __builtin_amdgcn_readfirstlane(o.geom), type = __builtin_amdgcn_readfirstlane(o.type);
+  return vadd(quat_rot(support_local(w, HV, geom, type, dir), o.rot), o.pos);
 }
 
 __device__ __forceinline__ V3 center(const DevWorld& w, const GObj& o) {
@@ -180,11 +181,15 @@ __device__ __forceinline__ bool vec_is_origin(const V3& v) {
   return ccd_eq(v.x, 0.0) && ccd_eq(v.y, 0.0) && ccd_eq(v.z, 0.0);
 }
 
+// libccd __ccdSupport: v = support1(dir) - support2(-dir)
 __device__ __forceinline__ V3 msupport(const DevWorld& w, cptr<double> HV, const GObj& a,
                                        const GObj& b, const V3& dir) {
-  const V3 s1 = support(w, HV, a, dir);
-  const V3 s2 = support(w, HV, b, vscale(dir, -1.0));
-  return vsub(s1, s2);
+  const V3 da = quat_rot(dir, a.rot_inv), db = quat_rot(vscale(dir, -1.0), b.rot_inv);
+  const int ga = __builtin_amdgcn_readfirstlane(a.geom), ta = __builtin_amdgcn_readfirstlane(a.type);
+  const int gb = __builtin_amdgcn_readfirstlane(b.geom), tb = __builtin_amdgcn_readfirstlane(b.type);
+  const V3 la = support_local(w, HV, ga, ta, da);
+  const V3 lb = support_local(w, HV, gb, tb, db);
+  return vsub(vadd(quat_rot(la, a.rot), a.pos), vadd(quat_rot(lb, b.rot), b.pos));
 }
 
 // ---------------------------------------------------------------------------
@@ -487,18 +492,6 @@ __global__ __launch_bounds__(BLOCK) void cull_kernel(DevWorld w, const double* _
     for (int m = 0; m < w.n_moving; ++m) put(m, bp_from_pose7(w.bp, in + (c * w.n_links + w.moving_link[m]) * 7, m));
   } else {
     bp_fk(w.bp, in + c * w.dof, save + tid, BLOCK, put);
-    // exact fp64 sin/cos of every revolute move-group joint, once per
-    // configuration, for the narrow phase's chain FK (same values as the
-    // glibc sincos restatement it would otherwise run per candidate)
-    if (live)
-      for (int j = 0; j < w.nj; ++j) {
-        const int src = w.joint_q_source[j];
-        if (src < 0 || !joint_is_revolute(w.joint_type[j])) continue;
-        double sv, cv;
-        mpg_sincos(in[cfg * w.dof + src], &sv, &cv);
-        sc[(cfg * w.dof + src) * 2] = sv;
-        sc[(cfg * w.dof + src) * 2 + 1] = cv;
-      }
   }
   if (w.debug_mode == 1) {
     if (live && cen[tid] == 12345.f) flags[cfg] = 2;  // keep the records alive
@@ -544,8 +537,43 @@ __global__ __launch_bounds__(BLOCK) void cull_kernel(DevWorld w, const double* _
     }
   }
   if (tail != head) sat_drain<BLOCK>(w, cen, rq, cap, cfg0, survw, queue, head, tail - head, wbase, lane);
+  bool any = false;
   if (live)
-    for (int k = 0; k < w.W; ++k) surv[(long long)k * cap + cfg] = survw[k * BLOCK + tid];
+    for (int k = 0; k < w.W; ++k) {
+      const uint32_t b = survw[k * BLOCK + tid];
+      surv[(long long)k * cap + cfg] = b;
+      any |= b != 0u;
+    }
+  if (FROM_POSES) return;
+  // Exact fp64 sin/cos of every revolute move-group joint for the narrow
+  // phase's chain FK (the glibc sincos restatement), only for configurations
+  // with a candidate pair (about a quarter of them): compacted across the
+  // block through LDS (the SAT queues are free now) so every lane works.
+  uint32_t* list = survw + (size_t)w.W * BLOCK;  // [BLOCK] + per-wave counts [BLOCK / 64]
+  uint32_t* wcnt = list + BLOCK;
+  __syncthreads();
+  const unsigned long long bal = __ballot(any);
+  if (lane == 0) wcnt[tid >> 6] = (uint32_t)__popcll(bal);
+  __syncthreads();
+  uint32_t off = 0, total = 0;
+  for (int k = 0; k < BLOCK / 64; ++k) {
+    off += k < (tid >> 6) ? wcnt[k] : 0u;
+    total += wcnt[k];
+  }
+  if (any)
+    list[off + __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u))] = tid;
+  __syncthreads();
+  if ((uint32_t)tid < total) {
+    const long long r = cfg0 + list[tid];
+    for (int j = 0; j < w.nj; ++j) {
+      const int src = w.joint_q_source[j];
+      if (src < 0 || !joint_is_revolute(w.joint_type[j])) continue;
+      double sv, cv;
+      mpg_sincos(in[r * w.dof + src], &sv, &cv);
+      sc[(r * w.dof + src) * 2] = sv;
+      sc[(r * w.dof + src) * 2 + 1] = cv;
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -2059,14 +2087,15 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
   std::vector<int> gstart(std::max(d->n_geoms, 1), 0), ngroups(std::max(d->n_geoms, 1), 0);
   std::vector<double> hull;
   std::vector<int> cbase(std::max(d->n_geoms, 1), -1);
-  std::vector<uint32_t> cell_start;
-  std::vector<double> cell_pts;
+  std::vector<double> cell_rec, cell_ovf;
   for (int g = 0; g < d->n_geoms; ++g) {
     if (d->geom_type[g] != MPG_GEOM_CONVEX) continue;
-    const int cs0 = (int)cell_start.size();
-    if (build_hull_cells(d->vertices + 3 * (size_t)d->geom_vertex_start[g], d->geom_vertex_count[g], cell_start,
-                         cell_pts))
-      cbase[g] = cs0;
+    std::vector<uint32_t> cstart;
+    std::vector<double> cpts;
+    if (build_hull_cells(d->vertices + 3 * (size_t)d->geom_vertex_start[g], d->geom_vertex_count[g], cstart, cpts)) {
+      cbase[g] = (int)(cell_rec.size() / kCellRec);
+      pack_cell_records(cstart.data(), cpts.data(), cell_rec, cell_ovf);
+    }
     const double* V = d->vertices + 3 * (size_t)d->geom_vertex_start[g];
     const int nv = d->geom_vertex_count[g], ng = (nv + 3) / 4;
     gstart[g] = (int)(hull.size() / 12);
@@ -2079,8 +2108,8 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
         }
   }
   if (hull.empty()) hull.assign(12, 0.0);
-  if (cell_start.empty()) cell_start.assign(1, 0u);
-  if (cell_pts.empty()) cell_pts.assign(4, 0.0);
+  if (cell_rec.empty()) cell_rec.assign(kCellRec, 0.0);
+  if (cell_ovf.empty()) cell_ovf.assign(4, 0.0);
   // per link: joints from the root to link_parent (chain FK in phase B)
   std::vector<int> chain_start, chain_len, chain_joints;
   for (int l = 0; l < d->n_links; ++l) {
@@ -2133,8 +2162,8 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
   const size_t o_grec = bb.add(geom_rec.data(), geom_rec.size());
   const size_t o_v = bb.add(hull.data(), hull.size());
   const size_t o_cb = bb.add(cbase.data(), cbase.size());
-  const size_t o_cst = bb.add(cell_start.data(), cell_start.size());
-  const size_t o_cpt = bb.add(cell_pts.data(), cell_pts.size());
+  const size_t o_crec = bb.add(cell_rec.data(), cell_rec.size());
+  const size_t o_covf = bb.add(cell_ovf.data(), cell_ovf.size());
   const size_t o_ml = bb.add(d->moving_link, d->n_moving);
   const size_t o_mg = bb.add(d->moving_geom, d->n_moving);
   const size_t o_mo = bb.add(d->moving_offset, 12 * (size_t)d->n_moving);
@@ -2213,8 +2242,8 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
   dw.hull = to_cptr<double>(base + o_v);
   dw.hull_doubles = (int)hull.size();
   dw.geom_cbase = to_cptr<int>(base + o_cb);
-  dw.cell_start = to_cptr<uint32_t>(base + o_cst);
-  dw.cell_pts = to_cptr<double>(base + o_cpt);
+  dw.cell_rec = to_cptr<double>(base + o_crec);
+  dw.cell_ovf = to_cptr<double>(base + o_covf);
   dw.moving_link = to_cptr<int>(base + o_ml);
   dw.moving_geom = to_cptr<int>(base + o_mg);
   dw.moving_offset = to_cptr<double>(base + o_mo);

@@ -66,6 +66,9 @@ long host_hull_support(const double* V, int nv, const double* dirs, long n, doub
   std::vector<uint32_t> start;
   std::vector<double> pts;
   if (!mpg::build_hull_cells(V, nv, start, pts)) return -1;
+  std::vector<double> rec, ovf;
+  mpg::pack_cell_records(start.data(), pts.data(), rec, ovf);
+  if (ovf.empty()) ovf.assign(4, 0.0);
   long bad = 0;
   stats[0] = stats[1] = stats[2] = 0;
   for (long i = 0; i < n; ++i) {
@@ -89,21 +92,8 @@ long host_hull_support(const double* V, int nv, const double* dirs, long n, doub
     stats[0] += 1;
     stats[1] += e1 - e0;
     stats[2] = std::max<long>(stats[2], e1 - e0);
-    double cb = -DBL_MAX, bx = 0, by = 0, bz = 0;
-    for (uint32_t e = e0; e < e1; ++e) {
-      const double* P = pts.data() + 4 * e;
-      const double dd = (d[0] * P[0] + d[1] * P[1]) + d[2] * P[2];
-      if (dd > cb) {
-        cb = dd;
-        bx = P[0];
-        by = P[1];
-        bz = P[2];
-      }
-    }
-    cell[3 * i] = bx;
-    cell[3 * i + 1] = by;
-    cell[3 * i + 2] = bz;
-    if (bx != full[3 * i] || by != full[3 * i + 1] || bz != full[3 * i + 2]) ++bad;
+    mpg::cell_record_support(rec.data() + (size_t)mpg::kCellRec * c, ovf.data(), d[0], d[1], d[2], cell + 3 * i);
+    if (cell[3 * i] != full[3 * i] || cell[3 * i + 1] != full[3 * i + 1] || cell[3 * i + 2] != full[3 * i + 2]) ++bad;
   }
   return bad;
 }

@@ -60,7 +60,7 @@ def adversarial_dirs(V, rng, n_random=20000):
     d += [corners, axes, np.nextafter(corners, 0)]
     D = np.vstack(d)
     # magnitudes: unit scale, small and large (cells), extreme (full-scan path)
-    scales = [1.0, 1e-90, 1e90, 1e-120, 1e120]
+    scales = [1.0, 1e-25, 1e25, 1e-40, 1e40]
     out = [D * s for s in scales]
     out.append(np.array([[0.0, 0.0, 0.0], [np.nan, 1.0, 0.0], [1.0, np.inf, 0.0], [-np.inf, 0.0, 0.0],
                          [0.0, np.nan, np.nan], [1.0, 1.0, np.nan]]))
