@@ -29,7 +29,7 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 STAGES = ("cull", "bucket", "narrow")  # MPG_STAGE_* (include/mpgpu.h)
-KERNEL_NAME = {"cull": "cull_kernel", "bucket": "tile_count/pair_scan/chunk_scan/scatter", "narrow": "narrow_kernel"}
+KERNEL_NAME = {"cull": "cull_kernel", "bucket": "pair_scan/chunk_scan/scatter", "narrow": "narrow_kernel"}
 FP64_VALU_PEAK_TFLOPS = 78.6  # MI355X spec (vector FP64; FMA counted as 2)
 
 

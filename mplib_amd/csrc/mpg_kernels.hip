@@ -11,7 +11,8 @@
 // Two phases per chunk of configurations (DESIGN.md "Kernels"):
 //   A  cull_kernel      lane per configuration: fp32 FK + conservative broad
 //                       phase (mpg_broadphase.h) -> survivor bits [word][cfg]
-//      tile_count / pair_scan / chunk_scan / scatter: bucket the survivors
+//      (cull also writes the per-tile survivor counts)
+//      pair_scan / chunk_scan / scatter: bucket the survivors
 //                       into per-pair candidate lists (deterministic, no
 //                       global atomics)
 //   B  narrow_kernel    wave per 64 candidates of ONE pair: exact fp64 FK of
@@ -454,7 +455,8 @@ template <int BLOCK, bool FROM_POSES>
 __global__ __launch_bounds__(BLOCK) void cull_kernel(DevWorld w, const double* __restrict__ in, long long n,
                                                     uint8_t* __restrict__ flags, uint32_t* __restrict__ masks,
                                                     uint32_t* __restrict__ surv, float* __restrict__ rq,
-                                                    double* __restrict__ sc, long long cap) {
+                                                    double* __restrict__ sc, long long cap,
+                                                    uint32_t* __restrict__ cnt, int n_tiles) {
   extern __shared__ __attribute__((aligned(16))) float lds_f[];
   float* cen = lds_f;                                                    // [n_moving][3][BLOCK]
   float* save = cen + (size_t)w.n_moving * 3 * BLOCK;  // [n_saves - kRegSaves][12][BLOCK]
@@ -537,13 +539,26 @@ __global__ __launch_bounds__(BLOCK) void cull_kernel(DevWorld w, const double* _
     }
   }
   if (tail != head) sat_drain<BLOCK>(w, cen, rq, cap, cfg0, survw, queue, head, tail - head, wbase, lane);
+  // survivor words -> surv, and this wave's candidate count per pair ->
+  // cnt[pair][tile] (the bucketing's tile counts; cnt is zeroed before the
+  // launch, pairs without a survivor in the tile are skipped): one step per
+  // distinct surviving pair of the wave
   bool any = false;
-  if (live)
-    for (int k = 0; k < w.W; ++k) {
-      const uint32_t b = survw[k * BLOCK + tid];
-      surv[(long long)k * cap + cfg] = b;
-      any |= b != 0u;
+  const long long tile = (cfg0 >> 6) + (tid >> 6);
+  for (int k = 0; k < w.W; ++k) {
+    uint32_t x = live ? survw[k * BLOCK + tid] : 0u;
+    if (live) surv[(long long)k * cap + cfg] = x;
+    any |= x != 0u;
+    for (;;) {
+      const unsigned long long m = __ballot(x != 0u);
+      if (m == 0) break;
+      const uint32_t xl = __builtin_amdgcn_readlane(x, __builtin_ctzll(m));
+      const int b = __builtin_ctz(xl);
+      const unsigned long long bb = __ballot((x >> b) & 1u);
+      x &= ~(1u << b);
+      if (lane == 0) cnt[(long long)(k * 32 + b) * n_tiles + tile] = (uint32_t)__popcll(bb);
     }
+  }
   if (FROM_POSES) return;
   // Exact fp64 sin/cos of every revolute move-group joint for the narrow
   // phase's chain FK (the glibc sincos restatement), only for configurations
@@ -581,22 +596,6 @@ __global__ __launch_bounds__(BLOCK) void cull_kernel(DevWorld w, const double* _
 // (no global atomics): count per (pair, 64-config tile) -> per-pair scan ->
 // scatter.  Candidates of a pair end up contiguous and sorted by config.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void tile_count_kernel(const uint32_t* __restrict__ surv, long long n, long long cap,
-                                                        int n_pairs, int W, int n_tiles,
-                                                        uint32_t* __restrict__ cnt) {
-  const uint32_t lane = lane_id();
-  const long long wid = __builtin_amdgcn_readfirstlane((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
-  if (wid >= (long long)n_tiles * W) return;
-  const int wd = (int)(wid / n_tiles), t = (int)(wid % n_tiles);
-  const long long cfg = (long long)t * 64 + lane;
-  const uint32_t x = cfg < n ? surv[(long long)wd * cap + cfg] : 0u;
-  const int nb = min(32, n_pairs - wd * 32);
-  for (int b = 0; b < nb; ++b) {
-    const unsigned long long bal = __ballot((x >> b) & 1u);
-    if (lane == (uint32_t)b) cnt[(long long)(wd * 32 + b) * n_tiles + t] = (uint32_t)__popcll(bal);
-  }
-}
-
 // one block per pair: exclusive scan of its tile counts (in place) + total
 __global__ __launch_bounds__(1024) void pair_scan_kernel(uint32_t* __restrict__ cnt, int n_tiles,
                                                         uint32_t* __restrict__ seg_len) {
@@ -623,20 +622,54 @@ __global__ __launch_bounds__(1024) void pair_scan_kernel(uint32_t* __restrict__ 
   if (threadIdx.x == 1023) seg_len[blockIdx.x] = part[1023];
 }
 
-// segment starts + prefix of narrow-phase tasks (kTask candidates of one pair)
-__global__ void chunk_scan_kernel(const uint32_t* __restrict__ seg_len, int n_pairs, uint32_t* __restrict__ seg_start,
-                                  uint32_t* __restrict__ prefix, unsigned long long* units) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  uint32_t acc = 0, start = 0;
-  for (int p = 0; p < n_pairs; ++p) {
-    prefix[p] = acc;
-    seg_start[p] = start;
-    acc += (seg_len[p] + kTask - 1) / kTask;
-    start += seg_len[p];
+// inclusive scan of one value per lane across the wave
+__device__ __forceinline__ uint32_t wave_inclusive_scan(uint32_t v, uint32_t lane) {
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t u = __shfl_up(v, off);
+    if (lane >= (uint32_t)off) v += u;
   }
-  prefix[n_pairs] = acc;
-  prefix[n_pairs + 1] = 0;  // narrow-phase task counter
-  if (units) atomicAdd(units, (unsigned long long)start);  // profiling: narrow-phase candidates
+  return v;
+}
+
+// segment starts + prefix of narrow-phase tasks (kTask candidates of one
+// pair): one block, 256 pairs per round
+__global__ __launch_bounds__(256) void chunk_scan_kernel(const uint32_t* __restrict__ seg_len, int n_pairs,
+                                                        uint32_t* __restrict__ seg_start,
+                                                        uint32_t* __restrict__ prefix, unsigned long long* units) {
+  __shared__ uint32_t wl[4], wt[4];
+  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+  uint32_t cl = 0, ct = 0;  // carries over rounds
+  for (int p0 = 0; p0 < n_pairs; p0 += 256) {
+    const int p = p0 + (int)threadIdx.x;
+    const uint32_t len = p < n_pairs ? seg_len[p] : 0u;
+    const uint32_t tasks = (len + kTask - 1) / kTask;
+    const uint32_t il = wave_inclusive_scan(len, lane), it = wave_inclusive_scan(tasks, lane);
+    if (lane == 63) {
+      wl[wv] = il;
+      wt[wv] = it;
+    }
+    __syncthreads();
+    uint32_t bl = cl, bt = ct;
+    for (uint32_t k = 0; k < wv; ++k) {
+      bl += wl[k];
+      bt += wt[k];
+    }
+    if (p < n_pairs) {
+      seg_start[p] = bl + il - len;
+      prefix[p] = bt + it - tasks;
+    }
+    for (uint32_t k = 0; k < 4; ++k) {
+      cl += wl[k];
+      ct += wt[k];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    prefix[n_pairs] = ct;
+    prefix[n_pairs + 1] = 0;  // narrow-phase task counter
+    if (units) atomicAdd(units, (unsigned long long)cl);  // profiling: narrow-phase candidates
+  }
 }
 
 __global__ __launch_bounds__(256) void scatter_kernel(const uint32_t* __restrict__ surv, long long n, long long cap,
@@ -1909,36 +1942,34 @@ int launch_collide(mpg_world* w, const double* in, long long n, uint8_t* flags, 
     uint8_t* fl = flags + off;
     uint32_t* mk = masks ? masks + off * w->dw.W : nullptr;
     const unsigned grid = (unsigned)((m + w->block - 1) / w->block);
+    const int n_tiles = (int)((m + 63) / 64);
     StageTimer t_cull(w, stream, MPG_STAGE_CULL);
     if (w->prof) w->prof_cfg += m;
+    HIP_TRY(hipMemsetAsync(ws->cnt, 0, sizeof(uint32_t) * std::max(w->dw.n_pairs, 1) * (size_t)n_tiles, stream));
     switch (w->block) {
       case 256:
         hipLaunchKernelGGL((cull_kernel<256, FROM_POSES>), dim3(grid), dim3(256), w->lds_bytes, stream, w->dw, qin,
-                           m, fl, mk, ws->surv, ws->rq, ws->sc, ws->cap);
+                           m, fl, mk, ws->surv, ws->rq, ws->sc, ws->cap, ws->cnt, n_tiles);
         break;
       case 128:
         hipLaunchKernelGGL((cull_kernel<128, FROM_POSES>), dim3(grid), dim3(128), w->lds_bytes, stream, w->dw, qin,
-                           m, fl, mk, ws->surv, ws->rq, ws->sc, ws->cap);
+                           m, fl, mk, ws->surv, ws->rq, ws->sc, ws->cap, ws->cnt, n_tiles);
         break;
       default:
         hipLaunchKernelGGL((cull_kernel<64, FROM_POSES>), dim3(grid), dim3(64), w->lds_bytes, stream, w->dw, qin, m,
-                           fl, mk, ws->surv, ws->rq, ws->sc, ws->cap);
+                           fl, mk, ws->surv, ws->rq, ws->sc, ws->cap, ws->cnt, n_tiles);
         break;
     }
     HIP_TRY(hipGetLastError());
     t_cull.stop();
     StageTimer t_bucket(w, stream, MPG_STAGE_BUCKET);
-    const int n_tiles = (int)((m + 63) / 64);
     const long long tw = (long long)n_tiles * w->dw.W;  // one wave per (word, tile)
     const unsigned gb = (unsigned)((tw + 3) / 4);
-    hipLaunchKernelGGL(tile_count_kernel, dim3(gb), dim3(256), 0, stream, ws->surv, m, ws->cap, w->dw.n_pairs,
-                       w->dw.W, n_tiles, ws->cnt);
-    HIP_TRY(hipGetLastError());
     if (w->dw.n_pairs > 0) {
       hipLaunchKernelGGL(pair_scan_kernel, dim3(w->dw.n_pairs), dim3(1024), 0, stream, ws->cnt, n_tiles, ws->seg_len);
       HIP_TRY(hipGetLastError());
     }
-    hipLaunchKernelGGL(chunk_scan_kernel, dim3(1), dim3(64), 0, stream, ws->seg_len, w->dw.n_pairs, ws->seg_start,
+    hipLaunchKernelGGL(chunk_scan_kernel, dim3(1), dim3(256), 0, stream, ws->seg_len, w->dw.n_pairs, ws->seg_start,
                        ws->prefix, w->prof ? w->prof_units : nullptr);
     HIP_TRY(hipGetLastError());
     hipLaunchKernelGGL(scatter_kernel, dim3(gb), dim3(256), 0, stream, ws->surv, m, ws->cap, w->dw.n_pairs, w->dw.W,
