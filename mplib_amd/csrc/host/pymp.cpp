@@ -8,6 +8,7 @@
 #include <pybind11/stl.h>
 
 #include "host.hpp"
+#include "planner.hpp"
 
 namespace py = pybind11;
 using namespace mpgh;
@@ -645,4 +646,79 @@ PYBIND11_MODULE(pymp, m_all) {
            },
            "{stage: (milliseconds, launches, units)} accumulated since the last read; units are configurations "
            "(cull, bucket) or narrow-phase candidates (narrow).");
+
+  // ---- ompl (reference python/pybind_ompl.hpp:20-33) ----
+  auto mo = m_all.def_submodule("ompl");
+  py::class_<OMPLPlanner, std::shared_ptr<OMPLPlanner>>(mo, "OMPLPlanner")
+      .def(py::init([](const std::shared_ptr<PW>& world, py::object checker) {
+             auto p = std::make_shared<OMPLPlanner>(world);
+             if (!checker.is_none()) {
+               // a Python validity checker: f(states[n, dim] float64) -> valid[n]
+               auto fn = std::make_shared<py::object>(checker);
+               const int dim = (int)p->get_dim();
+               p->set_state_validity_checker([fn, dim](const double* st, int64_t n, uint8_t* valid) {
+                 py::gil_scoped_acquire acq;
+                 py::array_t<double> a({(ssize_t)n, (ssize_t)dim});
+                 std::copy(st, st + n * dim, a.mutable_data());
+                 auto r = py::array_t<bool, py::array::c_style | py::array::forcecast>((*fn)(a));
+                 if (r.size() != n) throw std::runtime_error("state_validity_checker returned a wrong length");
+                 const bool* v = r.data();
+                 for (int64_t i = 0; i < n; ++i) valid[i] = v[i] ? 1 : 0;
+               });
+             }
+             return p;
+           }),
+           py::arg("world"), py::arg("state_validity_checker") = py::none(),
+           "OMPL planner over the planned articulations' move-group joints. State validity runs as batched "
+           "device collide() calls; state_validity_checker (f(states[n, dim]) -> valid[n]) replaces it.")
+      .def("get_world", &OMPLPlanner::get_world)
+      .def("set_speculative_connect", &OMPLPlanner::set_speculative_connect, py::arg("enable") = true,
+           "RRTConnect: validate the extension and the whole speculative connect chain in one batch (default), "
+           "or one batch per growTree call as OMPL's loop is written (same tree, more round trips).")
+      .def("get_speculative_connect", &OMPLPlanner::get_speculative_connect)
+      .def("get_dim", &OMPLPlanner::get_dim)
+      .def("random_sample_nearby",
+           [](OMPLPlanner& p, const std::vector<double>& s) { auto v = p.random_sample_nearby(s); return vec(v.data(), (int)v.size()); },
+           py::arg("start_state"))
+      .def("plan",
+           [](OMPLPlanner& p, const std::vector<double>& start, const std::vector<std::vector<double>>& goals,
+              const std::string& name, double time, double range, double goal_bias, double w, bool only,
+              bool verbose) {
+             std::pair<std::string, std::vector<std::vector<double>>> r;
+             {
+               py::gil_scoped_release rel;
+               r = p.plan(start, goals, name, time, range, goal_bias, w, only, verbose);
+             }
+             const ssize_t dim = (ssize_t)p.get_dim();
+             py::array_t<double> path({(ssize_t)r.second.size(), dim});
+             auto m = path.mutable_unchecked<2>();
+             for (ssize_t i = 0; i < (ssize_t)r.second.size(); ++i)
+               for (ssize_t j = 0; j < dim; ++j) m(i, j) = r.second[(size_t)i][(size_t)j];
+             return py::make_tuple(r.first, path);
+           },
+           py::arg("start_state"), py::arg("goal_states"), py::arg("planner_name") = "RRTConnect",
+           py::arg("time") = 1.0, py::arg("range") = 0.0, py::arg("goal_bias") = 0.05,
+           py::arg("pathlen_obj_weight") = 10.0, py::arg("pathlen_obj_only") = false, py::arg("verbose") = false,
+           "Plan from start_state to any of goal_states (+-2pi variants of revolute joints are added); returns "
+           "(status, path[len, dim]). RRTConnect and RRT; every growth step is validated in one batched call.")
+      .def("get_last_plan_stats",
+           [](OMPLPlanner& p) {
+             const auto& s = p.last_stats();
+             py::dict d;
+             d["iterations"] = s.iterations;
+             d["batches"] = s.batches;
+             d["states_checked"] = s.states_checked;
+             d["start_tree"] = s.start_tree;
+             d["goal_tree"] = s.goal_tree;
+             d["seconds"] = s.seconds;
+             d["check_seconds"] = s.check_seconds;
+             return d;
+           },
+           "Counters of the last plan(): iterations, validity batches, states checked, tree sizes, seconds.")
+      .def("get_state_space",
+           [](OMPLPlanner& p) {
+             const auto& s = p.space();
+             return py::make_tuple(s.lo, s.hi, s.so2, s.revolute, s.max_extent, s.longest_valid_segment);
+           },
+           "(lower, upper, so2, is_revolute, maximum_extent, longest_valid_segment) of the compound state space.");
 }

@@ -16,6 +16,7 @@
 #include <sstream>
 
 #include "host.hpp"
+#include "planner.hpp"
 
 namespace mpgh {
 
@@ -705,6 +706,10 @@ std::vector<PlanningWorld::StageTime> PlanningWorld::profile_read() {
   return out;
 }
 
-void set_global_seed(unsigned seed) { std::srand(seed); }
+// random_utils.h:10-15: std::srand + OMPL's RNG seed (planner.cpp)
+void set_global_seed(unsigned seed) {
+  std::srand(seed);
+  plan_rng_seed(seed);
+}
 
 }  // namespace mpgh

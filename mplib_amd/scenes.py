@@ -87,3 +87,18 @@ def joint_limits(art) -> np.ndarray:
 def sample_states(art, n: int, seed: int) -> np.ndarray:
     lim = joint_limits(art)
     return np.random.default_rng(seed).uniform(lim[:, 0], lim[:, 1], size=(n, 7))
+
+
+# cfg5 (BASELINE.json configs[4]): RRTConnect plan() in the cfg3 scene.
+# Start: tests/test_basic.py:44 qpos (it touches the synthetic box1 in this
+# scene, so plan() resamples it nearby as ompl_planner.cpp:110-115 does).
+# Goals: collision-free IK solutions for the panda_hand pose (x, y, z, w=0,
+# x=1, y=0, z=0) -- test_basic.py:43's pose (0.4, 0.3, 0.12) grips into the
+# green cube here, so "near" is 8 cm above it; "far" reaches around box0 /
+# box1 / box2 (a few hundred RRTConnect iterations).  Computed offline by
+# least squares on the FK (tools/plan_goals.py), rounded to 1e-8.
+PLAN_START = [0.0, 0.2, 0.0, -2.6, 0.0, 3.0, 0.8]
+PLAN_GOALS = {
+    "near": [0.33129616, 0.29436923, 0.29083465, -2.39517156, -0.1845193, 2.67095513, 1.56051207],  # (0.4, 0.3, 0.2)
+    "far": [-2.41007622, -1.08236711, 1.81200205, -1.64528436, 1.08547798, 1.8186026, -0.00635181],  # (0.65, -0.15, 0.3)
+}

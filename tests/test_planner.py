@@ -1,0 +1,178 @@
+"""OMPLPlanner (reference src/ompl_planner.{h,cpp}, python/pybind_ompl.hpp):
+RRTConnect / RRT over MPlib's compound state space with batched validity.
+
+The planner's only input from the collision world is state validity, so every
+CPU test plugs the CPU oracle in as the state validity checker and checks the
+path the way OMPL defines a valid solution: every state valid, every edge's
+DiscreteMotionValidator states valid (restated below from OMPL 1.6.0:
+validSegmentCount = ceil(d / (0.01 * extent)), states j/nd), steps of at most
+`range`, endpoints at the (resampled) start and the goal.  The speculative
+batched connect (one validity batch per iteration) must build the same tree as
+OMPL's serial loop (one batch per growTree): identical paths for equal seeds.
+GPU tests: the device checker gives the identical path as the oracle checker.
+Real OMPL is absent: path parity with OMPL's RNG stream is
+unpinned; the semantics above are what is tested.
+"""
+import numpy as np
+import pytest
+
+import worlds as Wd
+from mplib_amd import pymp, scenes
+
+START = np.array(scenes.PLAN_START)
+GOALS = {k: np.array(v) for k, v in scenes.PLAN_GOALS.items()}
+_OW = {}
+
+
+def ow3():
+    if 3 not in _OW:
+        _OW[3] = Wd.oracle_world(3)
+    return _OW[3]
+
+
+def oracle_checker(states):
+    f, _ = ow3().collide_batch(states)
+    return f == 0
+
+
+def planner(checker=oracle_checker):
+    w, _ = scenes.world(3)
+    return pymp.ompl.OMPLPlanner(w, state_validity_checker=checker)
+
+
+def motion_states(a, b, lvs):
+    """DiscreteMotionValidator::checkMotion(a, b): b, then interpolate(a, b, j/nd)."""
+    d = float(np.abs(b - a).sum())  # compound distance of RealVector(1) subspaces
+    nd = int(np.ceil(d / lvs))
+    out = [b] + [a + (b - a) * (j / nd) for j in range(1, nd)]
+    return np.array(out)
+
+
+def assert_valid_solution(p, path, goal, rng_range, start=START):
+    lo, hi, so2, rev, extent, lvs = p.get_state_space()
+    assert np.array_equal(path[0], start)
+    assert np.array_equal(path[-1], goal)
+    first = 1 if not oracle_checker(start[None])[0] else 0  # resampled start prefixed
+    body = path[first:]
+    assert oracle_checker(body).all()
+    assert (body >= np.array(lo) - 1e-12).all() and (body <= np.array(hi) + 1e-12).all()
+    for a, b in zip(body[:-1], body[1:]):
+        assert np.abs(b - a).sum() <= rng_range * (1 + 1e-12)
+        assert oracle_checker(motion_states(a, b, lvs)).all()
+
+
+def test_state_space_matches_build_state_space():
+    p = planner()
+    lo, hi, so2, rev, extent, lvs = p.get_state_space()
+    lim = scenes.joint_limits(scenes.panda())
+    assert p.get_dim() == 7
+    assert np.array_equal(lo, lim[:, 0]) and np.array_equal(hi, lim[:, 1])
+    assert so2 == [0] * 7 and rev == [1] * 7
+    assert extent == pytest.approx(float((lim[:, 1] - lim[:, 0]).sum()), rel=1e-15)
+    assert lvs == pytest.approx(0.01 * extent, rel=1e-15)
+
+
+@pytest.mark.parametrize("goal", ["near", "far"])
+def test_rrtconnect_solution_is_valid(goal):
+    p = planner()
+    pymp.set_global_seed(0)
+    status, path = p.plan(START, [GOALS[goal]], range=0.1, time=60.0)
+    assert status == "Exact solution"
+    assert_valid_solution(p, path, GOALS[goal], 0.1)
+    s = p.get_last_plan_stats()
+    assert s["iterations"] >= 1 and s["states_checked"] > 0
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_speculative_connect_builds_the_serial_tree(seed):
+    p = planner()
+    out = []
+    for spec in (True, False):
+        p.set_speculative_connect(spec)
+        pymp.set_global_seed(seed)
+        out.append((p.plan(START, [GOALS["far"]], range=0.1, time=60.0), p.get_last_plan_stats()))
+    (s1, p1), st1 = out[0]
+    (s2, p2), st2 = out[1]
+    assert s1 == s2 == "Exact solution"
+    assert np.array_equal(p1, p2)
+    assert (st1["iterations"], st1["start_tree"], st1["goal_tree"]) == (st2["iterations"], st2["start_tree"],
+                                                                     st2["goal_tree"])
+    assert st1["batches"] <= st2["batches"]
+
+
+def test_plan_is_deterministic_under_set_global_seed():
+    p = planner()
+    pymp.set_global_seed(7)
+    a = p.plan(START, [GOALS["far"]], range=0.1, time=60.0)
+    pymp.set_global_seed(7)
+    b = p.plan(START, [GOALS["far"]], range=0.1, time=60.0)
+    assert a[0] == b[0] and np.array_equal(a[1], b[1])
+
+
+def test_default_range_is_fifth_of_extent():
+    p = planner()
+    pymp.set_global_seed(3)
+    status, path = p.plan(START, [GOALS["near"]], time=60.0)
+    assert status == "Exact solution"
+    assert_valid_solution(p, path, GOALS["near"], 0.2 * p.get_state_space()[4])
+
+
+def test_rrt_solution_is_valid():
+    p = planner()
+    pymp.set_global_seed(1)
+    status, path = p.plan(START, [GOALS["near"]], planner_name="RRT", range=0.1, time=60.0, goal_bias=0.05)
+    assert status == "Exact solution"
+    assert_valid_solution(p, path, GOALS["near"], 0.1)
+
+
+def test_valid_start_has_no_prefix():
+    p = planner()
+    start = GOALS["near"] + np.array([0, 0, 0, 0, 0, 0, 0.3])
+    assert oracle_checker(start[None])[0]
+    pymp.set_global_seed(0)
+    status, path = p.plan(start, [GOALS["near"]], range=0.1, time=60.0)
+    assert status == "Exact solution"
+    assert_valid_solution(p, path, GOALS["near"], 0.1, start=start)
+
+
+def test_multiple_goals_reach_one_of_them():
+    p = planner()
+    pymp.set_global_seed(4)
+    status, path = p.plan(START, [GOALS["far"], GOALS["near"]], range=0.1, time=60.0)
+    assert status == "Exact solution"
+    assert any(np.array_equal(path[-1], g) for g in GOALS.values())
+
+
+def test_colliding_goal_reports_failure():
+    p = planner()
+    bad = np.array(Wd.KAT_COLLIDING)
+    assert not oracle_checker(bad[None])[0]
+    status, path = p.plan(START, [bad], range=0.1, time=0.5)
+    assert status == "Timeout" and path.shape == (0, 7)
+
+
+def test_argument_errors():
+    p = planner()
+    with pytest.raises(RuntimeError):
+        p.plan(START[:6], [GOALS["near"]])
+    with pytest.raises(RuntimeError):
+        p.plan(START, [GOALS["near"][:6]])
+    with pytest.raises(NotImplementedError):
+        p.plan(START, [GOALS["near"]], planner_name="RRTstar")
+    with pytest.raises(RuntimeError):
+        p.plan(START, [GOALS["near"]], planner_name="NoSuchPlanner")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("goal,seed", [("near", 0), ("far", 0), ("far", 1), ("far", 5)])
+def test_device_checker_gives_the_oracle_path(goal, seed):
+    w, _ = scenes.world(3)
+    dev = pymp.ompl.OMPLPlanner(w)
+    ref = planner()
+    pymp.set_global_seed(seed)
+    s1, p1 = dev.plan(START, [GOALS[goal]], range=0.1, time=60.0)
+    pymp.set_global_seed(seed)
+    s2, p2 = ref.plan(START, [GOALS[goal]], range=0.1, time=60.0)
+    assert s1 == s2 == "Exact solution"
+    assert np.array_equal(p1, p2)
+    assert_valid_solution(ref, p1, GOALS[goal], 0.1)
