@@ -107,11 +107,33 @@ SeedGenerator& seeds() {
   static SeedGenerator g;
   return g;
 }
+// std::rand() of random_sample_nearby (ompl_planner.cpp:77) as a private glibc
+// TYPE_3 generator: the same sequence as rand() after srand(seed), immune to
+// other rand() users in the process (the HIP runtime draws from it at init)
+struct CRand {
+  char buf[128];
+  random_data rd{};
+  CRand() { seed(1); }
+  void seed(unsigned s) {
+    rd = random_data{};
+    initstate_r(s, buf, sizeof(buf), &rd);
+  }
+  int next() {
+    int32_t r;
+    random_r(&rd, &r);
+    return (int)r;
+  }
+};
+CRand& crand() {
+  static CRand c;
+  return c;
+}
 }  // namespace
 
 PlanRNG::PlanRNG() : gen_(seeds().next()) {}
 
 void plan_rng_seed(unsigned seed) {
+  crand().seed(seed);
   auto& g = seeds();
   g.gen.seed(seed);
   g.dist.reset();
@@ -194,7 +216,7 @@ std::vector<double> OMPLPlanner::random_sample_nearby(const std::vector<double>&
     for (; cnt <= 1000 && cnt < first + kChunk; ++cnt) {
       const double ratio = (double)(cnt + 1) / 1000;
       for (int i = 0; i < d; ++i) {
-        const double r = (double)std::rand() / RAND_MAX * 2 - 1;
+        const double r = (double)crand().next() / RAND_MAX * 2 - 1;
         double v = start[(size_t)i] + (space_.hi[(size_t)i] - space_.lo[(size_t)i]) * ratio * r;
         if (v < space_.lo[(size_t)i])
           v = space_.lo[(size_t)i];
