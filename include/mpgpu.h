@@ -168,6 +168,15 @@ int mpg_collide_batch(mpg_world *world, const double *q, int64_t n, uint8_t *fla
                       uint32_t *pair_mask, int mem, void *stream);
 
 /*
+ * Host-buffer calls (mem == MPG_MEM_HOST) of at most `n` configurations take
+ * the latency path: one launch with one wave per (pair, 64-configuration tile)
+ * and one synchronisation, instead of the throughput pipeline (6 launches).
+ * Identical results; default 1024 (env MPG_SMALL_BATCH_MAX), 0 disables.
+ * The planner's validity batches (mplib_amd OMPLPlanner) are this size.
+ */
+int mpg_set_small_batch_max(mpg_world *world, int64_t n);
+
+/*
  * Same pair evaluation as mpg_collide_batch, but the link poses are given
  * directly instead of being computed from joint values:
  * link_pose [n*n_links*7] = (px, py, pz, qw, qx, qy, qz) per user link.

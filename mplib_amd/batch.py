@@ -97,6 +97,10 @@ class DeviceWorld:
     def handle(self):
         return self._h
 
+    def set_small_batch_max(self, n: int):
+        """Host batches of at most n configurations take the one-launch latency path (0 disables)."""
+        C.check(C.lib().mpg_set_small_batch_max(self._h, int(n)), "mpg_set_small_batch_max")
+
     # ------------------------------------------------------------------
     def collide_batch(self, q, flags=None, pair_mask=None, stream: Optional[int] = None):
         """Host path (numpy): returns (flags[n] u8, pair_mask[n, W] u32).

@@ -555,12 +555,15 @@ class PlanningWorld {
   void check_motion_batch(const double* from, const double* to, int64_t n, double longest_valid_segment,
                           uint8_t* valid, int32_t* first_invalid, int32_t* segments);
   void profile_enable(bool on);
+  // host-buffer batches of at most n states take the one-launch latency path
+  void set_small_batch_max(int64_t n);
   struct StageTime { double ms; int64_t launches, units; };
   std::vector<StageTime> profile_read();  // per MPG_STAGE_*
 
  private:
   std::vector<WorldCollisionResult> run_scalar(const CollisionRequest& r, bool self, bool others);
   void ensure_snapshot(const CollisionRequest& r, bool need_device = true);
+  void apply_device_options();
   uint64_t snapshot_key(const CollisionRequest& r) const;
   std::vector<double> current_state() const;
   std::vector<std::string> attached_order() const;
@@ -581,6 +584,7 @@ class PlanningWorld {
   std::vector<PairInfo> pairs_;
   int state_dim_ = 0;
   double tol_ = 1e-6;
+  int64_t small_max_ = -1;  // -1: library default
 };
 
 void set_global_seed(unsigned seed);

@@ -634,6 +634,9 @@ PYBIND11_MODULE(pymp, m_all) {
              return py::make_tuple(ms.so2_mask, ms.max_extent);
            },
            "(so2_mask, maximum_extent) of the planner state space (src/ompl_planner.cpp:248-293).")
+      .def("set_small_batch_max", &PW::set_small_batch_max, py::arg("n"),
+           "Host-buffer batches of at most n states run as one launch (latency path, default 1024); 0 always "
+           "uses the throughput pipeline. Results are identical.")
       .def("profile_enable", &PW::profile_enable, py::arg("enable") = true,
            "Record HIP events around each device stage of the batched check (diagnostics).")
       .def("profile_read",

@@ -375,6 +375,7 @@ void PlanningWorld::ensure_snapshot(const CollisionRequest& r, bool need_device)
     if (need_device && !world_) {
       world_ = std::make_unique<DeviceWorld>(*desc_, default_device());
       world_key_ = key;
+      apply_device_options();
     }
     return;
   }
@@ -517,7 +518,18 @@ void PlanningWorld::ensure_snapshot(const CollisionRequest& r, bool need_device)
   if (need_device) {
     world_ = std::make_unique<DeviceWorld>(d, default_device());
     world_key_ = key;
+    apply_device_options();
   }
+}
+
+void PlanningWorld::apply_device_options() {
+  if (world_ && small_max_ >= 0) check_status(mpg_set_small_batch_max(world_->get(), small_max_), "mpg_set_small_batch_max");
+}
+
+void PlanningWorld::set_small_batch_max(int64_t n) {
+  if (n < 0) throw std::invalid_argument("small_batch_max must be >= 0");
+  small_max_ = n;
+  apply_device_options();
 }
 
 std::vector<WorldCollisionResult> PlanningWorld::run_scalar(const CollisionRequest& r, bool self, bool others) {

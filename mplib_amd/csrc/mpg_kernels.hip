@@ -210,12 +210,14 @@ __device__ __forceinline__ SE3 link_from_pose7(const double* p7) {
 // Moving object -> FCL GJK object (shapeToGJK on link pose * offset).
 // world transform of moving object `id` (link pose * collision origin) -- the
 // Isometry FCLModel::updateCollisionObjects hands to setTransform
-template <bool FROM_POSES>
+// USE_SC: joint (sin, cos) precomputed in `sc` (phase A), else computed inline
+template <bool FROM_POSES, bool USE_SC = true>
 __device__ __forceinline__ SE3 moving_tf(const DevWorld& w, const double* __restrict__ in,
                                          const double* __restrict__ sc, long long cfg, int id) {
   const int l = w.moving_link[id];
   const SE3 L = FROM_POSES ? link_from_pose7(in + (cfg * w.n_links + l) * 7)
-                           : link_from_oMi(w, chain_oMi(w, in + cfg * w.dof, l, sc + cfg * w.dof * 2), l, nullptr);
+                           : link_from_oMi(w, chain_oMi(w, in + cfg * w.dof, l, USE_SC ? sc + cfg * w.dof * 2 : nullptr), l,
+                                           nullptr);
   return se3_mul(L, load_se3(w.moving_offset + 12 * id));
 }
 
@@ -763,6 +765,125 @@ __global__ __launch_bounds__(256) void closed_form_kernel(DevWorld w, const doub
   }
 }
 
+// One libccd MPR step (ccdMPRIntersect = discoverPortal + refinePortal) for
+// a lane whose new Minkowski support point in direction `dir` is `s`.
+// States: MPR_V1..V3 discoverPortal (finding v1, v2, v3), MPR_V4 refinePortal.
+// Returns 1 = intersect, -1 = separated, 0 = continue with the updated dir.
+// The state is copied into locals and written back unconditionally: stores
+// under branches through the reference parameters get merged into stores
+// through a selected pointer, which keeps the caller's registers on the stack.
+__device__ __forceinline__ int mpr_advance(double mpr_tol, const V3& s, int& st_io, V3& v0_io, V3& v1_io, V3& v2_io,
+                                           V3& v3_io, V3& dir_io) {
+  int st = st_io;
+  V3 v0 = v0_io, v1 = v1_io, v2 = v2_io, v3 = v3_io, dir = dir_io;
+  int res = 0;  // 1 = intersect, -1 = separated
+  // Every state ends in one new search direction dir = normalize(a x b);
+  // the states only pick (a, b), so the costly normalize (sqrt + divide)
+  // runs once per step for all lanes instead of once per state branch.
+  const double dsd = vdot(s, dir);
+  V3 ca, cb;
+  bool post_swap = false, post_encl = false;
+  if (st == MPR_V4) {  // refinePortal: expand the portal (v1, v2, v3) towards v4 = s
+    if (!(is_zero(dsd) || dsd > 0.0)) {
+      res = -1;
+    } else {
+      const double dv1 = vdot(v1, dir), dv2 = vdot(v2, dir), dv3 = vdot(v3, dir);
+      double d1 = dsd - dv1;
+      const double dd2 = dsd - dv2, dd3 = dsd - dv3;
+      d1 = (d1 < dd2) ? d1 : dd2;  // CCD_FMIN
+      d1 = (d1 < dd3) ? d1 : dd3;
+      if (ccd_eq(d1, mpr_tol) || d1 < mpr_tol) {
+        res = -1;
+      } else {
+        const V3 v4v0 = vcross(s, v0);
+        if (vdot(v1, v4v0) > 0.0) {
+          if (vdot(v2, v4v0) > 0.0) v1 = s;
+          else v3 = s;
+        } else {
+          if (vdot(v3, v4v0) > 0.0) v2 = s;
+          else v1 = s;
+        }
+        ca = vsub(v2, v1);
+        cb = vsub(v3, v1);
+        post_encl = true;
+      }
+    }
+  } else if (is_zero(dsd) || dsd < 0.0) {  // discoverPortal: support not past the origin
+    res = -1;
+  } else if (st == MPR_V1) {
+    v1 = s;
+    ca = v0;
+    cb = v1;
+  } else if (st == MPR_V2) {
+    v2 = s;
+    ca = vsub(v1, v0);
+    cb = vsub(v2, v0);
+    post_swap = true;
+  } else {  // MPR_V3
+    v3 = s;
+    bool cont = false;
+    double d2 = vdot(vcross(v1, v3), v0);
+    if (d2 < 0.0 && !is_zero(d2)) {
+      v2 = v3;
+      cont = true;
+    }
+    if (!cont) {
+      d2 = vdot(vcross(v3, v2), v0);
+      if (d2 < 0.0 && !is_zero(d2)) {
+        v1 = v3;
+        cont = true;
+      }
+    }
+    if (cont) {
+      ca = vsub(v1, v0);
+      cb = vsub(v2, v0);
+    } else {  // portal found: refinePortal starts with (v1, v2, v3)
+      ca = vsub(v2, v1);
+      cb = vsub(v3, v1);
+      post_encl = true;
+      st = MPR_V4;
+    }
+  }
+  if (res == 0) {
+    const V3 cr = vcross(ca, cb);
+    if (st == MPR_V1 && is_zero(vdot(cr, cr))) {
+      res = 1;  // origin on v1 or on segment v0-v1
+    } else {
+      dir = vnormalize(cr);
+      if (st == MPR_V1) {
+        st = MPR_V2;
+      } else if (post_swap) {
+        if (vdot(dir, v0) > 0.0) {
+          const V3 t = v1;
+          v1 = v2;
+          v2 = t;
+          dir = vscale(dir, -1.0);
+        }
+        st = MPR_V3;
+      } else if (post_encl) {  // portalEncapsulesOrigin
+        const double d = vdot(dir, v1);
+        if (is_zero(d) || d > 0.0) res = 1;
+      }
+    }
+  }
+  st_io = st;
+  v0_io = v0;
+  v1_io = v1;
+  v2_io = v2;
+  v3_io = v3;
+  dir_io = dir;
+  return res;
+}
+
+// ccdMPRIntersect's start: findOrigin (v0 = centre difference, nudged off the
+// origin) and discoverPortal's first direction
+__device__ __forceinline__ void mpr_begin(const V3& ca, const V3& cb, int& st, V3& v0, V3& dir) {
+  v0 = vsub(ca, cb);
+  if (vec_is_origin(v0)) v0 = vadd(v0, mpg::v3(kCcdEps * 10.0, 0.0, 0.0));
+  dir = vnormalize(vscale(v0, -1.0));
+  st = MPR_V1;
+}
+
 template <bool FROM_POSES>
 __global__ __launch_bounds__(256) MPG_NARROW_WAVES void narrow_kernel(DevWorld w, const double* __restrict__ in,
                                                     const uint32_t* __restrict__ seg_len,
@@ -820,11 +941,7 @@ __global__ __launch_bounds__(256) MPG_NARROW_WAVES void narrow_kernel(DevWorld w
             cfg = cl[idx];
             if (am) A = moving_obj<FROM_POSES>(w, in, sc, cfg, a);
             if (bm) B = moving_obj<FROM_POSES>(w, in, sc, cfg, b);
-            // findOrigin; discoverPortal's v0 and first direction
-            v0 = vsub(center(w, A), center(w, B));
-            if (vec_is_origin(v0)) v0 = vadd(v0, mpg::v3(kCcdEps * 10.0, 0.0, 0.0));
-            dir = vnormalize(vscale(v0, -1.0));
-            st = MPR_V1;
+            mpr_begin(center(w, A), center(w, B), st, v0, dir);
 #ifdef MPG_STATS
             nsteps = 0;
 #endif
@@ -856,96 +973,7 @@ __global__ __launch_bounds__(256) MPG_NARROW_WAVES void narrow_kernel(DevWorld w
 #ifdef MPG_STATS
         c2 = __builtin_amdgcn_s_memtime();
 #endif
-        int res = 0;  // 1 = intersect, -1 = separated
-        // Every state ends in one new search direction dir = normalize(a x b);
-        // the states only pick (a, b), so the costly normalize (sqrt + divide)
-        // runs once per step for all lanes instead of once per state branch.
-        const double dsd = vdot(s, dir);
-        V3 ca, cb;
-        bool post_swap = false, post_encl = false;
-        if (st == MPR_V4) {  // refinePortal: expand the portal (v1, v2, v3) towards v4 = s
-          if (!(is_zero(dsd) || dsd > 0.0)) {
-            res = -1;
-          } else {
-            const double dv1 = vdot(v1, dir), dv2 = vdot(v2, dir), dv3 = vdot(v3, dir);
-            double d1 = dsd - dv1;
-            const double dd2 = dsd - dv2, dd3 = dsd - dv3;
-            d1 = (d1 < dd2) ? d1 : dd2;  // CCD_FMIN
-            d1 = (d1 < dd3) ? d1 : dd3;
-            if (ccd_eq(d1, w.mpr_tol) || d1 < w.mpr_tol) {
-              res = -1;
-            } else {
-              const V3 v4v0 = vcross(s, v0);
-              if (vdot(v1, v4v0) > 0.0) {
-                if (vdot(v2, v4v0) > 0.0) v1 = s;
-                else v3 = s;
-              } else {
-                if (vdot(v3, v4v0) > 0.0) v2 = s;
-                else v1 = s;
-              }
-              ca = vsub(v2, v1);
-              cb = vsub(v3, v1);
-              post_encl = true;
-            }
-          }
-        } else if (is_zero(dsd) || dsd < 0.0) {  // discoverPortal: support not past the origin
-          res = -1;
-        } else if (st == MPR_V1) {
-          v1 = s;
-          ca = v0;
-          cb = v1;
-        } else if (st == MPR_V2) {
-          v2 = s;
-          ca = vsub(v1, v0);
-          cb = vsub(v2, v0);
-          post_swap = true;
-        } else {  // MPR_V3
-          v3 = s;
-          bool cont = false;
-          double d2 = vdot(vcross(v1, v3), v0);
-          if (d2 < 0.0 && !is_zero(d2)) {
-            v2 = v3;
-            cont = true;
-          }
-          if (!cont) {
-            d2 = vdot(vcross(v3, v2), v0);
-            if (d2 < 0.0 && !is_zero(d2)) {
-              v1 = v3;
-              cont = true;
-            }
-          }
-          if (cont) {
-            ca = vsub(v1, v0);
-            cb = vsub(v2, v0);
-          } else {  // portal found: refinePortal starts with (v1, v2, v3)
-            ca = vsub(v2, v1);
-            cb = vsub(v3, v1);
-            post_encl = true;
-            st = MPR_V4;
-          }
-        }
-        if (res == 0) {
-          const V3 cr = vcross(ca, cb);
-          if (st == MPR_V1 && is_zero(vdot(cr, cr))) {
-            res = 1;  // origin on v1 or on segment v0-v1
-          } else {
-            dir = vnormalize(cr);
-            if (st == MPR_V1) {
-              st = MPR_V2;
-            } else if (post_swap) {
-              if (vdot(dir, v0) > 0.0) {
-                const V3 t = v1;
-                v1 = v2;
-                v2 = t;
-                dir = vscale(dir, -1.0);
-              }
-              st = MPR_V3;
-            } else if (post_encl) {  // portalEncapsulesOrigin
-              const double d = vdot(dir, v1);
-              if (is_zero(d) || d > 0.0) res = 1;
-            }
-          }
-        }
+        const int res = mpr_advance(w.mpr_tol, s, st, v0, v1, v2, v3, dir);
         if (res != 0) {
           if (res > 0) {
             if (masks) atomicOr(&masks[cfg * w.W + (p >> 5)], bit);
@@ -977,6 +1005,85 @@ __global__ __launch_bounds__(256) MPG_NARROW_WAVES void narrow_kernel(DevWorld w
 #endif
     }
   }
+}
+
+// ---------------------------------------------------------------------------
+// Latency path for small batches (the planner's regime: a few to a few
+// thousand states per call, one round trip each).  The two-phase pipeline
+// costs six dependent launches and a lane-serial cull whose critical path
+// alone is ~60 us; here ONE launch covers the batch with parallelism over
+// (pair x configuration): one wave per (pair, 64-configuration tile), the
+// pair wave-uniform as the MPR support scans need.  Per lane: exact fp64 FK of
+// the pair's two objects (sincos inline), a bounding-sphere separation test
+// (margin kSmallMargin >> MPR tolerance + fp64 FK error, so a skipped pair
+// cannot intersect), then the FCL closed form or libccd MPR -- the same
+// mpr_advance / support code as narrow_kernel, so every bit matches it.
+// Output: hit bytes [n_pairs][n], each written exactly once (no
+// initialisation, safe in host-mapped memory); the host folds them into
+// flags and pair masks.
+// ---------------------------------------------------------------------------
+constexpr double kSmallMargin = 1e-4;
+
+template <bool FROM_POSES>
+__global__ __launch_bounds__(256) void small_kernel(DevWorld w, const double* __restrict__ in, long long n, int n_tiles,
+                                                   uint8_t* __restrict__ hits) {
+  const cptr<double> HV = w.hull;
+  const uint32_t lane = lane_id();
+  const int wave = __builtin_amdgcn_readfirstlane((int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6));
+  const int p = wave / n_tiles;
+  if (p >= w.n_pairs) return;
+  const long long cfg = (long long)(wave - p * n_tiles) * 64 + lane;
+  const bool live = cfg < n;
+  const long long c = live ? cfg : n - 1;
+  uint8_t hit = 0;
+  const int a = w.pair_a[p], b = w.pair_b[p];
+  const bool am = a < w.n_moving, bm = b < w.n_moving;
+  const int cf = w.pair_cf[p];
+  if (!w.pair_allowed[p]) {  // ACM-allowed pairs are never reported (filterCollisions)
+    const SE3 TA = am ? moving_tf<FROM_POSES, false>(w, in, nullptr, c, a) : load_se3(w.static_T + 12 * (a - w.n_moving));
+    const SE3 TB = bm ? moving_tf<FROM_POSES, false>(w, in, nullptr, c, b) : load_se3(w.static_T + 12 * (b - w.n_moving));
+    const int ga = am ? w.moving_geom[a] : w.static_geom[a - w.n_moving];
+    const int gb = bm ? w.moving_geom[b] : w.static_geom[b - w.n_moving];
+    const cptr<double> ra = w.geom_rec + G_STRIDE * ga, rb = w.geom_rec + G_STRIDE * gb;
+    double d2 = 0.0;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const double ci = ((TA.R[3 * i] * ra[G_OBB_C] + TA.R[3 * i + 1] * ra[G_OBB_C + 1]) + TA.R[3 * i + 2] * ra[G_OBB_C + 2]) + TA.p[i];
+      const double cj = ((TB.R[3 * i] * rb[G_OBB_C] + TB.R[3 * i + 1] * rb[G_OBB_C + 1]) + TB.R[3 * i + 2] * rb[G_OBB_C + 2]) + TB.p[i];
+      d2 += (ci - cj) * (ci - cj);
+    }
+    const double rr = ra[G_RADIUS] + rb[G_RADIUS] + kSmallMargin;
+    const bool near = live && d2 <= rr * rr;
+    if (cf != CF_NONE) {
+      if (near && closed_form(cf, w, ga, TA, gb, TB)) hit = 1;
+    } else if (__ballot(near) != 0) {
+      GObj A, B;
+      A.rot = gjk_rot_from_matrix(TA.R);
+      A.rot_inv = quat_invert2(A.rot);
+      A.pos = v3(TA.p[0], TA.p[1], TA.p[2]);
+      A.geom = ga;
+      A.type = w.geom_type[ga];
+      B.rot = gjk_rot_from_matrix(TB.R);
+      B.rot_inv = quat_invert2(B.rot);
+      B.pos = v3(TB.p[0], TB.p[1], TB.p[2]);
+      B.geom = gb;
+      B.type = w.geom_type[gb];
+      int st = MPR_DONE;
+      V3 v0, v1, v2, v3, dir;
+      if (near) mpr_begin(center(w, A), center(w, B), st, v0, dir);
+      while (__ballot(st != MPR_DONE) != 0) {
+        if (st != MPR_DONE) {
+          const V3 s = msupport(w, HV, A, B, dir);
+          const int res = mpr_advance(w.mpr_tol, s, st, v0, v1, v2, v3, dir);
+          if (res != 0) {
+            hit = res > 0 ? 1 : 0;
+            st = MPR_DONE;
+          }
+        }
+      }
+    }
+  }
+  if (live) hits[(size_t)p * n + cfg] = hit;
 }
 
 // ---------------------------------------------------------------------------
@@ -1662,6 +1769,14 @@ struct mpg_world {
   unsigned long long* prof_units = nullptr;   // device counter: narrow candidates
   long long max_chunk = 1 << 20;
   int narrow_blocks = 1024;
+  // small-batch latency path (host buffers, n <= small_max): pinned input
+  // staging + host-mapped hit bytes written by small_kernel
+  long long small_max = 1024;
+  double* h_q = nullptr;       // pinned, [small cap * row]
+  uint8_t* h_hits = nullptr;   // pinned coherent host-mapped, [n_pairs * small cap]
+  uint8_t* d_hits = nullptr;   // device alias of h_hits
+  double* d_qs = nullptr;      // device input of the latency path
+  size_t small_cap = 0;
 };
 
 namespace {
@@ -2328,6 +2443,7 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
   w->narrow_blocks = cus * per_cu;
   // bound the candidate lists to 1 GiB: cap * n_pairs * 4 B
   w->max_chunk = std::max<long long>(4096, std::min<long long>(1 << 20, (1ll << 28) / std::max(d->n_pairs, 1)));
+  if (const char* e = std::getenv("MPG_SMALL_BATCH_MAX")) w->small_max = std::atoll(e);
   *out = w;
   return MPG_OK;
 }
@@ -2347,6 +2463,9 @@ int mpg_world_destroy(mpg_world* w) {
     hipFree(w->dw.stats);
   }
   hipFree(w->blob);
+  if (w->h_q) hipHostFree(w->h_q);
+  if (w->h_hits) hipHostFree(w->h_hits);
+  hipFree(w->d_qs);
   hipFree(w->d_q);
   hipFree(w->d_flags);
   hipFree(w->d_masks);
@@ -2394,6 +2513,63 @@ int mpg_world_get_info(const mpg_world* w, mpg_world_info* info) {
 }  // extern "C"
 
 namespace {
+int ensure_small(mpg_world* w, size_t ncfg, size_t row) {
+  if (ncfg <= w->small_cap) return MPG_OK;
+  if (w->h_q) hipHostFree(w->h_q);
+  if (w->h_hits) hipHostFree(w->h_hits);
+  if (w->d_qs) hipFree(w->d_qs);
+  w->h_q = nullptr;
+  w->h_hits = nullptr;
+  w->d_qs = nullptr;
+  w->small_cap = 0;
+  const size_t P = (size_t)std::max(w->dw.n_pairs, 1);
+  HIP_TRY(hipHostMalloc((void**)&w->h_q, sizeof(double) * ncfg * std::max<size_t>(row, 1), hipHostMallocDefault));
+  HIP_TRY(hipHostMalloc((void**)&w->h_hits, P * ncfg, hipHostMallocMapped | hipHostMallocCoherent));
+  HIP_TRY(hipHostGetDevicePointer((void**)&w->d_hits, w->h_hits, 0));
+  HIP_TRY(hipMalloc(&w->d_qs, sizeof(double) * ncfg * std::max<size_t>(row, 1)));
+  w->small_cap = ncfg;
+  return MPG_OK;
+}
+
+// one round trip: input to the device, one small_kernel launch writing hit
+// bytes straight into host memory, one synchronisation; the host folds the
+// hits into flags / pair masks
+template <bool FROM_POSES>
+int collide_small(mpg_world* w, const double* q, int64_t n, uint8_t* flags, uint32_t* pair_mask, hipStream_t s) {
+  const size_t row = FROM_POSES ? (size_t)w->dw.n_links * 7 : (size_t)w->dw.dof;
+  const size_t cap = std::max<size_t>((size_t)n, std::min<size_t>((size_t)w->small_max, 256));
+  int rc = ensure_small(w, cap, row);
+  if (rc) return rc;
+  const int P = w->dw.n_pairs, W = w->dw.W;
+  std::memset(flags, 0, (size_t)n);
+  if (pair_mask) std::memset(pair_mask, 0, sizeof(uint32_t) * (size_t)n * W);
+  if (P == 0) return MPG_OK;
+  if (row) {
+    std::memcpy(w->h_q, q, sizeof(double) * (size_t)n * row);
+    HIP_TRY(hipMemcpyAsync(w->d_qs, w->h_q, sizeof(double) * (size_t)n * row, hipMemcpyHostToDevice, s));
+  }
+  const int n_tiles = (int)((n + 63) / 64);
+  const long long waves = (long long)P * n_tiles;
+  StageTimer t_small(w, s, MPG_STAGE_NARROW);
+  if (w->prof) w->prof_cfg += n;
+  hipLaunchKernelGGL((small_kernel<FROM_POSES>), dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s, w->dw, w->d_qs,
+                     (long long)n, n_tiles, w->d_hits);
+  HIP_TRY(hipGetLastError());
+  t_small.stop();
+  HIP_TRY(hipStreamSynchronize(s));
+  const uint8_t* h = w->h_hits;
+  for (int p = 0; p < P; ++p) {
+    const uint8_t* hp = h + (size_t)p * n;
+    const uint32_t bit = 1u << (p & 31);
+    for (int64_t c = 0; c < n; ++c)
+      if (hp[c]) {
+        flags[c] = 1;
+        if (pair_mask) pair_mask[(size_t)c * W + (p >> 5)] |= bit;
+      }
+  }
+  return MPG_OK;
+}
+
 template <bool FROM_POSES>
 int collide_common(mpg_world* w, const double* q, int64_t n, uint8_t* flags, uint32_t* pair_mask, int mem,
                    void* stream) {
@@ -2406,6 +2582,7 @@ int collide_common(mpg_world* w, const double* q, int64_t n, uint8_t* flags, uin
   if (mem != MPG_MEM_HOST) return set_error(MPG_E_INVALID, "bad mem kind");
   const size_t row = FROM_POSES ? (size_t)w->dw.n_links * 7 : (size_t)w->dw.dof;
   std::lock_guard<std::mutex> lk(w->host_mu);
+  if (n > 0 && n <= w->small_max) return collide_small<FROM_POSES>(w, q, n, flags, pair_mask, s);
   int rc = ensure_staging(w, (size_t)n, std::max<size_t>(1, (size_t)n * row));
   if (rc) return rc;
   if (n == 0) return MPG_OK;
@@ -2422,6 +2599,14 @@ int collide_common(mpg_world* w, const double* q, int64_t n, uint8_t* flags, uin
 }  // namespace
 
 extern "C" {
+
+int mpg_set_small_batch_max(mpg_world* w, int64_t n) {
+  if (!w) return set_error(MPG_E_INVALID, "world is NULL");
+  if (n < 0) return set_error(MPG_E_INVALID, "n < 0");
+  std::lock_guard<std::mutex> lk(w->host_mu);
+  w->small_max = n;
+  return MPG_OK;
+}
 
 int mpg_collide_batch(mpg_world* w, const double* q, int64_t n, uint8_t* flags, uint32_t* pair_mask, int mem,
                       void* stream) {

@@ -293,10 +293,37 @@ def test_attached_box_in_box_scene_matches_oracle():
     fo, mo = o2.collide_batch(q, nthreads=NTHREADS)
     np.testing.assert_array_equal(f, fo)
     np.testing.assert_array_equal(m, mo)
+    w.set_small_batch_max(1 << 20)  # the same batch through the one-launch latency path
+    f2, m2 = w.collide_batch(q)
+    np.testing.assert_array_equal(f2, fo)
+    np.testing.assert_array_equal(m2, mo)
     held = [k for k, i in enumerate(w.get_collision_pair_info()) if i[3] == "held" or i[4] == "held"]
     box_box = [k for k in held if w.get_collision_pair_info()[k][0] != "self"]
     hits = [(mo[:, k >> 5] >> (k & 31)) & 1 for k in box_box]
     assert sum(int(h.sum()) for h in hits) > 0  # the closed form is exercised with both outcomes
+
+
+@pytest.mark.parametrize("cfg", [2, 3, 4])
+def test_latency_path_matches_oracle(cfg):
+    """Host batches up to the small-batch limit run as one small_kernel launch
+    (one wave per pair x 64-config tile, bounding-sphere test, MPR / closed
+    forms): bit-exact with the oracle and with the two-phase pipeline."""
+    w, art = scenes.world(cfg)
+    q = Wd.sample_q(ow(cfg).art, 20000, 40 + cfg)
+    fo, mo = ow(cfg).collide_batch(q, nthreads=NTHREADS)
+    w.set_small_batch_max(1 << 20)
+    f, m = w.collide_batch(q)
+    np.testing.assert_array_equal(f, fo)
+    np.testing.assert_array_equal(m, mo)
+    w.set_small_batch_max(1024)
+    for n in (1, 2, 63, 64, 65, 1000, 1024, 1025):
+        f, m = w.collide_batch(q[:n])
+        np.testing.assert_array_equal(f, fo[:n])
+        np.testing.assert_array_equal(m, mo[:n])
+    w.set_small_batch_max(0)
+    f, m = w.collide_batch(q[:1000])
+    np.testing.assert_array_equal(f, fo[:1000])
+    np.testing.assert_array_equal(m, mo[:1000])
 
 
 def test_spheres_closed_forms_match_oracle():
@@ -327,6 +354,10 @@ def test_spheres_closed_forms_match_oracle():
     np.testing.assert_array_equal(f, fo)
     bits = lambda M_, P: np.stack([(M_[:, p >> 5] >> (p & 31)) & 1 for p in P], 1)
     np.testing.assert_array_equal(bits(m, range(len(perm))), bits(mo, perm))
+    w.set_small_batch_max(1 << 20)  # closed forms through the latency path
+    f2, m2 = w.collide_batch(q)
+    np.testing.assert_array_equal(f2, fo)
+    np.testing.assert_array_equal(bits(m2, range(len(perm))), bits(mo, perm))
 
 
 # ------------------------------------------------------------------- distance
