@@ -84,6 +84,8 @@ extern "C" {
 #define MPG_GEOM_SPHERE 2   /* fcl::Sphere   : param = radius                */
 #define MPG_GEOM_CAPSULE 3  /* fcl::Capsule  : param = radius, lz            */
 #define MPG_GEOM_CYLINDER 4 /* fcl::Cylinder : param = radius, lz            */
+#define MPG_GEOM_OCTREE 5   /* fcl::OcTree   : param = first leaf, leaf count,
+                               resolution; static objects only          */
 
 /*
  * World descriptor.  SE3 values are 12 doubles: a row-major 3x3 rotation
@@ -139,6 +141,13 @@ typedef struct mpg_world_desc {
 
   /* --- CollisionRequest -------------------------------------------------------- */
   double gjk_tolerance;           /* CollisionRequest::gjk_tolerance (1e-6) */
+
+  /* --- octrees (MPG_GEOM_OCTREE): the occupied leaves of every octree
+   *     geometry as axis-aligned boxes in the octree frame, [min xyz, max xyz]
+   *     per leaf, as fcl::OcTree's getRootBV / computeChildBV recursion
+   *     yields them (PlanningWorldTpl::addPointCloud, planning_world.cpp:102-110) */
+  int64_t n_octree_leaves;
+  const double *octree_leaf;      /* [n_octree_leaves*6]                    */
 } mpg_world_desc;
 
 typedef struct mpg_world mpg_world;

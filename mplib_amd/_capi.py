@@ -42,6 +42,7 @@ class WorldDesc(ctypes.Structure):
         ("n_static", ctypes.c_int32), ("static_geom", _I32P), ("static_transform", _F64P),
         ("n_pairs", ctypes.c_int32), ("pair_a", _I32P), ("pair_b", _I32P), ("pair_allowed", _U8P),
         ("gjk_tolerance", ctypes.c_double),
+        ("n_octree_leaves", ctypes.c_int64), ("octree_leaf", _F64P),
     ]
 
 

@@ -69,6 +69,12 @@ class DeviceWorld:
         self._keep.append(al)
         d.pair_allowed = al.ctypes.data_as(C._U8P)
         d.gjk_tolerance = gjk_tolerance
+        leaves = np.ascontiguousarray(np.asarray(arrays.get("octree_leaf", np.zeros(0)), dtype=np.float64).reshape(-1))
+        d.n_octree_leaves = leaves.size // 6
+        if leaves.size == 0:
+            leaves = np.zeros(6)
+        self._keep.append(leaves)
+        d.octree_leaf = leaves.ctypes.data_as(C._F64P)
         h = ctypes.c_void_p()
         C.check(L.mpg_world_create(ctypes.byref(d), device, ctypes.byref(h)), "mpg_world_create")
         self._keep = []

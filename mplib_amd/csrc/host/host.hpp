@@ -73,6 +73,14 @@ struct Convex : CollisionGeometry {
     return {s[0] * inv, s[1] * inv, s[2] * inv};
   }
 };
+// fcl::OcTree built from a point cloud (octree.cpp): the occupied leaves as
+// [min xyz, max xyz] boxes in the octree frame
+struct OcTree : CollisionGeometry {
+  double resolution;
+  std::vector<std::array<double, 6>> leaves;
+  explicit OcTree(double res);
+  OcTree(const std::vector<Vec3>& points, double res);
+};
 // geometry kinds the reference binds that the device cannot evaluate yet
 struct UnsupportedGeometry : CollisionGeometry {
   explicit UnsupportedGeometry(const std::string& k) { kind = k; }
@@ -216,7 +224,7 @@ struct DescBuilder {
   std::vector<int32_t> link_parent;
   std::vector<double> link_placement;
   std::vector<int32_t> geom_type, geom_vertex_start, geom_vertex_count;
-  std::vector<double> geom_param, vertices;
+  std::vector<double> geom_param, vertices, octree_leaf;
   std::vector<int32_t> moving_link, moving_geom;
   std::vector<double> moving_offset;
   std::vector<int32_t> static_geom;
@@ -505,6 +513,8 @@ class PlanningWorld {
   ObjPtr get_normal_object(const std::string& n) const;
   bool has_normal_object(const std::string& n) const { return objs_.count(n) > 0; }
   void add_normal_object(const std::string& n, const ObjPtr& o);
+  // PlanningWorldTpl::addPointCloud (src/planning_world.cpp:102-110)
+  void add_point_cloud(const std::string& n, const std::vector<Vec3>& vertices, double resolution = 0.001);
   bool remove_normal_object(const std::string& n);
   bool is_normal_object_attached(const std::string& n) const { return attached_.count(n) > 0; }
   AttachedPtr get_attached_object(const std::string& n) const;

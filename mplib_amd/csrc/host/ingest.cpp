@@ -374,6 +374,11 @@ int DescBuilder::add_geometry(const CollisionGeometry* g) {
   } else if (auto cy = dynamic_cast<const Cylinder*>(g)) {
     prm[0] = cy->radius;
     prm[1] = cy->lz;
+  } else if (auto oc = dynamic_cast<const OcTree*>(g)) {
+    prm[0] = (double)(octree_leaf.size() / 6);
+    prm[1] = (double)oc->leaves.size();
+    prm[2] = oc->resolution;
+    for (auto& l : oc->leaves) octree_leaf.insert(octree_leaf.end(), l.begin(), l.end());
   } else if (auto cv = dynamic_cast<const Convex*>(g)) {
     vs = (int)(vertices.size() / 3);
     nv = (int)cv->vertices.size();
@@ -421,6 +426,8 @@ mpg_world_desc DescBuilder::desc() const {
   d.pair_b = pair_b.data();
   d.pair_allowed = pair_allowed.data();
   d.gjk_tolerance = gjk_tolerance;
+  d.n_octree_leaves = (int64_t)(octree_leaf.size() / 6);
+  d.octree_leaf = octree_leaf.data();
   return d;
 }
 

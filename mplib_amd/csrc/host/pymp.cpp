@@ -131,6 +131,28 @@ PYBIND11_MODULE(pymp, m_all) {
         return vec(p.data(), 3);
       });
 
+  // fcl.OcTree (python/pybind_fcl.hpp:221-236)
+  py::class_<OcTree, CollisionGeometry, std::shared_ptr<OcTree>>(m, "OcTree")
+      .def(py::init<double>(), py::arg("resolution"))
+      .def(py::init([](py::array_t<double, py::array::c_style | py::array::forcecast> v, double res) {
+             if (v.ndim() != 2 || v.shape(1) != 3) throw std::invalid_argument("vertices must be [N, 3]");
+             std::vector<Vec3> pts;
+             auto a = v.unchecked<2>();
+             for (ssize_t i = 0; i < v.shape(0); ++i) pts.push_back({a(i, 0), a(i, 1), a(i, 2)});
+             return std::make_shared<OcTree>(pts, res);
+           }),
+           py::arg("vertices"), py::arg("resolution"))
+      .def("get_resolution", [](const OcTree& o) { return o.resolution; })
+      .def("get_leaf_boxes",
+           [](const OcTree& o) {
+             py::array_t<double> a({(ssize_t)o.leaves.size(), (ssize_t)6});
+             auto x = a.mutable_unchecked<2>();
+             for (size_t i = 0; i < o.leaves.size(); ++i)
+               for (int k = 0; k < 6; ++k) x(i, k) = o.leaves[i][k];
+             return a;
+           },
+           "Occupied leaves as [min xyz, max xyz] boxes in the octree frame (FCL traversal order).");
+
   py::class_<CollisionObject, std::shared_ptr<CollisionObject>>(m, "CollisionObject")
       .def(py::init([](const GeomPtr& g, const std::vector<double>& p, const std::vector<double>& q) {
              return std::make_shared<CollisionObject>(g, se3_from_pq(vec3_arg(p), quat_arg(q)));
@@ -491,6 +513,16 @@ PYBIND11_MODULE(pymp, m_all) {
       .def("get_normal_object", &PW::get_normal_object, py::arg("name"))
       .def("has_normal_object", &PW::has_normal_object, py::arg("name"))
       .def("add_normal_object", &PW::add_normal_object, py::arg("name"), py::arg("collision_object"))
+      .def("add_point_cloud",
+           [](PW& w, const std::string& name, py::array_t<double, py::array::c_style | py::array::forcecast> v,
+              double res) {
+             if (v.ndim() != 2 || v.shape(1) != 3) throw std::invalid_argument("vertices must be [N, 3]");
+             std::vector<Vec3> pts;
+             auto a = v.unchecked<2>();
+             for (ssize_t i = 0; i < v.shape(0); ++i) pts.push_back({a(i, 0), a(i, 1), a(i, 2)});
+             w.add_point_cloud(name, pts, res);
+           },
+           py::arg("name"), py::arg("vertices"), py::arg("resolution") = 0.001)
       .def("remove_normal_object", &PW::remove_normal_object, py::arg("name"))
       .def("is_normal_object_attached", &PW::is_normal_object_attached, py::arg("name"))
       .def("get_attached_object", &PW::get_attached_object, py::arg("name"))

@@ -209,6 +209,13 @@ void PlanningWorld::add_normal_object(const std::string& n, const ObjPtr& o) {
   objs_[n] = o;
   ++structure_version_;
 }
+
+void PlanningWorld::add_point_cloud(const std::string& n, const std::vector<Vec3>& vertices, double resolution) {
+  SE3 I;
+  for (int i = 0; i < 9; ++i) I.R[i] = (i % 4 == 0) ? 1.0 : 0.0;
+  I.p[0] = I.p[1] = I.p[2] = 0.0;
+  add_normal_object(n, std::make_shared<CollisionObject>(std::make_shared<OcTree>(vertices, resolution), I));
+}
 bool PlanningWorld::remove_normal_object(const std::string& n) {
   if (!objs_.erase(n)) return false;
   obj_insertion_.erase(std::remove(obj_insertion_.begin(), obj_insertion_.end(), n), obj_insertion_.end());

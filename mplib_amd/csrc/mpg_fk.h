@@ -64,7 +64,14 @@ struct DevWorld {
   cptr<int> sched_start;  // [n_moving+1]
   cptr<int> sched_pair;
   cptr<int> sched_other;
+  // octrees: leaf boxes [L][6] (octree frame), per geometry a uniform grid
+  // record (OG_*), cell -> leaf lists (CSR)
+  cptr<double> oct_leaf;
+  cptr<double> oct_grid;   // [n_geoms * OG_STRIDE]
+  cptr<int> oct_cells;     // cell start offsets into oct_list
+  cptr<int> oct_list;      // leaf indices
 };
+enum { OG_ORIGIN = 0, OG_INV = 3, OG_DIMS = 4, OG_CELL0 = 7, OG_STRIDE = 8 };
 
 template <class P>
 MPG_INLINE SE3 load_se3(P p) {

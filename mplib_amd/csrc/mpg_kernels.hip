@@ -240,7 +240,7 @@ __device__ __forceinline__ GObj moving_obj(const DevWorld& w, const double* __re
 // specialisations, both argument orders), boolean part; same operation order
 // as the oracle (oracle/collide_oracle.c box_box_intersect & co.)
 // ---------------------------------------------------------------------------
-enum : int { CF_NONE = 0, CF_BOX_BOX = 1, CF_SPHERE_SPHERE = 2, CF_SPHERE_BOX = 3, CF_BOX_SPHERE = 4 };
+enum : int { CF_NONE = 0, CF_BOX_BOX = 1, CF_SPHERE_SPHERE = 2, CF_SPHERE_BOX = 3, CF_BOX_SPHERE = 4, CF_OCTREE = 5 };
 
 // detail::boxBox2 (box_box-inl.h, from ODE dBoxBox): return_code != 0
 __device__ __forceinline__ bool box_box_intersect(const double* side1, const SE3& T1, const double* side2,
@@ -368,6 +368,51 @@ __device__ __forceinline__ bool closed_form(int kind, const DevWorld& w, int ga,
     case CF_SPHERE_BOX: return sphere_box_intersect(sa[0], TA, sb, TB);
     default: return sphere_box_intersect(sb[0], TB, sa, TA);  // CF_BOX_SPHERE
   }
+}
+
+// fcl::OBB::overlap -> obbDisjoint (fcl/math/bv/OBB-inl.h [ext FCL 0.7.0]):
+// B = R1^T R2 (row-major), T = R1^T (c2 - c1), a / b the half extents; the
+// |B| entries are widened by 1e-6 before the 15 separating-axis tests.
+__device__ __forceinline__ bool obb_disjoint(const double* B, const double* T, const double* a, const double* b) {
+  const double reps = 1e-6;
+  double Bf[9];
+#pragma unroll
+  for (int i = 0; i < 9; ++i) Bf[i] = std::fabs(B[i]) + reps;
+  if (std::fabs(T[0]) > a[0] + ((Bf[0] * b[0] + Bf[1] * b[1]) + Bf[2] * b[2])) return true;
+  if (std::fabs((B[0] * T[0] + B[3] * T[1]) + B[6] * T[2]) > b[0] + ((Bf[0] * a[0] + Bf[3] * a[1]) + Bf[6] * a[2]))
+    return true;
+  if (std::fabs(T[1]) > a[1] + ((Bf[3] * b[0] + Bf[4] * b[1]) + Bf[5] * b[2])) return true;
+  if (std::fabs(T[2]) > a[2] + ((Bf[6] * b[0] + Bf[7] * b[1]) + Bf[8] * b[2])) return true;
+  if (std::fabs((B[1] * T[0] + B[4] * T[1]) + B[7] * T[2]) > b[1] + ((Bf[1] * a[0] + Bf[4] * a[1]) + Bf[7] * a[2]))
+    return true;
+  if (std::fabs((B[2] * T[0] + B[5] * T[1]) + B[8] * T[2]) > b[2] + ((Bf[2] * a[0] + Bf[5] * a[1]) + Bf[8] * a[2]))
+    return true;
+#define MPG_B(i, j) B[3 * (i) + (j)]
+#define MPG_BF(i, j) Bf[3 * (i) + (j)]
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {  // A0 x Bj
+    const int j1 = j == 0 ? 1 : 0, j2 = j == 2 ? 1 : 2;
+    const double sv = T[2] * MPG_B(1, j) - T[1] * MPG_B(2, j);
+    if (std::fabs(sv) > a[1] * MPG_BF(2, j) + a[2] * MPG_BF(1, j) + b[j1] * MPG_BF(0, j2) + b[j2] * MPG_BF(0, j1))
+      return true;
+  }
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {  // A1 x Bj
+    const int j1 = j == 0 ? 1 : 0, j2 = j == 2 ? 1 : 2;
+    const double sv = T[0] * MPG_B(2, j) - T[2] * MPG_B(0, j);
+    if (std::fabs(sv) > a[0] * MPG_BF(2, j) + a[2] * MPG_BF(0, j) + b[j1] * MPG_BF(1, j2) + b[j2] * MPG_BF(1, j1))
+      return true;
+  }
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {  // A2 x Bj
+    const int j1 = j == 0 ? 1 : 0, j2 = j == 2 ? 1 : 2;
+    const double sv = T[1] * MPG_B(0, j) - T[0] * MPG_B(1, j);
+    if (std::fabs(sv) > a[0] * MPG_BF(1, j) + a[1] * MPG_BF(0, j) + b[j1] * MPG_BF(2, j2) + b[j2] * MPG_BF(2, j1))
+      return true;
+  }
+#undef MPG_B
+#undef MPG_BF
+  return false;
 }
 
 __device__ __forceinline__ GObj static_obj(const DevWorld& w, int sid) {
@@ -720,8 +765,19 @@ __global__ __launch_bounds__(256) void scatter_kernel(const uint32_t* __restrict
 // ---------------------------------------------------------------------------
 enum : int { MPR_DONE = 0, MPR_V1 = 1, MPR_V2 = 2, MPR_V3 = 3, MPR_V4 = 4 };
 
-// FCL closed-form pairs (box-box, sphere-sphere, sphere-box) of the candidate
-// lists: one test per candidate.  A kernel of its own so the closed forms'
+__device__ __forceinline__ bool octree_hit(const DevWorld& w, cptr<double> HV, int go, const SE3& TO, int gs,
+                                           const SE3& TS);
+
+// one closed-form pair evaluation; an octree pair (CF_OCTREE) runs its leaves
+__device__ __forceinline__ bool pair_closed_form(int cf, const DevWorld& w, int ga, const SE3& TA, int gb,
+                                                 const SE3& TB) {
+  if (cf != CF_OCTREE) return closed_form(cf, w, ga, TA, gb, TB);
+  return w.geom_type[ga] == MPG_GEOM_OCTREE ? octree_hit(w, w.hull, ga, TA, gb, TB)
+                                            : octree_hit(w, w.hull, gb, TB, ga, TA);
+}
+
+// FCL closed-form pairs (box-box, sphere-sphere, sphere-box) and octree
+// pairs of the candidate lists: one test per candidate.  A kernel of its own so the closed forms'
 // registers do not lower the MPR kernel's occupancy.
 template <bool FROM_POSES>
 __global__ __launch_bounds__(256) void closed_form_kernel(DevWorld w, const double* __restrict__ in,
@@ -757,7 +813,7 @@ __global__ __launch_bounds__(256) void closed_form_kernel(DevWorld w, const doub
       const long long c = cl[idx];
       const SE3 TA = am ? moving_tf<FROM_POSES>(w, in, sc, c, a) : load_se3(w.static_T + 12 * (a - w.n_moving));
       const SE3 TB = bm ? moving_tf<FROM_POSES>(w, in, sc, c, b) : load_se3(w.static_T + 12 * (b - w.n_moving));
-      if (closed_form(cf, w, ga, TA, gb, TB)) {
+      if (pair_closed_form(cf, w, ga, TA, gb, TB)) {
         if (masks) atomicOr(&masks[c * w.W + (p >> 5)], 1u << (p & 31));
         flags[c] = 1;
       }
@@ -882,6 +938,126 @@ __device__ __forceinline__ void mpr_begin(const V3& ca, const V3& cb, int& st, V
   if (vec_is_origin(v0)) v0 = vadd(v0, mpg::v3(kCcdEps * 10.0, 0.0, 0.0));
   dir = vnormalize(vscale(v0, -1.0));
   st = MPR_V1;
+}
+
+// libccd support of (box with per-lane half sizes h) - (uniform shape b)
+__device__ __forceinline__ V3 msupport_box(const GObj& a, const double* h, const DevWorld& w, cptr<double> HV,
+                                           const GObj& b, const V3& dir) {
+  const V3 da = quat_rot(dir, a.rot_inv), db = quat_rot(vscale(dir, -1.0), b.rot_inv);
+  const V3 la = v3((da.x >= 0 ? 1.0 : -1.0) * h[0], (da.y >= 0 ? 1.0 : -1.0) * h[1], (da.z >= 0 ? 1.0 : -1.0) * h[2]);
+  const int gb = __builtin_amdgcn_readfirstlane(b.geom), tb = __builtin_amdgcn_readfirstlane(b.type);
+  const V3 lb = support_local(w, HV, gb, tb, db);
+  return vsub(vadd(quat_rot(la, a.rot), a.pos), vadd(quat_rot(lb, b.rot), b.pos));
+}
+
+// One lane's (shape, octree) pair: fcl OcTreeSolver::OcTreeShapeIntersectRecurse
+// [ext FCL 0.7.0] reduced to its result -- some occupied leaf whose OBB
+// overlaps the shape's OBB (computeBV(shape, I) -> convertBV(., tf), then
+// obbDisjoint) and whose box intersects the shape: shapeIntersect(box,
+// box_tf, shape, tf) with the leaf box first (box-box / box-sphere closed
+// forms, otherwise libccd MPR).  An ancestor's OBB contains its leaves', so
+// the recursion's pruning never hides a leaf this test would accept.  Leaves
+// come from the octree's grid cells under the shape's box in the octree frame
+// widened exactly as obbDisjoint's first three axes (|R| + 1e-6): a leaf
+// outside it fails those axes.  The pair's geometries are wave-uniform.
+__device__ __forceinline__ bool octree_hit(const DevWorld& w, cptr<double> HV, int go, const SE3& TO, int gs,
+                                           const SE3& TS) {
+  const cptr<double> grs = w.geom_rec + G_STRIDE * gs;
+  const int ts = w.geom_type[gs];
+  double sc[3], se[3], Rl[9], cl[3], hq[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) se[i] = grs[G_OBB_E + i];
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+    sc[i] = ((TS.R[3 * i] * grs[G_OBB_C] + TS.R[3 * i + 1] * grs[G_OBB_C + 1]) + TS.R[3 * i + 2] * grs[G_OBB_C + 2]) +
+            TS.p[i];
+  const double dsc[3] = {sc[0] - TO.p[0], sc[1] - TO.p[1], sc[2] - TO.p[2]};
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    cl[i] = (TO.R[i] * dsc[0] + TO.R[3 + i] * dsc[1]) + TO.R[6 + i] * dsc[2];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) Rl[3 * i + j] = (TO.R[i] * TS.R[j] + TO.R[3 + i] * TS.R[3 + j]) + TO.R[6 + i] * TS.R[6 + j];
+  }
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+    hq[i] = ((std::fabs(Rl[3 * i]) + 1e-6) * se[0] + (std::fabs(Rl[3 * i + 1]) + 1e-6) * se[1] +
+             (std::fabs(Rl[3 * i + 2]) + 1e-6) * se[2]) * (1.0 + 1e-12) + 1e-12;
+  const cptr<double> og = w.oct_grid + OG_STRIDE * go;
+  const double inv = og[OG_INV];
+  int c0[3], c1[3], dims[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    dims[i] = (int)og[OG_DIMS + i];
+    const double f0 = std::floor((cl[i] - hq[i] - og[OG_ORIGIN + i]) * inv);
+    const double f1 = std::floor((cl[i] + hq[i] - og[OG_ORIGIN + i]) * inv);
+    if (f1 < 0.0 || f0 >= (double)dims[i]) return false;
+    c0[i] = f0 < 0.0 ? 0 : (int)f0;
+    c1[i] = f1 >= (double)dims[i] ? dims[i] - 1 : (int)f1;
+  }
+  GObj A, B;  // A: the leaf box (rotation of the octree, per-leaf centre), B: the shape
+  A.rot = gjk_rot_from_matrix(TO.R);
+  A.rot_inv = quat_invert2(A.rot);
+  A.geom = go;
+  A.type = MPG_GEOM_BOX;
+  B.rot = gjk_rot_from_matrix(TS.R);
+  B.rot_inv = quat_invert2(B.rot);
+  B.pos = v3(TS.p[0], TS.p[1], TS.p[2]);
+  B.geom = gs;
+  B.type = ts;
+  const int cell0 = (int)og[OG_CELL0];
+  for (int x = c0[0]; x <= c1[0]; ++x)
+    for (int y = c0[1]; y <= c1[1]; ++y)
+      for (int z = c0[2]; z <= c1[2]; ++z) {
+        const int cell = cell0 + (x * dims[1] + y) * dims[2] + z;
+        const int k1 = w.oct_cells[cell + 1];
+        for (int k = w.oct_cells[cell]; k < k1; ++k) {
+          const cptr<double> L = w.oct_leaf + 6 * (size_t)w.oct_list[k];
+          bool out = false;
+#pragma unroll
+          for (int i = 0; i < 3; ++i) out |= L[i] > cl[i] + hq[i] || L[3 + i] < cl[i] - hq[i];
+          if (out) continue;
+          // leaf OBB: axes TO.R, centre TO * c, extent (max - min) * 0.5
+          double c[3], cw[3], a[3], side[3], T[3];
+#pragma unroll
+          for (int i = 0; i < 3; ++i) {
+            c[i] = (L[i] + L[3 + i]) * 0.5;
+            side[i] = L[3 + i] - L[i];
+            a[i] = side[i] * 0.5;
+          }
+#pragma unroll
+          for (int i = 0; i < 3; ++i) cw[i] = ((TO.R[3 * i] * c[0] + TO.R[3 * i + 1] * c[1]) + TO.R[3 * i + 2] * c[2]) + TO.p[i];
+          const double t[3] = {sc[0] - cw[0], sc[1] - cw[1], sc[2] - cw[2]};
+#pragma unroll
+          for (int i = 0; i < 3; ++i) T[i] = (TO.R[i] * t[0] + TO.R[3 + i] * t[1]) + TO.R[6 + i] * t[2];
+          if (obb_disjoint(Rl, T, a, se)) continue;
+          SE3 TL;  // box_tf = tf * Translation(centre)
+#pragma unroll
+          for (int i = 0; i < 9; ++i) TL.R[i] = TO.R[i];
+#pragma unroll
+          for (int i = 0; i < 3; ++i) TL.p[i] = cw[i];
+          bool hit;
+          if (ts == MPG_GEOM_BOX) {
+            const double sb[3] = {grs[G_PARAM], grs[G_PARAM + 1], grs[G_PARAM + 2]};
+            hit = box_box_intersect(side, TL, sb, TS);
+          } else if (ts == MPG_GEOM_SPHERE) {
+            hit = sphere_box_intersect(grs[G_PARAM], TS, side, TL);
+          } else {
+            A.pos = v3(cw[0], cw[1], cw[2]);
+            const double h[3] = {side[0] / 2.0, side[1] / 2.0, side[2] / 2.0};  // boxToGJK: side / 2
+            int st;
+            V3 v0, v1, v2, v3_, dir;
+            mpr_begin(A.pos, center(w, B), st, v0, dir);
+            int res = 0;
+            while (res == 0) {
+              const V3 sp = msupport_box(A, h, w, HV, B, dir);
+              res = mpr_advance(w.mpr_tol, sp, st, v0, v1, v2, v3_, dir);
+            }
+            hit = res > 0;
+          }
+          if (hit) return true;
+        }
+      }
+  return false;
 }
 
 template <bool FROM_POSES>
@@ -1055,7 +1231,7 @@ __global__ __launch_bounds__(256) void small_kernel(DevWorld w, const double* __
     const double rr = ra[G_RADIUS] + rb[G_RADIUS] + kSmallMargin;
     const bool near = live && d2 <= rr * rr;
     if (cf != CF_NONE) {
-      if (near && closed_form(cf, w, ga, TA, gb, TB)) hit = 1;
+      if (near && pair_closed_form(cf, w, ga, TA, gb, TB)) hit = 1;
     } else if (__ballot(near) != 0) {
       GObj A, B;
       A.rot = gjk_rot_from_matrix(TA.R);
@@ -1746,6 +1922,7 @@ struct mpg_world {
   } motion;
   std::mutex motion_mu;
   bool has_closed_form = false;  // a non-allowed pair uses an FCL closed form
+  bool has_octree = false;       // a non-allowed pair involves an octree
   bool any_closed_form = false;  // some pair (allowed or not) does
   // batched distance buffers (grow-only)
   struct Dist {
@@ -1805,6 +1982,7 @@ int obj_geom_type(const mpg_world_desc* d, int id) {
 // FCL closed-form pair for (o1, o2) in fcl::collide argument order
 int closed_form_kind(const mpg_world_desc* d, int a, int b) {
   const int ta = obj_geom_type(d, a), tb = obj_geom_type(d, b);
+  if (ta == MPG_GEOM_OCTREE || tb == MPG_GEOM_OCTREE) return CF_OCTREE;
   if (ta == MPG_GEOM_BOX && tb == MPG_GEOM_BOX) return CF_BOX_BOX;
   if (ta == MPG_GEOM_SPHERE && tb == MPG_GEOM_SPHERE) return CF_SPHERE_SPHERE;
   if (ta == MPG_GEOM_SPHERE && tb == MPG_GEOM_BOX) return CF_SPHERE_BOX;
@@ -1829,7 +2007,7 @@ int validate(const mpg_world_desc* d) {
     if (d->link_parent[l] < 0 || d->link_parent[l] > d->n_joints) return set_error(MPG_E_INVALID, "bad link_parent");
   for (int g = 0; g < d->n_geoms; ++g) {
     const int t = d->geom_type[g];
-    if (t < MPG_GEOM_CONVEX || t > MPG_GEOM_CYLINDER) return set_error(MPG_E_UNSUPPORTED, "unsupported geometry type");
+    if (t < MPG_GEOM_CONVEX || t > MPG_GEOM_OCTREE) return set_error(MPG_E_UNSUPPORTED, "unsupported geometry type");
     if (t == MPG_GEOM_CONVEX) {
       if (d->geom_vertex_count[g] <= 0 || d->geom_vertex_start[g] < 0 ||
           (int64_t)d->geom_vertex_start[g] + d->geom_vertex_count[g] > d->n_vertices)
@@ -1839,7 +2017,19 @@ int validate(const mpg_world_desc* d) {
   for (int m = 0; m < d->n_moving; ++m) {
     if (d->moving_link[m] < 0 || d->moving_link[m] >= d->n_links) return set_error(MPG_E_INVALID, "bad moving_link");
     if (d->moving_geom[m] < 0 || d->moving_geom[m] >= d->n_geoms) return set_error(MPG_E_INVALID, "bad moving_geom");
+    if (d->geom_type[d->moving_geom[m]] == MPG_GEOM_OCTREE)
+      return set_error(MPG_E_UNSUPPORTED, "an OcTree on a robot link or attached body is not supported");
   }
+  if (d->n_octree_leaves < 0 || (d->n_octree_leaves > 0 && !d->octree_leaf))
+    return set_error(MPG_E_INVALID, "bad octree leaf array");
+  for (int g = 0; g < d->n_geoms; ++g) {
+    if (d->geom_type[g] != MPG_GEOM_OCTREE) continue;
+    const double l0 = d->geom_param[4 * g], ln = d->geom_param[4 * g + 1];
+    if (!(l0 >= 0 && ln >= 0 && l0 == std::floor(l0) && ln == std::floor(ln) && l0 + ln <= (double)d->n_octree_leaves))
+      return set_error(MPG_E_INVALID, "octree leaf range out of bounds");
+  }
+  if (!finite_all(d->octree_leaf, 6 * (size_t)d->n_octree_leaves))
+    return set_error(MPG_E_INVALID, "non-finite octree leaf");
   for (int s = 0; s < d->n_static; ++s)
     if (d->static_geom[s] < 0 || d->static_geom[s] >= d->n_geoms) return set_error(MPG_E_INVALID, "bad static_geom");
   const int nobj = d->n_moving + d->n_static;
@@ -1902,6 +2092,17 @@ void geom_record(const mpg_world_desc* d, int g, double* rec) {
       hi[k] = d->geom_param[4 * g];
       lo[k] = -hi[k];
     }
+  } else if (t == MPG_GEOM_OCTREE) {  // union of the occupied leaf boxes (octree frame)
+    const int64_t l0 = (int64_t)d->geom_param[4 * g], ln = (int64_t)d->geom_param[4 * g + 1];
+    for (int k = 0; k < 3; ++k) {
+      lo[k] = ln > 0 ? DBL_MAX : 0.0;
+      hi[k] = ln > 0 ? -DBL_MAX : 0.0;
+    }
+    for (int64_t i = l0; i < l0 + ln; ++i)
+      for (int k = 0; k < 3; ++k) {
+        lo[k] = std::min(lo[k], d->octree_leaf[6 * i + k]);
+        hi[k] = std::max(hi[k], d->octree_leaf[6 * i + 3 + k]);
+      }
   } else {  // capsule / cylinder along z
     const double r = d->geom_param[4 * g], hz = d->geom_param[4 * g + 1] / 2.0 + (t == MPG_GEOM_CAPSULE ? r : 0.0);
     lo[0] = lo[1] = -r;
@@ -2256,6 +2457,56 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
   if (hull.empty()) hull.assign(12, 0.0);
   if (cell_rec.empty()) cell_rec.assign(kCellRec, 0.0);
   if (cell_ovf.empty()) cell_ovf.assign(4, 0.0);
+  // octrees: leaf boxes + a uniform grid per octree geometry (cells of at
+  // least the largest leaf, <= 64 per axis); a leaf is listed in every cell
+  // its box overlaps
+  std::vector<double> oct_leaf(6 * (size_t)std::max<int64_t>(d->n_octree_leaves, 1), 0.0);
+  if (d->n_octree_leaves > 0) std::copy(d->octree_leaf, d->octree_leaf + 6 * d->n_octree_leaves, oct_leaf.begin());
+  std::vector<double> oct_grid((size_t)OG_STRIDE * std::max(d->n_geoms, 1), 0.0);
+  std::vector<int> oct_cells, oct_list;
+  for (int g = 0; g < d->n_geoms; ++g) {
+    if (d->geom_type[g] != MPG_GEOM_OCTREE) continue;
+    const int64_t l0 = (int64_t)d->geom_param[4 * g], ln = (int64_t)d->geom_param[4 * g + 1];
+    double lo[3] = {0, 0, 0}, hi[3] = {0, 0, 0}, big = 0.0;
+    for (int64_t i = l0; i < l0 + ln; ++i)
+      for (int k = 0; k < 3; ++k) {
+        const double a = d->octree_leaf[6 * i + k], b = d->octree_leaf[6 * i + 3 + k];
+        lo[k] = i == l0 ? a : std::min(lo[k], a);
+        hi[k] = i == l0 ? b : std::max(hi[k], b);
+        big = std::max(big, b - a);
+      }
+    double ext = 0.0;
+    for (int k = 0; k < 3; ++k) ext = std::max(ext, hi[k] - lo[k]);
+    const double cell = std::max({big, ext / 64.0, 1e-9});
+    int dims[3];
+    for (int k = 0; k < 3; ++k) dims[k] = std::max(1, std::min(66, (int)std::ceil((hi[k] - lo[k]) / cell) + 1));
+    double* og = oct_grid.data() + (size_t)OG_STRIDE * g;
+    for (int k = 0; k < 3; ++k) og[OG_ORIGIN + k] = lo[k];
+    og[OG_INV] = 1.0 / cell;
+    for (int k = 0; k < 3; ++k) og[OG_DIMS + k] = dims[k];
+    og[OG_CELL0] = (double)oct_cells.size();
+    const size_t nc = (size_t)dims[0] * dims[1] * dims[2];
+    std::vector<std::vector<int>> lists(nc);
+    // the same cell arithmetic as the device query, so a leaf is found from
+    // every cell a query box overlapping it can touch
+    auto cidx = [&](double v, int k) {
+      const double f = std::floor((v - lo[k]) * og[OG_INV]);
+      return f < 0.0 ? 0 : (f >= dims[k] ? dims[k] - 1 : (int)f);
+    };
+    for (int64_t i = l0; i < l0 + ln; ++i) {
+      const double* L = d->octree_leaf + 6 * i;
+      for (int x = cidx(L[0], 0); x <= cidx(L[3], 0); ++x)
+        for (int y = cidx(L[1], 1); y <= cidx(L[4], 1); ++y)
+          for (int z = cidx(L[2], 2); z <= cidx(L[5], 2); ++z)
+            lists[((size_t)x * dims[1] + y) * dims[2] + z].push_back((int)i);
+    }
+    for (size_t c = 0; c < nc; ++c) {
+      oct_cells.push_back((int)oct_list.size());
+      oct_list.insert(oct_list.end(), lists[c].begin(), lists[c].end());
+    }
+  }
+  oct_cells.push_back((int)oct_list.size());
+  if (oct_list.empty()) oct_list.push_back(0);
   // per link: joints from the root to link_parent (chain FK in phase B)
   std::vector<int> chain_start, chain_len, chain_joints;
   for (int l = 0; l < d->n_links; ++l) {
@@ -2338,6 +2589,10 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
   const size_t o_bmo = bb.add(bpp.moff.data(), bpp.moff.size());
   const size_t o_bmb = bb.add(bpp.mobj.data(), bpp.mobj.size());
   const size_t o_bsb = bb.add(bpp.sobj.data(), bpp.sobj.size());
+  const size_t o_olf = bb.add(oct_leaf.data(), oct_leaf.size());
+  const size_t o_ogr = bb.add(oct_grid.data(), oct_grid.size());
+  const size_t o_oce = bb.add(oct_cells.data(), oct_cells.size());
+  const size_t o_oli = bb.add(oct_list.data(), oct_list.size());
 
   mpg_world* w = new mpg_world();
   w->device = device;
@@ -2401,6 +2656,7 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
   dw.pair_cf = to_cptr<int>(base + o_cf);
   for (int p = 0; p < d->n_pairs; ++p) {
     w->has_closed_form |= pair_cf[p] != CF_NONE && !allowed[p];
+    w->has_octree |= pair_cf[p] == CF_OCTREE && !allowed[p];
     w->any_closed_form |= pair_cf[p] != CF_NONE;
   }
   dw.static_T = to_cptr<double>(base + o_sT);
@@ -2434,6 +2690,10 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
   bp.moff = F(o_bmo);
   bp.mobj = F(o_bmb);
   bp.sobj = F(o_bsb);
+  dw.oct_leaf = to_cptr<double>(base + o_olf);
+  dw.oct_grid = to_cptr<double>(base + o_ogr);
+  dw.oct_cells = I(o_oce);
+  dw.oct_list = I(o_oli);
   int cus = 256;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0) cus = 256;
   // persistent narrow grid: exactly the resident workgroups
@@ -2701,6 +2961,7 @@ int mpg_distance_batch(mpg_world* w, const double* q, int64_t n, int32_t n_self_
   if (n > 0 && ((!q && w->dw.dof > 0) || !d_self || !p_self || !d_others || !p_others))
     return set_error(MPG_E_INVALID, "NULL buffer");
   if (mem != MPG_MEM_HOST && mem != MPG_MEM_DEVICE) return set_error(MPG_E_INVALID, "bad mem kind");
+  if (w->has_octree) return set_error(MPG_E_UNSUPPORTED, "distance to an OcTree is not implemented on the device");
   if (n == 0) return MPG_OK;
   HIP_TRY(hipSetDevice(w->device));
   hipStream_t s = static_cast<hipStream_t>(stream);
@@ -2759,7 +3020,8 @@ int mpg_collide_contacts(mpg_world* w, const double* input, int64_t n, int input
   if (mem != MPG_MEM_HOST && mem != MPG_MEM_DEVICE) return set_error(MPG_E_INVALID, "bad mem kind");
   if (w->has_closed_form)
     return set_error(MPG_E_UNSUPPORTED,
-                     "contacts for FCL closed-form pairs (box-box, sphere-sphere, sphere-box) are not implemented");
+                     "contacts for FCL closed-form pairs (box-box, sphere-sphere, sphere-box) and octree pairs are not "
+                     "implemented");
   if (n == 0) return MPG_OK;
   HIP_TRY(hipSetDevice(w->device));
   hipStream_t s = static_cast<hipStream_t>(stream);

@@ -102,3 +102,44 @@ PLAN_GOALS = {
     "near": [0.33129616, 0.29436923, 0.29083465, -2.39517156, -0.1845193, 2.67095513, 1.56051207],  # (0.4, 0.3, 0.2)
     "far": [-2.41007622, -1.08236711, 1.81200205, -1.64528436, 1.08547798, 1.8186026, -0.00635181],  # (0.65, -0.15, 0.3)
 }
+
+
+# Point-cloud worlds (PlanningWorld.add_point_cloud -> fcl::OcTree), the
+# reference examples' clouds with a numpy sampler in place of trimesh's
+# sample_surface (uniform on the box faces, area weighted):
+#   "floor": detect_collision.py:37-46 -- 10000 points on a 2 x 2 x 0.1 box
+#            shifted down 0.1 (default_rng(8)), resolution 1e-3
+#   "blue":  collision_avoidance.py:61-67 -- 1000 points on the blue cube's
+#            surface (0.1 x 0.4 x 0.2 at (0.55, 0, 0.1), default_rng(7)), in
+#            the cfg3 box scene, resolution 1e-3
+def box_surface_points(rng, side, n: int, center) -> np.ndarray:
+    side = np.asarray(side, dtype=np.float64)
+    areas = np.array([side[1] * side[2], side[0] * side[2], side[0] * side[1]])
+    face = rng.choice(3, n, p=areas / areas.sum())
+    sgn = rng.choice([-1.0, 1.0], n)
+    pts = rng.uniform(-side / 2, side / 2, (n, 3))
+    pts[np.arange(n), face] = sgn * side[face] / 2
+    return pts + np.asarray(center, dtype=np.float64)
+
+
+def cloud_points(kind: str) -> np.ndarray:
+    if kind == "floor":
+        return box_surface_points(np.random.default_rng(8), (2.0, 2.0, 0.1), 10000, (0.0, 0.0, -0.1))
+    if kind == "blue":
+        return box_surface_points(np.random.default_rng(7), (0.1, 0.4, 0.2), 1000, (0.55, 0.0, 0.1))
+    raise ValueError(kind)
+
+
+def cloud_world(kind: str, resolution: float = 1e-3):
+    """(PlanningWorld, ArticulatedModel) with the point cloud `kind` as 'scene_pcd'."""
+    if kind == "floor":
+        art = panda()
+        w = pymp.planning_world.PlanningWorld([art], ["panda"], [], [])
+    else:
+        w, art = world(3)
+    w.add_point_cloud("scene_pcd", cloud_points(kind), resolution)
+    return w, art
+
+
+# detect_collision.py:47-55: "this pose causes several joints to dip below the floor"
+FLOOR_COLLIDING = [0.0, 1.5, 0.0, -1.5, 0.0, 0.0, 0.0]

@@ -76,6 +76,7 @@ class _World(ctypes.Structure):
         ("n_scene", ctypes.c_int), ("scene_geom", _IP), ("scene_tf", _DP),
         ("n_pairs", ctypes.c_int),
         ("pa_kind", _IP), ("pa_idx", _IP), ("pb_kind", _IP), ("pb_idx", _IP), ("p_allowed", _IP),
+        ("oct_leaf", _DP),
     ]
 
 
@@ -132,7 +133,9 @@ class OracleWorld:
         att_geom = [self._geom_index(a[2], geoms, None) for a in self.attached]
         scene_geom = [self._geom_index(s[1], geoms, None) for s in self.scene]
         gtype, gvstart, gnv, gparam, ginterior, verts = [], [], [], [], [], []
+        leaves = []
         nverts = 0
+        nleaves = 0
         for g in geoms:
             if isinstance(g, M.ConvexGeom):
                 gtype.append(M.GEOM_CONVEX)
@@ -148,6 +151,14 @@ class OracleWorld:
                 gnv.append(0)
                 gparam += [float(g.side[0]), float(g.side[1]), float(g.side[2]), 0.0]
                 ginterior += [0.0] * 3
+            elif isinstance(g, M.OcTreeGeom):
+                gtype.append(M.GEOM_OCTREE)
+                gvstart.append(0)
+                gnv.append(0)
+                gparam += [float(nleaves), float(len(g.leaves)), g.resolution, 0.0]
+                ginterior += [0.0] * 3
+                leaves.append(np.asarray(g.leaves, dtype=np.float64).reshape(-1))
+                nleaves += len(g.leaves)
             elif isinstance(g, M.SphereGeom):
                 gtype.append(M.GEOM_SPHERE)
                 gvstart.append(0)
@@ -234,6 +245,7 @@ class OracleWorld:
         w.pb_kind = ia([p[2] for p in pairs])
         w.pb_idx = ia([p[3] for p in pairs])
         w.p_allowed = ia(allowed)
+        w.oct_leaf = da(np.concatenate(leaves) if leaves else [])
         self._w = w
         self.geoms = geoms
         self.dof = len(mg)

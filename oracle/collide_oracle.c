@@ -45,7 +45,7 @@ typedef double real;
 #define CCD_REAL_MAX DBL_MAX
 
 /* ---------------------------------------------------------------- world */
-enum { GEOM_CONVEX = 0, GEOM_BOX = 1, GEOM_SPHERE = 2, GEOM_CAPSULE = 3, GEOM_CYLINDER = 4 };
+enum { GEOM_CONVEX = 0, GEOM_BOX = 1, GEOM_SPHERE = 2, GEOM_CAPSULE = 3, GEOM_CYLINDER = 4, GEOM_OCTREE = 5 };
 enum { JT_RX, JT_RY, JT_RZ, JT_RU, JT_PX, JT_PY, JT_PZ, JT_PU, JT_RUBX, JT_RUBY, JT_RUBZ, JT_RUBU };
 enum { KIND_ROBOT = 0, KIND_ATTACHED = 1, KIND_SCENE = 2 };
 
@@ -86,6 +86,9 @@ typedef struct {
     /* pair table */
     int n_pairs;
     const int *pa_kind, *pa_idx, *pb_kind, *pb_idx, *p_allowed;
+    /* octree geometries: geom_param = (first leaf, leaf count, resolution);
+     * leaves [*6] = min xyz, max xyz in the octree frame */
+    const double *oct_leaf;
 } orc_world;
 
 typedef struct {
@@ -1029,6 +1032,114 @@ static void make_obj(const orc_world *w, int geom, const real *T, gjk_obj *o, or
     }
 }
 
+/* fcl obbDisjoint (fcl/math/bv/OBB-inl.h [ext FCL 0.7.0]): B = R1^T R2
+ * (row-major), T = R1^T (c2 - c1), a / b half extents, |B| + 1e-6. */
+static int obb_disjoint(const real *B, const real *T, const real *a, const real *b) {
+    const real reps = 1e-6;
+    real Bf[9];
+    for (int i = 0; i < 9; ++i) Bf[i] = fabs(B[i]) + reps;
+#define B_(i, j) B[3 * (i) + (j)]
+#define F_(i, j) Bf[3 * (i) + (j)]
+    real t, s;
+    t = fabs(T[0]); if (t > (a[0] + ((F_(0, 0) * b[0] + F_(0, 1) * b[1]) + F_(0, 2) * b[2]))) return 1;
+    s = (B_(0, 0) * T[0] + B_(1, 0) * T[1]) + B_(2, 0) * T[2];
+    t = fabs(s); if (t > (b[0] + ((F_(0, 0) * a[0] + F_(1, 0) * a[1]) + F_(2, 0) * a[2]))) return 1;
+    t = fabs(T[1]); if (t > (a[1] + ((F_(1, 0) * b[0] + F_(1, 1) * b[1]) + F_(1, 2) * b[2]))) return 1;
+    t = fabs(T[2]); if (t > (a[2] + ((F_(2, 0) * b[0] + F_(2, 1) * b[1]) + F_(2, 2) * b[2]))) return 1;
+    s = (B_(0, 1) * T[0] + B_(1, 1) * T[1]) + B_(2, 1) * T[2];
+    t = fabs(s); if (t > (b[1] + ((F_(0, 1) * a[0] + F_(1, 1) * a[1]) + F_(2, 1) * a[2]))) return 1;
+    s = (B_(0, 2) * T[0] + B_(1, 2) * T[1]) + B_(2, 2) * T[2];
+    t = fabs(s); if (t > (b[2] + ((F_(0, 2) * a[0] + F_(1, 2) * a[1]) + F_(2, 2) * a[2]))) return 1;
+    /* A0 x B0, B1, B2 */
+    s = T[2] * B_(1, 0) - T[1] * B_(2, 0);
+    if (fabs(s) > a[1] * F_(2, 0) + a[2] * F_(1, 0) + b[1] * F_(0, 2) + b[2] * F_(0, 1)) return 1;
+    s = T[2] * B_(1, 1) - T[1] * B_(2, 1);
+    if (fabs(s) > a[1] * F_(2, 1) + a[2] * F_(1, 1) + b[0] * F_(0, 2) + b[2] * F_(0, 0)) return 1;
+    s = T[2] * B_(1, 2) - T[1] * B_(2, 2);
+    if (fabs(s) > a[1] * F_(2, 2) + a[2] * F_(1, 2) + b[0] * F_(0, 1) + b[1] * F_(0, 0)) return 1;
+    /* A1 x B0, B1, B2 */
+    s = T[0] * B_(2, 0) - T[2] * B_(0, 0);
+    if (fabs(s) > a[0] * F_(2, 0) + a[2] * F_(0, 0) + b[1] * F_(1, 2) + b[2] * F_(1, 1)) return 1;
+    s = T[0] * B_(2, 1) - T[2] * B_(0, 1);
+    if (fabs(s) > a[0] * F_(2, 1) + a[2] * F_(0, 1) + b[0] * F_(1, 2) + b[2] * F_(1, 0)) return 1;
+    s = T[0] * B_(2, 2) - T[2] * B_(0, 2);
+    if (fabs(s) > a[0] * F_(2, 2) + a[2] * F_(0, 2) + b[0] * F_(1, 1) + b[1] * F_(1, 0)) return 1;
+    /* A2 x B0, B1, B2 */
+    s = T[1] * B_(0, 0) - T[0] * B_(1, 0);
+    if (fabs(s) > a[0] * F_(1, 0) + a[1] * F_(0, 0) + b[1] * F_(2, 2) + b[2] * F_(2, 1)) return 1;
+    s = T[1] * B_(0, 1) - T[0] * B_(1, 1);
+    if (fabs(s) > a[0] * F_(1, 1) + a[1] * F_(0, 1) + b[0] * F_(2, 2) + b[2] * F_(2, 0)) return 1;
+    s = T[1] * B_(0, 2) - T[0] * B_(1, 2);
+    if (fabs(s) > a[0] * F_(1, 2) + a[1] * F_(0, 2) + b[0] * F_(2, 1) + b[1] * F_(2, 0)) return 1;
+#undef B_
+#undef F_
+    return 0;
+}
+
+/* fcl::collide(shape, octree) -> OcTreeSolver::OcTreeShapeIntersectRecurse
+ * [ext FCL 0.7.0]: every occupied leaf in traversal order; a leaf whose OBB
+ * (octree axes, centre tf * c, extent (max - min) * 0.5) is obbDisjoint from
+ * the shape's OBB (computeBV(shape, I) -> convertBV(., tf)) is skipped,
+ * otherwise shapeIntersect(Box(max - min), tf * Translation(c), shape, tf)
+ * -- box first: boxBox2, sphereBoxIntersect or MPR -- and the first hit ends
+ * the query.  The inner nodes' OBB tests cannot reject a leaf that passes
+ * its own test (an ancestor's box contains it), so they are not restated. */
+static int octree_intersect(const orc_world *w, int go, const real *TO, int gs, const real *TS, orc_stats *st) {
+    const int l0 = (int)w->geom_param[4 * go], ln = (int)w->geom_param[4 * go + 1];
+    const int ts = w->geom_type[gs];
+    const real *ps = w->geom_param + 4 * gs;
+    /* the shape's local AABB (FCL computeBV with the identity) */
+    real lo[3], hi[3];
+    if (ts == GEOM_CONVEX) {
+        const real *V = w->verts + 3 * (size_t)w->geom_vstart[gs];
+        for (int k = 0; k < 3; ++k) lo[k] = hi[k] = V[k];
+        for (int i = 1; i < w->geom_nv[gs]; ++i)
+            for (int k = 0; k < 3; ++k) {
+                if (V[3 * i + k] < lo[k]) lo[k] = V[3 * i + k];
+                if (V[3 * i + k] > hi[k]) hi[k] = V[3 * i + k];
+            }
+    } else if (ts == GEOM_BOX) {
+        for (int k = 0; k < 3; ++k) { hi[k] = 0.5 * ps[k]; lo[k] = -hi[k]; }
+    } else if (ts == GEOM_SPHERE) {
+        for (int k = 0; k < 3; ++k) { hi[k] = ps[0]; lo[k] = -hi[k]; }
+    } else {
+        const real r = ps[0], hz = 0.5 * ps[1] + (ts == GEOM_CAPSULE ? r : 0.0);
+        lo[0] = lo[1] = -r; hi[0] = hi[1] = r; lo[2] = -hz; hi[2] = hz;
+    }
+    real lc[3], se[3], sc[3], B[9];
+    for (int k = 0; k < 3; ++k) { lc[k] = (lo[k] + hi[k]) * 0.5; se[k] = (hi[k] - lo[k]) * 0.5; }
+    for (int i = 0; i < 3; ++i) sc[i] = ((TS[3 * i] * lc[0] + TS[3 * i + 1] * lc[1]) + TS[3 * i + 2] * lc[2]) + TS[9 + i];
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) B[3 * i + j] = (TO[i] * TS[j] + TO[3 + i] * TS[3 + j]) + TO[6 + i] * TS[6 + j];
+    gjk_obj shape;
+    int shape_ready = 0;
+    for (int l = l0; l < l0 + ln; ++l) {
+        const real *L = w->oct_leaf + 6 * (size_t)l;
+        real c[3], a[3], side[3], TL[12], t[3], T[3];
+        for (int k = 0; k < 3; ++k) { c[k] = (L[k] + L[3 + k]) * 0.5; side[k] = L[3 + k] - L[k]; a[k] = side[k] * 0.5; }
+        for (int k = 0; k < 9; ++k) TL[k] = TO[k];
+        for (int i = 0; i < 3; ++i) TL[9 + i] = ((TO[3 * i] * c[0] + TO[3 * i + 1] * c[1]) + TO[3 * i + 2] * c[2]) + TO[9 + i];
+        for (int i = 0; i < 3; ++i) t[i] = sc[i] - TL[9 + i];
+        for (int i = 0; i < 3; ++i) T[i] = (TO[i] * t[0] + TO[3 + i] * t[1]) + TO[6 + i] * t[2];
+        if (obb_disjoint(B, T, a, se)) continue;
+        int hit;
+        if (ts == GEOM_BOX) hit = box_box_intersect(side, TL, ps, TS);
+        else if (ts == GEOM_SPHERE) hit = sphere_box_intersect(ps[0], TS, side, TL);
+        else {
+            if (!shape_ready) { make_obj(w, gs, TS, &shape, st); shape_ready = 1; }
+            gjk_obj box;
+            memset(&box, 0, sizeof box);
+            shape_to_gjk(TL, &box);
+            box.type = GEOM_BOX;
+            box.stats = st;
+            for (int k = 0; k < 3; ++k) box.dim[k] = side[k] / 2.0; /* boxToGJK */
+            hit = mpr_intersect(&box, &shape, 1e-6);
+        }
+        if (hit) return 1;
+    }
+    return 0;
+}
+
 #define MAX_OBJ 512
 
 /* Per-configuration worker: FK + every pair + ACM filter (allowed pairs are
@@ -1055,7 +1166,10 @@ static int collide_one(const orc_world *w, const real *q, uint32_t *mask, int W,
             else if (ks[s] == KIND_ATTACHED) { Ts[s] = att_T + 12 * is[s]; gs[s] = w->att_geom[is[s]]; }
             else { Ts[s] = w->scene_tf + 12 * is[s]; gs[s] = w->scene_geom[is[s]]; }
         }
-        int hit = closed_form_intersect(w, gs[0], Ts[0], gs[1], Ts[1]);
+        int hit;
+        if (w->geom_type[gs[1]] == GEOM_OCTREE) hit = octree_intersect(w, gs[1], Ts[1], gs[0], Ts[0], st);
+        else if (w->geom_type[gs[0]] == GEOM_OCTREE) hit = octree_intersect(w, gs[0], Ts[0], gs[1], Ts[1], st);
+        else hit = closed_form_intersect(w, gs[0], Ts[0], gs[1], Ts[1]);
         if (hit < 0) {
             for (int s = 0; s < 2; ++s) make_obj(w, gs[s], Ts[s], objs[s], st);
             hit = mpr_intersect(&a, &b, 1e-6);

@@ -404,6 +404,144 @@ class SphereGeom:
     radius: float
 
 
+GEOM_OCTREE = 5
+
+
+class OcTreeGeom:
+    """fcl::OcTree over an octomap::OcTree filled like PlanningWorld::addPointCloud
+    (src/planning_world.cpp:102-110) / fcl.OcTree(vertices, resolution)
+    (python/pybind_fcl.hpp:223-236): updateNode(point3d(x, y, z), true) per
+    point, lazy_eval = false.  Restated [ext octomap 1.9.8] from the published
+    algorithm: float point3d, coordToKeyChecked (floor(coord / res) + 32768,
+    16 levels), log-odds hit update 0.85f clamped to [-2, 3.5], the
+    early-abort search, pruned-leaf expansion, pruning of 8 equal leaf
+    children and parents holding the max child log-odds.  `leaves` are the
+    occupied leaves (log-odds >= 0, fcl::OcTree::isNodeOccupied) in FCL's
+    traversal order (children 0..7, depth first) as AABBs built by FCL's
+    getRootBV / computeChildBV recursion [ext FCL 0.7.0]: [L, 6] = min xyz,
+    max xyz in the octree frame."""
+
+    DEPTH = 16
+    MAX_KEY = 32768
+    HIT = np.float32(0.85)
+    CLAMP_MIN = np.float32(-2.0)
+    CLAMP_MAX = np.float32(3.5)
+
+    class _Node:
+        __slots__ = ("v", "ch")
+
+        def __init__(self, v=np.float32(0.0)):
+            self.v = np.float32(v)
+            self.ch = None
+
+    def __init__(self, points, resolution: float):
+        self.resolution = float(resolution)
+        self.root = None
+        inv = 1.0 / self.resolution
+        pts = np.asarray(points, dtype=np.float64).reshape(-1, 3).astype(np.float32)
+        for x, y, z in pts:
+            key = []
+            ok = True
+            for c in (x, y, z):
+                k = int(math.floor(inv * float(c))) + self.MAX_KEY
+                if k < 0 or k >= 2 * self.MAX_KEY:
+                    ok = False
+                    break
+                key.append(k)
+            if ok:
+                self._update(tuple(key))
+        self.leaves = self._leaf_boxes()
+
+    @staticmethod
+    def _has_children(n) -> bool:
+        return n.ch is not None and any(c is not None for c in n.ch)
+
+    @staticmethod
+    def _child_idx(key, bit) -> int:
+        return ((key[0] >> bit) & 1) | (((key[1] >> bit) & 1) << 1) | (((key[2] >> bit) & 1) << 2)
+
+    def _search(self, key):
+        n = self.root
+        if n is None:
+            return None
+        for bit in range(self.DEPTH - 1, -1, -1):
+            pos = self._child_idx(key, bit)
+            if n.ch is not None and n.ch[pos] is not None:
+                n = n.ch[pos]
+            elif not self._has_children(n):
+                return n
+            else:
+                return None
+        return n
+
+    def _update(self, key):
+        leaf = self._search(key)
+        if leaf is not None and leaf.v >= self.CLAMP_MAX:  # log_odds_update >= 0 and already clamped
+            return
+        created_root = False
+        if self.root is None:
+            self.root = self._Node()
+            created_root = True
+        self._recurs(self.root, created_root, key, 0)
+
+    def _recurs(self, node, just_created, key, depth):
+        if depth < self.DEPTH:
+            pos = self._child_idx(key, self.DEPTH - 1 - depth)
+            created = False
+            if node.ch is None or node.ch[pos] is None:
+                if not self._has_children(node) and not just_created:  # expand a pruned node
+                    node.ch = [self._Node(node.v) for _ in range(8)]
+                else:
+                    if node.ch is None:
+                        node.ch = [None] * 8
+                    node.ch[pos] = self._Node()
+                    created = True
+            self._recurs(node.ch[pos], created, key, depth + 1)
+            if not self._prune(node):
+                node.v = max(c.v for c in node.ch if c is not None)  # updateOccupancyChildren
+            return
+        v = np.float32(node.v + self.HIT)
+        node.v = min(max(v, self.CLAMP_MIN), self.CLAMP_MAX)
+
+    def _prune(self, node) -> bool:
+        ch = node.ch
+        if ch is None or ch[0] is None or self._has_children(ch[0]):
+            return False
+        for c in ch[1:]:
+            if c is None or self._has_children(c) or not (c.v == ch[0].v):
+                return False
+        node.v = ch[0].v
+        node.ch = None
+        return True
+
+    def _leaf_boxes(self) -> np.ndarray:
+        out = []
+        if self.root is None:
+            return np.zeros((0, 6))
+        delta = (1 << self.DEPTH) * self.resolution / 2
+
+        def rec(n, lo, hi):
+            if not self._has_children(n):
+                if n.v >= 0.0:
+                    out.append(lo + hi)
+                return
+            for i in range(8):
+                c = n.ch[i]
+                if c is None:
+                    continue
+                clo, chi = list(lo), list(hi)
+                for a in range(3):
+                    mid = (lo[a] + hi[a]) * 0.5
+                    if (i >> a) & 1:
+                        clo[a] = mid
+                    else:
+                        chi[a] = mid
+                rec(c, clo, chi)
+
+        rec(self.root, [-delta] * 3, [delta] * 3)
+        return np.array(out, dtype=np.float64).reshape(-1, 6)
+
+
 def load_convex_mesh(path: str, scale=(1.0, 1.0, 1.0)) -> ConvexGeom:
     verts, tris = load_stl(path)
     arr = np.array([[v[0] * scale[0], v[1] * scale[1], v[2] * scale[2]] for v in verts], dtype=np.float64)

@@ -504,3 +504,59 @@ def test_bench_two_ranks_gloo_one_gpu():
     r = json.loads(line)
     assert r["n_gpus"] == 2 and r["scaling"] == "weak" and r["value"] > 0
     assert r["config"]["configs_per_gpu"] == 65536
+
+
+# --------------------------------------------------------------- point clouds
+@pytest.mark.parametrize("kind", ["floor", "blue"])
+def test_point_cloud_world_matches_oracle(kind):
+    """add_point_cloud -> fcl::OcTree: (link, cloud) pairs through the device
+    octree test (grid cells -> obbDisjoint -> box-first MPR / closed forms)
+    on both the pipeline and the latency path, bit-exact with the oracle."""
+    w, art = scenes.cloud_world(kind)
+    ow_ = Wd.oracle_cloud_world(kind)
+    assert [(i[3], i[4]) for i in w.get_collision_pair_info()] == ow_.pair_names()
+    q = Wd.sample_q(ow_.art, 20000, 31)
+    fo, mo = ow_.collide_batch(q, nthreads=NTHREADS)
+    w.set_small_batch_max(0)
+    f, m = w.collide_batch(q)
+    np.testing.assert_array_equal(f, fo)
+    np.testing.assert_array_equal(m, mo)
+    w.set_small_batch_max(1 << 20)
+    f, m = w.collide_batch(q)
+    np.testing.assert_array_equal(f, fo)
+    np.testing.assert_array_equal(m, mo)
+
+
+def test_point_cloud_known_answers_and_unsupported_queries():
+    w, art = scenes.cloud_world("floor")
+    w.set_qpos_all(scenes.FLOOR_COLLIDING)
+    hits = [r for r in w.collide_with_others() if r.object_name2 == "scene_pcd"]
+    assert len(hits) >= 2  # detect_collision.py: several joints dip below the floor
+    w.set_qpos_all(Wd.KAT_FREE)
+    assert w.collide_with_others() == []
+    with pytest.raises(NotImplementedError):
+        w.distance_with_others()
+    with pytest.raises(NotImplementedError):
+        w.collide(pymp.fcl.CollisionRequest(enable_contact=True))
+
+
+def test_attached_box_against_point_cloud():
+    """An attached box (collision_avoidance.py:87-90) against the blue-cube
+    cloud: leaf boxes meet it through FCL's boxBox2 closed form."""
+    import oracle
+    from oracle import model as M
+    w, art = scenes.cloud_world("blue")
+    pose = [0.0, 0.0, 0.14, 1.0, 0.0, 0.0, 0.0]
+    w.attach_object("held", pymp.fcl.Box([0.04, 0.04, 0.12]), "panda", 8, pose, ["panda_hand"])
+    base = Wd.oracle_cloud_world("blue")
+    o2 = oracle.OracleWorld(base.art, scene=base.scene,
+                            attached=[("held", 8, M.BoxGeom((0.04, 0.04, 0.12)), _oracle_T(pose))],
+                            allowed=[("panda_hand", "held"), ("panda_link0", "table")])
+    assert [(i[3], i[4]) for i in w.get_collision_pair_info()] == o2.pair_names()
+    q = Wd.sample_q(base.art, 20000, 32)
+    f, m = w.collide_batch(q)
+    fo, mo = o2.collide_batch(q, nthreads=NTHREADS)
+    np.testing.assert_array_equal(f, fo)
+    np.testing.assert_array_equal(m, mo)
+    k = o2.pair_names().index(("held", "scene_pcd"))
+    assert int(((mo[:, k >> 5] >> (k & 31)) & 1).sum()) > 0

@@ -1,0 +1,100 @@
+"""Point clouds as world geometry: PlanningWorld.add_point_cloud / fcl.OcTree
+(src/planning_world.cpp:102-110, python/pybind_fcl.hpp:221-236).
+
+CPU: the product's octomap restatement (mplib_amd/csrc/host/octree.cpp) and
+the oracle's independent one (oracle/model.py OcTreeGeom) give identical
+leaf boxes; octomap's insertion semantics (float keys, pruning of equal
+children, clamping) on constructed clouds; the oracle's octree collision
+(obbDisjoint gate + box-first narrow phase, oracle/collide_oracle.c
+octree_intersect) against the same leaves checked one by one as scene boxes;
+the detect_collision.py floor known answers.  GPU parity: test_gpu_parity.py.
+octomap / FCL are absent here: parity with them is unpinned
+beyond these semantics.
+"""
+import numpy as np
+import pytest
+
+import oracle
+import worlds as Wd
+from mplib_amd import pymp, scenes
+from oracle import model as M
+
+
+def clouds():
+    rng = np.random.default_rng(0)
+    return [(scenes.cloud_points("blue"), 1e-3), (scenes.cloud_points("floor"), 1e-3),
+            (rng.uniform(-0.05, 0.05, (20000, 3)), 0.01),
+            (np.repeat(rng.uniform(-1, 1, (50, 3)), 7, axis=0), 0.05),
+            (rng.normal(0, 0.3, (3000, 3)), 0.004)]
+
+
+@pytest.mark.parametrize("k", range(5))
+def test_host_leaves_match_oracle_restatement(k):
+    pts, res = clouds()[k]
+    a = M.OcTreeGeom(pts, res).leaves
+    b = pymp.fcl.OcTree(pts, res).get_leaf_boxes()
+    assert a.shape == b.shape and np.array_equal(a, b)
+
+
+def test_pruning_merges_equal_children():
+    res = 0.02
+    g = (np.stack(np.meshgrid(*[np.arange(8)] * 3, indexing="ij"), -1).reshape(-1, 3) - 4 + 0.5) * res
+    leaves = M.OcTreeGeom(g, res).leaves  # 8 fully occupied 4x4x4 blocks -> 8 leaves of 4 res
+    assert len(leaves) == 8
+    assert np.allclose(leaves[:, 3:] - leaves[:, :3], 4 * res)
+    # one extra hit makes that voxel's log-odds differ: its block can no longer merge
+    leaves2 = M.OcTreeGeom(np.vstack([g, g[:1]]), res).leaves
+    assert len(leaves2) == 7 + 7 + 7 + 1  # the first octant splits down to single voxels at each level
+    assert np.array_equal(pymp.fcl.OcTree(np.vstack([g, g[:1]]), res).get_leaf_boxes(), leaves2)
+
+
+def test_keys_are_floor_of_float_coordinates():
+    res = 1e-3
+    o = M.OcTreeGeom(np.array([[-0.2, 0.0, 0.0005]]), res)
+    lo = o.leaves[0, :3]
+    # -0.2f = -0.200000003 -> key floor(-200.000003) = -201; 0.0 -> 0; 0.0005 -> 0
+    assert np.allclose(lo, [-0.201, 0.0, 0.0])
+    assert len(M.OcTreeGeom(np.array([[40.0, 0.0, 0.0]]), res).leaves) == 0  # outside 32.768 m: dropped
+
+
+def test_oracle_octree_equals_leaves_as_boxes():
+    """Octree collision (OBB gate + box-first MPR) vs every leaf as its own
+    scene box (no gate, box second): the same per-link answer."""
+    pts = scenes.cloud_points("blue")
+    oc = M.OcTreeGeom(pts, 1e-3)
+    art = Wd.panda_articulation()
+    ow = oracle.OracleWorld(art, scene=[("pcd", oc, M.IDENT)])
+    boxes = [(f"leaf{i}", M.BoxGeom(tuple(float(v) for v in L[3:] - L[:3])),
+              (list(M.IDENT[0]), [float(v) for v in (L[:3] + L[3:]) * 0.5])) for i, L in enumerate(oc.leaves)]
+    ob = oracle.OracleWorld(art, scene=boxes)
+    q = Wd.sample_q(art, 3000, 77)
+    # keep configurations that reach towards the cloud
+    f, m = ow.collide_batch(q, nthreads=8)
+    fb, mb = ob.collide_batch(q, nthreads=8)
+    n_self = ow.n_self_pairs
+    names = ow.pair_names()
+    nb = ob.pair_names()
+    for li, link in enumerate(Wd.PANDA_LINKS):
+        p = names.index((link, "pcd"))
+        got = (m[:, p >> 5] >> (p & 31)) & 1
+        idx = [k for k, nm in enumerate(nb) if nm[0] == link and nm[1].startswith("leaf")]
+        want = np.zeros(len(q), np.uint32)
+        for k in idx:
+            want |= (mb[:, k >> 5] >> (k & 31)) & 1
+        assert np.array_equal(got, want), link
+    assert f.sum() > 0 and (f == 0).sum() > 0
+    assert n_self == ob.n_self_pairs
+
+
+def test_floor_known_answers():
+    ow = Wd.oracle_cloud_world("floor")
+    f, m = ow.collide_batch(np.array([scenes.FLOOR_COLLIDING, Wd.KAT_FREE]))
+    hits = ow.decode(m[0])
+    assert f[0] == 1 and len([h for h in hits if h[1] == "scene_pcd"]) >= 2  # "several joints dip below"
+    assert f[1] == 0
+
+
+def test_product_pair_table_has_the_cloud():
+    w, _ = scenes.cloud_world("blue")
+    ow = Wd.oracle_cloud_world("blue")
+    assert [(i[3], i[4]) for i in w.get_collision_pair_info()] == ow.pair_names()
