@@ -768,10 +768,13 @@ enum : int { MPR_DONE = 0, MPR_V1 = 1, MPR_V2 = 2, MPR_V3 = 3, MPR_V4 = 4 };
 __device__ __forceinline__ bool octree_hit(const DevWorld& w, cptr<double> HV, int go, const SE3& TO, int gs,
                                            const SE3& TS);
 
-// one closed-form pair evaluation; an octree pair (CF_OCTREE) runs its leaves
+// one closed-form pair evaluation (OCT = false) or octree pair (OCT = true);
+// the two live in separate kernel instances so the octree walk's registers
+// never lower the other kernels' occupancy
+template <bool OCT>
 __device__ __forceinline__ bool pair_closed_form(int cf, const DevWorld& w, int ga, const SE3& TA, int gb,
                                                  const SE3& TB) {
-  if (cf != CF_OCTREE) return closed_form(cf, w, ga, TA, gb, TB);
+  if (!OCT) return closed_form(cf, w, ga, TA, gb, TB);
   return w.geom_type[ga] == MPG_GEOM_OCTREE ? octree_hit(w, w.hull, ga, TA, gb, TB)
                                             : octree_hit(w, w.hull, gb, TB, ga, TA);
 }
@@ -779,7 +782,7 @@ __device__ __forceinline__ bool pair_closed_form(int cf, const DevWorld& w, int 
 // FCL closed-form pairs (box-box, sphere-sphere, sphere-box) and octree
 // pairs of the candidate lists: one test per candidate.  A kernel of its own so the closed forms'
 // registers do not lower the MPR kernel's occupancy.
-template <bool FROM_POSES>
+template <bool FROM_POSES, bool OCT>
 __global__ __launch_bounds__(256) void closed_form_kernel(DevWorld w, const double* __restrict__ in,
                                                          const uint32_t* __restrict__ seg_len,
                                                          const uint32_t* __restrict__ seg_start,
@@ -800,7 +803,7 @@ __global__ __launch_bounds__(256) void closed_form_kernel(DevWorld w, const doub
     }
     const int p = lo;
     const int cf = w.pair_cf[p];
-    if (cf == CF_NONE) continue;
+    if (cf == CF_NONE || (cf == CF_OCTREE) != OCT) continue;
     const uint32_t t0 = (tk - prefix[p]) * kTask, t1 = min(seg_len[p], t0 + kTask);
     const int a = w.pair_a[p], b = w.pair_b[p];
     const bool am = a < w.n_moving, bm = b < w.n_moving;
@@ -813,7 +816,7 @@ __global__ __launch_bounds__(256) void closed_form_kernel(DevWorld w, const doub
       const long long c = cl[idx];
       const SE3 TA = am ? moving_tf<FROM_POSES>(w, in, sc, c, a) : load_se3(w.static_T + 12 * (a - w.n_moving));
       const SE3 TB = bm ? moving_tf<FROM_POSES>(w, in, sc, c, b) : load_se3(w.static_T + 12 * (b - w.n_moving));
-      if (pair_closed_form(cf, w, ga, TA, gb, TB)) {
+      if (pair_closed_form<OCT>(cf, w, ga, TA, gb, TB)) {
         if (masks) atomicOr(&masks[c * w.W + (p >> 5)], 1u << (p & 31));
         flags[c] = 1;
       }
@@ -1200,7 +1203,7 @@ __global__ __launch_bounds__(256) MPG_NARROW_WAVES void narrow_kernel(DevWorld w
 // ---------------------------------------------------------------------------
 constexpr double kSmallMargin = 1e-4;
 
-template <bool FROM_POSES>
+template <bool FROM_POSES, bool OCT>
 __global__ __launch_bounds__(256) void small_kernel(DevWorld w, const double* __restrict__ in, long long n, int n_tiles,
                                                    uint8_t* __restrict__ hits) {
   const cptr<double> HV = w.hull;
@@ -1208,6 +1211,7 @@ __global__ __launch_bounds__(256) void small_kernel(DevWorld w, const double* __
   const int wave = __builtin_amdgcn_readfirstlane((int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6));
   const int p = wave / n_tiles;
   if (p >= w.n_pairs) return;
+  if ((w.pair_cf[p] == CF_OCTREE) != OCT) return;  // octree pairs: the OCT instance
   const long long cfg = (long long)(wave - p * n_tiles) * 64 + lane;
   const bool live = cfg < n;
   const long long c = live ? cfg : n - 1;
@@ -1231,7 +1235,7 @@ __global__ __launch_bounds__(256) void small_kernel(DevWorld w, const double* __
     const double rr = ra[G_RADIUS] + rb[G_RADIUS] + kSmallMargin;
     const bool near = live && d2 <= rr * rr;
     if (cf != CF_NONE) {
-      if (near && pair_closed_form(cf, w, ga, TA, gb, TB)) hit = 1;
+      if (near && pair_closed_form<OCT>(cf, w, ga, TA, gb, TB)) hit = 1;
     } else if (__ballot(near) != 0) {
       GObj A, B;
       A.rot = gjk_rot_from_matrix(TA.R);
@@ -1923,7 +1927,8 @@ struct mpg_world {
   std::mutex motion_mu;
   bool has_closed_form = false;  // a non-allowed pair uses an FCL closed form
   bool has_octree = false;       // a non-allowed pair involves an octree
-  bool any_closed_form = false;  // some pair (allowed or not) does
+  bool any_closed_form = false;  // some pair (allowed or not) does, octrees aside
+  bool any_octree = false;       // some pair involves an octree
   // batched distance buffers (grow-only)
   struct Dist {
     double* poses = nullptr;
@@ -2300,8 +2305,13 @@ int launch_collide(mpg_world* w, const double* in, long long n, uint8_t* flags, 
                        ws->seg_start, ws->prefix, ws->cand, fl, mk, ws->prefix + w->dw.n_pairs + 1, ws->sc);
     HIP_TRY(hipGetLastError());
     if (w->any_closed_form) {
-      hipLaunchKernelGGL((closed_form_kernel<FROM_POSES>), dim3(w->narrow_blocks), dim3(256), 0, stream, w->dw, qin,
-                         ws->seg_len, ws->seg_start, ws->prefix, ws->cand, fl, mk, ws->sc);
+      hipLaunchKernelGGL((closed_form_kernel<FROM_POSES, false>), dim3(w->narrow_blocks), dim3(256), 0, stream, w->dw,
+                         qin, ws->seg_len, ws->seg_start, ws->prefix, ws->cand, fl, mk, ws->sc);
+      HIP_TRY(hipGetLastError());
+    }
+    if (w->any_octree) {
+      hipLaunchKernelGGL((closed_form_kernel<FROM_POSES, true>), dim3(w->narrow_blocks), dim3(256), 0, stream, w->dw,
+                         qin, ws->seg_len, ws->seg_start, ws->prefix, ws->cand, fl, mk, ws->sc);
       HIP_TRY(hipGetLastError());
     }
     if (co) {  // penetration info of the reported pairs (enable_contact)
@@ -2657,7 +2667,8 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
   for (int p = 0; p < d->n_pairs; ++p) {
     w->has_closed_form |= pair_cf[p] != CF_NONE && !allowed[p];
     w->has_octree |= pair_cf[p] == CF_OCTREE && !allowed[p];
-    w->any_closed_form |= pair_cf[p] != CF_NONE;
+    w->any_closed_form |= pair_cf[p] != CF_NONE && pair_cf[p] != CF_OCTREE;
+    w->any_octree |= pair_cf[p] == CF_OCTREE;
   }
   dw.static_T = to_cptr<double>(base + o_sT);
   dw.link_chain_start = to_cptr<int>(base + o_cs);
@@ -2812,9 +2823,14 @@ int collide_small(mpg_world* w, const double* q, int64_t n, uint8_t* flags, uint
   const long long waves = (long long)P * n_tiles;
   StageTimer t_small(w, s, MPG_STAGE_NARROW);
   if (w->prof) w->prof_cfg += n;
-  hipLaunchKernelGGL((small_kernel<FROM_POSES>), dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s, w->dw, w->d_qs,
-                     (long long)n, n_tiles, w->d_hits);
+  hipLaunchKernelGGL((small_kernel<FROM_POSES, false>), dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s, w->dw,
+                     w->d_qs, (long long)n, n_tiles, w->d_hits);
   HIP_TRY(hipGetLastError());
+  if (w->any_octree) {
+    hipLaunchKernelGGL((small_kernel<FROM_POSES, true>), dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s, w->dw,
+                       w->d_qs, (long long)n, n_tiles, w->d_hits);
+    HIP_TRY(hipGetLastError());
+  }
   t_small.stop();
   HIP_TRY(hipStreamSynchronize(s));
   const uint8_t* h = w->h_hits;
