@@ -10,7 +10,11 @@ A step = one pass of the hot path (FK + all 129 pairs + ACM filter) over one
 mpg_collide_batch call (cull -> bucket -> narrow kernels on one stream)
 writing flags[N] (u8) and pair_mask[N, 5] (u32).
 
-Usage:  python bench.py [--gpus N] [--steps K] [--warmup W] [--cpu-sample S]
+Other workloads (not the headline): --cfg 2 / 4 (self-only / convex
+obstacles), --cfg 6 (the detect_collision.py floor point cloud as an
+fcl::OcTree), --cfg 5 (RRTConnect plan() end to end: a step is one plan()).
+
+Usage:  python bench.py [--gpus N] [--steps K] [--warmup W] [--cpu-sample S] [--cfg C]
         torchrun --nproc-per-node N bench.py --gpus N ...
 Rank 0 prints ONE JSON line.
 """
@@ -38,7 +42,10 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--cfg", type=int, default=3, help="BASELINE config (2, 3 or 4)")
+    p.add_argument("--cfg", type=int, default=3,
+                   help="2, 3, 4: BASELINE collide configs; 5: RRTConnect plan(); 6: floor point cloud")
+    p.add_argument("--goal", default="far", help="cfg5 goal (scenes.PLAN_GOALS)")
+    p.add_argument("--cpu-plans", type=int, default=4, help="cfg5: plans timed with the CPU oracle checker")
     p.add_argument("--per-gpu", type=int, default=0, help="configs per GPU per step (default: BASELINE size)")
     p.add_argument("--cpu-sample", type=int, default=1 << 17,
                    help="configs timed on the CPU oracle for cpu_baseline (rank 0, N=1 only; 0 = skip)")
@@ -71,6 +78,8 @@ def main():
     from mplib_amd import scenes
 
     cfg = args.cfg
+    if cfg == 5:
+        return plan_main(args, world, rank, local, backend)
     n = args.per_gpu or (scenes.CFG_N[cfg] if cfg != 4 else (1 << 22) // max(world, 1))
     w, art = scenes.world(cfg)
     dim = w.get_state_dim()
@@ -152,6 +161,7 @@ def main():
 
     result = {
         "metric": "configs/sec full collide() Panda-7DoF+10 boxes" if cfg == 3 else f"configs/sec collide() cfg{cfg}",
+
         "value": value,
         "unit": "configs/s",
         "n_gpus": world,
@@ -183,6 +193,91 @@ def main():
 
     if rank == 0 and world == 1 and args.cpu_sample > 0:
         result["cpu_baseline"] = cpu_baseline(cfg, q_host[: args.cpu_sample], flags, masks, args.cpu_threads)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def plan_main(args, world, rank, local, backend):
+    """cfg5: RRTConnect plan() in the cfg3 scene, device validity (speculative
+    connect batches, latency path).  A step = one plan() from PLAN_START to
+    PLAN_GOALS[goal] with range 0.1 and seed = step index (+1000 * rank:
+    ranks are independent replicas)."""
+    import torch
+    import torch.distributed as dist
+    from mplib_amd import pymp, scenes
+
+    goal = scenes.PLAN_GOALS[args.goal]
+    w, _ = scenes.world(3)
+    planner = pymp.ompl.OMPLPlanner(w)
+
+    def one(seed):
+        pymp.set_global_seed(seed)
+        return planner.plan(scenes.PLAN_START, [goal], range=0.1, time=60.0)
+
+    for i in range(args.warmup):
+        one(10_000 + i)
+    w.profile_enable(True)
+    w.profile_read()
+    stats, paths, solved = [], {}, 0
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        st, path = one(1000 * rank + i)
+        solved += st == "Exact solution"
+        paths[i] = path
+        stats.append(planner.get_last_plan_stats())
+    elapsed = time.perf_counter() - t0
+    prof = w.profile_read()
+    w.profile_enable(False)
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda" if backend == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t[0])
+    mean = lambda k: float(np.mean([s[k] for s in stats]))  # noqa: E731
+    ms, launches, units = prof["narrow"]  # the latency path records its kernel as the narrow stage
+    kern_ms = ms / max(launches, 1)
+    states_per_launch = mean("states_checked") / max(mean("batches"), 1.0)
+    bytes_per_state = 8 * w.get_state_dim() + len(w.get_collision_pair_info())  # q row in + hit bytes out
+    achieved = bytes_per_state * states_per_launch / (kern_ms * 1e-3) / 1e9 if kern_ms > 0 else 0.0
+    result = {
+        "metric": "plans/sec RRTConnect plan() cfg5 (Panda + 10 boxes)", "value": args.steps * world / elapsed,
+        "unit": "plans/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic RRTConnect queries: seeds 0..steps-1, start tests/test_basic.py qpos, goal = IK of a "
+                "panda_hand pose (scenes.PLAN_GOALS)",
+        "config": {"workload": f"cfg5 RRTConnect {args.goal} goal, range 0.1, cfg3 scene", "goal": list(goal),
+                   "parallelism": f"replicas x{world}"},
+        "solved": solved, "mean_iterations": mean("iterations"), "mean_batches": mean("batches"),
+        "mean_states_checked": mean("states_checked"), "mean_check_ms": mean("check_seconds") * 1e3,
+        "roofline": {"bound": "latency", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBPS, "traffic": None, "kernel": "small_kernel",
+                     "kernel_ms": kern_ms, "units_per_launch": states_per_launch, "unit_kind": "states",
+                     "algorithmic_bytes_per_unit": bytes_per_state,
+                     "note": "one validity batch per planner iteration: round-trip latency, not bandwidth, "
+                             "bounds a plan"},
+    }
+    if rank == 0 and world == 1 and args.cpu_plans > 0:
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import worlds as Wd  # test fixture module: the oracle-built cfg3 world
+        ow = Wd.oracle_world(3)
+        cpu = pymp.ompl.OMPLPlanner(scenes.world(3)[0], state_validity_checker=lambda s: ow.collide_batch(s)[0] == 0)
+        cpu.set_speculative_connect(False)  # OMPL's serial loop: one batch per growTree
+        k = min(args.cpu_plans, args.steps)
+        same = True
+        t0 = time.perf_counter()
+        for i in range(k):
+            pymp.set_global_seed(i)
+            st, path = cpu.plan(scenes.PLAN_START, [goal], range=0.1, time=60.0)
+            same &= bool(np.array_equal(path, paths[i]))
+        dt = time.perf_counter() - t0
+        result["cpu_baseline"] = {"value": k / dt, "unit": "plans/s", "cores": 1, "kind": "port",
+                                  "sample": f"seeds 0..{k - 1}: the same planner with oracle/collide_oracle.c as "
+                                            f"its checker, one batch per growTree call, {dt:.1f} s",
+                                  "gpu_matches_cpu_on_sample": same}
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

@@ -7,6 +7,9 @@
         ACM (panda_link0, table) = ALWAYS  (2^20 states, default_rng(1))
   cfg4  Panda + 4 convex hulls (link3/link5/hand/link0 hulls at poses from
         default_rng(4321))  (2^22 states sharded over GPUs, default_rng(2))
+  cfg5  RRTConnect plan() in the cfg3 scene (PLAN_START -> PLAN_GOALS)
+  cfg6  Panda + the detect_collision.py floor point cloud (fcl::OcTree,
+        10000 points, resolution 1e-3)  (2^20 states, default_rng(6))
 
 States are uniform in the URDF joint limits (panda.urdf:37-157).
 """
@@ -25,9 +28,9 @@ PANDA_LINKS = ["panda_link0", "panda_link1", "panda_link2", "panda_link3", "pand
                "panda_link6", "panda_link7", "panda_hand", "panda_leftfinger", "panda_rightfinger"]
 PANDA_JOINTS = ["panda_joint1", "panda_joint2", "panda_joint3", "panda_joint4", "panda_joint5", "panda_joint6",
                 "panda_joint7", "panda_finger_joint1", "panda_finger_joint2"]
-CFG_SEED = {2: 0, 3: 1, 4: 2}
-CFG_N = {2: 1 << 16, 3: 1 << 20, 4: 1 << 22}
-CFG_NAME = {2: "panda_self", 3: "panda_10boxes", 4: "panda_4convex"}
+CFG_SEED = {2: 0, 3: 1, 4: 2, 6: 6}
+CFG_N = {2: 1 << 16, 3: 1 << 20, 4: 1 << 22, 6: 1 << 20}
+CFG_NAME = {2: "panda_self", 3: "panda_10boxes", 4: "panda_4convex", 6: "panda_floor_cloud"}
 
 
 def panda() -> "pymp.articulation.ArticulatedModel":
@@ -62,7 +65,10 @@ def _hulls():
 
 
 def world(cfg: int):
-    """(PlanningWorld, ArticulatedModel) for a BASELINE config."""
+    """(PlanningWorld, ArticulatedModel) for a BASELINE config (6: the
+    detect_collision.py floor point cloud, see cloud_world)."""
+    if cfg == 6:
+        return cloud_world("floor")
     art = panda()
     w = pymp.planning_world.PlanningWorld([art], ["panda"], [], [])
     if cfg == 3:
@@ -96,7 +102,7 @@ def sample_states(art, n: int, seed: int) -> np.ndarray:
 # x=1, y=0, z=0) -- test_basic.py:43's pose (0.4, 0.3, 0.12) grips into the
 # green cube here, so "near" is 8 cm above it; "far" reaches around box0 /
 # box1 / box2 (a few hundred RRTConnect iterations).  Computed offline by
-# least squares on the FK (tools/plan_goals.py), rounded to 1e-8.
+# least squares on the FK (tests/golden/gen_plan_goals.py), rounded to 1e-8.
 PLAN_START = [0.0, 0.2, 0.0, -2.6, 0.0, 3.0, 0.8]
 PLAN_GOALS = {
     "near": [0.33129616, 0.29436923, 0.29083465, -2.39517156, -0.1845193, 2.67095513, 1.56051207],  # (0.4, 0.3, 0.2)

@@ -4,7 +4,7 @@ The reference ships no golden vectors for this path, so
 these fixtures are REGRESSION pins of the oracle restatement, not reference
 outputs.  The only reference-sourced known answers are the two
 examples/detect_collision.py configurations, stored in kat.json.
-Run:  python tools/gen_golden.py
+Run:  python tests/golden/gen_golden.py
 """
 import json
 import os
@@ -12,7 +12,7 @@ import sys
 
 import numpy as np
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 import worlds as Wd  # noqa: E402

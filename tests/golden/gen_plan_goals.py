@@ -9,7 +9,7 @@ import sys
 import numpy as np
 from scipy.optimize import least_squares
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "tests")]
 import worlds as Wd  # noqa: E402
 

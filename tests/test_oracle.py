@@ -1,5 +1,5 @@
 """CPU: the oracle restatement against the reference's known answers and the
-committed golden vectors (regression pins; see tools/gen_golden.py)."""
+committed golden vectors (regression pins; see tests/golden/gen_golden.py)."""
 import json
 import os
 

@@ -94,6 +94,8 @@ def oracle_world(cfg: int) -> oracle.OracleWorld:
         return oracle.OracleWorld(art, scene=boxes_scene(), allowed=[("panda_link0", "table")])
     if cfg == 4:
         return oracle.OracleWorld(art, scene=convex_scene(art))
+    if cfg == 6:
+        return oracle_cloud_world("floor")
     raise ValueError(cfg)
 
 
