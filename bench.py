@@ -209,6 +209,11 @@ def plan_main(args, world, rank, local, backend):
     from mplib_amd import pymp, scenes
 
     goal = scenes.PLAN_GOALS[args.goal]
+    # plan() prints MPlib's messages ("invalid start state!! ...") on the C
+    # stdout, as the reference does: send them to stderr, keep stdout one line
+    sys.stdout.flush()
+    saved_stdout = os.dup(1)
+    os.dup2(2, 1)
     w, _ = scenes.world(3)
     planner = pymp.ompl.OMPLPlanner(w)
 
@@ -278,6 +283,8 @@ def plan_main(args, world, rank, local, backend):
                                   "sample": f"seeds 0..{k - 1}: the same planner with oracle/collide_oracle.c as "
                                             f"its checker, one batch per growTree call, {dt:.1f} s",
                                   "gpu_matches_cpu_on_sample": same}
+    sys.stdout.flush()
+    os.dup2(saved_stdout, 1)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:
