@@ -562,7 +562,10 @@ std::pair<std::string, std::vector<std::vector<double>>> OMPLPlanner::plan(
     Grow gsc = TRAPPED;
     if (!speculative_) {
       // OMPL's loop as written: one validity batch per growTree call
-      if (grow_serial(tree, tree_is_start, rstate, added) == TRAPPED) continue;
+      if (grow_serial(tree, tree_is_start, rstate, added) == TRAPPED) {
+        stats_.ext_trapped += 1;
+        continue;
+      }
       xmotion = added;
       rstate.assign(tree.state(added), tree.state(added) + d);  // copyState(rstate, tgi.xstate) when not REACHED
       gsc = grow_serial(other, other_is_start, rstate, xmotion);
@@ -626,7 +629,10 @@ std::pair<std::string, std::vector<std::vector<double>>> OMPLPlanner::plan(
     }
 
     check(batch, valid);
-    if (!all_valid(valid, 0, ext_end)) continue;  // extension TRAPPED
+    if (!all_valid(valid, 0, ext_end)) {  // extension TRAPPED
+      stats_.ext_trapped += 1;
+      continue;
+    }
     added = tree.add(target.data(), nm);
     (void)reach;
     // ---- connect: growTree on `other` while ADVANCED

@@ -90,7 +90,7 @@ class OMPLPlanner {
       bool verbose = false);
 
   struct Stats {
-    int64_t iterations = 0, batches = 0, states_checked = 0;
+    int64_t iterations = 0, batches = 0, states_checked = 0, ext_trapped = 0;
     int64_t start_tree = 0, goal_tree = 0;
     double seconds = 0.0, check_seconds = 0.0;
   };

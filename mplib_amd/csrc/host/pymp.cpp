@@ -741,6 +741,7 @@ PYBIND11_MODULE(pymp, m_all) {
              const auto& s = p.last_stats();
              py::dict d;
              d["iterations"] = s.iterations;
+             d["ext_trapped"] = s.ext_trapped;
              d["batches"] = s.batches;
              d["states_checked"] = s.states_checked;
              d["start_tree"] = s.start_tree;
