@@ -7,6 +7,8 @@
 
 #include <chrono>
 #include <cmath>
+#include <deque>
+#include <unordered_map>
 #include <cstdio>
 #include <cstdlib>
 #include <limits>
@@ -517,6 +519,23 @@ std::pair<std::string, std::vector<std::vector<double>>> OMPLPlanner::plan(
   };
   std::vector<Step> chain;
   const size_t kMaxChain = 1u << 20;
+  // speculative mode: a validity cache (a state's validity is a pure function
+  // of the state) and uniform samples drawn ahead of their iteration -- the
+  // sampler's draws do not depend on validity, so drawing early keeps the
+  // sequence
+  std::unordered_map<std::string, uint8_t> vcache;
+  auto vkey = [&](const double* st) { return std::string(reinterpret_cast<const char*>(st), sizeof(double) * d); };
+  std::deque<std::vector<double>> ahead;
+  auto peek_sample = [&](size_t j) -> const std::vector<double>& {
+    while (ahead.size() <= j) {
+      std::vector<double> r((size_t)d);
+      sample_uniform(r.data());
+      ahead.push_back(std::move(r));
+    }
+    return ahead[j];
+  };
+  std::vector<double> ext_states, chain_states, spec_states;
+  constexpr int kLookahead = 3;
   // RRTConnect::growTree (serial mode): nearest, step of at most maxDistance,
   // the motion's states in one batch
   auto grow_serial = [&](Tree& t, bool is_start, const std::vector<double>& r, int& xm) -> Grow {
@@ -555,7 +574,12 @@ std::pair<std::string, std::vector<std::vector<double>>> OMPLPlanner::plan(
         break;
       }
     }
-    sample_uniform(rstate.data());
+    if (!ahead.empty()) {
+      rstate = ahead.front();
+      ahead.pop_front();
+    } else {
+      sample_uniform(rstate.data());
+    }
 
     int added = -1, xmotion = -1;  // tgi.xmotion
     bool tgi_start = other_is_start;
@@ -583,15 +607,15 @@ std::pair<std::string, std::vector<std::vector<double>>> OMPLPlanner::plan(
       dstate = xstate.data();
       reach = false;
     }
-    batch.clear();
-    append_grow(sp, tree_is_start, tree.state(nm), dstate, batch);
-    const size_t ext_end = batch.size() / (size_t)d;
+    ext_states.clear();
+    append_grow(sp, tree_is_start, tree.state(nm), dstate, ext_states);
     const std::vector<double> target(dstate, dstate + d);  // rstate after "copyState(rstate, tgi.xstate)"
 
     // ---- speculative connect chain of `other` towards target, computed as
     // the serial loop would compute it if every motion were valid: each step
     // grows from the nearest node of other + the chain so far
     chain.clear();
+    chain_states.clear();
     double best_d;
     int tp = other.nearest(sp, target.data(), &best_d), cp = -1;
     std::vector<double> cur(other.state(tp), other.state(tp) + d);
@@ -609,9 +633,9 @@ std::pair<std::string, std::vector<std::vector<double>>> OMPLPlanner::plan(
         stp.state = target;
         stp.reach = true;
       }
-      stp.a = batch.size() / (size_t)d;
-      append_grow(sp, other_is_start, cur.data(), stp.state.data(), batch);
-      stp.b = batch.size() / (size_t)d;
+      stp.a = chain_states.size() / (size_t)d;
+      append_grow(sp, other_is_start, cur.data(), stp.state.data(), chain_states);
+      stp.b = chain_states.size() / (size_t)d;
       chain.push_back(std::move(stp));
       if (chain.back().reach) break;
       // nearest for the next growTree: the first strict minimum over the
@@ -628,8 +652,72 @@ std::pair<std::string, std::vector<std::vector<double>>> OMPLPlanner::plan(
         cur = chain[(size_t)cp].state;
     }
 
-    check(batch, valid);
-    if (!all_valid(valid, 0, ext_end)) {  // extension TRAPPED
+    // one batch: the states of this iteration not known yet, plus the
+    // extensions the next kLookahead iterations would try for every outcome
+    // of this one (assuming the ones in between are trapped)
+    auto known = [&](const std::vector<double>& st, size_t a, size_t b, bool& ok) {
+      ok = true;
+      bool all = true;
+      for (size_t i = a; i < b; ++i) {
+        auto it = vcache.find(vkey(st.data() + i * d));
+        if (it == vcache.end()) all = false;
+        else if (!it->second) ok = false;
+      }
+      return all;
+    };
+    auto need = [&](const std::vector<double>& st, size_t a, size_t b) {
+      for (size_t i = a; i < b; ++i)
+        if (!vcache.count(vkey(st.data() + i * d))) batch.insert(batch.end(), st.data() + i * d, st.data() + (i + 1) * d);
+    };
+    batch.clear();
+    bool ext_ok;
+    const size_t n_ext = ext_states.size() / (size_t)d;
+    const bool ext_known = known(ext_states, 0, n_ext, ext_ok);
+    if (!ext_known || ext_ok) {
+      need(ext_states, 0, n_ext);
+      need(chain_states, 0, chain_states.size() / (size_t)d);
+      if (!batch.empty()) {
+        spec_states.clear();
+        for (int j = 1; j <= kLookahead; ++j) {
+          const bool fut_other = (j & 1) != 0;  // iteration i+1 extends `other`, i+2 `tree`, ...
+          Tree& ft = fut_other ? other : tree;
+          const bool ft_start = fut_other ? other_is_start : tree_is_start;
+          const std::vector<double>& rj = peek_sample((size_t)j - 1);
+          std::vector<const double*> cand;
+          double be;
+          const int ne = ft.nearest(sp, rj.data(), &be);
+          cand.push_back(ft.state(ne));
+          if (fut_other) {  // prefix minima of the connect chain
+            double run = be;
+            for (auto& c : chain) {
+              const double dc = sp.distance(c.state.data(), rj.data());
+              if (dc < run) {
+                run = dc;
+                cand.push_back(c.state.data());
+              }
+            }
+          } else if (sp.distance(target.data(), rj.data()) < be) {
+            cand.push_back(target.data());
+          }
+          if (&ft == &tgoal && goals.sampled < goals.count() && goals.usable[goals.sample_pos])
+            cand.push_back(goals.state(goals.sample_pos));  // a goal root added at that iteration's start
+          for (const double* c : cand) {
+            const double dj = sp.distance(c, rj.data());
+            std::vector<double> x(rj);
+            if (dj > max_distance) {
+              sp.interpolate(c, rj.data(), max_distance / dj, x.data());
+              if (sp.equal(c, x.data())) continue;
+            }
+            append_grow(sp, ft_start, c, x.data(), spec_states);
+          }
+        }
+        need(spec_states, 0, spec_states.size() / (size_t)d);
+        check(batch, valid);
+        for (size_t i = 0; i < valid.size(); ++i) vcache[vkey(batch.data() + i * d)] = valid[i];
+      }
+      known(ext_states, 0, n_ext, ext_ok);
+    }
+    if (!ext_ok) {  // extension TRAPPED
       stats_.ext_trapped += 1;
       continue;
     }
@@ -640,7 +728,9 @@ std::pair<std::string, std::vector<std::vector<double>>> OMPLPlanner::plan(
     std::vector<int> node(chain.size(), -1);
     for (size_t k = 0; k < chain.size(); ++k) {
       const Step& s = chain[k];
-      if (!all_valid(valid, s.a, s.b)) {
+      bool step_ok;
+      known(chain_states, s.a, s.b, step_ok);
+      if (!step_ok) {
         gsc = TRAPPED;
         break;
       }
