@@ -7,8 +7,8 @@
 
 #include <chrono>
 #include <cmath>
+#include <cstring>
 #include <deque>
-#include <unordered_map>
 #include <cstdio>
 #include <cstdlib>
 #include <limits>
@@ -37,10 +37,30 @@ double PlanSpace::distance(const double* a, const double* b) const {
       const double d = std::fabs(a[i] - b[i]);
       di = d > kPi ? 2.0 * kPi - d : d;
     } else {
+      // sqrt(fl(x * x)) == |x| exactly unless x * x underflows
       const double diff = a[i] - b[i];
-      di = std::sqrt(diff * diff);
+      di = std::fabs(diff) > 1e-150 ? std::fabs(diff) : std::sqrt(diff * diff);
     }
     dist += 1.0 * di;
+  }
+  return dist;
+}
+
+double PlanSpace::distance_below(const double* a, const double* b, double bound) const {
+  // the compound distance if it is < bound, else a value >= bound: partial
+  // sums of non-negative terms never decrease, so stopping early is exact
+  double dist = 0.0;
+  for (int i = 0; i < dim; ++i) {
+    double di;
+    if (so2[i]) {
+      const double d = std::fabs(a[i] - b[i]);
+      di = d > kPi ? 2.0 * kPi - d : d;
+    } else {
+      const double diff = a[i] - b[i];
+      di = std::fabs(diff) > 1e-150 ? std::fabs(diff) : std::sqrt(diff * diff);
+    }
+    dist += 1.0 * di;
+    if (dist >= bound) return dist;
   }
   return dist;
 }
@@ -263,7 +283,7 @@ struct Tree {
     int best = -1;
     double bd = std::numeric_limits<double>::infinity();
     for (int i = 0; i < size(); ++i) {
-      const double d = sp.distance(state(i), q);
+      const double d = sp.distance_below(state(i), q, bd);
       if (d < bd) {
         bd = d;
         best = i;
@@ -304,6 +324,54 @@ bool all_valid(const std::vector<uint8_t>& v, size_t a, size_t b) {
     if (!v[i]) return false;
   return true;
 }
+
+// state -> validity, open addressing over a pool of the states' bits (no
+// per-entry allocation: the planner queries it hundreds of times per iteration)
+class ValidityCache {
+ public:
+  explicit ValidityCache(int dim) : dim_(dim), slots_(1024, -1) {}
+  // 1 valid, 0 invalid, -1 unknown
+  int find(const double* s) const {
+    size_t i = hash(s) & (slots_.size() - 1);
+    for (;; i = (i + 1) & (slots_.size() - 1)) {
+      const int e = slots_[i];
+      if (e < 0) return -1;
+      if (std::memcmp(pool_.data() + (size_t)e * dim_, s, sizeof(double) * dim_) == 0) return val_[(size_t)e];
+    }
+  }
+  void put(const double* s, uint8_t v) {
+    if (find(s) >= 0) return;
+    if (2 * (val_.size() + 1) > slots_.size()) grow();
+    insert_index(s, (int)val_.size());
+    pool_.insert(pool_.end(), s, s + dim_);
+    val_.push_back(v);
+  }
+
+ private:
+  uint64_t hash(const double* s) const {
+    uint64_t h = 0x9e3779b97f4a7c15ull;
+    for (int k = 0; k < dim_; ++k) {
+      uint64_t x;
+      std::memcpy(&x, s + k, 8);
+      h ^= x + 0x9e3779b97f4a7c15ull + (h << 6) + (h >> 2);
+      h *= 0xff51afd7ed558ccdull;
+    }
+    return h ^ (h >> 33);
+  }
+  void insert_index(const double* s, int e) {
+    size_t i = hash(s) & (slots_.size() - 1);
+    while (slots_[i] >= 0) i = (i + 1) & (slots_.size() - 1);
+    slots_[i] = e;
+  }
+  void grow() {
+    slots_.assign(slots_.size() * 2, -1);
+    for (size_t e = 0; e < val_.size(); ++e) insert_index(pool_.data() + e * dim_, (int)e);
+  }
+  int dim_;
+  std::vector<int> slots_;
+  std::vector<double> pool_;
+  std::vector<uint8_t> val_;
+};
 
 struct GoalSet {  // ob::GoalStates + PlannerInputStates goal sampling
   const PlanSpace* sp;
@@ -523,8 +591,7 @@ std::pair<std::string, std::vector<std::vector<double>>> OMPLPlanner::plan(
   // of the state) and uniform samples drawn ahead of their iteration -- the
   // sampler's draws do not depend on validity, so drawing early keeps the
   // sequence
-  std::unordered_map<std::string, uint8_t> vcache;
-  auto vkey = [&](const double* st) { return std::string(reinterpret_cast<const char*>(st), sizeof(double) * d); };
+  ValidityCache vcache(d);
   std::deque<std::vector<double>> ahead;
   auto peek_sample = [&](size_t j) -> const std::vector<double>& {
     while (ahead.size() <= j) {
@@ -614,6 +681,7 @@ std::pair<std::string, std::vector<std::vector<double>>> OMPLPlanner::plan(
     // ---- speculative connect chain of `other` towards target, computed as
     // the serial loop would compute it if every motion were valid: each step
     // grows from the nearest node of other + the chain so far
+    const auto tc0 = Clock::now();
     chain.clear();
     chain_states.clear();
     double best_d;
@@ -659,24 +727,31 @@ std::pair<std::string, std::vector<std::vector<double>>> OMPLPlanner::plan(
       ok = true;
       bool all = true;
       for (size_t i = a; i < b; ++i) {
-        auto it = vcache.find(vkey(st.data() + i * d));
-        if (it == vcache.end()) all = false;
-        else if (!it->second) ok = false;
+        const int v = vcache.find(st.data() + i * d);
+        if (v < 0) all = false;
+        else if (v == 0) ok = false;
       }
       return all;
     };
     auto need = [&](const std::vector<double>& st, size_t a, size_t b) {
       for (size_t i = a; i < b; ++i)
-        if (!vcache.count(vkey(st.data() + i * d))) batch.insert(batch.end(), st.data() + i * d, st.data() + (i + 1) * d);
+        if (vcache.find(st.data() + i * d) < 0) batch.insert(batch.end(), st.data() + i * d, st.data() + (i + 1) * d);
     };
+    // the connect chain's states go to the batch as they are (they are not
+    // queried again); extension states -- this iteration's and the
+    // speculated ones -- go through the cache
     batch.clear();
     bool ext_ok;
     const size_t n_ext = ext_states.size() / (size_t)d;
     const bool ext_known = known(ext_states, 0, n_ext, ext_ok);
+    size_t chain_off = 0;
     if (!ext_known || ext_ok) {
       need(ext_states, 0, n_ext);
-      need(chain_states, 0, chain_states.size() / (size_t)d);
+      chain_off = batch.size() / (size_t)d;
+      batch.insert(batch.end(), chain_states.begin(), chain_states.end());
       if (!batch.empty()) {
+        stats_.t_chain += seconds_since(tc0);
+        const auto ts0 = Clock::now();
         spec_states.clear();
         for (int j = 1; j <= kLookahead; ++j) {
           const bool fut_other = (j & 1) != 0;  // iteration i+1 extends `other`, i+2 `tree`, ...
@@ -711,9 +786,12 @@ std::pair<std::string, std::vector<std::vector<double>>> OMPLPlanner::plan(
             append_grow(sp, ft_start, c, x.data(), spec_states);
           }
         }
+        const size_t spec_off = batch.size() / (size_t)d;
         need(spec_states, 0, spec_states.size() / (size_t)d);
+        stats_.t_spec += seconds_since(ts0);
         check(batch, valid);
-        for (size_t i = 0; i < valid.size(); ++i) vcache[vkey(batch.data() + i * d)] = valid[i];
+        for (size_t i = 0; i < chain_off; ++i) vcache.put(batch.data() + i * d, valid[i]);
+        for (size_t i = spec_off; i < valid.size(); ++i) vcache.put(batch.data() + i * d, valid[i]);
       }
       known(ext_states, 0, n_ext, ext_ok);
     }
@@ -728,9 +806,7 @@ std::pair<std::string, std::vector<std::vector<double>>> OMPLPlanner::plan(
     std::vector<int> node(chain.size(), -1);
     for (size_t k = 0; k < chain.size(); ++k) {
       const Step& s = chain[k];
-      bool step_ok;
-      known(chain_states, s.a, s.b, step_ok);
-      if (!step_ok) {
+      if (!all_valid(valid, chain_off + s.a, chain_off + s.b)) {
         gsc = TRAPPED;
         break;
       }

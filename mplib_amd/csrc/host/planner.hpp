@@ -43,6 +43,7 @@ struct PlanSpace {
   double longest_valid_segment = 0.0;
 
   double distance(const double* a, const double* b) const;
+  double distance_below(const double* a, const double* b, double bound) const;
   void interpolate(const double* a, const double* b, double t, double* out) const;
   bool equal(const double* a, const double* b) const;
   unsigned valid_segment_count(const double* a, const double* b) const;
@@ -92,7 +93,7 @@ class OMPLPlanner {
   struct Stats {
     int64_t iterations = 0, batches = 0, states_checked = 0, ext_trapped = 0;
     int64_t start_tree = 0, goal_tree = 0;
-    double seconds = 0.0, check_seconds = 0.0;
+    double seconds = 0.0, check_seconds = 0.0, t_chain = 0.0, t_spec = 0.0;
   };
   const Stats& last_stats() const { return stats_; }
 

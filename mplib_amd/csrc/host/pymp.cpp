@@ -748,6 +748,8 @@ PYBIND11_MODULE(pymp, m_all) {
              d["goal_tree"] = s.goal_tree;
              d["seconds"] = s.seconds;
              d["check_seconds"] = s.check_seconds;
+             d["t_chain"] = s.t_chain;
+             d["t_spec"] = s.t_spec;
              return d;
            },
            "Counters of the last plan(): iterations, validity batches, states checked, tree sizes, seconds.")
