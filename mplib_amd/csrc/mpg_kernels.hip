@@ -1951,6 +1951,12 @@ struct mpg_world {
   unsigned long long* prof_units = nullptr;   // device counter: narrow candidates
   long long max_chunk = 1 << 20;
   int narrow_blocks = 1024;
+  // large batches: two halves, the second on an internal stream, so one
+  // half's latency-bound bucketing overlaps the other's compute
+  long long overlap_min = 1 << 18;  // 0 disables (env MPG_OVERLAP_MIN)
+  int overlap_parts = 2;             // env MPG_OVERLAP_PARTS
+  hipStream_t side = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   // small-batch latency path (host buffers, n <= small_max): pinned input
   // staging + host-mapped hit bytes written by small_kernel
   long long small_max = 1024;
@@ -2715,6 +2721,8 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
   // bound the candidate lists to 1 GiB: cap * n_pairs * 4 B
   w->max_chunk = std::max<long long>(4096, std::min<long long>(1 << 20, (1ll << 28) / std::max(d->n_pairs, 1)));
   if (const char* e = std::getenv("MPG_SMALL_BATCH_MAX")) w->small_max = std::atoll(e);
+  if (const char* e = std::getenv("MPG_OVERLAP_MIN")) w->overlap_min = std::atoll(e);
+  if (const char* e = std::getenv("MPG_OVERLAP_PARTS")) w->overlap_parts = std::atoi(e);
   *out = w;
   return MPG_OK;
 }
@@ -2737,6 +2745,9 @@ int mpg_world_destroy(mpg_world* w) {
   if (w->h_q) hipHostFree(w->h_q);
   if (w->h_hits) hipHostFree(w->h_hits);
   hipFree(w->d_qs);
+  if (w->side) hipStreamDestroy(w->side);
+  if (w->ev_fork) hipEventDestroy(w->ev_fork);
+  if (w->ev_join) hipEventDestroy(w->ev_join);
   hipFree(w->d_q);
   hipFree(w->d_flags);
   hipFree(w->d_masks);
@@ -2846,6 +2857,38 @@ int collide_small(mpg_world* w, const double* q, int64_t n, uint8_t* flags, uint
   return MPG_OK;
 }
 
+// stream-ordered for the caller: the side stream waits for everything queued
+// on `s` before the call, and `s` waits for the side stream's half
+template <bool FROM_POSES>
+int launch_collide_overlapped(mpg_world* w, const double* in, long long n, uint8_t* flags, uint32_t* masks,
+                              hipStream_t s) {
+  if (w->overlap_min <= 0 || n < w->overlap_min) return launch_collide<FROM_POSES>(w, in, n, flags, masks, s);
+  {
+    std::lock_guard<std::mutex> lk(w->ws_mu);
+    if (!w->side) {
+      HIP_TRY(hipStreamCreateWithFlags(&w->side, hipStreamNonBlocking));
+      HIP_TRY(hipEventCreateWithFlags(&w->ev_fork, hipEventDisableTiming));
+      HIP_TRY(hipEventCreateWithFlags(&w->ev_join, hipEventDisableTiming));
+    }
+  }
+  const size_t row = FROM_POSES ? (size_t)w->dw.n_links * 7 : (size_t)w->dw.dof;
+  // parts alternate between the caller's stream and the side stream
+  const int parts = std::max(2, w->overlap_parts);
+  const long long step = ((n + parts - 1) / parts + 63) / 64 * 64;
+  HIP_TRY(hipEventRecord(w->ev_fork, s));
+  HIP_TRY(hipStreamWaitEvent(w->side, w->ev_fork, 0));
+  int k = 0;
+  for (long long off = 0; off < n; off += step, ++k) {
+    const long long m = std::min(step, n - off);
+    const int rc = launch_collide<FROM_POSES>(w, in + (size_t)off * row, m, flags + off,
+                                              masks ? masks + (size_t)off * w->dw.W : nullptr, (k & 1) ? w->side : s);
+    if (rc) return rc;
+  }
+  HIP_TRY(hipEventRecord(w->ev_join, w->side));
+  HIP_TRY(hipStreamWaitEvent(s, w->ev_join, 0));
+  return MPG_OK;
+}
+
 template <bool FROM_POSES>
 int collide_common(mpg_world* w, const double* q, int64_t n, uint8_t* flags, uint32_t* pair_mask, int mem,
                    void* stream) {
@@ -2854,7 +2897,7 @@ int collide_common(mpg_world* w, const double* q, int64_t n, uint8_t* flags, uin
   if (n > 0 && (!q || !flags)) return set_error(MPG_E_INVALID, "input/flags is NULL");
   HIP_TRY(hipSetDevice(w->device));
   hipStream_t s = static_cast<hipStream_t>(stream);
-  if (mem == MPG_MEM_DEVICE) return launch_collide<FROM_POSES>(w, q, n, flags, pair_mask, s);
+  if (mem == MPG_MEM_DEVICE) return launch_collide_overlapped<FROM_POSES>(w, q, n, flags, pair_mask, s);
   if (mem != MPG_MEM_HOST) return set_error(MPG_E_INVALID, "bad mem kind");
   const size_t row = FROM_POSES ? (size_t)w->dw.n_links * 7 : (size_t)w->dw.dof;
   std::lock_guard<std::mutex> lk(w->host_mu);
@@ -2864,7 +2907,7 @@ int collide_common(mpg_world* w, const double* q, int64_t n, uint8_t* flags, uin
   if (n == 0) return MPG_OK;
   double* din = FROM_POSES ? w->d_out : w->d_q;
   if (row) HIP_TRY(hipMemcpyAsync(din, q, sizeof(double) * n * row, hipMemcpyHostToDevice, s));
-  rc = launch_collide<FROM_POSES>(w, din, n, w->d_flags, w->d_masks, s);
+  rc = launch_collide_overlapped<FROM_POSES>(w, din, n, w->d_flags, w->d_masks, s);
   if (rc) return rc;
   HIP_TRY(hipMemcpyAsync(flags, w->d_flags, n, hipMemcpyDeviceToHost, s));
   if (pair_mask)
