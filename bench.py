@@ -154,7 +154,7 @@ def main():
     if os.path.exists(pmc_file):
         try:
             pm = json.load(open(pmc_file))
-            if pm.get("configs_per_launch") == n and dom in pm.get("hbm_bytes_per_launch", {}):
+            if pm.get("configs_per_launch") == int(st["cull"]["units_per_launch"]) and dom in pm.get("hbm_bytes_per_launch", {}):
                 traffic = pm["hbm_bytes_per_launch"][dom]
         except Exception:
             traffic = None
