@@ -240,7 +240,10 @@ __device__ __forceinline__ GObj moving_obj(const DevWorld& w, const double* __re
 // specialisations, both argument orders), boolean part; same operation order
 // as the oracle (oracle/collide_oracle.c box_box_intersect & co.)
 // ---------------------------------------------------------------------------
-enum : int { CF_NONE = 0, CF_BOX_BOX = 1, CF_SPHERE_SPHERE = 2, CF_SPHERE_BOX = 3, CF_BOX_SPHERE = 4, CF_OCTREE = 5 };
+enum : int {
+  CF_NONE = 0, CF_BOX_BOX = 1, CF_SPHERE_SPHERE = 2, CF_SPHERE_BOX = 3, CF_BOX_SPHERE = 4, CF_OCTREE = 5,
+  CF_SPHERE_CAPSULE = 6, CF_CAPSULE_SPHERE = 7, CF_SPHERE_CYLINDER = 8, CF_CYLINDER_SPHERE = 9
+};
 
 // detail::boxBox2 (box_box-inl.h, from ODE dBoxBox): return_code != 0
 __device__ __forceinline__ bool box_box_intersect(const double* side1, const SE3& T1, const double* side2,
@@ -358,6 +361,68 @@ __device__ __forceinline__ bool sphere_box_intersect(double r, const SE3& TS, co
   return !(clamped && dd > r * r);
 }
 
+// the sphere centre in the other shape's frame: X_FO.inverse() * X_FS
+// translation, R^T p_S + (-(R^T p_O)) with Eigen's evaluation order
+__device__ __forceinline__ void centre_in_frame(const SE3& TS, const SE3& TO, double* c) {
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const double inv_t = -((TO.R[i] * TO.p[0] + TO.R[3 + i] * TO.p[1]) + TO.R[6 + i] * TO.p[2]);
+    c[i] = ((TO.R[i] * TS.p[0] + TO.R[3 + i] * TS.p[1]) + TO.R[6 + i] * TS.p[2]) + inv_t;
+  }
+}
+
+// detail::sphereCapsuleIntersect (sphere_capsule-inl.h): the closest point of
+// the capsule's axis segment (0,0,+lz/2)-(0,0,-lz/2) to the sphere centre
+// (lineSegmentPointClosestToPoint), then |diff| - r1 - r2 > 0 -> separated
+__device__ __forceinline__ bool sphere_capsule_intersect(double r1, const SE3& TS, double r2, double lz,
+                                                         const SE3& TC) {
+  double c[3];
+  centre_in_frame(TS, TC, c);
+  const double s1z = 0.5 * lz, s2z = -s1z;
+  const double vz = s2z - s1z;
+  const double w2 = c[2] - s1z;
+  const double c1 = (c[0] * 0.0 + c[1] * 0.0) + w2 * vz;
+  const double c2 = (0.0 * 0.0 + 0.0 * 0.0) + vz * vz;
+  double spz;
+  if (c1 <= 0) spz = s1z;
+  else if (c2 <= c1) spz = s2z;
+  else spz = s1z + vz * (c1 / c2);
+  const double d0 = c[0], d1 = c[1], d2 = c[2] - spz;
+  const double dist = std::sqrt((d0 * d0 + d1 * d1) + d2 * d2) - r1 - r2;
+  return !(dist > 0);
+}
+
+// detail::sphereCylinderIntersect (sphere_cylinder-inl.h): nearestPointInCylinder
+// (clamp z to +-lz/2, the radial part to the radius), inside -> intersect,
+// else squared distance against r^2
+__device__ __forceinline__ bool sphere_cylinder_intersect(double r, const SE3& TS, double rc, double lz,
+                                                          const SE3& TC) {
+  double c[3], n[3];
+  centre_in_frame(TS, TC, c);
+  const double h = lz / 2;
+  bool clamped = false;
+  n[0] = c[0];
+  n[1] = c[1];
+  n[2] = c[2];
+  if (c[2] > h) {
+    n[2] = h;
+    clamped = true;
+  } else if (c[2] < -h) {
+    n[2] = -h;
+    clamped = true;
+  }
+  const double rd2 = c[0] * c[0] + c[1] * c[1];
+  if (rd2 > rc * rc) {
+    const double scale = rc / std::sqrt(rd2);
+    n[0] = c[0] * scale;
+    n[1] = c[1] * scale;
+    clamped = true;
+  }
+  if (!clamped) return true;
+  const double d0 = n[0] - c[0], d1 = n[1] - c[1], d2 = n[2] - c[2];
+  return !(((d0 * d0 + d1 * d1) + d2 * d2) > r * r);
+}
+
 __device__ __forceinline__ bool closed_form(int kind, const DevWorld& w, int ga, const SE3& TA, int gb,
                                             const SE3& TB) {
   const cptr<double> pa = w.geom_rec + G_STRIDE * ga + G_PARAM, pb = w.geom_rec + G_STRIDE * gb + G_PARAM;
@@ -366,6 +431,10 @@ __device__ __forceinline__ bool closed_form(int kind, const DevWorld& w, int ga,
     case CF_BOX_BOX: return box_box_intersect(sa, TA, sb, TB);
     case CF_SPHERE_SPHERE: return sphere_sphere_intersect(sa[0], TA, sb[0], TB);
     case CF_SPHERE_BOX: return sphere_box_intersect(sa[0], TA, sb, TB);
+    case CF_SPHERE_CAPSULE: return sphere_capsule_intersect(sa[0], TA, sb[0], sb[1], TB);
+    case CF_CAPSULE_SPHERE: return sphere_capsule_intersect(sb[0], TB, sa[0], sa[1], TA);
+    case CF_SPHERE_CYLINDER: return sphere_cylinder_intersect(sa[0], TA, sb[0], sb[1], TB);
+    case CF_CYLINDER_SPHERE: return sphere_cylinder_intersect(sb[0], TB, sa[0], sa[1], TA);
     default: return sphere_box_intersect(sb[0], TB, sa, TA);  // CF_BOX_SPHERE
   }
 }
@@ -1998,6 +2067,10 @@ int closed_form_kind(const mpg_world_desc* d, int a, int b) {
   if (ta == MPG_GEOM_SPHERE && tb == MPG_GEOM_SPHERE) return CF_SPHERE_SPHERE;
   if (ta == MPG_GEOM_SPHERE && tb == MPG_GEOM_BOX) return CF_SPHERE_BOX;
   if (ta == MPG_GEOM_BOX && tb == MPG_GEOM_SPHERE) return CF_BOX_SPHERE;
+  if (ta == MPG_GEOM_SPHERE && tb == MPG_GEOM_CAPSULE) return CF_SPHERE_CAPSULE;
+  if (ta == MPG_GEOM_CAPSULE && tb == MPG_GEOM_SPHERE) return CF_CAPSULE_SPHERE;
+  if (ta == MPG_GEOM_SPHERE && tb == MPG_GEOM_CYLINDER) return CF_SPHERE_CYLINDER;
+  if (ta == MPG_GEOM_CYLINDER && tb == MPG_GEOM_SPHERE) return CF_CYLINDER_SPHERE;
   return CF_NONE;
 }
 
@@ -2048,20 +2121,9 @@ int validate(const mpg_world_desc* d) {
     const int a = d->pair_a[p], b = d->pair_b[p];
     if (a < 0 || a >= nobj || b < 0 || b >= nobj) return set_error(MPG_E_INVALID, "pair object id out of range");
     if (a >= d->n_moving && b >= d->n_moving) return set_error(MPG_E_INVALID, "static-static pair");
-    const int ta = d->geom_type[a < d->n_moving ? d->moving_geom[a] : d->static_geom[a - d->n_moving]];
-    const int tb = d->geom_type[b < d->n_moving ? d->moving_geom[b] : d->static_geom[b - d->n_moving]];
-    // FCL 0.7.0 GJKSolver_libccd routes these pairs to closed-form tests, not
-    // MPR; they are not implemented on the device yet.
-    // box-box, sphere-sphere and sphere-box run FCL's closed forms on the
-    // device; sphere-capsule / sphere-cylinder (and capsule-capsule, whose
-    // FCL 0.7 routing is unverified here) are not implemented yet
-    const bool sa = ta == MPG_GEOM_SPHERE, sb = tb == MPG_GEOM_SPHERE;
-    if ((sa && (tb == MPG_GEOM_CAPSULE || tb == MPG_GEOM_CYLINDER)) ||
-        (sb && (ta == MPG_GEOM_CAPSULE || ta == MPG_GEOM_CYLINDER)) ||
-        (ta == MPG_GEOM_CAPSULE && tb == MPG_GEOM_CAPSULE))
-      return set_error(MPG_E_UNSUPPORTED,
-                       "pair uses an FCL closed-form narrow phase (sphere-capsule/cylinder or capsule-capsule) "
-                       "that is not implemented on the device");
+    // FCL 0.7.0 GJKSolver_libccd: box-box, sphere-sphere, sphere-box,
+    // sphere-capsule and sphere-cylinder have closed forms (all on the
+    // device, closed_form_kind); every other shape pair is MPR
   }
   if (!finite_all(d->joint_placement, 12 * (size_t)d->n_joints) || !finite_all(d->link_placement, 12 * (size_t)d->n_links) ||
       !finite_all(d->vertices, 3 * (size_t)d->n_vertices))

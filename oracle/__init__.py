@@ -159,6 +159,12 @@ class OracleWorld:
                 ginterior += [0.0] * 3
                 leaves.append(np.asarray(g.leaves, dtype=np.float64).reshape(-1))
                 nleaves += len(g.leaves)
+            elif isinstance(g, (M.CapsuleGeom, M.CylinderGeom)):
+                gtype.append(M.GEOM_CAPSULE if isinstance(g, M.CapsuleGeom) else M.GEOM_CYLINDER)
+                gvstart.append(0)
+                gnv.append(0)
+                gparam += [float(g.radius), float(g.lz), 0.0, 0.0]
+                ginterior += [0.0] * 3
             elif isinstance(g, M.SphereGeom):
                 gtype.append(M.GEOM_SPHERE)
                 gvstart.append(0)

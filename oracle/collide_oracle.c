@@ -872,6 +872,60 @@ static int sphere_box_intersect(real r, const real *TS, const real *side, const 
     return 1;
 }
 
+/* the sphere centre in the other shape's frame: X_FO.inverse() * X_FS */
+static void centre_in_frame(const real *TS, const real *TO, real *c) {
+    for (int i = 0; i < 3; ++i) {
+        const real inv_t = -((TO[i] * TO[9] + TO[3 + i] * TO[10]) + TO[6 + i] * TO[11]);
+        c[i] = ((TO[i] * TS[9] + TO[3 + i] * TS[10]) + TO[6 + i] * TS[11]) + inv_t;
+    }
+}
+
+/* detail::sphereCapsuleIntersect (sphere_capsule-inl.h [ext FCL 0.7.0]):
+ * lineSegmentPointClosestToPoint(s_c, (0,0,lz/2), (0,0,-lz/2)), then
+ * |s_c - sp| - r1 - r2 > 0 -> separated */
+static int sphere_capsule_intersect(real r1, const real *TS, real r2, real lz, const real *TC) {
+    real c[3];
+    centre_in_frame(TS, TC, c);
+    const real s1[3] = {0.0, 0.0, 0.5 * lz}, s2[3] = {0.0, 0.0, -(0.5 * lz)};
+    const real v[3] = {s2[0] - s1[0], s2[1] - s1[1], s2[2] - s1[2]};
+    const real w[3] = {c[0] - s1[0], c[1] - s1[1], c[2] - s1[2]};
+    const real c1 = (w[0] * v[0] + w[1] * v[1]) + w[2] * v[2];
+    const real c2 = (v[0] * v[0] + v[1] * v[1]) + v[2] * v[2];
+    real sp[3];
+    if (c1 <= 0) { sp[0] = s1[0]; sp[1] = s1[1]; sp[2] = s1[2]; }
+    else if (c2 <= c1) { sp[0] = s2[0]; sp[1] = s2[1]; sp[2] = s2[2]; }
+    else {
+        const real b = c1 / c2;
+        for (int i = 0; i < 3; ++i) sp[i] = s1[i] + v[i] * b;
+    }
+    const real d[3] = {c[0] - sp[0], c[1] - sp[1], c[2] - sp[2]};
+    const real dist = sqrt((d[0] * d[0] + d[1] * d[1]) + d[2] * d[2]) - r1 - r2;
+    return !(dist > 0);
+}
+
+/* detail::sphereCylinderIntersect (sphere_cylinder-inl.h [ext FCL 0.7.0]):
+ * nearestPointInCylinder clamps z to +-lz/2 and the radial part to the
+ * radius; an unclamped centre is inside; else squared distance vs r^2 */
+static int sphere_cylinder_intersect(real r, const real *TS, real rc, real lz, const real *TC) {
+    real c[3], n[3];
+    centre_in_frame(TS, TC, c);
+    const real h = lz / 2;
+    int clamped = 0;
+    n[0] = c[0]; n[1] = c[1]; n[2] = c[2];
+    if (c[2] > h) { n[2] = h; clamped = 1; }
+    else if (c[2] < -h) { n[2] = -h; clamped = 1; }
+    const real rd2 = c[0] * c[0] + c[1] * c[1];
+    if (rd2 > rc * rc) {
+        const real scale = rc / sqrt(rd2);
+        n[0] = c[0] * scale;
+        n[1] = c[1] * scale;
+        clamped = 1;
+    }
+    if (!clamped) return 1;
+    const real d[3] = {n[0] - c[0], n[1] - c[1], n[2] - c[2]};
+    return !(((d[0] * d[0] + d[1] * d[1]) + d[2] * d[2]) > r * r);
+}
+
 /* 1/0 for a closed-form pair, -1 when the pair goes through MPR */
 static int closed_form_intersect(const orc_world *w, int ga, const real *Ta, int gb, const real *Tb) {
     const int ta = w->geom_type[ga], tb = w->geom_type[gb];
@@ -880,6 +934,10 @@ static int closed_form_intersect(const orc_world *w, int ga, const real *Ta, int
     if (ta == GEOM_SPHERE && tb == GEOM_SPHERE) return sphere_sphere_intersect(pa[0], Ta, pb[0], Tb);
     if (ta == GEOM_SPHERE && tb == GEOM_BOX) return sphere_box_intersect(pa[0], Ta, pb, Tb);
     if (ta == GEOM_BOX && tb == GEOM_SPHERE) return sphere_box_intersect(pb[0], Tb, pa, Ta);
+    if (ta == GEOM_SPHERE && tb == GEOM_CAPSULE) return sphere_capsule_intersect(pa[0], Ta, pb[0], pb[1], Tb);
+    if (ta == GEOM_CAPSULE && tb == GEOM_SPHERE) return sphere_capsule_intersect(pb[0], Tb, pa[0], pa[1], Ta);
+    if (ta == GEOM_SPHERE && tb == GEOM_CYLINDER) return sphere_cylinder_intersect(pa[0], Ta, pb[0], pb[1], Tb);
+    if (ta == GEOM_CYLINDER && tb == GEOM_SPHERE) return sphere_cylinder_intersect(pb[0], Tb, pa[0], pa[1], Ta);
     return -1;
 }
 

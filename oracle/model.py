@@ -404,6 +404,18 @@ class SphereGeom:
     radius: float
 
 
+@dataclass
+class CapsuleGeom:
+    radius: float
+    lz: float
+
+
+@dataclass
+class CylinderGeom:
+    radius: float
+    lz: float
+
+
 GEOM_OCTREE = 5
 
 

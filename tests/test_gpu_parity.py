@@ -560,3 +560,54 @@ def test_attached_box_against_point_cloud():
     np.testing.assert_array_equal(m, mo)
     k = o2.pair_names().index(("held", "scene_pcd"))
     assert int(((mo[:, k >> 5] >> (k & 31)) & 1).sum()) > 0
+
+
+def test_capsule_cylinder_worlds_match_oracle():
+    """Capsule / cylinder obstacles and attachments: convex-capsule and
+    capsule-capsule through MPR, sphere-capsule / sphere-cylinder (both
+    argument orders) through FCL's closed forms."""
+    import oracle
+    from oracle import model as M
+    w, art = scenes.world(3)
+    rng = np.random.default_rng(77)
+    extra = []
+    for k in range(6):
+        c = rng.uniform([0.2, -0.4, 0.1], [0.7, 0.4, 0.7])
+        q = rng.normal(size=4)
+        q /= np.linalg.norm(q)
+        r, lz = float(rng.uniform(0.03, 0.08)), float(rng.uniform(0.1, 0.3))
+        if k < 2:
+            g, og, name = pymp.fcl.Capsule(r, lz), M.CapsuleGeom(r, lz), f"cap{k}"
+        elif k < 4:
+            g, og, name = pymp.fcl.Cylinder(r, lz), M.CylinderGeom(r, lz), f"cyl{k}"
+        else:
+            g, og, name = pymp.fcl.Sphere(r), M.SphereGeom(r), f"ball{k}"
+        w.add_normal_object(name, pymp.fcl.CollisionObject(g, list(c), list(q)))
+        extra.append((name, og, _oracle_T(list(c) + list(q))))
+    p_orb = [0.0, 0.0, 0.12, 1.0, 0.0, 0.0, 0.0]
+    p_rod = [0.0, 0.05, 0.0, 0.7071067811865476, 0.7071067811865476, 0.0, 0.0]
+    w.attach_object("orb", pymp.fcl.Sphere(0.05), "panda", 8, p_orb, ["panda_hand"])
+    w.attach_object("rod", pymp.fcl.Capsule(0.02, 0.2), "panda", 6, p_rod, ["panda_link6", "panda_link7"])
+    base = ow(3)
+    o2 = oracle.OracleWorld(base.art, scene=list(base.scene) + extra,
+                            attached=[("orb", 8, M.SphereGeom(0.05), _oracle_T(p_orb)),
+                                      ("rod", 6, M.CapsuleGeom(0.02, 0.2), _oracle_T(p_rod))],
+                            allowed=[("panda_hand", "orb"), ("panda_link6", "rod"), ("panda_link7", "rod"),
+                                     ("panda_link0", "table")])
+    order = {pn: k for k, pn in enumerate(o2.pair_names())}
+    names = [(i[3], i[4]) for i in w.get_collision_pair_info()]
+    assert sorted(names) == sorted(o2.pair_names())
+    perm = [order[n] for n in names]
+    q = Wd.sample_q(base.art, 30000, 23)
+    fo, mo = o2.collide_batch(q, nthreads=NTHREADS)
+    bits = lambda M_, P: np.stack([(M_[:, p >> 5] >> (p & 31)) & 1 for p in P], 1)
+    for small in (0, 1 << 20):
+        w.set_small_batch_max(small)
+        f, m = w.collide_batch(q)
+        np.testing.assert_array_equal(f, fo)
+        np.testing.assert_array_equal(bits(m, range(len(perm))), bits(mo, perm))
+    hit = bits(mo, perm)
+    for pair in [("orb", "cap0"), ("orb", "cyl2"), ("rod", "ball4"), ("rod", "cap0")]:
+        if pair in names:
+            assert hit[:, names.index(pair)].sum() >= 0
+    assert int(hit.sum()) > 0

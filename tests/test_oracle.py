@@ -6,7 +6,9 @@ import os
 import numpy as np
 import pytest
 
+import oracle
 import worlds as Wd
+from oracle import model as M
 
 
 @pytest.fixture(scope="module")
@@ -261,3 +263,52 @@ def test_contact_batch_consistent_with_collide():
     nz = depth[hit == 1] > 0
     np.testing.assert_allclose(np.linalg.norm(normal[hit == 1][nz], axis=1), 1.0, atol=1e-12)
     assert (depth >= 0).all()
+
+
+def _pair(ow, ga, Ta, gb, Tb):
+    import ctypes
+    DP = ctypes.POINTER(ctypes.c_double)
+    a = np.ascontiguousarray(Ta, dtype=np.float64)
+    b = np.ascontiguousarray(Tb, dtype=np.float64)
+    return oracle.lib().orc_collide_pair(ctypes.byref(ow._w), ga, a.ctypes.data_as(DP), gb, b.ctypes.data_as(DP))
+
+
+def _rand_T(rng):
+    q = rng.normal(size=4)
+    q /= np.linalg.norm(q)
+    R = np.array(M.quat_to_mat(*q)).reshape(3, 3)
+    return R, rng.uniform(-0.3, 0.3, 3)
+
+
+def test_sphere_capsule_cylinder_closed_forms_match_geometry():
+    """FCL's sphereCapsuleIntersect / sphereCylinderIntersect restatements
+    against the plain geometry (sphere centre to axis segment / to the solid
+    cylinder), away from touching contact, both argument orders."""
+    cap, cyl, ball = M.CapsuleGeom(0.05, 0.3), M.CylinderGeom(0.06, 0.25), M.SphereGeom(0.08)
+    ow = oracle.OracleWorld(Wd.panda_articulation(),
+                            scene=[("cap", cap, M.IDENT), ("cyl", cyl, M.IDENT), ("ball", ball, M.IDENT)])
+    gi = {id(g): k for k, g in enumerate(ow.geoms)}
+    rng = np.random.default_rng(3)
+    checked = {"cap": [0, 0], "cyl": [0, 0]}
+    for _ in range(4000):
+        Rs, ps = _rand_T(rng)
+        Ro, po = _rand_T(rng)
+        Ts = np.concatenate([Rs.reshape(-1), ps])
+        To = np.concatenate([Ro.reshape(-1), po])
+        c = Ro.T @ (ps - po)  # sphere centre in the other shape's frame
+        for name, g in (("cap", cap), ("cyl", cyl)):
+            if name == "cap":
+                z = np.clip(c[2], -g.lz / 2, g.lz / 2)
+                d = np.linalg.norm(c - [0, 0, z]) - g.radius - ball.radius
+            else:
+                rxy = np.hypot(c[0], c[1])
+                dz = max(abs(c[2]) - g.lz / 2, 0.0)
+                dr = max(rxy - g.radius, 0.0)
+                d = np.hypot(dz, dr) - ball.radius
+            if abs(d) < 1e-9:
+                continue
+            want = int(d <= 0)
+            assert _pair(ow, gi[id(ball)], Ts, gi[id(g)], To) == want
+            assert _pair(ow, gi[id(g)], To, gi[id(ball)], Ts) == want
+            checked[name][want] += 1
+    assert min(min(v) for v in checked.values()) > 100  # both outcomes exercised

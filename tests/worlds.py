@@ -157,6 +157,16 @@ def desc_arrays(ow: oracle.OracleWorld) -> dict:
             nv += len(g.vertices)
             verts.append(g.vertices.reshape(-1))
             gparam += [0.0] * 4
+        elif isinstance(g, M.SphereGeom):
+            gtype.append(2)
+            gvs.append(0)
+            gnv.append(0)
+            gparam += [float(g.radius), 0.0, 0.0, 0.0]
+        elif isinstance(g, (M.CapsuleGeom, M.CylinderGeom)):
+            gtype.append(3 if isinstance(g, M.CapsuleGeom) else 4)
+            gvs.append(0)
+            gnv.append(0)
+            gparam += [float(g.radius), float(g.lz), 0.0, 0.0]
         else:
             gtype.append(1)
             gvs.append(0)
