@@ -25,6 +25,15 @@ namespace mpg {
 
 constexpr float kBpMargin = 1e-4f;  // metres
 
+// The broad phase is conservative by its margins, not bit-exact: its fp32
+// arithmetic may fuse multiply-adds (more accurate, fewer instructions) even
+// though the file is built with -ffp-contract=off for the exact fp64 path.
+#ifdef __clang__
+#define MPG_FP32_CONTRACT _Pragma("clang fp contract(fast)")
+#else
+#define MPG_FP32_CONTRACT
+#endif
+
 // per moving object float record: local OBB centre, half extents, radius
 enum { BM_C = 0, BM_E = 3, BM_R = 6, BM_STRIDE = 8 };
 // per static object float record: world OBB centre, axes (R columns), extents
@@ -68,6 +77,7 @@ MPG_INLINE F34 f34_load(P a) {
 }
 
 MPG_INLINE F34 f34_mul(const F34& A, const F34& B) {
+  MPG_FP32_CONTRACT
   F34 C;
 #pragma unroll
   for (int i = 0; i < 3; ++i) {
@@ -227,6 +237,7 @@ struct FObb {
 
 // 15-axis separating-axis test with every bound widened by `margin`
 MPG_INLINE bool fobb_separated(const FObb& A, const FObb& B, float margin) {
+  MPG_FP32_CONTRACT
   const float d[3] = {B.c[0] - A.c[0], B.c[1] - A.c[1], B.c[2] - A.c[2]};
   float Rm[3][3], Ab[3][3];
 #pragma unroll
@@ -269,6 +280,7 @@ MPG_INLINE bool fobb_separated(const FObb& A, const FObb& B, float margin) {
 // moving-object bounding sphere vs static OBB
 template <class P>
 MPG_INLINE bool fsphere_obb_separated(const float* c, float r, P sobj, float margin) {
+  MPG_FP32_CONTRACT
   const float d[3] = {c[0] - sobj[BS_C], c[1] - sobj[BS_C + 1], c[2] - sobj[BS_C + 2]};
   float acc = 0.f;
 #pragma unroll
