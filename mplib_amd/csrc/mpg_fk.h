@@ -64,7 +64,6 @@ struct DevWorld {
   cptr<int> sched_start;  // [n_moving+1]
   cptr<int> sched_pair;
   cptr<int> sched_other;
-  cptr<float> sched_box;  // [entries][6] pre-test box of a static partner
   // octrees: leaf boxes [L][6] (octree frame), per geometry a uniform grid
   // record (OG_*), cell -> leaf lists (CSR)
   cptr<double> oct_leaf;

@@ -626,13 +626,8 @@ __global__ __launch_bounds__(BLOCK) void cull_kernel(DevWorld w, const double* _
     for (int e = e0; e < e1; ++e) {
       const int p = w.sched_pair[e], o = w.sched_other[e];
       bool keep;
-      if (o >= w.n_moving) {  // box pre-test, the sphere-OBB test only where it passes
-        const cptr<float> bx = w.sched_box + 6 * e;
-        const bool in = cm[0] >= bx[0] && cm[0] <= bx[3] && cm[1] >= bx[1] && cm[1] <= bx[4] && cm[2] >= bx[2] &&
-                        cm[2] <= bx[5];
-        keep = in;
-        if (__ballot(in && live) != 0)
-          keep = in && !fsphere_obb_separated(cm, r_m, w.bp.sobj + BS_STRIDE * (o - w.n_moving), kBpMargin);
+      if (o >= w.n_moving) {
+        keep = !fsphere_obb_separated(cm, r_m, w.bp.sobj + BS_STRIDE * (o - w.n_moving), kBpMargin);
       } else {
         const float* ro = cen + (size_t)o * 3 * BLOCK + tid;
         const float dx = ro[0] - cm[0], dy = ro[BLOCK] - cm[1], dz = ro[2 * BLOCK] - cm[2];
@@ -680,7 +675,7 @@ __global__ __launch_bounds__(BLOCK) void cull_kernel(DevWorld w, const double* _
       if (lane == 0) cnt[(long long)(k * 32 + b) * n_tiles + tile] = (uint32_t)__popcll(bb);
     }
   }
-  if (FROM_POSES || w.debug_mode == 4) return;  // 4: diagnostics only (phase B then reads stale sin/cos)
+  if (FROM_POSES) return;
   // Exact fp64 sin/cos of every revolute move-group joint for the narrow
   // phase's chain FK (the glibc sincos restatement), only for configurations
   // with a candidate pair (about a quarter of them): compacted across the
@@ -2606,7 +2601,6 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
   for (int p = 0; p < d->n_pairs; ++p) pair_cf[p] = closed_form_kind(d, d->pair_a[p], d->pair_b[p]);
   // phase-A schedule: non-allowed pairs grouped by their lower moving object
   std::vector<int> sched_start(d->n_moving + 1, 0), sched_pair, sched_other;
-  std::vector<float> sched_box;
   for (int m = 0; m < d->n_moving; ++m) {
     sched_start[m] = (int)sched_pair.size();
     for (int p = 0; p < d->n_pairs; ++p) {
@@ -2616,22 +2610,6 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
       if (lo == m) {
         sched_pair.push_back(p);
         sched_other.push_back(hi);
-        // static partner: the world box that holds every centre whose sphere
-        // can pass the sphere-OBB test -- AABB(OBB) grown by r_m + margin,
-        // from the same fp32 record, rounded outward with 1e-5 m to spare
-        float bx[6] = {-FLT_MAX, -FLT_MAX, -FLT_MAX, FLT_MAX, FLT_MAX, FLT_MAX};
-        if (hi >= d->n_moving) {
-          const float* r = bpp.sobj.data() + BS_STRIDE * (hi - d->n_moving);
-          const double rr = (double)bpp.mobj[BM_STRIDE * m + BM_R] + (double)kBpMargin + 1e-5;
-          for (int i = 0; i < 3; ++i) {
-            double h = 0.0;
-            for (int j = 0; j < 3; ++j) h += std::fabs((double)r[BS_R + 3 * i + j]) * (double)r[BS_E + j];
-            h = h * (1.0 + 1e-6) + rr;
-            bx[i] = std::nextafter((float)((double)r[BS_C + i] - h), -INFINITY);
-            bx[3 + i] = std::nextafter((float)((double)r[BS_C + i] + h), INFINITY);
-          }
-        }
-        sched_box.insert(sched_box.end(), bx, bx + 6);
       }
     }
   }
@@ -2677,8 +2655,6 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
   const size_t o_ss = bb.add(sched_start.data(), sched_start.size());
   const size_t o_sp = bb.add(sched_pair.data(), sched_pair.size());
   const size_t o_so = bb.add(sched_other.data(), sched_other.size());
-  if (sched_box.empty()) sched_box.assign(6, 0.f);
-  const size_t o_sbx = bb.add(sched_box.data(), sched_box.size());
   const size_t o_bjs = bb.add(bpp.jsrc.data(), bpp.jsrc.size());
   const size_t o_bjv = bb.add(bpp.jsave.data(), bpp.jsave.size());
   const size_t o_bja = bb.add(bpp.jaxis.data(), bpp.jaxis.size());
@@ -2770,7 +2746,6 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
   dw.sched_start = I(o_ss);
   dw.sched_pair = I(o_sp);
   dw.sched_other = I(o_so);
-  dw.sched_box = to_cptr<float>(base + o_sbx);
   auto F = [&](size_t o) { return to_cptr<float>(base + o); };
   BpView& bp = dw.bp;
   bp.nj = d->n_joints;

@@ -1,5 +1,5 @@
 # Phase-timing ablation of the collide pipeline (diagnostic env switches in
-# mpg_kernels.hip): MPG_DEBUG_CULL=1 records only, 2 no SAT, 3 no MPR, 4 no exact sin/cos;
+# mpg_kernels.hip): MPG_DEBUG_CULL=1 records only, 2 no SAT, 3 no MPR;
 # MPG_STATS=1 prints narrow-phase candidate/support counts.
 set -o pipefail
 export TMPDIR=/tmp
