@@ -86,6 +86,9 @@ extern "C" {
 #define MPG_GEOM_CYLINDER 4 /* fcl::Cylinder : param = radius, lz            */
 #define MPG_GEOM_OCTREE 5   /* fcl::OcTree   : param = first leaf, leaf count,
                                resolution; static objects only          */
+#define MPG_GEOM_MESH 6     /* fcl::BVHModel<OBBRSS> (non-convex mesh):
+                               vertices, param = first triangle, triangle
+                               count (mesh_triangle)                     */
 
 /*
  * World descriptor.  SE3 values are 12 doubles: a row-major 3x3 rotation
@@ -148,6 +151,12 @@ typedef struct mpg_world_desc {
    *     yields them (PlanningWorldTpl::addPointCloud, planning_world.cpp:102-110) */
   int64_t n_octree_leaves;
   const double *octree_leaf;      /* [n_octree_leaves*6]                    */
+
+  /* --- BVH meshes (MPG_GEOM_MESH, load_mesh_as_BVH, src/urdf_utils.cpp:
+   *     136-155): triangles as three vertex indices relative to the mesh's
+   *     geom_vertex_start */
+  int64_t n_mesh_triangles;
+  const int32_t *mesh_triangle;   /* [n_mesh_triangles*3]                   */
 } mpg_world_desc;
 
 typedef struct mpg_world mpg_world;

@@ -43,6 +43,7 @@ class WorldDesc(ctypes.Structure):
         ("n_pairs", ctypes.c_int32), ("pair_a", _I32P), ("pair_b", _I32P), ("pair_allowed", _U8P),
         ("gjk_tolerance", ctypes.c_double),
         ("n_octree_leaves", ctypes.c_int64), ("octree_leaf", _F64P),
+        ("n_mesh_triangles", ctypes.c_int64), ("mesh_triangle", _I32P),
     ]
 
 

@@ -75,6 +75,12 @@ class DeviceWorld:
             leaves = np.zeros(6)
         self._keep.append(leaves)
         d.octree_leaf = leaves.ctypes.data_as(C._F64P)
+        tris = np.ascontiguousarray(np.asarray(arrays.get("mesh_triangle", np.zeros(0)), dtype=np.int32).reshape(-1))
+        d.n_mesh_triangles = tris.size // 3
+        if tris.size == 0:
+            tris = np.zeros(3, np.int32)
+        self._keep.append(tris)
+        d.mesh_triangle = tris.ctypes.data_as(C._I32P)
         h = ctypes.c_void_p()
         C.check(L.mpg_world_create(ctypes.byref(d), device, ctypes.byref(h)), "mpg_world_create")
         self._keep = []

@@ -81,6 +81,28 @@ struct OcTree : CollisionGeometry {
   explicit OcTree(double res);
   OcTree(const std::vector<Vec3>& points, double res);
 };
+// fcl::BVHModel<OBBRSS> of a triangle mesh (load_mesh_as_BVH,
+// src/urdf_utils.cpp:136-155): vertices and triangles as loaded
+struct BVHModel : CollisionGeometry {
+  std::vector<Vec3> vertices;
+  std::vector<std::array<int, 3>> triangles;
+  bool building = false;  // between beginModel and endModel
+  BVHModel() {
+    type = MPG_GEOM_MESH;
+    kind = "BVHModel";
+  }
+  BVHModel(std::vector<Vec3> v, std::vector<std::array<int, 3>> t) : BVHModel() { add_sub_model(v, t); }
+  // fcl BVHModel::addSubModel: vertices appended, triangle indices offset by
+  // the vertices already present
+  void add_sub_model(const std::vector<Vec3>& v, const std::vector<std::array<int, 3>>& t) {
+    const int off = (int)vertices.size();
+    for (auto& tr : t)
+      for (int k : tr)
+        if (k < 0 || k >= (int)v.size()) throw std::invalid_argument("BVHModel: triangle index out of range");
+    vertices.insert(vertices.end(), v.begin(), v.end());
+    for (auto& tr : t) triangles.push_back({tr[0] + off, tr[1] + off, tr[2] + off});
+  }
+};
 // geometry kinds the reference binds that the device cannot evaluate yet
 struct UnsupportedGeometry : CollisionGeometry {
   explicit UnsupportedGeometry(const std::string& k) { kind = k; }
@@ -191,6 +213,7 @@ struct MeshData {
 };
 MeshData load_stl(const std::string& path);
 std::shared_ptr<Convex> load_mesh_as_convex(const std::string& path, const Vec3& scale);
+std::shared_ptr<BVHModel> load_mesh_as_bvh(const std::string& path, const Vec3& scale);
 
 // ---------------------------------------------------------------------------
 // device world handle (RAII over mpg_world)
@@ -225,6 +248,7 @@ struct DescBuilder {
   std::vector<double> link_placement;
   std::vector<int32_t> geom_type, geom_vertex_start, geom_vertex_count;
   std::vector<double> geom_param, vertices, octree_leaf;
+  std::vector<int32_t> mesh_triangle;
   std::vector<int32_t> moving_link, moving_geom;
   std::vector<double> moving_offset;
   std::vector<int32_t> static_geom;

@@ -317,6 +317,16 @@ std::shared_ptr<Convex> load_mesh_as_convex(const std::string& path, const Vec3&
   return std::make_shared<Convex>(std::move(v), (int)m.faces.size(), std::move(f));
 }
 
+// load_mesh_as_BVH (src/urdf_utils.cpp:136-155): the same vertices
+// ((S)p * scale) and triangles, kept as a triangle mesh
+std::shared_ptr<BVHModel> load_mesh_as_bvh(const std::string& path, const Vec3& scale) {
+  MeshData m = load_stl(path);
+  std::vector<Vec3> v;
+  v.reserve(m.vertices.size());
+  for (auto& p : m.vertices) v.push_back({p[0] * scale[0], p[1] * scale[1], p[2] * scale[2]});
+  return std::make_shared<BVHModel>(std::move(v), std::move(m.faces));
+}
+
 // ---------------------------------------------------------------------------
 // request / device world helpers
 // ---------------------------------------------------------------------------
@@ -379,6 +389,18 @@ int DescBuilder::add_geometry(const CollisionGeometry* g) {
     prm[1] = (double)oc->leaves.size();
     prm[2] = oc->resolution;
     for (auto& l : oc->leaves) octree_leaf.insert(octree_leaf.end(), l.begin(), l.end());
+  } else if (auto bm = dynamic_cast<const BVHModel*>(g)) {
+    if (bm->building) throw std::invalid_argument("BVHModel used before endModel()");
+    vs = (int)(vertices.size() / 3);
+    nv = (int)bm->vertices.size();
+    for (auto& v : bm->vertices) {
+      vertices.push_back(v[0]);
+      vertices.push_back(v[1]);
+      vertices.push_back(v[2]);
+    }
+    prm[0] = (double)(mesh_triangle.size() / 3);
+    prm[1] = (double)bm->triangles.size();
+    for (auto& t : bm->triangles) mesh_triangle.insert(mesh_triangle.end(), t.begin(), t.end());
   } else if (auto cv = dynamic_cast<const Convex*>(g)) {
     vs = (int)(vertices.size() / 3);
     nv = (int)cv->vertices.size();
@@ -428,6 +450,8 @@ mpg_world_desc DescBuilder::desc() const {
   d.gjk_tolerance = gjk_tolerance;
   d.n_octree_leaves = (int64_t)(octree_leaf.size() / 6);
   d.octree_leaf = octree_leaf.data();
+  d.n_mesh_triangles = (int64_t)(mesh_triangle.size() / 3);
+  d.mesh_triangle = mesh_triangle.data();
   return d;
 }
 

@@ -405,7 +405,7 @@ void FCLModel::dfs(const UrdfModel& urdf, const std::string& link_name, const st
       std::string path = package_dir_.empty() ? fn : package_dir_ + "/" + fn;
       if (verbose_) std::cout << "File name " << fn << std::endl;
       if (convex) g = load_mesh_as_convex(path, geom.scale);
-      else g = std::make_shared<UnsupportedGeometry>("BVHModel");  // non-convex meshes: BVH narrow phase
+      else g = load_mesh_as_bvh(path, geom.scale);
     } else if (geom.kind == UrdfGeometry::CYLINDER) {
       g = std::make_shared<Cylinder>(geom.radius, geom.length);
     } else if (geom.kind == UrdfGeometry::BOX) {

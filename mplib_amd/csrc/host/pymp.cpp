@@ -131,6 +131,62 @@ PYBIND11_MODULE(pymp, m_all) {
         return vec(p.data(), 3);
       });
 
+  // fcl.BVHModel (python/pybind_fcl.hpp:177-219): triangle mesh built with
+  // beginModel / addSubModel / endModel
+  auto tri_arg = [](py::array_t<int, py::array::c_style | py::array::forcecast> f) {
+    if (f.ndim() != 2 || f.shape(1) != 3) throw std::invalid_argument("faces must be [M, 3]");
+    std::vector<std::array<int, 3>> t;
+    auto b = f.unchecked<2>();
+    for (ssize_t i = 0; i < f.shape(0); ++i) t.push_back({b(i, 0), b(i, 1), b(i, 2)});
+    return t;
+  };
+  auto vert_arg = [](py::array_t<double, py::array::c_style | py::array::forcecast> v) {
+    if (v.ndim() != 2 || v.shape(1) != 3) throw std::invalid_argument("vertices must be [N, 3]");
+    std::vector<Vec3> vv;
+    auto a = v.unchecked<2>();
+    for (ssize_t i = 0; i < v.shape(0); ++i) vv.push_back({a(i, 0), a(i, 1), a(i, 2)});
+    return vv;
+  };
+  py::class_<BVHModel, CollisionGeometry, std::shared_ptr<BVHModel>>(m, "BVHModel")
+      .def(py::init<>())
+      .def(
+          "beginModel",
+          [](BVHModel& b, int num_faces, int num_vertices) {
+            (void)num_faces;
+            (void)num_vertices;
+            b.vertices.clear();
+            b.triangles.clear();
+            b.building = true;
+          },
+          py::arg("num_faces") = 0, py::arg("num_vertices") = 0)
+      .def("endModel", [](BVHModel& b) { b.building = false; })
+      .def(
+          "addSubModel", [=](BVHModel& b, py::array_t<double> v) { b.add_sub_model(vert_arg(v), {}); },
+          py::arg("vertices"))
+      .def(
+          "addSubModel", [=](BVHModel& b, py::array_t<double> v, py::array_t<int> f) {
+            b.add_sub_model(vert_arg(v), tri_arg(f));
+          },
+          py::arg("vertices"), py::arg("faces"))
+      .def("get_vertices",
+           [](const BVHModel& b) {
+             py::array_t<double> a({(ssize_t)b.vertices.size(), (ssize_t)3});
+             auto x = a.mutable_unchecked<2>();
+             for (size_t i = 0; i < b.vertices.size(); ++i)
+               for (int k = 0; k < 3; ++k) x(i, k) = b.vertices[i][k];
+             return a;
+           })
+      .def("get_faces",
+           [](const BVHModel& b) {
+             py::array_t<int> a({(ssize_t)b.triangles.size(), (ssize_t)3});
+             auto x = a.mutable_unchecked<2>();
+             for (size_t i = 0; i < b.triangles.size(); ++i)
+               for (int k = 0; k < 3; ++k) x(i, k) = b.triangles[i][k];
+             return a;
+           })
+      .def_property_readonly("num_faces", [](const BVHModel& b) { return (int)b.triangles.size(); })
+      .def_property_readonly("num_vertices", [](const BVHModel& b) { return (int)b.vertices.size(); });
+
   // fcl.OcTree (python/pybind_fcl.hpp:221-236)
   py::class_<OcTree, CollisionGeometry, std::shared_ptr<OcTree>>(m, "OcTree")
       .def(py::init<double>(), py::arg("resolution"))
@@ -259,6 +315,9 @@ PYBIND11_MODULE(pymp, m_all) {
            py::call_guard<py::gil_scoped_release>())
       .def("print_collision_pairs", &FCLModel::print_collision_pairs);
 
+  m.def("load_mesh_as_BVH",
+        [](const std::string& path, const std::vector<double>& scale) { return load_mesh_as_bvh(path, vec3_arg(scale)); },
+        py::arg("mesh_path"), py::arg("scale"));
   m.def("load_mesh_as_Convex",
         [](const std::string& path, const std::vector<double>& scale) {
           return load_mesh_as_convex(path, vec3_arg(scale));

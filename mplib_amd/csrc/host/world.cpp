@@ -293,10 +293,8 @@ void PlanningWorld::attach_box(const Vec3& size, const std::string& art, int lin
   attach_object(art + "_" + std::to_string(link) + "_box", std::make_shared<Box>(size), art, link, pose);
 }
 void PlanningWorld::attach_mesh(const std::string& path, const std::string& art, int link, const Vec7& pose) {
-  // reference loads the mesh as a BVH (non-convex) model
-  (void)path;
-  attach_object(art + "_" + std::to_string(link) + "_mesh", std::make_shared<UnsupportedGeometry>("BVHModel"), art,
-                link, pose);
+  // load_mesh_as_BVH(mesh_path, (1, 1, 1)) (planning_world.cpp:212-218)
+  attach_object(art + "_" + std::to_string(link) + "_mesh", load_mesh_as_bvh(path, {1.0, 1.0, 1.0}), art, link, pose);
 }
 bool PlanningWorld::detach_object(const std::string& n, bool also_remove) {
   if (also_remove) {

@@ -70,8 +70,12 @@ struct DevWorld {
   cptr<double> oct_grid;   // [n_geoms * OG_STRIDE]
   cptr<int> oct_cells;     // cell start offsets into oct_list
   cptr<int> oct_list;      // leaf indices
+  // BVH meshes: one record per triangle (TR_*), mesh frame
+  cptr<double> mesh_tri;
 };
 enum { OG_ORIGIN = 0, OG_INV = 3, OG_DIMS = 4, OG_CELL0 = 7, OG_STRIDE = 8 };
+// triangle record: vertices P1 P2 P3, then the triangle's AABB
+enum { TR_P = 0, TR_LO = 9, TR_HI = 12, TR_STRIDE = 16 };
 
 template <class P>
 MPG_INLINE SE3 load_se3(P p) {

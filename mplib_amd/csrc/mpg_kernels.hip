@@ -242,8 +242,13 @@ __device__ __forceinline__ GObj moving_obj(const DevWorld& w, const double* __re
 // ---------------------------------------------------------------------------
 enum : int {
   CF_NONE = 0, CF_BOX_BOX = 1, CF_SPHERE_SPHERE = 2, CF_SPHERE_BOX = 3, CF_BOX_SPHERE = 4, CF_OCTREE = 5,
-  CF_SPHERE_CAPSULE = 6, CF_CAPSULE_SPHERE = 7, CF_SPHERE_CYLINDER = 8, CF_CYLINDER_SPHERE = 9
+  CF_SPHERE_CAPSULE = 6, CF_CAPSULE_SPHERE = 7, CF_SPHERE_CYLINDER = 8, CF_CYLINDER_SPHERE = 9, CF_MESH = 10
 };
+// narrow-phase classes of the candidate lists: each its own kernel instance
+enum : int { CLS_CLOSED = 0, CLS_OCTREE = 1, CLS_MESH = 2 };
+__host__ __device__ __forceinline__ int cf_class(int cf) {
+  return cf == CF_OCTREE ? CLS_OCTREE : cf == CF_MESH ? CLS_MESH : CLS_CLOSED;
+}
 
 // detail::boxBox2 (box_box-inl.h, from ODE dBoxBox): return_code != 0
 __device__ __forceinline__ bool box_box_intersect(const double* side1, const SE3& T1, const double* side2,
@@ -837,13 +842,17 @@ enum : int { MPR_DONE = 0, MPR_V1 = 1, MPR_V2 = 2, MPR_V3 = 3, MPR_V4 = 4 };
 __device__ __forceinline__ bool octree_hit(const DevWorld& w, cptr<double> HV, int go, const SE3& TO, int gs,
                                            const SE3& TS);
 
-// one closed-form pair evaluation (OCT = false) or octree pair (OCT = true);
-// the two live in separate kernel instances so the octree walk's registers
+__device__ __forceinline__ bool mesh_hit(const DevWorld& w, cptr<double> HV, int ga, const SE3& TA, int gb,
+                                         const SE3& TB);
+
+// one pair evaluation of class CLS: closed form, octree walk or BVH mesh
+// walk; each class lives in its own kernel instance so the walks' registers
 // never lower the other kernels' occupancy
-template <bool OCT>
+template <int CLS>
 __device__ __forceinline__ bool pair_closed_form(int cf, const DevWorld& w, int ga, const SE3& TA, int gb,
                                                  const SE3& TB) {
-  if (!OCT) return closed_form(cf, w, ga, TA, gb, TB);
+  if (CLS == CLS_CLOSED) return closed_form(cf, w, ga, TA, gb, TB);
+  if (CLS == CLS_MESH) return mesh_hit(w, w.hull, ga, TA, gb, TB);
   return w.geom_type[ga] == MPG_GEOM_OCTREE ? octree_hit(w, w.hull, ga, TA, gb, TB)
                                             : octree_hit(w, w.hull, gb, TB, ga, TA);
 }
@@ -851,7 +860,7 @@ __device__ __forceinline__ bool pair_closed_form(int cf, const DevWorld& w, int 
 // FCL closed-form pairs (box-box, sphere-sphere, sphere-box) and octree
 // pairs of the candidate lists: one test per candidate.  A kernel of its own so the closed forms'
 // registers do not lower the MPR kernel's occupancy.
-template <bool FROM_POSES, bool OCT>
+template <bool FROM_POSES, int CLS>
 __global__ __launch_bounds__(256) void closed_form_kernel(DevWorld w, const double* __restrict__ in,
                                                          const uint32_t* __restrict__ seg_len,
                                                          const uint32_t* __restrict__ seg_start,
@@ -872,7 +881,7 @@ __global__ __launch_bounds__(256) void closed_form_kernel(DevWorld w, const doub
     }
     const int p = lo;
     const int cf = w.pair_cf[p];
-    if (cf == CF_NONE || (cf == CF_OCTREE) != OCT) continue;
+    if (cf == CF_NONE || cf_class(cf) != CLS) continue;
     const uint32_t t0 = (tk - prefix[p]) * kTask, t1 = min(seg_len[p], t0 + kTask);
     const int a = w.pair_a[p], b = w.pair_b[p];
     const bool am = a < w.n_moving, bm = b < w.n_moving;
@@ -885,7 +894,7 @@ __global__ __launch_bounds__(256) void closed_form_kernel(DevWorld w, const doub
       const long long c = cl[idx];
       const SE3 TA = am ? moving_tf<FROM_POSES>(w, in, sc, c, a) : load_se3(w.static_T + 12 * (a - w.n_moving));
       const SE3 TB = bm ? moving_tf<FROM_POSES>(w, in, sc, c, b) : load_se3(w.static_T + 12 * (b - w.n_moving));
-      if (pair_closed_form<OCT>(cf, w, ga, TA, gb, TB)) {
+      if (pair_closed_form<CLS>(cf, w, ga, TA, gb, TB)) {
         if (masks) atomicOr(&masks[c * w.W + (p >> 5)], 1u << (p & 31));
         flags[c] = 1;
       }
@@ -1132,6 +1141,301 @@ __device__ __forceinline__ bool octree_hit(const DevWorld& w, cptr<double> HV, i
   return false;
 }
 
+
+// ---------------------------------------------------------------------------
+// BVH meshes (fcl::BVHModel<OBBRSS>, load_mesh_as_BVH src/urdf_utils.cpp:
+// 136-155).  fcl::collide's BVH traversal only prunes triangle (pairs) whose
+// bounding volumes are disjoint, so the boolean answer is "some leaf test
+// succeeds"; a lane walks the triangles behind a conservative AABB test in
+// the mesh frame (widened by 1e-9, far above rounding: a pruned triangle is
+// genuinely separated).  Leaf tests as FCL 0.7.0 runs them:
+//   mesh-mesh   Intersect::intersect_Triangle(p, q, R, T), R = R1^T R2,
+//               T = R1^T (t2 - t1), q' = R q + T
+//   shape-mesh  shapeTriangleIntersect(shape, tf, P1, P2, P3, tf_mesh): shape
+//               first; sphereTriangleIntersect for spheres, else libccd MPR
+//               on the triangle GJK object (triCreateGJKObject)
+// Same operation order as the oracle (oracle/collide_oracle.c).
+// ---------------------------------------------------------------------------
+constexpr double kMeshPad = 1e-9;
+
+__device__ __forceinline__ double d3(const double* a, const double* b) { return (a[0] * b[0] + a[1] * b[1]) + a[2] * b[2]; }
+__device__ __forceinline__ void c3(double* o, const double* a, const double* b) {
+  o[0] = a[1] * b[2] - a[2] * b[1];
+  o[1] = a[2] * b[0] - a[0] * b[2];
+  o[2] = a[0] * b[1] - a[1] * b[0];
+}
+
+// Intersect::project6
+__device__ __forceinline__ bool project6(const double* ax, const double* p2, const double* p3, const double* q1,
+                                         const double* q2, const double* q3) {
+  const double P1 = (ax[0] * 0.0 + ax[1] * 0.0) + ax[2] * 0.0;  // p1 = 0
+  const double P2 = d3(ax, p2), P3 = d3(ax, p3), Q1 = d3(ax, q1), Q2 = d3(ax, q2), Q3 = d3(ax, q3);
+  const double mx1 = fmax(P1, fmax(P2, P3)), mn1 = fmin(P1, fmin(P2, P3));
+  const double mx2 = fmax(Q1, fmax(Q2, Q3)), mn2 = fmin(Q1, fmin(Q2, Q3));
+  return !(mn1 > mx2) && !(mn2 > mx1);
+}
+
+// Intersect::intersect_Triangle without contact output: n1, m1, the nine
+// edge cross products, g1..g3, h1..h3
+__device__ __noinline__ bool tri_tri_intersect(const double* P, const double* Q) {
+  double p2[3], p3[3], q1[3], q2[3], q3[3], e[3][3], f[3][3], n1[3], m1[3], ax[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    p2[k] = P[3 + k] - P[k];
+    p3[k] = P[6 + k] - P[k];
+    q1[k] = Q[k] - P[k];
+    q2[k] = Q[3 + k] - P[k];
+    q3[k] = Q[6 + k] - P[k];
+  }
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    e[0][k] = p2[k] - 0.0;
+    e[1][k] = p3[k] - p2[k];
+    e[2][k] = 0.0 - p3[k];
+    f[0][k] = q2[k] - q1[k];
+    f[1][k] = q3[k] - q2[k];
+    f[2][k] = q1[k] - q3[k];
+  }
+  c3(n1, e[0], e[1]);
+  c3(m1, f[0], f[1]);
+  if (!project6(n1, p2, p3, q1, q2, q3)) return false;
+  if (!project6(m1, p2, p3, q1, q2, q3)) return false;
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) {
+      c3(ax, e[i], f[j]);
+      if (!project6(ax, p2, p3, q1, q2, q3)) return false;
+    }
+  for (int i = 0; i < 3; ++i) {
+    c3(ax, e[i], n1);
+    if (!project6(ax, p2, p3, q1, q2, q3)) return false;
+  }
+  for (int i = 0; i < 3; ++i) {
+    c3(ax, f[i], m1);
+    if (!project6(ax, p2, p3, q1, q2, q3)) return false;
+  }
+  return true;
+}
+
+// segmentSqrDistance (sphere_triangle-inl.h)
+__device__ __forceinline__ double segment_sqr_distance(const double* from, const double* to, const double* p) {
+  double diff[3], v[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    diff[k] = p[k] - from[k];
+    v[k] = to[k] - from[k];
+  }
+  double t = d3(v, diff);
+  if (t > 0) {
+    const double vv = d3(v, v);
+    if (t < vv) {
+      t /= vv;
+#pragma unroll
+      for (int k = 0; k < 3; ++k) diff[k] -= v[k] * t;
+    } else {
+#pragma unroll
+      for (int k = 0; k < 3; ++k) diff[k] -= v[k];
+    }
+  }
+  return d3(diff, diff);
+}
+
+// sphereTriangleIntersect (sphere_triangle-inl.h), boolean part; W = world
+// triangle (tf_mesh * P), c = sphere centre
+__device__ __noinline__ bool sphere_triangle_intersect(double radius, const double* c, const double* W) {
+  double a[3], b[3], n[3], pc[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    a[k] = W[3 + k] - W[k];
+    b[k] = W[6 + k] - W[k];
+  }
+  c3(n, a, b);
+  const double z = d3(n, n);
+  if (z > 0) {
+    const double s = std::sqrt(z);
+    n[0] /= s;
+    n[1] /= s;
+    n[2] /= s;
+  }
+  const double rt = radius + DBL_EPSILON;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) pc[k] = c[k] - W[k];
+  double dist = d3(pc, n);
+  if (dist < 0) {
+    dist *= -1;
+    n[0] *= -1;
+    n[1] *= -1;
+    n[2] *= -1;
+  }
+  if (!(dist < rt)) return false;
+  {  // projectInTriangle
+    double e1[3], e2[3], e3[3], u[3], v[3], x[3], en[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      e1[k] = W[3 + k] - W[k];
+      e2[k] = W[6 + k] - W[3 + k];
+      e3[k] = W[k] - W[6 + k];
+      u[k] = c[k] - W[k];
+      v[k] = c[k] - W[3 + k];
+      x[k] = c[k] - W[6 + k];
+    }
+    c3(en, e1, n);
+    const double r1 = d3(en, u);
+    c3(en, e2, n);
+    const double r2 = d3(en, v);
+    c3(en, e3, n);
+    const double r3 = d3(en, x);
+    if ((r1 > 0 && r2 > 0 && r3 > 0) || (r1 <= 0 && r2 <= 0 && r3 <= 0)) return true;
+  }
+  const double r2 = rt * rt;
+  if (segment_sqr_distance(W, W + 3, c) < r2) return true;
+  if (segment_sqr_distance(W + 3, W + 6, c) < r2) return true;
+  if (segment_sqr_distance(W + 6, W, c) < r2) return true;
+  return false;
+}
+
+// libccd support of (uniform shape a) - (per-lane triangle b: vertices P in
+// the mesh frame, centroid tc): supportTriangle picks argmax dir . (p - c)
+__device__ __forceinline__ V3 msupport_tri(const DevWorld& w, cptr<double> HV, const GObj& a, const GObj& b,
+                                           const double* P, const V3& tc, const V3& dir) {
+  const V3 da = quat_rot(dir, a.rot_inv), db = quat_rot(vscale(dir, -1.0), b.rot_inv);
+  const int ga = __builtin_amdgcn_readfirstlane(a.geom), ta = __builtin_amdgcn_readfirstlane(a.type);
+  const V3 la = support_local(w, HV, ga, ta, da);
+  double maxdot = -DBL_MAX;
+  V3 lb = v3(P[0], P[1], P[2]);
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const V3 pc = v3(P[3 * i] - tc.x, P[3 * i + 1] - tc.y, P[3 * i + 2] - tc.z);
+    const double dot = vdot(db, pc);
+    if (dot > maxdot) {
+      lb = v3(P[3 * i], P[3 * i + 1], P[3 * i + 2]);
+      maxdot = dot;
+    }
+  }
+  return vsub(vadd(quat_rot(la, a.rot), a.pos), vadd(quat_rot(lb, b.rot), b.pos));
+}
+
+// (shape gs at TS, mesh gm at TM): shape first in every leaf test
+__device__ __noinline__ bool mesh_shape_hit(const DevWorld& w, cptr<double> HV, int gm, const SE3& TM, int gs,
+                                            const SE3& TS) {
+  const cptr<double> grm = w.geom_rec + G_STRIDE * gm, grs = w.geom_rec + G_STRIDE * gs;
+  const int ts = w.geom_type[gs];
+  const int t0 = (int)grm[G_PARAM], tn = (int)grm[G_PARAM + 1];
+  // the shape's local box in the mesh frame, widened
+  double sc[3], cl[3], Rl[9], hq[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+    sc[i] = ((TS.R[3 * i] * grs[G_OBB_C] + TS.R[3 * i + 1] * grs[G_OBB_C + 1]) + TS.R[3 * i + 2] * grs[G_OBB_C + 2]) + TS.p[i];
+  const double dsc[3] = {sc[0] - TM.p[0], sc[1] - TM.p[1], sc[2] - TM.p[2]};
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    cl[i] = (TM.R[i] * dsc[0] + TM.R[3 + i] * dsc[1]) + TM.R[6 + i] * dsc[2];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) Rl[3 * i + j] = (TM.R[i] * TS.R[j] + TM.R[3 + i] * TS.R[3 + j]) + TM.R[6 + i] * TS.R[6 + j];
+  }
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+    hq[i] = ((std::fabs(Rl[3 * i]) * grs[G_OBB_E] + std::fabs(Rl[3 * i + 1]) * grs[G_OBB_E + 1]) +
+             std::fabs(Rl[3 * i + 2]) * grs[G_OBB_E + 2]) * (1.0 + 1e-9) + kMeshPad;
+  GObj A, B;  // A: the shape (o1), B: the triangle (mesh rotation / position)
+  A.rot = gjk_rot_from_matrix(TS.R);
+  A.rot_inv = quat_invert2(A.rot);
+  A.pos = v3(TS.p[0], TS.p[1], TS.p[2]);
+  A.geom = gs;
+  A.type = ts;
+  B.rot = gjk_rot_from_matrix(TM.R);
+  B.rot_inv = quat_invert2(B.rot);
+  B.pos = v3(TM.p[0], TM.p[1], TM.p[2]);
+  B.geom = gm;
+  B.type = MPG_GEOM_MESH;
+  for (int t = t0; t < t0 + tn; ++t) {
+    const cptr<double> rec = w.mesh_tri + TR_STRIDE * (size_t)t;
+    bool out = false;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) out |= rec[TR_LO + i] > cl[i] + hq[i] || rec[TR_HI + i] < cl[i] - hq[i];
+    if (out) continue;
+    double P[9];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) P[k] = rec[TR_P + k];
+    bool hit;
+    if (ts == MPG_GEOM_SPHERE) {
+      double W[9];
+#pragma unroll
+      for (int v = 0; v < 3; ++v)
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+          W[3 * v + i] = ((TM.R[3 * i] * P[3 * v] + TM.R[3 * i + 1] * P[3 * v + 1]) + TM.R[3 * i + 2] * P[3 * v + 2]) + TM.p[i];
+      hit = sphere_triangle_intersect(grs[G_PARAM], TS.p, W);
+    } else {
+      const V3 tc = v3((P[0] + P[3] + P[6]) / 3, (P[1] + P[4] + P[7]) / 3, (P[2] + P[5] + P[8]) / 3);
+      int st;
+      V3 v0, v1, v2, v3_, dir;
+      mpr_begin(center(w, A), vadd(quat_rot(tc, B.rot), B.pos), st, v0, dir);
+      int res = 0;
+      while (res == 0) {
+        const V3 sp = msupport_tri(w, HV, A, B, P, tc, dir);
+        res = mpr_advance(w.mpr_tol, sp, st, v0, v1, v2, v3_, dir);
+      }
+      hit = res > 0;
+    }
+    if (hit) return true;
+  }
+  return false;
+}
+
+// (mesh ga at TA, mesh gb at TB): B's triangles into A's frame, then A's
+// triangles under each transformed one
+__device__ __noinline__ bool mesh_mesh_hit(const DevWorld& w, int ga, const SE3& TA, int gb, const SE3& TB) {
+  const cptr<double> gra = w.geom_rec + G_STRIDE * ga, grb = w.geom_rec + G_STRIDE * gb;
+  const int a0 = (int)gra[G_PARAM], an = (int)gra[G_PARAM + 1];
+  const int b0 = (int)grb[G_PARAM], bn = (int)grb[G_PARAM + 1];
+  double R[9], T[3], alo[3], ahi[3];
+  const double dt[3] = {TB.p[0] - TA.p[0], TB.p[1] - TA.p[1], TB.p[2] - TA.p[2]};
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+#pragma unroll
+    for (int j = 0; j < 3; ++j) R[3 * i + j] = (TA.R[i] * TB.R[j] + TA.R[3 + i] * TB.R[3 + j]) + TA.R[6 + i] * TB.R[6 + j];
+    T[i] = (TA.R[i] * dt[0] + TA.R[3 + i] * dt[1]) + TA.R[6 + i] * dt[2];
+    alo[i] = gra[G_OBB_C + i] - gra[G_OBB_E + i] - kMeshPad;
+    ahi[i] = gra[G_OBB_C + i] + gra[G_OBB_E + i] + kMeshPad;
+  }
+  for (int j = b0; j < b0 + bn; ++j) {
+    const cptr<double> rq = w.mesh_tri + TR_STRIDE * (size_t)j;
+    double Q[9], qlo[3], qhi[3];
+#pragma unroll
+    for (int v = 0; v < 3; ++v)
+#pragma unroll
+      for (int i = 0; i < 3; ++i)
+        Q[3 * v + i] = ((R[3 * i] * rq[3 * v] + R[3 * i + 1] * rq[3 * v + 1]) + R[3 * i + 2] * rq[3 * v + 2]) + T[i];
+    bool out = false;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      qlo[i] = fmin(Q[i], fmin(Q[3 + i], Q[6 + i])) - kMeshPad;
+      qhi[i] = fmax(Q[i], fmax(Q[3 + i], Q[6 + i])) + kMeshPad;
+      out |= qlo[i] > ahi[i] || qhi[i] < alo[i];
+    }
+    if (out) continue;
+    for (int t = a0; t < a0 + an; ++t) {
+      const cptr<double> rp = w.mesh_tri + TR_STRIDE * (size_t)t;
+      bool o2 = false;
+#pragma unroll
+      for (int i = 0; i < 3; ++i) o2 |= rp[TR_LO + i] > qhi[i] || rp[TR_HI + i] < qlo[i];
+      if (o2) continue;
+      double P[9];
+#pragma unroll
+      for (int k = 0; k < 9; ++k) P[k] = rp[TR_P + k];
+      if (tri_tri_intersect(P, Q)) return true;
+    }
+  }
+  return false;
+}
+
+__device__ __forceinline__ bool mesh_hit(const DevWorld& w, cptr<double> HV, int ga, const SE3& TA, int gb,
+                                         const SE3& TB) {
+  const bool am = w.geom_type[ga] == MPG_GEOM_MESH, bm = w.geom_type[gb] == MPG_GEOM_MESH;
+  if (am && bm) return mesh_mesh_hit(w, ga, TA, gb, TB);
+  return am ? mesh_shape_hit(w, HV, ga, TA, gb, TB) : mesh_shape_hit(w, HV, gb, TB, ga, TA);
+}
+
 template <bool FROM_POSES>
 __global__ __launch_bounds__(256) MPG_NARROW_WAVES void narrow_kernel(DevWorld w, const double* __restrict__ in,
                                                     const uint32_t* __restrict__ seg_len,
@@ -1272,7 +1576,7 @@ __global__ __launch_bounds__(256) MPG_NARROW_WAVES void narrow_kernel(DevWorld w
 // ---------------------------------------------------------------------------
 constexpr double kSmallMargin = 1e-4;
 
-template <bool FROM_POSES, bool OCT>
+template <bool FROM_POSES, int CLS>
 __global__ __launch_bounds__(256) void small_kernel(DevWorld w, const double* __restrict__ in, long long n, int n_tiles,
                                                    uint8_t* __restrict__ hits) {
   const cptr<double> HV = w.hull;
@@ -1280,7 +1584,7 @@ __global__ __launch_bounds__(256) void small_kernel(DevWorld w, const double* __
   const int wave = __builtin_amdgcn_readfirstlane((int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6));
   const int p = wave / n_tiles;
   if (p >= w.n_pairs) return;
-  if ((w.pair_cf[p] == CF_OCTREE) != OCT) return;  // octree pairs: the OCT instance
+  if (cf_class(w.pair_cf[p]) != CLS) return;  // octree / mesh pairs: their own instances
   const long long cfg = (long long)(wave - p * n_tiles) * 64 + lane;
   const bool live = cfg < n;
   const long long c = live ? cfg : n - 1;
@@ -1304,7 +1608,7 @@ __global__ __launch_bounds__(256) void small_kernel(DevWorld w, const double* __
     const double rr = ra[G_RADIUS] + rb[G_RADIUS] + kSmallMargin;
     const bool near = live && d2 <= rr * rr;
     if (cf != CF_NONE) {
-      if (near && pair_closed_form<OCT>(cf, w, ga, TA, gb, TB)) hit = 1;
+      if (near && pair_closed_form<CLS>(cf, w, ga, TA, gb, TB)) hit = 1;
     } else if (__ballot(near) != 0) {
       GObj A, B;
       A.rot = gjk_rot_from_matrix(TA.R);
@@ -1998,6 +2302,8 @@ struct mpg_world {
   bool has_octree = false;       // a non-allowed pair involves an octree
   bool any_closed_form = false;  // some pair (allowed or not) does, octrees aside
   bool any_octree = false;       // some pair involves an octree
+  bool has_mesh = false;         // a non-allowed pair involves a BVH mesh
+  bool any_mesh = false;         // some pair involves a BVH mesh
   // batched distance buffers (grow-only)
   struct Dist {
     double* poses = nullptr;
@@ -2062,6 +2368,7 @@ int obj_geom_type(const mpg_world_desc* d, int id) {
 // FCL closed-form pair for (o1, o2) in fcl::collide argument order
 int closed_form_kind(const mpg_world_desc* d, int a, int b) {
   const int ta = obj_geom_type(d, a), tb = obj_geom_type(d, b);
+  if (ta == MPG_GEOM_MESH || tb == MPG_GEOM_MESH) return CF_MESH;
   if (ta == MPG_GEOM_OCTREE || tb == MPG_GEOM_OCTREE) return CF_OCTREE;
   if (ta == MPG_GEOM_BOX && tb == MPG_GEOM_BOX) return CF_BOX_BOX;
   if (ta == MPG_GEOM_SPHERE && tb == MPG_GEOM_SPHERE) return CF_SPHERE_SPHERE;
@@ -2091,11 +2398,21 @@ int validate(const mpg_world_desc* d) {
     if (d->link_parent[l] < 0 || d->link_parent[l] > d->n_joints) return set_error(MPG_E_INVALID, "bad link_parent");
   for (int g = 0; g < d->n_geoms; ++g) {
     const int t = d->geom_type[g];
-    if (t < MPG_GEOM_CONVEX || t > MPG_GEOM_OCTREE) return set_error(MPG_E_UNSUPPORTED, "unsupported geometry type");
-    if (t == MPG_GEOM_CONVEX) {
+    if (t < MPG_GEOM_CONVEX || t > MPG_GEOM_MESH) return set_error(MPG_E_UNSUPPORTED, "unsupported geometry type");
+    if (t == MPG_GEOM_CONVEX || t == MPG_GEOM_MESH) {
       if (d->geom_vertex_count[g] <= 0 || d->geom_vertex_start[g] < 0 ||
           (int64_t)d->geom_vertex_start[g] + d->geom_vertex_count[g] > d->n_vertices)
         return set_error(MPG_E_INVALID, "convex vertex range out of bounds");
+    }
+    if (t == MPG_GEOM_MESH) {
+      const double t0 = d->geom_param[4 * g], tn = d->geom_param[4 * g + 1];
+      if (!(t0 >= 0 && tn >= 0 && t0 == std::floor(t0) && tn == std::floor(tn) && t0 + tn <= (double)d->n_mesh_triangles))
+        return set_error(MPG_E_INVALID, "mesh triangle range out of bounds");
+      if (tn > 0 && !d->mesh_triangle) return set_error(MPG_E_INVALID, "bad mesh triangle array");
+      for (int64_t i = (int64_t)t0; i < (int64_t)(t0 + tn); ++i)
+        for (int k = 0; k < 3; ++k)
+          if (d->mesh_triangle[3 * i + k] < 0 || d->mesh_triangle[3 * i + k] >= d->geom_vertex_count[g])
+            return set_error(MPG_E_INVALID, "mesh triangle vertex index out of range");
     }
   }
   for (int m = 0; m < d->n_moving; ++m) {
@@ -2104,6 +2421,8 @@ int validate(const mpg_world_desc* d) {
     if (d->geom_type[d->moving_geom[m]] == MPG_GEOM_OCTREE)
       return set_error(MPG_E_UNSUPPORTED, "an OcTree on a robot link or attached body is not supported");
   }
+  if (d->n_mesh_triangles < 0 || (d->n_mesh_triangles > 0 && !d->mesh_triangle))
+    return set_error(MPG_E_INVALID, "bad mesh triangle array");
   if (d->n_octree_leaves < 0 || (d->n_octree_leaves > 0 && !d->octree_leaf))
     return set_error(MPG_E_INVALID, "bad octree leaf array");
   for (int g = 0; g < d->n_geoms; ++g) {
@@ -2121,6 +2440,9 @@ int validate(const mpg_world_desc* d) {
     const int a = d->pair_a[p], b = d->pair_b[p];
     if (a < 0 || a >= nobj || b < 0 || b >= nobj) return set_error(MPG_E_INVALID, "pair object id out of range");
     if (a >= d->n_moving && b >= d->n_moving) return set_error(MPG_E_INVALID, "static-static pair");
+    const int ta = obj_geom_type(d, a), tb = obj_geom_type(d, b);
+    if ((ta == MPG_GEOM_MESH && tb == MPG_GEOM_OCTREE) || (ta == MPG_GEOM_OCTREE && tb == MPG_GEOM_MESH))
+      return set_error(MPG_E_UNSUPPORTED, "BVH mesh vs OcTree pairs are not supported");
     // FCL 0.7.0 GJKSolver_libccd: box-box, sphere-sphere, sphere-box,
     // sphere-capsule and sphere-cylinder have closed forms (all on the
     // device, closed_form_kind); every other shape pair is MPR
@@ -2137,7 +2459,7 @@ void geom_record(const mpg_world_desc* d, int g, double* rec) {
   for (int k = 0; k < 4; ++k) rec[G_PARAM + k] = d->geom_param[4 * g + k];
   const int t = d->geom_type[g];
   double lo[3], hi[3];
-  if (t == MPG_GEOM_CONVEX) {
+  if (t == MPG_GEOM_CONVEX || t == MPG_GEOM_MESH) {
     const double* V = d->vertices + 3 * (size_t)d->geom_vertex_start[g];
     const int nv = d->geom_vertex_count[g];
     // FCL 0.7.0 Convex: interior point = (sum of vertices) * (1.0 / n)
@@ -2192,7 +2514,7 @@ void geom_record(const mpg_world_desc* d, int g, double* rec) {
     rec[G_OBB_E + k] = e * (1.0 + 1e-12) + 1e-12;
     r2 += rec[G_OBB_E + k] * rec[G_OBB_E + k];
   }
-  if (t == MPG_GEOM_CONVEX) {  // bounding sphere about the box centre: farthest vertex
+  if (t == MPG_GEOM_CONVEX || t == MPG_GEOM_MESH) {  // bounding sphere about the box centre: farthest vertex
     const double* V = d->vertices + 3 * (size_t)d->geom_vertex_start[g];
     r2 = 0.0;
     for (int i = 0; i < d->geom_vertex_count[g]; ++i) {
@@ -2373,13 +2695,18 @@ int launch_collide(mpg_world* w, const double* in, long long n, uint8_t* flags, 
                        ws->seg_start, ws->prefix, ws->cand, fl, mk, ws->prefix + w->dw.n_pairs + 1, ws->sc);
     HIP_TRY(hipGetLastError());
     if (w->any_closed_form) {
-      hipLaunchKernelGGL((closed_form_kernel<FROM_POSES, false>), dim3(w->narrow_blocks), dim3(256), 0, stream, w->dw,
-                         qin, ws->seg_len, ws->seg_start, ws->prefix, ws->cand, fl, mk, ws->sc);
+      hipLaunchKernelGGL((closed_form_kernel<FROM_POSES, CLS_CLOSED>), dim3(w->narrow_blocks), dim3(256), 0, stream,
+                         w->dw, qin, ws->seg_len, ws->seg_start, ws->prefix, ws->cand, fl, mk, ws->sc);
       HIP_TRY(hipGetLastError());
     }
     if (w->any_octree) {
-      hipLaunchKernelGGL((closed_form_kernel<FROM_POSES, true>), dim3(w->narrow_blocks), dim3(256), 0, stream, w->dw,
-                         qin, ws->seg_len, ws->seg_start, ws->prefix, ws->cand, fl, mk, ws->sc);
+      hipLaunchKernelGGL((closed_form_kernel<FROM_POSES, CLS_OCTREE>), dim3(w->narrow_blocks), dim3(256), 0, stream,
+                         w->dw, qin, ws->seg_len, ws->seg_start, ws->prefix, ws->cand, fl, mk, ws->sc);
+      HIP_TRY(hipGetLastError());
+    }
+    if (w->any_mesh) {
+      hipLaunchKernelGGL((closed_form_kernel<FROM_POSES, CLS_MESH>), dim3(w->narrow_blocks), dim3(256), 0, stream,
+                         w->dw, qin, ws->seg_len, ws->seg_start, ws->prefix, ws->cand, fl, mk, ws->sc);
       HIP_TRY(hipGetLastError());
     }
     if (co) {  // penetration info of the reported pairs (enable_contact)
@@ -2538,6 +2865,22 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
   // octrees: leaf boxes + a uniform grid per octree geometry (cells of at
   // least the largest leaf, <= 64 per axis); a leaf is listed in every cell
   // its box overlaps
+  // BVH meshes: per triangle its vertices (mesh frame) and AABB (TR_*)
+  std::vector<double> mesh_tri((size_t)TR_STRIDE * std::max<int64_t>(d->n_mesh_triangles, 1), 0.0);
+  for (int g = 0; g < d->n_geoms; ++g) {
+    if (d->geom_type[g] != MPG_GEOM_MESH) continue;
+    const double* V = d->vertices + 3 * (size_t)d->geom_vertex_start[g];
+    const int64_t t0 = (int64_t)d->geom_param[4 * g], tn = (int64_t)d->geom_param[4 * g + 1];
+    for (int64_t t = t0; t < t0 + tn; ++t) {
+      double* r = mesh_tri.data() + (size_t)TR_STRIDE * t;
+      for (int v = 0; v < 3; ++v)
+        for (int k = 0; k < 3; ++k) r[TR_P + 3 * v + k] = V[3 * (size_t)d->mesh_triangle[3 * t + v] + k];
+      for (int k = 0; k < 3; ++k) {
+        r[TR_LO + k] = std::min(r[TR_P + k], std::min(r[TR_P + 3 + k], r[TR_P + 6 + k]));
+        r[TR_HI + k] = std::max(r[TR_P + k], std::max(r[TR_P + 3 + k], r[TR_P + 6 + k]));
+      }
+    }
+  }
   std::vector<double> oct_leaf(6 * (size_t)std::max<int64_t>(d->n_octree_leaves, 1), 0.0);
   if (d->n_octree_leaves > 0) std::copy(d->octree_leaf, d->octree_leaf + 6 * d->n_octree_leaves, oct_leaf.begin());
   std::vector<double> oct_grid((size_t)OG_STRIDE * std::max(d->n_geoms, 1), 0.0);
@@ -2668,6 +3011,7 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
   const size_t o_bmb = bb.add(bpp.mobj.data(), bpp.mobj.size());
   const size_t o_bsb = bb.add(bpp.sobj.data(), bpp.sobj.size());
   const size_t o_olf = bb.add(oct_leaf.data(), oct_leaf.size());
+  const size_t o_mtr = bb.add(mesh_tri.data(), mesh_tri.size());
   const size_t o_ogr = bb.add(oct_grid.data(), oct_grid.size());
   const size_t o_oce = bb.add(oct_cells.data(), oct_cells.size());
   const size_t o_oli = bb.add(oct_list.data(), oct_list.size());
@@ -2735,8 +3079,10 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
   for (int p = 0; p < d->n_pairs; ++p) {
     w->has_closed_form |= pair_cf[p] != CF_NONE && !allowed[p];
     w->has_octree |= pair_cf[p] == CF_OCTREE && !allowed[p];
-    w->any_closed_form |= pair_cf[p] != CF_NONE && pair_cf[p] != CF_OCTREE;
+    w->any_closed_form |= pair_cf[p] != CF_NONE && cf_class(pair_cf[p]) == CLS_CLOSED;
     w->any_octree |= pair_cf[p] == CF_OCTREE;
+    w->has_mesh |= pair_cf[p] == CF_MESH && !allowed[p];
+    w->any_mesh |= pair_cf[p] == CF_MESH;
   }
   dw.static_T = to_cptr<double>(base + o_sT);
   dw.link_chain_start = to_cptr<int>(base + o_cs);
@@ -2770,6 +3116,7 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
   bp.mobj = F(o_bmb);
   bp.sobj = F(o_bsb);
   dw.oct_leaf = to_cptr<double>(base + o_olf);
+  dw.mesh_tri = to_cptr<double>(base + o_mtr);
   dw.oct_grid = to_cptr<double>(base + o_ogr);
   dw.oct_cells = I(o_oce);
   dw.oct_list = I(o_oli);
@@ -2896,12 +3243,17 @@ int collide_small(mpg_world* w, const double* q, int64_t n, uint8_t* flags, uint
   const long long waves = (long long)P * n_tiles;
   StageTimer t_small(w, s, MPG_STAGE_NARROW);
   if (w->prof) w->prof_cfg += n;
-  hipLaunchKernelGGL((small_kernel<FROM_POSES, false>), dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s, w->dw,
-                     w->d_qs, (long long)n, n_tiles, w->d_hits);
+  hipLaunchKernelGGL((small_kernel<FROM_POSES, CLS_CLOSED>), dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s,
+                     w->dw, w->d_qs, (long long)n, n_tiles, w->d_hits);
   HIP_TRY(hipGetLastError());
   if (w->any_octree) {
-    hipLaunchKernelGGL((small_kernel<FROM_POSES, true>), dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s, w->dw,
-                       w->d_qs, (long long)n, n_tiles, w->d_hits);
+    hipLaunchKernelGGL((small_kernel<FROM_POSES, CLS_OCTREE>), dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s,
+                       w->dw, w->d_qs, (long long)n, n_tiles, w->d_hits);
+    HIP_TRY(hipGetLastError());
+  }
+  if (w->any_mesh) {
+    hipLaunchKernelGGL((small_kernel<FROM_POSES, CLS_MESH>), dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s,
+                       w->dw, w->d_qs, (long long)n, n_tiles, w->d_hits);
     HIP_TRY(hipGetLastError());
   }
   t_small.stop();
@@ -3083,6 +3435,7 @@ int mpg_distance_batch(mpg_world* w, const double* q, int64_t n, int32_t n_self_
     return set_error(MPG_E_INVALID, "NULL buffer");
   if (mem != MPG_MEM_HOST && mem != MPG_MEM_DEVICE) return set_error(MPG_E_INVALID, "bad mem kind");
   if (w->has_octree) return set_error(MPG_E_UNSUPPORTED, "distance to an OcTree is not implemented on the device");
+  if (w->has_mesh) return set_error(MPG_E_UNSUPPORTED, "distance to a BVH mesh is not implemented on the device");
   if (n == 0) return MPG_OK;
   HIP_TRY(hipSetDevice(w->device));
   hipStream_t s = static_cast<hipStream_t>(stream);
@@ -3141,8 +3494,8 @@ int mpg_collide_contacts(mpg_world* w, const double* input, int64_t n, int input
   if (mem != MPG_MEM_HOST && mem != MPG_MEM_DEVICE) return set_error(MPG_E_INVALID, "bad mem kind");
   if (w->has_closed_form)
     return set_error(MPG_E_UNSUPPORTED,
-                     "contacts for FCL closed-form pairs (box-box, sphere-sphere, sphere-box) and octree pairs are not "
-                     "implemented");
+                     "contacts for FCL closed-form pairs (box-box, sphere-sphere, sphere-box), octree and BVH mesh "
+                     "pairs are not implemented");
   if (n == 0) return MPG_OK;
   HIP_TRY(hipSetDevice(w->device));
   hipStream_t s = static_cast<hipStream_t>(stream);

@@ -33,9 +33,11 @@ CFG_N = {2: 1 << 16, 3: 1 << 20, 4: 1 << 22, 6: 1 << 20}
 CFG_NAME = {2: "panda_self", 3: "panda_10boxes", 4: "panda_4convex", 6: "panda_floor_cloud"}
 
 
-def panda() -> "pymp.articulation.ArticulatedModel":
+def panda(convex: bool = True) -> "pymp.articulation.ArticulatedModel":
+    """convex=False loads the collision meshes as BVH triangle meshes
+    (load_mesh_as_BVH, fcl_model.cpp:224-227)."""
     a = pymp.articulation.ArticulatedModel(os.path.join(PANDA_DIR, "panda.urdf"), os.path.join(PANDA_DIR, "panda.srdf"),
-                                           [0, 0, -9.81], PANDA_JOINTS, PANDA_LINKS, verbose=False, convex=True)
+                                           [0, 0, -9.81], PANDA_JOINTS, PANDA_LINKS, verbose=False, convex=convex)
     a.set_move_group("panda_hand")
     return a
 
@@ -64,12 +66,13 @@ def _hulls():
     return out
 
 
-def world(cfg: int):
+def world(cfg: int, convex: bool = True):
     """(PlanningWorld, ArticulatedModel) for a BASELINE config (6: the
-    detect_collision.py floor point cloud, see cloud_world)."""
+    detect_collision.py floor point cloud, see cloud_world); convex=False:
+    the robot's links as BVH meshes."""
     if cfg == 6:
         return cloud_world("floor")
-    art = panda()
+    art = panda(convex)
     w = pymp.planning_world.PlanningWorld([art], ["panda"], [], [])
     if cfg == 3:
         for name, side, pos in _boxes():

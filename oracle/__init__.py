@@ -53,7 +53,25 @@ def lib():
         _lib.orc_distance_batch.restype = ctypes.c_int
         _lib.orc_contact_pair.restype = ctypes.c_int
         _lib.orc_contact_batch.restype = ctypes.c_int
+        _lib.orc_tri_tri.restype = ctypes.c_int
+        _lib.orc_sphere_tri.restype = ctypes.c_int
     return _lib
+
+
+def tri_tri(P, Q) -> bool:
+    """FCL Intersect::intersect_Triangle on two triangles ([3, 3] each)."""
+    a = np.ascontiguousarray(P, dtype=np.float64).reshape(9)
+    b = np.ascontiguousarray(Q, dtype=np.float64).reshape(9)
+    return bool(lib().orc_tri_tri(a.ctypes.data_as(_DP), b.ctypes.data_as(_DP)))
+
+
+def sphere_tri(radius: float, centre, P) -> bool:
+    """FCL sphereTriangleIntersect: a sphere at `centre` vs world triangle P."""
+    T = np.zeros(12)
+    T[[0, 4, 8]] = 1.0
+    T[9:] = centre
+    a = np.ascontiguousarray(P, dtype=np.float64).reshape(9)
+    return bool(lib().orc_sphere_tri(ctypes.c_double(radius), T.ctypes.data_as(_DP), a.ctypes.data_as(_DP)))
 
 
 _IP = ctypes.POINTER(ctypes.c_int)
@@ -77,6 +95,7 @@ class _World(ctypes.Structure):
         ("n_pairs", ctypes.c_int),
         ("pa_kind", _IP), ("pa_idx", _IP), ("pb_kind", _IP), ("pb_idx", _IP), ("p_allowed", _IP),
         ("oct_leaf", _DP),
+        ("mesh_tri", _IP),
     ]
 
 
@@ -134,6 +153,8 @@ class OracleWorld:
         scene_geom = [self._geom_index(s[1], geoms, None) for s in self.scene]
         gtype, gvstart, gnv, gparam, ginterior, verts = [], [], [], [], [], []
         leaves = []
+        tris = []
+        ntris = 0
         nverts = 0
         nleaves = 0
         for g in geoms:
@@ -145,6 +166,16 @@ class OracleWorld:
                 verts.append(np.asarray(g.vertices, dtype=np.float64).reshape(-1))
                 gparam += [0.0] * 4
                 ginterior += g.interior
+            elif isinstance(g, M.MeshGeom):
+                gtype.append(M.GEOM_MESH)
+                gvstart.append(nverts)
+                gnv.append(len(g.vertices))
+                nverts += len(g.vertices)
+                verts.append(np.asarray(g.vertices, dtype=np.float64).reshape(-1))
+                gparam += [float(ntris), float(len(g.faces)), 0.0, 0.0]
+                ginterior += [0.0] * 3
+                tris.append(np.asarray(g.faces, dtype=np.int32).reshape(-1))
+                ntris += len(g.faces)
             elif isinstance(g, M.BoxGeom):
                 gtype.append(M.GEOM_BOX)
                 gvstart.append(0)
@@ -191,6 +222,13 @@ class OracleWorld:
             for s, sc in enumerate(self.scene):
                 pairs.append((KIND_ATTACHED, k, KIND_SCENE, s, att[0], sc[0]))
         self.pairs = pairs
+        kinds = {KIND_ROBOT: [o.geom for o in art.objects], KIND_ATTACHED: [a[2] for a in self.attached],
+                 KIND_SCENE: [sc[1] for sc in self.scene]}
+        for p in pairs:
+            ga, gb = kinds[p[0]][p[1]], kinds[p[2]][p[3]]
+            if isinstance(ga, M.MeshGeom) or isinstance(gb, M.MeshGeom):
+                if isinstance(ga, M.OcTreeGeom) or isinstance(gb, M.OcTreeGeom):
+                    raise NotImplementedError("oracle: BVH mesh vs OcTree")
         self.W = max(1, (len(pairs) + 31) // 32)
         allowed = [1 if frozenset((p[4], p[5])) in self.allowed else 0 for p in pairs]
 
@@ -252,6 +290,7 @@ class OracleWorld:
         w.pb_idx = ia([p[3] for p in pairs])
         w.p_allowed = ia(allowed)
         w.oct_leaf = da(np.concatenate(leaves) if leaves else [])
+        w.mesh_tri = ia(np.concatenate(tris) if tris else [])
         self._w = w
         self.geoms = geoms
         self.dof = len(mg)

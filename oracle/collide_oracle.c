@@ -45,7 +45,8 @@ typedef double real;
 #define CCD_REAL_MAX DBL_MAX
 
 /* ---------------------------------------------------------------- world */
-enum { GEOM_CONVEX = 0, GEOM_BOX = 1, GEOM_SPHERE = 2, GEOM_CAPSULE = 3, GEOM_CYLINDER = 4, GEOM_OCTREE = 5 };
+enum { GEOM_CONVEX = 0, GEOM_BOX = 1, GEOM_SPHERE = 2, GEOM_CAPSULE = 3, GEOM_CYLINDER = 4, GEOM_OCTREE = 5, GEOM_MESH = 6,
+       GEOM_TRIANGLE = 100 /* one mesh triangle as a GJK object (internal) */ };
 enum { JT_RX, JT_RY, JT_RZ, JT_RU, JT_PX, JT_PY, JT_PZ, JT_PU, JT_RUBX, JT_RUBY, JT_RUBZ, JT_RUBU };
 enum { KIND_ROBOT = 0, KIND_ATTACHED = 1, KIND_SCENE = 2 };
 
@@ -89,6 +90,10 @@ typedef struct {
     /* octree geometries: geom_param = (first leaf, leaf count, resolution);
      * leaves [*6] = min xyz, max xyz in the octree frame */
     const double *oct_leaf;
+    /* BVH meshes (GEOM_MESH, fcl::BVHModel<OBBRSS>): geom_vstart/geom_nv give
+     * the vertices, geom_param = (first triangle, triangle count); triangles
+     * [*3] index the mesh's own vertices */
+    const int *mesh_tri;
 } orc_world;
 
 typedef struct {
@@ -345,6 +350,7 @@ typedef struct {
     const real *interior;
     real dim[3];       /* box half sizes */
     real radius, height; /* sphere / capsule / cylinder */
+    ccd_vec3_t tp[3], tc; /* triangle (triCreateGJKObject): vertices, centroid */
     orc_stats *stats;
 } gjk_obj;
 
@@ -431,8 +437,28 @@ static void support_cylinder(const gjk_obj *c, const ccd_vec3_t *dir_, ccd_vec3_
     ccdVec3Add(v, &c->pos);
 }
 
+/* supportTriangle (FCL gjk_libccd-inl.h): argmax of dir . (p_i - c), first
+ * maximum wins, then the vertex itself is transformed */
+static void support_triangle(const gjk_obj *t, const ccd_vec3_t *dir_, ccd_vec3_t *v) {
+    ccd_vec3_t dir, p;
+    real maxdot = -CCD_REAL_MAX, dot;
+    ccdVec3Copy(&dir, dir_);
+    ccdQuatRotVec(&dir, &t->rot_inv);
+    for (int i = 0; i < 3; ++i) {
+        ccdVec3Set(&p, t->tp[i].v[0] - t->tc.v[0], t->tp[i].v[1] - t->tc.v[1], t->tp[i].v[2] - t->tc.v[2]);
+        dot = ccdVec3Dot(&dir, &p);
+        if (dot > maxdot) {
+            ccdVec3Copy(v, &t->tp[i]);
+            maxdot = dot;
+        }
+    }
+    ccdQuatRotVec(v, &t->rot);
+    ccdVec3Add(v, &t->pos);
+}
+
 static void gjk_support(const gjk_obj *o, const ccd_vec3_t *dir, ccd_vec3_t *v) {
     switch (o->type) {
+    case GEOM_TRIANGLE: support_triangle(o, dir, v); break;
     case GEOM_CONVEX: support_convex(o, dir, v); break;
     case GEOM_BOX: support_box(o, dir, v); break;
     case GEOM_SPHERE: support_sphere(o, dir, v); break;
@@ -444,6 +470,10 @@ static void gjk_support(const gjk_obj *o, const ccd_vec3_t *dir, ccd_vec3_t *v) 
 static void gjk_center(const gjk_obj *o, ccd_vec3_t *c) {
     if (o->type == GEOM_CONVEX) { /* centerConvex */
         ccdVec3Set(c, o->interior[0], o->interior[1], o->interior[2]);
+        ccdQuatRotVec(c, &o->rot);
+        ccdVec3Add(c, &o->pos);
+    } else if (o->type == GEOM_TRIANGLE) { /* centerTriangle */
+        ccdVec3Copy(c, &o->tc);
         ccdQuatRotVec(c, &o->rot);
         ccdVec3Add(c, &o->pos);
     } else { /* centerShape */
@@ -1198,6 +1228,244 @@ static int octree_intersect(const orc_world *w, int go, const real *TO, int gs, 
     return 0;
 }
 
+/* ------------------------------------------------ BVH meshes
+ * fcl::BVHModel<OBBRSS> (load_mesh_as_BVH, src/urdf_utils.cpp:136-155) in
+ * fcl::collide [ext FCL 0.7.0]: the BVH traversal only prunes triangle pairs
+ * whose bounding volumes are disjoint, so with one requested contact the
+ * boolean result is "some leaf test succeeds".  Leaf tests:
+ *   mesh-mesh   MeshCollisionTraversalNodeOBBRSS::leafTesting ->
+ *               Intersect::intersect_Triangle(p1, p2, p3, q1, q2, q3, R, T)
+ *               with R = R1^T R2, T = R1^T (t2 - t1) (relativeTransform)
+ *   shape-mesh / mesh-shape  shapeTriangleIntersect(shape, tf_shape, P1, P2,
+ *               P3, tf_mesh): the shape is always o1; libccd MPR on the
+ *               triangle GJK object, sphereTriangleIntersect for spheres.
+ * The oracle enumerates every triangle (pair) behind a bounding-sphere test
+ * of its own (the device prunes with AABBs: the two never share a shortcut). */
+static real dot3(const real *a, const real *b) { return (a[0] * b[0] + a[1] * b[1]) + a[2] * b[2]; }
+static void cross3(real *o, const real *a, const real *b) {
+    o[0] = a[1] * b[2] - a[2] * b[1];
+    o[1] = a[2] * b[0] - a[0] * b[2];
+    o[2] = a[0] * b[1] - a[1] * b[0];
+}
+
+/* Intersect::project6 */
+static int project6(const real *ax, const real *p1, const real *p2, const real *p3, const real *q1, const real *q2,
+                    const real *q3) {
+    const real P1 = dot3(ax, p1), P2 = dot3(ax, p2), P3 = dot3(ax, p3);
+    const real Q1 = dot3(ax, q1), Q2 = dot3(ax, q2), Q3 = dot3(ax, q3);
+    const real mx1 = fmax(P1, fmax(P2, P3)), mn1 = fmin(P1, fmin(P2, P3));
+    const real mx2 = fmax(Q1, fmax(Q2, Q3)), mn2 = fmin(Q1, fmin(Q2, Q3));
+    if (mn1 > mx2) return 0;
+    if (mn2 > mx1) return 0;
+    return 1;
+}
+
+/* Intersect::intersect_Triangle (no contact output): 17 candidate axes in
+ * FCL's order -- n1, m1, the nine edge cross products, g1..g3, h1..h3 */
+static int tri_tri_intersect(const real *P1, const real *P2, const real *P3, const real *Q1, const real *Q2,
+                             const real *Q3) {
+    real p1[3] = {0.0, 0.0, 0.0}, p2[3], p3[3], q1[3], q2[3], q3[3];
+    for (int k = 0; k < 3; ++k) {
+        p2[k] = P2[k] - P1[k]; p3[k] = P3[k] - P1[k];
+        q1[k] = Q1[k] - P1[k]; q2[k] = Q2[k] - P1[k]; q3[k] = Q3[k] - P1[k];
+    }
+    real e[3][3], f[3][3];
+    for (int k = 0; k < 3; ++k) {
+        e[0][k] = p2[k] - p1[k]; e[1][k] = p3[k] - p2[k]; e[2][k] = p1[k] - p3[k];
+        f[0][k] = q2[k] - q1[k]; f[1][k] = q3[k] - q2[k]; f[2][k] = q1[k] - q3[k];
+    }
+    real n1[3], m1[3], ax[3];
+    cross3(n1, e[0], e[1]);
+    cross3(m1, f[0], f[1]);
+    if (!project6(n1, p1, p2, p3, q1, q2, q3)) return 0;
+    if (!project6(m1, p1, p2, p3, q1, q2, q3)) return 0;
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) {
+            cross3(ax, e[i], f[j]);
+            if (!project6(ax, p1, p2, p3, q1, q2, q3)) return 0;
+        }
+    for (int i = 0; i < 3; ++i) {
+        cross3(ax, e[i], n1);
+        if (!project6(ax, p1, p2, p3, q1, q2, q3)) return 0;
+    }
+    for (int i = 0; i < 3; ++i) {
+        cross3(ax, f[i], m1);
+        if (!project6(ax, p1, p2, p3, q1, q2, q3)) return 0;
+    }
+    return 1;
+}
+
+/* projectInTriangle (sphere_triangle-inl.h) */
+static int project_in_triangle(const real *p1, const real *p2, const real *p3, const real *n, const real *p) {
+    real e1[3], e2[3], e3[3], a[3], b[3], c[3], en1[3], en2[3], en3[3];
+    for (int k = 0; k < 3; ++k) {
+        e1[k] = p2[k] - p1[k]; e2[k] = p3[k] - p2[k]; e3[k] = p1[k] - p3[k];
+        a[k] = p[k] - p1[k]; b[k] = p[k] - p2[k]; c[k] = p[k] - p3[k];
+    }
+    cross3(en1, e1, n);
+    cross3(en2, e2, n);
+    cross3(en3, e3, n);
+    const real r1 = dot3(en1, a), r2 = dot3(en2, b), r3 = dot3(en3, c);
+    return (r1 > 0 && r2 > 0 && r3 > 0) || (r1 <= 0 && r2 <= 0 && r3 <= 0);
+}
+
+/* segmentSqrDistance (sphere_triangle-inl.h) */
+static real segment_sqr_distance(const real *from, const real *to, const real *p) {
+    real diff[3], v[3];
+    for (int k = 0; k < 3; ++k) { diff[k] = p[k] - from[k]; v[k] = to[k] - from[k]; }
+    real t = dot3(v, diff);
+    if (t > 0) {
+        const real vv = dot3(v, v);
+        if (t < vv) {
+            t /= vv;
+            for (int k = 0; k < 3; ++k) diff[k] -= v[k] * t;
+        } else {
+            for (int k = 0; k < 3; ++k) diff[k] -= v[k];
+        }
+    }
+    return dot3(diff, diff);
+}
+
+/* sphereTriangleIntersect (sphere_triangle-inl.h), boolean part; P1..P3 are
+ * world points (tf_mesh * P) */
+static int sphere_triangle_intersect(real radius, const real *TS, const real *P1, const real *P2, const real *P3) {
+    real a[3], b[3], n[3], pc[3];
+    for (int k = 0; k < 3; ++k) { a[k] = P2[k] - P1[k]; b[k] = P3[k] - P1[k]; }
+    cross3(n, a, b);
+    const real z = dot3(n, n);
+    if (z > 0) { const real s = sqrt(z); n[0] /= s; n[1] /= s; n[2] /= s; } /* Eigen normalize */
+    const real *center = TS + 9;
+    const real rt = radius + DBL_EPSILON;
+    for (int k = 0; k < 3; ++k) pc[k] = center[k] - P1[k];
+    real dist = dot3(pc, n);
+    if (dist < 0) {
+        dist *= -1;
+        n[0] *= -1; n[1] *= -1; n[2] *= -1;
+    }
+    if (!(dist < rt)) return 0;
+    if (project_in_triangle(P1, P2, P3, n, center)) return 1;
+    const real r2 = rt * rt;
+    if (segment_sqr_distance(P1, P2, center) < r2) return 1;
+    if (segment_sqr_distance(P2, P3, center) < r2) return 1;
+    if (segment_sqr_distance(P3, P1, center) < r2) return 1;
+    return 0;
+}
+
+/* Transform3 * point: (R p) + t */
+static void tf_point(const real *T, const real *p, real *o) {
+    for (int i = 0; i < 3; ++i) o[i] = ((T[3 * i] * p[0] + T[3 * i + 1] * p[1]) + T[3 * i + 2] * p[2]) + T[9 + i];
+}
+
+static void mesh_tri_points(const orc_world *w, int gm, int t, const real **P) {
+    const real *V = w->verts + 3 * (size_t)w->geom_vstart[gm];
+    const int *tri = w->mesh_tri + 3 * (size_t)t;
+    for (int k = 0; k < 3; ++k) P[k] = V + 3 * tri[k];
+}
+
+/* bounding sphere of a point set (centroid, farthest point), padded */
+static void bsphere(const real *const *P, int n, real *c, real *r) {
+    c[0] = c[1] = c[2] = 0.0;
+    for (int i = 0; i < n; ++i)
+        for (int k = 0; k < 3; ++k) c[k] += P[i][k] / n;
+    real m = 0.0;
+    for (int i = 0; i < n; ++i) {
+        const real d[3] = {P[i][0] - c[0], P[i][1] - c[1], P[i][2] - c[2]};
+        m = fmax(m, dot3(d, d));
+    }
+    *r = sqrt(m) * (1.0 + 1e-9) + 1e-9;
+}
+
+static int mesh_shape_intersect(const orc_world *w, int gm, const real *TM, int gs, const real *TS, orc_stats *st) {
+    const int t0 = (int)w->geom_param[4 * gm], tn = (int)w->geom_param[4 * gm + 1];
+    const int ts = w->geom_type[gs];
+    if (ts == GEOM_OCTREE || ts == GEOM_MESH) return 0; /* refused by the builder (oracle/__init__.py) */
+    /* shape bounding sphere in the world: about its origin (convex: about
+     * the farthest vertex from the origin) */
+    real rs = 0.0;
+    const real *ps = w->geom_param + 4 * gs;
+    if (ts == GEOM_CONVEX) {
+        const real *V = w->verts + 3 * (size_t)w->geom_vstart[gs];
+        for (int i = 0; i < w->geom_nv[gs]; ++i) rs = fmax(rs, dot3(V + 3 * i, V + 3 * i));
+        rs = sqrt(rs);
+    } else if (ts == GEOM_BOX) rs = 0.5 * sqrt(dot3(ps, ps));
+    else if (ts == GEOM_SPHERE) rs = ps[0];
+    else rs = sqrt(ps[0] * ps[0] + 0.25 * ps[1] * ps[1]) + (ts == GEOM_CAPSULE ? ps[0] : 0.0);
+    rs = rs * (1.0 + 1e-9) + 1e-9;
+    gjk_obj shape, tri;
+    int shape_ready = 0;
+    for (int t = t0; t < t0 + tn; ++t) {
+        const real *P[3];
+        mesh_tri_points(w, gm, t, P);
+        real W[3][3];
+        for (int k = 0; k < 3; ++k) tf_point(TM, P[k], W[k]);
+        const real *Wp[3] = {W[0], W[1], W[2]};
+        real c[3], r;
+        bsphere(Wp, 3, c, &r);
+        const real d[3] = {c[0] - TS[9], c[1] - TS[10], c[2] - TS[11]};
+        if (sqrt(dot3(d, d)) > r + rs) continue;
+        int hit;
+        if (ts == GEOM_SPHERE) hit = sphere_triangle_intersect(ps[0], TS, W[0], W[1], W[2]);
+        else {
+            if (!shape_ready) { make_obj(w, gs, TS, &shape, st); shape_ready = 1; }
+            memset(&tri, 0, sizeof tri);
+            shape_to_gjk(TM, &tri);
+            tri.type = GEOM_TRIANGLE;
+            tri.stats = st;
+            for (int k = 0; k < 3; ++k) ccdVec3Set(&tri.tp[k], P[k][0], P[k][1], P[k][2]);
+            ccdVec3Set(&tri.tc, (P[0][0] + P[1][0] + P[2][0]) / 3, (P[0][1] + P[1][1] + P[2][1]) / 3,
+                       (P[0][2] + P[1][2] + P[2][2]) / 3);
+            hit = mpr_intersect(&shape, &tri, 1e-6);
+        }
+        if (hit) return 1;
+    }
+    return 0;
+}
+
+static int mesh_mesh_intersect(const orc_world *w, int ga, const real *TA, int gb, const real *TB) {
+    const int a0 = (int)w->geom_param[4 * ga], an = (int)w->geom_param[4 * ga + 1];
+    const int b0 = (int)w->geom_param[4 * gb], bn = (int)w->geom_param[4 * gb + 1];
+    real R[9], T[3], dt[3];
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) R[3 * i + j] = (TA[i] * TB[j] + TA[3 + i] * TB[3 + j]) + TA[6 + i] * TB[6 + j];
+    for (int k = 0; k < 3; ++k) dt[k] = TB[9 + k] - TA[9 + k];
+    for (int i = 0; i < 3; ++i) T[i] = (TA[i] * dt[0] + TA[3 + i] * dt[1]) + TA[6 + i] * dt[2];
+    real (*QB)[9] = malloc(sizeof(real) * 9 * (size_t)(bn > 0 ? bn : 1));
+    real (*SB)[4] = malloc(sizeof(real) * 4 * (size_t)(bn > 0 ? bn : 1));
+    for (int j = 0; j < bn; ++j) {
+        const real *Q[3];
+        mesh_tri_points(w, gb, b0 + j, Q);
+        for (int k = 0; k < 3; ++k)
+            for (int i = 0; i < 3; ++i)
+                QB[j][3 * k + i] = ((R[3 * i] * Q[k][0] + R[3 * i + 1] * Q[k][1]) + R[3 * i + 2] * Q[k][2]) + T[i];
+        const real *Qp[3] = {QB[j], QB[j] + 3, QB[j] + 6};
+        bsphere(Qp, 3, SB[j], &SB[j][3]);
+    }
+    int hit = 0;
+    for (int i = 0; i < an && !hit; ++i) {
+        const real *P[3];
+        mesh_tri_points(w, ga, a0 + i, P);
+        real c[3], r;
+        bsphere(P, 3, c, &r);
+        for (int j = 0; j < bn; ++j) {
+            const real d[3] = {c[0] - SB[j][0], c[1] - SB[j][1], c[2] - SB[j][2]};
+            if (sqrt(dot3(d, d)) > r + SB[j][3]) continue;
+            if (tri_tri_intersect(P[0], P[1], P[2], QB[j], QB[j] + 3, QB[j] + 6)) { hit = 1; break; }
+        }
+    }
+    free(QB);
+    free(SB);
+    return hit;
+}
+
+/* 1/0 for a mesh pair, -1 when neither side is a mesh */
+static int mesh_intersect(const orc_world *w, int ga, const real *Ta, int gb, const real *Tb, orc_stats *st) {
+    const int ta = w->geom_type[ga], tb = w->geom_type[gb];
+    if (ta != GEOM_MESH && tb != GEOM_MESH) return -1;
+    if (ta == GEOM_MESH && tb == GEOM_MESH) return mesh_mesh_intersect(w, ga, Ta, gb, Tb);
+    if (ta == GEOM_MESH) return mesh_shape_intersect(w, ga, Ta, gb, Tb, st);
+    return mesh_shape_intersect(w, gb, Tb, ga, Ta, st);
+}
+
 #define MAX_OBJ 512
 
 /* Per-configuration worker: FK + every pair + ACM filter (allowed pairs are
@@ -1224,8 +1492,9 @@ static int collide_one(const orc_world *w, const real *q, uint32_t *mask, int W,
             else if (ks[s] == KIND_ATTACHED) { Ts[s] = att_T + 12 * is[s]; gs[s] = w->att_geom[is[s]]; }
             else { Ts[s] = w->scene_tf + 12 * is[s]; gs[s] = w->scene_geom[is[s]]; }
         }
-        int hit;
-        if (w->geom_type[gs[1]] == GEOM_OCTREE) hit = octree_intersect(w, gs[1], Ts[1], gs[0], Ts[0], st);
+        int hit = mesh_intersect(w, gs[0], Ts[0], gs[1], Ts[1], st);
+        if (hit >= 0) {}
+        else if (w->geom_type[gs[1]] == GEOM_OCTREE) hit = octree_intersect(w, gs[1], Ts[1], gs[0], Ts[0], st);
         else if (w->geom_type[gs[0]] == GEOM_OCTREE) hit = octree_intersect(w, gs[0], Ts[0], gs[1], Ts[1], st);
         else hit = closed_form_intersect(w, gs[0], Ts[0], gs[1], Ts[1]);
         if (hit < 0) {
@@ -1407,6 +1676,8 @@ double orc_distance_pair(const orc_world *w, int ga, const double *Ta, int gb, c
 }
 
 int orc_collide_pair(const orc_world *w, int ga, const double *Ta, int gb, const double *Tb) {
+    const int mh = mesh_intersect(w, ga, Ta, gb, Tb, NULL);
+    if (mh >= 0) return mh;
     const int cf = closed_form_intersect(w, ga, Ta, gb, Tb);
     if (cf >= 0) return cf;
     gjk_obj a, b;
@@ -1414,3 +1685,8 @@ int orc_collide_pair(const orc_world *w, int ga, const double *Ta, int gb, const
     make_obj(w, gb, Tb, &b, NULL);
     return mpr_intersect(&a, &b, 1e-6);
 }
+
+/* Intersect::intersect_Triangle / sphereTriangleIntersect on raw points
+ * (known-answer tests) */
+int orc_tri_tri(const double *P, const double *Q) { return tri_tri_intersect(P, P + 3, P + 6, Q, Q + 3, Q + 6); }
+int orc_sphere_tri(double r, const double *TS, const double *P) { return sphere_triangle_intersect(r, TS, P, P + 3, P + 6); }

@@ -554,6 +554,24 @@ class OcTreeGeom:
         return np.array(out, dtype=np.float64).reshape(-1, 6)
 
 
+GEOM_MESH = 6
+
+
+@dataclass
+class MeshGeom:
+    """fcl::BVHModel<OBBRSS> of a triangle mesh (load_mesh_as_BVH,
+    src/urdf_utils.cpp:136-155): the vertices and triangles as loaded."""
+    vertices: np.ndarray  # [n, 3] float64
+    faces: List[Tuple[int, int, int]]
+
+
+def load_bvh_mesh(path: str, scale=(1.0, 1.0, 1.0)) -> MeshGeom:
+    """load_mesh_as_BVH: dfs_build_mesh's vertices (S)p * scale and triangles."""
+    verts, tris = load_stl(path)
+    arr = np.array([[v[0] * scale[0], v[1] * scale[1], v[2] * scale[2]] for v in verts], dtype=np.float64)
+    return MeshGeom(arr.reshape(-1, 3), list(tris))
+
+
 def load_convex_mesh(path: str, scale=(1.0, 1.0, 1.0)) -> ConvexGeom:
     verts, tris = load_stl(path)
     arr = np.array([[v[0] * scale[0], v[1] * scale[1], v[2] * scale[2]] for v in verts], dtype=np.float64)
@@ -746,9 +764,8 @@ class Articulation:
                 fn = geom.filename
                 if convex and ".convex.stl" not in fn:
                     fn = fn + ".convex.stl"
-                if not convex:
-                    raise ValueError("oracle supports convex=True only")
-                g = load_convex_mesh(os.path.join(self.urdf.directory, fn), geom.scale)
+                path = os.path.join(self.urdf.directory, fn)
+                g = load_convex_mesh(path, geom.scale) if convex else load_bvh_mesh(path, geom.scale)
             elif geom.kind == "box":
                 g = BoxGeom(geom.size)
             else:

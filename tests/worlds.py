@@ -41,10 +41,10 @@ KAT_FREE = [0.0, 0.19, 0.0, -2.61, 0.0, 2.94, 0.78]
 KAT_COLLIDING = [0.0, 1.36, 0.0, -3.0, -3.0, 3.0, -1.0]
 
 
-def panda_articulation() -> M.Articulation:
+def panda_articulation(convex: bool = True) -> M.Articulation:
     d = panda_dir()
     return M.Articulation(os.path.join(d, "panda.urdf"), os.path.join(d, "panda.srdf"), PANDA_LINKS,
-                          PANDA_JOINTS, convex=True, move_group="panda_hand")
+                          PANDA_JOINTS, convex=convex, move_group="panda_hand")
 
 
 def _box(side, pos):
@@ -86,8 +86,8 @@ def convex_scene(art: M.Articulation) -> List[Tuple[str, object, tuple]]:
     return scene
 
 
-def oracle_world(cfg: int) -> oracle.OracleWorld:
-    art = panda_articulation()
+def oracle_world(cfg: int, convex: bool = True) -> oracle.OracleWorld:
+    art = panda_articulation(convex)
     if cfg in (1, 2):
         return oracle.OracleWorld(art)
     if cfg == 3:
@@ -139,11 +139,21 @@ def desc_arrays(ow: oracle.OracleWorld) -> dict:
         qsrc.append(src)
         qconst.append(const)
     geoms = ow.geoms
-    gtype, gvs, gnv, gparam, verts, leaves = [], [], [], [], [], []
+    gtype, gvs, gnv, gparam, verts, leaves, tris = [], [], [], [], [], [], []
     nv = 0
     nl = 0
+    nt = 0
     for g in geoms:
-        if isinstance(g, M.OcTreeGeom):
+        if isinstance(g, M.MeshGeom):
+            gtype.append(6)
+            gvs.append(nv)
+            gnv.append(len(g.vertices))
+            nv += len(g.vertices)
+            verts.append(g.vertices.reshape(-1))
+            gparam += [float(nt), float(len(g.faces)), 0.0, 0.0]
+            tris.append(np.asarray(g.faces, np.int32).reshape(-1))
+            nt += len(g.faces)
+        elif isinstance(g, M.OcTreeGeom):
             gtype.append(5)
             gvs.append(0)
             gnv.append(0)
@@ -206,4 +216,15 @@ def desc_arrays(ow: oracle.OracleWorld) -> dict:
         pair_a=[oid(p[0], p[1]) for p in ow.pairs], pair_b=[oid(p[2], p[3]) for p in ow.pairs],
         pair_allowed=[1 if frozenset((p[4], p[5])) in ow.allowed else 0 for p in ow.pairs],
         octree_leaf=np.concatenate(leaves) if leaves else np.zeros(0),
+        mesh_triangle=np.concatenate(tris) if tris else np.zeros(0, np.int32),
     )
+
+
+def collide_pair(ow: oracle.OracleWorld, ga: int, Ta, gb: int, Tb) -> bool:
+    """The oracle's fcl::collide on two posed geometries of ow (SE3 tuples)."""
+    import ctypes
+    DP = ctypes.POINTER(ctypes.c_double)
+    a = np.ascontiguousarray(oracle._se3_flat(Ta), dtype=np.float64)
+    b = np.ascontiguousarray(oracle._se3_flat(Tb), dtype=np.float64)
+    return bool(oracle.lib().orc_collide_pair(ctypes.byref(ow._w), ga, a.ctypes.data_as(DP), gb,
+                                              b.ctypes.data_as(DP)))
