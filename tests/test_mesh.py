@@ -202,8 +202,10 @@ def test_mesh_worlds_match_oracle(convex):
     p_orb = [0.0, 0.0, 0.12, 1.0, 0.0, 0.0, 0.0]
     p_blk = [0.0, 0.06, 0.0, 1.0, 0.0, 0.0, 0.0]
     p_fing = [0.0, 0.0, 0.2, 0.7071067811865476, 0.7071067811865476, 0.0, 0.0]
-    w.attach_object("orb", pymp.fcl.Sphere(0.05), "panda", 8, p_orb, ["panda_hand"])
-    w.attach_object("blk", pymp.fcl.Box([0.04, 0.04, 0.1]), "panda", 6, p_blk, ["panda_link6", "panda_link7"])
+    w.attach_object("orb", pymp.fcl.Sphere(0.05), "panda", 8, p_orb,
+                    ["panda_hand", "panda_leftfinger", "panda_rightfinger"])
+    w.attach_object("blk", pymp.fcl.Box([0.04, 0.04, 0.1]), "panda", 6, p_blk,
+                    ["panda_link5", "panda_link6", "panda_link7"])
     w.attach_object("tool", pymp.fcl.load_mesh_as_BVH(os.path.join(d, "finger.stl"), [2, 2, 2]), "panda", 8, p_fing,
                     ["panda_hand", "orb"])
     o2 = oracle.OracleWorld(base.art, scene=list(base.scene) + extra,
@@ -211,7 +213,8 @@ def test_mesh_worlds_match_oracle(convex):
                                       ("blk", 6, M.BoxGeom((0.04, 0.04, 0.1)), _oracle_T(p_blk)),
                                       ("tool", 8, M.load_bvh_mesh(os.path.join(d, "finger.stl"), (2, 2, 2)),
                                        _oracle_T(p_fing))],
-                            allowed=[("panda_hand", "orb"), ("panda_link6", "blk"), ("panda_link7", "blk"),
+                            allowed=[("panda_hand", "orb"), ("panda_leftfinger", "orb"), ("panda_rightfinger", "orb"),
+                                     ("panda_link5", "blk"), ("panda_link6", "blk"), ("panda_link7", "blk"),
                                      ("panda_hand", "tool"), ("orb", "tool"), ("panda_link0", "table")])
     order = {pn: k for k, pn in enumerate(o2.pair_names())}
     names = [(i[3], i[4]) for i in w.get_collision_pair_info()]
@@ -238,9 +241,9 @@ def test_mesh_worlds_match_oracle(convex):
 def test_mesh_world_unsupported_queries():
     w, _ = scenes.world(2, convex=False)
     w.set_qpos_all(Wd.KAT_COLLIDING)
-    assert len(w.collide()) > 0
+    assert w.collide() and len(w.collide_full()) > 0
     w.set_qpos_all(Wd.KAT_FREE)
-    assert w.collide() == []
+    assert not w.collide() and w.collide_full() == []
     with pytest.raises(NotImplementedError, match="BVH mesh"):
         w.self_distance()
     with pytest.raises(NotImplementedError):
