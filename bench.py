@@ -12,7 +12,8 @@ writing flags[N] (u8) and pair_mask[N, 5] (u32).
 
 Other workloads (not the headline): --cfg 2 / 4 (self-only / convex
 obstacles), --cfg 6 (the detect_collision.py floor point cloud as an
-fcl::OcTree), --cfg 5 (RRTConnect plan() end to end: a step is one plan()).
+fcl::OcTree), --cfg 7 (cfg3 with the Panda links as BVH triangle meshes,
+convex=False), --cfg 5 (RRTConnect plan() end to end: a step is one plan()).
 
 Usage:  python bench.py [--gpus N] [--steps K] [--warmup W] [--cpu-sample S] [--cfg C]
         torchrun --nproc-per-node N bench.py --gpus N ...
@@ -33,7 +34,8 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 STAGES = ("cull", "bucket", "narrow")  # MPG_STAGE_* (include/mpgpu.h)
-KERNEL_NAME = {"cull": "cull_kernel", "bucket": "pair_scan/chunk_scan/scatter", "narrow": "narrow_kernel"}
+KERNEL_NAME = {"cull": "cull_kernel", "bucket": "pair_scan/chunk_scan/scatter",
+               "narrow": "narrow stage (narrow_kernel + closed_form_kernel instances)"}
 FP64_VALU_PEAK_TFLOPS = 78.6  # MI355X spec (vector FP64; FMA counted as 2)
 
 
@@ -43,7 +45,8 @@ def parse():
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--cfg", type=int, default=3,
-                   help="2, 3, 4: BASELINE collide configs; 5: RRTConnect plan(); 6: floor point cloud")
+                   help="2, 3, 4: BASELINE collide configs; 5: RRTConnect plan(); 6: floor point cloud; "
+                        "7: cfg3 with BVH mesh links (convex=False)")
     p.add_argument("--goal", default="far", help="cfg5 goal (scenes.PLAN_GOALS)")
     p.add_argument("--cpu-plans", type=int, default=4, help="cfg5: plans timed with the CPU oracle checker")
     p.add_argument("--per-gpu", type=int, default=0, help="configs per GPU per step (default: BASELINE size)")
@@ -192,7 +195,8 @@ def main():
         result["gather_ms"] = gather_ms
 
     if rank == 0 and world == 1 and args.cpu_sample > 0:
-        result["cpu_baseline"] = cpu_baseline(cfg, q_host[: args.cpu_sample], flags, masks, args.cpu_threads)
+        k = args.cpu_sample if cfg != 7 else min(args.cpu_sample, 1 << 13)  # the mesh oracle is ~100x slower
+        result["cpu_baseline"] = cpu_baseline(cfg, q_host[:k], flags, masks, args.cpu_threads)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

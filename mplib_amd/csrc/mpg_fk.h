@@ -23,7 +23,7 @@ enum { S_ROT = 0, S_ROTINV = 4, S_POS = 8, S_OBBC = 11, S_R = 14, S_STRIDE = 23 
 struct DevWorld {
   int nj, dof, n_links, n_geoms, n_moving, n_static, n_pairs, W;
   double mpr_tol;
-  int debug_mode;  // diagnostics only: 1 = broad-phase records only, 2 = no SAT stage, 3 = no MPR
+  int debug_mode;  // diagnostics only: 1 = broad-phase records only, 2 = no SAT stage, 3 = no MPR, 5 / 6 = no mesh-mesh / mesh-shape walks
   unsigned long long* stats;  // diagnostics only (MPG_STATS=1), else NULL
   cptr<int> joint_type;      // [nj]
   cptr<int> joint_parent;    // [nj]
@@ -70,8 +70,14 @@ struct DevWorld {
   cptr<double> oct_grid;   // [n_geoms * OG_STRIDE]
   cptr<int> oct_cells;     // cell start offsets into oct_list
   cptr<int> oct_list;      // leaf indices
-  // BVH meshes: one record per triangle (TR_*), mesh frame
+  // BVH meshes: one record per triangle (TR_*, mesh frame) grouped into
+  // spatial clusters (the leaves of a median-split tree): cluster box [6],
+  // cluster (first triangle record, triangle count), per geometry (first
+  // cluster, cluster count)
   cptr<double> mesh_tri;
+  cptr<double> mesh_node;
+  cptr<int> mesh_link;  // [clusters * 2]
+  cptr<int> mesh_tree;  // [n_geoms * 2]
 };
 enum { OG_ORIGIN = 0, OG_INV = 3, OG_DIMS = 4, OG_CELL0 = 7, OG_STRIDE = 8 };
 // triangle record: vertices P1 P2 P3, then the triangle's AABB

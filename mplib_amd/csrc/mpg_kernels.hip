@@ -842,8 +842,8 @@ enum : int { MPR_DONE = 0, MPR_V1 = 1, MPR_V2 = 2, MPR_V3 = 3, MPR_V4 = 4 };
 __device__ __forceinline__ bool octree_hit(const DevWorld& w, cptr<double> HV, int go, const SE3& TO, int gs,
                                            const SE3& TS);
 
-__device__ __forceinline__ bool mesh_hit(const DevWorld& w, cptr<double> HV, int ga, const SE3& TA, int gb,
-                                         const SE3& TB);
+__device__ __forceinline__ unsigned long long mesh_wave_eval(const DevWorld& w, cptr<double> HV, int ga, const SE3& TA,
+                                                            int gb, const SE3& TB, bool active);
 
 // one pair evaluation of class CLS: closed form, octree walk or BVH mesh
 // walk; each class lives in its own kernel instance so the walks' registers
@@ -852,7 +852,7 @@ template <int CLS>
 __device__ __forceinline__ bool pair_closed_form(int cf, const DevWorld& w, int ga, const SE3& TA, int gb,
                                                  const SE3& TB) {
   if (CLS == CLS_CLOSED) return closed_form(cf, w, ga, TA, gb, TB);
-  if (CLS == CLS_MESH) return mesh_hit(w, w.hull, ga, TA, gb, TB);
+  if (CLS == CLS_MESH) return false;  // evaluated wave-wide (mesh_wave_eval)
   return w.geom_type[ga] == MPG_GEOM_OCTREE ? octree_hit(w, w.hull, ga, TA, gb, TB)
                                             : octree_hit(w, w.hull, gb, TB, ga, TA);
 }
@@ -890,6 +890,21 @@ __global__ __launch_bounds__(256) void closed_form_kernel(DevWorld w, const doub
     const uint32_t* __restrict__ cl = cand + seg_start[p];
     for (uint32_t base = t0; base < t1; base += 64) {
       const uint32_t idx = base + lane;
+      if (CLS == CLS_MESH) {  // the wave walks each candidate's triangles together
+        const bool active = idx < t1;
+        const long long c = active ? cl[idx] : 0;
+        SE3 TA = {}, TB = {};
+        if (active) {
+          TA = am ? moving_tf<FROM_POSES>(w, in, sc, c, a) : load_se3(w.static_T + 12 * (a - w.n_moving));
+          TB = bm ? moving_tf<FROM_POSES>(w, in, sc, c, b) : load_se3(w.static_T + 12 * (b - w.n_moving));
+        }
+        const unsigned long long hits = mesh_wave_eval(w, w.hull, ga, TA, gb, TB, active);
+        if ((hits >> lane) & 1ull) {
+          if (masks) atomicOr(&masks[c * w.W + (p >> 5)], 1u << (p & 31));
+          flags[c] = 1;
+        }
+        continue;
+      }
       if (idx >= t1) continue;
       const long long c = cl[idx];
       const SE3 TA = am ? moving_tf<FROM_POSES>(w, in, sc, c, a) : load_se3(w.static_T + 12 * (a - w.n_moving));
@@ -1146,9 +1161,9 @@ __device__ __forceinline__ bool octree_hit(const DevWorld& w, cptr<double> HV, i
 // BVH meshes (fcl::BVHModel<OBBRSS>, load_mesh_as_BVH src/urdf_utils.cpp:
 // 136-155).  fcl::collide's BVH traversal only prunes triangle (pairs) whose
 // bounding volumes are disjoint, so the boolean answer is "some leaf test
-// succeeds"; a lane walks the triangles behind a conservative AABB test in
-// the mesh frame (widened by 1e-9, far above rounding: a pruned triangle is
-// genuinely separated).  Leaf tests as FCL 0.7.0 runs them:
+// succeeds"; the wave walks one candidate's triangles at a time (64 lanes
+// side by side) behind a conservative AABB test in the mesh frame (widened
+// by 1e-9, far above rounding: a pruned triangle is genuinely separated).  Leaf tests as FCL 0.7.0 runs them:
 //   mesh-mesh   Intersect::intersect_Triangle(p, q, R, T), R = R1^T R2,
 //               T = R1^T (t2 - t1), q' = R q + T
 //   shape-mesh  shapeTriangleIntersect(shape, tf, P1, P2, P3, tf_mesh): shape
@@ -1177,7 +1192,7 @@ __device__ __forceinline__ bool project6(const double* ax, const double* p2, con
 
 // Intersect::intersect_Triangle without contact output: n1, m1, the nine
 // edge cross products, g1..g3, h1..h3
-__device__ __noinline__ bool tri_tri_intersect(const double* P, const double* Q) {
+__device__ __forceinline__ bool tri_tri_intersect(const double* P, const double* Q) {
   double p2[3], p3[3], q1[3], q2[3], q3[3], e[3][3], f[3][3], n1[3], m1[3], ax[3];
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
@@ -1241,7 +1256,7 @@ __device__ __forceinline__ double segment_sqr_distance(const double* from, const
 
 // sphereTriangleIntersect (sphere_triangle-inl.h), boolean part; W = world
 // triangle (tf_mesh * P), c = sphere centre
-__device__ __noinline__ bool sphere_triangle_intersect(double radius, const double* c, const double* W) {
+__device__ __forceinline__ bool sphere_triangle_intersect(double radius, const double* c, const double* W) {
   double a[3], b[3], n[3], pc[3];
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
@@ -1314,13 +1329,115 @@ __device__ __forceinline__ V3 msupport_tri(const DevWorld& w, cptr<double> HV, c
   return vsub(vadd(quat_rot(la, a.rot), a.pos), vadd(quat_rot(lb, b.rot), b.pos));
 }
 
-// (shape gs at TS, mesh gm at TM): shape first in every leaf test
-__device__ __noinline__ bool mesh_shape_hit(const DevWorld& w, cptr<double> HV, int gm, const SE3& TM, int gs,
-                                            const SE3& TS) {
+// One (config, pair) at a time per wave, the 64 lanes split the triangle
+// loops.  Inputs are wave-uniform (broadcast from the lane that owns the
+// candidate).
+__device__ __forceinline__ double bcast(double v, int k) {
+  const unsigned long long u = __double_as_longlong(v);
+  const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)u, k), hi = __builtin_amdgcn_readlane((uint32_t)(u >> 32), k);
+  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+__device__ __forceinline__ SE3 bcast_se3(const SE3& T, int k) {
+  SE3 o;
+#pragma unroll
+  for (int i = 0; i < 9; ++i) o.R[i] = bcast(T.R[i], k);
+#pragma unroll
+  for (int i = 0; i < 3; ++i) o.p[i] = bcast(T.p[i], k);
+  return o;
+}
+
+__device__ __forceinline__ bool mesh_mesh_wave(const DevWorld& w, int ga, const SE3& TA, int gb, const SE3& TB) {
+  // lanes take 64 of B's triangles into A's frame; each one that meets A's
+  // box is then broadcast, A's cluster boxes are tested one per lane, and
+  // the triangles of up to 8 overlapping clusters are tested at once (8
+  // lanes per cluster)
+  const uint32_t lane = lane_id();
+  const cptr<double> gra = w.geom_rec + G_STRIDE * ga, grb = w.geom_rec + G_STRIDE * gb;
+  const int b0 = (int)grb[G_PARAM], b1 = b0 + (int)grb[G_PARAM + 1];
+  const int c0 = w.mesh_tree[2 * ga], c1 = c0 + w.mesh_tree[2 * ga + 1];
+  double R[9], T[3], alo[3], ahi[3];
+  const double dt[3] = {TB.p[0] - TA.p[0], TB.p[1] - TA.p[1], TB.p[2] - TA.p[2]};
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+#pragma unroll
+    for (int j = 0; j < 3; ++j) R[3 * i + j] = (TA.R[i] * TB.R[j] + TA.R[3 + i] * TB.R[3 + j]) + TA.R[6 + i] * TB.R[6 + j];
+    T[i] = (TA.R[i] * dt[0] + TA.R[3 + i] * dt[1]) + TA.R[6 + i] * dt[2];
+    alo[i] = gra[G_OBB_C + i] - gra[G_OBB_E + i];
+    ahi[i] = gra[G_OBB_C + i] + gra[G_OBB_E + i];
+  }
+  for (int j0 = b0; j0 < b1; j0 += 64) {
+    const int j = j0 + (int)lane;
+    bool keep = j < b1;
+    const cptr<double> rq = w.mesh_tri + TR_STRIDE * (size_t)(keep ? j : b0);
+    double Q[9], qlo[3], qhi[3];
+#pragma unroll
+    for (int v = 0; v < 3; ++v)
+#pragma unroll
+      for (int i = 0; i < 3; ++i)
+        Q[3 * v + i] = ((R[3 * i] * rq[3 * v] + R[3 * i + 1] * rq[3 * v + 1]) + R[3 * i + 2] * rq[3 * v + 2]) + T[i];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      qlo[i] = fmin(Q[i], fmin(Q[3 + i], Q[6 + i])) - kMeshPad;
+      qhi[i] = fmax(Q[i], fmax(Q[3 + i], Q[6 + i])) + kMeshPad;
+      keep &= !(qlo[i] > ahi[i] || qhi[i] < alo[i]);
+    }
+    unsigned long long todo = __ballot(keep);
+    while (todo) {
+      const int k = __builtin_ctzll(todo);
+      todo &= todo - 1;
+      double Qk[9], lk[3], hk[3];
+#pragma unroll
+      for (int i = 0; i < 9; ++i) Qk[i] = bcast(Q[i], k);
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        lk[i] = bcast(qlo[i], k);
+        hk[i] = bcast(qhi[i], k);
+      }
+      for (int cb = c0; cb < c1; cb += 64) {
+        const int c = cb + (int)lane;
+        bool ov = c < c1;
+        if (ov) {
+          const cptr<double> bx = w.mesh_node + 6 * (size_t)c;
+#pragma unroll
+          for (int i = 0; i < 3; ++i) ov &= !(bx[i] > hk[i] || bx[3 + i] < lk[i]);
+        }
+        unsigned long long m = __ballot(ov);
+        while (m) {
+          int myc = -1;  // cluster of this lane's group of 8
+          for (int g = 0; g < 8 && m; ++g) {
+            const int cc = __builtin_ctzll(m);
+            m &= m - 1;
+            if (g == (int)(lane >> 3)) myc = cb + cc;
+          }
+          bool hit = false;
+          if (myc >= 0) {
+            const int t1 = w.mesh_link[2 * myc] + w.mesh_link[2 * myc + 1];
+            for (int t = w.mesh_link[2 * myc] + (int)(lane & 7); t < t1 && !hit; t += 8) {
+              const cptr<double> rp = w.mesh_tri + TR_STRIDE * (size_t)t;
+              bool o2 = false;
+#pragma unroll
+              for (int i = 0; i < 3; ++i) o2 |= rp[TR_LO + i] > hk[i] || rp[TR_HI + i] < lk[i];
+              if (o2) continue;
+              double P[9];
+#pragma unroll
+              for (int q = 0; q < 9; ++q) P[q] = rp[TR_P + q];
+              hit = tri_tri_intersect(P, Qk);
+            }
+          }
+          if (__ballot(hit) != 0) return true;
+        }
+      }
+    }
+  }
+  return false;
+}
+
+__device__ __forceinline__ bool mesh_shape_wave(const DevWorld& w, cptr<double> HV, int gm, const SE3& TM, int gs,
+                                             const SE3& TS) {
+  const uint32_t lane = lane_id();
   const cptr<double> grm = w.geom_rec + G_STRIDE * gm, grs = w.geom_rec + G_STRIDE * gs;
   const int ts = w.geom_type[gs];
-  const int t0 = (int)grm[G_PARAM], tn = (int)grm[G_PARAM + 1];
-  // the shape's local box in the mesh frame, widened
+  const int t0 = (int)grm[G_PARAM], t1 = t0 + (int)grm[G_PARAM + 1];
   double sc[3], cl[3], Rl[9], hq[3];
 #pragma unroll
   for (int i = 0; i < 3; ++i)
@@ -1336,7 +1453,7 @@ __device__ __noinline__ bool mesh_shape_hit(const DevWorld& w, cptr<double> HV, 
   for (int i = 0; i < 3; ++i)
     hq[i] = ((std::fabs(Rl[3 * i]) * grs[G_OBB_E] + std::fabs(Rl[3 * i + 1]) * grs[G_OBB_E + 1]) +
              std::fabs(Rl[3 * i + 2]) * grs[G_OBB_E + 2]) * (1.0 + 1e-9) + kMeshPad;
-  GObj A, B;  // A: the shape (o1), B: the triangle (mesh rotation / position)
+  GObj A, B;
   A.rot = gjk_rot_from_matrix(TS.R);
   A.rot_inv = quat_invert2(A.rot);
   A.pos = v3(TS.p[0], TS.p[1], TS.p[2]);
@@ -1347,94 +1464,65 @@ __device__ __noinline__ bool mesh_shape_hit(const DevWorld& w, cptr<double> HV, 
   B.pos = v3(TM.p[0], TM.p[1], TM.p[2]);
   B.geom = gm;
   B.type = MPG_GEOM_MESH;
-  for (int t = t0; t < t0 + tn; ++t) {
-    const cptr<double> rec = w.mesh_tri + TR_STRIDE * (size_t)t;
-    bool out = false;
+  const V3 ca = center(w, A);
+  for (int b = t0; b < t1; b += 64) {
+    const int t = b + (int)lane;
+    bool cand = t < t1;
+    const cptr<double> rec = w.mesh_tri + TR_STRIDE * (size_t)(cand ? t : t0);
 #pragma unroll
-    for (int i = 0; i < 3; ++i) out |= rec[TR_LO + i] > cl[i] + hq[i] || rec[TR_HI + i] < cl[i] - hq[i];
-    if (out) continue;
-    double P[9];
-#pragma unroll
-    for (int k = 0; k < 9; ++k) P[k] = rec[TR_P + k];
-    bool hit;
-    if (ts == MPG_GEOM_SPHERE) {
-      double W[9];
-#pragma unroll
-      for (int v = 0; v < 3; ++v)
-#pragma unroll
-        for (int i = 0; i < 3; ++i)
-          W[3 * v + i] = ((TM.R[3 * i] * P[3 * v] + TM.R[3 * i + 1] * P[3 * v + 1]) + TM.R[3 * i + 2] * P[3 * v + 2]) + TM.p[i];
-      hit = sphere_triangle_intersect(grs[G_PARAM], TS.p, W);
-    } else {
-      const V3 tc = v3((P[0] + P[3] + P[6]) / 3, (P[1] + P[4] + P[7]) / 3, (P[2] + P[5] + P[8]) / 3);
-      int st;
-      V3 v0, v1, v2, v3_, dir;
-      mpr_begin(center(w, A), vadd(quat_rot(tc, B.rot), B.pos), st, v0, dir);
-      int res = 0;
-      while (res == 0) {
-        const V3 sp = msupport_tri(w, HV, A, B, P, tc, dir);
-        res = mpr_advance(w.mpr_tol, sp, st, v0, v1, v2, v3_, dir);
-      }
-      hit = res > 0;
-    }
-    if (hit) return true;
-  }
-  return false;
-}
-
-// (mesh ga at TA, mesh gb at TB): B's triangles into A's frame, then A's
-// triangles under each transformed one
-__device__ __noinline__ bool mesh_mesh_hit(const DevWorld& w, int ga, const SE3& TA, int gb, const SE3& TB) {
-  const cptr<double> gra = w.geom_rec + G_STRIDE * ga, grb = w.geom_rec + G_STRIDE * gb;
-  const int a0 = (int)gra[G_PARAM], an = (int)gra[G_PARAM + 1];
-  const int b0 = (int)grb[G_PARAM], bn = (int)grb[G_PARAM + 1];
-  double R[9], T[3], alo[3], ahi[3];
-  const double dt[3] = {TB.p[0] - TA.p[0], TB.p[1] - TA.p[1], TB.p[2] - TA.p[2]};
-#pragma unroll
-  for (int i = 0; i < 3; ++i) {
-#pragma unroll
-    for (int j = 0; j < 3; ++j) R[3 * i + j] = (TA.R[i] * TB.R[j] + TA.R[3 + i] * TB.R[3 + j]) + TA.R[6 + i] * TB.R[6 + j];
-    T[i] = (TA.R[i] * dt[0] + TA.R[3 + i] * dt[1]) + TA.R[6 + i] * dt[2];
-    alo[i] = gra[G_OBB_C + i] - gra[G_OBB_E + i] - kMeshPad;
-    ahi[i] = gra[G_OBB_C + i] + gra[G_OBB_E + i] + kMeshPad;
-  }
-  for (int j = b0; j < b0 + bn; ++j) {
-    const cptr<double> rq = w.mesh_tri + TR_STRIDE * (size_t)j;
-    double Q[9], qlo[3], qhi[3];
-#pragma unroll
-    for (int v = 0; v < 3; ++v)
-#pragma unroll
-      for (int i = 0; i < 3; ++i)
-        Q[3 * v + i] = ((R[3 * i] * rq[3 * v] + R[3 * i + 1] * rq[3 * v + 1]) + R[3 * i + 2] * rq[3 * v + 2]) + T[i];
-    bool out = false;
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-      qlo[i] = fmin(Q[i], fmin(Q[3 + i], Q[6 + i])) - kMeshPad;
-      qhi[i] = fmax(Q[i], fmax(Q[3 + i], Q[6 + i])) + kMeshPad;
-      out |= qlo[i] > ahi[i] || qhi[i] < alo[i];
-    }
-    if (out) continue;
-    for (int t = a0; t < a0 + an; ++t) {
-      const cptr<double> rp = w.mesh_tri + TR_STRIDE * (size_t)t;
-      bool o2 = false;
-#pragma unroll
-      for (int i = 0; i < 3; ++i) o2 |= rp[TR_LO + i] > qhi[i] || rp[TR_HI + i] < qlo[i];
-      if (o2) continue;
+    for (int i = 0; i < 3; ++i) cand &= !(rec[TR_LO + i] > cl[i] + hq[i] || rec[TR_HI + i] < cl[i] - hq[i]);
+    if (__ballot(cand) == 0) continue;
+    bool hit = false;
+    if (cand) {
       double P[9];
 #pragma unroll
-      for (int k = 0; k < 9; ++k) P[k] = rp[TR_P + k];
-      if (tri_tri_intersect(P, Q)) return true;
+      for (int k = 0; k < 9; ++k) P[k] = rec[TR_P + k];
+      if (ts == MPG_GEOM_SPHERE) {
+        double W[9];
+#pragma unroll
+        for (int v = 0; v < 3; ++v)
+#pragma unroll
+          for (int i = 0; i < 3; ++i)
+            W[3 * v + i] = ((TM.R[3 * i] * P[3 * v] + TM.R[3 * i + 1] * P[3 * v + 1]) + TM.R[3 * i + 2] * P[3 * v + 2]) + TM.p[i];
+        hit = sphere_triangle_intersect(grs[G_PARAM], TS.p, W);
+      } else {
+        const V3 tc = v3((P[0] + P[3] + P[6]) / 3, (P[1] + P[4] + P[7]) / 3, (P[2] + P[5] + P[8]) / 3);
+        int st;
+        V3 v0, v1, v2, v3_, dir;
+        mpr_begin(ca, vadd(quat_rot(tc, B.rot), B.pos), st, v0, dir);
+        int res = 0;
+        while (res == 0) {
+          const V3 sp = msupport_tri(w, HV, A, B, P, tc, dir);
+          res = mpr_advance(w.mpr_tol, sp, st, v0, v1, v2, v3_, dir);
+        }
+        hit = res > 0;
+      }
     }
+    if (__ballot(hit) != 0) return true;
   }
   return false;
 }
 
-__device__ __forceinline__ bool mesh_hit(const DevWorld& w, cptr<double> HV, int ga, const SE3& TA, int gb,
-                                         const SE3& TB) {
+// every active lane's (TA, TB) candidate of the (wave-uniform) mesh pair
+// (ga, gb), one after the other with the whole wave; bit k = lane k's hit
+__device__ __forceinline__ unsigned long long mesh_wave_eval(const DevWorld& w, cptr<double> HV, int ga, const SE3& TA,
+                                                            int gb, const SE3& TB, bool active) {
   const bool am = w.geom_type[ga] == MPG_GEOM_MESH, bm = w.geom_type[gb] == MPG_GEOM_MESH;
-  if (am && bm) return mesh_mesh_hit(w, ga, TA, gb, TB);
-  return am ? mesh_shape_hit(w, HV, ga, TA, gb, TB) : mesh_shape_hit(w, HV, gb, TB, ga, TA);
+  unsigned long long todo = __ballot(active), hits = 0;
+  while (todo) {
+    const int k = __builtin_ctzll(todo);
+    todo &= todo - 1;
+    const SE3 A = bcast_se3(TA, k), B = bcast_se3(TB, k);
+    if (w.debug_mode == (am && bm ? 5 : 6)) continue;
+    bool h;
+    if (am && bm) h = mesh_mesh_wave(w, ga, A, gb, B);
+    else if (am) h = mesh_shape_wave(w, HV, ga, A, gb, B);
+    else h = mesh_shape_wave(w, HV, gb, B, ga, A);
+    if (h) hits |= 1ull << k;
+  }
+  return hits;
 }
+
 
 template <bool FROM_POSES>
 __global__ __launch_bounds__(256) MPG_NARROW_WAVES void narrow_kernel(DevWorld w, const double* __restrict__ in,
@@ -1607,7 +1695,9 @@ __global__ __launch_bounds__(256) void small_kernel(DevWorld w, const double* __
     }
     const double rr = ra[G_RADIUS] + rb[G_RADIUS] + kSmallMargin;
     const bool near = live && d2 <= rr * rr;
-    if (cf != CF_NONE) {
+    if (CLS == CLS_MESH) {
+      hit = (mesh_wave_eval(w, HV, ga, TA, gb, TB, near) >> lane) & 1ull;
+    } else if (cf != CF_NONE) {
       if (near && pair_closed_form<CLS>(cf, w, ga, TA, gb, TB)) hit = 1;
     } else if (__ballot(near) != 0) {
       GObj A, B;
@@ -2344,6 +2434,44 @@ struct mpg_world {
 
 namespace {
 
+// Spatial clusters of one mesh's triangle records: the leaves of a median
+// split (centroids, longest axis) with at most `leaf` triangles each, in
+// order; triangle k of the clusters' ranges is rec[order[k]].
+void mesh_build_clusters(const std::vector<double>& rec, std::vector<int>& order, int lo, int hi, int leaf, int rec0,
+                         std::vector<double>& box, std::vector<int>& link) {
+  auto cen = [&](int t, int k) {
+    const double* r = rec.data() + (size_t)TR_STRIDE * t;
+    return r[TR_LO + k] + r[TR_HI + k];
+  };
+  if (hi - lo <= leaf) {
+    double blo[3] = {DBL_MAX, DBL_MAX, DBL_MAX}, bhi[3] = {-DBL_MAX, -DBL_MAX, -DBL_MAX};
+    for (int i = lo; i < hi; ++i) {
+      const double* r = rec.data() + (size_t)TR_STRIDE * order[i];
+      for (int k = 0; k < 3; ++k) {
+        blo[k] = std::min(blo[k], r[TR_LO + k]);
+        bhi[k] = std::max(bhi[k], r[TR_HI + k]);
+      }
+    }
+    box.insert(box.end(), {blo[0], blo[1], blo[2], bhi[0], bhi[1], bhi[2]});
+    link.insert(link.end(), {rec0 + lo, hi - lo});
+    return;
+  }
+  double clo[3] = {DBL_MAX, DBL_MAX, DBL_MAX}, chi[3] = {-DBL_MAX, -DBL_MAX, -DBL_MAX};
+  for (int i = lo; i < hi; ++i)
+    for (int k = 0; k < 3; ++k) {
+      clo[k] = std::min(clo[k], cen(order[i], k));
+      chi[k] = std::max(chi[k], cen(order[i], k));
+    }
+  int ax = 0;
+  for (int k = 1; k < 3; ++k)
+    if (chi[k] - clo[k] > chi[ax] - clo[ax]) ax = k;
+  const int mid = (lo + hi) / 2;
+  std::nth_element(order.begin() + lo, order.begin() + mid, order.begin() + hi,
+                   [&](int a, int b) { return cen(a, ax) < cen(b, ax) || (cen(a, ax) == cen(b, ax) && a < b); });
+  mesh_build_clusters(rec, order, lo, mid, leaf, rec0, box, link);
+  mesh_build_clusters(rec, order, mid, hi, leaf, rec0, box, link);
+}
+
 struct BlobBuilder {
   std::vector<char> bytes;
   template <class T>
@@ -2865,22 +2993,37 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
   // octrees: leaf boxes + a uniform grid per octree geometry (cells of at
   // least the largest leaf, <= 64 per axis); a leaf is listed in every cell
   // its box overlaps
-  // BVH meshes: per triangle its vertices (mesh frame) and AABB (TR_*)
+  // BVH meshes: per triangle its vertices (mesh frame) and AABB (TR_*), in
+  // cluster order
   std::vector<double> mesh_tri((size_t)TR_STRIDE * std::max<int64_t>(d->n_mesh_triangles, 1), 0.0);
+  std::vector<double> mesh_node;
+  std::vector<int> mesh_link, mesh_tree(2 * (size_t)std::max(d->n_geoms, 1), 0);
   for (int g = 0; g < d->n_geoms; ++g) {
     if (d->geom_type[g] != MPG_GEOM_MESH) continue;
     const double* V = d->vertices + 3 * (size_t)d->geom_vertex_start[g];
     const int64_t t0 = (int64_t)d->geom_param[4 * g], tn = (int64_t)d->geom_param[4 * g + 1];
-    for (int64_t t = t0; t < t0 + tn; ++t) {
-      double* r = mesh_tri.data() + (size_t)TR_STRIDE * t;
+    std::vector<double> rec((size_t)TR_STRIDE * std::max<int64_t>(tn, 1), 0.0);
+    for (int64_t t = 0; t < tn; ++t) {
+      double* r = rec.data() + (size_t)TR_STRIDE * t;
       for (int v = 0; v < 3; ++v)
-        for (int k = 0; k < 3; ++k) r[TR_P + 3 * v + k] = V[3 * (size_t)d->mesh_triangle[3 * t + v] + k];
+        for (int k = 0; k < 3; ++k) r[TR_P + 3 * v + k] = V[3 * (size_t)d->mesh_triangle[3 * (t0 + t) + v] + k];
       for (int k = 0; k < 3; ++k) {
         r[TR_LO + k] = std::min(r[TR_P + k], std::min(r[TR_P + 3 + k], r[TR_P + 6 + k]));
         r[TR_HI + k] = std::max(r[TR_P + k], std::max(r[TR_P + 3 + k], r[TR_P + 6 + k]));
       }
     }
+    std::vector<int> order((size_t)tn);
+    for (int64_t t = 0; t < tn; ++t) order[t] = (int)t;
+    // clusters of <= max(8, T / 64) triangles: ~64 cluster boxes per mesh
+    mesh_tree[2 * g] = (int)(mesh_link.size() / 2);
+    mesh_build_clusters(rec, order, 0, (int)tn, std::max<int>(8, (int)((tn + 63) / 64)), (int)t0, mesh_node, mesh_link);
+    mesh_tree[2 * g + 1] = (int)(mesh_link.size() / 2) - mesh_tree[2 * g];
+    for (int64_t k = 0; k < tn; ++k)
+      std::copy(rec.begin() + (size_t)TR_STRIDE * order[k], rec.begin() + (size_t)TR_STRIDE * (order[k] + 1),
+                mesh_tri.begin() + (size_t)TR_STRIDE * (t0 + k));
   }
+  if (mesh_node.empty()) mesh_node.assign(6, 0.0);
+  if (mesh_link.empty()) mesh_link.assign(2, 0);
   std::vector<double> oct_leaf(6 * (size_t)std::max<int64_t>(d->n_octree_leaves, 1), 0.0);
   if (d->n_octree_leaves > 0) std::copy(d->octree_leaf, d->octree_leaf + 6 * d->n_octree_leaves, oct_leaf.begin());
   std::vector<double> oct_grid((size_t)OG_STRIDE * std::max(d->n_geoms, 1), 0.0);
@@ -3012,6 +3155,9 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
   const size_t o_bsb = bb.add(bpp.sobj.data(), bpp.sobj.size());
   const size_t o_olf = bb.add(oct_leaf.data(), oct_leaf.size());
   const size_t o_mtr = bb.add(mesh_tri.data(), mesh_tri.size());
+  const size_t o_mnd = bb.add(mesh_node.data(), mesh_node.size());
+  const size_t o_mln = bb.add(mesh_link.data(), mesh_link.size());
+  const size_t o_mtt = bb.add(mesh_tree.data(), mesh_tree.size());
   const size_t o_ogr = bb.add(oct_grid.data(), oct_grid.size());
   const size_t o_oce = bb.add(oct_cells.data(), oct_cells.size());
   const size_t o_oli = bb.add(oct_list.data(), oct_list.size());
@@ -3117,6 +3263,9 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
   bp.sobj = F(o_bsb);
   dw.oct_leaf = to_cptr<double>(base + o_olf);
   dw.mesh_tri = to_cptr<double>(base + o_mtr);
+  dw.mesh_node = to_cptr<double>(base + o_mnd);
+  dw.mesh_link = to_cptr<int>(base + o_mln);
+  dw.mesh_tree = to_cptr<int>(base + o_mtt);
   dw.oct_grid = to_cptr<double>(base + o_ogr);
   dw.oct_cells = I(o_oce);
   dw.oct_list = I(o_oli);

@@ -28,9 +28,10 @@ PANDA_LINKS = ["panda_link0", "panda_link1", "panda_link2", "panda_link3", "pand
                "panda_link6", "panda_link7", "panda_hand", "panda_leftfinger", "panda_rightfinger"]
 PANDA_JOINTS = ["panda_joint1", "panda_joint2", "panda_joint3", "panda_joint4", "panda_joint5", "panda_joint6",
                 "panda_joint7", "panda_finger_joint1", "panda_finger_joint2"]
-CFG_SEED = {2: 0, 3: 1, 4: 2, 6: 6}
-CFG_N = {2: 1 << 16, 3: 1 << 20, 4: 1 << 22, 6: 1 << 20}
-CFG_NAME = {2: "panda_self", 3: "panda_10boxes", 4: "panda_4convex", 6: "panda_floor_cloud"}
+CFG_SEED = {2: 0, 3: 1, 4: 2, 6: 6, 7: 7}
+CFG_N = {2: 1 << 16, 3: 1 << 20, 4: 1 << 22, 6: 1 << 20, 7: 1 << 18}
+CFG_NAME = {2: "panda_self", 3: "panda_10boxes", 4: "panda_4convex", 6: "panda_floor_cloud",
+            7: "panda_bvh_meshes_10boxes"}
 
 
 def panda(convex: bool = True) -> "pymp.articulation.ArticulatedModel":
@@ -72,6 +73,8 @@ def world(cfg: int, convex: bool = True):
     the robot's links as BVH meshes."""
     if cfg == 6:
         return cloud_world("floor")
+    if cfg == 7:  # cfg3 with the links as BVH meshes (convex=False)
+        return world(3, convex=False)
     art = panda(convex)
     w = pymp.planning_world.PlanningWorld([art], ["panda"], [], [])
     if cfg == 3:

@@ -87,6 +87,8 @@ def convex_scene(art: M.Articulation) -> List[Tuple[str, object, tuple]]:
 
 
 def oracle_world(cfg: int, convex: bool = True) -> oracle.OracleWorld:
+    if cfg == 7:
+        return oracle_world(3, convex=False)
     art = panda_articulation(convex)
     if cfg in (1, 2):
         return oracle.OracleWorld(art)
