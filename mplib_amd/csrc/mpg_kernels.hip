@@ -839,10 +839,11 @@ __global__ __launch_bounds__(256) void scatter_kernel(const uint32_t* __restrict
 // ---------------------------------------------------------------------------
 enum : int { MPR_DONE = 0, MPR_V1 = 1, MPR_V2 = 2, MPR_V3 = 3, MPR_V4 = 4 };
 
-__device__ __forceinline__ bool octree_hit(const DevWorld& w, cptr<double> HV, int go, const SE3& TO, int gs,
+__device__ __forceinline__ bool octree_wave(const DevWorld& w, cptr<double> HV, int go, const SE3& TO, int gs,
                                            const SE3& TS);
 
-__device__ __forceinline__ unsigned long long mesh_wave_eval(const DevWorld& w, cptr<double> HV, int ga, const SE3& TA,
+template <int CLS>
+__device__ __forceinline__ unsigned long long walk_wave_eval(const DevWorld& w, cptr<double> HV, int ga, const SE3& TA,
                                                             int gb, const SE3& TB, bool active);
 
 // one pair evaluation of class CLS: closed form, octree walk or BVH mesh
@@ -852,9 +853,7 @@ template <int CLS>
 __device__ __forceinline__ bool pair_closed_form(int cf, const DevWorld& w, int ga, const SE3& TA, int gb,
                                                  const SE3& TB) {
   if (CLS == CLS_CLOSED) return closed_form(cf, w, ga, TA, gb, TB);
-  if (CLS == CLS_MESH) return false;  // evaluated wave-wide (mesh_wave_eval)
-  return w.geom_type[ga] == MPG_GEOM_OCTREE ? octree_hit(w, w.hull, ga, TA, gb, TB)
-                                            : octree_hit(w, w.hull, gb, TB, ga, TA);
+  return false;  // octree / mesh pairs: evaluated wave-wide (walk_wave_eval)
 }
 
 // FCL closed-form pairs (box-box, sphere-sphere, sphere-box) and octree
@@ -890,7 +889,7 @@ __global__ __launch_bounds__(256) void closed_form_kernel(DevWorld w, const doub
     const uint32_t* __restrict__ cl = cand + seg_start[p];
     for (uint32_t base = t0; base < t1; base += 64) {
       const uint32_t idx = base + lane;
-      if (CLS == CLS_MESH) {  // the wave walks each candidate's triangles together
+      if (CLS != CLS_CLOSED) {  // octree / mesh walks: the wave walks each candidate together
         const bool active = idx < t1;
         const long long c = active ? cl[idx] : 0;
         SE3 TA = {}, TB = {};
@@ -898,7 +897,7 @@ __global__ __launch_bounds__(256) void closed_form_kernel(DevWorld w, const doub
           TA = am ? moving_tf<FROM_POSES>(w, in, sc, c, a) : load_se3(w.static_T + 12 * (a - w.n_moving));
           TB = bm ? moving_tf<FROM_POSES>(w, in, sc, c, b) : load_se3(w.static_T + 12 * (b - w.n_moving));
         }
-        const unsigned long long hits = mesh_wave_eval(w, w.hull, ga, TA, gb, TB, active);
+        const unsigned long long hits = walk_wave_eval<CLS>(w, w.hull, ga, TA, gb, TB, active);
         if ((hits >> lane) & 1ull) {
           if (masks) atomicOr(&masks[c * w.W + (p >> 5)], 1u << (p & 31));
           flags[c] = 1;
@@ -1055,8 +1054,9 @@ __device__ __forceinline__ V3 msupport_box(const GObj& a, const double* h, const
 // the recursion's pruning never hides a leaf this test would accept.  Leaves
 // come from the octree's grid cells under the shape's box in the octree frame
 // widened exactly as obbDisjoint's first three axes (|R| + 1e-6): a leaf
-// outside it fails those axes.  The pair's geometries are wave-uniform.
-__device__ __forceinline__ bool octree_hit(const DevWorld& w, cptr<double> HV, int go, const SE3& TO, int gs,
+// outside it fails those axes.  Inputs are wave-uniform: the whole wave
+// walks one candidate.
+__device__ __forceinline__ bool octree_wave(const DevWorld& w, cptr<double> HV, int go, const SE3& TO, int gs,
                                            const SE3& TS) {
   const cptr<double> grs = w.geom_rec + G_STRIDE * gs;
   const int ts = w.geom_type[gs];
@@ -1100,60 +1100,75 @@ __device__ __forceinline__ bool octree_hit(const DevWorld& w, cptr<double> HV, i
   B.pos = v3(TS.p[0], TS.p[1], TS.p[2]);
   B.geom = gs;
   B.type = ts;
+  // one candidate per wave: the leaves listed in the cells under the box
+  // are queued 64 at a time (one per lane) and tested side by side
+  auto leaf_hit = [&](int leaf) -> bool {
+    const cptr<double> L = w.oct_leaf + 6 * (size_t)leaf;
+    bool out = false;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) out |= L[i] > cl[i] + hq[i] || L[3 + i] < cl[i] - hq[i];
+    if (out) return false;
+    // leaf OBB: axes TO.R, centre TO * c, extent (max - min) * 0.5
+    double c[3], cw[3], a[3], side[3], T[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      c[i] = (L[i] + L[3 + i]) * 0.5;
+      side[i] = L[3 + i] - L[i];
+      a[i] = side[i] * 0.5;
+    }
+#pragma unroll
+    for (int i = 0; i < 3; ++i) cw[i] = ((TO.R[3 * i] * c[0] + TO.R[3 * i + 1] * c[1]) + TO.R[3 * i + 2] * c[2]) + TO.p[i];
+    const double t[3] = {sc[0] - cw[0], sc[1] - cw[1], sc[2] - cw[2]};
+#pragma unroll
+    for (int i = 0; i < 3; ++i) T[i] = (TO.R[i] * t[0] + TO.R[3 + i] * t[1]) + TO.R[6 + i] * t[2];
+    if (obb_disjoint(Rl, T, a, se)) return false;
+    SE3 TL;  // box_tf = tf * Translation(centre)
+#pragma unroll
+    for (int i = 0; i < 9; ++i) TL.R[i] = TO.R[i];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) TL.p[i] = cw[i];
+    if (ts == MPG_GEOM_BOX) {
+      const double sb[3] = {grs[G_PARAM], grs[G_PARAM + 1], grs[G_PARAM + 2]};
+      return box_box_intersect(side, TL, sb, TS);
+    }
+    if (ts == MPG_GEOM_SPHERE) return sphere_box_intersect(grs[G_PARAM], TS, side, TL);
+    GObj A1 = A;
+    A1.pos = v3(cw[0], cw[1], cw[2]);
+    const double h[3] = {side[0] / 2.0, side[1] / 2.0, side[2] / 2.0};  // boxToGJK: side / 2
+    int st;
+    V3 v0, v1, v2, v3_, dir;
+    mpr_begin(A1.pos, center(w, B), st, v0, dir);
+    int res = 0;
+    while (res == 0) {
+      const V3 sp = msupport_box(A1, h, w, HV, B, dir);
+      res = mpr_advance(w.mpr_tol, sp, st, v0, v1, v2, v3_, dir);
+    }
+    return res > 0;
+  };
+  const uint32_t lane = lane_id();
   const int cell0 = (int)og[OG_CELL0];
+  int mine = -1, fill = 0;
   for (int x = c0[0]; x <= c1[0]; ++x)
     for (int y = c0[1]; y <= c1[1]; ++y)
       for (int z = c0[2]; z <= c1[2]; ++z) {
         const int cell = cell0 + (x * dims[1] + y) * dims[2] + z;
+        int k = w.oct_cells[cell];
         const int k1 = w.oct_cells[cell + 1];
-        for (int k = w.oct_cells[cell]; k < k1; ++k) {
-          const cptr<double> L = w.oct_leaf + 6 * (size_t)w.oct_list[k];
-          bool out = false;
-#pragma unroll
-          for (int i = 0; i < 3; ++i) out |= L[i] > cl[i] + hq[i] || L[3 + i] < cl[i] - hq[i];
-          if (out) continue;
-          // leaf OBB: axes TO.R, centre TO * c, extent (max - min) * 0.5
-          double c[3], cw[3], a[3], side[3], T[3];
-#pragma unroll
-          for (int i = 0; i < 3; ++i) {
-            c[i] = (L[i] + L[3 + i]) * 0.5;
-            side[i] = L[3 + i] - L[i];
-            a[i] = side[i] * 0.5;
+        while (k < k1) {
+          const int take = min(64 - fill, k1 - k);
+          if ((int)lane >= fill && (int)lane < fill + take) mine = w.oct_list[k + (int)lane - fill];
+          fill += take;
+          k += take;
+          if (fill == 64) {
+            const bool hit = leaf_hit(mine);
+            if (__ballot(hit) != 0) return true;
+            fill = 0;
+            mine = -1;
           }
-#pragma unroll
-          for (int i = 0; i < 3; ++i) cw[i] = ((TO.R[3 * i] * c[0] + TO.R[3 * i + 1] * c[1]) + TO.R[3 * i + 2] * c[2]) + TO.p[i];
-          const double t[3] = {sc[0] - cw[0], sc[1] - cw[1], sc[2] - cw[2]};
-#pragma unroll
-          for (int i = 0; i < 3; ++i) T[i] = (TO.R[i] * t[0] + TO.R[3 + i] * t[1]) + TO.R[6 + i] * t[2];
-          if (obb_disjoint(Rl, T, a, se)) continue;
-          SE3 TL;  // box_tf = tf * Translation(centre)
-#pragma unroll
-          for (int i = 0; i < 9; ++i) TL.R[i] = TO.R[i];
-#pragma unroll
-          for (int i = 0; i < 3; ++i) TL.p[i] = cw[i];
-          bool hit;
-          if (ts == MPG_GEOM_BOX) {
-            const double sb[3] = {grs[G_PARAM], grs[G_PARAM + 1], grs[G_PARAM + 2]};
-            hit = box_box_intersect(side, TL, sb, TS);
-          } else if (ts == MPG_GEOM_SPHERE) {
-            hit = sphere_box_intersect(grs[G_PARAM], TS, side, TL);
-          } else {
-            A.pos = v3(cw[0], cw[1], cw[2]);
-            const double h[3] = {side[0] / 2.0, side[1] / 2.0, side[2] / 2.0};  // boxToGJK: side / 2
-            int st;
-            V3 v0, v1, v2, v3_, dir;
-            mpr_begin(A.pos, center(w, B), st, v0, dir);
-            int res = 0;
-            while (res == 0) {
-              const V3 sp = msupport_box(A, h, w, HV, B, dir);
-              res = mpr_advance(w.mpr_tol, sp, st, v0, v1, v2, v3_, dir);
-            }
-            hit = res > 0;
-          }
-          if (hit) return true;
         }
       }
-  return false;
+  const bool hit = mine >= 0 && leaf_hit(mine);
+  return __ballot(hit) != 0;
 }
 
 
@@ -1503,24 +1518,39 @@ __device__ __forceinline__ bool mesh_shape_wave(const DevWorld& w, cptr<double> 
   return false;
 }
 
-// every active lane's (TA, TB) candidate of the (wave-uniform) mesh pair
-// (ga, gb), one after the other with the whole wave; bit k = lane k's hit
-__device__ __forceinline__ unsigned long long mesh_wave_eval(const DevWorld& w, cptr<double> HV, int ga, const SE3& TA,
+// every active lane's (TA, TB) candidate of the (wave-uniform) mesh or
+// octree pair (ga, gb), one after the other with the whole wave; bit k =
+// lane k's hit
+template <int CLS>
+__device__ __forceinline__ unsigned long long walk_wave_eval(const DevWorld& w, cptr<double> HV, int ga, const SE3& TA,
                                                             int gb, const SE3& TB, bool active) {
-  const bool am = w.geom_type[ga] == MPG_GEOM_MESH, bm = w.geom_type[gb] == MPG_GEOM_MESH;
-  unsigned long long todo = __ballot(active), hits = 0;
-  while (todo) {
-    const int k = __builtin_ctzll(todo);
-    todo &= todo - 1;
-    const SE3 A = bcast_se3(TA, k), B = bcast_se3(TB, k);
-    if (w.debug_mode == (am && bm ? 5 : 6)) continue;
-    bool h;
-    if (am && bm) h = mesh_mesh_wave(w, ga, A, gb, B);
-    else if (am) h = mesh_shape_wave(w, HV, ga, A, gb, B);
-    else h = mesh_shape_wave(w, HV, gb, B, ga, A);
-    if (h) hits |= 1ull << k;
+  const int tga = w.geom_type[ga], tgb = w.geom_type[gb];
+  if constexpr (CLS == CLS_OCTREE) {
+    unsigned long long todo = __ballot(active), hits = 0;
+    while (todo) {
+      const int k = __builtin_ctzll(todo);
+      todo &= todo - 1;
+      const SE3 A = bcast_se3(TA, k), B = bcast_se3(TB, k);
+      const bool h = tga == MPG_GEOM_OCTREE ? octree_wave(w, HV, ga, A, gb, B) : octree_wave(w, HV, gb, B, ga, A);
+      if (h) hits |= 1ull << k;
+    }
+    return hits;
+  } else {
+    const bool am = tga == MPG_GEOM_MESH, bm = tgb == MPG_GEOM_MESH;
+    unsigned long long todo = __ballot(active), hits = 0;
+    while (todo) {
+      const int k = __builtin_ctzll(todo);
+      todo &= todo - 1;
+      const SE3 A = bcast_se3(TA, k), B = bcast_se3(TB, k);
+      if (w.debug_mode == (am && bm ? 5 : 6)) continue;
+      bool h;
+      if (am && bm) h = mesh_mesh_wave(w, ga, A, gb, B);
+      else if (am) h = mesh_shape_wave(w, HV, ga, A, gb, B);
+      else h = mesh_shape_wave(w, HV, gb, B, ga, A);
+      if (h) hits |= 1ull << k;
+    }
+    return hits;
   }
-  return hits;
 }
 
 
@@ -1695,8 +1725,8 @@ __global__ __launch_bounds__(256) void small_kernel(DevWorld w, const double* __
     }
     const double rr = ra[G_RADIUS] + rb[G_RADIUS] + kSmallMargin;
     const bool near = live && d2 <= rr * rr;
-    if (CLS == CLS_MESH) {
-      hit = (mesh_wave_eval(w, HV, ga, TA, gb, TB, near) >> lane) & 1ull;
+    if (CLS != CLS_CLOSED) {
+      hit = (walk_wave_eval<CLS>(w, HV, ga, TA, gb, TB, near) >> lane) & 1ull;
     } else if (cf != CF_NONE) {
       if (near && pair_closed_form<CLS>(cf, w, ga, TA, gb, TB)) hit = 1;
     } else if (__ballot(near) != 0) {
