@@ -1078,14 +1078,38 @@ __device__ __forceinline__ bool octree_wave(const DevWorld& w, cptr<double> HV, 
   for (int i = 0; i < 3; ++i)
     hq[i] = ((std::fabs(Rl[3 * i]) + 1e-6) * se[0] + (std::fabs(Rl[3 * i + 1]) + 1e-6) * se[1] +
              (std::fabs(Rl[3 * i + 2]) + 1e-6) * se[2]) * (1.0 + 1e-12) + 1e-12;
+  // tighter: the shape's own extent along the octree axes (its support in
+  // +-axis), padded; a leaf beyond it on an octree axis is separated from
+  // the shape, so every leaf test on it fails
+  double blo[3], bhi[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const double ax[3] = {TO.R[i], TO.R[3 + i], TO.R[6 + i]};
+    const V3 dl = v3((TS.R[0] * ax[0] + TS.R[3] * ax[1]) + TS.R[6] * ax[2],
+                     (TS.R[1] * ax[0] + TS.R[4] * ax[1]) + TS.R[7] * ax[2],
+                     (TS.R[2] * ax[0] + TS.R[5] * ax[1]) + TS.R[8] * ax[2]);
+    const V3 sp = support_local(w, HV, gs, ts, dl), sn = support_local(w, HV, gs, ts, vscale(dl, -1.0));
+    double ep = 0.0, en = 0.0;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const double lp = (k == 0 ? sp.x : k == 1 ? sp.y : sp.z), ln = (k == 0 ? sn.x : k == 1 ? sn.y : sn.z);
+      ep += ax[0] * TS.R[k] * lp + ax[1] * TS.R[3 + k] * lp + ax[2] * TS.R[6 + k] * lp;
+      en += ax[0] * TS.R[k] * ln + ax[1] * TS.R[3 + k] * ln + ax[2] * TS.R[6 + k] * ln;
+    }
+    const double base = (ax[0] * (TS.p[0] - TO.p[0]) + ax[1] * (TS.p[1] - TO.p[1])) + ax[2] * (TS.p[2] - TO.p[2]);
+    const double pad = 1e-9 + 1e-12 * (std::fabs(base) + std::fabs(ep) + std::fabs(en));
+    blo[i] = fmax(cl[i] - hq[i], base + en - pad);
+    bhi[i] = fmin(cl[i] + hq[i], base + ep + pad);
+    if (blo[i] > bhi[i]) return false;
+  }
   const cptr<double> og = w.oct_grid + OG_STRIDE * go;
   const double inv = og[OG_INV];
   int c0[3], c1[3], dims[3];
 #pragma unroll
   for (int i = 0; i < 3; ++i) {
     dims[i] = (int)og[OG_DIMS + i];
-    const double f0 = std::floor((cl[i] - hq[i] - og[OG_ORIGIN + i]) * inv);
-    const double f1 = std::floor((cl[i] + hq[i] - og[OG_ORIGIN + i]) * inv);
+    const double f0 = std::floor((blo[i] - og[OG_ORIGIN + i]) * inv);
+    const double f1 = std::floor((bhi[i] - og[OG_ORIGIN + i]) * inv);
     if (f1 < 0.0 || f0 >= (double)dims[i]) return false;
     c0[i] = f0 < 0.0 ? 0 : (int)f0;
     c1[i] = f1 >= (double)dims[i] ? dims[i] - 1 : (int)f1;
@@ -1106,7 +1130,7 @@ __device__ __forceinline__ bool octree_wave(const DevWorld& w, cptr<double> HV, 
     const cptr<double> L = w.oct_leaf + 6 * (size_t)leaf;
     bool out = false;
 #pragma unroll
-    for (int i = 0; i < 3; ++i) out |= L[i] > cl[i] + hq[i] || L[3 + i] < cl[i] - hq[i];
+    for (int i = 0; i < 3; ++i) out |= L[i] > bhi[i] || L[3 + i] < blo[i];
     if (out) return false;
     // leaf OBB: axes TO.R, centre TO * c, extent (max - min) * 0.5
     double c[3], cw[3], a[3], side[3], T[3];
@@ -1145,30 +1169,45 @@ __device__ __forceinline__ bool octree_wave(const DevWorld& w, cptr<double> HV, 
     }
     return res > 0;
   };
-  const uint32_t lane = lane_id();
+  // cells of the range 64 at a time (one per lane, loads in parallel); a
+  // wave prefix sum of their leaf counts hands out the leaves 64 at a time
+  __shared__ int s_k0[4][64], s_end[4][64];  // per wave of the 256-thread block
+  const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
   const int cell0 = (int)og[OG_CELL0];
-  int mine = -1, fill = 0;
-  for (int x = c0[0]; x <= c1[0]; ++x)
-    for (int y = c0[1]; y <= c1[1]; ++y)
-      for (int z = c0[2]; z <= c1[2]; ++z) {
-        const int cell = cell0 + (x * dims[1] + y) * dims[2] + z;
-        int k = w.oct_cells[cell];
-        const int k1 = w.oct_cells[cell + 1];
-        while (k < k1) {
-          const int take = min(64 - fill, k1 - k);
-          if ((int)lane >= fill && (int)lane < fill + take) mine = w.oct_list[k + (int)lane - fill];
-          fill += take;
-          k += take;
-          if (fill == 64) {
-            const bool hit = leaf_hit(mine);
-            if (__ballot(hit) != 0) return true;
-            fill = 0;
-            mine = -1;
-          }
+  const int nx = c1[0] - c0[0] + 1, ny = c1[1] - c0[1] + 1, nz = c1[2] - c0[2] + 1;
+  const int ncell = nx * ny * nz;
+  for (int cb = 0; cb < ncell; cb += 64) {
+    const int ci = cb + (int)lane;
+    int k0 = 0, cnt = 0;
+    if (ci < ncell) {
+      const int z = ci % nz, y = (ci / nz) % ny, x = ci / (nz * ny);
+      const int cell = cell0 + ((c0[0] + x) * dims[1] + (c0[1] + y)) * dims[2] + (c0[2] + z);
+      k0 = w.oct_cells[cell];
+      cnt = w.oct_cells[cell + 1] - k0;
+    }
+    const uint32_t incl = wave_inclusive_scan((uint32_t)cnt, lane);
+    const int total = (int)__builtin_amdgcn_readlane(incl, 63);
+    s_k0[wv][lane] = k0;
+    s_end[wv][lane] = (int)incl;
+    __builtin_amdgcn_wave_barrier();
+    for (int ib = 0; ib < total; ib += 64) {
+      const int j = ib + (int)lane;
+      bool hit = false;
+      if (j < total) {
+        int lo = 0, hi = 63;  // first cell slot whose inclusive end exceeds j
+        while (lo < hi) {
+          const int mid = (lo + hi) >> 1;
+          if (s_end[wv][mid] > j) hi = mid;
+          else lo = mid + 1;
         }
+        const int start = lo > 0 ? s_end[wv][lo - 1] : 0;
+        hit = leaf_hit(w.oct_list[s_k0[wv][lo] + (j - start)]);
       }
-  const bool hit = mine >= 0 && leaf_hit(mine);
-  return __ballot(hit) != 0;
+      if (__ballot(hit) != 0) return true;
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+  return false;
 }
 
 
