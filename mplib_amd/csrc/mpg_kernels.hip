@@ -860,7 +860,7 @@ __device__ __forceinline__ bool pair_closed_form(int cf, const DevWorld& w, int 
 // pairs of the candidate lists: one test per candidate.  A kernel of its own so the closed forms'
 // registers do not lower the MPR kernel's occupancy.
 template <bool FROM_POSES, int CLS>
-__global__ __launch_bounds__(256) void closed_form_kernel(DevWorld w, const double* __restrict__ in,
+__global__ __launch_bounds__(256, CLS == CLS_OCTREE ? 2 : 1) void closed_form_kernel(DevWorld w, const double* __restrict__ in,
                                                          const uint32_t* __restrict__ seg_len,
                                                          const uint32_t* __restrict__ seg_start,
                                                          const uint32_t* __restrict__ prefix,
