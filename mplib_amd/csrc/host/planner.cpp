@@ -603,6 +603,38 @@ std::pair<std::string, std::vector<std::vector<double>>> OMPLPlanner::plan(
   };
   std::vector<double> ext_states, chain_states, spec_states;
   constexpr int kLookahead = 3;
+  constexpr size_t kSpecCap = 4096;  // speculated states per batch
+  constexpr int kSpecSteps = 8;      // growTree steps of a speculated connect chain
+  // the connect chain growTree would run on t (plus `extra`, its newest
+  // node) towards x if every motion were valid (as below for the current
+  // iteration); its motions' states are appended to out
+  auto spec_chain = [&](const Tree& t, bool t_is_start, const double* extra, const double* x, std::vector<double>& out) {
+    double best;
+    const int n0 = t.nearest(sp, x, &best);
+    std::vector<double> cur(t.state(n0), t.state(n0) + d), stt((size_t)d);
+    if (extra && sp.distance(extra, x) < best) {
+      best = sp.distance(extra, x);
+      cur.assign(extra, extra + d);
+    }
+    for (int k = 0; k < kSpecSteps; ++k) {
+      const double dc = sp.distance(cur.data(), x);
+      bool reach_k = false;
+      if (dc > max_distance) {
+        sp.interpolate(cur.data(), x, max_distance / dc, stt.data());
+        if (sp.equal(cur.data(), stt.data())) return;
+      } else {
+        stt.assign(x, x + d);
+        reach_k = true;
+      }
+      append_grow(sp, t_is_start, cur.data(), stt.data(), out);
+      if (reach_k) return;
+      const double dn = sp.distance(stt.data(), x);
+      if (dn < best) {
+        best = dn;
+        cur = stt;
+      }
+    }
+  };
   // RRTConnect::growTree (serial mode): nearest, step of at most maxDistance,
   // the motion's states in one batch
   auto grow_serial = [&](Tree& t, bool is_start, const std::vector<double>& r, int& xm) -> Grow {
@@ -737,18 +769,17 @@ std::pair<std::string, std::vector<std::vector<double>>> OMPLPlanner::plan(
       for (size_t i = a; i < b; ++i)
         if (vcache.find(st.data() + i * d) < 0) batch.insert(batch.end(), st.data() + i * d, st.data() + (i + 1) * d);
     };
-    // the connect chain's states go to the batch as they are (they are not
-    // queried again); extension states -- this iteration's and the
-    // speculated ones -- go through the cache
+    // every state goes through the cache: this iteration's extension and
+    // connect chain, and the speculated ones (the next iterations'
+    // extensions for every outcome of this one, and the connect chains the
+    // next iteration would run after them)
     batch.clear();
     bool ext_ok;
     const size_t n_ext = ext_states.size() / (size_t)d;
     const bool ext_known = known(ext_states, 0, n_ext, ext_ok);
-    size_t chain_off = 0;
     if (!ext_known || ext_ok) {
       need(ext_states, 0, n_ext);
-      chain_off = batch.size() / (size_t)d;
-      batch.insert(batch.end(), chain_states.begin(), chain_states.end());
+      need(chain_states, 0, chain_states.size() / (size_t)d);
       if (!batch.empty()) {
         stats_.t_chain += seconds_since(tc0);
         const auto ts0 = Clock::now();
@@ -784,14 +815,18 @@ std::pair<std::string, std::vector<std::vector<double>>> OMPLPlanner::plan(
               if (sp.equal(c, x.data())) continue;
             }
             append_grow(sp, ft_start, c, x.data(), spec_states);
+            // iteration i+1 connects `tree` (with this iteration's new node)
+            // towards x if that extension is valid
+            if (j == 1 && c == cand.front() && spec_states.size() < kSpecCap * (size_t)d)
+              spec_chain(tree, tree_is_start, target.data(), x.data(), spec_states);
           }
         }
         const size_t spec_off = batch.size() / (size_t)d;
         need(spec_states, 0, spec_states.size() / (size_t)d);
         stats_.t_spec += seconds_since(ts0);
+        (void)spec_off;
         check(batch, valid);
-        for (size_t i = 0; i < chain_off; ++i) vcache.put(batch.data() + i * d, valid[i]);
-        for (size_t i = spec_off; i < valid.size(); ++i) vcache.put(batch.data() + i * d, valid[i]);
+        for (size_t i = 0; i < valid.size(); ++i) vcache.put(batch.data() + i * d, valid[i]);
       }
       known(ext_states, 0, n_ext, ext_ok);
     }
@@ -806,7 +841,9 @@ std::pair<std::string, std::vector<std::vector<double>>> OMPLPlanner::plan(
     std::vector<int> node(chain.size(), -1);
     for (size_t k = 0; k < chain.size(); ++k) {
       const Step& s = chain[k];
-      if (!all_valid(valid, chain_off + s.a, chain_off + s.b)) {
+      bool ok_k = true;
+      for (size_t i = s.a; i < s.b && ok_k; ++i) ok_k = vcache.find(chain_states.data() + i * d) == 1;
+      if (!ok_k) {
         gsc = TRAPPED;
         break;
       }
