@@ -2498,6 +2498,8 @@ struct mpg_world {
   uint8_t* h_hits = nullptr;   // pinned coherent host-mapped, [n_pairs * small cap]
   uint8_t* d_hits = nullptr;   // device alias of h_hits
   double* d_qs = nullptr;      // device input of the latency path
+  double* d_qmap = nullptr;    // h_q as the device sees it (zero-copy input)
+  bool small_zero_copy = true; // MPG_SMALL_ZEROCOPY=0: stage through d_qs
   size_t small_cap = 0;
 };
 
@@ -3348,6 +3350,7 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
   // bound the candidate lists to 1 GiB: cap * n_pairs * 4 B
   w->max_chunk = std::max<long long>(4096, std::min<long long>(1 << 20, (1ll << 28) / std::max(d->n_pairs, 1)));
   if (const char* e = std::getenv("MPG_SMALL_BATCH_MAX")) w->small_max = std::atoll(e);
+  if (const char* e = std::getenv("MPG_SMALL_ZEROCOPY")) w->small_zero_copy = std::atoi(e) != 0;
   if (const char* e = std::getenv("MPG_OVERLAP_MIN")) w->overlap_min = std::atoll(e);
   if (const char* e = std::getenv("MPG_OVERLAP_PARTS")) w->overlap_parts = std::atoi(e);
   *out = w;
@@ -3432,7 +3435,9 @@ int ensure_small(mpg_world* w, size_t ncfg, size_t row) {
   w->d_qs = nullptr;
   w->small_cap = 0;
   const size_t P = (size_t)std::max(w->dw.n_pairs, 1);
-  HIP_TRY(hipHostMalloc((void**)&w->h_q, sizeof(double) * ncfg * std::max<size_t>(row, 1), hipHostMallocDefault));
+  HIP_TRY(hipHostMalloc((void**)&w->h_q, sizeof(double) * ncfg * std::max<size_t>(row, 1),
+                        hipHostMallocMapped | hipHostMallocCoherent));
+  HIP_TRY(hipHostGetDevicePointer((void**)&w->d_qmap, w->h_q, 0));
   HIP_TRY(hipHostMalloc((void**)&w->h_hits, P * ncfg, hipHostMallocMapped | hipHostMallocCoherent));
   HIP_TRY(hipHostGetDevicePointer((void**)&w->d_hits, w->h_hits, 0));
   HIP_TRY(hipMalloc(&w->d_qs, sizeof(double) * ncfg * std::max<size_t>(row, 1)));
@@ -3453,25 +3458,27 @@ int collide_small(mpg_world* w, const double* q, int64_t n, uint8_t* flags, uint
   std::memset(flags, 0, (size_t)n);
   if (pair_mask) std::memset(pair_mask, 0, sizeof(uint32_t) * (size_t)n * W);
   if (P == 0) return MPG_OK;
-  if (row) {
+  const double* qin = w->small_zero_copy ? w->d_qmap : w->d_qs;
+  if (row) {  // zero-copy: the kernel reads the pinned rows directly, no copy launch
     std::memcpy(w->h_q, q, sizeof(double) * (size_t)n * row);
-    HIP_TRY(hipMemcpyAsync(w->d_qs, w->h_q, sizeof(double) * (size_t)n * row, hipMemcpyHostToDevice, s));
+    if (!w->small_zero_copy)
+      HIP_TRY(hipMemcpyAsync(w->d_qs, w->h_q, sizeof(double) * (size_t)n * row, hipMemcpyHostToDevice, s));
   }
   const int n_tiles = (int)((n + 63) / 64);
   const long long waves = (long long)P * n_tiles;
   StageTimer t_small(w, s, MPG_STAGE_NARROW);
   if (w->prof) w->prof_cfg += n;
   hipLaunchKernelGGL((small_kernel<FROM_POSES, CLS_CLOSED>), dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s,
-                     w->dw, w->d_qs, (long long)n, n_tiles, w->d_hits);
+                     w->dw, qin, (long long)n, n_tiles, w->d_hits);
   HIP_TRY(hipGetLastError());
   if (w->any_octree) {
     hipLaunchKernelGGL((small_kernel<FROM_POSES, CLS_OCTREE>), dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s,
-                       w->dw, w->d_qs, (long long)n, n_tiles, w->d_hits);
+                       w->dw, qin, (long long)n, n_tiles, w->d_hits);
     HIP_TRY(hipGetLastError());
   }
   if (w->any_mesh) {
     hipLaunchKernelGGL((small_kernel<FROM_POSES, CLS_MESH>), dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s,
-                       w->dw, w->d_qs, (long long)n, n_tiles, w->d_hits);
+                       w->dw, qin, (long long)n, n_tiles, w->d_hits);
     HIP_TRY(hipGetLastError());
   }
   t_small.stop();
