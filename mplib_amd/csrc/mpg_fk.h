@@ -23,7 +23,7 @@ enum { S_ROT = 0, S_ROTINV = 4, S_POS = 8, S_OBBC = 11, S_R = 14, S_STRIDE = 23 
 struct DevWorld {
   int nj, dof, n_links, n_geoms, n_moving, n_static, n_pairs, W;
   double mpr_tol;
-  int debug_mode;  // diagnostics only: 1 = broad-phase records only, 2 = no SAT stage, 3 = no MPR, 5 / 6 = no mesh-mesh / mesh-shape walks
+  int debug_mode;  // diagnostics only: 1 = broad-phase records only, 2 = no SAT stage, 3 = no MPR (latency path: no narrow test), 5 / 6 = no mesh-mesh / mesh-shape walks, 7 = latency path: FK + sphere test only
   unsigned long long* stats;  // diagnostics only (MPG_STATS=1), else NULL
   cptr<int> joint_type;      // [nj]
   cptr<int> joint_parent;    // [nj]

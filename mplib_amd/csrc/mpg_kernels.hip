@@ -1733,9 +1733,27 @@ __global__ __launch_bounds__(256) MPG_NARROW_WAVES void narrow_kernel(DevWorld w
 // ---------------------------------------------------------------------------
 constexpr double kSmallMargin = 1e-4;
 
+// the latency path's joint sin/cos: one lane per (configuration, move-group
+// dof), shared by every pair's wave of the following small_kernel
+__global__ __launch_bounds__(256) void small_sincos_kernel(DevWorld w, const double* __restrict__ in, long long n,
+                                                          double* __restrict__ sc) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n * w.dof) return;
+  const long long r = i / w.dof;
+  const int src = (int)(i - r * w.dof);
+  for (int j = 0; j < w.nj; ++j) {
+    if (w.joint_q_source[j] != src || !joint_is_revolute(w.joint_type[j])) continue;
+    double sv, cv;
+    mpg_sincos(in[r * w.dof + src], &sv, &cv);
+    sc[(r * w.dof + src) * 2] = sv;
+    sc[(r * w.dof + src) * 2 + 1] = cv;
+    return;
+  }
+}
+
 template <bool FROM_POSES, int CLS>
 __global__ __launch_bounds__(256) void small_kernel(DevWorld w, const double* __restrict__ in, long long n, int n_tiles,
-                                                   uint8_t* __restrict__ hits) {
+                                                   uint8_t* __restrict__ hits, const double* __restrict__ sc) {
   const cptr<double> HV = w.hull;
   const uint32_t lane = lane_id();
   const int wave = __builtin_amdgcn_readfirstlane((int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6));
@@ -1750,8 +1768,8 @@ __global__ __launch_bounds__(256) void small_kernel(DevWorld w, const double* __
   const bool am = a < w.n_moving, bm = b < w.n_moving;
   const int cf = w.pair_cf[p];
   if (!w.pair_allowed[p]) {  // ACM-allowed pairs are never reported (filterCollisions)
-    const SE3 TA = am ? moving_tf<FROM_POSES, false>(w, in, nullptr, c, a) : load_se3(w.static_T + 12 * (a - w.n_moving));
-    const SE3 TB = bm ? moving_tf<FROM_POSES, false>(w, in, nullptr, c, b) : load_se3(w.static_T + 12 * (b - w.n_moving));
+    const SE3 TA = am ? moving_tf<FROM_POSES>(w, in, sc, c, a) : load_se3(w.static_T + 12 * (a - w.n_moving));
+    const SE3 TB = bm ? moving_tf<FROM_POSES>(w, in, sc, c, b) : load_se3(w.static_T + 12 * (b - w.n_moving));
     const int ga = am ? w.moving_geom[a] : w.static_geom[a - w.n_moving];
     const int gb = bm ? w.moving_geom[b] : w.static_geom[b - w.n_moving];
     const cptr<double> ra = w.geom_rec + G_STRIDE * ga, rb = w.geom_rec + G_STRIDE * gb;
@@ -1763,7 +1781,7 @@ __global__ __launch_bounds__(256) void small_kernel(DevWorld w, const double* __
       d2 += (ci - cj) * (ci - cj);
     }
     const double rr = ra[G_RADIUS] + rb[G_RADIUS] + kSmallMargin;
-    const bool near = live && d2 <= rr * rr;
+    const bool near = live && d2 <= rr * rr && w.debug_mode != 3 && !(w.debug_mode == 7 && d2 >= 0.0);
     if (CLS != CLS_CLOSED) {
       hit = (walk_wave_eval<CLS>(w, HV, ga, TA, gb, TB, near) >> lane) & 1ull;
     } else if (cf != CF_NONE) {
@@ -2499,6 +2517,7 @@ struct mpg_world {
   uint8_t* d_hits = nullptr;   // device alias of h_hits
   double* d_qs = nullptr;      // device input of the latency path
   double* d_qmap = nullptr;    // h_q as the device sees it (zero-copy input)
+  double* d_ssc = nullptr;     // latency path joint (sin, cos) [small cap * dof * 2]
   bool small_zero_copy = true; // MPG_SMALL_ZEROCOPY=0: stage through d_qs
   size_t small_cap = 0;
 };
@@ -3375,6 +3394,7 @@ int mpg_world_destroy(mpg_world* w) {
   if (w->h_q) hipHostFree(w->h_q);
   if (w->h_hits) hipHostFree(w->h_hits);
   hipFree(w->d_qs);
+  if (w->d_ssc) hipFree(w->d_ssc);
   if (w->side) hipStreamDestroy(w->side);
   if (w->ev_fork) hipEventDestroy(w->ev_fork);
   if (w->ev_join) hipEventDestroy(w->ev_join);
@@ -3430,6 +3450,8 @@ int ensure_small(mpg_world* w, size_t ncfg, size_t row) {
   if (w->h_q) hipHostFree(w->h_q);
   if (w->h_hits) hipHostFree(w->h_hits);
   if (w->d_qs) hipFree(w->d_qs);
+  if (w->d_ssc) hipFree(w->d_ssc);
+  w->d_ssc = nullptr;
   w->h_q = nullptr;
   w->h_hits = nullptr;
   w->d_qs = nullptr;
@@ -3441,6 +3463,7 @@ int ensure_small(mpg_world* w, size_t ncfg, size_t row) {
   HIP_TRY(hipHostMalloc((void**)&w->h_hits, P * ncfg, hipHostMallocMapped | hipHostMallocCoherent));
   HIP_TRY(hipHostGetDevicePointer((void**)&w->d_hits, w->h_hits, 0));
   HIP_TRY(hipMalloc(&w->d_qs, sizeof(double) * ncfg * std::max<size_t>(row, 1)));
+  HIP_TRY(hipMalloc(&w->d_ssc, sizeof(double) * 2 * ncfg * std::max<int>(w->dw.dof, 1)));
   w->small_cap = ncfg;
   return MPG_OK;
 }
@@ -3468,17 +3491,23 @@ int collide_small(mpg_world* w, const double* q, int64_t n, uint8_t* flags, uint
   const long long waves = (long long)P * n_tiles;
   StageTimer t_small(w, s, MPG_STAGE_NARROW);
   if (w->prof) w->prof_cfg += n;
+  if (!FROM_POSES && w->dw.dof > 0) {
+    const long long nt = n * w->dw.dof;
+    hipLaunchKernelGGL(small_sincos_kernel, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, s, w->dw, qin,
+                       (long long)n, w->d_ssc);
+    HIP_TRY(hipGetLastError());
+  }
   hipLaunchKernelGGL((small_kernel<FROM_POSES, CLS_CLOSED>), dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s,
-                     w->dw, qin, (long long)n, n_tiles, w->d_hits);
+                     w->dw, qin, (long long)n, n_tiles, w->d_hits, w->d_ssc);
   HIP_TRY(hipGetLastError());
   if (w->any_octree) {
     hipLaunchKernelGGL((small_kernel<FROM_POSES, CLS_OCTREE>), dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s,
-                       w->dw, qin, (long long)n, n_tiles, w->d_hits);
+                       w->dw, qin, (long long)n, n_tiles, w->d_hits, w->d_ssc);
     HIP_TRY(hipGetLastError());
   }
   if (w->any_mesh) {
     hipLaunchKernelGGL((small_kernel<FROM_POSES, CLS_MESH>), dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s,
-                       w->dw, qin, (long long)n, n_tiles, w->d_hits);
+                       w->dw, qin, (long long)n, n_tiles, w->d_hits, w->d_ssc);
     HIP_TRY(hipGetLastError());
   }
   t_small.stop();
