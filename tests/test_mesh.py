@@ -248,3 +248,25 @@ def test_mesh_world_unsupported_queries():
         w.self_distance()
     with pytest.raises(NotImplementedError):
         w.collide(pymp.fcl.CollisionRequest(enable_contact=True))
+
+
+@pytest.mark.gpu
+def test_planner_on_mesh_robot_matches_oracle_checker():
+    """RRTConnect on the Panda with BVH mesh links: the device checker
+    (latency path, mesh walk) gives the same path as the oracle's mesh
+    restatement used as the checker."""
+    ob = Wd.oracle_world(3, convex=False)
+    w, _ = scenes.world(3, convex=False)
+    dev = pymp.ompl.OMPLPlanner(w)
+    ref = pymp.ompl.OMPLPlanner(scenes.world(3, convex=False)[0],
+                                state_validity_checker=lambda s: ob.collide_batch(s)[0] == 0)
+    start = np.array(scenes.PLAN_START)
+    goal = np.array(scenes.PLAN_GOALS["near"])
+    pymp.set_global_seed(3)
+    s1, p1 = dev.plan(start, [goal], range=0.1, time=60.0)
+    pymp.set_global_seed(3)
+    s2, p2 = ref.plan(start, [goal], range=0.1, time=60.0)
+    assert s1 == s2 == "Exact solution"
+    assert np.array_equal(p1, p2)
+    body = p1[1:] if ob.collide_batch(start[None])[0][0] else p1  # an invalid start is resampled and prefixed
+    assert (ob.collide_batch(body)[0] == 0).all()
