@@ -21,7 +21,20 @@ OUT = os.path.join(ROOT, "tests", "golden")
 os.makedirs(OUT, exist_ok=True)
 
 
+def vectors(cfg, n, name):
+    ow = Wd.oracle_world(cfg)
+    q = Wd.sample_q(ow.art, n, Wd.CFG_SEED[cfg])
+    fl, mk = ow.collide_batch(q, nthreads=8)
+    np.savez_compressed(os.path.join(OUT, name + ".npz"), q=q, flags=fl, masks=mk,
+                        pairs=np.array([list(p) for p in ow.pair_names()]))
+    print(name, "collision rate", fl.mean())
+
+
 def main():
+    if "--only" in sys.argv:  # one fixture, e.g. --only 7 panda_mesh_1024
+        k = sys.argv.index("--only")
+        vectors(int(sys.argv[k + 1]), 1024, sys.argv[k + 2])
+        return
     ow2 = Wd.oracle_world(2)
     art = ow2.art
     # model facts + pair table
@@ -42,13 +55,9 @@ def main():
     with open(os.path.join(OUT, "kat.json"), "w") as fh:
         json.dump(kat, fh, indent=1)
     # per-config vectors
-    for cfg, n, name in [(2, 4096, "panda_self_4096"), (3, 4096, "panda_boxes_4096"), (4, 1024, "panda_convex_1024")]:
-        ow = Wd.oracle_world(cfg)
-        q = Wd.sample_q(ow.art, n, Wd.CFG_SEED[cfg])
-        fl, mk = ow.collide_batch(q, nthreads=8)
-        np.savez_compressed(os.path.join(OUT, name + ".npz"), q=q, flags=fl, masks=mk,
-                            pairs=np.array([list(p) for p in ow.pair_names()]))
-        print(name, "collision rate", fl.mean())
+    for cfg, n, name in [(2, 4096, "panda_self_4096"), (3, 4096, "panda_boxes_4096"), (4, 1024, "panda_convex_1024"),
+                         (7, 1024, "panda_mesh_1024")]:
+        vectors(cfg, n, name)
     q = Wd.sample_q(art, 64, 7)
     poses, objT = ow2.fk_batch(q)
     np.savez_compressed(os.path.join(OUT, "panda_fk_64.npz"), q=q, link_pose=poses, obj_T=objT)

@@ -54,7 +54,8 @@ def test_device_sincos_matches_libm():
     assert int((s != rs).sum()) == 0 and int((c != rc).sum()) == 0
 
 
-@pytest.mark.parametrize("name,cfg", [("panda_self_4096", 2), ("panda_boxes_4096", 3), ("panda_convex_1024", 4)])
+@pytest.mark.parametrize("name,cfg", [("panda_self_4096", 2), ("panda_boxes_4096", 3), ("panda_convex_1024", 4),
+                                      ("panda_mesh_1024", 7)])
 def test_capi_matches_golden(golden_dir, name, cfg):
     g = np.load(os.path.join(golden_dir, name + ".npz"))
     f, m = dw(cfg).collide_batch(g["q"])
@@ -94,7 +95,8 @@ def test_device_pointer_path_matches_host_path():
 
 
 # ----------------------------------------------------------------- product path
-@pytest.mark.parametrize("cfg,name", [(2, "panda_self_4096"), (3, "panda_boxes_4096"), (4, "panda_convex_1024")])
+@pytest.mark.parametrize("cfg,name", [(2, "panda_self_4096"), (3, "panda_boxes_4096"), (4, "panda_convex_1024"),
+                                      (7, "panda_mesh_1024")])
 def test_product_world_matches_golden(golden_dir, cfg, name):
     g = np.load(os.path.join(golden_dir, name + ".npz"))
     w, _ = scenes.world(cfg)

@@ -47,7 +47,8 @@ def test_detect_collision_known_answers(ow2):
     assert len(ow2.decode(m[1])) > 0
 
 
-@pytest.mark.parametrize("name,cfg", [("panda_self_4096", 2), ("panda_boxes_4096", 3), ("panda_convex_1024", 4)])
+@pytest.mark.parametrize("name,cfg", [("panda_self_4096", 2), ("panda_boxes_4096", 3), ("panda_convex_1024", 4),
+                                      ("panda_mesh_1024", 7)])
 def test_oracle_reproduces_golden(golden_dir, name, cfg):
     g = np.load(os.path.join(golden_dir, name + ".npz"))
     ow = Wd.oracle_world(cfg)

@@ -117,7 +117,7 @@ def sample_q(art: M.Articulation, n: int, seed: int) -> np.ndarray:
     return np.random.default_rng(seed).uniform(lim[:, 0], lim[:, 1], size=(n, 7))
 
 
-CFG_SEED = {2: 0, 3: 1, 4: 2}
+CFG_SEED = {2: 0, 3: 1, 4: 2, 7: 7}
 CFG_N = {2: 1 << 16, 3: 1 << 20, 4: 1 << 22}
 
 
