@@ -98,3 +98,23 @@ def test_product_pair_table_has_the_cloud():
     w, _ = scenes.cloud_world("blue")
     ow = Wd.oracle_cloud_world("blue")
     assert [(i[3], i[4]) for i in w.get_collision_pair_info()] == ow.pair_names()
+
+
+@pytest.mark.gpu
+def test_planner_on_point_cloud_world_matches_oracle_checker():
+    """RRTConnect over the detect_collision.py floor cloud: the device checker
+    (latency path, octree walk) gives the oracle checker's path."""
+    ob = Wd.oracle_cloud_world("floor")
+    dev = pymp.ompl.OMPLPlanner(scenes.cloud_world("floor")[0])
+    ref = pymp.ompl.OMPLPlanner(scenes.cloud_world("floor")[0],
+                                state_validity_checker=lambda s: ob.collide_batch(s)[0] == 0)
+    start = np.array(scenes.PLAN_START)
+    goal = np.array(scenes.PLAN_GOALS["far"])
+    pymp.set_global_seed(2)
+    s1, p1 = dev.plan(start, [goal], range=0.1, time=60.0)
+    pymp.set_global_seed(2)
+    s2, p2 = ref.plan(start, [goal], range=0.1, time=60.0)
+    assert s1 == s2 == "Exact solution"
+    assert np.array_equal(p1, p2)
+    body = p1[1:] if ob.collide_batch(start[None])[0][0] else p1
+    assert (ob.collide_batch(body)[0] == 0).all()
