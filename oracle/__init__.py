@@ -58,6 +58,58 @@ def lib():
     return _lib
 
 
+# Oracle variants (DESIGN.md "Oracle variants"): the same restatement built with
+# one open arithmetic choice switched, to count how many flags / pair bits each
+# choice can change.  Test infrastructure like the rest of this package.
+VARIANTS = {
+    "ccd_float": ["-DORC_CCD_FLOAT"],            # libccd v2.1 default CMake build (single precision)
+    "fcl_walk": ["-DORC_FCL_WALK"],              # FCL 0.7.0 Convex::findExtremeVertex neighbour walk
+    "pin_cross": ["-DORC_PIN_REVOLUTE_CROSS"],   # column-wise SE3 x TransformRevolute with a cross product
+    "eigen_slice": ["-DORC_EIGEN_ORDER=1"],      # Eigen 3.4 SSE2 slice-vectorised 3x3 products
+    "eigen_tree": ["-DORC_EIGEN_ORDER=2"],       # Eigen redux-tree order for every coefficient
+}
+_variant_libs: Dict[str, ctypes.CDLL] = {}
+
+
+def variant_lib(name: str):
+    """Build (once) and load oracle/build/variants/liboracle_<name>.so.
+    ``name`` is a '+'-joined list of VARIANTS keys."""
+    if name not in _variant_libs:
+        flags = []
+        for part in name.split("+"):
+            flags += VARIANTS[part]
+        src = os.path.join(_HERE, "collide_oracle.c")
+        out = os.path.join(_HERE, "build", "variants", f"liboracle_{name}.so")
+        os.makedirs(os.path.dirname(out), exist_ok=True)
+        if not os.path.exists(out) or os.path.getmtime(out) < os.path.getmtime(src):
+            subprocess.check_call(["gcc", "-O2", "-ffp-contract=off", "-fno-fast-math", "-fPIC", "-std=c99",
+                                   "-D_POSIX_C_SOURCE=200809L", *flags, "-shared", "-o", out, src, "-lm", "-lpthread"])
+        L = ctypes.CDLL(out)
+        L.orc_collide_batch.restype = ctypes.c_int
+        L.orc_fk_batch.restype = ctypes.c_int
+        _variant_libs[name] = L
+    return _variant_libs[name]
+
+
+def fcl_convex_neighbors(nv: int, faces) -> List[int]:
+    """FCL 0.7.0 ``Convex::FindVertexNeighbors`` encoding [ext]: entry i
+    (i < nv) is the offset of vertex i's record = [count, sorted neighbours...];
+    each face contributes its consecutive edges (and the closing edge)."""
+    nb = [set() for _ in range(nv)]
+    for f in faces:
+        prev = f[-1]
+        for v in f:
+            nb[v].add(prev)
+            nb[prev].add(v)
+            prev = v
+    out = [0] * nv
+    for i in range(nv):
+        out[i] = len(out)
+        out.append(len(nb[i]))
+        out.extend(sorted(nb[i]))
+    return out
+
+
 def tri_tri(P, Q) -> bool:
     """FCL Intersect::intersect_Triangle on two triangles ([3, 3] each)."""
     a = np.ascontiguousarray(P, dtype=np.float64).reshape(9)
@@ -96,6 +148,7 @@ class _World(ctypes.Structure):
         ("pa_kind", _IP), ("pa_idx", _IP), ("pb_kind", _IP), ("pb_idx", _IP), ("p_allowed", _IP),
         ("oct_leaf", _DP),
         ("mesh_tri", _IP),
+        ("conv_nbr", _IP),
     ]
 
 
@@ -154,6 +207,7 @@ class OracleWorld:
         gtype, gvstart, gnv, gparam, ginterior, verts = [], [], [], [], [], []
         leaves = []
         tris = []
+        nbr_all: List[int] = []
         ntris = 0
         nverts = 0
         nleaves = 0
@@ -164,7 +218,8 @@ class OracleWorld:
                 gnv.append(len(g.vertices))
                 nverts += len(g.vertices)
                 verts.append(np.asarray(g.vertices, dtype=np.float64).reshape(-1))
-                gparam += [0.0] * 4
+                gparam += [float(len(nbr_all)), 0.0, 0.0, 0.0]
+                nbr_all += fcl_convex_neighbors(len(g.vertices), g.faces)
                 ginterior += g.interior
             elif isinstance(g, M.MeshGeom):
                 gtype.append(M.GEOM_MESH)
@@ -291,18 +346,21 @@ class OracleWorld:
         w.p_allowed = ia(allowed)
         w.oct_leaf = da(np.concatenate(leaves) if leaves else [])
         w.mesh_tri = ia(np.concatenate(tris) if tris else [])
+        w.conv_nbr = ia(nbr_all)
         self._w = w
         self.geoms = geoms
         self.dof = len(mg)
 
     # ------------------------------------------------------------------
-    def collide_batch(self, q: np.ndarray, nthreads: int = 1, want_stats: bool = False):
+    def collide_batch(self, q: np.ndarray, nthreads: int = 1, want_stats: bool = False, variant: str = ""):
+        """flags[n], masks[n, W].  ``variant`` names an oracle-variant build
+        (``variant_lib``) used only by the variant study."""
         q = np.ascontiguousarray(q, dtype=np.float64).reshape(-1, self.dof)
         n = q.shape[0]
         flags = np.zeros(n, dtype=np.uint8)
         masks = np.zeros((n, self.W), dtype=np.uint32)
         st = Stats()
-        rc = lib().orc_collide_batch(ctypes.byref(self._w), q.ctypes.data_as(_DP), ctypes.c_long(n),
+        rc = (variant_lib(variant) if variant else lib()).orc_collide_batch(ctypes.byref(self._w), q.ctypes.data_as(_DP), ctypes.c_long(n),
                                      flags.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)),
                                      masks.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)),
                                      ctypes.c_int(self.W), ctypes.c_int(nthreads), ctypes.byref(st))

@@ -40,9 +40,28 @@
 #include <stdlib.h>
 #include <string.h>
 
-typedef double real;
+typedef double real; /* Eigen / pinocchio / FCL scalar (S = double) */
+
+/* libccd 2.1 scalar (ccd/config.h, ccd/compiler.h).  The default build is
+ * double (CCD_DOUBLE).  ORC_CCD_FLOAT builds the single-precision variant a
+ * bare `cmake ..` of libccd v2.1 produces (ENABLE_DOUBLE_PRECISION OFF), as
+ * /root/reference docker/Dockerfile:16-20 does -- see DESIGN.md "Oracle
+ * variants" for what it changes. */
+#ifdef ORC_CCD_FLOAT
+typedef float ccd_real_t;
+#define CCD_EPS FLT_EPSILON
+#define CCD_REAL_MAX FLT_MAX
+#define CCD_SQRT(x) sqrtf(x)
+#define CCD_FABS(x) fabsf(x)
+#else
+typedef double ccd_real_t;
 #define CCD_EPS DBL_EPSILON
 #define CCD_REAL_MAX DBL_MAX
+#define CCD_SQRT(x) sqrt(x)
+#define CCD_FABS(x) fabs(x)
+#endif
+#define CCD_REAL(x) ((ccd_real_t)(x))
+#define CCD_ONE CCD_REAL(1.)
 
 /* ---------------------------------------------------------------- world */
 enum { GEOM_CONVEX = 0, GEOM_BOX = 1, GEOM_SPHERE = 2, GEOM_CAPSULE = 3, GEOM_CYLINDER = 4, GEOM_OCTREE = 5, GEOM_MESH = 6,
@@ -94,6 +113,9 @@ typedef struct {
      * the vertices, geom_param = (first triangle, triangle count); triangles
      * [*3] index the mesh's own vertices */
     const int *mesh_tri;
+    /* convex hulls: FCL 0.7.0 Convex::neighbors_ encoding per geometry
+     * (geom_param[0] = offset); NULL when not supplied */
+    const int *conv_nbr;
 } orc_world;
 
 typedef struct {
@@ -104,11 +126,33 @@ typedef struct {
 } orc_stats;
 
 /* ----------------------------------------------------------- SE3 / Eigen */
+/* Three-term inner product of row i of a 3x3 lazy product.  Default
+ * (ORC_EIGEN_ORDER 0): ((x0 + x1) + x2) for every row.  Variants for the
+ * oracle-variant study (DESIGN.md "Oracle variants"):
+ *   1: Eigen 3.4 SSE2 slice-vectorised assignment -- rows 0-1 as one Packet2d
+ *      accumulated in k order, row 2 through coeff() = redux tree
+ *      x0 + (x1 + x2);
+ *   2: no vectorisation -- every coefficient through the redux tree. */
+#ifndef ORC_EIGEN_ORDER
+#define ORC_EIGEN_ORDER 0
+#endif
+static inline real edot3(int row, real x0, real x1, real x2) {
+#if ORC_EIGEN_ORDER == 0
+    (void)row;
+    return (x0 + x1) + x2;
+#elif ORC_EIGEN_ORDER == 1
+    return row < 2 ? (x0 + x1) + x2 : x0 + (x1 + x2);
+#else
+    (void)row;
+    return x0 + (x1 + x2);
+#endif
+}
+
 static void mat3_mul(const real *a, const real *b, real *out) {
     real r[9];
     for (int i = 0; i < 3; ++i)
         for (int j = 0; j < 3; ++j)
-            r[3 * i + j] = (a[3 * i] * b[j] + a[3 * i + 1] * b[3 + j]) + a[3 * i + 2] * b[6 + j];
+            r[3 * i + j] = edot3(i, a[3 * i] * b[j], a[3 * i + 1] * b[3 + j], a[3 * i + 2] * b[6 + j]);
     memcpy(out, r, sizeof r);
 }
 
@@ -117,7 +161,7 @@ static void se3_mul(const real *A, const real *B, real *C) {
     real R[9], p[3];
     mat3_mul(A, B, R);
     for (int i = 0; i < 3; ++i)
-        p[i] = ((A[3 * i] * B[9] + A[3 * i + 1] * B[10]) + A[3 * i + 2] * B[11]) + A[9 + i];
+        p[i] = edot3(i, A[3 * i] * B[9], A[3 * i + 1] * B[10], A[3 * i + 2] * B[11]) + A[9 + i];
     memcpy(C, R, sizeof R);
     memcpy(C + 9, p, sizeof p);
 }
@@ -211,6 +255,31 @@ static void joint_motion(int type, const real *axis, const real *qj, real *M) {
     }
 }
 
+#ifdef ORC_PIN_REVOLUTE_CROSS
+/* Variant (oracle-variant study): jointPlacement * TransformRevolute computed
+ * column-wise the way a specialised SE3 x TransformRevolute action would --
+ * the two rotated columns as c*P_a + s*P_b, the third untouched, and the
+ * remaining one as a cross product of the other two; translation = P's. */
+static void ecross(const real *a, const real *b, real *o) {
+    o[0] = a[1] * b[2] - a[2] * b[1];
+    o[1] = a[2] * b[0] - a[0] * b[2];
+    o[2] = a[0] * b[1] - a[1] * b[0];
+}
+static void revolute_cross(int type, const real *P, real q, real *L) {
+    real s, c, col[3][3], pc[3][3];
+    sincos(q, &s, &c);
+    for (int k = 0; k < 3; ++k)
+        for (int i = 0; i < 3; ++i) pc[k][i] = P[3 * i + k];
+    int a = type == JT_RX ? 0 : type == JT_RY ? 1 : 2; /* the axis column (unchanged) */
+    int u = (a + 1) % 3, v = (a + 2) % 3;              /* rotated: col_u = c P_u + s P_v */
+    for (int i = 0; i < 3; ++i) { col[a][i] = pc[a][i]; col[u][i] = c * pc[u][i] + s * pc[v][i]; }
+    ecross(col[a], col[u], col[v]);
+    for (int k = 0; k < 3; ++k)
+        for (int i = 0; i < 3; ++i) L[3 * i + k] = col[k][i];
+    L[9] = P[9]; L[10] = P[10]; L[11] = P[11];
+}
+#endif
+
 /* full user qpos from move-group dof values (ArticulatedModel::setQpos, full=false) */
 static void user_qpos(const orc_world *w, const real *q, real *qu) {
     memcpy(qu, w->qpos_template, (size_t)w->nq_user * sizeof(real));
@@ -247,8 +316,16 @@ static void fk_links(const orc_world *w, const real *q, real *oMi, real *link_T,
     se3_identity(oMi); /* oMi[0] = universe */
     for (int j = 1; j <= w->nj; ++j) {
         real M[12], li[12];
-        joint_motion(w->jtype[j - 1], w->jaxis + 3 * (j - 1), qp + w->jidx_q[j - 1], M);
-        se3_mul(w->jplace + 12 * (j - 1), M, li);
+        const int jt = w->jtype[j - 1];
+#ifdef ORC_PIN_REVOLUTE_CROSS
+        if (jt == JT_RX || jt == JT_RY || jt == JT_RZ)
+            revolute_cross(jt, w->jplace + 12 * (j - 1), qp[w->jidx_q[j - 1]], li);
+        else
+#endif
+        {
+            joint_motion(jt, w->jaxis + 3 * (j - 1), qp + w->jidx_q[j - 1], M);
+            se3_mul(w->jplace + 12 * (j - 1), M, li);
+        }
         int par = w->jparent[j - 1];
         if (par > 0)
             se3_mul(oMi + 12 * par, li, oMi + 12 * j);
@@ -271,20 +348,20 @@ static void fk_links(const orc_world *w, const real *q, real *oMi, real *link_T,
 }
 
 /* -------------------------------------------------------------- libccd */
-typedef struct { real v[3]; } ccd_vec3_t;
-typedef struct { real q[4]; } ccd_quat_t; /* x y z w */
+typedef struct { ccd_real_t v[3]; } ccd_vec3_t;
+typedef struct { ccd_real_t q[4]; } ccd_quat_t; /* x y z w */
 typedef struct { ccd_vec3_t v, v1, v2; } ccd_support_t;
 typedef struct { ccd_support_t ps[4]; int last; } ccd_simplex_t;
 
-static int ccdIsZero(real val) { return fabs(val) < CCD_EPS; }
-static int ccdEq(real _a, real _b) {
-    real ab = fabs(_a - _b);
-    if (fabs(ab) < CCD_EPS) return 1;
-    real a = fabs(_a), b = fabs(_b);
+static int ccdIsZero(ccd_real_t val) { return CCD_FABS(val) < CCD_EPS; }
+static int ccdEq(ccd_real_t _a, ccd_real_t _b) {
+    ccd_real_t ab = CCD_FABS(_a - _b);
+    if (CCD_FABS(ab) < CCD_EPS) return 1;
+    ccd_real_t a = CCD_FABS(_a), b = CCD_FABS(_b);
     if (b > a) return ab < CCD_EPS * b;
     return ab < CCD_EPS * a;
 }
-static void ccdVec3Set(ccd_vec3_t *v, real x, real y, real z) { v->v[0] = x; v->v[1] = y; v->v[2] = z; }
+static void ccdVec3Set(ccd_vec3_t *v, ccd_real_t x, ccd_real_t y, ccd_real_t z) { v->v[0] = x; v->v[1] = y; v->v[2] = z; }
 static void ccdVec3Copy(ccd_vec3_t *a, const ccd_vec3_t *b) { *a = *b; }
 static void ccdVec3Sub2(ccd_vec3_t *d, const ccd_vec3_t *v, const ccd_vec3_t *w) {
     d->v[0] = v->v[0] - w->v[0]; d->v[1] = v->v[1] - w->v[1]; d->v[2] = v->v[2] - w->v[2];
@@ -292,16 +369,16 @@ static void ccdVec3Sub2(ccd_vec3_t *d, const ccd_vec3_t *v, const ccd_vec3_t *w)
 static void ccdVec3Add(ccd_vec3_t *v, const ccd_vec3_t *w) {
     v->v[0] += w->v[0]; v->v[1] += w->v[1]; v->v[2] += w->v[2];
 }
-static void ccdVec3Scale(ccd_vec3_t *d, real k) { d->v[0] *= k; d->v[1] *= k; d->v[2] *= k; }
-static real ccdVec3Dot(const ccd_vec3_t *a, const ccd_vec3_t *b) {
-    real dot = a->v[0] * b->v[0];
+static void ccdVec3Scale(ccd_vec3_t *d, ccd_real_t k) { d->v[0] *= k; d->v[1] *= k; d->v[2] *= k; }
+static ccd_real_t ccdVec3Dot(const ccd_vec3_t *a, const ccd_vec3_t *b) {
+    ccd_real_t dot = a->v[0] * b->v[0];
     dot += a->v[1] * b->v[1];
     dot += a->v[2] * b->v[2];
     return dot;
 }
-static real ccdVec3Len2(const ccd_vec3_t *v) { return ccdVec3Dot(v, v); }
+static ccd_real_t ccdVec3Len2(const ccd_vec3_t *v) { return ccdVec3Dot(v, v); }
 static void ccdVec3Normalize(ccd_vec3_t *d) {
-    real k = 1.0 / sqrt(ccdVec3Len2(d));
+    ccd_real_t k = CCD_ONE / CCD_SQRT(ccdVec3Len2(d));
     ccdVec3Scale(d, k);
 }
 static void ccdVec3Cross(ccd_vec3_t *d, const ccd_vec3_t *a, const ccd_vec3_t *b) {
@@ -313,24 +390,24 @@ static int ccdVec3Eq(const ccd_vec3_t *a, const ccd_vec3_t *b) {
     return ccdEq(a->v[0], b->v[0]) && ccdEq(a->v[1], b->v[1]) && ccdEq(a->v[2], b->v[2]);
 }
 static void ccdQuatRotVec(ccd_vec3_t *v, const ccd_quat_t *q) {
-    real vx = v->v[0], vy = v->v[1], vz = v->v[2];
-    real w = q->q[3], x = q->q[0], y = q->q[1], z = q->q[2];
-    real c1x = y * vz - z * vy + w * vx;
-    real c1y = z * vx - x * vz + w * vy;
-    real c1z = x * vy - y * vx + w * vz;
-    real c2x = y * c1z - z * c1y;
-    real c2y = z * c1x - x * c1z;
-    real c2z = x * c1y - y * c1x;
+    ccd_real_t vx = v->v[0], vy = v->v[1], vz = v->v[2];
+    ccd_real_t w = q->q[3], x = q->q[0], y = q->q[1], z = q->q[2];
+    ccd_real_t c1x = y * vz - z * vy + w * vx;
+    ccd_real_t c1y = z * vx - x * vz + w * vy;
+    ccd_real_t c1z = x * vy - y * vx + w * vz;
+    ccd_real_t c2x = y * c1z - z * c1y;
+    ccd_real_t c2y = z * c1x - x * c1z;
+    ccd_real_t c2z = x * c1y - y * c1x;
     ccdVec3Set(v, vx + 2 * c2x, vy + 2 * c2y, vz + 2 * c2z);
 }
 static int ccdQuatInvert2(ccd_quat_t *dest, const ccd_quat_t *src) {
     *dest = *src;
-    real len2 = dest->q[0] * dest->q[0];
+    ccd_real_t len2 = dest->q[0] * dest->q[0];
     len2 += dest->q[1] * dest->q[1];
     len2 += dest->q[2] * dest->q[2];
     len2 += dest->q[3] * dest->q[3];
     if (len2 < CCD_EPS) return -1;
-    len2 = 1.0 / len2;
+    len2 = CCD_ONE / len2;
     dest->q[0] = -dest->q[0] * len2;
     dest->q[1] = -dest->q[1] * len2;
     dest->q[2] = -dest->q[2] * len2;
@@ -345,18 +422,19 @@ typedef struct {
     ccd_vec3_t pos;
     ccd_quat_t rot, rot_inv;
     int type;
-    const real *verts; /* convex */
+    const real *verts; /* convex (FCL Vector3<double>) */
     int nv;
     const real *interior;
-    real dim[3];       /* box half sizes */
-    real radius, height; /* sphere / capsule / cylinder */
+    const int *nbr;    /* convex: FCL neighbors_ encoding (ORC_FCL_WALK variant) */
+    ccd_real_t dim[3];       /* box half sizes */
+    ccd_real_t radius, height; /* sphere / capsule / cylinder */
     ccd_vec3_t tp[3], tc; /* triangle (triCreateGJKObject): vertices, centroid */
     orc_stats *stats;
 } gjk_obj;
 
 /* shapeToGJK: Quaternion q(tf.linear()); pos = T; rot = (x,y,z,w); rot_inv */
 static void shape_to_gjk(const real *T, gjk_obj *o) {
-    real q[4];
+    real q[4]; /* Eigen Quaternion<double>, then ccdVec3Set / ccdQuatSet convert */
     mat_to_quat(T, q);
     ccdVec3Set(&o->pos, T[9], T[10], T[11]);
     o->rot.q[0] = q[1]; o->rot.q[1] = q[2]; o->rot.q[2] = q[3]; o->rot.q[3] = q[0];
@@ -369,10 +447,40 @@ static void support_convex(const gjk_obj *c, const ccd_vec3_t *dir_, ccd_vec3_t 
     ccdQuatRotVec(&dir, &c->rot_inv);
     /* Convex::findExtremeVertex: argmax of dir . vertex, first maximum wins */
     const real *p = c->verts;
-    real maxdot = -CCD_REAL_MAX;
+    const real dC[3] = {dir.v[0], dir.v[1], dir.v[2]}; /* Vector3<S> dir_C{S(dir.v[0]), ...} */
+    real maxdot = -DBL_MAX;
     int best = 0;
+#ifdef ORC_FCL_WALK
+    /* Variant: FCL 0.7.0 Convex::findExtremeVertex hill climb (vertex count >
+     * kMinVertCountForEdgeWalking = 32): start at vertex 0, scan the current
+     * vertex's sorted neighbour list (FindVertexNeighbors, std::set order),
+     * step to every unvisited neighbour with value >= the best so far. */
+    if (c->nbr && c->nv > 32 && c->nv <= 4096) {
+        unsigned char visited[4096];
+        memset(visited, 0, (size_t)c->nv);
+        maxdot = (dC[0] * p[0] + dC[1] * p[1]) + dC[2] * p[2];
+        visited[0] = 1;
+        int keep = 1;
+        while (keep) {
+            keep = 0;
+            const int start = c->nbr[best], cnt = c->nbr[start];
+            for (int k = start + 1; k <= start + cnt; ++k) {
+                const int vi = c->nbr[k];
+                if (visited[vi]) continue;
+                visited[vi] = 1;
+                real d = (dC[0] * p[3 * vi] + dC[1] * p[3 * vi + 1]) + dC[2] * p[3 * vi + 2];
+                if (d >= maxdot) { keep = 1; best = vi; maxdot = d; }
+            }
+        }
+        if (c->stats) c->stats->vertex_dots += c->nv;
+        ccdVec3Set(v, p[3 * best], p[3 * best + 1], p[3 * best + 2]);
+        ccdQuatRotVec(v, &c->rot);
+        ccdVec3Add(v, &c->pos);
+        return;
+    }
+#endif
     for (int i = 0; i < c->nv; ++i) {
-        real dot = (dir.v[0] * p[3 * i] + dir.v[1] * p[3 * i + 1]) + dir.v[2] * p[3 * i + 2];
+        real dot = (dC[0] * p[3 * i] + dC[1] * p[3 * i + 1]) + dC[2] * p[3 * i + 2];
         if (dot > maxdot) { maxdot = dot; best = i; }
     }
     if (c->stats) c->stats->vertex_dots += c->nv;
@@ -398,7 +506,7 @@ static void support_sphere(const gjk_obj *s, const ccd_vec3_t *dir_, ccd_vec3_t 
     ccdQuatRotVec(&dir, &s->rot_inv);
     ccdVec3Copy(v, &dir);
     ccdVec3Scale(v, s->radius);
-    ccdVec3Scale(v, 1.0 / sqrt(ccdVec3Len2(&dir)));
+    ccdVec3Scale(v, CCD_ONE / CCD_SQRT(ccdVec3Len2(&dir)));
     ccdQuatRotVec(v, &s->rot);
     ccdVec3Add(v, &s->pos);
 }
@@ -422,11 +530,11 @@ static void support_capsule(const gjk_obj *o, const ccd_vec3_t *dir_, ccd_vec3_t
 
 static void support_cylinder(const gjk_obj *c, const ccd_vec3_t *dir_, ccd_vec3_t *v) {
     ccd_vec3_t dir;
-    real zdist, rad;
+    ccd_real_t zdist, rad;
     ccdVec3Copy(&dir, dir_);
     ccdQuatRotVec(&dir, &c->rot_inv);
     zdist = dir.v[0] * dir.v[0] + dir.v[1] * dir.v[1];
-    zdist = sqrt(zdist);
+    zdist = CCD_SQRT(zdist);
     if (ccdIsZero(zdist))
         ccdVec3Set(v, 0.0, 0.0, (dir.v[2] > 0 ? 1.0 : -1.0) * c->height);
     else {
@@ -441,7 +549,7 @@ static void support_cylinder(const gjk_obj *c, const ccd_vec3_t *dir_, ccd_vec3_
  * maximum wins, then the vertex itself is transformed */
 static void support_triangle(const gjk_obj *t, const ccd_vec3_t *dir_, ccd_vec3_t *v) {
     ccd_vec3_t dir, p;
-    real maxdot = -CCD_REAL_MAX, dot;
+    ccd_real_t maxdot = -CCD_REAL_MAX, dot;
     ccdVec3Copy(&dir, dir_);
     ccdQuatRotVec(&dir, &t->rot_inv);
     for (int i = 0; i < 3; ++i) {
@@ -502,7 +610,7 @@ static void find_origin(const gjk_obj *o1, const gjk_obj *o2, ccd_support_t *cen
 
 static int discover_portal(const gjk_obj *o1, const gjk_obj *o2, ccd_simplex_t *portal) {
     ccd_vec3_t dir, va, vb;
-    real dot;
+    ccd_real_t dot;
     int cont;
     find_origin(o1, o2, SP(portal, 0));
     portal->last = 0;
@@ -580,29 +688,29 @@ static void portal_dir(const ccd_simplex_t *portal, ccd_vec3_t *dir) {
 }
 
 static int portal_encapsules_origin(const ccd_simplex_t *portal, const ccd_vec3_t *dir) {
-    real dot = ccdVec3Dot(dir, &portal->ps[1].v);
+    ccd_real_t dot = ccdVec3Dot(dir, &portal->ps[1].v);
     return ccdIsZero(dot) || dot > 0.0;
 }
 
 static int portal_reach_tolerance(const ccd_simplex_t *portal, const ccd_support_t *v4,
-                                  const ccd_vec3_t *dir, real tol) {
-    real dv1 = ccdVec3Dot(&portal->ps[1].v, dir);
-    real dv2 = ccdVec3Dot(&portal->ps[2].v, dir);
-    real dv3 = ccdVec3Dot(&portal->ps[3].v, dir);
-    real dv4 = ccdVec3Dot(&v4->v, dir);
-    real dot1 = dv4 - dv1, dot2 = dv4 - dv2, dot3 = dv4 - dv3;
+                                  const ccd_vec3_t *dir, ccd_real_t tol) {
+    ccd_real_t dv1 = ccdVec3Dot(&portal->ps[1].v, dir);
+    ccd_real_t dv2 = ccdVec3Dot(&portal->ps[2].v, dir);
+    ccd_real_t dv3 = ccdVec3Dot(&portal->ps[3].v, dir);
+    ccd_real_t dv4 = ccdVec3Dot(&v4->v, dir);
+    ccd_real_t dot1 = dv4 - dv1, dot2 = dv4 - dv2, dot3 = dv4 - dv3;
     dot1 = (dot1 < dot2) ? dot1 : dot2; /* CCD_FMIN */
     dot1 = (dot1 < dot3) ? dot1 : dot3;
     return ccdEq(dot1, tol) || dot1 < tol;
 }
 
 static int portal_can_encapsule_origin(const ccd_support_t *v4, const ccd_vec3_t *dir) {
-    real dot = ccdVec3Dot(&v4->v, dir);
+    ccd_real_t dot = ccdVec3Dot(&v4->v, dir);
     return ccdIsZero(dot) || dot > 0.0;
 }
 
 static void expand_portal(ccd_simplex_t *portal, const ccd_support_t *v4) {
-    real dot;
+    ccd_real_t dot;
     ccd_vec3_t v4v0;
     ccdVec3Cross(&v4v0, &v4->v, &portal->ps[0].v);
     dot = ccdVec3Dot(&portal->ps[1].v, &v4v0);
@@ -617,7 +725,7 @@ static void expand_portal(ccd_simplex_t *portal, const ccd_support_t *v4) {
     }
 }
 
-static int refine_portal(const gjk_obj *o1, const gjk_obj *o2, ccd_simplex_t *portal, real tol) {
+static int refine_portal(const gjk_obj *o1, const gjk_obj *o2, ccd_simplex_t *portal, ccd_real_t tol) {
     ccd_vec3_t dir;
     ccd_support_t v4;
     for (;;) {
@@ -632,7 +740,7 @@ static int refine_portal(const gjk_obj *o1, const gjk_obj *o2, ccd_simplex_t *po
 }
 
 /* ccdMPRIntersect */
-static int mpr_intersect(const gjk_obj *o1, const gjk_obj *o2, real tol) {
+static int mpr_intersect(const gjk_obj *o1, const gjk_obj *o2, ccd_real_t tol) {
     ccd_simplex_t portal;
     if (o1->stats) o1->stats->mpr_runs++;
     int res = discover_portal(o1, o2, &portal);
@@ -648,9 +756,9 @@ static int mpr_intersect(const gjk_obj *o1, const gjk_obj *o2, real tol) {
  * GJKCollide runs it for CollisionRequest(enable_contact=True):
  * max_iterations = 500 (GJKSolver_libccd::max_collision_iterations),
  * mpr_tolerance = gjk_tolerance.  dir points from object 1 to object 2. */
-static real point_segment_dist2(const ccd_vec3_t *P, const ccd_vec3_t *x0, const ccd_vec3_t *b, ccd_vec3_t *witness) {
+static ccd_real_t point_segment_dist2(const ccd_vec3_t *P, const ccd_vec3_t *x0, const ccd_vec3_t *b, ccd_vec3_t *witness) {
     ccd_vec3_t d, a;
-    real t, dist;
+    ccd_real_t t, dist;
     ccdVec3Sub2(&d, b, x0);
     ccdVec3Sub2(&a, x0, P);
     t = -1.0 * ccdVec3Dot(&a, &d);
@@ -670,10 +778,10 @@ static real point_segment_dist2(const ccd_vec3_t *P, const ccd_vec3_t *x0, const
     return dist;
 }
 
-static real point_tri_dist2(const ccd_vec3_t *P, const ccd_vec3_t *x0, const ccd_vec3_t *B, const ccd_vec3_t *C,
+static ccd_real_t point_tri_dist2(const ccd_vec3_t *P, const ccd_vec3_t *x0, const ccd_vec3_t *B, const ccd_vec3_t *C,
                             ccd_vec3_t *witness) {
     ccd_vec3_t d1, d2, a, witness2;
-    real u, v, w, p, q, r, d, s, t, dist, dist2;
+    ccd_real_t u, v, w, p, q, r, d, s, t, dist, dist2;
     ccdVec3Sub2(&d1, B, x0);
     ccdVec3Sub2(&d2, C, x0);
     ccdVec3Sub2(&a, x0, P);
@@ -711,7 +819,7 @@ static real point_tri_dist2(const ccd_vec3_t *P, const ccd_vec3_t *x0, const ccd
 
 static void find_pos(const ccd_simplex_t *portal, ccd_vec3_t *pos) {
     ccd_vec3_t dir, vec, p1, p2;
-    real b[4], sum, inv;
+    ccd_real_t b[4], sum, inv;
     portal_dir(portal, &dir);
     ccdVec3Cross(&vec, &portal->ps[1].v, &portal->ps[2].v);
     b[0] = ccdVec3Dot(&vec, &portal->ps[3].v);
@@ -732,7 +840,7 @@ static void find_pos(const ccd_simplex_t *portal, ccd_vec3_t *pos) {
         b[3] = ccdVec3Dot(&vec, &dir);
         sum = b[1] + b[2] + b[3];
     }
-    inv = 1.0 / sum;
+    inv = CCD_ONE / sum;
     ccdVec3Set(&p1, 0.0, 0.0, 0.0);
     ccdVec3Set(&p2, 0.0, 0.0, 0.0);
     for (int i = 0; i < 4; ++i) {
@@ -751,8 +859,9 @@ static void find_pos(const ccd_simplex_t *portal, ccd_vec3_t *pos) {
 }
 
 /* 1 = penetrating (depth/dir/pos set), 0 = separated */
-static int mpr_penetration(const gjk_obj *o1, const gjk_obj *o2, real tol, real *depth, real dir_out[3],
+static int mpr_penetration(const gjk_obj *o1, const gjk_obj *o2, ccd_real_t tol, real *depth_out, real dir_out[3],
                            real pos_out[3]) {
+    ccd_real_t depth_v = 0, *depth = &depth_v;
     ccd_simplex_t portal;
     ccd_vec3_t dir, pos;
     int res = discover_portal(o1, o2, &portal);
@@ -768,7 +877,7 @@ static int mpr_penetration(const gjk_obj *o1, const gjk_obj *o2, real tol, real 
         ccdVec3Add(&pos, &portal.ps[1].v2);
         ccdVec3Scale(&pos, 0.5);
         ccdVec3Copy(&dir, &portal.ps[1].v);
-        *depth = sqrt(ccdVec3Len2(&dir));
+        *depth = CCD_SQRT(ccdVec3Len2(&dir));
         ccdVec3Normalize(&dir);
     } else {
         if (refine_portal(o1, o2, &portal, tol) < 0) return 0;
@@ -781,7 +890,7 @@ static int mpr_penetration(const gjk_obj *o1, const gjk_obj *o2, real tol, real 
             if (portal_reach_tolerance(&portal, &v4, &dir, tol) || iterations > 500UL) {
                 ccd_vec3_t origin;
                 ccdVec3Set(&origin, 0.0, 0.0, 0.0);
-                *depth = sqrt(point_tri_dist2(&origin, &portal.ps[1].v, &portal.ps[2].v, &portal.ps[3].v, &dir));
+                *depth = CCD_SQRT(point_tri_dist2(&origin, &portal.ps[1].v, &portal.ps[2].v, &portal.ps[3].v, &dir));
                 if (ccdIsZero(*depth)) ccdVec3Set(&dir, 0.0, 0.0, 0.0);
                 else ccdVec3Normalize(&dir);
                 find_pos(&portal, &pos);
@@ -791,6 +900,7 @@ static int mpr_penetration(const gjk_obj *o1, const gjk_obj *o2, real tol, real 
             iterations++;
         }
     }
+    *depth_out = depth_v;
     for (int i = 0; i < 3; ++i) { dir_out[i] = dir.v[i]; pos_out[i] = pos.v[i]; }
     return 1;
 }
@@ -1111,6 +1221,7 @@ static void make_obj(const orc_world *w, int geom, const real *T, gjk_obj *o, or
         o->verts = w->verts + 3 * (size_t)w->geom_vstart[geom];
         o->nv = w->geom_nv[geom];
         o->interior = w->geom_interior + 3 * geom;
+        o->nbr = w->conv_nbr ? w->conv_nbr + (size_t)prm[0] : NULL;
         break;
     case GEOM_BOX: /* boxToGJK: dim = side / 2 */
         o->dim[0] = prm[0] / 2.0; o->dim[1] = prm[1] / 2.0; o->dim[2] = prm[2] / 2.0; break;
