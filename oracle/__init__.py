@@ -62,8 +62,8 @@ def lib():
 # one open arithmetic choice switched, to count how many flags / pair bits each
 # choice can change.  Test infrastructure like the rest of this package.
 VARIANTS = {
-    "ccd_float": ["-DORC_CCD_FLOAT"],            # libccd v2.1 default CMake build (single precision)
-    "fcl_walk": ["-DORC_FCL_WALK"],              # FCL 0.7.0 Convex::findExtremeVertex neighbour walk
+    "ccd_double": ["-DORC_CCD_DOUBLE"],          # libccd built with ENABLE_DOUBLE_PRECISION=ON
+    "fcl_linear": ["-DORC_FCL_LINEAR"],          # linear first-maximum convex support (no neighbour walk)
     "pin_cross": ["-DORC_PIN_REVOLUTE_CROSS"],   # column-wise SE3 x TransformRevolute with a cross product
     "eigen_slice": ["-DORC_EIGEN_ORDER=1"],      # Eigen 3.4 SSE2 slice-vectorised 3x3 products
     "eigen_tree": ["-DORC_EIGEN_ORDER=2"],       # Eigen redux-tree order for every coefficient
@@ -91,23 +91,29 @@ def variant_lib(name: str):
     return _variant_libs[name]
 
 
-def fcl_convex_neighbors(nv: int, faces) -> List[int]:
+def fcl_convex_neighbors(nv: int, faces) -> Tuple[List[int], bool]:
     """FCL 0.7.0 ``Convex::FindVertexNeighbors`` encoding [ext]: entry i
     (i < nv) is the offset of vertex i's record = [count, sorted neighbours...];
-    each face contributes its consecutive edges (and the closing edge)."""
+    each face contributes its consecutive edges (and the closing edge).
+    Second value: ``ValidateTopology`` passed (every edge shared by exactly two
+    faces, every vertex in some face) -- FCL walks neighbours only then."""
     nb = [set() for _ in range(nv)]
+    edge_faces: Dict[Tuple[int, int], int] = {}
     for f in faces:
         prev = f[-1]
         for v in f:
             nb[v].add(prev)
             nb[prev].add(v)
+            e = (min(v, prev), max(v, prev))
+            edge_faces[e] = edge_faces.get(e, 0) + 1
             prev = v
     out = [0] * nv
     for i in range(nv):
         out[i] = len(out)
         out.append(len(nb[i]))
         out.extend(sorted(nb[i]))
-    return out
+    ok = all(len(s) > 0 for s in nb) and all(c == 2 for c in edge_faces.values())
+    return out, ok
 
 
 def tri_tri(P, Q) -> bool:
@@ -218,8 +224,10 @@ class OracleWorld:
                 gnv.append(len(g.vertices))
                 nverts += len(g.vertices)
                 verts.append(np.asarray(g.vertices, dtype=np.float64).reshape(-1))
-                gparam += [float(len(nbr_all)), 0.0, 0.0, 0.0]
-                nbr_all += fcl_convex_neighbors(len(g.vertices), g.faces)
+                enc, ok = fcl_convex_neighbors(len(g.vertices), g.faces)
+                gparam += [float(len(nbr_all)) if ok else -1.0, 0.0, 0.0, 0.0]
+                if ok:
+                    nbr_all += enc
                 ginterior += g.interior
             elif isinstance(g, M.MeshGeom):
                 gtype.append(M.GEOM_MESH)

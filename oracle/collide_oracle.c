@@ -42,12 +42,15 @@
 
 typedef double real; /* Eigen / pinocchio / FCL scalar (S = double) */
 
-/* libccd 2.1 scalar (ccd/config.h, ccd/compiler.h).  The default build is
- * double (CCD_DOUBLE).  ORC_CCD_FLOAT builds the single-precision variant a
- * bare `cmake ..` of libccd v2.1 produces (ENABLE_DOUBLE_PRECISION OFF), as
- * /root/reference docker/Dockerfile:16-20 does -- see DESIGN.md "Oracle
- * variants" for what it changes. */
-#ifdef ORC_CCD_FLOAT
+/* libccd 2.1 scalar (ccd/config.h, ccd/compiler.h).  The reference's build
+ * image compiles libccd v2.1 with a bare `cmake ..` (docker/Dockerfile:16-20);
+ * libccd's CMake option ENABLE_DOUBLE_PRECISION defaults to OFF, so its
+ * ccd_real_t is float (CCD_SINGLE) and FCL 0.7.0's libccd glue converts every
+ * double it hands over (shapeToGJK, ccdVec3Set in the supports, the MPR
+ * tolerance) to float.  The default here follows that build;
+ * ORC_CCD_DOUBLE is the variant with a double-precision libccd (DESIGN.md
+ * "Oracle variants"). */
+#ifndef ORC_CCD_DOUBLE
 typedef float ccd_real_t;
 #define CCD_EPS FLT_EPSILON
 #define CCD_REAL_MAX FLT_MAX
@@ -450,11 +453,17 @@ static void support_convex(const gjk_obj *c, const ccd_vec3_t *dir_, ccd_vec3_t 
     const real dC[3] = {dir.v[0], dir.v[1], dir.v[2]}; /* Vector3<S> dir_C{S(dir.v[0]), ...} */
     real maxdot = -DBL_MAX;
     int best = 0;
-#ifdef ORC_FCL_WALK
-    /* Variant: FCL 0.7.0 Convex::findExtremeVertex hill climb (vertex count >
-     * kMinVertCountForEdgeWalking = 32): start at vertex 0, scan the current
-     * vertex's sorted neighbour list (FindVertexNeighbors, std::set order),
-     * step to every unvisited neighbour with value >= the best so far. */
+#ifndef ORC_FCL_LINEAR
+    /* FCL 0.7.0 Convex::findExtremeVertex hill climb, used when the hull has
+     * more than kMinVertCountForEdgeWalking = 32 vertices and its faces passed
+     * ValidateTopology (every edge in exactly two faces, every vertex in a
+     * face; else nbr == NULL): start at vertex 0, scan the current vertex's
+     * sorted neighbour list (FindVertexNeighbors, std::set order) and step to
+     * every unvisited neighbour whose value is >= the best so far.  The Panda
+     * hull triangulations are not convex (vertices up to 5.7 cm above face
+     * planes), so the climb can stop at a local maximum: a different support
+     * point than the linear scan (ORC_FCL_LINEAR variant) for ~1e-4 of
+     * directions. */
     if (c->nbr && c->nv > 32 && c->nv <= 4096) {
         unsigned char visited[4096];
         memset(visited, 0, (size_t)c->nv);
@@ -1221,7 +1230,7 @@ static void make_obj(const orc_world *w, int geom, const real *T, gjk_obj *o, or
         o->verts = w->verts + 3 * (size_t)w->geom_vstart[geom];
         o->nv = w->geom_nv[geom];
         o->interior = w->geom_interior + 3 * geom;
-        o->nbr = w->conv_nbr ? w->conv_nbr + (size_t)prm[0] : NULL;
+        o->nbr = (w->conv_nbr && prm[0] >= 0.0) ? w->conv_nbr + (size_t)prm[0] : NULL;
         break;
     case GEOM_BOX: /* boxToGJK: dim = side / 2 */
         o->dim[0] = prm[0] / 2.0; o->dim[1] = prm[1] / 2.0; o->dim[2] = prm[2] / 2.0; break;
