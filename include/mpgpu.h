@@ -79,7 +79,8 @@ extern "C" {
 #define MPG_JOINT_RUB_UNALIGNED 11
 
 /* FCL geometry kinds supported on the device */
-#define MPG_GEOM_CONVEX 0   /* fcl::Convex   : param unused, vertices        */
+#define MPG_GEOM_CONVEX 0   /* fcl::Convex   : vertices, param = first face
+                               int, face count (convex_face)             */
 #define MPG_GEOM_BOX 1      /* fcl::Box      : param = side x, y, z          */
 #define MPG_GEOM_SPHERE 2   /* fcl::Sphere   : param = radius                */
 #define MPG_GEOM_CAPSULE 3  /* fcl::Capsule  : param = radius, lz            */
@@ -157,6 +158,17 @@ typedef struct mpg_world_desc {
    *     geom_vertex_start */
   int64_t n_mesh_triangles;
   const int32_t *mesh_triangle;   /* [n_mesh_triangles*3]                   */
+
+  /* --- convex faces: fcl::Convex(vertices, num_faces, faces) keeps them and
+   *     FCL 0.7.0 derives its support from them (Convex::findExtremeVertex
+   *     walks the face graph when the hull has more than 32 vertices and the
+   *     faces are watertight: src/urdf_utils.cpp:156-183 builds every link hull
+   *     that way).  FCL layout: count, count vertex indices (relative to the
+   *     geometry's geom_vertex_start), count, ...  For MPG_GEOM_CONVEX,
+   *     geom_param[0] = first int of the geometry's faces in convex_face,
+   *     geom_param[1] = number of faces (0 = no faces: linear support).     */
+  int64_t n_convex_face_ints;
+  const int32_t *convex_face;     /* [n_convex_face_ints]                   */
 } mpg_world_desc;
 
 typedef struct mpg_world mpg_world;
@@ -273,6 +285,16 @@ int mpg_fk_batch(mpg_world *world, const double *q, int64_t n, double *link_pose
 #define MPG_NUM_STAGES 3
 int mpg_profile_enable(mpg_world *world, int enable);
 int mpg_profile_read(mpg_world *world, double *ms, int64_t *launches, int64_t *units, int n_stages);
+
+/*
+ * Diagnostics: fcl::collide(geometry geom_a at Ta[i], geometry geom_b at
+ * Tb[i]) for i < n (SE3 as 12 doubles each; host buffers), through the same
+ * narrow-phase dispatch as mpg_collide_batch (FCL closed form, octree / BVH
+ * mesh walk, or libccd MPR) -- the narrow phase without forward kinematics,
+ * for parity tests against the CPU restatement.  hit[i] = 1 on contact.
+ */
+int mpg_debug_collide_pairs(mpg_world *world, int32_t geom_a, int32_t geom_b, int64_t n, const double *Ta,
+                            const double *Tb, uint8_t *hit);
 
 /* Diagnostics: the device sin/cos used by the FK (host buffers). */
 int mpg_debug_sincos(const double *x, int64_t n, double *s, double *c, int device);

@@ -44,6 +44,7 @@ class WorldDesc(ctypes.Structure):
         ("gjk_tolerance", ctypes.c_double),
         ("n_octree_leaves", ctypes.c_int64), ("octree_leaf", _F64P),
         ("n_mesh_triangles", ctypes.c_int64), ("mesh_triangle", _I32P),
+        ("n_convex_face_ints", ctypes.c_int64), ("convex_face", _I32P),
     ]
 
 
@@ -77,6 +78,8 @@ SIGNATURES = {
     "mpg_profile_enable": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "mpg_profile_read": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double),
                                         ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64), ctypes.c_int]),
+    "mpg_debug_collide_pairs": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_int64,
+                                                ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "mpg_debug_sincos": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p,
                                         ctypes.c_int]),
     "mpg_synchronize": (ctypes.c_int, [ctypes.c_int]),

@@ -81,6 +81,12 @@ class DeviceWorld:
             tris = np.zeros(3, np.int32)
         self._keep.append(tris)
         d.mesh_triangle = tris.ctypes.data_as(C._I32P)
+        faces = np.ascontiguousarray(np.asarray(arrays.get("convex_face", np.zeros(0)), dtype=np.int32).reshape(-1))
+        d.n_convex_face_ints = faces.size
+        if faces.size == 0:
+            faces = np.zeros(1, np.int32)
+        self._keep.append(faces)
+        d.convex_face = faces.ctypes.data_as(C._I32P)
         h = ctypes.c_void_p()
         C.check(L.mpg_world_create(ctypes.byref(d), device, ctypes.byref(h)), "mpg_world_create")
         self._keep = []
@@ -135,6 +141,18 @@ class DeviceWorld:
                                           fl.ctypes.data_as(ctypes.c_void_p), pm.ctypes.data_as(ctypes.c_void_p),
                                           C.MPG_MEM_HOST, ctypes.c_void_p(stream or 0)), "mpg_collide_batch")
         return fl, pm
+
+    def debug_collide_pairs(self, geom_a: int, geom_b: int, Ta, Tb) -> np.ndarray:
+        """Narrow phase only: fcl::collide(geometry geom_a at Ta[i], geom_b at
+        Tb[i]) (SE3 rows of 12 doubles) -> uint8 hits (mpg_debug_collide_pairs)."""
+        A = np.ascontiguousarray(Ta, dtype=np.float64).reshape(-1, 12)
+        B = np.ascontiguousarray(Tb, dtype=np.float64).reshape(-1, 12)
+        n = len(A)
+        hit = np.zeros(n, np.uint8)
+        C.check(C.lib().mpg_debug_collide_pairs(self._h, int(geom_a), int(geom_b), n, A.ctypes.data_as(ctypes.c_void_p),
+                                                B.ctypes.data_as(ctypes.c_void_p), hit.ctypes.data_as(ctypes.c_void_p)),
+                "mpg_debug_collide_pairs")
+        return hit
 
     def fk_batch(self, q) -> np.ndarray:
         """[n, n_links, 7] link poses (p, wxyz) -- getLinkPose for every user link."""

@@ -249,6 +249,7 @@ struct DescBuilder {
   std::vector<int32_t> geom_type, geom_vertex_start, geom_vertex_count;
   std::vector<double> geom_param, vertices, octree_leaf;
   std::vector<int32_t> mesh_triangle;
+  std::vector<int32_t> convex_face;  // FCL layout faces of the convex geometries
   std::vector<int32_t> moving_link, moving_geom;
   std::vector<double> moving_offset;
   std::vector<int32_t> static_geom;

@@ -409,6 +409,10 @@ int DescBuilder::add_geometry(const CollisionGeometry* g) {
       vertices.push_back(v[1]);
       vertices.push_back(v[2]);
     }
+    // the faces decide FCL 0.7.0's support (neighbour walk), include/mpgpu.h
+    prm[0] = (double)convex_face.size();
+    prm[1] = (double)cv->num_faces;
+    convex_face.insert(convex_face.end(), cv->faces.begin(), cv->faces.end());
   }
   geom_vertex_start.push_back(vs);
   geom_vertex_count.push_back(nv);
@@ -452,6 +456,8 @@ mpg_world_desc DescBuilder::desc() const {
   d.octree_leaf = octree_leaf.data();
   d.n_mesh_triangles = (int64_t)(mesh_triangle.size() / 3);
   d.mesh_triangle = mesh_triangle.data();
+  d.n_convex_face_ints = (int64_t)convex_face.size();
+  d.convex_face = convex_face.data();
   return d;
 }
 

@@ -16,13 +16,17 @@ namespace mpg {
 constexpr int kMaxJoints = 32;
 
 // per-geometry double record
-enum { G_PARAM = 0, G_INTERIOR = 4, G_OBB_C = 7, G_OBB_E = 10, G_RADIUS = 13, G_VMAX = 14, G_STRIDE = 15 };
+// G_OBB_E: local AABB half extents widened for rounding (bounding tests);
+// G_AABB_E: the exact half extents (hi - lo) * 0.5 of FCL's computeBV
+enum { G_PARAM = 0, G_INTERIOR = 4, G_OBB_C = 7, G_OBB_E = 10, G_RADIUS = 13, G_VMAX = 14, G_AABB_E = 15, G_STRIDE = 18 };
 // per-static-object double record
 enum { S_ROT = 0, S_ROTINV = 4, S_POS = 8, S_OBBC = 11, S_R = 14, S_STRIDE = 23 };
 
 struct DevWorld {
   int nj, dof, n_links, n_geoms, n_moving, n_static, n_pairs, W;
   double mpr_tol;
+  float bp_margin;      // phase-A culling margin (metres), kBpMargin or the libccd false-hit reach
+  double small_margin;  // the latency path's bounding-sphere margin, same rule
   int debug_mode;  // diagnostics only: 1 = broad-phase records only, 2 = no SAT stage, 3 = no MPR (latency path: no narrow test), 5 / 6 = no mesh-mesh / mesh-shape walks, 7 = latency path: FK + sphere test only
   unsigned long long* stats;  // diagnostics only (MPG_STATS=1), else NULL
   cptr<int> joint_type;      // [nj]
@@ -43,6 +47,13 @@ struct DevWorld {
   cptr<int> geom_cbase;      // [n_geoms] first cell record of the hull, -1 = none (full scan)
   cptr<double> cell_rec;     // kCellsPerHull records of kCellRec doubles per hull (mpg_hullcells.h)
   cptr<double> cell_ovf;     // list entries beyond the inline ones: x, y, z, 0
+  // FCL 0.7.0 neighbour-walk hulls (mpg_hullcells.h): geom_nbr[g] = start of
+  // the hull's neighbors_ encoding in hull_nbr, -1 = linear support; their
+  // cell records (kWalkRec doubles, indexed by geom_cbase) and overflow entries
+  cptr<int> geom_nbr;
+  cptr<int> hull_nbr;
+  cptr<double> wcell_rec;
+  cptr<double> wcell_ovf;
   cptr<int> moving_link;     // [n_moving]
   cptr<int> moving_geom;
   cptr<double> moving_offset;  // [n_moving*12]

@@ -21,6 +21,7 @@
 #include <cmath>
 #include <cstdint>
 #include <algorithm>
+#include <array>
 #include <vector>
 #include "mpg_math.h"
 
@@ -184,6 +185,129 @@ MPG_INLINE void cell_record_support(PD R, PD ovf, double x, double y, double z, 
   out[0] = bx;
   out[1] = by;
   out[2] = bz;
+}
+
+// --------------------------------------------------------------------------
+// FCL 0.7.0 neighbour-walk hulls [ext: geometry/shape/convex-inl.h]
+// --------------------------------------------------------------------------
+// Convex::FindVertexNeighbors + ValidateTopology: faces in FCL's layout
+// (count, i0 .. i(count-1), count, ...) -> neighbors_ encoding (entry i < nv:
+// offset of vertex i's record [count, neighbours in ascending order], std::set
+// order), appended to out.  Returns whether FCL walks this hull:
+// find_extreme_via_neighbors_ = (nv > kMinVertCountForEdgeWalking = 32) and
+// the topology is valid (every vertex in some face, every edge in exactly two
+// faces).  Faces must index [0, nv) (the descriptor validation checks).
+constexpr int kMinVertCountForEdgeWalking = 32;
+constexpr int kMaxWalkVerts = 512;  // device visited mask (convex_walk)
+inline bool fcl_convex_neighbors(int nv, const int32_t* faces, int num_faces, std::vector<int>& out) {
+  std::vector<std::vector<int>> nb(nv);
+  std::vector<std::pair<int, int>> edges;
+  int fi = 0;
+  for (int f = 0; f < num_faces; ++f) {
+    const int cnt = faces[fi];
+    int prev = faces[fi + cnt];
+    for (int j = fi + 1; j <= fi + cnt; ++j) {
+      const int v = faces[j];
+      nb[v].push_back(prev);
+      nb[prev].push_back(v);
+      edges.push_back({std::min(v, prev), std::max(v, prev)});
+      prev = v;
+    }
+    fi += cnt + 1;
+  }
+  const size_t base = out.size();
+  out.resize(base + nv);
+  bool connected = true;
+  for (int i = 0; i < nv; ++i) {
+    std::sort(nb[i].begin(), nb[i].end());
+    nb[i].erase(std::unique(nb[i].begin(), nb[i].end()), nb[i].end());
+    connected &= !nb[i].empty();
+    out[base + i] = (int)(out.size() - base);
+    out.push_back((int)nb[i].size());
+    out.insert(out.end(), nb[i].begin(), nb[i].end());
+  }
+  std::sort(edges.begin(), edges.end());
+  bool watertight = true;
+  for (size_t k = 0; k < edges.size();) {
+    size_t e = k;
+    while (e < edges.size() && edges[e] == edges[k]) ++e;
+    watertight &= (e - k) == 2;
+    k = e;
+  }
+  return nv > kMinVertCountForEdgeWalking && connected && watertight;
+}
+
+// Walk-hull cell records (convex_support_local on the device): per cell the
+// vertices the walk can END at for some direction of the (widened) cell cone
+// -- a vertex w is left out only when one of its neighbours u beats it on every
+// corner ray by the margin of build_hull_cells, so u's rounded dot product is
+// strictly above w's for every direction of the cell and the walk never stops
+// at w -- in vertex order, each with the neighbour beating it most often
+// (its witness).  The first maximum of the list is the global first maximum
+// (the list contains every vertex build_hull_cells keeps).
+constexpr int kWalkHead = 4;    // n, overflow offset (entries), pad, pad
+constexpr int kWalkEnt = 8;     // x, y, z, vertex index, witness x, y, z, pad
+constexpr int kWalkInline = 2;  // entries stored in the record itself
+constexpr int kWalkRec = kWalkHead + kWalkInline * kWalkEnt;
+inline bool build_walk_cells(const double* V, int nv, const int* nbr, std::vector<double>& rec,
+                             std::vector<double>& ovf) {
+  double X = 0.0;
+  for (int i = 0; i < 3 * nv; ++i) X = std::max(X, std::fabs(V[i]));
+  if (nv <= 0 || !(X >= kHullMin && X <= kHullMax)) return false;
+  const double delta = kCellWiden, rel = 1e-9;
+  std::vector<double> P((size_t)nv * 4);
+  for (int f = 0; f < 3; ++f)
+    for (int s = 0; s < 2; ++s)
+      for (int iu = 0; iu < kCellK; ++iu)
+        for (int iv = 0; iv < kCellK; ++iv) {
+          double r[4][3], M[4];
+          const double u0 = -1.0 + 2.0 * iu / kCellK - delta, u1 = -1.0 + 2.0 * (iu + 1) / kCellK + delta;
+          const double v0 = -1.0 + 2.0 * iv / kCellK - delta, v1 = -1.0 + 2.0 * (iv + 1) / kCellK + delta;
+          for (int k = 0; k < 4; ++k) {
+            r[k][f] = s ? -1.0 : 1.0;
+            r[k][(f + 1) % 3] = (k & 1) ? u1 : u0;
+            r[k][(f + 2) % 3] = (k & 2) ? v1 : v0;
+            M[k] = rel * (std::fabs(r[k][0]) + std::fabs(r[k][1]) + std::fabs(r[k][2])) * X;
+          }
+          for (int i = 0; i < nv; ++i)
+            for (int k = 0; k < 4; ++k) P[4 * i + k] = r[k][0] * V[3 * i] + r[k][1] * V[3 * i + 1] + r[k][2] * V[3 * i + 2];
+          auto margin = [&](int u, int i) {  // > 0: u beats i on the whole cell
+            double m = DBL_MAX;
+            for (int k = 0; k < 4; ++k) m = std::min(m, P[4 * u + k] - P[4 * i + k] - M[k]);
+            return m;
+          };
+          std::vector<std::array<double, 8>> ents;
+          for (int i = 0; i < nv; ++i) {
+            const int* nb = nbr + nbr[i];
+            int wit = -1;
+            double best = -DBL_MAX;
+            bool dominated = false;
+            for (int k = 1; k <= nb[0]; ++k) {
+              const double m = margin(nb[k], i);
+              if (m > 0.0) dominated = true;
+              if (m > best) {
+                best = m;
+                wit = nb[k];
+              }
+            }
+            if (dominated) continue;
+            if (wit < 0) wit = i;  // isolated vertex (not a walk hull then)
+            ents.push_back({V[3 * i], V[3 * i + 1], V[3 * i + 2], (double)i, V[3 * wit], V[3 * wit + 1],
+                            V[3 * wit + 2], 0.0});
+          }
+          const size_t r0 = rec.size();
+          rec.resize(r0 + kWalkRec, 0.0);
+          rec[r0] = (double)ents.size();
+          rec[r0 + 1] = (double)(ovf.size() / kWalkEnt);
+          for (size_t e = 0; e < ents.size(); ++e) {
+            if ((int)e < kWalkInline) {
+              for (int j = 0; j < kWalkEnt; ++j) rec[r0 + kWalkHead + kWalkEnt * e + j] = ents[e][j];
+            } else {
+              ovf.insert(ovf.end(), ents[e].begin(), ents[e].end());
+            }
+          }
+        }
+  return true;
 }
 
 }  // namespace mpg

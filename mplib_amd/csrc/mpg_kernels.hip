@@ -46,7 +46,6 @@ using namespace mpg;
 
 namespace {
 
-constexpr double kCcdEps = DBL_EPSILON;
 
 thread_local std::string g_last_error;
 
@@ -72,17 +71,27 @@ int set_error(int code, const std::string& msg) {
 // FCL GJK objects + libccd MPR
 // ---------------------------------------------------------------------------
 struct GObj {
-  Q4 rot, rot_inv;
-  V3 pos;
+  CQ4 rot, rot_inv;  // libccd ccd_quat_t (ccd_real)
+  CV3 pos;
   int geom;
   int type;
 };
 
-// Convex::findExtremeVertex over the whole hull: argmax dir . vertex (fp64),
-// first maximum wins.  HV: the hulls in AoSoA-4 layout (per group of 4
-// vertices: x0..3, y0..3, z0..3), padded to whole groups with copies of the
-// hull's first vertex, which can never win the strict '>', so the result
-// equals the unpadded scan.  Only for directions without a cell.
+// vertex i of hull `geom` (AoSoA-4 groups: x0..3, y0..3, z0..3)
+__device__ __forceinline__ V3 hull_vertex(const DevWorld& w, cptr<double> HV, int geom, int i) {
+  const cptr<double> G = HV + 12 * (size_t)(w.geom_gstart[geom] + (i >> 2)) + (i & 3);
+  return v3(G[0], G[4], G[8]);
+}
+
+// Dot product in Eigen's Vector3d::dot order, as Convex::findExtremeVertex
+// evaluates v_C.dot(vertex): (x0*p0 + x1*p1) + x2*p2.
+__device__ __forceinline__ double edot(const V3& d, const V3& p) { return (d.x * p.x + d.y * p.y) + d.z * p.z; }
+
+// Convex::findExtremeVertex, linear branch (hulls of <= 32 vertices, or whose
+// faces failed FCL's ValidateTopology): argmax dir . vertex (fp64), first
+// maximum wins.  The AoSoA groups are padded with copies of the hull's first
+// vertex, which can never win the strict '>', so the result equals the
+// unpadded scan.  Only for directions without a cell.
 __device__ __forceinline__ V3 convex_full_scan(const DevWorld& w, cptr<double> HV, int geom, const V3& dir) {
   const int g0 = w.geom_gstart[geom], ng = w.geom_ng[geom];
   const cptr<double> P = HV + 12 * (size_t)g0;
@@ -104,12 +113,101 @@ __device__ __forceinline__ V3 convex_full_scan(const DevWorld& w, cptr<double> H
   return v3(B[0], B[4], B[8]);
 }
 
-// Convex support through the cell record of dir (mpg_hullcells.h: every
-// vertex left out of a cell's list is strictly beaten in fp64 by a listed one
-// and the list is in vertex order, so its first maximum is the full scan's).
+// Convex::findExtremeVertex, neighbour-walk branch [ext FCL 0.7.0
+// geometry/shape/convex-inl.h] (hulls of > 32 vertices whose faces passed
+// ValidateTopology, oracle/collide_oracle.c support_convex): start at vertex
+// 0, scan the current vertex's neighbour list (FindVertexNeighbors: sorted,
+// from the faces), step to every unvisited neighbour whose value is >= the
+// best so far, until a pass moves nowhere.  The visited set is a 512-bit
+// register mask (world creation rejects larger walk hulls).  Kept out of
+// line: most supports are resolved by the cell test below without it.
+__device__ __attribute__((noinline)) V3 convex_walk(const DevWorld& w, cptr<double> HV, int geom, const V3 d) {
+  const cptr<int> nb = w.hull_nbr + w.geom_nbr[geom];
+  uint64_t vis[8] = {1ull, 0, 0, 0, 0, 0, 0, 0};
+  double best = edot(d, hull_vertex(w, HV, geom, 0));
+  int bi = 0;
+  bool keep = true;
+  while (keep) {
+    keep = false;
+    const int start = nb[bi], cnt = nb[start];
+    for (int k = start + 1; k <= start + cnt; ++k) {
+      const int vi = nb[k];
+      const int wd = vi >> 6;
+      const uint64_t m = 1ull << (vi & 63);
+      uint64_t word = 0;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) word = j == wd ? vis[j] : word;
+      if (word & m) continue;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) vis[j] = j == wd ? (vis[j] | m) : vis[j];
+      const double dd = edot(d, hull_vertex(w, HV, geom, vi));
+      if (dd >= best) {
+        keep = true;
+        bi = vi;
+        best = dd;
+      }
+    }
+  }
+  return hull_vertex(w, HV, geom, bi);
+}
+
+// true if some neighbour of vertex vi has a dot product strictly above dd: then
+// the walk cannot end at vi (every vertex it evaluates is compared with the
+// running maximum, which only grows)
+__device__ __forceinline__ bool neighbour_beats(const DevWorld& w, cptr<double> HV, int geom, int vi, double dd,
+                                                const V3& d) {
+  const cptr<int> nb = w.hull_nbr + w.geom_nbr[geom];
+  const int start = nb[vi], cnt = nb[start];
+  for (int k = start + 1; k <= start + cnt; ++k)
+    if (edot(d, hull_vertex(w, HV, geom, nb[k])) > dd) return true;
+  return false;
+}
+
+// Walk-hull support through its cell record (mpg_hullcells.h
+// build_walk_cells): the cell lists every vertex the walk could end at for a
+// direction of the cell (the others have a neighbour beating them on the whole
+// cell), in vertex order, each with a witness neighbour.  The walk ends at a
+// vertex none of whose neighbours is strictly greater; the first maximum g of
+// the list always qualifies, so when every other listed vertex has a strictly
+// greater neighbour (usually its witness) the walk ends at g.  Otherwise (a
+// local maximum of the non-convex triangulation, or a tie) the walk is run.
+__device__ __forceinline__ V3 walk_cell_support(const DevWorld& w, cptr<double> HV, int geom, cptr<double> R,
+                                                const V3& d) {
+  const int n = (int)R[0];
+  const cptr<double> ovf = w.wcell_ovf + kWalkEnt * (size_t)R[1];
+  double best = -DBL_MAX;
+  int g = 0;
+  for (int k = 0; k < n; ++k) {
+    const cptr<double> e = k < kWalkInline ? R + kWalkHead + kWalkEnt * k : ovf + kWalkEnt * (k - kWalkInline);
+    const double dd = (d.x * e[0] + d.y * e[1]) + d.z * e[2];
+    if (dd > best) {
+      best = dd;
+      g = k;
+    }
+  }
+  bool ok = true;
+  for (int k = 0; k < n && ok; ++k) {
+    if (k == g) continue;
+    const cptr<double> e = k < kWalkInline ? R + kWalkHead + kWalkEnt * k : ovf + kWalkEnt * (k - kWalkInline);
+    const double dd = (d.x * e[0] + d.y * e[1]) + d.z * e[2];
+    const double dw = (d.x * e[4] + d.y * e[5]) + d.z * e[6];
+    if (dw > dd) continue;
+    ok = neighbour_beats(w, HV, geom, (int)e[3], dd, d);
+  }
+  if (!ok) return convex_walk(w, HV, geom, d);
+  const cptr<double> e = g < kWalkInline ? R + kWalkHead + kWalkEnt * g : ovf + kWalkEnt * (g - kWalkInline);
+  return v3(e[0], e[1], e[2]);
+}
+
+// Convex support in the hull frame (FCL 0.7.0 supportConvex: the ccd
+// direction converted to Vector3<double>, findExtremeVertex in fp64).
 __device__ __forceinline__ V3 convex_support_local(const DevWorld& w, cptr<double> HV, int geom, const V3& d) {
   const int cb = w.geom_cbase[geom];
   const int c = cb >= 0 ? hull_cell(d.x, d.y, d.z) : -1;
+  if (w.geom_nbr[geom] >= 0) {  // neighbour-walk hull (wave-uniform branch)
+    if (c < 0) return convex_walk(w, HV, geom, d);
+    return walk_cell_support(w, HV, geom, w.wcell_rec + kWalkRec * (size_t)(cb + c), d);
+  }
   if (c < 0) return convex_full_scan(w, HV, geom, d);
   double p[3];
   cell_record_support(w.cell_rec + kCellRec * (size_t)(cb + c), w.cell_ovf, d.x, d.y, d.z, p);
@@ -117,79 +215,103 @@ __device__ __forceinline__ V3 convex_support_local(const DevWorld& w, cptr<doubl
 }
 
 // support mapping of one shape in its own frame (FCL shapeToGJK supports:
-// supportConvex, supportBox, supportSphere, supportCap, supportCyl)
-__device__ __forceinline__ V3 support_local(const DevWorld& w, cptr<double> HV, int geom, int type, const V3& dir) {
+// supportConvex, supportBox, supportSphere, supportCap, supportCyl), in the
+// libccd scalar: the shape parameters are the ccd_real values FCL's
+// *ToGJK functions store (box: dim = side / 2; capsule / cylinder: height =
+// lz / 2).
+__device__ __forceinline__ CV3 support_local(const DevWorld& w, cptr<double> HV, int geom, int type, const CV3& dir) {
   const cptr<double> rec = w.geom_rec + G_STRIDE * geom;
-  V3 v;
+  CV3 v;
   if (type == MPG_GEOM_CONVEX) {
-    v = convex_support_local(w, HV, geom, dir);
+    const V3 p = convex_support_local(w, HV, geom, to_v3(dir));
+    v = cv3(p.x, p.y, p.z);
   } else if (type == MPG_GEOM_BOX) {
-    const double hx = rec[G_PARAM + 0] / 2.0, hy = rec[G_PARAM + 1] / 2.0, hz = rec[G_PARAM + 2] / 2.0;
-    v = v3((dir.x >= 0 ? 1.0 : -1.0) * hx, (dir.y >= 0 ? 1.0 : -1.0) * hy, (dir.z >= 0 ? 1.0 : -1.0) * hz);
+    const ccd_real hx = (ccd_real)(rec[G_PARAM + 0] / 2.0), hy = (ccd_real)(rec[G_PARAM + 1] / 2.0),
+                   hz = (ccd_real)(rec[G_PARAM + 2] / 2.0);
+    v = CV3{(dir.x >= 0 ? ccd_real(1) : ccd_real(-1)) * hx, (dir.y >= 0 ? ccd_real(1) : ccd_real(-1)) * hy,
+            (dir.z >= 0 ? ccd_real(1) : ccd_real(-1)) * hz};
   } else if (type == MPG_GEOM_SPHERE) {
-    const double r = rec[G_PARAM];
-    v = vscale(vscale(dir, r), 1.0 / std::sqrt(vdot(dir, dir)));
+    const ccd_real r = (ccd_real)rec[G_PARAM];
+    v = vscale(vscale(dir, r), ccd_real(1) / std::sqrt(vdot(dir, dir)));
   } else if (type == MPG_GEOM_CAPSULE) {
-    const double r = rec[G_PARAM], h = rec[G_PARAM + 1] / 2.0;
-    const V3 n = vscale(vnormalize(dir), r);
-    V3 p1 = v3(0.0, 0.0, h), p2 = v3(0.0, 0.0, -h);
+    const ccd_real r = (ccd_real)rec[G_PARAM], h = (ccd_real)(rec[G_PARAM + 1] / 2.0);
+    const CV3 n = vscale(vnormalize(dir), r);
+    CV3 p1 = CV3{0, 0, h}, p2 = CV3{0, 0, -h};
     p1 = vadd(p1, n);
     p2 = vadd(p2, n);
     v = dir.z > 0 ? p1 : p2;
   } else {  // cylinder
-    const double r = rec[G_PARAM], h = rec[G_PARAM + 1] / 2.0;
-    double zdist = dir.x * dir.x + dir.y * dir.y;
+    const ccd_real r = (ccd_real)rec[G_PARAM], h = (ccd_real)(rec[G_PARAM + 1] / 2.0);
+    ccd_real zdist = dir.x * dir.x + dir.y * dir.y;
     zdist = std::sqrt(zdist);
     if (std::fabs(zdist) < kCcdEps) {
-      v = v3(0.0, 0.0, (dir.z > 0 ? 1.0 : -1.0) * h);
+      v = CV3{0, 0, (dir.z > 0 ? ccd_real(1) : ccd_real(-1)) * h};
     } else {
-      const double rad = r / zdist;
-      v = v3(rad * dir.x, rad * dir.y, (dir.z > 0 ? 1.0 : -1.0) * h);
+      const ccd_real rad = r / zdist;
+      v = CV3{rad * dir.x, rad * dir.y, (dir.z > 0 ? ccd_real(1) : ccd_real(-1)) * h};
     }
   }
   return v;
+}
+
+// True extreme point of a shape along dir in its own frame, fp64 (every
+// vertex for hulls, whatever FCL's walk would return): conservative range
+// tests only, never an output bit.
+__device__ __forceinline__ V3 support_local_exact(const DevWorld& w, cptr<double> HV, int geom, int type, const V3& dir) {
+  const cptr<double> rec = w.geom_rec + G_STRIDE * geom;
+  if (type == MPG_GEOM_CONVEX) return convex_full_scan(w, HV, geom, dir);
+  if (type == MPG_GEOM_BOX)
+    return v3((dir.x >= 0 ? 1.0 : -1.0) * rec[G_PARAM] / 2.0, (dir.y >= 0 ? 1.0 : -1.0) * rec[G_PARAM + 1] / 2.0,
+              (dir.z >= 0 ? 1.0 : -1.0) * rec[G_PARAM + 2] / 2.0);
+  if (type == MPG_GEOM_SPHERE) return vscale(vscale(dir, rec[G_PARAM]), 1.0 / std::sqrt(vdot(dir, dir)));
+  const double r = rec[G_PARAM], h = rec[G_PARAM + 1] / 2.0;
+  if (type == MPG_GEOM_CAPSULE) return vadd(v3(0.0, 0.0, dir.z > 0 ? h : -h), vscale(vnormalize(dir), r));
+  const double zd = std::sqrt(dir.x * dir.x + dir.y * dir.y);  // cylinder
+  const double rad = zd > 0.0 ? r / zd : 0.0;
+  return v3(rad * dir.x, rad * dir.y, (dir.z > 0 ? 1.0 : -1.0) * h);
 }
 
 // libccd support of one GJK object: direction into the object frame
 // (ccdQuatRotVec with rot_inv), local support, back to the world frame.  The
 // geometry is the same on every lane of the wave (one pair per wave): say so,
 // so parameter reads stay scalar loads.
-__device__ __forceinline__ V3 support(const DevWorld& w, cptr<double> HV, const GObj& o, const V3& dir_world) {
-  const V3 dir = quat_rot(dir_world, o.rot_inv);
+__device__ __forceinline__ CV3 support(const DevWorld& w, cptr<double> HV, const GObj& o, const CV3& dir_world) {
+  const CV3 dir = quat_rot(dir_world, o.rot_inv);
   const int geom = __builtin_amdgcn_readfirstlane(o.geom), type = __builtin_amdgcn_readfirstlane(o.type);
   return vadd(quat_rot(support_local(w, HV, geom, type, dir), o.rot), o.pos);
 }
 
-__device__ __forceinline__ V3 center(const DevWorld& w, const GObj& o) {
+// centerConvex (interior point ccdVec3Set, rotated, translated) / centerShape
+__device__ __forceinline__ CV3 center(const DevWorld& w, const GObj& o) {
   if (__builtin_amdgcn_readfirstlane(o.type) == MPG_GEOM_CONVEX) {
     const cptr<double> rec = w.geom_rec + G_STRIDE * __builtin_amdgcn_readfirstlane(o.geom);
-    return vadd(quat_rot(v3(rec[G_INTERIOR], rec[G_INTERIOR + 1], rec[G_INTERIOR + 2]), o.rot), o.pos);
+    return vadd(quat_rot(cv3(rec[G_INTERIOR], rec[G_INTERIOR + 1], rec[G_INTERIOR + 2]), o.rot), o.pos);
   }
   return o.pos;
 }
 
-__device__ __forceinline__ bool is_zero(double v) { return std::fabs(v) < kCcdEps; }
+__device__ __forceinline__ bool is_zero(ccd_real v) { return std::fabs(v) < kCcdEps; }
 
-__device__ __forceinline__ bool ccd_eq(double _a, double _b) {
-  const double ab = std::fabs(_a - _b);
+__device__ __forceinline__ bool ccd_eq(ccd_real _a, ccd_real _b) {
+  const ccd_real ab = std::fabs(_a - _b);
   if (std::fabs(ab) < kCcdEps) return true;
-  const double a = std::fabs(_a), b = std::fabs(_b);
+  const ccd_real a = std::fabs(_a), b = std::fabs(_b);
   if (b > a) return ab < kCcdEps * b;
   return ab < kCcdEps * a;
 }
 
-__device__ __forceinline__ bool vec_is_origin(const V3& v) {
-  return ccd_eq(v.x, 0.0) && ccd_eq(v.y, 0.0) && ccd_eq(v.z, 0.0);
+__device__ __forceinline__ bool vec_is_origin(const CV3& v) {
+  return ccd_eq(v.x, ccd_real(0)) && ccd_eq(v.y, ccd_real(0)) && ccd_eq(v.z, ccd_real(0));
 }
 
 // libccd __ccdSupport: v = support1(dir) - support2(-dir)
-__device__ __forceinline__ V3 msupport(const DevWorld& w, cptr<double> HV, const GObj& a,
-                                       const GObj& b, const V3& dir) {
-  const V3 da = quat_rot(dir, a.rot_inv), db = quat_rot(vscale(dir, -1.0), b.rot_inv);
+__device__ __forceinline__ CV3 msupport(const DevWorld& w, cptr<double> HV, const GObj& a,
+                                        const GObj& b, const CV3& dir) {
+  const CV3 da = quat_rot(dir, a.rot_inv), db = quat_rot(vscale(dir, ccd_real(-1)), b.rot_inv);
   const int ga = __builtin_amdgcn_readfirstlane(a.geom), ta = __builtin_amdgcn_readfirstlane(a.type);
   const int gb = __builtin_amdgcn_readfirstlane(b.geom), tb = __builtin_amdgcn_readfirstlane(b.type);
-  const V3 la = support_local(w, HV, ga, ta, da);
-  const V3 lb = support_local(w, HV, gb, tb, db);
+  const CV3 la = support_local(w, HV, ga, ta, da);
+  const CV3 lb = support_local(w, HV, gb, tb, db);
   return vsub(vadd(quat_rot(la, a.rot), a.pos), vadd(quat_rot(lb, b.rot), b.pos));
 }
 
@@ -229,7 +351,7 @@ __device__ __forceinline__ GObj moving_obj(const DevWorld& w, const double* __re
   GObj o;
   o.rot = gjk_rot_from_matrix(T.R);
   o.rot_inv = quat_invert2(o.rot);
-  o.pos = v3(T.p[0], T.p[1], T.p[2]);
+  o.pos = cv3(T.p[0], T.p[1], T.p[2]);
   o.geom = w.moving_geom[id];
   o.type = w.geom_type[o.geom];
   return o;
@@ -492,9 +614,10 @@ __device__ __forceinline__ bool obb_disjoint(const double* B, const double* T, c
 __device__ __forceinline__ GObj static_obj(const DevWorld& w, int sid) {
   const cptr<double> r = w.static_rec + S_STRIDE * sid;
   GObj o;
-  o.rot = Q4{r[S_ROT], r[S_ROT + 1], r[S_ROT + 2], r[S_ROT + 3]};
-  o.rot_inv = Q4{r[S_ROTINV], r[S_ROTINV + 1], r[S_ROTINV + 2], r[S_ROTINV + 3]};
-  o.pos = v3(r[S_POS], r[S_POS + 1], r[S_POS + 2]);
+  // static_record stores the ccd_real values (exactly representable in fp64)
+  o.rot = CQ4{(ccd_real)r[S_ROT], (ccd_real)r[S_ROT + 1], (ccd_real)r[S_ROT + 2], (ccd_real)r[S_ROT + 3]};
+  o.rot_inv = CQ4{(ccd_real)r[S_ROTINV], (ccd_real)r[S_ROTINV + 1], (ccd_real)r[S_ROTINV + 2], (ccd_real)r[S_ROTINV + 3]};
+  o.pos = cv3(r[S_POS], r[S_POS + 1], r[S_POS + 2]);
   o.geom = w.static_geom[sid];
   o.type = w.geom_type[o.geom];
   return o;
@@ -567,7 +690,7 @@ __device__ __forceinline__ void sat_drain(const DevWorld& w, const float* __rest
     const int p = (int)(e >> 6), t = wbase + (int)(e & 63u);
     const FObb A = bp_obb<BLOCK>(w, cen, rq, cap, w.pair_a[p], t, cfg0 + t);
     const FObb B = bp_obb<BLOCK>(w, cen, rq, cap, w.pair_b[p], t, cfg0 + t);
-    if (!fobb_separated(A, B, kBpMargin)) atomicOr(&survw[(p >> 5) * BLOCK + t], 1u << (p & 31));
+    if (!fobb_separated(A, B, w.bp_margin)) atomicOr(&survw[(p >> 5) * BLOCK + t], 1u << (p & 31));
   }
   __builtin_amdgcn_wave_barrier();
 }
@@ -632,11 +755,11 @@ __global__ __launch_bounds__(BLOCK) void cull_kernel(DevWorld w, const double* _
       const int p = w.sched_pair[e], o = w.sched_other[e];
       bool keep;
       if (o >= w.n_moving) {
-        keep = !fsphere_obb_separated(cm, r_m, w.bp.sobj + BS_STRIDE * (o - w.n_moving), kBpMargin);
+        keep = !fsphere_obb_separated(cm, r_m, w.bp.sobj + BS_STRIDE * (o - w.n_moving), w.bp_margin);
       } else {
         const float* ro = cen + (size_t)o * 3 * BLOCK + tid;
         const float dx = ro[0] - cm[0], dy = ro[BLOCK] - cm[1], dz = ro[2 * BLOCK] - cm[2];
-        const float rr = r_m + w.bp.mobj[BM_STRIDE * o + BM_R] + kBpMargin;
+        const float rr = r_m + w.bp.mobj[BM_STRIDE * o + BM_R] + w.bp_margin;
         keep = dx * dx + dy * dy + dz * dz <= rr * rr;
       }
       keep = keep && live;
@@ -923,35 +1046,35 @@ __global__ __launch_bounds__(256, CLS == CLS_OCTREE ? 2 : 1) void closed_form_ke
 // The state is copied into locals and written back unconditionally: stores
 // under branches through the reference parameters get merged into stores
 // through a selected pointer, which keeps the caller's registers on the stack.
-__device__ __forceinline__ int mpr_advance(double mpr_tol, const V3& s, int& st_io, V3& v0_io, V3& v1_io, V3& v2_io,
-                                           V3& v3_io, V3& dir_io) {
+__device__ __forceinline__ int mpr_advance(ccd_real mpr_tol, const CV3& s, int& st_io, CV3& v0_io, CV3& v1_io, CV3& v2_io,
+                                           CV3& v3_io, CV3& dir_io) {
   int st = st_io;
-  V3 v0 = v0_io, v1 = v1_io, v2 = v2_io, v3 = v3_io, dir = dir_io;
+  CV3 v0 = v0_io, v1 = v1_io, v2 = v2_io, v3 = v3_io, dir = dir_io;
   int res = 0;  // 1 = intersect, -1 = separated
   // Every state ends in one new search direction dir = normalize(a x b);
   // the states only pick (a, b), so the costly normalize (sqrt + divide)
   // runs once per step for all lanes instead of once per state branch.
-  const double dsd = vdot(s, dir);
-  V3 ca, cb;
+  const ccd_real dsd = vdot(s, dir);
+  CV3 ca, cb;
   bool post_swap = false, post_encl = false;
   if (st == MPR_V4) {  // refinePortal: expand the portal (v1, v2, v3) towards v4 = s
-    if (!(is_zero(dsd) || dsd > 0.0)) {
+    if (!(is_zero(dsd) || dsd > 0)) {
       res = -1;
     } else {
-      const double dv1 = vdot(v1, dir), dv2 = vdot(v2, dir), dv3 = vdot(v3, dir);
-      double d1 = dsd - dv1;
-      const double dd2 = dsd - dv2, dd3 = dsd - dv3;
+      const ccd_real dv1 = vdot(v1, dir), dv2 = vdot(v2, dir), dv3 = vdot(v3, dir);
+      ccd_real d1 = dsd - dv1;
+      const ccd_real dd2 = dsd - dv2, dd3 = dsd - dv3;
       d1 = (d1 < dd2) ? d1 : dd2;  // CCD_FMIN
       d1 = (d1 < dd3) ? d1 : dd3;
       if (ccd_eq(d1, mpr_tol) || d1 < mpr_tol) {
         res = -1;
       } else {
-        const V3 v4v0 = vcross(s, v0);
-        if (vdot(v1, v4v0) > 0.0) {
-          if (vdot(v2, v4v0) > 0.0) v1 = s;
+        const CV3 v4v0 = vcross(s, v0);
+        if (vdot(v1, v4v0) > 0) {
+          if (vdot(v2, v4v0) > 0) v1 = s;
           else v3 = s;
         } else {
-          if (vdot(v3, v4v0) > 0.0) v2 = s;
+          if (vdot(v3, v4v0) > 0) v2 = s;
           else v1 = s;
         }
         ca = vsub(v2, v1);
@@ -959,7 +1082,7 @@ __device__ __forceinline__ int mpr_advance(double mpr_tol, const V3& s, int& st_
         post_encl = true;
       }
     }
-  } else if (is_zero(dsd) || dsd < 0.0) {  // discoverPortal: support not past the origin
+  } else if (is_zero(dsd) || dsd < 0) {  // discoverPortal: support not past the origin
     res = -1;
   } else if (st == MPR_V1) {
     v1 = s;
@@ -973,14 +1096,14 @@ __device__ __forceinline__ int mpr_advance(double mpr_tol, const V3& s, int& st_
   } else {  // MPR_V3
     v3 = s;
     bool cont = false;
-    double d2 = vdot(vcross(v1, v3), v0);
-    if (d2 < 0.0 && !is_zero(d2)) {
+    ccd_real d2 = vdot(vcross(v1, v3), v0);
+    if (d2 < 0 && !is_zero(d2)) {
       v2 = v3;
       cont = true;
     }
     if (!cont) {
       d2 = vdot(vcross(v3, v2), v0);
-      if (d2 < 0.0 && !is_zero(d2)) {
+      if (d2 < 0 && !is_zero(d2)) {
         v1 = v3;
         cont = true;
       }
@@ -996,7 +1119,7 @@ __device__ __forceinline__ int mpr_advance(double mpr_tol, const V3& s, int& st_
     }
   }
   if (res == 0) {
-    const V3 cr = vcross(ca, cb);
+    const CV3 cr = vcross(ca, cb);
     if (st == MPR_V1 && is_zero(vdot(cr, cr))) {
       res = 1;  // origin on v1 or on segment v0-v1
     } else {
@@ -1004,16 +1127,16 @@ __device__ __forceinline__ int mpr_advance(double mpr_tol, const V3& s, int& st_
       if (st == MPR_V1) {
         st = MPR_V2;
       } else if (post_swap) {
-        if (vdot(dir, v0) > 0.0) {
-          const V3 t = v1;
+        if (vdot(dir, v0) > 0) {
+          const CV3 t = v1;
           v1 = v2;
           v2 = t;
-          dir = vscale(dir, -1.0);
+          dir = vscale(dir, ccd_real(-1));
         }
         st = MPR_V3;
       } else if (post_encl) {  // portalEncapsulesOrigin
-        const double d = vdot(dir, v1);
-        if (is_zero(d) || d > 0.0) res = 1;
+        const ccd_real d = vdot(dir, v1);
+        if (is_zero(d) || d > 0) res = 1;
       }
     }
   }
@@ -1028,20 +1151,21 @@ __device__ __forceinline__ int mpr_advance(double mpr_tol, const V3& s, int& st_
 
 // ccdMPRIntersect's start: findOrigin (v0 = centre difference, nudged off the
 // origin) and discoverPortal's first direction
-__device__ __forceinline__ void mpr_begin(const V3& ca, const V3& cb, int& st, V3& v0, V3& dir) {
+__device__ __forceinline__ void mpr_begin(const CV3& ca, const CV3& cb, int& st, CV3& v0, CV3& dir) {
   v0 = vsub(ca, cb);
-  if (vec_is_origin(v0)) v0 = vadd(v0, mpg::v3(kCcdEps * 10.0, 0.0, 0.0));
-  dir = vnormalize(vscale(v0, -1.0));
+  if (vec_is_origin(v0)) v0 = vadd(v0, cv3(kCcdEps * ccd_real(10), 0.0, 0.0));
+  dir = vnormalize(vscale(v0, ccd_real(-1)));
   st = MPR_V1;
 }
 
 // libccd support of (box with per-lane half sizes h) - (uniform shape b)
-__device__ __forceinline__ V3 msupport_box(const GObj& a, const double* h, const DevWorld& w, cptr<double> HV,
-                                           const GObj& b, const V3& dir) {
-  const V3 da = quat_rot(dir, a.rot_inv), db = quat_rot(vscale(dir, -1.0), b.rot_inv);
-  const V3 la = v3((da.x >= 0 ? 1.0 : -1.0) * h[0], (da.y >= 0 ? 1.0 : -1.0) * h[1], (da.z >= 0 ? 1.0 : -1.0) * h[2]);
+__device__ __forceinline__ CV3 msupport_box(const GObj& a, const ccd_real* h, const DevWorld& w, cptr<double> HV,
+                                           const GObj& b, const CV3& dir) {
+  const CV3 da = quat_rot(dir, a.rot_inv), db = quat_rot(vscale(dir, ccd_real(-1)), b.rot_inv);
+  const CV3 la = CV3{(da.x >= 0 ? ccd_real(1) : ccd_real(-1)) * h[0], (da.y >= 0 ? ccd_real(1) : ccd_real(-1)) * h[1],
+                     (da.z >= 0 ? ccd_real(1) : ccd_real(-1)) * h[2]};
   const int gb = __builtin_amdgcn_readfirstlane(b.geom), tb = __builtin_amdgcn_readfirstlane(b.type);
-  const V3 lb = support_local(w, HV, gb, tb, db);
+  const CV3 lb = support_local(w, HV, gb, tb, db);
   return vsub(vadd(quat_rot(la, a.rot), a.pos), vadd(quat_rot(lb, b.rot), b.pos));
 }
 
@@ -1062,7 +1186,9 @@ __device__ __forceinline__ bool octree_wave(const DevWorld& w, cptr<double> HV, 
   const int ts = w.geom_type[gs];
   double sc[3], se[3], Rl[9], cl[3], hq[3];
 #pragma unroll
-  for (int i = 0; i < 3; ++i) se[i] = grs[G_OBB_E + i];
+  // FCL's exact computeBV extents: with float libccd behind the gate, a leaf
+  // the gate passes only by a widening could become an MPR hit
+  for (int i = 0; i < 3; ++i) se[i] = grs[G_AABB_E + i];
 #pragma unroll
   for (int i = 0; i < 3; ++i)
     sc[i] = ((TS.R[3 * i] * grs[G_OBB_C] + TS.R[3 * i + 1] * grs[G_OBB_C + 1]) + TS.R[3 * i + 2] * grs[G_OBB_C + 2]) +
@@ -1088,7 +1214,7 @@ __device__ __forceinline__ bool octree_wave(const DevWorld& w, cptr<double> HV, 
     const V3 dl = v3((TS.R[0] * ax[0] + TS.R[3] * ax[1]) + TS.R[6] * ax[2],
                      (TS.R[1] * ax[0] + TS.R[4] * ax[1]) + TS.R[7] * ax[2],
                      (TS.R[2] * ax[0] + TS.R[5] * ax[1]) + TS.R[8] * ax[2]);
-    const V3 sp = support_local(w, HV, gs, ts, dl), sn = support_local(w, HV, gs, ts, vscale(dl, -1.0));
+    const V3 sp = support_local_exact(w, HV, gs, ts, dl), sn = support_local_exact(w, HV, gs, ts, vscale(dl, -1.0));
     double ep = 0.0, en = 0.0;
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
@@ -1097,7 +1223,9 @@ __device__ __forceinline__ bool octree_wave(const DevWorld& w, cptr<double> HV, 
       en += ax[0] * TS.R[k] * ln + ax[1] * TS.R[3 + k] * ln + ax[2] * TS.R[6 + k] * ln;
     }
     const double base = (ax[0] * (TS.p[0] - TO.p[0]) + ax[1] * (TS.p[1] - TO.p[1])) + ax[2] * (TS.p[2] - TO.p[2]);
-    const double pad = 1e-9 + 1e-12 * (std::fabs(base) + std::fabs(ep) + std::fabs(en));
+    // libccd MPR can report a leaf within kCcdFalseHitReach of the shape as
+    // touching (mpg_math.h): keep every such leaf
+    const double pad = kCcdFalseHitReach * (1.0 + 1e-3) + 1e-5 + 1e-5 * (std::fabs(base) + std::fabs(ep) + std::fabs(en));
     blo[i] = fmax(cl[i] - hq[i], base + en - pad);
     bhi[i] = fmin(cl[i] + hq[i], base + ep + pad);
     if (blo[i] > bhi[i]) return false;
@@ -1121,7 +1249,7 @@ __device__ __forceinline__ bool octree_wave(const DevWorld& w, cptr<double> HV, 
   A.type = MPG_GEOM_BOX;
   B.rot = gjk_rot_from_matrix(TS.R);
   B.rot_inv = quat_invert2(B.rot);
-  B.pos = v3(TS.p[0], TS.p[1], TS.p[2]);
+  B.pos = cv3(TS.p[0], TS.p[1], TS.p[2]);
   B.geom = gs;
   B.type = ts;
   // one candidate per wave: the leaves listed in the cells under the box
@@ -1157,14 +1285,14 @@ __device__ __forceinline__ bool octree_wave(const DevWorld& w, cptr<double> HV, 
     }
     if (ts == MPG_GEOM_SPHERE) return sphere_box_intersect(grs[G_PARAM], TS, side, TL);
     GObj A1 = A;
-    A1.pos = v3(cw[0], cw[1], cw[2]);
-    const double h[3] = {side[0] / 2.0, side[1] / 2.0, side[2] / 2.0};  // boxToGJK: side / 2
+    A1.pos = cv3(cw[0], cw[1], cw[2]);
+    const ccd_real h[3] = {(ccd_real)(side[0] / 2.0), (ccd_real)(side[1] / 2.0), (ccd_real)(side[2] / 2.0)};  // boxToGJK
     int st;
-    V3 v0, v1, v2, v3_, dir;
+    CV3 v0, v1, v2, v3_, dir;
     mpr_begin(A1.pos, center(w, B), st, v0, dir);
     int res = 0;
     while (res == 0) {
-      const V3 sp = msupport_box(A1, h, w, HV, B, dir);
+      const CV3 sp = msupport_box(A1, h, w, HV, B, dir);
       res = mpr_advance(w.mpr_tol, sp, st, v0, v1, v2, v3_, dir);
     }
     return res > 0;
@@ -1226,6 +1354,9 @@ __device__ __forceinline__ bool octree_wave(const DevWorld& w, cptr<double> HV, 
 // Same operation order as the oracle (oracle/collide_oracle.c).
 // ---------------------------------------------------------------------------
 constexpr double kMeshPad = 1e-9;
+// shape-triangle pairs run libccd MPR: a triangle it can report as touching
+// lies within kCcdFalseHitReach of the shape (mpg_math.h)
+constexpr double kMeshShapePad = kCcdFalseHitReach * (1.0 + 1e-3) + 1e-5;
 
 __device__ __forceinline__ double d3(const double* a, const double* b) { return (a[0] * b[0] + a[1] * b[1]) + a[2] * b[2]; }
 __device__ __forceinline__ void c3(double* o, const double* a, const double* b) {
@@ -1364,19 +1495,19 @@ __device__ __forceinline__ bool sphere_triangle_intersect(double radius, const d
 
 // libccd support of (uniform shape a) - (per-lane triangle b: vertices P in
 // the mesh frame, centroid tc): supportTriangle picks argmax dir . (p - c)
-__device__ __forceinline__ V3 msupport_tri(const DevWorld& w, cptr<double> HV, const GObj& a, const GObj& b,
-                                           const double* P, const V3& tc, const V3& dir) {
-  const V3 da = quat_rot(dir, a.rot_inv), db = quat_rot(vscale(dir, -1.0), b.rot_inv);
+__device__ __forceinline__ CV3 msupport_tri(const DevWorld& w, cptr<double> HV, const GObj& a, const GObj& b,
+                                            const CV3* P, const CV3& tc, const CV3& dir) {
+  const CV3 da = quat_rot(dir, a.rot_inv), db = quat_rot(vscale(dir, ccd_real(-1)), b.rot_inv);
   const int ga = __builtin_amdgcn_readfirstlane(a.geom), ta = __builtin_amdgcn_readfirstlane(a.type);
-  const V3 la = support_local(w, HV, ga, ta, da);
-  double maxdot = -DBL_MAX;
-  V3 lb = v3(P[0], P[1], P[2]);
+  const CV3 la = support_local(w, HV, ga, ta, da);
+  ccd_real maxdot = -FLT_MAX;
+  CV3 lb = P[0];
 #pragma unroll
   for (int i = 0; i < 3; ++i) {
-    const V3 pc = v3(P[3 * i] - tc.x, P[3 * i + 1] - tc.y, P[3 * i + 2] - tc.z);
-    const double dot = vdot(db, pc);
+    const CV3 pc = vsub(P[i], tc);
+    const ccd_real dot = vdot(db, pc);
     if (dot > maxdot) {
-      lb = v3(P[3 * i], P[3 * i + 1], P[3 * i + 2]);
+      lb = P[i];
       maxdot = dot;
     }
   }
@@ -1506,19 +1637,21 @@ __device__ __forceinline__ bool mesh_shape_wave(const DevWorld& w, cptr<double> 
 #pragma unroll
   for (int i = 0; i < 3; ++i)
     hq[i] = ((std::fabs(Rl[3 * i]) * grs[G_OBB_E] + std::fabs(Rl[3 * i + 1]) * grs[G_OBB_E + 1]) +
-             std::fabs(Rl[3 * i + 2]) * grs[G_OBB_E + 2]) * (1.0 + 1e-9) + kMeshPad;
+             std::fabs(Rl[3 * i + 2]) * grs[G_OBB_E + 2]) * (1.0 + 1e-9) +
+            kMeshShapePad * (1.0 + std::fabs(TS.p[0]) + std::fabs(TS.p[1]) + std::fabs(TS.p[2]) + std::fabs(TM.p[0]) +
+                             std::fabs(TM.p[1]) + std::fabs(TM.p[2]));
   GObj A, B;
   A.rot = gjk_rot_from_matrix(TS.R);
   A.rot_inv = quat_invert2(A.rot);
-  A.pos = v3(TS.p[0], TS.p[1], TS.p[2]);
+  A.pos = cv3(TS.p[0], TS.p[1], TS.p[2]);
   A.geom = gs;
   A.type = ts;
   B.rot = gjk_rot_from_matrix(TM.R);
   B.rot_inv = quat_invert2(B.rot);
-  B.pos = v3(TM.p[0], TM.p[1], TM.p[2]);
+  B.pos = cv3(TM.p[0], TM.p[1], TM.p[2]);
   B.geom = gm;
   B.type = MPG_GEOM_MESH;
-  const V3 ca = center(w, A);
+  const CV3 ca = center(w, A);
   for (int b = t0; b < t1; b += 64) {
     const int t = b + (int)lane;
     bool cand = t < t1;
@@ -1540,13 +1673,15 @@ __device__ __forceinline__ bool mesh_shape_wave(const DevWorld& w, cptr<double> 
             W[3 * v + i] = ((TM.R[3 * i] * P[3 * v] + TM.R[3 * i + 1] * P[3 * v + 1]) + TM.R[3 * i + 2] * P[3 * v + 2]) + TM.p[i];
         hit = sphere_triangle_intersect(grs[G_PARAM], TS.p, W);
       } else {
-        const V3 tc = v3((P[0] + P[3] + P[6]) / 3, (P[1] + P[4] + P[7]) / 3, (P[2] + P[5] + P[8]) / 3);
+        // triCreateGJKObject: centre in fp64, then vertices and centre as ccd_real
+        const CV3 tc = cv3((P[0] + P[3] + P[6]) / 3, (P[1] + P[4] + P[7]) / 3, (P[2] + P[5] + P[8]) / 3);
+        const CV3 TP[3] = {cv3(P[0], P[1], P[2]), cv3(P[3], P[4], P[5]), cv3(P[6], P[7], P[8])};
         int st;
-        V3 v0, v1, v2, v3_, dir;
+        CV3 v0, v1, v2, v3_, dir;
         mpr_begin(ca, vadd(quat_rot(tc, B.rot), B.pos), st, v0, dir);
         int res = 0;
         while (res == 0) {
-          const V3 sp = msupport_tri(w, HV, A, B, P, tc, dir);
+          const CV3 sp = msupport_tri(w, HV, A, B, TP, tc, dir);
           res = mpr_advance(w.mpr_tol, sp, st, v0, v1, v2, v3_, dir);
         }
         hit = res > 0;
@@ -1631,7 +1766,7 @@ __global__ __launch_bounds__(256) MPG_NARROW_WAVES void narrow_kernel(DevWorld w
     GObj A, B;
     if (!am) A = static_obj(w, a - w.n_moving);
     if (!bm) B = static_obj(w, b - w.n_moving);
-    V3 v0, v1, v2, v3, dir;
+    CV3 v0, v1, v2, v3, dir;
 #ifdef MPG_STATS
     int nsteps = 0;
 #endif
@@ -1675,7 +1810,7 @@ __global__ __launch_bounds__(256) MPG_NARROW_WAVES void narrow_kernel(DevWorld w
       unsigned long long c2 = 0;
 #endif
       if (st != MPR_DONE) {
-        const V3 s = msupport(w, HV, A, B, dir);
+        const CV3 s = msupport(w, HV, A, B, dir);
 #ifdef MPG_STATS
         ++nsteps;
 #endif
@@ -1780,7 +1915,7 @@ __global__ __launch_bounds__(256) void small_kernel(DevWorld w, const double* __
       const double cj = ((TB.R[3 * i] * rb[G_OBB_C] + TB.R[3 * i + 1] * rb[G_OBB_C + 1]) + TB.R[3 * i + 2] * rb[G_OBB_C + 2]) + TB.p[i];
       d2 += (ci - cj) * (ci - cj);
     }
-    const double rr = ra[G_RADIUS] + rb[G_RADIUS] + kSmallMargin;
+    const double rr = ra[G_RADIUS] + rb[G_RADIUS] + w.small_margin;
     const bool near = live && d2 <= rr * rr && w.debug_mode != 3 && !(w.debug_mode == 7 && d2 >= 0.0);
     if (CLS != CLS_CLOSED) {
       hit = (walk_wave_eval<CLS>(w, HV, ga, TA, gb, TB, near) >> lane) & 1ull;
@@ -1790,20 +1925,20 @@ __global__ __launch_bounds__(256) void small_kernel(DevWorld w, const double* __
       GObj A, B;
       A.rot = gjk_rot_from_matrix(TA.R);
       A.rot_inv = quat_invert2(A.rot);
-      A.pos = v3(TA.p[0], TA.p[1], TA.p[2]);
+      A.pos = cv3(TA.p[0], TA.p[1], TA.p[2]);
       A.geom = ga;
       A.type = w.geom_type[ga];
       B.rot = gjk_rot_from_matrix(TB.R);
       B.rot_inv = quat_invert2(B.rot);
-      B.pos = v3(TB.p[0], TB.p[1], TB.p[2]);
+      B.pos = cv3(TB.p[0], TB.p[1], TB.p[2]);
       B.geom = gb;
       B.type = w.geom_type[gb];
       int st = MPR_DONE;
-      V3 v0, v1, v2, v3, dir;
+      CV3 v0, v1, v2, v3, dir;
       if (near) mpr_begin(center(w, A), center(w, B), st, v0, dir);
       while (__ballot(st != MPR_DONE) != 0) {
         if (st != MPR_DONE) {
-          const V3 s = msupport(w, HV, A, B, dir);
+          const CV3 s = msupport(w, HV, A, B, dir);
           const int res = mpr_advance(w.mpr_tol, s, st, v0, v1, v2, v3, dir);
           if (res != 0) {
             hit = res > 0 ? 1 : 0;
@@ -1814,6 +1949,57 @@ __global__ __launch_bounds__(256) void small_kernel(DevWorld w, const double* __
     }
   }
   if (live) hits[(size_t)p * n + cfg] = hit;
+}
+
+// ---------------------------------------------------------------------------
+// Diagnostics: fcl::collide of two posed geometries of the world, n pose
+// pairs at a time (one lane each; the geometries are the same for the whole
+// launch, as the narrow phase's wave-uniform support scans need): the exact
+// dispatch collide() uses -- FCL closed form, octree or BVH-mesh walk, or
+// libccd MPR.  Lets tests compare the narrow phase with the oracle directly,
+// without forward kinematics (mpg_debug_collide_pairs).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void debug_pairs_kernel(DevWorld w, int ga, int gb, int cf, long long n,
+                                                         const double* __restrict__ Ta, const double* __restrict__ Tb,
+                                                         uint8_t* __restrict__ hit) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool live = i < n;
+  const long long c = live ? i : n - 1;
+  const SE3 TA = load_se3(Ta + 12 * c), TB = load_se3(Tb + 12 * c);
+  bool h = false;
+  if (cf == CF_OCTREE) {
+    h = (walk_wave_eval<CLS_OCTREE>(w, w.hull, ga, TA, gb, TB, live) >> lane_id()) & 1ull;
+  } else if (cf == CF_MESH) {
+    h = (walk_wave_eval<CLS_MESH>(w, w.hull, ga, TA, gb, TB, live) >> lane_id()) & 1ull;
+  } else if (cf != CF_NONE) {
+    h = live && closed_form(cf, w, ga, TA, gb, TB);
+  } else {
+    GObj A, B;
+    A.rot = gjk_rot_from_matrix(TA.R);
+    A.rot_inv = quat_invert2(A.rot);
+    A.pos = cv3(TA.p[0], TA.p[1], TA.p[2]);
+    A.geom = ga;
+    A.type = w.geom_type[ga];
+    B.rot = gjk_rot_from_matrix(TB.R);
+    B.rot_inv = quat_invert2(B.rot);
+    B.pos = cv3(TB.p[0], TB.p[1], TB.p[2]);
+    B.geom = gb;
+    B.type = w.geom_type[gb];
+    int st = MPR_DONE;
+    CV3 v0, v1, v2, v3, dir;
+    if (live) mpr_begin(center(w, A), center(w, B), st, v0, dir);
+    while (__ballot(st != MPR_DONE) != 0) {
+      if (st != MPR_DONE) {
+        const CV3 s = msupport(w, w.hull, A, B, dir);
+        const int res = mpr_advance(w.mpr_tol, s, st, v0, v1, v2, v3, dir);
+        if (res != 0) {
+          h = res > 0;
+          st = MPR_DONE;
+        }
+      }
+    }
+  }
+  if (live) hit[i] = h ? 1 : 0;
 }
 
 // ---------------------------------------------------------------------------
@@ -1834,7 +2020,7 @@ __global__ __launch_bounds__(128) void pose_kernel(DevWorld w, const double* __r
   const long long cfg = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (cfg >= n) return;
   auto store = [&](int m, const SE3& T) {
-    const Q4 r = gjk_rot_from_matrix(T.R);
+    const CQ4 r = gjk_rot_from_matrix(T.R);
     double* g = poses + ((size_t)m * kPoseStride) * n + cfg;  // [m][field][cfg]
     g[0 * n] = r.x;
     g[1 * n] = r.y;
@@ -2005,12 +2191,12 @@ __device__ __forceinline__ bool simplex_closest(V3 P[4], int& n, V3& v) {
 }
 
 __device__ double gjk_distance(const DevWorld& w, cptr<double> HV, const GObj& A, const GObj& B) {
-  V3 v = vsub(center(w, A), center(w, B));
+  V3 v = vsub(to_v3(center(w, A)), to_v3(center(w, B)));
   if (d3dot(v, v) == 0.0) v.x = 1e-12;
   V3 P[4];
   int n = 0;
   for (int it = 0; it < 128; ++it) {
-    const V3 wv = msupport(w, HV, A, B, V3{-v.x, -v.y, -v.z});
+    const V3 wv = to_v3(msupport(w, HV, A, B, cv3(-v.x, -v.y, -v.z)));
     const double vv = d3dot(v, v), vw = d3dot(v, wv);
     if (n > 0 && vv - vw <= 1e-12 * vv) break;
     bool dup = false;
@@ -2030,9 +2216,9 @@ __device__ __forceinline__ GObj pose_obj(const DevWorld& w, const double* __rest
   if (id < w.n_moving) {
     const double* g = poses + ((size_t)id * kPoseStride) * n + cfg;
     GObj o;
-    o.rot = Q4{g[0], g[n], g[2 * n], g[3 * n]};
+    o.rot = CQ4{(ccd_real)g[0], (ccd_real)g[n], (ccd_real)g[2 * n], (ccd_real)g[3 * n]};
     o.rot_inv = quat_invert2(o.rot);
-    o.pos = v3(g[4 * n], g[5 * n], g[6 * n]);
+    o.pos = cv3(g[4 * n], g[5 * n], g[6 * n]);
     o.geom = w.moving_geom[id];
     o.type = w.geom_type[o.geom];
     c = v3(g[7 * n], g[8 * n], g[9 * n]);
@@ -2088,33 +2274,33 @@ __global__ __launch_bounds__(128) void distance_kernel(DevWorld w, const double*
 // portal keeps each vertex's per-object support points (v1, v2) for findPos.
 // ---------------------------------------------------------------------------
 struct SupP {
-  V3 v, v1, v2;
+  CV3 v, v1, v2;
 };
 
 __device__ __forceinline__ SupP msupport3(const DevWorld& w, cptr<double> HV, const GObj& a, const GObj& b,
-                                          const V3& dir) {
+                                          const CV3& dir) {
   SupP s;
   s.v1 = support(w, HV, a, dir);
-  s.v2 = support(w, HV, b, vscale(dir, -1.0));
+  s.v2 = support(w, HV, b, vscale(dir, ccd_real(-1)));
   s.v = vsub(s.v1, s.v2);
   return s;
 }
 
-__device__ __forceinline__ V3 portal_dir3(const SupP P[4]) {
+__device__ __forceinline__ CV3 portal_dir3(const SupP P[4]) {
   return vnormalize(vcross(vsub(P[2].v, P[1].v), vsub(P[3].v, P[1].v)));
 }
 
-__device__ __forceinline__ bool reach_tol(const SupP P[4], const V3& v4, const V3& dir, double tol) {
-  const double dv1 = vdot(P[1].v, dir), dv2 = vdot(P[2].v, dir), dv3 = vdot(P[3].v, dir), dv4 = vdot(v4, dir);
-  double d1 = dv4 - dv1;
-  const double d2 = dv4 - dv2, d3 = dv4 - dv3;
+__device__ __forceinline__ bool reach_tol(const SupP P[4], const CV3& v4, const CV3& dir, ccd_real tol) {
+  const ccd_real dv1 = vdot(P[1].v, dir), dv2 = vdot(P[2].v, dir), dv3 = vdot(P[3].v, dir), dv4 = vdot(v4, dir);
+  ccd_real d1 = dv4 - dv1;
+  const ccd_real d2 = dv4 - dv2, d3 = dv4 - dv3;
   d1 = (d1 < d2) ? d1 : d2;
   d1 = (d1 < d3) ? d1 : d3;
   return ccd_eq(d1, tol) || d1 < tol;
 }
 
 __device__ __forceinline__ void expand3(SupP P[4], const SupP& v4) {
-  const V3 v4v0 = vcross(v4.v, P[0].v);
+  const CV3 v4v0 = vcross(v4.v, P[0].v);
   if (vdot(P[1].v, v4v0) > 0.0) {
     if (vdot(P[2].v, v4v0) > 0.0) P[1] = v4;
     else P[3] = v4;
@@ -2124,9 +2310,9 @@ __device__ __forceinline__ void expand3(SupP P[4], const SupP& v4) {
   }
 }
 
-__device__ __forceinline__ double seg_dist2(const V3& x0, const V3& b, V3& wit) {
-  const V3 d = vsub(b, x0), a = x0;  // P = origin
-  double t = -1.0 * vdot(a, d);
+__device__ __forceinline__ ccd_real seg_dist2(const CV3& x0, const CV3& b, CV3& wit) {
+  const CV3 d = vsub(b, x0), a = x0;  // P = origin
+  ccd_real t = -1.0 * vdot(a, d);
   t /= vdot(d, d);
   if (t < 0.0 || is_zero(t)) {
     wit = x0;
@@ -2139,11 +2325,11 @@ __device__ __forceinline__ double seg_dist2(const V3& x0, const V3& b, V3& wit) 
 }
 
 // ccdVec3PointTriDist2(origin, x0, B, C, witness)
-__device__ __forceinline__ double tri_dist2(const V3& x0, const V3& B, const V3& C, V3& wit) {
-  const V3 d1 = vsub(B, x0), d2 = vsub(C, x0), a = x0;
-  const double v = vdot(d1, d1), w_ = vdot(d2, d2), p = vdot(a, d1), q = vdot(a, d2), r = vdot(d1, d2);
-  const double d = w_ * v - r * r;
-  double s, t;
+__device__ __forceinline__ ccd_real tri_dist2(const CV3& x0, const CV3& B, const CV3& C, CV3& wit) {
+  const CV3 d1 = vsub(B, x0), d2 = vsub(C, x0), a = x0;
+  const ccd_real v = vdot(d1, d1), w_ = vdot(d2, d2), p = vdot(a, d1), q = vdot(a, d2), r = vdot(d1, d2);
+  const ccd_real d = w_ * v - r * r;
+  ccd_real s, t;
   if (is_zero(d)) {
     s = t = -1.0;
   } else {
@@ -2155,9 +2341,9 @@ __device__ __forceinline__ double tri_dist2(const V3& x0, const V3& B, const V3&
     wit = vadd(vadd(x0, vscale(d1, s)), vscale(d2, t));
     return vdot(wit, wit);
   }
-  V3 w2;
-  double dist = seg_dist2(x0, B, wit);
-  double dist2 = seg_dist2(x0, C, w2);
+  CV3 w2;
+  ccd_real dist = seg_dist2(x0, B, wit);
+  ccd_real dist2 = seg_dist2(x0, C, w2);
   if (dist2 < dist) {
     dist = dist2;
     wit = w2;
@@ -2170,14 +2356,14 @@ __device__ __forceinline__ double tri_dist2(const V3& x0, const V3& B, const V3&
   return dist;
 }
 
-__device__ __forceinline__ V3 find_pos3(const SupP P[4]) {
-  const V3 dir = portal_dir3(P);
-  double b[4];
+__device__ __forceinline__ CV3 find_pos3(const SupP P[4]) {
+  const CV3 dir = portal_dir3(P);
+  ccd_real b[4];
   b[0] = vdot(vcross(P[1].v, P[2].v), P[3].v);
   b[1] = vdot(vcross(P[3].v, P[2].v), P[0].v);
   b[2] = vdot(vcross(P[0].v, P[1].v), P[3].v);
   b[3] = vdot(vcross(P[2].v, P[1].v), P[0].v);
-  double sum = b[0] + b[1] + b[2] + b[3];
+  ccd_real sum = b[0] + b[1] + b[2] + b[3];
   if (is_zero(sum) || sum < 0.0) {
     b[0] = 0.0;
     b[1] = vdot(vcross(P[2].v, P[3].v), dir);
@@ -2185,35 +2371,35 @@ __device__ __forceinline__ V3 find_pos3(const SupP P[4]) {
     b[3] = vdot(vcross(P[1].v, P[2].v), dir);
     sum = b[1] + b[2] + b[3];
   }
-  const double inv = 1.0 / sum;
-  V3 p1{0, 0, 0}, p2{0, 0, 0};
+  const ccd_real inv = ccd_real(1) / sum;
+  CV3 p1{0, 0, 0}, p2{0, 0, 0};
   for (int i = 0; i < 4; ++i) {
     p1 = vadd(p1, vscale(P[i].v1, b[i]));
     p2 = vadd(p2, vscale(P[i].v2, b[i]));
   }
   p1 = vscale(p1, inv);
   p2 = vscale(p2, inv);
-  return vscale(vadd(p1, p2), 0.5);
+  return vscale(vadd(p1, p2), ccd_real(0.5));
 }
 
 // ccdMPRPenetration: true if penetrating (depth, dir, pos set)
-__device__ bool mpr_penetration(const DevWorld& w, cptr<double> HV, const GObj& A, const GObj& B, double& depth,
-                                V3& dir_out, V3& pos_out) {
+__device__ bool mpr_penetration_ccd(const DevWorld& w, cptr<double> HV, const GObj& A, const GObj& B, ccd_real& depth,
+                                    CV3& dir_out, CV3& pos_out) {
   SupP P[4];
   P[0].v1 = center(w, A);
   P[0].v2 = center(w, B);
   P[0].v = vsub(P[0].v1, P[0].v2);
-  if (vec_is_origin(P[0].v)) P[0].v = vadd(P[0].v, mpg::v3(kCcdEps * 10.0, 0.0, 0.0));
-  V3 dir = vnormalize(vscale(P[0].v, -1.0));
+  if (vec_is_origin(P[0].v)) P[0].v = vadd(P[0].v, cv3(kCcdEps * ccd_real(10), 0.0, 0.0));
+  CV3 dir = vnormalize(vscale(P[0].v, ccd_real(-1)));
   P[1] = msupport3(w, HV, A, B, dir);
-  double dot = vdot(P[1].v, dir);
+  ccd_real dot = vdot(P[1].v, dir);
   if (is_zero(dot) || dot < 0.0) return false;
   dir = vcross(P[0].v, P[1].v);
   if (is_zero(vdot(dir, dir))) {
-    pos_out = vscale(vadd(P[1].v1, P[1].v2), 0.5);
+    pos_out = vscale(vadd(P[1].v1, P[1].v2), ccd_real(0.5));
     if (vec_is_origin(P[1].v)) {  // findPenetrTouch
       depth = 0.0;
-      dir_out = mpg::v3(0.0, 0.0, 0.0);
+      dir_out = cv3(0.0, 0.0, 0.0);
     } else {  // findPenetrSegment
       dir_out = P[1].v;
       depth = std::sqrt(vdot(dir_out, dir_out));
@@ -2230,14 +2416,14 @@ __device__ bool mpr_penetration(const DevWorld& w, cptr<double> HV, const GObj& 
     const SupP t = P[1];
     P[1] = P[2];
     P[2] = t;
-    dir = vscale(dir, -1.0);
+    dir = vscale(dir, ccd_real(-1));
   }
   for (;;) {
     P[3] = msupport3(w, HV, A, B, dir);
     dot = vdot(P[3].v, dir);
     if (is_zero(dot) || dot < 0.0) return false;
     bool cont = false;
-    double d2 = vdot(vcross(P[1].v, P[3].v), P[0].v);
+    ccd_real d2 = vdot(vcross(P[1].v, P[3].v), P[0].v);
     if (d2 < 0.0 && !is_zero(d2)) {
       P[2] = P[3];
       cont = true;
@@ -2255,10 +2441,10 @@ __device__ bool mpr_penetration(const DevWorld& w, cptr<double> HV, const GObj& 
   // refinePortal
   for (;;) {
     dir = portal_dir3(P);
-    const double d = vdot(dir, P[1].v);
+    const ccd_real d = vdot(dir, P[1].v);
     if (is_zero(d) || d > 0.0) break;
     const SupP v4 = msupport3(w, HV, A, B, dir);
-    const double dv4 = vdot(v4.v, dir);
+    const ccd_real dv4 = vdot(v4.v, dir);
     if (!(is_zero(dv4) || dv4 > 0.0) || reach_tol(P, v4.v, dir, w.mpr_tol)) return false;
     expand3(P, v4);
   }
@@ -2267,14 +2453,28 @@ __device__ bool mpr_penetration(const DevWorld& w, cptr<double> HV, const GObj& 
     dir = portal_dir3(P);
     const SupP v4 = msupport3(w, HV, A, B, dir);
     if (reach_tol(P, v4.v, dir, w.mpr_tol) || it > 500UL) {
-      V3 wit;
+      CV3 wit;
       depth = std::sqrt(tri_dist2(P[1].v, P[2].v, P[3].v, wit));
-      dir_out = is_zero(depth) ? mpg::v3(0.0, 0.0, 0.0) : vnormalize(wit);
+      dir_out = is_zero(depth) ? cv3(0.0, 0.0, 0.0) : vnormalize(wit);
       pos_out = find_pos3(P);
       return true;
     }
     expand3(P, v4);
   }
+}
+
+// FCL reads the contact back into fp64 (Contact<double>)
+__device__ bool mpr_penetration(const DevWorld& w, cptr<double> HV, const GObj& A, const GObj& B, double& depth,
+                                V3& dir_out, V3& pos_out) {
+  ccd_real d = 0;
+  CV3 n{0, 0, 0}, ps{0, 0, 0};
+  const bool hit = mpr_penetration_ccd(w, HV, A, B, d, n, ps);
+  if (hit) {
+    depth = d;
+    dir_out = to_v3(n);
+    pos_out = to_v3(ps);
+  }
+  return hit;
 }
 
 template <bool FROM_POSES>
@@ -2428,6 +2628,8 @@ __global__ void sincos_kernel(const double* __restrict__ x, long long n, double*
 struct mpg_world {
   int device = 0;
   DevWorld dw{};
+  int n_geoms = 0;
+  std::vector<int> geom_type_h;  // host copy of the geometry kinds (diagnostics)
   void* blob = nullptr;
   size_t blob_bytes = 0;
   int block = 128;
@@ -2622,6 +2824,24 @@ int validate(const mpg_world_desc* d) {
           (int64_t)d->geom_vertex_start[g] + d->geom_vertex_count[g] > d->n_vertices)
         return set_error(MPG_E_INVALID, "convex vertex range out of bounds");
     }
+    if (t == MPG_GEOM_CONVEX) {  // faces (FCL layout) inside convex_face, indices inside the hull
+      const double f0 = d->geom_param[4 * g], fn = d->geom_param[4 * g + 1];
+      if (!(f0 >= 0 && fn >= 0 && f0 == std::floor(f0) && fn == std::floor(fn)))
+        return set_error(MPG_E_INVALID, "convex face range out of bounds");
+      if (fn > 0) {
+        if (!d->convex_face) return set_error(MPG_E_INVALID, "bad convex face array");
+        int64_t i = (int64_t)f0;
+        for (int64_t f = 0; f < (int64_t)fn; ++f) {
+          if (i >= d->n_convex_face_ints) return set_error(MPG_E_INVALID, "convex face range out of bounds");
+          const int cnt = d->convex_face[i];
+          if (cnt < 1 || i + cnt >= d->n_convex_face_ints) return set_error(MPG_E_INVALID, "convex face range out of bounds");
+          for (int k = 1; k <= cnt; ++k)
+            if (d->convex_face[i + k] < 0 || d->convex_face[i + k] >= d->geom_vertex_count[g])
+              return set_error(MPG_E_INVALID, "convex face vertex index out of range");
+          i += cnt + 1;
+        }
+      }
+    }
     if (t == MPG_GEOM_MESH) {
       const double t0 = d->geom_param[4 * g], tn = d->geom_param[4 * g + 1];
       if (!(t0 >= 0 && tn >= 0 && t0 == std::floor(t0) && tn == std::floor(tn) && t0 + tn <= (double)d->n_mesh_triangles))
@@ -2730,6 +2950,7 @@ void geom_record(const mpg_world_desc* d, int g, double* rec) {
     const double e = 0.5 * (hi[k] - lo[k]);
     rec[G_OBB_C + k] = c;
     rec[G_OBB_E + k] = e * (1.0 + 1e-12) + 1e-12;
+    rec[G_AABB_E + k] = (hi[k] - lo[k]) * 0.5;
     r2 += rec[G_OBB_E + k] * rec[G_OBB_E + k];
   }
   if (t == MPG_GEOM_CONVEX || t == MPG_GEOM_MESH) {  // bounding sphere about the box centre: farthest vertex
@@ -2755,8 +2976,8 @@ void geom_record(const mpg_world_desc* d, int g, double* rec) {
 
 void static_record(const mpg_world_desc* d, int s, const double* geom_rec_all, double* rec) {
   const double* T = d->static_transform + 12 * s;
-  const Q4 r = gjk_rot_from_matrix(T);
-  const Q4 ri = quat_invert2(r);
+  const CQ4 r = gjk_rot_from_matrix(T);  // the ccd_real rotation MPR uses
+  const CQ4 ri = quat_invert2(r);
   rec[S_ROT] = r.x; rec[S_ROT + 1] = r.y; rec[S_ROT + 2] = r.z; rec[S_ROT + 3] = r.w;
   rec[S_ROTINV] = ri.x; rec[S_ROTINV + 1] = ri.y; rec[S_ROTINV + 2] = ri.z; rec[S_ROTINV + 3] = ri.w;
   rec[S_POS] = T[9]; rec[S_POS + 1] = T[10]; rec[S_POS + 2] = T[11];
@@ -3056,15 +3277,31 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
   // hulls in AoSoA-4 groups, padded with copies of the hull's first vertex
   std::vector<int> gstart(std::max(d->n_geoms, 1), 0), ngroups(std::max(d->n_geoms, 1), 0);
   std::vector<double> hull;
-  std::vector<int> cbase(std::max(d->n_geoms, 1), -1);
-  std::vector<double> cell_rec, cell_ovf;
+  std::vector<int> cbase(std::max(d->n_geoms, 1), -1), geom_nbr(std::max(d->n_geoms, 1), -1), hull_nbr;
+  std::vector<double> cell_rec, cell_ovf, wcell_rec, wcell_ovf;
   for (int g = 0; g < d->n_geoms; ++g) {
     if (d->geom_type[g] != MPG_GEOM_CONVEX) continue;
-    std::vector<uint32_t> cstart;
-    std::vector<double> cpts;
-    if (build_hull_cells(d->vertices + 3 * (size_t)d->geom_vertex_start[g], d->geom_vertex_count[g], cstart, cpts)) {
-      cbase[g] = (int)(cell_rec.size() / kCellRec);
-      pack_cell_records(cstart.data(), cpts.data(), cell_rec, cell_ovf);
+    const double* Vg = d->vertices + 3 * (size_t)d->geom_vertex_start[g];
+    const int nvg = d->geom_vertex_count[g];
+    // FCL 0.7.0 Convex: neighbour walk for > 32 vertices with valid faces
+    std::vector<int> enc;
+    const int nf = (int)d->geom_param[4 * g + 1];
+    const bool walk = nf > 0 && fcl_convex_neighbors(nvg, d->convex_face + (int64_t)d->geom_param[4 * g], nf, enc);
+    if (walk) {
+      if (nvg > kMaxWalkVerts)
+        return set_error(MPG_E_UNSUPPORTED, "convex hull with more than 512 vertices and watertight faces "
+                                            "(FCL's neighbour-walk support) is not supported on the device");
+      geom_nbr[g] = (int)hull_nbr.size();
+      hull_nbr.insert(hull_nbr.end(), enc.begin(), enc.end());
+      const size_t r0 = wcell_rec.size();
+      if (build_walk_cells(Vg, nvg, enc.data(), wcell_rec, wcell_ovf)) cbase[g] = (int)(r0 / kWalkRec);
+    } else {
+      std::vector<uint32_t> cstart;
+      std::vector<double> cpts;
+      if (build_hull_cells(Vg, nvg, cstart, cpts)) {
+        cbase[g] = (int)(cell_rec.size() / kCellRec);
+        pack_cell_records(cstart.data(), cpts.data(), cell_rec, cell_ovf);
+      }
     }
     const double* V = d->vertices + 3 * (size_t)d->geom_vertex_start[g];
     const int nv = d->geom_vertex_count[g], ng = (nv + 3) / 4;
@@ -3080,6 +3317,9 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
   if (hull.empty()) hull.assign(12, 0.0);
   if (cell_rec.empty()) cell_rec.assign(kCellRec, 0.0);
   if (cell_ovf.empty()) cell_ovf.assign(4, 0.0);
+  if (hull_nbr.empty()) hull_nbr.assign(1, 0);
+  if (wcell_rec.empty()) wcell_rec.assign(kWalkRec, 0.0);
+  if (wcell_ovf.empty()) wcell_ovf.assign(kWalkEnt, 0.0);
   // octrees: leaf boxes + a uniform grid per octree geometry (cells of at
   // least the largest leaf, <= 64 per axis); a leaf is listed in every cell
   // its box overlaps
@@ -3215,6 +3455,10 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
   const size_t o_cb = bb.add(cbase.data(), cbase.size());
   const size_t o_crec = bb.add(cell_rec.data(), cell_rec.size());
   const size_t o_covf = bb.add(cell_ovf.data(), cell_ovf.size());
+  const size_t o_gnb = bb.add(geom_nbr.data(), geom_nbr.size());
+  const size_t o_hnb = bb.add(hull_nbr.data(), hull_nbr.size());
+  const size_t o_wrec = bb.add(wcell_rec.data(), wcell_rec.size());
+  const size_t o_wovf = bb.add(wcell_ovf.data(), wcell_ovf.size());
   const size_t o_ml = bb.add(d->moving_link, d->n_moving);
   const size_t o_mg = bb.add(d->moving_geom, d->n_moving);
   const size_t o_mo = bb.add(d->moving_offset, 12 * (size_t)d->n_moving);
@@ -3254,6 +3498,8 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
 
   mpg_world* w = new mpg_world();
   w->device = device;
+  w->n_geoms = d->n_geoms;
+  w->geom_type_h.assign(d->geom_type, d->geom_type + d->n_geoms);
   w->block = block;
   w->lds_bytes = lds;
   w->blob_bytes = bb.bytes.size();
@@ -3279,6 +3525,20 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
   dw.n_pairs = d->n_pairs;
   dw.W = W;
   dw.mpr_tol = d->gjk_tolerance;
+  {  // culling margins: pairs that can reach libccd MPR (directly, on octree
+     // leaves or on mesh triangles) keep everything within its false-hit reach
+    bool may_mpr = false;
+    for (int p = 0; p < d->n_pairs; ++p) {
+      if (allowed[p]) continue;
+      const int ta = obj_geom_type(d, d->pair_a[p]), tb = obj_geom_type(d, d->pair_b[p]);
+      const bool closed = pair_cf[p] != CF_NONE && cf_class(pair_cf[p]) == CLS_CLOSED;
+      const bool mesh_mesh = ta == MPG_GEOM_MESH && tb == MPG_GEOM_MESH;
+      may_mpr |= !closed && !mesh_mesh;
+    }
+    const double reach = kCcdFalseHitReach * (1.0 + 1e-3) + 1e-5;
+    dw.bp_margin = may_mpr ? (float)std::max((double)kBpMargin, reach) : kBpMargin;
+    dw.small_margin = may_mpr ? std::max(kSmallMargin, reach) : kSmallMargin;
+  }
   dw.debug_mode = std::getenv("MPG_DEBUG_CULL") ? std::atoi(std::getenv("MPG_DEBUG_CULL")) : 0;
   dw.stats = nullptr;
   if (std::getenv("MPG_STATS") && std::atoi(std::getenv("MPG_STATS")) > 0) {
@@ -3303,6 +3563,10 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
   dw.geom_cbase = to_cptr<int>(base + o_cb);
   dw.cell_rec = to_cptr<double>(base + o_crec);
   dw.cell_ovf = to_cptr<double>(base + o_covf);
+  dw.geom_nbr = to_cptr<int>(base + o_gnb);
+  dw.hull_nbr = to_cptr<int>(base + o_hnb);
+  dw.wcell_rec = to_cptr<double>(base + o_wrec);
+  dw.wcell_ovf = to_cptr<double>(base + o_wovf);
   dw.moving_link = to_cptr<int>(base + o_ml);
   dw.moving_geom = to_cptr<int>(base + o_mg);
   dw.moving_offset = to_cptr<double>(base + o_mo);
@@ -3819,6 +4083,45 @@ int mpg_fk_batch(mpg_world* w, const double* q, int64_t n, double* link_pose, in
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipMemcpyAsync(link_pose, w->d_out, sizeof(double) * nout, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
+  return MPG_OK;
+}
+
+int mpg_debug_collide_pairs(mpg_world* w, int32_t geom_a, int32_t geom_b, int64_t n, const double* Ta,
+                            const double* Tb, uint8_t* hit) {
+  if (!w || n < 0 || (n > 0 && (!Ta || !Tb || !hit))) return set_error(MPG_E_INVALID, "bad arguments");
+  if (geom_a < 0 || geom_b < 0 || geom_a >= w->n_geoms || geom_b >= w->n_geoms)
+    return set_error(MPG_E_INVALID, "geometry index out of range");
+  if (n == 0) return MPG_OK;
+  const int ta = w->geom_type_h[geom_a], tb = w->geom_type_h[geom_b];
+  int cf = CF_NONE;
+  if (ta == MPG_GEOM_MESH || tb == MPG_GEOM_MESH) cf = CF_MESH;
+  else if (ta == MPG_GEOM_OCTREE || tb == MPG_GEOM_OCTREE) cf = CF_OCTREE;
+  else if (ta == MPG_GEOM_BOX && tb == MPG_GEOM_BOX) cf = CF_BOX_BOX;
+  else if (ta == MPG_GEOM_SPHERE && tb == MPG_GEOM_SPHERE) cf = CF_SPHERE_SPHERE;
+  else if (ta == MPG_GEOM_SPHERE && tb == MPG_GEOM_BOX) cf = CF_SPHERE_BOX;
+  else if (ta == MPG_GEOM_BOX && tb == MPG_GEOM_SPHERE) cf = CF_BOX_SPHERE;
+  else if (ta == MPG_GEOM_SPHERE && tb == MPG_GEOM_CAPSULE) cf = CF_SPHERE_CAPSULE;
+  else if (ta == MPG_GEOM_CAPSULE && tb == MPG_GEOM_SPHERE) cf = CF_CAPSULE_SPHERE;
+  else if (ta == MPG_GEOM_SPHERE && tb == MPG_GEOM_CYLINDER) cf = CF_SPHERE_CYLINDER;
+  else if (ta == MPG_GEOM_CYLINDER && tb == MPG_GEOM_SPHERE) cf = CF_CYLINDER_SPHERE;
+  if ((cf == CF_OCTREE && ta == tb) || (cf == CF_MESH && (ta == MPG_GEOM_OCTREE || tb == MPG_GEOM_OCTREE)))
+    return set_error(MPG_E_UNSUPPORTED, "geometry pair not supported");
+  HIP_TRY(hipSetDevice(w->device));
+  double *dA = nullptr, *dB = nullptr;
+  uint8_t* dh = nullptr;
+  HIP_TRY(hipMalloc(&dA, sizeof(double) * 12 * n));
+  HIP_TRY(hipMalloc(&dB, sizeof(double) * 12 * n));
+  HIP_TRY(hipMalloc(&dh, (size_t)n));
+  HIP_TRY(hipMemcpy(dA, Ta, sizeof(double) * 12 * n, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(dB, Tb, sizeof(double) * 12 * n, hipMemcpyHostToDevice));
+  // (walk_wave_eval finds the octree / mesh argument itself)
+  hipLaunchKernelGGL(debug_pairs_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, 0, w->dw, geom_a, geom_b, cf,
+                     (long long)n, dA, dB, dh);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpy(hit, dh, (size_t)n, hipMemcpyDeviceToHost));
+  hipFree(dA);
+  hipFree(dB);
+  hipFree(dh);
   return MPG_OK;
 }
 

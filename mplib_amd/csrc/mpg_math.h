@@ -377,64 +377,109 @@ MPG_INLINE void axis_rot(const double* ax, double c, double s, double* R) {
 }
 
 // --------------------------------------------------------------------------
-// libccd 2.1 vec3 / quat (ccd/vec3.h, ccd/quat.h)
+// libccd 2.1 vec3 / quat (ccd/vec3.h, ccd/quat.h) over its scalar ccd_real_t.
+// The reference's libccd is a bare `cmake ..` build of v2.1
+// (docker/Dockerfile:16-20), whose ENABLE_DOUBLE_PRECISION option defaults to
+// OFF: ccd_real_t = float, CCD_EPS = FLT_EPSILON, and FCL 0.7.0's glue
+// converts the doubles it hands over (object poses, support points, the MPR
+// tolerance) to float.  MPG_CCD_DOUBLE builds the double-precision variant
+// (oracle variant "ccd_double", DESIGN.md "Oracle variants").
+// V3T<double> (V3) serves the fp64 code outside libccd.
 // --------------------------------------------------------------------------
-struct V3 {
-  double x, y, z;
+#ifdef MPG_CCD_DOUBLE
+using ccd_real = double;
+constexpr ccd_real kCcdEps = 2.220446049250313080847e-16;  // DBL_EPSILON
+#else
+using ccd_real = float;
+constexpr ccd_real kCcdEps = 1.19209289550781250e-7f;  // FLT_EPSILON
+#endif
+
+// Reach of libccd's MPR false positives (DESIGN.md "Broad-phase soundness"):
+// discoverPortal reports "origin on segment v0-v1" (intersect) when
+// |v0 x v1|^2 < CCD_EPS.  v0 (centre difference) and the point x where the
+// segment v0-v1 crosses the plane through the origin normal to v0 are both in
+// the Minkowski difference, so for shapes separated by D, |v0| >= D, |x| >= D
+// and |v0 x v1| >= |v0||x| >= D^2: the exit needs D < CCD_EPS^(1/4).  Every
+// other MPR exit reports intersection only within ~CCD_EPS of contact.
+// float libccd: 0.0186 m; double: 1.2e-4 m.  Culling tests keep every pair
+// within this reach (plus rounding) of touching.
+constexpr double kCcdFalseHitReach = sizeof(ccd_real) == 4 ? 0.018581 : 1.2208e-4;
+
+template <class T>
+struct V3T {
+  T x, y, z;
 };
+using V3 = V3T<double>;
+using CV3 = V3T<ccd_real>;
 
 MPG_INLINE V3 v3(double x, double y, double z) { return V3{x, y, z}; }
-MPG_INLINE V3 vsub(const V3& a, const V3& b) { return V3{a.x - b.x, a.y - b.y, a.z - b.z}; }
-MPG_INLINE V3 vadd(const V3& a, const V3& b) { return V3{a.x + b.x, a.y + b.y, a.z + b.z}; }
-MPG_INLINE V3 vscale(const V3& a, double k) { return V3{a.x * k, a.y * k, a.z * k}; }
-MPG_INLINE double vdot(const V3& a, const V3& b) {
-  double d = a.x * b.x;
+// ccdVec3Set: converts to ccd_real_t
+MPG_INLINE CV3 cv3(double x, double y, double z) { return CV3{(ccd_real)x, (ccd_real)y, (ccd_real)z}; }
+MPG_INLINE V3 to_v3(const CV3& a) { return V3{a.x, a.y, a.z}; }
+template <class T>
+MPG_INLINE V3T<T> vsub(const V3T<T>& a, const V3T<T>& b) { return V3T<T>{a.x - b.x, a.y - b.y, a.z - b.z}; }
+template <class T>
+MPG_INLINE V3T<T> vadd(const V3T<T>& a, const V3T<T>& b) { return V3T<T>{a.x + b.x, a.y + b.y, a.z + b.z}; }
+template <class T>
+MPG_INLINE V3T<T> vscale(const V3T<T>& a, T k) { return V3T<T>{a.x * k, a.y * k, a.z * k}; }
+template <class T>
+MPG_INLINE T vdot(const V3T<T>& a, const V3T<T>& b) {
+  T d = a.x * b.x;
   d += a.y * b.y;
   d += a.z * b.z;
   return d;
 }
-MPG_INLINE V3 vcross(const V3& a, const V3& b) {
-  return V3{(a.y * b.z) - (a.z * b.y), (a.z * b.x) - (a.x * b.z), (a.x * b.y) - (a.y * b.x)};
+template <class T>
+MPG_INLINE V3T<T> vcross(const V3T<T>& a, const V3T<T>& b) {
+  return V3T<T>{(a.y * b.z) - (a.z * b.y), (a.z * b.x) - (a.x * b.z), (a.x * b.y) - (a.y * b.x)};
 }
-MPG_INLINE V3 vnormalize(const V3& d) {
-  double k = 1.0 / std::sqrt(vdot(d, d));
+// ccdVec3Normalize: k = CCD_ONE / CCD_SQRT(len2)
+template <class T>
+MPG_INLINE V3T<T> vnormalize(const V3T<T>& d) {
+  const T k = T(1) / std::sqrt(vdot(d, d));
   return vscale(d, k);
 }
 
 // quaternion stored (x, y, z, w) as libccd does
-struct Q4 {
-  double x, y, z, w;
+template <class T>
+struct Q4T {
+  T x, y, z, w;
 };
+using Q4 = Q4T<double>;
+using CQ4 = Q4T<ccd_real>;
 
-MPG_INLINE V3 quat_rot(const V3& v, const Q4& q) {
-  const double vx = v.x, vy = v.y, vz = v.z;
-  const double w = q.w, x = q.x, y = q.y, z = q.z;
-  const double c1x = y * vz - z * vy + w * vx;
-  const double c1y = z * vx - x * vz + w * vy;
-  const double c1z = x * vy - y * vx + w * vz;
-  const double c2x = y * c1z - z * c1y;
-  const double c2y = z * c1x - x * c1z;
-  const double c2z = x * c1y - y * c1x;
-  return V3{vx + 2 * c2x, vy + 2 * c2y, vz + 2 * c2z};
+template <class T>
+MPG_INLINE V3T<T> quat_rot(const V3T<T>& v, const Q4T<T>& q) {
+  const T vx = v.x, vy = v.y, vz = v.z;
+  const T w = q.w, x = q.x, y = q.y, z = q.z;
+  const T c1x = y * vz - z * vy + w * vx;
+  const T c1y = z * vx - x * vz + w * vy;
+  const T c1z = x * vy - y * vx + w * vz;
+  const T c2x = y * c1z - z * c1y;
+  const T c2y = z * c1x - x * c1z;
+  const T c2z = x * c1y - y * c1x;
+  return V3T<T>{vx + T(2) * c2x, vy + T(2) * c2y, vz + T(2) * c2z};
 }
 
-MPG_INLINE Q4 quat_invert2(const Q4& q) {
-  double len2 = q.x * q.x;
+template <class T>
+MPG_INLINE Q4T<T> quat_invert2(const Q4T<T>& q) {
+  T len2 = q.x * q.x;
   len2 += q.y * q.y;
   len2 += q.z * q.z;
   len2 += q.w * q.w;
   // ccdQuatInvert returns -1 (leaving dest = src) when len2 < CCD_EPS; unit
   // quaternions from Eigen never take that branch, kept for fidelity.
-  if (len2 < 2.220446049250313080847e-16) return q;
-  len2 = 1.0 / len2;
-  return Q4{-q.x * len2, -q.y * len2, -q.z * len2, q.w * len2};
+  if (len2 < (sizeof(T) == 4 ? (T)1.19209289550781250e-7 : (T)2.220446049250313080847e-16)) return q;
+  len2 = T(1) / len2;
+  return Q4T<T>{-q.x * len2, -q.y * len2, -q.z * len2, q.w * len2};
 }
 
-// FCL shapeToGJK: Quaternion q(tf.linear()) -> rot (x,y,z,w)
-MPG_INLINE Q4 gjk_rot_from_matrix(const double* R) {
+// FCL shapeToGJK: Quaternion<double> q(tf.linear()), then
+// ccdQuatSet(&o->rot, q.x(), q.y(), q.z(), q.w()) -> ccd_real_t
+MPG_INLINE CQ4 gjk_rot_from_matrix(const double* R) {
   double w, xyz[3];
   mat_to_quat(R, &w, xyz);
-  return Q4{xyz[0], xyz[1], xyz[2], w};
+  return CQ4{(ccd_real)xyz[0], (ccd_real)xyz[1], (ccd_real)xyz[2], (ccd_real)w};
 }
 
 }  // namespace mpg

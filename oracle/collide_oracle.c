@@ -1522,7 +1522,11 @@ static int mesh_shape_intersect(const orc_world *w, int gm, const real *TM, int 
         real c[3], r;
         bsphere(Wp, 3, c, &r);
         const real d[3] = {c[0] - TS[9], c[1] - TS[10], c[2] - TS[11]};
-        if (sqrt(dot3(d, d)) > r + rs) continue;
+        /* libccd's MPR can report a triangle within CCD_EPS^(1/4) of the
+         * shape as touching (discoverPortal's |v0 x v1|^2 < CCD_EPS exit, see
+         * DESIGN.md "Broad-phase soundness"): keep every such triangle */
+        const real pad = 1.001 * sqrt(sqrt((double)CCD_EPS)) + 1e-5 * (1.0 + fabs(TS[9]) + fabs(TS[10]) + fabs(TS[11]) + fabs(TM[9]) + fabs(TM[10]) + fabs(TM[11]));
+        if (sqrt(dot3(d, d)) > r + rs + pad) continue;
         int hit;
         if (ts == GEOM_SPHERE) hit = sphere_triangle_intersect(ps[0], TS, W[0], W[1], W[2]);
         else {
@@ -1798,6 +1802,8 @@ double orc_distance_pair(const orc_world *w, int ga, const double *Ta, int gb, c
 int orc_collide_pair(const orc_world *w, int ga, const double *Ta, int gb, const double *Tb) {
     const int mh = mesh_intersect(w, ga, Ta, gb, Tb, NULL);
     if (mh >= 0) return mh;
+    if (w->geom_type[gb] == GEOM_OCTREE) return octree_intersect(w, gb, Tb, ga, Ta, NULL);
+    if (w->geom_type[ga] == GEOM_OCTREE) return octree_intersect(w, ga, Ta, gb, Tb, NULL);
     const int cf = closed_form_intersect(w, ga, Ta, gb, Tb);
     if (cf >= 0) return cf;
     gjk_obj a, b;

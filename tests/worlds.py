@@ -141,7 +141,7 @@ def desc_arrays(ow: oracle.OracleWorld) -> dict:
         qsrc.append(src)
         qconst.append(const)
     geoms = ow.geoms
-    gtype, gvs, gnv, gparam, verts, leaves, tris = [], [], [], [], [], [], []
+    gtype, gvs, gnv, gparam, verts, leaves, tris, cfaces = [], [], [], [], [], [], [], []
     nv = 0
     nl = 0
     nt = 0
@@ -168,7 +168,9 @@ def desc_arrays(ow: oracle.OracleWorld) -> dict:
             gnv.append(len(g.vertices))
             nv += len(g.vertices)
             verts.append(g.vertices.reshape(-1))
-            gparam += [0.0] * 4
+            gparam += [float(len(cfaces)), float(len(g.faces)), 0.0, 0.0]  # FCL layout faces
+            for f in g.faces:
+                cfaces += [len(f)] + [int(v) for v in f]
         elif isinstance(g, M.SphereGeom):
             gtype.append(2)
             gvs.append(0)
@@ -219,6 +221,7 @@ def desc_arrays(ow: oracle.OracleWorld) -> dict:
         pair_allowed=[1 if frozenset((p[4], p[5])) in ow.allowed else 0 for p in ow.pairs],
         octree_leaf=np.concatenate(leaves) if leaves else np.zeros(0),
         mesh_triangle=np.concatenate(tris) if tris else np.zeros(0, np.int32),
+        convex_face=np.asarray(cfaces, np.int32),
     )
 
 
