@@ -32,6 +32,7 @@ constexpr int kCellsPerHull = 6 * kCellK * kCellK;
 constexpr double kCellMin = 1e-30, kCellMax = 1e30;  // |dir| range with cells
 constexpr double kHullMin = 1e-100, kHullMax = 1e100;  // max|coord| range with cells
 constexpr double kCellWiden = 1e-5;  // cone widening: covers the fp32 cell arithmetic below
+constexpr int kSubK = 8;  // walk hulls: subcells per axis of a cell that is not trap-free
 
 // cell of direction (x, y, z), or -1 (no cell: full scan).  The range checks
 // are exact (fp64); the cell arithmetic is fp32: the ratios u/|m| are off by
@@ -60,6 +61,40 @@ MPG_INLINE int hull_cell(double x, double y, double z) {
   int iu = (int)(((float)u * inv + 1.0f) * h), iv = (int)(((float)v * inv + 1.0f) * h);
   iu = iu < 0 ? 0 : (iu >= kCellK ? kCellK - 1 : iu);
   iv = iv < 0 ? 0 : (iv >= kCellK ? kCellK - 1 : iv);
+  return ((2 * f + (m < 0.0 ? 1 : 0)) * kCellK + iu) * kCellK + iv;
+}
+
+// hull_cell plus the subcell (kSubK x kSubK per cell) of the direction: the
+// same fp32 ratios, so the direction lies in the widened subcone as well
+// (kCellWiden >> the ratio error).  -1 / sub undefined when there is no cell.
+MPG_INLINE int hull_cell_sub(double x, double y, double z, int* sub) {
+  const double ax = std::fabs(x), ay = std::fabs(y), az = std::fabs(z);
+  if (!(ax <= kCellMax && ay <= kCellMax && az <= kCellMax)) return -1;  // also NaN
+  if (!(ax >= kCellMin || ay >= kCellMin || az >= kCellMin)) return -1;
+  int f;
+  double m, u, v;
+  if (ax >= ay && ax >= az) {
+    f = 0; m = x; u = y; v = z;
+  } else if (ay >= az) {
+    f = 1; m = y; u = z; v = x;
+  } else {
+    f = 2; m = z; u = x; v = y;
+  }
+  const float am = (float)std::fabs(m);
+#if defined(__HIP_DEVICE_COMPILE__)
+  const float inv = __builtin_amdgcn_rcpf(am);
+#else
+  const float inv = 1.0f / am;
+#endif
+  const float h = 0.5f * kCellK;
+  const float fu = ((float)u * inv + 1.0f) * h, fv = ((float)v * inv + 1.0f) * h;
+  int iu = (int)fu, iv = (int)fv;
+  iu = iu < 0 ? 0 : (iu >= kCellK ? kCellK - 1 : iu);
+  iv = iv < 0 ? 0 : (iv >= kCellK ? kCellK - 1 : iv);
+  int su = (int)((fu - (float)iu) * kSubK), sv = (int)((fv - (float)iv) * kSubK);
+  su = su < 0 ? 0 : (su >= kSubK ? kSubK - 1 : su);
+  sv = sv < 0 ? 0 : (sv >= kSubK ? kSubK - 1 : sv);
+  *sub = su * kSubK + sv;
   return ((2 * f + (m < 0.0 ? 1 : 0)) * kCellK + iu) * kCellK + iv;
 }
 
@@ -245,68 +280,169 @@ inline bool fcl_convex_neighbors(int nv, const int32_t* faces, int num_faces, st
 // at w -- in vertex order, each with the neighbour beating it most often
 // (its witness).  The first maximum of the list is the global first maximum
 // (the list contains every vertex build_hull_cells keeps).
-constexpr int kWalkHead = 4;    // n, overflow offset (entries), pad, pad
-constexpr int kWalkEnt = 8;     // x, y, z, vertex index, witness x, y, z, pad
+constexpr int kWalkHead = 4;    // n, overflow offset (entries), trap-free flag, pad
+constexpr int kWalkEnt = 8;     // x, y, z, vertex index, witness x, y, z, list-neighbour mask
 constexpr int kWalkInline = 2;  // entries stored in the record itself
 constexpr int kWalkRec = kWalkHead + kWalkInline * kWalkEnt;
-inline bool build_walk_cells(const double* V, int nv, const int* nbr, std::vector<double>& rec,
+// Clip the convex polygon (u, v) by a*u + b*v + c <= 0 (Sutherland-Hodgman).
+inline void clip_poly(std::vector<std::array<double, 2>>& poly, double a, double b, double c) {
+  std::vector<std::array<double, 2>> out;
+  const size_t n = poly.size();
+  for (size_t i = 0; i < n; ++i) {
+    const auto& P = poly[i];
+    const auto& Q = poly[(i + 1) % n];
+    const double fp = a * P[0] + b * P[1] + c, fq = a * Q[0] + b * Q[1] + c;
+    if (fp <= 0) out.push_back(P);
+    if ((fp < 0 && fq > 0) || (fp > 0 && fq < 0)) {
+      const double t = fp / (fp - fq);
+      out.push_back({P[0] + t * (Q[0] - P[0]), P[1] + t * (Q[1] - P[1])});
+    }
+  }
+  poly.swap(out);
+}
+
+// A cell is trap-free when for every listed vertex w, on the part R_w of
+// the (widened) cell where no neighbour beats w (clipped polygon, each
+// neighbour half-space loosened by the rounding margin), w beats every
+// non-neighbour by the margin.  Then the walk's endpoint e (which lies in the
+// list, on R_e) is >= its neighbours and strictly above every other vertex:
+// it is the computed maximum, and when that maximum is unique it is the first
+// maximum g of the list -- the walk needs not run.  (A tie at the maximum, only
+// possible between neighbours, still takes the exact path.)
+inline bool walk_cell_trap_free(const double* V, int nv, const int* nbr, const std::vector<int>& list, int f,
+                                double sg, double u0, double u1, double v0, double v1, double X) {
+  const double rel = 1e-9, m = rel * 3.0 * X;
+  std::vector<char> adj(nv);
+  for (int w : list) {
+    const int* nb = nbr + nbr[w];
+    std::vector<std::array<double, 2>> poly = {{u0, v0}, {u1, v0}, {u1, v1}, {u0, v1}};
+    std::fill(adj.begin(), adj.end(), 0);
+    for (int k = 1; k <= nb[0] && !poly.empty(); ++k) {
+      const int u = nb[k];
+      adj[u] = 1;
+      const double a[3] = {V[3 * u] - V[3 * w], V[3 * u + 1] - V[3 * w + 1], V[3 * u + 2] - V[3 * w + 2]};
+      clip_poly(poly, a[(f + 1) % 3], a[(f + 2) % 3], sg * a[f] - m);  // d . a <= m
+    }
+    for (int k = 1; k <= nb[0]; ++k) adj[nb[k]] = 1;
+    for (const auto& pt : poly) {
+      double d[3];
+      d[f] = sg;
+      d[(f + 1) % 3] = pt[0];
+      d[(f + 2) % 3] = pt[1];
+      const double dw = d[0] * V[3 * w] + d[1] * V[3 * w + 1] + d[2] * V[3 * w + 2];
+      const double M = rel * (std::fabs(d[0]) + std::fabs(d[1]) + std::fabs(d[2])) * X;
+      for (int v = 0; v < nv; ++v) {
+        if (v == w || adj[v]) continue;
+        if (!(d[0] * V[3 * v] + d[1] * V[3 * v + 1] + d[2] * V[3 * v + 2] - dw < -M)) return false;
+      }
+    }
+  }
+  return true;
+}
+
+// One walk record for the cone spanned by face f (sign sg) over u in
+// [u0, u1], v in [v0, v1] (already widened): appended to rec (its overflow
+// entries to ovf).  Returns whether the cone is trap-free.
+inline bool walk_cone_record(const double* V, int nv, const int* nbr, int f, double sg, double u0, double u1,
+                             double v0, double v1, double X, std::vector<double>& rec, std::vector<double>& ovf) {
+  const double rel = 1e-9;
+  double r[4][3], M[4];
+  for (int k = 0; k < 4; ++k) {
+    r[k][f] = sg;
+    r[k][(f + 1) % 3] = (k & 1) ? u1 : u0;
+    r[k][(f + 2) % 3] = (k & 2) ? v1 : v0;
+    M[k] = rel * (std::fabs(r[k][0]) + std::fabs(r[k][1]) + std::fabs(r[k][2])) * X;
+  }
+  std::vector<double> P((size_t)nv * 4);
+  for (int i = 0; i < nv; ++i)
+    for (int k = 0; k < 4; ++k) P[4 * i + k] = r[k][0] * V[3 * i] + r[k][1] * V[3 * i + 1] + r[k][2] * V[3 * i + 2];
+  auto margin = [&](int u, int i) {  // > 0: u beats i on the whole cone
+    double m = DBL_MAX;
+    for (int k = 0; k < 4; ++k) m = std::min(m, P[4 * u + k] - P[4 * i + k] - M[k]);
+    return m;
+  };
+  std::vector<std::array<double, 8>> ents;
+  std::vector<int> ids;
+  for (int i = 0; i < nv; ++i) {
+    const int* nb = nbr + nbr[i];
+    int wit = -1;
+    double best = -DBL_MAX;
+    bool dominated = false;
+    for (int k = 1; k <= nb[0]; ++k) {
+      const double m = margin(nb[k], i);
+      if (m > 0.0) dominated = true;
+      if (m > best) {
+        best = m;
+        wit = nb[k];
+      }
+    }
+    if (dominated) continue;
+    if (wit < 0) wit = i;  // isolated vertex (not a walk hull then)
+    ents.push_back({V[3 * i], V[3 * i + 1], V[3 * i + 2], (double)i, V[3 * wit], V[3 * wit + 1], V[3 * wit + 2], 0.0});
+    ids.push_back(i);
+  }
+  // bit k: list entry k (k < 32) is a neighbour of this entry -- when it is
+  // the maximum and strictly above this entry, the walk cannot end here, no
+  // extra dot product needed
+  for (size_t e = 0; e < ents.size(); ++e) {
+    const int* nb = nbr + nbr[ids[e]];
+    uint32_t mask = 0;
+    for (size_t k = 0; k < ents.size() && k < 32; ++k)
+      for (int j = 1; j <= nb[0]; ++j)
+        if (nb[j] == ids[k]) mask |= 1u << k;
+    ents[e][7] = (double)mask;
+  }
+  const bool free = walk_cell_trap_free(V, nv, nbr, ids, f, sg, u0, u1, v0, v1, X);
+  const size_t r0 = rec.size();
+  rec.resize(r0 + kWalkRec, 0.0);
+  rec[r0] = (double)ents.size();
+  rec[r0 + 1] = (double)(ovf.size() / kWalkEnt);
+  rec[r0 + 2] = free ? 1.0 : 0.0;
+  rec[r0 + 3] = -1.0;  // subcell table (set by build_walk_cells)
+  for (size_t e = 0; e < ents.size(); ++e) {
+    if ((int)e < kWalkInline) {
+      for (int j = 0; j < kWalkEnt; ++j) rec[r0 + kWalkHead + kWalkEnt * e + j] = ents[e][j];
+    } else {
+      ovf.insert(ovf.end(), ents[e].begin(), ents[e].end());
+    }
+  }
+  return free;
+}
+
+// Walk-hull cell table: kCellsPerHull records (hull_cell order); a cell that
+// is not trap-free gets kSubK x kSubK subcell records (its cone cut the same
+// way, each widened by kCellWiden; record slot 3 = absolute index of the
+// first), appended after the hull's cells, so the exact walk runs only in the
+// subcells the non-convex triangulation actually traps.  rec_base: the
+// absolute record index of this hull's first cell.
+inline bool build_walk_cells(const double* V, int nv, const int* nbr, size_t rec_base, std::vector<double>& rec,
                              std::vector<double>& ovf) {
   double X = 0.0;
   for (int i = 0; i < 3 * nv; ++i) X = std::max(X, std::fabs(V[i]));
   if (nv <= 0 || !(X >= kHullMin && X <= kHullMax)) return false;
-  const double delta = kCellWiden, rel = 1e-9;
-  std::vector<double> P((size_t)nv * 4);
+  const double delta = kCellWiden, cw = 2.0 / kCellK;
+  const size_t c0 = rec.size();
+  std::vector<int> trapped;
   for (int f = 0; f < 3; ++f)
     for (int s = 0; s < 2; ++s)
       for (int iu = 0; iu < kCellK; ++iu)
         for (int iv = 0; iv < kCellK; ++iv) {
-          double r[4][3], M[4];
-          const double u0 = -1.0 + 2.0 * iu / kCellK - delta, u1 = -1.0 + 2.0 * (iu + 1) / kCellK + delta;
-          const double v0 = -1.0 + 2.0 * iv / kCellK - delta, v1 = -1.0 + 2.0 * (iv + 1) / kCellK + delta;
-          for (int k = 0; k < 4; ++k) {
-            r[k][f] = s ? -1.0 : 1.0;
-            r[k][(f + 1) % 3] = (k & 1) ? u1 : u0;
-            r[k][(f + 2) % 3] = (k & 2) ? v1 : v0;
-            M[k] = rel * (std::fabs(r[k][0]) + std::fabs(r[k][1]) + std::fabs(r[k][2])) * X;
-          }
-          for (int i = 0; i < nv; ++i)
-            for (int k = 0; k < 4; ++k) P[4 * i + k] = r[k][0] * V[3 * i] + r[k][1] * V[3 * i + 1] + r[k][2] * V[3 * i + 2];
-          auto margin = [&](int u, int i) {  // > 0: u beats i on the whole cell
-            double m = DBL_MAX;
-            for (int k = 0; k < 4; ++k) m = std::min(m, P[4 * u + k] - P[4 * i + k] - M[k]);
-            return m;
-          };
-          std::vector<std::array<double, 8>> ents;
-          for (int i = 0; i < nv; ++i) {
-            const int* nb = nbr + nbr[i];
-            int wit = -1;
-            double best = -DBL_MAX;
-            bool dominated = false;
-            for (int k = 1; k <= nb[0]; ++k) {
-              const double m = margin(nb[k], i);
-              if (m > 0.0) dominated = true;
-              if (m > best) {
-                best = m;
-                wit = nb[k];
-              }
-            }
-            if (dominated) continue;
-            if (wit < 0) wit = i;  // isolated vertex (not a walk hull then)
-            ents.push_back({V[3 * i], V[3 * i + 1], V[3 * i + 2], (double)i, V[3 * wit], V[3 * wit + 1],
-                            V[3 * wit + 2], 0.0});
-          }
-          const size_t r0 = rec.size();
-          rec.resize(r0 + kWalkRec, 0.0);
-          rec[r0] = (double)ents.size();
-          rec[r0 + 1] = (double)(ovf.size() / kWalkEnt);
-          for (size_t e = 0; e < ents.size(); ++e) {
-            if ((int)e < kWalkInline) {
-              for (int j = 0; j < kWalkEnt; ++j) rec[r0 + kWalkHead + kWalkEnt * e + j] = ents[e][j];
-            } else {
-              ovf.insert(ovf.end(), ents[e].begin(), ents[e].end());
-            }
-          }
+          const double u0 = -1.0 + cw * iu - delta, u1 = -1.0 + cw * (iu + 1) + delta;
+          const double v0 = -1.0 + cw * iv - delta, v1 = -1.0 + cw * (iv + 1) + delta;
+          if (!walk_cone_record(V, nv, nbr, f, s ? -1.0 : 1.0, u0, u1, v0, v1, X, rec, ovf))
+            trapped.push_back(((2 * f + s) * kCellK + iu) * kCellK + iv);
         }
+  for (int c : trapped) {
+    const int iv = c % kCellK, iu = (c / kCellK) % kCellK, fs = c / (kCellK * kCellK), f = fs >> 1, s = fs & 1;
+    rec[c0 + (size_t)kWalkRec * c + 3] = (double)(rec_base + (rec.size() - c0) / kWalkRec);
+    const double sw = cw / kSubK;
+    for (int su = 0; su < kSubK; ++su)
+      for (int sv = 0; sv < kSubK; ++sv) {
+        const double u0 = -1.0 + cw * iu + sw * su - delta, u1 = -1.0 + cw * iu + sw * (su + 1) + delta;
+        const double v0 = -1.0 + cw * iv + sw * sv - delta, v1 = -1.0 + cw * iv + sw * (sv + 1) + delta;
+        walk_cone_record(V, nv, nbr, f, s ? -1.0 : 1.0, u0, u1, v0, v1, X, rec, ovf);
+      }
+  }
   return true;
 }
 

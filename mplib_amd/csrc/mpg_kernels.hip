@@ -118,12 +118,17 @@ __device__ __forceinline__ V3 convex_full_scan(const DevWorld& w, cptr<double> H
 // ValidateTopology, oracle/collide_oracle.c support_convex): start at vertex
 // 0, scan the current vertex's neighbour list (FindVertexNeighbors: sorted,
 // from the faces), step to every unvisited neighbour whose value is >= the
-// best so far, until a pass moves nowhere.  The visited set is a 512-bit
-// register mask (world creation rejects larger walk hulls).  Kept out of
-// line: most supports are resolved by the cell test below without it.
-__device__ __attribute__((noinline)) V3 convex_walk(const DevWorld& w, cptr<double> HV, int geom, const V3 d) {
+// best so far, until a pass moves nowhere.  Rarely run (the cell test below
+// settles most supports), so its visited set lives in LDS -- 512 bits per
+// thread of a block of <= 256 (world creation rejects larger walk hulls) --
+// instead of registers every caller would have to reserve.
+constexpr int kWalkWords = kMaxWalkVerts / 64;
+__device__ __forceinline__ V3 convex_walk(const DevWorld& w, cptr<double> HV, int geom, const V3 d) {
+  __shared__ uint64_t s_vis[kWalkWords][256];
+  uint64_t* vis = &s_vis[0][threadIdx.x];  // word j at vis[256 * j]
   const cptr<int> nb = w.hull_nbr + w.geom_nbr[geom];
-  uint64_t vis[8] = {1ull, 0, 0, 0, 0, 0, 0, 0};
+  const int nwords = (w.geom_nvert[geom] + 63) >> 6;
+  for (int j = 0; j < nwords; ++j) vis[256 * j] = j == 0 ? 1ull : 0ull;
   double best = edot(d, hull_vertex(w, HV, geom, 0));
   int bi = 0;
   bool keep = true;
@@ -132,14 +137,10 @@ __device__ __attribute__((noinline)) V3 convex_walk(const DevWorld& w, cptr<doub
     const int start = nb[bi], cnt = nb[start];
     for (int k = start + 1; k <= start + cnt; ++k) {
       const int vi = nb[k];
-      const int wd = vi >> 6;
+      uint64_t* word = vis + 256 * (vi >> 6);
       const uint64_t m = 1ull << (vi & 63);
-      uint64_t word = 0;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) word = j == wd ? vis[j] : word;
-      if (word & m) continue;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) vis[j] = j == wd ? (vis[j] | m) : vis[j];
+      if (*word & m) continue;
+      *word |= m;
       const double dd = edot(d, hull_vertex(w, HV, geom, vi));
       if (dd >= best) {
         keep = true;
@@ -177,23 +178,40 @@ __device__ __forceinline__ V3 walk_cell_support(const DevWorld& w, cptr<double> 
   const cptr<double> ovf = w.wcell_ovf + kWalkEnt * (size_t)R[1];
   double best = -DBL_MAX;
   int g = 0;
+  bool tie = false;
   for (int k = 0; k < n; ++k) {
     const cptr<double> e = k < kWalkInline ? R + kWalkHead + kWalkEnt * k : ovf + kWalkEnt * (k - kWalkInline);
     const double dd = (d.x * e[0] + d.y * e[1]) + d.z * e[2];
+    tie = dd == best || (tie && !(dd > best));
     if (dd > best) {
       best = dd;
       g = k;
     }
+  }
+#ifdef MPG_STATS
+  if (w.stats) {
+    atomicAdd(&w.stats[10], 1ull);
+    if (R[2] != 0.0 && !tie) atomicAdd(&w.stats[11], 1ull);
+  }
+#endif
+  if ((R[2] != 0.0 && !tie) || w.debug_mode == 9) {  // trap-free cell (build_walk_cells), unique maximum
+    const cptr<double> e = g < kWalkInline ? R + kWalkHead + kWalkEnt * g : ovf + kWalkEnt * (g - kWalkInline);
+    return v3(e[0], e[1], e[2]);
   }
   bool ok = true;
   for (int k = 0; k < n && ok; ++k) {
     if (k == g) continue;
     const cptr<double> e = k < kWalkInline ? R + kWalkHead + kWalkEnt * k : ovf + kWalkEnt * (k - kWalkInline);
     const double dd = (d.x * e[0] + d.y * e[1]) + d.z * e[2];
+    // the maximum g is a neighbour of this entry and strictly above it
+    if (g < 32 && ((((uint32_t)e[7]) >> g) & 1u) && best > dd) continue;
     const double dw = (d.x * e[4] + d.y * e[5]) + d.z * e[6];
     if (dw > dd) continue;
     ok = neighbour_beats(w, HV, geom, (int)e[3], dd, d);
   }
+#ifdef MPG_STATS
+  if (w.stats) atomicAdd(&w.stats[ok ? 12 : 13], 1ull);
+#endif
   if (!ok) return convex_walk(w, HV, geom, d);
   const cptr<double> e = g < kWalkInline ? R + kWalkHead + kWalkEnt * g : ovf + kWalkEnt * (g - kWalkInline);
   return v3(e[0], e[1], e[2]);
@@ -203,11 +221,15 @@ __device__ __forceinline__ V3 walk_cell_support(const DevWorld& w, cptr<double> 
 // direction converted to Vector3<double>, findExtremeVertex in fp64).
 __device__ __forceinline__ V3 convex_support_local(const DevWorld& w, cptr<double> HV, int geom, const V3& d) {
   const int cb = w.geom_cbase[geom];
-  const int c = cb >= 0 ? hull_cell(d.x, d.y, d.z) : -1;
   if (w.geom_nbr[geom] >= 0) {  // neighbour-walk hull (wave-uniform branch)
+    int sub = 0;
+    const int c = cb >= 0 ? hull_cell_sub(d.x, d.y, d.z, &sub) : -1;
     if (c < 0) return convex_walk(w, HV, geom, d);
-    return walk_cell_support(w, HV, geom, w.wcell_rec + kWalkRec * (size_t)(cb + c), d);
+    cptr<double> R = w.wcell_rec + kWalkRec * (size_t)(cb + c);
+    if (R[3] >= 0.0) R = w.wcell_rec + kWalkRec * ((size_t)R[3] + sub);  // trapped cell: its subcell
+    return walk_cell_support(w, HV, geom, R, d);
   }
+  const int c = cb >= 0 ? hull_cell(d.x, d.y, d.z) : -1;
   if (c < 0) return convex_full_scan(w, HV, geom, d);
   double p[3];
   cell_record_support(w.cell_rec + kCellRec * (size_t)(cb + c), w.cell_ovf, d.x, d.y, d.z, p);
@@ -2709,8 +2731,12 @@ struct mpg_world {
   // half's latency-bound bucketing overlaps the other's compute
   long long overlap_min = 1 << 18;  // 0 disables (env MPG_OVERLAP_MIN)
   int overlap_parts = 2;             // env MPG_OVERLAP_PARTS
-  hipStream_t side = nullptr;
-  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  // large batches: half of the parts on a side stream (per caller stream)
+  struct Side {
+    hipStream_t side;
+    hipEvent_t fork, join;
+  };
+  std::map<hipStream_t, Side> sides;  // guarded by ws_mu
   // small-batch latency path (host buffers, n <= small_max): pinned input
   // staging + host-mapped hit bytes written by small_kernel
   long long small_max = 1024;
@@ -2721,7 +2747,8 @@ struct mpg_world {
   double* d_qmap = nullptr;    // h_q as the device sees it (zero-copy input)
   double* d_ssc = nullptr;     // latency path joint (sin, cos) [small cap * dof * 2]
   bool small_zero_copy = true; // MPG_SMALL_ZEROCOPY=0: stage through d_qs
-  size_t small_cap = 0;
+  size_t small_cap = 0;   // configurations (hit bytes per pair)
+  size_t small_qcap = 0;  // input doubles (h_q, d_qs)
 };
 
 namespace {
@@ -3286,7 +3313,8 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
     // FCL 0.7.0 Convex: neighbour walk for > 32 vertices with valid faces
     std::vector<int> enc;
     const int nf = (int)d->geom_param[4 * g + 1];
-    const bool walk = nf > 0 && fcl_convex_neighbors(nvg, d->convex_face + (int64_t)d->geom_param[4 * g], nf, enc);
+    const bool walk = nf > 0 && fcl_convex_neighbors(nvg, d->convex_face + (int64_t)d->geom_param[4 * g], nf, enc) &&
+                      !std::getenv("MPG_DEBUG_NO_WALK");  // ablation only: changes results
     if (walk) {
       if (nvg > kMaxWalkVerts)
         return set_error(MPG_E_UNSUPPORTED, "convex hull with more than 512 vertices and watertight faces "
@@ -3294,7 +3322,7 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
       geom_nbr[g] = (int)hull_nbr.size();
       hull_nbr.insert(hull_nbr.end(), enc.begin(), enc.end());
       const size_t r0 = wcell_rec.size();
-      if (build_walk_cells(Vg, nvg, enc.data(), wcell_rec, wcell_ovf)) cbase[g] = (int)(r0 / kWalkRec);
+      if (build_walk_cells(Vg, nvg, enc.data(), r0 / kWalkRec, wcell_rec, wcell_ovf)) cbase[g] = (int)(r0 / kWalkRec);
     } else {
       std::vector<uint32_t> cstart;
       std::vector<double> cpts;
@@ -3538,12 +3566,16 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
     const double reach = kCcdFalseHitReach * (1.0 + 1e-3) + 1e-5;
     dw.bp_margin = may_mpr ? (float)std::max((double)kBpMargin, reach) : kBpMargin;
     dw.small_margin = may_mpr ? std::max(kSmallMargin, reach) : kSmallMargin;
+    if (const char* m = std::getenv("MPG_DEBUG_MARGIN")) {  // ablation only: changes results
+      dw.bp_margin = (float)std::atof(m);
+      dw.small_margin = std::atof(m);
+    }
   }
   dw.debug_mode = std::getenv("MPG_DEBUG_CULL") ? std::atoi(std::getenv("MPG_DEBUG_CULL")) : 0;
   dw.stats = nullptr;
   if (std::getenv("MPG_STATS") && std::atoi(std::getenv("MPG_STATS")) > 0) {
-    HIP_TRY(hipMalloc(&dw.stats, 10 * sizeof(unsigned long long)));
-    HIP_TRY(hipMemset(dw.stats, 0, 10 * sizeof(unsigned long long)));
+    HIP_TRY(hipMalloc(&dw.stats, 16 * sizeof(unsigned long long)));
+    HIP_TRY(hipMemset(dw.stats, 0, 16 * sizeof(unsigned long long)));
   }
   dw.joint_type = to_cptr<int>(base + o_jt);
   dw.joint_parent = to_cptr<int>(base + o_jp);
@@ -3644,9 +3676,11 @@ int mpg_world_destroy(mpg_world* w) {
   if (!w) return MPG_OK;
   hipSetDevice(w->device);
   if (w->dw.stats) {
-    unsigned long long st[10];
+    unsigned long long st[16];
     hipDeviceSynchronize();
     hipMemcpy(st, w->dw.stats, sizeof(st), hipMemcpyDeviceToHost);
+    std::fprintf(stderr, "[mpg stats] walk hulls: supports %llu, trap-free fast %llu, verified %llu, full walks %llu\n",
+                 st[10], st[11], st[12], st[13]);
     std::fprintf(stderr,
                  "[mpg stats] narrow: refill %llu, support %llu, update %llu (memtime ticks, summed over waves); "
                  "steps %llu, mean active lanes/step %.1f; hits %llu (%.2f supports each), misses %llu (%.2f)\n",
@@ -3659,9 +3693,11 @@ int mpg_world_destroy(mpg_world* w) {
   if (w->h_hits) hipHostFree(w->h_hits);
   hipFree(w->d_qs);
   if (w->d_ssc) hipFree(w->d_ssc);
-  if (w->side) hipStreamDestroy(w->side);
-  if (w->ev_fork) hipEventDestroy(w->ev_fork);
-  if (w->ev_join) hipEventDestroy(w->ev_join);
+  for (auto& kv : w->sides) {
+    hipStreamDestroy(kv.second.side);
+    hipEventDestroy(kv.second.fork);
+    hipEventDestroy(kv.second.join);
+  }
   hipFree(w->d_q);
   hipFree(w->d_flags);
   hipFree(w->d_masks);
@@ -3709,8 +3745,14 @@ int mpg_world_get_info(const mpg_world* w, mpg_world_info* info) {
 }  // extern "C"
 
 namespace {
+// pinned input rows (ncfg * row doubles: q rows or link poses), hit bytes
+// (n_pairs * ncfg) and joint sincos: the input capacity is tracked in doubles,
+// since the same buffers serve q rows (dof) and link-pose rows (n_links * 7)
 int ensure_small(mpg_world* w, size_t ncfg, size_t row) {
-  if (ncfg <= w->small_cap) return MPG_OK;
+  const size_t want_q = ncfg * std::max<size_t>(row, 1);
+  if (ncfg <= w->small_cap && want_q <= w->small_qcap) return MPG_OK;
+  ncfg = std::max(ncfg, w->small_cap);
+  const size_t qcap = std::max(want_q, w->small_qcap);
   if (w->h_q) hipHostFree(w->h_q);
   if (w->h_hits) hipHostFree(w->h_hits);
   if (w->d_qs) hipFree(w->d_qs);
@@ -3720,15 +3762,16 @@ int ensure_small(mpg_world* w, size_t ncfg, size_t row) {
   w->h_hits = nullptr;
   w->d_qs = nullptr;
   w->small_cap = 0;
+  w->small_qcap = 0;
   const size_t P = (size_t)std::max(w->dw.n_pairs, 1);
-  HIP_TRY(hipHostMalloc((void**)&w->h_q, sizeof(double) * ncfg * std::max<size_t>(row, 1),
-                        hipHostMallocMapped | hipHostMallocCoherent));
+  HIP_TRY(hipHostMalloc((void**)&w->h_q, sizeof(double) * qcap, hipHostMallocMapped | hipHostMallocCoherent));
   HIP_TRY(hipHostGetDevicePointer((void**)&w->d_qmap, w->h_q, 0));
   HIP_TRY(hipHostMalloc((void**)&w->h_hits, P * ncfg, hipHostMallocMapped | hipHostMallocCoherent));
   HIP_TRY(hipHostGetDevicePointer((void**)&w->d_hits, w->h_hits, 0));
-  HIP_TRY(hipMalloc(&w->d_qs, sizeof(double) * ncfg * std::max<size_t>(row, 1)));
+  HIP_TRY(hipMalloc(&w->d_qs, sizeof(double) * qcap));
   HIP_TRY(hipMalloc(&w->d_ssc, sizeof(double) * 2 * ncfg * std::max<int>(w->dw.dof, 1)));
   w->small_cap = ncfg;
+  w->small_qcap = qcap;
   return MPG_OK;
 }
 
@@ -3795,29 +3838,38 @@ template <bool FROM_POSES>
 int launch_collide_overlapped(mpg_world* w, const double* in, long long n, uint8_t* flags, uint32_t* masks,
                               hipStream_t s) {
   if (w->overlap_min <= 0 || n < w->overlap_min) return launch_collide<FROM_POSES>(w, in, n, flags, masks, s);
+  // one side stream and fork/join event pair per caller stream: callers on
+  // different streams (one host thread each, include/mpgpu.h) never record
+  // into or wait on each other's events, and each side stream has its own
+  // workspace (get_workspace keys by stream)
+  mpg_world::Side sd;
   {
     std::lock_guard<std::mutex> lk(w->ws_mu);
-    if (!w->side) {
-      HIP_TRY(hipStreamCreateWithFlags(&w->side, hipStreamNonBlocking));
-      HIP_TRY(hipEventCreateWithFlags(&w->ev_fork, hipEventDisableTiming));
-      HIP_TRY(hipEventCreateWithFlags(&w->ev_join, hipEventDisableTiming));
+    auto it = w->sides.find(s);
+    if (it == w->sides.end()) {
+      mpg_world::Side n{};
+      HIP_TRY(hipStreamCreateWithFlags(&n.side, hipStreamNonBlocking));
+      HIP_TRY(hipEventCreateWithFlags(&n.fork, hipEventDisableTiming));
+      HIP_TRY(hipEventCreateWithFlags(&n.join, hipEventDisableTiming));
+      it = w->sides.emplace(s, n).first;
     }
+    sd = it->second;
   }
   const size_t row = FROM_POSES ? (size_t)w->dw.n_links * 7 : (size_t)w->dw.dof;
   // parts alternate between the caller's stream and the side stream
   const int parts = std::max(2, w->overlap_parts);
   const long long step = ((n + parts - 1) / parts + 63) / 64 * 64;
-  HIP_TRY(hipEventRecord(w->ev_fork, s));
-  HIP_TRY(hipStreamWaitEvent(w->side, w->ev_fork, 0));
+  HIP_TRY(hipEventRecord(sd.fork, s));
+  HIP_TRY(hipStreamWaitEvent(sd.side, sd.fork, 0));
   int k = 0;
   for (long long off = 0; off < n; off += step, ++k) {
     const long long m = std::min(step, n - off);
     const int rc = launch_collide<FROM_POSES>(w, in + (size_t)off * row, m, flags + off,
-                                              masks ? masks + (size_t)off * w->dw.W : nullptr, (k & 1) ? w->side : s);
+                                              masks ? masks + (size_t)off * w->dw.W : nullptr, (k & 1) ? sd.side : s);
     if (rc) return rc;
   }
-  HIP_TRY(hipEventRecord(w->ev_join, w->side));
-  HIP_TRY(hipStreamWaitEvent(s, w->ev_join, 0));
+  HIP_TRY(hipEventRecord(sd.join, sd.side));
+  HIP_TRY(hipStreamWaitEvent(s, sd.join, 0));
   return MPG_OK;
 }
 

@@ -267,23 +267,7 @@ class OracleWorld:
                 ginterior += [0.0] * 3
             else:
                 raise TypeError(f"oracle: unsupported geometry {type(g)}")
-        names = [o.link for o in art.objects]
-        pairs = []  # (ka, ia, kb, ib, name1, name2)
-        for a, b in art.pairs:
-            pairs.append((KIND_ROBOT, a, KIND_ROBOT, b, names[a], names[b]))
-        for k, att in enumerate(self.attached):
-            for i in range(len(art.objects)):
-                pairs.append((KIND_ATTACHED, k, KIND_ROBOT, i, names[i], att[0]))
-        for k in range(len(self.attached)):
-            for k2 in range(k):
-                pairs.append((KIND_ATTACHED, k, KIND_ATTACHED, k2, self.attached[k][0], self.attached[k2][0]))
-        self.n_self_pairs = len(pairs)
-        for s, sc in enumerate(self.scene):
-            for i in range(len(art.objects)):
-                pairs.append((KIND_ROBOT, i, KIND_SCENE, s, names[i], sc[0]))
-        for k, att in enumerate(self.attached):
-            for s, sc in enumerate(self.scene):
-                pairs.append((KIND_ATTACHED, k, KIND_SCENE, s, att[0], sc[0]))
+        pairs, self.n_self_pairs = self._pair_table()
         self.pairs = pairs
         kinds = {KIND_ROBOT: [o.geom for o in art.objects], KIND_ATTACHED: [a[2] for a in self.attached],
                  KIND_SCENE: [sc[1] for sc in self.scene]}
@@ -359,6 +343,31 @@ class OracleWorld:
         self.geoms = geoms
         self.dof = len(mg)
 
+    def _pair_table(self):
+        """(pairs, n_self) in PlanningWorldTpl::selfCollide then
+        collideWithOthers order for one planned articulation
+        (src/planning_world.cpp:277-481); entries (ka, ia, kb, ib, name1,
+        name2) keep fcl::collide's (o1, o2) argument order."""
+        art = self.art
+        names = [o.link for o in art.objects]
+        pairs = []
+        for a, b in art.pairs:
+            pairs.append((KIND_ROBOT, a, KIND_ROBOT, b, names[a], names[b]))
+        for k, att in enumerate(self.attached):
+            for i in range(len(art.objects)):
+                pairs.append((KIND_ATTACHED, k, KIND_ROBOT, i, names[i], att[0]))
+        for k in range(len(self.attached)):
+            for k2 in range(k):
+                pairs.append((KIND_ATTACHED, k, KIND_ATTACHED, k2, self.attached[k][0], self.attached[k2][0]))
+        n_self = len(pairs)
+        for s, sc in enumerate(self.scene):
+            for i in range(len(art.objects)):
+                pairs.append((KIND_ROBOT, i, KIND_SCENE, s, names[i], sc[0]))
+        for k, att in enumerate(self.attached):
+            for s, sc in enumerate(self.scene):
+                pairs.append((KIND_ATTACHED, k, KIND_SCENE, s, att[0], sc[0]))
+        return pairs, n_self
+
     # ------------------------------------------------------------------
     def collide_batch(self, q: np.ndarray, nthreads: int = 1, want_stats: bool = False, variant: str = ""):
         """flags[n], masks[n, W].  ``variant`` names an oracle-variant build
@@ -427,3 +436,114 @@ class OracleWorld:
             if (int(mask_row[p >> 5]) >> (p & 31)) & 1:
                 out.append((pr[4], pr[5]))
         return out
+
+
+class _MergedArticulation:
+    """Several articulations as ONE kinematic forest for the C restatement:
+    each articulation's pinocchio joints, frames, user joints/links, user qpos
+    and collision objects appended with their indices offset (a root joint's
+    parent stays the universe, so oMi = liMi as in its own model).  The move
+    group -- setQposAll's state -- is the planned articulations' move groups
+    concatenated in the given (std::map name) order; unplanned articulations
+    and non-move-group joints keep their current qpos."""
+
+    def __init__(self, parts):
+        from types import SimpleNamespace
+        joints, names, frames, objects = [None], ["universe"], [M.PinFrame("universe", "FIXED_JOINT", 0, M.IDENT)], []
+        self.user_joints, self.link_frames, self.obj_user_link, self.current_qpos = [], [], [], []
+        self.obj_base, self.user_link_base, self.qpos_base = {}, {}, {}
+        nq = nv = 0
+        mg = []
+        for name, art, planned in parts:
+            jo, fo = len(joints) - 1, len(frames) - 1  # art joint j >= 1 -> jo + j; frame f >= 1 -> fo + f
+            for j in art.pin.joints[1:]:
+                joints.append(M.PinJoint(j.name, j.jtype, j.parent + jo if j.parent > 0 else 0, j.placement, j.axis,
+                                         j.idx_q + nq, j.nq, j.nv, j.lower, j.upper))
+                names.append(j.name)
+            for f in art.pin.frames[1:]:
+                frames.append(M.PinFrame(f.name, f.ftype, f.parent + jo if f.parent > 0 else 0, f.placement))
+            self.qpos_base[name] = len(self.current_qpos)
+            self.user_link_base[name] = len(self.link_frames)
+            self.obj_base[name] = len(objects)
+            self.user_joints += [j + jo if j > 0 else 0 for j in art.user_joints]
+            self.link_frames += [f + fo if f > 0 else 0 for f in art.link_frames]
+            self.obj_user_link += [self.user_link_base[name] + u for u in art.obj_user_link]
+            objects += art.objects
+            if planned:
+                mg += [self.qpos_base[name] + i for i in art.move_group_qpos_index()]
+            self.current_qpos += list(art.current_qpos)
+            nq += art.pin.nq
+            nv += art.pin.nv
+        self.pin = SimpleNamespace(joints=joints, names=names, frames=frames, nq=nq, nv=nv)
+        self.objects = objects
+        self.nv = len(self.current_qpos)
+        self._mg = mg
+
+    def move_group_qpos_index(self):
+        return list(self._mg)
+
+
+class MultiOracleWorld(OracleWorld):
+    """PlanningWorld with several articulations (reference
+    src/planning_world.cpp:250-481): ``arts`` = [(name, Articulation,
+    planned)] -- the planned ones in std::map (name) order, the unplanned in
+    the order collideWithOthers iterates them; ``attached`` = [(name,
+    art name, user link index, geom, pose)].  Pairs are matched with the
+    product by (object names, link names), see ``pair_keys``."""
+
+    def __init__(self, arts, scene=(), attached=(), allowed=()):
+        self.parts = list(arts)
+        merged = _MergedArticulation(self.parts)
+        self.att_art = [a[1] for a in attached]
+        att = [(a[0], merged.user_link_base[a[1]] + a[2], a[3], a[4]) for a in attached]
+        super().__init__(merged, scene=scene, attached=att, allowed=allowed)
+
+    def _pair_table(self):
+        m = self.art
+        planned = [(n, a) for n, a, p in self.parts if p]
+        unplanned = [(n, a) for n, a, p in self.parts if not p]
+        pairs, keys = [], []
+
+        def add(ka, ia, kb, ib, n1, n2, on1, on2):
+            pairs.append((ka, ia, kb, ib, n1, n2))
+            keys.append((on1, on2, n1, n2))
+
+        def links(a):
+            return [o.link for o in a.objects]
+
+        for ai, (an, A) in enumerate(planned):  # selfCollide
+            base, ln = m.obj_base[an], links(A)
+            for a, b in A.pairs:
+                add(KIND_ROBOT, base + a, KIND_ROBOT, base + b, ln[a], ln[b], an, an)
+            for bn, B in planned[:ai]:
+                b0, ln2 = m.obj_base[bn], links(B)
+                for i in range(len(ln)):
+                    for j in range(len(ln2)):
+                        add(KIND_ROBOT, base + i, KIND_ROBOT, b0 + j, ln[i], ln2[j], an, bn)
+            for k, att in enumerate(self.attached):
+                for i in range(len(ln)):
+                    add(KIND_ATTACHED, k, KIND_ROBOT, base + i, ln[i], att[0], an, att[0])
+        for k in range(len(self.attached)):
+            for k2 in range(k):
+                n1, n2 = self.attached[k][0], self.attached[k2][0]
+                add(KIND_ATTACHED, k, KIND_ATTACHED, k2, n1, n2, n1, n2)
+        n_self = len(pairs)
+        for an, A in planned:  # collideWithOthers
+            base, ln = m.obj_base[an], links(A)
+            for bn, B in unplanned:
+                b0, ln2 = m.obj_base[bn], links(B)
+                for i in range(len(ln)):
+                    for j in range(len(ln2)):
+                        add(KIND_ROBOT, base + i, KIND_ROBOT, b0 + j, ln[i], ln2[j], an, bn)
+            for s, sc in enumerate(self.scene):
+                for i in range(len(ln)):
+                    add(KIND_ROBOT, base + i, KIND_SCENE, s, ln[i], sc[0], an, sc[0])
+        for k, att in enumerate(self.attached):
+            for bn, B in unplanned:
+                b0, ln2 = m.obj_base[bn], links(B)
+                for i in range(len(ln2)):
+                    add(KIND_ATTACHED, k, KIND_ROBOT, b0 + i, att[0], ln2[i], att[0], bn)
+            for s, sc in enumerate(self.scene):
+                add(KIND_ATTACHED, k, KIND_SCENE, s, att[0], sc[0], att[0], sc[0])
+        self.pair_keys = keys
+        return pairs, n_self
