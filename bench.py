@@ -33,10 +33,14 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+# VALU issue: a wave issues one VALU instruction per 2 cycles on its SIMD
+# (MI355X_MICROARCH.md "Wave scheduling"); 1024 SIMDs at 2.4 GHz.  FP64 VALU
+# instructions run at half the FP32 rate (78.6 TF vs 157.3 TF vector, spec):
+# they occupy the issue port twice as long.
+SIMDS, CLOCK_HZ, VALU_ISSUE_CYCLES = 1024, 2.4e9, 2
 STAGES = ("cull", "bucket", "narrow")  # MPG_STAGE_* (include/mpgpu.h)
 KERNEL_NAME = {"cull": "cull_kernel", "bucket": "pair_scan/chunk_scan/scatter",
                "narrow": "narrow stage (narrow_kernel + closed_form_kernel instances)"}
-FP64_VALU_PEAK_TFLOPS = 78.6  # MI355X spec (vector FP64; FMA counted as 2)
 
 
 def parse():
@@ -52,7 +56,8 @@ def parse():
     p.add_argument("--per-gpu", type=int, default=0, help="configs per GPU per step (default: BASELINE size)")
     p.add_argument("--cpu-sample", type=int, default=1 << 17,
                    help="configs timed on the CPU oracle for cpu_baseline (rank 0, N=1 only; 0 = skip)")
-    p.add_argument("--cpu-threads", type=int, default=1)
+    p.add_argument("--cpu-threads", type=int, default=0,
+                   help="threads of the all-core CPU baseline (0: the box's share, OMP_NUM_THREADS or nproc)")
     p.add_argument("--gather", action="store_true", help="also time an all-gather of the results to every rank")
     return p.parse_args()
 
@@ -143,24 +148,34 @@ def main():
 
     total = n * world * args.steps
     value = total / elapsed
-    # algorithmic bytes per unit (DESIGN.md "Roofline"):
-    #   cull:   per configuration  q row in + flag + pair-mask zeroing (8*dof + 1 + 4W)
-    #           + survivor words out (4W)
-    #   narrow: per candidate      candidate index + q row + mask word read-modify-write + flag
-    bytes_per_unit = {"cull": 8 * dim + 1 + 4 * W + 4 * W, "narrow": 4 + 8 * dim + 8 + 1,
-                      "bucket": 4 * W * 3 + 4 * (n_pairs + 1)}
+    # roofline of the dominant kernel (DESIGN.md "Measurement"): achieved =
+    # SURVEY.md 8(d)'s algorithmic bytes per configuration (q row 8*dof + flag 1
+    # + pair mask 4W: 77 B for cfg3) x the configurations one launch covers,
+    # over that kernel's average duration (HIP events on its launch stream)
+    bytes_per_config = 8 * dim + 1 + 4 * W
     dom = max(("cull", "narrow"), key=lambda k: st[k]["ms_per_launch"])
-    units = st[dom]["units_per_launch"]
-    achieved_gbps = bytes_per_unit[dom] * units / (st[dom]["ms_per_launch"] * 1e-3) / 1e9
-    traffic = None
-    pmc_file = os.path.join(ROOT, "profiles", f"pmc_cfg{cfg}.json")
-    if os.path.exists(pmc_file):
-        try:
-            pm = json.load(open(pmc_file))
-            if pm.get("configs_per_launch") == int(st["cull"]["units_per_launch"]) and dom in pm.get("hbm_bytes_per_launch", {}):
-                traffic = pm["hbm_bytes_per_launch"][dom]
-        except Exception:
-            traffic = None
+    cfg_per_launch = st["cull"]["units_per_launch"]  # both stages run once per batch part
+    kernel_s = st[dom]["ms_per_launch"] * 1e-3
+    achieved_gbps = bytes_per_config * cfg_per_launch / kernel_s / 1e9
+    traffic, valu = None, None
+    pm = pmc_record(cfg)
+    if pm is not None and pm.get("configs_per_launch") == int(cfg_per_launch):
+        k = pm.get("kernels", {}).get(dom, {})
+        traffic = k.get("hbm_bytes")
+        if "SQ_INSTS_VALU" in k:
+            f64 = sum(k.get(c, 0.0) for c in ("SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_FMA_F64",
+                                                "SQ_INSTS_VALU_TRANS_F64"))
+            # the PMC kernel is the dominant stage's main kernel (narrow_kernel / cull_kernel); its duration is
+            # the live event time of the stage launch
+            issue_s = (k["SQ_INSTS_VALU"] + f64) * VALU_ISSUE_CYCLES / (SIMDS * CLOCK_HZ)
+            valu = {"bound": "valu", "achieved": issue_s / kernel_s, "peak": 1.0, "unit": "issue-port fraction",
+                    "frac": issue_s / kernel_s, "valu_insts_per_launch": k["SQ_INSTS_VALU"],
+                    "fp64_insts_per_launch": f64,
+                    "lane_activity": (k["SQ_THREAD_CYCLES_VALU"] / (64.0 * k["SQ_ACTIVE_INST_VALU"])
+                                      if k.get("SQ_ACTIVE_INST_VALU") else None),
+                    "wait_frac": (k["SQ_WAIT_ANY"] / k["SQ_WAVE_CYCLES"] if k.get("SQ_WAVE_CYCLES") else None),
+                    "note": "VALU instructions x 2 issue cycles (fp64 counted twice) over 1024 SIMDs x 2.4 GHz "
+                            "x the kernel's live duration; PMC counts from " + pm.get("source", "?")}
 
     result = {
         "metric": "configs/sec full collide() Panda-7DoF+10 boxes" if cfg == 3 else f"configs/sec collide() cfg{cfg}",
@@ -183,10 +198,12 @@ def main():
         "roofline": {"bound": "hbm", "achieved": achieved_gbps, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": achieved_gbps / HBM_PEAK_GBPS, "traffic": traffic,
                      "kernel": KERNEL_NAME[dom], "kernel_ms": st[dom]["ms_per_launch"],
-                     "units_per_launch": units, "unit_kind": "configs" if dom == "cull" else "candidates",
-                     "algorithmic_bytes_per_unit": bytes_per_unit[dom],
-                     "note": "the path is fp32/fp64-VALU and latency bound, not HBM bound (DESIGN.md); "
-                             "HBM fraction reported as mandated"},
+                     "units_per_launch": cfg_per_launch, "unit_kind": "configs",
+                     "algorithmic_bytes_per_unit": bytes_per_config,
+                     "note": "SURVEY.md 8(d) bytes per configuration; the path is VALU and latency bound, not HBM "
+                             "bound (DESIGN.md), see valu_roofline"},
+        "valu_roofline": valu,
+        "lib_hash": lib_hash(),
         "stages": {k: {"ms_per_step": st[k]["ms_per_launch"] * st[k]["launches_per_step"],
                        "units_per_launch": st[k]["units_per_launch"]} for k in STAGES},
         "step_ms_events": step_ms,
@@ -196,7 +213,8 @@ def main():
 
     if rank == 0 and world == 1 and args.cpu_sample > 0:
         k = args.cpu_sample if cfg != 7 else min(args.cpu_sample, 1 << 13)  # the mesh oracle is ~100x slower
-        result["cpu_baseline"] = cpu_baseline(cfg, q_host[:k], flags, masks, args.cpu_threads)
+        threads = args.cpu_threads or box_threads()
+        result["cpu_baseline"] = cpu_baseline(cfg, q_host[:k], flags, masks, threads)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:
@@ -269,11 +287,28 @@ def plan_main(args, world, rank, local, backend):
                      "note": "one validity batch per planner iteration: round-trip latency, not bandwidth, "
                              "bounds a plan"},
     }
+    # the validity round trip the planner pays per batch: one state, host buffers
+    one = np.array([scenes.PLAN_START])
+    for _ in range(20):
+        w.collide_batch(one)
+    rt = []
+    for _ in range(300):
+        t1 = time.perf_counter()
+        w.collide_batch(one)
+        rt.append(time.perf_counter() - t1)
+    result_rt = {"one_state_round_trip_us_median": float(np.median(rt) * 1e6),
+                 "one_state_round_trip_us_p90": float(np.percentile(rt, 90) * 1e6)}
     if rank == 0 and world == 1 and args.cpu_plans > 0:
+        import ctypes
         sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import oracle  # test infrastructure: the CPU baseline's checker
         import worlds as Wd  # test fixture module: the oracle-built cfg3 world
         ow = Wd.oracle_world(3)
-        cpu = pymp.ompl.OMPLPlanner(scenes.world(3)[0], state_validity_checker=lambda s: ow.collide_batch(s)[0] == 0)
+        cpu = pymp.ompl.OMPLPlanner(scenes.world(3)[0])
+        # C-level checker (oracle orc_validity_batch): no Python per validity call, as OMPL's
+        # C++ StateValidityChecker would be called by the reference
+        cpu.set_native_state_validity_checker(ctypes.cast(oracle.lib().orc_validity_batch, ctypes.c_void_p).value,
+                                              ctypes.addressof(ow._w))
         cpu.set_speculative_connect(False)  # OMPL's serial loop: one batch per growTree
         k = min(args.cpu_plans, args.steps)
         same = True
@@ -284,9 +319,11 @@ def plan_main(args, world, rank, local, backend):
             same &= bool(np.array_equal(path, paths[i]))
         dt = time.perf_counter() - t0
         result["cpu_baseline"] = {"value": k / dt, "unit": "plans/s", "cores": 1, "kind": "port",
-                                  "sample": f"seeds 0..{k - 1}: the same planner with oracle/collide_oracle.c as "
-                                            f"its checker, one batch per growTree call, {dt:.1f} s",
-                                  "gpu_matches_cpu_on_sample": same}
+                                  "sample": f"seeds 0..{k - 1}: the same planner with oracle/collide_oracle.c "
+                                            f"(orc_validity_batch, called from C++) as its checker, OMPL's serial "
+                                            f"loop (one check per growTree step), {dt:.1f} s",
+                                  "cpu_model": cpu_model(), "gpu_matches_cpu_on_sample": same}
+    result.update(result_rt)
     sys.stdout.flush()
     os.dup2(saved_stdout, 1)
     if rank == 0:
@@ -295,23 +332,69 @@ def plan_main(args, world, rank, local, backend):
         dist.destroy_process_group()
 
 
+def lib_hash() -> str:
+    """sha256 (16 hex) of the HIP library this run loaded: profiles are keyed by it."""
+    import hashlib
+    p = os.path.join(ROOT, "mplib_amd", "lib", "libmpgpu.so")
+    return hashlib.sha256(open(p, "rb").read()).hexdigest()[:16] if os.path.exists(p) else ""
+
+
+def pmc_record(cfg):
+    """profiles/pmc_cfg<cfg>.json (tools/pmc_summary.py) when it was collected
+    with this very library build, else None."""
+    f = os.path.join(ROOT, "profiles", f"pmc_cfg{cfg}.json")
+    try:
+        pm = json.load(open(f))
+    except (OSError, ValueError):
+        return None
+    return pm if pm.get("lib_hash") == lib_hash() else None
+
+
+def box_threads() -> int:
+    """The host cores this job may use: OMP_NUM_THREADS (16 per GPU on the
+    GPU pool) or nproc."""
+    try:
+        return max(1, int(os.environ.get("OMP_NUM_THREADS", "0"))) if os.environ.get("OMP_NUM_THREADS") else \
+            len(os.sched_getaffinity(0))
+    except (ValueError, AttributeError):
+        return os.cpu_count() or 1
+
+
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(cfg, q_sample, flags, masks, threads):
     """The CPU restatement of MPlib's PlanningWorld::collide (oracle/) timed on
-    this host on a bounded sample; also cross-checks the GPU results on it."""
+    this host: one core (the reference's execution model) on a bounded sample,
+    and `threads` cores on the whole sample; also cross-checks the GPU results."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import worlds as Wd  # test fixture module: oracle-built world of the same config
 
     ow = Wd.oracle_world(cfg)
-    ow.collide_batch(q_sample[:256], nthreads=threads)  # warm
+    k = len(q_sample)
+    k1 = max(256, k // 8)
+    ow.collide_batch(q_sample[:256], nthreads=1)  # warm
+    t0 = time.perf_counter()
+    ow.collide_batch(q_sample[:k1], nthreads=1)
+    dt1 = time.perf_counter() - t0
     t0 = time.perf_counter()
     fo, mo = ow.collide_batch(q_sample, nthreads=threads)
     dt = time.perf_counter() - t0
-    k = len(q_sample)
     parity = bool(np.array_equal(fo, flags[:k].cpu().numpy()) and
                   np.array_equal(mo, masks[:k].cpu().numpy().view(np.uint32)))
     return {"value": k / dt, "unit": "configs/s", "cores": threads, "kind": "port",
+            "single_core": {"value": k1 / dt1, "unit": "configs/s", "cores": 1,
+                            "sample": f"first {k1} configs, {dt1:.1f} s"},
+            "cpu_model": cpu_model(), "nproc": os.cpu_count(),
             "sample": f"first {k} configs of the rank-0 batch, oracle/collide_oracle.c (C restatement of "
-                      f"FK + FCL/libccd MPR + PlanningWorld loops), {threads} thread(s), {dt:.1f} s",
+                      f"FK + FCL/libccd MPR + PlanningWorld loops) on {threads} threads, {dt:.1f} s",
             "gpu_matches_cpu_on_sample": parity}
 
 

@@ -765,6 +765,20 @@ PYBIND11_MODULE(pymp, m_all) {
            py::arg("world"), py::arg("state_validity_checker") = py::none(),
            "OMPL planner over the planned articulations' move-group joints. State validity runs as batched "
            "device collide() calls; state_validity_checker (f(states[n, dim]) -> valid[n]) replaces it.")
+      .def("set_native_state_validity_checker",
+           [](OMPLPlanner& p, uintptr_t fn, uintptr_t ctx) {
+             // a C validity checker: int fn(void* ctx, const double* states, int64_t n, uint8_t* valid)
+             // (0 = ok), called without Python in the loop, as OMPL calls a C++ StateValidityChecker
+             using Fn = int (*)(void*, const double*, int64_t, uint8_t*);
+             if (!fn) throw std::invalid_argument("null checker");
+             Fn f = reinterpret_cast<Fn>(fn);
+             void* c = reinterpret_cast<void*>(ctx);
+             p.set_state_validity_checker([f, c](const double* st, int64_t n, uint8_t* valid) {
+               if (f(c, st, n, valid) != 0) throw std::runtime_error("native state validity checker failed");
+             });
+           },
+           py::arg("fn_address"), py::arg("ctx_address"),
+           "Replace the device checker by a C function int fn(ctx, states[n*dim], n, valid[n]) (0 = ok).")
       .def("get_world", &OMPLPlanner::get_world)
       .def("set_speculative_connect", &OMPLPlanner::set_speculative_connect, py::arg("enable") = true,
            "RRTConnect: validate the extension and the whole speculative connect chain in one batch (default), "

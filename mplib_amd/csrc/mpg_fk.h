@@ -49,11 +49,13 @@ struct DevWorld {
   cptr<double> cell_ovf;     // list entries beyond the inline ones: x, y, z, 0
   // FCL 0.7.0 neighbour-walk hulls (mpg_hullcells.h): geom_nbr[g] = start of
   // the hull's neighbors_ encoding in hull_nbr, -1 = linear support; their
-  // cell records (kWalkRec doubles, indexed by geom_cbase) and overflow entries
+  // cell records (kCellRec doubles, indexed by geom_cbase), overflow entries
   cptr<int> geom_nbr;
   cptr<int> hull_nbr;
   cptr<double> wcell_rec;
   cptr<double> wcell_ovf;
+  cptr<double> wcell_aux;  // trapped (sub)cells' verification data (mpg_hullcells.h)
+  int walk_subk;           // subcells per axis of a trapped cell
   cptr<int> moving_link;     // [n_moving]
   cptr<int> moving_geom;
   cptr<double> moving_offset;  // [n_moving*12]

@@ -20,6 +20,7 @@
 #include <cfloat>
 #include <cmath>
 #include <cstdint>
+#include <cstring>
 #include <algorithm>
 #include <array>
 #include <vector>
@@ -32,7 +33,7 @@ constexpr int kCellsPerHull = 6 * kCellK * kCellK;
 constexpr double kCellMin = 1e-30, kCellMax = 1e30;  // |dir| range with cells
 constexpr double kHullMin = 1e-100, kHullMax = 1e100;  // max|coord| range with cells
 constexpr double kCellWiden = 1e-5;  // cone widening: covers the fp32 cell arithmetic below
-constexpr int kSubK = 8;  // walk hulls: subcells per axis of a cell that is not trap-free
+constexpr int kSubK = 8;  // walk hulls: default subcells per axis of a cell that is not trap-free
 
 // cell of direction (x, y, z), or -1 (no cell: full scan).  The range checks
 // are exact (fp64); the cell arithmetic is fp32: the ratios u/|m| are off by
@@ -67,7 +68,7 @@ MPG_INLINE int hull_cell(double x, double y, double z) {
 // hull_cell plus the subcell (kSubK x kSubK per cell) of the direction: the
 // same fp32 ratios, so the direction lies in the widened subcone as well
 // (kCellWiden >> the ratio error).  -1 / sub undefined when there is no cell.
-MPG_INLINE int hull_cell_sub(double x, double y, double z, int* sub) {
+MPG_INLINE int hull_cell_sub(double x, double y, double z, int subk, int* sub) {
   const double ax = std::fabs(x), ay = std::fabs(y), az = std::fabs(z);
   if (!(ax <= kCellMax && ay <= kCellMax && az <= kCellMax)) return -1;  // also NaN
   if (!(ax >= kCellMin || ay >= kCellMin || az >= kCellMin)) return -1;
@@ -91,10 +92,10 @@ MPG_INLINE int hull_cell_sub(double x, double y, double z, int* sub) {
   int iu = (int)fu, iv = (int)fv;
   iu = iu < 0 ? 0 : (iu >= kCellK ? kCellK - 1 : iu);
   iv = iv < 0 ? 0 : (iv >= kCellK ? kCellK - 1 : iv);
-  int su = (int)((fu - (float)iu) * kSubK), sv = (int)((fv - (float)iv) * kSubK);
-  su = su < 0 ? 0 : (su >= kSubK ? kSubK - 1 : su);
-  sv = sv < 0 ? 0 : (sv >= kSubK ? kSubK - 1 : sv);
-  *sub = su * kSubK + sv;
+  int su = (int)((fu - (float)iu) * (float)subk), sv = (int)((fv - (float)iv) * (float)subk);
+  su = su < 0 ? 0 : (su >= subk ? subk - 1 : su);
+  sv = sv < 0 ? 0 : (sv >= subk ? subk - 1 : sv);
+  *sub = su * subk + sv;
   return ((2 * f + (m < 0.0 ? 1 : 0)) * kCellK + iu) * kCellK + iv;
 }
 
@@ -277,13 +278,22 @@ inline bool fcl_convex_neighbors(int nv, const int32_t* faces, int num_faces, st
 // -- a vertex w is left out only when one of its neighbours u beats it on every
 // corner ray by the margin of build_hull_cells, so u's rounded dot product is
 // strictly above w's for every direction of the cell and the walk never stops
-// at w -- in vertex order, each with the neighbour beating it most often
-// (its witness).  The first maximum of the list is the global first maximum
-// (the list contains every vertex build_hull_cells keeps).
-constexpr int kWalkHead = 4;    // n, overflow offset (entries), trap-free flag, pad
-constexpr int kWalkEnt = 8;     // x, y, z, vertex index, witness x, y, z, list-neighbour mask
-constexpr int kWalkInline = 2;  // entries stored in the record itself
-constexpr int kWalkRec = kWalkHead + kWalkInline * kWalkEnt;
+// at w -- in vertex order.  The first maximum of the list is the global first
+// maximum (the list contains every vertex build_hull_cells keeps).
+// Record layout (kCellRec doubles, like the linear hulls' records): three
+// entries inline (x, y, z; short lists padded with their first entry), then
+//   slot 9   n + 256 * (overflow offset, entries of 4 doubles x, y, z, 0),
+//   slot 10  0, or k + 1: verification data at aux entry k (kWalkAux doubles
+//            per list entry: vertex index, witness neighbour x, y, z -- the
+//            neighbour beating it on most of the cell -- and the mask of the
+//            list entries that are its neighbours),
+//   slot 11  the bits (uint64) of the trap-free mask: bit s set when subcell s
+//            (kSubK x kSubK per cell, hull_cell_sub order) is trap-free
+//            (walk_cell_trap_free on the subcell's own list); all ones for a
+//            trap-free cell.  In a trap-free subcell the unique maximum of the
+//            cell's list is the walk's endpoint (the list contains every
+//            possible maximum of the cell).
+constexpr int kWalkAux = 5;
 // Clip the convex polygon (u, v) by a*u + b*v + c <= 0 (Sutherland-Hodgman).
 inline void clip_poly(std::vector<std::array<double, 2>>& poly, double a, double b, double c) {
   std::vector<std::array<double, 2>> out;
@@ -340,11 +350,11 @@ inline bool walk_cell_trap_free(const double* V, int nv, const int* nbr, const s
   return true;
 }
 
-// One walk record for the cone spanned by face f (sign sg) over u in
-// [u0, u1], v in [v0, v1] (already widened): appended to rec (its overflow
-// entries to ovf).  Returns whether the cone is trap-free.
-inline bool walk_cone_record(const double* V, int nv, const int* nbr, int f, double sg, double u0, double u1,
-                             double v0, double v1, double X, std::vector<double>& rec, std::vector<double>& ovf) {
+// The vertices the walk can end at for some direction of the cone spanned by
+// face f (sign sg) over u in [u0, u1], v in [v0, v1] (already widened), in
+// vertex order, each with its witness neighbour (see above).
+inline void walk_cone_list(const double* V, int nv, const int* nbr, int f, double sg, double u0, double u1, double v0,
+                           double v1, double X, std::vector<int>& ids, std::vector<int>& wits) {
   const double rel = 1e-9;
   double r[4][3], M[4];
   for (int k = 0; k < 4; ++k) {
@@ -356,20 +366,16 @@ inline bool walk_cone_record(const double* V, int nv, const int* nbr, int f, dou
   std::vector<double> P((size_t)nv * 4);
   for (int i = 0; i < nv; ++i)
     for (int k = 0; k < 4; ++k) P[4 * i + k] = r[k][0] * V[3 * i] + r[k][1] * V[3 * i + 1] + r[k][2] * V[3 * i + 2];
-  auto margin = [&](int u, int i) {  // > 0: u beats i on the whole cone
-    double m = DBL_MAX;
-    for (int k = 0; k < 4; ++k) m = std::min(m, P[4 * u + k] - P[4 * i + k] - M[k]);
-    return m;
-  };
-  std::vector<std::array<double, 8>> ents;
-  std::vector<int> ids;
+  ids.clear();
+  wits.clear();
   for (int i = 0; i < nv; ++i) {
     const int* nb = nbr + nbr[i];
     int wit = -1;
     double best = -DBL_MAX;
     bool dominated = false;
     for (int k = 1; k <= nb[0]; ++k) {
-      const double m = margin(nb[k], i);
+      double m = DBL_MAX;  // > 0: neighbour k beats i on the whole cone
+      for (int c = 0; c < 4; ++c) m = std::min(m, P[4 * nb[k] + c] - P[4 * i + c] - M[c]);
       if (m > 0.0) dominated = true;
       if (m > best) {
         best = m;
@@ -377,72 +383,66 @@ inline bool walk_cone_record(const double* V, int nv, const int* nbr, int f, dou
       }
     }
     if (dominated) continue;
-    if (wit < 0) wit = i;  // isolated vertex (not a walk hull then)
-    ents.push_back({V[3 * i], V[3 * i + 1], V[3 * i + 2], (double)i, V[3 * wit], V[3 * wit + 1], V[3 * wit + 2], 0.0});
     ids.push_back(i);
+    wits.push_back(wit < 0 ? i : wit);  // wit < 0: isolated vertex (not a walk hull then)
   }
-  // bit k: list entry k (k < 32) is a neighbour of this entry -- when it is
-  // the maximum and strictly above this entry, the walk cannot end here, no
-  // extra dot product needed
-  for (size_t e = 0; e < ents.size(); ++e) {
-    const int* nb = nbr + nbr[ids[e]];
-    uint32_t mask = 0;
-    for (size_t k = 0; k < ents.size() && k < 32; ++k)
-      for (int j = 1; j <= nb[0]; ++j)
-        if (nb[j] == ids[k]) mask |= 1u << k;
-    ents[e][7] = (double)mask;
-  }
-  const bool free = walk_cell_trap_free(V, nv, nbr, ids, f, sg, u0, u1, v0, v1, X);
-  const size_t r0 = rec.size();
-  rec.resize(r0 + kWalkRec, 0.0);
-  rec[r0] = (double)ents.size();
-  rec[r0 + 1] = (double)(ovf.size() / kWalkEnt);
-  rec[r0 + 2] = free ? 1.0 : 0.0;
-  rec[r0 + 3] = -1.0;  // subcell table (set by build_walk_cells)
-  for (size_t e = 0; e < ents.size(); ++e) {
-    if ((int)e < kWalkInline) {
-      for (int j = 0; j < kWalkEnt; ++j) rec[r0 + kWalkHead + kWalkEnt * e + j] = ents[e][j];
-    } else {
-      ovf.insert(ovf.end(), ents[e].begin(), ents[e].end());
-    }
-  }
-  return free;
 }
 
-// Walk-hull cell table: kCellsPerHull records (hull_cell order); a cell that
-// is not trap-free gets kSubK x kSubK subcell records (its cone cut the same
-// way, each widened by kCellWiden; record slot 3 = absolute index of the
-// first), appended after the hull's cells, so the exact walk runs only in the
-// subcells the non-convex triangulation actually traps.  rec_base: the
-// absolute record index of this hull's first cell.
-inline bool build_walk_cells(const double* V, int nv, const int* nbr, size_t rec_base, std::vector<double>& rec,
-                             std::vector<double>& ovf) {
+// Walk-hull cell table: kCellsPerHull records in hull_cell order (layout
+// above), overflow entries in ovf, verification data of trapped cells in aux.
+inline bool build_walk_cells(const double* V, int nv, const int* nbr, int subk, std::vector<double>& rec,
+                             std::vector<double>& ovf, std::vector<double>& aux) {
   double X = 0.0;
   for (int i = 0; i < 3 * nv; ++i) X = std::max(X, std::fabs(V[i]));
-  if (nv <= 0 || !(X >= kHullMin && X <= kHullMax)) return false;
-  const double delta = kCellWiden, cw = 2.0 / kCellK;
-  const size_t c0 = rec.size();
-  std::vector<int> trapped;
+  if (nv <= 0 || !(X >= kHullMin && X <= kHullMax) || subk < 1 || subk * subk > 64) return false;
+  const double delta = kCellWiden, cw = 2.0 / kCellK, sw = cw / subk;
+  std::vector<int> ids, wits, sids, swits;
   for (int f = 0; f < 3; ++f)
     for (int s = 0; s < 2; ++s)
       for (int iu = 0; iu < kCellK; ++iu)
         for (int iv = 0; iv < kCellK; ++iv) {
+          const double sg = s ? -1.0 : 1.0;
           const double u0 = -1.0 + cw * iu - delta, u1 = -1.0 + cw * (iu + 1) + delta;
           const double v0 = -1.0 + cw * iv - delta, v1 = -1.0 + cw * (iv + 1) + delta;
-          if (!walk_cone_record(V, nv, nbr, f, s ? -1.0 : 1.0, u0, u1, v0, v1, X, rec, ovf))
-            trapped.push_back(((2 * f + s) * kCellK + iu) * kCellK + iv);
+          walk_cone_list(V, nv, nbr, f, sg, u0, u1, v0, v1, X, ids, wits);
+          uint64_t free_mask = ~0ull;
+          if (!walk_cell_trap_free(V, nv, nbr, ids, f, sg, u0, u1, v0, v1, X)) {
+            free_mask = 0;
+            for (int su = 0; su < subk; ++su)
+              for (int sv = 0; sv < subk; ++sv) {
+                const double a0 = -1.0 + cw * iu + sw * su - delta, a1 = -1.0 + cw * iu + sw * (su + 1) + delta;
+                const double b0 = -1.0 + cw * iv + sw * sv - delta, b1 = -1.0 + cw * iv + sw * (sv + 1) + delta;
+                walk_cone_list(V, nv, nbr, f, sg, a0, a1, b0, b1, X, sids, swits);
+                if (walk_cell_trap_free(V, nv, nbr, sids, f, sg, a0, a1, b0, b1, X))
+                  free_mask |= 1ull << (su * subk + sv);
+              }
+          }
+          const size_t r0 = rec.size(), n = ids.size();
+          rec.resize(r0 + kCellRec, 0.0);
+          for (int k = 0; k < kCellInline; ++k) {
+            const int i = ids[k < (int)n ? k : 0];
+            for (int j = 0; j < 3; ++j) rec[r0 + 3 * k + j] = V[3 * i + j];
+          }
+          rec[r0 + 9] = (double)n + 256.0 * (double)(ovf.size() / 4);
+          for (size_t e = kCellInline; e < n; ++e) {
+            for (int j = 0; j < 3; ++j) ovf.push_back(V[3 * ids[e] + j]);
+            ovf.push_back(0.0);
+          }
+          if (free_mask != ~0ull) {
+            rec[r0 + 10] = (double)(aux.size() / kWalkAux) + 1.0;
+            for (size_t e = 0; e < n; ++e) {
+              const int* nb = nbr + nbr[ids[e]];
+              uint32_t mask = 0;  // bit k: list entry k (k < 32) is a neighbour
+              for (size_t k = 0; k < n && k < 32; ++k)
+                for (int j = 1; j <= nb[0]; ++j)
+                  if (nb[j] == ids[k]) mask |= 1u << k;
+              aux.push_back((double)ids[e]);
+              for (int j = 0; j < 3; ++j) aux.push_back(V[3 * wits[e] + j]);
+              aux.push_back((double)mask);
+            }
+          }
+          std::memcpy(&rec[r0 + 11], &free_mask, 8);
         }
-  for (int c : trapped) {
-    const int iv = c % kCellK, iu = (c / kCellK) % kCellK, fs = c / (kCellK * kCellK), f = fs >> 1, s = fs & 1;
-    rec[c0 + (size_t)kWalkRec * c + 3] = (double)(rec_base + (rec.size() - c0) / kWalkRec);
-    const double sw = cw / kSubK;
-    for (int su = 0; su < kSubK; ++su)
-      for (int sv = 0; sv < kSubK; ++sv) {
-        const double u0 = -1.0 + cw * iu + sw * su - delta, u1 = -1.0 + cw * iu + sw * (su + 1) + delta;
-        const double v0 = -1.0 + cw * iv + sw * sv - delta, v1 = -1.0 + cw * iv + sw * (sv + 1) + delta;
-        walk_cone_record(V, nv, nbr, f, s ? -1.0 : 1.0, u0, u1, v0, v1, X, rec, ovf);
-      }
-  }
   return true;
 }
 

@@ -167,20 +167,33 @@ __device__ __forceinline__ bool neighbour_beats(const DevWorld& w, cptr<double> 
 // Walk-hull support through its cell record (mpg_hullcells.h
 // build_walk_cells): the cell lists every vertex the walk could end at for a
 // direction of the cell (the others have a neighbour beating them on the whole
-// cell), in vertex order, each with a witness neighbour.  The walk ends at a
-// vertex none of whose neighbours is strictly greater; the first maximum g of
-// the list always qualifies, so when every other listed vertex has a strictly
-// greater neighbour (usually its witness) the walk ends at g.  Otherwise (a
-// local maximum of the non-convex triangulation, or a tie) the walk is run.
+// cell), in vertex order.  In a trap-free (sub)cell the list's unique maximum
+// is the walk's endpoint.  Otherwise the walk ends at a vertex none of whose
+// neighbours is strictly greater; the first maximum g of the list always
+// qualifies, so when every other listed vertex has a strictly greater
+// neighbour (g itself when adjacent, else usually its witness) the walk ends
+// at g; if not (a local maximum of the non-convex triangulation, or a tie)
+// the walk is run.
 __device__ __forceinline__ V3 walk_cell_support(const DevWorld& w, cptr<double> HV, int geom, cptr<double> R,
-                                                const V3& d) {
-  const int n = (int)R[0];
-  const cptr<double> ovf = w.wcell_ovf + kWalkEnt * (size_t)R[1];
+                                                int sub, const V3& d) {
+  const long long no = (long long)R[9];
+  const int n = (int)(no & 255);
+  const cptr<double> ovf = w.wcell_ovf + 4 * (size_t)(no >> 8);
   double best = -DBL_MAX;
   int g = 0;
   bool tie = false;
-  for (int k = 0; k < n; ++k) {
-    const cptr<double> e = k < kWalkInline ? R + kWalkHead + kWalkEnt * k : ovf + kWalkEnt * (k - kWalkInline);
+#pragma unroll
+  for (int k = 0; k < kCellInline; ++k) {
+    const double dd = (d.x * R[3 * k] + d.y * R[3 * k + 1]) + d.z * R[3 * k + 2];
+    const bool in = k < n;
+    tie = in && (dd == best || (tie && !(dd > best)));
+    if (in && dd > best) {
+      best = dd;
+      g = k;
+    }
+  }
+  for (int k = kCellInline; k < n; ++k) {
+    const cptr<double> e = ovf + 4 * (k - kCellInline);
     const double dd = (d.x * e[0] + d.y * e[1]) + d.z * e[2];
     tie = dd == best || (tie && !(dd > best));
     if (dd > best) {
@@ -188,32 +201,35 @@ __device__ __forceinline__ V3 walk_cell_support(const DevWorld& w, cptr<double> 
       g = k;
     }
   }
+  const uint64_t free_mask = (uint64_t)__double_as_longlong(R[11]);
+  const bool fast = ((free_mask >> sub) & 1ull) && !tie;
 #ifdef MPG_STATS
   if (w.stats) {
     atomicAdd(&w.stats[10], 1ull);
-    if (R[2] != 0.0 && !tie) atomicAdd(&w.stats[11], 1ull);
+    if (fast) atomicAdd(&w.stats[11], 1ull);
   }
 #endif
-  if ((R[2] != 0.0 && !tie) || w.debug_mode == 9) {  // trap-free cell (build_walk_cells), unique maximum
-    const cptr<double> e = g < kWalkInline ? R + kWalkHead + kWalkEnt * g : ovf + kWalkEnt * (g - kWalkInline);
-    return v3(e[0], e[1], e[2]);
-  }
-  bool ok = true;
-  for (int k = 0; k < n && ok; ++k) {
-    if (k == g) continue;
-    const cptr<double> e = k < kWalkInline ? R + kWalkHead + kWalkEnt * k : ovf + kWalkEnt * (k - kWalkInline);
-    const double dd = (d.x * e[0] + d.y * e[1]) + d.z * e[2];
-    // the maximum g is a neighbour of this entry and strictly above it
-    if (g < 32 && ((((uint32_t)e[7]) >> g) & 1u) && best > dd) continue;
-    const double dw = (d.x * e[4] + d.y * e[5]) + d.z * e[6];
-    if (dw > dd) continue;
-    ok = neighbour_beats(w, HV, geom, (int)e[3], dd, d);
-  }
+  auto entry = [&](int k) { return k < kCellInline ? R + 3 * k : ovf + 4 * (k - kCellInline); };
+  if (!fast) {
+    const double info = R[10];
+    bool ok = info > 0.0;  // trap-free but tied: straight to the walk
+    const cptr<double> A = w.wcell_aux + kWalkAux * (size_t)(ok ? info - 1.0 : 0.0);
+    for (int k = 0; k < n && ok; ++k) {
+      if (k == g) continue;
+      const cptr<double> e = entry(k), a = A + kWalkAux * k;
+      const double dd = (d.x * e[0] + d.y * e[1]) + d.z * e[2];
+      // the maximum g is a neighbour of this entry and strictly above it
+      if (g < 32 && ((((uint32_t)a[4]) >> g) & 1u) && best > dd) continue;
+      const double dw = (d.x * a[1] + d.y * a[2]) + d.z * a[3];
+      if (dw > dd) continue;
+      ok = neighbour_beats(w, HV, geom, (int)a[0], dd, d);
+    }
 #ifdef MPG_STATS
-  if (w.stats) atomicAdd(&w.stats[ok ? 12 : 13], 1ull);
+    if (w.stats) atomicAdd(&w.stats[ok ? 12 : 13], 1ull);
 #endif
-  if (!ok) return convex_walk(w, HV, geom, d);
-  const cptr<double> e = g < kWalkInline ? R + kWalkHead + kWalkEnt * g : ovf + kWalkEnt * (g - kWalkInline);
+    if (!ok) return convex_walk(w, HV, geom, d);
+  }
+  const cptr<double> e = entry(g);
   return v3(e[0], e[1], e[2]);
 }
 
@@ -223,11 +239,9 @@ __device__ __forceinline__ V3 convex_support_local(const DevWorld& w, cptr<doubl
   const int cb = w.geom_cbase[geom];
   if (w.geom_nbr[geom] >= 0) {  // neighbour-walk hull (wave-uniform branch)
     int sub = 0;
-    const int c = cb >= 0 ? hull_cell_sub(d.x, d.y, d.z, &sub) : -1;
+    const int c = cb >= 0 ? hull_cell_sub(d.x, d.y, d.z, w.walk_subk, &sub) : -1;
     if (c < 0) return convex_walk(w, HV, geom, d);
-    cptr<double> R = w.wcell_rec + kWalkRec * (size_t)(cb + c);
-    if (R[3] >= 0.0) R = w.wcell_rec + kWalkRec * ((size_t)R[3] + sub);  // trapped cell: its subcell
-    return walk_cell_support(w, HV, geom, R, d);
+    return walk_cell_support(w, HV, geom, w.wcell_rec + kCellRec * (size_t)(cb + c), sub, d);
   }
   const int c = cb >= 0 ? hull_cell(d.x, d.y, d.z) : -1;
   if (c < 0) return convex_full_scan(w, HV, geom, d);
@@ -1908,7 +1922,11 @@ __global__ __launch_bounds__(256) void small_sincos_kernel(DevWorld w, const dou
   }
 }
 
-template <bool FROM_POSES, int CLS>
+// INLINE_SC: each lane computes its joints' exact sin/cos itself (one launch
+// per validity batch -- the planner's round trip); otherwise they come from
+// small_sincos_kernel (larger batches, where the P-fold recomputation costs
+// more than the extra launch)
+template <bool FROM_POSES, int CLS, bool INLINE_SC = false>
 __global__ __launch_bounds__(256) void small_kernel(DevWorld w, const double* __restrict__ in, long long n, int n_tiles,
                                                    uint8_t* __restrict__ hits, const double* __restrict__ sc) {
   const cptr<double> HV = w.hull;
@@ -1925,8 +1943,8 @@ __global__ __launch_bounds__(256) void small_kernel(DevWorld w, const double* __
   const bool am = a < w.n_moving, bm = b < w.n_moving;
   const int cf = w.pair_cf[p];
   if (!w.pair_allowed[p]) {  // ACM-allowed pairs are never reported (filterCollisions)
-    const SE3 TA = am ? moving_tf<FROM_POSES>(w, in, sc, c, a) : load_se3(w.static_T + 12 * (a - w.n_moving));
-    const SE3 TB = bm ? moving_tf<FROM_POSES>(w, in, sc, c, b) : load_se3(w.static_T + 12 * (b - w.n_moving));
+    const SE3 TA = am ? moving_tf<FROM_POSES, !INLINE_SC>(w, in, sc, c, a) : load_se3(w.static_T + 12 * (a - w.n_moving));
+    const SE3 TB = bm ? moving_tf<FROM_POSES, !INLINE_SC>(w, in, sc, c, b) : load_se3(w.static_T + 12 * (b - w.n_moving));
     const int ga = am ? w.moving_geom[a] : w.static_geom[a - w.n_moving];
     const int gb = bm ? w.moving_geom[b] : w.static_geom[b - w.n_moving];
     const cptr<double> ra = w.geom_rec + G_STRIDE * ga, rb = w.geom_rec + G_STRIDE * gb;
@@ -2747,6 +2765,7 @@ struct mpg_world {
   double* d_qmap = nullptr;    // h_q as the device sees it (zero-copy input)
   double* d_ssc = nullptr;     // latency path joint (sin, cos) [small cap * dof * 2]
   bool small_zero_copy = true; // MPG_SMALL_ZEROCOPY=0: stage through d_qs
+  int64_t small_inline_sc = 256;  // latency batches up to this size: sin/cos inline (MPG_SMALL_INLINE_SC)
   size_t small_cap = 0;   // configurations (hit bytes per pair)
   size_t small_qcap = 0;  // input doubles (h_q, d_qs)
 };
@@ -3305,7 +3324,9 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
   std::vector<int> gstart(std::max(d->n_geoms, 1), 0), ngroups(std::max(d->n_geoms, 1), 0);
   std::vector<double> hull;
   std::vector<int> cbase(std::max(d->n_geoms, 1), -1), geom_nbr(std::max(d->n_geoms, 1), -1), hull_nbr;
-  std::vector<double> cell_rec, cell_ovf, wcell_rec, wcell_ovf;
+  std::vector<double> cell_rec, cell_ovf, wcell_rec, wcell_ovf, wcell_aux;
+  const int walk_subk =
+      std::getenv("MPG_WALK_SUBK") ? std::max(1, std::min(8, std::atoi(std::getenv("MPG_WALK_SUBK")))) : kSubK;
   for (int g = 0; g < d->n_geoms; ++g) {
     if (d->geom_type[g] != MPG_GEOM_CONVEX) continue;
     const double* Vg = d->vertices + 3 * (size_t)d->geom_vertex_start[g];
@@ -3322,7 +3343,8 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
       geom_nbr[g] = (int)hull_nbr.size();
       hull_nbr.insert(hull_nbr.end(), enc.begin(), enc.end());
       const size_t r0 = wcell_rec.size();
-      if (build_walk_cells(Vg, nvg, enc.data(), r0 / kWalkRec, wcell_rec, wcell_ovf)) cbase[g] = (int)(r0 / kWalkRec);
+      if (build_walk_cells(Vg, nvg, enc.data(), walk_subk, wcell_rec, wcell_ovf, wcell_aux))
+        cbase[g] = (int)(r0 / kCellRec);
     } else {
       std::vector<uint32_t> cstart;
       std::vector<double> cpts;
@@ -3346,8 +3368,9 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
   if (cell_rec.empty()) cell_rec.assign(kCellRec, 0.0);
   if (cell_ovf.empty()) cell_ovf.assign(4, 0.0);
   if (hull_nbr.empty()) hull_nbr.assign(1, 0);
-  if (wcell_rec.empty()) wcell_rec.assign(kWalkRec, 0.0);
-  if (wcell_ovf.empty()) wcell_ovf.assign(kWalkEnt, 0.0);
+  if (wcell_rec.empty()) wcell_rec.assign(kCellRec, 0.0);
+  if (wcell_ovf.empty()) wcell_ovf.assign(4, 0.0);
+  if (wcell_aux.empty()) wcell_aux.assign(kWalkAux, 0.0);
   // octrees: leaf boxes + a uniform grid per octree geometry (cells of at
   // least the largest leaf, <= 64 per axis); a leaf is listed in every cell
   // its box overlaps
@@ -3487,6 +3510,7 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
   const size_t o_hnb = bb.add(hull_nbr.data(), hull_nbr.size());
   const size_t o_wrec = bb.add(wcell_rec.data(), wcell_rec.size());
   const size_t o_wovf = bb.add(wcell_ovf.data(), wcell_ovf.size());
+  const size_t o_waux = bb.add(wcell_aux.data(), wcell_aux.size());
   const size_t o_ml = bb.add(d->moving_link, d->n_moving);
   const size_t o_mg = bb.add(d->moving_geom, d->n_moving);
   const size_t o_mo = bb.add(d->moving_offset, 12 * (size_t)d->n_moving);
@@ -3599,6 +3623,8 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
   dw.hull_nbr = to_cptr<int>(base + o_hnb);
   dw.wcell_rec = to_cptr<double>(base + o_wrec);
   dw.wcell_ovf = to_cptr<double>(base + o_wovf);
+  dw.wcell_aux = to_cptr<double>(base + o_waux);
+  dw.walk_subk = walk_subk;
   dw.moving_link = to_cptr<int>(base + o_ml);
   dw.moving_geom = to_cptr<int>(base + o_mg);
   dw.moving_offset = to_cptr<double>(base + o_mo);
@@ -3667,6 +3693,7 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
   if (const char* e = std::getenv("MPG_SMALL_BATCH_MAX")) w->small_max = std::atoll(e);
   if (const char* e = std::getenv("MPG_SMALL_ZEROCOPY")) w->small_zero_copy = std::atoi(e) != 0;
   if (const char* e = std::getenv("MPG_OVERLAP_MIN")) w->overlap_min = std::atoll(e);
+  if (const char* e = std::getenv("MPG_SMALL_INLINE_SC")) w->small_inline_sc = std::atoll(e);
   if (const char* e = std::getenv("MPG_OVERLAP_PARTS")) w->overlap_parts = std::atoi(e);
   *out = w;
   return MPG_OK;
@@ -3798,25 +3825,24 @@ int collide_small(mpg_world* w, const double* q, int64_t n, uint8_t* flags, uint
   const long long waves = (long long)P * n_tiles;
   StageTimer t_small(w, s, MPG_STAGE_NARROW);
   if (w->prof) w->prof_cfg += n;
-  if (!FROM_POSES && w->dw.dof > 0) {
+  // batches of up to kSmallInlineSc states: one launch (sin/cos inline)
+  const bool inline_sc = FROM_POSES || n <= w->small_inline_sc;
+  if (!inline_sc && w->dw.dof > 0) {
     const long long nt = n * w->dw.dof;
     hipLaunchKernelGGL(small_sincos_kernel, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, s, w->dw, qin,
                        (long long)n, w->d_ssc);
     HIP_TRY(hipGetLastError());
   }
-  hipLaunchKernelGGL((small_kernel<FROM_POSES, CLS_CLOSED>), dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s,
-                     w->dw, qin, (long long)n, n_tiles, w->d_hits, w->d_ssc);
-  HIP_TRY(hipGetLastError());
-  if (w->any_octree) {
-    hipLaunchKernelGGL((small_kernel<FROM_POSES, CLS_OCTREE>), dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s,
-                       w->dw, qin, (long long)n, n_tiles, w->d_hits, w->d_ssc);
-    HIP_TRY(hipGetLastError());
-  }
-  if (w->any_mesh) {
-    hipLaunchKernelGGL((small_kernel<FROM_POSES, CLS_MESH>), dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s,
-                       w->dw, qin, (long long)n, n_tiles, w->d_hits, w->d_ssc);
-    HIP_TRY(hipGetLastError());
-  }
+  const dim3 grid((unsigned)((waves + 3) / 4));
+  auto launch = [&](auto kern) {  // every class instance reads the same sin/cos source
+    hipLaunchKernelGGL(kern, grid, dim3(256), 0, s, w->dw, qin, (long long)n, n_tiles, w->d_hits, w->d_ssc);
+    return hipGetLastError();
+  };
+  HIP_TRY(inline_sc ? launch(small_kernel<FROM_POSES, CLS_CLOSED, true>) : launch(small_kernel<FROM_POSES, CLS_CLOSED>));
+  if (w->any_octree)
+    HIP_TRY(inline_sc ? launch(small_kernel<FROM_POSES, CLS_OCTREE, true>) : launch(small_kernel<FROM_POSES, CLS_OCTREE>));
+  if (w->any_mesh)
+    HIP_TRY(inline_sc ? launch(small_kernel<FROM_POSES, CLS_MESH, true>) : launch(small_kernel<FROM_POSES, CLS_MESH>));
   t_small.stop();
   HIP_TRY(hipStreamSynchronize(s));
   const uint8_t* h = w->h_hits;

@@ -1730,6 +1730,21 @@ int orc_collide_batch(const orc_world *w, const double *q, long n, uint8_t *flag
     return 0;
 }
 
+/* State validity (OMPL ValidityChecker::isValid = !collide(), src/ompl_planner.h:59-62)
+ * for n states, single-threaded as OMPL calls it: the C-level checker the
+ * planner's CPU baseline plugs in (OMPLPlanner.set_native_state_validity_checker). */
+int orc_validity_batch(void *ctx, const double *q, long long n, uint8_t *valid) {
+    const orc_world *w = (const orc_world *)ctx;
+    if (w->nq_user > 64 || w->nq_pin > 64) return -1;
+    real oMi[12 * 65], link_T[12 * 257], obj_T[12 * MAX_OBJ], att_T[12 * MAX_OBJ];
+    uint32_t mask[64];
+    const int W = (w->n_pairs + 31) / 32;
+    if (w->nj > 64 || w->n_links > 256 || w->n_obj > MAX_OBJ || w->n_att > MAX_OBJ || W > 64) return -1;
+    for (long long i = 0; i < n; ++i)
+        valid[i] = (uint8_t)!collide_one(w, q + (size_t)i * w->dof, mask, W > 0 ? W : 1, NULL, oMi, link_T, obj_T, att_T);
+    return 0;
+}
+
 /* FK entry point: link_pose7[n*n_links*7] (getLinkPose), obj_T[n*n_obj*12]
  * (collision object transforms after updateCollisionObjects).  Either output
  * may be NULL. */

@@ -609,7 +609,7 @@ def test_capsule_cylinder_worlds_match_oracle():
         np.testing.assert_array_equal(f, fo)
         np.testing.assert_array_equal(bits(m, range(len(perm))), bits(mo, perm))
     hit = bits(mo, perm)
+    # every closed-form class is exercised (oracle counts for this sample: 64, 65, 65, 63)
     for pair in [("orb", "cap0"), ("orb", "cyl2"), ("rod", "ball4"), ("rod", "cap0")]:
-        if pair in names:
-            assert hit[:, names.index(pair)].sum() >= 0
+        assert hit[:, names.index(pair)].sum() > 0, pair
     assert int(hit.sum()) > 0

@@ -229,10 +229,9 @@ def test_mesh_worlds_match_oracle(convex):
         np.testing.assert_array_equal(f, fo)
         np.testing.assert_array_equal(_bits(m, range(len(perm))), _bits(mo, perm))
     hit = _bits(mo, perm)
-    for pair in [("orb", "scene_mesh"), ("tool", "scene_mesh"), ("panda_link4", "scene_mesh"),
-                 ("panda_link3", "panda_link5")]:
-        if pair in names:
-            assert hit[:, names.index(pair)].sum() >= 0
+    # sphere-triangle, mesh-mesh and link-mesh classes are exercised (oracle counts: 31, 11, 54)
+    for pair in [("orb", "scene_mesh"), ("tool", "scene_mesh"), ("panda_link4", "scene_mesh")]:
+        assert hit[:, names.index(pair)].sum() > 0, pair
     assert 0 < int(fo.sum()) < len(q)
     assert int(hit.sum()) > 0
 

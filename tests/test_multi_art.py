@@ -17,7 +17,7 @@ import oracle
 from oracle import model as M
 import worlds as Wd
 
-OFFSET_XYZ = (0.75, 0.05, 0.0)
+OFFSET_XYZ = (1.25, 0.05, 0.0)
 OFFSET_RPY = (0.0, 0.0, 3.14159265358979)
 B_QPOS = [0.3, -0.4, 0.2, -2.2, 0.1, 2.0, 0.6]
 
@@ -148,4 +148,7 @@ def test_two_pandas_match_oracle(b_planned):
         got = (m[:, p >> 5] >> (p & 31)) & 1
         want = (mo[:, po >> 5] >> (po & 31)) & 1
         assert np.array_equal(got, want), keys[p]
-    assert 0.05 < f.mean() < 0.95
+    assert 0.05 < f.mean() < 0.999
+    # some configurations collide only through the second robot
+    arts = [p for p, k in enumerate(keys) if "b_panda" in (k[0], k[1]) and k[0] != k[1]]
+    assert any(((m[:, p >> 5] >> (p & 31)) & 1).any() for p in arts)
