@@ -493,6 +493,10 @@ using AcmPtr = std::shared_ptr<AllowedCollisionMatrix>;
 // ---------------------------------------------------------------------------
 // AttachedBody + PlanningWorld (reference src/attached_body.h, src/planning_world.{h,cpp})
 // ---------------------------------------------------------------------------
+// src/attached_body.h:17-73: an object rigidly attached to a link of an
+// articulation.  pose = link -> object; the global pose is
+// posevec_to_transform(getLinkPose(link)) * pose (attached_body.h:50-53), i.e.
+// the link pose goes through its 7-vector (quaternion) form first.
 struct AttachedBody {
   std::string name;
   ObjPtr object;
@@ -500,6 +504,17 @@ struct AttachedBody {
   int link_id;
   SE3 pose;
   std::vector<std::string> touch_links;
+  uint64_t version = 0;  // bumped by set_pose: the world's device snapshot bakes `pose` in
+
+  SE3 global_pose() const;
+  // attached_body.h:56.  Writes the transform without bumping the object's
+  // version: an attached object's own transform is not part of the device
+  // snapshot (its pose comes from the link), so no rebuild follows.
+  void update_pose() const { object->tf = global_pose(); }
+  void set_pose(const SE3& p) {
+    pose = p;
+    ++version;
+  }
 };
 using AttachedPtr = std::shared_ptr<AttachedBody>;
 

@@ -36,6 +36,18 @@ py::array_t<double> mat3(const SE3& T) {
     for (int j = 0; j < 3; ++j) m(i, j) = T.R[3 * i + j];
   return a;
 }
+py::array_t<double> mat4(const SE3& T) {  // homogeneous matrix of an Isometry3d
+  py::array_t<double> a({4, 4});
+  auto m = a.mutable_unchecked<2>();
+  for (int i = 0; i < 3; ++i) {
+    for (int j = 0; j < 3; ++j) m(i, j) = T.R[3 * i + j];
+    m(i, 3) = T.p[i];
+    m(3, i) = 0.0;
+  }
+  m(3, 3) = 1.0;
+  return a;
+}
+
 py::array_t<double> vec(const double* p, int n) {
   py::array_t<double> a(n);
   auto m = a.mutable_unchecked<1>();
@@ -528,14 +540,41 @@ PYBIND11_MODULE(pymp, m_all) {
       .def("__str__", &ACM::print);
 
   // -------------------------------------------------------- planning_world
+  // -------------------------------------------------------- attached_body
+  // python/pybind_attached_body.hpp:22-60.  get_pose / get_global_pose return
+  // the 4x4 homogeneous matrix (the reference returns an Eigen::Transform,
+  // for which its binding registers no converter).
+  auto mab = m_all.def_submodule("attached_body");
+  auto ab_cls =
+      py::class_<AttachedBody, std::shared_ptr<AttachedBody>>(mab, "AttachedBody")
+          .def(py::init([](const S& name, const ObjPtr& object, const ArtPtr& art, int link_id,
+                           const std::vector<double>& pose, const VS& touch_links) {
+                 if (!object || !art) throw std::invalid_argument("object and attached_articulation are required");
+                 if (link_id < 0 || link_id >= (int)art->get_user_link_names().size())
+                   throw std::out_of_range("attached_link_id out of range");
+                 auto b = std::make_shared<AttachedBody>(
+                     AttachedBody{name, object, art, link_id, se3_from_pose7(vec7_arg(pose)), touch_links});
+                 b->update_pose();  // attached_body.cpp:22
+                 return b;
+               }),
+               py::arg("name"), py::arg("object"), py::arg("attached_articulation"), py::arg("attached_link_id"),
+               py::arg("pose"), py::arg("touch_links") = VS())
+          .def("get_name", [](const AttachedBody& b) { return b.name; })
+          .def("get_object", [](const AttachedBody& b) { return b.object; })
+          .def("get_attached_articulation", [](const AttachedBody& b) { return b.articulation; })
+          .def("get_attached_link_id", [](const AttachedBody& b) { return b.link_id; })
+          .def("get_pose", [](const AttachedBody& b) { return mat4(b.pose); })
+          .def(
+              "set_pose",
+              [](AttachedBody& b, const std::vector<double>& pose) { b.set_pose(se3_from_pose7(vec7_arg(pose))); },
+              py::arg("pose"))
+          .def("get_global_pose", [](const AttachedBody& b) { return mat4(b.global_pose()); })
+          .def("update_pose", &AttachedBody::update_pose)
+          .def("get_touch_links", [](const AttachedBody& b) { return b.touch_links; })
+          .def("set_touch_links", [](AttachedBody& b, const VS& t) { b.touch_links = t; }, py::arg("touch_links"));
+
   auto mw = m_all.def_submodule("planning_world");
-  py::class_<AttachedBody, std::shared_ptr<AttachedBody>>(mw, "AttachedBody")
-      .def("get_name", [](const AttachedBody& b) { return b.name; })
-      .def("get_object", [](const AttachedBody& b) { return b.object; })
-      .def("get_attached_articulation", [](const AttachedBody& b) { return b.articulation; })
-      .def("get_attached_link_id", [](const AttachedBody& b) { return b.link_id; })
-      .def("get_touch_links", [](const AttachedBody& b) { return b.touch_links; })
-      .def("set_touch_links", [](AttachedBody& b, const VS& t) { b.touch_links = t; });
+  mw.attr("AttachedBody") = ab_cls;
 
   py::class_<WorldCollisionResult, std::shared_ptr<WorldCollisionResult>>(mw, "WorldCollisionResult")
       .def(py::init<>())

@@ -227,6 +227,10 @@ bool PlanningWorld::remove_normal_object(const std::string& n) {
   ++structure_version_;
   return true;
 }
+SE3 AttachedBody::global_pose() const {
+  return mpg::se3_mul(se3_from_pose7(articulation->get_pinocchio_model()->get_link_pose(link_id)), pose);
+}
+
 AttachedPtr PlanningWorld::get_attached_object(const std::string& n) const {
   auto it = attached_.find(n);
   return it == attached_.end() ? nullptr : it->second;
@@ -238,6 +242,7 @@ void PlanningWorld::attach_object(const std::string& n, const std::string& art, 
   auto a = planned_.at(art);
   if (link < 0 || link >= (int)a->get_user_link_names().size()) throw std::out_of_range("link_id out of range");
   auto body = std::make_shared<AttachedBody>(AttachedBody{n, obj, a, link, se3_from_pose7(pose), touch_links});
+  body->update_pose();  // AttachedBody ctor (attached_body.cpp:22)
   auto it = attached_.find(n);
   if (it != attached_.end()) acm_->remove_entry(n, it->second->touch_links);
   else attached_insertion_.push_back(n);
@@ -251,6 +256,7 @@ void PlanningWorld::attach_object(const std::string& n, const std::string& art, 
   auto a = planned_.at(art);
   if (link < 0 || link >= (int)a->get_user_link_names().size()) throw std::out_of_range("link_id out of range");
   auto body = std::make_shared<AttachedBody>(AttachedBody{n, obj, a, link, se3_from_pose7(pose), {}});
+  body->update_pose();  // AttachedBody ctor (attached_body.cpp:22)
   auto it = attached_.find(n);
   if (it != attached_.end()) {
     body->touch_links = it->second->touch_links;
@@ -369,7 +375,10 @@ uint64_t PlanningWorld::snapshot_key(const CollisionRequest& r) const {
       if (std::find(slots.begin(), slots.end(), (int)i) == slots.end()) mixd(q[i]);
   }
   for (auto& n : obj_insertion_) mix(objs_.at(n)->version);
-  for (auto& n : attached_insertion_) mix((uint64_t)(uintptr_t)attached_.at(n).get());
+  for (auto& n : attached_insertion_) {
+    mix((uint64_t)(uintptr_t)attached_.at(n).get());
+    mix(attached_.at(n)->version);
+  }
   return h;
 }
 

@@ -47,14 +47,19 @@ struct DevWorld {
   cptr<int> geom_cbase;      // [n_geoms] first cell record of the hull, -1 = none (full scan)
   cptr<double> cell_rec;     // kCellsPerHull records of kCellRec doubles per hull (mpg_hullcells.h)
   cptr<double> cell_ovf;     // list entries beyond the inline ones: x, y, z, 0
-  // FCL 0.7.0 neighbour-walk hulls (mpg_hullcells.h): geom_nbr[g] = start of
-  // the hull's neighbors_ encoding in hull_nbr, -1 = linear support; their
-  // cell records (kCellRec doubles, indexed by geom_cbase), overflow entries
+  // FCL 0.7.0 neighbour-walk hulls (mpg_hullcells.h): geom_nbr[g] = the
+  // hull's first vertex in hull_nbr, -1 = linear support.  hull_nbr holds per
+  // vertex (first entry, count) of its sorted neighbour list in nbr_ent, whose
+  // entries carry the neighbour's coordinates inline (x, y, z, index): one
+  // load per climb step.  Then the hull's cell records (kCellRec doubles,
+  // indexed by geom_cbase) and their overflow entries.
   cptr<int> geom_nbr;
   cptr<int> hull_nbr;
+  cptr<double> nbr_ent;
   cptr<double> wcell_rec;
   cptr<double> wcell_ovf;
   cptr<double> wcell_aux;  // trapped (sub)cells' verification data (mpg_hullcells.h)
+  cptr<int> wcell_end;     // certified walk endpoints of the trapped subcells' fine cells
   int walk_subk;           // subcells per axis of a trapped cell
   cptr<int> moving_link;     // [n_moving]
   cptr<int> moving_geom;

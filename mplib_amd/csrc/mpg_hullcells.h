@@ -34,6 +34,7 @@ constexpr double kCellMin = 1e-30, kCellMax = 1e30;  // |dir| range with cells
 constexpr double kHullMin = 1e-100, kHullMax = 1e100;  // max|coord| range with cells
 constexpr double kCellWiden = 1e-5;  // cone widening: covers the fp32 cell arithmetic below
 constexpr int kSubK = 8;  // walk hulls: default subcells per axis of a cell that is not trap-free
+constexpr int kSub2K = 16;  // walk hulls: fine cells per axis of a trapped subcell (certified endpoints)
 
 // cell of direction (x, y, z), or -1 (no cell: full scan).  The range checks
 // are exact (fp64); the cell arithmetic is fp32: the ratios u/|m| are off by
@@ -65,10 +66,12 @@ MPG_INLINE int hull_cell(double x, double y, double z) {
   return ((2 * f + (m < 0.0 ? 1 : 0)) * kCellK + iu) * kCellK + iv;
 }
 
-// hull_cell plus the subcell (kSubK x kSubK per cell) of the direction: the
-// same fp32 ratios, so the direction lies in the widened subcone as well
-// (kCellWiden >> the ratio error).  -1 / sub undefined when there is no cell.
-MPG_INLINE int hull_cell_sub(double x, double y, double z, int subk, int* sub) {
+// hull_cell plus the subcell (subk x subk per cell) of the direction and its
+// fine cell within the subcell (kSub2K x kSub2K): the same fp32 ratios, so the
+// direction lies in the widened subcone and fine cone as well (kCellWiden >>
+// the ratio error; the scalings by subk * kSub2K are exact for powers of two).
+// -1 / sub, fine undefined when there is no cell.
+MPG_INLINE int hull_cell_sub(double x, double y, double z, int subk, int* sub, int* fine) {
   const double ax = std::fabs(x), ay = std::fabs(y), az = std::fabs(z);
   if (!(ax <= kCellMax && ay <= kCellMax && az <= kCellMax)) return -1;  // also NaN
   if (!(ax >= kCellMin || ay >= kCellMin || az >= kCellMin)) return -1;
@@ -92,10 +95,12 @@ MPG_INLINE int hull_cell_sub(double x, double y, double z, int subk, int* sub) {
   int iu = (int)fu, iv = (int)fv;
   iu = iu < 0 ? 0 : (iu >= kCellK ? kCellK - 1 : iu);
   iv = iv < 0 ? 0 : (iv >= kCellK ? kCellK - 1 : iv);
-  int su = (int)((fu - (float)iu) * (float)subk), sv = (int)((fv - (float)iv) * (float)subk);
-  su = su < 0 ? 0 : (su >= subk ? subk - 1 : su);
-  sv = sv < 0 ? 0 : (sv >= subk ? subk - 1 : sv);
-  *sub = su * subk + sv;
+  const int kf = subk * kSub2K;
+  int ku = (int)((fu - (float)iu) * (float)kf), kv = (int)((fv - (float)iv) * (float)kf);
+  ku = ku < 0 ? 0 : (ku >= kf ? kf - 1 : ku);
+  kv = kv < 0 ? 0 : (kv >= kf ? kf - 1 : kv);
+  *sub = (ku / kSub2K) * subk + kv / kSub2K;
+  *fine = (ku % kSub2K) * kSub2K + kv % kSub2K;
   return ((2 * f + (m < 0.0 ? 1 : 0)) * kCellK + iu) * kCellK + iv;
 }
 
@@ -273,27 +278,35 @@ inline bool fcl_convex_neighbors(int nv, const int32_t* faces, int num_faces, st
   return nv > kMinVertCountForEdgeWalking && connected && watertight;
 }
 
-// Walk-hull cell records (convex_support_local on the device): per cell the
-// vertices the walk can END at for some direction of the (widened) cell cone
-// -- a vertex w is left out only when one of its neighbours u beats it on every
+// Walk-hull cell records (convex_support_local on the device).  Per cell two
+// lists: the linear list of build_hull_cells (every vertex that can be the
+// global first maximum for a direction of the cell) and the walk list (every
+// vertex the walk can END at for some direction of the (widened) cell cone --
+// a vertex w is left out only when one of its neighbours u beats it on every
 // corner ray by the margin of build_hull_cells, so u's rounded dot product is
 // strictly above w's for every direction of the cell and the walk never stops
-// at w -- in vertex order.  The first maximum of the list is the global first
-// maximum (the list contains every vertex build_hull_cells keeps).
+// at w -- in vertex order).  The walk list contains the linear list, and in a
+// trap-free (sub)cell the walk ends at the unique maximum of the walk list,
+// which is then the unique global maximum: the linear list's.  So the record,
+// read on every support, carries the short linear list; the walk list lives
+// with the rarely read data of trapped cells.
 // Record layout (kCellRec doubles, like the linear hulls' records): three
-// entries inline (x, y, z; short lists padded with their first entry), then
+// linear-list entries inline (x, y, z; short lists padded with their first
+// entry), then
 //   slot 9   n + 256 * (overflow offset, entries of 4 doubles x, y, z, 0),
-//   slot 10  0, or k + 1: verification data at aux entry k (kWalkAux doubles
-//            per list entry: vertex index, witness neighbour x, y, z -- the
-//            neighbour beating it on most of the cell -- and the mask of the
-//            list entries that are its neighbours),
+//   slot 10  0, or k + 1: the trapped cell's data at aux entry k (kWalkAux
+//            doubles each): a header (the index of its first endpoint table
+//            in ends: one table of kSub2K x kSub2K fine-cell endpoints, vertex
+//            index or -1, per trapped subcell in subcell order; the walk
+//            list's length), then per walk-list entry: vertex index, witness
+//            neighbour x, y, z -- the neighbour beating it on most of the cell
+//            --, the mask of the walk-list entries that are its neighbours,
+//            and its x, y, z,
 //   slot 11  the bits (uint64) of the trap-free mask: bit s set when subcell s
 //            (kSubK x kSubK per cell, hull_cell_sub order) is trap-free
 //            (walk_cell_trap_free on the subcell's own list); all ones for a
-//            trap-free cell.  In a trap-free subcell the unique maximum of the
-//            cell's list is the walk's endpoint (the list contains every
-//            possible maximum of the cell).
-constexpr int kWalkAux = 5;
+//            trap-free cell.
+constexpr int kWalkAux = 8;
 // Clip the convex polygon (u, v) by a*u + b*v + c <= 0 (Sutherland-Hodgman).
 inline void clip_poly(std::vector<std::array<double, 2>>& poly, double a, double b, double c) {
   std::vector<std::array<double, 2>> out;
@@ -388,19 +401,75 @@ inline void walk_cone_list(const double* V, int nv, const int* nbr, int f, doubl
   }
 }
 
+// The walk's endpoint for every direction of the cone spanned by face f (sign
+// sg) over [u0, u1] x [v0, v1], or -1.  The climb is replayed once; each of its
+// comparisons 'value(u) >= value(b)' (b the running maximum) must come out the
+// same on the whole cone: (u - b) . r_k beyond the rounding margin on all four
+// corner rays (every direction of the cone is a non-negative combination of
+// them, so the rounded fp64 dot products then compare the same way), or u and
+// b coincide (equal values, '>=' holds).  Then every direction of the cone
+// takes the same path and ends at the same vertex.
+inline int walk_cone_endpoint(const double* V, int nv, const int* nbr, int f, double sg, double u0, double u1,
+                              double v0, double v1, double X, std::vector<char>& vis) {
+  const double rel = 1e-9;
+  double r[4][3], M[4];
+  for (int k = 0; k < 4; ++k) {
+    r[k][f] = sg;
+    r[k][(f + 1) % 3] = (k & 1) ? u1 : u0;
+    r[k][(f + 2) % 3] = (k & 2) ? v1 : v0;
+    M[k] = rel * (std::fabs(r[k][0]) + std::fabs(r[k][1]) + std::fabs(r[k][2])) * X;
+  }
+  vis.assign(nv, 0);
+  vis[0] = 1;
+  int bi = 0;
+  bool keep = true;
+  while (keep) {
+    keep = false;
+    const int* nb = nbr + nbr[bi];
+    for (int k = 1; k <= nb[0]; ++k) {
+      const int u = nb[k];
+      if (vis[u]) continue;
+      vis[u] = 1;
+      const double a[3] = {V[3 * u] - V[3 * bi], V[3 * u + 1] - V[3 * bi + 1], V[3 * u + 2] - V[3 * bi + 2]};
+      bool ge = a[0] == 0.0 && a[1] == 0.0 && a[2] == 0.0;
+      if (!ge) {
+        int above = 0, below = 0;
+        for (int c = 0; c < 4; ++c) {
+          const double t = r[c][0] * a[0] + r[c][1] * a[1] + r[c][2] * a[2];
+          above += t > M[c];
+          below += t < -M[c];
+        }
+        if (above != 4 && below != 4) return -1;  // the comparison flips inside the cone
+        ge = above == 4;
+      }
+      if (ge) {
+        keep = true;
+        bi = u;
+      }
+    }
+  }
+  return bi;
+}
+
 // Walk-hull cell table: kCellsPerHull records in hull_cell order (layout
-// above), overflow entries in ovf, verification data of trapped cells in aux.
+// above), overflow entries in ovf, trapped cells' walk lists and verification
+// data in aux, certified endpoints of the trapped subcells' fine cells in ends.
 inline bool build_walk_cells(const double* V, int nv, const int* nbr, int subk, std::vector<double>& rec,
-                             std::vector<double>& ovf, std::vector<double>& aux) {
+                             std::vector<double>& ovf, std::vector<double>& aux, std::vector<int>& ends) {
   double X = 0.0;
   for (int i = 0; i < 3 * nv; ++i) X = std::max(X, std::fabs(V[i]));
   if (nv <= 0 || !(X >= kHullMin && X <= kHullMax) || subk < 1 || subk * subk > 64) return false;
-  const double delta = kCellWiden, cw = 2.0 / kCellK, sw = cw / subk;
+  std::vector<uint32_t> lstart;
+  std::vector<double> lpts;
+  if (!build_hull_cells(V, nv, lstart, lpts)) return false;
+  const double delta = kCellWiden, cw = 2.0 / kCellK, sw = cw / subk, fw = sw / kSub2K;
   std::vector<int> ids, wits, sids, swits;
+  std::vector<char> vis;
+  int c = 0;  // hull_cell order: ((2 f + s) K + iu) K + iv
   for (int f = 0; f < 3; ++f)
     for (int s = 0; s < 2; ++s)
       for (int iu = 0; iu < kCellK; ++iu)
-        for (int iv = 0; iv < kCellK; ++iv) {
+        for (int iv = 0; iv < kCellK; ++iv, ++c) {
           const double sg = s ? -1.0 : 1.0;
           const double u0 = -1.0 + cw * iu - delta, u1 = -1.0 + cw * (iu + 1) + delta;
           const double v0 = -1.0 + cw * iv - delta, v1 = -1.0 + cw * (iv + 1) + delta;
@@ -417,28 +486,44 @@ inline bool build_walk_cells(const double* V, int nv, const int* nbr, int subk, 
                   free_mask |= 1ull << (su * subk + sv);
               }
           }
-          const size_t r0 = rec.size(), n = ids.size();
+          // the linear list inline / in the overflow
+          const uint32_t l0 = lstart[c], n = lstart[c + 1] - lstart[c];
+          const size_t r0 = rec.size();
           rec.resize(r0 + kCellRec, 0.0);
           for (int k = 0; k < kCellInline; ++k) {
-            const int i = ids[k < (int)n ? k : 0];
-            for (int j = 0; j < 3; ++j) rec[r0 + 3 * k + j] = V[3 * i + j];
+            const uint32_t e = l0 + (k < (int)n ? k : 0);
+            for (int j = 0; j < 3; ++j) rec[r0 + 3 * k + j] = lpts[4 * e + j];
           }
           rec[r0 + 9] = (double)n + 256.0 * (double)(ovf.size() / 4);
-          for (size_t e = kCellInline; e < n; ++e) {
-            for (int j = 0; j < 3; ++j) ovf.push_back(V[3 * ids[e] + j]);
-            ovf.push_back(0.0);
-          }
+          for (uint32_t e = l0 + kCellInline; e < l0 + n; ++e)
+            for (int j = 0; j < 4; ++j) ovf.push_back(lpts[4 * e + j]);
           if (free_mask != ~0ull) {
             rec[r0 + 10] = (double)(aux.size() / kWalkAux) + 1.0;
-            for (size_t e = 0; e < n; ++e) {
+            const size_t nw = ids.size();
+            aux.insert(aux.end(), {(double)(ends.size() / (kSub2K * kSub2K)), (double)nw, 0.0, 0.0, 0.0, 0.0, 0.0,
+                                   0.0});
+            for (int su = 0; su < subk; ++su)
+              for (int sv = 0; sv < subk; ++sv) {
+                if ((free_mask >> (su * subk + sv)) & 1ull) continue;
+                for (int fu = 0; fu < kSub2K; ++fu)
+                  for (int fv = 0; fv < kSub2K; ++fv) {
+                    const double a0 = -1.0 + cw * iu + sw * su + fw * fu - delta;
+                    const double a1 = -1.0 + cw * iu + sw * su + fw * (fu + 1) + delta;
+                    const double b0 = -1.0 + cw * iv + sw * sv + fw * fv - delta;
+                    const double b1 = -1.0 + cw * iv + sw * sv + fw * (fv + 1) + delta;
+                    ends.push_back(walk_cone_endpoint(V, nv, nbr, f, sg, a0, a1, b0, b1, X, vis));
+                  }
+              }
+            for (size_t e = 0; e < nw; ++e) {
               const int* nb = nbr + nbr[ids[e]];
-              uint32_t mask = 0;  // bit k: list entry k (k < 32) is a neighbour
-              for (size_t k = 0; k < n && k < 32; ++k)
+              uint32_t mask = 0;  // bit k: walk-list entry k (k < 32) is a neighbour
+              for (size_t k = 0; k < nw && k < 32; ++k)
                 for (int j = 1; j <= nb[0]; ++j)
                   if (nb[j] == ids[k]) mask |= 1u << k;
               aux.push_back((double)ids[e]);
               for (int j = 0; j < 3; ++j) aux.push_back(V[3 * wits[e] + j]);
               aux.push_back((double)mask);
+              for (int j = 0; j < 3; ++j) aux.push_back(V[3 * ids[e] + j]);
             }
           }
           std::memcpy(&rec[r0 + 11], &free_mask, 8);

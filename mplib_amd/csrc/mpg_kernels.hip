@@ -118,38 +118,83 @@ __device__ __forceinline__ V3 convex_full_scan(const DevWorld& w, cptr<double> H
 // ValidateTopology, oracle/collide_oracle.c support_convex): start at vertex
 // 0, scan the current vertex's neighbour list (FindVertexNeighbors: sorted,
 // from the faces), step to every unvisited neighbour whose value is >= the
-// best so far, until a pass moves nowhere.  Rarely run (the cell test below
-// settles most supports), so its visited set lives in LDS -- 512 bits per
-// thread of a block of <= 256 (world creation rejects larger walk hulls) --
-// instead of registers every caller would have to reserve.
+// best so far, until a pass moves nowhere.
+//
+// Most supports never walk: the direction's cell record settles them
+// (walk_cell_fast).  The few that must walk -- a lane or two per wave every
+// few MPR steps -- are resolved by the whole wave together, one pending lane
+// at a time (wave_walk): per step of the climb the active lanes load the
+// current vertex's neighbours and their dot products in parallel and the
+// pass's sequential '>=' scan replays from LDS, so a climb costs one memory
+// round trip per step instead of one per neighbour, and the per-lane rare path
+// no longer holds the other 63 lanes for the length of a serial walk.
 constexpr int kWalkWords = kMaxWalkVerts / 64;
-__device__ __forceinline__ V3 convex_walk(const DevWorld& w, cptr<double> HV, int geom, const V3 d) {
-  __shared__ uint64_t s_vis[kWalkWords][256];
-  uint64_t* vis = &s_vis[0][threadIdx.x];  // word j at vis[256 * j]
-  const cptr<int> nb = w.hull_nbr + w.geom_nbr[geom];
+struct WalkScratch {  // one per wave (blocks of <= 256 threads)
+  uint64_t vis[kWalkWords];
+  double dd[64];
+  int vi[64];
+};
+
+__device__ __forceinline__ WalkScratch& walk_scratch() {
+  __shared__ WalkScratch s_walk[4];
+  return s_walk[(threadIdx.x >> 6) & 3];
+}
+
+// LDS written by some lanes of this wave, read by others: keep the compiler
+// from moving the accesses across (the LDS unit serves one wave in order)
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
+__device__ __forceinline__ double lane_bcast(double v, int L) {
+  const unsigned long long u = (unsigned long long)__double_as_longlong(v);
+  const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)u, L);
+  const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(u >> 32), L);
+  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+
+// The climb for one (wave-uniform) direction d, by the wave's active lanes
+// (rank among nact).  Returns the final vertex index (uniform).
+__device__ __forceinline__ int wave_walk(const DevWorld& w, cptr<double> HV, int geom, const V3& d, int rank,
+                                         int nact) {
+  WalkScratch& S = walk_scratch();
+  const cptr<int> hd = w.hull_nbr + 2 * w.geom_nbr[geom];
   const int nwords = (w.geom_nvert[geom] + 63) >> 6;
-  for (int j = 0; j < nwords; ++j) vis[256 * j] = j == 0 ? 1ull : 0ull;
+  for (int j = rank; j < nwords; j += nact) S.vis[j] = j == 0 ? 1ull : 0ull;
+  wave_lds_sync();
   double best = edot(d, hull_vertex(w, HV, geom, 0));
   int bi = 0;
   bool keep = true;
   while (keep) {
     keep = false;
-    const int start = nb[bi], cnt = nb[start];
-    for (int k = start + 1; k <= start + cnt; ++k) {
-      const int vi = nb[k];
-      uint64_t* word = vis + 256 * (vi >> 6);
-      const uint64_t m = 1ull << (vi & 63);
-      if (*word & m) continue;
-      *word |= m;
-      const double dd = edot(d, hull_vertex(w, HV, geom, vi));
-      if (dd >= best) {
-        keep = true;
-        bi = vi;
-        best = dd;
+    const int start = hd[2 * bi], cnt = hd[2 * bi + 1];
+    for (int c0 = 0; c0 < cnt; c0 += nact) {
+      const int m = min(cnt - c0, nact);
+      if (rank < m) {
+        const cptr<double> e = w.nbr_ent + 4 * (size_t)(start + c0 + rank);
+        const int vi = (int)e[3];
+        const uint64_t bit = 1ull << (vi & 63);
+        const bool seen = (S.vis[vi >> 6] & bit) != 0ull;
+        if (!seen) atomicOr((unsigned long long*)&S.vis[vi >> 6], (unsigned long long)bit);
+        S.vi[rank] = seen ? -1 : vi;
+        S.dd[rank] = seen ? 0.0 : (d.x * e[0] + d.y * e[1]) + d.z * e[2];
       }
+      wave_lds_sync();
+      for (int k = 0; k < m; ++k) {  // the pass's scan, in list order
+        const int vi = S.vi[k];
+        const double dd = S.dd[k];
+        if (vi >= 0 && dd >= best) {
+          keep = true;
+          bi = vi;
+          best = dd;
+        }
+      }
+      wave_lds_sync();
     }
+    bi = __builtin_amdgcn_readfirstlane(bi);
   }
-  return hull_vertex(w, HV, geom, bi);
+  return bi;
 }
 
 // true if some neighbour of vertex vi has a dot product strictly above dd: then
@@ -157,25 +202,23 @@ __device__ __forceinline__ V3 convex_walk(const DevWorld& w, cptr<double> HV, in
 // running maximum, which only grows)
 __device__ __forceinline__ bool neighbour_beats(const DevWorld& w, cptr<double> HV, int geom, int vi, double dd,
                                                 const V3& d) {
-  const cptr<int> nb = w.hull_nbr + w.geom_nbr[geom];
-  const int start = nb[vi], cnt = nb[start];
-  for (int k = start + 1; k <= start + cnt; ++k)
-    if (edot(d, hull_vertex(w, HV, geom, nb[k])) > dd) return true;
+  const cptr<int> hd = w.hull_nbr + 2 * (w.geom_nbr[geom] + vi);
+  const cptr<double> e = w.nbr_ent + 4 * (size_t)hd[0];
+  const int cnt = hd[1];
+  for (int k = 0; k < cnt; ++k)
+    if ((d.x * e[4 * k] + d.y * e[4 * k + 1]) + d.z * e[4 * k + 2] > dd) return true;
   return false;
 }
 
 // Walk-hull support through its cell record (mpg_hullcells.h
-// build_walk_cells): the cell lists every vertex the walk could end at for a
-// direction of the cell (the others have a neighbour beating them on the whole
-// cell), in vertex order.  In a trap-free (sub)cell the list's unique maximum
-// is the walk's endpoint.  Otherwise the walk ends at a vertex none of whose
-// neighbours is strictly greater; the first maximum g of the list always
-// qualifies, so when every other listed vertex has a strictly greater
-// neighbour (g itself when adjacent, else usually its witness) the walk ends
-// at g; if not (a local maximum of the non-convex triangulation, or a tie)
-// the walk is run.
-__device__ __forceinline__ V3 walk_cell_support(const DevWorld& w, cptr<double> HV, int geom, cptr<double> R,
-                                                int sub, const V3& d) {
+// build_walk_cells).  In a trap-free subcell the walk ends at the unique
+// global maximum, the maximum of the record's linear list: returned, pend =
+// false.  In a trapped subcell whose fine cell has a certified endpoint (one
+// climb path for the whole fine cone) that vertex is returned.  Otherwise (a
+// tie at the maximum, or an uncertified fine cell) pend = true with the
+// linear list's first maximum in hand, for walk_resolve_wave.
+__device__ __forceinline__ V3 walk_cell_fast(const DevWorld& w, cptr<double> HV, int geom, cptr<double> R, int sub,
+                                             int fine, const V3& d, bool& pend) {
   const long long no = (long long)R[9];
   const int n = (int)(no & 255);
   const cptr<double> ovf = w.wcell_ovf + 4 * (size_t)(no >> 8);
@@ -202,52 +245,140 @@ __device__ __forceinline__ V3 walk_cell_support(const DevWorld& w, cptr<double> 
     }
   }
   const uint64_t free_mask = (uint64_t)__double_as_longlong(R[11]);
-  const bool fast = ((free_mask >> sub) & 1ull) && !tie;
+  const bool sub_free = (free_mask >> sub) & 1ull;
+  pend = !(sub_free && !tie);
+  int endp = -1;
+  if (!sub_free) {  // trapped subcell: its fine cell's certified endpoint, if any
+    const cptr<double> A = w.wcell_aux + kWalkAux * (size_t)(R[10] - 1.0);
+    const int t = (int)A[0] + __popcll(~free_mask & ((1ull << sub) - 1ull));
+    endp = w.wcell_end[(size_t)t * (kSub2K * kSub2K) + fine];
+    pend = endp < 0;
+  }
 #ifdef MPG_STATS
   if (w.stats) {
     atomicAdd(&w.stats[10], 1ull);
-    if (fast) atomicAdd(&w.stats[11], 1ull);
+    if (!pend) atomicAdd(&w.stats[11], 1ull);
+    if (endp >= 0) atomicAdd(&w.stats[14], 1ull);
   }
 #endif
-  auto entry = [&](int k) { return k < kCellInline ? R + 3 * k : ovf + 4 * (k - kCellInline); };
-  if (!fast) {
-    const double info = R[10];
-    bool ok = info > 0.0;  // trap-free but tied: straight to the walk
-    const cptr<double> A = w.wcell_aux + kWalkAux * (size_t)(ok ? info - 1.0 : 0.0);
-    for (int k = 0; k < n && ok; ++k) {
-      if (k == g) continue;
-      const cptr<double> e = entry(k), a = A + kWalkAux * k;
-      const double dd = (d.x * e[0] + d.y * e[1]) + d.z * e[2];
-      // the maximum g is a neighbour of this entry and strictly above it
-      if (g < 32 && ((((uint32_t)a[4]) >> g) & 1u) && best > dd) continue;
-      const double dw = (d.x * a[1] + d.y * a[2]) + d.z * a[3];
-      if (dw > dd) continue;
-      ok = neighbour_beats(w, HV, geom, (int)a[0], dd, d);
-    }
-#ifdef MPG_STATS
-    if (w.stats) atomicAdd(&w.stats[ok ? 12 : 13], 1ull);
-#endif
-    if (!ok) return convex_walk(w, HV, geom, d);
-  }
-  const cptr<double> e = entry(g);
+  if (endp >= 0) return hull_vertex(w, HV, geom, endp);
+  const cptr<double> e = g < kCellInline ? R + 3 * g : ovf + 4 * (g - kCellInline);
   return v3(e[0], e[1], e[2]);
 }
 
-// Convex support in the hull frame (FCL 0.7.0 supportConvex: the ccd
-// direction converted to Vector3<double>, findExtremeVertex in fp64).
-__device__ __forceinline__ V3 convex_support_local(const DevWorld& w, cptr<double> HV, int geom, const V3& d) {
+// The pending lanes of a wave, one at a time by every active lane.  For lane
+// L's trapped cell: the walk ends at the first maximum g of the walk list when
+// every other listed vertex has a strictly greater neighbour (g itself when
+// adjacent, else usually its witness, else a neighbour scan); the entries are
+// checked in parallel.  g is the global first maximum, already in lane L's p.
+// If that fails (a local maximum of the non-convex triangulation, a tie, or no
+// cell) the climb is run (wave_walk).
+__device__ __forceinline__ V3 walk_resolve_wave(const DevWorld& w, cptr<double> HV, int geom, const V3& d, int c,
+                                                bool pend, V3 p) {
+#ifdef MPG_AB_NORESOLVE  // timing ablation only: wrong results
+  return p;
+#endif
+  unsigned long long pm = __ballot(pend);
+#ifdef MPG_AB_NEVER  // timing ablation only: the resolve code stays, never runs
+  if (w.walk_subk > 0) return p;
+#endif
+  if (pm == 0ull) return p;
+  const unsigned long long act = __ballot(true);
+  const int nact = __popcll(act);
+  const int rank = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(act >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0u));
+  const int lane = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
   const int cb = w.geom_cbase[geom];
+  while (pm) {
+    const int L = __builtin_ctzll(pm);
+    pm &= pm - 1ull;
+    const V3 dL = v3(lane_bcast(d.x, L), lane_bcast(d.y, L), lane_bcast(d.z, L));
+    const int cL = __builtin_amdgcn_readlane(c, L);
+    bool ok = false;
+#ifdef MPG_STATS
+    const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+#endif
+    if (cL >= 0) {
+      const double info = w.wcell_rec[kCellRec * (size_t)(cb + cL) + 10];
+#ifdef MPG_WALK_NOVERIFY  // timing ablation: every pending lane climbs
+      ok = false;
+#else
+      ok = info > 0.0;  // trap-free cell but tied: straight to the walk
+#endif
+      if (ok) {
+        const cptr<double> A = w.wcell_aux + kWalkAux * (size_t)(info - 1.0);
+        const int nw = (int)A[1];
+        const cptr<double> E = A + kWalkAux;  // walk-list entries
+        double bL = -DBL_MAX;
+        int gL = 0;
+        for (int k = 0; k < nw; ++k) {  // its first maximum (uniform)
+          const cptr<double> e = E + kWalkAux * k;
+          const double dd = (dL.x * e[5] + dL.y * e[6]) + dL.z * e[7];
+          if (dd > bL) {
+            bL = dd;
+            gL = k;
+          }
+        }
+        bool fail = false;
+        for (int k = rank; k < nw; k += nact) {
+          if (k == gL) continue;
+          const cptr<double> a = E + kWalkAux * k;
+          const double dd = (dL.x * a[5] + dL.y * a[6]) + dL.z * a[7];
+          // the maximum g is a neighbour of this entry and strictly above it
+          if (gL < 32 && ((((uint32_t)a[4]) >> gL) & 1u) && bL > dd) continue;
+          const double dw = (dL.x * a[1] + dL.y * a[2]) + dL.z * a[3];
+          if (dw > dd) continue;
+          if (!neighbour_beats(w, HV, geom, (int)a[0], dd, dL)) fail = true;
+        }
+        ok = __ballot(fail) == 0ull;
+      }
+    }
+#ifdef MPG_STATS
+    const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+    if (w.stats && rank == 0) {
+      atomicAdd(&w.stats[ok ? 12 : 13], 1ull);
+      atomicAdd(&w.stats[9], t1 - t0);
+    }
+#endif
+    if (!ok) {
+      const int bi = wave_walk(w, HV, geom, dL, rank, nact);
+      if (lane == L) p = hull_vertex(w, HV, geom, bi);
+#ifdef MPG_STATS
+      if (w.stats && rank == 0) atomicAdd(&w.stats[15], __builtin_amdgcn_s_memtime() - t1);
+#endif
+    }
+  }
+  return p;
+}
+
+// Convex support in the hull frame (FCL 0.7.0 supportConvex: the ccd
+// direction converted to Vector3<double>, findExtremeVertex in fp64).  Called
+// by all active lanes of the wave together (geom is wave-uniform).
+__device__ __forceinline__ V3 convex_support_fast(const DevWorld& w, cptr<double> HV, int geom, const V3& d, bool& pend,
+                                                  int& cell) {
+  const int cb = w.geom_cbase[geom];
+  pend = false;
+  cell = -1;
   if (w.geom_nbr[geom] >= 0) {  // neighbour-walk hull (wave-uniform branch)
-    int sub = 0;
-    const int c = cb >= 0 ? hull_cell_sub(d.x, d.y, d.z, w.walk_subk, &sub) : -1;
-    if (c < 0) return convex_walk(w, HV, geom, d);
-    return walk_cell_support(w, HV, geom, w.wcell_rec + kCellRec * (size_t)(cb + c), sub, d);
+    int sub = 0, fine = 0;
+    pend = true;
+    cell = cb >= 0 ? hull_cell_sub(d.x, d.y, d.z, w.walk_subk, &sub, &fine) : -1;
+    V3 p = v3(0.0, 0.0, 0.0);
+    if (cell >= 0) p = walk_cell_fast(w, HV, geom, w.wcell_rec + kCellRec * (size_t)(cb + cell), sub, fine, d, pend);
+    return p;
   }
   const int c = cb >= 0 ? hull_cell(d.x, d.y, d.z) : -1;
   if (c < 0) return convex_full_scan(w, HV, geom, d);
   double p[3];
   cell_record_support(w.cell_rec + kCellRec * (size_t)(cb + c), w.cell_ovf, d.x, d.y, d.z, p);
   return v3(p[0], p[1], p[2]);
+}
+
+__device__ __forceinline__ V3 convex_support_local(const DevWorld& w, cptr<double> HV, int geom, const V3& d) {
+  bool pend;
+  int cell;
+  const V3 p = convex_support_fast(w, HV, geom, d, pend, cell);
+  if (w.geom_nbr[geom] < 0) return p;
+  return walk_resolve_wave(w, HV, geom, d, cell, pend, p);
 }
 
 // support mapping of one shape in its own frame (FCL shapeToGJK supports:
@@ -346,8 +477,33 @@ __device__ __forceinline__ CV3 msupport(const DevWorld& w, cptr<double> HV, cons
   const CV3 da = quat_rot(dir, a.rot_inv), db = quat_rot(vscale(dir, ccd_real(-1)), b.rot_inv);
   const int ga = __builtin_amdgcn_readfirstlane(a.geom), ta = __builtin_amdgcn_readfirstlane(a.type);
   const int gb = __builtin_amdgcn_readfirstlane(b.geom), tb = __builtin_amdgcn_readfirstlane(b.type);
-  const CV3 la = support_local(w, HV, ga, ta, da);
-  const CV3 lb = support_local(w, HV, gb, tb, db);
+  // walk hulls: both fast paths first, then one resolve site for the lanes
+  // either left pending (one inlined copy of the rare path instead of two)
+  bool pa = false, pb = false;
+  int ca = -1, cb = -1;
+  CV3 la, lb;
+  if (ta == MPG_GEOM_CONVEX) {
+    const V3 p = convex_support_fast(w, HV, ga, to_v3(da), pa, ca);
+    la = cv3(p.x, p.y, p.z);
+  } else {
+    la = support_local(w, HV, ga, ta, da);
+  }
+  if (tb == MPG_GEOM_CONVEX) {
+    const V3 p = convex_support_fast(w, HV, gb, to_v3(db), pb, cb);
+    lb = cv3(p.x, p.y, p.z);
+  } else {
+    lb = support_local(w, HV, gb, tb, db);
+  }
+  if (__ballot(pa || pb) != 0ull) {
+#pragma unroll 1
+    for (int s = 0; s < 2; ++s) {
+      const int g = s ? gb : ga;
+      const CV3 l = s ? lb : la;
+      const V3 p = walk_resolve_wave(w, HV, g, to_v3(s ? db : da), s ? cb : ca, s ? pb : pa, v3(l.x, l.y, l.z));
+      if (s) lb = cv3(p.x, p.y, p.z);
+      else la = cv3(p.x, p.y, p.z);
+    }
+  }
   return vsub(vadd(quat_rot(la, a.rot), a.pos), vadd(quat_rot(lb, b.rot), b.pos));
 }
 
@@ -3323,8 +3479,8 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
   // hulls in AoSoA-4 groups, padded with copies of the hull's first vertex
   std::vector<int> gstart(std::max(d->n_geoms, 1), 0), ngroups(std::max(d->n_geoms, 1), 0);
   std::vector<double> hull;
-  std::vector<int> cbase(std::max(d->n_geoms, 1), -1), geom_nbr(std::max(d->n_geoms, 1), -1), hull_nbr;
-  std::vector<double> cell_rec, cell_ovf, wcell_rec, wcell_ovf, wcell_aux;
+  std::vector<int> cbase(std::max(d->n_geoms, 1), -1), geom_nbr(std::max(d->n_geoms, 1), -1), hull_nbr, wcell_end;
+  std::vector<double> cell_rec, cell_ovf, wcell_rec, wcell_ovf, wcell_aux, nbr_ent;
   const int walk_subk =
       std::getenv("MPG_WALK_SUBK") ? std::max(1, std::min(8, std::atoi(std::getenv("MPG_WALK_SUBK")))) : kSubK;
   for (int g = 0; g < d->n_geoms; ++g) {
@@ -3340,10 +3496,18 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
       if (nvg > kMaxWalkVerts)
         return set_error(MPG_E_UNSUPPORTED, "convex hull with more than 512 vertices and watertight faces "
                                             "(FCL's neighbour-walk support) is not supported on the device");
-      geom_nbr[g] = (int)hull_nbr.size();
-      hull_nbr.insert(hull_nbr.end(), enc.begin(), enc.end());
+      geom_nbr[g] = (int)(hull_nbr.size() / 2);
+      for (int i = 0; i < nvg; ++i) {
+        const int st = enc[i], cnt = enc[st];
+        hull_nbr.push_back((int)(nbr_ent.size() / 4));
+        hull_nbr.push_back(cnt);
+        for (int k = 1; k <= cnt; ++k) {
+          const int vi = enc[st + k];
+          nbr_ent.insert(nbr_ent.end(), {Vg[3 * vi], Vg[3 * vi + 1], Vg[3 * vi + 2], (double)vi});
+        }
+      }
       const size_t r0 = wcell_rec.size();
-      if (build_walk_cells(Vg, nvg, enc.data(), walk_subk, wcell_rec, wcell_ovf, wcell_aux))
+      if (build_walk_cells(Vg, nvg, enc.data(), walk_subk, wcell_rec, wcell_ovf, wcell_aux, wcell_end))
         cbase[g] = (int)(r0 / kCellRec);
     } else {
       std::vector<uint32_t> cstart;
@@ -3367,10 +3531,12 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
   if (hull.empty()) hull.assign(12, 0.0);
   if (cell_rec.empty()) cell_rec.assign(kCellRec, 0.0);
   if (cell_ovf.empty()) cell_ovf.assign(4, 0.0);
-  if (hull_nbr.empty()) hull_nbr.assign(1, 0);
+  if (hull_nbr.empty()) hull_nbr.assign(2, 0);
+  if (nbr_ent.empty()) nbr_ent.assign(4, 0.0);
   if (wcell_rec.empty()) wcell_rec.assign(kCellRec, 0.0);
   if (wcell_ovf.empty()) wcell_ovf.assign(4, 0.0);
   if (wcell_aux.empty()) wcell_aux.assign(kWalkAux, 0.0);
+  if (wcell_end.empty()) wcell_end.assign(1, -1);
   // octrees: leaf boxes + a uniform grid per octree geometry (cells of at
   // least the largest leaf, <= 64 per axis); a leaf is listed in every cell
   // its box overlaps
@@ -3508,9 +3674,11 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
   const size_t o_covf = bb.add(cell_ovf.data(), cell_ovf.size());
   const size_t o_gnb = bb.add(geom_nbr.data(), geom_nbr.size());
   const size_t o_hnb = bb.add(hull_nbr.data(), hull_nbr.size());
+  const size_t o_nent = bb.add(nbr_ent.data(), nbr_ent.size());
   const size_t o_wrec = bb.add(wcell_rec.data(), wcell_rec.size());
   const size_t o_wovf = bb.add(wcell_ovf.data(), wcell_ovf.size());
   const size_t o_waux = bb.add(wcell_aux.data(), wcell_aux.size());
+  const size_t o_wend = bb.add(wcell_end.data(), wcell_end.size());
   const size_t o_ml = bb.add(d->moving_link, d->n_moving);
   const size_t o_mg = bb.add(d->moving_geom, d->n_moving);
   const size_t o_mo = bb.add(d->moving_offset, 12 * (size_t)d->n_moving);
@@ -3621,9 +3789,11 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
   dw.cell_ovf = to_cptr<double>(base + o_covf);
   dw.geom_nbr = to_cptr<int>(base + o_gnb);
   dw.hull_nbr = to_cptr<int>(base + o_hnb);
+  dw.nbr_ent = to_cptr<double>(base + o_nent);
   dw.wcell_rec = to_cptr<double>(base + o_wrec);
   dw.wcell_ovf = to_cptr<double>(base + o_wovf);
   dw.wcell_aux = to_cptr<double>(base + o_waux);
+  dw.wcell_end = to_cptr<int>(base + o_wend);
   dw.walk_subk = walk_subk;
   dw.moving_link = to_cptr<int>(base + o_ml);
   dw.moving_geom = to_cptr<int>(base + o_mg);
@@ -3706,8 +3876,9 @@ int mpg_world_destroy(mpg_world* w) {
     unsigned long long st[16];
     hipDeviceSynchronize();
     hipMemcpy(st, w->dw.stats, sizeof(st), hipMemcpyDeviceToHost);
-    std::fprintf(stderr, "[mpg stats] walk hulls: supports %llu, trap-free fast %llu, verified %llu, full walks %llu\n",
-                 st[10], st[11], st[12], st[13]);
+    std::fprintf(stderr, "[mpg stats] walk hulls: supports %llu, trap-free fast %llu, verified %llu, full walks %llu, "
+                 "certified endpoints %llu; resolve ticks: verify %llu, walk %llu\n",
+                 st[10], st[11], st[12], st[13], st[14], st[9], st[15]);
     std::fprintf(stderr,
                  "[mpg stats] narrow: refill %llu, support %llu, update %llu (memtime ticks, summed over waves); "
                  "steps %llu, mean active lanes/step %.1f; hits %llu (%.2f supports each), misses %llu (%.2f)\n",

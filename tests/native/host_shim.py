@@ -16,3 +16,17 @@ def lib():
         subprocess.check_call(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-fPIC", "-shared", "-o", out, src])
         _lib = ctypes.CDLL(out)
     return _lib
+
+
+_walk = None
+
+
+def walk_lib():
+    """tests/native/walk_cells.cpp: mpg_hullcells.h's walk-hull tables on the host."""
+    global _walk
+    if _walk is None:
+        out = os.path.join(tempfile.gettempdir(), "mplib_amd_walk_cells_%d.so" % os.getuid())
+        src = os.path.join(_HERE, "walk_cells.cpp")
+        subprocess.check_call(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-fPIC", "-shared", "-o", out, src])
+        _walk = ctypes.CDLL(out)
+    return _walk

@@ -1,0 +1,143 @@
+// Test shim: the walk-hull cell machinery of mplib_amd/csrc/mpg_hullcells.h
+// (cell lists, trap-free subcells, certified fine-cell endpoints) compiled for
+// the host, replayed per direction the way the device's walk_cell_fast /
+// walk_resolve_wave decide, and compared with FCL 0.7.0's neighbour walk run
+// from vertex 0 (oracle/collide_oracle.c support_convex).  Not part of the
+// product.
+#include <cfloat>
+#include <cstdint>
+#include <cstring>
+#include <vector>
+
+#include "../../mplib_amd/csrc/mpg_hullcells.h"
+
+using namespace mpg;
+
+namespace {
+
+double edot(const double* d, const double* p) { return (d[0] * p[0] + d[1] * p[1]) + d[2] * p[2]; }
+
+int fcl_walk(const double* V, int nv, const int* nbr, const double* d) {
+  std::vector<char> vis(nv, 0);
+  vis[0] = 1;
+  int bi = 0;
+  double best = edot(d, V);
+  bool keep = true;
+  while (keep) {
+    keep = false;
+    const int* nb = nbr + nbr[bi];
+    for (int k = 1; k <= nb[0]; ++k) {
+      const int u = nb[k];
+      if (vis[u]) continue;
+      vis[u] = 1;
+      const double dd = edot(d, V + 3 * u);
+      if (dd >= best) {
+        keep = true;
+        bi = u;
+        best = dd;
+      }
+    }
+  }
+  return bi;
+}
+
+}  // namespace
+
+extern "C" {
+// st: [0] directions, [1] trap-free fast, [2] certified endpoint, [3] pending,
+// [4] pending settled by the neighbour verification, [5] mismatches, [6]
+// trapped fine cells without a certified endpoint, [7] trapped fine cells,
+// [8 + j] directions whose cell list is longer than 3 + j
+// Returns -1 when FCL would not walk this hull.
+int walk_cells_check(const double* V, int nv, const int* faces, int nf, const double* dirs, long long n, int subk,
+                     long long* st) {
+  std::vector<int> enc;
+  if (!fcl_convex_neighbors(nv, faces, nf, enc)) return -1;
+  std::vector<double> rec, ovf, aux;
+  std::vector<int> ends;
+  if (!build_walk_cells(V, nv, enc.data(), subk, rec, ovf, aux, ends)) return -2;
+  for (int e : ends) {
+    st[7] += 1;
+    st[6] += e < 0;
+  }
+  const int* nbr = enc.data();
+  for (long long i = 0; i < n; ++i) {
+    const double* d = dirs + 3 * i;
+    st[0] += 1;
+    const int want = fcl_walk(V, nv, nbr, d);
+    int sub = 0, fine = 0;
+    const int c = hull_cell_sub(d[0], d[1], d[2], subk, &sub, &fine);
+    const double* got = nullptr;
+    if (c >= 0) {
+      const double* R = rec.data() + kCellRec * (size_t)c;
+      const long long no = (long long)R[9];
+      const int cnt = (int)(no & 255);
+      const double* O = ovf.data() + 4 * (size_t)(no >> 8);
+      auto entry = [&](int k) { return k < kCellInline ? R + 3 * k : O + 4 * (k - kCellInline); };
+      for (int j = 0; j < 4; ++j) st[8 + j] += cnt > 3 + j;  // list lengths
+      double best = -DBL_MAX;
+      int g = 0;
+      bool tie = false;
+      for (int k = 0; k < cnt; ++k) {
+        const double dd = edot(d, entry(k));
+        tie = dd == best || (tie && !(dd > best));
+        if (dd > best) {
+          best = dd;
+          g = k;
+        }
+      }
+      uint64_t free_mask;
+      std::memcpy(&free_mask, R + 11, 8);
+      const bool sub_free = (free_mask >> sub) & 1ull;
+      if (sub_free && !tie) {
+        got = entry(g);
+        st[1] += 1;
+      } else if (!sub_free) {
+        const double* A = aux.data() + kWalkAux * (size_t)(R[10] - 1.0);
+        const int t = (int)A[0] + __builtin_popcountll(~free_mask & ((1ull << sub) - 1ull));
+        const int e = ends[(size_t)t * (kSub2K * kSub2K) + fine];
+        if (e >= 0) {
+          got = V + 3 * e;
+          st[2] += 1;
+        }
+      }
+      if (!got && R[10] > 0.0) {  // the device's verification, over the walk list
+        st[3] += 1;
+        const double* A = aux.data() + kWalkAux * (size_t)(R[10] - 1.0);
+        const int nw = (int)A[1];
+        const double* E = A + kWalkAux;
+        double bw = -DBL_MAX;
+        int gw = 0;
+        for (int k = 0; k < nw; ++k)
+          if (edot(d, E + kWalkAux * k + 5) > bw) {
+            bw = edot(d, E + kWalkAux * k + 5);
+            gw = k;
+          }
+        bool ok = std::memcmp(E + kWalkAux * gw + 5, entry(g), 3 * sizeof(double)) == 0;  // same first maximum
+        if (!ok) st[5] += 1000000;
+        for (int k = 0; k < nw && ok; ++k) {
+          if (k == gw) continue;
+          const double* a = E + kWalkAux * k;
+          const double dd = edot(d, a + 5);
+          if (gw < 32 && ((((uint32_t)a[4]) >> gw) & 1u) && bw > dd) continue;
+          if (edot(d, a + 1) > dd) continue;
+          const int* nb = nbr + nbr[(int)a[0]];
+          bool beat = false;
+          for (int j = 1; j <= nb[0] && !beat; ++j) beat = edot(d, V + 3 * nb[j]) > dd;
+          ok = beat;
+        }
+        if (ok) {
+          got = entry(g);
+          st[4] += 1;
+        }
+      } else if (!got) {
+        st[3] += 1;
+      }
+    } else {
+      st[3] += 1;
+    }
+    if (got && std::memcmp(got, V + 3 * want, 3 * sizeof(double)) != 0) st[5] += 1;
+  }
+  return 0;
+}
+}

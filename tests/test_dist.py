@@ -55,3 +55,48 @@ def test_collide_sharded_gloo_world2(tmp_path):
         np.testing.assert_array_equal(d["flags"], fo)
         np.testing.assert_array_equal(d["masks"], mo)
     assert int(np.load(tmp_path / "r0.npz")["count"]) == 501
+
+
+def _worker_device(rank, world, port, q, out_dir):
+    """collide_sharded_device's split + gather with CPU tensors over gloo; the
+    per-rank compute (the oracle) writes into the given output slices."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    import torch
+    import torch.distributed as dist
+    import worlds as Wd
+    from mplib_amd.dist import collide_sharded_device
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    ow = Wd.oracle_world(3)
+    W = ow.W
+
+    def compute(qs, f, m):
+        fo, mo = ow.collide_batch(qs.numpy(), nthreads=1)
+        f.copy_(torch.from_numpy(fo))
+        m.copy_(torch.from_numpy(mo.view(np.int32)))
+
+    f, m, (s, c) = collide_sharded_device(compute, torch.from_numpy(q), mask_words=W)
+    fs, ms, _ = collide_sharded_device(compute, torch.from_numpy(q), gather=False, mask_words=W)
+    np.savez(os.path.join(out_dir, f"d{rank}.npz"), flags=f.numpy(), masks=m.numpy(), start=s, count=c,
+             shard_flags=fs.numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("n", [1001, 1000])
+def test_collide_sharded_device_gloo_world2(tmp_path, n):
+    mp = pytest.importorskip("torch.multiprocessing")
+    import worlds as Wd
+    ow = Wd.oracle_world(3)
+    q = Wd.sample_q(ow.art, n, 37)  # 1001: ragged shards, padding dropped after the gather
+    mp.start_processes(_worker_device, args=(2, _free_port(), q, str(tmp_path)), nprocs=2, join=True,
+                       start_method="spawn")
+    fo, mo = ow.collide_batch(q, nthreads=4)
+    for r in range(2):
+        d = np.load(tmp_path / f"d{r}.npz")
+        np.testing.assert_array_equal(d["flags"], fo)
+        np.testing.assert_array_equal(d["masks"].view(np.uint32), mo)
+        s, c = int(d["start"]), int(d["count"])
+        np.testing.assert_array_equal(d["shard_flags"], fo[s:s + c])
+    assert 0.0 < fo.mean() < 1.0

@@ -484,6 +484,50 @@ def test_concurrent_streams_do_not_share_workspace():
         np.testing.assert_array_equal(md.cpu().numpy().view(np.uint32), mo)
 
 
+def test_two_threads_overlapped_launches_race_free():
+    """Two host threads, each on its own torch stream, each launching
+    >= 2^19-configuration batches (the overlapped two-stream path) whose input
+    a copy kernel on that stream produced just before: per-call fork/join
+    events keep each call's side half ordered after its own stream only
+    (include/mpgpu.h thread-safety contract)."""
+    import threading
+    torch = pytest.importorskip("torch")
+    d = dw(3)
+    n = 1 << 19
+    qs = [[Wd.sample_q(ow(3).art, n, 300 + 10 * t + k) for k in range(2)] for t in range(2)]
+    srcs = [[torch.from_numpy(q).cuda() for q in row] for row in qs]
+    torch.cuda.synchronize()
+    outs = [[None, None], [None, None]]
+    errs = []
+
+    def run(t):
+        try:
+            s = torch.cuda.Stream()
+            for k in range(2):
+                with torch.cuda.stream(s):
+                    qd = srcs[t][k].clone()  # produced on s right before the call
+                    fd = torch.empty(n, dtype=torch.uint8, device="cuda")
+                    md = torch.empty((n, d.mask_words), dtype=torch.int32, device="cuda")
+                d.collide_batch(qd, fd, md, stream=s.cuda_stream)
+                outs[t][k] = (qd, fd, md)
+            s.synchronize()
+        except Exception as e:  # noqa: BLE001 - reported below
+            errs.append(e)
+
+    th = [threading.Thread(target=run, args=(t,)) for t in range(2)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    assert not errs, errs
+    torch.cuda.synchronize()
+    for t in range(2):
+        for k in range(2):
+            fo, mo = ow(3).collide_batch(qs[t][k], nthreads=NTHREADS)
+            np.testing.assert_array_equal(outs[t][k][1].cpu().numpy(), fo)
+            np.testing.assert_array_equal(outs[t][k][2].cpu().numpy().view(np.uint32), mo)
+
+
 def test_bench_two_ranks_gloo_one_gpu():
     """bench.py's multi-rank path (barrier, max over ranks, weak scaling) with
     two ranks sharing this box's GPU over gloo."""

@@ -76,6 +76,7 @@ def test_acm_change_updates_pair_table():
     assert len(changed) == 1 and (info[changed[0]][3], info[changed[0]][4]) == ("panda_hand", "red_cube")
 
 
+@pytest.mark.gpu  # attachObject's AttachedBody ctor evaluates the link pose (device FK)
 def test_attached_body_pairs():
     w, art = scenes.world(4)
     w.attach_object("held", pymp.fcl.Box([0.04, 0.04, 0.12]), "panda", 8, [0, 0, 0.14, 1, 0, 0, 0], ["panda_hand"])

@@ -1,7 +1,9 @@
-# headline bench, 3 repetitions (quick A/B against the previous commit's numbers)
+#!/bin/bash
+# full GPU suite, then kernel timings of every variants/*.so, the NO_WALK
+# ablation and the stats build
 set -o pipefail
 mkdir -p gpurun_out
-for i in 1 2 3; do
-  timeout -k 10 300 python bench.py --cpu-sample 0 --steps 30 > gpurun_out/ab_$i.json 2>/dev/null || exit 1
-  python3 -c "import json;d=json.load(open('gpurun_out/ab_$i.json'));print(round(d['value']/1e9,4), 'e9', round(d['step_ms_events'],4), {k:round(v['ms_per_step'],4) for k,v in d['stages'].items()})"
-done
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1; rc=$?
+tail -5 gpurun_out/pytest_gpu.log
+[ $rc -eq 0 ] || exit $rc
+bash tools/sweep.sh && bash tools/kt.sh nowalk MPG_DEBUG_NO_WALK=1 > /tmp/kt2.out 2>&1 && grep -E "==|narrow|cull" /tmp/kt2.out && bash tools/stats2.sh
