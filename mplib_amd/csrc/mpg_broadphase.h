@@ -24,6 +24,11 @@
 namespace mpg {
 
 constexpr float kBpMargin = 1e-4f;  // metres
+// fp32 cull rounding relative to the largest world coordinate it computes
+// (~20 dependent fp32 operations along a chain, each 6e-8 relative: 1.2e-6,
+// with 3x headroom); world creation keeps the margin above this times the
+// coordinate bound, so far-from-origin worlds keep the soundness argument
+constexpr double kFp32CullRel = 4e-6;
 
 // The broad phase is conservative by its margins, not bit-exact: its fp32
 // arithmetic may fuse multiply-adds (more accurate, fewer instructions) even

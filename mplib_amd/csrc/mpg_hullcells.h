@@ -35,6 +35,7 @@ constexpr double kHullMin = 1e-100, kHullMax = 1e100;  // max|coord| range with 
 constexpr double kCellWiden = 1e-5;  // cone widening: covers the fp32 cell arithmetic below
 constexpr int kSubK = 8;  // walk hulls: default subcells per axis of a cell that is not trap-free
 constexpr int kSub2K = 16;  // walk hulls: fine cells per axis of a trapped subcell (certified endpoints)
+constexpr int kSub3K = 4;   // walk hulls: finer cells per axis of a fine cell without a certified endpoint
 
 // cell of direction (x, y, z), or -1 (no cell: full scan).  The range checks
 // are exact (fp64); the cell arithmetic is fp32: the ratios u/|m| are off by
@@ -66,12 +67,13 @@ MPG_INLINE int hull_cell(double x, double y, double z) {
   return ((2 * f + (m < 0.0 ? 1 : 0)) * kCellK + iu) * kCellK + iv;
 }
 
-// hull_cell plus the subcell (subk x subk per cell) of the direction and its
-// fine cell within the subcell (kSub2K x kSub2K): the same fp32 ratios, so the
+// hull_cell plus the subcell (subk x subk per cell) of the direction, its
+// fine cell within the subcell (kSub2K x kSub2K) and its finer cell within the
+// fine cell (kSub3K x kSub3K): the same fp32 ratios, so the
 // direction lies in the widened subcone and fine cone as well (kCellWiden >>
 // the ratio error; the scalings by subk * kSub2K are exact for powers of two).
 // -1 / sub, fine undefined when there is no cell.
-MPG_INLINE int hull_cell_sub(double x, double y, double z, int subk, int* sub, int* fine) {
+MPG_INLINE int hull_cell_sub(double x, double y, double z, int subk, int* sub, int* fine, int* fine2) {
   const double ax = std::fabs(x), ay = std::fabs(y), az = std::fabs(z);
   if (!(ax <= kCellMax && ay <= kCellMax && az <= kCellMax)) return -1;  // also NaN
   if (!(ax >= kCellMin || ay >= kCellMin || az >= kCellMin)) return -1;
@@ -95,12 +97,14 @@ MPG_INLINE int hull_cell_sub(double x, double y, double z, int subk, int* sub, i
   int iu = (int)fu, iv = (int)fv;
   iu = iu < 0 ? 0 : (iu >= kCellK ? kCellK - 1 : iu);
   iv = iv < 0 ? 0 : (iv >= kCellK ? kCellK - 1 : iv);
-  const int kf = subk * kSub2K;
+  constexpr int kq = kSub2K * kSub3K;
+  const int kf = subk * kq;
   int ku = (int)((fu - (float)iu) * (float)kf), kv = (int)((fv - (float)iv) * (float)kf);
   ku = ku < 0 ? 0 : (ku >= kf ? kf - 1 : ku);
   kv = kv < 0 ? 0 : (kv >= kf ? kf - 1 : kv);
-  *sub = (ku / kSub2K) * subk + kv / kSub2K;
-  *fine = (ku % kSub2K) * kSub2K + kv % kSub2K;
+  *sub = (ku / kq) * subk + kv / kq;
+  *fine = ((ku % kq) / kSub3K) * kSub2K + (kv % kq) / kSub3K;
+  *fine2 = (ku % kSub3K) * kSub3K + kv % kSub3K;
   return ((2 * f + (m < 0.0 ? 1 : 0)) * kCellK + iu) * kCellK + iv;
 }
 
@@ -297,7 +301,8 @@ inline bool fcl_convex_neighbors(int nv, const int32_t* faces, int num_faces, st
 //   slot 10  0, or k + 1: the trapped cell's data at aux entry k (kWalkAux
 //            doubles each): a header (the index of its first endpoint table
 //            in ends: one table of kSub2K x kSub2K fine-cell endpoints, vertex
-//            index or -1, per trapped subcell in subcell order; the walk
+//            index, -1 (none), or -2 - r: finer table r of ends2 (kSub3K x
+//            kSub3K endpoints or -1), per trapped subcell in subcell order; the walk
 //            list's length), then per walk-list entry: vertex index, witness
 //            neighbour x, y, z -- the neighbour beating it on most of the cell
 //            --, the mask of the walk-list entries that are its neighbours,
@@ -451,19 +456,62 @@ inline int walk_cone_endpoint(const double* V, int nv, const int* nbr, int f, do
   return bi;
 }
 
+// The vertex that beats every other vertex by the rounding margin on the whole
+// cone (then it is the unique computed maximum for every direction of the
+// cone), or -1.
+inline int cone_single_max(const double* V, int nv, int f, double sg, double u0, double u1, double v0, double v1,
+                           double X) {
+  const double rel = 1e-9;
+  double r[4][3], M[4];
+  for (int k = 0; k < 4; ++k) {
+    r[k][f] = sg;
+    r[k][(f + 1) % 3] = (k & 1) ? u1 : u0;
+    r[k][(f + 2) % 3] = (k & 2) ? v1 : v0;
+    M[k] = rel * (std::fabs(r[k][0]) + std::fabs(r[k][1]) + std::fabs(r[k][2])) * X;
+  }
+  const double c[3] = {r[0][0] + r[3][0], r[0][1] + r[3][1], r[0][2] + r[3][2]};
+  int u = 0;
+  for (int i = 1; i < nv; ++i)
+    if (c[0] * V[3 * i] + c[1] * V[3 * i + 1] + c[2] * V[3 * i + 2] >
+        c[0] * V[3 * u] + c[1] * V[3 * u + 1] + c[2] * V[3 * u + 2])
+      u = i;
+  for (int i = 0; i < nv; ++i) {
+    if (i == u) continue;
+    const double a[3] = {V[3 * u] - V[3 * i], V[3 * u + 1] - V[3 * i + 1], V[3 * u + 2] - V[3 * i + 2]};
+    for (int k = 0; k < 4; ++k)
+      if (!(r[k][0] * a[0] + r[k][1] * a[1] + r[k][2] * a[2] > M[k])) return -1;
+  }
+  return u;
+}
+
+// Certified walk endpoint of a cone: one climb path for the whole cone
+// (walk_cone_endpoint), or a trap-free cone (walk_cell_trap_free on its own
+// walk list) whose maximum is one vertex by the margin everywhere -- the walk
+// ends at the computed maximum there, whatever path it takes.  -1: neither.
+inline int cone_endpoint(const double* V, int nv, const int* nbr, int f, double sg, double u0, double u1, double v0,
+                         double v1, double X, std::vector<char>& vis, std::vector<int>& ids, std::vector<int>& wits) {
+  const int e = walk_cone_endpoint(V, nv, nbr, f, sg, u0, u1, v0, v1, X, vis);
+  if (e >= 0) return e;
+  const int u = cone_single_max(V, nv, f, sg, u0, u1, v0, v1, X);
+  if (u < 0) return -1;
+  walk_cone_list(V, nv, nbr, f, sg, u0, u1, v0, v1, X, ids, wits);
+  return walk_cell_trap_free(V, nv, nbr, ids, f, sg, u0, u1, v0, v1, X) ? u : -1;
+}
+
 // Walk-hull cell table: kCellsPerHull records in hull_cell order (layout
 // above), overflow entries in ovf, trapped cells' walk lists and verification
 // data in aux, certified endpoints of the trapped subcells' fine cells in ends.
 inline bool build_walk_cells(const double* V, int nv, const int* nbr, int subk, std::vector<double>& rec,
-                             std::vector<double>& ovf, std::vector<double>& aux, std::vector<int>& ends) {
+                             std::vector<double>& ovf, std::vector<double>& aux, std::vector<int>& ends,
+                             std::vector<int>& ends2) {
   double X = 0.0;
   for (int i = 0; i < 3 * nv; ++i) X = std::max(X, std::fabs(V[i]));
   if (nv <= 0 || !(X >= kHullMin && X <= kHullMax) || subk < 1 || subk * subk > 64) return false;
   std::vector<uint32_t> lstart;
   std::vector<double> lpts;
   if (!build_hull_cells(V, nv, lstart, lpts)) return false;
-  const double delta = kCellWiden, cw = 2.0 / kCellK, sw = cw / subk, fw = sw / kSub2K;
-  std::vector<int> ids, wits, sids, swits;
+  const double delta = kCellWiden, cw = 2.0 / kCellK, sw = cw / subk, fw = sw / kSub2K, gw = fw / kSub3K;
+  std::vector<int> ids, wits, sids, swits, fids, fwits;
   std::vector<char> vis;
   int c = 0;  // hull_cell order: ((2 f + s) K + iu) K + iv
   for (int f = 0; f < 3; ++f)
@@ -511,7 +559,24 @@ inline bool build_walk_cells(const double* V, int nv, const int* nbr, int subk, 
                     const double a1 = -1.0 + cw * iu + sw * su + fw * (fu + 1) + delta;
                     const double b0 = -1.0 + cw * iv + sw * sv + fw * fv - delta;
                     const double b1 = -1.0 + cw * iv + sw * sv + fw * (fv + 1) + delta;
-                    ends.push_back(walk_cone_endpoint(V, nv, nbr, f, sg, a0, a1, b0, b1, X, vis));
+                    int e = cone_endpoint(V, nv, nbr, f, sg, a0, a1, b0, b1, X, vis, fids, fwits);
+                    if (e < 0) {  // a climb decision flips inside: try its kSub3K x kSub3K finer cells
+                      const size_t r = ends2.size() / (kSub3K * kSub3K);
+                      int found = 0;
+                      for (int gu = 0; gu < kSub3K; ++gu)
+                        for (int gv = 0; gv < kSub3K; ++gv) {
+                          const double c0 = -1.0 + cw * iu + sw * su + fw * fu + gw * gu - delta;
+                          const double c1 = -1.0 + cw * iu + sw * su + fw * fu + gw * (gu + 1) + delta;
+                          const double d0 = -1.0 + cw * iv + sw * sv + fw * fv + gw * gv - delta;
+                          const double d1 = -1.0 + cw * iv + sw * sv + fw * fv + gw * (gv + 1) + delta;
+                          const int e2 = cone_endpoint(V, nv, nbr, f, sg, c0, c1, d0, d1, X, vis, fids, fwits);
+                          ends2.push_back(e2);
+                          found += e2 >= 0;
+                        }
+                      if (found) e = -2 - (int)r;
+                      else ends2.resize(r * (kSub3K * kSub3K));
+                    }
+                    ends.push_back(e);
                   }
               }
             for (size_t e = 0; e < nw; ++e) {

@@ -218,7 +218,7 @@ __device__ __forceinline__ bool neighbour_beats(const DevWorld& w, cptr<double> 
 // tie at the maximum, or an uncertified fine cell) pend = true with the
 // linear list's first maximum in hand, for walk_resolve_wave.
 __device__ __forceinline__ V3 walk_cell_fast(const DevWorld& w, cptr<double> HV, int geom, cptr<double> R, int sub,
-                                             int fine, const V3& d, bool& pend) {
+                                             int fine, int fine2, const V3& d, bool& pend) {
   const long long no = (long long)R[9];
   const int n = (int)(no & 255);
   const cptr<double> ovf = w.wcell_ovf + 4 * (size_t)(no >> 8);
@@ -246,12 +246,16 @@ __device__ __forceinline__ V3 walk_cell_fast(const DevWorld& w, cptr<double> HV,
   }
   const uint64_t free_mask = (uint64_t)__double_as_longlong(R[11]);
   const bool sub_free = (free_mask >> sub) & 1ull;
+#ifdef MPG_AB_NOTIE  // timing ablation only
+  tie = false;
+#endif
   pend = !(sub_free && !tie);
   int endp = -1;
-  if (!sub_free) {  // trapped subcell: its fine cell's certified endpoint, if any
+  if (__builtin_expect(!sub_free, 0)) {  // trapped subcell: its fine cell's certified endpoint, if any
     const cptr<double> A = w.wcell_aux + kWalkAux * (size_t)(R[10] - 1.0);
     const int t = (int)A[0] + __popcll(~free_mask & ((1ull << sub) - 1ull));
     endp = w.wcell_end[(size_t)t * (kSub2K * kSub2K) + fine];
+    if (endp <= -2) endp = w.wcell_end2[(size_t)(-2 - endp) * (kSub3K * kSub3K) + fine2];
     pend = endp < 0;
   }
 #ifdef MPG_STATS
@@ -259,6 +263,7 @@ __device__ __forceinline__ V3 walk_cell_fast(const DevWorld& w, cptr<double> HV,
     atomicAdd(&w.stats[10], 1ull);
     if (!pend) atomicAdd(&w.stats[11], 1ull);
     if (endp >= 0) atomicAdd(&w.stats[14], 1ull);
+    if (pend) atomicAdd(&w.stats[sub_free ? 16 : 17], 1ull);  // pending: tie / uncertified fine cell
   }
 #endif
   if (endp >= 0) return hull_vertex(w, HV, geom, endp);
@@ -282,7 +287,7 @@ __device__ __forceinline__ V3 walk_resolve_wave(const DevWorld& w, cptr<double> 
 #ifdef MPG_AB_NEVER  // timing ablation only: the resolve code stays, never runs
   if (w.walk_subk > 0) return p;
 #endif
-  if (pm == 0ull) return p;
+  if (__builtin_expect(pm == 0ull, 1)) return p;
   const unsigned long long act = __ballot(true);
   const int nact = __popcll(act);
   const int rank = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(act >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0u));
@@ -359,11 +364,12 @@ __device__ __forceinline__ V3 convex_support_fast(const DevWorld& w, cptr<double
   pend = false;
   cell = -1;
   if (w.geom_nbr[geom] >= 0) {  // neighbour-walk hull (wave-uniform branch)
-    int sub = 0, fine = 0;
+    int sub = 0, fine = 0, fine2 = 0;
     pend = true;
-    cell = cb >= 0 ? hull_cell_sub(d.x, d.y, d.z, w.walk_subk, &sub, &fine) : -1;
+    cell = cb >= 0 ? hull_cell_sub(d.x, d.y, d.z, w.walk_subk, &sub, &fine, &fine2) : -1;
     V3 p = v3(0.0, 0.0, 0.0);
-    if (cell >= 0) p = walk_cell_fast(w, HV, geom, w.wcell_rec + kCellRec * (size_t)(cb + cell), sub, fine, d, pend);
+    if (cell >= 0)
+      p = walk_cell_fast(w, HV, geom, w.wcell_rec + kCellRec * (size_t)(cb + cell), sub, fine, fine2, d, pend);
     return p;
   }
   const int c = cb >= 0 ? hull_cell(d.x, d.y, d.z) : -1;
@@ -494,7 +500,7 @@ __device__ __forceinline__ CV3 msupport(const DevWorld& w, cptr<double> HV, cons
   } else {
     lb = support_local(w, HV, gb, tb, db);
   }
-  if (__ballot(pa || pb) != 0ull) {
+  if (__builtin_expect(__ballot(pa || pb) != 0ull, 0)) {  // rare: laid out off the hot path
 #pragma unroll 1
     for (int s = 0; s < 2; ++s) {
       const int g = s ? gb : ga;
@@ -3479,7 +3485,7 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
   // hulls in AoSoA-4 groups, padded with copies of the hull's first vertex
   std::vector<int> gstart(std::max(d->n_geoms, 1), 0), ngroups(std::max(d->n_geoms, 1), 0);
   std::vector<double> hull;
-  std::vector<int> cbase(std::max(d->n_geoms, 1), -1), geom_nbr(std::max(d->n_geoms, 1), -1), hull_nbr, wcell_end;
+  std::vector<int> cbase(std::max(d->n_geoms, 1), -1), geom_nbr(std::max(d->n_geoms, 1), -1), hull_nbr, wcell_end, wcell_end2;
   std::vector<double> cell_rec, cell_ovf, wcell_rec, wcell_ovf, wcell_aux, nbr_ent;
   const int walk_subk =
       std::getenv("MPG_WALK_SUBK") ? std::max(1, std::min(8, std::atoi(std::getenv("MPG_WALK_SUBK")))) : kSubK;
@@ -3507,7 +3513,7 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
         }
       }
       const size_t r0 = wcell_rec.size();
-      if (build_walk_cells(Vg, nvg, enc.data(), walk_subk, wcell_rec, wcell_ovf, wcell_aux, wcell_end))
+      if (build_walk_cells(Vg, nvg, enc.data(), walk_subk, wcell_rec, wcell_ovf, wcell_aux, wcell_end, wcell_end2))
         cbase[g] = (int)(r0 / kCellRec);
     } else {
       std::vector<uint32_t> cstart;
@@ -3537,6 +3543,7 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
   if (wcell_ovf.empty()) wcell_ovf.assign(4, 0.0);
   if (wcell_aux.empty()) wcell_aux.assign(kWalkAux, 0.0);
   if (wcell_end.empty()) wcell_end.assign(1, -1);
+  if (wcell_end2.empty()) wcell_end2.assign(1, -1);
   // octrees: leaf boxes + a uniform grid per octree geometry (cells of at
   // least the largest leaf, <= 64 per axis); a leaf is listed in every cell
   // its box overlaps
@@ -3679,6 +3686,7 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
   const size_t o_wovf = bb.add(wcell_ovf.data(), wcell_ovf.size());
   const size_t o_waux = bb.add(wcell_aux.data(), wcell_aux.size());
   const size_t o_wend = bb.add(wcell_end.data(), wcell_end.size());
+  const size_t o_wend2 = bb.add(wcell_end2.data(), wcell_end2.size());
   const size_t o_ml = bb.add(d->moving_link, d->n_moving);
   const size_t o_mg = bb.add(d->moving_geom, d->n_moving);
   const size_t o_mo = bb.add(d->moving_offset, 12 * (size_t)d->n_moving);
@@ -3757,6 +3765,24 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
     }
     const double reach = kCcdFalseHitReach * (1.0 + 1e-3) + 1e-5;
     dw.bp_margin = may_mpr ? (float)std::max((double)kBpMargin, reach) : kBpMargin;
+    // the fp32 broad phase's rounding grows with coordinate magnitude: bound
+    // every world coordinate the cull computes (the chain's reach -- sum of
+    // the placement translations, revolute joints cannot lengthen it --,
+    // moving offsets, static poses, geometry radii; a prismatic joint of the
+    // move group adds its travel, which the snapshot cannot bound) and keep
+    // the margin above kFp32CullRel of it (kBpMargin covers a ~2 m world
+    // near the origin)
+    auto sq3 = [](const double* v) { return v[0] * v[0] + v[1] * v[1] + v[2] * v[2]; };
+    double reach_x = 0.0, geo_r = 0.0, stat_x = 0.0;
+    for (int j = 0; j < d->n_joints; ++j) reach_x += std::sqrt(sq3(d->joint_placement + 12 * j + 9));
+    for (int l = 0; l < d->n_links; ++l) reach_x += std::sqrt(sq3(d->link_placement + 12 * l + 9));
+    double off = 0.0;
+    for (int m = 0; m < d->n_moving; ++m) off = std::max(off, std::sqrt(sq3(d->moving_offset + 12 * m + 9)));
+    for (int g = 0; g < d->n_geoms; ++g) geo_r = std::max(geo_r, geom_rec[G_STRIDE * g + G_RADIUS] +
+                                                                     std::sqrt(sq3(&geom_rec[G_STRIDE * g + G_OBB_C])));
+    for (int s2 = 0; s2 < d->n_static; ++s2) stat_x = std::max(stat_x, std::sqrt(sq3(d->static_transform + 12 * s2 + 9)));
+    const double X = std::max(reach_x + off, stat_x) + geo_r;
+    dw.bp_margin = std::max(dw.bp_margin, (float)(kFp32CullRel * X));
     dw.small_margin = may_mpr ? std::max(kSmallMargin, reach) : kSmallMargin;
     if (const char* m = std::getenv("MPG_DEBUG_MARGIN")) {  // ablation only: changes results
       dw.bp_margin = (float)std::atof(m);
@@ -3766,8 +3792,8 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
   dw.debug_mode = std::getenv("MPG_DEBUG_CULL") ? std::atoi(std::getenv("MPG_DEBUG_CULL")) : 0;
   dw.stats = nullptr;
   if (std::getenv("MPG_STATS") && std::atoi(std::getenv("MPG_STATS")) > 0) {
-    HIP_TRY(hipMalloc(&dw.stats, 16 * sizeof(unsigned long long)));
-    HIP_TRY(hipMemset(dw.stats, 0, 16 * sizeof(unsigned long long)));
+    HIP_TRY(hipMalloc(&dw.stats, 24 * sizeof(unsigned long long)));
+    HIP_TRY(hipMemset(dw.stats, 0, 24 * sizeof(unsigned long long)));
   }
   dw.joint_type = to_cptr<int>(base + o_jt);
   dw.joint_parent = to_cptr<int>(base + o_jp);
@@ -3794,6 +3820,7 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
   dw.wcell_ovf = to_cptr<double>(base + o_wovf);
   dw.wcell_aux = to_cptr<double>(base + o_waux);
   dw.wcell_end = to_cptr<int>(base + o_wend);
+  dw.wcell_end2 = to_cptr<int>(base + o_wend2);
   dw.walk_subk = walk_subk;
   dw.moving_link = to_cptr<int>(base + o_ml);
   dw.moving_geom = to_cptr<int>(base + o_mg);
@@ -3873,12 +3900,12 @@ int mpg_world_destroy(mpg_world* w) {
   if (!w) return MPG_OK;
   hipSetDevice(w->device);
   if (w->dw.stats) {
-    unsigned long long st[16];
+    unsigned long long st[24];
     hipDeviceSynchronize();
     hipMemcpy(st, w->dw.stats, sizeof(st), hipMemcpyDeviceToHost);
     std::fprintf(stderr, "[mpg stats] walk hulls: supports %llu, trap-free fast %llu, verified %llu, full walks %llu, "
-                 "certified endpoints %llu; resolve ticks: verify %llu, walk %llu\n",
-                 st[10], st[11], st[12], st[13], st[14], st[9], st[15]);
+                 "certified endpoints %llu; pending: tie %llu, uncertified %llu; resolve ticks: verify %llu, walk %llu\n",
+                 st[10], st[11], st[12], st[13], st[14], st[16], st[17], st[9], st[15]);
     std::fprintf(stderr,
                  "[mpg stats] narrow: refill %llu, support %llu, update %llu (memtime ticks, summed over waves); "
                  "steps %llu, mean active lanes/step %.1f; hits %llu (%.2f supports each), misses %llu (%.2f)\n",

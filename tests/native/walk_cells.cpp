@@ -46,7 +46,7 @@ int fcl_walk(const double* V, int nv, const int* nbr, const double* d) {
 extern "C" {
 // st: [0] directions, [1] trap-free fast, [2] certified endpoint, [3] pending,
 // [4] pending settled by the neighbour verification, [5] mismatches, [6]
-// trapped fine cells without a certified endpoint, [7] trapped fine cells,
+// trapped fine cells with neither a certified endpoint nor a finer table, [7] trapped fine cells,
 // [8 + j] directions whose cell list is longer than 3 + j
 // Returns -1 when FCL would not walk this hull.
 int walk_cells_check(const double* V, int nv, const int* faces, int nf, const double* dirs, long long n, int subk,
@@ -54,19 +54,19 @@ int walk_cells_check(const double* V, int nv, const int* faces, int nf, const do
   std::vector<int> enc;
   if (!fcl_convex_neighbors(nv, faces, nf, enc)) return -1;
   std::vector<double> rec, ovf, aux;
-  std::vector<int> ends;
-  if (!build_walk_cells(V, nv, enc.data(), subk, rec, ovf, aux, ends)) return -2;
+  std::vector<int> ends, ends2;
+  if (!build_walk_cells(V, nv, enc.data(), subk, rec, ovf, aux, ends, ends2)) return -2;
   for (int e : ends) {
     st[7] += 1;
-    st[6] += e < 0;
+    st[6] += e == -1;
   }
   const int* nbr = enc.data();
   for (long long i = 0; i < n; ++i) {
     const double* d = dirs + 3 * i;
     st[0] += 1;
     const int want = fcl_walk(V, nv, nbr, d);
-    int sub = 0, fine = 0;
-    const int c = hull_cell_sub(d[0], d[1], d[2], subk, &sub, &fine);
+    int sub = 0, fine = 0, fine2 = 0;
+    const int c = hull_cell_sub(d[0], d[1], d[2], subk, &sub, &fine, &fine2);
     const double* got = nullptr;
     if (c >= 0) {
       const double* R = rec.data() + kCellRec * (size_t)c;
@@ -95,7 +95,8 @@ int walk_cells_check(const double* V, int nv, const int* faces, int nf, const do
       } else if (!sub_free) {
         const double* A = aux.data() + kWalkAux * (size_t)(R[10] - 1.0);
         const int t = (int)A[0] + __builtin_popcountll(~free_mask & ((1ull << sub) - 1ull));
-        const int e = ends[(size_t)t * (kSub2K * kSub2K) + fine];
+        int e = ends[(size_t)t * (kSub2K * kSub2K) + fine];
+        if (e <= -2) e = ends2[(size_t)(-2 - e) * (kSub3K * kSub3K) + fine2];
         if (e >= 0) {
           got = V + 3 * e;
           st[2] += 1;

@@ -105,9 +105,10 @@ def test_product_world_matches_golden(golden_dir, cfg, name):
     np.testing.assert_array_equal(m, g["masks"])
 
 
-@pytest.mark.parametrize("cfg,n", [(2, 1 << 16), (3, 1 << 20), (4, 1 << 18)])
+@pytest.mark.parametrize("cfg,n", [(2, 1 << 16), (3, 1 << 20), (4, 1 << 22)])
 def test_product_full_size_parity(cfg, n):
-    """BASELINE sizes (cfg4 reduced to 2^18 so the oracle finishes in seconds)."""
+    """Every flag and pair bit at the BASELINE sizes (cfg4: the whole 2^22
+    batch of BASELINE.json's strong-scaling config on one GPU)."""
     w, art = scenes.world(cfg)
     q = scenes.sample_states(art, n, scenes.CFG_SEED[cfg])
     f, m = w.collide_batch(q)

@@ -22,9 +22,9 @@ OFFSET_RPY = (0.0, 0.0, 3.14159265358979)
 B_QPOS = [0.3, -0.4, 0.2, -2.2, 0.1, 2.0, 0.6]
 
 
-def offset_panda_urdf() -> str:
-    """The Panda URDF with a new root link fixed at OFFSET (MPlib 0.1.1 has no
-    articulation base pose; a second robot gets its place from its URDF).
+def offset_panda_urdf(xyz=OFFSET_XYZ, rpy=OFFSET_RPY) -> str:
+    """The Panda URDF with a new root link fixed at (xyz, rpy) (MPlib 0.1.1 has
+    no articulation base pose; a second robot gets its place from its URDF).
     Written next to a link to the Panda's mesh directory."""
     src = os.path.join(Wd.panda_dir(), "panda.urdf")
     d = tempfile.mkdtemp(prefix="panda_off_")
@@ -33,8 +33,8 @@ def offset_panda_urdf() -> str:
     head = text.index(">", text.index("<robot")) + 1
     extra = ('\n  <link name="offset_base"/>\n  <joint name="offset_joint" type="fixed">\n'
              f'    <parent link="offset_base"/>\n    <child link="panda_link0"/>\n'
-             f'    <origin xyz="{OFFSET_XYZ[0]} {OFFSET_XYZ[1]} {OFFSET_XYZ[2]}" '
-             f'rpy="{OFFSET_RPY[0]} {OFFSET_RPY[1]} {OFFSET_RPY[2]}"/>\n  </joint>\n')
+             f'    <origin xyz="{xyz[0]} {xyz[1]} {xyz[2]}" '
+             f'rpy="{rpy[0]} {rpy[1]} {rpy[2]}"/>\n  </joint>\n')
     path = os.path.join(d, "panda.urdf")
     open(path, "w").write(text[:head] + extra + text[head:])
     return path
@@ -152,3 +152,32 @@ def test_two_pandas_match_oracle(b_planned):
     # some configurations collide only through the second robot
     arts = [p for p, k in enumerate(keys) if "b_panda" in (k[0], k[1]) and k[0] != k[1]]
     assert any(((m[:, p >> 5] >> (p & 31)) & 1).any() for p in arts)
+
+
+FAR = (310.0, -205.5, 42.25)
+
+
+@pytest.mark.gpu
+def test_far_from_origin_world_matches_oracle():
+    """The whole cfg3 world (robot base and boxes) moved ~370 m from the
+    origin: the fp32 cull's margin grows with the world's coordinate bound
+    (kFp32CullRel), so every flag and pair bit still equals the oracle's."""
+    from mplib_amd import pymp, scenes
+    urdf = offset_panda_urdf(FAR, (0.0, 0.0, 0.0))
+    art = pymp.articulation.ArticulatedModel(urdf, os.path.join(scenes.PANDA_DIR, "panda.srdf"), [0, 0, -9.81],
+                                             scenes.PANDA_JOINTS, scenes.PANDA_LINKS, verbose=False, convex=True)
+    art.set_move_group("panda_hand")
+    w = pymp.planning_world.PlanningWorld([art], ["panda"], [], [])
+    scene = []
+    for name, side, pos in scenes._boxes():
+        p = [pos[i] + FAR[i] for i in range(3)]
+        w.add_normal_object(name, pymp.fcl.CollisionObject(pymp.fcl.Box(list(side)), p, [1, 0, 0, 0]))
+        scene.append((name, M.BoxGeom(tuple(float(x) for x in side)), (list(M.IDENT[0]), [float(x) for x in p])))
+    w.get_allowed_collision_matrix().set_entry("panda_link0", "table", True)
+    ow = oracle.OracleWorld(oracle_panda(urdf), scene=scene, allowed=[("panda_link0", "table")])
+    q = Wd.sample_q(ow.art, 1 << 17, 77)
+    f, m = w.collide_batch(q)
+    fo, mo = ow.collide_batch(q, nthreads=16)
+    np.testing.assert_array_equal(f, fo)
+    np.testing.assert_array_equal(m.view(np.uint32), mo)
+    assert 0.05 < fo.mean() < 0.95
