@@ -61,6 +61,7 @@ struct DevWorld {
   cptr<double> wcell_aux;  // trapped (sub)cells' verification data (mpg_hullcells.h)
   cptr<int> wcell_end;     // certified walk endpoints of the trapped subcells' fine cells
   cptr<int> wcell_end2;    // ... and of the finer cells of uncertified fine cells
+  cptr<int> wcell_pre;     // climb prefix records of still undecided finer cells (WalkPrefix)
   int walk_subk;           // subcells per axis of a trapped cell
   cptr<int> moving_link;     // [n_moving]
   cptr<int> moving_geom;

@@ -301,8 +301,9 @@ inline bool fcl_convex_neighbors(int nv, const int32_t* faces, int num_faces, st
 //   slot 10  0, or k + 1: the trapped cell's data at aux entry k (kWalkAux
 //            doubles each): a header (the index of its first endpoint table
 //            in ends: one table of kSub2K x kSub2K fine-cell endpoints, vertex
-//            index, -1 (none), or -2 - r: finer table r of ends2 (kSub3K x
-//            kSub3K endpoints or -1), per trapped subcell in subcell order; the walk
+//            index, or -2 - r: finer table r of ends2 (kSub3K x kSub3K
+//            endpoints, or -2 - q: climb prefix record q of pres, kWalkPre ints
+//            -- see WalkPrefix), per trapped subcell in subcell order; the walk
 //            list's length), then per walk-list entry: vertex index, witness
 //            neighbour x, y, z -- the neighbour beating it on most of the cell
 //            --, the mask of the walk-list entries that are its neighbours,
@@ -414,8 +415,19 @@ inline void walk_cone_list(const double* V, int nv, const int* nbr, int f, doubl
 // them, so the rounded fp64 dot products then compare the same way), or u and
 // b coincide (equal values, '>=' holds).  Then every direction of the cone
 // takes the same path and ends at the same vertex.
+// Where the climb's replay stopped when a comparison flips inside the cone:
+// the running maximum bi, the pass vertex pv whose neighbour list was being
+// scanned, the undecided entry's index k in that list, whether the pass had
+// moved before it, and the visited set at that point.  The device resumes the
+// climb there (wave_walk) instead of from vertex 0.
+constexpr int kWalkPre = 4 + 2 * (kMaxWalkVerts / 64);  // ints per record
+struct WalkPrefix {
+  int bi, pv, k, keep;
+  uint64_t vis[kMaxWalkVerts / 64];
+};
+
 inline int walk_cone_endpoint(const double* V, int nv, const int* nbr, int f, double sg, double u0, double u1,
-                              double v0, double v1, double X, std::vector<char>& vis) {
+                              double v0, double v1, double X, std::vector<char>& vis, WalkPrefix* pre = nullptr) {
   const double rel = 1e-9;
   double r[4][3], M[4];
   for (int k = 0; k < 4; ++k) {
@@ -430,11 +442,11 @@ inline int walk_cone_endpoint(const double* V, int nv, const int* nbr, int f, do
   bool keep = true;
   while (keep) {
     keep = false;
-    const int* nb = nbr + nbr[bi];
+    const int pv = bi;
+    const int* nb = nbr + nbr[pv];
     for (int k = 1; k <= nb[0]; ++k) {
       const int u = nb[k];
       if (vis[u]) continue;
-      vis[u] = 1;
       const double a[3] = {V[3 * u] - V[3 * bi], V[3 * u + 1] - V[3 * bi + 1], V[3 * u + 2] - V[3 * bi + 2]};
       bool ge = a[0] == 0.0 && a[1] == 0.0 && a[2] == 0.0;
       if (!ge) {
@@ -444,9 +456,21 @@ inline int walk_cone_endpoint(const double* V, int nv, const int* nbr, int f, do
           above += t > M[c];
           below += t < -M[c];
         }
-        if (above != 4 && below != 4) return -1;  // the comparison flips inside the cone
+        if (above != 4 && below != 4) {  // the comparison flips inside the cone
+          if (pre) {
+            pre->bi = bi;
+            pre->pv = pv;
+            pre->k = k - 1;
+            pre->keep = keep;
+            std::memset(pre->vis, 0, sizeof(pre->vis));
+            for (int i = 0; i < nv; ++i)
+              if (vis[i]) pre->vis[i >> 6] |= 1ull << (i & 63);
+          }
+          return -1;
+        }
         ge = above == 4;
       }
+      vis[u] = 1;
       if (ge) {
         keep = true;
         bi = u;
@@ -489,8 +513,9 @@ inline int cone_single_max(const double* V, int nv, int f, double sg, double u0,
 // walk list) whose maximum is one vertex by the margin everywhere -- the walk
 // ends at the computed maximum there, whatever path it takes.  -1: neither.
 inline int cone_endpoint(const double* V, int nv, const int* nbr, int f, double sg, double u0, double u1, double v0,
-                         double v1, double X, std::vector<char>& vis, std::vector<int>& ids, std::vector<int>& wits) {
-  const int e = walk_cone_endpoint(V, nv, nbr, f, sg, u0, u1, v0, v1, X, vis);
+                         double v1, double X, std::vector<char>& vis, std::vector<int>& ids, std::vector<int>& wits,
+                         WalkPrefix* pre = nullptr) {
+  const int e = walk_cone_endpoint(V, nv, nbr, f, sg, u0, u1, v0, v1, X, vis, pre);
   if (e >= 0) return e;
   const int u = cone_single_max(V, nv, f, sg, u0, u1, v0, v1, X);
   if (u < 0) return -1;
@@ -503,7 +528,7 @@ inline int cone_endpoint(const double* V, int nv, const int* nbr, int f, double 
 // data in aux, certified endpoints of the trapped subcells' fine cells in ends.
 inline bool build_walk_cells(const double* V, int nv, const int* nbr, int subk, std::vector<double>& rec,
                              std::vector<double>& ovf, std::vector<double>& aux, std::vector<int>& ends,
-                             std::vector<int>& ends2) {
+                             std::vector<int>& ends2, std::vector<int>& pres) {
   double X = 0.0;
   for (int i = 0; i < 3 * nv; ++i) X = std::max(X, std::fabs(V[i]));
   if (nv <= 0 || !(X >= kHullMin && X <= kHullMax) || subk < 1 || subk * subk > 64) return false;
@@ -560,21 +585,26 @@ inline bool build_walk_cells(const double* V, int nv, const int* nbr, int subk, 
                     const double b0 = -1.0 + cw * iv + sw * sv + fw * fv - delta;
                     const double b1 = -1.0 + cw * iv + sw * sv + fw * (fv + 1) + delta;
                     int e = cone_endpoint(V, nv, nbr, f, sg, a0, a1, b0, b1, X, vis, fids, fwits);
-                    if (e < 0) {  // a climb decision flips inside: try its kSub3K x kSub3K finer cells
-                      const size_t r = ends2.size() / (kSub3K * kSub3K);
-                      int found = 0;
+                    if (e < 0) {  // a climb decision flips inside: its kSub3K x kSub3K finer cells
+                      e = -2 - (int)(ends2.size() / (kSub3K * kSub3K));
                       for (int gu = 0; gu < kSub3K; ++gu)
                         for (int gv = 0; gv < kSub3K; ++gv) {
                           const double c0 = -1.0 + cw * iu + sw * su + fw * fu + gw * gu - delta;
                           const double c1 = -1.0 + cw * iu + sw * su + fw * fu + gw * (gu + 1) + delta;
                           const double d0 = -1.0 + cw * iv + sw * sv + fw * fv + gw * gv - delta;
                           const double d1 = -1.0 + cw * iv + sw * sv + fw * fv + gw * (gv + 1) + delta;
-                          const int e2 = cone_endpoint(V, nv, nbr, f, sg, c0, c1, d0, d1, X, vis, fids, fwits);
+                          WalkPrefix pre;
+                          int e2 = cone_endpoint(V, nv, nbr, f, sg, c0, c1, d0, d1, X, vis, fids, fwits, &pre);
+                          if (e2 < 0) {  // still undecided: where the climb can resume
+                            e2 = -2 - (int)(pres.size() / kWalkPre);
+                            pres.insert(pres.end(), {pre.bi, pre.pv, pre.k, pre.keep});
+                            for (int j = 0; j < kMaxWalkVerts / 64; ++j) {
+                              pres.push_back((int)(uint32_t)pre.vis[j]);
+                              pres.push_back((int)(uint32_t)(pre.vis[j] >> 32));
+                            }
+                          }
                           ends2.push_back(e2);
-                          found += e2 >= 0;
                         }
-                      if (found) e = -2 - (int)r;
-                      else ends2.resize(r * (kSub3K * kSub3K));
                     }
                     ends.push_back(e);
                   }

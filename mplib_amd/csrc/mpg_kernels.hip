@@ -155,20 +155,26 @@ __device__ __forceinline__ double lane_bcast(double v, int L) {
 }
 
 // The climb for one (wave-uniform) direction d, by the wave's active lanes
-// (rank among nact).  Returns the final vertex index (uniform).
+// (rank among nact), from vertex 0 or resumed from a prefix record (pre:
+// mpg_hullcells.h WalkPrefix, the state where the host's replay stopped).
+// Returns the final vertex index (uniform).
 __device__ __forceinline__ int wave_walk(const DevWorld& w, cptr<double> HV, int geom, const V3& d, int rank,
-                                         int nact) {
+                                         int nact, cptr<int> pre) {
   WalkScratch& S = walk_scratch();
   const cptr<int> hd = w.hull_nbr + 2 * w.geom_nbr[geom];
   const int nwords = (w.geom_nvert[geom] + 63) >> 6;
-  for (int j = rank; j < nwords; j += nact) S.vis[j] = j == 0 ? 1ull : 0ull;
+  for (int j = rank; j < nwords; j += nact)
+    S.vis[j] = pre ? (uint64_t)(uint32_t)pre[4 + 2 * j] | ((uint64_t)(uint32_t)pre[5 + 2 * j] << 32) : (j == 0 ? 1ull : 0ull);
   wave_lds_sync();
-  double best = edot(d, hull_vertex(w, HV, geom, 0));
-  int bi = 0;
-  bool keep = true;
-  while (keep) {
-    keep = false;
-    const int start = hd[2 * bi], cnt = hd[2 * bi + 1];
+  int bi = pre ? pre[0] : 0, pv = pre ? pre[1] : 0, k0 = pre ? pre[2] : 0;
+  bool keep = pre ? pre[3] != 0 : false, first = true;
+  double best = edot(d, hull_vertex(w, HV, geom, bi));
+  do {
+    const int v = first ? pv : bi;  // the pass scans v's list (v fixed for the pass)
+    const int skip = first ? k0 : 0;
+    bool moved = first && keep;
+    first = false;
+    const int start = hd[2 * v] + skip, cnt = hd[2 * v + 1] - skip;
     for (int c0 = 0; c0 < cnt; c0 += nact) {
       const int m = min(cnt - c0, nact);
       if (rank < m) {
@@ -185,7 +191,7 @@ __device__ __forceinline__ int wave_walk(const DevWorld& w, cptr<double> HV, int
         const int vi = S.vi[k];
         const double dd = S.dd[k];
         if (vi >= 0 && dd >= best) {
-          keep = true;
+          moved = true;
           bi = vi;
           best = dd;
         }
@@ -193,7 +199,8 @@ __device__ __forceinline__ int wave_walk(const DevWorld& w, cptr<double> HV, int
       wave_lds_sync();
     }
     bi = __builtin_amdgcn_readfirstlane(bi);
-  }
+    keep = moved;
+  } while (keep);
   return bi;
 }
 
@@ -218,7 +225,7 @@ __device__ __forceinline__ bool neighbour_beats(const DevWorld& w, cptr<double> 
 // tie at the maximum, or an uncertified fine cell) pend = true with the
 // linear list's first maximum in hand, for walk_resolve_wave.
 __device__ __forceinline__ V3 walk_cell_fast(const DevWorld& w, cptr<double> HV, int geom, cptr<double> R, int sub,
-                                             int fine, int fine2, const V3& d, bool& pend) {
+                                             int fine, int fine2, const V3& d, bool& pend, int& pre) {
   const long long no = (long long)R[9];
   const int n = (int)(no & 255);
   const cptr<double> ovf = w.wcell_ovf + 4 * (size_t)(no >> 8);
@@ -257,6 +264,7 @@ __device__ __forceinline__ V3 walk_cell_fast(const DevWorld& w, cptr<double> HV,
     endp = w.wcell_end[(size_t)t * (kSub2K * kSub2K) + fine];
     if (endp <= -2) endp = w.wcell_end2[(size_t)(-2 - endp) * (kSub3K * kSub3K) + fine2];
     pend = endp < 0;
+    pre = endp <= -2 ? -2 - endp : -1;
   }
 #ifdef MPG_STATS
   if (w.stats) {
@@ -279,7 +287,7 @@ __device__ __forceinline__ V3 walk_cell_fast(const DevWorld& w, cptr<double> HV,
 // If that fails (a local maximum of the non-convex triangulation, a tie, or no
 // cell) the climb is run (wave_walk).
 __device__ __forceinline__ V3 walk_resolve_wave(const DevWorld& w, cptr<double> HV, int geom, const V3& d, int c,
-                                                bool pend, V3 p) {
+                                                bool pend, int pre, V3 p) {
 #ifdef MPG_AB_NORESOLVE  // timing ablation only: wrong results
   return p;
 #endif
@@ -298,6 +306,15 @@ __device__ __forceinline__ V3 walk_resolve_wave(const DevWorld& w, cptr<double> 
     pm &= pm - 1ull;
     const V3 dL = v3(lane_bcast(d.x, L), lane_bcast(d.y, L), lane_bcast(d.z, L));
     const int cL = __builtin_amdgcn_readlane(c, L);
+    const int preL = __builtin_amdgcn_readlane(pre, L);
+    if (preL >= 0) {  // undecided finer cell: resume the climb where the host's replay stopped
+      const int bi = wave_walk(w, HV, geom, dL, rank, nact, w.wcell_pre + kWalkPre * (size_t)preL);
+      if (lane == L) p = hull_vertex(w, HV, geom, bi);
+#ifdef MPG_STATS
+      if (w.stats && rank == 0) atomicAdd(&w.stats[18], 1ull);
+#endif
+      continue;
+    }
     bool ok = false;
 #ifdef MPG_STATS
     const unsigned long long t0 = __builtin_amdgcn_s_memtime();
@@ -345,7 +362,7 @@ __device__ __forceinline__ V3 walk_resolve_wave(const DevWorld& w, cptr<double> 
     }
 #endif
     if (!ok) {
-      const int bi = wave_walk(w, HV, geom, dL, rank, nact);
+      const int bi = wave_walk(w, HV, geom, dL, rank, nact, nullptr);
       if (lane == L) p = hull_vertex(w, HV, geom, bi);
 #ifdef MPG_STATS
       if (w.stats && rank == 0) atomicAdd(&w.stats[15], __builtin_amdgcn_s_memtime() - t1);
@@ -359,17 +376,18 @@ __device__ __forceinline__ V3 walk_resolve_wave(const DevWorld& w, cptr<double> 
 // direction converted to Vector3<double>, findExtremeVertex in fp64).  Called
 // by all active lanes of the wave together (geom is wave-uniform).
 __device__ __forceinline__ V3 convex_support_fast(const DevWorld& w, cptr<double> HV, int geom, const V3& d, bool& pend,
-                                                  int& cell) {
+                                                  int& cell, int& pre) {
   const int cb = w.geom_cbase[geom];
   pend = false;
   cell = -1;
+  pre = -1;
   if (w.geom_nbr[geom] >= 0) {  // neighbour-walk hull (wave-uniform branch)
     int sub = 0, fine = 0, fine2 = 0;
     pend = true;
     cell = cb >= 0 ? hull_cell_sub(d.x, d.y, d.z, w.walk_subk, &sub, &fine, &fine2) : -1;
     V3 p = v3(0.0, 0.0, 0.0);
     if (cell >= 0)
-      p = walk_cell_fast(w, HV, geom, w.wcell_rec + kCellRec * (size_t)(cb + cell), sub, fine, fine2, d, pend);
+      p = walk_cell_fast(w, HV, geom, w.wcell_rec + kCellRec * (size_t)(cb + cell), sub, fine, fine2, d, pend, pre);
     return p;
   }
   const int c = cb >= 0 ? hull_cell(d.x, d.y, d.z) : -1;
@@ -381,10 +399,10 @@ __device__ __forceinline__ V3 convex_support_fast(const DevWorld& w, cptr<double
 
 __device__ __forceinline__ V3 convex_support_local(const DevWorld& w, cptr<double> HV, int geom, const V3& d) {
   bool pend;
-  int cell;
-  const V3 p = convex_support_fast(w, HV, geom, d, pend, cell);
+  int cell, pre;
+  const V3 p = convex_support_fast(w, HV, geom, d, pend, cell, pre);
   if (w.geom_nbr[geom] < 0) return p;
-  return walk_resolve_wave(w, HV, geom, d, cell, pend, p);
+  return walk_resolve_wave(w, HV, geom, d, cell, pend, pre, p);
 }
 
 // support mapping of one shape in its own frame (FCL shapeToGJK supports:
@@ -486,16 +504,16 @@ __device__ __forceinline__ CV3 msupport(const DevWorld& w, cptr<double> HV, cons
   // walk hulls: both fast paths first, then one resolve site for the lanes
   // either left pending (one inlined copy of the rare path instead of two)
   bool pa = false, pb = false;
-  int ca = -1, cb = -1;
+  int ca = -1, cb = -1, qa = -1, qb = -1;
   CV3 la, lb;
   if (ta == MPG_GEOM_CONVEX) {
-    const V3 p = convex_support_fast(w, HV, ga, to_v3(da), pa, ca);
+    const V3 p = convex_support_fast(w, HV, ga, to_v3(da), pa, ca, qa);
     la = cv3(p.x, p.y, p.z);
   } else {
     la = support_local(w, HV, ga, ta, da);
   }
   if (tb == MPG_GEOM_CONVEX) {
-    const V3 p = convex_support_fast(w, HV, gb, to_v3(db), pb, cb);
+    const V3 p = convex_support_fast(w, HV, gb, to_v3(db), pb, cb, qb);
     lb = cv3(p.x, p.y, p.z);
   } else {
     lb = support_local(w, HV, gb, tb, db);
@@ -505,7 +523,8 @@ __device__ __forceinline__ CV3 msupport(const DevWorld& w, cptr<double> HV, cons
     for (int s = 0; s < 2; ++s) {
       const int g = s ? gb : ga;
       const CV3 l = s ? lb : la;
-      const V3 p = walk_resolve_wave(w, HV, g, to_v3(s ? db : da), s ? cb : ca, s ? pb : pa, v3(l.x, l.y, l.z));
+      const V3 p = walk_resolve_wave(w, HV, g, to_v3(s ? db : da), s ? cb : ca, s ? pb : pa, s ? qb : qa,
+                                     v3(l.x, l.y, l.z));
       if (s) lb = cv3(p.x, p.y, p.z);
       else la = cv3(p.x, p.y, p.z);
     }
@@ -3485,7 +3504,7 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
   // hulls in AoSoA-4 groups, padded with copies of the hull's first vertex
   std::vector<int> gstart(std::max(d->n_geoms, 1), 0), ngroups(std::max(d->n_geoms, 1), 0);
   std::vector<double> hull;
-  std::vector<int> cbase(std::max(d->n_geoms, 1), -1), geom_nbr(std::max(d->n_geoms, 1), -1), hull_nbr, wcell_end, wcell_end2;
+  std::vector<int> cbase(std::max(d->n_geoms, 1), -1), geom_nbr(std::max(d->n_geoms, 1), -1), hull_nbr, wcell_end, wcell_end2, wcell_pre;
   std::vector<double> cell_rec, cell_ovf, wcell_rec, wcell_ovf, wcell_aux, nbr_ent;
   const int walk_subk =
       std::getenv("MPG_WALK_SUBK") ? std::max(1, std::min(8, std::atoi(std::getenv("MPG_WALK_SUBK")))) : kSubK;
@@ -3513,7 +3532,7 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
         }
       }
       const size_t r0 = wcell_rec.size();
-      if (build_walk_cells(Vg, nvg, enc.data(), walk_subk, wcell_rec, wcell_ovf, wcell_aux, wcell_end, wcell_end2))
+      if (build_walk_cells(Vg, nvg, enc.data(), walk_subk, wcell_rec, wcell_ovf, wcell_aux, wcell_end, wcell_end2, wcell_pre))
         cbase[g] = (int)(r0 / kCellRec);
     } else {
       std::vector<uint32_t> cstart;
@@ -3544,6 +3563,7 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
   if (wcell_aux.empty()) wcell_aux.assign(kWalkAux, 0.0);
   if (wcell_end.empty()) wcell_end.assign(1, -1);
   if (wcell_end2.empty()) wcell_end2.assign(1, -1);
+  if (wcell_pre.empty()) wcell_pre.assign(kWalkPre, 0);
   // octrees: leaf boxes + a uniform grid per octree geometry (cells of at
   // least the largest leaf, <= 64 per axis); a leaf is listed in every cell
   // its box overlaps
@@ -3687,6 +3707,7 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
   const size_t o_waux = bb.add(wcell_aux.data(), wcell_aux.size());
   const size_t o_wend = bb.add(wcell_end.data(), wcell_end.size());
   const size_t o_wend2 = bb.add(wcell_end2.data(), wcell_end2.size());
+  const size_t o_wpre = bb.add(wcell_pre.data(), wcell_pre.size());
   const size_t o_ml = bb.add(d->moving_link, d->n_moving);
   const size_t o_mg = bb.add(d->moving_geom, d->n_moving);
   const size_t o_mo = bb.add(d->moving_offset, 12 * (size_t)d->n_moving);
@@ -3821,6 +3842,7 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
   dw.wcell_aux = to_cptr<double>(base + o_waux);
   dw.wcell_end = to_cptr<int>(base + o_wend);
   dw.wcell_end2 = to_cptr<int>(base + o_wend2);
+  dw.wcell_pre = to_cptr<int>(base + o_wpre);
   dw.walk_subk = walk_subk;
   dw.moving_link = to_cptr<int>(base + o_ml);
   dw.moving_geom = to_cptr<int>(base + o_mg);
@@ -3904,8 +3926,8 @@ int mpg_world_destroy(mpg_world* w) {
     hipDeviceSynchronize();
     hipMemcpy(st, w->dw.stats, sizeof(st), hipMemcpyDeviceToHost);
     std::fprintf(stderr, "[mpg stats] walk hulls: supports %llu, trap-free fast %llu, verified %llu, full walks %llu, "
-                 "certified endpoints %llu; pending: tie %llu, uncertified %llu; resolve ticks: verify %llu, walk %llu\n",
-                 st[10], st[11], st[12], st[13], st[14], st[16], st[17], st[9], st[15]);
+                 "certified endpoints %llu; pending: tie %llu, uncertified %llu, resumed %llu; resolve ticks: verify %llu, walk %llu\n",
+                 st[10], st[11], st[12], st[13], st[14], st[16], st[17], st[18], st[9], st[15]);
     std::fprintf(stderr,
                  "[mpg stats] narrow: refill %llu, support %llu, update %llu (memtime ticks, summed over waves); "
                  "steps %llu, mean active lanes/step %.1f; hits %llu (%.2f supports each), misses %llu (%.2f)\n",

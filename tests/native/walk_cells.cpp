@@ -54,8 +54,8 @@ int walk_cells_check(const double* V, int nv, const int* faces, int nf, const do
   std::vector<int> enc;
   if (!fcl_convex_neighbors(nv, faces, nf, enc)) return -1;
   std::vector<double> rec, ovf, aux;
-  std::vector<int> ends, ends2;
-  if (!build_walk_cells(V, nv, enc.data(), subk, rec, ovf, aux, ends, ends2)) return -2;
+  std::vector<int> ends, ends2, pres;
+  if (!build_walk_cells(V, nv, enc.data(), subk, rec, ovf, aux, ends, ends2, pres)) return -2;
   for (int e : ends) {
     st[7] += 1;
     st[6] += e == -1;
@@ -100,6 +100,34 @@ int walk_cells_check(const double* V, int nv, const int* faces, int nf, const do
         if (e >= 0) {
           got = V + 3 * e;
           st[2] += 1;
+        } else if (e <= -2) {  // resume the climb from the prefix record, as the device does
+          const int* P = pres.data() + (size_t)kWalkPre * (-2 - e);
+          std::vector<char> vis(nv, 0);
+          for (int i = 0; i < nv; ++i) vis[i] = ((uint32_t)P[4 + 2 * (i >> 6) + ((i & 63) >> 5)] >> (i & 31)) & 1u;
+          int bi = P[0], pv = P[1], k0 = P[2];
+          bool keep = P[3] != 0, first = true;
+          double best = edot(d, V + 3 * bi);
+          do {
+            const int v = first ? pv : bi;
+            const int* nb = nbr + nbr[v];
+            bool moved = first ? keep : false;
+            for (int k = (first ? k0 : 0) + 1; k <= nb[0]; ++k) {
+              const int u = nb[k];
+              if (vis[u]) continue;
+              vis[u] = 1;
+              const double dd = edot(d, V + 3 * u);
+              if (dd >= best) {
+                moved = true;
+                bi = u;
+                best = dd;
+              }
+            }
+            first = false;
+            keep = moved;
+          } while (keep);
+          st[3] += 1;
+          st[4] += 1;  // counted as settled without the full climb
+          got = V + 3 * bi;
         }
       }
       if (!got && R[10] > 0.0) {  // the device's verification, over the walk list
