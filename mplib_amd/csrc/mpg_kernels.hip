@@ -229,28 +229,35 @@ __device__ __forceinline__ V3 walk_cell_fast(const DevWorld& w, cptr<double> HV,
   const long long no = (long long)R[9];
   const int n = (int)(no & 255);
   const cptr<double> ovf = w.wcell_ovf + 4 * (size_t)(no >> 8);
+  // first maximum (strict '>', as the reference's scan) ...
   double best = -DBL_MAX;
   int g = 0;
-  bool tie = false;
+  double di[kCellInline];
 #pragma unroll
   for (int k = 0; k < kCellInline; ++k) {
-    const double dd = (d.x * R[3 * k] + d.y * R[3 * k + 1]) + d.z * R[3 * k + 2];
-    const bool in = k < n;
-    tie = in && (dd == best || (tie && !(dd > best)));
-    if (in && dd > best) {
-      best = dd;
+    di[k] = (d.x * R[3 * k] + d.y * R[3 * k + 1]) + d.z * R[3 * k + 2];
+    if (k < n && di[k] > best) {
+      best = di[k];
       g = k;
     }
   }
+  int nmax = 0;  // ... and how many entries reach it (a tie when > 1)
   for (int k = kCellInline; k < n; ++k) {
     const cptr<double> e = ovf + 4 * (k - kCellInline);
     const double dd = (d.x * e[0] + d.y * e[1]) + d.z * e[2];
-    tie = dd == best || (tie && !(dd > best));
-    if (dd > best) {
+    if (dd > best) {  // a new maximum: the inline entries are all below it
       best = dd;
       g = k;
+      nmax = 1;
+    } else if (dd == best) {
+      ++nmax;
     }
   }
+  // the inline entries, compared with the final maximum (short lists repeat
+  // their first entry: count only k < n)
+#pragma unroll
+  for (int k = 0; k < kCellInline; ++k) nmax += (k < n && di[k] == best) ? 1 : 0;
+  bool tie = nmax > 1;
   const uint64_t free_mask = (uint64_t)__double_as_longlong(R[11]);
   const bool sub_free = (free_mask >> sub) & 1ull;
 #ifdef MPG_AB_NOTIE  // timing ablation only
