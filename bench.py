@@ -346,10 +346,11 @@ def plan_main(args, world, rank, local, backend):
 
 
 def lib_hash() -> str:
-    """sha256 (16 hex) of the HIP library this run loaded: profiles are keyed by it."""
-    import hashlib
-    p = os.path.join(ROOT, "mplib_amd", "lib", "libmpgpu.so")
-    return hashlib.sha256(open(p, "rb").read()).hexdigest()[:16] if os.path.exists(p) else ""
+    """Hash of the sources and HIP flags libmpgpu.so is built from
+    (tools/build_hash.py): profiles are keyed by it."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    from build_hash import build_hash
+    return build_hash()
 
 
 def pmc_record(cfg):

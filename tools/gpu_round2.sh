@@ -18,3 +18,7 @@ for c in 2 4 5; do
   head -c 400 gpurun_out/bench_${TAG}_cfg$c.json; echo
 done
 NCFG=524288 bash tools/profile.sh $TAG
+# the bench line again with the PMC record of this very build (valu_roofline, traffic)
+cp gpurun_out/prof_$TAG/pmc_summary.json profiles/pmc_cfg3.json
+timeout -k 10 300 python bench.py > gpurun_out/bench_${TAG}_final.json 2> gpurun_out/bench_${TAG}_final.err || { tail gpurun_out/bench_${TAG}_final.err; exit 1; }
+cat gpurun_out/bench_${TAG}_final.json
