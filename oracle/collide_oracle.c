@@ -1090,6 +1090,384 @@ static int closed_form_intersect(const orc_world *w, int ga, const real *Ta, int
     return -1;
 }
 
+/* ------------------------------------------------ FCL closed-form contacts
+ * CollisionRequest(enable_contact=True) on a closed-form pair: the contacts
+ * GJKSolver_libccd::shapeIntersect's specialisations emit [ext FCL 0.7.0,
+ * not under /root/reference: restated from its published source, parity
+ * unpinned], reduced to the ONE contact ShapeShapeCollide keeps for
+ * MPlib's num_max_contacts = 1: with more contacts than free slots it
+ * std::partial_sort()s them by descending penetration_depth and keeps the
+ * first, which for one slot is the first contact with the largest value.
+ * box-sphere orders flip the normal (flipNormal).  Output: depth, normal,
+ * pos (world frame); returns the boolean result.  *n_contacts = contacts
+ * emitted (0 when boxBox2 reports a collision without a contact point). */
+
+/* ODE dLineClosestApproach as box_box-inl.h lineClosestApproach */
+static void line_closest_approach(const real *pa, const real *ua, const real *pb, const real *ub, real *alpha,
+                                  real *beta) {
+    const real p[3] = {pb[0] - pa[0], pb[1] - pa[1], pb[2] - pa[2]};
+    const real uaub = (ua[0] * ub[0] + ua[1] * ub[1]) + ua[2] * ub[2];
+    const real q1 = (ua[0] * p[0] + ua[1] * p[1]) + ua[2] * p[2];
+    const real q2 = -((ub[0] * p[0] + ub[1] * p[1]) + ub[2] * p[2]);
+    real d = 1 - uaub * uaub;
+    if (d <= (real)0.0001f) { *alpha = 0; *beta = 0; }
+    else { d = 1 / d; *alpha = (q1 + uaub * q2) * d; *beta = (uaub * q1 + q2) * d; }
+}
+
+/* ODE intersectRectQuad as box_box-inl.h intersectRectQuad2: clip the quad
+ * p (4 points) against the rectangle |x| <= h[0], |y| <= h[1] */
+static int intersect_rect_quad(const real h[2], real p[8], real ret[16]) {
+    int nq = 4, nr = 0;
+    real buffer[16];
+    real *q = p, *r = ret;
+    for (int dir = 0; dir <= 1; ++dir) {
+        for (int sign = -1; sign <= 1; sign += 2) {
+            real *pq = q, *pr = r;
+            nr = 0;
+            for (int i = nq; i > 0; --i) {
+                if (sign * pq[dir] < h[dir]) {
+                    pr[0] = pq[0]; pr[1] = pq[1];
+                    pr += 2; nr++;
+                    if (nr & 8) { q = r; goto done; }
+                }
+                real *nextq = (i > 1) ? pq + 2 : q;
+                if ((sign * pq[dir] < h[dir]) ^ (sign * nextq[dir] < h[dir])) {
+                    pr[1 - dir] = pq[1 - dir] + (nextq[1 - dir] - pq[1 - dir]) / (nextq[dir] - pq[dir]) * (sign * h[dir] - pq[dir]);
+                    pr[dir] = sign * h[dir];
+                    pr += 2; nr++;
+                    if (nr & 8) { q = r; goto done; }
+                }
+                pq += 2;
+            }
+            q = r;
+            r = (q == ret) ? buffer : ret;
+            nq = nr;
+        }
+    }
+done:
+    if (q != ret) memcpy(ret, q, (size_t)nr * 2 * sizeof(real));
+    return nr;
+}
+
+/* ODE cullPoints as box_box-inl.h cullPoints2: m of the n clipped points,
+ * the deepest (i0) first, then the ones nearest to evenly spaced angles */
+static void cull_points(int n, const real p[], int m, int i0, int iret[]) {
+    real a, cx, cy, q;
+    if (n == 1) { cx = p[0]; cy = p[1]; }
+    else if (n == 2) { cx = 0.5 * (p[0] + p[2]); cy = 0.5 * (p[1] + p[3]); }
+    else {
+        a = 0; cx = 0; cy = 0;
+        for (int i = 0; i < n - 1; ++i) {
+            q = p[i * 2] * p[i * 2 + 3] - p[i * 2 + 2] * p[i * 2 + 1];
+            a += q;
+            cx += q * (p[i * 2] + p[i * 2 + 2]);
+            cy += q * (p[i * 2 + 1] + p[i * 2 + 3]);
+        }
+        q = p[n * 2 - 2] * p[1] - p[0] * p[n * 2 - 1];
+        if (fabs(a + q) > DBL_EPSILON) a = 1 / (3 * (a + q));
+        else a = 1e18f;
+        cx = a * (cx + q * (p[n * 2 - 2] + p[0]));
+        cy = a * (cy + q * (p[n * 2 - 1] + p[1]));
+    }
+    real A[8];
+    for (int i = 0; i < n; ++i) A[i] = atan2(p[i * 2 + 1] - cy, p[i * 2] - cx);
+    int avail[8];
+    for (int i = 0; i < n; ++i) avail[i] = 1;
+    avail[i0] = 0;
+    iret[0] = i0;
+    int k = 1;
+    const real pi = 3.14159265358979323846;
+    for (int j = 1; j < m; ++j) {
+        a = j * (2 * pi / m) + A[i0];
+        if (a > pi) a -= 2 * pi;
+        real maxdiff = 1e9, diff;
+        iret[k] = i0;
+        for (int i = 0; i < n; ++i) {
+            if (avail[i]) {
+                diff = fabs(A[i] - a);
+                if (diff > pi) diff = 2 * pi - diff;
+                if (diff < maxdiff) { maxdiff = diff; iret[k] = i; }
+            }
+        }
+        avail[iret[k]] = 0;
+        k++;
+    }
+}
+
+/* keep the first contact with the largest penetration_depth (partial_sort
+ * for one free slot) */
+static void keep_contact(int *n, real pd, const real *nrm, const real *pos, real *depth, real *normal, real *posout) {
+    if (*n == 0 || pd > *depth) {
+        *depth = pd;
+        for (int i = 0; i < 3; ++i) { normal[i] = nrm[i]; posout[i] = pos[i]; }
+    }
+    (*n)++;
+}
+
+/* detail::boxBox2 with contacts (maxc = 4), as boxBoxIntersect calls it */
+static int box_box_contact(const real *side1, const real *T1, const real *side2, const real *T2, real *depth_out,
+                           real *normal_out, real *pos_out, int *n_contacts) {
+#define R1_(i, j) T1[3 * (i) + (j)]
+#define R2_(i, j) T2[3 * (i) + (j)]
+    *n_contacts = 0;
+    const real t1[3] = {T1[9], T1[10], T1[11]}, t2[3] = {T2[9], T2[10], T2[11]};
+    const real p[3] = {t2[0] - t1[0], t2[1] - t1[1], t2[2] - t1[2]};
+    real pp[3], A[3], B[3], R[3][3], Q[3][3];
+    for (int i = 0; i < 3; ++i) pp[i] = (R1_(0, i) * p[0] + R1_(1, i) * p[1]) + R1_(2, i) * p[2];
+    for (int i = 0; i < 3; ++i) { A[i] = side1[i] * 0.5; B[i] = side2[i] * 0.5; }
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) {
+            R[i][j] = (R1_(0, i) * R2_(0, j) + R1_(1, i) * R2_(1, j)) + R1_(2, i) * R2_(2, j);
+            Q[i][j] = fabs(R[i][j]);
+        }
+    real s = -DBL_MAX, s2, tmp, normalC[3] = {0, 0, 0};
+    int code = 0, best_col = -1, normal_r2 = 0, invert = 0;
+    for (int i = 0; i < 3; ++i) {
+        tmp = pp[i];
+        s2 = fabs(tmp) - (((Q[i][0] * B[0] + Q[i][1] * B[1]) + Q[i][2] * B[2]) + A[i]);
+        if (s2 > 0) return 0;
+        if (s2 > s) { s = s2; best_col = i; normal_r2 = 0; invert = tmp < 0; code = 1 + i; }
+    }
+    for (int j = 0; j < 3; ++j) {
+        tmp = (R2_(0, j) * p[0] + R2_(1, j) * p[1]) + R2_(2, j) * p[2];
+        s2 = fabs(tmp) - (((Q[0][j] * A[0] + Q[1][j] * A[1]) + Q[2][j] * A[2]) + B[j]);
+        if (s2 > 0) return 0;
+        if (s2 > s) { s = s2; best_col = j; normal_r2 = 1; invert = tmp < 0; code = 4 + j; }
+    }
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) Q[i][j] += 1.0e-6;
+    const real eps = DBL_EPSILON, fudge = 1.05;
+    real n[3], l;
+#define EDGE(TMP, S2, N0, N1, N2, CODE)                                                         \
+    tmp = (TMP);                                                                                \
+    s2 = fabs(tmp) - (S2);                                                                      \
+    if (s2 > eps) return 0;                                                                     \
+    n[0] = (N0); n[1] = (N1); n[2] = (N2);                                                      \
+    l = sqrt((n[0] * n[0] + n[1] * n[1]) + n[2] * n[2]);                                        \
+    if (l > eps) {                                                                              \
+        s2 /= l;                                                                                \
+        if (s2 * fudge > s) {                                                                   \
+            s = s2; best_col = -1; invert = tmp < 0; code = (CODE);                            \
+            normalC[0] = n[0] / l; normalC[1] = n[1] / l; normalC[2] = n[2] / l;               \
+        }                                                                                       \
+    }
+    EDGE(pp[2] * R[1][0] - pp[1] * R[2][0], ((A[1] * Q[2][0] + A[2] * Q[1][0]) + B[1] * Q[0][2]) + B[2] * Q[0][1],
+         0, -R[2][0], R[1][0], 7)
+    EDGE(pp[2] * R[1][1] - pp[1] * R[2][1], ((A[1] * Q[2][1] + A[2] * Q[1][1]) + B[0] * Q[0][2]) + B[2] * Q[0][0],
+         0, -R[2][1], R[1][1], 8)
+    EDGE(pp[2] * R[1][2] - pp[1] * R[2][2], ((A[1] * Q[2][2] + A[2] * Q[1][2]) + B[0] * Q[0][1]) + B[1] * Q[0][0],
+         0, -R[2][2], R[1][2], 9)
+    EDGE(pp[0] * R[2][0] - pp[2] * R[0][0], ((A[0] * Q[2][0] + A[2] * Q[0][0]) + B[1] * Q[1][2]) + B[2] * Q[1][1],
+         R[2][0], 0, -R[0][0], 10)
+    EDGE(pp[0] * R[2][1] - pp[2] * R[0][1], ((A[0] * Q[2][1] + A[2] * Q[0][1]) + B[0] * Q[1][2]) + B[2] * Q[1][0],
+         R[2][1], 0, -R[0][1], 11)
+    EDGE(pp[0] * R[2][2] - pp[2] * R[0][2], ((A[0] * Q[2][2] + A[2] * Q[0][2]) + B[0] * Q[1][1]) + B[1] * Q[1][0],
+         R[2][2], 0, -R[0][2], 12)
+    EDGE(pp[1] * R[0][0] - pp[0] * R[1][0], ((A[0] * Q[1][0] + A[1] * Q[0][0]) + B[1] * Q[2][2]) + B[2] * Q[2][1],
+         -R[1][0], R[0][0], 0, 13)
+    EDGE(pp[1] * R[0][1] - pp[0] * R[1][1], ((A[0] * Q[1][1] + A[1] * Q[0][1]) + B[0] * Q[2][2]) + B[2] * Q[2][0],
+         -R[1][1], R[0][1], 0, 14)
+    EDGE(pp[1] * R[0][2] - pp[0] * R[1][2], ((A[0] * Q[1][2] + A[1] * Q[0][2]) + B[0] * Q[2][1]) + B[1] * Q[2][0],
+         -R[1][2], R[0][2], 0, 15)
+#undef EDGE
+    if (!code) return 0;
+    /* the normal in world coordinates, from box 1 towards box 2 */
+    real normal[3];
+    if (best_col != -1) {
+        const real *T = normal_r2 ? T2 : T1;
+        for (int i = 0; i < 3; ++i) normal[i] = T[3 * i + best_col];
+    } else {
+        for (int i = 0; i < 3; ++i) normal[i] = (R1_(i, 0) * normalC[0] + R1_(i, 1) * normalC[1]) + R1_(i, 2) * normalC[2];
+    }
+    if (invert)
+        for (int i = 0; i < 3; ++i) normal[i] = -normal[i];
+    const real depth = -s;
+    if (code > 6) { /* edge-edge: the closest point of box 2's edge */
+        real pa[3] = {t1[0], t1[1], t1[2]}, pb[3] = {t2[0], t2[1], t2[2]}, sign;
+        for (int j = 0; j < 3; ++j) {
+            sign = (((R1_(0, j) * normal[0] + R1_(1, j) * normal[1]) + R1_(2, j) * normal[2]) > 0) ? 1 : -1;
+            for (int i = 0; i < 3; ++i) pa[i] += R1_(i, j) * (A[j] * sign);
+        }
+        for (int j = 0; j < 3; ++j) {
+            sign = (((R2_(0, j) * normal[0] + R2_(1, j) * normal[1]) + R2_(2, j) * normal[2]) > 0) ? -1 : 1;
+            for (int i = 0; i < 3; ++i) pb[i] += R2_(i, j) * (B[j] * sign);
+        }
+        real alpha, beta;
+        const int ca = (code - 7) / 3, cb = (code - 7) % 3;
+        const real ua[3] = {R1_(0, ca), R1_(1, ca), R1_(2, ca)}, ub[3] = {R2_(0, cb), R2_(1, cb), R2_(2, cb)};
+        line_closest_approach(pa, ua, pb, ub, &alpha, &beta);
+        for (int i = 0; i < 3; ++i) pb[i] += ub[i] * beta;
+        keep_contact(n_contacts, -depth, normal, pb, depth_out, normal_out, pos_out);
+        return 1;
+    }
+    /* face-something: face 'a' is the reference face, 'b' the incident box */
+    const real *Ta = code <= 3 ? T1 : T2, *Tb = code <= 3 ? T2 : T1;
+    const real *pa = code <= 3 ? t1 : t2, *pb = code <= 3 ? t2 : t1;
+    const real *Sa = code <= 3 ? A : B, *Sb = code <= 3 ? B : A;
+#define RA(i, j) Ta[3 * (i) + (j)]
+#define RB(i, j) Tb[3 * (i) + (j)]
+    real normal2[3], nr[3], anr[3];
+    for (int i = 0; i < 3; ++i) normal2[i] = code <= 3 ? normal[i] : -normal[i];
+    for (int j = 0; j < 3; ++j) {
+        nr[j] = (RB(0, j) * normal2[0] + RB(1, j) * normal2[1]) + RB(2, j) * normal2[2];
+        anr[j] = fabs(nr[j]);
+    }
+    int lanr, a1, a2;
+    if (anr[1] > anr[0]) {
+        if (anr[1] > anr[2]) { a1 = 0; lanr = 1; a2 = 2; }
+        else { a1 = 0; a2 = 1; lanr = 2; }
+    } else {
+        if (anr[0] > anr[2]) { lanr = 0; a1 = 1; a2 = 2; }
+        else { a1 = 0; a2 = 1; lanr = 2; }
+    }
+    real center[3];
+    for (int i = 0; i < 3; ++i)
+        center[i] = nr[lanr] < 0 ? (pb[i] - pa[i]) + RB(i, lanr) * Sb[lanr] : (pb[i] - pa[i]) - RB(i, lanr) * Sb[lanr];
+    const int codeN = code <= 3 ? code - 1 : code - 4;
+    int code1, code2;
+    if (codeN == 0) { code1 = 1; code2 = 2; }
+    else if (codeN == 1) { code1 = 0; code2 = 2; }
+    else { code1 = 0; code2 = 1; }
+    real quad[8];
+    const real c1 = (RA(0, code1) * center[0] + RA(1, code1) * center[1]) + RA(2, code1) * center[2];
+    const real c2 = (RA(0, code2) * center[0] + RA(1, code2) * center[1]) + RA(2, code2) * center[2];
+    real m11 = (RB(0, a1) * RA(0, code1) + RB(1, a1) * RA(1, code1)) + RB(2, a1) * RA(2, code1);
+    real m12 = (RB(0, a2) * RA(0, code1) + RB(1, a2) * RA(1, code1)) + RB(2, a2) * RA(2, code1);
+    real m21 = (RB(0, a1) * RA(0, code2) + RB(1, a1) * RA(1, code2)) + RB(2, a1) * RA(2, code2);
+    real m22 = (RB(0, a2) * RA(0, code2) + RB(1, a2) * RA(1, code2)) + RB(2, a2) * RA(2, code2);
+    {
+        const real k1 = m11 * Sb[a1], k2 = m21 * Sb[a1], k3 = m12 * Sb[a2], k4 = m22 * Sb[a2];
+        quad[0] = c1 - k1 - k3; quad[1] = c2 - k2 - k4;
+        quad[2] = c1 - k1 + k3; quad[3] = c2 - k2 + k4;
+        quad[4] = c1 + k1 + k3; quad[5] = c2 + k2 + k4;
+        quad[6] = c1 + k1 - k3; quad[7] = c2 + k2 - k4;
+    }
+    const real rect[2] = {Sa[code1], Sa[code2]};
+    real ret[16];
+    const int n_intersect = intersect_rect_quad(rect, quad, ret);
+    if (n_intersect < 1) return 1; /* collision without a contact point */
+    real points[8][3], dep[8];
+    const real det1 = 1.f / (m11 * m22 - m12 * m21);
+    m11 *= det1; m12 *= det1; m21 *= det1; m22 *= det1;
+    int cnum = 0;
+    for (int j = 0; j < n_intersect; ++j) {
+        const real k1 = m22 * (ret[j * 2] - c1) - m12 * (ret[j * 2 + 1] - c2);
+        const real k2 = -m21 * (ret[j * 2] - c1) + m11 * (ret[j * 2 + 1] - c2);
+        for (int i = 0; i < 3; ++i) points[cnum][i] = (center[i] + RB(i, a1) * k1) + RB(i, a2) * k2;
+        dep[cnum] = Sa[codeN] - ((normal2[0] * points[cnum][0] + normal2[1] * points[cnum][1]) + normal2[2] * points[cnum][2]);
+        if (dep[cnum] >= 0) {
+            ret[cnum * 2] = ret[j * 2];
+            ret[cnum * 2 + 1] = ret[j * 2 + 1];
+            cnum++;
+        }
+    }
+    if (cnum < 1) return 1;
+    int maxc = 4;
+    if (maxc > cnum) maxc = cnum;
+    int iret[8];
+    if (cnum <= maxc) {
+        for (int j = 0; j < cnum; ++j) iret[j] = j;
+    } else {
+        int i1 = 0;
+        real maxdepth = dep[0];
+        for (int i = 1; i < cnum; ++i)
+            if (dep[i] > maxdepth) { maxdepth = dep[i]; i1 = i; }
+        cull_points(cnum, ret, maxc, i1, iret);
+        cnum = maxc;
+    }
+    for (int j = 0; j < cnum; ++j) {
+        const int k = iret[j];
+        real w[3];
+        for (int i = 0; i < 3; ++i) w[i] = code < 4 ? points[k][i] + pa[i] : (points[k][i] + pa[i]) - normal[i] * dep[k];
+        keep_contact(n_contacts, -dep[k], normal, w, depth_out, normal_out, pos_out);
+    }
+#undef RA
+#undef RB
+#undef R1_
+#undef R2_
+    return 1;
+}
+
+/* detail::sphereSphereIntersect with its contact */
+static int sphere_sphere_contact(real r1, const real *T1, real r2, const real *T2, real *depth, real *normal,
+                                 real *pos) {
+    const real d[3] = {T2[9] - T1[9], T2[10] - T1[10], T2[11] - T1[11]};
+    const real len = sqrt((d[0] * d[0] + d[1] * d[1]) + d[2] * d[2]);
+    if (len > r1 + r2) return 0;
+    for (int i = 0; i < 3; ++i) {
+        normal[i] = len > 0 ? d[i] / len : d[i];
+        pos[i] = T1[9 + i] + d[i] * r1 / (r1 + r2);
+    }
+    *depth = r1 + r2 - len;
+    return 1;
+}
+
+/* detail::sphereBoxIntersect with its contact: normal from the sphere into
+ * the box; centre inside the box -> the nearest face (first minimum over
+ * x, y, z), depth = its distance + r; contact half way between the sphere's
+ * deepest point and the box surface, p_BC + n (r - depth / 2) */
+static int sphere_box_contact(real r, const real *TS, const real *side, const real *TB, real *depth, real *normal,
+                              real *pos) {
+    real c[3], nq[3];
+    for (int i = 0; i < 3; ++i) {
+        const real inv_t = -((TB[i] * TB[9] + TB[3 + i] * TB[10]) + TB[6 + i] * TB[11]);
+        c[i] = ((TB[i] * TS[9] + TB[3 + i] * TS[10]) + TB[6 + i] * TS[11]) + inv_t;
+    }
+    int clamped = 0;
+    for (int i = 0; i < 3; ++i) {
+        const real h = side[i] / 2;
+        nq[i] = c[i];
+        if (c[i] < -h) { clamped = 1; nq[i] = -h; }
+        if (c[i] > h) { clamped = 1; nq[i] = h; }
+    }
+    const real d[3] = {c[0] - nq[0], c[1] - nq[1], c[2] - nq[2]};
+    const real dd = (d[0] * d[0] + d[1] * d[1]) + d[2] * d[2];
+    if (clamped && dd > r * r) return 0;
+    real n[3] = {0, 0, 0}, dep;
+    if (clamped) {
+        const real dist = sqrt(dd);
+        for (int i = 0; i < 3; ++i) n[i] = -d[i] / dist;
+        dep = r - dist;
+    } else {
+        real min_d = INFINITY;
+        int ax = 0;
+        for (int i = 0; i < 3; ++i) {
+            const real di = side[i] / 2 - fabs(c[i]);
+            if (di < min_d) { min_d = di; ax = i; }
+        }
+        n[ax] = c[ax] >= 0 ? -1 : 1;
+        dep = min_d + r;
+    }
+    real pc[3];
+    for (int i = 0; i < 3; ++i) pc[i] = c[i] + n[i] * (r - dep / 2);
+    for (int i = 0; i < 3; ++i) {
+        normal[i] = (TB[3 * i] * n[0] + TB[3 * i + 1] * n[1]) + TB[3 * i + 2] * n[2];
+        pos[i] = ((TB[3 * i] * pc[0] + TB[3 * i + 1] * pc[1]) + TB[3 * i + 2] * pc[2]) + TB[9 + i];
+    }
+    *depth = dep;
+    return 1;
+}
+
+/* the closed-form contact of a pair; -1 when the pair is not one of
+ * box-box, sphere-sphere, sphere-box, box-sphere */
+static int closed_form_contact(const orc_world *w, int ga, const real *Ta, int gb, const real *Tb, real *depth,
+                               real *normal, real *pos) {
+    const int ta = w->geom_type[ga], tb = w->geom_type[gb];
+    const real *pa = w->geom_param + 4 * ga, *pb = w->geom_param + 4 * gb;
+    *depth = 0;
+    for (int i = 0; i < 3; ++i) normal[i] = pos[i] = 0;
+    int nc = 0;
+    if (ta == GEOM_BOX && tb == GEOM_BOX) return box_box_contact(pa, Ta, pb, Tb, depth, normal, pos, &nc);
+    if (ta == GEOM_SPHERE && tb == GEOM_SPHERE) return sphere_sphere_contact(pa[0], Ta, pb[0], Tb, depth, normal, pos);
+    if (ta == GEOM_SPHERE && tb == GEOM_BOX) return sphere_box_contact(pa[0], Ta, pb, Tb, depth, normal, pos);
+    if (ta == GEOM_BOX && tb == GEOM_SPHERE) {
+        const int h = sphere_box_contact(pb[0], Tb, pa, Ta, depth, normal, pos);
+        for (int i = 0; i < 3; ++i) normal[i] = -normal[i]; /* flipNormal */
+        return h;
+    }
+    return -1;
+}
+
 /* ------------------------------------------------ GJK distance
  * PlanningWorld::distance* (src/planning_world.cpp:493-720) calls
  * fcl::distance -> GJKSolver_libccd::shapeDistance -> libccd GJK distance
@@ -1765,6 +2143,8 @@ int orc_fk_batch(const orc_world *w, const double *q, long n, double *link_pose7
 /* Single-pair entry (fcl.collide(o1, o2) on two posed shapes). */
 int orc_contact_pair(const orc_world *w, int ga, const double *Ta, int gb, const double *Tb, double *depth,
                      double *normal, double *pos) {
+    const int cf = closed_form_contact(w, ga, Ta, gb, Tb, depth, normal, pos);
+    if (cf >= 0) return cf;
     gjk_obj a, b;
     make_obj(w, ga, Ta, &a, NULL);
     make_obj(w, gb, Tb, &b, NULL);
@@ -1792,14 +2172,16 @@ int orc_contact_batch(const orc_world *w, const double *q, long n, uint8_t *hit,
             if (w->p_allowed[p]) continue;
             int ks[2] = {w->pa_kind[p], w->pb_kind[p]}, is[2] = {w->pa_idx[p], w->pb_idx[p]};
             gjk_obj o[2];
+            const real *Ts[2];
+            int gs[2];
             for (int s = 0; s < 2; ++s) {
-                const real *T;
-                int gg;
-                if (ks[s] == KIND_ROBOT) { T = obj_T + 12 * is[s]; gg = w->obj_geom[is[s]]; }
-                else if (ks[s] == KIND_ATTACHED) { T = att_T + 12 * is[s]; gg = w->att_geom[is[s]]; }
-                else { T = w->scene_tf + 12 * is[s]; gg = w->scene_geom[is[s]]; }
-                make_obj(w, gg, T, &o[s], NULL);
+                if (ks[s] == KIND_ROBOT) { Ts[s] = obj_T + 12 * is[s]; gs[s] = w->obj_geom[is[s]]; }
+                else if (ks[s] == KIND_ATTACHED) { Ts[s] = att_T + 12 * is[s]; gs[s] = w->att_geom[is[s]]; }
+                else { Ts[s] = w->scene_tf + 12 * is[s]; gs[s] = w->scene_geom[is[s]]; }
             }
+            const int cf = closed_form_contact(w, gs[0], Ts[0], gs[1], Ts[1], depth + k, normal + 3 * k, pos + 3 * k);
+            if (cf >= 0) { hit[k] = (uint8_t)cf; continue; }
+            for (int s = 0; s < 2; ++s) make_obj(w, gs[s], Ts[s], &o[s], NULL);
             hit[k] = (uint8_t)mpr_penetration(&o[0], &o[1], 1e-6, depth + k, normal + 3 * k, pos + 3 * k);
         }
     }

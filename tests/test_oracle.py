@@ -315,3 +315,107 @@ def test_sphere_capsule_cylinder_closed_forms_match_geometry():
             assert _pair(ow, gi[id(g)], To, gi[id(ball)], Ts) == want
             checked[name][want] += 1
     assert min(min(v) for v in checked.values()) > 100  # both outcomes exercised
+
+
+# ------------------------------------------- closed-form contacts (enable_contact)
+def _contact(w, ga, Ta, gb, Tb):
+    import ctypes
+    import oracle
+    P = ctypes.POINTER(ctypes.c_double)
+    depth = ctypes.c_double()
+    nrm, pos = np.zeros(3), np.zeros(3)
+    r = oracle.lib().orc_contact_pair(ctypes.byref(w._w), ga, Ta.ctypes.data_as(P), gb, Tb.ctypes.data_as(P),
+                                      ctypes.byref(depth), nrm.ctypes.data_as(P), pos.ctypes.data_as(P))
+    return r, depth.value, nrm, pos
+
+
+def test_sphere_contacts_known_answers():
+    """FCL 0.7.0 sphereSphereIntersect / sphereBoxIntersect contacts (plain
+    geometry): normal from object 1 into object 2, depth, and the contact
+    point (sphere-sphere: on the centre line at r1/(r1+r2); sphere-box: half
+    way between the sphere's deepest point and the box surface)."""
+    from oracle import model as M
+    w, (s5, s3, box) = _pair_world([M.SphereGeom(0.5), M.SphereGeom(0.3), M.BoxGeom((1.0, 1.0, 1.0))])
+    r, d, n, p = _contact(w, s5, _T(), s3, _T(p=(0.7, 0.0, 0.0)))
+    assert r == 1 and abs(d - 0.1) < 1e-12
+    np.testing.assert_allclose(n, [1, 0, 0], atol=1e-15)
+    np.testing.assert_allclose(p, [0.4375, 0, 0], atol=1e-15)
+    assert _contact(w, s5, _T(), s3, _T(p=(0.81, 0.0, 0.0)))[0] == 0
+    # sphere centre outside the box: nearest point (0.5, 0, 0), distance 0.4
+    r, d, n, p = _contact(w, s5, _T(p=(0.9, 0.0, 0.0)), box, _T())
+    assert r == 1 and abs(d - 0.1) < 1e-12
+    np.testing.assert_allclose(n, [-1, 0, 0], atol=1e-15)
+    np.testing.assert_allclose(p, [0.45, 0, 0], atol=1e-12)
+    # box first: flipNormal
+    r, d2, n2, p2 = _contact(w, box, _T(), s5, _T(p=(0.9, 0.0, 0.0)))
+    assert r == 1 and d2 == d
+    np.testing.assert_array_equal(n2, -n)
+    np.testing.assert_array_equal(p2, p)
+    # centre inside the box: the nearest face (+x, 0.2 away), depth 0.2 + r
+    r, d, n, p = _contact(w, s3, _T(p=(0.3, 0.1, 0.0)), box, _T())
+    assert r == 1 and abs(d - 0.5) < 1e-12
+    np.testing.assert_allclose(n, [-1, 0, 0], atol=1e-15)
+    np.testing.assert_allclose(p, [0.3 - (0.3 - 0.25), 0.1, 0.0], atol=1e-12)
+    # rotated box: the normal and point come back to the world frame
+    q = (np.cos(0.3), 0.0, 0.0, np.sin(0.3))
+    T = _T(q=q, p=(0.1, 0.2, 0.3))
+    R = T[:9].reshape(3, 3)
+    Ts = _T(p=tuple(R @ np.array([0.9, 0.0, 0.0]) + T[9:]))
+    r, d, n, p = _contact(w, s5, Ts, box, T)
+    assert r == 1 and abs(d - 0.1) < 1e-12
+    np.testing.assert_allclose(n, R @ [-1, 0, 0], atol=1e-12)
+    np.testing.assert_allclose(p, R @ [0.45, 0, 0] + T[9:], atol=1e-12)
+
+
+def test_box_box_contact_known_answers():
+    """FCL 0.7.0 boxBox2 with contacts (ODE dBoxBox): face-face contact points
+    on the incident face, normal from box 1 to box 2, and FCL's stored
+    penetration_depth = -(depth of the point) (the sign boxBox2 emits; with
+    one requested contact ShapeShapeCollide keeps the largest value)."""
+    from oracle import model as M
+    w, (b1, b2) = _pair_world([M.BoxGeom((1.0, 1.0, 1.0)), M.BoxGeom((1.0, 0.5, 0.5))])
+    r, d, n, p = _contact(w, b1, _T(), b1, _T(p=(0.9, 0.02, 0.01)))
+    assert r == 1 and abs(d + 0.1) < 1e-12
+    np.testing.assert_allclose(n, [1, 0, 0], atol=1e-15)
+    assert abs(p[0] - 0.4) < 1e-12 and abs(p[1]) <= 0.5 + 1e-12 and abs(p[2]) <= 0.5 + 1e-12
+    # box 2 below box 1 along z: normal -z, reference face is box 1's
+    r, d, n, p = _contact(w, b1, _T(), b2, _T(p=(0.1, 0.0, -0.7)))
+    assert r == 1 and abs(d + 0.05) < 1e-12
+    np.testing.assert_allclose(n, [0, 0, -1], atol=1e-15)
+    assert abs(p[2] + 0.45) < 1e-12
+    # tilted incident box: the shallowest of the clipped points is kept
+    q = (np.cos(0.1), np.sin(0.1), 0.0, 0.0)
+    r, d, n, p = _contact(w, b1, _T(), b2, _T(q=q, p=(0.0, 0.0, 0.7)))
+    assert r == 1 and n[2] > 0.99 and -0.2 < d < 0.0
+    # edge-edge: box 2 turned 45 degrees about z and x, just touching an edge
+    s = np.sqrt(0.5)
+    q = (np.cos(np.pi / 8) * np.cos(np.pi / 8), np.sin(np.pi / 8) * np.cos(np.pi / 8),
+         np.cos(np.pi / 8) * np.sin(np.pi / 8), -np.sin(np.pi / 8) * np.sin(np.pi / 8))
+    assert _contact(w, b1, _T(), b1, _T(q=q, p=(1.4, 0.0, 0.0)))[0] == 0
+    r, d, n, p = _contact(w, b1, _T(), b1, _T(q=q, p=(1.05, 0.3, 0.2)))
+    assert r == 1 and d <= 0.0 and n[0] > 0.0 and s > 0
+    # separated
+    assert _contact(w, b1, _T(), b1, _T(p=(1.01, 0.0, 0.0)))[0] == 0
+
+
+def test_closed_form_contact_batch_consistent_with_collide():
+    """collision_avoidance.py:87-90's attached box in the cfg3 box scene:
+    the oracle's contact pass reports exactly the pairs collide() reports
+    (box-box through boxBox2's contact path, box-convex through MPR), with
+    unit normals and boxBox2's non-positive stored depth."""
+    base = Wd.oracle_world(3)
+    pose = [0.0, 0.0, 0.14, 1.0, 0.0, 0.0, 0.0]
+    T = (M.quat_to_mat(*pose[3:]), pose[:3])
+    o2 = oracle.OracleWorld(base.art, scene=base.scene, attached=[("held", 8, M.BoxGeom((0.04, 0.04, 0.12)), T)],
+                            allowed=[("panda_hand", "held"), ("panda_link0", "table")])
+    q = Wd.sample_q(base.art, 3000, 18)
+    hit, depth, normal, pos = o2.contact_batch(q)
+    _, masks = o2.collide_batch(q)
+    P = len(o2.pairs)
+    bits = np.stack([(masks[:, p >> 5] >> (p & 31)) & 1 for p in range(P)], 1)
+    np.testing.assert_array_equal(hit, bits)
+    bb = [k for k, (a, b) in enumerate(o2.pair_names()) if a == "held"]  # held x scene boxes: boxBox2
+    h = hit[:, bb].astype(bool)
+    assert h.sum() > 0
+    np.testing.assert_allclose(np.linalg.norm(normal[:, bb][h], axis=1), 1.0, atol=1e-12)
+    assert (depth[:, bb][h] <= 0).all()
