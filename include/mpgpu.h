@@ -256,8 +256,13 @@ int mpg_distance_batch(mpg_world *world, const double *q, int64_t n, int32_t n_s
  * ccdMPRPenetration, the one contact FCL reports for an MPR pair):
  *   depth[i*P + p], normal[(i*P + p)*3 ..] (from object 1 to object 2),
  *   pos[(i*P + p)*3 ..]; zeros for pairs not reported.  P = n_pairs.
- * Worlds whose non-allowed pairs include FCL closed forms (box-box,
- * sphere-sphere, sphere-box) return MPG_E_UNSUPPORTED.
+ * FCL closed-form pairs report the contact FCL 0.7's specialisation emits
+ * (box-box: boxBox2's clipped face points / edge-edge closest point, with its
+ * stored penetration_depth = -(point depth) <= 0; sphere-sphere; sphere-box
+ * and box-sphere, normal flipped for the latter), reduced to the one contact
+ * ShapeShapeCollide keeps for num_max_contacts = 1.  Worlds whose non-allowed
+ * pairs include sphere-capsule / sphere-cylinder closed forms, octree or BVH
+ * mesh pairs return MPG_E_UNSUPPORTED.
  */
 #define MPG_INPUT_Q 0
 #define MPG_INPUT_LINK_POSES 1

@@ -2705,6 +2705,425 @@ __device__ bool mpr_penetration(const DevWorld& w, cptr<double> HV, const GObj& 
   return hit;
 }
 
+// ---------------------------------------------------------------------------
+// FCL closed-form contacts (CollisionRequest(enable_contact=True) on box-box,
+// sphere-sphere, sphere-box, box-sphere pairs): the contacts FCL 0.7.0's
+// GJKSolver_libccd::shapeIntersect specialisations emit, reduced to the one
+// ShapeShapeCollide keeps for num_max_contacts = 1 (partial_sort by
+// descending penetration_depth, first of equals).  Same operation order as
+// oracle/collide_oracle.c box_box_contact & co (parity unpinned: FCL's
+// contact code is not under /root/reference).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void cf_keep(int& n, double pd, const double* nrm, const double* p, double& depth, V3& nd,
+                                        V3& ps) {
+  if (n == 0 || pd > depth) {
+    depth = pd;
+    nd = v3(nrm[0], nrm[1], nrm[2]);
+    ps = v3(p[0], p[1], p[2]);
+  }
+  ++n;
+}
+
+// ODE intersectRectQuad (box_box-inl.h intersectRectQuad2)
+__device__ int cf_rect_quad(const double h[2], double p[8], double ret[16]) {
+  int nq = 4, nr = 0;
+  double buffer[16];
+  double* q = p;
+  double* r = ret;
+  for (int dir = 0; dir <= 1; ++dir) {
+    for (int sign = -1; sign <= 1; sign += 2) {
+      double* pq = q;
+      double* pr = r;
+      nr = 0;
+      for (int i = nq; i > 0; --i) {
+        if (sign * pq[dir] < h[dir]) {
+          pr[0] = pq[0];
+          pr[1] = pq[1];
+          pr += 2;
+          nr++;
+          if (nr & 8) {
+            q = r;
+            goto done;
+          }
+        }
+        double* nextq = (i > 1) ? pq + 2 : q;
+        if ((sign * pq[dir] < h[dir]) ^ (sign * nextq[dir] < h[dir])) {
+          pr[1 - dir] = pq[1 - dir] + (nextq[1 - dir] - pq[1 - dir]) / (nextq[dir] - pq[dir]) * (sign * h[dir] - pq[dir]);
+          pr[dir] = sign * h[dir];
+          pr += 2;
+          nr++;
+          if (nr & 8) {
+            q = r;
+            goto done;
+          }
+        }
+        pq += 2;
+      }
+      q = r;
+      r = (q == ret) ? buffer : ret;
+      nq = nr;
+    }
+  }
+done:
+  if (q != ret)
+    for (int i = 0; i < 2 * nr; ++i) ret[i] = q[i];
+  return nr;
+}
+
+// ODE cullPoints (box_box-inl.h cullPoints2)
+__device__ void cf_cull_points(int n, const double* p, int m, int i0, int* iret) {
+  double a, cx, cy, q;
+  if (n == 1) {
+    cx = p[0];
+    cy = p[1];
+  } else if (n == 2) {
+    cx = 0.5 * (p[0] + p[2]);
+    cy = 0.5 * (p[1] + p[3]);
+  } else {
+    a = 0;
+    cx = 0;
+    cy = 0;
+    for (int i = 0; i < n - 1; ++i) {
+      q = p[i * 2] * p[i * 2 + 3] - p[i * 2 + 2] * p[i * 2 + 1];
+      a += q;
+      cx += q * (p[i * 2] + p[i * 2 + 2]);
+      cy += q * (p[i * 2 + 1] + p[i * 2 + 3]);
+    }
+    q = p[n * 2 - 2] * p[1] - p[0] * p[n * 2 - 1];
+    if (std::fabs(a + q) > DBL_EPSILON) a = 1 / (3 * (a + q));
+    else a = (double)1e18f;
+    cx = a * (cx + q * (p[n * 2 - 2] + p[0]));
+    cy = a * (cy + q * (p[n * 2 - 1] + p[1]));
+  }
+  double A[8];
+  int avail[8];
+  for (int i = 0; i < n; ++i) {
+    A[i] = std::atan2(p[i * 2 + 1] - cy, p[i * 2] - cx);
+    avail[i] = 1;
+  }
+  avail[i0] = 0;
+  iret[0] = i0;
+  const double pi = 3.14159265358979323846;
+  for (int j = 1; j < m; ++j) {
+    a = j * (2 * pi / m) + A[i0];
+    if (a > pi) a -= 2 * pi;
+    double maxdiff = 1e9, diff;
+    iret[j] = i0;
+    for (int i = 0; i < n; ++i) {
+      if (avail[i]) {
+        diff = std::fabs(A[i] - a);
+        if (diff > pi) diff = 2 * pi - diff;
+        if (diff < maxdiff) {
+          maxdiff = diff;
+          iret[j] = i;
+        }
+      }
+    }
+    avail[iret[j]] = 0;
+  }
+}
+
+// detail::boxBox2 with contacts (maxc 4) -> the kept contact
+__device__ bool box_box_contact(const double* side1, const SE3& T1, const double* side2, const SE3& T2, double& dout,
+                                V3& nout, V3& pout) {
+#define R1_(i, j) T1.R[3 * (i) + (j)]
+#define R2_(i, j) T2.R[3 * (i) + (j)]
+  int nc = 0;
+  const double p[3] = {T2.p[0] - T1.p[0], T2.p[1] - T1.p[1], T2.p[2] - T1.p[2]};
+  double pp[3], A[3], B[3], R[3][3], Q[3][3];
+  for (int i = 0; i < 3; ++i) pp[i] = (R1_(0, i) * p[0] + R1_(1, i) * p[1]) + R1_(2, i) * p[2];
+  for (int i = 0; i < 3; ++i) {
+    A[i] = side1[i] * 0.5;
+    B[i] = side2[i] * 0.5;
+  }
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) {
+      R[i][j] = (R1_(0, i) * R2_(0, j) + R1_(1, i) * R2_(1, j)) + R1_(2, i) * R2_(2, j);
+      Q[i][j] = std::fabs(R[i][j]);
+    }
+  double s = -DBL_MAX, s2, tmp, normalC[3] = {0, 0, 0};
+  int code = 0, best_col = -1, normal_r2 = 0, invert = 0;
+  for (int i = 0; i < 3; ++i) {
+    tmp = pp[i];
+    s2 = std::fabs(tmp) - (((Q[i][0] * B[0] + Q[i][1] * B[1]) + Q[i][2] * B[2]) + A[i]);
+    if (s2 > 0) return false;
+    if (s2 > s) {
+      s = s2;
+      best_col = i;
+      normal_r2 = 0;
+      invert = tmp < 0;
+      code = 1 + i;
+    }
+  }
+  for (int j = 0; j < 3; ++j) {
+    tmp = (R2_(0, j) * p[0] + R2_(1, j) * p[1]) + R2_(2, j) * p[2];
+    s2 = std::fabs(tmp) - (((Q[0][j] * A[0] + Q[1][j] * A[1]) + Q[2][j] * A[2]) + B[j]);
+    if (s2 > 0) return false;
+    if (s2 > s) {
+      s = s2;
+      best_col = j;
+      normal_r2 = 1;
+      invert = tmp < 0;
+      code = 4 + j;
+    }
+  }
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) Q[i][j] += 1.0e-6;
+  const double eps = DBL_EPSILON, fudge = 1.05;
+  auto edge = [&](double t, double rad, double n0, double n1, double n2, int c) -> bool {
+    tmp = t;
+    s2 = std::fabs(tmp) - rad;
+    if (s2 > eps) return true;
+    const double l = std::sqrt((n0 * n0 + n1 * n1) + n2 * n2);
+    if (l > eps) {
+      s2 /= l;
+      if (s2 * fudge > s) {
+        s = s2;
+        best_col = -1;
+        invert = tmp < 0;
+        code = c;
+        normalC[0] = n0 / l;
+        normalC[1] = n1 / l;
+        normalC[2] = n2 / l;
+      }
+    }
+    return false;
+  };
+  if (edge(pp[2] * R[1][0] - pp[1] * R[2][0], ((A[1] * Q[2][0] + A[2] * Q[1][0]) + B[1] * Q[0][2]) + B[2] * Q[0][1], 0,
+           -R[2][0], R[1][0], 7)) return false;
+  if (edge(pp[2] * R[1][1] - pp[1] * R[2][1], ((A[1] * Q[2][1] + A[2] * Q[1][1]) + B[0] * Q[0][2]) + B[2] * Q[0][0], 0,
+           -R[2][1], R[1][1], 8)) return false;
+  if (edge(pp[2] * R[1][2] - pp[1] * R[2][2], ((A[1] * Q[2][2] + A[2] * Q[1][2]) + B[0] * Q[0][1]) + B[1] * Q[0][0], 0,
+           -R[2][2], R[1][2], 9)) return false;
+  if (edge(pp[0] * R[2][0] - pp[2] * R[0][0], ((A[0] * Q[2][0] + A[2] * Q[0][0]) + B[1] * Q[1][2]) + B[2] * Q[1][1],
+           R[2][0], 0, -R[0][0], 10)) return false;
+  if (edge(pp[0] * R[2][1] - pp[2] * R[0][1], ((A[0] * Q[2][1] + A[2] * Q[0][1]) + B[0] * Q[1][2]) + B[2] * Q[1][0],
+           R[2][1], 0, -R[0][1], 11)) return false;
+  if (edge(pp[0] * R[2][2] - pp[2] * R[0][2], ((A[0] * Q[2][2] + A[2] * Q[0][2]) + B[0] * Q[1][1]) + B[1] * Q[1][0],
+           R[2][2], 0, -R[0][2], 12)) return false;
+  if (edge(pp[1] * R[0][0] - pp[0] * R[1][0], ((A[0] * Q[1][0] + A[1] * Q[0][0]) + B[1] * Q[2][2]) + B[2] * Q[2][1],
+           -R[1][0], R[0][0], 0, 13)) return false;
+  if (edge(pp[1] * R[0][1] - pp[0] * R[1][1], ((A[0] * Q[1][1] + A[1] * Q[0][1]) + B[0] * Q[2][2]) + B[2] * Q[2][0],
+           -R[1][1], R[0][1], 0, 14)) return false;
+  if (edge(pp[1] * R[0][2] - pp[0] * R[1][2], ((A[0] * Q[1][2] + A[1] * Q[0][2]) + B[0] * Q[2][1]) + B[1] * Q[2][0],
+           -R[1][2], R[0][2], 0, 15)) return false;
+  if (!code) return false;
+  double normal[3];
+  if (best_col != -1) {
+    const double* Rm = normal_r2 ? T2.R : T1.R;
+    for (int i = 0; i < 3; ++i) normal[i] = Rm[3 * i + best_col];
+  } else {
+    for (int i = 0; i < 3; ++i) normal[i] = (R1_(i, 0) * normalC[0] + R1_(i, 1) * normalC[1]) + R1_(i, 2) * normalC[2];
+  }
+  if (invert)
+    for (int i = 0; i < 3; ++i) normal[i] = -normal[i];
+  const double depth = -s;
+  if (code > 6) {  // edge-edge: the closest point of box 2's edge
+    double pa[3] = {T1.p[0], T1.p[1], T1.p[2]}, pb[3] = {T2.p[0], T2.p[1], T2.p[2]}, sign;
+    for (int j = 0; j < 3; ++j) {
+      sign = (((R1_(0, j) * normal[0] + R1_(1, j) * normal[1]) + R1_(2, j) * normal[2]) > 0) ? 1 : -1;
+      for (int i = 0; i < 3; ++i) pa[i] += R1_(i, j) * (A[j] * sign);
+    }
+    for (int j = 0; j < 3; ++j) {
+      sign = (((R2_(0, j) * normal[0] + R2_(1, j) * normal[1]) + R2_(2, j) * normal[2]) > 0) ? -1 : 1;
+      for (int i = 0; i < 3; ++i) pb[i] += R2_(i, j) * (B[j] * sign);
+    }
+    const int ca = (code - 7) / 3, cb = (code - 7) % 3;
+    const double ua[3] = {R1_(0, ca), R1_(1, ca), R1_(2, ca)}, ub[3] = {R2_(0, cb), R2_(1, cb), R2_(2, cb)};
+    // lineClosestApproach (ODE dLineClosestApproach); only beta is used
+    const double d0 = pb[0] - pa[0], d1 = pb[1] - pa[1], d2 = pb[2] - pa[2];
+    const double uaub = (ua[0] * ub[0] + ua[1] * ub[1]) + ua[2] * ub[2];
+    const double q1 = (ua[0] * d0 + ua[1] * d1) + ua[2] * d2;
+    const double q2 = -((ub[0] * d0 + ub[1] * d1) + ub[2] * d2);
+    double dd = 1 - uaub * uaub, beta = 0;
+    if (!(dd <= (double)0.0001f)) {
+      dd = 1 / dd;
+      beta = (uaub * q1 + q2) * dd;
+    }
+    for (int i = 0; i < 3; ++i) pb[i] += ub[i] * beta;
+    cf_keep(nc, -depth, normal, pb, dout, nout, pout);
+    return true;
+  }
+  // face-something: reference face on box a, incident box b
+  const double* Ra = code <= 3 ? T1.R : T2.R;
+  const double* Rb = code <= 3 ? T2.R : T1.R;
+  const double* pa = code <= 3 ? T1.p : T2.p;
+  const double* pb = code <= 3 ? T2.p : T1.p;
+  const double* Sa = code <= 3 ? A : B;
+  const double* Sb = code <= 3 ? B : A;
+#define RA(i, j) Ra[3 * (i) + (j)]
+#define RB(i, j) Rb[3 * (i) + (j)]
+  double normal2[3], nr[3], anr[3];
+  for (int i = 0; i < 3; ++i) normal2[i] = code <= 3 ? normal[i] : -normal[i];
+  for (int j = 0; j < 3; ++j) {
+    nr[j] = (RB(0, j) * normal2[0] + RB(1, j) * normal2[1]) + RB(2, j) * normal2[2];
+    anr[j] = std::fabs(nr[j]);
+  }
+  int lanr, a1, a2;
+  if (anr[1] > anr[0]) {
+    if (anr[1] > anr[2]) { a1 = 0; lanr = 1; a2 = 2; }
+    else { a1 = 0; a2 = 1; lanr = 2; }
+  } else {
+    if (anr[0] > anr[2]) { lanr = 0; a1 = 1; a2 = 2; }
+    else { a1 = 0; a2 = 1; lanr = 2; }
+  }
+  double center[3];
+  for (int i = 0; i < 3; ++i)
+    center[i] = nr[lanr] < 0 ? (pb[i] - pa[i]) + RB(i, lanr) * Sb[lanr] : (pb[i] - pa[i]) - RB(i, lanr) * Sb[lanr];
+  const int codeN = code <= 3 ? code - 1 : code - 4;
+  const int code1 = codeN == 0 ? 1 : 0, code2 = codeN == 2 ? 1 : 2;
+  const double c1 = (RA(0, code1) * center[0] + RA(1, code1) * center[1]) + RA(2, code1) * center[2];
+  const double c2 = (RA(0, code2) * center[0] + RA(1, code2) * center[1]) + RA(2, code2) * center[2];
+  double m11 = (RB(0, a1) * RA(0, code1) + RB(1, a1) * RA(1, code1)) + RB(2, a1) * RA(2, code1);
+  double m12 = (RB(0, a2) * RA(0, code1) + RB(1, a2) * RA(1, code1)) + RB(2, a2) * RA(2, code1);
+  double m21 = (RB(0, a1) * RA(0, code2) + RB(1, a1) * RA(1, code2)) + RB(2, a1) * RA(2, code2);
+  double m22 = (RB(0, a2) * RA(0, code2) + RB(1, a2) * RA(1, code2)) + RB(2, a2) * RA(2, code2);
+  double quad[8];
+  {
+    const double k1 = m11 * Sb[a1], k2 = m21 * Sb[a1], k3 = m12 * Sb[a2], k4 = m22 * Sb[a2];
+    quad[0] = c1 - k1 - k3;
+    quad[1] = c2 - k2 - k4;
+    quad[2] = c1 - k1 + k3;
+    quad[3] = c2 - k2 + k4;
+    quad[4] = c1 + k1 + k3;
+    quad[5] = c2 + k2 + k4;
+    quad[6] = c1 + k1 - k3;
+    quad[7] = c2 + k2 - k4;
+  }
+  const double rect[2] = {Sa[code1], Sa[code2]};
+  double ret[16];
+  const int n_intersect = cf_rect_quad(rect, quad, ret);
+  if (n_intersect < 1) return true;  // collision without a contact point
+  double points[8][3], dep[8];
+  const double det1 = 1.f / (m11 * m22 - m12 * m21);
+  m11 *= det1;
+  m12 *= det1;
+  m21 *= det1;
+  m22 *= det1;
+  int cnum = 0;
+  for (int j = 0; j < n_intersect; ++j) {
+    const double k1 = m22 * (ret[j * 2] - c1) - m12 * (ret[j * 2 + 1] - c2);
+    const double k2 = -m21 * (ret[j * 2] - c1) + m11 * (ret[j * 2 + 1] - c2);
+    for (int i = 0; i < 3; ++i) points[cnum][i] = (center[i] + RB(i, a1) * k1) + RB(i, a2) * k2;
+    dep[cnum] = Sa[codeN] - ((normal2[0] * points[cnum][0] + normal2[1] * points[cnum][1]) + normal2[2] * points[cnum][2]);
+    if (dep[cnum] >= 0) {
+      ret[cnum * 2] = ret[j * 2];
+      ret[cnum * 2 + 1] = ret[j * 2 + 1];
+      cnum++;
+    }
+  }
+  if (cnum < 1) return true;
+  int iret[8];
+  if (cnum <= 4) {
+    for (int j = 0; j < cnum; ++j) iret[j] = j;
+  } else {
+    int i1 = 0;
+    double maxdepth = dep[0];
+    for (int i = 1; i < cnum; ++i)
+      if (dep[i] > maxdepth) {
+        maxdepth = dep[i];
+        i1 = i;
+      }
+    cf_cull_points(cnum, ret, 4, i1, iret);
+    cnum = 4;
+  }
+  for (int j = 0; j < cnum; ++j) {
+    const int k = iret[j];
+    double wpt[3];
+    for (int i = 0; i < 3; ++i) wpt[i] = code < 4 ? points[k][i] + pa[i] : (points[k][i] + pa[i]) - normal[i] * dep[k];
+    cf_keep(nc, -dep[k], normal, wpt, dout, nout, pout);
+  }
+#undef RA
+#undef RB
+#undef R1_
+#undef R2_
+  return true;
+}
+
+// detail::sphereSphereIntersect with its contact
+__device__ bool sphere_sphere_contact(double r1, const SE3& T1, double r2, const SE3& T2, double& depth, V3& nd,
+                                      V3& ps) {
+  const double d0 = T2.p[0] - T1.p[0], d1 = T2.p[1] - T1.p[1], d2 = T2.p[2] - T1.p[2];
+  const double len = std::sqrt((d0 * d0 + d1 * d1) + d2 * d2);
+  if (len > r1 + r2) return false;
+  nd = len > 0 ? v3(d0 / len, d1 / len, d2 / len) : v3(d0, d1, d2);
+  ps = v3(T1.p[0] + d0 * r1 / (r1 + r2), T1.p[1] + d1 * r1 / (r1 + r2), T1.p[2] + d2 * r1 / (r1 + r2));
+  depth = r1 + r2 - len;
+  return true;
+}
+
+// detail::sphereBoxIntersect with its contact (normal from the sphere into the box)
+__device__ bool sphere_box_contact(double r, const SE3& TS, const double* side, const SE3& TB, double& depth, V3& nd,
+                                   V3& ps) {
+  double c[3], d[3];
+  bool clamped = false;
+  for (int i = 0; i < 3; ++i) {
+    const double inv_t = -((TB.R[i] * TB.p[0] + TB.R[3 + i] * TB.p[1]) + TB.R[6 + i] * TB.p[2]);
+    c[i] = ((TB.R[i] * TS.p[0] + TB.R[3 + i] * TS.p[1]) + TB.R[6 + i] * TS.p[2]) + inv_t;
+    const double h = side[i] / 2;
+    double nq = c[i];
+    if (c[i] < -h) {
+      clamped = true;
+      nq = -h;
+    }
+    if (c[i] > h) {
+      clamped = true;
+      nq = h;
+    }
+    d[i] = c[i] - nq;
+  }
+  const double dd = (d[0] * d[0] + d[1] * d[1]) + d[2] * d[2];
+  if (clamped && dd > r * r) return false;
+  double n[3] = {0, 0, 0}, dep;
+  if (clamped) {
+    const double dist = std::sqrt(dd);
+    for (int i = 0; i < 3; ++i) n[i] = -d[i] / dist;
+    dep = r - dist;
+  } else {
+    double min_d = INFINITY;
+    int ax = 0;
+    for (int i = 0; i < 3; ++i) {
+      const double di = side[i] / 2 - std::fabs(c[i]);
+      if (di < min_d) {
+        min_d = di;
+        ax = i;
+      }
+    }
+    n[ax] = c[ax] >= 0 ? -1 : 1;
+    dep = min_d + r;
+  }
+  double pc[3], nw[3], pw[3];
+  for (int i = 0; i < 3; ++i) pc[i] = c[i] + n[i] * (r - dep / 2);
+  for (int i = 0; i < 3; ++i) {
+    nw[i] = (TB.R[3 * i] * n[0] + TB.R[3 * i + 1] * n[1]) + TB.R[3 * i + 2] * n[2];
+    pw[i] = ((TB.R[3 * i] * pc[0] + TB.R[3 * i + 1] * pc[1]) + TB.R[3 * i + 2] * pc[2]) + TB.p[i];
+  }
+  nd = v3(nw[0], nw[1], nw[2]);
+  ps = v3(pw[0], pw[1], pw[2]);
+  depth = dep;
+  return true;
+}
+
+__host__ __device__ __forceinline__ bool cf_has_contact(int cf) {
+  return cf == CF_BOX_BOX || cf == CF_SPHERE_SPHERE || cf == CF_SPHERE_BOX || cf == CF_BOX_SPHERE;
+}
+
+__device__ bool closed_form_contact(int cf, const DevWorld& w, int ga, const SE3& TA, int gb, const SE3& TB,
+                                    double& depth, V3& nd, V3& ps) {
+  const cptr<double> pa = w.geom_rec + G_STRIDE * ga + G_PARAM, pb = w.geom_rec + G_STRIDE * gb + G_PARAM;
+  const double sa[3] = {pa[0], pa[1], pa[2]}, sb[3] = {pb[0], pb[1], pb[2]};
+  switch (cf) {
+    case CF_BOX_BOX: return box_box_contact(sa, TA, sb, TB, depth, nd, ps);
+    case CF_SPHERE_SPHERE: return sphere_sphere_contact(sa[0], TA, sb[0], TB, depth, nd, ps);
+    case CF_SPHERE_BOX: return sphere_box_contact(sa[0], TA, sb, TB, depth, nd, ps);
+    default: {  // CF_BOX_SPHERE: flipNormal
+      const bool h = sphere_box_contact(sb[0], TB, sa, TA, depth, nd, ps);
+      nd = v3(-nd.x, -nd.y, -nd.z);
+      return h;
+    }
+  }
+}
+
 template <bool FROM_POSES>
 __global__ __launch_bounds__(256) void contact_kernel(DevWorld w, const double* __restrict__ in,
                                                      const uint32_t* __restrict__ seg_len,
@@ -2734,11 +3153,19 @@ __global__ __launch_bounds__(256) void contact_kernel(DevWorld w, const double* 
       if (idx >= t1) continue;
       const long long c = cand[seg_start[p] + idx];
       if (!((masks[c * w.W + (p >> 5)] >> (p & 31)) & 1u)) continue;
-      const GObj A = a < w.n_moving ? moving_obj<FROM_POSES>(w, in, sc, c, a) : static_obj(w, a - w.n_moving);
-      const GObj B = b < w.n_moving ? moving_obj<FROM_POSES>(w, in, sc, c, b) : static_obj(w, b - w.n_moving);
       double dp = 0.0;
       V3 nd{0, 0, 0}, ps{0, 0, 0};
-      mpr_penetration(w, HV, A, B, dp, nd, ps);
+      if (cf_has_contact(w.pair_cf[p])) {
+        const SE3 TA = a < w.n_moving ? moving_tf<FROM_POSES>(w, in, sc, c, a) : load_se3(w.static_T + 12 * (a - w.n_moving));
+        const SE3 TB = b < w.n_moving ? moving_tf<FROM_POSES>(w, in, sc, c, b) : load_se3(w.static_T + 12 * (b - w.n_moving));
+        const int ga = a < w.n_moving ? w.moving_geom[a] : w.static_geom[a - w.n_moving];
+        const int gb = b < w.n_moving ? w.moving_geom[b] : w.static_geom[b - w.n_moving];
+        closed_form_contact(w.pair_cf[p], w, ga, TA, gb, TB, dp, nd, ps);
+      } else {
+        const GObj A = a < w.n_moving ? moving_obj<FROM_POSES>(w, in, sc, c, a) : static_obj(w, a - w.n_moving);
+        const GObj B = b < w.n_moving ? moving_obj<FROM_POSES>(w, in, sc, c, b) : static_obj(w, b - w.n_moving);
+        mpr_penetration(w, HV, A, B, dp, nd, ps);
+      }
       const size_t k = (size_t)c * w.n_pairs + p;
       depth[k] = dp;
       normal[3 * k] = nd.x;
@@ -2906,6 +3333,7 @@ struct mpg_world {
   } motion;
   std::mutex motion_mu;
   bool has_closed_form = false;  // a non-allowed pair uses an FCL closed form
+  bool has_contactless = false;  // a non-allowed pair whose contacts the device does not compute
   bool has_octree = false;       // a non-allowed pair involves an octree
   bool any_closed_form = false;  // some pair (allowed or not) does, octrees aside
   bool any_octree = false;       // some pair involves an octree
@@ -3862,6 +4290,7 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
   dw.pair_cf = to_cptr<int>(base + o_cf);
   for (int p = 0; p < d->n_pairs; ++p) {
     w->has_closed_form |= pair_cf[p] != CF_NONE && !allowed[p];
+    w->has_contactless |= pair_cf[p] != CF_NONE && !cf_has_contact(pair_cf[p]) && !allowed[p];
     w->has_octree |= pair_cf[p] == CF_OCTREE && !allowed[p];
     w->any_closed_form |= pair_cf[p] != CF_NONE && cf_class(pair_cf[p]) == CLS_CLOSED;
     w->any_octree |= pair_cf[p] == CF_OCTREE;
@@ -4315,10 +4744,10 @@ int mpg_collide_contacts(mpg_world* w, const double* input, int64_t n, int input
   if (n > 0 && ((!input && row > 0) || !flags || !pair_mask || !depth || !normal || !pos))
     return set_error(MPG_E_INVALID, "NULL buffer");
   if (mem != MPG_MEM_HOST && mem != MPG_MEM_DEVICE) return set_error(MPG_E_INVALID, "bad mem kind");
-  if (w->has_closed_form)
+  if (w->has_contactless)
     return set_error(MPG_E_UNSUPPORTED,
-                     "contacts for FCL closed-form pairs (box-box, sphere-sphere, sphere-box), octree and BVH mesh "
-                     "pairs are not implemented");
+                     "contacts for sphere-capsule / sphere-cylinder closed forms, octree and BVH mesh pairs are not "
+                     "implemented");
   if (n == 0) return MPG_OK;
   HIP_TRY(hipSetDevice(w->device));
   hipStream_t s = static_cast<hipStream_t>(stream);

@@ -454,6 +454,79 @@ def test_contacts_scalar_api():
             np.testing.assert_allclose(c.pos, rp[i, p], atol=1e-9)
 
 
+def _check_scalar_contacts(w, o2, q):
+    """collide_full(CollisionRequest(enable_contact=True)) per configuration
+    against the oracle's contact pass: the same reported pairs, each with the
+    oracle's (depth, normal, position) within 1e-9."""
+    req = pymp.fcl.CollisionRequest(enable_contact=True)
+    hit, rd, rn, rp = o2.contact_batch(q)
+    names = o2.pair_names()
+    for i in range(len(q)):
+        w.set_qpos_all(list(q[i]))
+        got = {(c.link_name1, c.link_name2): c.res.get_contacts()[0] for c in w.collide_full(req)}
+        exp = {names[p]: p for p in np.nonzero(hit[i])[0]}
+        assert set(got) == set(exp)
+        for k, p in exp.items():
+            c = got[k]
+            assert abs(c.penetration_depth - rd[i, p]) < 1e-9, (k, c.penetration_depth, rd[i, p])
+            np.testing.assert_allclose(c.normal, rn[i, p], atol=1e-9)
+            np.testing.assert_allclose(c.pos, rp[i, p], atol=1e-9)
+    return hit
+
+
+def test_closed_form_contacts_attached_box_scene():
+    """collision_avoidance.py:87-90's attached box with enable_contact=True:
+    the held box against the scene boxes takes boxBox2's contact path
+    (face-face clipping, edge-edge closest points), the other pairs MPR
+    penetration; every reported contact equals the oracle's within 1e-9."""
+    import oracle
+    from oracle import model as M
+    w, art = scenes.world(3)
+    pose = [0.0, 0.0, 0.14, 1.0, 0.0, 0.0, 0.0]
+    w.attach_object("held", pymp.fcl.Box([0.04, 0.04, 0.12]), "panda", 8, pose, ["panda_hand"])
+    base = ow(3)
+    o2 = oracle.OracleWorld(base.art, scene=base.scene,
+                            attached=[("held", 8, M.BoxGeom((0.04, 0.04, 0.12)), _oracle_T(pose))],
+                            allowed=[("panda_hand", "held"), ("panda_link0", "table")])
+    q = Wd.sample_q(base.art, 30000, 18)
+    _, mo = o2.collide_batch(q, nthreads=NTHREADS)
+    bb = [k for k, (a, b) in enumerate(o2.pair_names()) if a == "held"]
+    sel = np.nonzero(np.any(np.stack([(mo[:, k >> 5] >> (k & 31)) & 1 for k in bb], 1), 1))[0]
+    assert len(sel) >= 20
+    q = np.concatenate([q[sel[:150]], q[:20]])
+    hit = _check_scalar_contacts(w, o2, q)
+    assert hit[:, bb].sum() >= 20
+
+
+def test_closed_form_contacts_spheres():
+    """Sphere obstacles + an attached sphere with enable_contact=True:
+    sphereSphereIntersect / sphereBoxIntersect contacts (both argument
+    orders) and MPR for sphere-convex, vs the oracle within 1e-9."""
+    import oracle
+    from oracle import model as M
+    w, art = scenes.world(3)
+    rng = np.random.default_rng(55)
+    spheres = []
+    for k in range(4):
+        c = rng.uniform([0.2, -0.4, 0.1], [0.7, 0.4, 0.7])
+        r = float(rng.uniform(0.05, 0.15))
+        w.add_normal_object(f"ball{k}", pymp.fcl.CollisionObject(pymp.fcl.Sphere(r), list(c), [1, 0, 0, 0]))
+        spheres.append((f"ball{k}", M.SphereGeom(r), _oracle_T(list(c) + [1.0, 0.0, 0.0, 0.0])))
+    pose = [0.0, 0.0, 0.12, 1.0, 0.0, 0.0, 0.0]
+    w.attach_object("orb", pymp.fcl.Sphere(0.05), "panda", 8, pose, ["panda_hand"])
+    base = ow(3)
+    o2 = oracle.OracleWorld(base.art, scene=list(base.scene) + spheres,
+                            attached=[("orb", 8, M.SphereGeom(0.05), _oracle_T(pose))],
+                            allowed=[("panda_hand", "orb"), ("panda_link0", "table")])
+    q = Wd.sample_q(base.art, 30000, 19)
+    _, mo = o2.collide_batch(q, nthreads=NTHREADS)
+    orb = [k for k, (a, b) in enumerate(o2.pair_names()) if a == "orb"]
+    sel = np.nonzero(np.any(np.stack([(mo[:, k >> 5] >> (k & 31)) & 1 for k in orb], 1), 1))[0]
+    assert len(sel) >= 20
+    hit = _check_scalar_contacts(w, o2, q[sel[:150]])
+    assert hit[:, orb].sum() >= 20
+
+
 # ------------------------------------------------------------ scale / streams
 def test_chunked_batch_across_workspace_chunks():
     """Batches larger than one workspace chunk (2^20 configurations) run as
