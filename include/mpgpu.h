@@ -259,9 +259,9 @@ int mpg_distance_batch(mpg_world *world, const double *q, int64_t n, int32_t n_s
  * FCL closed-form pairs report the contact FCL 0.7's specialisation emits
  * (box-box: boxBox2's clipped face points / edge-edge closest point, with its
  * stored penetration_depth = -(point depth) <= 0; sphere-sphere; sphere-box
- * and box-sphere, normal flipped for the latter), reduced to the one contact
- * ShapeShapeCollide keeps for num_max_contacts = 1.  Worlds whose non-allowed
- * pairs include sphere-capsule / sphere-cylinder closed forms, octree or BVH
+ * and box-sphere; sphere-capsule; sphere-cylinder; the shape-sphere orders
+ * flip the normal), reduced to the one contact ShapeShapeCollide keeps for
+ * num_max_contacts = 1.  Worlds whose non-allowed pairs include octree or BVH
  * mesh pairs return MPG_E_UNSUPPORTED.
  */
 #define MPG_INPUT_Q 0

@@ -2707,7 +2707,7 @@ __device__ bool mpr_penetration(const DevWorld& w, cptr<double> HV, const GObj& 
 
 // ---------------------------------------------------------------------------
 // FCL closed-form contacts (CollisionRequest(enable_contact=True) on box-box,
-// sphere-sphere, sphere-box, box-sphere pairs): the contacts FCL 0.7.0's
+// sphere-sphere, sphere-box, sphere-capsule, sphere-cylinder pairs, both orders): the contacts FCL 0.7.0's
 // GJKSolver_libccd::shapeIntersect specialisations emit, reduced to the one
 // ShapeShapeCollide keeps for num_max_contacts = 1 (partial_sort by
 // descending penetration_depth, first of equals).  Same operation order as
@@ -3104,8 +3104,103 @@ __device__ bool sphere_box_contact(double r, const SE3& TS, const double* side, 
   return true;
 }
 
+// detail::sphereCapsuleIntersect with its contact (oracle sphere_capsule_contact)
+__device__ bool sphere_capsule_contact(double r1, const SE3& TS, double r2, double lz, const SE3& TC, double& depth,
+                                       V3& nd, V3& ps) {
+  double c[3];
+  centre_in_frame(TS, TC, c);
+  const double s1z = 0.5 * lz, s2z = -s1z;
+  const double vz = s2z - s1z;
+  const double w2 = c[2] - s1z;
+  const double c1 = (c[0] * 0.0 + c[1] * 0.0) + w2 * vz;
+  const double c2 = (0.0 * 0.0 + 0.0 * 0.0) + vz * vz;
+  double spz;
+  if (c1 <= 0) spz = s1z;
+  else if (c2 <= c1) spz = s2z;
+  else spz = s1z + vz * (c1 / c2);
+  const double d[3] = {c[0], c[1], c[2] - spz};
+  const double sq = (d[0] * d[0] + d[1] * d[1]) + d[2] * d[2];
+  const double dist = std::sqrt(sq) - r1 - r2;
+  if (dist > 0) return false;
+  const double nn = std::sqrt(sq);
+  double ln[3], lp[3], nw[3], pw[3];
+  for (int i = 0; i < 3; ++i) ln[i] = sq > 0 ? -(d[i] / nn) : -d[i];
+  lp[0] = 0.0 + ln[0] * dist;
+  lp[1] = 0.0 + ln[1] * dist;
+  lp[2] = spz + ln[2] * dist;
+  for (int i = 0; i < 3; ++i) {
+    nw[i] = (TC.R[3 * i] * ln[0] + TC.R[3 * i + 1] * ln[1]) + TC.R[3 * i + 2] * ln[2];
+    pw[i] = ((TC.R[3 * i] * lp[0] + TC.R[3 * i + 1] * lp[1]) + TC.R[3 * i + 2] * lp[2]) + TC.p[i];
+  }
+  nd = v3(nw[0], nw[1], nw[2]);
+  ps = v3(pw[0], pw[1], pw[2]);
+  depth = -dist;
+  return true;
+}
+
+// detail::sphereCylinderIntersect with its contact (oracle sphere_cylinder_contact)
+__device__ bool sphere_cylinder_contact(double r, const SE3& TS, double rc, double lz, const SE3& TC, double& depth,
+                                        V3& nd, V3& ps) {
+  double c[3], q[3];
+  centre_in_frame(TS, TC, c);
+  const double h = lz / 2;
+  bool clamped = false;
+  q[0] = c[0];
+  q[1] = c[1];
+  q[2] = c[2];
+  if (c[2] > h) {
+    q[2] = h;
+    clamped = true;
+  } else if (c[2] < -h) {
+    q[2] = -h;
+    clamped = true;
+  }
+  const double rd2 = c[0] * c[0] + c[1] * c[1];
+  if (rd2 > rc * rc) {
+    const double scale = rc / std::sqrt(rd2);
+    q[0] = c[0] * scale;
+    q[1] = c[1] * scale;
+    clamped = true;
+  }
+  const double d[3] = {q[0] - c[0], q[1] - c[1], q[2] - c[2]};
+  const double dd = (d[0] * d[0] + d[1] * d[1]) + d[2] * d[2];
+  if (clamped && dd > r * r) return false;
+  double n[3] = {0, 0, 0}, dep;
+  if (clamped) {
+    const double dist = std::sqrt(dd);
+    for (int i = 0; i < 3; ++i) n[i] = d[i] / dist;
+    dep = r - dist;
+  } else {
+    const double face = h - std::fabs(c[2]);
+    const double rad = std::sqrt(rd2);
+    const double barrel = rc - rad;
+    if (face <= barrel) {
+      n[2] = c[2] >= 0 ? -1 : 1;
+      dep = face + r;
+    } else {
+      if (rad > 0) {
+        n[0] = -(c[0] / rad);
+        n[1] = -(c[1] / rad);
+      } else {
+        n[0] = -1;
+      }
+      dep = barrel + r;
+    }
+  }
+  double pc[3], nw[3], pw[3];
+  for (int i = 0; i < 3; ++i) pc[i] = c[i] + n[i] * (r - dep / 2);
+  for (int i = 0; i < 3; ++i) {
+    nw[i] = (TC.R[3 * i] * n[0] + TC.R[3 * i + 1] * n[1]) + TC.R[3 * i + 2] * n[2];
+    pw[i] = ((TC.R[3 * i] * pc[0] + TC.R[3 * i + 1] * pc[1]) + TC.R[3 * i + 2] * pc[2]) + TC.p[i];
+  }
+  nd = v3(nw[0], nw[1], nw[2]);
+  ps = v3(pw[0], pw[1], pw[2]);
+  depth = dep;
+  return true;
+}
+
 __host__ __device__ __forceinline__ bool cf_has_contact(int cf) {
-  return cf == CF_BOX_BOX || cf == CF_SPHERE_SPHERE || cf == CF_SPHERE_BOX || cf == CF_BOX_SPHERE;
+  return cf != CF_NONE && cf != CF_OCTREE && cf != CF_MESH;
 }
 
 __device__ bool closed_form_contact(int cf, const DevWorld& w, int ga, const SE3& TA, int gb, const SE3& TB,
@@ -3116,12 +3211,17 @@ __device__ bool closed_form_contact(int cf, const DevWorld& w, int ga, const SE3
     case CF_BOX_BOX: return box_box_contact(sa, TA, sb, TB, depth, nd, ps);
     case CF_SPHERE_SPHERE: return sphere_sphere_contact(sa[0], TA, sb[0], TB, depth, nd, ps);
     case CF_SPHERE_BOX: return sphere_box_contact(sa[0], TA, sb, TB, depth, nd, ps);
-    default: {  // CF_BOX_SPHERE: flipNormal
-      const bool h = sphere_box_contact(sb[0], TB, sa, TA, depth, nd, ps);
-      nd = v3(-nd.x, -nd.y, -nd.z);
-      return h;
-    }
+    case CF_SPHERE_CAPSULE: return sphere_capsule_contact(sa[0], TA, sb[0], sb[1], TB, depth, nd, ps);
+    case CF_SPHERE_CYLINDER: return sphere_cylinder_contact(sa[0], TA, sb[0], sb[1], TB, depth, nd, ps);
+    default: break;
   }
+  // the shape-sphere orders: the sphere first, then flipNormal
+  bool h;
+  if (cf == CF_CAPSULE_SPHERE) h = sphere_capsule_contact(sb[0], TB, sa[0], sa[1], TA, depth, nd, ps);
+  else if (cf == CF_CYLINDER_SPHERE) h = sphere_cylinder_contact(sb[0], TB, sa[0], sa[1], TA, depth, nd, ps);
+  else h = sphere_box_contact(sb[0], TB, sa, TA, depth, nd, ps);  // CF_BOX_SPHERE
+  nd = v3(-nd.x, -nd.y, -nd.z);
+  return h;
 }
 
 template <bool FROM_POSES>
@@ -4746,8 +4846,7 @@ int mpg_collide_contacts(mpg_world* w, const double* input, int64_t n, int input
   if (mem != MPG_MEM_HOST && mem != MPG_MEM_DEVICE) return set_error(MPG_E_INVALID, "bad mem kind");
   if (w->has_contactless)
     return set_error(MPG_E_UNSUPPORTED,
-                     "contacts for sphere-capsule / sphere-cylinder closed forms, octree and BVH mesh pairs are not "
-                     "implemented");
+                     "contacts for octree and BVH mesh pairs are not implemented");
   if (n == 0) return MPG_OK;
   HIP_TRY(hipSetDevice(w->device));
   hipStream_t s = static_cast<hipStream_t>(stream);

@@ -1448,8 +1448,92 @@ static int sphere_box_contact(real r, const real *TS, const real *side, const re
     return 1;
 }
 
+/* detail::sphereCapsuleIntersect with its contact: diff = s_c - segment
+ * point, distance = |diff| - r1 - r2, local normal -diff.normalized(), point
+ * tf2 * (segment point + local normal * distance), depth -distance */
+static int sphere_capsule_contact(real r1, const real *TS, real r2, real lz, const real *TC, real *depth,
+                                  real *normal, real *pos) {
+    real c[3];
+    centre_in_frame(TS, TC, c);
+    const real s1[3] = {0.0, 0.0, 0.5 * lz}, s2[3] = {0.0, 0.0, -(0.5 * lz)};
+    const real v[3] = {s2[0] - s1[0], s2[1] - s1[1], s2[2] - s1[2]};
+    const real w[3] = {c[0] - s1[0], c[1] - s1[1], c[2] - s1[2]};
+    const real c1 = (w[0] * v[0] + w[1] * v[1]) + w[2] * v[2];
+    const real c2 = (v[0] * v[0] + v[1] * v[1]) + v[2] * v[2];
+    real sp[3];
+    if (c1 <= 0) { sp[0] = s1[0]; sp[1] = s1[1]; sp[2] = s1[2]; }
+    else if (c2 <= c1) { sp[0] = s2[0]; sp[1] = s2[1]; sp[2] = s2[2]; }
+    else { const real b = c1 / c2; for (int i = 0; i < 3; ++i) sp[i] = s1[i] + v[i] * b; }
+    const real d[3] = {c[0] - sp[0], c[1] - sp[1], c[2] - sp[2]};
+    const real sq = (d[0] * d[0] + d[1] * d[1]) + d[2] * d[2];
+    const real dist = sqrt(sq) - r1 - r2;
+    if (dist > 0) return 0;
+    real ln[3], lp[3];
+    const real nn = sqrt(sq);
+    for (int i = 0; i < 3; ++i) ln[i] = sq > 0 ? -(d[i] / nn) : -d[i];
+    for (int i = 0; i < 3; ++i) lp[i] = sp[i] + ln[i] * dist;
+    for (int i = 0; i < 3; ++i) {
+        normal[i] = (TC[3 * i] * ln[0] + TC[3 * i + 1] * ln[1]) + TC[3 * i + 2] * ln[2];
+        pos[i] = ((TC[3 * i] * lp[0] + TC[3 * i + 1] * lp[1]) + TC[3 * i + 2] * lp[2]) + TC[9 + i];
+    }
+    *depth = -dist;
+    return 1;
+}
+
+/* detail::sphereCylinderIntersect with its contact (normal from the sphere
+ * into the cylinder): centre outside -> towards the nearest point, depth
+ * r - distance; centre inside -> the nearer of the cap (ties) and the barrel
+ * (on the axis: -x), depth + r; contact c + n (r - depth / 2) */
+static int sphere_cylinder_contact(real r, const real *TS, real rc, real lz, const real *TC, real *depth,
+                                   real *normal, real *pos) {
+    real c[3], nq[3];
+    centre_in_frame(TS, TC, c);
+    const real h = lz / 2;
+    int clamped = 0;
+    nq[0] = c[0]; nq[1] = c[1]; nq[2] = c[2];
+    if (c[2] > h) { nq[2] = h; clamped = 1; }
+    else if (c[2] < -h) { nq[2] = -h; clamped = 1; }
+    const real rd2 = c[0] * c[0] + c[1] * c[1];
+    if (rd2 > rc * rc) {
+        const real scale = rc / sqrt(rd2);
+        nq[0] = c[0] * scale;
+        nq[1] = c[1] * scale;
+        clamped = 1;
+    }
+    const real d[3] = {nq[0] - c[0], nq[1] - c[1], nq[2] - c[2]};
+    const real dd = (d[0] * d[0] + d[1] * d[1]) + d[2] * d[2];
+    if (clamped && dd > r * r) return 0;
+    real n[3] = {0, 0, 0}, dep;
+    if (clamped) {
+        const real dist = sqrt(dd);
+        for (int i = 0; i < 3; ++i) n[i] = d[i] / dist;
+        dep = r - dist;
+    } else {
+        const real face = h - fabs(c[2]);
+        const real rad = sqrt(rd2);
+        const real barrel = rc - rad;
+        if (face <= barrel) {
+            n[2] = c[2] >= 0 ? -1 : 1;
+            dep = face + r;
+        } else {
+            if (rad > 0) { n[0] = -(c[0] / rad); n[1] = -(c[1] / rad); }
+            else n[0] = -1;
+            dep = barrel + r;
+        }
+    }
+    real pc[3];
+    for (int i = 0; i < 3; ++i) pc[i] = c[i] + n[i] * (r - dep / 2);
+    for (int i = 0; i < 3; ++i) {
+        normal[i] = (TC[3 * i] * n[0] + TC[3 * i + 1] * n[1]) + TC[3 * i + 2] * n[2];
+        pos[i] = ((TC[3 * i] * pc[0] + TC[3 * i + 1] * pc[1]) + TC[3 * i + 2] * pc[2]) + TC[9 + i];
+    }
+    *depth = dep;
+    return 1;
+}
+
 /* the closed-form contact of a pair; -1 when the pair is not one of
- * box-box, sphere-sphere, sphere-box, box-sphere */
+ * FCL's closed forms (box-box, sphere-sphere, sphere-box, sphere-capsule,
+ * sphere-cylinder, both orders) */
 static int closed_form_contact(const orc_world *w, int ga, const real *Ta, int gb, const real *Tb, real *depth,
                                real *normal, real *pos) {
     const int ta = w->geom_type[ga], tb = w->geom_type[gb];
@@ -1465,7 +1549,14 @@ static int closed_form_contact(const orc_world *w, int ga, const real *Ta, int g
         for (int i = 0; i < 3; ++i) normal[i] = -normal[i]; /* flipNormal */
         return h;
     }
-    return -1;
+    int h = -1, flip = 0;
+    if (ta == GEOM_SPHERE && tb == GEOM_CAPSULE) h = sphere_capsule_contact(pa[0], Ta, pb[0], pb[1], Tb, depth, normal, pos);
+    if (ta == GEOM_CAPSULE && tb == GEOM_SPHERE) { h = sphere_capsule_contact(pb[0], Tb, pa[0], pa[1], Ta, depth, normal, pos); flip = 1; }
+    if (ta == GEOM_SPHERE && tb == GEOM_CYLINDER) h = sphere_cylinder_contact(pa[0], Ta, pb[0], pb[1], Tb, depth, normal, pos);
+    if (ta == GEOM_CYLINDER && tb == GEOM_SPHERE) { h = sphere_cylinder_contact(pb[0], Tb, pa[0], pa[1], Ta, depth, normal, pos); flip = 1; }
+    if (flip)
+        for (int i = 0; i < 3; ++i) normal[i] = -normal[i]; /* flipNormal */
+    return h;
 }
 
 /* ------------------------------------------------ GJK distance

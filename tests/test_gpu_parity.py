@@ -527,6 +527,50 @@ def test_closed_form_contacts_spheres():
     assert hit[:, orb].sum() >= 20
 
 
+def test_closed_form_contacts_capsules_cylinders():
+    """The capsule / cylinder world of test_capsule_cylinder_worlds_match_oracle
+    with enable_contact=True: sphere-capsule / sphere-cylinder contacts (both
+    argument orders, flipNormal) and MPR for convex-capsule, capsule-capsule;
+    every reported contact within 1e-9 of the oracle."""
+    import oracle
+    from oracle import model as M
+    w, art = scenes.world(3)
+    rng = np.random.default_rng(77)
+    extra = []
+    for k in range(6):
+        c = rng.uniform([0.2, -0.4, 0.1], [0.7, 0.4, 0.7])
+        q = rng.normal(size=4)
+        q /= np.linalg.norm(q)
+        r, lz = float(rng.uniform(0.03, 0.08)), float(rng.uniform(0.1, 0.3))
+        if k < 2:
+            g, og, name = pymp.fcl.Capsule(r, lz), M.CapsuleGeom(r, lz), f"cap{k}"
+        elif k < 4:
+            g, og, name = pymp.fcl.Cylinder(r, lz), M.CylinderGeom(r, lz), f"cyl{k}"
+        else:
+            g, og, name = pymp.fcl.Sphere(r), M.SphereGeom(r), f"ball{k}"
+        w.add_normal_object(name, pymp.fcl.CollisionObject(g, list(c), list(q)))
+        extra.append((name, og, _oracle_T(list(c) + list(q))))
+    p_orb = [0.0, 0.0, 0.12, 1.0, 0.0, 0.0, 0.0]
+    p_rod = [0.0, 0.05, 0.0, 0.7071067811865476, 0.7071067811865476, 0.0, 0.0]
+    w.attach_object("orb", pymp.fcl.Sphere(0.05), "panda", 8, p_orb, ["panda_hand"])
+    w.attach_object("rod", pymp.fcl.Capsule(0.02, 0.2), "panda", 6, p_rod, ["panda_link6", "panda_link7"])
+    base = ow(3)
+    o2 = oracle.OracleWorld(base.art, scene=list(base.scene) + extra,
+                            attached=[("orb", 8, M.SphereGeom(0.05), _oracle_T(p_orb)),
+                                      ("rod", 6, M.CapsuleGeom(0.02, 0.2), _oracle_T(p_rod))],
+                            allowed=[("panda_hand", "orb"), ("panda_link6", "rod"), ("panda_link7", "rod"),
+                                     ("panda_link0", "table")])
+    q = Wd.sample_q(base.art, 30000, 23)
+    _, mo = o2.collide_batch(q, nthreads=NTHREADS)
+    cf = [k for k, (a, b) in enumerate(o2.pair_names())
+          if (a == "orb" and b[:3] in ("cap", "cyl")) or (a == "rod" and b.startswith("ball"))]
+    assert cf
+    sel = np.nonzero(np.any(np.stack([(mo[:, k >> 5] >> (k & 31)) & 1 for k in cf], 1), 1))[0]
+    assert len(sel) >= 5
+    hit = _check_scalar_contacts(w, o2, np.concatenate([q[sel[:150]], q[:20]]))
+    assert hit[:, cf].sum() >= 5
+
+
 # ------------------------------------------------------------ scale / streams
 def test_chunked_batch_across_workspace_chunks():
     """Batches larger than one workspace chunk (2^20 configurations) run as

@@ -419,3 +419,42 @@ def test_closed_form_contact_batch_consistent_with_collide():
     assert h.sum() > 0
     np.testing.assert_allclose(np.linalg.norm(normal[:, bb][h], axis=1), 1.0, atol=1e-12)
     assert (depth[:, bb][h] <= 0).all()
+
+
+def test_sphere_capsule_cylinder_contacts_known_answers():
+    """FCL 0.7.0 sphereCapsuleIntersect / sphereCylinderIntersect contacts
+    (plain geometry; parity unpinned): normal from the sphere into the other
+    shape, the capsule's point on the sphere side of the axis point, the
+    cylinder's half way between the sphere's deepest point and the surface;
+    the other argument order flips the normal."""
+    w, (sph, cap, cyl, small) = _pair_world([M.SphereGeom(0.2), M.CapsuleGeom(0.1, 0.4), M.CylinderGeom(0.1, 0.4),
+                                             M.SphereGeom(0.05)])
+    r, d, n, p = _contact(w, sph, _T(p=(0.25, 0.0, 0.1)), cap, _T())
+    assert r == 1 and abs(d - 0.05) < 1e-12
+    np.testing.assert_allclose(n, [-1, 0, 0], atol=1e-15)
+    np.testing.assert_allclose(p, [0.05, 0, 0.1], atol=1e-12)
+    r, d2, n2, p2 = _contact(w, cap, _T(), sph, _T(p=(0.25, 0.0, 0.1)))
+    assert r == 1 and d2 == d
+    np.testing.assert_array_equal(n2, -n)
+    np.testing.assert_array_equal(p2, p)
+    assert _contact(w, sph, _T(p=(0.31, 0.0, 0.1)), cap, _T())[0] == 0
+    # beyond the capsule's end cap: the segment end is the nearest axis point
+    r, d, n, p = _contact(w, sph, _T(p=(0.0, 0.0, 0.45)), cap, _T())
+    assert r == 1 and abs(d - 0.05) < 1e-12
+    np.testing.assert_allclose(n, [0, 0, -1], atol=1e-15)
+    r, d, n, p = _contact(w, sph, _T(p=(0.25, 0.0, 0.1)), cyl, _T())
+    assert r == 1 and abs(d - 0.05) < 1e-12
+    np.testing.assert_allclose(n, [-1, 0, 0], atol=1e-15)
+    np.testing.assert_allclose(p, [0.075, 0, 0.1], atol=1e-12)
+    # centre inside the cylinder, nearer the top cap than the barrel
+    r, d, n, p = _contact(w, small, _T(p=(0.02, 0.0, 0.15)), cyl, _T())
+    assert r == 1 and abs(d - 0.1) < 1e-12
+    np.testing.assert_allclose(n, [0, 0, -1], atol=1e-15)
+    np.testing.assert_allclose(p, [0.02, 0, 0.15], atol=1e-12)
+    # nearer the barrel
+    r, d, n, p = _contact(w, small, _T(p=(0.07, 0.0, 0.0)), cyl, _T())
+    assert r == 1 and abs(d - 0.08) < 1e-12
+    np.testing.assert_allclose(n, [-1, 0, 0], atol=1e-15)
+    r, d2, n2, _ = _contact(w, cyl, _T(), small, _T(p=(0.07, 0.0, 0.0)))
+    assert r == 1 and d2 == d
+    np.testing.assert_array_equal(n2, -n)
