@@ -975,24 +975,44 @@ __global__ __launch_bounds__(BLOCK) void cull_kernel(DevWorld w, const double* _
     const float* rm = cen + (size_t)m * 3 * BLOCK + tid;
     const float cm[3] = {rm[0], rm[BLOCK], rm[2 * BLOCK]};
     const float r_m = w.bp.mobj[BM_STRIDE * m + BM_R];
-    for (int e = e0; e < e1; ++e) {
-      const int p = w.sched_pair[e], o = w.sched_other[e];
-      bool keep;
-      if (o >= w.n_moving) {
-        keep = !fsphere_obb_separated(cm, r_m, w.bp.sobj + BS_STRIDE * (o - w.n_moving), w.bp_margin);
-      } else {
-        const float* ro = cen + (size_t)o * 3 * BLOCK + tid;
-        const float dx = ro[0] - cm[0], dy = ro[BLOCK] - cm[1], dz = ro[2 * BLOCK] - cm[2];
-        const float rr = r_m + w.bp.mobj[BM_STRIDE * o + BM_R] + w.bp_margin;
-        keep = dx * dx + dy * dy + dz * dz <= rr * rr;
+    // up to 32 schedule entries at a time: first every bounding test into a
+    // per-lane bit set (a plain loop the compiler unrolls, its scalar loads
+    // issued ahead), then only the entries some lane kept are queued
+    for (int eb = e0; eb < e1; eb += 32) {
+      const int ee = min(e1, eb + 32);
+      uint32_t kb = 0u;
+#pragma unroll 4
+      for (int e = eb; e < ee; ++e) {
+        const int o = w.sched_other[e];
+        bool keep;
+        if (o >= w.n_moving) {
+          keep = !fsphere_obb_separated(cm, r_m, w.bp.sobj + BS_STRIDE * (o - w.n_moving), w.bp_margin);
+        } else {
+          const float* ro = cen + (size_t)o * 3 * BLOCK + tid;
+          const float dx = ro[0] - cm[0], dy = ro[BLOCK] - cm[1], dz = ro[2 * BLOCK] - cm[2];
+          const float rr = r_m + w.bp.mobj[BM_STRIDE * o + BM_R] + w.bp_margin;
+          keep = dx * dx + dy * dy + dz * dz <= rr * rr;
+        }
+        kb |= (uint32_t)keep << (e - eb);
       }
-      keep = keep && live;
+      if (!live) kb = 0u;
       if (w.debug_mode == 2) {
-        if (keep) survw[(p >> 5) * BLOCK + tid] |= 1u << (p & 31);
+        for (int e = eb; e < ee; ++e) {
+          const int p = w.sched_pair[e];
+          if ((kb >> (e - eb)) & 1u) survw[(p >> 5) * BLOCK + tid] |= 1u << (p & 31);
+        }
         continue;
       }
-      const unsigned long long bal = __ballot(keep);
-      if (bal) {
+      uint32_t any_kb = kb;  // entries some lane of the wave kept
+#pragma unroll
+      for (int sh = 1; sh < 64; sh <<= 1) any_kb |= (uint32_t)__shfl_xor((int)any_kb, sh);
+      any_kb = __builtin_amdgcn_readfirstlane(any_kb);
+      while (any_kb) {
+        const int i = __builtin_ctz(any_kb);
+        any_kb &= any_kb - 1u;
+        const int p = w.sched_pair[eb + i];
+        const bool keep = (kb >> i) & 1u;
+        const unsigned long long bal = __ballot(keep);
         if (keep) {
           const uint32_t rank =
               __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
@@ -1007,6 +1027,10 @@ __global__ __launch_bounds__(BLOCK) void cull_kernel(DevWorld w, const double* _
     }
   }
   if (tail != head) sat_drain<BLOCK>(w, cen, rq, cap, cfg0, survw, queue, head, tail - head, wbase, lane);
+  if (w.debug_mode == 8) {  // ablation: bounding tests + SAT only
+    if (live && survw[tid] == 12345u) flags[cfg] = 2;
+    return;
+  }
   // survivor words -> surv, and this wave's candidate count per pair ->
   // cnt[pair][tile] (the bucketing's tile counts; cnt is zeroed before the
   // launch, pairs without a survivor in the tile are skipped): one step per
@@ -1027,7 +1051,7 @@ __global__ __launch_bounds__(BLOCK) void cull_kernel(DevWorld w, const double* _
       if (lane == 0) cnt[(long long)(k * 32 + b) * n_tiles + tile] = (uint32_t)__popcll(bb);
     }
   }
-  if (FROM_POSES) return;
+  if (FROM_POSES || w.debug_mode == 9) return;  // 9: ablation without the sincos pass
   // Exact fp64 sin/cos of every revolute move-group joint for the narrow
   // phase's chain FK (the glibc sincos restatement), only for configurations
   // with a candidate pair (about a quarter of them): compacted across the
