@@ -243,7 +243,10 @@ int mpg_check_motion_batch(mpg_world *world, const double *q_from, const double 
  * penetrate) is compared with strict '<', so the first minimum wins.
  * d_*: minimum distance (DBL_MAX if the group is empty), p_*: its pair
  * index (-1 if none).  Distances are within 1e-5 of FCL's GJK (GJK run to
- * 1e-12 relative convergence on the same support mappings).
+ * 1e-12 relative convergence on the same support mappings).  A point cloud
+ * (OcTree) pair's distance is the minimum over its occupied leaf boxes
+ * (OcTreeShapeDistanceRecurse, leaf box first); worlds with BVH-mesh pairs
+ * return MPG_E_UNSUPPORTED.
  */
 int mpg_distance_batch(mpg_world *world, const double *q, int64_t n, int32_t n_self_pairs, double *d_self,
                        int32_t *p_self, double *d_others, int32_t *p_others, int mem, void *stream);

@@ -2442,13 +2442,15 @@ __device__ __forceinline__ bool simplex_closest(V3 P[4], int& n, V3& v) {
   return false;
 }
 
-__device__ double gjk_distance(const DevWorld& w, cptr<double> HV, const GObj& A, const GObj& B) {
-  V3 v = vsub(to_v3(center(w, A)), to_v3(center(w, B)));
+// GJK distance from v = centre(A) - centre(B) over the support map sup(dir)
+// of A - B (the oracle's gjk_distance)
+template <typename Sup>
+__device__ double gjk_distance_from(V3 v, Sup sup) {
   if (d3dot(v, v) == 0.0) v.x = 1e-12;
   V3 P[4];
   int n = 0;
   for (int it = 0; it < 128; ++it) {
-    const V3 wv = to_v3(msupport(w, HV, A, B, cv3(-v.x, -v.y, -v.z)));
+    const V3 wv = to_v3(sup(cv3(-v.x, -v.y, -v.z)));
     const double vv = d3dot(v, v), vw = d3dot(v, wv);
     if (n > 0 && vv - vw <= 1e-12 * vv) break;
     bool dup = false;
@@ -2461,6 +2463,47 @@ __device__ double gjk_distance(const DevWorld& w, cptr<double> HV, const GObj& A
     if (n > 1 && nv >= vv) break;
   }
   return std::sqrt(d3dot(v, v));
+}
+
+__device__ double gjk_distance(const DevWorld& w, cptr<double> HV, const GObj& A, const GObj& B) {
+  return gjk_distance_from(vsub(to_v3(center(w, A)), to_v3(center(w, B))),
+                           [&](const CV3& d) { return msupport(w, HV, A, B, d); });
+}
+
+// fcl::distance(shape, OcTree) [ext FCL 0.7.0 OcTreeShapeDistanceRecurse]:
+// the minimum over the occupied leaves of shapeDistance(leaf box, shape) with
+// the box first (constructBox: box_tf = tf * Translation(centre), boxToGJK);
+// FCL's pruning only skips leaves that cannot lower the minimum and it stops
+// at the first penetrating leaf (-1).  Leaves whose bounding sphere cannot
+// beat the running minimum `best` (the caller's) are skipped the same way.
+__device__ double octree_distance(const DevWorld& w, cptr<double> HV, int go, const SE3& TO, const GObj& S,
+                                  const V3& cs, double rs, double best) {
+  const cptr<double> go_rec = w.geom_rec + G_STRIDE * go;
+  const int l0 = (int)go_rec[G_PARAM], ln = (int)go_rec[G_PARAM + 1];
+  GObj A;
+  A.rot = gjk_rot_from_matrix(TO.R);
+  A.rot_inv = quat_invert2(A.rot);
+  A.geom = go;
+  A.type = MPG_GEOM_BOX;
+  for (int l = l0; l < l0 + ln && best != -1.0; ++l) {
+    const cptr<double> L = w.oct_leaf + 6 * (size_t)l;
+    double c[3], side[3], cw[3];
+    for (int i = 0; i < 3; ++i) {
+      c[i] = (L[i] + L[3 + i]) * 0.5;
+      side[i] = L[3 + i] - L[i];
+    }
+    for (int i = 0; i < 3; ++i) cw[i] = ((TO.R[3 * i] * c[0] + TO.R[3 * i + 1] * c[1]) + TO.R[3 * i + 2] * c[2]) + TO.p[i];
+    const double dx = cw[0] - cs.x, dy = cw[1] - cs.y, dz = cw[2] - cs.z;
+    const double rl = 0.5 * std::sqrt((side[0] * side[0] + side[1] * side[1]) + side[2] * side[2]);
+    if (std::sqrt(dx * dx + dy * dy + dz * dz) - rs - rl - 1e-9 >= best) continue;
+    GObj A1 = A;
+    A1.pos = cv3(cw[0], cw[1], cw[2]);
+    const ccd_real h[3] = {(ccd_real)(side[0] / 2.0), (ccd_real)(side[1] / 2.0), (ccd_real)(side[2] / 2.0)};
+    const double d = gjk_distance_from(vsub(to_v3(A1.pos), to_v3(center(w, S))),
+                                       [&](const CV3& dir) { return msupport_box(A1, h, w, HV, S, dir); });
+    if (d < best) best = d;
+  }
+  return best;
 }
 
 __device__ __forceinline__ GObj pose_obj(const DevWorld& w, const double* __restrict__ poses, long long n, long long cfg,
@@ -2500,6 +2543,16 @@ __global__ __launch_bounds__(128) void distance_kernel(DevWorld w, const double*
     const GObj A = pose_obj(w, poses, n, cfg, a, ca);
     const GObj B = pose_obj(w, poses, n, cfg, b, cb);
     const double ra = w.geom_rec[G_STRIDE * A.geom + G_RADIUS], rb = w.geom_rec[G_STRIDE * B.geom + G_RADIUS];
+    if (w.pair_cf[p] == CF_OCTREE) {  // the octree is the pair's static side (b)
+      if (!live || best[g] == -1.0) continue;
+      const SE3 TO = load_se3(w.static_T + 12 * (b - w.n_moving));
+      const double d = octree_distance(w, HV, B.geom, TO, A, ca, ra, best[g]);
+      if (d < best[g]) {
+        best[g] = d;
+        bp[g] = p;
+      }
+      continue;
+    }
     const V3 dc = vsub(cb, ca);
     // bounding spheres: the pair cannot beat the running minimum
     const double lb = std::sqrt(d3dot(dc, dc)) - ra - rb - 1e-9;
@@ -4810,7 +4863,6 @@ int mpg_distance_batch(mpg_world* w, const double* q, int64_t n, int32_t n_self_
   if (n > 0 && ((!q && w->dw.dof > 0) || !d_self || !p_self || !d_others || !p_others))
     return set_error(MPG_E_INVALID, "NULL buffer");
   if (mem != MPG_MEM_HOST && mem != MPG_MEM_DEVICE) return set_error(MPG_E_INVALID, "bad mem kind");
-  if (w->has_octree) return set_error(MPG_E_UNSUPPORTED, "distance to an OcTree is not implemented on the device");
   if (w->has_mesh) return set_error(MPG_E_UNSUPPORTED, "distance to a BVH mesh is not implemented on the device");
   if (n == 0) return MPG_OK;
   HIP_TRY(hipSetDevice(w->device));

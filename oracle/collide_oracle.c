@@ -2131,6 +2131,32 @@ static void *worker(void *arg) {
  * pairs are skipped before any distance (src/planning_world.cpp:509-510);
  * strict '<' keeps the first minimum.  best = DBL_MAX / pair -1 when a group
  * has no pair. */
+/* fcl::distance(shape, OcTree) [ext FCL 0.7.0 OcTreeSolver::
+ * OcTreeShapeDistanceRecurse]: every occupied leaf as a box (constructBox:
+ * box_tf = tf * Translation(centre), boxToGJK), shapeDistance(box, shape);
+ * its internal-node pruning only skips leaves that cannot lower the running
+ * minimum, and it stops at the first penetrating leaf (-1, isSatisfied), so
+ * the result is the minimum over all leaves.  Box first, as FCL calls it. */
+static double octree_distance(const orc_world *w, int go, const real *TO, const gjk_obj *shape) {
+    const int l0 = (int)w->geom_param[4 * go], ln = (int)w->geom_param[4 * go + 1];
+    double best = DBL_MAX;
+    for (int l = l0; l < l0 + ln && best != -1.0; ++l) {
+        const real *L = w->oct_leaf + 6 * (size_t)l;
+        real c[3], side[3], TL[12];
+        for (int k = 0; k < 3; ++k) { c[k] = (L[k] + L[3 + k]) * 0.5; side[k] = L[3 + k] - L[k]; }
+        for (int k = 0; k < 9; ++k) TL[k] = TO[k];
+        for (int i = 0; i < 3; ++i) TL[9 + i] = ((TO[3 * i] * c[0] + TO[3 * i + 1] * c[1]) + TO[3 * i + 2] * c[2]) + TO[9 + i];
+        gjk_obj box;
+        memset(&box, 0, sizeof box);
+        shape_to_gjk(TL, &box);
+        box.type = GEOM_BOX;
+        for (int k = 0; k < 3; ++k) box.dim[k] = side[k] / 2.0; /* boxToGJK */
+        const double d = gjk_distance(&box, shape);
+        if (d < best) best = d;
+    }
+    return best;
+}
+
 int orc_distance_batch(const orc_world *w, const double *q, long n, int n_self, double *d_self, int *p_self,
                        double *d_others, int *p_others) {
     real *oMi = malloc(sizeof(real) * 12 * (size_t)(w->nj + 1));
@@ -2149,15 +2175,19 @@ int orc_distance_batch(const orc_world *w, const double *q, long n, int n_self, 
             if (best[g] == -1.0) continue;  /* nothing is below -1 */
             int ks[2] = {w->pa_kind[p], w->pb_kind[p]}, is[2] = {w->pa_idx[p], w->pb_idx[p]};
             gjk_obj o[2];
+            const real *Ts[2];
+            int gs[2];
             for (int s = 0; s < 2; ++s) {
                 const real *T;
                 int gg;
                 if (ks[s] == KIND_ROBOT) { T = obj_T + 12 * is[s]; gg = w->obj_geom[is[s]]; }
                 else if (ks[s] == KIND_ATTACHED) { T = att_T + 12 * is[s]; gg = w->att_geom[is[s]]; }
                 else { T = w->scene_tf + 12 * is[s]; gg = w->scene_geom[is[s]]; }
-                make_obj(w, gg, T, &o[s], NULL);
+                Ts[s] = T; gs[s] = gg;
+                if (w->geom_type[gg] != GEOM_OCTREE) make_obj(w, gg, T, &o[s], NULL);
             }
-            const double d = gjk_distance(&o[0], &o[1]);
+            const int oi = w->geom_type[gs[0]] == GEOM_OCTREE ? 0 : w->geom_type[gs[1]] == GEOM_OCTREE ? 1 : -1;
+            const double d = oi < 0 ? gjk_distance(&o[0], &o[1]) : octree_distance(w, gs[oi], Ts[oi], &o[1 - oi]);
             if (d < best[g]) { best[g] = d; bp[g] = p; }
         }
         d_self[c] = best[0]; p_self[c] = bp[0]; d_others[c] = best[1]; p_others[c] = bp[1];

@@ -699,9 +699,30 @@ def test_point_cloud_known_answers_and_unsupported_queries():
     w.set_qpos_all(Wd.KAT_FREE)
     assert w.collide_with_others() == []
     with pytest.raises(NotImplementedError):
-        w.distance_with_others()
-    with pytest.raises(NotImplementedError):
         w.collide(pymp.fcl.CollisionRequest(enable_contact=True))
+
+
+@pytest.mark.parametrize("cloud,n", [("floor", 96), ("blue", 512)])
+def test_point_cloud_distance_matches_oracle(cloud, n):
+    """distance to a point cloud (fcl::distance(shape, OcTree): the minimum
+    over the occupied leaf boxes of GJK(leaf box, shape)): batched and scalar
+    distances equal the oracle's within 1e-9, argmin pair equal."""
+    w, art = scenes.cloud_world(cloud)
+    o = Wd.oracle_cloud_world(cloud)
+    q = scenes.sample_states(art, n, 97)
+    ds, ps, do, po = w.distance_batch(q)
+    rs, rps, ro, rpo = o.distance_batch(q)
+    for d, r in ((ds, rs), (do, ro)):
+        np.testing.assert_array_equal(d == -1.0, r == -1.0)
+        np.testing.assert_allclose(d, r, rtol=0, atol=1e-9)
+    assert (ps == rps).mean() > 0.99 and (po == rpo).mean() > 0.99
+    names = [(i[3], i[4]) for i in w.get_collision_pair_info()]
+    if cloud == "floor":  # the floor is the nearest object for most configurations
+        assert np.mean([names[p][1] == "scene_pcd" for p in po]) > 0.5
+    for i in range(4):
+        w.set_qpos_all(list(q[i]))
+        r = w.distance_with_others()
+        assert abs(r.min_distance - ro[i]) < 1e-9 and (r.link_name1, r.link_name2) == names[rpo[i]]
 
 
 def test_attached_box_against_point_cloud():
