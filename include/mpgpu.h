@@ -264,8 +264,11 @@ int mpg_distance_batch(mpg_world *world, const double *q, int64_t n, int32_t n_s
  * stored penetration_depth = -(point depth) <= 0; sphere-sphere; sphere-box
  * and box-sphere; sphere-capsule; sphere-cylinder; the shape-sphere orders
  * flip the normal), reduced to the one contact ShapeShapeCollide keeps for
- * num_max_contacts = 1.  Worlds whose non-allowed pairs include octree or BVH
- * mesh pairs return MPG_E_UNSUPPORTED.
+ * num_max_contacts = 1.  A point-cloud (OcTree) pair reports the contact of
+ * the first occupied leaf of FCL's traversal that intersects the shape, with
+ * the tree as the contact's o1 (normal from the leaf box into the shape).
+ * Worlds whose non-allowed pairs include BVH mesh pairs return
+ * MPG_E_UNSUPPORTED.
  */
 #define MPG_INPUT_Q 0
 #define MPG_INPUT_LINK_POSES 1

@@ -2687,16 +2687,18 @@ __device__ __forceinline__ CV3 find_pos3(const SupP P[4]) {
   return vscale(vadd(p1, p2), ccd_real(0.5));
 }
 
-// ccdMPRPenetration: true if penetrating (depth, dir, pos set)
-__device__ bool mpr_penetration_ccd(const DevWorld& w, cptr<double> HV, const GObj& A, const GObj& B, ccd_real& depth,
-                                    CV3& dir_out, CV3& pos_out) {
+// ccdMPRPenetration: true if penetrating (depth, dir, pos set); sup(dir)
+// gives the Minkowski support with both objects' points, c1 / c2 the centres
+template <typename Sup3>
+__device__ bool mpr_penetration_core(ccd_real tol, const CV3& c1, const CV3& c2, Sup3 msup, ccd_real& depth,
+                                     CV3& dir_out, CV3& pos_out) {
   SupP P[4];
-  P[0].v1 = center(w, A);
-  P[0].v2 = center(w, B);
+  P[0].v1 = c1;
+  P[0].v2 = c2;
   P[0].v = vsub(P[0].v1, P[0].v2);
   if (vec_is_origin(P[0].v)) P[0].v = vadd(P[0].v, cv3(kCcdEps * ccd_real(10), 0.0, 0.0));
   CV3 dir = vnormalize(vscale(P[0].v, ccd_real(-1)));
-  P[1] = msupport3(w, HV, A, B, dir);
+  P[1] = msup(dir);
   ccd_real dot = vdot(P[1].v, dir);
   if (is_zero(dot) || dot < 0.0) return false;
   dir = vcross(P[0].v, P[1].v);
@@ -2713,7 +2715,7 @@ __device__ bool mpr_penetration_ccd(const DevWorld& w, cptr<double> HV, const GO
     return true;
   }
   dir = vnormalize(dir);
-  P[2] = msupport3(w, HV, A, B, dir);
+  P[2] = msup(dir);
   dot = vdot(P[2].v, dir);
   if (is_zero(dot) || dot < 0.0) return false;
   dir = vnormalize(vcross(vsub(P[1].v, P[0].v), vsub(P[2].v, P[0].v)));
@@ -2724,7 +2726,7 @@ __device__ bool mpr_penetration_ccd(const DevWorld& w, cptr<double> HV, const GO
     dir = vscale(dir, ccd_real(-1));
   }
   for (;;) {
-    P[3] = msupport3(w, HV, A, B, dir);
+    P[3] = msup(dir);
     dot = vdot(P[3].v, dir);
     if (is_zero(dot) || dot < 0.0) return false;
     bool cont = false;
@@ -2748,16 +2750,16 @@ __device__ bool mpr_penetration_ccd(const DevWorld& w, cptr<double> HV, const GO
     dir = portal_dir3(P);
     const ccd_real d = vdot(dir, P[1].v);
     if (is_zero(d) || d > 0.0) break;
-    const SupP v4 = msupport3(w, HV, A, B, dir);
+    const SupP v4 = msup(dir);
     const ccd_real dv4 = vdot(v4.v, dir);
-    if (!(is_zero(dv4) || dv4 > 0.0) || reach_tol(P, v4.v, dir, w.mpr_tol)) return false;
+    if (!(is_zero(dv4) || dv4 > 0.0) || reach_tol(P, v4.v, dir, tol)) return false;
     expand3(P, v4);
   }
   // findPenetr
   for (unsigned long it = 0;; ++it) {
     dir = portal_dir3(P);
-    const SupP v4 = msupport3(w, HV, A, B, dir);
-    if (reach_tol(P, v4.v, dir, w.mpr_tol) || it > 500UL) {
+    const SupP v4 = msup(dir);
+    if (reach_tol(P, v4.v, dir, tol) || it > 500UL) {
       CV3 wit;
       depth = std::sqrt(tri_dist2(P[1].v, P[2].v, P[3].v, wit));
       dir_out = is_zero(depth) ? cv3(0.0, 0.0, 0.0) : vnormalize(wit);
@@ -2766,6 +2768,12 @@ __device__ bool mpr_penetration_ccd(const DevWorld& w, cptr<double> HV, const GO
     }
     expand3(P, v4);
   }
+}
+
+__device__ bool mpr_penetration_ccd(const DevWorld& w, cptr<double> HV, const GObj& A, const GObj& B, ccd_real& depth,
+                                    CV3& dir_out, CV3& pos_out) {
+  return mpr_penetration_core(w.mpr_tol, center(w, A), center(w, B),
+                              [&](const CV3& d) { return msupport3(w, HV, A, B, d); }, depth, dir_out, pos_out);
 }
 
 // FCL reads the contact back into fp64 (Contact<double>)
@@ -3276,9 +3284,99 @@ __device__ bool sphere_cylinder_contact(double r, const SE3& TS, double rc, doub
   return true;
 }
 
+// CollisionRequest(enable_contact=True) on a (shape, OcTree) pair
+// [ext FCL 0.7.0 OcTreeShapeIntersectRecurse with contacts]: the first
+// occupied leaf in traversal order (the leaf list's order) whose OBB
+// overlaps the shape's and whose box intersects it; its contact from
+// shapeIntersect(leaf box, shape): the tree is the contact's o1, the normal
+// points from the leaf into the shape (oracle octree_contact).  One lane
+// walks the whole leaf list: contacts are a scalar-API path.
+__device__ bool octree_first_contact(const DevWorld& w, cptr<double> HV, int go, const SE3& TO, int gs, const SE3& TS,
+                                     double& depth, V3& nd, V3& ps) {
+  const cptr<double> grs = w.geom_rec + G_STRIDE * gs;
+  const int ts = w.geom_type[gs];
+  double sc[3], se[3], Rl[9];
+  for (int i = 0; i < 3; ++i) se[i] = grs[G_AABB_E + i];
+  for (int i = 0; i < 3; ++i)
+    sc[i] = ((TS.R[3 * i] * grs[G_OBB_C] + TS.R[3 * i + 1] * grs[G_OBB_C + 1]) + TS.R[3 * i + 2] * grs[G_OBB_C + 2]) +
+            TS.p[i];
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) Rl[3 * i + j] = (TO.R[i] * TS.R[j] + TO.R[3 + i] * TS.R[3 + j]) + TO.R[6 + i] * TS.R[6 + j];
+  GObj B;
+  B.rot = gjk_rot_from_matrix(TS.R);
+  B.rot_inv = quat_invert2(B.rot);
+  B.pos = cv3(TS.p[0], TS.p[1], TS.p[2]);
+  B.geom = gs;
+  B.type = ts;
+  GObj A;
+  A.rot = gjk_rot_from_matrix(TO.R);
+  A.rot_inv = quat_invert2(A.rot);
+  A.geom = go;
+  A.type = MPG_GEOM_BOX;
+  const double sb[3] = {grs[G_PARAM], grs[G_PARAM + 1], grs[G_PARAM + 2]};
+  const cptr<double> gor = w.geom_rec + G_STRIDE * go;
+  const int l0 = (int)gor[G_PARAM], ln = (int)gor[G_PARAM + 1];
+  for (int l = l0; l < l0 + ln; ++l) {
+    const cptr<double> L = w.oct_leaf + 6 * (size_t)l;
+    double c[3], cw[3], a[3], side[3], t[3], T[3];
+    for (int i = 0; i < 3; ++i) {
+      c[i] = (L[i] + L[3 + i]) * 0.5;
+      side[i] = L[3 + i] - L[i];
+      a[i] = side[i] * 0.5;
+    }
+    for (int i = 0; i < 3; ++i) cw[i] = ((TO.R[3 * i] * c[0] + TO.R[3 * i + 1] * c[1]) + TO.R[3 * i + 2] * c[2]) + TO.p[i];
+    for (int i = 0; i < 3; ++i) t[i] = sc[i] - cw[i];
+    for (int i = 0; i < 3; ++i) T[i] = (TO.R[i] * t[0] + TO.R[3 + i] * t[1]) + TO.R[6 + i] * t[2];
+    if (obb_disjoint(Rl, T, a, se)) continue;
+    SE3 TL;
+    for (int i = 0; i < 9; ++i) TL.R[i] = TO.R[i];
+    for (int i = 0; i < 3; ++i) TL.p[i] = cw[i];
+    depth = 0.0;
+    nd = v3(0, 0, 0);
+    ps = v3(0, 0, 0);
+    bool hit;
+    if (ts == MPG_GEOM_BOX) {
+      hit = box_box_contact(side, TL, sb, TS, depth, nd, ps);
+    } else if (ts == MPG_GEOM_SPHERE) {
+      hit = sphere_box_contact(sb[0], TS, side, TL, depth, nd, ps);
+      nd = v3(-nd.x, -nd.y, -nd.z);  // flipNormal
+    } else {
+      GObj A1 = A;
+      A1.pos = cv3(cw[0], cw[1], cw[2]);
+      const ccd_real h[3] = {(ccd_real)(side[0] / 2.0), (ccd_real)(side[1] / 2.0), (ccd_real)(side[2] / 2.0)};
+      ccd_real dc = 0;
+      CV3 n{0, 0, 0}, pc{0, 0, 0};
+      hit = mpr_penetration_core(
+          w.mpr_tol, A1.pos, center(w, B),
+          [&](const CV3& d) {
+            SupP sp;
+            const CV3 da = quat_rot(d, A1.rot_inv);
+            const CV3 la = CV3{(da.x >= 0 ? ccd_real(1) : ccd_real(-1)) * h[0], (da.y >= 0 ? ccd_real(1) : ccd_real(-1)) * h[1],
+                               (da.z >= 0 ? ccd_real(1) : ccd_real(-1)) * h[2]};
+            sp.v1 = vadd(quat_rot(la, A1.rot), A1.pos);
+            sp.v2 = support(w, HV, B, vscale(d, ccd_real(-1)));
+            sp.v = vsub(sp.v1, sp.v2);
+            return sp;
+          },
+          dc, n, pc);
+      if (hit) {
+        depth = dc;
+        nd = to_v3(n);
+        ps = to_v3(pc);
+      }
+    }
+    if (hit) return true;
+  }
+  depth = 0.0;
+  nd = v3(0, 0, 0);
+  ps = v3(0, 0, 0);
+  return false;
+}
+
 __host__ __device__ __forceinline__ bool cf_has_contact(int cf) {
   return cf != CF_NONE && cf != CF_OCTREE && cf != CF_MESH;
 }
+__host__ __device__ __forceinline__ bool cf_contact_supported(int cf) { return cf != CF_MESH; }
 
 __device__ bool closed_form_contact(int cf, const DevWorld& w, int ga, const SE3& TA, int gb, const SE3& TB,
                                     double& depth, V3& nd, V3& ps) {
@@ -3332,7 +3430,11 @@ __global__ __launch_bounds__(256) void contact_kernel(DevWorld w, const double* 
       if (!((masks[c * w.W + (p >> 5)] >> (p & 31)) & 1u)) continue;
       double dp = 0.0;
       V3 nd{0, 0, 0}, ps{0, 0, 0};
-      if (cf_has_contact(w.pair_cf[p])) {
+      if (w.pair_cf[p] == CF_OCTREE) {  // the octree is the static side (b)
+        const SE3 TA = moving_tf<FROM_POSES>(w, in, sc, c, a);
+        const SE3 TB = load_se3(w.static_T + 12 * (b - w.n_moving));
+        octree_first_contact(w, HV, w.static_geom[b - w.n_moving], TB, w.moving_geom[a], TA, dp, nd, ps);
+      } else if (cf_has_contact(w.pair_cf[p])) {
         const SE3 TA = a < w.n_moving ? moving_tf<FROM_POSES>(w, in, sc, c, a) : load_se3(w.static_T + 12 * (a - w.n_moving));
         const SE3 TB = b < w.n_moving ? moving_tf<FROM_POSES>(w, in, sc, c, b) : load_se3(w.static_T + 12 * (b - w.n_moving));
         const int ga = a < w.n_moving ? w.moving_geom[a] : w.static_geom[a - w.n_moving];
@@ -4467,7 +4569,7 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
   dw.pair_cf = to_cptr<int>(base + o_cf);
   for (int p = 0; p < d->n_pairs; ++p) {
     w->has_closed_form |= pair_cf[p] != CF_NONE && !allowed[p];
-    w->has_contactless |= pair_cf[p] != CF_NONE && !cf_has_contact(pair_cf[p]) && !allowed[p];
+    w->has_contactless |= !cf_contact_supported(pair_cf[p]) && !allowed[p];
     w->has_octree |= pair_cf[p] == CF_OCTREE && !allowed[p];
     w->any_closed_form |= pair_cf[p] != CF_NONE && cf_class(pair_cf[p]) == CLS_CLOSED;
     w->any_octree |= pair_cf[p] == CF_OCTREE;
@@ -4922,7 +5024,7 @@ int mpg_collide_contacts(mpg_world* w, const double* input, int64_t n, int input
   if (mem != MPG_MEM_HOST && mem != MPG_MEM_DEVICE) return set_error(MPG_E_INVALID, "bad mem kind");
   if (w->has_contactless)
     return set_error(MPG_E_UNSUPPORTED,
-                     "contacts for octree and BVH mesh pairs are not implemented");
+                     "contacts for BVH mesh pairs are not implemented");
   if (n == 0) return MPG_OK;
   HIP_TRY(hipSetDevice(w->device));
   hipStream_t s = static_cast<hipStream_t>(stream);

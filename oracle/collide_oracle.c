@@ -1817,6 +1817,75 @@ static int octree_intersect(const orc_world *w, int go, const real *TO, int gs, 
     return 0;
 }
 
+/* CollisionRequest(enable_contact=True) on a (shape, OcTree) pair
+ * [ext FCL 0.7.0 OcTreeShapeIntersectRecurse with contacts]: the traversal
+ * stops at the first occupied leaf (children in order) whose OBB overlaps
+ * the shape's and whose box intersects it, and reports that leaf's contact
+ * from shapeIntersect(leaf box, box_tf, shape, tf): the tree is the
+ * contact's o1, so the normal points from the leaf box into the shape
+ * (box-box: boxBox2; box-sphere: sphereBox flipped; otherwise libccd MPR
+ * penetration with the box first). */
+static int octree_contact(const orc_world *w, int go, const real *TO, int gs, const real *TS, real *depth,
+                          real *normal, real *pos) {
+    const int l0 = (int)w->geom_param[4 * go], ln = (int)w->geom_param[4 * go + 1];
+    const int ts = w->geom_type[gs];
+    const real *ps = w->geom_param + 4 * gs;
+    real lo[3], hi[3];
+    if (ts == GEOM_CONVEX) {
+        const real *V = w->verts + 3 * (size_t)w->geom_vstart[gs];
+        for (int k = 0; k < 3; ++k) lo[k] = hi[k] = V[k];
+        for (int i = 1; i < w->geom_nv[gs]; ++i)
+            for (int k = 0; k < 3; ++k) {
+                if (V[3 * i + k] < lo[k]) lo[k] = V[3 * i + k];
+                if (V[3 * i + k] > hi[k]) hi[k] = V[3 * i + k];
+            }
+    } else if (ts == GEOM_BOX) {
+        for (int k = 0; k < 3; ++k) { hi[k] = 0.5 * ps[k]; lo[k] = -hi[k]; }
+    } else if (ts == GEOM_SPHERE) {
+        for (int k = 0; k < 3; ++k) { hi[k] = ps[0]; lo[k] = -hi[k]; }
+    } else {
+        const real r = ps[0], hz = 0.5 * ps[1] + (ts == GEOM_CAPSULE ? r : 0.0);
+        lo[0] = lo[1] = -r; hi[0] = hi[1] = r; lo[2] = -hz; hi[2] = hz;
+    }
+    real lc[3], se[3], sc[3], B[9];
+    for (int k = 0; k < 3; ++k) { lc[k] = (lo[k] + hi[k]) * 0.5; se[k] = (hi[k] - lo[k]) * 0.5; }
+    for (int i = 0; i < 3; ++i) sc[i] = ((TS[3 * i] * lc[0] + TS[3 * i + 1] * lc[1]) + TS[3 * i + 2] * lc[2]) + TS[9 + i];
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) B[3 * i + j] = (TO[i] * TS[j] + TO[3 + i] * TS[3 + j]) + TO[6 + i] * TS[6 + j];
+    gjk_obj shape;
+    int shape_ready = 0;
+    for (int l = l0; l < l0 + ln; ++l) {
+        const real *L = w->oct_leaf + 6 * (size_t)l;
+        real c[3], a[3], side[3], TL[12], t[3], T[3];
+        for (int k = 0; k < 3; ++k) { c[k] = (L[k] + L[3 + k]) * 0.5; side[k] = L[3 + k] - L[k]; a[k] = side[k] * 0.5; }
+        for (int k = 0; k < 9; ++k) TL[k] = TO[k];
+        for (int i = 0; i < 3; ++i) TL[9 + i] = ((TO[3 * i] * c[0] + TO[3 * i + 1] * c[1]) + TO[3 * i + 2] * c[2]) + TO[9 + i];
+        for (int i = 0; i < 3; ++i) t[i] = sc[i] - TL[9 + i];
+        for (int i = 0; i < 3; ++i) T[i] = (TO[i] * t[0] + TO[3 + i] * t[1]) + TO[6 + i] * t[2];
+        if (obb_disjoint(B, T, a, se)) continue;
+        int hit, nc = 0;
+        *depth = 0;
+        for (int i = 0; i < 3; ++i) normal[i] = pos[i] = 0;
+        if (ts == GEOM_BOX) hit = box_box_contact(side, TL, ps, TS, depth, normal, pos, &nc);
+        else if (ts == GEOM_SPHERE) {
+            hit = sphere_box_contact(ps[0], TS, side, TL, depth, normal, pos);
+            for (int i = 0; i < 3; ++i) normal[i] = -normal[i]; /* flipNormal */
+        } else {
+            if (!shape_ready) { make_obj(w, gs, TS, &shape, NULL); shape_ready = 1; }
+            gjk_obj box;
+            memset(&box, 0, sizeof box);
+            shape_to_gjk(TL, &box);
+            box.type = GEOM_BOX;
+            for (int k = 0; k < 3; ++k) box.dim[k] = side[k] / 2.0; /* boxToGJK */
+            hit = mpr_penetration(&box, &shape, 1e-6, depth, normal, pos);
+        }
+        if (hit) return 1;
+    }
+    *depth = 0;
+    for (int i = 0; i < 3; ++i) normal[i] = pos[i] = 0;
+    return 0;
+}
+
 /* ------------------------------------------------ BVH meshes
  * fcl::BVHModel<OBBRSS> (load_mesh_as_BVH, src/urdf_utils.cpp:136-155) in
  * fcl::collide [ext FCL 0.7.0]: the BVH traversal only prunes triangle pairs
@@ -2302,6 +2371,10 @@ int orc_contact_batch(const orc_world *w, const double *q, long n, uint8_t *hit,
             }
             const int cf = closed_form_contact(w, gs[0], Ts[0], gs[1], Ts[1], depth + k, normal + 3 * k, pos + 3 * k);
             if (cf >= 0) { hit[k] = (uint8_t)cf; continue; }
+            if (w->geom_type[gs[1]] == GEOM_OCTREE) {
+                hit[k] = (uint8_t)octree_contact(w, gs[1], Ts[1], gs[0], Ts[0], depth + k, normal + 3 * k, pos + 3 * k);
+                continue;
+            }
             for (int s = 0; s < 2; ++s) make_obj(w, gs[s], Ts[s], &o[s], NULL);
             hit[k] = (uint8_t)mpr_penetration(&o[0], &o[1], 1e-6, depth + k, normal + 3 * k, pos + 3 * k);
         }

@@ -698,8 +698,25 @@ def test_point_cloud_known_answers_and_unsupported_queries():
     assert len(hits) >= 2  # detect_collision.py: several joints dip below the floor
     w.set_qpos_all(Wd.KAT_FREE)
     assert w.collide_with_others() == []
-    with pytest.raises(NotImplementedError):
-        w.collide(pymp.fcl.CollisionRequest(enable_contact=True))
+    assert w.collide(pymp.fcl.CollisionRequest(enable_contact=True)) is False
+    assert w.collide_full(pymp.fcl.CollisionRequest(enable_contact=True)) == []
+
+
+@pytest.mark.parametrize("cloud", ["floor", "blue"])
+def test_point_cloud_contacts_match_oracle(cloud):
+    """enable_contact=True against a point cloud: the first leaf of the
+    traversal that intersects the shape gives the contact (leaf box first:
+    boxBox2 / sphereBox flipped / MPR penetration), the tree as the
+    contact's o1; equal to the oracle within 1e-9."""
+    w, art = scenes.cloud_world(cloud)
+    o = Wd.oracle_cloud_world(cloud)
+    q = scenes.sample_states(art, 4000, 98)
+    _, mo = o.collide_batch(q, nthreads=NTHREADS)
+    pc = [k for k, (a, b) in enumerate(o.pair_names()) if b == "scene_pcd"]
+    sel = np.nonzero(np.any(np.stack([(mo[:, k >> 5] >> (k & 31)) & 1 for k in pc], 1), 1))[0]
+    assert len(sel) >= 5
+    hit = _check_scalar_contacts(w, o, q[sel[:40]])
+    assert hit[:, pc].sum() >= 5
 
 
 @pytest.mark.parametrize("cloud,n", [("floor", 96), ("blue", 512)])
