@@ -458,3 +458,22 @@ def test_sphere_capsule_cylinder_contacts_known_answers():
     r, d2, n2, _ = _contact(w, cyl, _T(), small, _T(p=(0.07, 0.0, 0.0)))
     assert r == 1 and d2 == d
     np.testing.assert_array_equal(n2, -n)
+
+
+@pytest.mark.parametrize("cloud", ["blue"])
+def test_point_cloud_contact_batch_consistent_with_collide(cloud):
+    """The oracle's contact pass on a point-cloud world reports exactly the
+    pairs collide() reports: the first intersecting leaf (contact) exists
+    iff some leaf intersects (boolean), and its normal is a unit vector."""
+    o = Wd.oracle_cloud_world(cloud)
+    q = Wd.sample_q(o.art, 600, 8)
+    hit, depth, normal, pos = o.contact_batch(q)
+    _, masks = o.collide_batch(q)
+    P = len(o.pairs)
+    bits = np.stack([(masks[:, p >> 5] >> (p & 31)) & 1 for p in range(P)], 1)
+    np.testing.assert_array_equal(hit, bits)
+    pc = [k for k, (a, b) in enumerate(o.pair_names()) if b == "scene_pcd"]
+    h = hit[:, pc].astype(bool)
+    assert h.sum() > 0
+    nz = depth[:, pc][h] != 0
+    np.testing.assert_allclose(np.linalg.norm(normal[:, pc][h][nz], axis=1), 1.0, atol=1e-6)
