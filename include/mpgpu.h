@@ -207,6 +207,15 @@ int mpg_collide_batch(mpg_world *world, const double *q, int64_t n, uint8_t *fla
 int mpg_set_small_batch_max(mpg_world *world, int64_t n);
 
 /*
+ * Drops the device state the world keeps for one caller stream (its phase
+ * A/B workspace and the internal side stream of large batches).  Call before
+ * destroying a stream that was passed to MPG_MEM_DEVICE calls; without it the
+ * state of at most 32 streams is kept, least recently used evicted first.
+ * No reference counterpart (the reference has no device state).
+ */
+int mpg_release_stream(mpg_world *world, void *stream);
+
+/*
  * Same pair evaluation as mpg_collide_batch, but the link poses are given
  * directly instead of being computed from joint values:
  * link_pose [n*n_links*7] = (px, py, pz, qw, qx, qy, qz) per user link.

@@ -119,6 +119,10 @@ class DeviceWorld:
         """Host batches of at most n configurations take the one-launch latency path (0 disables)."""
         C.check(C.lib().mpg_set_small_batch_max(self._h, int(n)), "mpg_set_small_batch_max")
 
+    def release_stream(self, stream: int):
+        """Drop the workspace / side stream kept for a caller stream (call before destroying it)."""
+        C.check(C.lib().mpg_release_stream(self._h, ctypes.c_void_p(int(stream))), "mpg_release_stream")
+
     # ------------------------------------------------------------------
     def collide_batch(self, q, flags=None, pair_mask=None, stream: Optional[int] = None):
         """Host path (numpy): returns (flags[n] u8, pair_mask[n, W] u32).

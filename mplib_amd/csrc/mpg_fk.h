@@ -29,6 +29,17 @@ struct DevWorld {
   double small_margin;  // the latency path's bounding-sphere margin, same rule
   int debug_mode;  // diagnostics only: 1 = broad-phase records only, 2 = no SAT stage, 3 = no MPR (latency path: no narrow test), 5 / 6 = no mesh-mesh / mesh-shape walks, 7 = latency path: FK + sphere test only
   unsigned long long* stats;  // diagnostics only (MPG_STATS=1), else NULL
+  // the ablation switch as the kernels read it: compiled in only under the
+  // MPG_DIAG macro (tools/ablate*.sh build such a library); the product
+  // library ignores MPG_DEBUG_CULL entirely, so no result can change
+  __host__ __device__ __forceinline__ bool dbg(int k) const {
+#ifdef MPG_DIAG
+    return debug_mode == k;
+#else
+    (void)k;
+    return false;
+#endif
+  }
   cptr<int> joint_type;      // [nj]
   cptr<int> joint_parent;    // [nj]
   cptr<int> joint_q_source;  // [nj]

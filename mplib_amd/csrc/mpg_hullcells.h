@@ -243,7 +243,18 @@ MPG_INLINE void cell_record_support(PD R, PD ovf, double x, double y, double z, 
 // the topology is valid (every vertex in some face, every edge in exactly two
 // faces).  Faces must index [0, nv) (the descriptor validation checks).
 constexpr int kMinVertCountForEdgeWalking = 32;
-constexpr int kMaxWalkVerts = 512;  // device visited mask (convex_walk)
+// Device visited mask of the climb (wave_walk, one LDS set per wave): walk
+// hulls up to kMaxWalkVerts vertices.  Direction tables (build_walk_cells)
+// are built for hulls up to kMaxCellWalkVerts (their host build is
+// O(cells * nv^2)); larger walk hulls climb from vertex 0 on every support,
+// exact and slower.
+constexpr int kMaxWalkVerts = 4096;
+constexpr int kMaxCellWalkVerts = 512;
+// record slot 9 packs the linear list's length n (n <= nv <= kMaxCellWalkVerts)
+// and its overflow offset: n + kCellCountMul * offset
+constexpr int kCellCountBits = 12;
+constexpr double kCellCountMul = (double)(1 << kCellCountBits);
+static_assert(kMaxCellWalkVerts < (1 << kCellCountBits), "walk-cell list length must fit its field");
 inline bool fcl_convex_neighbors(int nv, const int32_t* faces, int num_faces, std::vector<int>& out) {
   std::vector<std::vector<int>> nb(nv);
   std::vector<std::pair<int, int>> edges;
@@ -297,7 +308,7 @@ inline bool fcl_convex_neighbors(int nv, const int32_t* faces, int num_faces, st
 // Record layout (kCellRec doubles, like the linear hulls' records): three
 // linear-list entries inline (x, y, z; short lists padded with their first
 // entry), then
-//   slot 9   n + 256 * (overflow offset, entries of 4 doubles x, y, z, 0),
+//   slot 9   n + kCellCountMul * (overflow offset, entries of 4 doubles x, y, z, 0),
 //   slot 10  0, or k + 1: the trapped cell's data at aux entry k (kWalkAux
 //            doubles each): a header (the index of its first endpoint table
 //            in ends: one table of kSub2K x kSub2K fine-cell endpoints, vertex
@@ -420,10 +431,10 @@ inline void walk_cone_list(const double* V, int nv, const int* nbr, int f, doubl
 // scanned, the undecided entry's index k in that list, whether the pass had
 // moved before it, and the visited set at that point.  The device resumes the
 // climb there (wave_walk) instead of from vertex 0.
-constexpr int kWalkPre = 4 + 2 * (kMaxWalkVerts / 64);  // ints per record
+constexpr int kWalkPre = 4 + 2 * (kMaxCellWalkVerts / 64);  // ints per record
 struct WalkPrefix {
   int bi, pv, k, keep;
-  uint64_t vis[kMaxWalkVerts / 64];
+  uint64_t vis[kMaxCellWalkVerts / 64];
 };
 
 inline int walk_cone_endpoint(const double* V, int nv, const int* nbr, int f, double sg, double u0, double u1,
@@ -531,7 +542,8 @@ inline bool build_walk_cells(const double* V, int nv, const int* nbr, int subk, 
                              std::vector<int>& ends2, std::vector<int>& pres) {
   double X = 0.0;
   for (int i = 0; i < 3 * nv; ++i) X = std::max(X, std::fabs(V[i]));
-  if (nv <= 0 || !(X >= kHullMin && X <= kHullMax) || subk < 1 || subk * subk > 64) return false;
+  if (nv <= 0 || nv > kMaxCellWalkVerts || !(X >= kHullMin && X <= kHullMax) || subk < 1 || subk * subk > 64)
+    return false;
   std::vector<uint32_t> lstart;
   std::vector<double> lpts;
   if (!build_hull_cells(V, nv, lstart, lpts)) return false;
@@ -567,7 +579,8 @@ inline bool build_walk_cells(const double* V, int nv, const int* nbr, int subk, 
             const uint32_t e = l0 + (k < (int)n ? k : 0);
             for (int j = 0; j < 3; ++j) rec[r0 + 3 * k + j] = lpts[4 * e + j];
           }
-          rec[r0 + 9] = (double)n + 256.0 * (double)(ovf.size() / 4);
+          if (n > (uint32_t)kMaxCellWalkVerts) return false;  // cannot happen: n <= nv
+          rec[r0 + 9] = (double)n + kCellCountMul * (double)(ovf.size() / 4);
           for (uint32_t e = l0 + kCellInline; e < l0 + n; ++e)
             for (int j = 0; j < 4; ++j) ovf.push_back(lpts[4 * e + j]);
           if (free_mask != ~0ull) {
@@ -598,7 +611,7 @@ inline bool build_walk_cells(const double* V, int nv, const int* nbr, int subk, 
                           if (e2 < 0) {  // still undecided: where the climb can resume
                             e2 = -2 - (int)(pres.size() / kWalkPre);
                             pres.insert(pres.end(), {pre.bi, pre.pv, pre.k, pre.keep});
-                            for (int j = 0; j < kMaxWalkVerts / 64; ++j) {
+                            for (int j = 0; j < kMaxCellWalkVerts / 64; ++j) {
                               pres.push_back((int)(uint32_t)pre.vis[j]);
                               pres.push_back((int)(uint32_t)(pre.vis[j] >> 32));
                             }

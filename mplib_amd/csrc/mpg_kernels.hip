@@ -227,8 +227,8 @@ __device__ __forceinline__ bool neighbour_beats(const DevWorld& w, cptr<double> 
 __device__ __forceinline__ V3 walk_cell_fast(const DevWorld& w, cptr<double> HV, int geom, cptr<double> R, int sub,
                                              int fine, int fine2, const V3& d, bool& pend, int& pre) {
   const long long no = (long long)R[9];
-  const int n = (int)(no & 255);
-  const cptr<double> ovf = w.wcell_ovf + 4 * (size_t)(no >> 8);
+  const int n = (int)(no & ((1 << kCellCountBits) - 1));
+  const cptr<double> ovf = w.wcell_ovf + 4 * (size_t)(no >> kCellCountBits);
   // first maximum (strict '>', as the reference's scan) ...
   double best = -DBL_MAX;
   int g = 0;
@@ -963,7 +963,7 @@ __global__ __launch_bounds__(BLOCK) void cull_kernel(DevWorld w, const double* _
   } else {
     bp_fk(w.bp, in + c * w.dof, save + tid, BLOCK, put);
   }
-  if (w.debug_mode == 1) {
+  if (w.dbg(1)) {
     if (live && cen[tid] == 12345.f) flags[cfg] = 2;  // keep the records alive
     return;
   }
@@ -996,7 +996,7 @@ __global__ __launch_bounds__(BLOCK) void cull_kernel(DevWorld w, const double* _
         kb |= (uint32_t)keep << (e - eb);
       }
       if (!live) kb = 0u;
-      if (w.debug_mode == 2) {
+      if (w.dbg(2)) {
         for (int e = eb; e < ee; ++e) {
           const int p = w.sched_pair[e];
           if ((kb >> (e - eb)) & 1u) survw[(p >> 5) * BLOCK + tid] |= 1u << (p & 31);
@@ -1027,7 +1027,7 @@ __global__ __launch_bounds__(BLOCK) void cull_kernel(DevWorld w, const double* _
     }
   }
   if (tail != head) sat_drain<BLOCK>(w, cen, rq, cap, cfg0, survw, queue, head, tail - head, wbase, lane);
-  if (w.debug_mode == 8) {  // ablation: bounding tests + SAT only
+  if (w.dbg(8)) {  // ablation: bounding tests + SAT only
     if (live && survw[tid] == 12345u) flags[cfg] = 2;
     return;
   }
@@ -1051,7 +1051,7 @@ __global__ __launch_bounds__(BLOCK) void cull_kernel(DevWorld w, const double* _
       if (lane == 0) cnt[(long long)(k * 32 + b) * n_tiles + tile] = (uint32_t)__popcll(bb);
     }
   }
-  if (FROM_POSES || w.debug_mode == 9) return;  // 9: ablation without the sincos pass
+  if (FROM_POSES || w.dbg(9)) return;  // 9: ablation without the sincos pass
   // Exact fp64 sin/cos of every revolute move-group joint for the narrow
   // phase's chain FK (the glibc sincos restatement), only for configurations
   // with a candidate pair (about a quarter of them): compacted across the
@@ -1964,7 +1964,7 @@ __device__ __forceinline__ unsigned long long walk_wave_eval(const DevWorld& w, 
       const int k = __builtin_ctzll(todo);
       todo &= todo - 1;
       const SE3 A = bcast_se3(TA, k), B = bcast_se3(TB, k);
-      if (w.debug_mode == (am && bm ? 5 : 6)) continue;
+      if (w.dbg(am && bm ? 5 : 6)) continue;
       bool h;
       if (am && bm) h = mesh_mesh_wave(w, ga, A, gb, B);
       else if (am) h = mesh_shape_wave(w, HV, ga, A, gb, B);
@@ -2168,7 +2168,7 @@ __global__ __launch_bounds__(256) void small_kernel(DevWorld w, const double* __
       d2 += (ci - cj) * (ci - cj);
     }
     const double rr = ra[G_RADIUS] + rb[G_RADIUS] + w.small_margin;
-    const bool near = live && d2 <= rr * rr && w.debug_mode != 3 && !(w.debug_mode == 7 && d2 >= 0.0);
+    const bool near = live && d2 <= rr * rr && !w.dbg(3) && !(w.dbg(7) && d2 >= 0.0);
     if (CLS != CLS_CLOSED) {
       hit = (walk_wave_eval<CLS>(w, HV, ga, TA, gb, TB, near) >> lane) & 1ull;
     } else if (cf != CF_NONE) {
@@ -2543,10 +2543,12 @@ __global__ __launch_bounds__(128) void distance_kernel(DevWorld w, const double*
     const GObj A = pose_obj(w, poses, n, cfg, a, ca);
     const GObj B = pose_obj(w, poses, n, cfg, b, cb);
     const double ra = w.geom_rec[G_STRIDE * A.geom + G_RADIUS], rb = w.geom_rec[G_STRIDE * B.geom + G_RADIUS];
-    if (w.pair_cf[p] == CF_OCTREE) {  // the octree is the pair's static side (b)
+    if (w.pair_cf[p] == CF_OCTREE) {  // the octree is the pair's static side (b, or a through the C ABI)
       if (!live || best[g] == -1.0) continue;
-      const SE3 TO = load_se3(w.static_T + 12 * (b - w.n_moving));
-      const double d = octree_distance(w, HV, B.geom, TO, A, ca, ra, best[g]);
+      const bool oa = A.type == MPG_GEOM_OCTREE;  // distance is symmetric: leaf box first either way
+      const SE3 TO = load_se3(w.static_T + 12 * ((oa ? a : b) - w.n_moving));
+      const double d = oa ? octree_distance(w, HV, A.geom, TO, B, cb, rb, best[g])
+                          : octree_distance(w, HV, B.geom, TO, A, ca, ra, best[g]);
       if (d < best[g]) {
         best[g] = d;
         bp[g] = p;
@@ -3587,6 +3589,7 @@ struct mpg_world {
     float* rq = nullptr;            // [n_moving * 4 * cap] phase-A rotations for the SAT stage
     double* sc = nullptr;           // [cap * dof * 2] exact joint (sin, cos) for phase B
     long long cap = 0;
+    uint64_t last = 0;              // LRU tick (get_workspace)
   };
   std::mutex ws_mu;
   std::map<hipStream_t, Workspace> ws;
@@ -3614,6 +3617,7 @@ struct mpg_world {
   bool has_closed_form = false;  // a non-allowed pair uses an FCL closed form
   bool has_contactless = false;  // a non-allowed pair whose contacts the device does not compute
   bool has_octree = false;       // a non-allowed pair involves an octree
+  bool octree_first = false;     // a non-allowed pair has its octree as o1 (C ABI only; pymp puts it second)
   bool any_closed_form = false;  // some pair (allowed or not) does, octrees aside
   bool any_octree = false;       // some pair involves an octree
   bool has_mesh = false;         // a non-allowed pair involves a BVH mesh
@@ -3648,8 +3652,14 @@ struct mpg_world {
   struct Side {
     hipStream_t side;
     hipEvent_t fork, join;
+    uint64_t last;
   };
   std::map<hipStream_t, Side> sides;  // guarded by ws_mu
+  // per-stream state (workspaces, side streams) is kept for at most
+  // kMaxStreamState caller streams, least recently used evicted first;
+  // mpg_release_stream drops one explicitly
+  static constexpr size_t kMaxStreamState = 32;
+  uint64_t ws_tick = 0;
   // small-batch latency path (host buffers, n <= small_max): pinned input
   // staging + host-mapped hit bytes written by small_kernel
   long long small_max = 1024;
@@ -3954,16 +3964,75 @@ int choose_block(size_t per_thread, size_t* lds) {
   return best;
 }
 
+void free_workspace(mpg_world::Workspace& ws) {
+  for (uint32_t* p : {ws.surv, ws.cnt, ws.seg_len, ws.seg_start, ws.prefix, ws.cand})
+    if (p) hipFree(p);
+  if (ws.rq) hipFree(ws.rq);
+  if (ws.sc) hipFree(ws.sc);
+  ws = mpg_world::Workspace{};
+}
+
+// drops the state kept for caller stream s (its workspace, its side stream
+// and the side stream's workspace); the device is synchronised first, so no
+// queued kernel still uses the buffers.  Caller holds ws_mu.
+void release_stream_locked(mpg_world* w, hipStream_t s) {
+  const auto wi = w->ws.find(s);
+  const auto si = w->sides.find(s);
+  if (wi == w->ws.end() && si == w->sides.end()) return;
+  hipDeviceSynchronize();
+  if (wi != w->ws.end()) {
+    free_workspace(wi->second);
+    w->ws.erase(wi);
+  }
+  if (si != w->sides.end()) {
+    const auto sw = w->ws.find(si->second.side);
+    if (sw != w->ws.end()) {
+      free_workspace(sw->second);
+      w->ws.erase(sw);
+    }
+    hipStreamDestroy(si->second.side);
+    hipEventDestroy(si->second.fork);
+    hipEventDestroy(si->second.join);
+    w->sides.erase(si);
+  }
+}
+
+// evicts the least recently used caller stream's state when a new stream
+// would exceed kMaxStreamState (side-stream workspaces are owned by their
+// caller stream's entry).  Caller holds ws_mu.
+void evict_streams_locked(mpg_world* w) {
+  std::map<hipStream_t, uint64_t> callers;
+  for (auto& kv : w->ws) callers[kv.first] = kv.second.last;
+  for (auto& kv : w->sides) {
+    callers.erase(kv.second.side);
+    uint64_t& t = callers[kv.first];
+    t = std::max(t, kv.second.last);
+  }
+  while (callers.size() >= mpg_world::kMaxStreamState) {
+    auto lru = callers.begin();
+    for (auto it = callers.begin(); it != callers.end(); ++it)
+      if (it->second < lru->second) lru = it;
+    release_stream_locked(w, lru->first);
+    callers.erase(lru);
+  }
+}
+
+bool is_side_stream_locked(const mpg_world* w, hipStream_t s) {
+  for (auto& kv : w->sides)
+    if (kv.second.side == s) return true;
+  return false;
+}
+
 int get_workspace(mpg_world* w, hipStream_t s, long long want, mpg_world::Workspace** out) {
   std::lock_guard<std::mutex> lk(w->ws_mu);
+  if (w->ws.find(s) == w->ws.end() && !is_side_stream_locked(w, s) && w->sides.find(s) == w->sides.end())
+    evict_streams_locked(w);
   auto& ws = w->ws[s];
+  ws.last = ++w->ws_tick;
   const long long np = std::max(w->dw.n_pairs, 1);
   if (ws.cap < want) {
-    for (uint32_t* p : {ws.surv, ws.cnt, ws.seg_len, ws.seg_start, ws.prefix, ws.cand})
-      if (p) HIP_TRY(hipFree(p));
-    if (ws.rq) HIP_TRY(hipFree(ws.rq));
-    if (ws.sc) HIP_TRY(hipFree(ws.sc));
-    ws = mpg_world::Workspace{};
+    free_workspace(ws);
+    ws.last = w->ws_tick;
     const long long tiles = (want + 63) / 64;
     HIP_TRY(hipMalloc(&ws.surv, sizeof(uint32_t) * w->dw.W * want));
     HIP_TRY(hipMalloc(&ws.cnt, sizeof(uint32_t) * np * tiles));
@@ -4229,12 +4298,15 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
     // FCL 0.7.0 Convex: neighbour walk for > 32 vertices with valid faces
     std::vector<int> enc;
     const int nf = (int)d->geom_param[4 * g + 1];
-    const bool walk = nf > 0 && fcl_convex_neighbors(nvg, d->convex_face + (int64_t)d->geom_param[4 * g], nf, enc) &&
-                      !std::getenv("MPG_DEBUG_NO_WALK");  // ablation only: changes results
+    bool walk = nf > 0 && fcl_convex_neighbors(nvg, d->convex_face + (int64_t)d->geom_param[4 * g], nf, enc);
+#ifdef MPG_DIAG  // ablation builds only (changes results)
+    if (std::getenv("MPG_DEBUG_NO_WALK")) walk = false;
+#endif
     if (walk) {
       if (nvg > kMaxWalkVerts)
-        return set_error(MPG_E_UNSUPPORTED, "convex hull with more than 512 vertices and watertight faces "
-                                            "(FCL's neighbour-walk support) is not supported on the device");
+        return set_error(MPG_E_UNSUPPORTED, "convex hull with more than " + std::to_string(kMaxWalkVerts) +
+                                                " vertices and watertight faces (FCL's neighbour-walk support) "
+                                                "is not supported on the device");
       geom_nbr[g] = (int)(hull_nbr.size() / 2);
       for (int i = 0; i < nvg; ++i) {
         const int st = enc[i], cnt = enc[st];
@@ -4519,12 +4591,17 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
     const double X = std::max(reach_x + off, stat_x) + geo_r;
     dw.bp_margin = std::max(dw.bp_margin, (float)(kFp32CullRel * X));
     dw.small_margin = may_mpr ? std::max(kSmallMargin, reach) : kSmallMargin;
-    if (const char* m = std::getenv("MPG_DEBUG_MARGIN")) {  // ablation only: changes results
+#ifdef MPG_DIAG  // ablation builds only (changes results)
+    if (const char* m = std::getenv("MPG_DEBUG_MARGIN")) {
       dw.bp_margin = (float)std::atof(m);
       dw.small_margin = std::atof(m);
     }
+#endif
   }
-  dw.debug_mode = std::getenv("MPG_DEBUG_CULL") ? std::atoi(std::getenv("MPG_DEBUG_CULL")) : 0;
+  dw.debug_mode = 0;
+#ifdef MPG_DIAG  // ablation builds only (changes results)
+  if (const char* e = std::getenv("MPG_DEBUG_CULL")) dw.debug_mode = std::atoi(e);
+#endif
   dw.stats = nullptr;
   if (std::getenv("MPG_STATS") && std::atoi(std::getenv("MPG_STATS")) > 0) {
     HIP_TRY(hipMalloc(&dw.stats, 24 * sizeof(unsigned long long)));
@@ -4571,6 +4648,7 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
     w->has_closed_form |= pair_cf[p] != CF_NONE && !allowed[p];
     w->has_contactless |= !cf_contact_supported(pair_cf[p]) && !allowed[p];
     w->has_octree |= pair_cf[p] == CF_OCTREE && !allowed[p];
+    w->octree_first |= pair_cf[p] == CF_OCTREE && !allowed[p] && obj_geom_type(d, d->pair_a[p]) == MPG_GEOM_OCTREE;
     w->any_closed_form |= pair_cf[p] != CF_NONE && cf_class(pair_cf[p]) == CLS_CLOSED;
     w->any_octree |= pair_cf[p] == CF_OCTREE;
     w->has_mesh |= pair_cf[p] == CF_MESH && !allowed[p];
@@ -4808,12 +4886,14 @@ int launch_collide_overlapped(mpg_world* w, const double* in, long long n, uint8
     std::lock_guard<std::mutex> lk(w->ws_mu);
     auto it = w->sides.find(s);
     if (it == w->sides.end()) {
+      if (w->ws.find(s) == w->ws.end()) evict_streams_locked(w);
       mpg_world::Side n{};
       HIP_TRY(hipStreamCreateWithFlags(&n.side, hipStreamNonBlocking));
       HIP_TRY(hipEventCreateWithFlags(&n.fork, hipEventDisableTiming));
       HIP_TRY(hipEventCreateWithFlags(&n.join, hipEventDisableTiming));
       it = w->sides.emplace(s, n).first;
     }
+    it->second.last = ++w->ws_tick;
     sd = it->second;
   }
   const size_t row = FROM_POSES ? (size_t)w->dw.n_links * 7 : (size_t)w->dw.dof;
@@ -4863,6 +4943,14 @@ int collide_common(mpg_world* w, const double* q, int64_t n, uint8_t* flags, uin
 }  // namespace
 
 extern "C" {
+
+int mpg_release_stream(mpg_world* w, void* stream) {
+  if (!w) return set_error(MPG_E_INVALID, "world is NULL");
+  HIP_TRY(hipSetDevice(w->device));
+  std::lock_guard<std::mutex> lk(w->ws_mu);
+  release_stream_locked(w, static_cast<hipStream_t>(stream));
+  return MPG_OK;
+}
 
 int mpg_set_small_batch_max(mpg_world* w, int64_t n) {
   if (!w) return set_error(MPG_E_INVALID, "world is NULL");
@@ -5025,6 +5113,8 @@ int mpg_collide_contacts(mpg_world* w, const double* input, int64_t n, int input
   if (w->has_contactless)
     return set_error(MPG_E_UNSUPPORTED,
                      "contacts for BVH mesh pairs are not implemented");
+  if (w->octree_first)  // contact_kernel reports the (shape, octree) order PlanningWorld uses
+    return set_error(MPG_E_UNSUPPORTED, "contacts for a pair whose first object is an OcTree are not implemented");
   if (n == 0) return MPG_OK;
   HIP_TRY(hipSetDevice(w->device));
   hipStream_t s = static_cast<hipStream_t>(stream);
@@ -5118,21 +5208,30 @@ int mpg_debug_collide_pairs(mpg_world* w, int32_t geom_a, int32_t geom_b, int64_
   if ((cf == CF_OCTREE && ta == tb) || (cf == CF_MESH && (ta == MPG_GEOM_OCTREE || tb == MPG_GEOM_OCTREE)))
     return set_error(MPG_E_UNSUPPORTED, "geometry pair not supported");
   HIP_TRY(hipSetDevice(w->device));
-  double *dA = nullptr, *dB = nullptr;
-  uint8_t* dh = nullptr;
-  HIP_TRY(hipMalloc(&dA, sizeof(double) * 12 * n));
-  HIP_TRY(hipMalloc(&dB, sizeof(double) * 12 * n));
-  HIP_TRY(hipMalloc(&dh, (size_t)n));
-  HIP_TRY(hipMemcpy(dA, Ta, sizeof(double) * 12 * n, hipMemcpyHostToDevice));
-  HIP_TRY(hipMemcpy(dB, Tb, sizeof(double) * 12 * n, hipMemcpyHostToDevice));
+  struct Guard {  // every exit path frees the buffers and the private stream
+    double *dA = nullptr, *dB = nullptr;
+    uint8_t* dh = nullptr;
+    hipStream_t s = nullptr;
+    ~Guard() {
+      if (s) hipStreamSynchronize(s);
+      hipFree(dA);
+      hipFree(dB);
+      hipFree(dh);
+      if (s) hipStreamDestroy(s);
+    }
+  } g;
+  HIP_TRY(hipStreamCreateWithFlags(&g.s, hipStreamNonBlocking));
+  HIP_TRY(hipMalloc(&g.dA, sizeof(double) * 12 * n));
+  HIP_TRY(hipMalloc(&g.dB, sizeof(double) * 12 * n));
+  HIP_TRY(hipMalloc(&g.dh, (size_t)n));
+  HIP_TRY(hipMemcpyAsync(g.dA, Ta, sizeof(double) * 12 * n, hipMemcpyHostToDevice, g.s));
+  HIP_TRY(hipMemcpyAsync(g.dB, Tb, sizeof(double) * 12 * n, hipMemcpyHostToDevice, g.s));
   // (walk_wave_eval finds the octree / mesh argument itself)
-  hipLaunchKernelGGL(debug_pairs_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, 0, w->dw, geom_a, geom_b, cf,
-                     (long long)n, dA, dB, dh);
+  hipLaunchKernelGGL(debug_pairs_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, g.s, w->dw, geom_a, geom_b, cf,
+                     (long long)n, g.dA, g.dB, g.dh);
   HIP_TRY(hipGetLastError());
-  HIP_TRY(hipMemcpy(hit, dh, (size_t)n, hipMemcpyDeviceToHost));
-  hipFree(dA);
-  hipFree(dB);
-  hipFree(dh);
+  HIP_TRY(hipMemcpyAsync(hit, g.dh, (size_t)n, hipMemcpyDeviceToHost, g.s));
+  HIP_TRY(hipStreamSynchronize(g.s));
   return MPG_OK;
 }
 

@@ -464,8 +464,9 @@ static void support_convex(const gjk_obj *c, const ccd_vec3_t *dir_, ccd_vec3_t 
      * planes), so the climb can stop at a local maximum: a different support
      * point than the linear scan (ORC_FCL_LINEAR variant) for ~1e-4 of
      * directions. */
-    if (c->nbr && c->nv > 32 && c->nv <= 4096) {
-        unsigned char visited[4096];
+    if (c->nbr && c->nv > 32) {
+        unsigned char stack_vis[4096];
+        unsigned char *visited = c->nv <= 4096 ? stack_vis : (unsigned char *)malloc((size_t)c->nv);
         memset(visited, 0, (size_t)c->nv);
         maxdot = (dC[0] * p[0] + dC[1] * p[1]) + dC[2] * p[2];
         visited[0] = 1;
@@ -481,6 +482,7 @@ static void support_convex(const gjk_obj *c, const ccd_vec3_t *dir_, ccd_vec3_t 
                 if (d >= maxdot) { keep = 1; best = vi; maxdot = d; }
             }
         }
+        if (visited != stack_vis) free(visited);
         if (c->stats) c->stats->vertex_dots += c->nv;
         ccdVec3Set(v, p[3 * best], p[3 * best + 1], p[3 * best + 2]);
         ccdQuatRotVec(v, &c->rot);

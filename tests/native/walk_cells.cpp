@@ -71,8 +71,8 @@ int walk_cells_check(const double* V, int nv, const int* faces, int nf, const do
     if (c >= 0) {
       const double* R = rec.data() + kCellRec * (size_t)c;
       const long long no = (long long)R[9];
-      const int cnt = (int)(no & 255);
-      const double* O = ovf.data() + 4 * (size_t)(no >> 8);
+      const int cnt = (int)(no & ((1 << mpg::kCellCountBits) - 1));
+      const double* O = ovf.data() + 4 * (size_t)(no >> mpg::kCellCountBits);
       auto entry = [&](int k) { return k < kCellInline ? R + 3 * k : O + 4 * (k - kCellInline); };
       for (int j = 0; j < 4; ++j) st[8 + j] += cnt > 3 + j;  // list lengths
       double best = -DBL_MAX;

@@ -91,3 +91,23 @@ def test_capsule_pairs_accepted():
         raise
     except RuntimeError:
         pass  # validation passed; without a device the creation stops at hipSetDevice
+
+
+def test_result_changing_switches_only_in_diag_builds():
+    """every getenv of a switch that can change an output bit
+    (MPG_DEBUG_*) sits inside an `#ifdef MPG_DIAG` block, and the device-side
+    ablation checks go through DevWorld::dbg(), which is constant false
+    without that macro."""
+    src = open(os.path.join(ROOT, "mplib_amd", "csrc", "mpg_kernels.hip")).read().splitlines()
+    depth, diag = 0, []
+    for ln in src:
+        s = ln.strip()
+        if s.startswith("#if"):
+            diag.append("MPG_DIAG" in s)
+        elif s.startswith("#endif"):
+            diag.pop()
+        elif "getenv(\"MPG_DEBUG" in s:
+            assert any(diag), ln
+        assert "debug_mode ==" not in s, ln
+    hdr = open(os.path.join(ROOT, "mplib_amd", "csrc", "mpg_fk.h")).read()
+    assert "#ifdef MPG_DIAG\n    return debug_mode == k;" in hdr

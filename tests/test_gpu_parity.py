@@ -70,6 +70,21 @@ def test_fk_bit_exact(golden_dir):
     np.testing.assert_array_equal(dw(2).fk_batch(q), ow(2).fk_batch(q)[0])
 
 
+def test_debug_switches_do_not_change_results(monkeypatch):
+    """The product library ignores the ablation switches (compiled in only
+    under MPG_DIAG): a world created with them set still matches the oracle."""
+    monkeypatch.setenv("MPG_DEBUG_CULL", "1")
+    monkeypatch.setenv("MPG_DEBUG_MARGIN", "0")
+    monkeypatch.setenv("MPG_DEBUG_NO_WALK", "1")
+    d = DeviceWorld(Wd.desc_arrays(ow(3)))
+    for n in (200, 20000):  # latency path and pipeline
+        q = Wd.sample_q(ow(3).art, n, 4242 + n)
+        f, m = d.collide_batch(q)
+        fo, mo = ow(3).collide_batch(q, nthreads=NTHREADS)
+        np.testing.assert_array_equal(f, fo)
+        np.testing.assert_array_equal(m, mo)
+
+
 @pytest.mark.parametrize("n", [0, 1, 2, 63, 64, 65, 127, 129, 1000])
 def test_ragged_batch_sizes(n):
     q = Wd.sample_q(ow(3).art, max(n, 1), 100 + n)[:n]
@@ -813,3 +828,19 @@ def test_capsule_cylinder_worlds_match_oracle():
     for pair in [("orb", "cap0"), ("orb", "cyl2"), ("rod", "ball4"), ("rod", "cap0")]:
         assert hit[:, names.index(pair)].sum() > 0, pair
     assert int(hit.sum()) > 0
+
+
+def test_big_walk_hulls_match_oracle():
+    """a 302-vertex cone (cell lists of ~300 rim vertices) and a
+    770-vertex sphere (above the 512-vertex direction-table limit: every
+    support climbs) as FCL neighbour-walk obstacles -- both batch paths, every
+    flag and pair bit vs the oracle."""
+    o = Wd.big_hull_world()
+    d = DeviceWorld(Wd.desc_arrays(o))
+    for n in (300, 1 << 14):
+        q = Wd.sample_q(o.art, n, 31 + n)
+        f, m = d.collide_batch(q)
+        fo, mo = o.collide_batch(q, nthreads=NTHREADS)
+        assert fo.mean() > 0.05
+        np.testing.assert_array_equal(f, fo)
+        np.testing.assert_array_equal(m, mo)

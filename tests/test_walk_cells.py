@@ -58,3 +58,14 @@ def test_walk_pending_share_small():
     assert tot[5] == 0
     assert tot[3] < 1e-3 * tot[0], tot  # certified fine cells settle the trapped subcells
     assert tot[6] < 0.15 * tot[7], tot  # most trapped fine cells have a certified endpoint
+
+
+def test_cone_with_long_cell_lists():
+    """a cone's base keeps ~300 rim vertices in one cell list; the
+    record's count field must hold it (was n + 256 * offset)."""
+    g = Wd.cone_hull(300)
+    rng = np.random.default_rng(3)
+    d = np.vstack([rng.standard_normal((20000, 3)), np.array([[0.0, 0.0, -1.0], [1e-3, 2e-3, -1.0]]),
+                   rng.standard_normal((5000, 3)) * [0.05, 0.05, 1.0] - [0, 0, 2.0]])
+    st = check(g, d.astype(np.float32).astype(np.float64))
+    assert st[5] == 0, f"{st[5]} of {st[0]} directions disagree with the walk"

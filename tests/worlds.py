@@ -233,3 +233,50 @@ def collide_pair(ow: oracle.OracleWorld, ga: int, Ta, gb: int, Tb) -> bool:
     b = np.ascontiguousarray(oracle._se3_flat(Tb), dtype=np.float64)
     return bool(oracle.lib().orc_collide_pair(ctypes.byref(ow._w), ga, a.ctypes.data_as(DP), gb,
                                               b.ctypes.data_as(DP)))
+
+
+def cone_hull(n_rim: int = 300, r: float = 0.12, h: float = 0.25):
+    """A watertight triangulated cone: n_rim rim vertices (z = 0), apex, base
+    centre.  Its flat base keeps every rim vertex in the walk cells around
+    -z (lists of >= 256 entries)."""
+    t = 2 * np.pi * np.arange(n_rim) / n_rim
+    V = [[r * np.cos(a), r * np.sin(a), 0.0] for a in t] + [[0.0, 0.0, h], [0.0, 0.0, 0.0]]
+    apex, ctr = n_rim, n_rim + 1
+    F = [(i, (i + 1) % n_rim, apex) for i in range(n_rim)] + [(ctr, (i + 1) % n_rim, i) for i in range(n_rim)]
+    return M.ConvexGeom(np.asarray(V, np.float64), F)
+
+
+def uv_sphere_hull(stacks: int = 24, slices: int = 32, r: float = 0.1):
+    """A watertight UV sphere of (stacks - 1) * slices + 2 vertices (770 by
+    default: more than the 512-vertex direction-table limit)."""
+    V = [[0.0, 0.0, r]]
+    for i in range(1, stacks):
+        th = np.pi * i / stacks
+        for j in range(slices):
+            ph = 2 * np.pi * j / slices
+            V.append([r * np.sin(th) * np.cos(ph), r * np.sin(th) * np.sin(ph), r * np.cos(th)])
+    V.append([0.0, 0.0, -r])
+    bot = len(V) - 1
+
+    def ring(i, j):
+        return 1 + (i - 1) * slices + j % slices
+
+    F = [(0, ring(1, j), ring(1, j + 1)) for j in range(slices)]
+    for i in range(1, stacks - 1):
+        for j in range(slices):
+            a, b, c, d = ring(i, j), ring(i, j + 1), ring(i + 1, j), ring(i + 1, j + 1)
+            F += [(a, c, b), (b, c, d)]
+    F += [(ring(stacks - 1, j), bot, ring(stacks - 1, j + 1)) for j in range(slices)]
+    return M.ConvexGeom(np.asarray(V, np.float64), F)
+
+
+def big_hull_world() -> oracle.OracleWorld:
+    """Panda + a 302-vertex cone + a 770-vertex sphere (FCL neighbour-walk
+    hulls beyond the round-2 device limits), at fixed random poses."""
+    art = panda_articulation()
+    rng = np.random.default_rng(99)
+    scene = []
+    for name, g, pos in (("cone", cone_hull(), (0.45, 0.15, 0.3)), ("ball", uv_sphere_hull(), (0.35, -0.3, 0.5))):
+        w, x, y, z = random_quat(rng)
+        scene.append((name, g, (M.quat_to_mat(w, x, y, z), list(pos))))
+    return oracle.OracleWorld(art, scene=scene)

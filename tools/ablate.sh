@@ -1,4 +1,5 @@
-# Phase-timing ablation of the collide pipeline (diagnostic env switches in
+# Phase-timing ablation of the collide pipeline (diagnostic env switches, read
+# only by a library built with `make -C mplib_amd EXTRA=-DMPG_DIAG`, in
 # mpg_kernels.hip): MPG_DEBUG_CULL=1 records only, 2 no SAT, 3 no MPR, 8 cull
 # without its tail (survivor words, tile counts, sincos), 9 cull without sincos;
 # MPG_STATS=1 prints narrow-phase candidate/support counts.
