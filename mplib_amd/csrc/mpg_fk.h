@@ -32,7 +32,7 @@ struct DevWorld {
   // the ablation switch as the kernels read it: compiled in only under the
   // MPG_DIAG macro (tools/ablate*.sh build such a library); the product
   // library ignores MPG_DEBUG_CULL entirely, so no result can change
-  __host__ __device__ __forceinline__ bool dbg(int k) const {
+  MPG_INLINE bool dbg(int k) const {
 #ifdef MPG_DIAG
     return debug_mode == k;
 #else
@@ -95,6 +95,8 @@ struct DevWorld {
   cptr<int> sched_start;  // [n_moving+1]
   cptr<int> sched_pair;
   cptr<int> sched_other;
+  cptr<int> sched_mid;      // [n_moving] first moving-partner entry of the object (static partners before it)
+  cptr<float> sched_srec;   // [entries * BS_STRIDE] static partner's OBB record, inline per entry
   // octrees: leaf boxes [L][6] (octree frame), per geometry a uniform grid
   // record (OG_*), cell -> leaf lists (CSR)
   cptr<double> oct_leaf;

@@ -969,61 +969,70 @@ __global__ __launch_bounds__(BLOCK) void cull_kernel(DevWorld w, const double* _
   }
 
   uint32_t head = 0, tail = 0;  // wave-uniform queue cursors
+  // queue the entries [eb, eb + 32) some lane kept (kb: this lane's bits);
+  // drain 64 queued (pair, lane) entries through the SAT at a time
+  auto push = [&](int eb, uint32_t kb) {
+    if (!live) kb = 0u;
+    if (w.dbg(2)) {
+      for (int i = 0; i < 32; ++i) {
+        if (!((kb >> i) & 1u)) continue;
+        const int p = w.sched_pair[eb + i];
+        survw[(p >> 5) * BLOCK + tid] |= 1u << (p & 31);
+      }
+      return;
+    }
+    uint32_t any_kb = kb;  // entries some lane of the wave kept
+#pragma unroll
+    for (int sh = 1; sh < 64; sh <<= 1) any_kb |= (uint32_t)__shfl_xor((int)any_kb, sh);
+    any_kb = __builtin_amdgcn_readfirstlane(any_kb);
+    while (any_kb) {
+      const int i = __builtin_ctz(any_kb);
+      any_kb &= any_kb - 1u;
+      const int p = w.sched_pair[eb + i];
+      const bool keep = (kb >> i) & 1u;
+      const unsigned long long bal = __ballot(keep);
+      if (keep) {
+        const uint32_t rank =
+            __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+        queue[(tail + rank) & (kQueue - 1)] = ((uint32_t)p << 6) | lane;
+      }
+      tail += (uint32_t)__popcll(bal);
+      if (tail - head >= 64) {
+        sat_drain<BLOCK>(w, cen, rq, cap, cfg0, survw, queue, head, 64, wbase, lane);
+        head += 64;
+      }
+    }
+  };
   for (int m = 0; m < w.n_moving; ++m) {
-    const int e0 = w.sched_start[m], e1 = w.sched_start[m + 1];
+    const int e0 = w.sched_start[m], em = w.sched_mid[m], e1 = w.sched_start[m + 1];
     if (e0 == e1) continue;
     const float* rm = cen + (size_t)m * 3 * BLOCK + tid;
     const float cm[3] = {rm[0], rm[BLOCK], rm[2 * BLOCK]};
     const float r_m = w.bp.mobj[BM_STRIDE * m + BM_R];
-    // up to 32 schedule entries at a time: first every bounding test into a
-    // per-lane bit set (a plain loop the compiler unrolls, its scalar loads
-    // issued ahead), then only the entries some lane kept are queued
-    for (int eb = e0; eb < e1; eb += 32) {
+    // static partners: the partner's OBB record is inline in the schedule
+    // entry (one 64-byte scalar load, no partner-index indirection), so the
+    // unrolled loop issues the next entries' loads ahead of the tests
+    for (int eb = e0; eb < em; eb += 32) {
+      const int ee = min(em, eb + 32);
+      uint32_t kb = 0u;
+#pragma unroll 4
+      for (int e = eb; e < ee; ++e)
+        kb |= (uint32_t)!fsphere_obb_separated(cm, r_m, w.sched_srec + BS_STRIDE * e, w.bp_margin) << (e - eb);
+      push(eb, kb);
+    }
+    // moving partners: bounding spheres (the partner's centre from LDS)
+    for (int eb = em; eb < e1; eb += 32) {
       const int ee = min(e1, eb + 32);
       uint32_t kb = 0u;
 #pragma unroll 4
       for (int e = eb; e < ee; ++e) {
         const int o = w.sched_other[e];
-        bool keep;
-        if (o >= w.n_moving) {
-          keep = !fsphere_obb_separated(cm, r_m, w.bp.sobj + BS_STRIDE * (o - w.n_moving), w.bp_margin);
-        } else {
-          const float* ro = cen + (size_t)o * 3 * BLOCK + tid;
-          const float dx = ro[0] - cm[0], dy = ro[BLOCK] - cm[1], dz = ro[2 * BLOCK] - cm[2];
-          const float rr = r_m + w.bp.mobj[BM_STRIDE * o + BM_R] + w.bp_margin;
-          keep = dx * dx + dy * dy + dz * dz <= rr * rr;
-        }
-        kb |= (uint32_t)keep << (e - eb);
+        const float* ro = cen + (size_t)o * 3 * BLOCK + tid;
+        const float dx = ro[0] - cm[0], dy = ro[BLOCK] - cm[1], dz = ro[2 * BLOCK] - cm[2];
+        const float rr = r_m + w.bp.mobj[BM_STRIDE * o + BM_R] + w.bp_margin;
+        kb |= (uint32_t)(dx * dx + dy * dy + dz * dz <= rr * rr) << (e - eb);
       }
-      if (!live) kb = 0u;
-      if (w.dbg(2)) {
-        for (int e = eb; e < ee; ++e) {
-          const int p = w.sched_pair[e];
-          if ((kb >> (e - eb)) & 1u) survw[(p >> 5) * BLOCK + tid] |= 1u << (p & 31);
-        }
-        continue;
-      }
-      uint32_t any_kb = kb;  // entries some lane of the wave kept
-#pragma unroll
-      for (int sh = 1; sh < 64; sh <<= 1) any_kb |= (uint32_t)__shfl_xor((int)any_kb, sh);
-      any_kb = __builtin_amdgcn_readfirstlane(any_kb);
-      while (any_kb) {
-        const int i = __builtin_ctz(any_kb);
-        any_kb &= any_kb - 1u;
-        const int p = w.sched_pair[eb + i];
-        const bool keep = (kb >> i) & 1u;
-        const unsigned long long bal = __ballot(keep);
-        if (keep) {
-          const uint32_t rank =
-              __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
-          queue[(tail + rank) & (kQueue - 1)] = ((uint32_t)p << 6) | lane;
-        }
-        tail += (uint32_t)__popcll(bal);
-        if (tail - head >= 64) {
-          sat_drain<BLOCK>(w, cen, rq, cap, cfg0, survw, queue, head, 64, wbase, lane);
-          head += 64;
-        }
-      }
+      push(eb, kb);
     }
   }
   if (tail != head) sat_drain<BLOCK>(w, cen, rq, cap, cfg0, survw, queue, head, tail - head, wbase, lane);
@@ -1124,18 +1133,42 @@ __device__ __forceinline__ uint32_t wave_inclusive_scan(uint32_t v, uint32_t lan
   return v;
 }
 
-// segment starts + prefix of narrow-phase tasks (kTask candidates of one
-// pair): one block, 256 pairs per round
+// segment starts + prefix of narrow-phase tasks (ts candidates of one pair
+// each): one block, 256 pairs per round.  The task size adapts to the batch:
+// ts = total candidates / target tasks (the narrow grid's resident waves),
+// clamped to [kTaskMin, kTask] and rounded up to a multiple of 8 -- small
+// batches (cfg2's 2^16 self pairs: ~27k candidates) spread over the whole
+// chip instead of a few hundred full waves.  prefix[n_pairs] = task count,
+// prefix[n_pairs + 1] = the narrow phase's task counter, prefix[n_pairs + 2]
+// = ts, prefix[n_pairs + 3] = the candidate count.
+constexpr uint32_t kTaskMin = 8;
+
+__device__ __forceinline__ uint32_t block_sum256(uint32_t v, uint32_t* red) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+  __syncthreads();
+  if ((threadIdx.x & 63u) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  return red[0] + red[1] + red[2] + red[3];
+}
+
 __global__ __launch_bounds__(256) void chunk_scan_kernel(const uint32_t* __restrict__ seg_len, int n_pairs,
                                                         uint32_t* __restrict__ seg_start,
-                                                        uint32_t* __restrict__ prefix, unsigned long long* units) {
-  __shared__ uint32_t wl[4], wt[4];
+                                                        uint32_t* __restrict__ prefix, unsigned long long* units,
+                                                        uint32_t target_tasks) {
+  __shared__ uint32_t wl[4], wt[4], red[4];
   const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+  uint32_t part = 0;
+  for (int p = (int)threadIdx.x; p < n_pairs; p += 256) part += seg_len[p];
+  const uint32_t all = block_sum256(part, red);
+  uint32_t ts = target_tasks ? (all + target_tasks - 1) / target_tasks : kTask;
+  ts = ts < kTaskMin ? kTaskMin : (ts > kTask ? kTask : ts);
+  ts = (ts + 7u) & ~7u;
   uint32_t cl = 0, ct = 0;  // carries over rounds
   for (int p0 = 0; p0 < n_pairs; p0 += 256) {
     const int p = p0 + (int)threadIdx.x;
     const uint32_t len = p < n_pairs ? seg_len[p] : 0u;
-    const uint32_t tasks = (len + kTask - 1) / kTask;
+    const uint32_t tasks = (len + ts - 1) / ts;
     const uint32_t il = wave_inclusive_scan(len, lane), it = wave_inclusive_scan(tasks, lane);
     if (lane == 63) {
       wl[wv] = il;
@@ -1160,6 +1193,8 @@ __global__ __launch_bounds__(256) void chunk_scan_kernel(const uint32_t* __restr
   if (threadIdx.x == 0) {
     prefix[n_pairs] = ct;
     prefix[n_pairs + 1] = 0;  // narrow-phase task counter
+    prefix[n_pairs + 2] = ts;
+    prefix[n_pairs + 3] = cl;  // candidates in all (diagnostics)
     if (units) atomicAdd(units, (unsigned long long)cl);  // profiling: narrow-phase candidates
   }
 }
@@ -1185,6 +1220,17 @@ __global__ __launch_bounds__(256) void scatter_kernel(const uint32_t* __restrict
       cand[seg_start[p] + off[(long long)p * n_tiles + t] + rank] = (uint32_t)cfg;
     }
   }
+}
+
+// binary search of the pair whose task range holds task tk: prefix[p] <= tk < prefix[p + 1]
+__device__ __forceinline__ int task_pair(const uint32_t* __restrict__ prefix, int n_pairs, uint32_t tk) {
+  int lo = 0, hi = n_pairs;
+  while (hi - lo > 1) {
+    const int mid = (lo + hi) >> 1;
+    if (prefix[mid] <= tk) lo = mid;
+    else hi = mid;
+  }
+  return lo;
 }
 
 // ---------------------------------------------------------------------------
@@ -1252,7 +1298,8 @@ __global__ __launch_bounds__(256, CLS == CLS_OCTREE ? 2 : 1) void closed_form_ke
     const int p = lo;
     const int cf = w.pair_cf[p];
     if (cf == CF_NONE || cf_class(cf) != CLS) continue;
-    const uint32_t t0 = (tk - prefix[p]) * kTask, t1 = min(seg_len[p], t0 + kTask);
+    const uint32_t ts = prefix[w.n_pairs + 2];
+    const uint32_t t0 = (tk - prefix[p]) * ts, t1 = min(seg_len[p], t0 + ts);
     const int a = w.pair_a[p], b = w.pair_b[p];
     const bool am = a < w.n_moving, bm = b < w.n_moving;
     const int ga = am ? w.moving_geom[a] : w.static_geom[a - w.n_moving];
@@ -1976,6 +2023,18 @@ __device__ __forceinline__ unsigned long long walk_wave_eval(const DevWorld& w, 
 }
 
 
+
+// Refill idle lanes once at least this many are idle (a refill is two loads
+// and the MPR start once the pose pass has built the GJK objects)
+#ifndef MPG_REFILL_MIN
+#define MPG_REFILL_MIN 32
+#endif
+// take the next task early once the current one is handed out and this many
+// lanes are idle: a task of the same pair continues without a drain
+#ifndef MPG_STEAL_MIN
+#define MPG_STEAL_MIN 64
+#endif
+
 template <bool FROM_POSES>
 __global__ __launch_bounds__(256) MPG_NARROW_WAVES void narrow_kernel(DevWorld w, const double* __restrict__ in,
                                                     const uint32_t* __restrict__ seg_len,
@@ -1988,27 +2047,33 @@ __global__ __launch_bounds__(256) MPG_NARROW_WAVES void narrow_kernel(DevWorld w
   // (staging the hulls in LDS measured slower: +60 VGPRs, occupancy 4 -> 3)
   const cptr<double> HV = w.hull;
   const uint32_t lane = lane_id();
-  const uint32_t total = prefix[w.n_pairs];
-  for (;;) {
-    uint32_t tk = 0;  // dynamic task queue: waves that drew cheap tasks take more
-    if (lane == 0) tk = atomicAdd(task_ctr, 1u);
-    tk = __builtin_amdgcn_readfirstlane(tk);
-    if (tk >= total) break;
-    int lo = 0, hi = w.n_pairs;  // prefix[lo] <= tk < prefix[hi]
-    while (hi - lo > 1) {
-      const int mid = (lo + hi) >> 1;
-      if (prefix[mid] <= tk) lo = mid;
-      else hi = mid;
+  const uint32_t total = prefix[w.n_pairs], ts = prefix[w.n_pairs + 2];
+  // dynamic task queue: waves that drew cheap tasks take more.
+  // The first task of every wave is its wave index (the counter starts past
+  // them): half the atomics on the one counter, which a small batch's waves
+  // otherwise all hit at once.  (A relaxed load to skip the atomic once the
+  // queue is drained measured 2x slower on cfg3: keep atomics out of the loop.)
+  const uint32_t n_waves = (gridDim.x * blockDim.x) >> 6;
+  auto fetch = [&]() {
+    uint32_t t = 0;
+    if (lane == 0) t = n_waves + atomicAdd(task_ctr, 1u);
+    return (uint32_t)__builtin_amdgcn_readfirstlane(t);
+  };
+  uint32_t tk = __builtin_amdgcn_readfirstlane((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+  while (tk < total) {
+    const int p = task_pair(prefix, w.n_pairs, tk);
+    if (w.pair_cf[p] != CF_NONE) {  // closed-form pairs: closed_form_kernel
+      tk = fetch();
+      continue;
     }
-    const int p = lo;
-    const uint32_t t0 = (tk - prefix[p]) * kTask;
-    const uint32_t t1 = min(seg_len[p], t0 + kTask);
+    uint32_t next = (tk - prefix[p]) * ts;  // wave-uniform cursor into the pair's candidates
+    uint32_t t1 = min(seg_len[p], next + ts);
+    uint32_t pend = 0xffffffffu;  // a task of another pair, taken early: runs after this one
+    bool more = true;             // the queue may still hold tasks
     const uint32_t* __restrict__ cl = cand + seg_start[p];
     const int a = w.pair_a[p], b = w.pair_b[p];
     const bool am = a < w.n_moving, bm = b < w.n_moving;
     const uint32_t bit = 1u << (p & 31);
-    if (w.pair_cf[p] != CF_NONE) continue;  // closed-form pairs: closed_form_kernel
-    uint32_t next = t0;  // wave-uniform
     int st = MPR_DONE;
     long long cfg = 0;
     GObj A, B;
@@ -2021,10 +2086,21 @@ __global__ __launch_bounds__(256) MPG_NARROW_WAVES void narrow_kernel(DevWorld w
     for (;;) {
       const unsigned long long idle = __ballot(st == MPR_DONE);
       const uint32_t n_idle = (uint32_t)__popcll(idle);
+      if (next >= t1 && pend == 0xffffffffu && more && n_idle >= MPG_STEAL_MIN) {
+        const uint32_t t2 = fetch();
+        if (t2 >= total) {
+          more = false;
+        } else if (task_pair(prefix, w.n_pairs, t2) == p) {  // same pair: continue without draining
+          next = (t2 - prefix[p]) * ts;
+          t1 = min(seg_len[p], next + ts);
+        } else {
+          pend = t2;
+        }
+      }
 #ifdef MPG_STATS
       const unsigned long long c0 = __builtin_amdgcn_s_memtime();
 #endif
-      if (next < t1 && (n_idle >= MPG_REFILL || n_idle == 64)) {  // batched refill
+      if (next < t1 && (n_idle >= MPG_REFILL_MIN || n_idle == 64)) {  // refill the idle lanes
         if (st == MPR_DONE) {
           const uint32_t rank =
               __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
@@ -2051,7 +2127,7 @@ __global__ __launch_bounds__(256) MPG_NARROW_WAVES void narrow_kernel(DevWorld w
       }
 #endif
       if (__ballot(st != MPR_DONE) == 0) {
-        if (next >= t1) break;
+        if (next >= t1 && (pend != 0xffffffffu || !more)) break;
         continue;
       }
 #ifdef MPG_STATS
@@ -2061,8 +2137,6 @@ __global__ __launch_bounds__(256) MPG_NARROW_WAVES void narrow_kernel(DevWorld w
         const CV3 s = msupport(w, HV, A, B, dir);
 #ifdef MPG_STATS
         ++nsteps;
-#endif
-#ifdef MPG_STATS
         c2 = __builtin_amdgcn_s_memtime();
 #endif
         const int res = mpr_advance(w.mpr_tol, s, st, v0, v1, v2, v3, dir);
@@ -2096,6 +2170,7 @@ __global__ __launch_bounds__(256) MPG_NARROW_WAVES void narrow_kernel(DevWorld w
       }
 #endif
     }
+    tk = pend != 0xffffffffu ? pend : (more ? fetch() : total);
   }
 }
 
@@ -3423,7 +3498,8 @@ __global__ __launch_bounds__(256) void contact_kernel(DevWorld w, const double* 
       else hi = mid;
     }
     const int p = lo;
-    const uint32_t t0 = (tk - prefix[p]) * kTask, t1 = min(seg_len[p], t0 + kTask);
+    const uint32_t ts = prefix[w.n_pairs + 2];
+    const uint32_t t0 = (tk - prefix[p]) * ts, t1 = min(seg_len[p], t0 + ts);
     const int a = w.pair_a[p], b = w.pair_b[p];
     for (uint32_t base = t0; base < t1; base += 64) {
       const uint32_t idx = base + lane;
@@ -4038,7 +4114,7 @@ int get_workspace(mpg_world* w, hipStream_t s, long long want, mpg_world::Worksp
     HIP_TRY(hipMalloc(&ws.cnt, sizeof(uint32_t) * np * tiles));
     HIP_TRY(hipMalloc(&ws.seg_len, sizeof(uint32_t) * np));
     HIP_TRY(hipMalloc(&ws.seg_start, sizeof(uint32_t) * np));
-    HIP_TRY(hipMalloc(&ws.prefix, sizeof(uint32_t) * (np + 2)));
+    HIP_TRY(hipMalloc(&ws.prefix, sizeof(uint32_t) * (np + 4)));
     HIP_TRY(hipMalloc(&ws.cand, sizeof(uint32_t) * np * want));
     HIP_TRY(hipMalloc(&ws.rq, sizeof(float) * 4 * std::max(w->dw.n_moving, 1) * want));
     HIP_TRY(hipMalloc(&ws.sc, sizeof(double) * 2 * std::max(w->dw.dof, 1) * want));
@@ -4130,7 +4206,7 @@ int launch_collide(mpg_world* w, const double* in, long long n, uint8_t* flags, 
       HIP_TRY(hipGetLastError());
     }
     hipLaunchKernelGGL(chunk_scan_kernel, dim3(1), dim3(256), 0, stream, ws->seg_len, w->dw.n_pairs, ws->seg_start,
-                       ws->prefix, w->prof ? w->prof_units : nullptr);
+                       ws->prefix, w->prof ? w->prof_units : nullptr, (uint32_t)(4 * w->narrow_blocks));
     HIP_TRY(hipGetLastError());
     hipLaunchKernelGGL(scatter_kernel, dim3(gb), dim3(256), 0, stream, ws->surv, m, ws->cap, w->dw.n_pairs, w->dw.W,
                        n_tiles, ws->cnt, ws->seg_start, ws->cand);
@@ -4138,7 +4214,7 @@ int launch_collide(mpg_world* w, const double* in, long long n, uint8_t* flags, 
     t_bucket.stop();
     StageTimer t_narrow(w, stream, MPG_STAGE_NARROW);
     // persistent narrow phase: enough waves to fill the chip, fewer for tiny batches
-    const long long want_waves = (m * std::max(w->dw.n_pairs, 1) + kTask - 1) / kTask;
+    const long long want_waves = (m * std::max(w->dw.n_pairs, 1) + kTaskMin - 1) / kTaskMin;
     const unsigned nb = (unsigned)std::max<long long>(1, std::min<long long>(w->narrow_blocks, (want_waves + 3) / 4));
     hipLaunchKernelGGL((narrow_kernel<FROM_POSES>), dim3(nb), dim3(256), 0, stream, w->dw, qin, ws->seg_len,
                        ws->seg_start, ws->prefix, ws->cand, fl, mk, ws->prefix + w->dw.n_pairs + 1, ws->sc);
@@ -4446,16 +4522,26 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
   std::vector<int> pair_cf(std::max(d->n_pairs, 1), 0);
   for (int p = 0; p < d->n_pairs; ++p) pair_cf[p] = closed_form_kind(d, d->pair_a[p], d->pair_b[p]);
   // phase-A schedule: non-allowed pairs grouped by their lower moving object
-  std::vector<int> sched_start(d->n_moving + 1, 0), sched_pair, sched_other;
+  // per moving object: its static partners first (their OBB record inline in
+  // the entry), then its moving partners
+  std::vector<int> sched_start(d->n_moving + 1, 0), sched_mid(std::max(d->n_moving, 1), 0), sched_pair, sched_other;
+  std::vector<float> sched_srec;
   for (int m = 0; m < d->n_moving; ++m) {
     sched_start[m] = (int)sched_pair.size();
-    for (int p = 0; p < d->n_pairs; ++p) {
-      if (allowed[p]) continue;
-      const int a = d->pair_a[p], b = d->pair_b[p];
-      const int lo = std::min(a, b), hi = std::max(a, b);  // static ids are >= n_moving
-      if (lo == m) {
+    for (int pass = 0; pass < 2; ++pass) {
+      if (pass == 1) sched_mid[m] = (int)sched_pair.size();
+      for (int p = 0; p < d->n_pairs; ++p) {
+        if (allowed[p]) continue;
+        const int a = d->pair_a[p], b = d->pair_b[p];
+        const int lo = std::min(a, b), hi = std::max(a, b);  // static ids are >= n_moving
+        if (lo != m || (hi >= d->n_moving) != (pass == 0)) continue;
         sched_pair.push_back(p);
         sched_other.push_back(hi);
+        if (pass == 0)
+          sched_srec.insert(sched_srec.end(), bpp.sobj.begin() + (size_t)BS_STRIDE * (hi - d->n_moving),
+                            bpp.sobj.begin() + (size_t)BS_STRIDE * (hi - d->n_moving + 1));
+        else
+          sched_srec.insert(sched_srec.end(), BS_STRIDE, 0.f);
       }
     }
   }
@@ -4464,6 +4550,7 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
     sched_pair.push_back(0);
     sched_other.push_back(0);
   }
+  if (sched_srec.empty()) sched_srec.assign(BS_STRIDE, 0.f);
 
   BlobBuilder bb;
   const size_t o_jt = bb.add(d->joint_type, d->n_joints);
@@ -4510,6 +4597,8 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
   const size_t o_ss = bb.add(sched_start.data(), sched_start.size());
   const size_t o_sp = bb.add(sched_pair.data(), sched_pair.size());
   const size_t o_so = bb.add(sched_other.data(), sched_other.size());
+  const size_t o_sm = bb.add(sched_mid.data(), sched_mid.size());
+  const size_t o_ssr = bb.add(sched_srec.data(), sched_srec.size());
   const size_t o_bjs = bb.add(bpp.jsrc.data(), bpp.jsrc.size());
   const size_t o_bjv = bb.add(bpp.jsave.data(), bpp.jsave.size());
   const size_t o_bja = bb.add(bpp.jaxis.data(), bpp.jaxis.size());
@@ -4662,6 +4751,8 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
   dw.sched_start = I(o_ss);
   dw.sched_pair = I(o_sp);
   dw.sched_other = I(o_so);
+  dw.sched_mid = I(o_sm);
+  dw.sched_srec = to_cptr<float>(base + o_ssr);
   auto F = [&](size_t o) { return to_cptr<float>(base + o); };
   BpView& bp = dw.bp;
   bp.nj = d->n_joints;
