@@ -169,6 +169,15 @@ typedef struct mpg_world_desc {
    *     geom_param[1] = number of faces (0 = no faces: linear support).     */
   int64_t n_convex_face_ints;
   const int32_t *convex_face;     /* [n_convex_face_ints]                   */
+
+  /* --- joint limits (PinocchioModelTpl::getJointLimit, src/pinocchio_model.cpp:
+   *     59-83): [lower, upper] of each joint value, -inf / +inf or NULL =
+   *     unbounded.  Only the broad phase reads them: the travel of a prismatic
+   *     move-group joint bounds the fp32 cull's coordinates.  A configuration
+   *     outside them is still evaluated exactly (every pair of it goes to the
+   *     narrow phase), so no input changes a result.                         */
+  const double *joint_lower;      /* [n_joints] or NULL                     */
+  const double *joint_upper;      /* [n_joints] or NULL                     */
 } mpg_world_desc;
 
 typedef struct mpg_world mpg_world;

@@ -45,6 +45,7 @@ class WorldDesc(ctypes.Structure):
         ("n_octree_leaves", ctypes.c_int64), ("octree_leaf", _F64P),
         ("n_mesh_triangles", ctypes.c_int64), ("mesh_triangle", _I32P),
         ("n_convex_face_ints", ctypes.c_int64), ("convex_face", _I32P),
+        ("joint_lower", _F64P), ("joint_upper", _F64P),
     ]
 
 

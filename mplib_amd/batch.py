@@ -87,6 +87,11 @@ class DeviceWorld:
             faces = np.zeros(1, np.int32)
         self._keep.append(faces)
         d.convex_face = faces.ctypes.data_as(C._I32P)
+        for f in ("joint_lower", "joint_upper"):  # optional: NULL = unbounded
+            if f in arrays and arrays[f] is not None:
+                a = np.ascontiguousarray(np.asarray(arrays[f], dtype=np.float64).reshape(-1))
+                self._keep.append(a)
+                setattr(d, f, a.ctypes.data_as(C._F64P))
         h = ctypes.c_void_p()
         C.check(L.mpg_world_create(ctypes.byref(d), device, ctypes.byref(h)), "mpg_world_create")
         self._keep = []

@@ -243,6 +243,7 @@ int default_device();
 struct DescBuilder {
   std::vector<int32_t> joint_type, joint_parent, joint_q_source;
   std::vector<double> joint_axis, joint_placement, joint_q_const;
+  std::vector<double> joint_lower, joint_upper;  // getJointLimit (first coordinate; +-inf for continuous)
   int32_t dof = 0;
   std::vector<int32_t> link_parent;
   std::vector<double> link_placement;

@@ -458,6 +458,9 @@ mpg_world_desc DescBuilder::desc() const {
   d.mesh_triangle = mesh_triangle.data();
   d.n_convex_face_ints = (int64_t)convex_face.size();
   d.convex_face = convex_face.data();
+  const bool lim = joint_lower.size() == joint_type.size() && joint_upper.size() == joint_type.size();
+  d.joint_lower = lim ? joint_lower.data() : nullptr;
+  d.joint_upper = lim ? joint_upper.data() : nullptr;
   return d;
 }
 

@@ -12,6 +12,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <iostream>
+#include <limits>
 
 #include "host.hpp"
 
@@ -201,6 +202,9 @@ void PinocchioModel::fill_kinematics(DescBuilder& d, int joint_offset, const std
     push_se3(d.joint_placement, pj.placement);
     d.joint_q_source.push_back(q_source[j - 1]);
     d.joint_q_const.push_back(q_const[j - 1]);
+    const bool one = pj.nq == 1 && !pj.lower.empty() && !pj.upper.empty();
+    d.joint_lower.push_back(one ? pj.lower[0] : -std::numeric_limits<double>::infinity());
+    d.joint_upper.push_back(one ? pj.upper[0] : std::numeric_limits<double>::infinity());
   }
   for (int f : link_index_user2pin_) {
     const PinFrame& fr = frames_[f];

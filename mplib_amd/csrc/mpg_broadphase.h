@@ -29,6 +29,8 @@ constexpr float kBpMargin = 1e-4f;  // metres
 // with 3x headroom); world creation keeps the margin above this times the
 // coordinate bound, so far-from-origin worlds keep the soundness argument
 constexpr double kFp32CullRel = 4e-6;
+// travel bound of a prismatic move-group joint without finite limits (metres)
+constexpr double kDefaultTravel = 10.0;
 
 // The broad phase is conservative by its margins, not bit-exact: its fp32
 // arithmetic may fuse multiply-adds (more accurate, fewer instructions) even

@@ -96,6 +96,11 @@ struct DevWorld {
   cptr<int> sched_pair;
   cptr<int> sched_other;
   cptr<int> sched_mid;      // [n_moving] first moving-partner entry of the object (static partners before it)
+  cptr<int> sched_keep;     // [n_moving] end of the static partners its reach ball can bring near (the rest: link-pose input only)
+  int n_prism;              // prismatic move-group joints with a value bound (a configuration beyond it: every pair)
+  cptr<double> prism_bound; // [nj] |q| bound of such a joint, 0 = none
+  double pose_bound;        // link-pose input: |position| bound of every link (beyond it: every pair)
+  cptr<int> all_mask;       // [W] bits of every non-allowed pair
   cptr<float> sched_srec;   // [entries * BS_STRIDE] static partner's OBB record, inline per entry
   // octrees: leaf boxes [L][6] (octree frame), per geometry a uniform grid
   // record (OG_*), cell -> leaf lists (CSR)

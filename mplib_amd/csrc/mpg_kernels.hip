@@ -958,10 +958,21 @@ __global__ __launch_bounds__(BLOCK) void cull_kernel(DevWorld w, const double* _
     for (int i = 0; i < 3; ++i)
       r[i * BLOCK] = T.R[3 * i] * g[BM_C] + T.R[3 * i + 1] * g[BM_C + 1] + T.R[3 * i + 2] * g[BM_C + 2] + T.p[i];
   };
+  // a configuration outside the bounds the cull's margins assume (a prismatic
+  // value beyond its travel bound, or a given link pose beyond the chain's
+  // reach) is evaluated with every pair
+  bool forced = false;
   if (FROM_POSES) {
     for (int m = 0; m < w.n_moving; ++m) put(m, bp_from_pose7(w.bp, in + (c * w.n_links + w.moving_link[m]) * 7, m));
+    for (int l = 0; l < w.n_links; ++l) {
+      const double* pl = in + (c * w.n_links + l) * 7;
+      forced |= !(std::fabs(pl[0]) <= w.pose_bound && std::fabs(pl[1]) <= w.pose_bound && std::fabs(pl[2]) <= w.pose_bound);
+    }
   } else {
     bp_fk(w.bp, in + c * w.dof, save + tid, BLOCK, put);
+    if (w.n_prism)
+      for (int j = 0; j < w.nj; ++j)
+        if (w.prism_bound[j] > 0.0) forced |= !(std::fabs(in[c * w.dof + w.joint_q_source[j]]) <= w.prism_bound[j]);
   }
   if (w.dbg(1)) {
     if (live && cen[tid] == 12345.f) flags[cfg] = 2;  // keep the records alive
@@ -1004,7 +1015,9 @@ __global__ __launch_bounds__(BLOCK) void cull_kernel(DevWorld w, const double* _
     }
   };
   for (int m = 0; m < w.n_moving; ++m) {
+    // link-pose input: every static partner (the reach balls assume kinematics)
     const int e0 = w.sched_start[m], em = w.sched_mid[m], e1 = w.sched_start[m + 1];
+    const int es = FROM_POSES ? em : w.sched_keep[m];
     if (e0 == e1) continue;
     const float* rm = cen + (size_t)m * 3 * BLOCK + tid;
     const float cm[3] = {rm[0], rm[BLOCK], rm[2 * BLOCK]};
@@ -1012,8 +1025,8 @@ __global__ __launch_bounds__(BLOCK) void cull_kernel(DevWorld w, const double* _
     // static partners: the partner's OBB record is inline in the schedule
     // entry (one 64-byte scalar load, no partner-index indirection), so the
     // unrolled loop issues the next entries' loads ahead of the tests
-    for (int eb = e0; eb < em; eb += 32) {
-      const int ee = min(em, eb + 32);
+    for (int eb = e0; eb < es; eb += 32) {
+      const int ee = min(es, eb + 32);
       uint32_t kb = 0u;
 #pragma unroll 4
       for (int e = eb; e < ee; ++e)
@@ -1036,6 +1049,8 @@ __global__ __launch_bounds__(BLOCK) void cull_kernel(DevWorld w, const double* _
     }
   }
   if (tail != head) sat_drain<BLOCK>(w, cen, rq, cap, cfg0, survw, queue, head, tail - head, wbase, lane);
+  if (forced)
+    for (int k = 0; k < w.W; ++k) survw[k * BLOCK + tid] = (uint32_t)w.all_mask[k];
   if (w.dbg(8)) {  // ablation: bounding tests + SAT only
     if (live && survw[tid] == 12345u) flags[cfg] = 2;
     return;
@@ -4522,22 +4537,129 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
   std::vector<int> pair_cf(std::max(d->n_pairs, 1), 0);
   for (int p = 0; p < d->n_pairs; ++p) pair_cf[p] = closed_form_kind(d, d->pair_a[p], d->pair_b[p]);
   // phase-A schedule: non-allowed pairs grouped by their lower moving object
+  // ---- culling margins: pairs that can reach libccd MPR (directly, on octree
+  // leaves or on mesh triangles) keep everything within its false-hit reach
+  bool may_mpr = false;
+  for (int p = 0; p < d->n_pairs; ++p) {
+    if (allowed[p]) continue;
+    const int ta = obj_geom_type(d, d->pair_a[p]), tb = obj_geom_type(d, d->pair_b[p]);
+    const bool closed = pair_cf[p] != CF_NONE && cf_class(pair_cf[p]) == CLS_CLOSED;
+    const bool mesh_mesh = ta == MPG_GEOM_MESH && tb == MPG_GEOM_MESH;
+    may_mpr |= !closed && !mesh_mesh;
+  }
+  const double reach = kCcdFalseHitReach * (1.0 + 1e-3) + 1e-5;
+  float bp_margin = may_mpr ? (float)std::max((double)kBpMargin, reach) : kBpMargin;
+  // The travel of each prismatic joint: a move-group joint's value bound from
+  // its limits (kDefaultTravel when unbounded), a fixed joint's own value.
+  // A configuration whose prismatic value exceeds its bound is evaluated with
+  // every pair (the cull's coordinate bound below would not hold for it).
+  auto sq3 = [](const double* v) { return v[0] * v[0] + v[1] * v[1] + v[2] * v[2]; };
+  std::vector<double> travel(std::max(d->n_joints, 1), 0.0), prism_bound(std::max(d->n_joints, 1), 0.0);
+  int n_prism = 0;
+  for (int j = 0; j < d->n_joints; ++j) {
+    const int t = d->joint_type[j];
+    if (t < MPG_JOINT_PX || t > MPG_JOINT_PRISMATIC_UNALIGNED) continue;
+    const double an = t == MPG_JOINT_PRISMATIC_UNALIGNED ? std::sqrt(sq3(d->joint_axis + 3 * j)) : 1.0;
+    if (d->joint_q_source[j] >= 0) {
+      double qb = kDefaultTravel;
+      if (d->joint_lower && d->joint_upper && std::isfinite(d->joint_lower[j]) && std::isfinite(d->joint_upper[j]))
+        qb = std::max(std::fabs(d->joint_lower[j]), std::fabs(d->joint_upper[j]));
+      prism_bound[j] = qb;
+      ++n_prism;
+      travel[j] = qb * an;
+    } else {
+      travel[j] = std::fabs(d->joint_q_const[j]) * an;
+    }
+  }
+  // the fp32 broad phase's rounding grows with coordinate magnitude: bound
+  // every world coordinate the cull computes (the chain's reach -- sum of the
+  // placement translations and prismatic travels, revolute joints cannot
+  // lengthen it --, moving offsets, static poses, geometry radii) and keep the
+  // margin above kFp32CullRel of it (kBpMargin covers a ~2 m world near the
+  // origin)
+  double reach_x = 0.0, geo_r = 0.0, stat_x = 0.0;
+  for (int j = 0; j < d->n_joints; ++j) reach_x += std::sqrt(sq3(d->joint_placement + 12 * j + 9)) + travel[j];
+  for (int l = 0; l < d->n_links; ++l) reach_x += std::sqrt(sq3(d->link_placement + 12 * l + 9));
+  double off = 0.0;
+  for (int m = 0; m < d->n_moving; ++m) off = std::max(off, std::sqrt(sq3(d->moving_offset + 12 * m + 9)));
+  for (int g = 0; g < d->n_geoms; ++g) geo_r = std::max(geo_r, geom_rec[G_STRIDE * g + G_RADIUS] +
+                                                                   std::sqrt(sq3(&geom_rec[G_STRIDE * g + G_OBB_C])));
+  for (int s2 = 0; s2 < d->n_static; ++s2) stat_x = std::max(stat_x, std::sqrt(sq3(d->static_transform + 12 * s2 + 9)));
+  const double X = std::max(reach_x + off, stat_x) + geo_r;
+  bp_margin = std::max(bp_margin, (float)(kFp32CullRel * X));
+  const double small_margin = may_mpr ? std::max(kSmallMargin, reach) : kSmallMargin;
+  // link poses given directly (mpg_collide_link_poses): a pose beyond the
+  // chain's reach falls outside the coordinate bound -> every pair
+  const double pose_bound = reach_x;
+  // Reach ball of each moving object: its centre stays within radius R of
+  // the origin of the first joint of its chain (every later joint origin is
+  // a fixed distance from its parent's, plus a prismatic travel; revolute
+  // angles cannot lengthen the chain), or is fixed when the chain is empty.
+  // A static partner farther than R + the object's radius + the culling
+  // margin from that ball can never be a candidate: its schedule entry is
+  // kept only for the link-pose input, whose poses are not kinematic.
+  std::vector<std::array<double, 4>> ball(std::max(d->n_moving, 1));  // centre, radius (object radius included)
+  for (int m = 0; m < d->n_moving; ++m) {
+    const int l = d->moving_link[m];
+    const double* g = geom_rec.data() + G_STRIDE * d->moving_geom[m];
+    const double* mo = d->moving_offset + 12 * m;
+    const double* lp = d->link_placement + 12 * l;
+    double a[3], bpt[3];
+    for (int i = 0; i < 3; ++i)
+      a[i] = mo[3 * i] * g[G_OBB_C] + mo[3 * i + 1] * g[G_OBB_C + 1] + mo[3 * i + 2] * g[G_OBB_C + 2] + mo[9 + i];
+    for (int i = 0; i < 3; ++i) bpt[i] = lp[3 * i] * a[0] + lp[3 * i + 1] * a[1] + lp[3 * i + 2] * a[2] + lp[9 + i];
+    const int cs = chain_start[l], cn = chain_len[l];
+    double R = g[G_RADIUS];
+    if (cn == 0) {
+      ball[m] = {bpt[0], bpt[1], bpt[2], R};
+      continue;
+    }
+    const int j1 = chain_joints[cs] - 1;
+    const double* p1 = d->joint_placement + 12 * j1 + 9;
+    R += travel[j1] + std::sqrt(sq3(bpt));
+    for (int k = 1; k < cn; ++k) {
+      const int j = chain_joints[cs + k] - 1;
+      R += std::sqrt(sq3(d->joint_placement + 12 * j + 9)) + travel[j];
+    }
+    ball[m] = {p1[0], p1[1], p1[2], R * (1.0 + 1e-9) + 1e-9};
+  }
+  auto never_near = [&](int m, int sid) {  // exact fp64 distance, reach ball vs the static OBB
+    const double* sr = static_rec.data() + (size_t)S_STRIDE * sid;
+    const double* gs = geom_rec.data() + G_STRIDE * d->static_geom[sid];
+    double e2 = 0.0;
+    for (int k = 0; k < 3; ++k) {  // box axis k = column k of S_R
+      double t = 0.0;
+      for (int i = 0; i < 3; ++i) t += (ball[m][i] - sr[S_OBBC + i]) * sr[S_R + 3 * i + k];
+      const double ex = std::max(std::fabs(t) - gs[G_OBB_E + k], 0.0);
+      e2 += ex * ex;
+    }
+    const double slack = 1e-6 * (1.0 + X);
+    return std::sqrt(e2) - ball[m][3] > (double)bp_margin + slack;
+  };
+  // bits of every non-allowed pair (a configuration evaluated with all pairs)
+  std::vector<int> all_mask(std::max(W, 1), 0);
+  for (int p = 0; p < d->n_pairs; ++p)
+    if (!allowed[p]) all_mask[p >> 5] |= (int)(1u << (p & 31));
   // per moving object: its static partners first (their OBB record inline in
-  // the entry), then its moving partners
-  std::vector<int> sched_start(d->n_moving + 1, 0), sched_mid(std::max(d->n_moving, 1), 0), sched_pair, sched_other;
+  // the entry; those that can be near before those that never are), then its
+  // moving partners
+  std::vector<int> sched_start(d->n_moving + 1, 0), sched_mid(std::max(d->n_moving, 1), 0),
+      sched_keep(std::max(d->n_moving, 1), 0), sched_pair, sched_other;
   std::vector<float> sched_srec;
   for (int m = 0; m < d->n_moving; ++m) {
     sched_start[m] = (int)sched_pair.size();
-    for (int pass = 0; pass < 2; ++pass) {
-      if (pass == 1) sched_mid[m] = (int)sched_pair.size();
+    for (int pass = 0; pass < 3; ++pass) {  // statics that can be near, statics never near, movers
+      if (pass == 1) sched_keep[m] = (int)sched_pair.size();
+      if (pass == 2) sched_mid[m] = (int)sched_pair.size();
       for (int p = 0; p < d->n_pairs; ++p) {
         if (allowed[p]) continue;
         const int a = d->pair_a[p], b = d->pair_b[p];
         const int lo = std::min(a, b), hi = std::max(a, b);  // static ids are >= n_moving
-        if (lo != m || (hi >= d->n_moving) != (pass == 0)) continue;
+        if (lo != m || (hi >= d->n_moving) != (pass < 2)) continue;
+        if (pass < 2 && never_near(m, hi - d->n_moving) != (pass == 1)) continue;
         sched_pair.push_back(p);
         sched_other.push_back(hi);
-        if (pass == 0)
+        if (pass < 2)
           sched_srec.insert(sched_srec.end(), bpp.sobj.begin() + (size_t)BS_STRIDE * (hi - d->n_moving),
                             bpp.sobj.begin() + (size_t)BS_STRIDE * (hi - d->n_moving + 1));
         else
@@ -4598,6 +4720,9 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
   const size_t o_sp = bb.add(sched_pair.data(), sched_pair.size());
   const size_t o_so = bb.add(sched_other.data(), sched_other.size());
   const size_t o_sm = bb.add(sched_mid.data(), sched_mid.size());
+  const size_t o_sk = bb.add(sched_keep.data(), sched_keep.size());
+  const size_t o_pbd = bb.add(prism_bound.data(), prism_bound.size());
+  const size_t o_amk = bb.add(all_mask.data(), all_mask.size());
   const size_t o_ssr = bb.add(sched_srec.data(), sched_srec.size());
   const size_t o_bjs = bb.add(bpp.jsrc.data(), bpp.jsrc.size());
   const size_t o_bjv = bb.add(bpp.jsave.data(), bpp.jsave.size());
@@ -4649,44 +4774,18 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
   dw.n_pairs = d->n_pairs;
   dw.W = W;
   dw.mpr_tol = d->gjk_tolerance;
-  {  // culling margins: pairs that can reach libccd MPR (directly, on octree
-     // leaves or on mesh triangles) keep everything within its false-hit reach
-    bool may_mpr = false;
-    for (int p = 0; p < d->n_pairs; ++p) {
-      if (allowed[p]) continue;
-      const int ta = obj_geom_type(d, d->pair_a[p]), tb = obj_geom_type(d, d->pair_b[p]);
-      const bool closed = pair_cf[p] != CF_NONE && cf_class(pair_cf[p]) == CLS_CLOSED;
-      const bool mesh_mesh = ta == MPG_GEOM_MESH && tb == MPG_GEOM_MESH;
-      may_mpr |= !closed && !mesh_mesh;
-    }
-    const double reach = kCcdFalseHitReach * (1.0 + 1e-3) + 1e-5;
-    dw.bp_margin = may_mpr ? (float)std::max((double)kBpMargin, reach) : kBpMargin;
-    // the fp32 broad phase's rounding grows with coordinate magnitude: bound
-    // every world coordinate the cull computes (the chain's reach -- sum of
-    // the placement translations, revolute joints cannot lengthen it --,
-    // moving offsets, static poses, geometry radii; a prismatic joint of the
-    // move group adds its travel, which the snapshot cannot bound) and keep
-    // the margin above kFp32CullRel of it (kBpMargin covers a ~2 m world
-    // near the origin)
-    auto sq3 = [](const double* v) { return v[0] * v[0] + v[1] * v[1] + v[2] * v[2]; };
-    double reach_x = 0.0, geo_r = 0.0, stat_x = 0.0;
-    for (int j = 0; j < d->n_joints; ++j) reach_x += std::sqrt(sq3(d->joint_placement + 12 * j + 9));
-    for (int l = 0; l < d->n_links; ++l) reach_x += std::sqrt(sq3(d->link_placement + 12 * l + 9));
-    double off = 0.0;
-    for (int m = 0; m < d->n_moving; ++m) off = std::max(off, std::sqrt(sq3(d->moving_offset + 12 * m + 9)));
-    for (int g = 0; g < d->n_geoms; ++g) geo_r = std::max(geo_r, geom_rec[G_STRIDE * g + G_RADIUS] +
-                                                                     std::sqrt(sq3(&geom_rec[G_STRIDE * g + G_OBB_C])));
-    for (int s2 = 0; s2 < d->n_static; ++s2) stat_x = std::max(stat_x, std::sqrt(sq3(d->static_transform + 12 * s2 + 9)));
-    const double X = std::max(reach_x + off, stat_x) + geo_r;
-    dw.bp_margin = std::max(dw.bp_margin, (float)(kFp32CullRel * X));
-    dw.small_margin = may_mpr ? std::max(kSmallMargin, reach) : kSmallMargin;
+  dw.bp_margin = bp_margin;
+  dw.small_margin = small_margin;
+  dw.n_prism = n_prism;
+  dw.prism_bound = to_cptr<double>(base + o_pbd);
+  dw.pose_bound = pose_bound;
+  dw.all_mask = to_cptr<int>(base + o_amk);
 #ifdef MPG_DIAG  // ablation builds only (changes results)
-    if (const char* m = std::getenv("MPG_DEBUG_MARGIN")) {
-      dw.bp_margin = (float)std::atof(m);
-      dw.small_margin = std::atof(m);
-    }
-#endif
+  if (const char* m = std::getenv("MPG_DEBUG_MARGIN")) {
+    dw.bp_margin = (float)std::atof(m);
+    dw.small_margin = std::atof(m);
   }
+#endif
   dw.debug_mode = 0;
 #ifdef MPG_DIAG  // ablation builds only (changes results)
   if (const char* e = std::getenv("MPG_DEBUG_CULL")) dw.debug_mode = std::atoi(e);
@@ -4752,6 +4851,7 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
   dw.sched_pair = I(o_sp);
   dw.sched_other = I(o_so);
   dw.sched_mid = I(o_sm);
+  dw.sched_keep = I(o_sk);
   dw.sched_srec = to_cptr<float>(base + o_ssr);
   auto F = [&](size_t o) { return to_cptr<float>(base + o); };
   BpView& bp = dw.bp;

@@ -181,3 +181,65 @@ def test_far_from_origin_world_matches_oracle():
     np.testing.assert_array_equal(f, fo)
     np.testing.assert_array_equal(m.view(np.uint32), mo)
     assert 0.05 < fo.mean() < 0.95
+
+
+RAIL_AT = (300.0, -12.0, 0.5)
+RAIL_JOINTS = ["rail_joint"] + Wd.PANDA_JOINTS
+
+
+def rail_panda_urdf(lower: float = 0.0, upper: float = 5.0) -> str:
+    """The Panda on a prismatic rail along x (limits [lower, upper] m) whose
+    base sits ~300 m from the origin."""
+    src = os.path.join(Wd.panda_dir(), "panda.urdf")
+    d = tempfile.mkdtemp(prefix="panda_rail_")
+    os.symlink(os.path.join(Wd.panda_dir(), "franka_description"), os.path.join(d, "franka_description"))
+    text = open(src).read()
+    head = text.index(">", text.index("<robot")) + 1
+    extra = ('\n  <link name="rail_base"/>\n  <joint name="rail_joint" type="prismatic">\n'
+             '    <parent link="rail_base"/>\n    <child link="panda_link0"/>\n'
+             f'    <origin xyz="{RAIL_AT[0]} {RAIL_AT[1]} {RAIL_AT[2]}" rpy="0 0 0"/>\n'
+             '    <axis xyz="1 0 0"/>\n'
+             f'    <limit effort="100" lower="{lower}" upper="{upper}" velocity="1.0"/>\n  </joint>\n')
+    path = os.path.join(d, "panda.urdf")
+    open(path, "w").write(text[:head] + extra + text[head:])
+    return path
+
+
+@pytest.mark.gpu
+def test_prismatic_rail_far_from_origin_matches_oracle():
+    """a Panda on a 5 m prismatic rail ~300 m from the origin
+    (the rail's travel enters the fp32 cull's coordinate bound), boxes along
+    the rail; 2^16 configurations in the limits plus 4096 with the rail value
+    far outside them (evaluated with every pair), every flag and pair bit vs
+    the oracle."""
+    from mplib_amd import pymp, scenes
+    urdf = rail_panda_urdf()
+    art = pymp.articulation.ArticulatedModel(urdf, os.path.join(scenes.PANDA_DIR, "panda.srdf"), [0, 0, -9.81],
+                                             RAIL_JOINTS, scenes.PANDA_LINKS, verbose=False, convex=True)
+    art.set_move_group("panda_hand")
+    w = pymp.planning_world.PlanningWorld([art], ["panda"], [], [])
+    scene, allowed = [], []
+    for copy, dx in (("a", 1.0), ("b", 3.5)):
+        for name, side, pos in scenes._boxes():
+            p = [RAIL_AT[0] + dx + pos[0], RAIL_AT[1] + pos[1], RAIL_AT[2] + pos[2]]
+            w.add_normal_object(f"{name}_{copy}", pymp.fcl.CollisionObject(pymp.fcl.Box(list(side)), p, [1, 0, 0, 0]))
+            scene.append((f"{name}_{copy}", M.BoxGeom(tuple(float(x) for x in side)),
+                          (list(M.IDENT[0]), [float(x) for x in p])))
+        w.get_allowed_collision_matrix().set_entry("panda_link0", f"table_{copy}", True)
+        allowed.append(("panda_link0", f"table_{copy}"))
+    oart = M.Articulation(urdf, os.path.join(Wd.panda_dir(), "panda.srdf"), Wd.PANDA_LINKS, RAIL_JOINTS, convex=True,
+                          move_group="panda_hand")
+    ow = oracle.OracleWorld(oart, scene=scene, allowed=allowed)
+    assert w.get_state_dim() == 8 and ow.dof == 8
+    lim = oart.joint_limits()[:8]
+    assert np.allclose(lim[0], [0.0, 5.0])
+    rng = np.random.default_rng(2024)
+    q = rng.uniform(lim[:, 0], lim[:, 1], size=(1 << 16, 8))
+    out = rng.uniform(lim[:, 0], lim[:, 1], size=(4096, 8))
+    out[:, 0] = rng.choice([-1.0, 1.0], 4096) * rng.uniform(6.0, 40.0, 4096)  # beyond the rail's travel bound
+    q = np.concatenate([q, out])
+    f, m = w.collide_batch(q)
+    fo, mo = ow.collide_batch(q, nthreads=16)
+    np.testing.assert_array_equal(f, fo)
+    np.testing.assert_array_equal(m.view(np.uint32), mo)
+    assert 0.05 < fo[:1 << 16].mean() < 0.95

@@ -222,6 +222,8 @@ def desc_arrays(ow: oracle.OracleWorld) -> dict:
         octree_leaf=np.concatenate(leaves) if leaves else np.zeros(0),
         mesh_triangle=np.concatenate(tris) if tris else np.zeros(0, np.int32),
         convex_face=np.asarray(cfaces, np.int32),
+        joint_lower=[j.lower[0] if j.nq == 1 else -np.inf for j in J],
+        joint_upper=[j.upper[0] if j.nq == 1 else np.inf for j in J],
     )
 
 
