@@ -101,7 +101,9 @@ struct DevWorld {
   cptr<double> prism_bound; // [nj] |q| bound of such a joint, 0 = none
   double pose_bound;        // link-pose input: |position| bound of every link (beyond it: every pair)
   cptr<int> all_mask;       // [W] bits of every non-allowed pair
-  cptr<float> sched_srec;   // [entries * BS_STRIDE] static partner's OBB record, inline per entry
+  cptr<float> sched_srec;   // static partners' OBB records inline, in interleaved pairs [pair][BS_STRIDE][2]
+  cptr<int> sched_pr0;      // [n_moving] first record pair of the object's near static partners
+  cptr<int> sched_pr1;      // [n_moving] first record pair of its never-near static partners
   // octrees: leaf boxes [L][6] (octree frame), per geometry a uniform grid
   // record (OG_*), cell -> leaf lists (CSR)
   cptr<double> oct_leaf;

@@ -1015,23 +1015,28 @@ __global__ __launch_bounds__(BLOCK) void cull_kernel(DevWorld w, const double* _
     }
   };
   for (int m = 0; m < w.n_moving; ++m) {
-    // link-pose input: every static partner (the reach balls assume kinematics)
+    // link-pose input: every static partner, also those the reach balls
+    // rule out (they assume kinematics)
     const int e0 = w.sched_start[m], em = w.sched_mid[m], e1 = w.sched_start[m + 1];
-    const int es = FROM_POSES ? em : w.sched_keep[m];
     if (e0 == e1) continue;
     const float* rm = cen + (size_t)m * 3 * BLOCK + tid;
     const float cm[3] = {rm[0], rm[BLOCK], rm[2 * BLOCK]};
     const float r_m = w.bp.mobj[BM_STRIDE * m + BM_R];
-    // static partners: the partner's OBB record is inline in the schedule
-    // entry (one 64-byte scalar load, no partner-index indirection), so the
-    // unrolled loop issues the next entries' loads ahead of the tests
-    for (int eb = e0; eb < es; eb += 32) {
-      const int ee = min(es, eb + 32);
-      uint32_t kb = 0u;
-#pragma unroll 4
-      for (int e = eb; e < ee; ++e)
-        kb |= (uint32_t)!fsphere_obb_separated(cm, r_m, w.sched_srec + BS_STRIDE * e, w.bp_margin) << (e - eb);
-      push(eb, kb);
+    // static partners, two per test: the partners' OBB records are inline in
+    // the schedule, interleaved in pairs (fsphere_obb_keep2: packed fp32 math
+    // on whole scalar-register pairs, no partner-index indirection)
+    for (int seg = 0; seg < (FROM_POSES ? 2 : 1); ++seg) {
+      const int s0 = seg ? w.sched_keep[m] : e0, s1 = seg ? em : w.sched_keep[m];
+      const int p0 = seg ? w.sched_pr1[m] : w.sched_pr0[m];
+      for (int eb = s0; eb < s1; eb += 32) {
+        const int ee = min(s1, eb + 32);
+        uint32_t kb = 0u;
+        int pr = p0 + ((eb - s0) >> 1);
+#pragma unroll 2
+        for (int e = eb; e < ee; e += 2, ++pr)
+          kb |= fsphere_obb_keep2(cm, r_m, w.sched_srec + 2 * BS_STRIDE * pr, w.bp_margin) << (e - eb);
+        push(eb, kb);
+      }
     }
     // moving partners: bounding spheres (the partner's centre from LDS)
     for (int eb = em; eb < e1; eb += 32) {
@@ -4644,12 +4649,34 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
   // the entry; those that can be near before those that never are), then its
   // moving partners
   std::vector<int> sched_start(d->n_moving + 1, 0), sched_mid(std::max(d->n_moving, 1), 0),
-      sched_keep(std::max(d->n_moving, 1), 0), sched_pair, sched_other;
-  std::vector<float> sched_srec;
+      sched_keep(std::max(d->n_moving, 1), 0), sched_pr0(std::max(d->n_moving, 1), 0),
+      sched_pr1(std::max(d->n_moving, 1), 0), sched_pair, sched_other;
+  std::vector<float> sched_srec;  // static records in pairs, interleaved (2 * BS_STRIDE floats per pair)
+  // a record no sphere can reach: the odd entry of a segment's last pair
+  std::vector<float> far_rec(BS_STRIDE, 0.f);
+  for (int k = 0; k < 3; ++k) far_rec[BS_C + k] = 1e15f;
+  for (int k = 0; k < 3; ++k) far_rec[BS_R + 4 * k] = 1.f;
+  std::vector<const float*> seg_recs;
+  auto flush_pairs = [&]() {  // seg_recs -> interleaved pairs
+    for (size_t i = 0; i < seg_recs.size(); i += 2) {
+      const float* ra = seg_recs[i];
+      const float* rb = i + 1 < seg_recs.size() ? seg_recs[i + 1] : far_rec.data();
+      for (int k = 0; k < BS_STRIDE; ++k) {
+        sched_srec.push_back(ra[k]);
+        sched_srec.push_back(rb[k]);
+      }
+    }
+    seg_recs.clear();
+  };
   for (int m = 0; m < d->n_moving; ++m) {
     sched_start[m] = (int)sched_pair.size();
     for (int pass = 0; pass < 3; ++pass) {  // statics that can be near, statics never near, movers
-      if (pass == 1) sched_keep[m] = (int)sched_pair.size();
+      flush_pairs();
+      if (pass == 0) sched_pr0[m] = (int)(sched_srec.size() / (2 * BS_STRIDE));
+      if (pass == 1) {
+        sched_keep[m] = (int)sched_pair.size();
+        sched_pr1[m] = (int)(sched_srec.size() / (2 * BS_STRIDE));
+      }
       if (pass == 2) sched_mid[m] = (int)sched_pair.size();
       for (int p = 0; p < d->n_pairs; ++p) {
         if (allowed[p]) continue;
@@ -4659,11 +4686,7 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
         if (pass < 2 && never_near(m, hi - d->n_moving) != (pass == 1)) continue;
         sched_pair.push_back(p);
         sched_other.push_back(hi);
-        if (pass < 2)
-          sched_srec.insert(sched_srec.end(), bpp.sobj.begin() + (size_t)BS_STRIDE * (hi - d->n_moving),
-                            bpp.sobj.begin() + (size_t)BS_STRIDE * (hi - d->n_moving + 1));
-        else
-          sched_srec.insert(sched_srec.end(), BS_STRIDE, 0.f);
+        if (pass < 2) seg_recs.push_back(bpp.sobj.data() + (size_t)BS_STRIDE * (hi - d->n_moving));
       }
     }
   }
@@ -4672,7 +4695,8 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
     sched_pair.push_back(0);
     sched_other.push_back(0);
   }
-  if (sched_srec.empty()) sched_srec.assign(BS_STRIDE, 0.f);
+  flush_pairs();
+  if (sched_srec.empty()) sched_srec.assign(2 * BS_STRIDE, 0.f);
 
   BlobBuilder bb;
   const size_t o_jt = bb.add(d->joint_type, d->n_joints);
@@ -4721,6 +4745,8 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
   const size_t o_so = bb.add(sched_other.data(), sched_other.size());
   const size_t o_sm = bb.add(sched_mid.data(), sched_mid.size());
   const size_t o_sk = bb.add(sched_keep.data(), sched_keep.size());
+  const size_t o_spr0 = bb.add(sched_pr0.data(), sched_pr0.size());
+  const size_t o_spr1 = bb.add(sched_pr1.data(), sched_pr1.size());
   const size_t o_pbd = bb.add(prism_bound.data(), prism_bound.size());
   const size_t o_amk = bb.add(all_mask.data(), all_mask.size());
   const size_t o_ssr = bb.add(sched_srec.data(), sched_srec.size());
@@ -4852,6 +4878,8 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
   dw.sched_other = I(o_so);
   dw.sched_mid = I(o_sm);
   dw.sched_keep = I(o_sk);
+  dw.sched_pr0 = I(o_spr0);
+  dw.sched_pr1 = I(o_spr1);
   dw.sched_srec = to_cptr<float>(base + o_ssr);
   auto F = [&](size_t o) { return to_cptr<float>(base + o); };
   BpView& bp = dw.bp;

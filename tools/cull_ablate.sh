@@ -7,7 +7,7 @@ set -o pipefail
 export TMPDIR=/tmp MPG_OVERLAP_MIN=0
 OUT=gpurun_out/${1:-abl}; mkdir -p $OUT
 cp mplib_amd/lib/libmpgpu.so /tmp/libmpgpu_orig.so
-cp variants/diag.so mplib_amd/lib/libmpgpu.so
+cp variants/${DIAG:-diag}.so mplib_amd/lib/libmpgpu.so
 for m in ${MODES:-0 1 2 8 9}; do
   MPG_DEBUG_CULL=$m timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $OUT/m$m -o t --output-format csv -- python3 bench.py --steps 5 --warmup 1 --cpu-sample 0 > $OUT/m$m.log 2>&1 || { cp /tmp/libmpgpu_orig.so mplib_amd/lib/libmpgpu.so; exit 1; }
   python3 -c "
