@@ -325,6 +325,24 @@ int mpg_profile_read(mpg_world *world, double *ms, int64_t *launches, int64_t *u
 int mpg_debug_collide_pairs(mpg_world *world, int32_t geom_a, int32_t geom_b, int64_t n, const double *Ta,
                             const double *Tb, uint8_t *hit);
 
+/*
+ * Planner.generate_collision_pair (mplib/planner.py:118-163), batched: n
+ * configurations of the world's state drawn uniformly in [lower, upper]
+ * (dof values each) on the device, evaluated as mpg_collide_batch does, and
+ * counts[p] (host, n_pairs) = how many of them report pair p (collide_full()
+ * of the sample).  The reference loops set_qpos(random, full=True) +
+ * collide_full() 10^6 times on the host; build the world with every joint of
+ * the planned articulations as a state value for that semantics.
+ * Sampler: value i of the batch (row-major) is lower + (upper - lower) * u,
+ * u = (splitmix64(seed + (i + 1) * 0x9E3779B97F4A7C15) >> 11) * 2^-53;
+ * mpg_sample_uniform returns the same values (host buffer, rows counted from
+ * row_offset).  dof <= 64.
+ */
+int mpg_collide_count(mpg_world *world, const double *lower, const double *upper, int64_t n, uint64_t seed,
+                      int64_t *counts, void *stream);
+int mpg_sample_uniform(const double *lower, const double *upper, int32_t dof, int64_t n, uint64_t seed,
+                       int64_t row_offset, double *q, int device);
+
 /* Diagnostics: the device sin/cos used by the FK (host buffers). */
 int mpg_debug_sincos(const double *x, int64_t n, double *s, double *c, int device);
 

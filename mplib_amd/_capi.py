@@ -62,6 +62,10 @@ SIGNATURES = {
     "mpg_world_get_info": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(WorldInfo)]),
     "mpg_set_small_batch_max": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64]),
     "mpg_release_stream": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
+    "mpg_collide_count": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
+                                         ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p]),
+    "mpg_sample_uniform": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64,
+                                          ctypes.c_uint64, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int]),
     "mpg_collide_batch": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p,
                                          ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]),
     "mpg_collide_link_poses": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p,

@@ -605,6 +605,14 @@ class PlanningWorld {
   MotionSpace motion_space();
   void check_motion_batch(const double* from, const double* to, int64_t n, double longest_valid_segment,
                           uint8_t* valid, int32_t* first_invalid, int32_t* segments);
+  // Planner.generate_collision_pair (mplib/planner.py:118-163), batched: per
+  // pair of pair_table(), how many of n random FULL configurations of the
+  // planned articulations (every joint, as set_qpos(q, full=True) sets it)
+  // drawn uniformly in the joint limits report it in collide_full()
+  std::vector<int64_t> sample_pair_counts(int64_t n, uint64_t seed);
+  // the full state those samples range over: limits per value (continuous
+  // joints [-pi, pi]), planned articulations in map order
+  std::pair<std::vector<double>, std::vector<double>> full_state_limits();
   void profile_enable(bool on);
   // host-buffer batches of at most n states take the one-launch latency path
   void set_small_batch_max(int64_t n);
@@ -634,6 +642,13 @@ class PlanningWorld {
   uint64_t world_key_ = ~0ull;
   std::vector<PairInfo> pairs_;
   int state_dim_ = 0;
+  // the same snapshot with every joint of the planned articulations a state
+  // value (sample_pair_counts)
+  std::vector<int32_t> full_src_;
+  std::vector<double> full_lo_, full_hi_;
+  int full_dof_ = 0;
+  std::unique_ptr<DeviceWorld> full_world_;
+  uint64_t full_key_ = ~0ull;
   double tol_ = 1e-6;
   int64_t small_max_ = -1;  // -1: library default
 };

@@ -692,6 +692,22 @@ PYBIND11_MODULE(pymp, m_all) {
            "Batched self_distance / distance_with_others: (d_self[N], pair_self[N], d_others[N], pair_others[N]); "
            "-1 = a penetrating pair, pair indices into get_collision_pair_info().")
       // ---- batched validity (new; one device launch for N states) ----
+      .def("sample_pair_counts",
+           [](PW& w, int64_t n, uint64_t seed) {
+             std::vector<int64_t> c;
+             {
+               py::gil_scoped_release rel;
+               c = w.sample_pair_counts(n, seed);
+             }
+             return c;
+           },
+           py::arg("n"), py::arg("seed") = 0,
+           "Planner.generate_collision_pair batched: per pair of get_collision_pair_info(), how many of n random "
+           "full configurations (every joint of the planned articulations, uniform in the joint limits, drawn on "
+           "the device) report it in collide_full().")
+      .def("get_full_state_limits",
+           [](PW& w) { return w.full_state_limits(); },
+           "(lower, upper) of the full state sample_pair_counts draws from.")
       .def("get_state_dim", &PW::state_dim)
       .def("get_mask_words", &PW::mask_words)
       .def("get_collision_pair_info",

@@ -399,6 +399,12 @@ void PlanningWorld::ensure_snapshot(const CollisionRequest& r, bool need_device)
   DescBuilder& d = *desc_;
   d.gjk_tolerance = r.gjk_tolerance;
   pairs_.clear();
+  full_src_.clear();
+  full_lo_.clear();
+  full_hi_.clear();
+  full_dof_ = 0;
+  full_world_.reset();
+  full_key_ = ~0ull;
   // ---- kinematic forest: planned articulations (map order), then unplanned
   struct ArtInfo {
     ArtPtr art;
@@ -422,6 +428,21 @@ void PlanningWorld::ensure_snapshot(const CollisionRequest& r, bool need_device)
       auto it = std::find(slots.begin(), slots.end(), s);
       if (it != slots.end()) src[j] = dof + (int)(it - slots.begin());
       else cst[j] = q[s];
+    }
+    // full-state variant: every user slot of a planned articulation
+    for (size_t j = 0; j < user_slot.size(); ++j)
+      full_src_.push_back(planned && user_slot[j] >= 0 ? full_dof_ + user_slot[j] : src[j]);
+    if (planned) {
+      std::vector<double> lo(pin->nv(), 0.0), hi(pin->nv(), 0.0);
+      for (size_t u = 0; u < pin->user_joints().size(); ++u) {
+        auto lim = pin->get_joint_limit(u, true);
+        if (lim.empty() || u >= pin->user_vidx().size()) continue;
+        lo[pin->user_vidx()[u]] = lim[0][0];
+        hi[pin->user_vidx()[u]] = lim[0][1];
+      }
+      full_lo_.insert(full_lo_.end(), lo.begin(), lo.end());
+      full_hi_.insert(full_hi_.end(), hi.begin(), hi.end());
+      full_dof_ += pin->nv();
     }
     const int link_base = (int)d.link_parent.size();
     pin->fill_kinematics(d, joint_offset, src, cst);
@@ -736,6 +757,31 @@ std::vector<PlanningWorld::StageTime> PlanningWorld::profile_read() {
 void set_global_seed(unsigned seed) {
   std::srand(seed);
   plan_rng_seed(seed);
+}
+
+}  // namespace mpgh
+
+namespace mpgh {
+
+std::pair<std::vector<double>, std::vector<double>> PlanningWorld::full_state_limits() {
+  ensure_snapshot(CollisionRequest(), false);
+  return {full_lo_, full_hi_};
+}
+
+std::vector<int64_t> PlanningWorld::sample_pair_counts(int64_t n, uint64_t seed) {
+  if (n < 0) throw std::invalid_argument("sample_pair_counts: n < 0");
+  ensure_snapshot(CollisionRequest(), false);
+  if (!full_world_ || full_key_ != desc_key_) {
+    DescBuilder f = *desc_;
+    f.joint_q_source = full_src_;
+    f.dof = full_dof_;
+    full_world_ = std::make_unique<DeviceWorld>(f, default_device());
+    full_key_ = desc_key_;
+  }
+  std::vector<int64_t> counts(pairs_.size(), 0);
+  check_status(mpg_collide_count(full_world_->get(), full_lo_.data(), full_hi_.data(), n, seed, counts.data(), nullptr),
+               "mpg_collide_count");
+  return counts;
 }
 
 }  // namespace mpgh

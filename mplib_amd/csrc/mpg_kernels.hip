@@ -3652,6 +3652,56 @@ __global__ void sincos_kernel(const double* __restrict__ x, long long n, double*
   mpg_sincos(x[i], s + i, c + i);
 }
 
+// ---------------------------------------------------------------------------
+// generate_collision_pair (mplib/planner.py:118-163), batched: random full
+// configurations drawn on the device, the pairs collide_full() reports
+// counted per pair.
+// Sampler: value i (row-major, rows counted from the call's first sample) is
+// lo + (hi - lo) * u, u = (splitmix64(seed + (i + 1) * golden) >> 11) * 2^-53
+// (mplib_amd/planner.py sample_uniform restates it on the host).
+// ---------------------------------------------------------------------------
+constexpr int kSampleMaxDof = 64;
+struct SampleRange {
+  double lo[kSampleMaxDof], hi[kSampleMaxDof];
+};
+
+__device__ __forceinline__ double splitmix_u01(uint64_t seed, uint64_t i) {
+  uint64_t z = seed + (i + 1ull) * 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  return (double)(z >> 11) * (1.0 / 9007199254740992.0);
+}
+
+__global__ __launch_bounds__(256) void sample_uniform_kernel(SampleRange r, int dof, long long n, uint64_t seed,
+                                                            long long row0, double* __restrict__ out) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n * dof) return;
+  const int k = (int)(i % dof);
+  const double u = splitmix_u01(seed, (uint64_t)(row0 * dof + i));
+  out[i] = r.lo[k] + (r.hi[k] - r.lo[k]) * u;
+}
+
+// per pair, the configurations whose pair mask has its bit: LDS counters per
+// block (atomics on the block's own copy), then one global add per pair
+__global__ __launch_bounds__(256) void pair_count_kernel(const uint32_t* __restrict__ masks, long long n, int W,
+                                                        int P, unsigned long long* __restrict__ counts) {
+  extern __shared__ uint32_t c_lds[];
+  for (int p = threadIdx.x; p < P; p += blockDim.x) c_lds[p] = 0u;
+  __syncthreads();
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+    for (int k = 0; k < W; ++k) {
+      uint32_t x = masks[i * W + k];
+      while (x) {
+        atomicAdd(&c_lds[32 * k + __builtin_ctz(x)], 1u);
+        x &= x - 1u;
+      }
+    }
+  __syncthreads();
+  for (int p = threadIdx.x; p < P; p += blockDim.x)
+    if (c_lds[p]) atomicAdd(&counts[p], (unsigned long long)c_lds[p]);
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------------------
@@ -5451,6 +5501,92 @@ int mpg_debug_collide_pairs(mpg_world* w, int32_t geom_a, int32_t geom_b, int64_
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipMemcpyAsync(hit, g.dh, (size_t)n, hipMemcpyDeviceToHost, g.s));
   HIP_TRY(hipStreamSynchronize(g.s));
+  return MPG_OK;
+}
+
+int mpg_sample_uniform(const double* lower, const double* upper, int32_t dof, int64_t n, uint64_t seed,
+                       int64_t row_offset, double* q, int device) {
+  if (dof < 0 || dof > kSampleMaxDof) return set_error(MPG_E_INVALID, "dof out of range [0, 64]");
+  if (n < 0 || row_offset < 0 || (n > 0 && dof > 0 && (!lower || !upper || !q)))
+    return set_error(MPG_E_INVALID, "bad arguments");
+  if (n == 0 || dof == 0) return MPG_OK;
+  SampleRange r{};
+  for (int k = 0; k < dof; ++k) {
+    if (!(std::isfinite(lower[k]) && std::isfinite(upper[k]) && lower[k] <= upper[k]))
+      return set_error(MPG_E_INVALID, "sampling range must be finite with lower <= upper");
+    r.lo[k] = lower[k];
+    r.hi[k] = upper[k];
+  }
+  HIP_TRY(hipSetDevice(device));
+  double* d = nullptr;
+  HIP_TRY(hipMalloc(&d, sizeof(double) * (size_t)n * dof));
+  const long long tot = (long long)n * dof;
+  hipLaunchKernelGGL(sample_uniform_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, 0, r, (int)dof,
+                     (long long)n, seed, (long long)row_offset, d);
+  hipError_t e = hipGetLastError();
+  if (e == hipSuccess) e = hipMemcpy(q, d, sizeof(double) * (size_t)tot, hipMemcpyDeviceToHost);
+  hipFree(d);
+  if (e != hipSuccess) return set_error(MPG_E_HIP, std::string("mpg_sample_uniform: ") + hipGetErrorString(e));
+  return MPG_OK;
+}
+
+int mpg_collide_count(mpg_world* w, const double* lower, const double* upper, int64_t n, uint64_t seed,
+                      int64_t* counts, void* stream) {
+  if (!w) return set_error(MPG_E_INVALID, "world is NULL");
+  const int dof = w->dw.dof, P = w->dw.n_pairs, W = w->dw.W;
+  if (dof > kSampleMaxDof) return set_error(MPG_E_UNSUPPORTED, "mpg_collide_count supports dof <= 64");
+  if (n < 0 || (P > 0 && !counts) || (dof > 0 && (!lower || !upper))) return set_error(MPG_E_INVALID, "bad arguments");
+  if ((size_t)P * sizeof(uint32_t) > 64 * 1024) return set_error(MPG_E_UNSUPPORTED, "mpg_collide_count supports <= 16384 pairs");
+  for (int p = 0; p < P; ++p) counts[p] = 0;
+  if (n == 0 || P == 0) return MPG_OK;
+  SampleRange r{};
+  for (int k = 0; k < dof; ++k) {
+    if (!(std::isfinite(lower[k]) && std::isfinite(upper[k]) && lower[k] <= upper[k]))
+      return set_error(MPG_E_INVALID, "sampling range must be finite with lower <= upper");
+    r.lo[k] = lower[k];
+    r.hi[k] = upper[k];
+  }
+  HIP_TRY(hipSetDevice(w->device));
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const long long chunk = std::min<long long>(n, w->max_chunk);
+  struct Bufs {  // freed on every exit path, after the stream drained
+    double* q = nullptr;
+    uint8_t* fl = nullptr;
+    uint32_t* mk = nullptr;
+    unsigned long long* cnt = nullptr;
+    hipStream_t s = nullptr;
+    ~Bufs() {
+      hipStreamSynchronize(s);
+      hipFree(q);
+      hipFree(fl);
+      hipFree(mk);
+      hipFree(cnt);
+    }
+  } b;
+  b.s = s;
+  HIP_TRY(hipMalloc(&b.q, sizeof(double) * (size_t)chunk * std::max(dof, 1)));
+  HIP_TRY(hipMalloc(&b.fl, (size_t)chunk));
+  HIP_TRY(hipMalloc(&b.mk, sizeof(uint32_t) * (size_t)chunk * W));
+  HIP_TRY(hipMalloc(&b.cnt, sizeof(unsigned long long) * P));
+  HIP_TRY(hipMemsetAsync(b.cnt, 0, sizeof(unsigned long long) * P, s));
+  for (long long off = 0; off < n; off += chunk) {
+    const long long m = std::min(chunk, n - off);
+    if (dof > 0) {
+      const long long tot = m * dof;
+      hipLaunchKernelGGL(sample_uniform_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, r, dof, m, seed,
+                         off, b.q);
+      HIP_TRY(hipGetLastError());
+    }
+    const int rc = launch_collide_overlapped<false>(w, b.q, m, b.fl, b.mk, s);
+    if (rc) return rc;
+    const unsigned grid = (unsigned)std::min<long long>(1024, (m + 255) / 256);
+    hipLaunchKernelGGL(pair_count_kernel, dim3(grid), dim3(256), sizeof(uint32_t) * P, s, b.mk, m, W, P, b.cnt);
+    HIP_TRY(hipGetLastError());
+  }
+  std::vector<unsigned long long> h(P);
+  HIP_TRY(hipMemcpyAsync(h.data(), b.cnt, sizeof(unsigned long long) * P, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  for (int p = 0; p < P; ++p) counts[p] = (int64_t)h[p];
   return MPG_OK;
 }
 
