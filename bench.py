@@ -52,7 +52,8 @@ def parse():
                    help="2, 3, 4: BASELINE collide configs; 5: RRTConnect plan(); 6: floor point cloud; "
                         "7: cfg3 with BVH mesh links (convex=False)")
     p.add_argument("--goal", default="far", help="cfg5 goal (scenes.PLAN_GOALS)")
-    p.add_argument("--cpu-plans", type=int, default=4, help="cfg5: plans timed with the CPU oracle checker")
+    p.add_argument("--cpu-plans", type=int, default=-1,
+                   help="cfg5: plans timed with the CPU oracle checker (-1: the same seeds as the GPU run, 0: none)")
     p.add_argument("--per-gpu", type=int, default=0, help="configs per GPU per step (default: BASELINE size)")
     p.add_argument("--cpu-sample", type=int, default=1 << 17,
                    help="configs timed on the CPU oracle for cpu_baseline (rank 0, N=1 only; 0 = skip)")
@@ -311,7 +312,7 @@ def plan_main(args, world, rank, local, backend):
         rt.append(time.perf_counter() - t1)
     result_rt = {"one_state_round_trip_us_median": float(np.median(rt) * 1e6),
                  "one_state_round_trip_us_p90": float(np.percentile(rt, 90) * 1e6)}
-    if rank == 0 and world == 1 and args.cpu_plans > 0:
+    if rank == 0 and world == 1 and args.cpu_plans != 0:
         import ctypes
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         import oracle  # test infrastructure: the CPU baseline's checker
@@ -323,7 +324,7 @@ def plan_main(args, world, rank, local, backend):
         cpu.set_native_state_validity_checker(ctypes.cast(oracle.lib().orc_validity_batch, ctypes.c_void_p).value,
                                               ctypes.addressof(ow._w))
         cpu.set_speculative_connect(False)  # OMPL's serial loop: one batch per growTree
-        k = min(args.cpu_plans, args.steps)
+        k = args.steps if args.cpu_plans < 0 else min(args.cpu_plans, args.steps)
         same = True
         t0 = time.perf_counter()
         for i in range(k):
