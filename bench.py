@@ -179,15 +179,26 @@ def main():
                                                 "SQ_INSTS_VALU_TRANS_F64"))
             # the PMC kernel is the dominant stage's main kernel (narrow_kernel / cull_kernel); its duration is
             # the live event time of the stage launch
-            issue_s = (k["SQ_INSTS_VALU"] + f64) * VALU_ISSUE_CYCLES / (SIMDS * CLOCK_HZ)
-            valu = {"bound": "valu", "achieved": issue_s / kernel_s, "peak": 1.0, "unit": "issue-port fraction",
-                    "frac": issue_s / kernel_s, "valu_insts_per_launch": k["SQ_INSTS_VALU"],
+            issue_cyc = (k["SQ_INSTS_VALU"] + f64) * VALU_ISSUE_CYCLES / SIMDS  # per SIMD
+            clk = k.get("clock_ghz")
+            # the measured clock (GRBM_GUI_ACTIVE / 8 / dispatch time in the PMC pass), else the nominal one
+            hz = clk * 1e9 if clk else CLOCK_HZ
+            frac_live = issue_cyc / (hz * kernel_s)
+            # the same kernel alone in the PMC pass: VALU issue cycles over its own active cycles
+            frac_pmc = issue_cyc / (k["GRBM_GUI_ACTIVE"] / 8.0) if k.get("GRBM_GUI_ACTIVE") else None
+            valu = {"bound": "valu", "achieved": frac_live, "peak": 1.0, "unit": "issue-port fraction",
+                    "frac": frac_live, "frac_alone": frac_pmc, "clock_ghz": clk,
+                    "clock_source": "GRBM_GUI_ACTIVE/8/dispatch ns (PMC pass)" if clk else "nominal 2.4 GHz",
+                    "pmc_dispatch_ms": k.get("pmc_dispatch_ns", 0.0) / 1e6 or None,
+                    "valu_insts_per_launch": k["SQ_INSTS_VALU"],
                     "fp64_insts_per_launch": f64,
                     "lane_activity": (k["SQ_THREAD_CYCLES_VALU"] / (64.0 * k["SQ_ACTIVE_INST_VALU"])
                                       if k.get("SQ_ACTIVE_INST_VALU") else None),
                     "wait_frac": (k["SQ_WAIT_ANY"] / k["SQ_WAVE_CYCLES"] if k.get("SQ_WAVE_CYCLES") else None),
-                    "note": "VALU instructions x 2 issue cycles (fp64 counted twice) over 1024 SIMDs x 2.4 GHz "
-                            "x the kernel's live duration; PMC counts from " + pm.get("source", "?")}
+                    "note": "VALU instructions x 2 issue cycles (fp64 counted twice) per SIMD over the measured "
+                            "clock x the kernel's live duration (frac; the two halves' kernels overlap on two "
+                            "streams) and over its active cycles when it runs alone in the PMC pass (frac_alone); "
+                            "PMC counts from " + pm.get("source", "?")}
 
     result = {
         "metric": "configs/sec full collide() Panda-7DoF+10 boxes" if cfg == 3 else f"configs/sec collide() cfg{cfg}",

@@ -1484,6 +1484,66 @@ __device__ __forceinline__ CV3 msupport_box(const GObj& a, const ccd_real* h, co
   return vsub(vadd(quat_rot(la, a.rot), a.pos), vadd(quat_rot(lb, b.rot), b.pos));
 }
 
+// The occupied leaves of octree `go` listed in the grid cells under the box
+// [blo, bhi] (octree frame), handed out one per lane: the cells of the range
+// 64 at a time (one per lane, loads in parallel), then a wave prefix sum of
+// their leaf counts gives the leaves 64 at a time.  leaf_hit(leaf) -> bool;
+// true as soon as some lane's leaf hits.  Wave-uniform inputs.  (A leaf in
+// several cells may be tested more than once: the answer is an OR.)
+template <typename F>
+__device__ __forceinline__ bool octree_range_any(const DevWorld& w, int go, const double* blo, const double* bhi,
+                                                 F leaf_hit) {
+  const cptr<double> og = w.oct_grid + OG_STRIDE * go;
+  const double inv = og[OG_INV];
+  int c0[3], c1[3], dims[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    dims[i] = (int)og[OG_DIMS + i];
+    const double f0 = std::floor((blo[i] - og[OG_ORIGIN + i]) * inv);
+    const double f1 = std::floor((bhi[i] - og[OG_ORIGIN + i]) * inv);
+    if (f1 < 0.0 || f0 >= (double)dims[i]) return false;
+    c0[i] = f0 < 0.0 ? 0 : (int)f0;
+    c1[i] = f1 >= (double)dims[i] ? dims[i] - 1 : (int)f1;
+  }
+  __shared__ int s_k0[4][64], s_end[4][64];  // per wave of the 256-thread block
+  const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
+  const int cell0 = (int)og[OG_CELL0];
+  const int nx = c1[0] - c0[0] + 1, ny = c1[1] - c0[1] + 1, nz = c1[2] - c0[2] + 1;
+  const int ncell = nx * ny * nz;
+  for (int cb = 0; cb < ncell; cb += 64) {
+    const int ci = cb + (int)lane;
+    int k0 = 0, cnt = 0;
+    if (ci < ncell) {
+      const int z = ci % nz, y = (ci / nz) % ny, x = ci / (nz * ny);
+      const int cell = cell0 + ((c0[0] + x) * dims[1] + (c0[1] + y)) * dims[2] + (c0[2] + z);
+      k0 = w.oct_cells[cell];
+      cnt = w.oct_cells[cell + 1] - k0;
+    }
+    const uint32_t incl = wave_inclusive_scan((uint32_t)cnt, lane);
+    const int total = (int)__builtin_amdgcn_readlane(incl, 63);
+    s_k0[wv][lane] = k0;
+    s_end[wv][lane] = (int)incl;
+    __builtin_amdgcn_wave_barrier();
+    for (int ib = 0; ib < total; ib += 64) {
+      const int j = ib + (int)lane;
+      bool hit = false;
+      if (j < total) {
+        int lo = 0, hi = 63;  // first cell slot whose inclusive end exceeds j
+        while (lo < hi) {
+          const int mid = (lo + hi) >> 1;
+          if (s_end[wv][mid] > j) hi = mid;
+          else lo = mid + 1;
+        }
+        const int start = lo > 0 ? s_end[wv][lo - 1] : 0;
+        hit = leaf_hit(w.oct_list[s_k0[wv][lo] + (j - start)]);
+      }
+      if (__ballot(hit) != 0) return true;
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+  return false;
+}
+
 // One lane's (shape, octree) pair: fcl OcTreeSolver::OcTreeShapeIntersectRecurse
 // [ext FCL 0.7.0] reduced to its result -- some occupied leaf whose OBB
 // overlaps the shape's OBB (computeBV(shape, I) -> convertBV(., tf), then
@@ -1545,18 +1605,6 @@ __device__ __forceinline__ bool octree_wave(const DevWorld& w, cptr<double> HV, 
     bhi[i] = fmin(cl[i] + hq[i], base + ep + pad);
     if (blo[i] > bhi[i]) return false;
   }
-  const cptr<double> og = w.oct_grid + OG_STRIDE * go;
-  const double inv = og[OG_INV];
-  int c0[3], c1[3], dims[3];
-#pragma unroll
-  for (int i = 0; i < 3; ++i) {
-    dims[i] = (int)og[OG_DIMS + i];
-    const double f0 = std::floor((blo[i] - og[OG_ORIGIN + i]) * inv);
-    const double f1 = std::floor((bhi[i] - og[OG_ORIGIN + i]) * inv);
-    if (f1 < 0.0 || f0 >= (double)dims[i]) return false;
-    c0[i] = f0 < 0.0 ? 0 : (int)f0;
-    c1[i] = f1 >= (double)dims[i] ? dims[i] - 1 : (int)f1;
-  }
   GObj A, B;  // A: the leaf box (rotation of the octree, per-leaf centre), B: the shape
   A.rot = gjk_rot_from_matrix(TO.R);
   A.rot_inv = quat_invert2(A.rot);
@@ -1612,45 +1660,7 @@ __device__ __forceinline__ bool octree_wave(const DevWorld& w, cptr<double> HV, 
     }
     return res > 0;
   };
-  // cells of the range 64 at a time (one per lane, loads in parallel); a
-  // wave prefix sum of their leaf counts hands out the leaves 64 at a time
-  __shared__ int s_k0[4][64], s_end[4][64];  // per wave of the 256-thread block
-  const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
-  const int cell0 = (int)og[OG_CELL0];
-  const int nx = c1[0] - c0[0] + 1, ny = c1[1] - c0[1] + 1, nz = c1[2] - c0[2] + 1;
-  const int ncell = nx * ny * nz;
-  for (int cb = 0; cb < ncell; cb += 64) {
-    const int ci = cb + (int)lane;
-    int k0 = 0, cnt = 0;
-    if (ci < ncell) {
-      const int z = ci % nz, y = (ci / nz) % ny, x = ci / (nz * ny);
-      const int cell = cell0 + ((c0[0] + x) * dims[1] + (c0[1] + y)) * dims[2] + (c0[2] + z);
-      k0 = w.oct_cells[cell];
-      cnt = w.oct_cells[cell + 1] - k0;
-    }
-    const uint32_t incl = wave_inclusive_scan((uint32_t)cnt, lane);
-    const int total = (int)__builtin_amdgcn_readlane(incl, 63);
-    s_k0[wv][lane] = k0;
-    s_end[wv][lane] = (int)incl;
-    __builtin_amdgcn_wave_barrier();
-    for (int ib = 0; ib < total; ib += 64) {
-      const int j = ib + (int)lane;
-      bool hit = false;
-      if (j < total) {
-        int lo = 0, hi = 63;  // first cell slot whose inclusive end exceeds j
-        while (lo < hi) {
-          const int mid = (lo + hi) >> 1;
-          if (s_end[wv][mid] > j) hi = mid;
-          else lo = mid + 1;
-        }
-        const int start = lo > 0 ? s_end[wv][lo - 1] : 0;
-        hit = leaf_hit(w.oct_list[s_k0[wv][lo] + (j - start)]);
-      }
-      if (__ballot(hit) != 0) return true;
-    }
-    __builtin_amdgcn_wave_barrier();
-  }
-  return false;
+  return octree_range_any(w, go, blo, bhi, leaf_hit);
 }
 
 
@@ -2007,6 +2017,133 @@ __device__ __forceinline__ bool mesh_shape_wave(const DevWorld& w, cptr<double> 
   return false;
 }
 
+// libccd support of (box, per-lane half sizes h) - (triangle, per-lane: its
+// vertices P and centroid tc in the mesh frame, rotation/position of b)
+__device__ __forceinline__ CV3 msupport_box_tri(const GObj& a, const ccd_real* h, const GObj& b, const CV3* P,
+                                                const CV3& tc, const CV3& dir) {
+  const CV3 da = quat_rot(dir, a.rot_inv), db = quat_rot(vscale(dir, ccd_real(-1)), b.rot_inv);
+  const CV3 la = CV3{(da.x >= 0 ? ccd_real(1) : ccd_real(-1)) * h[0], (da.y >= 0 ? ccd_real(1) : ccd_real(-1)) * h[1],
+                     (da.z >= 0 ? ccd_real(1) : ccd_real(-1)) * h[2]};
+  ccd_real maxdot = -FLT_MAX;
+  CV3 lb = P[0];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const ccd_real dot = vdot(db, vsub(P[i], tc));
+    if (dot > maxdot) {
+      lb = P[i];
+      maxdot = dot;
+    }
+  }
+  return vsub(vadd(quat_rot(la, a.rot), a.pos), vadd(quat_rot(lb, b.rot), b.pos));
+}
+
+// fcl::collide(mesh, OcTree) in either order [ext FCL 0.7.0 OcTreeSolver::
+// OcTreeMeshIntersectRecurse; MeshOcTreeIntersect passes the tree first]:
+// some (occupied leaf, triangle) whose shapeTriangleIntersect(Box(leaf),
+// box_tf, P1, P2, P3, tf_mesh) -- libccd MPR, leaf box first, triangle GJK
+// object second -- reports a hit (oracle mesh_octree_intersect).  The
+// traversal's BV tests only prune genuinely separated pairs, so every pair
+// within libccd's false-hit reach is run.  Leaves: the octree grid cells under
+// the mesh's box (octree frame, padded), one leaf per lane; each lane walks
+// the mesh's cluster boxes and triangle boxes against its leaf's box in the
+// mesh frame (padded) and runs MPR on the survivors.  Wave-uniform inputs.
+__device__ __forceinline__ bool mesh_octree_wave(const DevWorld& w, int gm, const SE3& TM, int go, const SE3& TO) {
+  const cptr<double> grm = w.geom_rec + G_STRIDE * gm;
+  const double pad = kMeshShapePad * (1.0 + std::fabs(TO.p[0]) + std::fabs(TO.p[1]) + std::fabs(TO.p[2]) +
+                                      std::fabs(TM.p[0]) + std::fabs(TM.p[1]) + std::fabs(TM.p[2]));
+  double Rm[9], Ro[9];  // Rm = TO.R^T TM.R (mesh axes in the octree frame), Ro = Rm^T
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      Rm[3 * i + j] = (TO.R[i] * TM.R[j] + TO.R[3 + i] * TM.R[3 + j]) + TO.R[6 + i] * TM.R[6 + j];
+      Ro[3 * j + i] = Rm[3 * i + j];
+    }
+  // the mesh's local box (G_OBB) in the octree frame, padded
+  double mcw[3], blo[3], bhi[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+    mcw[i] = ((TM.R[3 * i] * grm[G_OBB_C] + TM.R[3 * i + 1] * grm[G_OBB_C + 1]) + TM.R[3 * i + 2] * grm[G_OBB_C + 2]) +
+             TM.p[i];
+  const double dmo[3] = {mcw[0] - TO.p[0], mcw[1] - TO.p[1], mcw[2] - TO.p[2]};
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const double c = (TO.R[i] * dmo[0] + TO.R[3 + i] * dmo[1]) + TO.R[6 + i] * dmo[2];
+    const double e = ((std::fabs(Rm[3 * i]) * grm[G_OBB_E] + std::fabs(Rm[3 * i + 1]) * grm[G_OBB_E + 1]) +
+                      std::fabs(Rm[3 * i + 2]) * grm[G_OBB_E + 2]) * (1.0 + 1e-9) + 1e-9 + pad;
+    blo[i] = c - e;
+    bhi[i] = c + e;
+  }
+  GObj A, B;  // A: the leaf box (octree rotation, per-leaf centre), B: the mesh frame of the triangles
+  A.rot = gjk_rot_from_matrix(TO.R);
+  A.rot_inv = quat_invert2(A.rot);
+  A.geom = go;
+  A.type = MPG_GEOM_BOX;
+  B.rot = gjk_rot_from_matrix(TM.R);
+  B.rot_inv = quat_invert2(B.rot);
+  B.pos = cv3(TM.p[0], TM.p[1], TM.p[2]);
+  B.geom = gm;
+  B.type = MPG_GEOM_MESH;
+  const int c0 = w.mesh_tree[2 * gm], c1 = c0 + w.mesh_tree[2 * gm + 1];
+  auto leaf_hit = [&](int leaf) -> bool {
+    const cptr<double> L = w.oct_leaf + 6 * (size_t)leaf;
+    bool out = false;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) out |= L[i] > bhi[i] || L[3 + i] < blo[i];
+    if (out) return false;
+    double c[3], side[3], cw[3], cm[3], hm[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      c[i] = (L[i] + L[3 + i]) * 0.5;
+      side[i] = L[3 + i] - L[i];
+    }
+#pragma unroll
+    for (int i = 0; i < 3; ++i) cw[i] = ((TO.R[3 * i] * c[0] + TO.R[3 * i + 1] * c[1]) + TO.R[3 * i + 2] * c[2]) + TO.p[i];
+    const double dm[3] = {cw[0] - TM.p[0], cw[1] - TM.p[1], cw[2] - TM.p[2]};
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {  // the leaf box in the mesh frame: centre, padded half extents
+      cm[i] = (TM.R[i] * dm[0] + TM.R[3 + i] * dm[1]) + TM.R[6 + i] * dm[2];
+      hm[i] = ((std::fabs(Ro[3 * i]) * side[0] + std::fabs(Ro[3 * i + 1]) * side[1]) + std::fabs(Ro[3 * i + 2]) * side[2]) *
+                  0.5 * (1.0 + 1e-9) + 1e-9 + pad;
+    }
+    GObj A1 = A;
+    A1.pos = cv3(cw[0], cw[1], cw[2]);
+    const ccd_real h[3] = {(ccd_real)(side[0] / 2.0), (ccd_real)(side[1] / 2.0), (ccd_real)(side[2] / 2.0)};  // boxToGJK
+    for (int cl = c0; cl < c1; ++cl) {
+      const cptr<double> bx = w.mesh_node + 6 * (size_t)cl;
+      bool away = false;
+#pragma unroll
+      for (int i = 0; i < 3; ++i) away |= bx[i] > cm[i] + hm[i] || bx[3 + i] < cm[i] - hm[i];
+      if (away) continue;
+      const int t1 = w.mesh_link[2 * cl] + w.mesh_link[2 * cl + 1];
+      for (int t = w.mesh_link[2 * cl]; t < t1; ++t) {
+        const cptr<double> rec = w.mesh_tri + TR_STRIDE * (size_t)t;
+        bool o2 = false;
+#pragma unroll
+        for (int i = 0; i < 3; ++i) o2 |= rec[TR_LO + i] > cm[i] + hm[i] || rec[TR_HI + i] < cm[i] - hm[i];
+        if (o2) continue;
+        double P[9];
+#pragma unroll
+        for (int k = 0; k < 9; ++k) P[k] = rec[TR_P + k];
+        // triCreateGJKObject: centre in fp64, then vertices and centre as ccd_real
+        const CV3 tc = cv3((P[0] + P[3] + P[6]) / 3, (P[1] + P[4] + P[7]) / 3, (P[2] + P[5] + P[8]) / 3);
+        const CV3 TP[3] = {cv3(P[0], P[1], P[2]), cv3(P[3], P[4], P[5]), cv3(P[6], P[7], P[8])};
+        int st;
+        CV3 v0, v1, v2, v3_, dir;
+        mpr_begin(A1.pos, vadd(quat_rot(tc, B.rot), B.pos), st, v0, dir);
+        int res = 0;
+        while (res == 0) {
+          const CV3 sp = msupport_box_tri(A1, h, B, TP, tc, dir);
+          res = mpr_advance(w.mpr_tol, sp, st, v0, v1, v2, v3_, dir);
+        }
+        if (res > 0) return true;
+      }
+    }
+    return false;
+  };
+  return octree_range_any(w, go, blo, bhi, leaf_hit);
+}
+
 // every active lane's (TA, TB) candidate of the (wave-uniform) mesh or
 // octree pair (ga, gb), one after the other with the whole wave; bit k =
 // lane k's hit
@@ -2034,6 +2171,8 @@ __device__ __forceinline__ unsigned long long walk_wave_eval(const DevWorld& w, 
       if (w.dbg(am && bm ? 5 : 6)) continue;
       bool h;
       if (am && bm) h = mesh_mesh_wave(w, ga, A, gb, B);
+      else if (tgb == MPG_GEOM_OCTREE) h = mesh_octree_wave(w, ga, A, gb, B);
+      else if (tga == MPG_GEOM_OCTREE) h = mesh_octree_wave(w, gb, B, ga, A);
       else if (am) h = mesh_shape_wave(w, HV, ga, A, gb, B);
       else h = mesh_shape_wave(w, HV, gb, B, ga, A);
       if (h) hits |= 1ull << k;
@@ -2044,16 +2183,42 @@ __device__ __forceinline__ unsigned long long walk_wave_eval(const DevWorld& w, 
 
 
 
-// Refill idle lanes once at least this many are idle (a refill is two loads
-// and the MPR start once the pose pass has built the GJK objects)
+// Refill idle lanes once at least this many are idle.  A refill hands out
+// candidates whose GJK objects and MPR start were staged in LDS beforehand
+// (all 64 lanes compute the chain FK of the next 64 candidates at once), so
+// it costs a few LDS reads and can run every few steps.
 #ifndef MPG_REFILL_MIN
-#define MPG_REFILL_MIN 32
+#define MPG_REFILL_MIN 8
 #endif
 // take the next task early once the current one is handed out and this many
 // lanes are idle: a task of the same pair continues without a drain
 #ifndef MPG_STEAL_MIN
 #define MPG_STEAL_MIN 64
 #endif
+
+// staged candidate of the narrow phase: per moving object its GJK rotation,
+// inverse rotation and position (11 floats), then the MPR start v0 and dir
+enum { STG_A = 0, STG_B = 11, STG_V0 = 22, STG_DIR = 25, STG_N = 28 };
+
+__device__ __forceinline__ void stage_obj(float (*stg)[64], int c0, uint32_t slot, const GObj& o) {
+  stg[c0 + 0][slot] = o.rot.x;
+  stg[c0 + 1][slot] = o.rot.y;
+  stg[c0 + 2][slot] = o.rot.z;
+  stg[c0 + 3][slot] = o.rot.w;
+  stg[c0 + 4][slot] = o.rot_inv.x;
+  stg[c0 + 5][slot] = o.rot_inv.y;
+  stg[c0 + 6][slot] = o.rot_inv.z;
+  stg[c0 + 7][slot] = o.rot_inv.w;
+  stg[c0 + 8][slot] = o.pos.x;
+  stg[c0 + 9][slot] = o.pos.y;
+  stg[c0 + 10][slot] = o.pos.z;
+}
+
+__device__ __forceinline__ void unstage_obj(float (*stg)[64], int c0, uint32_t slot, GObj& o) {
+  o.rot = CQ4{stg[c0 + 0][slot], stg[c0 + 1][slot], stg[c0 + 2][slot], stg[c0 + 3][slot]};
+  o.rot_inv = CQ4{stg[c0 + 4][slot], stg[c0 + 5][slot], stg[c0 + 6][slot], stg[c0 + 7][slot]};
+  o.pos = CV3{stg[c0 + 8][slot], stg[c0 + 9][slot], stg[c0 + 10][slot]};
+}
 
 template <bool FROM_POSES>
 __global__ __launch_bounds__(256) MPG_NARROW_WAVES void narrow_kernel(DevWorld w, const double* __restrict__ in,
@@ -2068,6 +2233,10 @@ __global__ __launch_bounds__(256) MPG_NARROW_WAVES void narrow_kernel(DevWorld w
   const cptr<double> HV = w.hull;
   const uint32_t lane = lane_id();
   const uint32_t total = prefix[w.n_pairs], ts = prefix[w.n_pairs + 2];
+  __shared__ float s_stage[4][STG_N][64];
+  __shared__ uint32_t s_cfg[4][64];
+  float (*stg)[64] = s_stage[threadIdx.x >> 6];
+  uint32_t* scfg = s_cfg[threadIdx.x >> 6];
   // dynamic task queue: waves that drew cheap tasks take more.
   // The first task of every wave is its wave index (the counter starts past
   // them): half the atomics on the one counter, which a small batch's waves
@@ -2099,14 +2268,23 @@ __global__ __launch_bounds__(256) MPG_NARROW_WAVES void narrow_kernel(DevWorld w
     GObj A, B;
     if (!am) A = static_obj(w, a - w.n_moving);
     if (!bm) B = static_obj(w, b - w.n_moving);
+    if (am) {
+      A.geom = w.moving_geom[a];
+      A.type = w.geom_type[A.geom];
+    }
+    if (bm) {
+      B.geom = w.moving_geom[b];
+      B.type = w.geom_type[B.geom];
+    }
     CV3 v0, v1, v2, v3, dir;
+    uint32_t sh = 0, sn = 0;  // staged candidates: [sh, sn) not yet handed out
 #ifdef MPG_STATS
     int nsteps = 0;
 #endif
     for (;;) {
       const unsigned long long idle = __ballot(st == MPR_DONE);
       const uint32_t n_idle = (uint32_t)__popcll(idle);
-      if (next >= t1 && pend == 0xffffffffu && more && n_idle >= MPG_STEAL_MIN) {
+      if (next >= t1 && sh == sn && pend == 0xffffffffu && more && n_idle >= MPG_STEAL_MIN) {
         const uint32_t t2 = fetch();
         if (t2 >= total) {
           more = false;
@@ -2120,22 +2298,50 @@ __global__ __launch_bounds__(256) MPG_NARROW_WAVES void narrow_kernel(DevWorld w
 #ifdef MPG_STATS
       const unsigned long long c0 = __builtin_amdgcn_s_memtime();
 #endif
-      if (next < t1 && (n_idle >= MPG_REFILL_MIN || n_idle == 64)) {  // refill the idle lanes
-        if (st == MPR_DONE) {
+      if ((sh < sn || next < t1) && (n_idle >= MPG_REFILL_MIN || n_idle == 64)) {
+        if (sh == sn) {  // stage the next <= 64 candidates: chain FK and MPR start with every lane
+          const uint32_t cnt = min(64u, t1 - next);
+          if (lane < cnt) {
+            const long long c = cl[next + lane];
+            GObj sa = A, sb = B;
+            if (am) sa = moving_obj<FROM_POSES>(w, in, sc, c, a);
+            if (bm) sb = moving_obj<FROM_POSES>(w, in, sc, c, b);
+            int s0;
+            CV3 w0, d0;
+            mpr_begin(center(w, sa), center(w, sb), s0, w0, d0);
+            scfg[lane] = (uint32_t)c;
+            if (am) stage_obj(stg, STG_A, lane, sa);
+            if (bm) stage_obj(stg, STG_B, lane, sb);
+            stg[STG_V0][lane] = w0.x;
+            stg[STG_V0 + 1][lane] = w0.y;
+            stg[STG_V0 + 2][lane] = w0.z;
+            stg[STG_DIR][lane] = d0.x;
+            stg[STG_DIR + 1][lane] = d0.y;
+            stg[STG_DIR + 2][lane] = d0.z;
+          }
+          wave_lds_sync();
+          sh = 0;
+          sn = cnt;
+          next += cnt;
+        }
+        if (st == MPR_DONE) {  // hand the staged candidates to the idle lanes
           const uint32_t rank =
               __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
-          const uint32_t idx = next + rank;
-          if (idx < t1) {
-            cfg = cl[idx];
-            if (am) A = moving_obj<FROM_POSES>(w, in, sc, cfg, a);
-            if (bm) B = moving_obj<FROM_POSES>(w, in, sc, cfg, b);
-            mpr_begin(center(w, A), center(w, B), st, v0, dir);
+          if (rank < sn - sh) {
+            const uint32_t k = sh + rank;
+            cfg = scfg[k];
+            if (am) unstage_obj(stg, STG_A, k, A);
+            if (bm) unstage_obj(stg, STG_B, k, B);
+            v0 = CV3{stg[STG_V0][k], stg[STG_V0 + 1][k], stg[STG_V0 + 2][k]};
+            dir = CV3{stg[STG_DIR][k], stg[STG_DIR + 1][k], stg[STG_DIR + 2][k]};
+            st = MPR_V1;
 #ifdef MPG_STATS
             nsteps = 0;
 #endif
           }
         }
-        next = min(t1, next + n_idle);
+        sh = min(sn, sh + n_idle);
+        wave_lds_sync();  // every read done before the next staging overwrites
       }
 #ifdef MPG_STATS
       const unsigned long long c1 = __builtin_amdgcn_s_memtime();
@@ -2147,7 +2353,7 @@ __global__ __launch_bounds__(256) MPG_NARROW_WAVES void narrow_kernel(DevWorld w
       }
 #endif
       if (__ballot(st != MPR_DONE) == 0) {
-        if (next >= t1 && (pend != 0xffffffffu || !more)) break;
+        if (next >= t1 && sh == sn && (pend != 0xffffffffu || !more)) break;
         continue;
       }
 #ifdef MPG_STATS
@@ -2359,7 +2565,7 @@ __global__ __launch_bounds__(256) void debug_pairs_kernel(DevWorld w, int ga, in
 // minimum.  Same algorithm as the oracle (oracle/collide_oracle.c
 // gjk_distance); the north star's bar vs FCL's GJK is 1e-5.
 // ---------------------------------------------------------------------------
-constexpr int kPoseStride = 12;  // rot xyzw, pos xyz, world OBB centre xyz, pad
+constexpr int kPoseStride = 20;  // rot xyzw, pos xyz, world OBB centre xyz, fp64 rotation (mesh pairs), pad
 
 template <bool FROM_POSES>
 __global__ __launch_bounds__(128) void pose_kernel(DevWorld w, const double* __restrict__ in, long long n,
@@ -2381,6 +2587,8 @@ __global__ __launch_bounds__(128) void pose_kernel(DevWorld w, const double* __r
     for (int i = 0; i < 3; ++i)
       g[(7 + i) * n] = ((T.R[3 * i] * gr[G_OBB_C] + T.R[3 * i + 1] * gr[G_OBB_C + 1]) + T.R[3 * i + 2] * gr[G_OBB_C + 2]) +
                        T.p[i];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) g[(10 + i) * n] = T.R[i];
   };
   if (FROM_POSES) {
     for (int m = 0; m < w.n_moving; ++m)
@@ -2620,6 +2828,367 @@ __device__ __forceinline__ GObj pose_obj(const DevWorld& w, const double* __rest
   return static_obj(w, sid);
 }
 
+// fp64 transform of object `id` for configuration cfg (pose_kernel fields)
+__device__ __forceinline__ SE3 pose_se3(const DevWorld& w, const double* __restrict__ poses, long long n, long long cfg,
+                                        int id) {
+  if (id >= w.n_moving) return load_se3(w.static_T + 12 * (id - w.n_moving));
+  const double* g = poses + ((size_t)id * kPoseStride) * n + cfg;
+  SE3 T;
+#pragma unroll
+  for (int i = 0; i < 9; ++i) T.R[i] = g[(10 + i) * n];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) T.p[i] = g[(4 + i) * n];
+  return T;
+}
+
+// ---------------------------------------------------------------------------
+// Distance with BVH meshes (fcl::distance on BVHModel<OBBRSS>, FCL 0.7.0):
+//   mesh-shape   MeshShapeDistanceTraversalNodeOBBRSS: min over triangles of
+//                shapeTriangleDistance(shape, tf, P1, P2, P3, tf_mesh) (GJK,
+//                shape first; -1 once one intersects)
+//   mesh-mesh    MeshDistanceTraversalNodeOBBRSS: min of triDistance over the
+//                triangle pairs, B's triangles in A's frame (0 if one pair
+//                intersects)
+//   mesh-OcTree  OcTreeMeshDistanceRecurse: min over (leaf box, triangle) of
+//                shapeTriangleDistance(box, box_tf, ...), box first
+// The traversal only skips what cannot lower the running minimum; here the
+// cluster and triangle boxes are skipped when their lower bound exceeds the
+// running minimum by more than the float support rounding (mesh_dist_slack
+// in the oracle).  One lane per configuration, as distance_kernel.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ double mesh_dist_slack(const SE3& A, const SE3& B) {
+  return 1e-5 * (1.0 + std::fabs(A.p[0]) + std::fabs(A.p[1]) + std::fabs(A.p[2]) + std::fabs(B.p[0]) +
+                 std::fabs(B.p[1]) + std::fabs(B.p[2]));
+}
+
+// distance from point c to the box [lo, hi]
+__device__ __forceinline__ double point_box_distance(const double* c, const double* lo, const double* hi) {
+  double s = 0.0;
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const double e = fmax(fmax(lo[i] - c[i], c[i] - hi[i]), 0.0);
+    s += e * e;
+  }
+  return std::sqrt(s);
+}
+
+// PQP TriDist as FCL's TriangleDistance::segPoints / triDistance (oracle
+// seg_points / tri_face_case / tri_distance, same operation order)
+__device__ void seg_points(const double* P, const double* A, const double* Q, const double* B, double* VEC, double* X,
+                           double* Y) {
+  double T[3], TMP[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) T[k] = Q[k] - P[k];
+  const double AA = d3(A, A), BB = d3(B, B), AB = d3(A, B), AT = d3(A, T), BT = d3(B, T);
+  const double denom = AA * BB - AB * AB;
+  double t = (AT * BB - BT * AB) / denom;
+  if (t < 0 || std::isnan(t)) t = 0;
+  else if (t > 1) t = 1;
+  const double u = (t * AB - BT) / BB;
+  if (u <= 0 || std::isnan(u)) {
+    for (int k = 0; k < 3; ++k) Y[k] = Q[k];
+    t = AT / AA;
+    if (t <= 0 || std::isnan(t)) {
+      for (int k = 0; k < 3; ++k) {
+        X[k] = P[k];
+        VEC[k] = Q[k] - P[k];
+      }
+    } else if (t >= 1) {
+      for (int k = 0; k < 3; ++k) {
+        X[k] = P[k] + A[k];
+        VEC[k] = Q[k] - X[k];
+      }
+    } else {
+      for (int k = 0; k < 3; ++k) X[k] = P[k] + A[k] * t;
+      c3(TMP, T, A);
+      c3(VEC, A, TMP);
+    }
+  } else if (u >= 1) {
+    for (int k = 0; k < 3; ++k) Y[k] = Q[k] + B[k];
+    t = (AB + AT) / AA;
+    if (t <= 0 || std::isnan(t)) {
+      for (int k = 0; k < 3; ++k) {
+        X[k] = P[k];
+        VEC[k] = Y[k] - P[k];
+      }
+    } else if (t >= 1) {
+      for (int k = 0; k < 3; ++k) {
+        X[k] = P[k] + A[k];
+        VEC[k] = Y[k] - X[k];
+      }
+    } else {
+      for (int k = 0; k < 3; ++k) {
+        X[k] = P[k] + A[k] * t;
+        T[k] = Y[k] - P[k];
+      }
+      c3(TMP, T, A);
+      c3(VEC, A, TMP);
+    }
+  } else {
+    for (int k = 0; k < 3; ++k) Y[k] = Q[k] + B[k] * u;
+    if (t <= 0 || std::isnan(t)) {
+      for (int k = 0; k < 3; ++k) X[k] = P[k];
+      c3(TMP, T, B);
+      c3(VEC, B, TMP);
+    } else if (t >= 1) {
+      for (int k = 0; k < 3; ++k) {
+        X[k] = P[k] + A[k];
+        T[k] = Q[k] - X[k];
+      }
+      c3(TMP, T, B);
+      c3(VEC, B, TMP);
+    } else {
+      for (int k = 0; k < 3; ++k) X[k] = P[k] + A[k] * t;
+      c3(VEC, A, B);
+      if (d3(VEC, T) < 0)
+        for (int k = 0; k < 3; ++k) VEC[k] = -VEC[k];
+    }
+  }
+}
+
+__device__ bool tri_face_case(const double* S, const double* Sv, const double* T, bool& disjoint, double& dist) {
+  double Sn[3], V[3], Z[3], Tp[3];
+  c3(Sn, Sv, Sv + 3);
+  const double Snl = d3(Sn, Sn);
+  if (!(Snl > 1e-15)) return false;
+  for (int i = 0; i < 3; ++i) {
+    for (int k = 0; k < 3; ++k) V[k] = S[k] - T[3 * i + k];
+    Tp[i] = d3(V, Sn);
+  }
+  int point = -1;
+  if (Tp[0] > 0 && Tp[1] > 0 && Tp[2] > 0) {
+    point = Tp[0] < Tp[1] ? 0 : 1;
+    if (Tp[2] < Tp[point]) point = 2;
+  } else if (Tp[0] < 0 && Tp[1] < 0 && Tp[2] < 0) {
+    point = Tp[0] > Tp[1] ? 0 : 1;
+    if (Tp[2] > Tp[point]) point = 2;
+  }
+  if (point < 0) return false;
+  disjoint = true;
+  for (int e = 0; e < 3; ++e) {
+    for (int k = 0; k < 3; ++k) V[k] = T[3 * point + k] - S[3 * e + k];
+    c3(Z, Sn, Sv + 3 * e);
+    if (!(d3(V, Z) > 0)) return false;
+  }
+  double D[3];
+  const double s = Tp[point] / Snl;
+  for (int k = 0; k < 3; ++k) D[k] = (T[3 * point + k] + Sn[k] * s) - T[3 * point + k];
+  dist = std::sqrt(d3(D, D));
+  return true;
+}
+
+// S, T: 3 vertices each, row-major [3][3]
+__device__ double tri_distance(const double* S, const double* T) {
+  double Sv[9], Tv[9], VEC[3], P[3], Q[3], V[3], Z[3];
+  for (int k = 0; k < 3; ++k) {
+    Sv[k] = S[3 + k] - S[k];
+    Sv[3 + k] = S[6 + k] - S[3 + k];
+    Sv[6 + k] = S[k] - S[6 + k];
+    Tv[k] = T[3 + k] - T[k];
+    Tv[3 + k] = T[6 + k] - T[3 + k];
+    Tv[6 + k] = T[k] - T[6 + k];
+  }
+  bool shown_disjoint = false;
+  for (int k = 0; k < 3; ++k) V[k] = S[k] - T[k];
+  double mindd = d3(V, V) + 1;
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) {
+      seg_points(S + 3 * i, Sv + 3 * i, T + 3 * j, Tv + 3 * j, VEC, P, Q);
+      for (int k = 0; k < 3; ++k) V[k] = Q[k] - P[k];
+      const double dd = d3(V, V);
+      if (dd <= mindd) {
+        mindd = dd;
+        const int i2 = (i + 2) % 3, j2 = (j + 2) % 3;
+        for (int k = 0; k < 3; ++k) Z[k] = S[3 * i2 + k] - P[k];
+        double a = d3(Z, VEC);
+        for (int k = 0; k < 3; ++k) Z[k] = T[3 * j2 + k] - Q[k];
+        double b = d3(Z, VEC);
+        if (a <= 0 && b >= 0) return std::sqrt(dd);
+        const double p = d3(V, VEC);
+        if (a < 0) a = 0;
+        if (b > 0) b = 0;
+        if (p - a + b > 0) shown_disjoint = true;
+      }
+    }
+  double d;
+  if (tri_face_case(S, Sv, T, shown_disjoint, d)) return d;
+  if (tri_face_case(T, Tv, S, shown_disjoint, d)) return d;
+  return shown_disjoint ? std::sqrt(mindd) : 0.0;
+}
+
+__device__ __forceinline__ GObj mesh_frame_obj(int gm, const SE3& TM) {
+  GObj B;
+  B.rot = gjk_rot_from_matrix(TM.R);
+  B.rot_inv = quat_invert2(B.rot);
+  B.pos = cv3(TM.p[0], TM.p[1], TM.p[2]);
+  B.geom = gm;
+  B.type = MPG_GEOM_MESH;
+  return B;
+}
+
+// point p (world) in the frame T
+__device__ __forceinline__ void to_frame(const SE3& T, const double* p, double* o) {
+  const double d[3] = {p[0] - T.p[0], p[1] - T.p[1], p[2] - T.p[2]};
+#pragma unroll
+  for (int i = 0; i < 3; ++i) o[i] = (T.R[i] * d[0] + T.R[3 + i] * d[1]) + T.R[6 + i] * d[2];
+}
+
+// min over triangles of GJK(shape S, triangle), or something >= best when no
+// triangle can beat the running minimum `best`
+__device__ double mesh_shape_distance_lane(const DevWorld& w, cptr<double> HV, int gm, const SE3& TM, const GObj& S,
+                                           const SE3& TS, double best) {
+  const cptr<double> grs = w.geom_rec + G_STRIDE * S.geom;
+  double cs[3], csm[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+    cs[i] = ((TS.R[3 * i] * grs[G_OBB_C] + TS.R[3 * i + 1] * grs[G_OBB_C + 1]) + TS.R[3 * i + 2] * grs[G_OBB_C + 2]) + TS.p[i];
+  to_frame(TM, cs, csm);
+  const double rs = grs[G_RADIUS], slack = mesh_dist_slack(TM, TS);
+  const GObj B = mesh_frame_obj(gm, TM);
+  const CV3 ca = center(w, S);
+  const int c0 = w.mesh_tree[2 * gm], c1 = c0 + w.mesh_tree[2 * gm + 1];
+  for (int cl = c0; cl < c1 && best != -1.0; ++cl) {
+    const cptr<double> bx = w.mesh_node + 6 * (size_t)cl;
+    const double lo[3] = {bx[0], bx[1], bx[2]}, hi[3] = {bx[3], bx[4], bx[5]};
+    if (point_box_distance(csm, lo, hi) - rs > best + slack) continue;
+    const int t1 = w.mesh_link[2 * cl] + w.mesh_link[2 * cl + 1];
+    for (int t = w.mesh_link[2 * cl]; t < t1 && best != -1.0; ++t) {
+      const cptr<double> rec = w.mesh_tri + TR_STRIDE * (size_t)t;
+      const double tlo[3] = {rec[TR_LO], rec[TR_LO + 1], rec[TR_LO + 2]}, thi[3] = {rec[TR_HI], rec[TR_HI + 1], rec[TR_HI + 2]};
+      if (point_box_distance(csm, tlo, thi) - rs > best + slack) continue;
+      double P[9];
+#pragma unroll
+      for (int k = 0; k < 9; ++k) P[k] = rec[TR_P + k];
+      const CV3 tc = cv3((P[0] + P[3] + P[6]) / 3, (P[1] + P[4] + P[7]) / 3, (P[2] + P[5] + P[8]) / 3);
+      const CV3 TP[3] = {cv3(P[0], P[1], P[2]), cv3(P[3], P[4], P[5]), cv3(P[6], P[7], P[8])};
+      const double d = gjk_distance_from(vsub(to_v3(ca), to_v3(vadd(quat_rot(tc, B.rot), B.pos))),
+                                         [&](const CV3& dir) { return msupport_tri(w, HV, S, B, TP, tc, dir); });
+      if (d < best) best = d;
+    }
+  }
+  return best;
+}
+
+// min of triDistance over (triangle of A, triangle of B in A's frame)
+__device__ double mesh_mesh_distance_lane(const DevWorld& w, int ga, const SE3& TA, int gb, const SE3& TB, double best) {
+  double R[9], T[3];
+  const double dt[3] = {TB.p[0] - TA.p[0], TB.p[1] - TA.p[1], TB.p[2] - TA.p[2]};
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+#pragma unroll
+    for (int j = 0; j < 3; ++j) R[3 * i + j] = (TA.R[i] * TB.R[j] + TA.R[3 + i] * TB.R[3 + j]) + TA.R[6 + i] * TB.R[6 + j];
+    T[i] = (TA.R[i] * dt[0] + TA.R[3 + i] * dt[1]) + TA.R[6 + i] * dt[2];
+  }
+  const double slack = mesh_dist_slack(TA, TB);
+  const int a0 = w.mesh_tree[2 * ga], a1 = a0 + w.mesh_tree[2 * ga + 1];
+  const int b0 = w.mesh_tree[2 * gb], b1 = b0 + w.mesh_tree[2 * gb + 1];
+  for (int cb = b0; cb < b1 && best != 0.0; ++cb) {
+    const cptr<double> bb = w.mesh_node + 6 * (size_t)cb;
+    double cc[3], cca[3], e2 = 0.0;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      cc[k] = (bb[k] + bb[3 + k]) * 0.5;
+      e2 += (bb[3 + k] - bb[k]) * (bb[3 + k] - bb[k]);
+    }
+    const double rb = 0.5 * std::sqrt(e2) * (1.0 + 1e-9) + 1e-9;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) cca[i] = ((R[3 * i] * cc[0] + R[3 * i + 1] * cc[1]) + R[3 * i + 2] * cc[2]) + T[i];
+    for (int ca = a0; ca < a1 && best != 0.0; ++ca) {
+      const cptr<double> ba = w.mesh_node + 6 * (size_t)ca;
+      const double lo[3] = {ba[0], ba[1], ba[2]}, hi[3] = {ba[3], ba[4], ba[5]};
+      if (point_box_distance(cca, lo, hi) - rb > best + slack) continue;
+      const int tb1 = w.mesh_link[2 * cb] + w.mesh_link[2 * cb + 1];
+      for (int tb = w.mesh_link[2 * cb]; tb < tb1 && best != 0.0; ++tb) {
+        const cptr<double> rq = w.mesh_tri + TR_STRIDE * (size_t)tb;
+        double Q[9], qc[3], qr = 0.0;
+#pragma unroll
+        for (int v = 0; v < 3; ++v)
+#pragma unroll
+          for (int i = 0; i < 3; ++i)
+            Q[3 * v + i] = ((R[3 * i] * rq[3 * v] + R[3 * i + 1] * rq[3 * v + 1]) + R[3 * i + 2] * rq[3 * v + 2]) + T[i];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) qc[i] = (Q[i] + Q[3 + i] + Q[6 + i]) / 3.0;
+#pragma unroll
+        for (int v = 0; v < 3; ++v) {
+          const double dx = Q[3 * v] - qc[0], dy = Q[3 * v + 1] - qc[1], dz = Q[3 * v + 2] - qc[2];
+          qr = fmax(qr, dx * dx + dy * dy + dz * dz);
+        }
+        qr = std::sqrt(qr) * (1.0 + 1e-9) + 1e-9;
+        if (point_box_distance(qc, lo, hi) - qr > best + slack) continue;
+        const int ta1 = w.mesh_link[2 * ca] + w.mesh_link[2 * ca + 1];
+        for (int ta = w.mesh_link[2 * ca]; ta < ta1; ++ta) {
+          const cptr<double> rp = w.mesh_tri + TR_STRIDE * (size_t)ta;
+          const double tlo[3] = {rp[TR_LO], rp[TR_LO + 1], rp[TR_LO + 2]}, thi[3] = {rp[TR_HI], rp[TR_HI + 1], rp[TR_HI + 2]};
+          if (point_box_distance(qc, tlo, thi) - qr > best + slack) continue;
+          double P[9];
+#pragma unroll
+          for (int k = 0; k < 9; ++k) P[k] = rp[TR_P + k];
+          const double d = tri_distance(P, Q);
+          if (d < best) best = d;
+          if (best == 0.0) break;
+        }
+      }
+    }
+  }
+  return best;
+}
+
+// min over (occupied leaf box, triangle) of GJK(box, triangle)
+__device__ double mesh_octree_distance_lane(const DevWorld& w, int gm, const SE3& TM, int go, const SE3& TO, double best) {
+  const cptr<double> grm = w.geom_rec + G_STRIDE * gm, go_rec = w.geom_rec + G_STRIDE * go;
+  const int l0 = (int)go_rec[G_PARAM], ln = (int)go_rec[G_PARAM + 1];
+  double mcw[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+    mcw[i] = ((TM.R[3 * i] * grm[G_OBB_C] + TM.R[3 * i + 1] * grm[G_OBB_C + 1]) + TM.R[3 * i + 2] * grm[G_OBB_C + 2]) + TM.p[i];
+  const double rm = grm[G_RADIUS], slack = mesh_dist_slack(TM, TO);
+  const GObj B = mesh_frame_obj(gm, TM);
+  GObj A;
+  A.rot = gjk_rot_from_matrix(TO.R);
+  A.rot_inv = quat_invert2(A.rot);
+  A.geom = go;
+  A.type = MPG_GEOM_BOX;
+  const int c0 = w.mesh_tree[2 * gm], c1 = c0 + w.mesh_tree[2 * gm + 1];
+  for (int l = l0; l < l0 + ln && best != -1.0; ++l) {
+    const cptr<double> L = w.oct_leaf + 6 * (size_t)l;
+    double c[3], side[3], cw[3], cm[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      c[i] = (L[i] + L[3 + i]) * 0.5;
+      side[i] = L[3 + i] - L[i];
+    }
+#pragma unroll
+    for (int i = 0; i < 3; ++i) cw[i] = ((TO.R[3 * i] * c[0] + TO.R[3 * i + 1] * c[1]) + TO.R[3 * i + 2] * c[2]) + TO.p[i];
+    const double rl = 0.5 * std::sqrt((side[0] * side[0] + side[1] * side[1]) + side[2] * side[2]) * (1.0 + 1e-9) + 1e-9;
+    const double dx = cw[0] - mcw[0], dy = cw[1] - mcw[1], dz = cw[2] - mcw[2];
+    if (std::sqrt(dx * dx + dy * dy + dz * dz) - rl - rm > best + slack) continue;
+    to_frame(TM, cw, cm);
+    GObj A1 = A;
+    A1.pos = cv3(cw[0], cw[1], cw[2]);
+    const ccd_real h[3] = {(ccd_real)(side[0] / 2.0), (ccd_real)(side[1] / 2.0), (ccd_real)(side[2] / 2.0)};
+    for (int cl = c0; cl < c1 && best != -1.0; ++cl) {
+      const cptr<double> bx = w.mesh_node + 6 * (size_t)cl;
+      const double lo[3] = {bx[0], bx[1], bx[2]}, hi[3] = {bx[3], bx[4], bx[5]};
+      if (point_box_distance(cm, lo, hi) - rl > best + slack) continue;
+      const int t1 = w.mesh_link[2 * cl] + w.mesh_link[2 * cl + 1];
+      for (int t = w.mesh_link[2 * cl]; t < t1 && best != -1.0; ++t) {
+        const cptr<double> rec = w.mesh_tri + TR_STRIDE * (size_t)t;
+        const double tlo[3] = {rec[TR_LO], rec[TR_LO + 1], rec[TR_LO + 2]}, thi[3] = {rec[TR_HI], rec[TR_HI + 1], rec[TR_HI + 2]};
+        if (point_box_distance(cm, tlo, thi) - rl > best + slack) continue;
+        double P[9];
+#pragma unroll
+        for (int k = 0; k < 9; ++k) P[k] = rec[TR_P + k];
+        const CV3 tc = cv3((P[0] + P[3] + P[6]) / 3, (P[1] + P[4] + P[7]) / 3, (P[2] + P[5] + P[8]) / 3);
+        const CV3 TP[3] = {cv3(P[0], P[1], P[2]), cv3(P[3], P[4], P[5]), cv3(P[6], P[7], P[8])};
+        const double d = gjk_distance_from(vsub(to_v3(A1.pos), to_v3(vadd(quat_rot(tc, B.rot), B.pos))),
+                                           [&](const CV3& dir) { return msupport_box_tri(A1, h, B, TP, tc, dir); });
+        if (d < best) best = d;
+      }
+    }
+  }
+  return best;
+}
+
 __global__ __launch_bounds__(128) void distance_kernel(DevWorld w, const double* __restrict__ poses, long long n,
                                                        int n_self, double* __restrict__ d_self,
                                                        int32_t* __restrict__ p_self, double* __restrict__ d_others,
@@ -2638,6 +3207,21 @@ __global__ __launch_bounds__(128) void distance_kernel(DevWorld w, const double*
     const GObj A = pose_obj(w, poses, n, cfg, a, ca);
     const GObj B = pose_obj(w, poses, n, cfg, b, cb);
     const double ra = w.geom_rec[G_STRIDE * A.geom + G_RADIUS], rb = w.geom_rec[G_STRIDE * B.geom + G_RADIUS];
+    if (w.pair_cf[p] == CF_MESH) {
+      if (!live || best[g] == -1.0) continue;
+      const SE3 TA = pose_se3(w, poses, n, cfg, a), TB = pose_se3(w, poses, n, cfg, b);
+      double d;
+      if (A.type == MPG_GEOM_MESH && B.type == MPG_GEOM_MESH) d = mesh_mesh_distance_lane(w, A.geom, TA, B.geom, TB, best[g]);
+      else if (A.type == MPG_GEOM_OCTREE) d = mesh_octree_distance_lane(w, B.geom, TB, A.geom, TA, best[g]);
+      else if (B.type == MPG_GEOM_OCTREE) d = mesh_octree_distance_lane(w, A.geom, TA, B.geom, TB, best[g]);
+      else if (A.type == MPG_GEOM_MESH) d = mesh_shape_distance_lane(w, HV, A.geom, TA, B, TB, best[g]);
+      else d = mesh_shape_distance_lane(w, HV, B.geom, TB, A, TA, best[g]);
+      if (d < best[g]) {
+        best[g] = d;
+        bp[g] = p;
+      }
+      continue;
+    }
     if (w.pair_cf[p] == CF_OCTREE) {  // the octree is the pair's static side (b, or a through the C ABI)
       if (!live || best[g] == -1.0) continue;
       const bool oa = A.type == MPG_GEOM_OCTREE;  // distance is symmetric: leaf box first either way
@@ -3975,9 +4559,6 @@ int validate(const mpg_world_desc* d) {
     const int a = d->pair_a[p], b = d->pair_b[p];
     if (a < 0 || a >= nobj || b < 0 || b >= nobj) return set_error(MPG_E_INVALID, "pair object id out of range");
     if (a >= d->n_moving && b >= d->n_moving) return set_error(MPG_E_INVALID, "static-static pair");
-    const int ta = obj_geom_type(d, a), tb = obj_geom_type(d, b);
-    if ((ta == MPG_GEOM_MESH && tb == MPG_GEOM_OCTREE) || (ta == MPG_GEOM_OCTREE && tb == MPG_GEOM_MESH))
-      return set_error(MPG_E_UNSUPPORTED, "BVH mesh vs OcTree pairs are not supported");
     // FCL 0.7.0 GJKSolver_libccd: box-box, sphere-sphere, sphere-box,
     // sphere-capsule and sphere-cylinder have closed forms (all on the
     // device, closed_form_kind); every other shape pair is MPR
@@ -5322,7 +5903,6 @@ int mpg_distance_batch(mpg_world* w, const double* q, int64_t n, int32_t n_self_
   if (n > 0 && ((!q && w->dw.dof > 0) || !d_self || !p_self || !d_others || !p_others))
     return set_error(MPG_E_INVALID, "NULL buffer");
   if (mem != MPG_MEM_HOST && mem != MPG_MEM_DEVICE) return set_error(MPG_E_INVALID, "bad mem kind");
-  if (w->has_mesh) return set_error(MPG_E_UNSUPPORTED, "distance to a BVH mesh is not implemented on the device");
   if (n == 0) return MPG_OK;
   HIP_TRY(hipSetDevice(w->device));
   hipStream_t s = static_cast<hipStream_t>(stream);

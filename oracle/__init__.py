@@ -55,6 +55,7 @@ def lib():
         _lib.orc_contact_batch.restype = ctypes.c_int
         _lib.orc_tri_tri.restype = ctypes.c_int
         _lib.orc_sphere_tri.restype = ctypes.c_int
+        _lib.orc_tri_distance.restype = ctypes.c_double
     return _lib
 
 
@@ -121,6 +122,13 @@ def tri_tri(P, Q) -> bool:
     a = np.ascontiguousarray(P, dtype=np.float64).reshape(9)
     b = np.ascontiguousarray(Q, dtype=np.float64).reshape(9)
     return bool(lib().orc_tri_tri(a.ctypes.data_as(_DP), b.ctypes.data_as(_DP)))
+
+
+def tri_distance(P, Q) -> float:
+    """FCL TriangleDistance::triDistance (PQP TriDist) of two triangles ([3, 3] each)."""
+    a = np.ascontiguousarray(P, dtype=np.float64).reshape(9)
+    b = np.ascontiguousarray(Q, dtype=np.float64).reshape(9)
+    return float(lib().orc_tri_distance(a.ctypes.data_as(_DP), b.ctypes.data_as(_DP)))
 
 
 def sphere_tri(radius: float, centre, P) -> bool:
@@ -269,13 +277,6 @@ class OracleWorld:
                 raise TypeError(f"oracle: unsupported geometry {type(g)}")
         pairs, self.n_self_pairs = self._pair_table()
         self.pairs = pairs
-        kinds = {KIND_ROBOT: [o.geom for o in art.objects], KIND_ATTACHED: [a[2] for a in self.attached],
-                 KIND_SCENE: [sc[1] for sc in self.scene]}
-        for p in pairs:
-            ga, gb = kinds[p[0]][p[1]], kinds[p[2]][p[3]]
-            if isinstance(ga, M.MeshGeom) or isinstance(gb, M.MeshGeom):
-                if isinstance(ga, M.OcTreeGeom) or isinstance(gb, M.OcTreeGeom):
-                    raise NotImplementedError("oracle: BVH mesh vs OcTree")
         self.W = max(1, (len(pairs) + 31) // 32)
         allowed = [1 if frozenset((p[4], p[5])) in self.allowed else 0 for p in pairs]
 

@@ -2121,11 +2121,106 @@ static int mesh_mesh_intersect(const orc_world *w, int ga, const real *TA, int g
     return hit;
 }
 
+/* triCreateGJKObject(P1, P2, P3, tf_mesh): the mesh transform, the vertices
+ * and their centroid (computed in double, stored as ccd_real) */
+static void tri_gjk_obj(const orc_world *w, int gm, const gjk_obj *frame, int t, gjk_obj *tri) {
+    const real *P[3];
+    mesh_tri_points(w, gm, t, P);
+    *tri = *frame;
+    tri->type = GEOM_TRIANGLE;
+    for (int k = 0; k < 3; ++k) ccdVec3Set(&tri->tp[k], P[k][0], P[k][1], P[k][2]);
+    ccdVec3Set(&tri->tc, (P[0][0] + P[1][0] + P[2][0]) / 3, (P[0][1] + P[1][1] + P[2][1]) / 3,
+               (P[0][2] + P[1][2] + P[2][2]) / 3);
+}
+
+/* world-space vertices and bounding spheres of a mesh's triangles */
+static void mesh_world_tris(const orc_world *w, int gm, const real *TM, real (*Wt)[9], real (*S)[4]) {
+    const int t0 = (int)w->geom_param[4 * gm], tn = (int)w->geom_param[4 * gm + 1];
+    for (int t = 0; t < tn; ++t) {
+        const real *P[3];
+        mesh_tri_points(w, gm, t0 + t, P);
+        for (int k = 0; k < 3; ++k) tf_point(TM, P[k], Wt[t] + 3 * k);
+        const real *Wp[3] = {Wt[t], Wt[t] + 3, Wt[t] + 6};
+        bsphere(Wp, 3, S[t], &S[t][3]);
+    }
+}
+
+/* occupied leaf l of an octree as FCL's constructBox: side = max - min,
+ * box_tf = tf * Translation(centre) */
+static void octree_leaf_box(const orc_world *w, int l, const real *TO, real side[3], real TL[12]) {
+    const real *L = w->oct_leaf + 6 * (size_t)l;
+    real c[3];
+    for (int k = 0; k < 3; ++k) { c[k] = (L[k] + L[3 + k]) * 0.5; side[k] = L[3 + k] - L[k]; }
+    for (int k = 0; k < 9; ++k) TL[k] = TO[k];
+    for (int i = 0; i < 3; ++i) TL[9 + i] = ((TO[3 * i] * c[0] + TO[3 * i + 1] * c[1]) + TO[3 * i + 2] * c[2]) + TO[9 + i];
+}
+
+static void leaf_box_obj(const real side[3], const real TL[12], gjk_obj *box) {
+    memset(box, 0, sizeof *box);
+    shape_to_gjk(TL, box);
+    box->type = GEOM_BOX;
+    for (int k = 0; k < 3; ++k) box->dim[k] = side[k] / 2.0; /* boxToGJK */
+}
+
+/* fcl::collide(mesh, OcTree) in either order [ext FCL 0.7.0
+ * OcTreeSolver::OcTreeMeshIntersectRecurse; MeshOcTreeIntersect calls it with
+ * the tree first]: the leaf test is shapeTriangleIntersect(Box(leaf), box_tf,
+ * P1, P2, P3, tf_mesh) -- libccd MPR with the leaf box first and the triangle
+ * GJK object second (there is no box-triangle closed form in
+ * GJKSolver_libccd).  The traversal only prunes disjoint bounding volumes, so
+ * the answer is "some (occupied leaf, triangle) pair's MPR reports a hit";
+ * here every pair whose bounding spheres lie within libccd's false-hit reach
+ * is run (as mesh_shape_intersect does for shapes). */
+static int mesh_octree_intersect(const orc_world *w, int gm, const real *TM, int go, const real *TO, orc_stats *st) {
+    const int t0 = (int)w->geom_param[4 * gm], tn = (int)w->geom_param[4 * gm + 1];
+    const int l0 = (int)w->geom_param[4 * go], ln = (int)w->geom_param[4 * go + 1];
+    if (tn <= 0 || ln <= 0) return 0;
+    real (*Wt)[9] = malloc(sizeof(real) * 9 * (size_t)tn);
+    real (*S)[4] = malloc(sizeof(real) * 4 * (size_t)tn);
+    mesh_world_tris(w, gm, TM, Wt, S);
+    real lo[3], hi[3];  /* the mesh's world AABB -> one sphere around it */
+    for (int k = 0; k < 3; ++k) { lo[k] = DBL_MAX; hi[k] = -DBL_MAX; }
+    for (int t = 0; t < tn; ++t)
+        for (int v = 0; v < 3; ++v)
+            for (int k = 0; k < 3; ++k) { lo[k] = fmin(lo[k], Wt[t][3 * v + k]); hi[k] = fmax(hi[k], Wt[t][3 * v + k]); }
+    real mc[3], dm[3];
+    for (int k = 0; k < 3; ++k) { mc[k] = (lo[k] + hi[k]) * 0.5; dm[k] = hi[k] - lo[k]; }
+    const real mr = 0.5 * sqrt(dot3(dm, dm)) * (1.0 + 1e-9) + 1e-9;
+    const real pad = 1.001 * sqrt(sqrt((double)CCD_EPS)) + 1e-5 * (1.0 + fabs(TO[9]) + fabs(TO[10]) + fabs(TO[11]) +
+                                                                 fabs(TM[9]) + fabs(TM[10]) + fabs(TM[11]));
+    gjk_obj frame;
+    memset(&frame, 0, sizeof frame);
+    shape_to_gjk(TM, &frame);
+    frame.stats = st;
+    int hit = 0;
+    for (int l = l0; l < l0 + ln && !hit; ++l) {
+        real side[3], TL[12];
+        octree_leaf_box(w, l, TO, side, TL);
+        const real rl = 0.5 * sqrt(dot3(side, side)) * (1.0 + 1e-9) + 1e-9;
+        const real dc[3] = {TL[9] - mc[0], TL[10] - mc[1], TL[11] - mc[2]};
+        if (sqrt(dot3(dc, dc)) > rl + mr + pad) continue;
+        gjk_obj box, tri;
+        leaf_box_obj(side, TL, &box);
+        box.stats = st;
+        for (int t = 0; t < tn; ++t) {
+            const real d[3] = {TL[9] - S[t][0], TL[10] - S[t][1], TL[11] - S[t][2]};
+            if (sqrt(dot3(d, d)) > rl + S[t][3] + pad) continue;
+            tri_gjk_obj(w, gm, &frame, t0 + t, &tri);
+            if (mpr_intersect(&box, &tri, 1e-6)) { hit = 1; break; }
+        }
+    }
+    free(Wt);
+    free(S);
+    return hit;
+}
+
 /* 1/0 for a mesh pair, -1 when neither side is a mesh */
 static int mesh_intersect(const orc_world *w, int ga, const real *Ta, int gb, const real *Tb, orc_stats *st) {
     const int ta = w->geom_type[ga], tb = w->geom_type[gb];
     if (ta != GEOM_MESH && tb != GEOM_MESH) return -1;
     if (ta == GEOM_MESH && tb == GEOM_MESH) return mesh_mesh_intersect(w, ga, Ta, gb, Tb);
+    if (ta == GEOM_OCTREE) return mesh_octree_intersect(w, gb, Tb, ga, Ta, st);
+    if (tb == GEOM_OCTREE) return mesh_octree_intersect(w, ga, Ta, gb, Tb, st);
     if (ta == GEOM_MESH) return mesh_shape_intersect(w, ga, Ta, gb, Tb, st);
     return mesh_shape_intersect(w, gb, Tb, ga, Ta, st);
 }
@@ -2228,6 +2323,263 @@ static double octree_distance(const orc_world *w, int go, const real *TO, const 
     return best;
 }
 
+/* PQP TriDist as FCL 0.7.0 TriangleDistance::segPoints / triDistance
+ * restate it [ext fcl/narrowphase/detail/primitive_shape_algorithm/
+ * triangle_distance-inl.h]: closest points of segments (P, P + A) and
+ * (Q, Q + B); VEC is the separating direction the slab test uses. */
+static void seg_points(const real *P, const real *A, const real *Q, const real *B, real *VEC, real *X, real *Y) {
+    real T[3], TMP[3];
+    for (int k = 0; k < 3; ++k) T[k] = Q[k] - P[k];
+    const real AA = dot3(A, A), BB = dot3(B, B), AB = dot3(A, B), AT = dot3(A, T), BT = dot3(B, T);
+    const real denom = AA * BB - AB * AB;
+    real t = (AT * BB - BT * AB) / denom;
+    if (t < 0 || isnan(t)) t = 0;
+    else if (t > 1) t = 1;
+    real u = (t * AB - BT) / BB;
+    if (u <= 0 || isnan(u)) {
+        for (int k = 0; k < 3; ++k) Y[k] = Q[k];
+        t = AT / AA;
+        if (t <= 0 || isnan(t)) {
+            for (int k = 0; k < 3; ++k) { X[k] = P[k]; VEC[k] = Q[k] - P[k]; }
+        } else if (t >= 1) {
+            for (int k = 0; k < 3; ++k) { X[k] = P[k] + A[k]; VEC[k] = Q[k] - X[k]; }
+        } else {
+            for (int k = 0; k < 3; ++k) X[k] = P[k] + A[k] * t;
+            cross3(TMP, T, A);
+            cross3(VEC, A, TMP);
+        }
+    } else if (u >= 1) {
+        for (int k = 0; k < 3; ++k) Y[k] = Q[k] + B[k];
+        t = (AB + AT) / AA;
+        if (t <= 0 || isnan(t)) {
+            for (int k = 0; k < 3; ++k) { X[k] = P[k]; VEC[k] = Y[k] - P[k]; }
+        } else if (t >= 1) {
+            for (int k = 0; k < 3; ++k) { X[k] = P[k] + A[k]; VEC[k] = Y[k] - X[k]; }
+        } else {
+            for (int k = 0; k < 3; ++k) { X[k] = P[k] + A[k] * t; T[k] = Y[k] - P[k]; }
+            cross3(TMP, T, A);
+            cross3(VEC, A, TMP);
+        }
+    } else {
+        for (int k = 0; k < 3; ++k) Y[k] = Q[k] + B[k] * u;
+        if (t <= 0 || isnan(t)) {
+            for (int k = 0; k < 3; ++k) X[k] = P[k];
+            cross3(TMP, T, B);
+            cross3(VEC, B, TMP);
+        } else if (t >= 1) {
+            for (int k = 0; k < 3; ++k) { X[k] = P[k] + A[k]; T[k] = Q[k] - X[k]; }
+            cross3(TMP, T, B);
+            cross3(VEC, B, TMP);
+        } else {
+            for (int k = 0; k < 3; ++k) X[k] = P[k] + A[k] * t;
+            cross3(VEC, A, B);
+            if (dot3(VEC, T) < 0) for (int k = 0; k < 3; ++k) VEC[k] = -VEC[k];
+        }
+    }
+}
+
+/* one triangle's normal as a separating direction: the closest vertex of
+ * the other triangle, if its projection falls inside this face, gives the
+ * distance (PQP TriDist case 1) */
+static int tri_face_case(const real S[3][3], const real Sv[3][3], const real T[3][3], int *disjoint, real *dist) {
+    real Sn[3], V[3], Z[3], Tp[3];
+    cross3(Sn, Sv[0], Sv[1]);
+    const real Snl = dot3(Sn, Sn);
+    if (!(Snl > 1e-15)) return 0;
+    for (int i = 0; i < 3; ++i) {
+        for (int k = 0; k < 3; ++k) V[k] = S[0][k] - T[i][k];
+        Tp[i] = dot3(V, Sn);
+    }
+    int point = -1;
+    if (Tp[0] > 0 && Tp[1] > 0 && Tp[2] > 0) {
+        point = Tp[0] < Tp[1] ? 0 : 1;
+        if (Tp[2] < Tp[point]) point = 2;
+    } else if (Tp[0] < 0 && Tp[1] < 0 && Tp[2] < 0) {
+        point = Tp[0] > Tp[1] ? 0 : 1;
+        if (Tp[2] > Tp[point]) point = 2;
+    }
+    if (point < 0) return 0;
+    *disjoint = 1;
+    for (int e = 0; e < 3; ++e) {
+        for (int k = 0; k < 3; ++k) V[k] = T[point][k] - S[e][k];
+        cross3(Z, Sn, Sv[e]);
+        if (!(dot3(V, Z) > 0)) return 0;
+    }
+    real Pp[3], D[3];
+    const real s = Tp[point] / Snl;
+    for (int k = 0; k < 3; ++k) { Pp[k] = T[point][k] + Sn[k] * s; D[k] = Pp[k] - T[point][k]; }
+    *dist = sqrt(dot3(D, D));
+    return 1;
+}
+
+/* TriangleDistance::triDistance(S, T): 0 for intersecting triangles */
+static real tri_distance(const real S[3][3], const real T[3][3]) {
+    real Sv[3][3], Tv[3][3], VEC[3], P[3], Q[3], V[3], Z[3];
+    for (int k = 0; k < 3; ++k) {
+        Sv[0][k] = S[1][k] - S[0][k]; Sv[1][k] = S[2][k] - S[1][k]; Sv[2][k] = S[0][k] - S[2][k];
+        Tv[0][k] = T[1][k] - T[0][k]; Tv[1][k] = T[2][k] - T[1][k]; Tv[2][k] = T[0][k] - T[2][k];
+    }
+    int shown_disjoint = 0;
+    for (int k = 0; k < 3; ++k) V[k] = S[0][k] - T[0][k];
+    real mindd = dot3(V, V) + 1;
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) {
+            seg_points(S[i], Sv[i], T[j], Tv[j], VEC, P, Q);
+            for (int k = 0; k < 3; ++k) V[k] = Q[k] - P[k];
+            const real dd = dot3(V, V);
+            if (dd <= mindd) {
+                mindd = dd;
+                for (int k = 0; k < 3; ++k) Z[k] = S[(i + 2) % 3][k] - P[k];
+                real a = dot3(Z, VEC);
+                for (int k = 0; k < 3; ++k) Z[k] = T[(j + 2) % 3][k] - Q[k];
+                real b = dot3(Z, VEC);
+                if (a <= 0 && b >= 0) return sqrt(dd);
+                const real p = dot3(V, VEC);
+                if (a < 0) a = 0;
+                if (b > 0) b = 0;
+                if (p - a + b > 0) shown_disjoint = 1;
+            }
+        }
+    real d;
+    if (tri_face_case(S, Sv, T, &shown_disjoint, &d)) return d;
+    if (tri_face_case(T, Tv, S, &shown_disjoint, &d)) return d;
+    return shown_disjoint ? sqrt(mindd) : 0.0;
+}
+
+/* lower-bound pruning slack for the mesh distance loops: a skipped triangle
+ * (pair) is farther than the running minimum by more than the float support
+ * rounding of libccd's GJK objects */
+static real mesh_dist_slack(const real *Ta, const real *Tb) {
+    return 1e-5 * (1.0 + fabs(Ta[9]) + fabs(Ta[10]) + fabs(Ta[11]) + fabs(Tb[9]) + fabs(Tb[10]) + fabs(Tb[11]));
+}
+
+/* fcl::distance(mesh, shape) / (shape, mesh) [ext FCL 0.7.0
+ * MeshShapeDistanceTraversalNodeOBBRSS]: the minimum over the triangles of
+ * shapeTriangleDistance(shape, tf, P1, P2, P3, tf_mesh) (libccd GJK distance
+ * on the triangle GJK object; -1 when they intersect); the BV traversal
+ * only skips triangles that cannot lower the running minimum. */
+static real mesh_shape_distance(const orc_world *w, int gm, const real *TM, int gs, const real *TS) {
+    const int t0 = (int)w->geom_param[4 * gm], tn = (int)w->geom_param[4 * gm + 1];
+    const int ts = w->geom_type[gs];
+    const real *ps = w->geom_param + 4 * gs;
+    real rs = 0.0;  /* the shape's bounding sphere about its origin (as mesh_shape_intersect) */
+    if (ts == GEOM_CONVEX) {
+        const real *V = w->verts + 3 * (size_t)w->geom_vstart[gs];
+        for (int i = 0; i < w->geom_nv[gs]; ++i) rs = fmax(rs, dot3(V + 3 * i, V + 3 * i));
+        rs = sqrt(rs);
+    } else if (ts == GEOM_BOX) rs = 0.5 * sqrt(dot3(ps, ps));
+    else if (ts == GEOM_SPHERE) rs = ps[0];
+    else rs = sqrt(ps[0] * ps[0] + 0.25 * ps[1] * ps[1]) + (ts == GEOM_CAPSULE ? ps[0] : 0.0);
+    rs = rs * (1.0 + 1e-9) + 1e-9;
+    real (*Wt)[9] = malloc(sizeof(real) * 9 * (size_t)(tn > 0 ? tn : 1));
+    real (*S)[4] = malloc(sizeof(real) * 4 * (size_t)(tn > 0 ? tn : 1));
+    mesh_world_tris(w, gm, TM, Wt, S);
+    const real slack = mesh_dist_slack(TM, TS);
+    gjk_obj shape, frame, tri;
+    make_obj(w, gs, TS, &shape, NULL);
+    memset(&frame, 0, sizeof frame);
+    shape_to_gjk(TM, &frame);
+    real best = DBL_MAX;
+    for (int t = 0; t < tn && best != -1.0; ++t) {
+        const real d[3] = {S[t][0] - TS[9], S[t][1] - TS[10], S[t][2] - TS[11]};
+        if (sqrt(dot3(d, d)) - S[t][3] - rs > best + slack) continue;
+        tri_gjk_obj(w, gm, &frame, t0 + t, &tri);
+        const real dt = gjk_distance(&shape, &tri);
+        if (dt < best) best = dt;
+    }
+    free(Wt);
+    free(S);
+    return best;
+}
+
+/* fcl::distance(mesh, mesh) [ext FCL 0.7.0 MeshDistanceTraversalNodeOBBRSS
+ * leafTesting]: the minimum of triDistance over the triangle pairs, B's
+ * triangles mapped into A's frame (R = R1^T R2, T = R1^T (t2 - t1)); 0 when
+ * some pair intersects. */
+static real mesh_mesh_distance(const orc_world *w, int ga, const real *TA, int gb, const real *TB) {
+    const int a0 = (int)w->geom_param[4 * ga], an = (int)w->geom_param[4 * ga + 1];
+    const int b0 = (int)w->geom_param[4 * gb], bn = (int)w->geom_param[4 * gb + 1];
+    real R[9], T[3], dt[3];
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) R[3 * i + j] = (TA[i] * TB[j] + TA[3 + i] * TB[3 + j]) + TA[6 + i] * TB[6 + j];
+    for (int k = 0; k < 3; ++k) dt[k] = TB[9 + k] - TA[9 + k];
+    for (int i = 0; i < 3; ++i) T[i] = (TA[i] * dt[0] + TA[3 + i] * dt[1]) + TA[6 + i] * dt[2];
+    real (*QB)[3][3] = malloc(sizeof(real) * 9 * (size_t)(bn > 0 ? bn : 1));
+    real (*SB)[4] = malloc(sizeof(real) * 4 * (size_t)(bn > 0 ? bn : 1));
+    for (int j = 0; j < bn; ++j) {
+        const real *Q[3];
+        mesh_tri_points(w, gb, b0 + j, Q);
+        for (int k = 0; k < 3; ++k)
+            for (int i = 0; i < 3; ++i)
+                QB[j][k][i] = ((R[3 * i] * Q[k][0] + R[3 * i + 1] * Q[k][1]) + R[3 * i + 2] * Q[k][2]) + T[i];
+        const real *Qp[3] = {QB[j][0], QB[j][1], QB[j][2]};
+        bsphere(Qp, 3, SB[j], &SB[j][3]);
+    }
+    const real slack = mesh_dist_slack(TA, TB);
+    real best = DBL_MAX;
+    for (int i = 0; i < an && best != 0.0; ++i) {
+        const real *P[3];
+        mesh_tri_points(w, ga, a0 + i, P);
+        real c[3], r, Sa[3][3];
+        bsphere(P, 3, c, &r);
+        for (int k = 0; k < 3; ++k)
+            for (int m = 0; m < 3; ++m) Sa[k][m] = P[k][m];
+        for (int j = 0; j < bn; ++j) {
+            const real d[3] = {c[0] - SB[j][0], c[1] - SB[j][1], c[2] - SB[j][2]};
+            if (sqrt(dot3(d, d)) - r - SB[j][3] > best + slack) continue;
+            const real dd = tri_distance(Sa, (const real (*)[3])QB[j]);
+            if (dd < best) best = dd;
+            if (best == 0.0) break;
+        }
+    }
+    free(QB);
+    free(SB);
+    return best;
+}
+
+/* fcl::distance(mesh, OcTree) in either order [ext FCL 0.7.0
+ * OcTreeSolver::OcTreeMeshDistanceRecurse]: the minimum over (occupied
+ * leaf, triangle) of shapeTriangleDistance(Box(leaf), box_tf, P1, P2, P3,
+ * tf_mesh), leaf box first; -1 once a pair intersects. */
+static real mesh_octree_distance(const orc_world *w, int gm, const real *TM, int go, const real *TO) {
+    const int t0 = (int)w->geom_param[4 * gm], tn = (int)w->geom_param[4 * gm + 1];
+    const int l0 = (int)w->geom_param[4 * go], ln = (int)w->geom_param[4 * go + 1];
+    real (*Wt)[9] = malloc(sizeof(real) * 9 * (size_t)(tn > 0 ? tn : 1));
+    real (*S)[4] = malloc(sizeof(real) * 4 * (size_t)(tn > 0 ? tn : 1));
+    mesh_world_tris(w, gm, TM, Wt, S);
+    const real slack = mesh_dist_slack(TM, TO);
+    gjk_obj frame, tri, box;
+    memset(&frame, 0, sizeof frame);
+    shape_to_gjk(TM, &frame);
+    real best = DBL_MAX;
+    for (int l = l0; l < l0 + ln && best != -1.0; ++l) {
+        real side[3], TL[12];
+        octree_leaf_box(w, l, TO, side, TL);
+        const real rl = 0.5 * sqrt(dot3(side, side)) * (1.0 + 1e-9) + 1e-9;
+        leaf_box_obj(side, TL, &box);
+        for (int t = 0; t < tn && best != -1.0; ++t) {
+            const real d[3] = {TL[9] - S[t][0], TL[10] - S[t][1], TL[11] - S[t][2]};
+            if (sqrt(dot3(d, d)) - rl - S[t][3] > best + slack) continue;
+            tri_gjk_obj(w, gm, &frame, t0 + t, &tri);
+            const real dt = gjk_distance(&box, &tri);
+            if (dt < best) best = dt;
+        }
+    }
+    free(Wt);
+    free(S);
+    return best;
+}
+
+/* fcl::distance on a pair with a BVH mesh side; -2 when neither is a mesh */
+static real mesh_distance(const orc_world *w, int ga, const real *Ta, int gb, const real *Tb) {
+    const int ta = w->geom_type[ga], tb = w->geom_type[gb];
+    if (ta != GEOM_MESH && tb != GEOM_MESH) return -2.0;
+    if (ta == GEOM_MESH && tb == GEOM_MESH) return mesh_mesh_distance(w, ga, Ta, gb, Tb);
+    if (ta == GEOM_OCTREE) return mesh_octree_distance(w, gb, Tb, ga, Ta);
+    if (tb == GEOM_OCTREE) return mesh_octree_distance(w, ga, Ta, gb, Tb);
+    return ta == GEOM_MESH ? mesh_shape_distance(w, ga, Ta, gb, Tb) : mesh_shape_distance(w, gb, Tb, ga, Ta);
+}
+
 int orc_distance_batch(const orc_world *w, const double *q, long n, int n_self, double *d_self, int *p_self,
                        double *d_others, int *p_others) {
     real *oMi = malloc(sizeof(real) * 12 * (size_t)(w->nj + 1));
@@ -2255,10 +2607,11 @@ int orc_distance_batch(const orc_world *w, const double *q, long n, int n_self, 
                 else if (ks[s] == KIND_ATTACHED) { T = att_T + 12 * is[s]; gg = w->att_geom[is[s]]; }
                 else { T = w->scene_tf + 12 * is[s]; gg = w->scene_geom[is[s]]; }
                 Ts[s] = T; gs[s] = gg;
-                if (w->geom_type[gg] != GEOM_OCTREE) make_obj(w, gg, T, &o[s], NULL);
+                if (w->geom_type[gg] != GEOM_OCTREE && w->geom_type[gg] != GEOM_MESH) make_obj(w, gg, T, &o[s], NULL);
             }
             const int oi = w->geom_type[gs[0]] == GEOM_OCTREE ? 0 : w->geom_type[gs[1]] == GEOM_OCTREE ? 1 : -1;
-            const double d = oi < 0 ? gjk_distance(&o[0], &o[1]) : octree_distance(w, gs[oi], Ts[oi], &o[1 - oi]);
+            double d = mesh_distance(w, gs[0], Ts[0], gs[1], Ts[1]);
+            if (d == -2.0) d = oi < 0 ? gjk_distance(&o[0], &o[1]) : octree_distance(w, gs[oi], Ts[oi], &o[1 - oi]);
             if (d < best[g]) { best[g] = d; bp[g] = p; }
         }
         d_self[c] = best[0]; p_self[c] = bp[0]; d_others[c] = best[1]; p_others[c] = bp[1];
@@ -2386,6 +2739,14 @@ int orc_contact_batch(const orc_world *w, const double *q, long n, uint8_t *hit,
 }
 
 double orc_distance_pair(const orc_world *w, int ga, const double *Ta, int gb, const double *Tb) {
+    const double dm = mesh_distance(w, ga, Ta, gb, Tb);
+    if (dm != -2.0) return dm;
+    if (w->geom_type[gb] == GEOM_OCTREE || w->geom_type[ga] == GEOM_OCTREE) {
+        const int oi = w->geom_type[ga] == GEOM_OCTREE ? 0 : 1;
+        gjk_obj s;
+        make_obj(w, oi ? ga : gb, oi ? Ta : Tb, &s, NULL);
+        return octree_distance(w, oi ? gb : ga, oi ? Tb : Ta, &s);
+    }
     gjk_obj a, b;
     make_obj(w, ga, Ta, &a, NULL);
     make_obj(w, gb, Tb, &b, NULL);
@@ -2408,4 +2769,10 @@ int orc_collide_pair(const orc_world *w, int ga, const double *Ta, int gb, const
 /* Intersect::intersect_Triangle / sphereTriangleIntersect on raw points
  * (known-answer tests) */
 int orc_tri_tri(const double *P, const double *Q) { return tri_tri_intersect(P, P + 3, P + 6, Q, Q + 3, Q + 6); }
+double orc_tri_distance(const double *P, const double *Q) {
+    real S[3][3], T[3][3];
+    for (int k = 0; k < 3; ++k)
+        for (int i = 0; i < 3; ++i) { S[k][i] = P[3 * k + i]; T[k][i] = Q[3 * k + i]; }
+    return tri_distance((const real (*)[3])S, (const real (*)[3])T);
+}
 int orc_sphere_tri(double r, const double *TS, const double *P) { return sphere_triangle_intersect(r, TS, P, P + 3, P + 6); }

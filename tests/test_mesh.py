@@ -55,6 +55,95 @@ def test_sphere_triangle_known_answers(c, r, want):
     assert oracle.sphere_tri(r, c, T0) is want
 
 
+def _seg_seg(p1, q1, p2, q2):
+    """exact distance of two segments (clamped closest-point parameters)"""
+    d1, d2, r = q1 - p1, q2 - p2, p1 - p2
+    a, e, f, c, b = d1 @ d1, d2 @ d2, d2 @ r, d1 @ r, d1 @ d2
+    den = a * e - b * b
+    s = np.clip((b * f - c * e) / den, 0, 1) if den != 0 else 0.0
+    t = (b * s + f) / e
+    if t < 0:
+        t, s = 0.0, np.clip(-c / a, 0, 1)
+    elif t > 1:
+        t, s = 1.0, np.clip((b - c) / a, 0, 1)
+    return float(np.linalg.norm(p1 + d1 * s - (p2 + d2 * t)))
+
+
+def _pt_tri(p, T):
+    a, b, c = T
+    n = np.cross(b - a, c - a)
+    n /= np.linalg.norm(n)
+    q = p - ((p - a) @ n) * n
+    sides = [np.cross(v - u, q - u) @ n for u, v in ((a, b), (b, c), (c, a))]
+    if all(x >= 0 for x in sides) or all(x <= 0 for x in sides):
+        return abs(float((p - a) @ n))
+    return min(float(np.linalg.norm(p - (u + np.clip((p - u) @ (v - u) / ((v - u) @ (v - u)), 0, 1) * (v - u))))
+               for u, v in ((a, b), (b, c), (c, a)))
+
+
+def _tri_distance_brute(S, T):
+    if oracle.tri_tri(S, T):
+        return 0.0
+    return min([_pt_tri(p, T) for p in S] + [_pt_tri(p, S) for p in T] +
+               [_seg_seg(S[i], S[(i + 1) % 3], T[j], T[(j + 1) % 3]) for i in range(3) for j in range(3)])
+
+
+@pytest.mark.parametrize("Q,want", [
+    ([[0, 0, 0.1], [1, 0, 0.1], [0, 1, 0.1]], 0.1),                   # parallel, 0.1 above
+    ([[0.2, 0.2, -0.5], [0.2, 0.2, 0.5], [0.3, 0.3, 0.5]], 0.0),      # pierces the interior
+    ([[2, 0, 0], [3, 0, 0], [2, 1, 0]], 1.0),                         # coplanar, vertex to vertex
+    ([[0.25, 0.25, 0.3], [0.25, 0.25, 1.0], [0.3, 0.2, 1.0]], 0.3),   # vertex above the face
+    ([[0.5, 0.5, 0.2], [1.5, 1.5, 0.2], [1.5, 1.5, 1.2]], 0.2),       # vertex above the hypotenuse
+    ([[0.5, -0.5, 1e-3], [0.5, 0.5, 1e-3], [0.5, 0.0, 1.0]], 1e-3),   # edge above the face
+])
+def test_triangle_distance_known_answers(Q, want):
+    """FCL TriangleDistance::triDistance (PQP TriDist, oracle tri_distance)"""
+    Q = np.array(Q, dtype=np.float64)
+    assert oracle.tri_distance(T0, Q) == pytest.approx(want, abs=1e-12)
+    assert oracle.tri_distance(Q, T0) == pytest.approx(want, abs=1e-12)
+
+
+def test_triangle_distance_matches_brute_force():
+    """triDistance equals the exact minimum over the vertex-face and
+    edge-edge distances (0 when the triangles intersect) on random pairs"""
+    rng = np.random.default_rng(0)
+    for _ in range(1500):
+        S = rng.normal(size=(3, 3))
+        T = rng.normal(size=(3, 3)) + rng.normal(size=3) * rng.uniform(0, 3)
+        assert abs(oracle.tri_distance(S, T) - _tri_distance_brute(S, T)) < 1e-9
+
+
+def test_mesh_octree_oracle_matches_leaf_boxes():
+    """fcl::collide / fcl::distance(mesh, OcTree) in the oracle equal the
+    same query against every occupied leaf as its own box (box first, as
+    OcTreeMeshIntersectRecurse / OcTreeMeshDistanceRecurse run the leaf
+    test), in both argument orders."""
+    art = Wd.panda_articulation(False)
+    mesh = next(o.geom for o in art.objects if o.link == "panda_link3")
+    rng = np.random.default_rng(3)
+    tree = M.OcTreeGeom(rng.uniform(-0.12, 0.12, (200, 3)), 0.02)
+    leaves = np.asarray(tree.leaves)
+    boxes = [(M.BoxGeom(tuple(float(v) for v in l[3:] - l[:3])), (M.IDENT[0], [float(v) for v in (l[:3] + l[3:]) * 0.5]))
+             for l in leaves]
+    ob = oracle.OracleWorld(art, scene=[("pcd", tree, M.IDENT), ("m", mesh, M.IDENT)] +
+                            [(f"b{i}", b, c) for i, (b, c) in enumerate(boxes)])
+    gt, gm = _gi(ob, tree), _gi(ob, mesh)
+    gb = [_gi(ob, b) for b, _ in boxes]
+    n_hit = n_far = 0
+    for k in range(120):
+        w, x, y, z = Wd.random_quat(rng)
+        T = (M.quat_to_mat(w, x, y, z), [float(v) for v in rng.uniform(-0.3, 0.3, 3)])
+        hit = Wd.collide_pair(ob, gm, T, gt, M.IDENT)
+        assert hit == Wd.collide_pair(ob, gt, M.IDENT, gm, T)
+        assert hit == any(Wd.collide_pair(ob, g, c, gm, T) for g, (_, c) in zip(gb, boxes))
+        d = Wd.distance_pair(ob, gm, T, gt, M.IDENT)
+        assert d == Wd.distance_pair(ob, gt, M.IDENT, gm, T)
+        assert d == min(Wd.distance_pair(ob, g, c, gm, T) for g, (_, c) in zip(gb, boxes))
+        n_hit += hit
+        n_far += d > 0.02
+    assert n_hit > 10 and n_far > 10
+
+
 def _gi(ob, g):
     return next(i for i, x in enumerate(ob.geoms) if x is g)
 
@@ -188,13 +277,11 @@ def _bits(M_, P):
     return np.stack([(M_[:, p >> 5] >> (p & 31)) & 1 for p in P], 1)
 
 
-@pytest.mark.gpu
-@pytest.mark.parametrize("convex", [False, True])
-def test_mesh_worlds_match_oracle(convex):
+def _full_mesh_world(convex):
     """Panda links as BVH meshes (convex=False) or hulls, the cfg3 boxes, a
     BVH mesh and a hull in the scene, an attached sphere, box and BVH mesh:
-    every pair class (mesh-mesh, mesh-box / sphere / convex, sphere
-    closed form vs triangles) on both batch paths."""
+    (PlanningWorld, OracleWorld, base oracle world, device pair names, perm
+    device pair -> oracle pair)."""
     d = os.path.join(Wd.panda_dir(), "franka_description", "meshes", "collision")
     w, art = scenes.world(3, convex=convex)
     base = Wd.oracle_world(3, convex=convex)
@@ -220,6 +307,15 @@ def test_mesh_worlds_match_oracle(convex):
     names = [(i[3], i[4]) for i in w.get_collision_pair_info()]
     assert sorted(names) == sorted(o2.pair_names())
     perm = [order[n] for n in names]
+    return w, o2, base, names, perm
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("convex", [False, True])
+def test_mesh_worlds_match_oracle(convex):
+    """_full_mesh_world: every pair class (mesh-mesh, mesh-box / sphere /
+    convex, sphere closed form vs triangles) on both batch paths."""
+    w, o2, base, names, perm = _full_mesh_world(convex)
     q = Wd.sample_q(base.art, 6000, 31)
     q = np.vstack([q, [Wd.KAT_FREE, Wd.KAT_COLLIDING]])
     fo, mo = o2.collide_batch(q, nthreads=min(16, os.cpu_count() or 1))
@@ -237,14 +333,78 @@ def test_mesh_worlds_match_oracle(convex):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("convex", [False, True])
+def test_mesh_distance_matches_oracle(convex):
+    """fcl::distance on BVH meshes (mesh-mesh triDistance, mesh-shape GJK
+    on the triangle GJK objects) in PlanningWorld::distanceSelf /
+    distanceOthers: batched minima within 1e-9 of the oracle, the same
+    nearest pair, penetration (-1) / touching meshes (0) the same; scalar
+    self_distance / distance_with_others on a few states."""
+    w, o2, base, names, perm = _full_mesh_world(convex)
+    q = np.vstack([Wd.sample_q(base.art, 400, 41), [Wd.KAT_FREE, Wd.KAT_COLLIDING]])
+    ds, ps, do, po = w.distance_batch(q)
+    rs, rps, ro, rpo = o2.distance_batch(q)
+    on = o2.pair_names()
+    for d, r, p, rp in ((ds, rs, ps, rps), (do, ro, po, rpo)):
+        np.testing.assert_array_equal(d == -1.0, r == -1.0)
+        np.testing.assert_allclose(d, r, rtol=0, atol=1e-9)
+        same = [names[a] == on[b] for a, b in zip(p, rp)]
+        assert np.mean(same) > 0.99
+    mesh_pairs = {n for n in names if "scene_mesh" in n or "tool" in n} | (set(names) if not convex else set())
+    assert any(names[p] in mesh_pairs for p in np.concatenate([ps, po]))  # a mesh pair is the nearest somewhere
+    for i in (0, 1, len(q) - 1):
+        w.set_qpos_all(list(q[i]))
+        a, b = w.self_distance(), w.distance_with_others()
+        assert abs(a.min_distance - rs[i]) < 1e-9 and abs(b.min_distance - ro[i]) < 1e-9
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cloud", ["floor", "blue"])
+def test_mesh_robot_point_cloud_matches_oracle(cloud):
+    """BVH mesh links against a point cloud (fcl::collide / fcl::distance on
+    (BVHModel, OcTree): box-first MPR / GJK on every (leaf, triangle) pair):
+    flags and pair bits on both batch paths bit-exact, distances within 1e-9
+    of the oracle."""
+    art = scenes.panda(convex=False)
+    if cloud == "floor":
+        w = pymp.planning_world.PlanningWorld([art], ["panda"], [], [])
+        scene = []
+        allowed = []
+    else:
+        w, art = scenes.world(3, convex=False)
+        scene = Wd.boxes_scene()
+        allowed = [("panda_link0", "table")]
+    w.add_point_cloud("scene_pcd", scenes.cloud_points(cloud), 1e-3)
+    o = oracle.OracleWorld(Wd.panda_articulation(False),
+                           scene=scene + [("scene_pcd", M.OcTreeGeom(scenes.cloud_points(cloud), 1e-3), M.IDENT)],
+                           allowed=allowed)
+    names = [(i[3], i[4]) for i in w.get_collision_pair_info()]
+    assert names == o.pair_names()
+    q = np.vstack([Wd.sample_q(o.art, 3000, 77), [scenes.FLOOR_COLLIDING, Wd.KAT_FREE]])
+    fo, mo = o.collide_batch(q, nthreads=min(16, os.cpu_count() or 1))
+    for small in (0, 1 << 20):
+        w.set_small_batch_max(small)
+        f, m = w.collide_batch(q)
+        np.testing.assert_array_equal(f, fo)
+        np.testing.assert_array_equal(m, mo)
+    k = names.index(("panda_link0", "scene_pcd")) if cloud == "floor" else names.index(("panda_hand", "scene_pcd"))
+    cloud_hits = sum(int(((mo[:, p >> 5] >> (p & 31)) & 1).sum()) for p, n in enumerate(names) if n[1] == "scene_pcd")
+    assert cloud_hits > 0, k
+    qd = q[-40:]
+    ds, ps, do, po = w.distance_batch(qd)
+    rs, rps, ro, rpo = o.distance_batch(qd)
+    for d, r in ((ds, rs), (do, ro)):
+        np.testing.assert_array_equal(d == -1.0, r == -1.0)
+        np.testing.assert_allclose(d, r, rtol=0, atol=1e-9)
+
+
+@pytest.mark.gpu
 def test_mesh_world_unsupported_queries():
     w, _ = scenes.world(2, convex=False)
     w.set_qpos_all(Wd.KAT_COLLIDING)
     assert w.collide() and len(w.collide_full()) > 0
     w.set_qpos_all(Wd.KAT_FREE)
     assert not w.collide() and w.collide_full() == []
-    with pytest.raises(NotImplementedError, match="BVH mesh"):
-        w.self_distance()
     with pytest.raises(NotImplementedError):
         w.collide(pymp.fcl.CollisionRequest(enable_contact=True))
 

@@ -237,6 +237,16 @@ def collide_pair(ow: oracle.OracleWorld, ga: int, Ta, gb: int, Tb) -> bool:
                                               b.ctypes.data_as(DP)))
 
 
+def distance_pair(ow: oracle.OracleWorld, ga: int, Ta, gb: int, Tb) -> float:
+    """The oracle's fcl::distance on two posed geometries of ow (SE3 tuples)."""
+    import ctypes
+    DP = ctypes.POINTER(ctypes.c_double)
+    a = np.ascontiguousarray(oracle._se3_flat(Ta), dtype=np.float64)
+    b = np.ascontiguousarray(oracle._se3_flat(Tb), dtype=np.float64)
+    return float(oracle.lib().orc_distance_pair(ctypes.byref(ow._w), ga, a.ctypes.data_as(DP), gb,
+                                                b.ctypes.data_as(DP)))
+
+
 def cone_hull(n_rim: int = 300, r: float = 0.12, h: float = 0.25):
     """A watertight triangulated cone: n_rim rim vertices (z = 0), apex, base
     centre.  Its flat base keeps every rim vertex in the walk cells around

@@ -23,9 +23,12 @@ def short(name):
 def main():
     d, n, out = sys.argv[1], int(sys.argv[2]), sys.argv[3]
     vals = defaultdict(lambda: defaultdict(list))
+    dur = defaultdict(list)  # dispatch wall time of the pass that holds GRBM_GUI_ACTIVE (ns)
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
             vals[r["Counter_Name"]][short(r["Kernel_Name"])].append(float(r["Counter_Value"]))
+            if r["Counter_Name"] == "GRBM_GUI_ACTIVE" and r.get("End_Timestamp"):
+                dur[short(r["Kernel_Name"])].append(float(r["End_Timestamp"]) - float(r["Start_Timestamp"]))
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     from build_hash import build_hash
     res = {"configs_per_launch": n, "source": os.path.relpath(d),
@@ -44,6 +47,14 @@ def main():
         if c not in ("FETCH_SIZE", "WRITE_SIZE"):
             for k, v in vals[c].items():
                 res["kernels"][k][c] = sum(v) / len(v)
+    # effective clock (MI355X_MICROARCH.md "DVFS give-back"): GRBM_GUI_ACTIVE is
+    # summed over the 8 XCDs; divided by the dispatch's wall time in that pass
+    for k, v in dur.items():
+        ns = sum(v) / len(v)
+        res["kernels"][k]["pmc_dispatch_ns"] = ns
+        g = res["kernels"][k].get("GRBM_GUI_ACTIVE")
+        if g and ns > 0:
+            res["kernels"][k]["clock_ghz"] = g / 8.0 / ns
     json.dump(res, open(out, "w"), indent=1, sort_keys=True)
     print(json.dumps({k: v.get("hbm_bytes") for k, v in res["kernels"].items()}))
 
