@@ -307,16 +307,18 @@ __device__ __forceinline__ V3 walk_resolve_wave(const DevWorld& w, cptr<double> 
   const int nact = __popcll(act);
   const int rank = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(act >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0u));
   const int lane = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
-  const int cb = w.geom_cbase[geom];
   while (pm) {
     const int L = __builtin_ctzll(pm);
     pm &= pm - 1ull;
+    // lane L's hull (the same on every lane when the wave's pair is uniform)
+    const int geomL = __builtin_amdgcn_readlane(geom, L);
+    const int cb = w.geom_cbase[geomL];
     const V3 dL = v3(lane_bcast(d.x, L), lane_bcast(d.y, L), lane_bcast(d.z, L));
     const int cL = __builtin_amdgcn_readlane(c, L);
     const int preL = __builtin_amdgcn_readlane(pre, L);
     if (preL >= 0) {  // undecided finer cell: resume the climb where the host's replay stopped
-      const int bi = wave_walk(w, HV, geom, dL, rank, nact, w.wcell_pre + kWalkPre * (size_t)preL);
-      if (lane == L) p = hull_vertex(w, HV, geom, bi);
+      const int bi = wave_walk(w, HV, geomL, dL, rank, nact, w.wcell_pre + kWalkPre * (size_t)preL);
+      if (lane == L) p = hull_vertex(w, HV, geomL, bi);
 #ifdef MPG_STATS
       if (w.stats && rank == 0) atomicAdd(&w.stats[18], 1ull);
 #endif
@@ -356,7 +358,7 @@ __device__ __forceinline__ V3 walk_resolve_wave(const DevWorld& w, cptr<double> 
           if (gL < 32 && ((((uint32_t)a[4]) >> gL) & 1u) && bL > dd) continue;
           const double dw = (dL.x * a[1] + dL.y * a[2]) + dL.z * a[3];
           if (dw > dd) continue;
-          if (!neighbour_beats(w, HV, geom, (int)a[0], dd, dL)) fail = true;
+          if (!neighbour_beats(w, HV, geomL, (int)a[0], dd, dL)) fail = true;
         }
         ok = __ballot(fail) == 0ull;
       }
@@ -369,8 +371,8 @@ __device__ __forceinline__ V3 walk_resolve_wave(const DevWorld& w, cptr<double> 
     }
 #endif
     if (!ok) {
-      const int bi = wave_walk(w, HV, geom, dL, rank, nact, nullptr);
-      if (lane == L) p = hull_vertex(w, HV, geom, bi);
+      const int bi = wave_walk(w, HV, geomL, dL, rank, nact, nullptr);
+      if (lane == L) p = hull_vertex(w, HV, geomL, bi);
 #ifdef MPG_STATS
       if (w.stats && rank == 0) atomicAdd(&w.stats[15], __builtin_amdgcn_s_memtime() - t1);
 #endif
@@ -480,9 +482,10 @@ __device__ __forceinline__ CV3 support(const DevWorld& w, cptr<double> HV, const
 }
 
 // centerConvex (interior point ccdVec3Set, rotated, translated) / centerShape
+template <bool UNI = true>
 __device__ __forceinline__ CV3 center(const DevWorld& w, const GObj& o) {
-  if (__builtin_amdgcn_readfirstlane(o.type) == MPG_GEOM_CONVEX) {
-    const cptr<double> rec = w.geom_rec + G_STRIDE * __builtin_amdgcn_readfirstlane(o.geom);
+  if ((UNI ? __builtin_amdgcn_readfirstlane(o.type) : o.type) == MPG_GEOM_CONVEX) {
+    const cptr<double> rec = w.geom_rec + G_STRIDE * (UNI ? __builtin_amdgcn_readfirstlane(o.geom) : o.geom);
     return vadd(quat_rot(cv3(rec[G_INTERIOR], rec[G_INTERIOR + 1], rec[G_INTERIOR + 2]), o.rot), o.pos);
   }
   return o.pos;
@@ -503,11 +506,14 @@ __device__ __forceinline__ bool vec_is_origin(const CV3& v) {
 }
 
 // libccd __ccdSupport: v = support1(dir) - support2(-dir)
+// UNI: the geometries are the same on every lane (one pair per wave): their
+// parameters come through scalar loads; otherwise every lane has its own pair
+template <bool UNI = true>
 __device__ __forceinline__ CV3 msupport(const DevWorld& w, cptr<double> HV, const GObj& a,
                                         const GObj& b, const CV3& dir) {
   const CV3 da = quat_rot(dir, a.rot_inv), db = quat_rot(vscale(dir, ccd_real(-1)), b.rot_inv);
-  const int ga = __builtin_amdgcn_readfirstlane(a.geom), ta = __builtin_amdgcn_readfirstlane(a.type);
-  const int gb = __builtin_amdgcn_readfirstlane(b.geom), tb = __builtin_amdgcn_readfirstlane(b.type);
+  const int ga = UNI ? __builtin_amdgcn_readfirstlane(a.geom) : a.geom, ta = UNI ? __builtin_amdgcn_readfirstlane(a.type) : a.type;
+  const int gb = UNI ? __builtin_amdgcn_readfirstlane(b.geom) : b.geom, tb = UNI ? __builtin_amdgcn_readfirstlane(b.type) : b.type;
   // walk hulls: both fast paths first, then one resolve site for the lanes
   // either left pending (one inlined copy of the rare path instead of two)
   bool pa = false, pb = false;
@@ -1117,32 +1123,6 @@ __global__ __launch_bounds__(BLOCK) void cull_kernel(DevWorld w, const double* _
 // (no global atomics): count per (pair, 64-config tile) -> per-pair scan ->
 // scatter.  Candidates of a pair end up contiguous and sorted by config.
 // ---------------------------------------------------------------------------
-// one block per pair: exclusive scan of its tile counts (in place) + total
-__global__ __launch_bounds__(1024) void pair_scan_kernel(uint32_t* __restrict__ cnt, int n_tiles,
-                                                        uint32_t* __restrict__ seg_len) {
-  __shared__ uint32_t part[1024];
-  uint32_t* c = cnt + (long long)blockIdx.x * n_tiles;
-  const int per = (n_tiles + 1023) / 1024;
-  const int lo = threadIdx.x * per, hi = min(n_tiles, lo + per);
-  uint32_t sum = 0;
-  for (int i = lo; i < hi; ++i) sum += c[i];
-  part[threadIdx.x] = sum;
-  __syncthreads();
-  for (int off = 1; off < 1024; off <<= 1) {  // Hillis-Steele inclusive scan
-    const uint32_t v = threadIdx.x >= (unsigned)off ? part[threadIdx.x - off] : 0u;
-    __syncthreads();
-    part[threadIdx.x] += v;
-    __syncthreads();
-  }
-  uint32_t run = part[threadIdx.x] - sum;
-  for (int i = lo; i < hi; ++i) {
-    const uint32_t v = c[i];
-    c[i] = run;
-    run += v;
-  }
-  if (threadIdx.x == 1023) seg_len[blockIdx.x] = part[1023];
-}
-
 // inclusive scan of one value per lane across the wave
 __device__ __forceinline__ uint32_t wave_inclusive_scan(uint32_t v, uint32_t lane) {
 #pragma unroll
@@ -1151,6 +1131,54 @@ __device__ __forceinline__ uint32_t wave_inclusive_scan(uint32_t v, uint32_t lan
     if (lane >= (uint32_t)off) v += u;
   }
   return v;
+}
+
+// one block per pair: exclusive scan of its tile counts (in place) + total.
+// Each thread holds up to 16 consecutive counts in registers (loads issued
+// together), one wave scan + one LDS exchange of the 16 wave totals.
+__global__ __launch_bounds__(1024) void pair_scan_kernel(uint32_t* __restrict__ cnt, int n_tiles,
+                                                        uint32_t* __restrict__ seg_len) {
+  __shared__ uint32_t part[16];
+  uint32_t* c = cnt + (long long)blockIdx.x * n_tiles;
+  const int per = (n_tiles + 1023) / 1024;
+  const int lo = threadIdx.x * per, hi = min(n_tiles, lo + per);
+  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+  uint32_t v[16];
+  uint32_t sum = 0;
+  if (per <= 16) {
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      v[k] = lo + k < hi ? c[lo + k] : 0u;
+      sum += v[k];
+    }
+  } else {
+    for (int i = lo; i < hi; ++i) sum += c[i];
+  }
+  const uint32_t incl = wave_inclusive_scan(sum, lane);
+  if (lane == 63u) part[wv] = incl;
+  __syncthreads();
+  uint32_t pre = 0, tot = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < 16; ++k) {
+    const uint32_t x = part[k];
+    pre += k < wv ? x : 0u;
+    tot += x;
+  }
+  uint32_t run = pre + incl - sum;
+  if (per <= 16) {
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      if (lo + k < hi) c[lo + k] = run;
+      run += v[k];
+    }
+  } else {
+    for (int i = lo; i < hi; ++i) {
+      const uint32_t x = c[i];
+      c[i] = run;
+      run += x;
+    }
+  }
+  if (threadIdx.x == 0) seg_len[blockIdx.x] = tot;
 }
 
 // segment starts + prefix of narrow-phase tasks (ts candidates of one pair
@@ -1219,6 +1247,9 @@ __global__ __launch_bounds__(256) void chunk_scan_kernel(const uint32_t* __restr
   }
 }
 
+// one wave per (survivor word, 64-config tile): the slot bases of the
+// word's surviving pairs come in one parallel load (lane b: pair 32 wd + b),
+// then each surviving pair's configurations are written at base + rank
 __global__ __launch_bounds__(256) void scatter_kernel(const uint32_t* __restrict__ surv, long long n, long long cap,
                                                      int n_pairs, int W, int n_tiles,
                                                      const uint32_t* __restrict__ off,
@@ -1230,15 +1261,24 @@ __global__ __launch_bounds__(256) void scatter_kernel(const uint32_t* __restrict
   const int wd = (int)(wid / n_tiles), t = (int)(wid % n_tiles);
   const long long cfg = (long long)t * 64 + lane;
   const uint32_t x = cfg < n ? surv[(long long)wd * cap + cfg] : 0u;
-  const int nb = min(32, n_pairs - wd * 32);
-  for (int b = 0; b < nb; ++b) {
+  uint32_t o = x;
+#pragma unroll
+  for (int sh = 1; sh < 64; sh <<= 1) o |= (uint32_t)__shfl_xor((int)o, sh);
+  o = __builtin_amdgcn_readfirstlane(o);
+  if (o == 0u) return;
+  uint32_t base = 0u;
+  if (lane < 32u && ((o >> lane) & 1u)) {
+    const int p = wd * 32 + (int)lane;
+    base = seg_start[p] + off[(long long)p * n_tiles + t];
+  }
+  for (uint32_t m = o; m; m &= m - 1u) {
+    const int b = __builtin_ctz(m);
     const uint32_t bit = (x >> b) & 1u;
     const unsigned long long bal = __ballot(bit);
-    if (bit) {
-      const int p = wd * 32 + b;
-      const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
-      cand[seg_start[p] + off[(long long)p * n_tiles + t] + rank] = (uint32_t)cfg;
-    }
+    const uint32_t bs = __builtin_amdgcn_readlane(base, b);
+    if (bit)
+      cand[bs + __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u))] =
+          (uint32_t)cfg;
   }
 }
 
