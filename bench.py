@@ -52,6 +52,7 @@ def parse():
                    help="2, 3, 4: BASELINE collide configs; 5: RRTConnect plan(); 6: floor point cloud; "
                         "7: cfg3 with BVH mesh links (convex=False)")
     p.add_argument("--goal", default="far", help="cfg5 goal (scenes.PLAN_GOALS)")
+    p.add_argument("--spec-nodes", type=int, default=None, help="cfg5: outcome-tree nodes explored before each batch")
     p.add_argument("--cpu-plans", type=int, default=-1,
                    help="cfg5: plans timed with the CPU oracle checker (-1: the same seeds as the GPU run, 0: none)")
     p.add_argument("--per-gpu", type=int, default=0, help="configs per GPU per step (default: BASELINE size)")
@@ -263,6 +264,8 @@ def plan_main(args, world, rank, local, backend):
     os.dup2(2, 1)
     w, _ = scenes.world(3)
     planner = pymp.ompl.OMPLPlanner(w)
+    if args.spec_nodes is not None:
+        planner.set_speculation_nodes(args.spec_nodes)
 
     def one(seed):
         pymp.set_global_seed(seed)
@@ -305,6 +308,8 @@ def plan_main(args, world, rank, local, backend):
                    "parallelism": f"replicas x{world}"},
         "solved": solved, "mean_iterations": mean("iterations"), "mean_batches": mean("batches"),
         "mean_states_checked": mean("states_checked"), "mean_check_ms": mean("check_seconds") * 1e3,
+        "mean_spec_nodes": mean("spec_nodes"), "mean_spec_wait_nodes": mean("spec_wait_nodes"),
+        "mean_spec_ms": mean("t_spec") * 1e3,
         "roofline": {"bound": "latency", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBPS, "traffic": None, "kernel": "small_kernel",
                      "kernel_ms": kern_ms, "units_per_launch": states_per_launch, "unit_kind": "states",

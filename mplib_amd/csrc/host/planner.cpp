@@ -5,6 +5,8 @@
 // in this image).  See planner.hpp for the batching scheme.
 #include "planner.hpp"
 
+#include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cmath>
 #include <cstring>
@@ -12,7 +14,10 @@
 #include <cstdio>
 #include <cstdlib>
 #include <limits>
+#include <queue>
 #include <stdexcept>
+#include <thread>
+#include <tuple>
 
 namespace mpgh {
 
@@ -325,14 +330,27 @@ bool all_valid(const std::vector<uint8_t>& v, size_t a, size_t b) {
   return true;
 }
 
+// bits of a state -> 64-bit key (validity cache, hypotheses, nearest memo)
+uint64_t hash_state(const double* s, int dim) {
+  uint64_t h = 0x9e3779b97f4a7c15ull;
+  for (int k = 0; k < dim; ++k) {
+    uint64_t x;
+    std::memcpy(&x, s + k, 8);
+    h ^= x + 0x9e3779b97f4a7c15ull + (h << 6) + (h >> 2);
+    h *= 0xff51afd7ed558ccdull;
+  }
+  return h ^ (h >> 33);
+}
+
 // state -> validity, open addressing over a pool of the states' bits (no
 // per-entry allocation: the planner queries it hundreds of times per iteration)
 class ValidityCache {
  public:
   explicit ValidityCache(int dim) : dim_(dim), slots_(1024, -1) {}
   // 1 valid, 0 invalid, -1 unknown
-  int find(const double* s) const {
-    size_t i = hash(s) & (slots_.size() - 1);
+  int find(const double* s) const { return find_h(s, hash_state(s, dim_)); }
+  int find_h(const double* s, uint64_t h) const {
+    size_t i = h & (slots_.size() - 1);
     for (;; i = (i + 1) & (slots_.size() - 1)) {
       const int e = slots_[i];
       if (e < 0) return -1;
@@ -340,32 +358,23 @@ class ValidityCache {
     }
   }
   void put(const double* s, uint8_t v) {
-    if (find(s) >= 0) return;
+    const uint64_t h = hash_state(s, dim_);
+    if (find_h(s, h) >= 0) return;
     if (2 * (val_.size() + 1) > slots_.size()) grow();
-    insert_index(s, (int)val_.size());
+    insert_index(h, (int)val_.size());
     pool_.insert(pool_.end(), s, s + dim_);
     val_.push_back(v);
   }
 
  private:
-  uint64_t hash(const double* s) const {
-    uint64_t h = 0x9e3779b97f4a7c15ull;
-    for (int k = 0; k < dim_; ++k) {
-      uint64_t x;
-      std::memcpy(&x, s + k, 8);
-      h ^= x + 0x9e3779b97f4a7c15ull + (h << 6) + (h >> 2);
-      h *= 0xff51afd7ed558ccdull;
-    }
-    return h ^ (h >> 33);
-  }
-  void insert_index(const double* s, int e) {
-    size_t i = hash(s) & (slots_.size() - 1);
+  void insert_index(uint64_t h, int e) {
+    size_t i = h & (slots_.size() - 1);
     while (slots_[i] >= 0) i = (i + 1) & (slots_.size() - 1);
     slots_[i] = e;
   }
   void grow() {
     slots_.assign(slots_.size() * 2, -1);
-    for (size_t e = 0; e < val_.size(); ++e) insert_index(pool_.data() + e * dim_, (int)e);
+    for (size_t e = 0; e < val_.size(); ++e) insert_index(hash_state(pool_.data() + e * dim_, dim_), (int)e);
   }
   int dim_;
   std::vector<int> slots_;
@@ -410,6 +419,675 @@ std::vector<std::vector<double>> path_rows(const PlanSpace& sp, const std::vecto
   for (const double* s : states) out.emplace_back(s, s + sp.dim);
   return out;
 }
+
+// start tree root .. sm, then gm .. goal tree root (RRTConnect's solution path)
+template <class T>
+std::vector<const double*> connect_path(const T& ts, int sm, const T& tg, int gm) {
+  std::vector<const double*> p1, out;
+  for (int m = sm; m >= 0; m = ts.parent[(size_t)m]) p1.push_back(ts.state(m));
+  for (auto it = p1.rbegin(); it != p1.rend(); ++it) out.push_back(*it);
+  for (int m = gm; m >= 0; m = tg.parent[(size_t)m]) out.push_back(tg.state(m));
+  return out;
+}
+template <class T>
+std::vector<const double*> root_path(const T& t, int m) {
+  std::vector<const double*> rev;
+  for (; m >= 0; m = t.parent[(size_t)m]) rev.push_back(t.state(m));
+  return std::vector<const double*>(rev.rbegin(), rev.rend());
+}
+
+// ---------------------------------------------------------------------------
+// RRTConnect with outcome-tree speculation
+//
+// The serial loop (above, OMPL's as written) asks for one motion's validity
+// at a time; each answer decides what is asked next.  Here the loop runs as
+// `advance` over a Branch: the two trees (committed nodes plus an overlay of
+// nodes added since the last batch), the iteration counter, the goal sampler
+// position and the position inside the iteration.  The real branch stops at
+// the first motion whose states are not in the validity cache.  From that
+// point an outcome tree is explored best first: each explored node is a copy
+// of the branch that assumes an outcome (valid / invalid) for every motion on
+// its path and stops at the next unknown motion; its probability is the
+// product of the outcome rates measured so far in this plan (extension and
+// connect motions separately).  One device batch carries the unknown states of
+// the real motion and of the explored nodes; while it runs on the GPU (a
+// helper thread waits on the synchronous C call) the host explores deeper.
+// When the answers arrive the real branch advances through the cache, the
+// explored node it stops at becomes the new root (its subtree is kept,
+// everything else dropped), and the unsent states below it form the next
+// batch.  Speculation only chooses which states ride in a batch; the real
+// branch consults nothing but the cache, so the tree is the serial loop's.
+// ---------------------------------------------------------------------------
+
+// committed tree nodes, rows plus columns (the nearest scan reads columns)
+struct BaseTree {
+  int dim = 0;
+  std::vector<double> st;
+  std::vector<std::vector<double>> col;
+  std::vector<int> parent;
+  void init(int d) {
+    dim = d;
+    col.assign((size_t)d, {});
+  }
+  int size() const { return (int)parent.size(); }
+  const double* state(int i) const { return st.data() + (size_t)i * dim; }
+  void add(const double* s, int par) {
+    st.insert(st.end(), s, s + dim);
+    for (int k = 0; k < dim; ++k) col[(size_t)k].push_back(s[k]);
+    parent.push_back(par);
+  }
+};
+
+// compound distances of nodes i0..i0+n of a column store to q, summed per node
+// in subspace order exactly as PlanSpace::distance does (vectorised across nodes)
+#pragma GCC push_options
+#pragma GCC optimize("O3", "no-math-errno")
+__attribute__((target_clones("avx2", "default"))) void l1_columns(const double* const* col, const uint8_t* so2,
+                                                                  int dim, const double* q, int64_t i0, int n,
+                                                                  double* out) {
+  for (int i = 0; i < n; ++i) out[i] = 0.0;
+  for (int k = 0; k < dim; ++k) {
+    const double* c = col[k] + i0;
+    const double qk = q[k];
+    if (so2[k]) {
+      for (int i = 0; i < n; ++i) {
+        const double dd = std::fabs(c[i] - qk);
+        out[i] += dd > kPi ? 2.0 * kPi - dd : dd;
+      }
+    } else {
+      for (int i = 0; i < n; ++i) {
+        const double diff = c[i] - qk;
+        const double a = std::fabs(diff);
+        out[i] += a > 1e-150 ? a : std::sqrt(diff * diff);
+      }
+    }
+  }
+}
+#pragma GCC pop_options
+
+// nearest committed node of tree t to q (first strict minimum in insertion
+// order), memoised per (tree, query) and extended when the tree grows
+class NearMemo {
+ public:
+  explicit NearMemo(const PlanSpace& sp) : sp_(sp), slots_(4096, -1) {}
+  std::pair<int, double> get(const BaseTree& bt, int t, const double* q) {
+    const int d = sp_.dim;
+    const uint64_t h = hash_state(q, d) ^ (0x632be59bd9b4e019ull * (uint64_t)(t + 1));
+    size_t i = h & (slots_.size() - 1);
+    int e = -1;
+    for (;; i = (i + 1) & (slots_.size() - 1)) {
+      e = slots_[i];
+      if (e < 0) break;
+      const Ent& x = ents_[(size_t)e];
+      if (x.t == t && std::memcmp(qpool_.data() + x.qoff, q, sizeof(double) * d) == 0) break;
+    }
+    if (e < 0) {
+      if (2 * (ents_.size() + 1) > slots_.size()) {
+        if (ents_.size() >= (1u << 16)) {  // bound the memory of long runs: start over
+          ents_.clear();
+          qpool_.clear();
+          slots_.assign(4096, -1);
+        } else {
+          grow();
+        }
+        return get(bt, t, q);
+      }
+      e = (int)ents_.size();
+      slots_[i] = e;
+      ents_.push_back(Ent{t, qpool_.size(), -1, std::numeric_limits<double>::infinity(), 0});
+      qpool_.insert(qpool_.end(), q, q + d);
+    }
+    Ent& x = ents_[(size_t)e];
+    if (x.upto < bt.size()) {
+      cols_.resize((size_t)d);
+      for (int k = 0; k < d; ++k) cols_[(size_t)k] = bt.col[(size_t)k].data();
+      const double* const* cols = cols_.data();
+      double buf[256];
+      const double* qq = qpool_.data() + x.qoff;
+      for (int i0 = x.upto; i0 < bt.size(); i0 += 256) {
+        const int n = std::min(256, bt.size() - i0);
+        l1_columns(cols, sp_.so2.data(), d, qq, i0, n, buf);
+        for (int k = 0; k < n; ++k)
+          if (buf[k] < x.dist) {
+            x.dist = buf[k];
+            x.best = i0 + k;
+          }
+      }
+      x.upto = bt.size();
+    }
+    return {x.best, x.dist};
+  }
+
+ private:
+  struct Ent {
+    int t;
+    size_t qoff;
+    int best;
+    double dist;
+    int upto;
+  };
+  void grow() {
+    slots_.assign(slots_.size() * 2, -1);
+    for (size_t e = 0; e < ents_.size(); ++e) {
+      const Ent& x = ents_[e];
+      const uint64_t h = hash_state(qpool_.data() + x.qoff, sp_.dim) ^ (0x632be59bd9b4e019ull * (uint64_t)(x.t + 1));
+      size_t i = h & (slots_.size() - 1);
+      while (slots_[i] >= 0) i = (i + 1) & (slots_.size() - 1);
+      slots_[i] = (int)e;
+    }
+  }
+  const PlanSpace& sp_;
+  std::vector<int> slots_;
+  std::vector<Ent> ents_;
+  std::vector<double> qpool_;
+  std::vector<const double*> cols_;
+};
+
+// one validity batch on the device from a helper thread, so that the planner
+// thread keeps exploring while the GPU works (the C call is synchronous)
+class AsyncCheck {
+ public:
+  explicit AsyncCheck(mpg_world* w) : w_(w), th_([this] { loop(); }) {}
+  ~AsyncCheck() {
+    state_.store(kQuit, std::memory_order_release);
+    th_.join();
+  }
+  void submit(const std::vector<double>& states, int dim) {
+    q_ = states;
+    n_ = (int64_t)(states.size() / (size_t)dim);
+    flags_.assign((size_t)n_, 0);
+    state_.store(kWork, std::memory_order_release);
+  }
+  bool done() const { return state_.load(std::memory_order_acquire) == kDone; }
+  // valid[i] for the submitted states; throws on a device error
+  void result(std::vector<uint8_t>& valid) {
+    while (!done()) cpu_relax();
+    state_.store(kIdle, std::memory_order_relaxed);
+    check_status(rc_, "mpg_collide_batch");
+    valid.resize((size_t)n_);
+    for (int64_t i = 0; i < n_; ++i) valid[(size_t)i] = flags_[(size_t)i] ? 0 : 1;
+  }
+
+ private:
+  static constexpr int kIdle = 0, kWork = 1, kDone = 2, kQuit = 3;
+  static void cpu_relax() { __builtin_ia32_pause(); }
+  void loop() {
+    for (;;) {
+      int s;
+      while ((s = state_.load(std::memory_order_acquire)) != kWork && s != kQuit) cpu_relax();
+      if (s == kQuit) return;
+      rc_ = mpg_collide_batch(w_, q_.data(), n_, flags_.data(), nullptr, MPG_MEM_HOST, nullptr);
+      state_.store(kDone, std::memory_order_release);
+    }
+  }
+  mpg_world* w_;
+  std::vector<double> q_;
+  std::vector<uint8_t> flags_;
+  int64_t n_ = 0;
+  int rc_ = 0;
+  std::atomic<int> state_{kIdle};
+  std::thread th_;
+};
+
+class ConnectEngine {
+ public:
+  using SampleFn = std::function<void(double*)>;
+  using TimeoutFn = std::function<bool()>;
+  using CheckFn = std::function<void(const std::vector<double>&, std::vector<uint8_t>&)>;
+
+  ConnectEngine(const PlanSpace& sp, const GoalSet& goals, const std::vector<double>& start, double maxd,
+                OMPLPlanner::Stats& stats, SampleFn sample, TimeoutFn timed_out, CheckFn check, mpg_world* dev,
+                int spec_nodes)
+      : sp_(sp), d_(sp.dim), goals_(goals), maxd_(maxd), stats_(stats), sample_fn_(std::move(sample)),
+        timed_out_(std::move(timed_out)), check_(std::move(check)), spec_nodes_(spec_nodes), vc_(sp.dim),
+        memo_(sp), rbuf_((size_t)sp.dim), xbuf_((size_t)sp.dim) {
+    base_[0].init(d_);
+    base_[1].init(d_);
+    base_[0].add(start.data(), -1);
+    if (dev) async_.reset(new AsyncCheck(dev));
+  }
+
+  // (status, path) as the serial loop returns them
+  std::pair<std::string, std::vector<const double*>> run() {
+    Branch& R = real_;
+    Blocked rb;
+    for (;;) {
+      const Adv a = advance(R, true, 0, rb);
+      if (a == A_SOLVED) {
+        commit();
+        int sm = R.tgi_start ? R.xmotion : R.added;
+        int gm = R.tgi_start ? R.added : R.xmotion;
+        if (base_[0].parent[(size_t)sm] >= 0)
+          sm = base_[0].parent[(size_t)sm];
+        else
+          gm = base_[1].parent[(size_t)gm];
+        sizes();
+        return {"Exact solution", connect_path(base_[0], sm, base_[1], gm)};
+      }
+      if (a != A_BLOCKED) break;  // timeout or no goal
+      batch_round(rb);
+    }
+    commit();
+    sizes();
+    if (approxsol_ >= 0) return {"Approximate solution", root_path(base_[0], approxsol_)};
+    return {"Timeout", {}};
+  }
+
+ private:
+  enum Adv { A_BLOCKED, A_SOLVED, A_END, A_LIMIT };
+  enum Kind { K_EXT = 0, K_CONN = 1 };
+  struct Branch {
+    std::vector<double> ost[2];  // overlay: nodes added since the last commit
+    std::vector<int> opar[2];    // their parents (global node indices)
+    int64_t it = 0;              // iteration (index of its uniform sample)
+    bool start_tree = true;      // RRTConnect::startTree_ before iteration `it`
+    size_t g_sampled = 0, g_pos = 0;
+    int phase = 0;  // 0 iteration start, 1 extension, 2 connect
+    int tr = 0;     // tree extended in this iteration (0 start, 1 goal)
+    std::vector<double> target;
+    int added = -1, xmotion = -1, n_conn = 0;
+    bool tgi_start = false;
+    std::vector<uint64_t> hv, hinv;  // assumed valid states, assumed invalid motions
+  };
+  struct Blocked {
+    std::vector<double> st;  // the motion's states not known yet
+    std::vector<uint64_t> h;
+    uint64_t key = 0;
+    int kind = K_EXT;
+  };
+  struct SNode {
+    Branch br;  // stopped at `blk`
+    Blocked blk;
+    double p = 1.0;  // probability of reaching it from the root
+    int child[2] = {-1, -1};  // [outcome invalid, valid]: -1 unexplored, -2 ends, else node
+  };
+
+  // ---- trees ----
+  int tree_size(const Branch& b, int t) const { return base_[t].size() + (int)b.opar[t].size(); }
+  const double* node(const Branch& b, int t, int gi) const {
+    const int nb = base_[t].size();
+    return gi < nb ? base_[t].state(gi) : b.ost[t].data() + (size_t)(gi - nb) * d_;
+  }
+  int add_node(Branch& b, int t, const double* s, int par) {
+    b.ost[t].insert(b.ost[t].end(), s, s + d_);
+    b.opar[t].push_back(par);
+    return tree_size(b, t) - 1;
+  }
+  int nearest(const Branch& b, int t, const double* q) {
+    auto bn = memo_.get(base_[t], t, q);
+    int best = bn.first;
+    double bd = bn.second;
+    const int nb = base_[t].size();
+    for (size_t k = 0; k < b.opar[t].size(); ++k) {
+      const double dd = sp_.distance_below(b.ost[t].data() + k * d_, q, bd);
+      if (dd < bd) {
+        bd = dd;
+        best = nb + (int)k;
+      }
+    }
+    return best;
+  }
+  const double* sample(int64_t it) {
+    while (samp0_ + (int64_t)(samp_.size() / (size_t)d_) <= it) {
+      const size_t o = samp_.size();
+      samp_.resize(o + (size_t)d_);
+      sample_fn_(samp_.data() + o);
+    }
+    return samp_.data() + (size_t)(it - samp0_) * d_;
+  }
+  const double* next_goal(Branch& b, bool keep_trying) const {  // GoalSet::next_goal on the branch's position
+    const size_t n = goals_.count();
+    while (b.g_sampled < n) {
+      const size_t idx = b.g_pos;
+      b.g_pos = (b.g_pos + 1) % n;
+      b.g_sampled += 1;
+      if (goals_.usable[idx]) return goals_.state(idx);
+      if (!keep_trying) break;
+    }
+    return nullptr;
+  }
+
+  // ---- validity: 1 valid, 0 invalid, -1 unknown (blk gets the unknown states)
+  int status(const Branch& b, const std::vector<double>& mot, Blocked& blk) const {
+    const size_t n = mot.size() / (size_t)d_;
+    blk.st.clear();
+    blk.h.clear();
+    uint64_t key = 0x2545f4914f6cdd1dull;
+    bool invalid = false;
+    for (size_t i = 0; i < n; ++i) {
+      const double* s = mot.data() + i * d_;
+      const uint64_t h = hash_state(s, d_);
+      key = (key ^ h) * 0x9e3779b97f4a7c15ull + (key >> 29);
+      const int v = vc_.find_h(s, h);
+      if (v == 0) invalid = true;
+      if (v < 0 && std::find(b.hv.begin(), b.hv.end(), h) == b.hv.end()) {
+        blk.st.insert(blk.st.end(), s, s + d_);
+        blk.h.push_back(h);
+      }
+    }
+    if (invalid) return 0;
+    if (blk.h.empty()) return 1;
+    blk.key = key;
+    if (std::find(b.hinv.begin(), b.hinv.end(), key) != b.hinv.end()) return 0;
+    return -1;
+  }
+  void record(int kind, int v) {
+    n_out_[kind] += 1;
+    n_ok_[kind] += v;
+  }
+  double prob(int kind, int outcome) const {
+    const double pv = (n_ok_[kind] + 1.0) / (n_out_[kind] + 2.0);
+    return outcome ? pv : 1.0 - pv;
+  }
+
+  // ---- the serial loop, resumable: runs b until a motion's validity is
+  // unknown (A_BLOCKED, blk = that motion), a connection (A_SOLVED) or the end
+  // (real: timeout / no goal; speculative: max_iters iterations, A_LIMIT)
+  Adv advance(Branch& b, bool real, int max_iters, Blocked& blk) {
+    int iters = 0;
+    for (;;) {
+      if (b.phase == 0) {
+        if (real) {
+          if (timed_out_()) return A_END;
+          stats_.iterations += 1;
+        } else if (++iters > max_iters) {
+          return A_LIMIT;
+        }
+        b.tr = b.start_tree ? 0 : 1;
+        b.start_tree = !b.start_tree;
+        const int gsize = tree_size(b, 1);
+        if (gsize == 0 || b.g_sampled < (size_t)gsize / 2) {
+          const double* g = next_goal(b, gsize == 0);
+          if (g) add_node(b, 1, g, -1);
+          if (tree_size(b, 1) == 0) return A_END;
+        }
+        b.phase = 1;
+      }
+      if (b.phase == 1) {  // extension: growTree(tree, rstate)
+        const double* r = sample(b.it);
+        std::copy(r, r + d_, rbuf_.begin());
+        const int n = nearest(b, b.tr, rbuf_.data());
+        const double* nst = node(b, b.tr, n);
+        const double* ds = rbuf_.data();
+        const double dd = sp_.distance(nst, rbuf_.data());
+        bool trapped = false;
+        if (dd > maxd_) {
+          sp_.interpolate(nst, rbuf_.data(), maxd_ / dd, xbuf_.data());
+          trapped = sp_.equal(nst, xbuf_.data());
+          ds = xbuf_.data();
+        }
+        if (!trapped) {
+          mot_.clear();
+          append_grow(sp_, b.tr == 0, nst, ds, mot_);
+          const int v = status(b, mot_, blk);
+          if (v < 0) {
+            blk.kind = K_EXT;
+            return A_BLOCKED;
+          }
+          if (real) record(K_EXT, v);
+          trapped = !v;
+          if (trapped && real) stats_.ext_trapped += 1;
+        }
+        if (trapped) {
+          b.it += 1;
+          b.phase = 0;
+          continue;
+        }
+        b.target.assign(ds, ds + d_);
+        b.added = add_node(b, b.tr, ds, n);
+        b.xmotion = b.added;
+        b.tgi_start = b.tr == 1;  // tgi.start = the connect tree is the start tree
+        b.n_conn = 0;
+        b.phase = 2;
+      }
+      // connect: growTree(other, target) while ADVANCED
+      const int o = 1 - b.tr;
+      const int n = nearest(b, o, b.target.data());
+      const double* nst = node(b, o, n);
+      const double* ds = b.target.data();
+      const double dd = sp_.distance(nst, b.target.data());
+      Grow g = REACHED;
+      bool need = true;
+      if (dd > maxd_) {
+        sp_.interpolate(nst, b.target.data(), maxd_ / dd, xbuf_.data());
+        ds = xbuf_.data();
+        g = ADVANCED;
+        if (sp_.equal(nst, xbuf_.data())) {
+          g = TRAPPED;
+          need = false;
+        }
+      }
+      if (need) {
+        mot_.clear();
+        append_grow(sp_, o == 0, nst, ds, mot_);
+        const int v = status(b, mot_, blk);
+        if (v < 0) {
+          blk.kind = K_CONN;
+          return A_BLOCKED;
+        }
+        if (real) record(K_CONN, v);
+        if (v)
+          b.xmotion = add_node(b, o, ds, n);
+        else
+          g = TRAPPED;
+      }
+      if (b.n_conn++ == 0 && g == TRAPPED) b.tgi_start = !b.tgi_start;
+      if (g == REACHED) return A_SOLVED;
+      if (g == TRAPPED) {
+        if (real && b.tgi_start) {  // approximate solution bookkeeping on the start tree
+          const double dist = goals_.distance_goal(node(b, 0, b.xmotion));
+          if (dist < approxdif_) {
+            approxdif_ = dist;
+            approxsol_ = b.xmotion;
+          }
+        }
+        b.it += 1;
+        b.phase = 0;
+      }
+    }
+  }
+
+  // move the real branch's overlay into the committed trees
+  void commit() {
+    for (int t = 0; t < 2; ++t) {
+      for (size_t k = 0; k < real_.opar[t].size(); ++k) base_[t].add(real_.ost[t].data() + k * d_, real_.opar[t][k]);
+      real_.ost[t].clear();
+      real_.opar[t].clear();
+    }
+  }
+  void sizes() {
+    stats_.start_tree = base_[0].size();
+    stats_.goal_tree = base_[1].size();
+  }
+
+  // explore outcome `o` of node `pi`'s motion
+  void expand(int pi, int o) {
+    SNode c;
+    c.br = nodes_[(size_t)pi].br;
+    const Blocked& pb = nodes_[(size_t)pi].blk;
+    if (o)
+      c.br.hv.insert(c.br.hv.end(), pb.h.begin(), pb.h.end());
+    else
+      c.br.hinv.push_back(pb.key);
+    c.p = nodes_[(size_t)pi].p * prob(pb.kind, o);
+    stats_.spec_nodes += 1;
+    if (advance(c.br, false, kMaxSpecIters, c.blk) != A_BLOCKED) {
+      nodes_[(size_t)pi].child[o] = -2;
+      return;
+    }
+    const int ci = (int)nodes_.size();
+    nodes_[(size_t)pi].child[o] = ci;
+    nodes_.push_back(std::move(c));
+    push_children(ci);
+  }
+  void push_children(int i) {
+    const SNode& s = nodes_[(size_t)i];
+    for (int o = 0; o < 2; ++o)
+      if (s.child[o] == -1) frontier_.emplace(s.p * prob(s.blk.kind, o), i, o);
+  }
+  bool expand_best() {
+    while (!frontier_.empty()) {
+      const auto top = frontier_.top();
+      frontier_.pop();
+      if (std::get<0>(top) < kMinProb) {
+        frontier_ = {};
+        return false;
+      }
+      if (nodes_[(size_t)std::get<1>(top)].child[std::get<2>(top)] != -1) continue;
+      expand(std::get<1>(top), std::get<2>(top));
+      return true;
+    }
+    return false;
+  }
+
+  // the real branch is blocked at `rb`: keep the explored subtree the real
+  // outcomes lead to (or start a new one), send its unknown states as one
+  // batch, explore while the batch runs, store the answers
+  void batch_round(const Blocked& rb) {
+    const auto t0 = Clock::now();
+    // descend along the real outcomes from the previous root
+    int cur = nodes_.empty() ? -1 : 0;
+    while (cur >= 0) {
+      const Blocked& b = nodes_[(size_t)cur].blk;
+      int v = 1;
+      for (size_t i = 0; i < b.h.size() && v != 0; ++i) {
+        const int x = vc_.find_h(b.st.data() + i * d_, b.h[i]);
+        if (x == 0) v = 0;
+        else if (x < 0) v = -1;
+      }
+      if (v < 0) break;
+      cur = nodes_[(size_t)cur].child[v];
+    }
+    const size_t n0 = real_.opar[0].size(), n1 = real_.opar[1].size();
+    bool keep = cur >= 0 && nodes_[(size_t)cur].blk.key == rb.key && nodes_[(size_t)cur].blk.h == rb.h &&
+                nodes_[(size_t)cur].br.it == real_.it && nodes_[(size_t)cur].br.opar[0].size() == n0 &&
+                nodes_[(size_t)cur].br.opar[1].size() == n1;
+    if (!keep) stats_.spec_resets += 1;
+    commit();
+    std::vector<SNode> kept;
+    frontier_ = {};
+    if (keep) {  // re-root: compact the subtree, probabilities relative to it
+      std::vector<int> q{cur};
+      std::vector<int> idx(nodes_.size(), -1);
+      idx[(size_t)cur] = 0;
+      kept.push_back(std::move(nodes_[(size_t)cur]));
+      kept[0].p = 1.0;
+      for (size_t h = 0; h < q.size(); ++h) {
+        const int ni = idx[(size_t)q[h]];
+        for (int o = 0; o < 2; ++o) {
+          const int c = kept[(size_t)ni].child[o];
+          if (c < 0) continue;
+          idx[(size_t)c] = (int)kept.size();
+          kept[(size_t)ni].child[o] = (int)kept.size();
+          SNode s = std::move(nodes_[(size_t)c]);
+          s.p = kept[(size_t)ni].p * prob(kept[(size_t)ni].blk.kind, o);
+          for (int t = 0; t < 2; ++t) {  // drop the committed prefix of the overlay
+            const size_t m = t ? n1 : n0;
+            s.br.ost[t].erase(s.br.ost[t].begin(), s.br.ost[t].begin() + (ptrdiff_t)(m * d_));
+            s.br.opar[t].erase(s.br.opar[t].begin(), s.br.opar[t].begin() + (ptrdiff_t)m);
+          }
+          kept.push_back(std::move(s));
+          q.push_back(c);
+        }
+      }
+      kept[0].br = real_;
+      kept[0].blk = rb;
+    } else {
+      SNode root;
+      root.br = real_;
+      root.blk = rb;
+      kept.push_back(std::move(root));
+    }
+    nodes_ = std::move(kept);
+    for (size_t i = 0; i < nodes_.size(); ++i) push_children((int)i);
+    // synchronous exploration when the kept subtree is small (or no GPU wait to hide it)
+    const int target_nodes = spec_nodes_ >= 0 ? spec_nodes_ : async_ ? kSyncNodes : kSyncCheckerNodes;
+    while ((int)nodes_.size() < target_nodes && (int)nodes_.size() < kMaxNodes && expand_best()) {
+    }
+    // the batch: unknown states of every node, by probability
+    std::vector<int> order(nodes_.size());
+    for (size_t i = 0; i < order.size(); ++i) order[i] = (int)i;
+    std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return nodes_[(size_t)a].p > nodes_[(size_t)b].p; });
+    batch_.clear();
+    seen_.assign(std::max<size_t>(64, 4 * nodes_.size() * 4), 0);
+    for (int i : order) {
+      const Blocked& b = nodes_[(size_t)i].blk;
+      for (size_t k = 0; k < b.h.size(); ++k) {
+        const double* s = b.st.data() + k * d_;
+        if (vc_.find_h(s, b.h[k]) >= 0 || !mark(b.h[k])) continue;
+        batch_.insert(batch_.end(), s, s + d_);
+      }
+      if (batch_.size() >= (size_t)kMaxBatch * d_) break;
+    }
+    stats_.t_spec += seconds_since(t0);
+    const auto tc = Clock::now();
+    if (async_) {
+      async_->submit(batch_, d_);
+      const auto tw = Clock::now();
+      const int64_t n_before = stats_.spec_nodes;
+      while (!async_->done() && (int)nodes_.size() < kMaxNodes && expand_best()) {
+      }
+      stats_.spec_wait_nodes += stats_.spec_nodes - n_before;
+      stats_.t_spec_wait += seconds_since(tw);
+      async_->result(valid_);
+      stats_.batches += 1;
+      stats_.states_checked += (int64_t)valid_.size();
+      stats_.check_seconds += seconds_since(tc);
+    } else {
+      check_(batch_, valid_);
+      // MPG_PLAN_EMULATE_WAIT=n: explore n more nodes after the batch is formed, as the device path does
+      // while a batch runs (lets CPU runs reproduce the device path's batches)
+      static const int emu = std::getenv("MPG_PLAN_EMULATE_WAIT") ? std::atoi(std::getenv("MPG_PLAN_EMULATE_WAIT")) : 0;
+      for (int k = 0; k < emu && (int)nodes_.size() < kMaxNodes && expand_best(); ++k) {
+      }
+    }
+    for (size_t i = 0; i < valid_.size(); ++i) vc_.put(batch_.data() + i * d_, valid_[i]);
+  }
+  // hash set of the batch's states (open addressing on the 64-bit keys)
+  bool mark(uint64_t h) {
+    const size_t m = seen_.size();
+    if (h == 0) h = 1;
+    for (size_t i = h % m;; i = (i + 1) % m) {
+      if (seen_[i] == h) return false;
+      if (seen_[i] == 0) {
+        seen_[i] = h;
+        return true;
+      }
+    }
+  }
+
+  static constexpr int kMaxSpecIters = 64;  // iterations a speculative branch may run without a new unknown
+  static constexpr int kMaxNodes = 4096;    // explored nodes kept
+  static constexpr int kMaxBatch = 2048;    // states per batch
+  static constexpr int kSyncNodes = 16;         // nodes explored before an asynchronous batch is sent
+  static constexpr int kSyncCheckerNodes = 64;  // nodes explored before a synchronous checker's batch
+  static constexpr double kMinProb = 1e-4;  // outcomes less likely than this are not explored
+
+  const PlanSpace& sp_;
+  const int d_;
+  const GoalSet& goals_;
+  const double maxd_;
+  OMPLPlanner::Stats& stats_;
+  SampleFn sample_fn_;
+  TimeoutFn timed_out_;
+  CheckFn check_;
+  const int spec_nodes_;
+  ValidityCache vc_;
+  NearMemo memo_;
+  BaseTree base_[2];
+  Branch real_;
+  std::vector<double> samp_;
+  int64_t samp0_ = 0;
+  std::vector<SNode> nodes_;
+  std::priority_queue<std::tuple<double, int, int>> frontier_;
+  std::unique_ptr<AsyncCheck> async_;
+  double n_out_[2] = {0, 0}, n_ok_[2] = {0, 0};
+  int approxsol_ = -1;
+  double approxdif_ = std::numeric_limits<double>::infinity();
+  std::vector<double> rbuf_, xbuf_, mot_, batch_;
+  std::vector<uint8_t> valid_;
+  std::vector<uint64_t> seen_;
+};
 
 }  // namespace
 
@@ -574,69 +1252,19 @@ std::pair<std::string, std::vector<std::vector<double>>> OMPLPlanner::plan(
   }
 
   // ---------------- RRTConnect (OMPL geometric/planners/rrt/src/RRTConnect.cpp) ----------------
+  if (speculative_) {
+    ConnectEngine eng(sp, goals, start, max_distance, stats_, [&](double* out) { sample_uniform(out); }, timed_out,
+                      [&](const std::vector<double>& st, std::vector<uint8_t>& v) { check(st, v); },
+                      custom_ ? nullptr : world_->device_world(), spec_nodes_);
+    auto r = eng.run();
+    return finish(r.first, path_rows(sp, r.second));
+  }
+  // OMPL's loop as written: one validity batch per growTree call
   Tree tstart(d), tgoal(d);
   tstart.add(start.data(), -1);
   bool start_tree = true;  // RRTConnect::startTree_
   int approxsol = -1;
   double approxdif = std::numeric_limits<double>::infinity();
-  struct Step {
-    std::vector<double> state;
-    int tree_parent, chain_parent;  // grows from a node of the other tree, or from chain step chain_parent
-    bool reach;
-    size_t a, b;  // its states in the batch
-  };
-  std::vector<Step> chain;
-  const size_t kMaxChain = 1u << 20;
-  // speculative mode: a validity cache (a state's validity is a pure function
-  // of the state) and uniform samples drawn ahead of their iteration -- the
-  // sampler's draws do not depend on validity, so drawing early keeps the
-  // sequence
-  ValidityCache vcache(d);
-  std::deque<std::vector<double>> ahead;
-  auto peek_sample = [&](size_t j) -> const std::vector<double>& {
-    while (ahead.size() <= j) {
-      std::vector<double> r((size_t)d);
-      sample_uniform(r.data());
-      ahead.push_back(std::move(r));
-    }
-    return ahead[j];
-  };
-  std::vector<double> ext_states, chain_states, spec_states;
-  constexpr int kLookahead = 3;
-  constexpr size_t kSpecCap = 4096;  // speculated states per batch
-  constexpr int kSpecSteps = 8;      // growTree steps of a speculated connect chain
-  // the connect chain growTree would run on t (plus `extra`, its newest
-  // node) towards x if every motion were valid (as below for the current
-  // iteration); its motions' states are appended to out
-  auto spec_chain = [&](const Tree& t, bool t_is_start, const double* extra, const double* x, std::vector<double>& out) {
-    double best;
-    const int n0 = t.nearest(sp, x, &best);
-    std::vector<double> cur(t.state(n0), t.state(n0) + d), stt((size_t)d);
-    if (extra && sp.distance(extra, x) < best) {
-      best = sp.distance(extra, x);
-      cur.assign(extra, extra + d);
-    }
-    for (int k = 0; k < kSpecSteps; ++k) {
-      const double dc = sp.distance(cur.data(), x);
-      bool reach_k = false;
-      if (dc > max_distance) {
-        sp.interpolate(cur.data(), x, max_distance / dc, stt.data());
-        if (sp.equal(cur.data(), stt.data())) return;
-      } else {
-        stt.assign(x, x + d);
-        reach_k = true;
-      }
-      append_grow(sp, t_is_start, cur.data(), stt.data(), out);
-      if (reach_k) return;
-      const double dn = sp.distance(stt.data(), x);
-      if (dn < best) {
-        best = dn;
-        cur = stt;
-      }
-    }
-  };
-  // RRTConnect::growTree (serial mode): nearest, step of at most maxDistance,
-  // the motion's states in one batch
   auto grow_serial = [&](Tree& t, bool is_start, const std::vector<double>& r, int& xm) -> Grow {
     const int n = t.nearest(sp, r.data());
     bool reach = true;
@@ -673,205 +1301,29 @@ std::pair<std::string, std::vector<std::vector<double>>> OMPLPlanner::plan(
         break;
       }
     }
-    if (!ahead.empty()) {
-      rstate = ahead.front();
-      ahead.pop_front();
-    } else {
-      sample_uniform(rstate.data());
-    }
-
+    sample_uniform(rstate.data());
     int added = -1, xmotion = -1;  // tgi.xmotion
     bool tgi_start = other_is_start;
-    Grow gsc = TRAPPED;
-    if (!speculative_) {
-      // OMPL's loop as written: one validity batch per growTree call
-      if (grow_serial(tree, tree_is_start, rstate, added) == TRAPPED) {
-        stats_.ext_trapped += 1;
-        continue;
-      }
-      xmotion = added;
-      rstate.assign(tree.state(added), tree.state(added) + d);  // copyState(rstate, tgi.xstate) when not REACHED
-      gsc = grow_serial(other, other_is_start, rstate, xmotion);
-      if (gsc == TRAPPED) tgi_start = !tgi_start;
-      while (gsc == ADVANCED) gsc = grow_serial(other, other_is_start, rstate, xmotion);
-    } else {
-    // ---- extension of `tree` towards rstate (growTree)
-    const int nm = tree.nearest(sp, rstate.data());
-    bool reach = true;
-    const double* dstate = rstate.data();
-    const double dd = sp.distance(tree.state(nm), rstate.data());
-    if (dd > max_distance) {
-      sp.interpolate(tree.state(nm), rstate.data(), max_distance / dd, xstate.data());
-      if (sp.equal(tree.state(nm), xstate.data())) continue;  // TRAPPED
-      dstate = xstate.data();
-      reach = false;
-    }
-    ext_states.clear();
-    append_grow(sp, tree_is_start, tree.state(nm), dstate, ext_states);
-    const std::vector<double> target(dstate, dstate + d);  // rstate after "copyState(rstate, tgi.xstate)"
-
-    // ---- speculative connect chain of `other` towards target, computed as
-    // the serial loop would compute it if every motion were valid: each step
-    // grows from the nearest node of other + the chain so far
-    const auto tc0 = Clock::now();
-    chain.clear();
-    chain_states.clear();
-    double best_d;
-    int tp = other.nearest(sp, target.data(), &best_d), cp = -1;
-    std::vector<double> cur(other.state(tp), other.state(tp) + d);
-    while (chain.size() < kMaxChain) {
-      Step stp;
-      stp.tree_parent = tp;
-      stp.chain_parent = cp;
-      const double dc = sp.distance(cur.data(), target.data());
-      if (dc > max_distance) {
-        stp.state.resize((size_t)d);
-        sp.interpolate(cur.data(), target.data(), max_distance / dc, stp.state.data());
-        if (sp.equal(cur.data(), stp.state.data())) break;  // TRAPPED without a motion
-        stp.reach = false;
-      } else {
-        stp.state = target;
-        stp.reach = true;
-      }
-      stp.a = chain_states.size() / (size_t)d;
-      append_grow(sp, other_is_start, cur.data(), stp.state.data(), chain_states);
-      stp.b = chain_states.size() / (size_t)d;
-      chain.push_back(std::move(stp));
-      if (chain.back().reach) break;
-      // nearest for the next growTree: the first strict minimum over the
-      // tree and the chain in insertion order
-      const double dn = sp.distance(chain.back().state.data(), target.data());
-      if (dn < best_d) {
-        best_d = dn;
-        tp = -1;
-        cp = (int)chain.size() - 1;
-      }
-      if (tp >= 0)
-        cur.assign(other.state(tp), other.state(tp) + d);
-      else
-        cur = chain[(size_t)cp].state;
-    }
-
-    // one batch: the states of this iteration not known yet, plus the
-    // extensions the next kLookahead iterations would try for every outcome
-    // of this one (assuming the ones in between are trapped)
-    auto known = [&](const std::vector<double>& st, size_t a, size_t b, bool& ok) {
-      ok = true;
-      bool all = true;
-      for (size_t i = a; i < b; ++i) {
-        const int v = vcache.find(st.data() + i * d);
-        if (v < 0) all = false;
-        else if (v == 0) ok = false;
-      }
-      return all;
-    };
-    auto need = [&](const std::vector<double>& st, size_t a, size_t b) {
-      for (size_t i = a; i < b; ++i)
-        if (vcache.find(st.data() + i * d) < 0) batch.insert(batch.end(), st.data() + i * d, st.data() + (i + 1) * d);
-    };
-    // every state goes through the cache: this iteration's extension and
-    // connect chain, and the speculated ones (the next iterations'
-    // extensions for every outcome of this one, and the connect chains the
-    // next iteration would run after them)
-    batch.clear();
-    bool ext_ok;
-    const size_t n_ext = ext_states.size() / (size_t)d;
-    const bool ext_known = known(ext_states, 0, n_ext, ext_ok);
-    if (!ext_known || ext_ok) {
-      need(ext_states, 0, n_ext);
-      need(chain_states, 0, chain_states.size() / (size_t)d);
-      if (!batch.empty()) {
-        stats_.t_chain += seconds_since(tc0);
-        const auto ts0 = Clock::now();
-        spec_states.clear();
-        for (int j = 1; j <= kLookahead; ++j) {
-          const bool fut_other = (j & 1) != 0;  // iteration i+1 extends `other`, i+2 `tree`, ...
-          Tree& ft = fut_other ? other : tree;
-          const bool ft_start = fut_other ? other_is_start : tree_is_start;
-          const std::vector<double>& rj = peek_sample((size_t)j - 1);
-          std::vector<const double*> cand;
-          double be;
-          const int ne = ft.nearest(sp, rj.data(), &be);
-          cand.push_back(ft.state(ne));
-          if (fut_other) {  // prefix minima of the connect chain
-            double run = be;
-            for (auto& c : chain) {
-              const double dc = sp.distance(c.state.data(), rj.data());
-              if (dc < run) {
-                run = dc;
-                cand.push_back(c.state.data());
-              }
-            }
-          } else if (sp.distance(target.data(), rj.data()) < be) {
-            cand.push_back(target.data());
-          }
-          if (&ft == &tgoal && goals.sampled < goals.count() && goals.usable[goals.sample_pos])
-            cand.push_back(goals.state(goals.sample_pos));  // a goal root added at that iteration's start
-          for (const double* c : cand) {
-            const double dj = sp.distance(c, rj.data());
-            std::vector<double> x(rj);
-            if (dj > max_distance) {
-              sp.interpolate(c, rj.data(), max_distance / dj, x.data());
-              if (sp.equal(c, x.data())) continue;
-            }
-            append_grow(sp, ft_start, c, x.data(), spec_states);
-            // iteration i+1 connects `tree` (with this iteration's new node)
-            // towards x if that extension is valid
-            if (j == 1 && c == cand.front() && spec_states.size() < kSpecCap * (size_t)d)
-              spec_chain(tree, tree_is_start, target.data(), x.data(), spec_states);
-          }
-        }
-        const size_t spec_off = batch.size() / (size_t)d;
-        need(spec_states, 0, spec_states.size() / (size_t)d);
-        stats_.t_spec += seconds_since(ts0);
-        (void)spec_off;
-        check(batch, valid);
-        for (size_t i = 0; i < valid.size(); ++i) vcache.put(batch.data() + i * d, valid[i]);
-      }
-      known(ext_states, 0, n_ext, ext_ok);
-    }
-    if (!ext_ok) {  // extension TRAPPED
+    if (grow_serial(tree, tree_is_start, rstate, added) == TRAPPED) {
       stats_.ext_trapped += 1;
       continue;
     }
-    added = tree.add(target.data(), nm);
-    (void)reach;
-    // ---- connect: growTree on `other` while ADVANCED
     xmotion = added;
-    std::vector<int> node(chain.size(), -1);
-    for (size_t k = 0; k < chain.size(); ++k) {
-      const Step& s = chain[k];
-      bool ok_k = true;
-      for (size_t i = s.a; i < s.b && ok_k; ++i) ok_k = vcache.find(chain_states.data() + i * d) == 1;
-      if (!ok_k) {
-        gsc = TRAPPED;
-        break;
-      }
-      node[k] = other.add(s.state.data(), s.tree_parent >= 0 ? s.tree_parent : node[(size_t)s.chain_parent]);
-      xmotion = node[k];
-      gsc = s.reach ? REACHED : ADVANCED;
-      if (gsc == REACHED) break;
-    }
-    if (gsc == ADVANCED) gsc = TRAPPED;  // chain ended on a step without progress
-    if (node.empty() || node[0] < 0) tgi_start = !tgi_start;  // the first connect growTree was TRAPPED
-    }
+    rstate.assign(tree.state(added), tree.state(added) + d);  // copyState(rstate, tgi.xstate) when not REACHED
+    Grow gsc = grow_serial(other, other_is_start, rstate, xmotion);
+    if (gsc == TRAPPED) tgi_start = !tgi_start;
+    while (gsc == ADVANCED) gsc = grow_serial(other, other_is_start, rstate, xmotion);
 
     if (gsc == REACHED) {  // isStartGoalPairValid: always true for GoalStates
       int sm = tgi_start ? xmotion : added;
       int gm = tgi_start ? added : xmotion;
-      Tree& ts = tstart;
-      Tree& tg = tgoal;
-      if (ts.parent[(size_t)sm] >= 0)
-        sm = ts.parent[(size_t)sm];
+      if (tstart.parent[(size_t)sm] >= 0)
+        sm = tstart.parent[(size_t)sm];
       else
-        gm = tg.parent[(size_t)gm];
-      std::vector<const double*> p1, out;
-      for (int m = sm; m >= 0; m = ts.parent[(size_t)m]) p1.push_back(ts.state(m));
-      for (auto it = p1.rbegin(); it != p1.rend(); ++it) out.push_back(*it);
-      for (int m = gm; m >= 0; m = tg.parent[(size_t)m]) out.push_back(tg.state(m));
+        gm = tgoal.parent[(size_t)gm];
       stats_.start_tree = tstart.size();
       stats_.goal_tree = tgoal.size();
-      return finish("Exact solution", path_rows(sp, out));
+      return finish("Exact solution", path_rows(sp, connect_path(tstart, sm, tgoal, gm)));
     }
     if (tgi_start) {  // approximate solution bookkeeping on the start tree
       const double dist = goals.distance_goal(tstart.state(xmotion));
@@ -883,12 +1335,7 @@ std::pair<std::string, std::vector<std::vector<double>>> OMPLPlanner::plan(
   }
   stats_.start_tree = tstart.size();
   stats_.goal_tree = tgoal.size();
-  if (approxsol >= 0) {
-    std::vector<const double*> rev;
-    for (int m = approxsol; m >= 0; m = tstart.parent[(size_t)m]) rev.push_back(tstart.state(m));
-    std::vector<const double*> fwd(rev.rbegin(), rev.rend());
-    return finish("Approximate solution", path_rows(sp, fwd));
-  }
+  if (approxsol >= 0) return finish("Approximate solution", path_rows(sp, root_path(tstart, approxsol)));
   return finish("Timeout", {});
 }
 

@@ -11,13 +11,15 @@
 //   * OMPL 1.6.0's RRTConnect / RRT and DiscreteMotionValidator semantics
 //     (restated; OMPL is not in this image).
 // OMPL evaluates isValid() one state at a time (ompl_planner.h:59-62).  Here
-// every growth step of RRTConnect -- the extension AND the whole speculative
-// connect chain of the other tree -- is validated in ONE batched collide call
-// (one device pipeline, one synchronisation), so a planner iteration costs one
-// round trip instead of tens to hundreds of serial collision queries.  The
-// tree that results is the one the serial algorithm builds: the chain is
-// computed exactly as the serial loop would, then cut at its first invalid
-// motion.
+// RRTConnect runs as a resumable loop that stops at the first motion whose
+// validity is not cached; an outcome tree of the loop's future (each motion
+// valid or invalid, explored best first by the outcome rates seen so far) is
+// explored from that point, and the unknown states of the real motion and of
+// the explored ones go to the device as ONE batched collide call.  The host
+// explores deeper while the batch runs (a helper thread waits on the device),
+// so a plan costs far fewer round trips than growTree calls.  The tree that
+// results is the serial algorithm's: the real loop reads nothing but the
+// validity cache; speculation only chooses what rides in a batch.
 #pragma once
 
 #include <cstdint>
@@ -78,10 +80,14 @@ class OMPLPlanner {
   // replace the batched device checker (OMPL's setStateValidityChecker);
   // an empty function restores the device path
   void set_state_validity_checker(Checker c) { custom_ = std::move(c); }
-  // RRTConnect: validate the extension and the whole connect chain in one
-  // batch (default), or one batch per growTree call as OMPL's loop is written
+  // RRTConnect: outcome-tree speculation (default), or one batch per growTree
+  // call as OMPL's loop is written
   void set_speculative_connect(bool on) { speculative_ = on; }
   bool get_speculative_connect() const { return speculative_; }
+  // outcome-tree nodes explored before each batch is sent (-1: 16 on the device
+  // path, which also explores while each batch runs; 64 for custom checkers)
+  void set_speculation_nodes(int n) { spec_nodes_ = n; }
+  int get_speculation_nodes() const { return spec_nodes_; }
 
   std::vector<double> random_sample_nearby(const std::vector<double>& start);
   std::pair<std::string, std::vector<std::vector<double>>> plan(
@@ -92,8 +98,8 @@ class OMPLPlanner {
 
   struct Stats {
     int64_t iterations = 0, batches = 0, states_checked = 0, ext_trapped = 0;
-    int64_t start_tree = 0, goal_tree = 0;
-    double seconds = 0.0, check_seconds = 0.0, t_chain = 0.0, t_spec = 0.0;
+    int64_t start_tree = 0, goal_tree = 0, spec_nodes = 0, spec_wait_nodes = 0, spec_resets = 0;
+    double seconds = 0.0, check_seconds = 0.0, t_spec = 0.0, t_spec_wait = 0.0;
   };
   const Stats& last_stats() const { return stats_; }
 
@@ -105,6 +111,7 @@ class OMPLPlanner {
   PlanSpace space_;
   Checker custom_;
   bool speculative_ = true;
+  int spec_nodes_ = -1;
   Stats stats_;
   std::vector<uint8_t> flags_;
 };

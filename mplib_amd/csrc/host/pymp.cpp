@@ -836,9 +836,15 @@ PYBIND11_MODULE(pymp, m_all) {
            "Replace the device checker by a C function int fn(ctx, states[n*dim], n, valid[n]) (0 = ok).")
       .def("get_world", &OMPLPlanner::get_world)
       .def("set_speculative_connect", &OMPLPlanner::set_speculative_connect, py::arg("enable") = true,
-           "RRTConnect: validate the extension and the whole speculative connect chain in one batch (default), "
-           "or one batch per growTree call as OMPL's loop is written (same tree, more round trips).")
+           "RRTConnect: validate the blocked motion plus the explored outcome tree of the loop's future in one "
+           "batch (default), or one batch per growTree call as OMPL's loop is written (same tree, more round "
+           "trips).")
       .def("get_speculative_connect", &OMPLPlanner::get_speculative_connect)
+      .def("set_speculation_nodes", &OMPLPlanner::set_speculation_nodes, py::arg("n"),
+           "Outcome-tree nodes explored before each validity batch is sent (-1: 16 on the device path, which "
+           "keeps exploring while the batch runs, 64 with a custom checker); 0 sends only what is already "
+           "explored.")
+      .def("get_speculation_nodes", &OMPLPlanner::get_speculation_nodes)
       .def("get_dim", &OMPLPlanner::get_dim)
       .def("random_sample_nearby",
            [](OMPLPlanner& p, const std::vector<double>& s) { auto v = p.random_sample_nearby(s); return vec(v.data(), (int)v.size()); },
@@ -863,7 +869,7 @@ PYBIND11_MODULE(pymp, m_all) {
            py::arg("time") = 1.0, py::arg("range") = 0.0, py::arg("goal_bias") = 0.05,
            py::arg("pathlen_obj_weight") = 10.0, py::arg("pathlen_obj_only") = false, py::arg("verbose") = false,
            "Plan from start_state to any of goal_states (+-2pi variants of revolute joints are added); returns "
-           "(status, path[len, dim]). RRTConnect and RRT; every growth step is validated in one batched call.")
+           "(status, path[len, dim]). RRTConnect (speculative batches, see set_speculative_connect) and RRT.")
       .def("get_last_plan_stats",
            [](OMPLPlanner& p) {
              const auto& s = p.last_stats();
@@ -876,7 +882,10 @@ PYBIND11_MODULE(pymp, m_all) {
              d["goal_tree"] = s.goal_tree;
              d["seconds"] = s.seconds;
              d["check_seconds"] = s.check_seconds;
-             d["t_chain"] = s.t_chain;
+             d["spec_nodes"] = s.spec_nodes;
+             d["spec_wait_nodes"] = s.spec_wait_nodes;
+             d["spec_resets"] = s.spec_resets;
+             d["t_spec_wait"] = s.t_spec_wait;
              d["t_spec"] = s.t_spec;
              return d;
            },

@@ -563,14 +563,19 @@ __device__ __forceinline__ SE3 link_from_pose7(const double* p7) {
 // world transform of moving object `id` (link pose * collision origin) -- the
 // Isometry FCLModel::updateCollisionObjects hands to setTransform
 // USE_SC: joint (sin, cos) precomputed in `sc` (phase A), else computed inline
+// sc_row: the configuration's [dof][2] (sin, cos), or nullptr (computed inline)
+template <bool FROM_POSES>
+__device__ __forceinline__ SE3 moving_tf_row(const DevWorld& w, const double* __restrict__ in,
+                                             const double* sc_row, long long cfg, int id) {
+  const int l = w.moving_link[id];
+  const SE3 L = FROM_POSES ? link_from_pose7(in + (cfg * w.n_links + l) * 7)
+                           : link_from_oMi(w, chain_oMi(w, in + cfg * w.dof, l, sc_row), l, nullptr);
+  return se3_mul(L, load_se3(w.moving_offset + 12 * id));
+}
 template <bool FROM_POSES, bool USE_SC = true>
 __device__ __forceinline__ SE3 moving_tf(const DevWorld& w, const double* __restrict__ in,
                                          const double* __restrict__ sc, long long cfg, int id) {
-  const int l = w.moving_link[id];
-  const SE3 L = FROM_POSES ? link_from_pose7(in + (cfg * w.n_links + l) * 7)
-                           : link_from_oMi(w, chain_oMi(w, in + cfg * w.dof, l, USE_SC ? sc + cfg * w.dof * 2 : nullptr), l,
-                                           nullptr);
-  return se3_mul(L, load_se3(w.moving_offset + 12 * id));
+  return moving_tf_row<FROM_POSES>(w, in, USE_SC ? sc + cfg * w.dof * 2 : nullptr, cfg, id);
 }
 
 // Moving object -> FCL GJK object (shapeToGJK on link pose * offset).
@@ -2475,10 +2480,15 @@ __global__ __launch_bounds__(256) void small_sincos_kernel(DevWorld w, const dou
   }
 }
 
-// INLINE_SC: each lane computes its joints' exact sin/cos itself (one launch
-// per validity batch -- the planner's round trip); otherwise they come from
-// small_sincos_kernel (larger batches, where the P-fold recomputation costs
-// more than the extra launch)
+// INLINE_SC: each lane computes its configuration's exact joint sin/cos itself
+// (one launch per validity batch -- the planner's round trip) into its own LDS
+// row, kLatScGroup independent evaluations at a time so that their table loads
+// overlap (evaluated inside the chain walk they serialise: two objects' chains
+// of up to nine joints, each waiting on its table reads); otherwise they come
+// from small_sincos_kernel (larger batches, where the P-fold recomputation
+// costs more than the extra launch)
+constexpr int kLatScDof = 16;   // move-group dof the inline path holds (host: more -> small_sincos_kernel)
+constexpr int kLatScGroup = 4;
 template <bool FROM_POSES, int CLS, bool INLINE_SC = false>
 __global__ __launch_bounds__(256) void small_kernel(DevWorld w, const double* __restrict__ in, long long n, int n_tiles,
                                                    uint8_t* __restrict__ hits, const double* __restrict__ sc) {
@@ -2496,8 +2506,28 @@ __global__ __launch_bounds__(256) void small_kernel(DevWorld w, const double* __
   const bool am = a < w.n_moving, bm = b < w.n_moving;
   const int cf = w.pair_cf[p];
   if (!w.pair_allowed[p]) {  // ACM-allowed pairs are never reported (filterCollisions)
-    const SE3 TA = am ? moving_tf<FROM_POSES, !INLINE_SC>(w, in, sc, c, a) : load_se3(w.static_T + 12 * (a - w.n_moving));
-    const SE3 TB = bm ? moving_tf<FROM_POSES, !INLINE_SC>(w, in, sc, c, b) : load_se3(w.static_T + 12 * (b - w.n_moving));
+    const double* sc_row = FROM_POSES ? nullptr : sc + c * w.dof * 2;
+    if constexpr (INLINE_SC && !FROM_POSES) {
+      __shared__ double lat_sc[4][64][2 * kLatScDof];
+      double* mine = lat_sc[threadIdx.x >> 6][lane];
+      const double* qrow = in + c * w.dof;
+      if (am || bm) {
+        for (int k0 = 0; k0 < w.dof; k0 += kLatScGroup) {
+          double sv[kLatScGroup], cv[kLatScGroup];
+#pragma unroll
+          for (int i = 0; i < kLatScGroup; ++i) mpg_sincos(qrow[min(k0 + i, w.dof - 1)], &sv[i], &cv[i]);
+#pragma unroll
+          for (int i = 0; i < kLatScGroup; ++i)
+            if (k0 + i < w.dof) {
+              mine[2 * (k0 + i)] = sv[i];
+              mine[2 * (k0 + i) + 1] = cv[i];
+            }
+        }
+      }
+      sc_row = mine;
+    }
+    const SE3 TA = am ? moving_tf_row<FROM_POSES>(w, in, sc_row, c, a) : load_se3(w.static_T + 12 * (a - w.n_moving));
+    const SE3 TB = bm ? moving_tf_row<FROM_POSES>(w, in, sc_row, c, b) : load_se3(w.static_T + 12 * (b - w.n_moving));
     const int ga = am ? w.moving_geom[a] : w.static_geom[a - w.n_moving];
     const int gb = bm ? w.moving_geom[b] : w.static_geom[b - w.n_moving];
     const cptr<double> ra = w.geom_rec + G_STRIDE * ga, rb = w.geom_rec + G_STRIDE * gb;
@@ -5729,7 +5759,7 @@ int collide_small(mpg_world* w, const double* q, int64_t n, uint8_t* flags, uint
   StageTimer t_small(w, s, MPG_STAGE_NARROW);
   if (w->prof) w->prof_cfg += n;
   // batches of up to kSmallInlineSc states: one launch (sin/cos inline)
-  const bool inline_sc = FROM_POSES || n <= w->small_inline_sc;
+  const bool inline_sc = FROM_POSES || (n <= w->small_inline_sc && w->dw.dof <= kLatScDof);
   if (!inline_sc && w->dw.dof > 0) {
     const long long nt = n * w->dw.dof;
     hipLaunchKernelGGL(small_sincos_kernel, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, s, w->dw, qin,

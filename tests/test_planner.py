@@ -83,9 +83,12 @@ def test_rrtconnect_solution_is_valid(goal):
     assert s["iterations"] >= 1 and s["states_checked"] > 0
 
 
-@pytest.mark.parametrize("seed", [0, 1, 2])
-def test_speculative_connect_builds_the_serial_tree(seed):
+@pytest.mark.parametrize("seed,nodes", [(0, -1), (1, -1), (2, -1), (3, 0), (4, 3), (5, 200)])
+def test_speculative_connect_builds_the_serial_tree(seed, nodes):
+    """Outcome-tree speculation (any exploration budget) only changes which
+    states ride in a batch: same tree, same path, fewer batches."""
     p = planner()
+    p.set_speculation_nodes(nodes)
     out = []
     for spec in (True, False):
         p.set_speculative_connect(spec)
