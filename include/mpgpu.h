@@ -285,8 +285,13 @@ int mpg_distance_batch(mpg_world *world, const double *q, int64_t n, int32_t n_s
  * num_max_contacts = 1.  A point-cloud (OcTree) pair reports the contact of
  * the first occupied leaf of FCL's traversal that intersects the shape, with
  * the tree as the contact's o1 (normal from the leaf box into the shape).
- * Worlds whose non-allowed pairs include BVH mesh pairs return
- * MPG_E_UNSUPPORTED.
+ * A BVH-mesh pair reports the contact of its first intersecting triangle
+ * (pair) in triangle index order: mesh-mesh intersect_Triangle's deepest
+ * point of the shallower triangle (o1's frame -> world), shape-mesh the
+ * sphere-triangle contact or libccd MPR penetration of (shape, triangle),
+ * mesh-OcTree MPR penetration of (first hit leaf box, triangle).  FCL picks
+ * the first in its OBBRSS traversal order, so with several intersecting
+ * triangles the contact can be another of them (collision flags are equal).
  */
 #define MPG_INPUT_Q 0
 #define MPG_INPUT_LINK_POSES 1

@@ -120,8 +120,8 @@ struct DevWorld {
   cptr<int> mesh_tree;  // [n_geoms * 2]
 };
 enum { OG_ORIGIN = 0, OG_INV = 3, OG_DIMS = 4, OG_CELL0 = 7, OG_STRIDE = 8 };
-// triangle record: vertices P1 P2 P3, then the triangle's AABB
-enum { TR_P = 0, TR_LO = 9, TR_HI = 12, TR_STRIDE = 16 };
+// triangle record: vertices P1 P2 P3, the triangle's AABB, its index in the mesh
+enum { TR_P = 0, TR_LO = 9, TR_HI = 12, TR_ID = 15, TR_STRIDE = 16 };
 
 template <class P>
 MPG_INLINE SE3 load_se3(P p) {

@@ -2512,10 +2512,17 @@ __global__ __launch_bounds__(256) void small_kernel(DevWorld w, const double* __
       double* mine = lat_sc[threadIdx.x >> 6][lane];
       const double* qrow = in + c * w.dof;
       if (am || bm) {
+        // the row first, in one round of loads (it may sit in host memory)
+        double qv[kLatScDof];
+#pragma unroll
+        for (int k = 0; k < kLatScDof; ++k) qv[k] = qrow[min(k, w.dof - 1)];
+#pragma unroll
+        for (int k = 0; k < kLatScDof; ++k)
+          if (k < w.dof) mine[2 * k] = qv[k];
         for (int k0 = 0; k0 < w.dof; k0 += kLatScGroup) {
           double sv[kLatScGroup], cv[kLatScGroup];
 #pragma unroll
-          for (int i = 0; i < kLatScGroup; ++i) mpg_sincos(qrow[min(k0 + i, w.dof - 1)], &sv[i], &cv[i]);
+          for (int i = 0; i < kLatScGroup; ++i) mpg_sincos(mine[2 * min(k0 + i, w.dof - 1)], &sv[i], &cv[i]);
 #pragma unroll
           for (int i = 0; i < kLatScGroup; ++i)
             if (k0 + i < w.dof) {
@@ -4127,7 +4134,6 @@ __device__ bool octree_first_contact(const DevWorld& w, cptr<double> HV, int go,
 __host__ __device__ __forceinline__ bool cf_has_contact(int cf) {
   return cf != CF_NONE && cf != CF_OCTREE && cf != CF_MESH;
 }
-__host__ __device__ __forceinline__ bool cf_contact_supported(int cf) { return cf != CF_MESH; }
 
 __device__ bool closed_form_contact(int cf, const DevWorld& w, int ga, const SE3& TA, int gb, const SE3& TB,
                                     double& depth, V3& nd, V3& ps) {
@@ -4148,6 +4154,488 @@ __device__ bool closed_form_contact(int cf, const DevWorld& w, int ga, const SE3
   else h = sphere_box_contact(sb[0], TB, sa, TA, depth, nd, ps);  // CF_BOX_SPHERE
   nd = v3(-nd.x, -nd.y, -nd.z);
   return h;
+}
+
+// ---------------------------------------------------------------------------
+// Contacts on BVH-mesh pairs (CollisionRequest(enable_contact=True)), one lane
+// per reported (configuration, pair), the lane alone -- the same restatement
+// as oracle/collide_oracle.c mesh_contact [ext FCL 0.7.0, parity unpinned]:
+// the first intersecting triangle (pair) in triangle index order (FCL's own
+// order follows its OBBRSS traversal, not restated), then
+//   mesh-mesh    intersect_Triangle's contact branch (computeDeepestPoints
+//                of each triangle against the other's plane), o1's frame ->
+//                world;
+//   shape-mesh   sphereTriangleIntersect's contact for spheres, libccd MPR
+//                penetration of (shape, triangle GJK object) otherwise; the
+//                mesh-first order negates the normal;
+//   mesh-OcTree  the first occupied leaf in traversal order with a hit, MPR
+//                penetration of (leaf box, lowest such triangle).
+// The AABB prefilters only skip separated triangles, so the first hit in
+// index order is the oracle's (which prunes with bounding spheres).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void tri_plane(const double* v1, const double* v2, const double* v3, double* n, double& t) {
+  double a[3], b[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    a[k] = v2[k] - v1[k];
+    b[k] = v3[k] - v1[k];
+  }
+  c3(n, a, b);
+  const double z = d3(n, n);
+  if (!(z > 0)) {
+    n[0] = n[1] = n[2] = 0.0;
+    t = 0.0;
+    return;
+  }
+  const double r = std::sqrt(z);
+#pragma unroll
+  for (int k = 0; k < 3; ++k) n[k] /= r;
+  t = d3(n, v1);
+}
+
+// Intersect::computeDeepestPoints: depth and the first deepest vertex
+__device__ __forceinline__ int deepest_points(const double* T, const double* n, double t, double& pen, double* first) {
+  double max_depth = -DBL_MAX;
+  int num = 0, num_neg = 0, num_pos = 0, num_zero = 0;
+  for (int i = 0; i < 3; ++i) {
+    const double dist = -(d3(n, T + 3 * i) - t);
+    if (dist > 1e-5) num_pos++;
+    else if (dist < -1e-5) num_neg++;
+    else num_zero++;
+    if (dist > max_depth) {
+      max_depth = dist;
+      num = 1;
+      first[0] = T[3 * i];
+      first[1] = T[3 * i + 1];
+      first[2] = T[3 * i + 2];
+    } else if (dist + 1e-6 >= max_depth) {
+      num++;
+    }
+  }
+  if (max_depth < -1e-5) num = 0;
+  if (num_zero == 0 && (num_neg == 0 || num_pos == 0)) num = 0;
+  pen = max_depth;
+  return num;
+}
+
+__device__ int tri_tri_contact(const double* P, const double* Q, double* point, double* normal, double& depth) {
+  double n1[3], n2[3], t1, t2, d1[3] = {0, 0, 0}, d2[3] = {0, 0, 0}, pen1, pen2;
+  tri_plane(P, P + 3, P + 6, n1, t1);
+  tri_plane(Q, Q + 3, Q + 6, n2, t2);
+  const int k2 = deepest_points(Q, n1, t1, pen2, d2);
+  const int k1 = deepest_points(P, n2, t2, pen1, d1);
+  if (pen1 > pen2) {
+    for (int k = 0; k < 3; ++k) {
+      point[k] = d2[k];
+      normal[k] = -n1[k];
+    }
+    depth = pen2;
+    return min(k2, 2);
+  }
+  for (int k = 0; k < 3; ++k) {
+    point[k] = d1[k];
+    normal[k] = n2[k];
+  }
+  depth = pen1;
+  return min(k1, 2);
+}
+
+__device__ __forceinline__ double seg_sqr_dist_nearest(const double* from, const double* to, const double* p,
+                                                       double* nearest) {
+  double diff[3], v[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    diff[k] = p[k] - from[k];
+    v[k] = to[k] - from[k];
+  }
+  double t = d3(v, diff);
+  if (t > 0) {
+    const double vv = d3(v, v);
+    if (t < vv) {
+      t /= vv;
+#pragma unroll
+      for (int k = 0; k < 3; ++k) diff[k] -= v[k] * t;
+    } else {
+      t = 1;
+#pragma unroll
+      for (int k = 0; k < 3; ++k) diff[k] -= v[k];
+    }
+  } else {
+    t = 0;
+  }
+#pragma unroll
+  for (int k = 0; k < 3; ++k) nearest[k] = from[k] + v[k] * t;
+  return d3(diff, diff);
+}
+
+// sphereTriangleIntersect with its contact (W = world triangle)
+__device__ bool sphere_triangle_contact(double radius, const double* c, const double* W, double& depth, V3& nd,
+                                        V3& ps) {
+  double a[3], b[3], n[3], pc[3], cp[3] = {0, 0, 0};
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    a[k] = W[3 + k] - W[k];
+    b[k] = W[6 + k] - W[k];
+  }
+  c3(n, a, b);
+  const double z = d3(n, n);
+  if (z > 0) {
+    const double s = std::sqrt(z);
+    n[0] /= s;
+    n[1] /= s;
+    n[2] /= s;
+  }
+  const double rt = radius + DBL_EPSILON;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) pc[k] = c[k] - W[k];
+  double dist = d3(pc, n);
+  if (dist < 0) {
+    dist *= -1;
+    n[0] *= -1;
+    n[1] *= -1;
+    n[2] *= -1;
+  }
+  bool has = false;
+  if (dist < rt) {
+    double e1[3], e2[3], e3[3], u[3], v[3], x[3], en[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      e1[k] = W[3 + k] - W[k];
+      e2[k] = W[6 + k] - W[3 + k];
+      e3[k] = W[k] - W[6 + k];
+      u[k] = c[k] - W[k];
+      v[k] = c[k] - W[3 + k];
+      x[k] = c[k] - W[6 + k];
+    }
+    c3(en, e1, n);
+    const double r1 = d3(en, u);
+    c3(en, e2, n);
+    const double r2 = d3(en, v);
+    c3(en, e3, n);
+    const double r3 = d3(en, x);
+    if ((r1 > 0 && r2 > 0 && r3 > 0) || (r1 <= 0 && r2 <= 0 && r3 <= 0)) {
+      has = true;
+#pragma unroll
+      for (int k = 0; k < 3; ++k) cp[k] = c[k] - n[k] * dist;
+    } else {
+      const double rr = rt * rt;
+      double ne[3];
+      if (seg_sqr_dist_nearest(W, W + 3, c, ne) < rr) {
+        has = true;
+        cp[0] = ne[0]; cp[1] = ne[1]; cp[2] = ne[2];
+      }
+      if (seg_sqr_dist_nearest(W + 3, W + 6, c, ne) < rr) {
+        has = true;
+        cp[0] = ne[0]; cp[1] = ne[1]; cp[2] = ne[2];
+      }
+      if (seg_sqr_dist_nearest(W + 6, W, c, ne) < rr) {
+        has = true;
+        cp[0] = ne[0]; cp[1] = ne[1]; cp[2] = ne[2];
+      }
+    }
+  }
+  if (!has) return false;
+  const double cc[3] = {cp[0] - c[0], cp[1] - c[1], cp[2] - c[2]};
+  const double d2 = d3(cc, cc);
+  if (!(d2 < rt * rt)) return false;
+  if (d2 > 0) {
+    const double d = std::sqrt(d2);
+    nd = v3(cc[0] / d, cc[1] / d, cc[2] / d);
+    depth = -(radius - d);
+  } else {
+    nd = v3(-n[0], -n[1], -n[2]);
+    depth = -radius;
+  }
+  ps = v3(cp[0], cp[1], cp[2]);
+  return true;
+}
+
+// triangle GJK object support (supportTriangle) in world coordinates
+__device__ __forceinline__ CV3 tri_support(const GObj& b, const CV3* P, const CV3& tc, const CV3& dir) {
+  const CV3 db = quat_rot(dir, b.rot_inv);
+  ccd_real maxdot = -FLT_MAX;
+  CV3 lb = P[0];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const ccd_real dot = vdot(db, vsub(P[i], tc));
+    if (dot > maxdot) {
+      lb = P[i];
+      maxdot = dot;
+    }
+  }
+  return vadd(quat_rot(lb, b.rot), b.pos);
+}
+
+// MPR penetration of (object a, triangle of record rec in b's frame); a is a
+// shape (h == nullptr) or a box with half sizes h
+__device__ bool tri_mpr_penetration(const DevWorld& w, cptr<double> HV, const GObj& a, const ccd_real* h,
+                                    const GObj& b, cptr<double> rec, double& depth, V3& nd, V3& ps) {
+  double P[9];
+#pragma unroll
+  for (int k = 0; k < 9; ++k) P[k] = rec[TR_P + k];
+  const CV3 tc = cv3((P[0] + P[3] + P[6]) / 3, (P[1] + P[4] + P[7]) / 3, (P[2] + P[5] + P[8]) / 3);
+  const CV3 TP[3] = {cv3(P[0], P[1], P[2]), cv3(P[3], P[4], P[5]), cv3(P[6], P[7], P[8])};
+  ccd_real dc = 0;
+  CV3 n{0, 0, 0}, pc{0, 0, 0};
+  const CV3 ca = h ? a.pos : center(w, a);
+  const bool hit = mpr_penetration_core(
+      w.mpr_tol, ca, vadd(quat_rot(tc, b.rot), b.pos),
+      [&](const CV3& d) {
+        SupP sp;
+        if (h) {
+          const CV3 da = quat_rot(d, a.rot_inv);
+          const CV3 la = CV3{(da.x >= 0 ? ccd_real(1) : ccd_real(-1)) * h[0], (da.y >= 0 ? ccd_real(1) : ccd_real(-1)) * h[1],
+                             (da.z >= 0 ? ccd_real(1) : ccd_real(-1)) * h[2]};
+          sp.v1 = vadd(quat_rot(la, a.rot), a.pos);
+        } else {
+          sp.v1 = support(w, HV, a, d);
+        }
+        sp.v2 = tri_support(b, TP, tc, vscale(d, ccd_real(-1)));
+        sp.v = vsub(sp.v1, sp.v2);
+        return sp;
+      },
+      dc, n, pc);
+  if (hit) {
+    depth = dc;
+    nd = to_v3(n);
+    ps = to_v3(pc);
+  }
+  return hit;
+}
+
+__device__ __forceinline__ GObj posed_obj(const SE3& T, int g, int type) {
+  GObj o;
+  o.rot = gjk_rot_from_matrix(T.R);
+  o.rot_inv = quat_invert2(o.rot);
+  o.pos = cv3(T.p[0], T.p[1], T.p[2]);
+  o.geom = g;
+  o.type = type;
+  return o;
+}
+
+__device__ bool mesh_shape_first_contact(const DevWorld& w, cptr<double> HV, int gm, const SE3& TM, int gs,
+                                         const SE3& TS, bool mesh_first, double& depth, V3& nd, V3& ps) {
+  const cptr<double> grm = w.geom_rec + G_STRIDE * gm, grs = w.geom_rec + G_STRIDE * gs;
+  const int ts = w.geom_type[gs];
+  const int t0 = (int)grm[G_PARAM], t1 = t0 + (int)grm[G_PARAM + 1];
+  double sc[3], cl[3], Rl[9], hq[3];  // the shape's box in the mesh frame, as mesh_shape_wave
+  for (int i = 0; i < 3; ++i)
+    sc[i] = ((TS.R[3 * i] * grs[G_OBB_C] + TS.R[3 * i + 1] * grs[G_OBB_C + 1]) + TS.R[3 * i + 2] * grs[G_OBB_C + 2]) + TS.p[i];
+  const double dsc[3] = {sc[0] - TM.p[0], sc[1] - TM.p[1], sc[2] - TM.p[2]};
+  for (int i = 0; i < 3; ++i) {
+    cl[i] = (TM.R[i] * dsc[0] + TM.R[3 + i] * dsc[1]) + TM.R[6 + i] * dsc[2];
+    for (int j = 0; j < 3; ++j) Rl[3 * i + j] = (TM.R[i] * TS.R[j] + TM.R[3 + i] * TS.R[3 + j]) + TM.R[6 + i] * TS.R[6 + j];
+  }
+  for (int i = 0; i < 3; ++i)
+    hq[i] = ((std::fabs(Rl[3 * i]) * grs[G_OBB_E] + std::fabs(Rl[3 * i + 1]) * grs[G_OBB_E + 1]) +
+             std::fabs(Rl[3 * i + 2]) * grs[G_OBB_E + 2]) * (1.0 + 1e-9) +
+            kMeshShapePad * (1.0 + std::fabs(TS.p[0]) + std::fabs(TS.p[1]) + std::fabs(TS.p[2]) + std::fabs(TM.p[0]) +
+                             std::fabs(TM.p[1]) + std::fabs(TM.p[2]));
+  const GObj A = posed_obj(TS, gs, ts), B = posed_obj(TM, gm, MPG_GEOM_MESH);
+  int best = INT_MAX;
+  double bd = 0.0;
+  V3 bn{0, 0, 0}, bp{0, 0, 0};
+  for (int t = t0; t < t1; ++t) {
+    const cptr<double> rec = w.mesh_tri + TR_STRIDE * (size_t)t;
+    const int id = (int)rec[TR_ID];
+    if (id >= best) continue;
+    bool out = false;
+    for (int i = 0; i < 3; ++i) out |= rec[TR_LO + i] > cl[i] + hq[i] || rec[TR_HI + i] < cl[i] - hq[i];
+    if (out) continue;
+    double dp = 0.0;
+    V3 n{0, 0, 0}, p{0, 0, 0};
+    bool hit;
+    if (ts == MPG_GEOM_SPHERE) {
+      double W[9];
+      for (int v = 0; v < 3; ++v)
+        for (int i = 0; i < 3; ++i)
+          W[3 * v + i] = ((TM.R[3 * i] * rec[3 * v] + TM.R[3 * i + 1] * rec[3 * v + 1]) + TM.R[3 * i + 2] * rec[3 * v + 2]) +
+                         TM.p[i];
+      hit = sphere_triangle_contact(grs[G_PARAM], TS.p, W, dp, n, p);
+    } else {
+      hit = tri_mpr_penetration(w, HV, A, nullptr, B, rec, dp, n, p);
+    }
+    if (hit) {
+      best = id;
+      bd = dp;
+      bn = n;
+      bp = p;
+    }
+  }
+  depth = bd;
+  nd = mesh_first ? v3(-bn.x, -bn.y, -bn.z) : bn;
+  ps = bp;
+  return best != INT_MAX;
+}
+
+__device__ bool mesh_mesh_first_contact(const DevWorld& w, int ga, const SE3& TA, int gb, const SE3& TB, double& depth,
+                                        V3& nd, V3& ps) {
+  const cptr<double> gra = w.geom_rec + G_STRIDE * ga, grb = w.geom_rec + G_STRIDE * gb;
+  const int b0 = (int)grb[G_PARAM], b1 = b0 + (int)grb[G_PARAM + 1];
+  const int c0 = w.mesh_tree[2 * ga], c1 = c0 + w.mesh_tree[2 * ga + 1];
+  double R[9], T[3], alo[3], ahi[3];
+  const double dt[3] = {TB.p[0] - TA.p[0], TB.p[1] - TA.p[1], TB.p[2] - TA.p[2]};
+  for (int i = 0; i < 3; ++i) {
+    for (int j = 0; j < 3; ++j) R[3 * i + j] = (TA.R[i] * TB.R[j] + TA.R[3 + i] * TB.R[3 + j]) + TA.R[6 + i] * TB.R[6 + j];
+    T[i] = (TA.R[i] * dt[0] + TA.R[3 + i] * dt[1]) + TA.R[6 + i] * dt[2];
+    alo[i] = gra[G_OBB_C + i] - gra[G_OBB_E + i];
+    ahi[i] = gra[G_OBB_C + i] + gra[G_OBB_E + i];
+  }
+  long long best = LLONG_MAX;
+  int best_a = -1, best_b = -1;
+  for (int j = b0; j < b1; ++j) {
+    const cptr<double> rq = w.mesh_tri + TR_STRIDE * (size_t)j;
+    const long long idb = (long long)rq[TR_ID];
+    double Q[9], qlo[3], qhi[3];
+    for (int v = 0; v < 3; ++v)
+      for (int i = 0; i < 3; ++i)
+        Q[3 * v + i] = ((R[3 * i] * rq[3 * v] + R[3 * i + 1] * rq[3 * v + 1]) + R[3 * i + 2] * rq[3 * v + 2]) + T[i];
+    bool keep = true;
+    for (int i = 0; i < 3; ++i) {
+      qlo[i] = fmin(Q[i], fmin(Q[3 + i], Q[6 + i])) - kMeshPad;
+      qhi[i] = fmax(Q[i], fmax(Q[3 + i], Q[6 + i])) + kMeshPad;
+      keep &= !(qlo[i] > ahi[i] || qhi[i] < alo[i]);
+    }
+    if (!keep) continue;
+    for (int c = c0; c < c1; ++c) {
+      const cptr<double> bx = w.mesh_node + 6 * (size_t)c;
+      bool ov = true;
+      for (int i = 0; i < 3; ++i) ov &= !(bx[i] > qhi[i] || bx[3 + i] < qlo[i]);
+      if (!ov) continue;
+      const int t1 = w.mesh_link[2 * c] + w.mesh_link[2 * c + 1];
+      for (int t = w.mesh_link[2 * c]; t < t1; ++t) {
+        const cptr<double> rp = w.mesh_tri + TR_STRIDE * (size_t)t;
+        const long long key = ((long long)rp[TR_ID] << 32) | idb;
+        if (key >= best) continue;
+        bool o2 = false;
+        for (int i = 0; i < 3; ++i) o2 |= rp[TR_LO + i] > qhi[i] || rp[TR_HI + i] < qlo[i];
+        if (o2) continue;
+        double P[9];
+        for (int q = 0; q < 9; ++q) P[q] = rp[TR_P + q];
+        if (tri_tri_intersect(P, Q)) {
+          best = key;
+          best_a = t;
+          best_b = j;
+        }
+      }
+    }
+  }
+  depth = 0.0;
+  nd = v3(0, 0, 0);
+  ps = v3(0, 0, 0);
+  if (best_a < 0) return false;
+  double P[9], Q[9], pt[3], nl[3], pen;
+  const cptr<double> rp = w.mesh_tri + TR_STRIDE * (size_t)best_a, rq = w.mesh_tri + TR_STRIDE * (size_t)best_b;
+  for (int q = 0; q < 9; ++q) P[q] = rp[TR_P + q];
+  for (int v = 0; v < 3; ++v)
+    for (int i = 0; i < 3; ++i)
+      Q[3 * v + i] = ((R[3 * i] * rq[3 * v] + R[3 * i + 1] * rq[3 * v + 1]) + R[3 * i + 2] * rq[3 * v + 2]) + T[i];
+  if (tri_tri_contact(P, Q, pt, nl, pen) > 0) {
+    double wp[3], wn[3];
+    for (int i = 0; i < 3; ++i) {
+      wp[i] = ((TA.R[3 * i] * pt[0] + TA.R[3 * i + 1] * pt[1]) + TA.R[3 * i + 2] * pt[2]) + TA.p[i];
+      wn[i] = (TA.R[3 * i] * nl[0] + TA.R[3 * i + 1] * nl[1]) + TA.R[3 * i + 2] * nl[2];
+    }
+    depth = pen;
+    nd = v3(wn[0], wn[1], wn[2]);
+    ps = v3(wp[0], wp[1], wp[2]);
+  }
+  return true;
+}
+
+__device__ bool mesh_octree_first_contact(const DevWorld& w, int gm, const SE3& TM, int go, const SE3& TO,
+                                          double& depth, V3& nd, V3& ps) {
+  const cptr<double> grm = w.geom_rec + G_STRIDE * gm;
+  const double pad = kMeshShapePad * (1.0 + std::fabs(TO.p[0]) + std::fabs(TO.p[1]) + std::fabs(TO.p[2]) +
+                                      std::fabs(TM.p[0]) + std::fabs(TM.p[1]) + std::fabs(TM.p[2]));
+  double Rm[9], Ro[9], mcw[3], blo[3], bhi[3];  // as mesh_octree_wave
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) {
+      Rm[3 * i + j] = (TO.R[i] * TM.R[j] + TO.R[3 + i] * TM.R[3 + j]) + TO.R[6 + i] * TM.R[6 + j];
+      Ro[3 * j + i] = Rm[3 * i + j];
+    }
+  for (int i = 0; i < 3; ++i)
+    mcw[i] = ((TM.R[3 * i] * grm[G_OBB_C] + TM.R[3 * i + 1] * grm[G_OBB_C + 1]) + TM.R[3 * i + 2] * grm[G_OBB_C + 2]) +
+             TM.p[i];
+  const double dmo[3] = {mcw[0] - TO.p[0], mcw[1] - TO.p[1], mcw[2] - TO.p[2]};
+  for (int i = 0; i < 3; ++i) {
+    const double c = (TO.R[i] * dmo[0] + TO.R[3 + i] * dmo[1]) + TO.R[6 + i] * dmo[2];
+    const double e = ((std::fabs(Rm[3 * i]) * grm[G_OBB_E] + std::fabs(Rm[3 * i + 1]) * grm[G_OBB_E + 1]) +
+                      std::fabs(Rm[3 * i + 2]) * grm[G_OBB_E + 2]) * (1.0 + 1e-9) + 1e-9 + pad;
+    blo[i] = c - e;
+    bhi[i] = c + e;
+  }
+  GObj A = posed_obj(TO, go, MPG_GEOM_BOX);
+  const GObj B = posed_obj(TM, gm, MPG_GEOM_MESH);
+  const int c0 = w.mesh_tree[2 * gm], c1 = c0 + w.mesh_tree[2 * gm + 1];
+  const cptr<double> gor = w.geom_rec + G_STRIDE * go;
+  const int l0 = (int)gor[G_PARAM], ln = (int)gor[G_PARAM + 1];
+  for (int l = l0; l < l0 + ln; ++l) {
+    const cptr<double> L = w.oct_leaf + 6 * (size_t)l;
+    bool out = false;
+    for (int i = 0; i < 3; ++i) out |= L[i] > bhi[i] || L[3 + i] < blo[i];
+    if (out) continue;
+    double c[3], side[3], cw[3], cm[3], hm[3];
+    for (int i = 0; i < 3; ++i) {
+      c[i] = (L[i] + L[3 + i]) * 0.5;
+      side[i] = L[3 + i] - L[i];
+    }
+    for (int i = 0; i < 3; ++i) cw[i] = ((TO.R[3 * i] * c[0] + TO.R[3 * i + 1] * c[1]) + TO.R[3 * i + 2] * c[2]) + TO.p[i];
+    const double dm[3] = {cw[0] - TM.p[0], cw[1] - TM.p[1], cw[2] - TM.p[2]};
+    for (int i = 0; i < 3; ++i) {
+      cm[i] = (TM.R[i] * dm[0] + TM.R[3 + i] * dm[1]) + TM.R[6 + i] * dm[2];
+      hm[i] = ((std::fabs(Ro[3 * i]) * side[0] + std::fabs(Ro[3 * i + 1]) * side[1]) + std::fabs(Ro[3 * i + 2]) * side[2]) *
+                  0.5 * (1.0 + 1e-9) + 1e-9 + pad;
+    }
+    A.pos = cv3(cw[0], cw[1], cw[2]);
+    const ccd_real h[3] = {(ccd_real)(side[0] / 2.0), (ccd_real)(side[1] / 2.0), (ccd_real)(side[2] / 2.0)};
+    int best = INT_MAX;
+    double bd = 0.0;
+    V3 bn{0, 0, 0}, bp{0, 0, 0};
+    for (int cl = c0; cl < c1; ++cl) {
+      const cptr<double> bx = w.mesh_node + 6 * (size_t)cl;
+      bool away = false;
+      for (int i = 0; i < 3; ++i) away |= bx[i] > cm[i] + hm[i] || bx[3 + i] < cm[i] - hm[i];
+      if (away) continue;
+      const int t1 = w.mesh_link[2 * cl] + w.mesh_link[2 * cl + 1];
+      for (int t = w.mesh_link[2 * cl]; t < t1; ++t) {
+        const cptr<double> rec = w.mesh_tri + TR_STRIDE * (size_t)t;
+        const int id = (int)rec[TR_ID];
+        if (id >= best) continue;
+        bool o2 = false;
+        for (int i = 0; i < 3; ++i) o2 |= rec[TR_LO + i] > cm[i] + hm[i] || rec[TR_HI + i] < cm[i] - hm[i];
+        if (o2) continue;
+        double dp = 0.0;
+        V3 n{0, 0, 0}, p{0, 0, 0};
+        if (tri_mpr_penetration(w, w.hull, A, h, B, rec, dp, n, p)) {
+          best = id;
+          bd = dp;
+          bn = n;
+          bp = p;
+        }
+      }
+    }
+    if (best != INT_MAX) {
+      depth = bd;
+      nd = bn;
+      ps = bp;
+      return true;
+    }
+  }
+  depth = 0.0;
+  nd = v3(0, 0, 0);
+  ps = v3(0, 0, 0);
+  return false;
+}
+
+__device__ bool mesh_first_contact(const DevWorld& w, cptr<double> HV, int ga, const SE3& TA, int gb, const SE3& TB,
+                                   double& depth, V3& nd, V3& ps) {
+  const int ta = w.geom_type[ga], tb = w.geom_type[gb];
+  if (ta == MPG_GEOM_MESH && tb == MPG_GEOM_MESH) return mesh_mesh_first_contact(w, ga, TA, gb, TB, depth, nd, ps);
+  if (tb == MPG_GEOM_OCTREE) return mesh_octree_first_contact(w, ga, TA, gb, TB, depth, nd, ps);
+  if (ta == MPG_GEOM_OCTREE) return mesh_octree_first_contact(w, gb, TB, ga, TA, depth, nd, ps);
+  if (ta == MPG_GEOM_MESH) return mesh_shape_first_contact(w, HV, ga, TA, gb, TB, true, depth, nd, ps);
+  return mesh_shape_first_contact(w, HV, gb, TB, ga, TA, false, depth, nd, ps);
 }
 
 template <bool FROM_POSES>
@@ -4186,6 +4674,12 @@ __global__ __launch_bounds__(256) void contact_kernel(DevWorld w, const double* 
         const SE3 TA = moving_tf<FROM_POSES>(w, in, sc, c, a);
         const SE3 TB = load_se3(w.static_T + 12 * (b - w.n_moving));
         octree_first_contact(w, HV, w.static_geom[b - w.n_moving], TB, w.moving_geom[a], TA, dp, nd, ps);
+      } else if (w.pair_cf[p] == CF_MESH) {
+        const SE3 TA = a < w.n_moving ? moving_tf<FROM_POSES>(w, in, sc, c, a) : load_se3(w.static_T + 12 * (a - w.n_moving));
+        const SE3 TB = b < w.n_moving ? moving_tf<FROM_POSES>(w, in, sc, c, b) : load_se3(w.static_T + 12 * (b - w.n_moving));
+        const int ga = a < w.n_moving ? w.moving_geom[a] : w.static_geom[a - w.n_moving];
+        const int gb = b < w.n_moving ? w.moving_geom[b] : w.static_geom[b - w.n_moving];
+        mesh_first_contact(w, HV, ga, TA, gb, TB, dp, nd, ps);
       } else if (cf_has_contact(w.pair_cf[p])) {
         const SE3 TA = a < w.n_moving ? moving_tf<FROM_POSES>(w, in, sc, c, a) : load_se3(w.static_T + 12 * (a - w.n_moving));
         const SE3 TB = b < w.n_moving ? moving_tf<FROM_POSES>(w, in, sc, c, b) : load_se3(w.static_T + 12 * (b - w.n_moving));
@@ -4415,7 +4909,6 @@ struct mpg_world {
   } motion;
   std::mutex motion_mu;
   bool has_closed_form = false;  // a non-allowed pair uses an FCL closed form
-  bool has_contactless = false;  // a non-allowed pair whose contacts the device does not compute
   bool has_octree = false;       // a non-allowed pair involves an octree
   bool octree_first = false;     // a non-allowed pair has its octree as o1 (C ABI only; pymp puts it second)
   bool any_closed_form = false;  // some pair (allowed or not) does, octrees aside
@@ -5168,6 +5661,7 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
         r[TR_LO + k] = std::min(r[TR_P + k], std::min(r[TR_P + 3 + k], r[TR_P + 6 + k]));
         r[TR_HI + k] = std::max(r[TR_P + k], std::max(r[TR_P + 3 + k], r[TR_P + 6 + k]));
       }
+      r[TR_ID] = (double)t;  // the triangle's index in the mesh (contacts: first in index order)
     }
     std::vector<int> order((size_t)tn);
     for (int64_t t = 0; t < tn; ++t) order[t] = (int)t;
@@ -5561,7 +6055,6 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
   dw.pair_cf = to_cptr<int>(base + o_cf);
   for (int p = 0; p < d->n_pairs; ++p) {
     w->has_closed_form |= pair_cf[p] != CF_NONE && !allowed[p];
-    w->has_contactless |= !cf_contact_supported(pair_cf[p]) && !allowed[p];
     w->has_octree |= pair_cf[p] == CF_OCTREE && !allowed[p];
     w->octree_first |= pair_cf[p] == CF_OCTREE && !allowed[p] && obj_geom_type(d, d->pair_a[p]) == MPG_GEOM_OCTREE;
     w->any_closed_form |= pair_cf[p] != CF_NONE && cf_class(pair_cf[p]) == CLS_CLOSED;
@@ -6029,9 +6522,6 @@ int mpg_collide_contacts(mpg_world* w, const double* input, int64_t n, int input
   if (n > 0 && ((!input && row > 0) || !flags || !pair_mask || !depth || !normal || !pos))
     return set_error(MPG_E_INVALID, "NULL buffer");
   if (mem != MPG_MEM_HOST && mem != MPG_MEM_DEVICE) return set_error(MPG_E_INVALID, "bad mem kind");
-  if (w->has_contactless)
-    return set_error(MPG_E_UNSUPPORTED,
-                     "contacts for BVH mesh pairs are not implemented");
   if (w->octree_first)  // contact_kernel reports the (shape, octree) order PlanningWorld uses
     return set_error(MPG_E_UNSUPPORTED, "contacts for a pair whose first object is an OcTree are not implemented");
   if (n == 0) return MPG_OK;

@@ -2225,6 +2225,316 @@ static int mesh_intersect(const orc_world *w, int ga, const real *Ta, int gb, co
     return mesh_shape_intersect(w, gb, Tb, ga, Ta, st);
 }
 
+/* ------------------------------------------------ BVH-mesh contacts
+ * CollisionRequest(enable_contact=True) on a pair with a BVH-mesh side
+ * [ext FCL 0.7.0, restated from its published source; FCL is not under
+ * /root/reference, so this is parity unpinned]:
+ *   mesh-mesh   MeshCollisionTraversalNodeOBBRSS::leafTesting with contacts:
+ *               Intersect::intersect_Triangle(P, Q, R, T, contacts, &n,
+ *               &penetration, &normal) -- the same 17-axis test, then
+ *               buildTrianglePlane of both triangles and computeDeepestPoints
+ *               of each triangle's vertices against the other's plane
+ *               (EPSILON 1e-5, ties within 1e-6): if penetration1 >
+ *               penetration2 the contacts are Q's deepest points, normal -n1,
+ *               depth penetration2, else P's, n2, penetration1; FCL stores
+ *               tf1 * point and tf1.linear() * normal (o1's frame -> world).
+ *   shape-mesh / mesh-shape  shapeTriangleIntersect with contact output:
+ *               sphereTriangleIntersect's contact for spheres (stored depth
+ *               -(r - |c - p|)), otherwise GJKCollide -> ccdMPRPenetration of
+ *               (shape, triangle GJK object); the mesh-first node stores
+ *               -normal, so the normal points from o1 to o2 in both orders.
+ *   mesh-OcTree OcTreeMeshIntersectRecurse with contacts: MPR penetration of
+ *               (leaf box, triangle); the tree is the contact's o1.
+ * num_max_contacts = 1 keeps the first leaf test that emits a contact in
+ * FCL's traversal order.  For meshes that order follows FCL's OBBRSS tree,
+ * which is not restated: here the first is the lowest triangle index
+ * (mesh-mesh: the lexicographically lowest (triangle of o1, triangle of o2);
+ * octree pairs: the first occupied leaf in traversal order, then the lowest
+ * triangle).  With several intersecting triangle (pairs) the contact
+ * reported can be a different one of them than FCL's; the collision flag is
+ * the same.  A triangle pair whose deepest-point sets are both empty
+ * (degenerate triangles) is reported with a zero contact. */
+static real plane_dist(const real *n, real t, const real *v) { return dot3(n, v) - t; }
+
+/* buildTrianglePlane: unit normal (v2 - v1) x (v3 - v1) and offset n . v1 */
+static void build_triangle_plane(const real *v1, const real *v2, const real *v3, real *n, real *t) {
+    real a[3], b[3];
+    for (int k = 0; k < 3; ++k) { a[k] = v2[k] - v1[k]; b[k] = v3[k] - v1[k]; }
+    cross3(n, a, b);
+    const real s = dot3(n, n);
+    if (!(s > 0)) { n[0] = n[1] = n[2] = 0.0; *t = 0.0; return; }
+    const real r = sqrt(s);
+    for (int k = 0; k < 3; ++k) n[k] /= r;
+    *t = dot3(n, v1);
+}
+
+/* Intersect::computeDeepestPoints over a triangle's three vertices */
+static void deepest_points(const real *const *pts, const real *n, real t, real *pen, real *first, int *num_out) {
+    real max_depth = -DBL_MAX;
+    int num = 0, num_neg = 0, num_pos = 0, num_zero = 0;
+    for (int i = 0; i < 3; ++i) {
+        const real dist = -plane_dist(n, t, pts[i]);
+        if (dist > 1e-5) num_pos++;
+        else if (dist < -1e-5) num_neg++;
+        else num_zero++;
+        if (dist > max_depth) {
+            max_depth = dist;
+            num = 1;
+            for (int k = 0; k < 3; ++k) first[k] = pts[i][k];
+        } else if (dist + 1e-6 >= max_depth) {
+            num++;
+        }
+    }
+    if (max_depth < -1e-5) num = 0;
+    if (num_zero == 0 && (num_neg == 0 || num_pos == 0)) num = 0;
+    *pen = max_depth;
+    *num_out = num;
+}
+
+/* the first contact of intersect_Triangle's contact branch (P and Q in o1's
+ * frame); returns the number of contacts it emits (0..2) */
+static int tri_tri_contact(const real *P1, const real *P2, const real *P3, const real *Q1, const real *Q2,
+                           const real *Q3, real *point, real *normal, real *depth) {
+    real n1[3], n2[3], t1, t2, d1[3] = {0, 0, 0}, d2[3] = {0, 0, 0}, pen1, pen2;
+    int k1, k2;
+    build_triangle_plane(P1, P2, P3, n1, &t1);
+    build_triangle_plane(Q1, Q2, Q3, n2, &t2);
+    const real *Pp[3] = {P1, P2, P3}, *Qp[3] = {Q1, Q2, Q3};
+    deepest_points(Qp, n1, t1, &pen2, d2, &k2);
+    deepest_points(Pp, n2, t2, &pen1, d1, &k1);
+    if (pen1 > pen2) {
+        for (int k = 0; k < 3; ++k) { point[k] = d2[k]; normal[k] = -n1[k]; }
+        *depth = pen2;
+        return k2 < 2 ? k2 : 2;
+    }
+    for (int k = 0; k < 3; ++k) { point[k] = d1[k]; normal[k] = n2[k]; }
+    *depth = pen1;
+    return k1 < 2 ? k1 : 2;
+}
+
+/* segmentSqrDistance with the nearest point */
+static real segment_sqr_distance_nearest(const real *from, const real *to, const real *p, real *nearest) {
+    real diff[3], v[3];
+    for (int k = 0; k < 3; ++k) { diff[k] = p[k] - from[k]; v[k] = to[k] - from[k]; }
+    real t = dot3(v, diff);
+    if (t > 0) {
+        const real vv = dot3(v, v);
+        if (t < vv) {
+            t /= vv;
+            for (int k = 0; k < 3; ++k) diff[k] -= v[k] * t;
+        } else {
+            t = 1;
+            for (int k = 0; k < 3; ++k) diff[k] -= v[k];
+        }
+    } else {
+        t = 0;
+    }
+    for (int k = 0; k < 3; ++k) nearest[k] = from[k] + v[k] * t;
+    return dot3(diff, diff);
+}
+
+/* sphereTriangleIntersect with its contact (world triangle W1..W3): normal
+ * from the centre towards the contact point, stored depth -(r - distance) */
+static int sphere_triangle_contact(real radius, const real *TS, const real *P1, const real *P2, const real *P3,
+                                   real *depth, real *normal, real *pos) {
+    real a[3], b[3], n[3], pc[3], cp[3] = {0, 0, 0};
+    for (int k = 0; k < 3; ++k) { a[k] = P2[k] - P1[k]; b[k] = P3[k] - P1[k]; }
+    cross3(n, a, b);
+    const real z = dot3(n, n);
+    if (z > 0) { const real s = sqrt(z); n[0] /= s; n[1] /= s; n[2] /= s; }
+    const real *center = TS + 9;
+    const real rt = radius + DBL_EPSILON;
+    for (int k = 0; k < 3; ++k) pc[k] = center[k] - P1[k];
+    real dist = dot3(pc, n);
+    if (dist < 0) {
+        dist *= -1;
+        n[0] *= -1; n[1] *= -1; n[2] *= -1;
+    }
+    int has = 0;
+    if (dist < rt) {
+        if (project_in_triangle(P1, P2, P3, n, center)) {
+            has = 1;
+            for (int k = 0; k < 3; ++k) cp[k] = center[k] - n[k] * dist;
+        } else {
+            const real r2 = rt * rt;
+            real ne[3];
+            if (segment_sqr_distance_nearest(P1, P2, center, ne) < r2) { has = 1; memcpy(cp, ne, sizeof ne); }
+            if (segment_sqr_distance_nearest(P2, P3, center, ne) < r2) { has = 1; memcpy(cp, ne, sizeof ne); }
+            if (segment_sqr_distance_nearest(P3, P1, center, ne) < r2) { has = 1; memcpy(cp, ne, sizeof ne); }
+        }
+    }
+    if (!has) return 0;
+    real cc[3];
+    for (int k = 0; k < 3; ++k) cc[k] = cp[k] - center[k];
+    const real d2 = dot3(cc, cc);
+    if (!(d2 < rt * rt)) return 0;
+    if (d2 > 0) {
+        const real d = sqrt(d2);
+        for (int k = 0; k < 3; ++k) normal[k] = cc[k] / d;  /* Eigen normalized() */
+        *depth = -(radius - d);
+    } else {
+        for (int k = 0; k < 3; ++k) normal[k] = -n[k];
+        *depth = -radius;
+    }
+    for (int k = 0; k < 3; ++k) pos[k] = cp[k];
+    return 1;
+}
+
+static void zero_contact(real *depth, real *normal, real *pos) {
+    *depth = 0.0;
+    for (int k = 0; k < 3; ++k) normal[k] = pos[k] = 0.0;
+}
+
+static int mesh_mesh_contact(const orc_world *w, int ga, const real *TA, int gb, const real *TB, real *depth,
+                             real *normal, real *pos) {
+    const int a0 = (int)w->geom_param[4 * ga], an = (int)w->geom_param[4 * ga + 1];
+    const int b0 = (int)w->geom_param[4 * gb], bn = (int)w->geom_param[4 * gb + 1];
+    real R[9], T[3], dt[3];
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) R[3 * i + j] = (TA[i] * TB[j] + TA[3 + i] * TB[3 + j]) + TA[6 + i] * TB[6 + j];
+    for (int k = 0; k < 3; ++k) dt[k] = TB[9 + k] - TA[9 + k];
+    for (int i = 0; i < 3; ++i) T[i] = (TA[i] * dt[0] + TA[3 + i] * dt[1]) + TA[6 + i] * dt[2];
+    real (*QB)[9] = malloc(sizeof(real) * 9 * (size_t)(bn > 0 ? bn : 1));
+    real (*SB)[4] = malloc(sizeof(real) * 4 * (size_t)(bn > 0 ? bn : 1));
+    for (int j = 0; j < bn; ++j) {
+        const real *Q[3];
+        mesh_tri_points(w, gb, b0 + j, Q);
+        for (int k = 0; k < 3; ++k)
+            for (int i = 0; i < 3; ++i)
+                QB[j][3 * k + i] = ((R[3 * i] * Q[k][0] + R[3 * i + 1] * Q[k][1]) + R[3 * i + 2] * Q[k][2]) + T[i];
+        const real *Qp[3] = {QB[j], QB[j] + 3, QB[j] + 6};
+        bsphere(Qp, 3, SB[j], &SB[j][3]);
+    }
+    int hit = 0;
+    zero_contact(depth, normal, pos);
+    for (int i = 0; i < an && !hit; ++i) {
+        const real *P[3];
+        mesh_tri_points(w, ga, a0 + i, P);
+        real c[3], r;
+        bsphere(P, 3, c, &r);
+        for (int j = 0; j < bn; ++j) {
+            const real d[3] = {c[0] - SB[j][0], c[1] - SB[j][1], c[2] - SB[j][2]};
+            if (sqrt(dot3(d, d)) > r + SB[j][3]) continue;
+            if (!tri_tri_intersect(P[0], P[1], P[2], QB[j], QB[j] + 3, QB[j] + 6)) continue;
+            hit = 1;
+            real pt[3], nl[3], pen;
+            if (tri_tri_contact(P[0], P[1], P[2], QB[j], QB[j] + 3, QB[j] + 6, pt, nl, &pen) > 0) {
+                tf_point(TA, pt, pos);
+                for (int k = 0; k < 3; ++k) normal[k] = (TA[3 * k] * nl[0] + TA[3 * k + 1] * nl[1]) + TA[3 * k + 2] * nl[2];
+                *depth = pen;
+            }
+            break;
+        }
+    }
+    free(QB);
+    free(SB);
+    return hit;
+}
+
+static int mesh_shape_contact(const orc_world *w, int gm, const real *TM, int gs, const real *TS, int mesh_first,
+                              real *depth, real *normal, real *pos) {
+    const int t0 = (int)w->geom_param[4 * gm], tn = (int)w->geom_param[4 * gm + 1];
+    const int ts = w->geom_type[gs];
+    real rs = 0.0;  /* as mesh_shape_intersect */
+    const real *ps = w->geom_param + 4 * gs;
+    if (ts == GEOM_CONVEX) {
+        const real *V = w->verts + 3 * (size_t)w->geom_vstart[gs];
+        for (int i = 0; i < w->geom_nv[gs]; ++i) rs = fmax(rs, dot3(V + 3 * i, V + 3 * i));
+        rs = sqrt(rs);
+    } else if (ts == GEOM_BOX) rs = 0.5 * sqrt(dot3(ps, ps));
+    else if (ts == GEOM_SPHERE) rs = ps[0];
+    else rs = sqrt(ps[0] * ps[0] + 0.25 * ps[1] * ps[1]) + (ts == GEOM_CAPSULE ? ps[0] : 0.0);
+    rs = rs * (1.0 + 1e-9) + 1e-9;
+    gjk_obj shape, tri;
+    int shape_ready = 0;
+    zero_contact(depth, normal, pos);
+    for (int t = t0; t < t0 + tn; ++t) {
+        const real *P[3];
+        mesh_tri_points(w, gm, t, P);
+        real W[3][3];
+        for (int k = 0; k < 3; ++k) tf_point(TM, P[k], W[k]);
+        const real *Wp[3] = {W[0], W[1], W[2]};
+        real c[3], r;
+        bsphere(Wp, 3, c, &r);
+        const real d[3] = {c[0] - TS[9], c[1] - TS[10], c[2] - TS[11]};
+        const real pad = 1.001 * sqrt(sqrt((double)CCD_EPS)) + 1e-5 * (1.0 + fabs(TS[9]) + fabs(TS[10]) + fabs(TS[11]) + fabs(TM[9]) + fabs(TM[10]) + fabs(TM[11]));
+        if (sqrt(dot3(d, d)) > r + rs + pad) continue;
+        int hit;
+        if (ts == GEOM_SPHERE) {
+            hit = sphere_triangle_contact(ps[0], TS, W[0], W[1], W[2], depth, normal, pos);
+        } else {
+            if (!shape_ready) { make_obj(w, gs, TS, &shape, NULL); shape_ready = 1; }
+            memset(&tri, 0, sizeof tri);
+            shape_to_gjk(TM, &tri);
+            tri_gjk_obj(w, gm, &tri, t, &tri);
+            hit = mpr_penetration(&shape, &tri, 1e-6, depth, normal, pos);
+        }
+        if (hit) {
+            if (mesh_first)
+                for (int k = 0; k < 3; ++k) normal[k] = -normal[k];
+            return 1;
+        }
+    }
+    zero_contact(depth, normal, pos);
+    return 0;
+}
+
+static int mesh_octree_contact(const orc_world *w, int gm, const real *TM, int go, const real *TO, real *depth,
+                               real *normal, real *pos) {
+    const int t0 = (int)w->geom_param[4 * gm], tn = (int)w->geom_param[4 * gm + 1];
+    const int l0 = (int)w->geom_param[4 * go], ln = (int)w->geom_param[4 * go + 1];
+    zero_contact(depth, normal, pos);
+    if (tn <= 0 || ln <= 0) return 0;
+    real (*Wt)[9] = malloc(sizeof(real) * 9 * (size_t)tn);
+    real (*S)[4] = malloc(sizeof(real) * 4 * (size_t)tn);
+    mesh_world_tris(w, gm, TM, Wt, S);
+    real lo[3], hi[3];
+    for (int k = 0; k < 3; ++k) { lo[k] = DBL_MAX; hi[k] = -DBL_MAX; }
+    for (int t = 0; t < tn; ++t)
+        for (int v = 0; v < 3; ++v)
+            for (int k = 0; k < 3; ++k) { lo[k] = fmin(lo[k], Wt[t][3 * v + k]); hi[k] = fmax(hi[k], Wt[t][3 * v + k]); }
+    real mc[3], dm[3];
+    for (int k = 0; k < 3; ++k) { mc[k] = (lo[k] + hi[k]) * 0.5; dm[k] = hi[k] - lo[k]; }
+    const real mr = 0.5 * sqrt(dot3(dm, dm)) * (1.0 + 1e-9) + 1e-9;
+    const real pad = 1.001 * sqrt(sqrt((double)CCD_EPS)) + 1e-5 * (1.0 + fabs(TO[9]) + fabs(TO[10]) + fabs(TO[11]) +
+                                                                 fabs(TM[9]) + fabs(TM[10]) + fabs(TM[11]));
+    gjk_obj frame;
+    memset(&frame, 0, sizeof frame);
+    shape_to_gjk(TM, &frame);
+    int hit = 0;
+    for (int l = l0; l < l0 + ln && !hit; ++l) {
+        real side[3], TL[12];
+        octree_leaf_box(w, l, TO, side, TL);
+        const real rl = 0.5 * sqrt(dot3(side, side)) * (1.0 + 1e-9) + 1e-9;
+        const real dc[3] = {TL[9] - mc[0], TL[10] - mc[1], TL[11] - mc[2]};
+        if (sqrt(dot3(dc, dc)) > rl + mr + pad) continue;
+        gjk_obj box, tri;
+        leaf_box_obj(side, TL, &box);
+        for (int t = 0; t < tn; ++t) {
+            const real d[3] = {TL[9] - S[t][0], TL[10] - S[t][1], TL[11] - S[t][2]};
+            if (sqrt(dot3(d, d)) > rl + S[t][3] + pad) continue;
+            tri_gjk_obj(w, gm, &frame, t0 + t, &tri);
+            if (mpr_penetration(&box, &tri, 1e-6, depth, normal, pos)) { hit = 1; break; }
+        }
+    }
+    free(Wt);
+    free(S);
+    if (!hit) zero_contact(depth, normal, pos);
+    return hit;
+}
+
+/* the contact of a pair with a mesh side; -1 when neither side is a mesh */
+static int mesh_contact(const orc_world *w, int ga, const real *Ta, int gb, const real *Tb, real *depth, real *normal,
+                        real *pos) {
+    const int ta = w->geom_type[ga], tb = w->geom_type[gb];
+    if (ta != GEOM_MESH && tb != GEOM_MESH) return -1;
+    if (ta == GEOM_MESH && tb == GEOM_MESH) return mesh_mesh_contact(w, ga, Ta, gb, Tb, depth, normal, pos);
+    if (ta == GEOM_OCTREE) return mesh_octree_contact(w, gb, Tb, ga, Ta, depth, normal, pos);
+    if (tb == GEOM_OCTREE) return mesh_octree_contact(w, ga, Ta, gb, Tb, depth, normal, pos);
+    if (ta == GEOM_MESH) return mesh_shape_contact(w, ga, Ta, gb, Tb, 1, depth, normal, pos);
+    return mesh_shape_contact(w, gb, Tb, ga, Ta, 0, depth, normal, pos);
+}
+
 #define MAX_OBJ 512
 
 /* Per-configuration worker: FK + every pair + ACM filter (allowed pairs are
@@ -2688,6 +2998,8 @@ int orc_fk_batch(const orc_world *w, const double *q, long n, double *link_pose7
 /* Single-pair entry (fcl.collide(o1, o2) on two posed shapes). */
 int orc_contact_pair(const orc_world *w, int ga, const double *Ta, int gb, const double *Tb, double *depth,
                      double *normal, double *pos) {
+    const int mc = mesh_contact(w, ga, Ta, gb, Tb, depth, normal, pos);
+    if (mc >= 0) return mc;
     const int cf = closed_form_contact(w, ga, Ta, gb, Tb, depth, normal, pos);
     if (cf >= 0) return cf;
     gjk_obj a, b;
@@ -2724,6 +3036,8 @@ int orc_contact_batch(const orc_world *w, const double *q, long n, uint8_t *hit,
                 else if (ks[s] == KIND_ATTACHED) { Ts[s] = att_T + 12 * is[s]; gs[s] = w->att_geom[is[s]]; }
                 else { Ts[s] = w->scene_tf + 12 * is[s]; gs[s] = w->scene_geom[is[s]]; }
             }
+            const int mc = mesh_contact(w, gs[0], Ts[0], gs[1], Ts[1], depth + k, normal + 3 * k, pos + 3 * k);
+            if (mc >= 0) { hit[k] = (uint8_t)mc; continue; }
             const int cf = closed_form_contact(w, gs[0], Ts[0], gs[1], Ts[1], depth + k, normal + 3 * k, pos + 3 * k);
             if (cf >= 0) { hit[k] = (uint8_t)cf; continue; }
             if (w->geom_type[gs[1]] == GEOM_OCTREE) {

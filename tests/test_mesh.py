@@ -202,6 +202,80 @@ def test_mesh_mesh_hull_surfaces():
     assert both > 20
 
 
+def _box_mesh(side):
+    """a box surface as a BVH mesh: 12 triangles, vertex i = (x, y, z) bits"""
+    h = np.asarray(side, dtype=np.float64) / 2
+    v = np.array([[x, y, z] for x in (-h[0], h[0]) for y in (-h[1], h[1]) for z in (-h[2], h[2])])
+    f = [(0, 1, 3), (0, 3, 2), (4, 6, 7), (4, 7, 5), (0, 4, 5), (0, 5, 1), (2, 3, 7), (2, 7, 6), (0, 2, 6), (0, 6, 4),
+         (1, 5, 7), (1, 7, 3)]
+    return M.MeshGeom(v, f)
+
+
+def _flatT(R=None, p=(0.0, 0.0, 0.0)):
+    R = np.eye(3) if R is None else np.asarray(R)
+    return np.concatenate([R.reshape(-1), np.asarray(p, dtype=np.float64)])
+
+
+def _contact_pair(ob, ga, Ta, gb, Tb):
+    import ctypes
+    P = ctypes.POINTER(ctypes.c_double)
+    depth = ctypes.c_double()
+    nrm, pos = np.zeros(3), np.zeros(3)
+    Ta, Tb = np.ascontiguousarray(Ta), np.ascontiguousarray(Tb)
+    r = oracle.lib().orc_contact_pair(ctypes.byref(ob._w), ga, Ta.ctypes.data_as(P), gb, Tb.ctypes.data_as(P),
+                                      ctypes.byref(depth), nrm.ctypes.data_as(P), pos.ctypes.data_as(P))
+    return r, depth.value, nrm, pos
+
+
+def test_mesh_contacts_known_answers():
+    """The oracle's BVH-mesh contact restatement on plain geometry:
+    sphere over a box surface mesh -> sphereTriangleIntersect's contact on the
+    first hit triangle (projection of the centre, normal from the centre to
+    it, stored depth -(r - d)); a small box mesh sunk 0.05 into a unit box
+    mesh -> intersect_Triangle's deepest point (a bottom corner of the small
+    box, depth 0.05, normal -n1 of the big box's top triangle = -z); the
+    mesh-first order negates the normal; shape vs mesh through MPR
+    penetration: unit normal, positive depth, mirrored by the other order."""
+    big, small, ball, blk = _box_mesh((1, 1, 1)), _box_mesh((0.2, 0.2, 0.2)), M.SphereGeom(0.1), M.BoxGeom((0.2, 0.2, 0.2))
+    ob = oracle.OracleWorld(Wd.panda_articulation(), scene=[(f"g{i}", g, M.IDENT) for i, g in
+                                                            enumerate((big, small, ball, blk))])
+    gb, gs, gp, gx = (_gi(ob, g) for g in (big, small, ball, blk))
+    # sphere 0.06 above the top face, over triangle 10 (1, 5, 7): y < x
+    r, d, n, p = _contact_pair(ob, gp, _flatT(p=(0.05, -0.02, 0.56)), gb, _flatT())
+    assert r == 1 and abs(d - (-(0.1 - 0.06))) < 1e-12
+    np.testing.assert_allclose(n, [0, 0, -1], atol=1e-12)
+    np.testing.assert_allclose(p, [0.05, -0.02, 0.5], atol=1e-12)
+    r2, d2, n2, p2 = _contact_pair(ob, gb, _flatT(), gp, _flatT(p=(0.05, -0.02, 0.56)))
+    assert r2 == 1 and d2 == d and np.array_equal(n2, -n) and np.array_equal(p2, p)
+    # mesh-mesh: the small box's bottom (z = 0.45) below the big box's top face
+    c = np.cos(0.3), np.sin(0.3)
+    Rz = [[c[0], -c[1], 0], [c[1], c[0], 0], [0, 0, 1]]
+    Ts = _flatT(Rz, (0.13, -0.21, 0.55))
+    r, d, n, p = _contact_pair(ob, gb, _flatT(), gs, Ts)
+    assert r == 1 and abs(d - 0.05) < 1e-12
+    np.testing.assert_allclose(n, [0, 0, -1], atol=1e-12)
+    corners = (np.array(Rz) @ small.vertices.T).T + [0.13, -0.21, 0.55]
+    assert abs(p[2] - 0.45) < 1e-12 and np.min(np.linalg.norm(corners - p, axis=1)) < 1e-12
+    assert _contact_pair(ob, gb, _flatT(), gs, _flatT(Rz, (0.13, -0.21, 0.75)))[0] == 0
+    # box shape vs mesh (MPR penetration of (box, triangle)), both orders
+    r, d, n, p = _contact_pair(ob, gx, Ts, gb, _flatT())
+    r2, d2, n2, p2 = _contact_pair(ob, gb, _flatT(), gx, Ts)
+    assert r == r2 == 1 and d > 0 and d == d2
+    assert abs(np.linalg.norm(n) - 1) < 1e-6 and np.array_equal(n2, -n) and np.array_equal(p2, p)
+
+
+def test_mesh_contact_batch_consistent_with_collide():
+    """The oracle's contact pass on a convex=False world reports exactly the
+    pairs its collide pass does (same leaf tests decide)."""
+    ow = Wd.oracle_world(3, convex=False)
+    q = Wd.sample_q(ow.art, 24, 6)
+    hit, depth, normal, pos = ow.contact_batch(q)
+    _, masks = ow.collide_batch(q)
+    bits = np.stack([(masks[:, p >> 5] >> (p & 31)) & 1 for p in range(len(ow.pairs))], 1)
+    np.testing.assert_array_equal(hit, bits)
+    assert hit.sum() > 0
+
+
 def test_host_loader_matches_oracle_loader():
     d = os.path.join(Wd.panda_dir(), "franka_description", "meshes", "collision")
     for name in ("link0.stl", "link3.stl", "finger.stl"):
@@ -399,14 +473,77 @@ def test_mesh_robot_point_cloud_matches_oracle(cloud):
 
 
 @pytest.mark.gpu
-def test_mesh_world_unsupported_queries():
+def test_mesh_world_scalar_queries():
     w, _ = scenes.world(2, convex=False)
     w.set_qpos_all(Wd.KAT_COLLIDING)
     assert w.collide() and len(w.collide_full()) > 0
+    assert w.collide(pymp.fcl.CollisionRequest(enable_contact=True))
     w.set_qpos_all(Wd.KAT_FREE)
     assert not w.collide() and w.collide_full() == []
-    with pytest.raises(NotImplementedError):
-        w.collide(pymp.fcl.CollisionRequest(enable_contact=True))
+
+
+def _check_scalar_contacts(w, o2, q):
+    """collide_full(CollisionRequest(enable_contact=True)) per configuration
+    against the oracle's contact pass: the same reported pairs, each with the
+    oracle's (depth, normal, position) within 1e-9."""
+    req = pymp.fcl.CollisionRequest(enable_contact=True)
+    hit, rd, rn, rp = o2.contact_batch(q)
+    names = o2.pair_names()
+    for i in range(len(q)):
+        w.set_qpos_all(list(q[i]))
+        got = {(c.link_name1, c.link_name2): c.res.get_contacts()[0] for c in w.collide_full(req)}
+        exp = {names[p]: p for p in np.nonzero(hit[i])[0]}
+        assert set(got) == set(exp)
+        for k, p in exp.items():
+            c = got[k]
+            assert abs(c.penetration_depth - rd[i, p]) < 1e-9, (k, c.penetration_depth, rd[i, p])
+            np.testing.assert_allclose(c.normal, rn[i, p], atol=1e-9)
+            np.testing.assert_allclose(c.pos, rp[i, p], atol=1e-9)
+    return hit
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("convex", [False, True])
+def test_mesh_contacts_match_oracle(convex):
+    """enable_contact=True on every BVH-mesh pair class of _full_mesh_world
+    (mesh-mesh deepest points, sphere-triangle, shape-triangle MPR
+    penetration, both argument orders): the device reports the pairs the
+    oracle does, each contact within 1e-9 of the oracle's restatement."""
+    w, o2, base, names, perm = _full_mesh_world(convex)
+    q = Wd.sample_q(base.art, 6000, 31)
+    _, mo = o2.collide_batch(q, nthreads=min(16, os.cpu_count() or 1))
+    on = o2.pair_names()
+    mesh_pairs = [k for k, n in enumerate(on) if "scene_mesh" in n or "tool" in n or not convex]
+    sel = np.nonzero(np.any(np.stack([(mo[:, k >> 5] >> (k & 31)) & 1 for k in mesh_pairs], 1), 1))[0]
+    assert len(sel) >= 20
+    hit = _check_scalar_contacts(w, o2, q[sel[:60]])
+    assert hit[:, mesh_pairs].sum() >= 20
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cloud", ["floor", "blue"])
+def test_mesh_robot_point_cloud_contacts_match_oracle(cloud):
+    """enable_contact=True between BVH mesh links and a point cloud: the
+    first occupied leaf with a hit, MPR penetration of (leaf box, lowest
+    such triangle), within 1e-9 of the oracle."""
+    art = scenes.panda(convex=False)
+    if cloud == "floor":
+        w = pymp.planning_world.PlanningWorld([art], ["panda"], [], [])
+        scene, allowed = [], []
+    else:
+        w, art = scenes.world(3, convex=False)
+        scene, allowed = Wd.boxes_scene(), [("panda_link0", "table")]
+    w.add_point_cloud("scene_pcd", scenes.cloud_points(cloud), 1e-3)
+    o = oracle.OracleWorld(Wd.panda_articulation(False),
+                           scene=scene + [("scene_pcd", M.OcTreeGeom(scenes.cloud_points(cloud), 1e-3), M.IDENT)],
+                           allowed=allowed)
+    q = np.vstack([Wd.sample_q(o.art, 600, 78), [scenes.FLOOR_COLLIDING]])
+    _, mo = o.collide_batch(q, nthreads=min(16, os.cpu_count() or 1))
+    pc = [k for k, (a, b) in enumerate(o.pair_names()) if b == "scene_pcd"]
+    sel = np.nonzero(np.any(np.stack([(mo[:, k >> 5] >> (k & 31)) & 1 for k in pc], 1), 1))[0]
+    assert len(sel) >= 1
+    hit = _check_scalar_contacts(w, o, q[sel[:12]])
+    assert hit[:, pc].sum() >= 1
 
 
 @pytest.mark.gpu
