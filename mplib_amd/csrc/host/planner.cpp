@@ -448,10 +448,13 @@ std::vector<const double*> root_path(const T& t, int m) {
 // point an outcome tree is explored best first: each explored node is a copy
 // of the branch that assumes an outcome (valid / invalid) for every motion on
 // its path and stops at the next unknown motion; its probability is the
-// product of the outcome rates measured so far in this plan (extension and
-// connect motions separately).  One device batch carries the unknown states of
-// the real motion and of the explored nodes; while it runs on the GPU (a
-// helper thread waits on the synchronous C call) the host explores deeper.
+// product of the outcome rates measured so far in this plan, per motion kind:
+// extension, first connect step, later connect steps (on cfg5 ~0.65, ~0.07
+// and ~0.77 valid: the first step towards the other tree rarely gets through,
+// a chain that has started usually continues).  One device batch carries
+// the unknown states of the real motion and of the explored nodes; while it
+// runs on the GPU (a helper thread waits on the synchronous C call) the host
+// explores deeper.
 // When the answers arrive the real branch advances through the cache, the
 // explored node it stops at becomes the new root (its subtree is kept,
 // everything else dropped), and the unsent states below it form the next
@@ -675,7 +678,7 @@ class ConnectEngine {
 
  private:
   enum Adv { A_BLOCKED, A_SOLVED, A_END, A_LIMIT };
-  enum Kind { K_EXT = 0, K_CONN = 1 };
+  enum Kind { K_EXT = 0, K_CONN = 1, K_CONN2 = 2 };  // extension, first connect step, later connect steps
   struct Branch {
     std::vector<double> ost[2];  // overlay: nodes added since the last commit
     std::vector<int> opar[2];    // their parents (global node indices)
@@ -861,11 +864,12 @@ class ConnectEngine {
         mot_.clear();
         append_grow(sp_, o == 0, nst, ds, mot_);
         const int v = status(b, mot_, blk);
+        const int kind = b.n_conn == 0 ? K_CONN : K_CONN2;
         if (v < 0) {
-          blk.kind = K_CONN;
+          blk.kind = kind;
           return A_BLOCKED;
         }
-        if (real) record(K_CONN, v);
+        if (real) record(kind, v);
         if (v)
           b.xmotion = add_node(b, o, ds, n);
         else
@@ -1081,7 +1085,7 @@ class ConnectEngine {
   std::vector<SNode> nodes_;
   std::priority_queue<std::tuple<double, int, int>> frontier_;
   std::unique_ptr<AsyncCheck> async_;
-  double n_out_[2] = {0, 0}, n_ok_[2] = {0, 0};
+  double n_out_[3] = {0, 0, 0}, n_ok_[3] = {0, 0, 0};
   int approxsol_ = -1;
   double approxdif_ = std::numeric_limits<double>::infinity();
   std::vector<double> rbuf_, xbuf_, mot_, batch_;
