@@ -703,6 +703,7 @@ class ConnectEngine {
     Blocked blk;
     double p = 1.0;  // probability of reaching it from the root
     int child[2] = {-1, -1};  // [outcome invalid, valid]: -1 unexplored, -2 ends, else node
+    bool sent = false;        // its unknown states went into a batch
   };
 
   // ---- trees ----
@@ -996,6 +997,7 @@ class ConnectEngine {
       }
       kept[0].br = real_;
       kept[0].blk = rb;
+      kept[0].sent = false;
     } else {
       SNode root;
       root.br = real_;
@@ -1008,20 +1010,28 @@ class ConnectEngine {
     const int target_nodes = spec_nodes_ >= 0 ? spec_nodes_ : async_ ? kSyncNodes : kSyncCheckerNodes;
     while ((int)nodes_.size() < target_nodes && (int)nodes_.size() < kMaxNodes && expand_best()) {
     }
-    // the batch: unknown states of every node, by probability
-    std::vector<int> order(nodes_.size());
-    for (size_t i = 0; i < order.size(); ++i) order[i] = (int)i;
-    std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return nodes_[(size_t)a].p > nodes_[(size_t)b].p; });
+    // the batch: unknown states of the nodes not sent yet, by probability
+    order_.clear();
+    size_t cand = 0;
+    for (size_t i = 0; i < nodes_.size(); ++i)
+      if (!nodes_[i].sent) {
+        order_.push_back((int)i);
+        cand += nodes_[i].blk.h.size();
+      }
+    std::stable_sort(order_.begin(), order_.end(),
+                     [&](int a, int b) { return nodes_[(size_t)a].p > nodes_[(size_t)b].p; });
     batch_.clear();
-    seen_.assign(std::max<size_t>(64, 4 * nodes_.size() * 4), 0);
-    for (int i : order) {
-      const Blocked& b = nodes_[(size_t)i].blk;
+    seen_reset(cand);
+    for (int i : order_) {
+      if (batch_.size() >= (size_t)kMaxBatch * d_) break;
+      SNode& nd = nodes_[(size_t)i];
+      const Blocked& b = nd.blk;
       for (size_t k = 0; k < b.h.size(); ++k) {
         const double* s = b.st.data() + k * d_;
         if (vc_.find_h(s, b.h[k]) >= 0 || !mark(b.h[k])) continue;
         batch_.insert(batch_.end(), s, s + d_);
       }
-      if (batch_.size() >= (size_t)kMaxBatch * d_) break;
+      nd.sent = true;
     }
     stats_.t_spec += seconds_since(t0);
     const auto tc = Clock::now();
@@ -1047,16 +1057,26 @@ class ConnectEngine {
     }
     for (size_t i = 0; i < valid_.size(); ++i) vc_.put(batch_.data() + i * d_, valid_[i]);
   }
-  // hash set of the batch's states (open addressing on the 64-bit keys)
+  // hash set of the batch's states (open addressing on the 64-bit keys, a
+  // slot is live when its generation is the current one: no clearing)
+  void seen_reset(size_t n) {
+    size_t m = 64;
+    while (m < 2 * n + 2) m <<= 1;
+    if (seen_.size() < m) {
+      seen_.assign(m, 0);
+      seen_gen_.assign(m, 0);
+    }
+    gen_ += 1;
+  }
   bool mark(uint64_t h) {
-    const size_t m = seen_.size();
-    if (h == 0) h = 1;
-    for (size_t i = h % m;; i = (i + 1) % m) {
-      if (seen_[i] == h) return false;
-      if (seen_[i] == 0) {
+    const size_t m = seen_.size() - 1;  // a power of two minus one
+    for (size_t i = h & m;; i = (i + 1) & m) {
+      if (seen_gen_[i] != gen_) {
+        seen_gen_[i] = gen_;
         seen_[i] = h;
         return true;
       }
+      if (seen_[i] == h) return false;
     }
   }
 
@@ -1091,6 +1111,9 @@ class ConnectEngine {
   std::vector<double> rbuf_, xbuf_, mot_, batch_;
   std::vector<uint8_t> valid_;
   std::vector<uint64_t> seen_;
+  std::vector<uint32_t> seen_gen_;
+  uint32_t gen_ = 0;
+  std::vector<int> order_;
 };
 
 }  // namespace
