@@ -2489,6 +2489,59 @@ __global__ __launch_bounds__(256) void small_sincos_kernel(DevWorld w, const dou
 // costs more than the extra launch)
 constexpr int kLatScDof = 16;   // move-group dof the inline path holds (host: more -> small_sincos_kernel)
 constexpr int kLatScGroup = 4;
+
+// The latency kernel's joint table, staged per wave in LDS by one round of
+// parallel loads (lane j: joint j; lanes 0..31 / 32..63: the two objects'
+// chains): the chain walk then reads LDS instead of waiting, joint after
+// joint, on dependent scalar loads of the chain list and the joint records.
+struct LatJoints {
+  double place[kMaxJoints][12];
+  double axis[kMaxJoints][3];
+  double qc[kMaxJoints];
+  int type[kMaxJoints], src[kMaxJoints];
+  int chain[2][kMaxJoints];
+};
+
+__device__ __forceinline__ void stage_lat_joints(const DevWorld& w, LatJoints& J, uint32_t lane, int la, int lb) {
+  if ((int)lane < w.nj) {
+    const int j = (int)lane;
+#pragma unroll
+    for (int i = 0; i < 12; ++i) J.place[j][i] = w.joint_place[12 * j + i];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) J.axis[j][i] = w.joint_axis[3 * j + i];
+    J.qc[j] = w.joint_q_const[j];
+    J.type[j] = w.joint_type[j];
+    J.src[j] = w.joint_q_source[j];
+  }
+  const int s = lane >> 5, k = (int)(lane & 31u), l = s ? lb : la;
+  if (l >= 0 && k < w.link_chain_len[l]) J.chain[s][k] = w.chain_joints[w.link_chain_start[l] + k];
+  wave_lds_sync();
+}
+
+// chain_oMi on the staged table: the same products in the same order
+__device__ __forceinline__ SE3 chain_oMi_lat(const DevWorld& w, const LatJoints& J, int s, int l,
+                                             const double* __restrict__ qrow, const double* screw) {
+  const int cl = w.link_chain_len[l];
+  SE3 T;
+  se3_identity(T);
+  for (int k = 0; k < cl; ++k) {
+    const int j = J.chain[s][k];
+    const int src = J.src[j - 1];
+    const int type = J.type[j - 1];
+    const bool pre = src >= 0 && joint_is_revolute(type);
+    const double v = pre ? 0.0 : src >= 0 ? qrow[src] : J.qc[j - 1];
+    const SE3 M = joint_motion(type, J.axis[j - 1], v, pre ? screw + 2 * src : nullptr);
+    SE3 P;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) P.R[i] = J.place[j - 1][i];
+    P.p[0] = J.place[j - 1][9];
+    P.p[1] = J.place[j - 1][10];
+    P.p[2] = J.place[j - 1][11];
+    const SE3 li = se3_mul(P, M);
+    T = k == 0 ? li : se3_mul(T, li);
+  }
+  return T;
+}
 template <bool FROM_POSES, int CLS, bool INLINE_SC = false>
 __global__ __launch_bounds__(256) void small_kernel(DevWorld w, const double* __restrict__ in, long long n, int n_tiles,
                                                    uint8_t* __restrict__ hits, const double* __restrict__ sc) {
@@ -2533,8 +2586,23 @@ __global__ __launch_bounds__(256) void small_kernel(DevWorld w, const double* __
       }
       sc_row = mine;
     }
-    const SE3 TA = am ? moving_tf_row<FROM_POSES>(w, in, sc_row, c, a) : load_se3(w.static_T + 12 * (a - w.n_moving));
-    const SE3 TB = bm ? moving_tf_row<FROM_POSES>(w, in, sc_row, c, b) : load_se3(w.static_T + 12 * (b - w.n_moving));
+    SE3 TA, TB;
+    if constexpr (INLINE_SC && !FROM_POSES) {
+      __shared__ LatJoints lat_j[4];
+      LatJoints& J = lat_j[threadIdx.x >> 6];
+      const int la = am ? w.moving_link[a] : -1, lb = bm ? w.moving_link[b] : -1;
+      stage_lat_joints(w, J, lane, la, lb);
+      const double* qrow = in + c * w.dof;
+      auto tf = [&](int id, int s, int l) {
+        const SE3 L = link_from_oMi(w, chain_oMi_lat(w, J, s, l, qrow, sc_row), l, nullptr);
+        return se3_mul(L, load_se3(w.moving_offset + 12 * id));
+      };
+      TA = am ? tf(a, 0, la) : load_se3(w.static_T + 12 * (a - w.n_moving));
+      TB = bm ? tf(b, 1, lb) : load_se3(w.static_T + 12 * (b - w.n_moving));
+    } else {
+      TA = am ? moving_tf_row<FROM_POSES>(w, in, sc_row, c, a) : load_se3(w.static_T + 12 * (a - w.n_moving));
+      TB = bm ? moving_tf_row<FROM_POSES>(w, in, sc_row, c, b) : load_se3(w.static_T + 12 * (b - w.n_moving));
+    }
     const int ga = am ? w.moving_geom[a] : w.static_geom[a - w.n_moving];
     const int gb = bm ? w.moving_geom[b] : w.static_geom[b - w.n_moving];
     const cptr<double> ra = w.geom_rec + G_STRIDE * ga, rb = w.geom_rec + G_STRIDE * gb;
