@@ -448,10 +448,11 @@ std::vector<const double*> root_path(const T& t, int m) {
 // point an outcome tree is explored best first: each explored node is a copy
 // of the branch that assumes an outcome (valid / invalid) for every motion on
 // its path and stops at the next unknown motion; its probability is the
-// product of the outcome rates measured so far in this plan, per motion kind:
-// extension, first connect step, later connect steps (on cfg5 ~0.65, ~0.07
-// and ~0.77 valid: the first step towards the other tree rarely gets through,
-// a chain that has started usually continues).  One device batch carries
+// product of the outcome rates measured so far in this plan, per motion kind
+// and tree: extension, first connect step, later connect steps, each for the
+// start and the goal tree (on cfg5 ~0.65, ~0.07 and ~0.77 valid: the first
+// step towards the other tree rarely gets through, a chain that has started
+// usually continues; splitting by tree saves another ~13 % of the batches).  One device batch carries
 // the unknown states of the real motion and of the explored nodes; while it
 // runs on the GPU (a helper thread waits on the synchronous C call) the host
 // explores deeper.
@@ -678,7 +679,9 @@ class ConnectEngine {
 
  private:
   enum Adv { A_BLOCKED, A_SOLVED, A_END, A_LIMIT };
-  enum Kind { K_EXT = 0, K_CONN = 1, K_CONN2 = 2 };  // extension, first connect step, later connect steps
+  // motion kinds of the outcome model: extension, first connect step, later
+  // connect steps; + 3 when the motion grows the goal tree
+  enum Kind { K_EXT = 0, K_CONN = 1, K_CONN2 = 2 };
   struct Branch {
     std::vector<double> ost[2];  // overlay: nodes added since the last commit
     std::vector<int> opar[2];    // their parents (global node indices)
@@ -825,10 +828,10 @@ class ConnectEngine {
           append_grow(sp_, b.tr == 0, nst, ds, mot_);
           const int v = status(b, mot_, blk);
           if (v < 0) {
-            blk.kind = K_EXT;
+            blk.kind = K_EXT + 3 * b.tr;
             return A_BLOCKED;
           }
-          if (real) record(K_EXT, v);
+          if (real) record(K_EXT + 3 * b.tr, v);
           trapped = !v;
           if (trapped && real) stats_.ext_trapped += 1;
         }
@@ -865,7 +868,7 @@ class ConnectEngine {
         mot_.clear();
         append_grow(sp_, o == 0, nst, ds, mot_);
         const int v = status(b, mot_, blk);
-        const int kind = b.n_conn == 0 ? K_CONN : K_CONN2;
+        const int kind = (b.n_conn == 0 ? K_CONN : K_CONN2) + 3 * o;
         if (v < 0) {
           blk.kind = kind;
           return A_BLOCKED;
@@ -1105,7 +1108,7 @@ class ConnectEngine {
   std::vector<SNode> nodes_;
   std::priority_queue<std::tuple<double, int, int>> frontier_;
   std::unique_ptr<AsyncCheck> async_;
-  double n_out_[3] = {0, 0, 0}, n_ok_[3] = {0, 0, 0};
+  double n_out_[6] = {0, 0, 0, 0, 0, 0}, n_ok_[6] = {0, 0, 0, 0, 0, 0};
   int approxsol_ = -1;
   double approxdif_ = std::numeric_limits<double>::infinity();
   std::vector<double> rbuf_, xbuf_, mot_, batch_;
