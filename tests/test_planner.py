@@ -167,10 +167,15 @@ def test_argument_errors():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("goal,seed", [("near", 0), ("far", 0), ("far", 1), ("far", 5)])
-def test_device_checker_gives_the_oracle_path(goal, seed):
+@pytest.mark.parametrize("goal,seed,nodes", [("near", 0, -1), ("far", 0, -1), ("far", 1, -1), ("far", 5, -1),
+                                             ("far", 2, 0), ("far", 3, 64)])
+def test_device_checker_gives_the_oracle_path(goal, seed, nodes):
+    """The device path (helper-thread batches, exploration while the GPU
+    runs, any synchronous exploration budget) plans the oracle checker's
+    path bit-for-bit."""
     w, _ = scenes.world(3)
     dev = pymp.ompl.OMPLPlanner(w)
+    dev.set_speculation_nodes(nodes)
     ref = planner()
     pymp.set_global_seed(seed)
     s1, p1 = dev.plan(START, [GOALS[goal]], range=0.1, time=60.0)

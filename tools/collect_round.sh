@@ -15,6 +15,13 @@ for p in gpurun_out/prof_$TAG/pmc_*/; do
 done
 cp gpurun_out/prof_$TAG/pmc_summary.json $D/pmc_summary.json
 cp gpurun_out/prof_$TAG/pmc_summary.json profiles/pmc_cfg3.json
+for c in 2 4; do  # tools/gpu_round3.sh: per-config PMC records
+  if [ -f gpurun_out/prof_${TAG}_cfg$c/pmc_summary.json ]; then
+    cp gpurun_out/prof_${TAG}_cfg$c/pmc_summary.json $D/pmc_summary_cfg$c.json
+    cp gpurun_out/prof_${TAG}_cfg$c/pmc_summary.json profiles/pmc_cfg$c.json
+    cp gpurun_out/prof_${TAG}_cfg$c/trace/trace_kernel_stats.csv $D/kernel_stats_cfg$c.csv
+  fi
+done
 tail -3 gpurun_out/pytest_gpu.log > $D/pytest_gpu.txt
 cp gpurun_out/smoke.log $D/smoke.txt
 ls $D
