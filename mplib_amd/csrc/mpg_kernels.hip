@@ -1194,7 +1194,10 @@ __global__ __launch_bounds__(1024) void pair_scan_kernel(uint32_t* __restrict__ 
 // chip instead of a few hundred full waves.  prefix[n_pairs] = task count,
 // prefix[n_pairs + 1] = the narrow phase's task counter, prefix[n_pairs + 2]
 // = ts, prefix[n_pairs + 3] = the candidate count.
-constexpr uint32_t kTaskMin = 8;
+#ifndef MPG_TASK_MIN
+#define MPG_TASK_MIN 8
+#endif
+constexpr uint32_t kTaskMin = MPG_TASK_MIN;
 
 __device__ __forceinline__ uint32_t block_sum256(uint32_t v, uint32_t* red) {
 #pragma unroll
