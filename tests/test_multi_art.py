@@ -154,6 +154,33 @@ def test_two_pandas_match_oracle(b_planned):
     assert any(((m[:, p >> 5] >> (p & 31)) & 1).any() for p in arts)
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("b_planned", [False, True])
+def test_two_pandas_latency_path_matches_oracle(b_planned):
+    """The planner's one-launch latency path (batches of <= 256 states: each
+    lane's joint sin/cos and both objects' chains staged in LDS) on the
+    two-Panda forest (18 joints, dof 7 or 14): every flag and pair bit equals
+    the oracle's."""
+    w = product_world(b_planned)
+    mw = oracle_world(b_planned)
+    keys = [(i[1], i[2], i[3], i[4]) for i in w.get_collision_pair_info()]
+    perm = [mw.pair_keys.index(k) for k in keys]
+    n = 2048
+    qa = Wd.sample_q(mw.parts[0][1], n, 43)
+    q = np.concatenate([qa, Wd.sample_q(mw.parts[0][1], n, 44)], axis=1) if b_planned else qa
+    fo, mo = mw.collide_batch(q, nthreads=16)
+    w.set_small_batch_max(1 << 20)
+    for i in range(0, n, 200):
+        f, m = w.collide_batch(q[i:i + 200])
+        np.testing.assert_array_equal(f, fo[i:i + 200])
+        m = m.view(np.uint32)
+        for p, po in enumerate(perm):
+            got = (m[:, p >> 5] >> (p & 31)) & 1
+            want = (mo[i:i + 200, po >> 5] >> (po & 31)) & 1
+            assert np.array_equal(got, want), keys[p]
+    assert 0.05 < fo.mean() < 0.999
+
+
 FAR = (310.0, -205.5, 42.25)
 
 
