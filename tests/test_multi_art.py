@@ -181,6 +181,27 @@ def test_two_pandas_latency_path_matches_oracle(b_planned):
     assert 0.05 < fo.mean() < 0.999
 
 
+@pytest.mark.gpu
+def test_two_pandas_planner_matches_oracle_checker():
+    """RRTConnect over the two planned Pandas' 14-dof compound space: the
+    device checker (speculative batches on the latency path) plans the path
+    the oracle checker gives."""
+    from mplib_amd import pymp
+    w = product_world(True)
+    mw = oracle_world(True)
+    dev = pymp.ompl.OMPLPlanner(w)
+    ref = pymp.ompl.OMPLPlanner(product_world(True), state_validity_checker=lambda s: mw.collide_batch(s)[0] == 0)
+    start = np.array([0.0, 0.2, 0.0, -2.6, 0.0, 3.0, 0.8] + list(B_QPOS[:7]))
+    goal = np.array([0.3, -0.3, 0.2, -2.0, 0.1, 2.2, 0.5] + list(B_QPOS[:7]))
+    assert (mw.collide_batch(goal[None])[0] == 0).all()
+    pymp.set_global_seed(11)
+    s1, p1 = dev.plan(start, [goal], range=0.2, time=60.0)
+    pymp.set_global_seed(11)
+    s2, p2 = ref.plan(start, [goal], range=0.2, time=60.0)
+    assert s1 == s2 == "Exact solution"
+    assert np.array_equal(p1, p2)
+
+
 FAR = (310.0, -205.5, 42.25)
 
 
