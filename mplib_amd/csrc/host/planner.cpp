@@ -542,23 +542,16 @@ class NearMemo {
       qpool_.insert(qpool_.end(), q, q + d);
     }
     Ent& x = ents_[(size_t)e];
-    if (x.upto < bt.size()) {
-      cols_.resize((size_t)d);
-      for (int k = 0; k < d; ++k) cols_[(size_t)k] = bt.col[(size_t)k].data();
-      const double* const* cols = cols_.data();
-      double buf[256];
-      const double* qq = qpool_.data() + x.qoff;
-      for (int i0 = x.upto; i0 < bt.size(); i0 += 256) {
-        const int n = std::min(256, bt.size() - i0);
-        l1_columns(cols, sp_.so2.data(), d, qq, i0, n, buf);
-        for (int k = 0; k < n; ++k)
-          if (buf[k] < x.dist) {
-            x.dist = buf[k];
-            x.best = i0 + k;
-          }
-      }
-      x.upto = bt.size();
-    }
+    extend(bt, qpool_.data() + x.qoff, x);
+    return {x.best, x.dist};
+  }
+  // the same for the uniform sample of iteration `it` (the extension's
+  // query): indexed by the iteration, no hashing
+  std::pair<int, double> get_sample(const BaseTree& bt, int t, int64_t it, const double* q) {
+    std::vector<Ent>& v = by_it_[t];
+    if ((int64_t)v.size() <= it) v.resize((size_t)it + 1, Ent{t, 0, -1, std::numeric_limits<double>::infinity(), 0});
+    Ent& x = v[(size_t)it];
+    extend(bt, q, x);
     return {x.best, x.dist};
   }
 
@@ -570,6 +563,25 @@ class NearMemo {
     double dist;
     int upto;
   };
+  // fold the tree nodes added since the entry's last query into its minimum
+  void extend(const BaseTree& bt, const double* q, Ent& x) {
+    if (x.upto >= bt.size()) return;
+    const int d = sp_.dim;
+    cols_.resize((size_t)d);
+    for (int k = 0; k < d; ++k) cols_[(size_t)k] = bt.col[(size_t)k].data();
+    double buf[256];
+    for (int i0 = x.upto; i0 < bt.size(); i0 += 256) {
+      const int n = std::min(256, bt.size() - i0);
+      l1_columns(cols_.data(), sp_.so2.data(), d, q, i0, n, buf);
+      for (int k = 0; k < n; ++k)
+        if (buf[k] < x.dist) {
+          x.dist = buf[k];
+          x.best = i0 + k;
+        }
+    }
+    x.upto = bt.size();
+  }
+  std::vector<Ent> by_it_[2];
   void grow() {
     slots_.assign(slots_.size() * 2, -1);
     for (size_t e = 0; e < ents_.size(); ++e) {
@@ -720,8 +732,8 @@ class ConnectEngine {
     b.opar[t].push_back(par);
     return tree_size(b, t) - 1;
   }
-  int nearest(const Branch& b, int t, const double* q) {
-    auto bn = memo_.get(base_[t], t, q);
+  int nearest(const Branch& b, int t, const double* q, int64_t sample_it = -1) {
+    auto bn = sample_it >= 0 ? memo_.get_sample(base_[t], t, sample_it, q) : memo_.get(base_[t], t, q);
     int best = bn.first;
     double bd = bn.second;
     const int nb = base_[t].size();
@@ -813,7 +825,7 @@ class ConnectEngine {
       if (b.phase == 1) {  // extension: growTree(tree, rstate)
         const double* r = sample(b.it);
         std::copy(r, r + d_, rbuf_.begin());
-        const int n = nearest(b, b.tr, rbuf_.data());
+        const int n = nearest(b, b.tr, rbuf_.data(), b.it);
         const double* nst = node(b, b.tr, n);
         const double* ds = rbuf_.data();
         const double dd = sp_.distance(nst, rbuf_.data());
