@@ -263,10 +263,8 @@ int mpg_check_motion_batch(mpg_world *world, const double *q_from, const double 
  * index (-1 if none).  Distances are within 1e-5 of FCL's GJK (GJK run to
  * 1e-12 relative convergence on the same support mappings).  A point cloud
  * (OcTree) pair's distance is the minimum over its occupied leaf boxes
- * (OcTreeShapeDistanceRecurse, leaf box first).  A BVH-mesh pair's is the
- * minimum over its triangles (mesh-mesh: TriangleDistance::triDistance over
- * the triangle pairs; mesh-shape: GJK of (shape, triangle); mesh-OcTree: GJK
- * of (leaf box, triangle)), -1 once one of them penetrates.
+ * (OcTreeShapeDistanceRecurse, leaf box first); worlds with BVH-mesh pairs
+ * return MPG_E_UNSUPPORTED.
  */
 int mpg_distance_batch(mpg_world *world, const double *q, int64_t n, int32_t n_self_pairs, double *d_self,
                        int32_t *p_self, double *d_others, int32_t *p_others, int mem, void *stream);
