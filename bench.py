@@ -17,6 +17,9 @@ convex=False), --cfg 5 (RRTConnect plan() end to end: a step is one plan()).
 
 Usage:  python bench.py [--gpus N] [--steps K] [--warmup W] [--cpu-sample S] [--cfg C]
         torchrun --nproc-per-node N bench.py --gpus N ...
+`python bench.py --gpus N` (N > 1) without a launcher starts the N ranks
+itself (torch.distributed.run as a child process, one process per GPU, RCCL);
+under a launcher whose WORLD_SIZE differs from --gpus it exits non-zero.
 Rank 0 prints ONE JSON line.
 """
 from __future__ import annotations
@@ -64,22 +67,44 @@ def parse():
     return p.parse_args()
 
 
+def launch_ranks(n: int) -> int:
+    """`bench.py --gpus N` started without a launcher: start N ranks (one
+    process per GPU) with torch.distributed.run as a child process and return
+    its exit code.  Nothing here has touched the GPU (the ranks do that)."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
 def main():
     args = parse()
+    launched = "WORLD_SIZE" in os.environ
+    if not launched and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks")
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # RCCL ("nccl") across GPUs; MPLIB_AMD_DIST_BACKEND=gloo rehearses the
     # multi-rank flow with several ranks sharing one GPU (tests / 1-GPU boxes)
     backend = os.environ.get("MPLIB_AMD_DIST_BACKEND", "nccl")
-    if world > 1:
+    if launched:  # a process group whenever a launcher started us (RCCL initialises even at N=1)
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             dist.init_process_group(backend)
+    if os.environ.get("MPLIB_AMD_BENCH_DRYRUN") == "1":
+        return dryrun_main(args, world, rank, launched)
     if backend != "nccl":
         local = 0
     torch.cuda.set_device(local)
@@ -113,7 +138,7 @@ def main():
     w.profile_read()
     starts = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
     ends = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
-    if world > 1:
+    if launched:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -122,7 +147,7 @@ def main():
         step()
         ends[i].record(stream)
     torch.cuda.synchronize()
-    if world > 1:
+    if dist.is_initialized():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     step_ms = float(np.mean([s.elapsed_time(e) for s, e in zip(starts, ends)]))
@@ -131,7 +156,7 @@ def main():
     # per-launch averages of each stage
     st = {k: {"ms_per_launch": v[0] / max(v[1], 1), "launches_per_step": v[1] / args.steps,
               "units_per_launch": v[2] / max(v[1], 1)} for k, v in prof.items()}
-    if world > 1:
+    if dist.is_initialized():
         t = torch.tensor([elapsed, step_ms] + [st[k]["ms_per_launch"] for k in STAGES], dtype=torch.float64,
                          device=q.device if backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -140,7 +165,7 @@ def main():
             st[k]["ms_per_launch"] = float(t[2 + i])
 
     gather_ms = None
-    if args.gather and world > 1 and backend == "nccl":
+    if args.gather and dist.is_initialized() and backend == "nccl":
         # every rank's flags + pair masks to every rank, device to device
         # (RCCL all-gather over xGMI; mplib_amd.dist.collide_sharded_device's
         # collective), timed apart from the check: not part of `value`
@@ -218,7 +243,7 @@ def main():
         "data": "synthetic (uniform in URDF joint limits)",
         "config": {"workload": f"cfg{cfg} {scenes.CFG_NAME[cfg]}: {n} configs/GPU/step, {n_pairs} pairs, "
                                f"full self+world collide() with ACM filter",
-                   "configs_per_gpu": n, "pairs": n_pairs, "parallelism": f"dp{world} (config shards, no "
+                   "configs_per_gpu": n, "pairs": n_pairs, "mask_words": W, "parallelism": f"dp{world} (config shards, no "
                                                                           "data-path collective)"},
         "roofline": {"bound": "hbm", "achieved": achieved_gbps, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": achieved_gbps / HBM_PEAK_GBPS, "traffic": traffic,
@@ -243,7 +268,25 @@ def main():
         result["cpu_baseline"] = cpu_baseline(cfg, q_host[:k], flags, masks, threads)
     if rank == 0:
         print(json.dumps(result), flush=True)
-    if world > 1:
+    if dist.is_initialized():
+        dist.destroy_process_group()
+
+
+def dryrun_main(args, world, rank, launched):
+    """MPLIB_AMD_BENCH_DRYRUN=1 (CPU tests of the rank fan-out, gloo): the
+    launch, process group, barrier and max-over-ranks reduction of a real run,
+    no device work; rank 0 prints a line with value null."""
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([float(rank)], dtype=torch.float64)
+    if launched:
+        dist.barrier()
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    if rank == 0:
+        print(json.dumps({"metric": "dry run (no device work)", "value": None, "n_gpus": world, "steps": args.steps,
+                          "warmup": args.warmup, "dry_run": True, "max_rank": int(t[0]),
+                          "backend": dist.get_backend() if launched else None}), flush=True)
+    if launched:
         dist.destroy_process_group()
 
 
@@ -276,7 +319,7 @@ def plan_main(args, world, rank, local, backend):
     w.profile_enable(True)
     w.profile_read()
     stats, paths, solved = [], {}, 0
-    if world > 1:
+    if dist.is_initialized():
         dist.barrier()
     t0 = time.perf_counter()
     for i in range(args.steps):
@@ -287,7 +330,7 @@ def plan_main(args, world, rank, local, backend):
     elapsed = time.perf_counter() - t0
     prof = w.profile_read()
     w.profile_enable(False)
-    if world > 1:
+    if dist.is_initialized():
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda" if backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t[0])
@@ -358,7 +401,7 @@ def plan_main(args, world, rank, local, backend):
     os.dup2(saved_stdout, 1)
     if rank == 0:
         print(json.dumps(result), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 

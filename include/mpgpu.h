@@ -263,8 +263,11 @@ int mpg_check_motion_batch(mpg_world *world, const double *q_from, const double 
  * index (-1 if none).  Distances are within 1e-5 of FCL's GJK (GJK run to
  * 1e-12 relative convergence on the same support mappings).  A point cloud
  * (OcTree) pair's distance is the minimum over its occupied leaf boxes
- * (OcTreeShapeDistanceRecurse, leaf box first); worlds with BVH-mesh pairs
- * return MPG_E_UNSUPPORTED.
+ * (OcTreeShapeDistanceRecurse, leaf box first).  A BVH-mesh pair's distance
+ * is the minimum over its triangles (mesh-mesh: PQP triDistance of triangle
+ * pairs; mesh-shape: GJK of (shape, triangle); mesh-OcTree: GJK of (leaf box,
+ * triangle)), as FCL's MeshDistanceTraversalNodeOBBRSS /
+ * MeshShapeDistanceTraversalNodeOBBRSS / OcTreeMeshDistanceRecurse report it.
  */
 int mpg_distance_batch(mpg_world *world, const double *q, int64_t n, int32_t n_self_pairs, double *d_self,
                        int32_t *p_self, double *d_others, int32_t *p_others, int mem, void *stream);
@@ -356,6 +359,16 @@ int mpg_synchronize(int device);
 
 int mpg_device_count(int *count);
 const char *mpg_last_error(void);
+/*
+ * The last error text of the calling thread copied into buf (at most size - 1
+ * bytes and a terminating NUL; truncated if longer).  Returns the full length
+ * of the text (excluding the NUL), as snprintf does, so a caller can size a
+ * buffer; buf may be NULL when size is 0.  This is SURVEY.md 8(b)'s
+ * mpg_last_error(char*, size_t) form for bindings that cannot hold a pointer
+ * into library-owned thread-local storage (cgo / JNI); mpg_last_error() above
+ * stays for C and ctypes callers.
+ */
+int mpg_last_error_copy(char *buf, size_t size);
 const char *mpg_version(void);
 
 #ifdef __cplusplus

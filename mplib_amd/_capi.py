@@ -91,6 +91,7 @@ SIGNATURES = {
     "mpg_synchronize": (ctypes.c_int, [ctypes.c_int]),
     "mpg_device_count": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int)]),
     "mpg_last_error": (ctypes.c_char_p, []),
+    "mpg_last_error_copy": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_size_t]),
     "mpg_version": (ctypes.c_char_p, []),
 }
 

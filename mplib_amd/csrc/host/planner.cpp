@@ -8,6 +8,9 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
 #include <cmath>
 #include <cstring>
 #include <deque>
@@ -600,24 +603,46 @@ class NearMemo {
 };
 
 // one validity batch on the device from a helper thread, so that the planner
-// thread keeps exploring while the GPU works (the C call is synchronous)
+// thread keeps exploring while the GPU works (the C call is synchronous).
+// Both sides spin for at most kSpin (a batch round trip is ~40 us, and the
+// planner submits the next batch right after reading a result), then block
+// on a condition variable: between plans and during long host phases no core
+// is held.  The destructor lets an in-flight batch finish before it stops the
+// helper (a ConnectEngine unwinding between submit() and result()).
 class AsyncCheck {
  public:
-  explicit AsyncCheck(mpg_world* w) : w_(w), th_([this] { loop(); }) {}
+  using BatchFn = std::function<int(const double*, int64_t, uint8_t*)>;
+  explicit AsyncCheck(mpg_world* w)
+      : AsyncCheck([w](const double* q, int64_t n, uint8_t* f) {
+          return mpg_collide_batch(w, q, n, f, nullptr, MPG_MEM_HOST, nullptr);
+        }) {}
+  explicit AsyncCheck(BatchFn fn) : fn_(std::move(fn)), th_([this] { loop(); }) {}
   ~AsyncCheck() {
-    state_.store(kQuit, std::memory_order_release);
+    {
+      std::unique_lock<std::mutex> lk(mu_);
+      cv_done_.wait(lk, [&] { return state_.load(std::memory_order_acquire) != kWork; });
+      state_.store(kQuit, std::memory_order_release);
+    }
+    cv_work_.notify_one();
     th_.join();
   }
   void submit(const std::vector<double>& states, int dim) {
     q_ = states;
     n_ = (int64_t)(states.size() / (size_t)dim);
     flags_.assign((size_t)n_, 0);
-    state_.store(kWork, std::memory_order_release);
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      state_.store(kWork, std::memory_order_release);
+    }
+    cv_work_.notify_one();
   }
   bool done() const { return state_.load(std::memory_order_acquire) == kDone; }
   // valid[i] for the submitted states; throws on a device error
   void result(std::vector<uint8_t>& valid) {
-    while (!done()) cpu_relax();
+    if (!spin_until([&] { return done(); })) {
+      std::unique_lock<std::mutex> lk(mu_);
+      cv_done_.wait(lk, [&] { return done(); });
+    }
     state_.store(kIdle, std::memory_order_relaxed);
     check_status(rc_, "mpg_collide_batch");
     valid.resize((size_t)n_);
@@ -626,24 +651,78 @@ class AsyncCheck {
 
  private:
   static constexpr int kIdle = 0, kWork = 1, kDone = 2, kQuit = 3;
-  static void cpu_relax() { __builtin_ia32_pause(); }
-  void loop() {
-    for (;;) {
-      int s;
-      while ((s = state_.load(std::memory_order_acquire)) != kWork && s != kQuit) cpu_relax();
-      if (s == kQuit) return;
-      rc_ = mpg_collide_batch(w_, q_.data(), n_, flags_.data(), nullptr, MPG_MEM_HOST, nullptr);
-      state_.store(kDone, std::memory_order_release);
+  static constexpr std::chrono::microseconds kSpin{200};
+  template <class Pred>
+  static bool spin_until(Pred pred) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int k = 0;; ++k) {
+      if (pred()) return true;
+      __builtin_ia32_pause();
+      if ((k & 63) == 63 && std::chrono::steady_clock::now() - t0 > kSpin) return pred();
     }
   }
-  mpg_world* w_;
+  void loop() {
+    for (;;) {
+      int s = kIdle;
+      auto ready = [&] {
+        s = state_.load(std::memory_order_acquire);
+        return s == kWork || s == kQuit;
+      };
+      if (!spin_until(ready)) {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_work_.wait(lk, ready);
+      }
+      if (s == kQuit) return;
+      rc_ = fn_(q_.data(), n_, flags_.data());
+      {
+        std::lock_guard<std::mutex> lk(mu_);
+        state_.store(kDone, std::memory_order_release);
+      }
+      cv_done_.notify_all();
+    }
+  }
+  BatchFn fn_;
   std::vector<double> q_;
   std::vector<uint8_t> flags_;
   int64_t n_ = 0;
   int rc_ = 0;
   std::atomic<int> state_{kIdle};
-  std::thread th_;
+  std::mutex mu_;
+  std::condition_variable cv_work_, cv_done_;
+  std::thread th_;  // last: started after every member above exists
+
 };
+
+// CPU self-test of AsyncCheck's shutdown (pymp._selftest): a fake batch that
+// takes `batch_ms`; with in_flight the helper is destroyed between submit()
+// and result(), as a ConnectEngine that throws there would.  Returns the
+// destructor's wall time in ms (it waits for the batch, it never hangs).
+double async_check_selftest_impl(double batch_ms, bool in_flight) {
+  std::atomic<int> calls{0};
+  auto t0 = std::chrono::steady_clock::now();
+  {
+    AsyncCheck a([&](const double*, int64_t n, uint8_t* f) {
+      std::this_thread::sleep_for(std::chrono::duration<double, std::milli>(batch_ms));
+      for (int64_t i = 0; i < n; ++i) f[i] = (uint8_t)(i & 1);
+      ++calls;
+      return 0;
+    });
+    std::vector<double> st(6, 0.0);
+    a.submit(st, 2);
+    if (!in_flight) {
+      std::vector<uint8_t> v;
+      a.result(v);
+      if (v.size() != 3 || v[0] != 1 || v[1] != 0) throw std::runtime_error("AsyncCheck selftest: bad result");
+      a.submit(st, 3);
+      a.result(v);
+      if (v.size() != 2) throw std::runtime_error("AsyncCheck selftest: bad result");
+    }
+    t0 = std::chrono::steady_clock::now();
+  }  // destructor
+  const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  if (calls.load() != (in_flight ? 1 : 2)) throw std::runtime_error("AsyncCheck selftest: batch count");
+  return ms;
+}
 
 class ConnectEngine {
  public:
@@ -1380,5 +1459,7 @@ std::pair<std::string, std::vector<std::vector<double>>> OMPLPlanner::plan(
   if (approxsol >= 0) return finish("Approximate solution", path_rows(sp, root_path(tstart, approxsol)));
   return finish("Timeout", {});
 }
+
+double async_check_selftest(double batch_ms, bool in_flight) { return async_check_selftest_impl(batch_ms, in_flight); }
 
 }  // namespace mpgh

@@ -116,4 +116,7 @@ class OMPLPlanner {
   std::vector<uint8_t> flags_;
 };
 
+// CPU self-test of the planner's asynchronous validity helper (pymp._selftest)
+double async_check_selftest(double batch_ms, bool in_flight);
+
 }  // namespace mpgh

@@ -86,6 +86,11 @@ PYBIND11_MODULE(pymp, m_all) {
   translate_exceptions();
   m_all.def("set_global_seed", &set_global_seed, py::arg("seed"));
   m_all.def("device_version", []() { return std::string(mpg_version()); });
+  auto m_st = m_all.def_submodule("_selftest", "host-only self tests (no device)");
+  m_st.def("async_check_shutdown", &async_check_selftest, py::arg("batch_ms"), py::arg("in_flight"),
+           py::call_guard<py::gil_scoped_release>(),
+           "Destroys the planner's asynchronous validity helper with a fake batch of batch_ms in flight "
+           "(or after two completed batches); returns the destructor's wall time in ms.");
 
   // ------------------------------------------------------------------ fcl
   auto m = m_all.def_submodule("fcl");

@@ -983,7 +983,7 @@ __global__ __launch_bounds__(BLOCK) void cull_kernel(DevWorld w, const double* _
     bp_fk(w.bp, in + c * w.dof, save + tid, BLOCK, put);
     if (w.n_prism)
       for (int j = 0; j < w.nj; ++j)
-        if (w.prism_bound[j] > 0.0) forced |= !(std::fabs(in[c * w.dof + w.joint_q_source[j]]) <= w.prism_bound[j]);
+        if (w.prism_bound[j] >= 0.0) forced |= !(std::fabs(in[c * w.dof + w.joint_q_source[j]]) <= w.prism_bound[j]);
   }
   if (w.dbg(1)) {
     if (live && cen[tid] == 12345.f) flags[cfg] = 2;  // keep the records alive
@@ -2567,7 +2567,7 @@ __global__ __launch_bounds__(256) void small_kernel(DevWorld w, const double* __
       __shared__ double lat_sc[4][64][2 * kLatScDof];
       double* mine = lat_sc[threadIdx.x >> 6][lane];
       const double* qrow = in + c * w.dof;
-      if (am || bm) {
+      if ((am || bm) && w.dof > 0) {  // dof 0: no row (q may be null), every joint is a constant
         // the row first, in one round of loads (it may sit in host memory)
         double qv[kLatScDof];
 #pragma unroll
@@ -5024,6 +5024,9 @@ struct mpg_world {
   // mpg_release_stream drops one explicitly
   static constexpr size_t kMaxStreamState = 32;
   uint64_t ws_tick = 0;
+  // caller streams with a call in progress (StreamPin): never evicted, so no
+  // thread frees a workspace or side stream another thread is using
+  std::map<hipStream_t, int> busy;  // guarded by ws_mu
   // small-batch latency path (host buffers, n <= small_max): pinned input
   // staging + host-mapped hit bytes written by small_kernel
   long long small_max = 1024;
@@ -5369,7 +5372,11 @@ void evict_streams_locked(mpg_world* w) {
     uint64_t& t = callers[kv.first];
     t = std::max(t, kv.second.last);
   }
-  while (callers.size() >= mpg_world::kMaxStreamState) {
+  for (auto& kv : w->busy)
+    if (kv.second > 0) callers.erase(kv.first);  // in use by a call: not evictable
+  size_t pinned = 0;
+  for (auto& kv : w->busy) pinned += kv.second > 0;
+  while (!callers.empty() && callers.size() + pinned >= mpg_world::kMaxStreamState) {
     auto lru = callers.begin();
     for (auto it = callers.begin(); it != callers.end(); ++it)
       if (it->second < lru->second) lru = it;
@@ -5377,6 +5384,21 @@ void evict_streams_locked(mpg_world* w) {
     callers.erase(lru);
   }
 }
+
+// keeps a caller stream's state (workspace, side stream) from eviction for
+// the duration of one call
+struct StreamPin {
+  mpg_world* w;
+  hipStream_t s;
+  StreamPin(mpg_world* w_, hipStream_t s_) : w(w_), s(s_) {
+    std::lock_guard<std::mutex> lk(w->ws_mu);
+    ++w->busy[s];
+  }
+  ~StreamPin() {
+    std::lock_guard<std::mutex> lk(w->ws_mu);
+    if (--w->busy[s] <= 0) w->busy.erase(s);
+  }
+};
 
 bool is_side_stream_locked(const mpg_world* w, hipStream_t s) {
   for (auto& kv : w->sides)
@@ -5452,6 +5474,7 @@ template <bool FROM_POSES>
 int launch_collide(mpg_world* w, const double* in, long long n, uint8_t* flags, uint32_t* masks, hipStream_t stream,
                    const ContactOut* co = nullptr) {
   if (n == 0) return MPG_OK;
+  StreamPin pin(w, stream);
   const long long chunk = std::min<long long>(n, w->max_chunk);
   mpg_world::Workspace* ws = nullptr;
   int rc = get_workspace(w, stream, chunk, &ws);
@@ -5560,6 +5583,16 @@ int ensure_staging(mpg_world* w, size_t ncfg, size_t nout) {
 extern "C" {
 
 const char* mpg_last_error(void) { return g_last_error.c_str(); }
+
+int mpg_last_error_copy(char* buf, size_t size) {
+  const size_t len = g_last_error.size();
+  if (buf && size > 0) {
+    const size_t k = std::min(len, size - 1);
+    std::memcpy(buf, g_last_error.data(), k);
+    buf[k] = '\0';
+  }
+  return (int)std::min<size_t>(len, 0x7fffffff);
+}
 
 const char* mpg_version(void) { return "mpgpu 0.1 (gfx950, fp64, libccd-MPR)"; }
 
@@ -5825,7 +5858,8 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
   // A configuration whose prismatic value exceeds its bound is evaluated with
   // every pair (the cull's coordinate bound below would not hold for it).
   auto sq3 = [](const double* v) { return v[0] * v[0] + v[1] * v[1] + v[2] * v[2]; };
-  std::vector<double> travel(std::max(d->n_joints, 1), 0.0), prism_bound(std::max(d->n_joints, 1), 0.0);
+  // prism_bound < 0: not a move-group prismatic joint (a [0, 0] limit is a real bound of 0)
+  std::vector<double> travel(std::max(d->n_joints, 1), 0.0), prism_bound(std::max(d->n_joints, 1), -1.0);
   int n_prism = 0;
   for (int j = 0; j < d->n_joints; ++j) {
     const int t = d->joint_type[j];
@@ -6360,6 +6394,7 @@ int collide_small(mpg_world* w, const double* q, int64_t n, uint8_t* flags, uint
 template <bool FROM_POSES>
 int launch_collide_overlapped(mpg_world* w, const double* in, long long n, uint8_t* flags, uint32_t* masks,
                               hipStream_t s) {
+  StreamPin pin(w, s);
   if (w->overlap_min <= 0 || n < w->overlap_min) return launch_collide<FROM_POSES>(w, in, n, flags, masks, s);
   // one side stream and fork/join event pair per caller stream: callers on
   // different streams (one host thread each, include/mpgpu.h) never record
@@ -6403,12 +6438,13 @@ int collide_common(mpg_world* w, const double* q, int64_t n, uint8_t* flags, uin
                    void* stream) {
   if (!w) return set_error(MPG_E_INVALID, "world is NULL");
   if (n < 0) return set_error(MPG_E_INVALID, "n < 0");
-  if (n > 0 && (!q || !flags)) return set_error(MPG_E_INVALID, "input/flags is NULL");
+  const size_t row = FROM_POSES ? (size_t)w->dw.n_links * 7 : (size_t)w->dw.dof;
+  // a world without inputs (dof 0) may pass q = NULL
+  if (n > 0 && ((!q && row > 0) || !flags)) return set_error(MPG_E_INVALID, "input/flags is NULL");
   HIP_TRY(hipSetDevice(w->device));
   hipStream_t s = static_cast<hipStream_t>(stream);
   if (mem == MPG_MEM_DEVICE) return launch_collide_overlapped<FROM_POSES>(w, q, n, flags, pair_mask, s);
   if (mem != MPG_MEM_HOST) return set_error(MPG_E_INVALID, "bad mem kind");
-  const size_t row = FROM_POSES ? (size_t)w->dw.n_links * 7 : (size_t)w->dw.dof;
   std::lock_guard<std::mutex> lk(w->host_mu);
   if (n > 0 && n <= w->small_max) return collide_small<FROM_POSES>(w, q, n, flags, pair_mask, s);
   int rc = ensure_staging(w, (size_t)n, std::max<size_t>(1, (size_t)n * row));
@@ -6432,6 +6468,8 @@ int mpg_release_stream(mpg_world* w, void* stream) {
   if (!w) return set_error(MPG_E_INVALID, "world is NULL");
   HIP_TRY(hipSetDevice(w->device));
   std::lock_guard<std::mutex> lk(w->ws_mu);
+  const auto b = w->busy.find(static_cast<hipStream_t>(stream));
+  if (b != w->busy.end() && b->second > 0) return set_error(MPG_E_INVALID, "stream has a call in progress");
   release_stream_locked(w, static_cast<hipStream_t>(stream));
   return MPG_OK;
 }

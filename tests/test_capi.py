@@ -111,3 +111,50 @@ def test_result_changing_switches_only_in_diag_builds():
         assert "debug_mode ==" not in s, ln
     hdr = open(os.path.join(ROOT, "mplib_amd", "csrc", "mpg_fk.h")).read()
     assert "#ifdef MPG_DIAG\n    return debug_mode == k;" in hdr
+
+
+def test_last_error_copy():
+    """mpg_last_error_copy(char*, size_t): SURVEY.md 8(b)'s copy-out form of
+    the thread's last error, snprintf-style (full length returned, truncated
+    with a NUL)."""
+    L = C.lib()
+    ow = Wd.oracle_world(3)
+    with pytest.raises(ValueError, match="joint_parent"):
+        _create(_desc(ow, joint_parent=[5, 0, 0, 0, 0, 0, 0, 0, 0]))
+    full = L.mpg_last_error().decode()
+    assert "joint_parent" in full
+    n = L.mpg_last_error_copy(None, 0)
+    assert n == len(full)
+    buf = ctypes.create_string_buffer(len(full) + 1)
+    assert L.mpg_last_error_copy(buf, len(buf)) == len(full) and buf.value.decode() == full
+    small = ctypes.create_string_buffer(8)
+    assert L.mpg_last_error_copy(small, 8) == len(full) and small.value.decode() == full[:7]
+
+
+def test_lib_hash_keys_the_code_object_only(tmp_path):
+    """the profile key (tools/build_hash.py) is a hash of the
+    gfx950 code objects (.hip_fatbin) and host code (.text, .rodata) of
+    libmpgpu.so, not of source text, so a
+    comment-only change cannot invalidate a PMC record.  A rebuild of the same
+    code in another directory with a comment added to the header and the kernel
+    file was checked to give the same key; here: bytes outside the
+    section leave the key alone, a byte inside it changes it."""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import build_hash as B
+    lib = B.LIB
+    data = bytearray(open(lib, "rb").read())
+    key = B.build_hash(lib)
+    off, size = B.elf_section_range(bytes(data), ".hip_fatbin")
+    outside = bytearray(data)
+    outside += b"// appended comment\n"  # not inside any section
+    i, _ = B.elf_section_range(bytes(data), ".comment")  # compiler identification strings
+    outside[i + 1] ^= 0x20
+    p1 = tmp_path / "a.so"
+    p1.write_bytes(bytes(outside))
+    assert B.build_hash(str(p1)) == key
+    inside = bytearray(data)
+    inside[off + size // 2] ^= 0xFF
+    p2 = tmp_path / "b.so"
+    p2.write_bytes(bytes(inside))
+    assert B.build_hash(str(p2)) != key

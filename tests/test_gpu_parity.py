@@ -685,6 +685,49 @@ def test_bench_two_ranks_gloo_one_gpu():
     assert r["config"]["configs_per_gpu"] == 65536
 
 
+@pytest.mark.gpu
+def test_bench_gpus2_self_launch_gloo_one_gpu():
+    """`python bench.py --gpus 2` with no launcher starts its two ranks itself
+    (here sharing this box's GPU over gloo) and reports n_gpus 2."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["MPLIB_AMD_DIST_BACKEND"] = "gloo"
+    out = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup",
+                          "1", "--per-gpu", "65536", "--cpu-sample", "0"],
+                         env=env, capture_output=True, text=True, timeout=600, cwd=root)
+    assert out.returncode == 0, out.stderr[-2000:]
+    r = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][-1])
+    assert r["n_gpus"] == 2 and r["value"] > 0
+
+
+@pytest.mark.gpu
+def test_bench_one_rank_nccl_gather():
+    """RCCL on hardware: one rank launched by torch.distributed.run with the
+    nccl backend (RCCL) initialises its communicator and times the all-gather
+    of flags + pair masks (--gather)."""
+    import json
+    import socket
+    import subprocess
+    import sys
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k != "MPLIB_AMD_DIST_BACKEND"}
+    out = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+                          "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(root, "bench.py"),
+                          "--gpus", "1", "--steps", "3", "--warmup", "1", "--per-gpu", "65536", "--cpu-sample", "0",
+                          "--gather"], env=env, capture_output=True, text=True, timeout=600, cwd=root)
+    assert out.returncode == 0, out.stderr[-2000:]
+    r = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][-1])
+    assert r["n_gpus"] == 1 and r["value"] > 0 and r["gather_ms"] > 0
+    assert r["gather_bytes_per_rank"] == 65536 * (1 + 4 * r["config"]["mask_words"])
+
+
 # --------------------------------------------------------------- point clouds
 @pytest.mark.parametrize("kind", ["floor", "blue"])
 def test_point_cloud_world_matches_oracle(kind):
@@ -844,3 +887,34 @@ def test_big_walk_hulls_match_oracle():
         assert fo.mean() > 0.05
         np.testing.assert_array_equal(f, fo)
         np.testing.assert_array_equal(m, mo)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [5, 300, 5000])
+def test_dof0_world_with_moving_links(n):
+    """a world whose robot links move but whose move group
+    is empty (dof 0, q = NULL): every joint is a constant, every configuration
+    is the same state.  Latency path (n <= 1024, host buffers) and pipeline,
+    both equal to the oracle at that state."""
+    from mplib_amd import _capi as C
+    o = ow(3)
+    q0 = np.array(Wd.KAT_COLLIDING)
+    a = Wd.desc_arrays(o)
+    mg = o.art.move_group_qpos_index()
+    src = list(a["joint_q_source"])
+    const = list(a["joint_q_const"])
+    for j, s in enumerate(src):
+        if s >= 0:
+            const[j] = float(q0[s])
+            src[j] = -1
+    a.update(joint_q_source=src, joint_q_const=const, dof=0)
+    assert len(mg) == 7
+    d = DeviceWorld(a)
+    fl = np.full(n, 7, np.uint8)
+    pm = np.zeros((n, d.mask_words), np.uint32)
+    C.check(C.lib().mpg_collide_batch(d._h, None, n, fl.ctypes.data_as(ctypes.c_void_p),
+                                      pm.ctypes.data_as(ctypes.c_void_p), C.MPG_MEM_HOST, None), "dof0")
+    fo, mo = o.collide_batch(q0[None])
+    assert fo[0] == 1
+    np.testing.assert_array_equal(fl, np.repeat(fo, n))
+    np.testing.assert_array_equal(pm, np.repeat(mo, n, axis=0))
