@@ -273,6 +273,30 @@ int mpg_distance_batch(mpg_world *world, const double *q, int64_t n, int32_t n_s
                        int32_t *p_self, double *d_others, int32_t *p_others, int mem, void *stream);
 
 /*
+ * mpg_distance_batch with DistanceRequest's options (python/pybind_fcl.hpp:
+ * 310-316, passed to fcl::distance by PlanningWorldTpl::distance*,
+ * src/planning_world.cpp:512, 537):
+ *   MPG_DISTANCE_SIGNED          enable_signed_distance: an intersecting pair's
+ *                                distance is -(penetration depth) (FCL 0.7.0
+ *                                ccdGJKSignedDist: GJK then EPA), not -1;
+ *   MPG_DISTANCE_NEAREST_POINTS  enable_nearest_points.
+ * pts_self / pts_others ([n*6], may be NULL): the nearest points (p1 on the
+ * pair's first object, p2 on its second, world frame) of each group's
+ * minimum pair.  Shape-shape pairs report them whatever the flags, as FCL's
+ * shape distance leaf computes them (libccd extractClosestPoints: the
+ * barycentric weights of the final GJK simplex; penEPAPosClosest for signed
+ * penetrations); zeros for an unsigned penetration (-1).  Point-cloud and
+ * BVH-mesh pairs report zeros; with either flag set a world with such pairs
+ * returns MPG_E_UNSUPPORTED.  EPA runs in fp64 to 1e-10 m (at most 64
+ * polytope vertices); FCL's float EPA stops at libccd's epa_tolerance (1e-4).
+ */
+#define MPG_DISTANCE_SIGNED 1
+#define MPG_DISTANCE_NEAREST_POINTS 2
+int mpg_distance_batch_ex(mpg_world *world, const double *q, int64_t n, int32_t n_self_pairs, int32_t flags,
+                          double *d_self, int32_t *p_self, double *pts_self, double *d_others, int32_t *p_others,
+                          double *pts_others, int mem, void *stream);
+
+/*
  * Collide with contacts: CollisionRequest(enable_contact=True).  Same flags /
  * pair_mask as mpg_collide_batch (input_kind MPG_INPUT_Q: q rows) or
  * mpg_collide_link_poses (MPG_INPUT_LINK_POSES), plus, for every reported

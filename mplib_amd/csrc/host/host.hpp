@@ -145,8 +145,10 @@ struct DistanceRequest {
   bool enable_signed_distance = false;
   double rel_err = 0.0, abs_err = 0.0, distance_tolerance = 1e-6;
   GJKSolverType gjk_solver_type = GST_LIBCCD;
-  // the device computes the plain (unsigned, -1 on penetration) GJK distance
+  // GST_INDEP is not implemented on the device (raises)
   void check_supported() const;
+  // MPG_DISTANCE_* flags of the C ABI
+  int32_t flags() const;
 };
 struct DistanceResult {
   double min_distance = std::numeric_limits<double>::max();
@@ -587,6 +589,9 @@ class PlanningWorld {
   // per configuration: (self group, others group) minimum and pair index
   void distance_batch(const double* q, int64_t n, double* d_self, int32_t* p_self, double* d_others,
                       int32_t* p_others);
+  // with DistanceRequest's flags and the nearest points [n*6] (may be NULL)
+  void distance_batch_ex(const double* q, int64_t n, int32_t flags, double* d_self, int32_t* p_self, double* pts_self,
+                         double* d_others, int32_t* p_others, double* pts_others);
   int n_self_pairs();
 
   // batch API (one launch for N configurations)

@@ -407,12 +407,17 @@ PYBIND11_MODULE(pymp, m_all) {
         d.pair_b.push_back(1);
         d.pair_allowed.push_back(0);
         DeviceWorld w(d, default_device());
-        double ds = 0, dd = 0;
+        double ds = 0, dd = 0, qs[6], qo[6];
         int32_t ps = -1, po = -1;
-        check_status(mpg_distance_batch(w.get(), nullptr, 1, 0, &ds, &ps, &dd, &po, MPG_MEM_HOST, nullptr),
-                     "mpg_distance_batch");
+        check_status(mpg_distance_batch_ex(w.get(), nullptr, 1, 0, req.flags(), &ds, &ps, qs, &dd, &po, qo,
+                                           MPG_MEM_HOST, nullptr),
+                     "mpg_distance_batch_ex");
         DistanceResult r;
         r.min_distance = dd;
+        for (int k = 0; k < 3; ++k) {
+          r.nearest_points[0][k] = qo[k];
+          r.nearest_points[1][k] = qo[3 + k];
+        }
         return r;
       },
       py::arg("o1"), py::arg("o2"), py::arg("request") = DistanceRequest());
@@ -677,25 +682,43 @@ PYBIND11_MODULE(pymp, m_all) {
       .def("distance_with_others", &PW::distance_with_others, py::arg("request") = DistanceRequest())
       .def("distance_full", &PW::distance_full, py::arg("request") = DistanceRequest())
       .def("distance_batch",
-           [](PW& w, py::array_t<double, py::array::c_style | py::array::forcecast> states) {
+           [](PW& w, py::array_t<double, py::array::c_style | py::array::forcecast> states, py::object request,
+              bool nearest_points) -> py::tuple {
              const int dim = w.state_dim();
              if (states.ndim() != 2 || states.shape(1) != dim)
                throw std::invalid_argument("states must be [N, " + std::to_string(dim) + "] float64");
+             int32_t flags = 0;
+             if (!request.is_none()) {
+               const DistanceRequest& r = request.cast<const DistanceRequest&>();
+               r.check_supported();
+               flags = r.flags();
+             }
              const int64_t n = states.shape(0);
              py::array_t<double> ds(n), dot(n);
              py::array_t<int32_t> ps(n), po(n);
              const double* q = states.data();
              double *a = ds.mutable_data(), *b = dot.mutable_data();
              int32_t *c = ps.mutable_data(), *d = po.mutable_data();
+             if (!nearest_points && flags == 0) {
+               {
+                 py::gil_scoped_release rel;
+                 w.distance_batch(q, n, a, c, b, d);
+               }
+               return py::tuple(py::make_tuple(ds, ps, dot, po));
+             }
+             py::array_t<double> qs({n, (int64_t)6}), qo({n, (int64_t)6});
+             double *e = qs.mutable_data(), *f = qo.mutable_data();
              {
                py::gil_scoped_release rel;
-               w.distance_batch(q, n, a, c, b, d);
+               w.distance_batch_ex(q, n, flags, a, c, e, b, d, f);
              }
-             return py::make_tuple(ds, ps, dot, po);
+             return py::tuple(py::make_tuple(ds, ps, dot, po, qs, qo));
            },
-           py::arg("states"),
+           py::arg("states"), py::arg("request") = py::none(), py::arg("nearest_points") = false,
            "Batched self_distance / distance_with_others: (d_self[N], pair_self[N], d_others[N], pair_others[N]); "
-           "-1 = a penetrating pair, pair indices into get_collision_pair_info().")
+           "-1 = a penetrating pair, pair indices into get_collision_pair_info().  With a DistanceRequest "
+           "(enable_signed_distance: -penetration depth instead of -1) or nearest_points=True, also the nearest "
+           "points (p1, p2) of each group's minimum pair: (..., pts_self[N, 6], pts_others[N, 6]).")
       // ---- batched validity (new; one device launch for N states) ----
       .def("sample_pair_counts",
            [](PW& w, int64_t n, uint64_t seed) {
@@ -803,6 +826,66 @@ PYBIND11_MODULE(pymp, m_all) {
 
   // ---- ompl (reference python/pybind_ompl.hpp:20-33) ----
   auto mo = m_all.def_submodule("ompl");
+  // ValidityCheckerTpl (src/ompl_planner.h:54-81): isValid / clearance of one
+  // state through the world (which they leave at that state), and batched
+  // twins that leave the world alone (one device launch for N states)
+  struct ValidityChecker {
+    std::shared_ptr<PW> world;
+  };
+  auto states_arg = [](PW& w, const py::array_t<double, py::array::c_style | py::array::forcecast>& st) {
+    const int dim = w.state_dim();
+    if (st.ndim() != 2 || st.shape(1) != dim)
+      throw std::invalid_argument("states must be [N, " + std::to_string(dim) + "] float64");
+    return (int64_t)st.shape(0);
+  };
+  py::class_<ValidityChecker, std::shared_ptr<ValidityChecker>>(mo, "ValidityChecker")
+      .def(py::init([](const std::shared_ptr<PW>& w) { return std::make_shared<ValidityChecker>(ValidityChecker{w}); }),
+           py::arg("world"))
+      .def("is_valid",
+           [](ValidityChecker& v, const std::vector<double>& state) {
+             v.world->set_qpos_all(state);
+             return !v.world->collide();
+           },
+           py::arg("state"), "setQposAll(state); !collide()  (ompl_planner.h:59-62)")
+      .def("clearance",
+           [](ValidityChecker& v, const std::vector<double>& state) {
+             v.world->set_qpos_all(state);
+             return v.world->distance();
+           },
+           py::arg("state"),
+           "setQposAll(state); distance(): the distance to the nearest invalid state, -1 in collision "
+           "(ompl_planner.h:69-72, planning_world.h:271-273)")
+      .def("is_valid_batch",
+           [states_arg](ValidityChecker& v, py::array_t<double, py::array::c_style | py::array::forcecast> states) {
+             const int64_t n = states_arg(*v.world, states);
+             std::vector<uint8_t> fl((size_t)n);
+             std::vector<uint32_t> mk((size_t)n * (size_t)std::max(v.world->mask_words(), 1));
+             {
+               py::gil_scoped_release rel;
+               v.world->collide_batch(states.data(), n, fl.data(), mk.data());
+             }
+             py::array_t<bool> out(n);
+             for (int64_t i = 0; i < n; ++i) out.mutable_data()[i] = fl[(size_t)i] == 0;
+             return out;
+           },
+           py::arg("states"))
+      .def("clearance_batch",
+           [states_arg](ValidityChecker& v, py::array_t<double, py::array::c_style | py::array::forcecast> states) {
+             const int64_t n = states_arg(*v.world, states);
+             std::vector<double> ds((size_t)n), dot((size_t)n);
+             std::vector<int32_t> ps((size_t)n), po((size_t)n);
+             {
+               py::gil_scoped_release rel;
+               v.world->distance_batch(states.data(), n, ds.data(), ps.data(), dot.data(), po.data());
+             }
+             py::array_t<double> out(n);
+             for (int64_t i = 0; i < n; ++i)  // distanceFull: the smaller group minimum (planning_world.cpp:718-719)
+               out.mutable_data()[i] = ds[(size_t)i] < dot[(size_t)i] ? ds[(size_t)i] : dot[(size_t)i];
+             return out;
+           },
+           py::arg("states"),
+           "clearance() of N states in one device launch (MaximizeMinClearanceObjective's query, "
+           "ompl_planner.cpp:180-186), world state untouched");
   py::class_<OMPLPlanner, std::shared_ptr<OMPLPlanner>>(mo, "OMPLPlanner")
       .def(py::init([](const std::shared_ptr<PW>& world, py::object checker) {
              auto p = std::make_shared<OMPLPlanner>(world);

@@ -675,12 +675,12 @@ void PlanningWorld::check_motion_batch(const double* from, const double* to, int
 }
 
 void DistanceRequest::check_supported() const {
-  if (enable_signed_distance)
-    throw std::logic_error("NotImplemented: DistanceRequest(enable_signed_distance=True) is not implemented on the device");
-  if (enable_nearest_points)
-    throw std::logic_error("NotImplemented: DistanceRequest(enable_nearest_points=True) is not implemented on the device");
   if (gjk_solver_type != GST_LIBCCD)
     throw std::logic_error("NotImplemented: only GJKSolverType.GST_LIBCCD is implemented on the device");
+}
+
+int32_t DistanceRequest::flags() const {
+  return (enable_signed_distance ? MPG_DISTANCE_SIGNED : 0) | (enable_nearest_points ? MPG_DISTANCE_NEAREST_POINTS : 0);
 }
 
 int PlanningWorld::n_self_pairs() {
@@ -700,13 +700,28 @@ void PlanningWorld::distance_batch(const double* q, int64_t n, double* d_self, i
                "mpg_distance_batch");
 }
 
+void PlanningWorld::distance_batch_ex(const double* q, int64_t n, int32_t flags, double* d_self, int32_t* p_self,
+                                      double* pts_self, double* d_others, int32_t* p_others, double* pts_others) {
+  const int ns = n_self_pairs();
+  ensure_snapshot(CollisionRequest());
+  check_status(mpg_distance_batch_ex(world_->get(), q, n, ns, flags, d_self, p_self, pts_self, d_others, p_others,
+                                     pts_others, MPG_MEM_HOST, nullptr),
+               "mpg_distance_batch_ex");
+}
+
 namespace {
-WorldDistanceResult distance_result(double d, int p, const std::vector<PairInfo>& pairs) {
+// the WorldDistanceResult of a group's minimum pair p (DistanceResult with
+// its nearest points, planning_world.cpp:512-525)
+WorldDistanceResult distance_result(double d, int p, const std::vector<PairInfo>& pairs, const double* pts) {
   WorldDistanceResult r;
   if (p < 0) return r;
   const PairInfo& pi = pairs[p];
   r.min_distance = d;
   r.res.min_distance = d;
+  for (int k = 0; k < 3; ++k) {
+    r.res.nearest_points[0][k] = pts[k];
+    r.res.nearest_points[1][k] = pts[3 + k];
+  }
   r.distance_type = pi.collision_type;
   r.object_name1 = pi.object_name1;
   r.object_name2 = pi.object_name2;
@@ -719,28 +734,29 @@ WorldDistanceResult distance_result(double d, int p, const std::vector<PairInfo>
 WorldDistanceResult PlanningWorld::self_distance(const DistanceRequest& r) {
   r.check_supported();
   std::vector<double> s = current_state();
-  double ds, dot;
+  double ds, dot, qs[6], qo[6];
   int32_t ps, po;
-  distance_batch(s.data(), 1, &ds, &ps, &dot, &po);
-  return distance_result(ds, ps, pairs_);
+  distance_batch_ex(s.data(), 1, r.flags(), &ds, &ps, qs, &dot, &po, qo);
+  return distance_result(ds, ps, pairs_, qs);
 }
 WorldDistanceResult PlanningWorld::distance_with_others(const DistanceRequest& r) {
   r.check_supported();
   std::vector<double> s = current_state();
-  double ds, dot;
+  double ds, dot, qs[6], qo[6];
   int32_t ps, po;
-  distance_batch(s.data(), 1, &ds, &ps, &dot, &po);
-  return distance_result(dot, po, pairs_);
+  distance_batch_ex(s.data(), 1, r.flags(), &ds, &ps, qs, &dot, &po, qo);
+  return distance_result(dot, po, pairs_, qo);
 }
 WorldDistanceResult PlanningWorld::distance_full(const DistanceRequest& r) {
   r.check_supported();
   std::vector<double> s = current_state();
-  double ds, dot;
+  double ds, dot, qs[6], qo[6];
   int32_t ps, po;
-  distance_batch(s.data(), 1, &ds, &ps, &dot, &po);
-  auto r1 = distance_result(ds, ps, pairs_), r2 = distance_result(dot, po, pairs_);
+  distance_batch_ex(s.data(), 1, r.flags(), &ds, &ps, qs, &dot, &po, qo);
+  auto r1 = distance_result(ds, ps, pairs_, qs), r2 = distance_result(dot, po, pairs_, qo);
   return r1.min_distance < r2.min_distance ? r1 : r2;  // planning_world.cpp:718-719
 }
+// the reference ignores the request here (planning_world.h:271-273)
 double PlanningWorld::distance(const DistanceRequest&) { return distance_full().min_distance; }
 
 void PlanningWorld::profile_enable(bool on) { check_status(mpg_profile_enable(device_world(), on ? 1 : 0), "mpg_profile_enable"); }

@@ -888,6 +888,16 @@ __device__ __forceinline__ uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi
 constexpr int kQueue = 128;  // entries per wave: < 64 pending + <= 64 pushed
 constexpr uint32_t kTask = MPG_TASK;  // narrow phase: candidates of one pair per wave task
 
+// inclusive scan of one value per lane across the wave
+__device__ __forceinline__ uint32_t wave_inclusive_scan(uint32_t v, uint32_t lane) {
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t u = __shfl_up(v, off);
+    if (lane >= (uint32_t)off) v += u;
+  }
+  return v;
+}
+
 template <int BLOCK>
 __device__ __forceinline__ FObb bp_obb(const DevWorld& w, const float* __restrict__ cen, const float* __restrict__ rq,
                                        long long cap, int id, int t, long long cfg) {
@@ -921,8 +931,8 @@ __device__ __forceinline__ void sat_drain(const DevWorld& w, const float* __rest
                                           uint32_t head, uint32_t cnt, int wbase, uint32_t lane) {
   __builtin_amdgcn_wave_barrier();
   if (lane < cnt) {
-    const uint32_t e = queue[(head + lane) & (kQueue - 1)];
-    const int p = (int)(e >> 6), t = wbase + (int)(e & 63u);
+    const uint32_t e = queue[(head + lane) & (kQueue - 1)];  // (schedule entry, lane)
+    const int p = w.sched_pair[(int)(e >> 6)], t = wbase + (int)(e & 63u);
     const FObb A = bp_obb<BLOCK>(w, cen, rq, cap, w.pair_a[p], t, cfg0 + t);
     const FObb B = bp_obb<BLOCK>(w, cen, rq, cap, w.pair_b[p], t, cfg0 + t);
     if (!fobb_separated(A, B, w.bp_margin)) atomicOr(&survw[(p >> 5) * BLOCK + t], 1u << (p & 31));
@@ -1003,6 +1013,27 @@ __global__ __launch_bounds__(BLOCK) void cull_kernel(DevWorld w, const double* _
       }
       return;
     }
+    // one wave scan of the kept counts: each lane writes its own entries
+    // (schedule index, lane) at its offset, no per-entry wave-level loop
+    const uint32_t c = (uint32_t)__popc(kb);
+    const uint32_t incl = wave_inclusive_scan(c, lane);
+    const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+    if (total == 0u) return;
+    if (tail - head + total <= (uint32_t)kQueue) {
+      uint32_t pos = tail + incl - c;
+      while (kb) {
+        const int i = __builtin_ctz(kb);
+        kb &= kb - 1u;
+        queue[pos++ & (kQueue - 1)] = ((uint32_t)(eb + i) << 6) | lane;
+      }
+      tail += total;
+      while (tail - head >= 64) {
+        sat_drain<BLOCK>(w, cen, rq, cap, cfg0, survw, queue, head, 64, wbase, lane);
+        head += 64;
+      }
+      return;
+    }
+    // more than the queue holds: entry by entry, draining as it fills
     uint32_t any_kb = kb;  // entries some lane of the wave kept
 #pragma unroll
     for (int sh = 1; sh < 64; sh <<= 1) any_kb |= (uint32_t)__shfl_xor((int)any_kb, sh);
@@ -1010,13 +1041,12 @@ __global__ __launch_bounds__(BLOCK) void cull_kernel(DevWorld w, const double* _
     while (any_kb) {
       const int i = __builtin_ctz(any_kb);
       any_kb &= any_kb - 1u;
-      const int p = w.sched_pair[eb + i];
       const bool keep = (kb >> i) & 1u;
       const unsigned long long bal = __ballot(keep);
       if (keep) {
         const uint32_t rank =
             __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
-        queue[(tail + rank) & (kQueue - 1)] = ((uint32_t)p << 6) | lane;
+        queue[(tail + rank) & (kQueue - 1)] = ((uint32_t)(eb + i) << 6) | lane;
       }
       tail += (uint32_t)__popcll(bal);
       if (tail - head >= 64) {
@@ -1128,16 +1158,6 @@ __global__ __launch_bounds__(BLOCK) void cull_kernel(DevWorld w, const double* _
 // (no global atomics): count per (pair, 64-config tile) -> per-pair scan ->
 // scatter.  Candidates of a pair end up contiguous and sorted by config.
 // ---------------------------------------------------------------------------
-// inclusive scan of one value per lane across the wave
-__device__ __forceinline__ uint32_t wave_inclusive_scan(uint32_t v, uint32_t lane) {
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const uint32_t u = __shfl_up(v, off);
-    if (lane >= (uint32_t)off) v += u;
-  }
-  return v;
-}
-
 // one block per pair: exclusive scan of its tile counts (in place) + total.
 // Each thread holds up to 16 consecutive counts in registers (loads issued
 // together), one wave scan + one LDS exchange of the 16 wave totals.
@@ -2921,6 +2941,360 @@ __device__ double gjk_distance(const DevWorld& w, cptr<double> HV, const GObj& A
                            [&](const CV3& d) { return msupport(w, HV, A, B, d); });
 }
 
+// ---------------------------------------------------------------------------
+// Nearest points and signed distance (DistanceRequest enable_signed_distance;
+// FCL 0.7.0 ShapeDistanceTraversalNode::leafTesting -> GJKSolver_libccd
+// shapeDistance / shapeSignedDistance [ext]): gjk_query runs gjk_distance's
+// iteration with each simplex vertex's two supports and barycentric weights
+// (extractClosestPoints: world-frame points on each shape); for intersecting
+// shapes in signed mode, EPA from GJK's enclosing tetrahedron (blow_up first
+// when the origin lies on a lower simplex), depth = distance from the origin
+// to the nearest polytope face, points from its barycentric weights
+// (penEPAPosClosest).  Operation for operation the oracle's gjk_query /
+// blow_up / epa_depth (oracle/collide_oracle.c), same capacities.
+// ---------------------------------------------------------------------------
+struct GSV {
+  V3 w, a, b;
+};
+
+template <bool UNI = true>
+__device__ __forceinline__ GSV msupport_pts(const DevWorld& w, cptr<double> HV, const GObj& A, const GObj& B,
+                                            const V3& d) {
+  const CV3 dir = cv3(d.x, d.y, d.z);
+  // the same operations as msupport: v = (R_a la + p_a) - (R_b lb + p_b) in ccd_real
+  const CV3 da = quat_rot(dir, A.rot_inv), db = quat_rot(vscale(dir, ccd_real(-1)), B.rot_inv);
+  const int ga = UNI ? __builtin_amdgcn_readfirstlane(A.geom) : A.geom, ta = UNI ? __builtin_amdgcn_readfirstlane(A.type) : A.type;
+  const int gb = UNI ? __builtin_amdgcn_readfirstlane(B.geom) : B.geom, tb = UNI ? __builtin_amdgcn_readfirstlane(B.type) : B.type;
+  const CV3 la = support_local(w, HV, ga, ta, da), lb = support_local(w, HV, gb, tb, db);
+  const CV3 va = vadd(quat_rot(la, A.rot), A.pos), vb = vadd(quat_rot(lb, B.rot), B.pos);
+  GSV g;
+  g.w = to_v3(vsub(va, vb));
+  g.a = to_v3(va);
+  g.b = to_v3(vb);
+  return g;
+}
+
+__device__ __forceinline__ void tri_lambda(const V3& a, const V3& b, const V3& c, double lam[3]) {
+  const V3 ab = vsub(b, a), ac = vsub(c, a);
+  lam[0] = lam[1] = lam[2] = 0.0;
+  const double d1 = -d3dot(ab, a), d2 = -d3dot(ac, a);
+  if (d1 <= 0 && d2 <= 0) {
+    lam[0] = 1.0;
+    return;
+  }
+  const double d3 = -d3dot(ab, b), d4 = -d3dot(ac, b);
+  if (d3 >= 0 && d4 <= d3) {
+    lam[1] = 1.0;
+    return;
+  }
+  const double vc = d1 * d4 - d3 * d2;
+  if (vc <= 0 && d1 >= 0 && d3 <= 0) {
+    const double t = d1 / (d1 - d3);
+    lam[0] = 1.0 - t;
+    lam[1] = t;
+    return;
+  }
+  const double d5 = -d3dot(ab, c), d6 = -d3dot(ac, c);
+  if (d6 >= 0 && d5 <= d6) {
+    lam[2] = 1.0;
+    return;
+  }
+  const double vb = d5 * d2 - d1 * d6;
+  if (vb <= 0 && d2 >= 0 && d6 <= 0) {
+    const double t = d2 / (d2 - d6);
+    lam[0] = 1.0 - t;
+    lam[2] = t;
+    return;
+  }
+  const double va = d3 * d6 - d5 * d4;
+  if (va <= 0 && (d4 - d3) >= 0 && (d5 - d6) >= 0) {
+    const double t = (d4 - d3) / ((d4 - d3) + (d5 - d6));
+    lam[1] = 1.0 - t;
+    lam[2] = t;
+    return;
+  }
+  const double den = 1.0 / (va + vb + vc), t1 = vb * den, t2 = vc * den;
+  lam[0] = 1.0 - t1 - t2;
+  lam[1] = t1;
+  lam[2] = t2;
+}
+
+// simplex_closest with the supports and the kept vertices' weights
+__device__ __forceinline__ bool simplex_closest_s(GSV S[4], int& n, V3& v, double lam[4]) {
+  if (n == 1) {
+    v = S[0].w;
+    lam[0] = 1.0;
+    return false;
+  }
+  if (n == 2) {
+    const V3 ab = vsub(S[1].w, S[0].w);
+    const double den = d3dot(ab, ab), t = den > 0 ? -d3dot(S[0].w, ab) / den : 0.0;
+    if (t <= 0) {
+      v = S[0].w;
+      n = 1;
+      lam[0] = 1.0;
+    } else if (t >= 1) {
+      v = S[1].w;
+      S[0] = S[1];
+      n = 1;
+      lam[0] = 1.0;
+    } else {
+      v = V3{S[0].w.x + t * ab.x, S[0].w.y + t * ab.y, S[0].w.z + t * ab.z};
+      lam[0] = 1.0 - t;
+      lam[1] = t;
+    }
+    return false;
+  }
+  if (n == 3) {
+    bool keep[3];
+    double l3[3];
+    v = tri_closest(S[0].w, S[1].w, S[2].w, keep);
+    tri_lambda(S[0].w, S[1].w, S[2].w, l3);
+    int m = 0;
+    for (int k = 0; k < 3; ++k)
+      if (keep[k]) {
+        S[m] = S[k];
+        lam[m] = l3[k];
+        ++m;
+      }
+    n = m;
+    return false;
+  }
+  const int F[4][4] = {{0, 1, 2, 3}, {0, 2, 3, 1}, {0, 3, 1, 2}, {1, 3, 2, 0}};
+  double best = DBL_MAX, bl[3] = {0, 0, 0};
+  V3 bv{0, 0, 0};
+  GSV BP[3];
+  int bn = 0;
+  bool any = false;
+  for (int f = 0; f < 4; ++f) {
+    const V3 a = S[F[f][0]].w, b = S[F[f][1]].w, c = S[F[f][2]].w, d = S[F[f][3]].w;
+    const V3 nrm = vcross(vsub(b, a), vsub(c, a));
+    const double sp = -d3dot(a, nrm), sd = d3dot(vsub(d, a), nrm);
+    if (!(sp * sd < 0 || sd == 0.0)) continue;
+    any = true;
+    bool keep[3];
+    double l3[3];
+    const V3 fv = tri_closest(a, b, c, keep);
+    const double dd = d3dot(fv, fv);
+    if (dd < best) {
+      tri_lambda(a, b, c, l3);
+      best = dd;
+      bv = fv;
+      bn = 0;
+      for (int k = 0; k < 3; ++k)
+        if (keep[k]) {
+          BP[bn] = S[F[f][k]];
+          bl[bn] = l3[k];
+          ++bn;
+        }
+    }
+  }
+  if (!any) return true;
+  for (int k = 0; k < bn; ++k) {
+    S[k] = BP[k];
+    lam[k] = bl[k];
+  }
+  n = bn;
+  v = bv;
+  return false;
+}
+
+constexpr int kEpaMaxV = 64, kEpaMaxF = 128;
+struct EpaFace {
+  int v[3];
+  V3 n;
+  double d;
+  int alive;
+};
+
+__device__ __forceinline__ bool epa_face_set(const GSV* V, int i, int j, int k, EpaFace& f) {
+  const V3 n = vcross(vsub(V[j].w, V[i].w), vsub(V[k].w, V[i].w));
+  const double l = std::sqrt(d3dot(n, n));
+  if (!(l > 0.0)) return false;
+  f.n = V3{n.x / l, n.y / l, n.z / l};
+  f.v[0] = i;
+  f.v[1] = j;
+  f.v[2] = k;
+  f.d = d3dot(f.n, V[i].w);
+  f.alive = 1;
+  return true;
+}
+
+__device__ __forceinline__ double epa_finish(const GSV* V, const EpaFace& f, V3& p1, V3& p2) {
+  const V3 a = V[f.v[0]].w, b = V[f.v[1]].w, c = V[f.v[2]].w;
+  const V3 pw{f.d * f.n.x, f.d * f.n.y, f.d * f.n.z};
+  const V3 v0 = vsub(b, a), v1 = vsub(c, a), v2 = vsub(pw, a);
+  const double d00 = d3dot(v0, v0), d01 = d3dot(v0, v1), d11 = d3dot(v1, v1), d20 = d3dot(v2, v0), d21 = d3dot(v2, v1);
+  const double den = d00 * d11 - d01 * d01;
+  const double lb = den != 0.0 ? (d11 * d20 - d01 * d21) / den : 0.0, lc = den != 0.0 ? (d00 * d21 - d01 * d20) / den : 0.0;
+  const double la = 1.0 - lb - lc;
+  const GSV &A = V[f.v[0]], &B = V[f.v[1]], &C = V[f.v[2]];
+  p1 = V3{(la * A.a.x + lb * B.a.x) + lc * C.a.x, (la * A.a.y + lb * B.a.y) + lc * C.a.y, (la * A.a.z + lb * B.a.z) + lc * C.a.z};
+  p2 = V3{(la * A.b.x + lb * B.b.x) + lc * C.b.x, (la * A.b.y + lb * B.b.y) + lc * C.b.y, (la * A.b.z + lb * B.b.z) + lc * C.b.z};
+  return f.d;
+}
+
+template <typename SupFn>
+__device__ double epa_depth(SupFn sup, const GSV S[4], V3& p1, V3& p2) {
+  GSV V[kEpaMaxV];
+  EpaFace F[kEpaMaxF];
+  int nv = 4, nf = 0;
+  for (int k = 0; k < 4; ++k) V[k] = S[k];
+  const int T[4][4] = {{0, 1, 2, 3}, {0, 3, 1, 2}, {0, 2, 3, 1}, {1, 3, 2, 0}};
+  for (int t = 0; t < 4; ++t) {
+    int i = T[t][0], j = T[t][1], k = T[t][2];
+    const int l = T[t][3];
+    const V3 n = vcross(vsub(V[j].w, V[i].w), vsub(V[k].w, V[i].w));
+    if (d3dot(n, vsub(V[l].w, V[i].w)) > 0.0) {
+      const int x = j;
+      j = k;
+      k = x;
+    }
+    if (!epa_face_set(V, i, j, k, F[nf])) return -1.0;
+    ++nf;
+  }
+  EpaFace fb;
+  for (int it = 0; it < 128; ++it) {
+    int best = -1;
+    for (int f = 0; f < nf; ++f)
+      if (F[f].alive && (best < 0 || F[f].d < F[best].d)) best = f;
+    if (best < 0) return -1.0;
+    fb = F[best];
+    const GSV s = sup(fb.n);
+    if (d3dot(s.w, fb.n) - fb.d <= 1e-10 || nv >= kEpaMaxV) break;
+    bool dup = false;
+    for (int k = 0; k < nv; ++k) dup |= (V[k].w.x == s.w.x && V[k].w.y == s.w.y && V[k].w.z == s.w.z);
+    if (dup) break;
+    const int si = nv;
+    V[nv++] = s;
+    int edges[kEpaMaxF][2], ne = 0;
+    for (int f = 0; f < nf; ++f) {
+      if (!F[f].alive) continue;
+      if (d3dot(F[f].n, vsub(s.w, V[F[f].v[0]].w)) <= 0.0) continue;
+      F[f].alive = 0;
+      for (int e = 0; e < 3; ++e) {
+        const int a = F[f].v[e], b = F[f].v[(e + 1) % 3];
+        int found = -1;
+        for (int x = 0; x < ne; ++x)
+          if (edges[x][0] == b && edges[x][1] == a) {
+            found = x;
+            break;
+          }
+        if (found >= 0) {
+          edges[found][0] = edges[ne - 1][0];
+          edges[found][1] = edges[ne - 1][1];
+          --ne;
+        } else if (ne < kEpaMaxF) {
+          edges[ne][0] = a;
+          edges[ne][1] = b;
+          ++ne;
+        } else {
+          return epa_finish(V, fb, p1, p2);
+        }
+      }
+    }
+    int slot = 0;
+    bool full = false;
+    for (int x = 0; x < ne && !full; ++x) {
+      while (slot < nf && F[slot].alive) ++slot;
+      if (slot == nf) {
+        if (nf == kEpaMaxF) {
+          full = true;
+          break;
+        }
+        ++nf;
+      }
+      if (!epa_face_set(V, edges[x][0], edges[x][1], si, F[slot])) F[slot].alive = 0;
+    }
+    if (full) return epa_finish(V, fb, p1, p2);
+  }
+  return epa_finish(V, fb, p1, p2);
+}
+
+template <typename SupFn>
+__device__ bool blow_up(SupFn sup, GSV S[4], int n) {
+  const double ax[6][3] = {{1, 0, 0}, {-1, 0, 0}, {0, 1, 0}, {0, -1, 0}, {0, 0, 1}, {0, 0, -1}};
+  if (n == 4) n = 3;
+  while (n < 3) {
+    bool grown = false;
+    for (int k = 0; k < 6 && !grown; ++k) {
+      const GSV s = sup(V3{ax[k][0], ax[k][1], ax[k][2]});
+      const V3 e = vsub(s.w, S[0].w);
+      if (n == 1) {
+        if (d3dot(e, e) > 1e-20) {
+          S[n++] = s;
+          grown = true;
+        }
+        continue;
+      }
+      const V3 u = vsub(S[1].w, S[0].w);
+      const V3 c = vcross(u, e);
+      if (d3dot(c, c) > 1e-20 * d3dot(u, u)) {
+        S[n++] = s;
+        grown = true;
+      }
+    }
+    if (!grown) return false;
+  }
+  V3 nr = vcross(vsub(S[1].w, S[0].w), vsub(S[2].w, S[0].w));
+  const double l = std::sqrt(d3dot(nr, nr));
+  if (!(l > 0.0)) return false;
+  nr = V3{nr.x / l, nr.y / l, nr.z / l};
+  const GSV sp = sup(nr), sm = sup(V3{-nr.x, -nr.y, -nr.z});
+  const double hp = d3dot(vsub(sp.w, S[0].w), nr), hm = -d3dot(vsub(sm.w, S[0].w), nr);
+  if (!(hp > 1e-12 || hm > 1e-12)) return false;
+  S[3] = hp >= hm ? sp : sm;
+  return true;
+}
+
+// gjk_distance with the nearest points; SIGNED: -EPA depth for intersecting
+// shapes (0 if they only touch).  Unsigned and intersecting: -1, zero points.
+template <bool SIGNED, typename SupFn>
+__device__ double gjk_query(V3 v, SupFn sup, V3& p1, V3& p2) {
+  if (d3dot(v, v) == 0.0) v.x = 1e-12;
+  GSV S[4];
+  double lam[4] = {0, 0, 0, 0};
+  int n = 0;
+  p1 = V3{0, 0, 0};
+  p2 = V3{0, 0, 0};
+  auto points = [&]() {
+    V3 a{0, 0, 0}, b{0, 0, 0};
+    for (int k = 0; k < n; ++k) {
+      a = V3{a.x + lam[k] * S[k].a.x, a.y + lam[k] * S[k].a.y, a.z + lam[k] * S[k].a.z};
+      b = V3{b.x + lam[k] * S[k].b.x, b.y + lam[k] * S[k].b.y, b.z + lam[k] * S[k].b.z};
+    }
+    p1 = a;
+    p2 = b;
+  };
+  for (int it = 0; it < 128; ++it) {
+    const GSV s = sup(V3{-v.x, -v.y, -v.z});
+    const double vv = d3dot(v, v), vw = d3dot(v, s.w);
+    if (n > 0 && vv - vw <= 1e-12 * vv) break;
+    bool dup = false;
+    for (int k = 0; k < n; ++k) dup |= (S[k].w.x == s.w.x && S[k].w.y == s.w.y && S[k].w.z == s.w.z);
+    if (dup) break;
+    S[n++] = s;
+    if (simplex_closest_s(S, n, v, lam)) {
+      if constexpr (!SIGNED) return -1.0;
+      const double dep = epa_depth(sup, S, p1, p2);
+      return dep >= 0.0 ? -dep : 0.0;
+    }
+    const double nv = d3dot(v, v);
+    if (nv <= 1e-24) {
+      if constexpr (!SIGNED) return -1.0;
+      if (blow_up(sup, S, n)) {
+        const double dep = epa_depth(sup, S, p1, p2);
+        if (dep >= 0.0) return -dep;
+      }
+      points();
+      return 0.0;
+    }
+    if (n > 1 && nv >= vv) break;
+  }
+  points();
+  return std::sqrt(d3dot(v, v));
+}
+
 // fcl::distance(shape, OcTree) [ext FCL 0.7.0 OcTreeShapeDistanceRecurse]:
 // the minimum over the occupied leaves of shapeDistance(leaf box, shape) with
 // the box first (constructBox: box_tf = tf * Translation(centre), boxToGJK);
@@ -3337,16 +3711,25 @@ __device__ double mesh_octree_distance_lane(const DevWorld& w, int gm, const SE3
   return best;
 }
 
+// MODE 0: distances only; MPG_DIST_POINTS: also the nearest points of each
+// group's minimum pair (pts [n][6]); | MPG_DIST_SIGNED: signed distances
+// (the host refuses signed requests on worlds with point-cloud / BVH-mesh pairs)
+constexpr int MPG_DIST_POINTS = 1, MPG_DIST_SIGNED = 2;
+template <int MODE>
 __global__ __launch_bounds__(128) void distance_kernel(DevWorld w, const double* __restrict__ poses, long long n,
                                                        int n_self, double* __restrict__ d_self,
                                                        int32_t* __restrict__ p_self, double* __restrict__ d_others,
-                                                       int32_t* __restrict__ p_others) {
+                                                       int32_t* __restrict__ p_others, double* __restrict__ pts_self,
+                                                       double* __restrict__ pts_others) {
+  constexpr bool SIGNED = (MODE & MPG_DIST_SIGNED) != 0;
+  constexpr bool PTS = MODE != 0;
   const long long cfg0 = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const bool live = cfg0 < n;
   const long long cfg = live ? cfg0 : n - 1;
   const cptr<double> HV = w.hull;
   double best[2] = {DBL_MAX, DBL_MAX};
   int bp[2] = {-1, -1};
+  V3 bpt[2][2] = {{{0, 0, 0}, {0, 0, 0}}, {{0, 0, 0}, {0, 0, 0}}};
   for (int p = 0; p < w.n_pairs; ++p) {
     if (w.pair_allowed[p]) continue;  // ACM before distance (planning_world.cpp:509-510)
     const int g = p < n_self ? 0 : 1;
@@ -3367,6 +3750,7 @@ __global__ __launch_bounds__(128) void distance_kernel(DevWorld w, const double*
       if (d < best[g]) {
         best[g] = d;
         bp[g] = p;
+        if constexpr (PTS) bpt[g][0] = bpt[g][1] = V3{0, 0, 0};
       }
       continue;
     }
@@ -3379,17 +3763,31 @@ __global__ __launch_bounds__(128) void distance_kernel(DevWorld w, const double*
       if (d < best[g]) {
         best[g] = d;
         bp[g] = p;
+        if constexpr (PTS) bpt[g][0] = bpt[g][1] = V3{0, 0, 0};
       }
       continue;
     }
     const V3 dc = vsub(cb, ca);
-    // bounding spheres: the pair cannot beat the running minimum
+    // bounding spheres: the pair cannot beat the running minimum (signed too:
+    // a penetration is never deeper than the bounding spheres' overlap)
     const double lb = std::sqrt(d3dot(dc, dc)) - ra - rb - 1e-9;
-    if (!live || best[g] == -1.0 || lb >= best[g]) continue;
-    const double d = gjk_distance(w, HV, A, B);
-    if (d < best[g]) {
-      best[g] = d;
-      bp[g] = p;
+    if (!live || (!SIGNED && best[g] == -1.0) || lb >= best[g]) continue;
+    if constexpr (PTS) {
+      V3 q1, q2;
+      const double d = gjk_query<SIGNED>(vsub(to_v3(center(w, A)), to_v3(center(w, B))),
+                                         [&](const V3& dir) { return msupport_pts(w, HV, A, B, dir); }, q1, q2);
+      if (d < best[g]) {
+        best[g] = d;
+        bp[g] = p;
+        bpt[g][0] = q1;
+        bpt[g][1] = q2;
+      }
+    } else {
+      const double d = gjk_distance(w, HV, A, B);
+      if (d < best[g]) {
+        best[g] = d;
+        bp[g] = p;
+      }
     }
   }
   if (!live) return;
@@ -3397,6 +3795,17 @@ __global__ __launch_bounds__(128) void distance_kernel(DevWorld w, const double*
   p_self[cfg] = bp[0];
   d_others[cfg] = best[1];
   p_others[cfg] = bp[1];
+  if constexpr (PTS) {
+    for (int g = 0; g < 2; ++g) {
+      double* o = (g ? pts_others : pts_self) + 6 * cfg;
+      o[0] = bpt[g][0].x;
+      o[1] = bpt[g][0].y;
+      o[2] = bpt[g][0].z;
+      o[3] = bpt[g][1].x;
+      o[4] = bpt[g][1].y;
+      o[5] = bpt[g][1].z;
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -4996,6 +5405,8 @@ struct mpg_world {
     size_t q_cap = 0;
     char* out = nullptr;
     size_t out_cap = 0;
+    double* pts = nullptr;  // device-buffer calls: points nobody asked for
+    size_t pts_cap = 0;
   } dist;
   std::mutex dist_mu;
   std::mutex prof_mu;
@@ -6269,6 +6680,7 @@ int mpg_world_destroy(mpg_world* w) {
   hipFree(w->dist.save64);
   hipFree(w->dist.q);
   hipFree(w->dist.out);
+  hipFree(w->dist.pts);
   hipFree(w->motion.edges);
   hipFree(w->motion.segs);
   hipFree(w->motion.offs);
@@ -6569,12 +6981,25 @@ int mpg_check_motion_batch(mpg_world* w, const double* q_from, const double* q_t
 
 int mpg_distance_batch(mpg_world* w, const double* q, int64_t n, int32_t n_self_pairs, double* d_self,
                        int32_t* p_self, double* d_others, int32_t* p_others, int mem, void* stream) {
+  return mpg_distance_batch_ex(w, q, n, n_self_pairs, 0, d_self, p_self, nullptr, d_others, p_others, nullptr, mem,
+                               stream);
+}
+
+int mpg_distance_batch_ex(mpg_world* w, const double* q, int64_t n, int32_t n_self_pairs, int32_t flags,
+                          double* d_self, int32_t* p_self, double* pts_self, double* d_others, int32_t* p_others,
+                          double* pts_others, int mem, void* stream) {
   if (!w) return set_error(MPG_E_INVALID, "world is NULL");
   if (n < 0) return set_error(MPG_E_INVALID, "n < 0");
   if (n_self_pairs < 0 || n_self_pairs > w->dw.n_pairs) return set_error(MPG_E_INVALID, "bad n_self_pairs");
   if (n > 0 && ((!q && w->dw.dof > 0) || !d_self || !p_self || !d_others || !p_others))
     return set_error(MPG_E_INVALID, "NULL buffer");
   if (mem != MPG_MEM_HOST && mem != MPG_MEM_DEVICE) return set_error(MPG_E_INVALID, "bad mem kind");
+  if (flags & ~(MPG_DISTANCE_SIGNED | MPG_DISTANCE_NEAREST_POINTS)) return set_error(MPG_E_INVALID, "bad flags");
+  if (flags && (w->has_mesh || w->has_octree))
+    return set_error(MPG_E_UNSUPPORTED,
+                     "signed distance / requested nearest points of point-cloud or BVH-mesh pairs are not implemented");
+  const bool want_pts = pts_self || pts_others;
+  const int mode = (want_pts || flags ? MPG_DIST_POINTS : 0) | (flags & MPG_DISTANCE_SIGNED ? MPG_DIST_SIGNED : 0);
   if (n == 0) return MPG_OK;
   HIP_TRY(hipSetDevice(w->device));
   hipStream_t s = static_cast<hipStream_t>(stream);
@@ -6593,29 +7018,43 @@ int mpg_distance_batch(mpg_world* w, const double* q, int64_t n, int32_t n_self_
   if ((rc = grow((void**)&D.poses, D.poses_cap, sizeof(double) * kPoseStride * nm * n))) return rc;
   if ((rc = grow((void**)&D.save64, D.save_cap, sizeof(double) * 12 * ns * n))) return rc;
   const double* qin = q;
-  double *ds = d_self, *dd = d_others;
+  double *ds = d_self, *dd = d_others, *qs = pts_self, *qo = pts_others;
   int32_t *ps = p_self, *po = p_others;
+  const size_t out_bytes = (2 * sizeof(double) + 2 * sizeof(int32_t) + (mode ? 12 * sizeof(double) : 0)) * n;
   if (mem == MPG_MEM_HOST) {
     if ((rc = grow((void**)&D.q, D.q_cap, sizeof(double) * std::max(w->dw.dof, 1) * n))) return rc;
-    if ((rc = grow((void**)&D.out, D.out_cap, (2 * sizeof(double) + 2 * sizeof(int32_t)) * n))) return rc;
+    if ((rc = grow((void**)&D.out, D.out_cap, out_bytes))) return rc;
     if (w->dw.dof) HIP_TRY(hipMemcpyAsync(D.q, q, sizeof(double) * w->dw.dof * n, hipMemcpyHostToDevice, s));
     qin = D.q;
     ds = reinterpret_cast<double*>(D.out);
     dd = ds + n;
-    ps = reinterpret_cast<int32_t*>(dd + n);
+    qs = dd + n;
+    qo = qs + (mode ? 6 * n : 0);
+    ps = reinterpret_cast<int32_t*>(qo + (mode ? 6 * n : 0));
     po = ps + n;
+  } else if (mode && (!qs || !qo)) {  // device buffers: scratch for the points nobody asked for
+    if ((rc = grow((void**)&D.pts, D.pts_cap, 12 * sizeof(double) * n))) return rc;
+    if (!qs) qs = D.pts;
+    if (!qo) qo = D.pts + 6 * n;
   }
   const unsigned grid = (unsigned)((n + 127) / 128);
   hipLaunchKernelGGL((pose_kernel<false>), dim3(grid), dim3(128), 0, s, w->dw, qin, (long long)n, D.poses, D.save64);
   HIP_TRY(hipGetLastError());
-  hipLaunchKernelGGL(distance_kernel, dim3(grid), dim3(128), 0, s, w->dw, D.poses, (long long)n, n_self_pairs, ds, ps,
-                     dd, po);
-  HIP_TRY(hipGetLastError());
+  auto launch = [&](auto kern) {
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(128), 0, s, w->dw, D.poses, (long long)n, n_self_pairs, ds, ps, dd, po,
+                       qs, qo);
+    return hipGetLastError();
+  };
+  if (mode == 0) HIP_TRY(launch(distance_kernel<0>));
+  else if (mode == MPG_DIST_POINTS) HIP_TRY(launch(distance_kernel<MPG_DIST_POINTS>));
+  else HIP_TRY(launch(distance_kernel<MPG_DIST_POINTS | MPG_DIST_SIGNED>));
   if (mem == MPG_MEM_HOST) {
     HIP_TRY(hipMemcpyAsync(d_self, ds, sizeof(double) * n, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipMemcpyAsync(d_others, dd, sizeof(double) * n, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipMemcpyAsync(p_self, ps, sizeof(int32_t) * n, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipMemcpyAsync(p_others, po, sizeof(int32_t) * n, hipMemcpyDeviceToHost, s));
+    if (mode && pts_self) HIP_TRY(hipMemcpyAsync(pts_self, qs, sizeof(double) * 6 * n, hipMemcpyDeviceToHost, s));
+    if (mode && pts_others) HIP_TRY(hipMemcpyAsync(pts_others, qo, sizeof(double) * 6 * n, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
   }
   return MPG_OK;

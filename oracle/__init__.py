@@ -51,6 +51,8 @@ def lib():
         _lib.orc_collide_pair.restype = ctypes.c_int
         _lib.orc_distance_pair.restype = ctypes.c_double
         _lib.orc_distance_batch.restype = ctypes.c_int
+        _lib.orc_distance_batch_ex.restype = ctypes.c_int
+        _lib.orc_distance_pair_ex.restype = ctypes.c_double
         _lib.orc_contact_pair.restype = ctypes.c_int
         _lib.orc_contact_batch.restype = ctypes.c_int
         _lib.orc_tri_tri.restype = ctypes.c_int
@@ -413,6 +415,28 @@ class OracleWorld:
         if rc != 0:
             raise RuntimeError("orc_distance_batch failed")
         return ds, ps, do, po
+
+    def distance_batch_ex(self, q: np.ndarray, signed: bool = False, nearest_points: bool = False):
+        """distance_batch with DistanceRequest(enable_signed_distance,
+        enable_nearest_points): (d_self, pair_self, pts_self[n, 6], d_others,
+        pair_others, pts_others[n, 6]); pts = (p1, p2) of the group's minimum
+        pair, world frame.  Point-cloud / BVH-mesh pairs with either option:
+        NotImplementedError (the device refuses them the same way)."""
+        q = np.ascontiguousarray(q, dtype=np.float64).reshape(-1, self.dof)
+        n = q.shape[0]
+        ds, do = np.zeros(n), np.zeros(n)
+        ps, po = np.zeros(n, np.int32), np.zeros(n, np.int32)
+        qs, qo = np.zeros((n, 6)), np.zeros((n, 6))
+        mode = (1 if signed else 0) | (2 if nearest_points else 0)
+        rc = lib().orc_distance_batch_ex(ctypes.byref(self._w), q.ctypes.data_as(_DP), ctypes.c_long(n),
+                                         ctypes.c_int(self.n_self_pairs), ctypes.c_int(mode),
+                                         ds.ctypes.data_as(_DP), ps.ctypes.data_as(_IP), qs.ctypes.data_as(_DP),
+                                         do.ctypes.data_as(_DP), po.ctypes.data_as(_IP), qo.ctypes.data_as(_DP))
+        if rc == -2:
+            raise NotImplementedError("signed distance / nearest points of point-cloud or BVH-mesh pairs")
+        if rc != 0:
+            raise RuntimeError("orc_distance_batch_ex failed")
+        return ds, ps, qs, do, po, qo
 
     def contact_batch(self, q: np.ndarray):
         """fcl::collide with CollisionRequest(enable_contact=True) on every pair:

@@ -39,6 +39,7 @@
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
+#include <stdio.h>
 
 typedef double real; /* Eigen / pinocchio / FCL scalar (S = double) */
 
@@ -1689,6 +1690,298 @@ static double gjk_distance(const gjk_obj *o1, const gjk_obj *o2) {
     return sqrt(d3dot(v, v));
 }
 
+/* ------------------------------------------- nearest points, signed distance
+ * FCL 0.7.0's distance leaf (ShapeDistanceTraversalNode::leafTesting [ext])
+ * asks GJKSolver_libccd for the distance AND the closest points of the two
+ * shapes, in the world frame (libccd_extension ccdGJKDist2 ->
+ * extractClosestPoints: the barycentric weights of the origin's projection on
+ * the final simplex applied to the supports of each shape), and with
+ * DistanceRequest(enable_signed_distance=True) runs ccdGJKSignedDist: GJK, and
+ * for intersecting shapes EPA, depth = -(distance from the origin to the
+ * Minkowski difference boundary), points from penEPAPosClosest (the same
+ * barycentric reconstruction on the nearest polytope face).
+ * Restated here on the same float supports as gjk_distance: gjk_query runs
+ * gjk_distance's iteration with identical arithmetic for v (so its distance is
+ * gjk_distance's, bit for bit) and carries each simplex vertex's two supports
+ * and barycentric weights; epa_depth is a textbook EPA in fp64 from GJK's
+ * enclosing tetrahedron, run to 1e-10 m (FCL's float EPA stops at libccd's
+ * epa_tolerance 1e-4: the depths agree within that).  Device twin:
+ * mplib_amd/csrc/mpg_kernels.hip gjk_query / epa_depth. */
+typedef struct { double w[3], a[3], b[3]; } gsv;
+
+static void tri_closest_l(const double *a, const double *b, const double *c, double *v, int keep[3], double lam[3]) {
+    tri_closest(a, b, c, v, keep);
+    /* the weights of the feature tri_closest reached (same case analysis) */
+    double ab[3], ac[3];
+    d3sub(ab, b, a); d3sub(ac, c, a);
+    lam[0] = lam[1] = lam[2] = 0.0;
+    const double d1 = -d3dot(ab, a), d2 = -d3dot(ac, a);
+    if (d1 <= 0 && d2 <= 0) { lam[0] = 1.0; return; }
+    const double d3 = -d3dot(ab, b), d4 = -d3dot(ac, b);
+    if (d3 >= 0 && d4 <= d3) { lam[1] = 1.0; return; }
+    const double vc = d1 * d4 - d3 * d2;
+    if (vc <= 0 && d1 >= 0 && d3 <= 0) { const double t = d1 / (d1 - d3); lam[0] = 1.0 - t; lam[1] = t; return; }
+    const double d5 = -d3dot(ab, c), d6 = -d3dot(ac, c);
+    if (d6 >= 0 && d5 <= d6) { lam[2] = 1.0; return; }
+    const double vb = d5 * d2 - d1 * d6;
+    if (vb <= 0 && d2 >= 0 && d6 <= 0) { const double t = d2 / (d2 - d6); lam[0] = 1.0 - t; lam[2] = t; return; }
+    const double va = d3 * d6 - d5 * d4;
+    if (va <= 0 && (d4 - d3) >= 0 && (d5 - d6) >= 0) {
+        const double t = (d4 - d3) / ((d4 - d3) + (d5 - d6));
+        lam[1] = 1.0 - t; lam[2] = t; return;
+    }
+    const double den = 1.0 / (va + vb + vc), t1 = vb * den, t2 = vc * den;
+    lam[0] = 1.0 - t1 - t2; lam[1] = t1; lam[2] = t2;
+}
+
+/* simplex_closest with the supports carried along; lam: weights of the kept vertices */
+static int simplex_closest_s(gsv S[4], int *n, double *v, double lam[4]) {
+    if (*n == 1) { memcpy(v, S[0].w, 24); lam[0] = 1.0; return 0; }
+    if (*n == 2) {
+        double ab[3];
+        d3sub(ab, S[1].w, S[0].w);
+        const double den = d3dot(ab, ab), t = den > 0 ? -d3dot(S[0].w, ab) / den : 0.0;
+        if (t <= 0) { memcpy(v, S[0].w, 24); *n = 1; lam[0] = 1.0; return 0; }
+        if (t >= 1) { memcpy(v, S[1].w, 24); S[0] = S[1]; *n = 1; lam[0] = 1.0; return 0; }
+        for (int i = 0; i < 3; ++i) v[i] = S[0].w[i] + t * ab[i];
+        lam[0] = 1.0 - t; lam[1] = t;
+        return 0;
+    }
+    if (*n == 3) {
+        int keep[3];
+        double l3[3];
+        tri_closest_l(S[0].w, S[1].w, S[2].w, v, keep, l3);
+        int m = 0;
+        for (int k = 0; k < 3; ++k) if (keep[k]) { if (m != k) S[m] = S[k]; lam[m] = l3[k]; ++m; }
+        *n = m;
+        return 0;
+    }
+    static const int F[4][4] = {{0, 1, 2, 3}, {0, 2, 3, 1}, {0, 3, 1, 2}, {1, 3, 2, 0}};
+    double best = DBL_MAX, bv[3] = {0, 0, 0}, bl[3] = {0, 0, 0};
+    gsv BP[3];
+    int bn = -1, any = 0;
+    for (int f = 0; f < 4; ++f) {
+        const double *a = S[F[f][0]].w, *b = S[F[f][1]].w, *c = S[F[f][2]].w, *d = S[F[f][3]].w;
+        double ab[3], ac[3], nrm[3], ad[3];
+        d3sub(ab, b, a); d3sub(ac, c, a); d3cross(nrm, ab, ac); d3sub(ad, d, a);
+        const double sp = -d3dot(a, nrm), sd = d3dot(ad, nrm);
+        if (!(sp * sd < 0 || sd == 0.0)) continue;
+        any = 1;
+        double fv[3], l3[3];
+        int keep[3];
+        tri_closest_l(a, b, c, fv, keep, l3);
+        const double dd = d3dot(fv, fv);
+        if (dd < best) {
+            best = dd; memcpy(bv, fv, 24); bn = 0;
+            for (int k = 0; k < 3; ++k) if (keep[k]) { BP[bn] = S[F[f][k]]; bl[bn] = l3[k]; ++bn; }
+        }
+    }
+    if (!any) return 1;
+    for (int k = 0; k < bn; ++k) { S[k] = BP[k]; lam[k] = bl[k]; }
+    *n = bn;
+    memcpy(v, bv, 24);
+    return 0;
+}
+
+static void gsv_support(const gjk_obj *o1, const gjk_obj *o2, const double *d, gsv *out) {
+    ccd_vec3_t dir;
+    ccd_support_t sp;
+    ccdVec3Set(&dir, d[0], d[1], d[2]);
+    ccd_support(o1, o2, &dir, &sp);
+    for (int i = 0; i < 3; ++i) { out->w[i] = sp.v.v[i]; out->a[i] = sp.v1.v[i]; out->b[i] = sp.v2.v[i]; }
+}
+
+/* EPA from the enclosing tetrahedron S[0..3]: depth (>= 0) and the witness
+ * points on each shape (world frame). */
+#define EPA_MAXV 64
+#define EPA_MAXF 128
+typedef struct { int v[3]; double n[3], d; int alive; } epa_face;
+
+static int epa_face_set(const gsv *V, int i, int j, int k, epa_face *f) {
+    double e1[3], e2[3], n[3];
+    d3sub(e1, V[j].w, V[i].w); d3sub(e2, V[k].w, V[i].w); d3cross(n, e1, e2);
+    const double l = sqrt(d3dot(n, n));
+    if (!(l > 0.0)) return 0;
+    for (int c = 0; c < 3; ++c) f->n[c] = n[c] / l;
+    f->v[0] = i; f->v[1] = j; f->v[2] = k;
+    f->d = d3dot(f->n, V[i].w);
+    f->alive = 1;
+    return 1;
+}
+
+static double epa_finish(const gsv *V, const epa_face *f, double *p1, double *p2);
+
+static double epa_depth(const gjk_obj *o1, const gjk_obj *o2, const gsv S[4], double *p1, double *p2) {
+    gsv V[EPA_MAXV];
+    epa_face F[EPA_MAXF];
+    int nv = 4, nf = 0;
+    for (int k = 0; k < 4; ++k) V[k] = S[k];
+    static const int T[4][4] = {{0, 1, 2, 3}, {0, 3, 1, 2}, {0, 2, 3, 1}, {1, 3, 2, 0}};
+    for (int t = 0; t < 4; ++t) {
+        int i = T[t][0], j = T[t][1], k = T[t][2];
+        const int l = T[t][3];
+        double e1[3], e2[3], n[3], dl[3];
+        d3sub(e1, V[j].w, V[i].w); d3sub(e2, V[k].w, V[i].w); d3cross(n, e1, e2); d3sub(dl, V[l].w, V[i].w);
+        if (d3dot(n, dl) > 0.0) { const int x = j; j = k; k = x; } /* outward: away from the 4th vertex */
+        if (!epa_face_set(V, i, j, k, &F[nf])) return -1.0;
+        ++nf;
+    }
+    epa_face fb; /* the nearest face of the current polytope */
+    for (int it = 0; it < 128; ++it) {
+        int best = -1;
+        for (int f = 0; f < nf; ++f)
+            if (F[f].alive && (best < 0 || F[f].d < F[best].d)) best = f;
+        if (best < 0) return -1.0;
+        fb = F[best];
+        gsv s;
+        gsv_support(o1, o2, fb.n, &s);
+        if (d3dot(s.w, fb.n) - fb.d <= 1e-10 || nv >= EPA_MAXV) break;
+        int dup = 0;
+        for (int k = 0; k < nv; ++k) dup |= (V[k].w[0] == s.w[0] && V[k].w[1] == s.w[1] && V[k].w[2] == s.w[2]);
+        if (dup) break;
+        const int si = nv;
+        V[nv++] = s;
+        /* faces that see the new vertex go; their unshared edges form the horizon */
+        int edges[EPA_MAXF][2], ne = 0;
+        for (int f = 0; f < nf; ++f) {
+            if (!F[f].alive) continue;
+            double ds[3];
+            d3sub(ds, s.w, V[F[f].v[0]].w);
+            if (d3dot(F[f].n, ds) <= 0.0) continue;
+            F[f].alive = 0;
+            for (int e = 0; e < 3; ++e) {
+                const int a = F[f].v[e], b = F[f].v[(e + 1) % 3];
+                int found = -1;
+                for (int x = 0; x < ne; ++x) if (edges[x][0] == b && edges[x][1] == a) { found = x; break; }
+                if (found >= 0) { edges[found][0] = edges[ne - 1][0]; edges[found][1] = edges[ne - 1][1]; --ne; }
+                else if (ne < EPA_MAXF) { edges[ne][0] = a; edges[ne][1] = b; ++ne; }
+                else return epa_finish(V, &fb, p1, p2); /* horizon beyond capacity: stop here */
+            }
+        }
+        /* new faces take the dead slots first (in index order), then the end */
+        int slot = 0, full = 0;
+        for (int x = 0; x < ne && !full; ++x) {
+            while (slot < nf && F[slot].alive) ++slot;
+            if (slot == nf) {
+                if (nf == EPA_MAXF) { full = 1; break; }
+                ++nf;
+            }
+            if (!epa_face_set(V, edges[x][0], edges[x][1], si, &F[slot])) F[slot].alive = 0;
+        }
+        if (full) return epa_finish(V, &fb, p1, p2);
+    }
+    return epa_finish(V, &fb, p1, p2);
+}
+
+/* the nearest face f: witness = d n, its barycentric weights on the face
+ * applied to each shape's supports */
+static double epa_finish(const gsv *V, const epa_face *f, double *p1, double *p2) {
+    const double *a = V[f->v[0]].w, *b = V[f->v[1]].w, *c = V[f->v[2]].w;
+    double pw[3] = {f->d * f->n[0], f->d * f->n[1], f->d * f->n[2]}, v0[3], v1[3], v2[3];
+    d3sub(v0, b, a); d3sub(v1, c, a); d3sub(v2, pw, a);
+    const double d00 = d3dot(v0, v0), d01 = d3dot(v0, v1), d11 = d3dot(v1, v1), d20 = d3dot(v2, v0), d21 = d3dot(v2, v1);
+    const double den = d00 * d11 - d01 * d01;
+    double lb = den != 0.0 ? (d11 * d20 - d01 * d21) / den : 0.0, lc = den != 0.0 ? (d00 * d21 - d01 * d20) / den : 0.0;
+    const double la = 1.0 - lb - lc;
+    for (int i = 0; i < 3; ++i) {
+        p1[i] = (la * V[f->v[0]].a[i] + lb * V[f->v[1]].a[i]) + lc * V[f->v[2]].a[i];
+        p2[i] = (la * V[f->v[0]].b[i] + lb * V[f->v[1]].b[i]) + lc * V[f->v[2]].b[i];
+    }
+    return f->d;
+}
+
+/* S[0..n) with the origin on it (n < 4, or a flat tetrahedron) -> a
+ * tetrahedron of Minkowski-difference supports that contains the origin:
+ * extra supports along directions off the simplex (libccd's
+ * simplexToPolytope2/3 idea: axes, then the triangle's normal, both sides,
+ * the farther one).  0 if the difference is flat there (shapes touching). */
+static int blow_up(const gjk_obj *o1, const gjk_obj *o2, gsv S[4], int n) {
+    static const double ax[6][3] = {{1, 0, 0}, {-1, 0, 0}, {0, 1, 0}, {0, -1, 0}, {0, 0, 1}, {0, 0, -1}};
+    if (n == 4) n = 3; /* a flat tetrahedron: rebuild from its first triangle */
+    while (n < 3) {
+        int grown = 0;
+        for (int k = 0; k < 6 && !grown; ++k) {
+            gsv s;
+            gsv_support(o1, o2, ax[k], &s);
+            double e[3], u[3], c[3];
+            d3sub(e, s.w, S[0].w);
+            if (n == 1) { if (d3dot(e, e) > 1e-20) { S[n++] = s; grown = 1; } continue; }
+            d3sub(u, S[1].w, S[0].w);
+            d3cross(c, u, e);
+            if (d3dot(c, c) > 1e-20 * d3dot(u, u)) { S[n++] = s; grown = 1; }
+        }
+        if (!grown) return 0;
+    }
+    double e1[3], e2[3], nr[3];
+    d3sub(e1, S[1].w, S[0].w); d3sub(e2, S[2].w, S[0].w); d3cross(nr, e1, e2);
+    const double l = sqrt(d3dot(nr, nr));
+    if (!(l > 0.0)) return 0;
+    for (int i = 0; i < 3; ++i) nr[i] /= l;
+    const double nn[3] = {-nr[0], -nr[1], -nr[2]};
+    gsv sp, sm;
+    gsv_support(o1, o2, nr, &sp);
+    gsv_support(o1, o2, nn, &sm);
+    double dp[3], dm[3];
+    d3sub(dp, sp.w, S[0].w); d3sub(dm, sm.w, S[0].w);
+    const double hp = d3dot(dp, nr), hm = -d3dot(dm, nr);
+    if (!(hp > 1e-12 || hm > 1e-12)) return 0;
+    S[3] = hp >= hm ? sp : sm;
+    return 1;
+}
+
+/* gjk_distance with the nearest points (world frame) and, when sgn, the
+ * signed distance of intersecting shapes (-EPA depth; 0 when the origin lies
+ * on the simplex).  Unsigned and intersecting: -1 and zero points, as
+ * ccdGJKDist2 leaves them. */
+static double gjk_query(const gjk_obj *o1, const gjk_obj *o2, int sgn, double *p1, double *p2) {
+    ccd_vec3_t c1, c2;
+    gjk_center(o1, &c1);
+    gjk_center(o2, &c2);
+    double v[3] = {c1.v[0] - c2.v[0], c1.v[1] - c2.v[1], c1.v[2] - c2.v[2]};
+    if (d3dot(v, v) == 0.0) v[0] = 1e-12;
+    gsv S[4];
+    double lam[4] = {0, 0, 0, 0};
+    int n = 0;
+    memset(p1, 0, 24); memset(p2, 0, 24);
+    for (int it = 0; it < 128; ++it) {
+        gsv s;
+        const double nd[3] = {-v[0], -v[1], -v[2]};
+        gsv_support(o1, o2, nd, &s);
+        const double vv = d3dot(v, v), vw = d3dot(v, s.w);
+        if (n > 0 && vv - vw <= 1e-12 * vv) break;
+        int dup = 0;
+        for (int k = 0; k < n; ++k) dup |= (S[k].w[0] == s.w[0] && S[k].w[1] == s.w[1] && S[k].w[2] == s.w[2]);
+        if (dup) break;
+        S[n++] = s;
+        if (simplex_closest_s(S, &n, v, lam)) {
+            if (!sgn) return -1.0;
+            const double dep = epa_depth(o1, o2, S, p1, p2);
+            return dep >= 0.0 ? -dep : 0.0;
+        }
+        const double nv = d3dot(v, v);
+        if (nv <= 1e-24) {
+            if (!sgn) return -1.0;
+            /* the origin lies on the simplex: grow it to a tetrahedron around
+             * the origin, then EPA (0 when the shapes only touch) */
+            if (blow_up(o1, o2, S, n)) {
+                const double dep = epa_depth(o1, o2, S, p1, p2);
+                if (dep >= 0.0) return -dep;
+            }
+            for (int i = 0; i < 3; ++i) {
+                p1[i] = 0.0; p2[i] = 0.0;
+                for (int k = 0; k < n; ++k) { p1[i] += lam[k] * S[k].a[i]; p2[i] += lam[k] * S[k].b[i]; }
+            }
+            return 0.0;
+        }
+        if (n > 1 && nv >= vv) break;
+    }
+    for (int i = 0; i < 3; ++i) {
+        p1[i] = 0.0; p2[i] = 0.0;
+        for (int k = 0; k < n; ++k) { p1[i] += lam[k] * S[k].a[i]; p2[i] += lam[k] * S[k].b[i]; }
+    }
+    return sqrt(d3dot(v, v));
+}
+
 /* ------------------------------------------------------- world collide */
 static void make_obj(const orc_world *w, int geom, const real *T, gjk_obj *o, orc_stats *st) {
     memset(o, 0, sizeof *o);
@@ -2928,6 +3221,77 @@ int orc_distance_batch(const orc_world *w, const double *q, long n, int n_self, 
     }
     free(oMi); free(link_T); free(obj_T); free(att_T);
     return 0;
+}
+
+/* orc_distance_batch with DistanceRequest's options (mode bit 0:
+ * enable_signed_distance, bit 1: enable_nearest_points) and the nearest points
+ * of each group's minimum pair, pts[c*6..] = (p1, p2) in the world frame
+ * (zeros when the minimum is an unsigned penetration, -1).  Shape-shape pairs
+ * always carry their GJK points (FCL's shape leaf computes them whatever the
+ * request); point-cloud and BVH-mesh pairs report zeros, and return -2
+ * (unsupported) when the request asks for signed distances or nearest points. */
+int orc_distance_batch_ex(const orc_world *w, const double *q, long n, int n_self, int mode, double *d_self, int *p_self,
+                          double *pts_self, double *d_others, int *p_others, double *pts_others) {
+    const int sgn = mode & 1;
+    real *oMi = malloc(sizeof(real) * 12 * (size_t)(w->nj + 1));
+    real *link_T = malloc(sizeof(real) * 12 * (size_t)(w->n_links + 1));
+    real *obj_T = malloc(sizeof(real) * 12 * (size_t)(w->n_obj + 1));
+    real *att_T = malloc(sizeof(real) * 12 * (size_t)(w->n_att + 1));
+    int rc = 0;
+    for (long c = 0; c < n && !rc; ++c) {
+        fk_links(w, q + (size_t)c * w->dof, oMi, link_T, NULL);
+        for (int i = 0; i < w->n_obj; ++i) se3_mul(link_T + 12 * w->obj_link[i], w->obj_origin + 12 * i, obj_T + 12 * i);
+        for (int i = 0; i < w->n_att; ++i) se3_mul(link_T + 12 * w->att_link[i], w->att_pose + 12 * i, att_T + 12 * i);
+        double best[2] = {DBL_MAX, DBL_MAX}, bpt[2][6];
+        int bp[2] = {-1, -1};
+        memset(bpt, 0, sizeof bpt);
+        for (int p = 0; p < w->n_pairs; ++p) {
+            if (w->p_allowed[p]) continue;
+            const int g = p < n_self ? 0 : 1;
+            if (!sgn && best[g] == -1.0) continue; /* nothing is below -1 */
+            int ks[2] = {w->pa_kind[p], w->pb_kind[p]}, is[2] = {w->pa_idx[p], w->pb_idx[p]};
+            gjk_obj o[2];
+            const real *Ts[2];
+            int gs[2];
+            for (int k = 0; k < 2; ++k) {
+                const real *T;
+                int gg;
+                if (ks[k] == KIND_ROBOT) { T = obj_T + 12 * is[k]; gg = w->obj_geom[is[k]]; }
+                else if (ks[k] == KIND_ATTACHED) { T = att_T + 12 * is[k]; gg = w->att_geom[is[k]]; }
+                else { T = w->scene_tf + 12 * is[k]; gg = w->scene_geom[is[k]]; }
+                Ts[k] = T; gs[k] = gg;
+                if (w->geom_type[gg] != GEOM_OCTREE && w->geom_type[gg] != GEOM_MESH) make_obj(w, gg, T, &o[k], NULL);
+            }
+            const int special = w->geom_type[gs[0]] == GEOM_OCTREE || w->geom_type[gs[1]] == GEOM_OCTREE ||
+                                w->geom_type[gs[0]] == GEOM_MESH || w->geom_type[gs[1]] == GEOM_MESH;
+            double d, pt[6] = {0, 0, 0, 0, 0, 0};
+            if (special) {
+                if (mode) { rc = -2; break; }
+                const int oi = w->geom_type[gs[0]] == GEOM_OCTREE ? 0 : w->geom_type[gs[1]] == GEOM_OCTREE ? 1 : -1;
+                d = mesh_distance(w, gs[0], Ts[0], gs[1], Ts[1]);
+                if (d == -2.0) d = octree_distance(w, gs[oi], Ts[oi], &o[1 - oi]);
+            } else {
+                d = gjk_query(&o[0], &o[1], sgn, pt, pt + 3);
+            }
+            if (d < best[g]) { best[g] = d; bp[g] = p; memcpy(bpt[g], pt, sizeof pt); }
+        }
+        d_self[c] = best[0]; p_self[c] = bp[0]; d_others[c] = best[1]; p_others[c] = bp[1];
+        if (pts_self) memcpy(pts_self + 6 * c, bpt[0], sizeof bpt[0]);
+        if (pts_others) memcpy(pts_others + 6 * c, bpt[1], sizeof bpt[1]);
+    }
+    free(oMi); free(link_T); free(obj_T); free(att_T);
+    return rc;
+}
+
+/* fcl::distance(geometry ga at Ta, geometry gb at Tb) of two shapes with
+ * DistanceRequest's options: distance (signed when mode & 1) and the nearest
+ * points pts[0..6) = (p1, p2) in the world frame. */
+double orc_distance_pair_ex(const orc_world *w, int ga, const double *Ta, int gb, const double *Tb, int mode,
+                            double *pts) {
+    gjk_obj a, b;
+    make_obj(w, ga, Ta, &a, NULL);
+    make_obj(w, gb, Tb, &b, NULL);
+    return gjk_query(&a, &b, mode & 1, pts, pts + 3);
 }
 
 /* Batch entry point.  flags[n], masks[n*W]; stats (may be NULL) receives

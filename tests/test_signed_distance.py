@@ -1,0 +1,226 @@
+"""DistanceRequest(enable_signed_distance, enable_nearest_points) in the
+oracle: FCL 0.7.0's shape distance leaf returns the world-frame
+nearest points of the two shapes with every distance (libccd ccdGJKDist2 ->
+extractClosestPoints), and with enable_signed_distance the depth of
+intersecting shapes from EPA (ccdGJKSignedDist -> penEPAPosClosest), as
+-depth.  Known answers from plain geometry, and random hulls against an
+independent computation (scipy's convex hull of the Minkowski difference:
+the penetration depth is the distance from the origin to its nearest facet;
+the separation distance is the QP of test_oracle)."""
+import numpy as np
+import pytest
+
+import worlds as Wd
+from test_oracle import _T, _pair_world, _qp_distance
+
+
+def _box(side):
+    from oracle import model as M
+    return M.BoxGeom(tuple(side))
+
+
+def test_nearest_points_known_answers():
+    from oracle import model as M
+    b, s = _box((1.0, 1.0, 1.0)), M.SphereGeom(0.25)
+    w, (gb, gs) = _pair_world([b, s])
+    d, p1, p2 = Wd.distance_pair_ex(w, gb, _T(), gb, _T(p=(1.7, 0.0, 0.0)))  # face-face
+    assert abs(d - 0.7) < 1e-6
+    assert abs(p1[0] - 0.5) < 1e-6 and abs(p2[0] - 1.2) < 1e-6
+    assert np.abs(p2 - p1 - [0.7, 0, 0]).max() < 1e-6 and np.abs(p1[1:]).max() <= 0.5 + 1e-6
+    d, p1, p2 = Wd.distance_pair_ex(w, gb, _T(), gb, _T(p=(1.5, 1.5, 0.0)))  # edge-edge
+    assert abs(d - np.sqrt(0.5)) < 1e-6
+    assert np.abs(p1[:2] - 0.5).max() < 1e-6 and np.abs(p2[:2] - 1.0).max() < 1e-6 and abs(p1[2] - p2[2]) < 1e-6
+    d, p1, p2 = Wd.distance_pair_ex(w, gs, _T(), gb, _T(p=(1.0, 0.0, 0.0)))  # sphere - box face
+    assert abs(d - 0.25) < 1e-6
+    np.testing.assert_allclose(p1, [0.25, 0, 0], atol=1e-6)
+    np.testing.assert_allclose(p2, [0.5, 0, 0], atol=1e-6)
+    # rotated box: corner towards the sphere
+    c = np.cos(np.pi / 8)
+    d, p1, p2 = Wd.distance_pair_ex(w, gb, _T(q=(c, 0.0, 0.0, np.sin(np.pi / 8))), gs, _T(p=(1.5, 0.0, 0.0)))
+    r = 0.5 * np.sqrt(2.0)
+    assert abs(d - (1.5 - r - 0.25)) < 1e-6
+    # the distance converges quadratically, the points only to ~sqrt of it
+    # against a curved support in float (libccd's ccd_real_t): 1e-4
+    np.testing.assert_allclose(p1, [r, 0, 0], atol=1e-4)
+    np.testing.assert_allclose(p2, [1.25, 0, 0], atol=1e-4)
+
+
+def test_unsigned_penetration_gives_minus_one_and_zero_points():
+    b = _box((1.0, 1.0, 1.0))
+    w, (g,) = _pair_world([b])
+    d, p1, p2 = Wd.distance_pair_ex(w, g, _T(), g, _T(p=(0.9, 0.2, 0.1)))
+    assert d == -1.0 and not p1.any() and not p2.any()
+
+
+def test_signed_distance_known_answers():
+    from oracle import model as M
+    b, s = _box((1.0, 1.0, 1.0)), M.SphereGeom(0.25)
+    w, (gb, gs) = _pair_world([b, s])
+    # boxes overlapping by 0.1 along x: depth 0.1, witness points on the faces
+    d, p1, p2 = Wd.distance_pair_ex(w, gb, _T(), gb, _T(p=(0.9, 0.02, 0.01)), signed=True)
+    assert abs(d + 0.1) < 1e-6
+    assert abs(p1[0] - 0.5) < 1e-6 and abs(p2[0] - 0.4) < 1e-6
+    np.testing.assert_allclose(p1 - p2, [0.1, 0, 0], atol=1e-6)
+    # separated shapes: the signed distance is the distance
+    d, _, _ = Wd.distance_pair_ex(w, gb, _T(), gb, _T(p=(1.7, 0.0, 0.0)), signed=True)
+    assert abs(d - 0.7) < 1e-6
+    # sphere 0.1 deep into a box face (curved: EPA's polytope approximates it)
+    d, p1, p2 = Wd.distance_pair_ex(w, gs, _T(p=(0.65, 0.0, 0.0)), gb, _T(), signed=True)
+    assert abs(d + 0.1) < 2e-3
+    assert abs(p2[0] - 0.5) < 2e-3 and abs(p1[0] - 0.4) < 2e-3
+
+
+def _facets(P):
+    from scipy.spatial import ConvexHull
+    h = ConvexHull(P)
+    return h.equations  # n . x + off <= 0 inside, |n| = 1
+
+
+@pytest.mark.parametrize("trial", range(10))
+def test_random_hulls_signed_distance_and_points(trial):
+    """Random convex hulls at random relative poses: separated -> distance ==
+    the QP minimum, |p1 - p2| == d, p1 on A, p2 on B; intersecting -> -depth
+    == minus the distance from the origin to the Minkowski difference's
+    nearest facet, p1 - p2 is that facet's witness."""
+    from oracle import model as M
+    rng = np.random.default_rng(100 + trial)
+    A = rng.normal(size=(rng.integers(8, 24), 3)) * 0.1
+    B = rng.normal(size=(rng.integers(8, 24), 3)) * 0.1
+    A, B = A.astype(np.float32).astype(np.float64), B.astype(np.float32).astype(np.float64)  # float libccd supports
+    gA, gB = M.ConvexGeom(A, []), M.ConvexGeom(B, [])
+    w, (ia, ib) = _pair_world([gA, gB])
+    for scale in (0.05, 0.15, 0.4):
+        off = rng.normal(size=3)
+        off *= scale / np.linalg.norm(off)
+        off = off.astype(np.float32).astype(np.float64)
+        d, p1, p2 = Wd.distance_pair_ex(w, ia, _T(), ib, _T(p=tuple(off)), signed=True)
+        Bo = B + off
+        FA, FB = _facets(A), _facets(Bo)
+        assert (FA[:, :3] @ p1 + FA[:, 3]).max() < 1e-6 and (FB[:, :3] @ p2 + FB[:, 3]).max() < 1e-6
+        if d >= 0:
+            ref = _qp_distance(A, Bo)
+            assert abs(d - ref) < 1e-6 and abs(np.linalg.norm(p1 - p2) - d) < 1e-6
+        else:
+            Mk = (A[:, None, :] - Bo[None, :, :]).reshape(-1, 3)
+            depth = (-_facets(Mk)[:, 3]).min()
+            assert abs(-d - depth) < 1e-6, (d, depth)
+            assert abs(np.linalg.norm(p1 - p2) + d) < 1e-6
+
+
+def test_distance_batch_ex_semantics():
+    """World level (cfg3): the unsigned minimum equals distance_batch's; the
+    signed one equals it on collision-free configurations and is the deepest
+    penetration (< 0) on colliding ones; nearest points lie |d| apart."""
+    ow = Wd.oracle_world(3)
+    q = Wd.sample_q(ow.art, 200, 9)
+    ds, ps, do, po = ow.distance_batch(q)
+    u = ow.distance_batch_ex(q)
+    np.testing.assert_array_equal(u[0], ds)
+    np.testing.assert_array_equal(u[3], do)
+    np.testing.assert_array_equal(u[1], ps)
+    sg = ow.distance_batch_ex(q, signed=True)
+    for dd, pts, ref in ((sg[0], sg[2], ds), (sg[3], sg[5], do)):
+        free = ref >= 0
+        np.testing.assert_array_equal(dd[free], ref[free])
+        assert (dd[~free] < 0).all() and (dd[~free] > -0.2).all()
+        gap = np.linalg.norm(pts[:, :3] - pts[:, 3:], axis=1)
+        ok = np.isfinite(dd) & (dd != np.finfo(float).max)
+        np.testing.assert_allclose(gap[ok], np.abs(dd[ok]), atol=2e-6)
+    # unsigned penetration: zero points
+    pen = u[0] == -1.0
+    assert pen.any() and not u[2][pen].any()
+
+
+# ------------------------------------------------------------------ device
+def _ow(cfg):
+    return Wd.oracle_world(cfg)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg", [3, 4])
+def test_device_signed_distance_and_points_match_oracle(cfg):
+    """DistanceRequest(enable_signed_distance=True) batched on the device vs
+    the oracle's restatement: distances and nearest points within 1e-9 (the
+    same fp64 GJK / EPA on the same float supports), argmin pairs equal; the
+    unsigned batch with nearest_points=True likewise."""
+    from mplib_amd import pymp, scenes
+    w, art = scenes.world(cfg)
+    q = scenes.sample_states(art, 2048, 300 + cfg)
+    o = _ow(cfg)
+    req = pymp.fcl.DistanceRequest(enable_signed_distance=True)
+    ds, ps, do, po, qs, qo = w.distance_batch(q, request=req)
+    rs, rps, rqs, ro, rpo, rqo = o.distance_batch_ex(q, signed=True)
+    for d, r, pp, rp, pt, rpt in ((ds, rs, ps, rps, qs, rqs), (do, ro, po, rpo, qo, rqo)):
+        np.testing.assert_allclose(d, r, rtol=0, atol=1e-9)
+        assert (pp == rp).mean() > 0.999
+        same = pp == rp
+        np.testing.assert_allclose(pt[same], rpt[same], rtol=0, atol=1e-9)
+    assert (np.minimum(ds, do) < 0).mean() > 0.05  # penetrations were exercised
+    u = w.distance_batch(q, nearest_points=True)
+    ru = o.distance_batch_ex(q)
+    for k in (0, 3):
+        np.testing.assert_allclose(u[k], ru[k], rtol=0, atol=1e-9)
+    same = u[1] == ru[1]
+    np.testing.assert_allclose(u[4][same], ru[2][same], rtol=0, atol=1e-9)
+    # the unsigned distances are the plain batch's
+    d0 = w.distance_batch(q)
+    np.testing.assert_array_equal(d0[0], u[0])
+    np.testing.assert_array_equal(d0[2], u[2])
+
+
+@pytest.mark.gpu
+def test_device_scalar_signed_distance_api():
+    from mplib_amd import pymp, scenes
+    w, art = scenes.world(3)
+    q = scenes.sample_states(art, 24, 77)
+    rs, rps, rqs, ro, rpo, rqo = _ow(3).distance_batch_ex(q, signed=True)
+    req = pymp.fcl.DistanceRequest(enable_signed_distance=True, enable_nearest_points=True)
+    for i in range(len(q)):
+        w.set_qpos_all(list(q[i]))
+        s, o = w.self_distance(req), w.distance_with_others(req)
+        assert abs(s.min_distance - rs[i]) < 1e-9 and abs(o.min_distance - ro[i]) < 1e-9
+        np.testing.assert_allclose(np.concatenate(s.res.nearest_points), rqs[i], atol=1e-9)
+        np.testing.assert_allclose(np.concatenate(o.res.nearest_points), rqo[i], atol=1e-9)
+        full = w.distance_full(req)
+        assert full.min_distance == min(s.min_distance, o.min_distance)
+    # fcl.distance on two objects: boxes 0.1 deep -> -0.1, witness points on the faces
+    a = pymp.fcl.CollisionObject(pymp.fcl.Box([1.0, 1.0, 1.0]), [0, 0, 0], [1, 0, 0, 0])
+    b = pymp.fcl.CollisionObject(pymp.fcl.Box([1.0, 1.0, 1.0]), [0.9, 0.02, 0.01], [1, 0, 0, 0])
+    r = pymp.fcl.distance(a, b, pymp.fcl.DistanceRequest(enable_signed_distance=True))
+    assert abs(r.min_distance + 0.1) < 1e-6
+    p1, p2 = np.asarray(r.nearest_points[0]), np.asarray(r.nearest_points[1])
+    assert abs(p1[0] - 0.5) < 1e-6 and abs(p2[0] - 0.4) < 1e-6
+    assert pymp.fcl.distance(a, b).min_distance == -1.0
+    c = pymp.fcl.CollisionObject(pymp.fcl.Box([1.0, 1.0, 1.0]), [1.7, 0.0, 0.0], [1, 0, 0, 0])
+    r = pymp.fcl.distance(a, c)
+    assert abs(r.min_distance - 0.7) < 1e-6
+    assert abs(r.nearest_points[0][0] - 0.5) < 1e-6 and abs(r.nearest_points[1][0] - 1.2) < 1e-6
+
+
+@pytest.mark.gpu
+def test_device_clearance_validity_checker():
+    """ValidityChecker.clearance (ompl_planner.h:69-72): world.distance() =
+    distanceFull().min_distance; the batch equals min(d_self, d_others) of the
+    oracle, and the scalar form sets the world's state as the reference does."""
+    from mplib_amd import pymp, scenes
+    w, art = scenes.world(3)
+    vc = pymp.ompl.ValidityChecker(w)
+    q = scenes.sample_states(art, 1000, 12)
+    rs, _, ro, _ = _ow(3).distance_batch(q)
+    c = vc.clearance_batch(q)
+    np.testing.assert_allclose(c, np.minimum(rs, ro), rtol=0, atol=1e-9)
+    f, _ = _ow(3).collide_batch(q)
+    np.testing.assert_array_equal(vc.is_valid_batch(q), f == 0)
+    for i in range(5):
+        assert abs(vc.clearance(list(q[i])) - c[i]) < 1e-12
+        assert vc.is_valid(list(q[i])) == (f[i] == 0)
+
+
+@pytest.mark.gpu
+def test_device_signed_distance_refused_for_mesh_worlds():
+    from mplib_amd import pymp, scenes
+    w, art = scenes.world(7)  # BVH-mesh links
+    q = scenes.sample_states(art, 4, 1)
+    with pytest.raises(NotImplementedError):
+        w.distance_batch(q, request=pymp.fcl.DistanceRequest(enable_signed_distance=True))
+    w.distance_batch(q)  # the plain distance still runs

@@ -247,6 +247,19 @@ def distance_pair(ow: oracle.OracleWorld, ga: int, Ta, gb: int, Tb) -> float:
                                                 b.ctypes.data_as(DP)))
 
 
+def distance_pair_ex(ow: oracle.OracleWorld, ga: int, Ta, gb: int, Tb, signed: bool = False):
+    """The oracle's fcl::distance of two posed shapes with the nearest points:
+    (distance, p1, p2); signed: enable_signed_distance (EPA depth)."""
+    import ctypes
+    DP = ctypes.POINTER(ctypes.c_double)
+    flat = lambda T: np.ascontiguousarray(T if np.ndim(T) == 1 else oracle._se3_flat(T), dtype=np.float64)  # noqa: E731
+    a, b = flat(Ta), flat(Tb)
+    pts = np.zeros(6)
+    d = float(oracle.lib().orc_distance_pair_ex(ctypes.byref(ow._w), ga, a.ctypes.data_as(DP), gb,
+                                                b.ctypes.data_as(DP), 1 if signed else 0, pts.ctypes.data_as(DP)))
+    return d, pts[:3], pts[3:]
+
+
 def cone_hull(n_rim: int = 300, r: float = 0.12, h: float = 0.25):
     """A watertight triangulated cone: n_rim rim vertices (z = 0), apex, base
     centre.  Its flat base keeps every rim vertex in the walk cells around
