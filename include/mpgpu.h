@@ -375,6 +375,19 @@ int mpg_collide_count(mpg_world *world, const double *lower, const double *upper
 int mpg_sample_uniform(const double *lower, const double *upper, int32_t dof, int64_t n, uint64_t seed,
                        int64_t row_offset, double *q, int device);
 
+/*
+ * Diagnostics (host only, no device): the FCL 0.7.0 BVHModel<OBBRSS> tree the
+ * snapshot builds for a BVH mesh (BVHModel::endModel -> buildTree:
+ * BVFitter<OBBRSS>::fit, SPLIT_METHOD_MEAN; OBB half), whose OBB tests gate
+ * mesh pairs as FCL's traversal does.  boxes [(2T - 1) * 15] = per node the
+ * row-major axis matrix (columns = box axes), centre, half extents; links
+ * [(2T - 1) * 3] = first child node (-(triangle + 1) for a leaf), first leaf
+ * position, leaf count; leaf_order [T] = primitive_indices after the build.
+ * Returns the node count (2T - 1) or a negative status.
+ */
+int mpg_fcl_bvh_build(const double *vertices, int32_t n_vertices, const int32_t *triangles, int32_t n_triangles,
+                      double *boxes, int32_t *links, int32_t *leaf_order);
+
 /* Diagnostics: the device sin/cos used by the FK (host buffers). */
 int mpg_debug_sincos(const double *x, int64_t n, double *s, double *c, int device);
 

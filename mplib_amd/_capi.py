@@ -92,6 +92,8 @@ SIGNATURES = {
                                                 ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "mpg_debug_sincos": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p,
                                         ctypes.c_int]),
+    "mpg_fcl_bvh_build": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_int32,
+                                         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "mpg_synchronize": (ctypes.c_int, [ctypes.c_int]),
     "mpg_device_count": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int)]),
     "mpg_last_error": (ctypes.c_char_p, []),

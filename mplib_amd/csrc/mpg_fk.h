@@ -118,7 +118,19 @@ struct DevWorld {
   cptr<double> mesh_node;
   cptr<int> mesh_link;  // [clusters * 2]
   cptr<int> mesh_tree;  // [n_geoms * 2]
+  // FCL 0.7.0 BVHModel<OBBRSS> of every mesh (OBB half; build_fcl_bvh):
+  // nodes [N][FB_STRIDE] (axis row-major, centre, half extents), links [N][3]
+  // (first child as a global node index, or -(triangle + 1) for a leaf; first
+  // primitive position; primitive count), per geometry its root (-1: none),
+  // per triangle (mesh_triangle order) its position in the leaf order; per
+  // geometry the OBB FCL's computeBV gives the shape in its own frame
+  cptr<double> fb_box;
+  cptr<int> fb_link;
+  cptr<int> fb_root;   // [n_geoms]
+  cptr<int> tri_pos;   // [n_mesh_triangles]
+  cptr<double> sobb;   // [n_geoms][FB_STRIDE]
 };
+enum { FB_AXIS = 0, FB_TO = 9, FB_EXT = 12, FB_STRIDE = 15 };
 enum { OG_ORIGIN = 0, OG_INV = 3, OG_DIMS = 4, OG_CELL0 = 7, OG_STRIDE = 8 };
 // triangle record: vertices P1 P2 P3, the triangle's AABB, its index in the mesh
 enum { TR_P = 0, TR_LO = 9, TR_HI = 12, TR_ID = 15, TR_STRIDE = 16 };

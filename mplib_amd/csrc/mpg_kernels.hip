@@ -1924,6 +1924,116 @@ __device__ __forceinline__ SE3 bcast_se3(const SE3& T, int k) {
   return o;
 }
 
+// ---------------------------------------------------------------------------
+// FCL's BVH traversal gates.  fcl::collide on a BVHModel<OBBRSS> runs a leaf
+// test only when every bounding-volume test on its way down the tree passed
+// (collisionRecurse; BVTesting = !overlap(R0, T0, bv1, bv2), OBB-inl.h).  The
+// device finds the intersecting triangles (pairs) with its own pruning (which
+// only drops triangles that cannot hit); fcl_gate_* then replays the OBB tests
+// of FCL's path to that leaf (pair), so a hit counts only where FCL would have
+// reached it.  Oracle: the traversal itself (oracle/collide_oracle.c
+// bvh_shape_walk / bvh_mesh_walk).
+// ---------------------------------------------------------------------------
+// overlap(R0, T0, a, b): R = a.axis^T (R0 b.axis), T = (R0 b.To + T0 - a.To)^T a.axis
+__device__ __forceinline__ bool fcl_overlap(const double* R0, const double* T0, const double* aA, const double* aT,
+                                            const double* aE, cptr<double> b) {
+  double R0b[9], R[9], Tt[3], T[3], bE[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+      R0b[3 * i + j] = (R0[3 * i] * b[FB_AXIS + j] + R0[3 * i + 1] * b[FB_AXIS + 3 + j]) + R0[3 * i + 2] * b[FB_AXIS + 6 + j];
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) R[3 * i + j] = (aA[i] * R0b[j] + aA[3 + i] * R0b[3 + j]) + aA[6 + i] * R0b[6 + j];
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+    Tt[i] = (((R0[3 * i] * b[FB_TO] + R0[3 * i + 1] * b[FB_TO + 1]) + R0[3 * i + 2] * b[FB_TO + 2]) + T0[i]) - aT[i];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) T[j] = (Tt[0] * aA[j] + Tt[1] * aA[3 + j]) + Tt[2] * aA[6 + j];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) bE[k] = b[FB_EXT + k];
+  return !obb_disjoint(R, T, aE, bE);
+}
+
+// the shape's OBB in the world (computeBV<OBB>(shape, tf): convex / box /
+// capsule / cylinder axis = R axis_local, sphere axis I; To = R To_local + T)
+__device__ __forceinline__ void fcl_shape_obb_world(const DevWorld& w, int gs, int ts, const SE3& TS, double* A,
+                                                    double* To, double* E) {
+  const cptr<double> o = w.sobb + FB_STRIDE * gs;
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+      A[3 * i + j] = ts == MPG_GEOM_SPHERE ? o[FB_AXIS + 3 * i + j]
+                                           : (TS.R[3 * i] * o[FB_AXIS + j] + TS.R[3 * i + 1] * o[FB_AXIS + 3 + j]) +
+                                                 TS.R[3 * i + 2] * o[FB_AXIS + 6 + j];
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+    To[i] = ((TS.R[3 * i] * o[FB_TO] + TS.R[3 * i + 1] * o[FB_TO + 1]) + TS.R[3 * i + 2] * o[FB_TO + 2]) + TS.p[i];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) E[k] = o[FB_EXT + k];
+}
+
+// MeshShape: the path from the root to triangle t's leaf (t: index in the
+// mesh), every node's OBB against the shape's (world) under (TM.R, TM.p)
+__device__ __forceinline__ bool fcl_gate_shape(const DevWorld& w, int gm, const SE3& TM, const double* sA,
+                                               const double* sT, const double* sE, int t) {
+  const int pos = w.tri_pos[(int)w.geom_rec[G_STRIDE * gm + G_PARAM] + t];
+  int node = w.fb_root[gm];
+  for (int depth = 0; depth < 256; ++depth) {
+    if (!fcl_overlap(TM.R, TM.p, sA, sT, sE, w.fb_box + FB_STRIDE * node)) return false;
+    const int c = w.fb_link[3 * node];
+    if (c < 0) return true;
+    node = pos < w.fb_link[3 * c + 1] + w.fb_link[3 * c + 2] ? c : c + 1;
+  }
+  return false;
+}
+
+__device__ __forceinline__ double fcl_obb_size(cptr<double> b) {
+  return (b[FB_EXT] * b[FB_EXT] + b[FB_EXT + 1] * b[FB_EXT + 1]) + b[FB_EXT + 2] * b[FB_EXT + 2];
+}
+
+// MeshMesh: FCL's descent to the leaf pair (ta in A, tb in B) -- the first
+// tree is descended when the second node is a leaf or the first is not and
+// is larger (firstOverSecond); key (optional) collects the left / right
+// choices, whose lexicographic order is FCL's visit order of leaf pairs
+__device__ __forceinline__ bool fcl_gate_mesh(const DevWorld& w, int ga, int gb, const double* R, const double* T,
+                                              int ta, int tb, uint64_t* key = nullptr) {
+  const int pa = w.tri_pos[(int)w.geom_rec[G_STRIDE * ga + G_PARAM] + ta];
+  const int pb = w.tri_pos[(int)w.geom_rec[G_STRIDE * gb + G_PARAM] + tb];
+  int a = w.fb_root[ga], b = w.fb_root[gb], nk = 0;
+  for (int depth = 0; depth < 512; ++depth) {
+    const cptr<double> ba = w.fb_box + FB_STRIDE * a;
+    double aA[9], aT[3], aE[3];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) aA[k] = ba[FB_AXIS + k];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      aT[k] = ba[FB_TO + k];
+      aE[k] = ba[FB_EXT + k];
+    }
+    const cptr<double> bb = w.fb_box + FB_STRIDE * b;
+    if (!fcl_overlap(R, T, aA, aT, aE, bb)) return false;
+    const int ca = w.fb_link[3 * a], cb = w.fb_link[3 * b];
+    if (ca < 0 && cb < 0) return true;
+    bool right;
+    if (cb < 0 || (ca >= 0 && fcl_obb_size(ba) > fcl_obb_size(bb))) {
+      right = !(pa < w.fb_link[3 * ca + 1] + w.fb_link[3 * ca + 2]);
+      a = right ? ca + 1 : ca;
+    } else {
+      right = !(pb < w.fb_link[3 * cb + 1] + w.fb_link[3 * cb + 2]);
+      b = right ? cb + 1 : cb;
+    }
+    if (key && nk < 128) {
+      if (right) key[nk >> 6] |= 1ull << (63 - (nk & 63));
+      ++nk;
+    }
+  }
+  return false;
+}
+
 __device__ __forceinline__ bool mesh_mesh_wave(const DevWorld& w, int ga, const SE3& TA, int gb, const SE3& TB) {
   // lanes take 64 of B's triangles into A's frame; each one that meets A's
   // box is then broadcast, A's cluster boxes are tested one per lane, and
@@ -1999,7 +2109,8 @@ __device__ __forceinline__ bool mesh_mesh_wave(const DevWorld& w, int ga, const 
               double P[9];
 #pragma unroll
               for (int q = 0; q < 9; ++q) P[q] = rp[TR_P + q];
-              hit = tri_tri_intersect(P, Qk);
+              hit = tri_tri_intersect(P, Qk) &&
+                    fcl_gate_mesh(w, ga, gb, R, T, (int)rp[TR_ID], (int)bcast(rq[TR_ID], k));
             }
           }
           if (__ballot(hit) != 0) return true;
@@ -2045,6 +2156,8 @@ __device__ __forceinline__ bool mesh_shape_wave(const DevWorld& w, cptr<double> 
   B.geom = gm;
   B.type = MPG_GEOM_MESH;
   const CV3 ca = center(w, A);
+  double sA[9], sT[3], sE[3];  // FCL's OBB of the shape (the traversal's BV tests)
+  fcl_shape_obb_world(w, gs, ts, TS, sA, sT, sE);
   for (int b = t0; b < t1; b += 64) {
     const int t = b + (int)lane;
     bool cand = t < t1;
@@ -2079,6 +2192,7 @@ __device__ __forceinline__ bool mesh_shape_wave(const DevWorld& w, cptr<double> 
         }
         hit = res > 0;
       }
+      hit = hit && fcl_gate_shape(w, gm, TM, sA, sT, sE, (int)rec[TR_ID]);
     }
     if (__ballot(hit) != 0) return true;
   }
@@ -4912,12 +5026,16 @@ __device__ bool mesh_shape_first_contact(const DevWorld& w, cptr<double> HV, int
             kMeshShapePad * (1.0 + std::fabs(TS.p[0]) + std::fabs(TS.p[1]) + std::fabs(TS.p[2]) + std::fabs(TM.p[0]) +
                              std::fabs(TM.p[1]) + std::fabs(TM.p[2]));
   const GObj A = posed_obj(TS, gs, ts), B = posed_obj(TM, gm, MPG_GEOM_MESH);
+  double sA[9], sT[3], sE[3];
+  fcl_shape_obb_world(w, gs, ts, TS, sA, sT, sE);
+  // FCL's traversal visits the leaves left to right: the first hit is the
+  // reachable (gated) hit of smallest leaf position
   int best = INT_MAX;
   double bd = 0.0;
   V3 bn{0, 0, 0}, bp{0, 0, 0};
   for (int t = t0; t < t1; ++t) {
     const cptr<double> rec = w.mesh_tri + TR_STRIDE * (size_t)t;
-    const int id = (int)rec[TR_ID];
+    const int id = w.tri_pos[t0 + (int)rec[TR_ID]];  // leaf position
     if (id >= best) continue;
     bool out = false;
     for (int i = 0; i < 3; ++i) out |= rec[TR_LO + i] > cl[i] + hq[i] || rec[TR_HI + i] < cl[i] - hq[i];
@@ -4935,7 +5053,7 @@ __device__ bool mesh_shape_first_contact(const DevWorld& w, cptr<double> HV, int
     } else {
       hit = tri_mpr_penetration(w, HV, A, nullptr, B, rec, dp, n, p);
     }
-    if (hit) {
+    if (hit && fcl_gate_shape(w, gm, TM, sA, sT, sE, (int)rec[TR_ID])) {
       best = id;
       bd = dp;
       bn = n;
@@ -4961,7 +5079,9 @@ __device__ bool mesh_mesh_first_contact(const DevWorld& w, int ga, const SE3& TA
     alo[i] = gra[G_OBB_C + i] - gra[G_OBB_E + i];
     ahi[i] = gra[G_OBB_C + i] + gra[G_OBB_E + i];
   }
-  long long best = LLONG_MAX;
+  // the first hit in FCL's visit order: the reachable intersecting pair whose
+  // descent (fcl_gate_mesh's left / right choices) is lexicographically smallest
+  uint64_t best[2] = {~0ull, ~0ull};
   int best_a = -1, best_b = -1;
   for (int j = b0; j < b1; ++j) {
     const cptr<double> rq = w.mesh_tri + TR_STRIDE * (size_t)j;
@@ -4985,15 +5105,17 @@ __device__ bool mesh_mesh_first_contact(const DevWorld& w, int ga, const SE3& TA
       const int t1 = w.mesh_link[2 * c] + w.mesh_link[2 * c + 1];
       for (int t = w.mesh_link[2 * c]; t < t1; ++t) {
         const cptr<double> rp = w.mesh_tri + TR_STRIDE * (size_t)t;
-        const long long key = ((long long)rp[TR_ID] << 32) | idb;
-        if (key >= best) continue;
         bool o2 = false;
         for (int i = 0; i < 3; ++i) o2 |= rp[TR_LO + i] > qhi[i] || rp[TR_HI + i] < qlo[i];
         if (o2) continue;
         double P[9];
         for (int q = 0; q < 9; ++q) P[q] = rp[TR_P + q];
-        if (tri_tri_intersect(P, Q)) {
-          best = key;
+        if (!tri_tri_intersect(P, Q)) continue;
+        uint64_t key[2] = {0ull, 0ull};
+        if (!fcl_gate_mesh(w, ga, gb, R, T, (int)rp[TR_ID], (int)idb, key)) continue;
+        if (key[0] < best[0] || (key[0] == best[0] && key[1] < best[1])) {
+          best[0] = key[0];
+          best[1] = key[1];
           best_a = t;
           best_b = j;
         }
@@ -5700,6 +5822,229 @@ void geom_record(const mpg_world_desc* d, int g, double* rec) {
   rec[G_VMAX] = vmax;
 }
 
+// ---------------------------------------------------------------------------
+// FCL 0.7.0 BVHModel<OBBRSS>::endModel -> buildTree for the meshes
+// (load_mesh_as_BVH, src/urdf_utils.cpp:136-155) [ext FCL BVH_model-inl.h,
+// BV_fitter-inl.h, BV_splitter-inl.h, math/geometry-inl.h; restated, FCL is
+// not under /root/reference]: BVFitter<OBBRSS>::fit (covariance of the
+// node's triangle vertices, Jacobi eigen_old, axisFromEigen, extent and
+// centre of the projections; only the OBB half decides collisions), the
+// SPLIT_METHOD_MEAN rule along the first axis (centroid . axis > mean goes
+// right, the rest are swapped to the front; an empty side -> n / 2), child
+// pairs allocated at num_bvs before recursing.  The oracle builds the same
+// tree from its own code (oracle/collide_oracle.c orc_bvh_build).
+// ---------------------------------------------------------------------------
+struct FclBvh {
+  std::vector<double> box;  // [n][FB_STRIDE]
+  std::vector<int> link;    // [n][3]
+};
+
+// eigen_old: Jacobi rotations; vout(r, c) = v[c][r], dout = eigenvalues
+void fcl_eigen_old(const double m[9], double dout[3], double vout[9]) {
+  double R[3][3] = {{m[0], m[1], m[2]}, {m[3], m[4], m[5]}, {m[6], m[7], m[8]}};
+  double b[3], z[3], v[3][3] = {{1, 0, 0}, {0, 1, 0}, {0, 0, 1}}, d[3];
+  for (int ip = 0; ip < 3; ++ip) {
+    b[ip] = d[ip] = R[ip][ip];
+    z[ip] = 0;
+  }
+  for (int i = 0; i < 50; ++i) {
+    double sm = 0;
+    for (int ip = 0; ip < 3; ++ip)
+      for (int iq = ip + 1; iq < 3; ++iq) sm += std::fabs(R[ip][iq]);
+    if (sm == 0.0) {
+      for (int c = 0; c < 3; ++c)
+        for (int r = 0; r < 3; ++r) vout[3 * r + c] = v[c][r];
+      for (int k = 0; k < 3; ++k) dout[k] = d[k];
+      return;
+    }
+    const double tresh = i < 3 ? 0.2 * sm / (3 * 3) : 0.0;
+    for (int ip = 0; ip < 3; ++ip)
+      for (int iq = ip + 1; iq < 3; ++iq) {
+        double g = 100.0 * std::fabs(R[ip][iq]);
+        if (i > 3 && std::fabs(d[ip]) + g == std::fabs(d[ip]) && std::fabs(d[iq]) + g == std::fabs(d[iq])) {
+          R[ip][iq] = 0.0;
+        } else if (std::fabs(R[ip][iq]) > tresh) {
+          double h = d[iq] - d[ip], t;
+          if (std::fabs(h) + g == std::fabs(h)) {
+            t = R[ip][iq] / h;
+          } else {
+            const double theta = 0.5 * h / R[ip][iq];
+            t = 1.0 / (std::fabs(theta) + std::sqrt(1.0 + theta * theta));
+            if (theta < 0.0) t = -t;
+          }
+          const double c = 1.0 / std::sqrt(1 + t * t), s = t * c, tau = s / (1.0 + c);
+          h = t * R[ip][iq];
+          z[ip] -= h;
+          z[iq] += h;
+          d[ip] -= h;
+          d[iq] += h;
+          R[ip][iq] = 0.0;
+          auto rot = [&](double& x, double& y) {
+            const double gg = x, hh = y;
+            x = gg - s * (hh + gg * tau);
+            y = hh + s * (gg - hh * tau);
+          };
+          for (int j = 0; j < ip; ++j) rot(R[j][ip], R[j][iq]);
+          for (int j = ip + 1; j < iq; ++j) rot(R[ip][j], R[j][iq]);
+          for (int j = iq + 1; j < 3; ++j) rot(R[ip][j], R[iq][j]);
+          for (int j = 0; j < 3; ++j) rot(v[j][ip], v[j][iq]);
+        }
+      }
+    for (int ip = 0; ip < 3; ++ip) {
+      b[ip] += z[ip];
+      d[ip] = b[ip];
+      z[ip] = 0.0;
+    }
+  }
+}
+
+// covariance sums -> M -> eigen -> axisFromEigen -> extent / centre of pts
+void fcl_fit_obb(const double S1[3], const double S2[6], double n_points, const std::vector<const double*>& pts,
+                 double* box) {
+  double M[9], E[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, ev[3] = {0, 0, 0};
+  M[0] = S2[0] - S1[0] * S1[0] / n_points;
+  M[4] = S2[1] - S1[1] * S1[1] / n_points;
+  M[8] = S2[2] - S1[2] * S1[2] / n_points;
+  M[1] = M[3] = S2[3] - S1[0] * S1[1] / n_points;
+  M[5] = M[7] = S2[5] - S1[1] * S1[2] / n_points;
+  M[2] = M[6] = S2[4] - S1[0] * S1[2] / n_points;
+  fcl_eigen_old(M, ev, E);
+  int mn, mid, mx;
+  if (ev[0] > ev[1]) {
+    mx = 0;
+    mn = 1;
+  } else {
+    mn = 0;
+    mx = 1;
+  }
+  if (ev[2] < ev[mn]) {
+    mid = mn;
+    mn = 2;
+  } else if (ev[2] > ev[mx]) {
+    mid = mx;
+    mx = 2;
+  } else {
+    mid = 2;
+  }
+  double* ax = box + FB_AXIS;
+  for (int r = 0; r < 3; ++r) {
+    ax[3 * r] = E[3 * mx + r];
+    ax[3 * r + 1] = E[3 * mid + r];
+  }
+  ax[2] = ax[3] * ax[7] - ax[6] * ax[4];
+  ax[5] = ax[6] * ax[1] - ax[0] * ax[7];
+  ax[8] = ax[0] * ax[4] - ax[3] * ax[1];
+  double lo[3] = {DBL_MAX, DBL_MAX, DBL_MAX}, hi[3] = {-DBL_MAX, -DBL_MAX, -DBL_MAX};
+  for (const double* p : pts)
+    for (int k = 0; k < 3; ++k) {
+      const double pr = (ax[k] * p[0] + ax[3 + k] * p[1]) + ax[6 + k] * p[2];
+      if (pr > hi[k]) hi[k] = pr;
+      if (pr < lo[k]) lo[k] = pr;
+    }
+  double o[3];
+  for (int k = 0; k < 3; ++k) o[k] = (hi[k] + lo[k]) / 2;
+  for (int i = 0; i < 3; ++i) box[FB_TO + i] = (ax[3 * i] * o[0] + ax[3 * i + 1] * o[1]) + ax[3 * i + 2] * o[2];
+  for (int k = 0; k < 3; ++k) box[FB_EXT + k] = (hi[k] - lo[k]) * 0.5;
+}
+
+void fcl_bvh_node(FclBvh& B, const double* V, const int32_t* tri, std::vector<int>& prim, int id, int first, int n,
+                  int base) {
+  int* cur = prim.data() + first;
+  double S1[3] = {0, 0, 0}, S2[6] = {0, 0, 0, 0, 0, 0};
+  std::vector<const double*> pts;
+  pts.reserve(3 * (size_t)n);
+  for (int i = 0; i < n; ++i) {
+    const int32_t* t = tri + 3 * cur[i];
+    const double *p1 = V + 3 * t[0], *p2 = V + 3 * t[1], *p3 = V + 3 * t[2];
+    for (int k = 0; k < 3; ++k) S1[k] += (p1[k] + p2[k]) + p3[k];
+    S2[0] += (p1[0] * p1[0] + p2[0] * p2[0]) + p3[0] * p3[0];
+    S2[1] += (p1[1] * p1[1] + p2[1] * p2[1]) + p3[1] * p3[1];
+    S2[2] += (p1[2] * p1[2] + p2[2] * p2[2]) + p3[2] * p3[2];
+    S2[3] += (p1[0] * p1[1] + p2[0] * p2[1]) + p3[0] * p3[1];
+    S2[4] += (p1[0] * p1[2] + p2[0] * p2[2]) + p3[0] * p3[2];
+    S2[5] += (p1[1] * p1[2] + p2[1] * p2[2]) + p3[1] * p3[2];
+    pts.push_back(p1);
+    pts.push_back(p2);
+    pts.push_back(p3);
+  }
+  double* box = B.box.data() + (size_t)FB_STRIDE * (base + id);
+  fcl_fit_obb(S1, S2, 3.0 * n, pts, box);
+  int* lk = B.link.data() + 3 * (size_t)(base + id);
+  lk[1] = first;
+  lk[2] = n;
+  if (n == 1) {
+    lk[0] = -(cur[0] + 1);
+    return;
+  }
+  const double sv[3] = {box[FB_AXIS], box[FB_AXIS + 3], box[FB_AXIS + 6]};
+  double c[3] = {0, 0, 0};
+  for (int i = 0; i < n; ++i) {
+    const int32_t* t = tri + 3 * cur[i];
+    for (int k = 0; k < 3; ++k) c[k] += (V[3 * t[0] + k] + V[3 * t[1] + k]) + V[3 * t[2] + k];
+  }
+  const double split = ((c[0] * sv[0] + c[1] * sv[1]) + c[2] * sv[2]) / (3 * n);
+  const int child = (int)(B.link.size() / 3) - base;  // num_bvs
+  lk[0] = base + child;
+  B.box.resize(B.box.size() + 2 * FB_STRIDE);
+  B.link.resize(B.link.size() + 6);
+  int c1 = 0;
+  for (int i = 0; i < n; ++i) {
+    const int32_t* t = tri + 3 * cur[i];
+    double p[3];
+    for (int k = 0; k < 3; ++k) p[k] = ((V[3 * t[0] + k] + V[3 * t[1] + k]) + V[3 * t[2] + k]) / 3.0;
+    if (!(((sv[0] * p[0] + sv[1] * p[1]) + sv[2] * p[2]) > split)) std::swap(cur[i], cur[c1++]);
+  }
+  if (c1 == 0 || c1 == n) c1 = n / 2;
+  fcl_bvh_node(B, V, tri, prim, child, first, c1, base);
+  fcl_bvh_node(B, V, tri, prim, child + 1, first + c1, n - c1, base);
+}
+
+// computeBV<OBB>(shape, identity): box I / side/2; sphere I / r; capsule
+// I / (r, r, lz/2 + r); cylinder I / (r, r, lz/2); convex: fitn over the
+// vertices (covariance of the points)
+void fcl_shape_obb(const mpg_world_desc* d, int g, double* o) {
+  std::fill(o, o + FB_STRIDE, 0.0);
+  o[FB_AXIS] = o[FB_AXIS + 4] = o[FB_AXIS + 8] = 1.0;
+  const double* p = d->geom_param + 4 * g;
+  switch (d->geom_type[g]) {
+    case MPG_GEOM_BOX:
+      for (int k = 0; k < 3; ++k) o[FB_EXT + k] = p[k] * 0.5;
+      break;
+    case MPG_GEOM_SPHERE:
+      o[FB_EXT] = o[FB_EXT + 1] = o[FB_EXT + 2] = p[0];
+      break;
+    case MPG_GEOM_CAPSULE:
+      o[FB_EXT] = o[FB_EXT + 1] = p[0];
+      o[FB_EXT + 2] = p[1] / 2 + p[0];
+      break;
+    case MPG_GEOM_CYLINDER:
+      o[FB_EXT] = o[FB_EXT + 1] = p[0];
+      o[FB_EXT + 2] = p[1] / 2;
+      break;
+    case MPG_GEOM_CONVEX: {
+      const double* V = d->vertices + 3 * (size_t)d->geom_vertex_start[g];
+      const int nv = d->geom_vertex_count[g];
+      double S1[3] = {0, 0, 0}, S2[6] = {0, 0, 0, 0, 0, 0};
+      std::vector<const double*> pts;
+      for (int i = 0; i < nv; ++i) {
+        const double* q = V + 3 * i;
+        for (int k = 0; k < 3; ++k) S1[k] += q[k];
+        S2[0] += q[0] * q[0];
+        S2[1] += q[1] * q[1];
+        S2[2] += q[2] * q[2];
+        S2[3] += q[0] * q[1];
+        S2[4] += q[0] * q[2];
+        S2[5] += q[1] * q[2];
+        pts.push_back(q);
+      }
+      if (nv > 0) fcl_fit_obb(S1, S2, (double)nv, pts, o);
+      break;
+    }
+    default:
+      break;
+  }
+}
+
 void static_record(const mpg_world_desc* d, int s, const double* geom_rec_all, double* rec) {
   const double* T = d->static_transform + 12 * s;
   const CQ4 r = gjk_rot_from_matrix(T);  // the ccd_real rotation MPR uses
@@ -5995,6 +6340,24 @@ extern "C" {
 
 const char* mpg_last_error(void) { return g_last_error.c_str(); }
 
+int mpg_fcl_bvh_build(const double* vertices, int32_t n_vertices, const int32_t* triangles, int32_t n_triangles,
+                      double* boxes, int32_t* links, int32_t* leaf_order) {
+  if (n_triangles <= 0 || !vertices || !triangles || !boxes || !links || !leaf_order)
+    return set_error(MPG_E_INVALID, "mpg_fcl_bvh_build: empty mesh or NULL buffer");
+  for (int64_t i = 0; i < 3 * (int64_t)n_triangles; ++i)
+    if (triangles[i] < 0 || triangles[i] >= n_vertices) return set_error(MPG_E_INVALID, "triangle vertex out of range");
+  FclBvh B;
+  B.box.resize(FB_STRIDE);
+  B.link.resize(3);
+  std::vector<int> prim((size_t)n_triangles);
+  for (int t = 0; t < n_triangles; ++t) prim[t] = t;
+  fcl_bvh_node(B, vertices, triangles, prim, 0, 0, n_triangles, 0);
+  std::copy(B.box.begin(), B.box.end(), boxes);
+  std::copy(B.link.begin(), B.link.end(), links);
+  std::copy(prim.begin(), prim.end(), leaf_order);
+  return (int)(B.link.size() / 3);
+}
+
 int mpg_last_error_copy(char* buf, size_t size) {
   const size_t len = g_last_error.size();
   if (buf && size > 0) {
@@ -6190,6 +6553,30 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
   }
   if (mesh_node.empty()) mesh_node.assign(6, 0.0);
   if (mesh_link.empty()) mesh_link.assign(2, 0);
+  // FCL's BVHModel<OBBRSS> trees (the traversal gates of mesh pairs) and the
+  // shapes' computeBV OBBs
+  FclBvh fbvh;
+  std::vector<int> fb_root(std::max(d->n_geoms, 1), -1), tri_pos(std::max<int64_t>(d->n_mesh_triangles, 1), 0);
+  std::vector<double> sobb((size_t)FB_STRIDE * std::max(d->n_geoms, 1), 0.0);
+  for (int g = 0; g < d->n_geoms; ++g) {
+    fcl_shape_obb(d, g, sobb.data() + (size_t)FB_STRIDE * g);
+    if (d->geom_type[g] != MPG_GEOM_MESH) continue;
+    const int64_t t0 = (int64_t)d->geom_param[4 * g], tn = (int64_t)d->geom_param[4 * g + 1];
+    if (tn <= 0) continue;
+    const int base = (int)(fbvh.link.size() / 3);
+    fb_root[g] = base;
+    fbvh.box.resize(fbvh.box.size() + FB_STRIDE);
+    fbvh.link.resize(fbvh.link.size() + 3);
+    std::vector<int> prim((size_t)tn);
+    for (int64_t t = 0; t < tn; ++t) prim[t] = (int)t;
+    fcl_bvh_node(fbvh, d->vertices + 3 * (size_t)d->geom_vertex_start[g], d->mesh_triangle + 3 * t0, prim, 0, 0,
+                 (int)tn, base);
+    for (int64_t k = 0; k < tn; ++k) tri_pos[t0 + prim[k]] = (int)k;
+  }
+  if (fbvh.box.empty()) {
+    fbvh.box.assign(FB_STRIDE, 0.0);
+    fbvh.link.assign(3, 0);
+  }
   std::vector<double> oct_leaf(6 * (size_t)std::max<int64_t>(d->n_octree_leaves, 1), 0.0);
   if (d->n_octree_leaves > 0) std::copy(d->octree_leaf, d->octree_leaf + 6 * d->n_octree_leaves, oct_leaf.begin());
   std::vector<double> oct_grid((size_t)OG_STRIDE * std::max(d->n_geoms, 1), 0.0);
@@ -6478,6 +6865,11 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
   const size_t o_mnd = bb.add(mesh_node.data(), mesh_node.size());
   const size_t o_mln = bb.add(mesh_link.data(), mesh_link.size());
   const size_t o_mtt = bb.add(mesh_tree.data(), mesh_tree.size());
+  const size_t o_fbb = bb.add(fbvh.box.data(), fbvh.box.size());
+  const size_t o_fbl = bb.add(fbvh.link.data(), fbvh.link.size());
+  const size_t o_fbr = bb.add(fb_root.data(), fb_root.size());
+  const size_t o_tps = bb.add(tri_pos.data(), tri_pos.size());
+  const size_t o_sob = bb.add(sobb.data(), sobb.size());
   const size_t o_ogr = bb.add(oct_grid.data(), oct_grid.size());
   const size_t o_oce = bb.add(oct_cells.data(), oct_cells.size());
   const size_t o_oli = bb.add(oct_list.data(), oct_list.size());
@@ -6619,6 +7011,11 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
   dw.mesh_node = to_cptr<double>(base + o_mnd);
   dw.mesh_link = to_cptr<int>(base + o_mln);
   dw.mesh_tree = to_cptr<int>(base + o_mtt);
+  dw.fb_box = to_cptr<double>(base + o_fbb);
+  dw.fb_link = to_cptr<int>(base + o_fbl);
+  dw.fb_root = to_cptr<int>(base + o_fbr);
+  dw.tri_pos = to_cptr<int>(base + o_tps);
+  dw.sobb = to_cptr<double>(base + o_sob);
   dw.oct_grid = to_cptr<double>(base + o_ogr);
   dw.oct_cells = I(o_oce);
   dw.oct_list = I(o_oli);

@@ -165,6 +165,7 @@ class _World(ctypes.Structure):
         ("oct_leaf", _DP),
         ("mesh_tri", _IP),
         ("conv_nbr", _IP),
+        ("bvh", ctypes.c_void_p),
     ]
 
 
@@ -342,9 +343,30 @@ class OracleWorld:
         w.oct_leaf = da(np.concatenate(leaves) if leaves else [])
         w.mesh_tri = ia(np.concatenate(tris) if tris else [])
         w.conv_nbr = ia(nbr_all)
+        w.bvh = None
+        lib().orc_bvh_build(ctypes.byref(w))  # FCL BVHModel<OBBRSS> trees + shape OBBs
         self._w = w
         self.geoms = geoms
         self.dof = len(mg)
+
+    def __del__(self):
+        try:
+            if getattr(self, "_w", None) is not None and self._w.bvh:
+                lib().orc_bvh_free(ctypes.byref(self._w))
+        except Exception:  # interpreter shutdown
+            pass
+
+    def bvh_nodes(self, geom: int):
+        """The FCL BVHModel<OBBRSS> tree (OBB half) the oracle built for a mesh
+        geometry: (boxes[n, 15] = axis row-major 9, To 3, extent 3,
+        links[n, 3] = first_child, first_prim, num_prim)."""
+        out15, out3 = np.zeros(15), np.zeros(3, np.int32)
+        n = lib().orc_bvh_node(ctypes.byref(self._w), geom, -1, out15.ctypes.data_as(_DP), out3.ctypes.data_as(_IP))
+        boxes, links = np.zeros((max(n, 0), 15)), np.zeros((max(n, 0), 3), np.int32)
+        for k in range(max(n, 0)):
+            lib().orc_bvh_node(ctypes.byref(self._w), geom, k, out15.ctypes.data_as(_DP), out3.ctypes.data_as(_IP))
+            boxes[k], links[k] = out15, out3
+        return boxes, links
 
     def _pair_table(self):
         """(pairs, n_self) in PlanningWorldTpl::selfCollide then

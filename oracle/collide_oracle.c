@@ -120,6 +120,9 @@ typedef struct {
     /* convex hulls: FCL 0.7.0 Convex::neighbors_ encoding per geometry
      * (geom_param[0] = offset); NULL when not supplied */
     const int *conv_nbr;
+    /* FCL BVHModel<OBBRSS> trees of the mesh geometries and the OBBs FCL's
+     * computeBV gives every shape (orc_bvh_build; NULL until built) */
+    void *bvh;
 } orc_world;
 
 typedef struct {
@@ -2328,90 +2331,455 @@ static void bsphere(const real *const *P, int n, real *c, real *r) {
     *r = sqrt(m) * (1.0 + 1e-9) + 1e-9;
 }
 
-static int mesh_shape_intersect(const orc_world *w, int gm, const real *TM, int gs, const real *TS, orc_stats *st) {
-    const int t0 = (int)w->geom_param[4 * gm], tn = (int)w->geom_param[4 * gm + 1];
-    const int ts = w->geom_type[gs];
-    if (ts == GEOM_OCTREE || ts == GEOM_MESH) return 0; /* refused by the builder (oracle/__init__.py) */
-    /* shape bounding sphere in the world: about its origin (convex: about
-     * the farthest vertex from the origin) */
-    real rs = 0.0;
-    const real *ps = w->geom_param + 4 * gs;
-    if (ts == GEOM_CONVEX) {
-        const real *V = w->verts + 3 * (size_t)w->geom_vstart[gs];
-        for (int i = 0; i < w->geom_nv[gs]; ++i) rs = fmax(rs, dot3(V + 3 * i, V + 3 * i));
-        rs = sqrt(rs);
-    } else if (ts == GEOM_BOX) rs = 0.5 * sqrt(dot3(ps, ps));
-    else if (ts == GEOM_SPHERE) rs = ps[0];
-    else rs = sqrt(ps[0] * ps[0] + 0.25 * ps[1] * ps[1]) + (ts == GEOM_CAPSULE ? ps[0] : 0.0);
-    rs = rs * (1.0 + 1e-9) + 1e-9;
-    gjk_obj shape, tri;
-    int shape_ready = 0;
-    for (int t = t0; t < t0 + tn; ++t) {
-        const real *P[3];
-        mesh_tri_points(w, gm, t, P);
-        real W[3][3];
-        for (int k = 0; k < 3; ++k) tf_point(TM, P[k], W[k]);
-        const real *Wp[3] = {W[0], W[1], W[2]};
-        real c[3], r;
-        bsphere(Wp, 3, c, &r);
-        const real d[3] = {c[0] - TS[9], c[1] - TS[10], c[2] - TS[11]};
-        /* libccd's MPR can report a triangle within CCD_EPS^(1/4) of the
-         * shape as touching (discoverPortal's |v0 x v1|^2 < CCD_EPS exit, see
-         * DESIGN.md "Broad-phase soundness"): keep every such triangle */
-        const real pad = 1.001 * sqrt(sqrt((double)CCD_EPS)) + 1e-5 * (1.0 + fabs(TS[9]) + fabs(TS[10]) + fabs(TS[11]) + fabs(TM[9]) + fabs(TM[10]) + fabs(TM[11]));
-        if (sqrt(dot3(d, d)) > r + rs + pad) continue;
-        int hit;
-        if (ts == GEOM_SPHERE) hit = sphere_triangle_intersect(ps[0], TS, W[0], W[1], W[2]);
-        else {
-            if (!shape_ready) { make_obj(w, gs, TS, &shape, st); shape_ready = 1; }
-            memset(&tri, 0, sizeof tri);
-            shape_to_gjk(TM, &tri);
-            tri.type = GEOM_TRIANGLE;
-            tri.stats = st;
-            for (int k = 0; k < 3; ++k) ccdVec3Set(&tri.tp[k], P[k][0], P[k][1], P[k][2]);
-            ccdVec3Set(&tri.tc, (P[0][0] + P[1][0] + P[2][0]) / 3, (P[0][1] + P[1][1] + P[2][1]) / 3,
-                       (P[0][2] + P[1][2] + P[2][2]) / 3);
-            hit = mpr_intersect(&shape, &tri, 1e-6);
+/* ------------------------------------------ FCL 0.7.0 BVHModel<OBBRSS>
+ * [ext fcl/geometry/bvh/BVH_model-inl.h, BV_fitter-inl.h, BV_splitter-inl.h,
+ * fcl/math/bv/utility-inl.h, OBB-inl.h; restated from upstream knowledge:
+ * FCL is not under /root/reference, parity unpinned]
+ * load_mesh_as_BVH (src/urdf_utils.cpp:136-155) calls beginModel /
+ * addSubModel / endModel -> buildTree: primitive_indices = 0..T-1,
+ * recursiveBuildTree(0, 0, T): each node's BV = BVFitter<OBBRSS>::fit over its
+ * triangles (covariance of their 3 vertices each -> Jacobi eigen_old ->
+ * axisFromEigen -> extent and centre of the projections); the split rule is
+ * SPLIT_METHOD_MEAN along the OBB's first axis (split_value = the mean of the
+ * vertex sums . axis / (3 n)); a triangle whose centroid projects strictly
+ * above the value goes right, the others are swapped to the front; an empty
+ * side -> n / 2.  Children are allocated in pairs at num_bvs before
+ * recursing.  Only the OBB half of OBBRSS decides collisions
+ * (OBBRSS::overlap = obb.overlap), so the RSS half is not built.
+ * The device's snapshot builds the same tree independently
+ * (mplib_amd/csrc/mpg_kernels.hip build_fcl_bvh). */
+typedef struct {
+    double axis[9]; /* row-major; column k = the k-th box axis */
+    double To[3], ext[3];
+    int first_child, first_prim, num_prim; /* first_child < 0: leaf of triangle -(first_child + 1) */
+} bvh_node;
+typedef struct { int n_nodes; bvh_node *nodes; int *prim; } bvh_tree;
+typedef struct {
+    bvh_tree *tree;     /* [n_geom] (n_nodes 0 for non-mesh geometries) */
+    double (*sobb)[15]; /* [n_geom] computeBV<OBB>(shape, identity): axis 9, To 3, extent 3 */
+} orc_bvh;
+
+/* eigen_old (fcl/math/geometry-inl.h): Jacobi rotations of a symmetric 3x3;
+ * vout(r, c) = v[c][r] ("row first eigen-vectors"), dout = eigenvalues */
+static void eigen_old(const double m[9], double dout[3], double vout[9]) {
+    double R[9];
+    memcpy(R, m, sizeof R);
+    const int n = 3;
+    double b[3], z[3], v[3][3] = {{1, 0, 0}, {0, 1, 0}, {0, 0, 1}}, d[3];
+#define RR(i, j) R[3 * (i) + (j)]
+    for (int ip = 0; ip < n; ++ip) { b[ip] = d[ip] = RR(ip, ip); z[ip] = 0; }
+    for (int i = 0; i < 50; ++i) {
+        double sm = 0;
+        for (int ip = 0; ip < n; ++ip)
+            for (int iq = ip + 1; iq < n; ++iq) sm += fabs(RR(ip, iq));
+        if (sm == 0.0) {
+            for (int c = 0; c < 3; ++c)
+                for (int r = 0; r < 3; ++r) vout[3 * r + c] = v[c][r];
+            dout[0] = d[0]; dout[1] = d[1]; dout[2] = d[2];
+            return;
         }
-        if (hit) return 1;
+        const double tresh = i < 3 ? 0.2 * sm / (n * n) : 0.0;
+        for (int ip = 0; ip < n; ++ip) {
+            for (int iq = ip + 1; iq < n; ++iq) {
+                double g = 100.0 * fabs(RR(ip, iq)), h, t, theta, c, s, tau;
+                if (i > 3 && fabs(d[ip]) + g == fabs(d[ip]) && fabs(d[iq]) + g == fabs(d[iq])) RR(ip, iq) = 0.0;
+                else if (fabs(RR(ip, iq)) > tresh) {
+                    h = d[iq] - d[ip];
+                    if (fabs(h) + g == fabs(h)) t = RR(ip, iq) / h;
+                    else {
+                        theta = 0.5 * h / RR(ip, iq);
+                        t = 1.0 / (fabs(theta) + sqrt(1.0 + theta * theta));
+                        if (theta < 0.0) t = -t;
+                    }
+                    c = 1.0 / sqrt(1 + t * t);
+                    s = t * c;
+                    tau = s / (1.0 + c);
+                    h = t * RR(ip, iq);
+                    z[ip] -= h; z[iq] += h; d[ip] -= h; d[iq] += h;
+                    RR(ip, iq) = 0.0;
+                    for (int j = 0; j < ip; ++j) {
+                        g = RR(j, ip); h = RR(j, iq);
+                        RR(j, ip) = g - s * (h + g * tau); RR(j, iq) = h + s * (g - h * tau);
+                    }
+                    for (int j = ip + 1; j < iq; ++j) {
+                        g = RR(ip, j); h = RR(j, iq);
+                        RR(ip, j) = g - s * (h + g * tau); RR(j, iq) = h + s * (g - h * tau);
+                    }
+                    for (int j = iq + 1; j < n; ++j) {
+                        g = RR(ip, j); h = RR(iq, j);
+                        RR(ip, j) = g - s * (h + g * tau); RR(iq, j) = h + s * (g - h * tau);
+                    }
+                    for (int j = 0; j < n; ++j) {
+                        g = v[j][ip]; h = v[j][iq];
+                        v[j][ip] = g - s * (h + g * tau); v[j][iq] = h + s * (g - h * tau);
+                    }
+                }
+            }
+        }
+        for (int ip = 0; ip < n; ++ip) { b[ip] += z[ip]; d[ip] = b[ip]; z[ip] = 0.0; }
     }
+#undef RR
+    /* too many iterations: FCL prints and leaves the outputs as they were */
+}
+
+/* axisFromEigen: columns 0, 1 = eigenvectors of the largest / middle
+ * eigenvalue (rows of eigenV), column 2 = their cross product */
+static void axis_from_eigen(const double E[9], const double s[3], double axis[9]) {
+    int mn, mid, mx;
+    if (s[0] > s[1]) { mx = 0; mn = 1; } else { mn = 0; mx = 1; }
+    if (s[2] < s[mn]) { mid = mn; mn = 2; }
+    else if (s[2] > s[mx]) { mid = mx; mx = 2; }
+    else mid = 2;
+    (void)mn;
+    for (int r = 0; r < 3; ++r) { axis[3 * r] = E[3 * mx + r]; axis[3 * r + 1] = E[3 * mid + r]; }
+    const double a[3] = {axis[0], axis[3], axis[6]}, b[3] = {axis[1], axis[4], axis[7]};
+    axis[2] = a[1] * b[2] - a[2] * b[1];
+    axis[5] = a[2] * b[0] - a[0] * b[2];
+    axis[8] = a[0] * b[1] - a[1] * b[0];
+}
+
+/* getExtentAndCenter over a point list (pts[k] = 3 doubles) */
+static void extent_center(const double *const *pts, int np, const double axis[9], double To[3], double ext[3]) {
+    double mn[3] = {DBL_MAX, DBL_MAX, DBL_MAX}, mx[3] = {-DBL_MAX, -DBL_MAX, -DBL_MAX};
+    for (int i = 0; i < np; ++i) {
+        const double *p = pts[i];
+        for (int k = 0; k < 3; ++k) {
+            const double pr = (axis[k] * p[0] + axis[3 + k] * p[1]) + axis[6 + k] * p[2];
+            if (pr > mx[k]) mx[k] = pr;
+            if (pr < mn[k]) mn[k] = pr;
+        }
+    }
+    double o[3];
+    for (int k = 0; k < 3; ++k) o[k] = (mx[k] + mn[k]) / 2;
+    for (int i = 0; i < 3; ++i) To[i] = (axis[3 * i] * o[0] + axis[3 * i + 1] * o[1]) + axis[3 * i + 2] * o[2];
+    for (int k = 0; k < 3; ++k) ext[k] = (mx[k] - mn[k]) * 0.5;
+}
+
+/* BVFitter<OBBRSS>::fit over triangles idx[0..n) (OBB part) */
+static void fit_tris(const double *V, const int *tri, const int *idx, int n, bvh_node *nd) {
+    double S1[3] = {0, 0, 0}, S2[6] = {0, 0, 0, 0, 0, 0}; /* 00 11 22 01 02 12 */
+    for (int i = 0; i < n; ++i) {
+        const int *t = tri + 3 * idx[i];
+        const double *p1 = V + 3 * t[0], *p2 = V + 3 * t[1], *p3 = V + 3 * t[2];
+        for (int k = 0; k < 3; ++k) S1[k] += (p1[k] + p2[k]) + p3[k];
+        S2[0] += (p1[0] * p1[0] + p2[0] * p2[0]) + p3[0] * p3[0];
+        S2[1] += (p1[1] * p1[1] + p2[1] * p2[1]) + p3[1] * p3[1];
+        S2[2] += (p1[2] * p1[2] + p2[2] * p2[2]) + p3[2] * p3[2];
+        S2[3] += (p1[0] * p1[1] + p2[0] * p2[1]) + p3[0] * p3[1];
+        S2[4] += (p1[0] * p1[2] + p2[0] * p2[2]) + p3[0] * p3[2];
+        S2[5] += (p1[1] * p1[2] + p2[1] * p2[2]) + p3[1] * p3[2];
+    }
+    const double np = 3.0 * n;
+    double M[9], E[9], ev[3] = {0, 0, 0};
+    M[0] = S2[0] - S1[0] * S1[0] / np;
+    M[4] = S2[1] - S1[1] * S1[1] / np;
+    M[8] = S2[2] - S1[2] * S1[2] / np;
+    M[1] = M[3] = S2[3] - S1[0] * S1[1] / np;
+    M[5] = M[7] = S2[5] - S1[1] * S1[2] / np;
+    M[2] = M[6] = S2[4] - S1[0] * S1[2] / np;
+    memset(E, 0, sizeof E);
+    eigen_old(M, ev, E);
+    axis_from_eigen(E, ev, nd->axis);
+    const double **pts = malloc(sizeof(double *) * 3 * (size_t)n);
+    for (int i = 0; i < n; ++i)
+        for (int k = 0; k < 3; ++k) pts[3 * i + k] = V + 3 * tri[3 * idx[i] + k];
+    extent_center(pts, 3 * n, nd->axis, nd->To, nd->ext);
+    free(pts);
+}
+
+static void bvh_recurse(bvh_tree *T, const double *V, const int *tri, int id, int first, int n) {
+    bvh_node *nd = &T->nodes[id];
+    int *cur = T->prim + first;
+    fit_tris(V, tri, cur, n, nd);
+    nd->first_prim = first;
+    nd->num_prim = n;
+    if (n == 1) { nd->first_child = -(cur[0] + 1); return; }
+    /* computeRule_mean: split along axis column 0 */
+    const double sv[3] = {nd->axis[0], nd->axis[3], nd->axis[6]};
+    double c[3] = {0, 0, 0};
+    for (int i = 0; i < n; ++i) {
+        const int *t = tri + 3 * cur[i];
+        for (int k = 0; k < 3; ++k) c[k] += (V[3 * t[0] + k] + V[3 * t[1] + k]) + V[3 * t[2] + k];
+    }
+    const double split = ((c[0] * sv[0] + c[1] * sv[1]) + c[2] * sv[2]) / (3 * n);
+    nd->first_child = T->n_nodes;
+    T->n_nodes += 2;
+    int c1 = 0;
+    for (int i = 0; i < n; ++i) {
+        const int *t = tri + 3 * cur[i];
+        double p[3];
+        for (int k = 0; k < 3; ++k) p[k] = ((V[3 * t[0] + k] + V[3 * t[1] + k]) + V[3 * t[2] + k]) / 3.0;
+        if (!(((sv[0] * p[0] + sv[1] * p[1]) + sv[2] * p[2]) > split)) {
+            const int tmp = cur[i]; cur[i] = cur[c1]; cur[c1] = tmp; ++c1;
+        }
+    }
+    if (c1 == 0 || c1 == n) c1 = n / 2;
+    const int l = nd->first_child; /* nd may move? no: nodes is preallocated */
+    bvh_recurse(T, V, tri, l, first, c1);
+    bvh_recurse(T, V, tri, l + 1, first + c1, n - c1);
+}
+
+/* fit of an OBB to n > 3 points (fitn: covariance of the points) */
+static void fit_points(const double *P, int n, double axis[9], double To[3], double ext[3]) {
+    double S1[3] = {0, 0, 0}, S2[6] = {0, 0, 0, 0, 0, 0};
+    for (int i = 0; i < n; ++i) {
+        const double *p = P + 3 * i;
+        for (int k = 0; k < 3; ++k) S1[k] += p[k];
+        S2[0] += p[0] * p[0]; S2[1] += p[1] * p[1]; S2[2] += p[2] * p[2];
+        S2[3] += p[0] * p[1]; S2[4] += p[0] * p[2]; S2[5] += p[1] * p[2];
+    }
+    const double np = (double)n;
+    double M[9], E[9], ev[3] = {0, 0, 0};
+    M[0] = S2[0] - S1[0] * S1[0] / np;
+    M[4] = S2[1] - S1[1] * S1[1] / np;
+    M[8] = S2[2] - S1[2] * S1[2] / np;
+    M[1] = M[3] = S2[3] - S1[0] * S1[1] / np;
+    M[5] = M[7] = S2[5] - S1[1] * S1[2] / np;
+    M[2] = M[6] = S2[4] - S1[0] * S1[2] / np;
+    memset(E, 0, sizeof E);
+    eigen_old(M, ev, E);
+    axis_from_eigen(E, ev, axis);
+    const double **pts = malloc(sizeof(double *) * (size_t)n);
+    for (int i = 0; i < n; ++i) pts[i] = P + 3 * i;
+    extent_center(pts, n, axis, To, ext);
+    free(pts);
+}
+
+/* computeBV<OBB>(shape, identity) [ext fcl/geometry/shape/utility-inl.h]:
+ * box: axis I, extent side / 2; sphere: I, r; capsule: I, (r, r, lz / 2 + r);
+ * cylinder: I, (r, r, lz / 2); convex: fit over its vertices (then axis =
+ * R axis, To = R To + T at the shape's pose) */
+static void shape_obb(const orc_world *w, int g, double *o) {
+    memset(o, 0, sizeof(double) * 15);
+    o[0] = o[4] = o[8] = 1.0;
+    const double *p = w->geom_param + 4 * g;
+    switch (w->geom_type[g]) {
+    case GEOM_BOX: o[12] = p[0] * 0.5; o[13] = p[1] * 0.5; o[14] = p[2] * 0.5; break;
+    case GEOM_SPHERE: o[12] = o[13] = o[14] = p[0]; break;
+    case GEOM_CAPSULE: o[12] = o[13] = p[0]; o[14] = p[1] / 2 + p[0]; break;
+    case GEOM_CYLINDER: o[12] = o[13] = p[0]; o[14] = p[1] / 2; break;
+    case GEOM_CONVEX: fit_points(w->verts + 3 * (size_t)w->geom_vstart[g], w->geom_nv[g], o, o + 9, o + 12); break;
+    default: break;
+    }
+}
+
+int orc_bvh_build(orc_world *w) {
+    orc_bvh *B = calloc(1, sizeof *B);
+    B->tree = calloc((size_t)w->n_geom, sizeof(bvh_tree));
+    B->sobb = calloc((size_t)w->n_geom, sizeof *B->sobb);
+    for (int g = 0; g < w->n_geom; ++g) {
+        shape_obb(w, g, B->sobb[g]);
+        if (w->geom_type[g] != GEOM_MESH) continue;
+        const int t0 = (int)w->geom_param[4 * g], tn = (int)w->geom_param[4 * g + 1];
+        if (tn <= 0) continue;
+        bvh_tree *T = &B->tree[g];
+        T->nodes = calloc((size_t)(2 * tn - 1), sizeof(bvh_node));
+        T->prim = malloc(sizeof(int) * (size_t)tn);
+        for (int i = 0; i < tn; ++i) T->prim[i] = i;
+        T->n_nodes = 1;
+        bvh_recurse(T, w->verts + 3 * (size_t)w->geom_vstart[g], w->mesh_tri + 3 * (size_t)t0, 0, 0, tn);
+    }
+    w->bvh = B;
     return 0;
 }
 
-static int mesh_mesh_intersect(const orc_world *w, int ga, const real *TA, int gb, const real *TB) {
-    const int a0 = (int)w->geom_param[4 * ga], an = (int)w->geom_param[4 * ga + 1];
-    const int b0 = (int)w->geom_param[4 * gb], bn = (int)w->geom_param[4 * gb + 1];
+void orc_bvh_free(orc_world *w) {
+    orc_bvh *B = w->bvh;
+    if (!B) return;
+    for (int g = 0; g < w->n_geom; ++g) { free(B->tree[g].nodes); free(B->tree[g].prim); }
+    free(B->tree); free(B->sobb); free(B);
+    w->bvh = NULL;
+}
+
+/* test access: node k of geometry g -> axis 9, To 3, ext 3, first_child,
+ * first_prim, num_prim; returns the node count */
+int orc_bvh_node(const orc_world *w, int g, int k, double *out15, int *out3) {
+    const orc_bvh *B = w->bvh;
+    if (!B || g < 0 || g >= w->n_geom) return -1;
+    const bvh_tree *T = &B->tree[g];
+    if (k >= 0 && k < T->n_nodes) {
+        memcpy(out15, T->nodes[k].axis, 9 * sizeof(double));
+        memcpy(out15 + 9, T->nodes[k].To, 3 * sizeof(double));
+        memcpy(out15 + 12, T->nodes[k].ext, 3 * sizeof(double));
+        out3[0] = T->nodes[k].first_child; out3[1] = T->nodes[k].first_prim; out3[2] = T->nodes[k].num_prim;
+    }
+    return T->n_nodes;
+}
+
+/* overlap(R0, T0, b1, b2) (fcl/math/bv/OBB-inl.h): b2 in the frame (R0, T0)
+ * relative to b1's: R = b1.axis^T (R0 b2.axis), T = (R0 b2.To + T0 -
+ * b1.To)^T b1.axis, then obbDisjoint(R, T, b1.extent, b2.extent) */
+static int obb_overlap_rel(const double R0[9], const double T0[3], const double *a_axis, const double *a_To,
+                           const double *a_ext, const double *b_axis, const double *b_To, const double *b_ext) {
+    double R0b2[9], R[9], Tt[3], T[3];
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j)
+            R0b2[3 * i + j] = (R0[3 * i] * b_axis[j] + R0[3 * i + 1] * b_axis[3 + j]) + R0[3 * i + 2] * b_axis[6 + j];
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j)
+            R[3 * i + j] = (a_axis[i] * R0b2[j] + a_axis[3 + i] * R0b2[3 + j]) + a_axis[6 + i] * R0b2[6 + j];
+    for (int i = 0; i < 3; ++i)
+        Tt[i] = ((((R0[3 * i] * b_To[0] + R0[3 * i + 1] * b_To[1]) + R0[3 * i + 2] * b_To[2]) + T0[i]) - a_To[i]);
+    for (int j = 0; j < 3; ++j) T[j] = (Tt[0] * a_axis[j] + Tt[1] * a_axis[3 + j]) + Tt[2] * a_axis[6 + j];
+    return !obb_disjoint(R, T, a_ext, b_ext);
+}
+
+/* the shape's OBB in the world (ComputeBVImpl<OBB, Convex>: axis = R axis,
+ * To = R To + T; the primitives: axis = R (sphere: I), To = T) */
+static void shape_obb_world(const orc_world *w, int gs, const real *TS, double axis[9], double To[3], double ext[3]) {
+    const double *o = ((const orc_bvh *)w->bvh)->sobb[gs];
+    const int ts = w->geom_type[gs];
+    if (ts == GEOM_SPHERE) memcpy(axis, o, 9 * sizeof(double));
+    else
+        for (int i = 0; i < 3; ++i)
+            for (int j = 0; j < 3; ++j) axis[3 * i + j] = (TS[3 * i] * o[j] + TS[3 * i + 1] * o[3 + j]) + TS[3 * i + 2] * o[6 + j];
+    for (int i = 0; i < 3; ++i) To[i] = ((TS[3 * i] * o[9] + TS[3 * i + 1] * o[10]) + TS[3 * i + 2] * o[11]) + TS[9 + i];
+    memcpy(ext, o + 12, 3 * sizeof(double));
+}
+
+static void tri_gjk_obj(const orc_world *w, int gm, const gjk_obj *frame, int t, gjk_obj *tri);
+static int tri_tri_contact(const real *P1, const real *P2, const real *P3, const real *Q1, const real *Q2,
+                           const real *Q3, real *point, real *normal, real *depth);
+static int sphere_triangle_contact(real radius, const real *TS, const real *P1, const real *P2, const real *P3,
+                                   real *depth, real *normal, real *pos);
+
+/* MeshShapeCollisionTraversalNodeOBBRSS under collisionRecurse
+ * [ext fcl/narrowphase/detail/traversal/collision_node-inl.h]: BVTesting =
+ * !overlap(tf_mesh.linear(), tf_mesh.translation(), shape OBB (world), node
+ * OBB); a leaf is tested only when its own OBB overlaps too; left child
+ * first; the walk stops at the first hit (canStop with num_max_contacts 1). */
+typedef int (*tri_leaf_fn)(void *ctx, int tri);
+static int bvh_shape_walk(const bvh_tree *T, int b, const real *TM, const double *sa, const double *sT,
+                          const double *se, tri_leaf_fn f, void *ctx) {
+    const bvh_node *nd = &T->nodes[b];
+    if (!obb_overlap_rel(TM, TM + 9, sa, sT, se, nd->axis, nd->To, nd->ext)) return 0;
+    if (nd->first_child < 0) return f(ctx, -(nd->first_child + 1));
+    if (bvh_shape_walk(T, nd->first_child, TM, sa, sT, se, f, ctx)) return 1;
+    return bvh_shape_walk(T, nd->first_child + 1, TM, sa, sT, se, f, ctx);
+}
+
+/* MeshCollisionTraversalNodeOBBRSS: BVTesting = !overlap(R, T, bv1, bv2) with
+ * R = R1^T R2, T = R1^T (t2 - t1); firstOverSecond descends the first tree
+ * when the second node is a leaf or the first is not and its OBB is larger
+ * (OBB::size = extent squaredNorm) */
+typedef int (*tri_pair_fn)(void *ctx, int ta, int tb);
+static double obb_size(const bvh_node *n) { return (n->ext[0] * n->ext[0] + n->ext[1] * n->ext[1]) + n->ext[2] * n->ext[2]; }
+static int bvh_mesh_walk(const bvh_tree *A, int a, const bvh_tree *B, int b, const double *R, const double *T,
+                         tri_pair_fn f, void *ctx) {
+    const bvh_node *na = &A->nodes[a], *nb = &B->nodes[b];
+    if (!obb_overlap_rel(R, T, na->axis, na->To, na->ext, nb->axis, nb->To, nb->ext)) return 0;
+    const int la = na->first_child < 0, lb = nb->first_child < 0;
+    if (la && lb) return f(ctx, -(na->first_child + 1), -(nb->first_child + 1));
+    if (lb || (!la && obb_size(na) > obb_size(nb))) {
+        if (bvh_mesh_walk(A, na->first_child, B, b, R, T, f, ctx)) return 1;
+        return bvh_mesh_walk(A, na->first_child + 1, B, b, R, T, f, ctx);
+    }
+    if (bvh_mesh_walk(A, a, B, nb->first_child, R, T, f, ctx)) return 1;
+    return bvh_mesh_walk(A, a, B, nb->first_child + 1, R, T, f, ctx);
+}
+
+typedef struct {
+    const orc_world *w;
+    int gm, gs, ts, mesh_first, contact;
+    const real *TM, *TS;
+    gjk_obj shape;
+    orc_stats *st;
+    real *depth, *normal, *pos;
+} ms_ctx;
+
+/* the leaf test: shapeTriangleIntersect(shape, tf_shape, P1, P2, P3,
+ * tf_mesh) -- sphereTriangleIntersect for spheres, libccd MPR on the
+ * triangle GJK object otherwise; with contacts their contact output */
+static int ms_leaf(void *vc, int t) {
+    ms_ctx *c = vc;
+    const orc_world *w = c->w;
+    const int tt = (int)w->geom_param[4 * c->gm] + t;
+    const real *P[3];
+    mesh_tri_points(w, c->gm, tt, P);
+    const real *ps = w->geom_param + 4 * c->gs;
+    int hit;
+    if (c->ts == GEOM_SPHERE) {
+        real W[3][3];
+        for (int k = 0; k < 3; ++k) tf_point(c->TM, P[k], W[k]);
+        hit = c->contact ? sphere_triangle_contact(ps[0], c->TS, W[0], W[1], W[2], c->depth, c->normal, c->pos)
+                         : sphere_triangle_intersect(ps[0], c->TS, W[0], W[1], W[2]);
+    } else {
+        gjk_obj tri;
+        memset(&tri, 0, sizeof tri);
+        shape_to_gjk(c->TM, &tri);
+        tri.stats = c->st;
+        tri_gjk_obj(w, c->gm, &tri, tt, &tri);
+        hit = c->contact ? mpr_penetration(&c->shape, &tri, 1e-6, c->depth, c->normal, c->pos)
+                         : mpr_intersect(&c->shape, &tri, 1e-6);
+    }
+    return hit;
+}
+
+static int mesh_shape_run(const orc_world *w, int gm, const real *TM, int gs, const real *TS, orc_stats *st,
+                          int contact, int mesh_first, real *depth, real *normal, real *pos) {
+    const int ts = w->geom_type[gs];
+    if (ts == GEOM_OCTREE || ts == GEOM_MESH) return 0; /* refused by the builder (oracle/__init__.py) */
+    const bvh_tree *T = &((const orc_bvh *)w->bvh)->tree[gm];
+    if (T->n_nodes == 0) return 0;
+    ms_ctx c;
+    memset(&c, 0, sizeof c);
+    c.w = w; c.gm = gm; c.gs = gs; c.ts = ts; c.TM = TM; c.TS = TS; c.st = st; c.contact = contact;
+    c.mesh_first = mesh_first; c.depth = depth; c.normal = normal; c.pos = pos;
+    if (ts != GEOM_SPHERE) make_obj(w, gs, TS, &c.shape, st);
+    double sa[9], sT[3], se[3];
+    shape_obb_world(w, gs, TS, sa, sT, se);
+    return bvh_shape_walk(T, 0, TM, sa, sT, se, ms_leaf, &c);
+}
+
+typedef struct {
+    const orc_world *w;
+    int ga, gb, contact;
+    const real *R, *T, *TA;
+    real *depth, *normal, *pos;
+} mm_ctx;
+
+static int mm_leaf(void *vc, int ta, int tb) {
+    mm_ctx *c = vc;
+    const orc_world *w = c->w;
+    const real *P[3], *Q[3];
+    mesh_tri_points(w, c->ga, (int)w->geom_param[4 * c->ga] + ta, P);
+    mesh_tri_points(w, c->gb, (int)w->geom_param[4 * c->gb] + tb, Q);
+    real QB[9];
+    for (int k = 0; k < 3; ++k)
+        for (int i = 0; i < 3; ++i)
+            QB[3 * k + i] = ((c->R[3 * i] * Q[k][0] + c->R[3 * i + 1] * Q[k][1]) + c->R[3 * i + 2] * Q[k][2]) + c->T[i];
+    if (!tri_tri_intersect(P[0], P[1], P[2], QB, QB + 3, QB + 6)) return 0;
+    if (c->contact) {
+        real pt[3], nl[3], pen;
+        if (tri_tri_contact(P[0], P[1], P[2], QB, QB + 3, QB + 6, pt, nl, &pen) > 0) {
+            tf_point(c->TA, pt, c->pos);
+            for (int k = 0; k < 3; ++k) c->normal[k] = (c->TA[3 * k] * nl[0] + c->TA[3 * k + 1] * nl[1]) + c->TA[3 * k + 2] * nl[2];
+            *c->depth = pen;
+        }
+    }
+    return 1;
+}
+
+static int mesh_mesh_run(const orc_world *w, int ga, const real *TA, int gb, const real *TB, int contact, real *depth,
+                         real *normal, real *pos) {
+    const orc_bvh *B = w->bvh;
+    const bvh_tree *A = &B->tree[ga], *Bt = &B->tree[gb];
+    if (A->n_nodes == 0 || Bt->n_nodes == 0) return 0;
     real R[9], T[3], dt[3];
     for (int i = 0; i < 3; ++i)
         for (int j = 0; j < 3; ++j) R[3 * i + j] = (TA[i] * TB[j] + TA[3 + i] * TB[3 + j]) + TA[6 + i] * TB[6 + j];
     for (int k = 0; k < 3; ++k) dt[k] = TB[9 + k] - TA[9 + k];
     for (int i = 0; i < 3; ++i) T[i] = (TA[i] * dt[0] + TA[3 + i] * dt[1]) + TA[6 + i] * dt[2];
-    real (*QB)[9] = malloc(sizeof(real) * 9 * (size_t)(bn > 0 ? bn : 1));
-    real (*SB)[4] = malloc(sizeof(real) * 4 * (size_t)(bn > 0 ? bn : 1));
-    for (int j = 0; j < bn; ++j) {
-        const real *Q[3];
-        mesh_tri_points(w, gb, b0 + j, Q);
-        for (int k = 0; k < 3; ++k)
-            for (int i = 0; i < 3; ++i)
-                QB[j][3 * k + i] = ((R[3 * i] * Q[k][0] + R[3 * i + 1] * Q[k][1]) + R[3 * i + 2] * Q[k][2]) + T[i];
-        const real *Qp[3] = {QB[j], QB[j] + 3, QB[j] + 6};
-        bsphere(Qp, 3, SB[j], &SB[j][3]);
-    }
-    int hit = 0;
-    for (int i = 0; i < an && !hit; ++i) {
-        const real *P[3];
-        mesh_tri_points(w, ga, a0 + i, P);
-        real c[3], r;
-        bsphere(P, 3, c, &r);
-        for (int j = 0; j < bn; ++j) {
-            const real d[3] = {c[0] - SB[j][0], c[1] - SB[j][1], c[2] - SB[j][2]};
-            if (sqrt(dot3(d, d)) > r + SB[j][3]) continue;
-            if (tri_tri_intersect(P[0], P[1], P[2], QB[j], QB[j] + 3, QB[j] + 6)) { hit = 1; break; }
-        }
-    }
-    free(QB);
-    free(SB);
-    return hit;
+    mm_ctx c = {w, ga, gb, contact, R, T, TA, depth, normal, pos};
+    return bvh_mesh_walk(A, 0, Bt, 0, R, T, mm_leaf, &c);
+}
+
+static int mesh_shape_intersect(const orc_world *w, int gm, const real *TM, int gs, const real *TS, orc_stats *st) {
+    return mesh_shape_run(w, gm, TM, gs, TS, st, 0, 0, NULL, NULL, NULL);
+}
+
+static int mesh_mesh_intersect(const orc_world *w, int ga, const real *TA, int gb, const real *TB) {
+    return mesh_mesh_run(w, ga, TA, gb, TB, 0, NULL, NULL, NULL);
 }
 
 /* triCreateGJKObject(P1, P2, P3, tf_mesh): the mesh transform, the vertices
@@ -2678,98 +3046,21 @@ static void zero_contact(real *depth, real *normal, real *pos) {
     for (int k = 0; k < 3; ++k) normal[k] = pos[k] = 0.0;
 }
 
+/* the contact of the first leaf test that hits in FCL's traversal order */
 static int mesh_mesh_contact(const orc_world *w, int ga, const real *TA, int gb, const real *TB, real *depth,
                              real *normal, real *pos) {
-    const int a0 = (int)w->geom_param[4 * ga], an = (int)w->geom_param[4 * ga + 1];
-    const int b0 = (int)w->geom_param[4 * gb], bn = (int)w->geom_param[4 * gb + 1];
-    real R[9], T[3], dt[3];
-    for (int i = 0; i < 3; ++i)
-        for (int j = 0; j < 3; ++j) R[3 * i + j] = (TA[i] * TB[j] + TA[3 + i] * TB[3 + j]) + TA[6 + i] * TB[6 + j];
-    for (int k = 0; k < 3; ++k) dt[k] = TB[9 + k] - TA[9 + k];
-    for (int i = 0; i < 3; ++i) T[i] = (TA[i] * dt[0] + TA[3 + i] * dt[1]) + TA[6 + i] * dt[2];
-    real (*QB)[9] = malloc(sizeof(real) * 9 * (size_t)(bn > 0 ? bn : 1));
-    real (*SB)[4] = malloc(sizeof(real) * 4 * (size_t)(bn > 0 ? bn : 1));
-    for (int j = 0; j < bn; ++j) {
-        const real *Q[3];
-        mesh_tri_points(w, gb, b0 + j, Q);
-        for (int k = 0; k < 3; ++k)
-            for (int i = 0; i < 3; ++i)
-                QB[j][3 * k + i] = ((R[3 * i] * Q[k][0] + R[3 * i + 1] * Q[k][1]) + R[3 * i + 2] * Q[k][2]) + T[i];
-        const real *Qp[3] = {QB[j], QB[j] + 3, QB[j] + 6};
-        bsphere(Qp, 3, SB[j], &SB[j][3]);
-    }
-    int hit = 0;
     zero_contact(depth, normal, pos);
-    for (int i = 0; i < an && !hit; ++i) {
-        const real *P[3];
-        mesh_tri_points(w, ga, a0 + i, P);
-        real c[3], r;
-        bsphere(P, 3, c, &r);
-        for (int j = 0; j < bn; ++j) {
-            const real d[3] = {c[0] - SB[j][0], c[1] - SB[j][1], c[2] - SB[j][2]};
-            if (sqrt(dot3(d, d)) > r + SB[j][3]) continue;
-            if (!tri_tri_intersect(P[0], P[1], P[2], QB[j], QB[j] + 3, QB[j] + 6)) continue;
-            hit = 1;
-            real pt[3], nl[3], pen;
-            if (tri_tri_contact(P[0], P[1], P[2], QB[j], QB[j] + 3, QB[j] + 6, pt, nl, &pen) > 0) {
-                tf_point(TA, pt, pos);
-                for (int k = 0; k < 3; ++k) normal[k] = (TA[3 * k] * nl[0] + TA[3 * k + 1] * nl[1]) + TA[3 * k + 2] * nl[2];
-                *depth = pen;
-            }
-            break;
-        }
-    }
-    free(QB);
-    free(SB);
-    return hit;
+    return mesh_mesh_run(w, ga, TA, gb, TB, 1, depth, normal, pos);
 }
 
 static int mesh_shape_contact(const orc_world *w, int gm, const real *TM, int gs, const real *TS, int mesh_first,
                               real *depth, real *normal, real *pos) {
-    const int t0 = (int)w->geom_param[4 * gm], tn = (int)w->geom_param[4 * gm + 1];
-    const int ts = w->geom_type[gs];
-    real rs = 0.0;  /* as mesh_shape_intersect */
-    const real *ps = w->geom_param + 4 * gs;
-    if (ts == GEOM_CONVEX) {
-        const real *V = w->verts + 3 * (size_t)w->geom_vstart[gs];
-        for (int i = 0; i < w->geom_nv[gs]; ++i) rs = fmax(rs, dot3(V + 3 * i, V + 3 * i));
-        rs = sqrt(rs);
-    } else if (ts == GEOM_BOX) rs = 0.5 * sqrt(dot3(ps, ps));
-    else if (ts == GEOM_SPHERE) rs = ps[0];
-    else rs = sqrt(ps[0] * ps[0] + 0.25 * ps[1] * ps[1]) + (ts == GEOM_CAPSULE ? ps[0] : 0.0);
-    rs = rs * (1.0 + 1e-9) + 1e-9;
-    gjk_obj shape, tri;
-    int shape_ready = 0;
     zero_contact(depth, normal, pos);
-    for (int t = t0; t < t0 + tn; ++t) {
-        const real *P[3];
-        mesh_tri_points(w, gm, t, P);
-        real W[3][3];
-        for (int k = 0; k < 3; ++k) tf_point(TM, P[k], W[k]);
-        const real *Wp[3] = {W[0], W[1], W[2]};
-        real c[3], r;
-        bsphere(Wp, 3, c, &r);
-        const real d[3] = {c[0] - TS[9], c[1] - TS[10], c[2] - TS[11]};
-        const real pad = 1.001 * sqrt(sqrt((double)CCD_EPS)) + 1e-5 * (1.0 + fabs(TS[9]) + fabs(TS[10]) + fabs(TS[11]) + fabs(TM[9]) + fabs(TM[10]) + fabs(TM[11]));
-        if (sqrt(dot3(d, d)) > r + rs + pad) continue;
-        int hit;
-        if (ts == GEOM_SPHERE) {
-            hit = sphere_triangle_contact(ps[0], TS, W[0], W[1], W[2], depth, normal, pos);
-        } else {
-            if (!shape_ready) { make_obj(w, gs, TS, &shape, NULL); shape_ready = 1; }
-            memset(&tri, 0, sizeof tri);
-            shape_to_gjk(TM, &tri);
-            tri_gjk_obj(w, gm, &tri, t, &tri);
-            hit = mpr_penetration(&shape, &tri, 1e-6, depth, normal, pos);
-        }
-        if (hit) {
-            if (mesh_first)
-                for (int k = 0; k < 3; ++k) normal[k] = -normal[k];
-            return 1;
-        }
-    }
-    zero_contact(depth, normal, pos);
-    return 0;
+    const int hit = mesh_shape_run(w, gm, TM, gs, TS, NULL, 1, mesh_first, depth, normal, pos);
+    if (!hit) { zero_contact(depth, normal, pos); return 0; }
+    if (mesh_first)
+        for (int k = 0; k < 3; ++k) normal[k] = -normal[k];
+    return 1;
 }
 
 static int mesh_octree_contact(const orc_world *w, int gm, const real *TM, int go, const real *TO, real *depth,
