@@ -5569,6 +5569,14 @@ struct mpg_world {
   double* d_qs = nullptr;      // device input of the latency path
   double* d_qmap = nullptr;    // h_q as the device sees it (zero-copy input)
   double* d_ssc = nullptr;     // latency path joint (sin, cos) [small cap * dof * 2]
+  double* h_ssc = nullptr;     // pinned host-mapped twin: sin/cos computed on the host (small batches)
+  double* d_sscmap = nullptr;  // h_ssc as the device sees it
+  int64_t small_host_sc = 64;  // latency batches up to this size: sin/cos on the host (MPG_SMALL_HOST_SC)
+  std::vector<int> h_rev_src;  // move-group slots of revolute joints (host copy of the snapshot's rule)
+  // host-buffer calls without a stream run on this non-blocking stream (not
+  // the legacy default stream, whose synchronisation covers every blocking
+  // stream of the device); MPG_OWN_STREAM=0 keeps the caller's NULL stream
+  hipStream_t own_stream = nullptr;
   bool small_zero_copy = true; // MPG_SMALL_ZEROCOPY=0: stage through d_qs
   int64_t small_inline_sc = 256;  // latency batches up to this size: sin/cos inline (MPG_SMALL_INLINE_SC)
   size_t small_cap = 0;   // configurations (hit bytes per pair)
@@ -7033,6 +7041,13 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
   if (const char* e = std::getenv("MPG_OVERLAP_MIN")) w->overlap_min = std::atoll(e);
   if (const char* e = std::getenv("MPG_SMALL_INLINE_SC")) w->small_inline_sc = std::atoll(e);
   if (const char* e = std::getenv("MPG_OVERLAP_PARTS")) w->overlap_parts = std::atoi(e);
+  if (const char* e = std::getenv("MPG_SMALL_HOST_SC")) w->small_host_sc = std::atoll(e);
+  for (int j = 0; j < d->n_joints; ++j)
+    if (d->joint_q_source[j] >= 0 && joint_is_revolute(d->joint_type[j]) &&
+        std::find(w->h_rev_src.begin(), w->h_rev_src.end(), d->joint_q_source[j]) == w->h_rev_src.end())
+      w->h_rev_src.push_back(d->joint_q_source[j]);
+  const char* own = std::getenv("MPG_OWN_STREAM");
+  if (!own || std::atoi(own) != 0) HIP_TRY(hipStreamCreateWithFlags(&w->own_stream, hipStreamNonBlocking));
   *out = w;
   return MPG_OK;
 }
@@ -7059,6 +7074,8 @@ int mpg_world_destroy(mpg_world* w) {
   if (w->h_hits) hipHostFree(w->h_hits);
   hipFree(w->d_qs);
   if (w->d_ssc) hipFree(w->d_ssc);
+  if (w->h_ssc) hipHostFree(w->h_ssc);
+  if (w->own_stream) hipStreamDestroy(w->own_stream);
   for (auto& kv : w->sides) {
     hipStreamDestroy(kv.second.side);
     hipEventDestroy(kv.second.fork);
@@ -7124,7 +7141,9 @@ int ensure_small(mpg_world* w, size_t ncfg, size_t row) {
   if (w->h_hits) hipHostFree(w->h_hits);
   if (w->d_qs) hipFree(w->d_qs);
   if (w->d_ssc) hipFree(w->d_ssc);
+  if (w->h_ssc) hipHostFree(w->h_ssc);
   w->d_ssc = nullptr;
+  w->h_ssc = nullptr;
   w->h_q = nullptr;
   w->h_hits = nullptr;
   w->d_qs = nullptr;
@@ -7137,6 +7156,9 @@ int ensure_small(mpg_world* w, size_t ncfg, size_t row) {
   HIP_TRY(hipHostGetDevicePointer((void**)&w->d_hits, w->h_hits, 0));
   HIP_TRY(hipMalloc(&w->d_qs, sizeof(double) * qcap));
   HIP_TRY(hipMalloc(&w->d_ssc, sizeof(double) * 2 * ncfg * std::max<int>(w->dw.dof, 1)));
+  HIP_TRY(hipHostMalloc((void**)&w->h_ssc, sizeof(double) * 2 * ncfg * std::max<int>(w->dw.dof, 1),
+                        hipHostMallocMapped | hipHostMallocCoherent));
+  HIP_TRY(hipHostGetDevicePointer((void**)&w->d_sscmap, w->h_ssc, 0));
   w->small_cap = ncfg;
   w->small_qcap = qcap;
   return MPG_OK;
@@ -7165,9 +7187,25 @@ int collide_small(mpg_world* w, const double* q, int64_t n, uint8_t* flags, uint
   const long long waves = (long long)P * n_tiles;
   StageTimer t_small(w, s, MPG_STAGE_NARROW);
   if (w->prof) w->prof_cfg += n;
-  // batches of up to kSmallInlineSc states: one launch (sin/cos inline)
-  const bool inline_sc = FROM_POSES || (n <= w->small_inline_sc && w->dw.dof <= kLatScDof);
-  if (!inline_sc && w->dw.dof > 0) {
+  // the smallest batches: joint sin/cos on the host (mpg_sincos, the device's
+  // own restatement of glibc's, bit for bit) into pinned mapped memory, one
+  // launch without the sin/cos work; up to small_inline_sc states: one launch
+  // with sin/cos inline; larger: a sin/cos launch first
+  const bool host_sc = !FROM_POSES && w->dw.dof > 0 && n <= w->small_host_sc;
+  const bool inline_sc = !host_sc && (FROM_POSES || (n <= w->small_inline_sc && w->dw.dof <= kLatScDof));
+  double* sc_src = w->d_ssc;
+  if (host_sc) {
+    const int dof = w->dw.dof;
+    for (int64_t c = 0; c < n; ++c)
+      for (const int src : w->h_rev_src) {
+        double sv, cv;
+        mpg_sincos(q[c * dof + src], &sv, &cv);
+        w->h_ssc[(c * dof + src) * 2] = sv;
+        w->h_ssc[(c * dof + src) * 2 + 1] = cv;
+      }
+    sc_src = w->d_sscmap;
+  }
+  if (!inline_sc && !host_sc && w->dw.dof > 0) {
     const long long nt = n * w->dw.dof;
     hipLaunchKernelGGL(small_sincos_kernel, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, s, w->dw, qin,
                        (long long)n, w->d_ssc);
@@ -7175,7 +7213,7 @@ int collide_small(mpg_world* w, const double* q, int64_t n, uint8_t* flags, uint
   }
   const dim3 grid((unsigned)((waves + 3) / 4));
   auto launch = [&](auto kern) {  // every class instance reads the same sin/cos source
-    hipLaunchKernelGGL(kern, grid, dim3(256), 0, s, w->dw, qin, (long long)n, n_tiles, w->d_hits, w->d_ssc);
+    hipLaunchKernelGGL(kern, grid, dim3(256), 0, s, w->dw, qin, (long long)n, n_tiles, w->d_hits, sc_src);
     return hipGetLastError();
   };
   HIP_TRY(inline_sc ? launch(small_kernel<FROM_POSES, CLS_CLOSED, true>) : launch(small_kernel<FROM_POSES, CLS_CLOSED>));
@@ -7255,6 +7293,7 @@ int collide_common(mpg_world* w, const double* q, int64_t n, uint8_t* flags, uin
   if (mem == MPG_MEM_DEVICE) return launch_collide_overlapped<FROM_POSES>(w, q, n, flags, pair_mask, s);
   if (mem != MPG_MEM_HOST) return set_error(MPG_E_INVALID, "bad mem kind");
   std::lock_guard<std::mutex> lk(w->host_mu);
+  if (!s && w->own_stream) s = w->own_stream;
   if (n > 0 && n <= w->small_max) return collide_small<FROM_POSES>(w, q, n, flags, pair_mask, s);
   int rc = ensure_staging(w, (size_t)n, std::max<size_t>(1, (size_t)n * row));
   if (rc) return rc;
