@@ -2076,6 +2076,7 @@ __device__ __forceinline__ bool mesh_mesh_wave(const DevWorld& w, int ga, const 
       double Qk[9], lk[3], hk[3];
 #pragma unroll
       for (int i = 0; i < 9; ++i) Qk[i] = bcast(Q[i], k);
+      const int tbk = (int)bcast(rq[TR_ID], k);  // B's triangle (read while every lane is active)
 #pragma unroll
       for (int i = 0; i < 3; ++i) {
         lk[i] = bcast(qlo[i], k);
@@ -2109,8 +2110,7 @@ __device__ __forceinline__ bool mesh_mesh_wave(const DevWorld& w, int ga, const 
               double P[9];
 #pragma unroll
               for (int q = 0; q < 9; ++q) P[q] = rp[TR_P + q];
-              hit = tri_tri_intersect(P, Qk) &&
-                    fcl_gate_mesh(w, ga, gb, R, T, (int)rp[TR_ID], (int)bcast(rq[TR_ID], k));
+              hit = tri_tri_intersect(P, Qk) && fcl_gate_mesh(w, ga, gb, R, T, (int)rp[TR_ID], tbk);
             }
           }
           if (__ballot(hit) != 0) return true;
