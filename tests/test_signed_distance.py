@@ -156,12 +156,14 @@ def test_device_signed_distance_and_points_match_oracle(cfg):
         same = pp == rp
         np.testing.assert_allclose(pt[same], rpt[same], rtol=0, atol=1e-9)
     assert (np.minimum(ds, do) < 0).mean() > 0.05  # penetrations were exercised
-    u = w.distance_batch(q, nearest_points=True)
-    ru = o.distance_batch_ex(q)
-    for k in (0, 3):
-        np.testing.assert_allclose(u[k], ru[k], rtol=0, atol=1e-9)
+    u = w.distance_batch(q, nearest_points=True)  # (d_self, p_self, d_others, p_others, pts_self, pts_others)
+    ru = o.distance_batch_ex(q)  # (d_self, p_self, pts_self, d_others, p_others, pts_others)
+    np.testing.assert_allclose(u[0], ru[0], rtol=0, atol=1e-9)
+    np.testing.assert_allclose(u[2], ru[3], rtol=0, atol=1e-9)
     same = u[1] == ru[1]
     np.testing.assert_allclose(u[4][same], ru[2][same], rtol=0, atol=1e-9)
+    same = u[3] == ru[4]
+    np.testing.assert_allclose(u[5][same], ru[5][same], rtol=0, atol=1e-9)
     # the unsigned distances are the plain batch's
     d0 = w.distance_batch(q)
     np.testing.assert_array_equal(d0[0], u[0])
