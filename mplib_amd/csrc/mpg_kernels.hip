@@ -1013,11 +1013,29 @@ __global__ __launch_bounds__(BLOCK) void cull_kernel(DevWorld w, const double* _
       }
       return;
     }
+#ifndef MPG_PUSH_SCAN
+#define MPG_PUSH_SCAN 1
+#endif
     // one wave scan of the kept counts: each lane writes its own entries
     // (schedule index, lane) at its offset, no per-entry wave-level loop
+    if (MPG_PUSH_SCAN) {
     const uint32_t c = (uint32_t)__popc(kb);
-    const uint32_t incl = wave_inclusive_scan(c, lane);
-    const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+    uint32_t incl, total;
+    if (MPG_PUSH_SCAN == 2) {
+      // the prefix sum by bit planes of the counts (<= 32: six ballots), no LDS
+      uint32_t ex = 0u;
+      total = 0u;
+#pragma unroll
+      for (int bit = 0; bit < 6; ++bit) {
+        const unsigned long long m = __ballot((c >> bit) & 1u);
+        ex += __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u)) << bit;
+        total += (uint32_t)__popcll(m) << bit;
+      }
+      incl = ex + c;
+    } else {
+      incl = wave_inclusive_scan(c, lane);
+      total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+    }
     if (total == 0u) return;
     if (tail - head + total <= (uint32_t)kQueue) {
       uint32_t pos = tail + incl - c;
@@ -1032,6 +1050,7 @@ __global__ __launch_bounds__(BLOCK) void cull_kernel(DevWorld w, const double* _
         head += 64;
       }
       return;
+    }
     }
     // more than the queue holds: entry by entry, draining as it fills
     uint32_t any_kb = kb;  // entries some lane of the wave kept
