@@ -59,8 +59,9 @@ def parse():
     p.add_argument("--cpu-plans", type=int, default=-1,
                    help="cfg5: plans timed with the CPU oracle checker (-1: the same seeds as the GPU run, 0: none)")
     p.add_argument("--per-gpu", type=int, default=0, help="configs per GPU per step (default: BASELINE size)")
-    p.add_argument("--cpu-sample", type=int, default=1 << 17,
-                   help="configs timed on the CPU oracle for cpu_baseline (rank 0, N=1 only; 0 = skip)")
+    p.add_argument("--cpu-sample", type=int, default=1 << 20,
+                   help="configs timed on the CPU oracle for cpu_baseline on all the box's cores (rank 0, N=1 only; "
+                        "0 = skip); a quarter of them on one core")
     p.add_argument("--cpu-threads", type=int, default=0,
                    help="threads of the all-core CPU baseline (0: the box's share, OMP_NUM_THREADS or nproc)")
     p.add_argument("--gather", action="store_true", help="also time an all-gather of the results to every rank")
@@ -453,7 +454,7 @@ def cpu_baseline(cfg, q_sample, flags, masks, threads):
 
     ow = Wd.oracle_world(cfg)
     k = len(q_sample)
-    k1 = max(256, k // 8)
+    k1 = max(256, k // 4)
     ow.collide_batch(q_sample[:256], nthreads=1)  # warm
     t0 = time.perf_counter()
     ow.collide_batch(q_sample[:k1], nthreads=1)
