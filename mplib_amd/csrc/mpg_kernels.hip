@@ -1014,7 +1014,7 @@ __global__ __launch_bounds__(BLOCK) void cull_kernel(DevWorld w, const double* _
       return;
     }
 #ifndef MPG_PUSH_SCAN
-#define MPG_PUSH_SCAN 1
+#define MPG_PUSH_SCAN 2
 #endif
     // one wave scan of the kept counts: each lane writes its own entries
     // (schedule index, lane) at its offset, no per-entry wave-level loop
@@ -5549,6 +5549,13 @@ struct mpg_world {
     double* pts = nullptr;  // device-buffer calls: points nobody asked for
     size_t pts_cap = 0;
   } dist;
+  // host-buffer contact calls: grow-only device staging (guarded by host_mu)
+  struct ContactStage {
+    double *in = nullptr, *out = nullptr;
+    uint8_t* fl = nullptr;
+    uint32_t* mk = nullptr;
+    size_t in_cap = 0, out_cap = 0, fl_cap = 0, mk_cap = 0;
+  } contact;
   std::mutex dist_mu;
   std::mutex prof_mu;
   bool prof = false;
@@ -7114,6 +7121,10 @@ int mpg_world_destroy(mpg_world* w) {
   hipFree(w->dist.q);
   hipFree(w->dist.out);
   hipFree(w->dist.pts);
+  hipFree(w->contact.in);
+  hipFree(w->contact.out);
+  hipFree(w->contact.fl);
+  hipFree(w->contact.mk);
   hipFree(w->motion.edges);
   hipFree(w->motion.segs);
   hipFree(w->motion.offs);
@@ -7536,24 +7547,31 @@ int mpg_collide_contacts(mpg_world* w, const double* input, int64_t n, int input
     return poses ? launch_collide<true>(w, input, n, flags, pair_mask, s, &co)
                  : launch_collide<false>(w, input, n, flags, pair_mask, s, &co);
   }
-  // host buffers: temporary device copies
-  double *d_in = nullptr, *d_out = nullptr;
-  uint8_t* d_fl = nullptr;
-  uint32_t* d_mk = nullptr;
-  auto cleanup = [&]() {
-    hipFree(d_in);
-    hipFree(d_out);
-    hipFree(d_fl);
-    hipFree(d_mk);
+  // host buffers: grow-only device staging kept by the world (one host call
+  // at a time: host_mu), no allocation per call
+  std::lock_guard<std::mutex> lk(w->host_mu);
+  if (!s && w->own_stream) s = w->own_stream;
+  auto grow = [&](void** p, size_t& cap, size_t want) -> bool {
+    if (cap >= want) return true;
+    if (*p) hipFree(*p);
+    *p = nullptr;
+    cap = 0;
+    if (hipMalloc(p, want) != hipSuccess) return false;
+    cap = want;
+    return true;
   };
+  auto& C = w->contact;
   int rc = MPG_OK;
   do {
-    if (hipMalloc(&d_in, sizeof(double) * std::max<size_t>(1, row * n)) != hipSuccess ||
-        hipMalloc(&d_out, sizeof(double) * 7 * P * n) != hipSuccess || hipMalloc(&d_fl, n) != hipSuccess ||
-        hipMalloc(&d_mk, sizeof(uint32_t) * W * n) != hipSuccess) {
+    if (!grow((void**)&C.in, C.in_cap, sizeof(double) * std::max<size_t>(1, row * n)) ||
+        !grow((void**)&C.out, C.out_cap, sizeof(double) * 7 * P * n) || !grow((void**)&C.fl, C.fl_cap, n) ||
+        !grow((void**)&C.mk, C.mk_cap, sizeof(uint32_t) * W * n)) {
       rc = set_error(MPG_E_NOMEM, "contact staging buffers");
       break;
     }
+    double *d_in = C.in, *d_out = C.out;
+    uint8_t* d_fl = C.fl;
+    uint32_t* d_mk = C.mk;
     if (row && hipMemcpyAsync(d_in, input, sizeof(double) * row * n, hipMemcpyHostToDevice, s) != hipSuccess) {
       rc = set_error(MPG_E_HIP, "copy input");
       break;
@@ -7569,7 +7587,6 @@ int mpg_collide_contacts(mpg_world* w, const double* input, int64_t n, int input
         hipStreamSynchronize(s) != hipSuccess)
       rc = set_error(MPG_E_HIP, "copy contact results");
   } while (false);
-  cleanup();
   return rc;
 }
 
