@@ -70,6 +70,7 @@ VARIANTS = {
     "pin_cross": ["-DORC_PIN_REVOLUTE_CROSS"],   # column-wise SE3 x TransformRevolute with a cross product
     "eigen_slice": ["-DORC_EIGEN_ORDER=1"],      # Eigen 3.4 SSE2 slice-vectorised 3x3 products
     "eigen_tree": ["-DORC_EIGEN_ORDER=2"],       # Eigen redux-tree order for every coefficient
+    "hist": ["-DORC_HIST"],                      # diagnostics: support calls per MPR (orc_hist_read)
 }
 _variant_libs: Dict[str, ctypes.CDLL] = {}
 

@@ -754,15 +754,29 @@ static int refine_portal(const gjk_obj *o1, const gjk_obj *o2, ccd_simplex_t *po
     }
 }
 
+/* ORC_HIST (diagnostic variant only, oracle.variant_lib("hist")): a histogram
+ * of the support calls each ccdMPRIntersect makes */
+#ifdef ORC_HIST
+static long long orc_hist_bins[1024];
+void orc_hist_read(long long *out) { memcpy(out, orc_hist_bins, sizeof orc_hist_bins); memset(orc_hist_bins, 0, sizeof orc_hist_bins); }
+#endif
+
 /* ccdMPRIntersect */
 static int mpr_intersect(const gjk_obj *o1, const gjk_obj *o2, ccd_real_t tol) {
     ccd_simplex_t portal;
     if (o1->stats) o1->stats->mpr_runs++;
+#ifdef ORC_HIST
+    const long long s0 = o1->stats ? o1->stats->support_calls : 0;
+#define ORC_HIST_DONE(r) do { if (o1->stats) { long long k = o1->stats->support_calls - s0; __atomic_fetch_add(&orc_hist_bins[k < 1023 ? k : 1023], 1, __ATOMIC_RELAXED); } return (r); } while (0)
+#else
+#define ORC_HIST_DONE(r) return (r)
+#endif
     int res = discover_portal(o1, o2, &portal);
-    if (res < 0) return 0;
-    if (res > 0) return 1;
+    if (res < 0) ORC_HIST_DONE(0);
+    if (res > 0) ORC_HIST_DONE(1);
     res = refine_portal(o1, o2, &portal, tol);
-    return res == 0 ? 1 : 0;
+    ORC_HIST_DONE(res == 0 ? 1 : 0);
+#undef ORC_HIST_DONE
 }
 
 /* ------------------------------------------------ libccd 2.1 ccdMPRPenetration
