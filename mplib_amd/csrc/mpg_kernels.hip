@@ -2698,9 +2698,14 @@ __device__ __forceinline__ SE3 chain_oMi_lat(const DevWorld& w, const LatJoints&
   }
   return T;
 }
-template <bool FROM_POSES, int CLS, bool INLINE_SC = false>
+// SCM (joint sin/cos source): 0 = sc buffer (device), chain FK from the
+// snapshot; 1 = computed inline per lane, joints staged in LDS; 2 = sc rows
+// in host-mapped memory (computed on the host), copied to LDS in one round of
+// loads, joints staged in LDS
+template <bool FROM_POSES, int CLS, int SCM = 0>
 __global__ __launch_bounds__(256) void small_kernel(DevWorld w, const double* __restrict__ in, long long n, int n_tiles,
                                                    uint8_t* __restrict__ hits, const double* __restrict__ sc) {
+  constexpr bool INLINE_SC = SCM == 1, STAGED = SCM >= 1;
   const cptr<double> HV = w.hull;
   const uint32_t lane = lane_id();
   const int wave = __builtin_amdgcn_readfirstlane((int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6));
@@ -2742,8 +2747,21 @@ __global__ __launch_bounds__(256) void small_kernel(DevWorld w, const double* __
       }
       sc_row = mine;
     }
+    if constexpr (SCM == 2 && !FROM_POSES) {
+      __shared__ double lat_sc2[4][64][2 * kLatScDof];
+      double* mine = lat_sc2[threadIdx.x >> 6][lane];
+      if ((am || bm) && w.dof > 0) {
+        double v[2 * kLatScDof];
+#pragma unroll
+        for (int k = 0; k < 2 * kLatScDof; ++k) v[k] = sc_row[min(k, 2 * w.dof - 1)];
+#pragma unroll
+        for (int k = 0; k < 2 * kLatScDof; ++k)
+          if (k < 2 * w.dof) mine[k] = v[k];
+      }
+      sc_row = mine;
+    }
     SE3 TA, TB;
-    if constexpr (INLINE_SC && !FROM_POSES) {
+    if constexpr (STAGED && !FROM_POSES) {
       __shared__ LatJoints lat_j[4];
       LatJoints& J = lat_j[threadIdx.x >> 6];
       const int la = am ? w.moving_link[a] : -1, lb = bm ? w.moving_link[b] : -1;
@@ -7246,11 +7264,16 @@ int collide_small(mpg_world* w, const double* q, int64_t n, uint8_t* flags, uint
     hipLaunchKernelGGL(kern, grid, dim3(256), 0, s, w->dw, qin, (long long)n, n_tiles, w->d_hits, sc_src);
     return hipGetLastError();
   };
-  HIP_TRY(inline_sc ? launch(small_kernel<FROM_POSES, CLS_CLOSED, true>) : launch(small_kernel<FROM_POSES, CLS_CLOSED>));
+  const bool host_staged = host_sc && w->dw.dof <= kLatScDof;
+  auto pick = [&](auto k0, auto k1, auto k2) { return inline_sc ? launch(k1) : host_staged ? launch(k2) : launch(k0); };
+  HIP_TRY(pick(small_kernel<FROM_POSES, CLS_CLOSED, 0>, small_kernel<FROM_POSES, CLS_CLOSED, 1>,
+               small_kernel<FROM_POSES, CLS_CLOSED, 2>));
   if (w->any_octree)
-    HIP_TRY(inline_sc ? launch(small_kernel<FROM_POSES, CLS_OCTREE, true>) : launch(small_kernel<FROM_POSES, CLS_OCTREE>));
+    HIP_TRY(pick(small_kernel<FROM_POSES, CLS_OCTREE, 0>, small_kernel<FROM_POSES, CLS_OCTREE, 1>,
+                 small_kernel<FROM_POSES, CLS_OCTREE, 2>));
   if (w->any_mesh)
-    HIP_TRY(inline_sc ? launch(small_kernel<FROM_POSES, CLS_MESH, true>) : launch(small_kernel<FROM_POSES, CLS_MESH>));
+    HIP_TRY(pick(small_kernel<FROM_POSES, CLS_MESH, 0>, small_kernel<FROM_POSES, CLS_MESH, 1>,
+                 small_kernel<FROM_POSES, CLS_MESH, 2>));
   t_small.stop();
   HIP_TRY(hipStreamSynchronize(s));
   const uint8_t* h = w->h_hits;
