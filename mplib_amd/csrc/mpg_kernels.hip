@@ -2706,6 +2706,7 @@ template <bool FROM_POSES, int CLS, int SCM = 0>
 __global__ __launch_bounds__(256) void small_kernel(DevWorld w, const double* __restrict__ in, long long n, int n_tiles,
                                                    uint8_t* __restrict__ hits, const double* __restrict__ sc) {
   constexpr bool INLINE_SC = SCM == 1, STAGED = SCM >= 1;
+  if (w.dbg(10)) return;  // diagnostics: the launch alone
   const cptr<double> HV = w.hull;
   const uint32_t lane = lane_id();
   const int wave = __builtin_amdgcn_readfirstlane((int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6));
