@@ -129,7 +129,20 @@ struct DevWorld {
   cptr<int> fb_root;   // [n_geoms]
   cptr<int> tri_pos;   // [n_mesh_triangles]
   cptr<double> sobb;   // [n_geoms][FB_STRIDE]
+  // latency path: per pair one contiguous record of everything its FK and
+  // bounding test read (LR_*; lat_rec_ok = every chain fits kLatChain)
+  cptr<double> lat_rec;  // [n_pairs][LR_STRIDE]
+  int lat_rec_ok;
 };
+constexpr int kLatChain = 12;
+// latency pair record: header, then per side (0 = pair_a, 1 = pair_b) the
+// chain of joints (type, source, constant, axis[3], placement[12] each), the
+// link placement, the moving offset (static side: its world transform) and
+// the geometry's bounding-sphere centre
+enum { LR_ALLOWED = 0, LR_CF = 1, LR_GA = 2, LR_GB = 3, LR_AM = 4, LR_BM = 5, LR_RA = 6, LR_RB = 7, LR_SIDE = 8 };
+enum { LS_CL = 0, LS_LINKPL = 1, LS_OFF = 13, LS_OBBC = 25, LS_J = 28, LJ_STRIDE = 18,
+       LS_STRIDE = LS_J + kLatChain * LJ_STRIDE };
+enum { LR_STRIDE = LR_SIDE + 2 * LS_STRIDE };
 enum { FB_AXIS = 0, FB_TO = 9, FB_EXT = 12, FB_STRIDE = 15 };
 enum { OG_ORIGIN = 0, OG_INV = 3, OG_DIMS = 4, OG_CELL0 = 7, OG_STRIDE = 8 };
 // triangle record: vertices P1 P2 P3, the triangle's AABB, its index in the mesh

@@ -2762,7 +2762,52 @@ __global__ __launch_bounds__(256) void small_kernel(DevWorld w, const double* __
       sc_row = mine;
     }
     SE3 TA, TB;
-    if constexpr (STAGED && !FROM_POSES) {
+    const double* LRec = nullptr;  // SCM 2: the pair's record in LDS
+    if constexpr (SCM == 2 && !FROM_POSES) {
+      // the pair's record in LDS: one round of loads (every lane a slice)
+      __shared__ double lat_r[4][LR_STRIDE];
+      double* R = lat_r[threadIdx.x >> 6];
+      LRec = R;
+      const cptr<double> src = w.lat_rec + (size_t)LR_STRIDE * p;
+      constexpr int kPer = (LR_STRIDE + 63) / 64;
+      double v[kPer];
+#pragma unroll
+      for (int i = 0; i < kPer; ++i) v[i] = (int)lane + 64 * i < LR_STRIDE ? src[lane + 64 * i] : 0.0;
+#pragma unroll
+      for (int i = 0; i < kPer; ++i)
+        if ((int)lane + 64 * i < LR_STRIDE) R[lane + 64 * i] = v[i];
+      wave_lds_sync();
+      const double* qrow = in + c * w.dof;
+      // chain_oMi_lat + link_from_oMi + moving offset on the record: the same
+      // products in the same order
+      auto tf = [&](int sd) {
+        const double* S = R + LR_SIDE + LS_STRIDE * sd;
+        if (R[sd ? LR_BM : LR_AM] == 0.0) return load_se3(S + LS_OFF);
+        const int cl = (int)S[LS_CL];
+        SE3 T;
+        se3_identity(T);
+        for (int k = 0; k < cl; ++k) {
+          const double* J = S + LS_J + LJ_STRIDE * k;
+          const int type = (int)J[0], srcq = (int)J[1];
+          const bool pre = srcq >= 0 && joint_is_revolute(type);
+          const double qv = pre ? 0.0 : srcq >= 0 ? qrow[srcq] : J[2];
+          const SE3 M = joint_motion(type, J + 3, qv, pre ? sc_row + 2 * srcq : nullptr);
+          const SE3 li = se3_mul(load_se3(J + 6), M);
+          T = k == 0 ? li : se3_mul(T, li);
+        }
+        const SE3 L = se3_mul(T, load_se3(S + LS_LINKPL));
+        double qw, qxyz[3];
+        mat_to_quat(L.R, &qw, qxyz);
+        SE3 Lr;
+        quat_to_mat(qw, qxyz[0], qxyz[1], qxyz[2], Lr.R);
+        Lr.p[0] = L.p[0];
+        Lr.p[1] = L.p[1];
+        Lr.p[2] = L.p[2];
+        return se3_mul(Lr, load_se3(S + LS_OFF));
+      };
+      TA = tf(0);
+      TB = tf(1);
+    } else if constexpr (STAGED && !FROM_POSES) {
       __shared__ LatJoints lat_j[4];
       LatJoints& J = lat_j[threadIdx.x >> 6];
       const int la = am ? w.moving_link[a] : -1, lb = bm ? w.moving_link[b] : -1;
@@ -2778,17 +2823,36 @@ __global__ __launch_bounds__(256) void small_kernel(DevWorld w, const double* __
       TA = am ? moving_tf_row<FROM_POSES>(w, in, sc_row, c, a) : load_se3(w.static_T + 12 * (a - w.n_moving));
       TB = bm ? moving_tf_row<FROM_POSES>(w, in, sc_row, c, b) : load_se3(w.static_T + 12 * (b - w.n_moving));
     }
-    const int ga = am ? w.moving_geom[a] : w.static_geom[a - w.n_moving];
-    const int gb = bm ? w.moving_geom[b] : w.static_geom[b - w.n_moving];
-    const cptr<double> ra = w.geom_rec + G_STRIDE * ga, rb = w.geom_rec + G_STRIDE * gb;
+    int ga, gb;
+    double oa[3], ob[3], rsum;
+    if (SCM == 2 && !FROM_POSES) {
+      ga = __builtin_amdgcn_readfirstlane((int)LRec[LR_GA]);
+      gb = __builtin_amdgcn_readfirstlane((int)LRec[LR_GB]);
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        oa[i] = LRec[LR_SIDE + LS_OBBC + i];
+        ob[i] = LRec[LR_SIDE + LS_STRIDE + LS_OBBC + i];
+      }
+      rsum = LRec[LR_RA] + LRec[LR_RB];
+    } else {
+      ga = am ? w.moving_geom[a] : w.static_geom[a - w.n_moving];
+      gb = bm ? w.moving_geom[b] : w.static_geom[b - w.n_moving];
+      const cptr<double> ra = w.geom_rec + G_STRIDE * ga, rb = w.geom_rec + G_STRIDE * gb;
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        oa[i] = ra[G_OBB_C + i];
+        ob[i] = rb[G_OBB_C + i];
+      }
+      rsum = ra[G_RADIUS] + rb[G_RADIUS];
+    }
     double d2 = 0.0;
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
-      const double ci = ((TA.R[3 * i] * ra[G_OBB_C] + TA.R[3 * i + 1] * ra[G_OBB_C + 1]) + TA.R[3 * i + 2] * ra[G_OBB_C + 2]) + TA.p[i];
-      const double cj = ((TB.R[3 * i] * rb[G_OBB_C] + TB.R[3 * i + 1] * rb[G_OBB_C + 1]) + TB.R[3 * i + 2] * rb[G_OBB_C + 2]) + TB.p[i];
+      const double ci = ((TA.R[3 * i] * oa[0] + TA.R[3 * i + 1] * oa[1]) + TA.R[3 * i + 2] * oa[2]) + TA.p[i];
+      const double cj = ((TB.R[3 * i] * ob[0] + TB.R[3 * i + 1] * ob[1]) + TB.R[3 * i + 2] * ob[2]) + TB.p[i];
       d2 += (ci - cj) * (ci - cj);
     }
-    const double rr = ra[G_RADIUS] + rb[G_RADIUS] + w.small_margin;
+    const double rr = rsum + w.small_margin;
     const bool near = live && d2 <= rr * rr && !w.dbg(3) && !(w.dbg(7) && d2 >= 0.0);
     if (CLS != CLS_CLOSED) {
       hit = (walk_wave_eval<CLS>(w, HV, ga, TA, gb, TB, near) >> lane) & 1ull;
@@ -6691,6 +6755,50 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
   for (int p = 0; p < d->n_pairs; ++p) allowed[p] = d->pair_allowed ? (d->pair_allowed[p] != 0) : 0;
   std::vector<int> pair_cf(std::max(d->n_pairs, 1), 0);
   for (int p = 0; p < d->n_pairs; ++p) pair_cf[p] = closed_form_kind(d, d->pair_a[p], d->pair_b[p]);
+  // latency pair records (LR_*): one round of loads per wave instead of a
+  // chain of dependent snapshot lookups (pair -> object -> link -> chain ->
+  // joints -> geometry)
+  std::vector<double> lat_rec((size_t)LR_STRIDE * std::max(d->n_pairs, 1), 0.0);
+  bool lat_rec_ok = true;
+  for (int p = 0; p < d->n_pairs; ++p) {
+    double* R = lat_rec.data() + (size_t)LR_STRIDE * p;
+    const int ids[2] = {d->pair_a[p], d->pair_b[p]};
+    R[LR_ALLOWED] = allowed[p];
+    R[LR_CF] = pair_cf[p];
+    for (int s2 = 0; s2 < 2; ++s2) {
+      const int id = ids[s2];
+      const bool mv = id < d->n_moving;
+      const int g = mv ? d->moving_geom[id] : d->static_geom[id - d->n_moving];
+      R[s2 ? LR_GB : LR_GA] = g;
+      R[s2 ? LR_BM : LR_AM] = mv ? 1.0 : 0.0;
+      R[s2 ? LR_RB : LR_RA] = geom_rec[G_STRIDE * (size_t)g + G_RADIUS];
+      double* S = R + LR_SIDE + LS_STRIDE * s2;
+      for (int k = 0; k < 3; ++k) S[LS_OBBC + k] = geom_rec[G_STRIDE * (size_t)g + G_OBB_C + k];
+      if (!mv) {
+        std::copy(d->static_transform + 12 * (size_t)(id - d->n_moving),
+                  d->static_transform + 12 * (size_t)(id - d->n_moving) + 12, S + LS_OFF);
+        continue;
+      }
+      const int l = d->moving_link[id];
+      const int cl = chain_len[l];
+      if (cl > kLatChain) {
+        lat_rec_ok = false;
+        continue;
+      }
+      S[LS_CL] = cl;
+      std::copy(d->link_placement + 12 * (size_t)l, d->link_placement + 12 * (size_t)l + 12, S + LS_LINKPL);
+      std::copy(d->moving_offset + 12 * (size_t)id, d->moving_offset + 12 * (size_t)id + 12, S + LS_OFF);
+      for (int k = 0; k < cl; ++k) {
+        const int j = chain_joints[chain_start[l] + k] - 1;
+        double* J = S + LS_J + LJ_STRIDE * k;
+        J[0] = d->joint_type[j];
+        J[1] = d->joint_q_source[j];
+        J[2] = d->joint_q_const[j];
+        for (int i = 0; i < 3; ++i) J[3 + i] = d->joint_axis[3 * (size_t)j + i];
+        for (int i = 0; i < 12; ++i) J[6 + i] = d->joint_placement[12 * (size_t)j + i];
+      }
+    }
+  }
   // phase-A schedule: non-allowed pairs grouped by their lower moving object
   // ---- culling margins: pairs that can reach libccd MPR (directly, on octree
   // leaves or on mesh triangles) keep everything within its false-hit reach
@@ -6918,6 +7026,7 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
   const size_t o_mnd = bb.add(mesh_node.data(), mesh_node.size());
   const size_t o_mln = bb.add(mesh_link.data(), mesh_link.size());
   const size_t o_mtt = bb.add(mesh_tree.data(), mesh_tree.size());
+  const size_t o_lrec = bb.add(lat_rec.data(), lat_rec.size());
   const size_t o_fbb = bb.add(fbvh.box.data(), fbvh.box.size());
   const size_t o_fbl = bb.add(fbvh.link.data(), fbvh.link.size());
   const size_t o_fbr = bb.add(fb_root.data(), fb_root.size());
@@ -7069,6 +7178,8 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
   dw.fb_root = to_cptr<int>(base + o_fbr);
   dw.tri_pos = to_cptr<int>(base + o_tps);
   dw.sobb = to_cptr<double>(base + o_sob);
+  dw.lat_rec = to_cptr<double>(base + o_lrec);
+  dw.lat_rec_ok = lat_rec_ok ? 1 : 0;
   dw.oct_grid = to_cptr<double>(base + o_ogr);
   dw.oct_cells = I(o_oce);
   dw.oct_list = I(o_oli);
@@ -7265,7 +7376,7 @@ int collide_small(mpg_world* w, const double* q, int64_t n, uint8_t* flags, uint
     hipLaunchKernelGGL(kern, grid, dim3(256), 0, s, w->dw, qin, (long long)n, n_tiles, w->d_hits, sc_src);
     return hipGetLastError();
   };
-  const bool host_staged = host_sc && w->dw.dof <= kLatScDof;
+  const bool host_staged = host_sc && w->dw.dof <= kLatScDof && w->dw.lat_rec_ok;
   auto pick = [&](auto k0, auto k1, auto k2) { return inline_sc ? launch(k1) : host_staged ? launch(k2) : launch(k0); };
   HIP_TRY(pick(small_kernel<FROM_POSES, CLS_CLOSED, 0>, small_kernel<FROM_POSES, CLS_CLOSED, 1>,
                small_kernel<FROM_POSES, CLS_CLOSED, 2>));

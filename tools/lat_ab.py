@@ -35,7 +35,8 @@ def main():
         floor_s = med(lambda: (x.add_(1), s.synchronize()))
     w, art = scenes.world(3)
     out = {"tag": tag, "torch_add_sync_us": floor, "torch_add_sync_side_stream_us": floor_s}
-    for n in (1, 8, 64, 256):
+    sizes = [int(v) for v in os.environ.get("LAT_N", "1,8,64,256").split(",")]
+    for n in sizes:
         q = scenes.sample_states(art, n, 3)
         out[f"n{n}_us"] = med(lambda: w.collide_batch(q))
     print(out, flush=True)
