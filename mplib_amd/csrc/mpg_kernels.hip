@@ -2707,6 +2707,19 @@ __global__ __launch_bounds__(256) void small_kernel(DevWorld w, const double* __
                                                    uint8_t* __restrict__ hits, const double* __restrict__ sc) {
   constexpr bool INLINE_SC = SCM == 1, STAGED = SCM >= 1;
   if (w.dbg(10)) return;  // diagnostics: the launch alone
+  // MPG_STATS: per-wave phase times (s_memrealtime, 100 MHz) into stats[24..31]
+  const uint64_t ts0 = w.stats ? __builtin_amdgcn_s_memrealtime() : 0;
+  auto tmark = [&](int k, uint64_t& last) {
+    if (w.stats) {
+      const uint64_t t = __builtin_amdgcn_s_memrealtime();
+      if (lane_id() == 0) {
+        atomicAdd(&w.stats[24 + k], t - last);
+        atomicMax(&w.stats[32 + k], t - last);
+      }
+      last = t;
+    }
+  };
+  uint64_t tlast = ts0;
   const cptr<double> HV = w.hull;
   const uint32_t lane = lane_id();
   const int wave = __builtin_amdgcn_readfirstlane((int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6));
@@ -2805,8 +2818,10 @@ __global__ __launch_bounds__(256) void small_kernel(DevWorld w, const double* __
         Lr.p[2] = L.p[2];
         return se3_mul(Lr, load_se3(S + LS_OFF));
       };
+      tmark(0, tlast);  // the record in LDS
       TA = tf(0);
       TB = tf(1);
+      tmark(1, tlast);  // FK of both objects
     } else if constexpr (STAGED && !FROM_POSES) {
       __shared__ LatJoints lat_j[4];
       LatJoints& J = lat_j[threadIdx.x >> 6];
@@ -2854,6 +2869,7 @@ __global__ __launch_bounds__(256) void small_kernel(DevWorld w, const double* __
     }
     const double rr = rsum + w.small_margin;
     const bool near = live && d2 <= rr * rr && !w.dbg(3) && !(w.dbg(7) && d2 >= 0.0);
+    tmark(2, tlast);  // bounding spheres
     if (CLS != CLS_CLOSED) {
       hit = (walk_wave_eval<CLS>(w, HV, ga, TA, gb, TB, near) >> lane) & 1ull;
     } else if (cf != CF_NONE) {
@@ -2884,8 +2900,14 @@ __global__ __launch_bounds__(256) void small_kernel(DevWorld w, const double* __
         }
       }
     }
+    tmark(3, tlast);  // narrow test
   }
   if (live) hits[(size_t)p * n + cfg] = hit;
+  if (w.stats) {
+    tmark(4, tlast);  // hit store
+    uint64_t t0c = ts0;
+    tmark(5, t0c);    // whole wave
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -7083,8 +7105,8 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
 #endif
   dw.stats = nullptr;
   if (std::getenv("MPG_STATS") && std::atoi(std::getenv("MPG_STATS")) > 0) {
-    HIP_TRY(hipMalloc(&dw.stats, 24 * sizeof(unsigned long long)));
-    HIP_TRY(hipMemset(dw.stats, 0, 24 * sizeof(unsigned long long)));
+    HIP_TRY(hipMalloc(&dw.stats, 40 * sizeof(unsigned long long)));
+    HIP_TRY(hipMemset(dw.stats, 0, 40 * sizeof(unsigned long long)));
   }
   dw.joint_type = to_cptr<int>(base + o_jt);
   dw.joint_parent = to_cptr<int>(base + o_jp);
@@ -7212,9 +7234,14 @@ int mpg_world_destroy(mpg_world* w) {
   if (!w) return MPG_OK;
   hipSetDevice(w->device);
   if (w->dw.stats) {
-    unsigned long long st[24];
+    unsigned long long st[40];
     hipDeviceSynchronize();
     hipMemcpy(st, w->dw.stats, sizeof(st), hipMemcpyDeviceToHost);
+    std::fprintf(stderr,
+                 "[mpg stats] small_kernel phases (sum over waves / max per wave, us): record %.1f/%.2f, fk %.1f/%.2f, "
+                 "spheres %.1f/%.2f, narrow %.1f/%.2f, store %.1f/%.2f, wave %.1f/%.2f\n",
+                 st[24] / 100.0, st[32] / 100.0, st[25] / 100.0, st[33] / 100.0, st[26] / 100.0, st[34] / 100.0,
+                 st[27] / 100.0, st[35] / 100.0, st[28] / 100.0, st[36] / 100.0, st[29] / 100.0, st[37] / 100.0);
     std::fprintf(stderr, "[mpg stats] walk hulls: supports %llu, trap-free fast %llu, verified %llu, full walks %llu, "
                  "certified endpoints %llu; pending: tie %llu, uncertified %llu, resumed %llu; resolve ticks: verify %llu, walk %llu\n",
                  st[10], st[11], st[12], st[13], st[14], st[16], st[17], st[18], st[9], st[15]);
