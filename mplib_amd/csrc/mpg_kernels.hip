@@ -2709,15 +2709,9 @@ __global__ __launch_bounds__(256) void small_kernel(DevWorld w, const double* __
   if (w.dbg(10)) return;  // diagnostics: the launch alone
   // MPG_STATS: per-wave phase times (s_memrealtime, 100 MHz) into stats[24..31]
   const uint64_t ts0 = w.stats ? __builtin_amdgcn_s_memrealtime() : 0;
-  auto tmark = [&](int k, uint64_t& last) {
-    if (w.stats) {
-      const uint64_t t = __builtin_amdgcn_s_memrealtime();
-      if (lane_id() == 0) {
-        atomicAdd(&w.stats[24 + k], t - last);
-        atomicMax(&w.stats[32 + k], t - last);
-      }
-      last = t;
-    }
+  uint64_t tm[6] = {ts0, ts0, ts0, ts0, ts0, ts0};  // phase ends, published at the end
+  auto tmark = [&](int k, uint64_t&) {
+    if (w.stats) tm[k] = __builtin_amdgcn_s_memrealtime();
   };
   uint64_t tlast = ts0;
   const cptr<double> HV = w.hull;
@@ -2904,9 +2898,19 @@ __global__ __launch_bounds__(256) void small_kernel(DevWorld w, const double* __
   }
   if (live) hits[(size_t)p * n + cfg] = hit;
   if (w.stats) {
-    tmark(4, tlast);  // hit store
-    uint64_t t0c = ts0;
-    tmark(5, t0c);    // whole wave
+    tmark(4, tlast);  // hit store issued
+    // phases that did not run (other kernel paths) took no time
+    for (int k = 1; k < 5; ++k) tm[k] = tm[k] < tm[k - 1] ? tm[k - 1] : tm[k];
+    if (lane_id() == 0) {
+      uint64_t prev = ts0;
+      for (int k = 0; k < 5; ++k) {
+        atomicAdd(&w.stats[24 + k], tm[k] - prev);
+        atomicMax(&w.stats[32 + k], tm[k] - prev);
+        prev = tm[k];
+      }
+      atomicAdd(&w.stats[29], tm[4] - ts0);
+      atomicMax(&w.stats[37], tm[4] - ts0);
+    }
   }
 }
 
