@@ -2709,7 +2709,7 @@ __global__ __launch_bounds__(256) void small_kernel(DevWorld w, const double* __
   if (w.dbg(10)) return;  // diagnostics: the launch alone
   // MPG_STATS: per-wave phase times (s_memrealtime, 100 MHz) into stats[24..31]
   const uint64_t ts0 = w.stats ? __builtin_amdgcn_s_memrealtime() : 0;
-  uint64_t tm[6] = {ts0, ts0, ts0, ts0, ts0, ts0};  // phase ends, published at the end
+  uint64_t tm[6] = {ts0, ts0, ts0, ts0, ts0, ts0};  // phase ends (pre, record, fk, spheres, narrow, store)
   auto tmark = [&](int k, uint64_t&) {
     if (w.stats) tm[k] = __builtin_amdgcn_s_memrealtime();
   };
@@ -2775,6 +2775,7 @@ __global__ __launch_bounds__(256) void small_kernel(DevWorld w, const double* __
       __shared__ double lat_r[4][LR_STRIDE];
       double* R = lat_r[threadIdx.x >> 6];
       LRec = R;
+      tmark(0, tlast);  // kernel entry -> before the record loads
       const cptr<double> src = w.lat_rec + (size_t)LR_STRIDE * p;
       constexpr int kPer = (LR_STRIDE + 63) / 64;
       double v[kPer];
@@ -2812,10 +2813,10 @@ __global__ __launch_bounds__(256) void small_kernel(DevWorld w, const double* __
         Lr.p[2] = L.p[2];
         return se3_mul(Lr, load_se3(S + LS_OFF));
       };
-      tmark(0, tlast);  // the record in LDS
+      tmark(1, tlast);  // the record in LDS
       TA = tf(0);
       TB = tf(1);
-      tmark(1, tlast);  // FK of both objects
+      tmark(2, tlast);  // FK of both objects
     } else if constexpr (STAGED && !FROM_POSES) {
       __shared__ LatJoints lat_j[4];
       LatJoints& J = lat_j[threadIdx.x >> 6];
@@ -2863,7 +2864,7 @@ __global__ __launch_bounds__(256) void small_kernel(DevWorld w, const double* __
     }
     const double rr = rsum + w.small_margin;
     const bool near = live && d2 <= rr * rr && !w.dbg(3) && !(w.dbg(7) && d2 >= 0.0);
-    tmark(2, tlast);  // bounding spheres
+    tmark(3, tlast);  // bounding spheres
     if (CLS != CLS_CLOSED) {
       hit = (walk_wave_eval<CLS>(w, HV, ga, TA, gb, TB, near) >> lane) & 1ull;
     } else if (cf != CF_NONE) {
@@ -2894,22 +2895,22 @@ __global__ __launch_bounds__(256) void small_kernel(DevWorld w, const double* __
         }
       }
     }
-    tmark(3, tlast);  // narrow test
+    tmark(4, tlast);  // narrow test
   }
   if (live) hits[(size_t)p * n + cfg] = hit;
   if (w.stats) {
-    tmark(4, tlast);  // hit store issued
+    tmark(5, tlast);  // hit store issued
     // phases that did not run (other kernel paths) took no time
-    for (int k = 1; k < 5; ++k) tm[k] = tm[k] < tm[k - 1] ? tm[k - 1] : tm[k];
+    for (int k = 1; k < 6; ++k) tm[k] = tm[k] < tm[k - 1] ? tm[k - 1] : tm[k];
     if (lane_id() == 0) {
       uint64_t prev = ts0;
-      for (int k = 0; k < 5; ++k) {
+      for (int k = 0; k < 6; ++k) {
         atomicAdd(&w.stats[24 + k], tm[k] - prev);
         atomicMax(&w.stats[32 + k], tm[k] - prev);
         prev = tm[k];
       }
-      atomicAdd(&w.stats[29], tm[4] - ts0);
-      atomicMax(&w.stats[37], tm[4] - ts0);
+      atomicAdd(&w.stats[30], tm[5] - ts0);
+      atomicMax(&w.stats[38], tm[5] - ts0);
     }
   }
 }
@@ -7242,10 +7243,11 @@ int mpg_world_destroy(mpg_world* w) {
     hipDeviceSynchronize();
     hipMemcpy(st, w->dw.stats, sizeof(st), hipMemcpyDeviceToHost);
     std::fprintf(stderr,
-                 "[mpg stats] small_kernel phases (sum over waves / max per wave, us): record %.1f/%.2f, fk %.1f/%.2f, "
-                 "spheres %.1f/%.2f, narrow %.1f/%.2f, store %.1f/%.2f, wave %.1f/%.2f\n",
+                 "[mpg stats] small_kernel phases (sum over waves / max per wave, us): pre %.1f/%.2f, record %.1f/%.2f, "
+                 "fk %.1f/%.2f, spheres %.1f/%.2f, narrow %.1f/%.2f, store %.1f/%.2f, wave %.1f/%.2f\n",
                  st[24] / 100.0, st[32] / 100.0, st[25] / 100.0, st[33] / 100.0, st[26] / 100.0, st[34] / 100.0,
-                 st[27] / 100.0, st[35] / 100.0, st[28] / 100.0, st[36] / 100.0, st[29] / 100.0, st[37] / 100.0);
+                 st[27] / 100.0, st[35] / 100.0, st[28] / 100.0, st[36] / 100.0, st[29] / 100.0, st[37] / 100.0,
+                 st[30] / 100.0, st[38] / 100.0);
     std::fprintf(stderr, "[mpg stats] walk hulls: supports %llu, trap-free fast %llu, verified %llu, full walks %llu, "
                  "certified endpoints %llu; pending: tie %llu, uncertified %llu, resumed %llu; resolve ticks: verify %llu, walk %llu\n",
                  st[10], st[11], st[12], st[13], st[14], st[16], st[17], st[18], st[9], st[15]);
