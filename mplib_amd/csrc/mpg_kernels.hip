@@ -2698,14 +2698,30 @@ __device__ __forceinline__ SE3 chain_oMi_lat(const DevWorld& w, const LatJoints&
   }
   return T;
 }
+// The smallest batches' rows by value in the kernel arguments (which the
+// launch writes to device memory anyway): row c = q[dof], then sin/cos
+// [2 dof] (revolute sources only), no read of host memory from the kernel
+constexpr int kLatIn = 64;
+struct LatIn {
+  double d[kLatIn];
+};
+static_assert(sizeof(DevWorld) + sizeof(LatIn) + 64 <= 4096, "small_kernel arguments exceed the kernarg limit");
+
+__device__ __forceinline__ double dbl_xor32(double v) {  // lane ^ 32's value
+  const unsigned long long u = (unsigned long long)__double_as_longlong(v);
+  const unsigned lo = (unsigned)__shfl_xor((int)(unsigned)u, 32), hi = (unsigned)__shfl_xor((int)(unsigned)(u >> 32), 32);
+  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+
 // SCM (joint sin/cos source): 0 = sc buffer (device), chain FK from the
 // snapshot; 1 = computed inline per lane, joints staged in LDS; 2 = sc rows
 // in host-mapped memory (computed on the host), copied to LDS in one round of
-// loads, joints staged in LDS
+// loads, FK on the pair's record; 3 = as 2 with the rows in the kernel
+// arguments (LatIn)
 template <bool FROM_POSES, int CLS, int SCM = 0>
 __global__ __launch_bounds__(256) void small_kernel(DevWorld w, const double* __restrict__ in, long long n, int n_tiles,
-                                                   uint8_t* __restrict__ hits, const double* __restrict__ sc) {
-  constexpr bool INLINE_SC = SCM == 1, STAGED = SCM >= 1;
+                                                   uint8_t* __restrict__ hits, const double* __restrict__ sc, LatIn args) {
+  constexpr bool INLINE_SC = SCM == 1, STAGED = SCM >= 1, REC = SCM >= 2 && !FROM_POSES;
   if (w.dbg(10)) return;  // diagnostics: the launch alone
   // MPG_STATS: per-wave phase times (s_memrealtime, 100 MHz) into stats[24..31]
   const uint64_t ts0 = w.stats ? __builtin_amdgcn_s_memrealtime() : 0;
@@ -2755,8 +2771,10 @@ __global__ __launch_bounds__(256) void small_kernel(DevWorld w, const double* __
       }
       sc_row = mine;
     }
+    double* sc2_wave = nullptr;
     if constexpr (SCM == 2 && !FROM_POSES) {
       __shared__ double lat_sc2[4][64][2 * kLatScDof];
+      sc2_wave = lat_sc2[threadIdx.x >> 6][0];
       double* mine = lat_sc2[threadIdx.x >> 6][lane];
       if ((am || bm) && w.dof > 0) {
         double v[2 * kLatScDof];
@@ -2769,8 +2787,8 @@ __global__ __launch_bounds__(256) void small_kernel(DevWorld w, const double* __
       sc_row = mine;
     }
     SE3 TA, TB;
-    const double* LRec = nullptr;  // SCM 2: the pair's record in LDS
-    if constexpr (SCM == 2 && !FROM_POSES) {
+    const double* LRec = nullptr;  // SCM 2/3: the pair's record in LDS
+    if constexpr (REC) {
       // the pair's record in LDS: one round of loads (every lane a slice)
       __shared__ double lat_r[4][LR_STRIDE];
       double* R = lat_r[threadIdx.x >> 6];
@@ -2781,11 +2799,26 @@ __global__ __launch_bounds__(256) void small_kernel(DevWorld w, const double* __
       double v[kPer];
 #pragma unroll
       for (int i = 0; i < kPer; ++i) v[i] = (int)lane + 64 * i < LR_STRIDE ? src[lane + 64 * i] : 0.0;
+      const double* qrow = in + c * w.dof;
+      // half waves: with at most 32 states, lanes 0-31 run side A's chain and
+      // lanes 32-63 side B's for state lane & 31, then swap (the products are
+      // the same, each computed once)
+      const bool split = n <= 32;
+      const int cs = split ? (int)min((long long)(lane & 31), n - 1) : (int)c;
+      if constexpr (SCM == 3) {
+        __shared__ double lat_in[4][kLatIn];
+        double* I = lat_in[threadIdx.x >> 6];
+        I[lane] = args.d[lane];
+        sc_row = I + (size_t)cs * 3 * w.dof + w.dof;
+        qrow = I + (size_t)cs * 3 * w.dof;
+      } else if (split) {  // state cs's rows: lane cs's LDS copy
+        sc_row = sc2_wave + (size_t)cs * 2 * kLatScDof;
+        qrow = in + (size_t)cs * w.dof;
+      }
 #pragma unroll
       for (int i = 0; i < kPer; ++i)
         if ((int)lane + 64 * i < LR_STRIDE) R[lane + 64 * i] = v[i];
       wave_lds_sync();
-      const double* qrow = in + c * w.dof;
       // chain_oMi_lat + link_from_oMi + moving offset on the record: the same
       // products in the same order
       auto tf = [&](int sd) {
@@ -2814,8 +2847,20 @@ __global__ __launch_bounds__(256) void small_kernel(DevWorld w, const double* __
         return se3_mul(Lr, load_se3(S + LS_OFF));
       };
       tmark(1, tlast);  // the record in LDS
-      TA = tf(0);
-      TB = tf(1);
+      if (split) {
+        const int sd = (int)(lane >> 5);
+        const SE3 T = tf(sd);
+        SE3 O;
+#pragma unroll
+        for (int i = 0; i < 9; ++i) O.R[i] = dbl_xor32(T.R[i]);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) O.p[i] = dbl_xor32(T.p[i]);
+        TA = sd ? O : T;
+        TB = sd ? T : O;
+      } else {
+        TA = tf(0);
+        TB = tf(1);
+      }
       tmark(2, tlast);  // FK of both objects
     } else if constexpr (STAGED && !FROM_POSES) {
       __shared__ LatJoints lat_j[4];
@@ -2835,7 +2880,7 @@ __global__ __launch_bounds__(256) void small_kernel(DevWorld w, const double* __
     }
     int ga, gb;
     double oa[3], ob[3], rsum;
-    if (SCM == 2 && !FROM_POSES) {
+    if (REC) {
       ga = __builtin_amdgcn_readfirstlane((int)LRec[LR_GA]);
       gb = __builtin_amdgcn_readfirstlane((int)LRec[LR_GB]);
 #pragma unroll
@@ -2911,6 +2956,7 @@ __global__ __launch_bounds__(256) void small_kernel(DevWorld w, const double* __
       }
       atomicAdd(&w.stats[30], tm[5] - ts0);
       atomicMax(&w.stats[38], tm[5] - ts0);
+      atomicMax(&w.stats[31], ((tm[4] - tm[3]) << 12) | (uint64_t)p);  // the slowest narrow test's pair
     }
   }
 }
@@ -5708,6 +5754,7 @@ struct mpg_world {
   double* h_ssc = nullptr;     // pinned host-mapped twin: sin/cos computed on the host (small batches)
   double* d_sscmap = nullptr;  // h_ssc as the device sees it
   int64_t small_host_sc = 64;  // latency batches up to this size: sin/cos on the host (MPG_SMALL_HOST_SC)
+  bool small_args = true;      // the fewest states' rows in the kernel arguments (MPG_SMALL_ARGS=0: off)
   std::vector<int> h_rev_src;  // move-group slots of revolute joints (host copy of the snapshot's rule)
   // host-buffer calls without a stream run on this non-blocking stream (not
   // the legacy default stream, whose synchronisation covers every blocking
@@ -7225,6 +7272,7 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
   if (const char* e = std::getenv("MPG_SMALL_INLINE_SC")) w->small_inline_sc = std::atoll(e);
   if (const char* e = std::getenv("MPG_OVERLAP_PARTS")) w->overlap_parts = std::atoi(e);
   if (const char* e = std::getenv("MPG_SMALL_HOST_SC")) w->small_host_sc = std::atoll(e);
+  if (const char* e = std::getenv("MPG_SMALL_ARGS")) w->small_args = std::atoi(e) != 0;
   for (int j = 0; j < d->n_joints; ++j)
     if (d->joint_q_source[j] >= 0 && joint_is_revolute(d->joint_type[j]) &&
         std::find(w->h_rev_src.begin(), w->h_rev_src.end(), d->joint_q_source[j]) == w->h_rev_src.end())
@@ -7248,6 +7296,8 @@ int mpg_world_destroy(mpg_world* w) {
                  st[24] / 100.0, st[32] / 100.0, st[25] / 100.0, st[33] / 100.0, st[26] / 100.0, st[34] / 100.0,
                  st[27] / 100.0, st[35] / 100.0, st[28] / 100.0, st[36] / 100.0, st[29] / 100.0, st[37] / 100.0,
                  st[30] / 100.0, st[38] / 100.0);
+    std::fprintf(stderr, "[mpg stats] small_kernel slowest narrow test: pair %llu, %.2f us\n",
+                 (unsigned long long)(st[31] & 4095), (st[31] >> 12) / 100.0);
     std::fprintf(stderr, "[mpg stats] walk hulls: supports %llu, trap-free fast %llu, verified %llu, full walks %llu, "
                  "certified endpoints %llu; pending: tie %llu, uncertified %llu, resumed %llu; resolve ticks: verify %llu, walk %llu\n",
                  st[10], st[11], st[12], st[13], st[14], st[16], st[17], st[18], st[9], st[15]);
@@ -7405,20 +7455,33 @@ int collide_small(mpg_world* w, const double* q, int64_t n, uint8_t* flags, uint
     HIP_TRY(hipGetLastError());
   }
   const dim3 grid((unsigned)((waves + 3) / 4));
+  const bool host_staged = host_sc && w->dw.dof <= kLatScDof && w->dw.lat_rec_ok;
+  // the fewest states: their rows travel in the kernel arguments
+  const bool by_args = host_staged && n * 3 * (int64_t)w->dw.dof <= kLatIn && w->small_args;
+  LatIn args{};
+  if (by_args) {
+    const int dof = w->dw.dof;
+    for (int64_t c = 0; c < n; ++c) {
+      double* r = args.d + c * 3 * dof;
+      std::memcpy(r, q + c * dof, sizeof(double) * (size_t)dof);
+      std::memcpy(r + dof, w->h_ssc + c * 2 * dof, sizeof(double) * 2 * (size_t)dof);
+    }
+  }
   auto launch = [&](auto kern) {  // every class instance reads the same sin/cos source
-    hipLaunchKernelGGL(kern, grid, dim3(256), 0, s, w->dw, qin, (long long)n, n_tiles, w->d_hits, sc_src);
+    hipLaunchKernelGGL(kern, grid, dim3(256), 0, s, w->dw, qin, (long long)n, n_tiles, w->d_hits, sc_src, args);
     return hipGetLastError();
   };
-  const bool host_staged = host_sc && w->dw.dof <= kLatScDof && w->dw.lat_rec_ok;
-  auto pick = [&](auto k0, auto k1, auto k2) { return inline_sc ? launch(k1) : host_staged ? launch(k2) : launch(k0); };
+  auto pick = [&](auto k0, auto k1, auto k2, auto k3) {
+    return inline_sc ? launch(k1) : by_args ? launch(k3) : host_staged ? launch(k2) : launch(k0);
+  };
   HIP_TRY(pick(small_kernel<FROM_POSES, CLS_CLOSED, 0>, small_kernel<FROM_POSES, CLS_CLOSED, 1>,
-               small_kernel<FROM_POSES, CLS_CLOSED, 2>));
+               small_kernel<FROM_POSES, CLS_CLOSED, 2>, small_kernel<FROM_POSES, CLS_CLOSED, 3>));
   if (w->any_octree)
     HIP_TRY(pick(small_kernel<FROM_POSES, CLS_OCTREE, 0>, small_kernel<FROM_POSES, CLS_OCTREE, 1>,
-                 small_kernel<FROM_POSES, CLS_OCTREE, 2>));
+                 small_kernel<FROM_POSES, CLS_OCTREE, 2>, small_kernel<FROM_POSES, CLS_OCTREE, 3>));
   if (w->any_mesh)
     HIP_TRY(pick(small_kernel<FROM_POSES, CLS_MESH, 0>, small_kernel<FROM_POSES, CLS_MESH, 1>,
-                 small_kernel<FROM_POSES, CLS_MESH, 2>));
+                 small_kernel<FROM_POSES, CLS_MESH, 2>, small_kernel<FROM_POSES, CLS_MESH, 3>));
   t_small.stop();
   HIP_TRY(hipStreamSynchronize(s));
   const uint8_t* h = w->h_hits;

@@ -334,10 +334,20 @@ def test_latency_path_matches_oracle(cfg):
     np.testing.assert_array_equal(f, fo)
     np.testing.assert_array_equal(m, mo)
     w.set_small_batch_max(1024)
-    for n in (1, 2, 63, 64, 65, 1000, 1024, 1025):
+    for n in (1, 2, 3, 5, 17, 32, 33, 63, 64, 65, 1000, 1024, 1025):
         f, m = w.collide_batch(q[:n])
         np.testing.assert_array_equal(f, fo[:n])
         np.testing.assert_array_equal(m, mo[:n])
+    # one or two states at a time (isStateValid): rows in the kernel
+    # arguments, half-wave FK; colliding and free states both
+    for i in range(0, 400, 2):
+        f, m = w.collide_batch(q[i:i + 1])
+        np.testing.assert_array_equal(f, fo[i:i + 1])
+        np.testing.assert_array_equal(m, mo[i:i + 1])
+        f, m = w.collide_batch(q[i:i + 2])
+        np.testing.assert_array_equal(f, fo[i:i + 2])
+        np.testing.assert_array_equal(m, mo[i:i + 2])
+    assert 0 < fo[:400].sum() < 400
     w.set_small_batch_max(0)
     f, m = w.collide_batch(q[:1000])
     np.testing.assert_array_equal(f, fo[:1000])
