@@ -28,6 +28,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cfloat>
 #include <cstdio>
 #include <cstdlib>
@@ -2698,10 +2699,81 @@ __device__ __forceinline__ SE3 chain_oMi_lat(const DevWorld& w, const LatJoints&
   }
   return T;
 }
+// World transform of one side of a latency record (LS_* layout: chain of
+// joints, link placement, moving offset; a static side holds its world
+// transform at LS_OFF): chain_oMi + link_from_oMi + the moving offset, the
+// same products in the same order
+__device__ __forceinline__ SE3 rec_side_tf(const double* S, bool moving, const double* qrow, const double* sc_row) {
+  if (!moving) return load_se3(S + LS_OFF);
+  const int cl = (int)S[LS_CL];
+  SE3 T;
+  se3_identity(T);
+  for (int k = 0; k < cl; ++k) {
+    const double* J = S + LS_J + LJ_STRIDE * k;
+    const int type = (int)J[0], srcq = (int)J[1];
+    const bool pre = srcq >= 0 && joint_is_revolute(type);
+    const double qv = pre ? 0.0 : srcq >= 0 ? qrow[srcq] : J[2];
+    const SE3 M = joint_motion(type, J + 3, qv, pre ? sc_row + 2 * srcq : nullptr);
+    const SE3 li = se3_mul(load_se3(J + 6), M);
+    T = k == 0 ? li : se3_mul(T, li);
+  }
+  const SE3 L = se3_mul(T, load_se3(S + LS_LINKPL));
+  double qw, qxyz[3];
+  mat_to_quat(L.R, &qw, qxyz);
+  SE3 Lr;
+  quat_to_mat(qw, qxyz[0], qxyz[1], qxyz[2], Lr.R);
+  Lr.p[0] = L.p[0];
+  Lr.p[1] = L.p[1];
+  Lr.p[2] = L.p[2];
+  return se3_mul(Lr, load_se3(S + LS_OFF));
+}
+
+// The latency paths' second bounding test (after the spheres): the two
+// objects' oriented boxes (local AABBs, world rotation) in fp64, every bound
+// widened by `margin` (the latency margin: at least libccd's false-hit reach,
+// as the cull's fp32 test), so a separated pair cannot be an MPR hit.  R:
+// row-major world rotation (column j = box axis j), c: world centre, e: half
+// extents.
+__device__ __forceinline__ bool dobb_separated(const double* RA, const double* ca, const double* ea, const double* RB,
+                                               const double* cb, const double* eb, double margin) {
+  const double d[3] = {cb[0] - ca[0], cb[1] - ca[1], cb[2] - ca[2]};
+  double Rm[3][3], Ab[3][3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      Rm[i][j] = RA[i] * RB[j] + RA[3 + i] * RB[3 + j] + RA[6 + i] * RB[6 + j];
+      Ab[i][j] = std::fabs(Rm[i][j]) + 1e-12;
+    }
+  double t[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) t[i] = d[0] * RA[i] + d[1] * RA[3 + i] + d[2] * RA[6 + i];
+  bool sep = false;
+#pragma unroll
+  for (int i = 0; i < 3; ++i) sep |= std::fabs(t[i]) > ea[i] + (eb[0] * Ab[i][0] + eb[1] * Ab[i][1] + eb[2] * Ab[i][2]) + margin;
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const double ra = ea[0] * Ab[0][j] + ea[1] * Ab[1][j] + ea[2] * Ab[2][j];
+    sep |= std::fabs(t[0] * Rm[0][j] + t[1] * Rm[1][j] + t[2] * Rm[2][j]) > ra + eb[j] + margin;
+  }
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const int i1 = (i + 1) % 3, i2 = (i + 2) % 3;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const int j1 = (j + 1) % 3, j2 = (j + 2) % 3;
+      const double ra = ea[i1] * Ab[i2][j] + ea[i2] * Ab[i1][j];
+      const double rb = eb[j1] * Ab[i][j2] + eb[j2] * Ab[i][j1];
+      sep |= std::fabs(t[i2] * Rm[i1][j] - t[i1] * Rm[i2][j]) > ra + rb + margin;
+    }
+  }
+  return sep;
+}
+
 // The smallest batches' rows by value in the kernel arguments (which the
 // launch writes to device memory anyway): row c = q[dof], then sin/cos
 // [2 dof] (revolute sources only), no read of host memory from the kernel
-constexpr int kLatIn = 64;
+constexpr int kLatIn = 256;  // 12 states of a 7-dof group
 struct LatIn {
   double d[kLatIn];
 };
@@ -2808,7 +2880,8 @@ __global__ __launch_bounds__(256) void small_kernel(DevWorld w, const double* __
       if constexpr (SCM == 3) {
         __shared__ double lat_in[4][kLatIn];
         double* I = lat_in[threadIdx.x >> 6];
-        I[lane] = args.d[lane];
+        const int nin = (int)n * 3 * w.dof;
+        for (int i = (int)lane; i < nin; i += 64) I[i] = args.d[i];
         sc_row = I + (size_t)cs * 3 * w.dof + w.dof;
         qrow = I + (size_t)cs * 3 * w.dof;
       } else if (split) {  // state cs's rows: lane cs's LDS copy
@@ -2819,32 +2892,8 @@ __global__ __launch_bounds__(256) void small_kernel(DevWorld w, const double* __
       for (int i = 0; i < kPer; ++i)
         if ((int)lane + 64 * i < LR_STRIDE) R[lane + 64 * i] = v[i];
       wave_lds_sync();
-      // chain_oMi_lat + link_from_oMi + moving offset on the record: the same
-      // products in the same order
       auto tf = [&](int sd) {
-        const double* S = R + LR_SIDE + LS_STRIDE * sd;
-        if (R[sd ? LR_BM : LR_AM] == 0.0) return load_se3(S + LS_OFF);
-        const int cl = (int)S[LS_CL];
-        SE3 T;
-        se3_identity(T);
-        for (int k = 0; k < cl; ++k) {
-          const double* J = S + LS_J + LJ_STRIDE * k;
-          const int type = (int)J[0], srcq = (int)J[1];
-          const bool pre = srcq >= 0 && joint_is_revolute(type);
-          const double qv = pre ? 0.0 : srcq >= 0 ? qrow[srcq] : J[2];
-          const SE3 M = joint_motion(type, J + 3, qv, pre ? sc_row + 2 * srcq : nullptr);
-          const SE3 li = se3_mul(load_se3(J + 6), M);
-          T = k == 0 ? li : se3_mul(T, li);
-        }
-        const SE3 L = se3_mul(T, load_se3(S + LS_LINKPL));
-        double qw, qxyz[3];
-        mat_to_quat(L.R, &qw, qxyz);
-        SE3 Lr;
-        quat_to_mat(qw, qxyz[0], qxyz[1], qxyz[2], Lr.R);
-        Lr.p[0] = L.p[0];
-        Lr.p[1] = L.p[1];
-        Lr.p[2] = L.p[2];
-        return se3_mul(Lr, load_se3(S + LS_OFF));
+        return rec_side_tf(R + LR_SIDE + LS_STRIDE * sd, R[sd ? LR_BM : LR_AM] != 0.0, qrow, sc_row);
       };
       tmark(1, tlast);  // the record in LDS
       if (split) {
@@ -2900,15 +2949,23 @@ __global__ __launch_bounds__(256) void small_kernel(DevWorld w, const double* __
       }
       rsum = ra[G_RADIUS] + rb[G_RADIUS];
     }
-    double d2 = 0.0;
+    double d2 = 0.0, wc[2][3];
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
       const double ci = ((TA.R[3 * i] * oa[0] + TA.R[3 * i + 1] * oa[1]) + TA.R[3 * i + 2] * oa[2]) + TA.p[i];
       const double cj = ((TB.R[3 * i] * ob[0] + TB.R[3 * i + 1] * ob[1]) + TB.R[3 * i + 2] * ob[2]) + TB.p[i];
+      wc[0][i] = ci;
+      wc[1][i] = cj;
       d2 += (ci - cj) * (ci - cj);
     }
     const double rr = rsum + w.small_margin;
-    const bool near = live && d2 <= rr * rr && !w.dbg(3) && !(w.dbg(7) && d2 >= 0.0);
+    bool near = live && d2 <= rr * rr && !w.dbg(3) && !(w.dbg(7) && d2 >= 0.0);
+    if (CLS == CLS_CLOSED && __ballot(near) != 0ull) {  // the boxes next (MPR / closed-form pairs)
+      const cptr<double> ra = w.geom_rec + G_STRIDE * ga, rb = w.geom_rec + G_STRIDE * gb;
+      const double ea[3] = {ra[G_OBB_E], ra[G_OBB_E + 1], ra[G_OBB_E + 2]};
+      const double eb[3] = {rb[G_OBB_E], rb[G_OBB_E + 1], rb[G_OBB_E + 2]};
+      if (near && dobb_separated(TA.R, wc[0], ea, TB.R, wc[1], eb, w.small_margin)) near = false;
+    }
     tmark(3, tlast);  // bounding spheres
     if (CLS != CLS_CLOSED) {
       hit = (walk_wave_eval<CLS>(w, HV, ga, TA, gb, TB, near) >> lane) & 1ull;
@@ -2957,6 +3014,286 @@ __global__ __launch_bounds__(256) void small_kernel(DevWorld w, const double* __
       atomicAdd(&w.stats[30], tm[5] - ts0);
       atomicMax(&w.stats[38], tm[5] - ts0);
       atomicMax(&w.stats[31], ((tm[4] - tm[3]) << 12) | (uint64_t)p);  // the slowest narrow test's pair
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Latency server: one resident workgroup that serves the smallest host
+// batches without a kernel launch each.  The host writes the rows (q, then
+// the joint sin/cos it computed) into host-mapped memory and bumps `seq`;
+// thread 0 polls it (system-scope loads, s_sleep between polls) and the
+// workgroup then runs one batch: FK per (state, moving object) from the
+// objects' records in LDS, the bounding-sphere test per (pair, state), the
+// near pairs' closed forms / MPR one pair per wave with lanes = states (the
+// code small_kernel runs), pair-mask words written with system-scope stores,
+// one barrier, ONE system-scope release store of `done` = seq.  It returns
+// after idle_ticks (s_memrealtime, 100 MHz) without a request, or when the
+// host sets `quit`: every path through the poll loop ends.
+// ---------------------------------------------------------------------------
+constexpr int kSrvN = 16;        // states per served batch
+constexpr int kSrvMaxW = 16;     // pair-mask words per state (512 pairs)
+constexpr int kSrvThreads = 512;
+constexpr int kSrvPT = 24;       // pair-table doubles per pair
+struct SrvCtl {
+  unsigned long long seq, n, quit, done, pad[4];
+  unsigned long long phase[8];  // s_memrealtime at the batch's phase ends (diagnostics)
+  double rows[kSrvN * 3 * kLatScDof];  // per state: q[dof], then (sin, cos)[dof]
+  uint32_t out[kSrvN * kSrvMaxW];      // per state: pair-mask words
+};
+
+__device__ __forceinline__ unsigned long long sys_load(const unsigned long long* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+constexpr int kSrvJT = 20;   // joint table: type, source, constant, parent, axis[3], pad, placement[12]
+constexpr int kSrvOB = 25;   // object table: link placement[12], moving offset[12], the link's parent joint
+// LDS carve-up (doubles, then 32-bit words): joint table, object table,
+// static rotations, pair table, rows, joint frames per state, object
+// transforms per state, near masks, near-pair list, hit masks
+__host__ __device__ inline size_t srv_lds_bytes(int M, int P, int dof, int W, int nj, int ns) {
+  const size_t dbl = (size_t)nj * kSrvJT + (size_t)M * kSrvOB + (size_t)ns * 9 + (size_t)P * kSrvPT +
+                     (size_t)kSrvN * 3 * dof + (size_t)kSrvN * nj * 12 + (size_t)kSrvN * M * 12;
+  return dbl * 8 + ((size_t)2 * P + (size_t)kSrvN * W) * 4;
+}
+
+__global__ __launch_bounds__(kSrvThreads) void lat_server_kernel(DevWorld w, SrvCtl* ctl, unsigned long long last,
+                                                                 unsigned long long idle_ticks) {
+  extern __shared__ double srv_lds[];
+  const int M = w.n_moving, P = w.n_pairs, dof = w.dof, W = w.W, nj = w.nj, NS = w.n_static;
+  double* JT = srv_lds;
+  double* OBJ = JT + (size_t)nj * kSrvJT;
+  double* SROT = OBJ + (size_t)M * kSrvOB;
+  double* PT = SROT + (size_t)NS * 9;
+  double* ROWS = PT + (size_t)P * kSrvPT;
+  double* OMI = ROWS + (size_t)kSrvN * 3 * dof;
+  double* TT = OMI + (size_t)kSrvN * nj * 12;
+  uint32_t* NEAR = reinterpret_cast<uint32_t*>(TT + (size_t)kSrvN * M * 12);
+  int* NLIST = reinterpret_cast<int*>(NEAR + P);
+  uint32_t* HM = reinterpret_cast<uint32_t*>(NLIST + P);
+  __shared__ unsigned long long s_cmd;
+  __shared__ int s_nl;
+  const int t = (int)threadIdx.x;
+  const cptr<double> HV = w.hull;
+  unsigned long long ph[6];  // thread 0's phase stamps
+  auto stamp = [&](int k) {
+    if (t == 0) ph[k] = __builtin_amdgcn_s_memrealtime();
+  };
+  // once per residency: joint, object, static-rotation and pair tables
+  for (int j = t; j < nj; j += kSrvThreads) {
+    double* J = JT + (size_t)kSrvJT * j;
+    J[0] = w.joint_type[j];
+    J[1] = w.joint_q_source[j];
+    J[2] = w.joint_q_const[j];
+    J[3] = w.joint_parent[j];
+    for (int i = 0; i < 3; ++i) J[4 + i] = w.joint_axis[3 * j + i];
+    for (int i = 0; i < 12; ++i) J[8 + i] = w.joint_place[12 * j + i];
+  }
+  for (int m = t; m < M; m += kSrvThreads) {
+    double* O = OBJ + (size_t)kSrvOB * m;
+    const int l = w.moving_link[m];
+    for (int i = 0; i < 12; ++i) O[i] = w.link_place[12 * l + i];
+    for (int i = 0; i < 12; ++i) O[12 + i] = w.moving_offset[12 * m + i];
+    O[24] = w.link_parent[l];
+  }
+  for (int i = t; i < NS * 9; i += kSrvThreads) SROT[i] = w.static_T[12 * (i / 9) + i % 9];
+  for (int p = t; p < P; p += kSrvThreads) {
+    const cptr<double> R = w.lat_rec + (size_t)LR_STRIDE * p;
+    double* E = PT + (size_t)kSrvPT * p;
+    E[0] = R[LR_ALLOWED];
+    E[1] = R[LR_CF];
+    E[2] = R[LR_GA];
+    E[3] = R[LR_GB];
+    E[4] = w.pair_a[p];
+    E[5] = w.pair_b[p];
+    E[6] = R[LR_RA] + R[LR_RB];
+    for (int i = 0; i < 3; ++i) {  // half extents of the boxes
+      E[13 + i] = w.geom_rec[G_STRIDE * (int)R[LR_GA] + G_OBB_E + i];
+      E[16 + i] = w.geom_rec[G_STRIDE * (int)R[LR_GB] + G_OBB_E + i];
+    }
+    for (int sd = 0; sd < 2; ++sd) {
+      const cptr<double> S = R + LR_SIDE + LS_STRIDE * sd;
+      const double o0 = S[LS_OBBC], o1 = S[LS_OBBC + 1], o2 = S[LS_OBBC + 2];
+      if (R[sd ? LR_BM : LR_AM] != 0.0) {  // moving: the centre in its own frame
+        E[7 + 3 * sd] = o0;
+        E[8 + 3 * sd] = o1;
+        E[9 + 3 * sd] = o2;
+      } else {  // static: its world centre, as small_kernel computes it
+        const SE3 T = load_se3(S + LS_OFF);
+        for (int i = 0; i < 3; ++i)
+          E[7 + 3 * sd + i] = ((T.R[3 * i] * o0 + T.R[3 * i + 1] * o1) + T.R[3 * i + 2] * o2) + T.p[i];
+      }
+    }
+  }
+  __syncthreads();
+  for (;;) {
+    if (t == 0) {
+      const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+      unsigned long long cmd = 0;
+      for (;;) {
+        const unsigned long long sq = sys_load(&ctl->seq);
+        if (sq != last) {
+          cmd = sq;
+          break;
+        }
+        if (sys_load(&ctl->quit) != 0ull) break;
+        if (__builtin_amdgcn_s_memrealtime() - t0 > idle_ticks) break;
+        __builtin_amdgcn_s_sleep(4);
+      }
+      s_cmd = cmd;  // the batch size rides in the low byte of seq
+      s_nl = 0;
+    }
+    __syncthreads();
+    const unsigned long long cmd = s_cmd;
+    if (cmd == 0ull) return;  // idle or quit: the whole workgroup leaves together
+    last = cmd;
+    stamp(0);
+    const int n = (int)min(cmd & 255ull, (unsigned long long)kSrvN);
+    for (int i = t; i < n * 3 * dof; i += kSrvThreads)
+      ROWS[i] = __longlong_as_double((long long)sys_load(reinterpret_cast<const unsigned long long*>(&ctl->rows[i])));
+    for (int i = t; i < P; i += kSrvThreads) NEAR[i] = 0u;
+    for (int i = t; i < n * W; i += kSrvThreads) HM[i] = 0u;
+    __syncthreads();
+    stamp(1);
+    // FK, first the joint frames (forward_kinematics: oMi[j] = oMi[parent] *
+    // (placement * M(q)), the products chain_oMi forms for every link), one
+    // state per thread ...
+    if (t < n) {
+      const double* row = ROWS + (size_t)t * 3 * dof;
+      double* om = OMI + (size_t)t * nj * 12;
+      for (int j = 0; j < nj; ++j) {
+        const double* J = JT + (size_t)kSrvJT * j;
+        const int type = (int)J[0], srcq = (int)J[1], par = (int)J[3];
+        const bool pre = srcq >= 0 && joint_is_revolute(type);
+        const double qv = pre ? 0.0 : srcq >= 0 ? row[srcq] : J[2];
+        const SE3 li = se3_mul(load_se3(J + 8), joint_motion(type, J + 4, qv, pre ? row + dof + 2 * srcq : nullptr));
+        const SE3 T = par > 0 ? se3_mul(load_se3(om + 12 * (par - 1)), li) : li;
+        double* o = om + 12 * j;
+#pragma unroll
+        for (int i = 0; i < 9; ++i) o[i] = T.R[i];
+        o[9] = T.p[0];
+        o[10] = T.p[1];
+        o[11] = T.p[2];
+      }
+    }
+    __syncthreads();
+    // ... then one (state, moving object) per thread: link_from_oMi and the
+    // moving offset, as rec_side_tf
+    for (int k = t; k < n * M; k += kSrvThreads) {
+      const int c = k / M, m = k - c * M;
+      const double* O = OBJ + (size_t)kSrvOB * m;
+      const int jl = (int)O[24];
+      SE3 P0;
+      if (jl > 0) P0 = load_se3(OMI + ((size_t)c * nj + jl - 1) * 12);
+      else se3_identity(P0);
+      const SE3 L = se3_mul(P0, load_se3(O));
+      double qw, qxyz[3];
+      mat_to_quat(L.R, &qw, qxyz);
+      SE3 Lr;
+      quat_to_mat(qw, qxyz[0], qxyz[1], qxyz[2], Lr.R);
+      Lr.p[0] = L.p[0];
+      Lr.p[1] = L.p[1];
+      Lr.p[2] = L.p[2];
+      const SE3 T = se3_mul(Lr, load_se3(O + 12));
+      double* o = TT + ((size_t)c * M + m) * 12;
+#pragma unroll
+      for (int i = 0; i < 9; ++i) o[i] = T.R[i];
+      o[9] = T.p[0];
+      o[10] = T.p[1];
+      o[11] = T.p[2];
+    }
+    __syncthreads();
+    stamp(2);
+    // bounding spheres: one (pair, state) per thread
+    for (int k = t; k < P * n; k += kSrvThreads) {
+      const int p = k / n, c = k - p * n;
+      const double* E = PT + (size_t)kSrvPT * p;
+      if (E[0] != 0.0) continue;  // ACM-allowed
+      double ce[2][3];
+      const double* Rs[2];
+      for (int sd = 0; sd < 2; ++sd) {
+        const int id = (int)E[4 + sd];
+        const double* oc = E + 7 + 3 * sd;
+        if (id < M) {
+          const double* T = TT + ((size_t)c * M + id) * 12;
+          Rs[sd] = T;
+#pragma unroll
+          for (int i = 0; i < 3; ++i) ce[sd][i] = ((T[3 * i] * oc[0] + T[3 * i + 1] * oc[1]) + T[3 * i + 2] * oc[2]) + T[9 + i];
+        } else {
+          Rs[sd] = nullptr;
+#pragma unroll
+          for (int i = 0; i < 3; ++i) ce[sd][i] = oc[i];
+        }
+      }
+      double d2 = 0.0;
+#pragma unroll
+      for (int i = 0; i < 3; ++i) d2 += (ce[0][i] - ce[1][i]) * (ce[0][i] - ce[1][i]);
+      const double rr = E[6] + w.small_margin;
+      if (!(d2 <= rr * rr)) continue;
+      for (int sd = 0; sd < 2; ++sd)  // static sides: their world rotation
+        if (!Rs[sd]) Rs[sd] = SROT + 9 * ((int)E[4 + sd] - M);
+      if (!dobb_separated(Rs[0], ce[0], E + 13, Rs[1], ce[1], E + 16, w.small_margin)) atomicOr(&NEAR[p], 1u << c);
+    }
+    __syncthreads();
+    for (int p = t; p < P; p += kSrvThreads)
+      if (NEAR[p]) NLIST[atomicAdd(&s_nl, 1)] = p;
+    __syncthreads();
+    stamp(3);
+    // narrow: one near pair per wave at a time, lanes = states
+    const int wv = t >> 6, lane = t & 63, nl = s_nl;
+    for (int k = wv; k < nl; k += kSrvThreads / 64) {
+      const int p = __builtin_amdgcn_readfirstlane(NLIST[k]);
+      const double* E = PT + (size_t)kSrvPT * p;
+      const int cf = __builtin_amdgcn_readfirstlane((int)E[1]);
+      const int ga = __builtin_amdgcn_readfirstlane((int)E[2]), gb = __builtin_amdgcn_readfirstlane((int)E[3]);
+      const int a = __builtin_amdgcn_readfirstlane((int)E[4]), b = __builtin_amdgcn_readfirstlane((int)E[5]);
+      const bool near = lane < n && ((NEAR[p] >> lane) & 1u);
+      const int c = lane < n ? lane : 0;
+      const SE3 TA = a < M ? load_se3(TT + ((size_t)c * M + a) * 12) : load_se3(w.static_T + 12 * (a - M));
+      const SE3 TB = b < M ? load_se3(TT + ((size_t)c * M + b) * 12) : load_se3(w.static_T + 12 * (b - M));
+      bool hit = false;
+      if (cf != CF_NONE) {
+        if (near && pair_closed_form<CLS_CLOSED>(cf, w, ga, TA, gb, TB)) hit = true;
+      } else {
+        GObj A, B;
+        A.rot = gjk_rot_from_matrix(TA.R);
+        A.rot_inv = quat_invert2(A.rot);
+        A.pos = cv3(TA.p[0], TA.p[1], TA.p[2]);
+        A.geom = ga;
+        A.type = w.geom_type[ga];
+        B.rot = gjk_rot_from_matrix(TB.R);
+        B.rot_inv = quat_invert2(B.rot);
+        B.pos = cv3(TB.p[0], TB.p[1], TB.p[2]);
+        B.geom = gb;
+        B.type = w.geom_type[gb];
+        int st = MPR_DONE;
+        CV3 v0, v1, v2, v3, dir;
+        if (near) mpr_begin(center(w, A), center(w, B), st, v0, dir);
+        while (__ballot(st != MPR_DONE) != 0) {
+          if (st != MPR_DONE) {
+            const CV3 sp = msupport(w, HV, A, B, dir);
+            const int res = mpr_advance(w.mpr_tol, sp, st, v0, v1, v2, v3, dir);
+            if (res != 0) {
+              hit = res > 0;
+              st = MPR_DONE;
+            }
+          }
+        }
+      }
+      if (hit) atomicOr(&HM[c * W + (p >> 5)], 1u << (p & 31));
+    }
+    __syncthreads();
+    stamp(4);
+    // publish: wave 0 writes every pair-mask word, then its lane 0 releases
+    // `done` at system scope (the release waits for the whole wave's stores)
+    if (t < 64) {
+      for (int i = t; i < n * W; i += 64) __hip_atomic_store(&ctl->out[i], HM[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      if (t == 0) {
+        ph[5] = __builtin_amdgcn_s_memrealtime();
+        for (int k = 0; k < 6; ++k) __hip_atomic_store(&ctl->phase[k], ph[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+      __builtin_amdgcn_s_waitcnt(0);
+      if (t == 0) __hip_atomic_store(&ctl->done, cmd, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
   }
 }
@@ -5762,6 +6099,20 @@ struct mpg_world {
   hipStream_t own_stream = nullptr;
   bool small_zero_copy = true; // MPG_SMALL_ZEROCOPY=0: stage through d_qs
   int64_t small_inline_sc = 256;  // latency batches up to this size: sin/cos inline (MPG_SMALL_INLINE_SC)
+  // latency server (lat_server_kernel): control block in host-mapped memory,
+  // its own stream; started on demand, leaves after srv_idle_us idle
+  SrvCtl* srv_h = nullptr;
+  SrvCtl* srv_d = nullptr;
+  hipStream_t srv_stream = nullptr;
+  unsigned long long srv_seq = 0;
+  bool srv_running = false;
+  bool srv_ok = false;      // the world fits the server (closed-form / MPR pairs only, records, LDS)
+  bool srv_broken = false;  // it failed to answer once: launches from then on
+  int srv_mode = 1;         // MPG_SMALL_SERVER=0: off
+  long long srv_idle_us = 1000;
+  size_t srv_lds = 0;
+  bool srv_stats = false;
+  double srv_stat[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   size_t small_cap = 0;   // configurations (hit bytes per pair)
   size_t small_qcap = 0;  // input doubles (h_q, d_qs)
 };
@@ -7277,6 +7628,12 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
     if (d->joint_q_source[j] >= 0 && joint_is_revolute(d->joint_type[j]) &&
         std::find(w->h_rev_src.begin(), w->h_rev_src.end(), d->joint_q_source[j]) == w->h_rev_src.end())
       w->h_rev_src.push_back(d->joint_q_source[j]);
+  if (const char* e = std::getenv("MPG_SMALL_SERVER")) w->srv_mode = std::atoi(e);
+  w->srv_stats = std::getenv("MPG_STATS") != nullptr;
+  if (const char* e = std::getenv("MPG_SMALL_SERVER_IDLE_US")) w->srv_idle_us = std::max(10ll, std::atoll(e));
+  w->srv_lds = srv_lds_bytes(d->n_moving, d->n_pairs, d->dof, w->dw.W, d->n_joints, d->n_static);
+  w->srv_ok = lat_rec_ok && !w->any_octree && !w->any_mesh && d->dof > 0 && d->dof <= kLatScDof &&
+              d->n_pairs > 0 && w->dw.W <= kSrvMaxW && w->srv_lds <= 150 * 1024;
   const char* own = std::getenv("MPG_OWN_STREAM");
   if (!own || std::atoi(own) != 0) HIP_TRY(hipStreamCreateWithFlags(&w->own_stream, hipStreamNonBlocking));
   *out = w;
@@ -7307,6 +7664,17 @@ int mpg_world_destroy(mpg_world* w) {
                  st[3], st[4], st[5], st[7], st[7] ? (double)st[6] / st[7] : 0.0, st[2],
                  st[2] ? (double)st[0] / st[2] : 0.0, st[8], st[8] ? (double)st[1] / st[8] : 0.0);
     hipFree(w->dw.stats);
+  }
+  if (w->srv_stats && w->srv_stat[5] > 0)
+    std::fprintf(stderr, "[mpg stats] latency server, mean us over %.0f batches: rows %.2f, fk %.2f, spheres %.2f, "
+                 "narrow %.2f, publish %.2f; host post->done %.2f\n", w->srv_stat[5], w->srv_stat[0] / w->srv_stat[5],
+                 w->srv_stat[1] / w->srv_stat[5], w->srv_stat[2] / w->srv_stat[5], w->srv_stat[3] / w->srv_stat[5],
+                 w->srv_stat[4] / w->srv_stat[5], w->srv_stat[6] / w->srv_stat[5]);
+  if (w->srv_h) {  // the server leaves at its next poll
+    __atomic_store_n(&w->srv_h->quit, 1ull, __ATOMIC_RELEASE);
+    hipStreamSynchronize(w->srv_stream);
+    hipStreamDestroy(w->srv_stream);
+    hipHostFree(w->srv_h);
   }
   hipFree(w->blob);
   if (w->h_q) hipHostFree(w->h_q);
@@ -7407,11 +7775,88 @@ int ensure_small(mpg_world* w, size_t ncfg, size_t row) {
   return MPG_OK;
 }
 
+// (re)start the latency server; it takes `done` as the last batch served
+int srv_start(mpg_world* w) {
+  if (!w->srv_h) {
+    HIP_TRY(hipHostMalloc((void**)&w->srv_h, sizeof(SrvCtl), hipHostMallocMapped | hipHostMallocCoherent));
+    std::memset(w->srv_h, 0, sizeof(SrvCtl));
+    HIP_TRY(hipHostGetDevicePointer((void**)&w->srv_d, w->srv_h, 0));
+    HIP_TRY(hipStreamCreateWithFlags(&w->srv_stream, hipStreamNonBlocking));
+    HIP_TRY(hipFuncSetAttribute((const void*)lat_server_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)w->srv_lds));
+  }
+  const unsigned long long last = __atomic_load_n(&w->srv_h->done, __ATOMIC_ACQUIRE);
+  hipLaunchKernelGGL(lat_server_kernel, dim3(1), dim3(kSrvThreads), w->srv_lds, w->srv_stream, w->dw, w->srv_d, last,
+                     (unsigned long long)w->srv_idle_us * 100ull);
+  HIP_TRY(hipGetLastError());
+  w->srv_running = true;
+  return MPG_OK;
+}
+
+// one batch through the resident server: rows (q, host sin/cos) into the
+// control block, seq bumped, the host spins on `done`.  The server may have
+// left (idle) before it saw the request: the stream is checked every 50 us
+// and the server restarted.  No answer within 2 s: the server is stopped and
+// marked broken, MPG_E_HIP (the caller then launches).
+int collide_served(mpg_world* w, const double* q, int64_t n, uint8_t* flags, uint32_t* pair_mask) {
+  if (!w->srv_running) {
+    const int rc = srv_start(w);
+    if (rc) return rc;
+  }
+  SrvCtl* C = w->srv_h;
+  const int dof = w->dw.dof, W = w->dw.W;
+  for (int64_t c = 0; c < n; ++c) {
+    double* r = C->rows + c * 3 * dof;
+    std::memcpy(r, q + c * dof, sizeof(double) * (size_t)dof);
+    for (const int src : w->h_rev_src) mpg_sincos(q[c * dof + src], &r[dof + 2 * src], &r[dof + 2 * src + 1]);
+  }
+  const unsigned long long seq = (++w->srv_seq << 8) | (unsigned long long)n;
+  __atomic_store_n(&C->seq, seq, __ATOMIC_RELEASE);
+  const auto t0 = std::chrono::steady_clock::now();
+  long long next_us = 50;
+  while (__atomic_load_n(&C->done, __ATOMIC_ACQUIRE) != seq) {
+    __builtin_ia32_pause();
+    const long long us =
+        std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t0).count();
+    if (us < next_us) continue;
+    next_us = us + 50;
+    const hipError_t e = hipStreamQuery(w->srv_stream);
+    if (e == hipSuccess) {  // it left before this request: start it again
+      w->srv_running = false;
+      const int rc = srv_start(w);
+      if (rc) return rc;
+    } else if (e != hipErrorNotReady || us > 2000000) {
+      __atomic_store_n(&C->quit, 1ull, __ATOMIC_RELEASE);
+      w->srv_broken = true;
+      return set_error(MPG_E_HIP, "latency server did not answer");
+    }
+  }
+  if (w->srv_stats) {  // MPG_STATS: phase sums (rows, fk, spheres, narrow, publish), us
+    w->srv_stat[5] += 1.0;
+    for (int k = 0; k < 5; ++k) w->srv_stat[k] += (double)(C->phase[k + 1] - C->phase[k]) / 100.0;
+    w->srv_stat[6] += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+  }
+  for (int64_t c = 0; c < n; ++c) {
+    uint32_t any = 0;
+    for (int k = 0; k < W; ++k) {
+      const uint32_t v = __atomic_load_n(&C->out[c * W + k], __ATOMIC_RELAXED);
+      any |= v;
+      if (pair_mask) pair_mask[c * W + k] = v;
+    }
+    flags[c] = any ? 1 : 0;
+  }
+  return MPG_OK;
+}
+
 // one round trip: input to the device, one small_kernel launch writing hit
 // bytes straight into host memory, one synchronisation; the host folds the
 // hits into flags / pair masks
 template <bool FROM_POSES>
 int collide_small(mpg_world* w, const double* q, int64_t n, uint8_t* flags, uint32_t* pair_mask, hipStream_t s) {
+  if (!FROM_POSES && w->srv_mode && w->srv_ok && !w->srv_broken && n <= kSrvN && w->dw.debug_mode == 0) {
+    const int rc = collide_served(w, q, n, flags, pair_mask);
+    if (rc == MPG_OK || !w->srv_broken) return rc;
+  }
   const size_t row = FROM_POSES ? (size_t)w->dw.n_links * 7 : (size_t)w->dw.dof;
   const size_t cap = std::max<size_t>((size_t)n, std::min<size_t>((size_t)w->small_max, 256));
   int rc = ensure_small(w, cap, row);

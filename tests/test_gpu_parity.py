@@ -321,11 +321,15 @@ def test_attached_box_in_box_scene_matches_oracle():
     assert sum(int(h.sum()) for h in hits) > 0  # the closed form is exercised with both outcomes
 
 
+@pytest.mark.parametrize("server", [1, 0])
 @pytest.mark.parametrize("cfg", [2, 3, 4])
-def test_latency_path_matches_oracle(cfg):
+def test_latency_path_matches_oracle(cfg, server, monkeypatch):
     """Host batches up to the small-batch limit run as one small_kernel launch
     (one wave per pair x 64-config tile, bounding-sphere test, MPR / closed
-    forms): bit-exact with the oracle and with the two-phase pipeline."""
+    forms), up to 16 states through the resident latency server
+    (MPG_SMALL_SERVER): bit-exact with the oracle and with the two-phase
+    pipeline."""
+    monkeypatch.setenv("MPG_SMALL_SERVER", str(server))
     w, art = scenes.world(cfg)
     q = Wd.sample_q(ow(cfg).art, 20000, 40 + cfg)
     fo, mo = ow(cfg).collide_batch(q, nthreads=NTHREADS)
@@ -348,10 +352,37 @@ def test_latency_path_matches_oracle(cfg):
         np.testing.assert_array_equal(f, fo[i:i + 2])
         np.testing.assert_array_equal(m, mo[i:i + 2])
     assert 0 < fo[:400].sum() < 400
+    for n in (4, 7, 16):  # served batches of several states
+        for i in range(0, 160, n):
+            f, m = w.collide_batch(q[i:i + n])
+            np.testing.assert_array_equal(f, fo[i:i + n])
+            np.testing.assert_array_equal(m, mo[i:i + n])
     w.set_small_batch_max(0)
     f, m = w.collide_batch(q[:1000])
     np.testing.assert_array_equal(f, fo[:1000])
     np.testing.assert_array_equal(m, mo[:1000])
+
+
+def test_latency_server_idle_restart_and_teardown(monkeypatch):
+    """The resident server leaves after its idle time and is started again by
+    the next request; worlds destroyed with their server resident; two
+    worlds' servers side by side."""
+    import gc
+    import time as _t
+    monkeypatch.setenv("MPG_SMALL_SERVER_IDLE_US", "200")
+    w, art = scenes.world(3)
+    w2, _ = scenes.world(3)
+    q = Wd.sample_q(ow(3).art, 64, 77)
+    fo, mo = ow(3).collide_batch(q, nthreads=NTHREADS)
+    for k in range(64):
+        for ww in (w, w2):
+            f, m = ww.collide_batch(q[k:k + 1])
+            np.testing.assert_array_equal(f, fo[k:k + 1])
+            np.testing.assert_array_equal(m, mo[k:k + 1])
+        if k % 8 == 0:
+            _t.sleep(0.002)  # > idle: the servers have left
+    del w, w2
+    gc.collect()
 
 
 def test_spheres_closed_forms_match_oracle():
