@@ -130,15 +130,15 @@ __device__ __forceinline__ V3 convex_full_scan(const DevWorld& w, cptr<double> H
 // round trip per step instead of one per neighbour, and the per-lane rare path
 // no longer holds the other 63 lanes for the length of a serial walk.
 constexpr int kWalkWords = kMaxWalkVerts / 64;
-struct WalkScratch {  // one per wave (blocks of <= 256 threads)
+struct WalkScratch {  // one per wave (blocks of <= 512 threads)
   uint64_t vis[kWalkWords];
   double dd[64];
   int vi[64];
 };
 
 __device__ __forceinline__ WalkScratch& walk_scratch() {
-  __shared__ WalkScratch s_walk[4];
-  return s_walk[(threadIdx.x >> 6) & 3];
+  __shared__ WalkScratch s_walk[8];  // one per wave: 256-thread blocks, the 512-thread latency server
+  return s_walk[(threadIdx.x >> 6) & 7];
 }
 
 // LDS written by some lanes of this wave, read by others: keep the compiler
@@ -3032,14 +3032,16 @@ __global__ __launch_bounds__(256) void small_kernel(DevWorld w, const double* __
 // host sets `quit`: every path through the poll loop ends.
 // ---------------------------------------------------------------------------
 constexpr int kSrvN = 16;        // states per served batch
+constexpr int kSrvMaxG = 8;      // workgroups (pair p belongs to workgroup p % G)
 constexpr int kSrvMaxW = 16;     // pair-mask words per state (512 pairs)
 constexpr int kSrvThreads = 512;
 constexpr int kSrvPT = 24;       // pair-table doubles per pair
 struct SrvCtl {
-  unsigned long long seq, n, quit, done, pad[4];
-  unsigned long long phase[8];  // s_memrealtime at the batch's phase ends (diagnostics)
+  unsigned long long seq, quit, pad[6];
+  unsigned long long done[kSrvMaxG];   // per workgroup: the last batch it published
+  unsigned long long phase[8];         // workgroup 0's s_memrealtime at the batch's phase ends (diagnostics)
   double rows[kSrvN * 3 * kLatScDof];  // per state: q[dof], then (sin, cos)[dof]
-  uint32_t out[kSrvN * kSrvMaxW];      // per state: pair-mask words
+  uint32_t out[kSrvMaxG][kSrvN * kSrvMaxW];  // per workgroup, per state: its pairs' mask words
 };
 
 __device__ __forceinline__ unsigned long long sys_load(const unsigned long long* p) {
@@ -3048,17 +3050,25 @@ __device__ __forceinline__ unsigned long long sys_load(const unsigned long long*
 
 constexpr int kSrvJT = 20;   // joint table: type, source, constant, parent, axis[3], pad, placement[12]
 constexpr int kSrvOB = 25;   // object table: link placement[12], moving offset[12], the link's parent joint
+// one element of se3_mul(A, B) (lane e: row e / 4, column e % 4 of the 3x4
+// [R | p]), by se3_mul's formula; se3_slot: where it lives in the 12 doubles
+__device__ __forceinline__ int se3_slot(int e) { return (e & 3) < 3 ? 3 * (e >> 2) + (e & 3) : 9 + (e >> 2); }
+__device__ __forceinline__ double se3_elem(const double* A, const double* B, int e) {
+  const int i = e >> 2, j = e & 3;
+  const double* a = A + 3 * i;
+  if (j < 3) return (a[0] * B[j] + a[1] * B[3 + j]) + a[2] * B[6 + j];
+  return ((a[0] * B[9] + a[1] * B[10]) + a[2] * B[11]) + A[9 + i];
+}
 // LDS carve-up (doubles, then 32-bit words): joint table, object table,
 // static rotations, pair table, rows, joint frames per state, object
 // transforms per state, near masks, near-pair list, hit masks
 __host__ __device__ inline size_t srv_lds_bytes(int M, int P, int dof, int W, int nj, int ns) {
   const size_t dbl = (size_t)nj * kSrvJT + (size_t)M * kSrvOB + (size_t)ns * 9 + (size_t)P * kSrvPT +
-                     (size_t)kSrvN * 3 * dof + (size_t)kSrvN * nj * 12 + (size_t)kSrvN * M * 12;
+                     (size_t)kSrvN * 3 * dof + (size_t)2 * kSrvN * nj * 12 + (size_t)kSrvN * M * 12;
   return dbl * 8 + ((size_t)2 * P + (size_t)kSrvN * W) * 4;
 }
 
-__global__ __launch_bounds__(kSrvThreads) void lat_server_kernel(DevWorld w, SrvCtl* ctl, unsigned long long last,
-                                                                 unsigned long long idle_ticks) {
+__global__ __launch_bounds__(kSrvThreads) void lat_server_kernel(DevWorld w, SrvCtl* ctl, unsigned long long idle_ticks) {
   extern __shared__ double srv_lds[];
   const int M = w.n_moving, P = w.n_pairs, dof = w.dof, W = w.W, nj = w.nj, NS = w.n_static;
   double* JT = srv_lds;
@@ -3067,14 +3077,17 @@ __global__ __launch_bounds__(kSrvThreads) void lat_server_kernel(DevWorld w, Srv
   double* PT = SROT + (size_t)NS * 9;
   double* ROWS = PT + (size_t)P * kSrvPT;
   double* OMI = ROWS + (size_t)kSrvN * 3 * dof;
-  double* TT = OMI + (size_t)kSrvN * nj * 12;
+  double* LI = OMI + (size_t)kSrvN * nj * 12;
+  double* TT = LI + (size_t)kSrvN * nj * 12;
   uint32_t* NEAR = reinterpret_cast<uint32_t*>(TT + (size_t)kSrvN * M * 12);
   int* NLIST = reinterpret_cast<int*>(NEAR + P);
   uint32_t* HM = reinterpret_cast<uint32_t*>(NLIST + P);
   __shared__ unsigned long long s_cmd;
   __shared__ int s_nl;
-  const int t = (int)threadIdx.x;
+  const int t = (int)threadIdx.x, g = (int)blockIdx.x, G = (int)gridDim.x;
+  const int PG = P > g ? (P - g + G - 1) / G : 0;  // this workgroup's pairs: g, g + G, ...
   const cptr<double> HV = w.hull;
+  unsigned long long last = sys_load(&ctl->done[g]);  // batches up to it are published
   unsigned long long ph[6];  // thread 0's phase stamps
   auto stamp = [&](int k) {
     if (t == 0) ph[k] = __builtin_amdgcn_s_memrealtime();
@@ -3157,23 +3170,39 @@ __global__ __launch_bounds__(kSrvThreads) void lat_server_kernel(DevWorld w, Srv
     stamp(1);
     // FK, first the joint frames (forward_kinematics: oMi[j] = oMi[parent] *
     // (placement * M(q)), the products chain_oMi forms for every link), one
-    // state per thread ...
-    if (t < n) {
-      const double* row = ROWS + (size_t)t * 3 * dof;
-      double* om = OMI + (size_t)t * nj * 12;
-      for (int j = 0; j < nj; ++j) {
-        const double* J = JT + (size_t)kSrvJT * j;
-        const int type = (int)J[0], srcq = (int)J[1], par = (int)J[3];
-        const bool pre = srcq >= 0 && joint_is_revolute(type);
-        const double qv = pre ? 0.0 : srcq >= 0 ? row[srcq] : J[2];
-        const SE3 li = se3_mul(load_se3(J + 8), joint_motion(type, J + 4, qv, pre ? row + dof + 2 * srcq : nullptr));
-        const SE3 T = par > 0 ? se3_mul(load_se3(om + 12 * (par - 1)), li) : li;
-        double* o = om + 12 * j;
-#pragma unroll
-        for (int i = 0; i < 9; ++i) o[i] = T.R[i];
-        o[9] = T.p[0];
-        o[10] = T.p[1];
-        o[11] = T.p[2];
+    // SE3 element per lane (se3_elem: se3_mul's formula for that element):
+    // every joint's placement * M(q) at once ...
+    for (int k = t; k < n * nj * 12; k += kSrvThreads) {
+      const int e = k % 12, cj = k / 12, c = cj / nj, j = cj - c * nj;
+      const double* row = ROWS + (size_t)c * 3 * dof;
+      const double* J = JT + (size_t)kSrvJT * j;
+      const int type = (int)J[0], srcq = (int)J[1];
+      const bool pre = srcq >= 0 && joint_is_revolute(type);
+      const double qv = pre ? 0.0 : srcq >= 0 ? row[srcq] : J[2];
+      const SE3 Mq = joint_motion(type, J + 4, qv, pre ? row + dof + 2 * srcq : nullptr);
+      const int jc = e & 3;  // the column of M(q) this element reads
+      const double b0 = jc == 0 ? Mq.R[0] : jc == 1 ? Mq.R[1] : jc == 2 ? Mq.R[2] : Mq.p[0];
+      const double b1 = jc == 0 ? Mq.R[3] : jc == 1 ? Mq.R[4] : jc == 2 ? Mq.R[5] : Mq.p[1];
+      const double b2 = jc == 0 ? Mq.R[6] : jc == 1 ? Mq.R[7] : jc == 2 ? Mq.R[8] : Mq.p[2];
+      const double* a = J + 8 + 3 * (e >> 2);
+      const double v = jc < 3 ? (a[0] * b0 + a[1] * b1) + a[2] * b2 : ((a[0] * b0 + a[1] * b1) + a[2] * b2) + J[8 + 9 + (e >> 2)];
+      LI[(size_t)cj * 12 + se3_slot(e)] = v;
+    }
+    __syncthreads();
+    // ... then the chain, joint after joint, twelve lanes per state (five
+    // states per wave, the group never straddles a wave)
+    {
+      const int g = lane_id() / 12, e = (int)lane_id() - 12 * g;
+      const int c = (t >> 6) * 5 + g;
+      if (g < 5 && c < n) {
+        double* om = OMI + (size_t)c * nj * 12;
+        const double* lic = LI + (size_t)c * nj * 12;
+        for (int j = 0; j < nj; ++j) {
+          const int par = (int)JT[(size_t)kSrvJT * j + 3];
+          const double v = par > 0 ? se3_elem(om + 12 * (par - 1), lic + 12 * j, e) : lic[12 * j + se3_slot(e)];
+          om[12 * j + se3_slot(e)] = v;
+          wave_lds_sync();
+        }
       }
     }
     __syncthreads();
@@ -3205,8 +3234,8 @@ __global__ __launch_bounds__(kSrvThreads) void lat_server_kernel(DevWorld w, Srv
     __syncthreads();
     stamp(2);
     // bounding spheres: one (pair, state) per thread
-    for (int k = t; k < P * n; k += kSrvThreads) {
-      const int p = k / n, c = k - p * n;
+    for (int k = t; k < PG * n; k += kSrvThreads) {
+      const int p = g + G * (k / n), c = k % n;
       const double* E = PT + (size_t)kSrvPT * p;
       if (E[0] != 0.0) continue;  // ACM-allowed
       double ce[2][3];
@@ -3235,7 +3264,7 @@ __global__ __launch_bounds__(kSrvThreads) void lat_server_kernel(DevWorld w, Srv
       if (!dobb_separated(Rs[0], ce[0], E + 13, Rs[1], ce[1], E + 16, w.small_margin)) atomicOr(&NEAR[p], 1u << c);
     }
     __syncthreads();
-    for (int p = t; p < P; p += kSrvThreads)
+    for (int p = g + G * t; p < P; p += G * kSrvThreads)
       if (NEAR[p]) NLIST[atomicAdd(&s_nl, 1)] = p;
     __syncthreads();
     stamp(3);
@@ -3287,13 +3316,13 @@ __global__ __launch_bounds__(kSrvThreads) void lat_server_kernel(DevWorld w, Srv
     // publish: wave 0 writes every pair-mask word, then its lane 0 releases
     // `done` at system scope (the release waits for the whole wave's stores)
     if (t < 64) {
-      for (int i = t; i < n * W; i += 64) __hip_atomic_store(&ctl->out[i], HM[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      if (t == 0) {
+      for (int i = t; i < n * W; i += 64) __hip_atomic_store(&ctl->out[g][i], HM[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      if (t == 0 && g == 0) {
         ph[5] = __builtin_amdgcn_s_memrealtime();
         for (int k = 0; k < 6; ++k) __hip_atomic_store(&ctl->phase[k], ph[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       }
       __builtin_amdgcn_s_waitcnt(0);
-      if (t == 0) __hip_atomic_store(&ctl->done, cmd, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      if (t == 0) __hip_atomic_store(&ctl->done[g], cmd, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
   }
 }
@@ -6110,6 +6139,7 @@ struct mpg_world {
   bool srv_broken = false;  // it failed to answer once: launches from then on
   int srv_mode = 1;         // MPG_SMALL_SERVER=0: off
   long long srv_idle_us = 1000;
+  int srv_g = 4;            // workgroups (MPG_SMALL_SERVER_WG)
   size_t srv_lds = 0;
   bool srv_stats = false;
   double srv_stat[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -7631,6 +7661,7 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
   if (const char* e = std::getenv("MPG_SMALL_SERVER")) w->srv_mode = std::atoi(e);
   w->srv_stats = std::getenv("MPG_STATS") != nullptr;
   if (const char* e = std::getenv("MPG_SMALL_SERVER_IDLE_US")) w->srv_idle_us = std::max(10ll, std::atoll(e));
+  if (const char* e = std::getenv("MPG_SMALL_SERVER_WG")) w->srv_g = std::min(kSrvMaxG, std::max(1, std::atoi(e)));
   w->srv_lds = srv_lds_bytes(d->n_moving, d->n_pairs, d->dof, w->dw.W, d->n_joints, d->n_static);
   w->srv_ok = lat_rec_ok && !w->any_octree && !w->any_mesh && d->dof > 0 && d->dof <= kLatScDof &&
               d->n_pairs > 0 && w->dw.W <= kSrvMaxW && w->srv_lds <= 150 * 1024;
@@ -7785,8 +7816,8 @@ int srv_start(mpg_world* w) {
     HIP_TRY(hipFuncSetAttribute((const void*)lat_server_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)w->srv_lds));
   }
-  const unsigned long long last = __atomic_load_n(&w->srv_h->done, __ATOMIC_ACQUIRE);
-  hipLaunchKernelGGL(lat_server_kernel, dim3(1), dim3(kSrvThreads), w->srv_lds, w->srv_stream, w->dw, w->srv_d, last,
+  __atomic_store_n(&w->srv_h->quit, 0ull, __ATOMIC_RELEASE);
+  hipLaunchKernelGGL(lat_server_kernel, dim3(w->srv_g), dim3(kSrvThreads), w->srv_lds, w->srv_stream, w->dw, w->srv_d,
                      (unsigned long long)w->srv_idle_us * 100ull);
   HIP_TRY(hipGetLastError());
   w->srv_running = true;
@@ -7814,13 +7845,26 @@ int collide_served(mpg_world* w, const double* q, int64_t n, uint8_t* flags, uin
   __atomic_store_n(&C->seq, seq, __ATOMIC_RELEASE);
   const auto t0 = std::chrono::steady_clock::now();
   long long next_us = 50;
-  while (__atomic_load_n(&C->done, __ATOMIC_ACQUIRE) != seq) {
+  bool forced = false;
+  auto all_done = [&] {
+    for (int k = 0; k < w->srv_g; ++k)
+      if (__atomic_load_n(&C->done[k], __ATOMIC_ACQUIRE) != seq) return false;
+    return true;
+  };
+  while (!all_done()) {
     __builtin_ia32_pause();
     const long long us =
         std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t0).count();
     if (us < next_us) continue;
     next_us = us + 50;
-    const hipError_t e = hipStreamQuery(w->srv_stream);
+    hipError_t e = hipStreamQuery(w->srv_stream);
+    if (e == hipErrorNotReady && us > 500 && !forced) {
+      // some workgroups left (idle) before the request, the others are
+      // still polling: stop them and start all again (once per request)
+      __atomic_store_n(&C->quit, 1ull, __ATOMIC_RELEASE);
+      e = hipStreamSynchronize(w->srv_stream);
+      forced = true;
+    }
     if (e == hipSuccess) {  // it left before this request: start it again
       w->srv_running = false;
       const int rc = srv_start(w);
@@ -7839,7 +7883,8 @@ int collide_served(mpg_world* w, const double* q, int64_t n, uint8_t* flags, uin
   for (int64_t c = 0; c < n; ++c) {
     uint32_t any = 0;
     for (int k = 0; k < W; ++k) {
-      const uint32_t v = __atomic_load_n(&C->out[c * W + k], __ATOMIC_RELAXED);
+      uint32_t v = 0;
+      for (int gg = 0; gg < w->srv_g; ++gg) v |= __atomic_load_n(&C->out[gg][c * W + k], __ATOMIC_RELAXED);
       any |= v;
       if (pair_mask) pair_mask[c * W + k] = v;
     }
@@ -7853,7 +7898,7 @@ int collide_served(mpg_world* w, const double* q, int64_t n, uint8_t* flags, uin
 // hits into flags / pair masks
 template <bool FROM_POSES>
 int collide_small(mpg_world* w, const double* q, int64_t n, uint8_t* flags, uint32_t* pair_mask, hipStream_t s) {
-  if (!FROM_POSES && w->srv_mode && w->srv_ok && !w->srv_broken && n <= kSrvN && w->dw.debug_mode == 0) {
+  if (!FROM_POSES && w->srv_mode && w->srv_ok && !w->srv_broken && n <= kSrvN && !w->dw.dbg(3) && !w->dw.dbg(7)) {
     const int rc = collide_served(w, q, n, flags, pair_mask);
     if (rc == MPG_OK || !w->srv_broken) return rc;
   }

@@ -928,6 +928,12 @@ def test_big_walk_hulls_match_oracle():
         assert fo.mean() > 0.05
         np.testing.assert_array_equal(f, fo)
         np.testing.assert_array_equal(m, mo)
+        if n == 300:  # batches of 1, 3 and 16 states: the latency server's waves climb side by side
+            for k in (1, 3, 16):
+                for i in range(0, 300, k):
+                    f, m = d.collide_batch(q[i:i + k])
+                    np.testing.assert_array_equal(f, fo[i:i + k])
+                    np.testing.assert_array_equal(m, mo[i:i + k])
 
 
 @pytest.mark.gpu
