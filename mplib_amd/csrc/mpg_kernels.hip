@@ -6137,7 +6137,7 @@ struct mpg_world {
   bool srv_running = false;
   bool srv_ok = false;      // the world fits the server (closed-form / MPR pairs only, records, LDS)
   bool srv_broken = false;  // it failed to answer once: launches from then on
-  int srv_mode = 1;         // MPG_SMALL_SERVER=0: off
+  int srv_mode = 0;         // MPG_SMALL_SERVER=1: on
   long long srv_idle_us = 1000;
   int srv_g = 4;            // workgroups (MPG_SMALL_SERVER_WG)
   size_t srv_lds = 0;
