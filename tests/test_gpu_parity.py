@@ -369,6 +369,7 @@ def test_latency_server_idle_restart_and_teardown(monkeypatch):
     worlds' servers side by side."""
     import gc
     import time as _t
+    monkeypatch.setenv("MPG_SMALL_SERVER", "1")
     monkeypatch.setenv("MPG_SMALL_SERVER_IDLE_US", "200")
     w, art = scenes.world(3)
     w2, _ = scenes.world(3)
@@ -914,11 +915,12 @@ def test_capsule_cylinder_worlds_match_oracle():
     assert int(hit.sum()) > 0
 
 
-def test_big_walk_hulls_match_oracle():
+def test_big_walk_hulls_match_oracle(monkeypatch):
     """a 302-vertex cone (cell lists of ~300 rim vertices) and a
     770-vertex sphere (above the 512-vertex direction-table limit: every
-    support climbs) as FCL neighbour-walk obstacles -- both batch paths, every
-    flag and pair bit vs the oracle."""
+    support climbs) as FCL neighbour-walk obstacles -- both batch paths and
+    the latency server, every flag and pair bit vs the oracle."""
+    monkeypatch.setenv("MPG_SMALL_SERVER", "1")
     o = Wd.big_hull_world()
     d = DeviceWorld(Wd.desc_arrays(o))
     for n in (300, 1 << 14):
