@@ -6140,6 +6140,7 @@ struct mpg_world {
   int srv_mode = 0;         // MPG_SMALL_SERVER=1: on
   long long srv_idle_us = 1000;
   int srv_g = 4;            // workgroups (MPG_SMALL_SERVER_WG)
+  int srv_max_n = kSrvN;    // batches up to this size go to the server (MPG_SMALL_SERVER_MAX)
   size_t srv_lds = 0;
   bool srv_stats = false;
   double srv_stat[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -7662,6 +7663,7 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
   w->srv_stats = std::getenv("MPG_STATS") != nullptr;
   if (const char* e = std::getenv("MPG_SMALL_SERVER_IDLE_US")) w->srv_idle_us = std::max(10ll, std::atoll(e));
   if (const char* e = std::getenv("MPG_SMALL_SERVER_WG")) w->srv_g = std::min(kSrvMaxG, std::max(1, std::atoi(e)));
+  if (const char* e = std::getenv("MPG_SMALL_SERVER_MAX")) w->srv_max_n = std::min(kSrvN, std::max(1, std::atoi(e)));
   w->srv_lds = srv_lds_bytes(d->n_moving, d->n_pairs, d->dof, w->dw.W, d->n_joints, d->n_static);
   w->srv_ok = lat_rec_ok && !w->any_octree && !w->any_mesh && d->dof > 0 && d->dof <= kLatScDof &&
               d->n_pairs > 0 && w->dw.W <= kSrvMaxW && w->srv_lds <= 150 * 1024;
@@ -7898,7 +7900,7 @@ int collide_served(mpg_world* w, const double* q, int64_t n, uint8_t* flags, uin
 // hits into flags / pair masks
 template <bool FROM_POSES>
 int collide_small(mpg_world* w, const double* q, int64_t n, uint8_t* flags, uint32_t* pair_mask, hipStream_t s) {
-  if (!FROM_POSES && w->srv_mode && w->srv_ok && !w->srv_broken && n <= kSrvN && !w->dw.dbg(3) && !w->dw.dbg(7)) {
+  if (!FROM_POSES && w->srv_mode && w->srv_ok && !w->srv_broken && n <= w->srv_max_n && !w->dw.dbg(3) && !w->dw.dbg(7)) {
     const int rc = collide_served(w, q, n, flags, pair_mask);
     if (rc == MPG_OK || !w->srv_broken) return rc;
   }
