@@ -6137,9 +6137,9 @@ struct mpg_world {
   bool srv_running = false;
   bool srv_ok = false;      // the world fits the server (closed-form / MPR pairs only, records, LDS)
   bool srv_broken = false;  // it failed to answer once: launches from then on
-  int srv_mode = 0;         // MPG_SMALL_SERVER=1: on
+  int srv_mode = 1;         // MPG_SMALL_SERVER=0: off
   long long srv_idle_us = 1000;
-  int srv_g = 4;            // workgroups (MPG_SMALL_SERVER_WG)
+  int srv_g = 8;            // workgroups (MPG_SMALL_SERVER_WG)
   int srv_max_n = kSrvN;    // batches up to this size go to the server (MPG_SMALL_SERVER_MAX)
   size_t srv_lds = 0;
   bool srv_stats = false;
