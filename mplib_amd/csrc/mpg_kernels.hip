@@ -7877,6 +7877,12 @@ int collide_served(mpg_world* w, const double* q, int64_t n, uint8_t* flags, uin
       return set_error(MPG_E_HIP, "latency server did not answer");
     }
   }
+  if (w->prof) {  // a served batch counts as one narrow-stage "launch" of its post -> done time
+    std::lock_guard<std::mutex> lk(w->prof_mu);
+    w->prof_ms[MPG_STAGE_NARROW] += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    w->prof_n[MPG_STAGE_NARROW] += 1;
+    w->prof_cfg += n;
+  }
   if (w->srv_stats) {  // MPG_STATS: phase sums (rows, fk, spheres, narrow, publish), us
     w->srv_stat[5] += 1.0;
     for (int k = 0; k < 5; ++k) w->srv_stat[k] += (double)(C->phase[k + 1] - C->phase[k]) / 100.0;
