@@ -3298,15 +3298,29 @@ __global__ __launch_bounds__(kSrvThreads) void lat_server_kernel(DevWorld w, Srv
         int st = MPR_DONE;
         CV3 v0, v1, v2, v3, dir;
         if (near) mpr_begin(center(w, A), center(w, B), st, v0, dir);
+        unsigned long long t_sup = 0, t_adv = 0, n_it = 0;  // MPG_STATS: MPR step costs (shader clocks)
         while (__ballot(st != MPR_DONE) != 0) {
+          const unsigned long long c0 = w.stats ? __builtin_amdgcn_s_memtime() : 0ull;
           if (st != MPR_DONE) {
             const CV3 sp = msupport(w, HV, A, B, dir);
+            const unsigned long long c1 = w.stats ? __builtin_amdgcn_s_memtime() : 0ull;
             const int res = mpr_advance(w.mpr_tol, sp, st, v0, v1, v2, v3, dir);
             if (res != 0) {
               hit = res > 0;
               st = MPR_DONE;
             }
+            if (w.stats) {
+              t_sup += c1 - c0;
+              t_adv += __builtin_amdgcn_s_memtime() - c1;
+            }
           }
+          ++n_it;
+        }
+        if (w.stats && lane == 0 && n_it > 0) {
+          atomicAdd(&w.stats[20], n_it);
+          atomicAdd(&w.stats[21], t_sup);
+          atomicAdd(&w.stats[22], t_adv);
+          atomicMax(&w.stats[23], n_it);
         }
       }
       if (hit) atomicOr(&HM[c * W + (p >> 5)], 1u << (p & 31));
@@ -7686,6 +7700,9 @@ int mpg_world_destroy(mpg_world* w) {
                  st[24] / 100.0, st[32] / 100.0, st[25] / 100.0, st[33] / 100.0, st[26] / 100.0, st[34] / 100.0,
                  st[27] / 100.0, st[35] / 100.0, st[28] / 100.0, st[36] / 100.0, st[29] / 100.0, st[37] / 100.0,
                  st[30] / 100.0, st[38] / 100.0);
+    if (st[20])
+      std::fprintf(stderr, "[mpg stats] latency server MPR steps: %llu (max %llu per pair), shader clocks per step: "
+                   "support %.0f, advance %.0f\n", st[20], st[23], (double)st[21] / st[20], (double)st[22] / st[20]);
     std::fprintf(stderr, "[mpg stats] small_kernel slowest narrow test: pair %llu, %.2f us\n",
                  (unsigned long long)(st[31] & 4095), (st[31] >> 12) / 100.0);
     std::fprintf(stderr, "[mpg stats] walk hulls: supports %llu, trap-free fast %llu, verified %llu, full walks %llu, "
