@@ -176,6 +176,10 @@ inline bool build_hull_cells(const double* V, int nv, std::vector<uint32_t>& sta
 // each).  A support is then one batch of loads for most cells.
 constexpr int kCellInline = 3;
 constexpr int kCellRec = 12;  // doubles per record: 3 x (x, y, z), count, offset, pad
+#ifndef MPG_OVF_BATCH
+#define MPG_OVF_BATCH 4
+#endif
+constexpr int kOvfBatch = MPG_OVF_BATCH;  // overflow entries loaded per memory round (device)
 
 // (host) converts build_hull_cells lists [start[0], start[kCellsPerHull]) into
 // kCellsPerHull records appended to rec, their overflow entries to ovf
@@ -215,15 +219,26 @@ MPG_INLINE void cell_record_support(PD R, PD ovf, double x, double y, double z, 
   const int n = (int)R[9];
   if (n > kCellInline) {
     const PD P0 = ovf + 4 * (size_t)R[10];
-    for (int k = 0; k < n - kCellInline; ++k) {
-      const PD P = P0 + 4 * k;
-      const double px = P[0], py = P[1], pz = P[2];
-      const double dd = (x * px + y * py) + z * pz;
-      if (dd > best) {
-        best = dd;
-        bx = px;
-        by = py;
-        bz = pz;
+    const int m = n - kCellInline;
+    for (int k0 = 0; k0 < m; k0 += kOvfBatch) {  // loads of a batch together, compares in list order
+      double ex[kOvfBatch], ey[kOvfBatch], ez[kOvfBatch];
+#pragma unroll
+      for (int j = 0; j < kOvfBatch; ++j) {
+        const PD P = P0 + 4 * (k0 + j < m ? k0 + j : m - 1);
+        ex[j] = P[0];
+        ey[j] = P[1];
+        ez[j] = P[2];
+      }
+#pragma unroll
+      for (int j = 0; j < kOvfBatch; ++j) {
+        if (k0 + j >= m) break;
+        const double dd = (x * ex[j] + y * ey[j]) + z * ez[j];
+        if (dd > best) {
+          best = dd;
+          bx = ex[j];
+          by = ey[j];
+          bz = ez[j];
+        }
       }
     }
   }

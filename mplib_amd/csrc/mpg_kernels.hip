@@ -243,15 +243,28 @@ __device__ __forceinline__ V3 walk_cell_fast(const DevWorld& w, cptr<double> HV,
     }
   }
   int nmax = 0;  // ... and how many entries reach it (a tie when > 1)
-  for (int k = kCellInline; k < n; ++k) {
-    const cptr<double> e = ovf + 4 * (k - kCellInline);
-    const double dd = (d.x * e[0] + d.y * e[1]) + d.z * e[2];
-    if (dd > best) {  // a new maximum: the inline entries are all below it
-      best = dd;
-      g = k;
-      nmax = 1;
-    } else if (dd == best) {
-      ++nmax;
+  // the overflow entries kOvfBatch at a time: their loads issued together
+  // (one memory round per batch, not per entry), then compared in list order
+  for (int k0 = kCellInline; k0 < n; k0 += kOvfBatch) {
+    double ex[kOvfBatch], ey[kOvfBatch], ez[kOvfBatch];
+#pragma unroll
+    for (int j = 0; j < kOvfBatch; ++j) {
+      const cptr<double> e = ovf + 4 * (min(k0 + j, n - 1) - kCellInline);
+      ex[j] = e[0];
+      ey[j] = e[1];
+      ez[j] = e[2];
+    }
+#pragma unroll
+    for (int j = 0; j < kOvfBatch; ++j) {
+      if (k0 + j >= n) break;
+      const double dd = (d.x * ex[j] + d.y * ey[j]) + d.z * ez[j];
+      if (dd > best) {  // a new maximum: the inline entries are all below it
+        best = dd;
+        g = k0 + j;
+        nmax = 1;
+      } else if (dd == best) {
+        ++nmax;
+      }
     }
   }
   // the inline entries, compared with the final maximum (short lists repeat
