@@ -3044,7 +3044,7 @@ __global__ __launch_bounds__(256) void small_kernel(DevWorld w, const double* __
 // after idle_ticks (s_memrealtime, 100 MHz) without a request, or when the
 // host sets `quit`: every path through the poll loop ends.
 // ---------------------------------------------------------------------------
-constexpr int kSrvN = 16;        // states per served batch
+constexpr int kSrvN = 32;        // states per served batch (at most)
 constexpr int kSrvMaxG = 8;      // workgroups (pair p belongs to workgroup p % G)
 constexpr int kSrvMaxW = 16;     // pair-mask words per state (512 pairs)
 constexpr int kSrvThreads = 512;
@@ -6167,7 +6167,7 @@ struct mpg_world {
   int srv_mode = 1;         // MPG_SMALL_SERVER=0: off
   long long srv_idle_us = 1000;
   int srv_g = 8;            // workgroups (MPG_SMALL_SERVER_WG)
-  int srv_max_n = kSrvN;    // batches up to this size go to the server (MPG_SMALL_SERVER_MAX)
+  int srv_max_n = 16;       // batches up to this size go to the server (MPG_SMALL_SERVER_MAX, <= kSrvN)
   size_t srv_lds = 0;
   bool srv_stats = false;
   double srv_stat[8] = {0, 0, 0, 0, 0, 0, 0, 0};

@@ -330,6 +330,7 @@ def test_latency_path_matches_oracle(cfg, server, monkeypatch):
     (MPG_SMALL_SERVER): bit-exact with the oracle and with the two-phase
     pipeline."""
     monkeypatch.setenv("MPG_SMALL_SERVER", str(server))
+    monkeypatch.setenv("MPG_SMALL_SERVER_MAX", "32")
     w, art = scenes.world(cfg)
     q = Wd.sample_q(ow(cfg).art, 20000, 40 + cfg)
     fo, mo = ow(cfg).collide_batch(q, nthreads=NTHREADS)
@@ -352,7 +353,7 @@ def test_latency_path_matches_oracle(cfg, server, monkeypatch):
         np.testing.assert_array_equal(f, fo[i:i + 2])
         np.testing.assert_array_equal(m, mo[i:i + 2])
     assert 0 < fo[:400].sum() < 400
-    for n in (4, 7, 16):  # served batches of several states
+    for n in (4, 7, 16, 32):  # served batches of several states (32: with MPG_SMALL_SERVER_MAX=32)
         for i in range(0, 160, n):
             f, m = w.collide_batch(q[i:i + n])
             np.testing.assert_array_equal(f, fo[i:i + n])
