@@ -6167,7 +6167,7 @@ struct mpg_world {
   int srv_mode = 1;         // MPG_SMALL_SERVER=0: off
   long long srv_idle_us = 1000;
   int srv_g = 8;            // workgroups (MPG_SMALL_SERVER_WG)
-  int srv_max_n = 16;       // batches up to this size go to the server (MPG_SMALL_SERVER_MAX, <= kSrvN)
+  int srv_max_n = kSrvN;    // batches up to this size go to the server (MPG_SMALL_SERVER_MAX)
   size_t srv_lds = 0;
   bool srv_stats = false;
   double srv_stat[8] = {0, 0, 0, 0, 0, 0, 0, 0};
