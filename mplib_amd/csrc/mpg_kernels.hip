@@ -3081,7 +3081,8 @@ __host__ __device__ inline size_t srv_lds_bytes(int M, int P, int dof, int W, in
   return dbl * 8 + ((size_t)2 * P + (size_t)kSrvN * W) * 4;
 }
 
-__global__ __launch_bounds__(kSrvThreads) void lat_server_kernel(DevWorld w, SrvCtl* ctl, unsigned long long idle_ticks) {
+__global__ __launch_bounds__(kSrvThreads) void lat_server_kernel(DevWorld w, SrvCtl* ctl, unsigned long long idle_ticks,
+                                                                 int phases) {
   extern __shared__ double srv_lds[];
   const int M = w.n_moving, P = w.n_pairs, dof = w.dof, W = w.W, nj = w.nj, NS = w.n_static;
   double* JT = srv_lds;
@@ -3164,7 +3165,7 @@ __global__ __launch_bounds__(kSrvThreads) void lat_server_kernel(DevWorld w, Srv
         }
         if (sys_load(&ctl->quit) != 0ull) break;
         if (__builtin_amdgcn_s_memrealtime() - t0 > idle_ticks) break;
-        __builtin_amdgcn_s_sleep(4);
+        __builtin_amdgcn_s_sleep(2);
       }
       s_cmd = cmd;  // the batch size rides in the low byte of seq
       s_nl = 0;
@@ -3344,7 +3345,7 @@ __global__ __launch_bounds__(kSrvThreads) void lat_server_kernel(DevWorld w, Srv
     // `done` at system scope (the release waits for the whole wave's stores)
     if (t < 64) {
       for (int i = t; i < n * W; i += 64) __hip_atomic_store(&ctl->out[g][i], HM[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      if (t == 0 && g == 0) {
+      if (t == 0 && g == 0 && phases) {  // MPG_STATS only: six more stores for the release to wait on
         ph[5] = __builtin_amdgcn_s_memrealtime();
         for (int k = 0; k < 6; ++k) __hip_atomic_store(&ctl->phase[k], ph[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       }
@@ -7850,7 +7851,7 @@ int srv_start(mpg_world* w) {
   }
   __atomic_store_n(&w->srv_h->quit, 0ull, __ATOMIC_RELEASE);
   hipLaunchKernelGGL(lat_server_kernel, dim3(w->srv_g), dim3(kSrvThreads), w->srv_lds, w->srv_stream, w->dw, w->srv_d,
-                     (unsigned long long)w->srv_idle_us * 100ull);
+                     (unsigned long long)w->srv_idle_us * 100ull, w->srv_stats ? 1 : 0);
   HIP_TRY(hipGetLastError());
   w->srv_running = true;
   return MPG_OK;
