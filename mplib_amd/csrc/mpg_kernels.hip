@@ -7694,7 +7694,7 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
   if (const char* e = std::getenv("MPG_SMALL_SERVER_MAX")) w->srv_max_n = std::min(kSrvN, std::max(1, std::atoi(e)));
   w->srv_lds = srv_lds_bytes(d->n_moving, d->n_pairs, d->dof, w->dw.W, d->n_joints, d->n_static);
   w->srv_ok = lat_rec_ok && !w->any_octree && !w->any_mesh && d->dof > 0 && d->dof <= kLatScDof &&
-              d->n_pairs > 0 && w->dw.W <= kSrvMaxW && w->srv_lds <= 150 * 1024;
+              d->n_pairs > 0 && w->dw.W <= kSrvMaxW && w->srv_lds <= 144 * 1024;  // + ~11 KB static LDS
   const char* own = std::getenv("MPG_OWN_STREAM");
   if (!own || std::atoi(own) != 0) HIP_TRY(hipStreamCreateWithFlags(&w->own_stream, hipStreamNonBlocking));
   *out = w;
@@ -7938,8 +7938,11 @@ int collide_served(mpg_world* w, const double* q, int64_t n, uint8_t* flags, uin
 template <bool FROM_POSES>
 int collide_small(mpg_world* w, const double* q, int64_t n, uint8_t* flags, uint32_t* pair_mask, hipStream_t s) {
   if (!FROM_POSES && w->srv_mode && w->srv_ok && !w->srv_broken && n <= w->srv_max_n && !w->dw.dbg(3) && !w->dw.dbg(7)) {
-    const int rc = collide_served(w, q, n, flags, pair_mask);
-    if (rc == MPG_OK || !w->srv_broken) return rc;
+    if (collide_served(w, q, n, flags, pair_mask) == MPG_OK) return MPG_OK;
+    // the server could not be started or did not answer: launches from now on
+    std::fprintf(stderr, "mplib_amd: latency server unavailable (%s); using one launch per batch\n", g_last_error.c_str());
+    w->srv_broken = true;
+    (void)hipGetLastError();
   }
   const size_t row = FROM_POSES ? (size_t)w->dw.n_links * 7 : (size_t)w->dw.dof;
   const size_t cap = std::max<size_t>((size_t)n, std::min<size_t>((size_t)w->small_max, 256));
