@@ -419,6 +419,10 @@ def test_spheres_closed_forms_match_oracle():
     f2, m2 = w.collide_batch(q)
     np.testing.assert_array_equal(f2, fo)
     np.testing.assert_array_equal(bits(m2, range(len(perm))), bits(mo, perm))
+    for i in range(0, 600, 3):  # ... and through the latency server (attached sphere included)
+        f3, m3 = w.collide_batch(q[i:i + 3])
+        np.testing.assert_array_equal(f3, fo[i:i + 3])
+        np.testing.assert_array_equal(bits(m3, range(len(perm))), bits(mo[i:i + 3], perm))
 
 
 # ------------------------------------------------------------------- distance
