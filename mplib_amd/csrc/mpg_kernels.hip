@@ -3124,6 +3124,27 @@ __global__ __launch_bounds__(kSrvThreads) void lat_server_kernel(DevWorld w, Srv
     O[24] = w.link_parent[l];
   }
   for (int i = t; i < NS * 9; i += kSrvThreads) SROT[i] = w.static_T[12 * (i / 9) + i % 9];
+  int probe_cb = -1;  // MPG_STATS probe: the first walk hull's cell records
+  if (w.stats && g == 0 && t == 0)
+    for (int gg = 0; gg < w.n_geoms && probe_cb < 0; ++gg)
+      if (w.geom_nbr[gg] >= 0 && w.geom_cbase[gg] >= 0) probe_cb = w.geom_cbase[gg];
+  if (probe_cb >= 0) {
+    // shader clocks of 16 dependent loads through one hull's walk cell
+    // records, first pass and again (the same addresses)
+    const int nrec = kCellsPerHull;
+    for (int pass = 0; pass < 2; ++pass) {
+      int idx = 7;
+      const unsigned long long c0 = __builtin_amdgcn_s_memtime();
+      for (int k = 0; k < 16; ++k) {
+        const double v = w.wcell_rec[kCellRec * (size_t)(probe_cb + (idx * 97 + k * 131) % nrec) + 9];
+        idx = (int)v & 1023;  // the next address depends on this load
+      }
+      asm volatile("" ::"v"(idx));  // the chain has completed before the clock is read
+      const unsigned long long c1 = __builtin_amdgcn_s_memtime();
+      atomicAdd(&w.stats[40 + pass], (c1 - c0) + (idx == -1 ? 1ull : 0ull));
+      atomicAdd(&w.stats[42 + pass], 16ull);
+    }
+  }
   for (int p = t; p < P; p += kSrvThreads) {
     const cptr<double> R = w.lat_rec + (size_t)LR_STRIDE * p;
     double* E = PT + (size_t)kSrvPT * p;
@@ -7567,8 +7588,8 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
 #endif
   dw.stats = nullptr;
   if (std::getenv("MPG_STATS") && std::atoi(std::getenv("MPG_STATS")) > 0) {
-    HIP_TRY(hipMalloc(&dw.stats, 40 * sizeof(unsigned long long)));
-    HIP_TRY(hipMemset(dw.stats, 0, 40 * sizeof(unsigned long long)));
+    HIP_TRY(hipMalloc(&dw.stats, 48 * sizeof(unsigned long long)));
+    HIP_TRY(hipMemset(dw.stats, 0, 48 * sizeof(unsigned long long)));
   }
   dw.joint_type = to_cptr<int>(base + o_jt);
   dw.joint_parent = to_cptr<int>(base + o_jp);
@@ -7705,7 +7726,7 @@ int mpg_world_destroy(mpg_world* w) {
   if (!w) return MPG_OK;
   hipSetDevice(w->device);
   if (w->dw.stats) {
-    unsigned long long st[40];
+    unsigned long long st[48];
     hipDeviceSynchronize();
     hipMemcpy(st, w->dw.stats, sizeof(st), hipMemcpyDeviceToHost);
     std::fprintf(stderr,
@@ -7714,6 +7735,9 @@ int mpg_world_destroy(mpg_world* w) {
                  st[24] / 100.0, st[32] / 100.0, st[25] / 100.0, st[33] / 100.0, st[26] / 100.0, st[34] / 100.0,
                  st[27] / 100.0, st[35] / 100.0, st[28] / 100.0, st[36] / 100.0, st[29] / 100.0, st[37] / 100.0,
                  st[30] / 100.0, st[38] / 100.0);
+    if (st[42])
+      std::fprintf(stderr, "[mpg stats] latency server probe: dependent cell-record loads, shader clocks each: "
+                   "first pass %.0f, again %.0f\n", (double)st[40] / st[42], (double)st[41] / st[43]);
     if (st[20])
       std::fprintf(stderr, "[mpg stats] latency server MPR steps: %llu (max %llu per pair), shader clocks per step: "
                    "support %.0f, advance %.0f\n", st[20], st[23], (double)st[21] / st[20], (double)st[22] / st[20]);
