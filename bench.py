@@ -358,7 +358,7 @@ def plan_main(args, world, rank, local, backend):
         "mean_spec_nodes": mean("spec_nodes"), "mean_spec_wait_nodes": mean("spec_wait_nodes"),
         "mean_spec_ms": mean("t_spec") * 1e3,
         "roofline": {"bound": "latency", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBPS, "traffic": None, "kernel": "lat_server_kernel (<=16 states) / small_kernel",
+                     "frac": achieved / HBM_PEAK_GBPS, "traffic": None, "kernel": "lat_server_kernel (<=32 states) / small_kernel",
                      "kernel_ms": kern_ms, "units_per_launch": states_per_launch, "unit_kind": "states",
                      "algorithmic_bytes_per_unit": bytes_per_state,
                      "note": "one validity batch per planner iteration: round-trip latency, not bandwidth, "

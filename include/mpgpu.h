@@ -312,13 +312,17 @@ int mpg_distance_batch_ex(mpg_world *world, const double *q, int64_t n, int32_t 
  * num_max_contacts = 1.  A point-cloud (OcTree) pair reports the contact of
  * the first occupied leaf of FCL's traversal that intersects the shape, with
  * the tree as the contact's o1 (normal from the leaf box into the shape).
- * A BVH-mesh pair reports the contact of its first intersecting triangle
- * (pair) in triangle index order: mesh-mesh intersect_Triangle's deepest
- * point of the shallower triangle (o1's frame -> world), shape-mesh the
- * sphere-triangle contact or libccd MPR penetration of (shape, triangle),
- * mesh-OcTree MPR penetration of (first hit leaf box, triangle).  FCL picks
- * the first in its OBBRSS traversal order, so with several intersecting
- * triangles the contact can be another of them (collision flags are equal).
+ * A BVH-mesh pair reports the contact of the first intersecting leaf test
+ * in FCL 0.7.0's traversal order of its BVHModel<OBBRSS> tree (the tree is
+ * rebuilt as FCL builds it, and only leaf tests FCL's OBB tests let through
+ * count): mesh-shape the smallest leaf position (left child first), with the
+ * sphere-triangle contact or libccd MPR penetration of (shape, triangle);
+ * mesh-mesh the pair whose descent (first tree descended when the second
+ * node is a leaf or the first is larger) is lexicographically first, with
+ * intersect_Triangle's deepest point of the shallower triangle (o1's frame ->
+ * world); mesh-OcTree the first in OcTreeMeshIntersectRecurse's interleaved
+ * descent (octree children 0..7, mesh left then right), MPR penetration of
+ * (leaf box, triangle).
  */
 #define MPG_INPUT_Q 0
 #define MPG_INPUT_LINK_POSES 1
@@ -390,6 +394,18 @@ int mpg_fcl_bvh_build(const double *vertices, int32_t n_vertices, const int32_t 
 
 /* Diagnostics: the device sin/cos used by the FK (host buffers). */
 int mpg_debug_sincos(const double *x, int64_t n, double *s, double *c, int device);
+
+/*
+ * Latency server accounting (the resident kernel behind host batches of at
+ * most MPG_SMALL_SERVER_MAX states): batches it answered,
+ * times it was (re)started, calls that fell back to one launch per batch
+ * because it could not be started or did not answer.  state: 0 = not used by
+ * this world (MPG_SMALL_SERVER=0, or pairs it does not serve), 1 = in use,
+ * 2 = fallen back (it is tried again one second after the failure).  Any
+ * output pointer may be NULL.  No reference counterpart (diagnostics).
+ */
+int mpg_latency_server_stats(mpg_world *world, int64_t *served, int64_t *starts, int64_t *fallbacks,
+                             int32_t *state);
 
 /* Synchronise the world's device (used after MPG_MEM_DEVICE calls). */
 int mpg_synchronize(int device);

@@ -94,6 +94,9 @@ SIGNATURES = {
                                         ctypes.c_int]),
     "mpg_fcl_bvh_build": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_int32,
                                          ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "mpg_latency_server_stats": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int64),
+                                                ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64),
+                                                ctypes.POINTER(ctypes.c_int32)]),
     "mpg_synchronize": (ctypes.c_int, [ctypes.c_int]),
     "mpg_device_count": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int)]),
     "mpg_last_error": (ctypes.c_char_p, []),

@@ -822,7 +822,23 @@ PYBIND11_MODULE(pymp, m_all) {
              return d;
            },
            "{stage: (milliseconds, launches, units)} accumulated since the last read; units are configurations "
-           "(cull, bucket) or narrow-phase candidates (narrow).");
+           "(cull, bucket) or narrow-phase candidates (narrow).")
+      .def("latency_server_stats",
+           [](PW& w) {
+             int64_t served = 0, starts = 0, fallbacks = 0;
+             int32_t state = 0;
+             check_status(mpg_latency_server_stats(w.device_world(), &served, &starts, &fallbacks, &state),
+                          "mpg_latency_server_stats");
+             static const char* names[3] = {"unused", "in_use", "fallen_back"};
+             py::dict d;
+             d["served"] = served;
+             d["starts"] = starts;
+             d["fallbacks"] = fallbacks;
+             d["state"] = names[state];
+             return d;
+           },
+           "Latency server accounting of the current snapshot (mpg_latency_server_stats): batches served, "
+           "(re)starts, fallbacks to one launch per batch, state.");
 
   // ---- ompl (reference python/pybind_ompl.hpp:20-33) ----
   auto mo = m_all.def_submodule("ompl");

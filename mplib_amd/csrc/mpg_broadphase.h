@@ -144,11 +144,7 @@ MPG_INLINE F34 f_joint_motion(int type, P axis, double v) {
   if (type <= MPG_JOINT_REVOLUTE_UNALIGNED || type >= MPG_JOINT_RUBX) {
     const double k = rint(v * 0.15915494309189535);
     const float a = (float)(v - k * 6.283185307179586);
-#if defined(MPG_FK_FASTSIN) && defined(__HIP_DEVICE_COMPILE__)
-    const float s = __sinf(a), c = __cosf(a);  // hardware v_sin/v_cos: ~1e-6 absolute on [-pi, pi]
-#else
     const float s = sinf(a), c = cosf(a);  // (__sinf / __cosf measured 5 % faster FK, not worth the weaker bound)
-#endif
     const int t = (type >= MPG_JOINT_RUBX) ? type - MPG_JOINT_RUBX : type;
     if (t == 0) {
       M.R[4] = c; M.R[5] = -s; M.R[7] = s; M.R[8] = c;
@@ -179,51 +175,17 @@ MPG_INLINE F34 f_joint_motion(int type, P axis, double v) {
 // beyond that.
 constexpr int kRegSaves = 2;
 
-#ifndef MPG_FK_SPARSE
-#define MPG_FK_SPARSE 0
-#endif
-#ifndef MPG_FK_UNROLL
-#define MPG_FK_UNROLL 1
-#endif
-// jointPlacement * M(q) for an axis-aligned revolute joint: only the two
-// columns the rotation mixes change (c, s: the joint's cos / sin)
-template <class P>
-MPG_INLINE F34 f_place_rot(P pl, int axis, float c, float s) {
-  MPG_FP32_CONTRACT
-  F34 L = f34_load(pl);
-  const int i0 = axis == 0 ? 1 : axis == 1 ? 2 : 0, i1 = axis == 0 ? 2 : axis == 1 ? 0 : 1;
-  // R_axis(a): column i0 -> c e_i0 + s e_i1, column i1 -> -s e_i0 + c e_i1
-#pragma unroll
-  for (int r = 0; r < 3; ++r) {
-    const float a0 = L.R[3 * r + i0], a1 = L.R[3 * r + i1];
-    L.R[3 * r + i0] = a0 * c + a1 * s;
-    L.R[3 * r + i1] = a1 * c - a0 * s;
-  }
-  return L;
-}
-
 template <class Sink>
 MPG_INLINE void bp_fk(const BpView& b, const double* __restrict__ qrow, float* save, int stride, Sink&& sink) {
   F34 cur, r0, r1;
-#pragma unroll MPG_FK_UNROLL
+#pragma unroll 1
   for (int j = 0; j <= b.nj; ++j) {
     if (j > 0) {
       const int jj = j - 1;
       const int src = b.joint_q_source[jj];
       const double v = src >= 0 ? qrow[src] : b.joint_q_const[jj];
       const int jt = b.joint_type[jj];
-      F34 li;
-      if (MPG_FK_SPARSE && (jt <= MPG_JOINT_RZ || (jt >= MPG_JOINT_RUBX && jt <= MPG_JOINT_RUBZ))) {
-        const double k = rint(v * 0.15915494309189535);
-        const float a = (float)(v - k * 6.283185307179586);
-#if defined(MPG_FK_FASTSIN) && defined(__HIP_DEVICE_COMPILE__)
-        li = f_place_rot(b.jplace + 12 * jj, jt >= MPG_JOINT_RUBX ? jt - MPG_JOINT_RUBX : jt, __cosf(a), __sinf(a));
-#else
-        li = f_place_rot(b.jplace + 12 * jj, jt >= MPG_JOINT_RUBX ? jt - MPG_JOINT_RUBX : jt, cosf(a), sinf(a));
-#endif
-      } else {
-        li = f34_mul(f34_load(b.jplace + 12 * jj), f_joint_motion(jt, b.jaxis + 3 * jj, v));
-      }
+      const F34 li = f34_mul(f34_load(b.jplace + 12 * jj), f_joint_motion(jt, b.jaxis + 3 * jj, v));
       const int s = b.jsrc[jj];
       if (s < 0) {
         cur = li;

@@ -274,9 +274,6 @@ __device__ __forceinline__ V3 walk_cell_fast(const DevWorld& w, cptr<double> HV,
   bool tie = nmax > 1;
   const uint64_t free_mask = (uint64_t)__double_as_longlong(R[11]);
   const bool sub_free = (free_mask >> sub) & 1ull;
-#ifdef MPG_AB_NOTIE  // timing ablation only
-  tie = false;
-#endif
   pend = !(sub_free && !tie);
   int endp = -1;
   if (__builtin_expect(!sub_free, 0)) {  // trapped subcell: its fine cell's certified endpoint, if any
@@ -309,13 +306,7 @@ __device__ __forceinline__ V3 walk_cell_fast(const DevWorld& w, cptr<double> HV,
 // cell) the climb is run (wave_walk).
 __device__ __forceinline__ V3 walk_resolve_wave(const DevWorld& w, cptr<double> HV, int geom, const V3& d, int c,
                                                 bool pend, int pre, V3 p) {
-#ifdef MPG_AB_NORESOLVE  // timing ablation only: wrong results
-  return p;
-#endif
   unsigned long long pm = __ballot(pend);
-#ifdef MPG_AB_NEVER  // timing ablation only: the resolve code stays, never runs
-  if (w.walk_subk > 0) return p;
-#endif
   if (__builtin_expect(pm == 0ull, 1)) return p;
   const unsigned long long act = __ballot(true);
   const int nact = __popcll(act);
@@ -1027,29 +1018,19 @@ __global__ __launch_bounds__(BLOCK) void cull_kernel(DevWorld w, const double* _
       }
       return;
     }
-#ifndef MPG_PUSH_SCAN
-#define MPG_PUSH_SCAN 2
-#endif
     // one wave scan of the kept counts: each lane writes its own entries
     // (schedule index, lane) at its offset, no per-entry wave-level loop
-    if (MPG_PUSH_SCAN) {
+    {
     const uint32_t c = (uint32_t)__popc(kb);
-    uint32_t incl, total;
-    if (MPG_PUSH_SCAN == 2) {
-      // the prefix sum by bit planes of the counts (<= 32: six ballots), no LDS
-      uint32_t ex = 0u;
-      total = 0u;
+    // the prefix sum by bit planes of the counts (<= 32: six ballots), no LDS
+    uint32_t ex = 0u, total = 0u;
 #pragma unroll
-      for (int bit = 0; bit < 6; ++bit) {
-        const unsigned long long m = __ballot((c >> bit) & 1u);
-        ex += __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u)) << bit;
-        total += (uint32_t)__popcll(m) << bit;
-      }
-      incl = ex + c;
-    } else {
-      incl = wave_inclusive_scan(c, lane);
-      total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+    for (int bit = 0; bit < 6; ++bit) {
+      const unsigned long long m = __ballot((c >> bit) & 1u);
+      ex += __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u)) << bit;
+      total += (uint32_t)__popcll(m) << bit;
     }
+    const uint32_t incl = ex + c;
     if (total == 0u) return;
     if (tail - head + total <= (uint32_t)kQueue) {
       uint32_t pos = tail + incl - c;
@@ -2010,18 +1991,22 @@ __device__ __forceinline__ void fcl_shape_obb_world(const DevWorld& w, int gs, i
 }
 
 // MeshShape: the path from the root to triangle t's leaf (t: index in the
-// mesh), every node's OBB against the shape's (world) under (TM.R, TM.p)
+// mesh), every node's OBB against the shape's (world) under (TM.R, TM.p).
+// mpg_world_create refuses trees deeper than kFclMaxDepth, so every descent
+// reaches its leaf inside the loop; the trailing `return true` (the hit
+// stands) is only there so that no bound can turn a hit into a miss.
+constexpr int kFclMaxDepth = 255;
 __device__ __forceinline__ bool fcl_gate_shape(const DevWorld& w, int gm, const SE3& TM, const double* sA,
                                                const double* sT, const double* sE, int t) {
   const int pos = w.tri_pos[(int)w.geom_rec[G_STRIDE * gm + G_PARAM] + t];
   int node = w.fb_root[gm];
-  for (int depth = 0; depth < 256; ++depth) {
+  for (int depth = 0; depth <= kFclMaxDepth; ++depth) {
     if (!fcl_overlap(TM.R, TM.p, sA, sT, sE, w.fb_box + FB_STRIDE * node)) return false;
     const int c = w.fb_link[3 * node];
     if (c < 0) return true;
     node = pos < w.fb_link[3 * c + 1] + w.fb_link[3 * c + 2] ? c : c + 1;
   }
-  return false;
+  return true;
 }
 
 __device__ __forceinline__ double fcl_obb_size(cptr<double> b) {
@@ -2037,7 +2022,7 @@ __device__ __forceinline__ bool fcl_gate_mesh(const DevWorld& w, int ga, int gb,
   const int pa = w.tri_pos[(int)w.geom_rec[G_STRIDE * ga + G_PARAM] + ta];
   const int pb = w.tri_pos[(int)w.geom_rec[G_STRIDE * gb + G_PARAM] + tb];
   int a = w.fb_root[ga], b = w.fb_root[gb], nk = 0;
-  for (int depth = 0; depth < 512; ++depth) {
+  for (int depth = 0; depth <= 2 * kFclMaxDepth; ++depth) {
     const cptr<double> ba = w.fb_box + FB_STRIDE * a;
     double aA[9], aT[3], aE[3];
 #pragma unroll
@@ -2064,7 +2049,7 @@ __device__ __forceinline__ bool fcl_gate_mesh(const DevWorld& w, int ga, int gb,
       ++nk;
     }
   }
-  return false;
+  return true;
 }
 
 __device__ __forceinline__ bool mesh_mesh_wave(const DevWorld& w, int ga, const SE3& TA, int gb, const SE3& TB) {
@@ -3052,6 +3037,7 @@ constexpr int kSrvPT = 24;       // pair-table doubles per pair
 struct SrvCtl {
   unsigned long long seq, quit, pad[6];
   unsigned long long done[kSrvMaxG];   // per workgroup: the last batch it published
+  unsigned long long gone[kSrvMaxG];   // per workgroup: 1 once it has left (idle or quit)
   unsigned long long phase[8];         // workgroup 0's s_memrealtime at the batch's phase ends (diagnostics)
   double rows[kSrvN * 3 * kLatScDof];  // per state: q[dof], then (sin, cos)[dof]
   uint32_t out[kSrvMaxG][kSrvN * kSrvMaxW];  // per workgroup, per state: its pairs' mask words
@@ -3181,7 +3167,10 @@ __global__ __launch_bounds__(kSrvThreads) void lat_server_kernel(DevWorld w, Srv
       for (;;) {
         const unsigned long long sq = sys_load(&ctl->seq);
         if (sq != last) {
-          cmd = sq;
+          // pairs with the host's release store of seq: the row loads below
+          // (this thread's, and the workgroup's after the barrier) are
+          // ordered after it by the memory model, not only by s_waitcnt
+          cmd = __hip_atomic_load(&ctl->seq, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
           break;
         }
         if (sys_load(&ctl->quit) != 0ull) break;
@@ -3193,7 +3182,10 @@ __global__ __launch_bounds__(kSrvThreads) void lat_server_kernel(DevWorld w, Srv
     }
     __syncthreads();
     const unsigned long long cmd = s_cmd;
-    if (cmd == 0ull) return;  // idle or quit: the whole workgroup leaves together
+    if (cmd == 0ull) {  // idle or quit: the whole workgroup leaves together
+      if (t == 0) __hip_atomic_store(&ctl->gone[g], 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      return;
+    }
     last = cmd;
     stamp(0);
     const int n = (int)min(cmd & 255ull, (unsigned long long)kSrvN);
@@ -6185,7 +6177,10 @@ struct mpg_world {
   unsigned long long srv_seq = 0;
   bool srv_running = false;
   bool srv_ok = false;      // the world fits the server (closed-form / MPR pairs only, records, LDS)
-  bool srv_broken = false;  // it failed to answer once: launches from then on
+  bool srv_broken = false;  // it failed to answer: launches until srv_retry_at
+  std::chrono::steady_clock::time_point srv_retry_at{};
+  bool srv_quitting = false;  // quit was set after a missed answer; the stream may still run
+  int64_t srv_served = 0, srv_starts = 0, srv_fallbacks = 0;  // mpg_latency_server_stats
   int srv_mode = 1;         // MPG_SMALL_SERVER=0: off
   long long srv_idle_us = 1000;
   int srv_g = 8;            // workgroups (MPG_SMALL_SERVER_WG)
@@ -6459,6 +6454,7 @@ void geom_record(const mpg_world_desc* d, int g, double* rec) {
 struct FclBvh {
   std::vector<double> box;  // [n][FB_STRIDE]
   std::vector<int> link;    // [n][3]
+  int max_depth = 0;        // deepest leaf (root = 0), bounds the device gates' descent
 };
 
 // eigen_old: Jacobi rotations; vout(r, c) = v[c][r], dout = eigenvalues
@@ -6570,7 +6566,8 @@ void fcl_fit_obb(const double S1[3], const double S2[6], double n_points, const 
 }
 
 void fcl_bvh_node(FclBvh& B, const double* V, const int32_t* tri, std::vector<int>& prim, int id, int first, int n,
-                  int base) {
+                  int base, int depth = 0) {
+  if (depth > B.max_depth) B.max_depth = depth;
   int* cur = prim.data() + first;
   double S1[3] = {0, 0, 0}, S2[6] = {0, 0, 0, 0, 0, 0};
   std::vector<const double*> pts;
@@ -6617,8 +6614,8 @@ void fcl_bvh_node(FclBvh& B, const double* V, const int32_t* tri, std::vector<in
     if (!(((sv[0] * p[0] + sv[1] * p[1]) + sv[2] * p[2]) > split)) std::swap(cur[i], cur[c1++]);
   }
   if (c1 == 0 || c1 == n) c1 = n / 2;
-  fcl_bvh_node(B, V, tri, prim, child, first, c1, base);
-  fcl_bvh_node(B, V, tri, prim, child + 1, first + c1, n - c1, base);
+  fcl_bvh_node(B, V, tri, prim, child, first, c1, base, depth + 1);
+  fcl_bvh_node(B, V, tri, prim, child + 1, first + c1, n - c1, base, depth + 1);
 }
 
 // computeBV<OBB>(shape, identity): box I / side/2; sphere I / r; capsule
@@ -7044,6 +7041,15 @@ int mpg_profile_read(mpg_world* w, double* ms, int64_t* launches, int64_t* units
   return MPG_OK;
 }
 
+int mpg_latency_server_stats(mpg_world* w, int64_t* served, int64_t* starts, int64_t* fallbacks, int32_t* state) {
+  if (!w) return set_error(MPG_E_INVALID, "world is NULL");
+  if (served) *served = w->srv_served;
+  if (starts) *starts = w->srv_starts;
+  if (fallbacks) *fallbacks = w->srv_fallbacks;
+  if (state) *state = !(w->srv_mode && w->srv_ok) ? 0 : w->srv_broken ? 2 : 1;
+  return MPG_OK;
+}
+
 int mpg_synchronize(int device) {
   HIP_TRY(hipSetDevice(device));
   HIP_TRY(hipDeviceSynchronize());
@@ -7191,8 +7197,13 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
     fbvh.link.resize(fbvh.link.size() + 3);
     std::vector<int> prim((size_t)tn);
     for (int64_t t = 0; t < tn; ++t) prim[t] = (int)t;
+    fbvh.max_depth = 0;
     fcl_bvh_node(fbvh, d->vertices + 3 * (size_t)d->geom_vertex_start[g], d->mesh_triangle + 3 * t0, prim, 0, 0,
                  (int)tn, base);
+    if (fbvh.max_depth > kFclMaxDepth)
+      return set_error(MPG_E_UNSUPPORTED, "BVH mesh geometry " + std::to_string(g) + ": FCL's mean-split tree is " +
+                                              std::to_string(fbvh.max_depth) + " levels deep (the device gates descend at most " +
+                                              std::to_string(kFclMaxDepth) + ")");
     for (int64_t k = 0; k < tn; ++k) tri_pos[t0 + prim[k]] = (int)k;
   }
   if (fbvh.box.empty()) {
@@ -7873,7 +7884,9 @@ int srv_start(mpg_world* w) {
     HIP_TRY(hipFuncSetAttribute((const void*)lat_server_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)w->srv_lds));
   }
+  for (int k = 0; k < kSrvMaxG; ++k) __atomic_store_n(&w->srv_h->gone[k], 0ull, __ATOMIC_RELAXED);
   __atomic_store_n(&w->srv_h->quit, 0ull, __ATOMIC_RELEASE);
+  ++w->srv_starts;
   hipLaunchKernelGGL(lat_server_kernel, dim3(w->srv_g), dim3(kSrvThreads), w->srv_lds, w->srv_stream, w->dw, w->srv_d,
                      (unsigned long long)w->srv_idle_us * 100ull, w->srv_stats ? 1 : 0);
   HIP_TRY(hipGetLastError());
@@ -7883,10 +7896,18 @@ int srv_start(mpg_world* w) {
 
 // one batch through the resident server: rows (q, host sin/cos) into the
 // control block, seq bumped, the host spins on `done`.  The server may have
-// left (idle) before it saw the request: the stream is checked every 50 us
-// and the server restarted.  No answer within 2 s: the server is stopped and
-// marked broken, MPG_E_HIP (the caller then launches).
+// left (idle) before it saw the request: every 50 us the host looks for
+// workgroups that have left (`gone`) without answering -- all of them (stream
+// complete): start it again; some of them: stop the rest and start all again.
+// Workgroups that are only slow (another stream sharing the GPU) are waited
+// for.  No answer within 2 s: the server is stopped, MPG_E_HIP (the caller
+// launches instead for a while, then tries the server again).
 int collide_served(mpg_world* w, const double* q, int64_t n, uint8_t* flags, uint32_t* pair_mask) {
+  if (w->srv_running && w->srv_quitting) {  // told to quit after a missed answer
+    if (hipStreamQuery(w->srv_stream) != hipSuccess) return set_error(MPG_E_HIP, "latency server has not left yet");
+    w->srv_running = false;
+    w->srv_quitting = false;
+  }
   if (!w->srv_running) {
     const int rc = srv_start(w);
     if (rc) return rc;
@@ -7915,9 +7936,13 @@ int collide_served(mpg_world* w, const double* q, int64_t n, uint8_t* flags, uin
     if (us < next_us) continue;
     next_us = us + 50;
     hipError_t e = hipStreamQuery(w->srv_stream);
-    if (e == hipErrorNotReady && us > 500 && !forced) {
-      // some workgroups left (idle) before the request, the others are
-      // still polling: stop them and start all again (once per request)
+    bool partial = false;  // a workgroup left before this request, others are still resident
+    for (int k = 0; k < w->srv_g && e == hipErrorNotReady; ++k)
+      partial |= __atomic_load_n(&C->gone[k], __ATOMIC_ACQUIRE) != 0ull &&
+                 __atomic_load_n(&C->done[k], __ATOMIC_ACQUIRE) != seq;
+    if (partial && !forced) {
+      // stop the ones still polling and start all again (once per request);
+      // they see quit within one poll, so this wait is short
       __atomic_store_n(&C->quit, 1ull, __ATOMIC_RELEASE);
       e = hipStreamSynchronize(w->srv_stream);
       forced = true;
@@ -7928,10 +7953,11 @@ int collide_served(mpg_world* w, const double* q, int64_t n, uint8_t* flags, uin
       if (rc) return rc;
     } else if (e != hipErrorNotReady || us > 2000000) {
       __atomic_store_n(&C->quit, 1ull, __ATOMIC_RELEASE);
-      w->srv_broken = true;
+      w->srv_quitting = true;  // not waited for here: the next try checks that it has left
       return set_error(MPG_E_HIP, "latency server did not answer");
     }
   }
+  ++w->srv_served;
   if (w->prof) {  // a served batch counts as one narrow-stage "launch" of its post -> done time
     std::lock_guard<std::mutex> lk(w->prof_mu);
     w->prof_ms[MPG_STAGE_NARROW] += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
@@ -7961,11 +7987,19 @@ int collide_served(mpg_world* w, const double* q, int64_t n, uint8_t* flags, uin
 // hits into flags / pair masks
 template <bool FROM_POSES>
 int collide_small(mpg_world* w, const double* q, int64_t n, uint8_t* flags, uint32_t* pair_mask, hipStream_t s) {
-  if (!FROM_POSES && w->srv_mode && w->srv_ok && !w->srv_broken && n <= w->srv_max_n && !w->dw.dbg(3) && !w->dw.dbg(7)) {
-    if (collide_served(w, q, n, flags, pair_mask) == MPG_OK) return MPG_OK;
-    // the server could not be started or did not answer: launches from now on
-    std::fprintf(stderr, "mplib_amd: latency server unavailable (%s); using one launch per batch\n", g_last_error.c_str());
+  if (!FROM_POSES && w->srv_mode && w->srv_ok && n <= w->srv_max_n && !w->dw.dbg(3) && !w->dw.dbg(7) &&
+      (!w->srv_broken || std::chrono::steady_clock::now() >= w->srv_retry_at)) {
+    if (collide_served(w, q, n, flags, pair_mask) == MPG_OK) {
+      w->srv_broken = false;
+      return MPG_OK;
+    }
+    // the server could not be started or did not answer: launches for the
+    // next second, then the server is tried again
+    std::fprintf(stderr, "mplib_amd: latency server unavailable (%s); one launch per batch for 1 s\n",
+                 g_last_error.c_str());
     w->srv_broken = true;
+    ++w->srv_fallbacks;
+    w->srv_retry_at = std::chrono::steady_clock::now() + std::chrono::seconds(1);
     (void)hipGetLastError();
   }
   const size_t row = FROM_POSES ? (size_t)w->dw.n_links * 7 : (size_t)w->dw.dof;

@@ -111,6 +111,24 @@ def test_result_changing_switches_only_in_diag_builds():
         assert "debug_mode ==" not in s, ln
     hdr = open(os.path.join(ROOT, "mplib_amd", "csrc", "mpg_fk.h")).read()
     assert "#ifdef MPG_DIAG\n    return debug_mode == k;" in hdr
+    # the measured +-1 % A/B variants are gone from the
+    # product source (their history is in profiles/), so the bit-exact path
+    # has one reading
+    csrc = os.path.join(ROOT, "mplib_amd", "csrc")
+    for fn in os.listdir(csrc):
+        if fn.endswith((".hip", ".h")):
+            text = open(os.path.join(csrc, fn)).read()
+            for macro in ("MPG_PUSH_SCAN", "MPG_FK_SPARSE", "MPG_FK_UNROLL", "MPG_FK_FASTSIN", "MPG_AB_"):
+                assert macro not in text, (fn, macro)
+
+
+def test_boundary_text_matches_the_code():
+    """the header describes the traversal-order contacts the
+    kernels compute (mpg_kernels.hip mesh_shape_first_contact /
+    mesh_mesh_first_contact), not the round-3 triangle-index order."""
+    hdr = open(os.path.join(ROOT, "include", "mpgpu.h")).read()
+    for stale in ("triangle index order", "is not restated"):
+        assert stale not in hdr, stale
 
 
 def test_last_error_copy():

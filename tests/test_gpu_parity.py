@@ -326,9 +326,10 @@ def test_attached_box_in_box_scene_matches_oracle():
 def test_latency_path_matches_oracle(cfg, server, monkeypatch):
     """Host batches up to the small-batch limit run as one small_kernel launch
     (one wave per pair x 64-config tile, bounding-sphere test, MPR / closed
-    forms), up to 16 states through the resident latency server
-    (MPG_SMALL_SERVER): bit-exact with the oracle and with the two-phase
-    pipeline."""
+    forms), up to 32 states (MPG_SMALL_SERVER_MAX) through the resident
+    latency server (MPG_SMALL_SERVER): bit-exact with the oracle and with the
+    two-phase pipeline.  With the server on, the batches of at most 32 states
+    really went through it (latency_server_stats: served, never fallen back)."""
     monkeypatch.setenv("MPG_SMALL_SERVER", str(server))
     monkeypatch.setenv("MPG_SMALL_SERVER_MAX", "32")
     w, art = scenes.world(cfg)
@@ -358,6 +359,13 @@ def test_latency_path_matches_oracle(cfg, server, monkeypatch):
             f, m = w.collide_batch(q[i:i + n])
             np.testing.assert_array_equal(f, fo[i:i + n])
             np.testing.assert_array_equal(m, mo[i:i + n])
+    st = w.latency_server_stats()
+    if server:
+        # every host batch of <= 32 states above: 6 + 400 + (40 + 23 + 10 + 5)
+        assert st["state"] == "in_use" and st["fallbacks"] == 0, st
+        assert st["served"] == 484 and st["starts"] >= 1, st
+    else:
+        assert st == {"served": 0, "starts": 0, "fallbacks": 0, "state": "unused"}, st
     w.set_small_batch_max(0)
     f, m = w.collide_batch(q[:1000])
     np.testing.assert_array_equal(f, fo[:1000])
@@ -383,6 +391,10 @@ def test_latency_server_idle_restart_and_teardown(monkeypatch):
             np.testing.assert_array_equal(m, mo[k:k + 1])
         if k % 8 == 0:
             _t.sleep(0.002)  # > idle: the servers have left
+    for ww in (w, w2):  # every request was answered by the server, restarted after each idle exit
+        st = ww.latency_server_stats()
+        assert st["served"] == 64 and st["fallbacks"] == 0 and st["state"] == "in_use", st
+        assert st["starts"] >= 8, st
     del w, w2
     gc.collect()
 
