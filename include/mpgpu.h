@@ -59,6 +59,8 @@ extern "C" {
 #define MPG_E_UNSUPPORTED 2 /* request or geometry pair not implemented     */
 #define MPG_E_HIP 3         /* HIP runtime error                            */
 #define MPG_E_NOMEM 4
+#define MPG_E_FAILED 5      /* the reference itself fails on this input
+                               (FCL throws: mpg_distance_batch_req)      */
 
 /* memory kinds for the batch calls */
 #define MPG_MEM_HOST 0
@@ -257,41 +259,79 @@ int mpg_check_motion_batch(mpg_world *world, const double *q_from, const double 
  * Batched distance: per configuration, PlanningWorldTpl::distanceSelf and
  * distanceOthers (src/planning_world.cpp:493-720) over the pair table, whose
  * first n_self_pairs entries form the self group: ACM-allowed pairs are
- * skipped, each pair's fcl::distance (DistanceRequest(): -1 when the shapes
- * penetrate) is compared with strict '<', so the first minimum wins.
+ * skipped, each pair's fcl::distance(o1 = pair_a, o2 = pair_b, request) is
+ * compared with strict '<' (:513), so the first minimum wins.
  * d_*: minimum distance (DBL_MAX if the group is empty), p_*: its pair
- * index (-1 if none).  Distances are within 1e-5 of FCL's GJK (GJK run to
- * 1e-12 relative convergence on the same support mappings).  A point cloud
- * (OcTree) pair's distance is the minimum over its occupied leaf boxes
- * (OcTreeShapeDistanceRecurse, leaf box first).  A BVH-mesh pair's distance
- * is the minimum over its triangles (mesh-mesh: PQP triDistance of triangle
- * pairs; mesh-shape: GJK of (shape, triangle); mesh-OcTree: GJK of (leaf box,
- * triangle)), as FCL's MeshDistanceTraversalNodeOBBRSS /
- * MeshShapeDistanceTraversalNodeOBBRSS / OcTreeMeshDistanceRecurse report it.
+ * index (-1 if none).  What fcl::distance computes [FCL 0.7.0, restated in
+ * oracle/collide_oracle.c pair_distance and oracle/fcl_gjk_dist.h]:
+ *   shape-shape   DistanceRequest(): GJKSolver_libccd::shapeDistance -- the
+ *                 closed forms for sphere-sphere / -box / -capsule /
+ *                 -cylinder (either order) and capsule-capsule, else
+ *                 GJKDistance: libccd's GJK (__ccdGJK, then _ccdDist) in float
+ *                 (ccd_real_t of the reference's libccd build), -1 once GJK
+ *                 finds the shapes intersecting.  With enable_signed_distance
+ *                 every shape pair runs GJKSignedDistance: GJK, then for
+ *                 intersecting shapes FCL's EPA (__ccdEPA to epa_tolerance
+ *                 1e-4, penEPAPosClosest): -(penetration depth).  One
+ *                 departure: where FCL's EPA would expand a nearest face the
+ *                 new support point does not see (its polytope turns
+ *                 non-convex and can cycle forever), the EPA stops at that
+ *                 face (oracle/fcl_gjk_dist.h, "convexity guard").
+ *   OcTree-shape  the minimum over the occupied leaves of shapeDistance(Box
+ *                 (leaf), shape) (OcTreeShapeDistanceRecurse).
+ *   mesh-shape    the minimum over the triangles of shapeTriangleDistance
+ *                 (sphereTriangleDistance for spheres, else GJK on the
+ *                 triangle GJK object) (MeshShapeDistanceTraversalNodeOBBRSS).
+ *   mesh-mesh     the minimum of triDistance over the triangle pairs (0 when
+ *                 one intersects) (MeshDistanceTraversalNodeOBBRSS).
+ *   mesh-OcTree   the minimum over (leaf box, triangle) of GJK distance
+ *                 (OcTreeMeshDistanceRecurse).
+ *   Mesh and OcTree pairs are unsigned whatever the request (their leaves
+ *   call the unsigned shapeDistance / triDistance), -1 once a leaf test
+ *   penetrates.
+ * Device and oracle agree bit for bit on the GJK/EPA floats; between equal
+ * minima of a mesh / OcTree pair the first leaf test in the oracle's scan
+ * order wins (FCL's RSS-ordered traversal may pick another equal one).
  */
 int mpg_distance_batch(mpg_world *world, const double *q, int64_t n, int32_t n_self_pairs, double *d_self,
                        int32_t *p_self, double *d_others, int32_t *p_others, int mem, void *stream);
 
 /*
- * mpg_distance_batch with DistanceRequest's options (python/pybind_fcl.hpp:
- * 310-316, passed to fcl::distance by PlanningWorldTpl::distance*,
- * src/planning_world.cpp:512, 537):
- *   MPG_DISTANCE_SIGNED          enable_signed_distance: an intersecting pair's
- *                                distance is -(penetration depth) (FCL 0.7.0
- *                                ccdGJKSignedDist: GJK then EPA), not -1;
- *   MPG_DISTANCE_NEAREST_POINTS  enable_nearest_points.
- * pts_self / pts_others ([n*6], may be NULL): the nearest points (p1 on the
- * pair's first object, p2 on its second, world frame) of each group's
- * minimum pair.  Shape-shape pairs report them whatever the flags, as FCL's
- * shape distance leaf computes them (libccd extractClosestPoints: the
- * barycentric weights of the final GJK simplex; penEPAPosClosest for signed
- * penetrations); zeros for an unsigned penetration (-1).  Point-cloud and
- * BVH-mesh pairs report zeros; with either flag set a world with such pairs
- * returns MPG_E_UNSUPPORTED.  EPA runs in fp64 to 1e-10 m (at most 64
- * polytope vertices); FCL's float EPA stops at libccd's epa_tolerance (1e-4).
+ * DistanceRequest (python/pybind_fcl.hpp:310-316) as PlanningWorldTpl::
+ * distance* passes it to fcl::distance (src/planning_world.cpp:512, 537):
+ *   flags: MPG_DISTANCE_SIGNED (enable_signed_distance),
+ *          MPG_DISTANCE_NEAREST_POINTS (enable_nearest_points);
+ *   distance_tolerance: GJKSolver_libccd::distance_tolerance, libccd's
+ *          dist_tolerance (default 1e-6).
+ * pts_self / pts_others ([n*6], may be NULL): DistanceResult::nearest_points
+ * [0] and [1] (world frame) of each group's minimum pair, as FCL leaves them:
+ *   shape-shape   always (the shape leaf computes them whatever the flags):
+ *                 points on o1 and o2; zeros for an unsigned penetration (-1);
+ *   OcTree-shape  always, (leaf box point, shape point) in that order for
+ *                 both argument orders (the tree is the traversal's o1);
+ *   mesh-shape    always; (mesh point, shape point), swapped to (shape, mesh)
+ *                 for a (shape, mesh) pair only with enable_nearest_points;
+ *   mesh-mesh     only with enable_nearest_points (zeros otherwise);
+ *   mesh-OcTree   always, (leaf box point, triangle point).
+ * Where FCL throws (its EPA's FCL_THROW_FAILED_AT_THIS_CONFIGURATION) the
+ * configuration's p_self = p_others = MPG_DISTANCE_FCL_THROWS and both
+ * distances are NaN; MPG_MEM_HOST calls then return MPG_E_FAILED.  A device
+ * EPA that outgrows its polytope (96 vertices) marks the configuration
+ * MPG_DISTANCE_EPA_CAPACITY (MPG_MEM_HOST: MPG_E_UNSUPPORTED) -- never a
+ * silently different value.
  */
 #define MPG_DISTANCE_SIGNED 1
 #define MPG_DISTANCE_NEAREST_POINTS 2
+#define MPG_DISTANCE_FCL_THROWS (-2)
+#define MPG_DISTANCE_EPA_CAPACITY (-3)
+typedef struct mpg_distance_request {
+  int32_t flags;
+  double distance_tolerance;
+} mpg_distance_request;
+int mpg_distance_batch_req(mpg_world *world, const double *q, int64_t n, int32_t n_self_pairs,
+                           const mpg_distance_request *request, double *d_self, int32_t *p_self, double *pts_self,
+                           double *d_others, int32_t *p_others, double *pts_others, int mem, void *stream);
+/* mpg_distance_batch_req with distance_tolerance = 1e-6 */
 int mpg_distance_batch_ex(mpg_world *world, const double *q, int64_t n, int32_t n_self_pairs, int32_t flags,
                           double *d_self, int32_t *p_self, double *pts_self, double *d_others, int32_t *p_others,
                           double *pts_others, int mem, void *stream);

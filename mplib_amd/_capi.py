@@ -13,7 +13,7 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libmpgpu.so")
 
-MPG_OK, MPG_E_INVALID, MPG_E_UNSUPPORTED, MPG_E_HIP, MPG_E_NOMEM = 0, 1, 2, 3, 4
+MPG_OK, MPG_E_INVALID, MPG_E_UNSUPPORTED, MPG_E_HIP, MPG_E_NOMEM, MPG_E_FAILED = 0, 1, 2, 3, 4, 5
 MPG_MEM_HOST, MPG_MEM_DEVICE = 0, 1
 STAGES = ("cull", "bucket", "narrow")  # MPG_STAGE_* order
 
@@ -80,6 +80,10 @@ SIGNATURES = {
                                              ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                              ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
                                              ctypes.c_void_p]),
+    "mpg_distance_batch_req": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32,
+                                              ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                              ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
+                                              ctypes.c_void_p]),
     "mpg_collide_contacts": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int,
                                             ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                             ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]),

@@ -149,6 +149,7 @@ struct DistanceRequest {
   void check_supported() const;
   // MPG_DISTANCE_* flags of the C ABI
   int32_t flags() const;
+  mpg_distance_request to_c() const;
 };
 struct DistanceResult {
   double min_distance = std::numeric_limits<double>::max();
@@ -590,8 +591,8 @@ class PlanningWorld {
   void distance_batch(const double* q, int64_t n, double* d_self, int32_t* p_self, double* d_others,
                       int32_t* p_others);
   // with DistanceRequest's flags and the nearest points [n*6] (may be NULL)
-  void distance_batch_ex(const double* q, int64_t n, int32_t flags, double* d_self, int32_t* p_self, double* pts_self,
-                         double* d_others, int32_t* p_others, double* pts_others);
+  void distance_batch_ex(const double* q, int64_t n, const DistanceRequest& r, double* d_self, int32_t* p_self,
+                         double* pts_self, double* d_others, int32_t* p_others, double* pts_others);
   int n_self_pairs();
 
   // batch API (one launch for N configurations)

@@ -409,9 +409,10 @@ PYBIND11_MODULE(pymp, m_all) {
         DeviceWorld w(d, default_device());
         double ds = 0, dd = 0, qs[6], qo[6];
         int32_t ps = -1, po = -1;
-        check_status(mpg_distance_batch_ex(w.get(), nullptr, 1, 0, req.flags(), &ds, &ps, qs, &dd, &po, qo,
-                                           MPG_MEM_HOST, nullptr),
-                     "mpg_distance_batch_ex");
+        const mpg_distance_request creq = req.to_c();
+        check_status(mpg_distance_batch_req(w.get(), nullptr, 1, 0, &creq, &ds, &ps, qs, &dd, &po, qo, MPG_MEM_HOST,
+                                            nullptr),
+                     "mpg_distance_batch_req");
         DistanceResult r;
         r.min_distance = dd;
         for (int k = 0; k < 3; ++k) {
@@ -687,19 +688,17 @@ PYBIND11_MODULE(pymp, m_all) {
              const int dim = w.state_dim();
              if (states.ndim() != 2 || states.shape(1) != dim)
                throw std::invalid_argument("states must be [N, " + std::to_string(dim) + "] float64");
-             int32_t flags = 0;
-             if (!request.is_none()) {
-               const DistanceRequest& r = request.cast<const DistanceRequest&>();
-               r.check_supported();
-               flags = r.flags();
-             }
+             DistanceRequest r;
+             if (!request.is_none()) r = request.cast<const DistanceRequest&>();
+             r.check_supported();
+             const int32_t flags = r.flags();
              const int64_t n = states.shape(0);
              py::array_t<double> ds(n), dot(n);
              py::array_t<int32_t> ps(n), po(n);
              const double* q = states.data();
              double *a = ds.mutable_data(), *b = dot.mutable_data();
              int32_t *c = ps.mutable_data(), *d = po.mutable_data();
-             if (!nearest_points && flags == 0) {
+             if (!nearest_points && flags == 0 && r.distance_tolerance == 1e-6) {
                {
                  py::gil_scoped_release rel;
                  w.distance_batch(q, n, a, c, b, d);
@@ -710,15 +709,16 @@ PYBIND11_MODULE(pymp, m_all) {
              double *e = qs.mutable_data(), *f = qo.mutable_data();
              {
                py::gil_scoped_release rel;
-               w.distance_batch_ex(q, n, flags, a, c, e, b, d, f);
+               w.distance_batch_ex(q, n, r, a, c, e, b, d, f);
              }
              return py::tuple(py::make_tuple(ds, ps, dot, po, qs, qo));
            },
            py::arg("states"), py::arg("request") = py::none(), py::arg("nearest_points") = false,
            "Batched self_distance / distance_with_others: (d_self[N], pair_self[N], d_others[N], pair_others[N]); "
            "-1 = a penetrating pair, pair indices into get_collision_pair_info().  With a DistanceRequest "
-           "(enable_signed_distance: -penetration depth instead of -1) or nearest_points=True, also the nearest "
-           "points (p1, p2) of each group's minimum pair: (..., pts_self[N, 6], pts_others[N, 6]).")
+           "(enable_signed_distance: -penetration depth instead of -1; distance_tolerance) or nearest_points=True, "
+           "also DistanceResult.nearest_points of each group's minimum pair: (..., pts_self[N, 6], pts_others[N, 6]) "
+           "(include/mpgpu.h mpg_distance_batch_req: which point is which).")
       // ---- batched validity (new; one device launch for N states) ----
       .def("sample_pair_counts",
            [](PW& w, int64_t n, uint64_t seed) {

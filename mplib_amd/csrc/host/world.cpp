@@ -683,6 +683,13 @@ int32_t DistanceRequest::flags() const {
   return (enable_signed_distance ? MPG_DISTANCE_SIGNED : 0) | (enable_nearest_points ? MPG_DISTANCE_NEAREST_POINTS : 0);
 }
 
+mpg_distance_request DistanceRequest::to_c() const {
+  mpg_distance_request r;
+  r.flags = flags();
+  r.distance_tolerance = distance_tolerance;
+  return r;
+}
+
 int PlanningWorld::n_self_pairs() {
   ensure_snapshot(CollisionRequest(), false);
   int n = 0;
@@ -700,13 +707,15 @@ void PlanningWorld::distance_batch(const double* q, int64_t n, double* d_self, i
                "mpg_distance_batch");
 }
 
-void PlanningWorld::distance_batch_ex(const double* q, int64_t n, int32_t flags, double* d_self, int32_t* p_self,
-                                      double* pts_self, double* d_others, int32_t* p_others, double* pts_others) {
+void PlanningWorld::distance_batch_ex(const double* q, int64_t n, const DistanceRequest& r, double* d_self,
+                                      int32_t* p_self, double* pts_self, double* d_others, int32_t* p_others,
+                                      double* pts_others) {
   const int ns = n_self_pairs();
   ensure_snapshot(CollisionRequest());
-  check_status(mpg_distance_batch_ex(world_->get(), q, n, ns, flags, d_self, p_self, pts_self, d_others, p_others,
-                                     pts_others, MPG_MEM_HOST, nullptr),
-               "mpg_distance_batch_ex");
+  const mpg_distance_request req = r.to_c();
+  check_status(mpg_distance_batch_req(world_->get(), q, n, ns, &req, d_self, p_self, pts_self, d_others, p_others,
+                                      pts_others, MPG_MEM_HOST, nullptr),
+               "mpg_distance_batch_req");
 }
 
 namespace {
@@ -736,7 +745,7 @@ WorldDistanceResult PlanningWorld::self_distance(const DistanceRequest& r) {
   std::vector<double> s = current_state();
   double ds, dot, qs[6], qo[6];
   int32_t ps, po;
-  distance_batch_ex(s.data(), 1, r.flags(), &ds, &ps, qs, &dot, &po, qo);
+  distance_batch_ex(s.data(), 1, r, &ds, &ps, qs, &dot, &po, qo);
   return distance_result(ds, ps, pairs_, qs);
 }
 WorldDistanceResult PlanningWorld::distance_with_others(const DistanceRequest& r) {
@@ -744,7 +753,7 @@ WorldDistanceResult PlanningWorld::distance_with_others(const DistanceRequest& r
   std::vector<double> s = current_state();
   double ds, dot, qs[6], qo[6];
   int32_t ps, po;
-  distance_batch_ex(s.data(), 1, r.flags(), &ds, &ps, qs, &dot, &po, qo);
+  distance_batch_ex(s.data(), 1, r, &ds, &ps, qs, &dot, &po, qo);
   return distance_result(dot, po, pairs_, qo);
 }
 WorldDistanceResult PlanningWorld::distance_full(const DistanceRequest& r) {
@@ -752,7 +761,7 @@ WorldDistanceResult PlanningWorld::distance_full(const DistanceRequest& r) {
   std::vector<double> s = current_state();
   double ds, dot, qs[6], qo[6];
   int32_t ps, po;
-  distance_batch_ex(s.data(), 1, r.flags(), &ds, &ps, qs, &dot, &po, qo);
+  distance_batch_ex(s.data(), 1, r, &ds, &ps, qs, &dot, &po, qo);
   auto r1 = distance_result(ds, ps, pairs_, qs), r2 = distance_result(dot, po, pairs_, qo);
   return r1.min_distance < r2.min_distance ? r1 : r2;  // planning_world.cpp:718-719
 }

@@ -110,6 +110,11 @@ struct DevWorld {
   cptr<double> oct_grid;   // [n_geoms * OG_STRIDE]
   cptr<int> oct_cells;     // cell start offsets into oct_list
   cptr<int> oct_list;      // leaf indices
+  // per leaf its path in FCL's octree (getRootBV halved by computeChildBV):
+  // child indices 3 bits per level, the root's first (most significant),
+  // and the number of levels (OcTreeMeshIntersectRecurse's gate)
+  cptr<uint64_t> oct_path;
+  cptr<int> oct_depth;
   // BVH meshes: one record per triangle (TR_*, mesh frame) grouped into
   // spatial clusters (the leaves of a median-split tree): cluster box [6],
   // cluster (first triangle record, triangle count), per geometry (first

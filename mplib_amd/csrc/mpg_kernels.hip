@@ -2052,6 +2052,87 @@ __device__ __forceinline__ bool fcl_gate_mesh(const DevWorld& w, int ga, int gb,
   return true;
 }
 
+// MeshOcTree: OcTreeMeshIntersectRecurse's descent to the (occupied leaf l,
+// triangle t) pair [ext FCL 0.7.0; oracle octmesh_rec].  Every node pair is
+// tested as two world OBBs: the octree node's AABB under TO (To = TO centre,
+// axis = R, half sizes) against the mesh node's OBBRSS under TM (To = TM To,
+// axis = R axis).  The octree node is split (its child on l's path, oct_path)
+// when the mesh node is a leaf or the octree node is not and its AABB size
+// (full width squared) exceeds the OBB's (half extents squared); else the mesh
+// node (left / right by t's position).  key (optional) collects the octree
+// child indices (3 bits) and the mesh choices (1 bit); at the first point two
+// descents differ they take the same kind of step, so the lexicographic order
+// of keys is the traversal's visit order (children 0..7, left before right).
+__device__ __forceinline__ bool fcl_overlap_world(const SE3& TO, const double* lo, const double* hi, const SE3& TM,
+                                                  cptr<double> b) {
+  double ctr[3], E1[3], To1[3], To2[3], ax2[9], t[3], T[3], R[9], E2[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    ctr[k] = (lo[k] + hi[k]) * 0.5;
+    E1[k] = (hi[k] - lo[k]) * 0.5;
+    E2[k] = b[FB_EXT + k];
+  }
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    To1[i] = ((TO.R[3 * i] * ctr[0] + TO.R[3 * i + 1] * ctr[1]) + TO.R[3 * i + 2] * ctr[2]) + TO.p[i];
+    To2[i] = ((TM.R[3 * i] * b[FB_TO] + TM.R[3 * i + 1] * b[FB_TO + 1]) + TM.R[3 * i + 2] * b[FB_TO + 2]) + TM.p[i];
+  }
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+      ax2[3 * i + j] = (TM.R[3 * i] * b[FB_AXIS + j] + TM.R[3 * i + 1] * b[FB_AXIS + 3 + j]) + TM.R[3 * i + 2] * b[FB_AXIS + 6 + j];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) t[k] = To2[k] - To1[k];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) T[i] = (TO.R[i] * t[0] + TO.R[3 + i] * t[1]) + TO.R[6 + i] * t[2];
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) R[3 * i + j] = (TO.R[i] * ax2[j] + TO.R[3 + i] * ax2[3 + j]) + TO.R[6 + i] * ax2[6 + j];
+  return !obb_disjoint(R, T, E1, E2);
+}
+
+constexpr int kOctKeyWords = 5;  // 16 octree levels x 3 bits + 2 x kFclMaxDepth mesh bits
+__device__ __forceinline__ bool fcl_gate_octree_mesh(const DevWorld& w, int go, const SE3& TO, int gm, const SE3& TM,
+                                                     int l, int t, uint64_t* key = nullptr) {
+  const double delta = (double)(1 << 16) * w.geom_rec[G_STRIDE * go + G_PARAM + 2] / 2;
+  double lo[3] = {-delta, -delta, -delta}, hi[3] = {delta, delta, delta};
+  const uint64_t path = w.oct_path[l];
+  const int od = w.oct_depth[l];
+  const int pos = w.tri_pos[(int)w.geom_rec[G_STRIDE * gm + G_PARAM] + t];
+  int lev = 0, node = w.fb_root[gm], nk = 0;
+  auto put = [&](unsigned v, int bits) {
+    if (!key) return;
+    for (int b = bits - 1; b >= 0; --b, ++nk)
+      if (((v >> b) & 1u) && nk < 64 * kOctKeyWords) key[nk >> 6] |= 1ull << (63 - (nk & 63));
+  };
+  for (int step = 0; step <= 16 + kFclMaxDepth; ++step) {
+    const cptr<double> bb = w.fb_box + FB_STRIDE * node;
+    if (!fcl_overlap_world(TO, lo, hi, TM, bb)) return false;
+    const bool oleaf = lev == od;
+    const int c = w.fb_link[3 * node];
+    if (oleaf && c < 0) return true;
+    const double d0 = hi[0] - lo[0], d1 = hi[1] - lo[1], d2 = hi[2] - lo[2];
+    if (c < 0 || (!oleaf && ((d0 * d0 + d1 * d1) + d2 * d2) > fcl_obb_size(bb))) {
+      const unsigned ci = (unsigned)(path >> (3 * (od - 1 - lev))) & 7u;
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        const double mid = (lo[k] + hi[k]) * 0.5;
+        if ((ci >> k) & 1u) lo[k] = mid;
+        else hi[k] = mid;
+      }
+      ++lev;
+      put(ci, 3);
+    } else {
+      const bool right = !(pos < w.fb_link[3 * c + 1] + w.fb_link[3 * c + 2]);
+      node = right ? c + 1 : c;
+      put(right ? 1u : 0u, 1);
+    }
+  }
+  return true;
+}
+
 __device__ __forceinline__ bool mesh_mesh_wave(const DevWorld& w, int ga, const SE3& TA, int gb, const SE3& TB) {
   // lanes take 64 of B's triangles into A's frame; each one that meets A's
   // box is then broadcast, A's cluster boxes are tested one per lane, and
@@ -2336,7 +2417,7 @@ __device__ __forceinline__ bool mesh_octree_wave(const DevWorld& w, int gm, cons
           const CV3 sp = msupport_box_tri(A1, h, B, TP, tc, dir);
           res = mpr_advance(w.mpr_tol, sp, st, v0, v1, v2, v3_, dir);
         }
-        if (res > 0) return true;
+        if (res > 0 && fcl_gate_octree_mesh(w, go, TO, gm, TM, leaf, (int)rec[TR_ID])) return true;
       }
     }
     return false;
@@ -3505,507 +3586,438 @@ __global__ __launch_bounds__(128) void pose_kernel(DevWorld w, const double* __r
 
 __device__ __forceinline__ double d3dot(const V3& a, const V3& b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
 
-// closest point of triangle (a, b, c) to the origin (Ericson 5.1.5); keep
-// marks the vertices of the reached feature
-__device__ __forceinline__ V3 tri_closest(const V3& a, const V3& b, const V3& c, bool keep[3]) {
-  const V3 ab = vsub(b, a), ac = vsub(c, a);
-  const double d1 = -d3dot(ab, a), d2 = -d3dot(ac, a);
-  keep[0] = keep[1] = keep[2] = false;
-  if (d1 <= 0 && d2 <= 0) {
-    keep[0] = true;
-    return a;
-  }
-  const double d3 = -d3dot(ab, b), d4 = -d3dot(ac, b);
-  if (d3 >= 0 && d4 <= d3) {
-    keep[1] = true;
-    return b;
-  }
-  const double vc = d1 * d4 - d3 * d2;
-  if (vc <= 0 && d1 >= 0 && d3 <= 0) {
-    const double t = d1 / (d1 - d3);
-    keep[0] = keep[1] = true;
-    return V3{a.x + t * ab.x, a.y + t * ab.y, a.z + t * ab.z};
-  }
-  const double d5 = -d3dot(ab, c), d6 = -d3dot(ac, c);
-  if (d6 >= 0 && d5 <= d6) {
-    keep[2] = true;
-    return c;
-  }
-  const double vb = d5 * d2 - d1 * d6;
-  if (vb <= 0 && d2 >= 0 && d6 <= 0) {
-    const double t = d2 / (d2 - d6);
-    keep[0] = keep[2] = true;
-    return V3{a.x + t * ac.x, a.y + t * ac.y, a.z + t * ac.z};
-  }
-  const double va = d3 * d6 - d5 * d4;
-  if (va <= 0 && (d4 - d3) >= 0 && (d5 - d6) >= 0) {
-    const double t = (d4 - d3) / ((d4 - d3) + (d5 - d6));
-    const V3 bc = vsub(c, b);
-    keep[1] = keep[2] = true;
-    return V3{b.x + t * bc.x, b.y + t * bc.y, b.z + t * bc.z};
-  }
-  const double den = 1.0 / (va + vb + vc), t1 = vb * den, t2 = vc * den;
-  keep[0] = keep[1] = keep[2] = true;
-  return V3{a.x + ab.x * t1 + ac.x * t2, a.y + ab.y * t1 + ac.y * t2, a.z + ab.z * t1 + ac.z * t2};
-}
-
-// simplex P[0..n) -> closest point, reduced simplex; true if it encloses the origin
-__device__ __forceinline__ bool simplex_closest(V3 P[4], int& n, V3& v) {
-  if (n == 1) {
-    v = P[0];
-    return false;
-  }
-  if (n == 2) {
-    const V3 ab = vsub(P[1], P[0]);
-    const double den = d3dot(ab, ab), t = den > 0 ? -d3dot(P[0], ab) / den : 0.0;
-    if (t <= 0) {
-      v = P[0];
-      n = 1;
-    } else if (t >= 1) {
-      v = P[1];
-      P[0] = P[1];
-      n = 1;
-    } else {
-      v = V3{P[0].x + t * ab.x, P[0].y + t * ab.y, P[0].z + t * ab.z};
-    }
-    return false;
-  }
-  if (n == 3) {
-    bool keep[3];
-    v = tri_closest(P[0], P[1], P[2], keep);
-    int m = 0;
-    for (int k = 0; k < 3; ++k)
-      if (keep[k]) P[m++] = P[k];
-    n = m;
-    return false;
-  }
-  const int F[4][4] = {{0, 1, 2, 3}, {0, 2, 3, 1}, {0, 3, 1, 2}, {1, 3, 2, 0}};
-  double best = DBL_MAX;
-  V3 bv{0, 0, 0}, BP[3];
-  int bn = 0;
-  bool any = false;
-  for (int f = 0; f < 4; ++f) {
-    const V3 a = P[F[f][0]], b = P[F[f][1]], c = P[F[f][2]], d = P[F[f][3]];
-    const V3 nrm = vcross(vsub(b, a), vsub(c, a));
-    const double sp = -d3dot(a, nrm), sd = d3dot(vsub(d, a), nrm);
-    if (!(sp * sd < 0 || sd == 0.0)) continue;
-    any = true;
-    bool keep[3];
-    const V3 fv = tri_closest(a, b, c, keep);
-    const double dd = d3dot(fv, fv);
-    if (dd < best) {
-      best = dd;
-      bv = fv;
-      bn = 0;
-      const V3 abc[3] = {a, b, c};
-      for (int k = 0; k < 3; ++k)
-        if (keep[k]) BP[bn++] = abc[k];
-    }
-  }
-  if (!any) return true;
-  for (int k = 0; k < bn; ++k) P[k] = BP[k];
-  n = bn;
-  v = bv;
-  return false;
-}
-
-// GJK distance from v = centre(A) - centre(B) over the support map sup(dir)
-// of A - B (the oracle's gjk_distance)
-template <typename Sup>
-__device__ double gjk_distance_from(V3 v, Sup sup) {
-  if (d3dot(v, v) == 0.0) v.x = 1e-12;
-  V3 P[4];
-  int n = 0;
-  for (int it = 0; it < 128; ++it) {
-    const V3 wv = to_v3(sup(cv3(-v.x, -v.y, -v.z)));
-    const double vv = d3dot(v, v), vw = d3dot(v, wv);
-    if (n > 0 && vv - vw <= 1e-12 * vv) break;
-    bool dup = false;
-    for (int k = 0; k < n; ++k) dup |= (P[k].x == wv.x && P[k].y == wv.y && P[k].z == wv.z);
-    if (dup) break;
-    P[n++] = wv;
-    if (simplex_closest(P, n, v)) return -1.0;
-    const double nv = d3dot(v, v);
-    if (nv <= 1e-24) return -1.0;
-    if (n > 1 && nv >= vv) break;
-  }
-  return std::sqrt(d3dot(v, v));
-}
-
-__device__ double gjk_distance(const DevWorld& w, cptr<double> HV, const GObj& A, const GObj& B) {
-  return gjk_distance_from(vsub(to_v3(center(w, A)), to_v3(center(w, B))),
-                           [&](const CV3& d) { return msupport(w, HV, A, B, d); });
-}
-
 // ---------------------------------------------------------------------------
-// Nearest points and signed distance (DistanceRequest enable_signed_distance;
-// FCL 0.7.0 ShapeDistanceTraversalNode::leafTesting -> GJKSolver_libccd
-// shapeDistance / shapeSignedDistance [ext]): gjk_query runs gjk_distance's
-// iteration with each simplex vertex's two supports and barycentric weights
-// (extractClosestPoints: world-frame points on each shape); for intersecting
-// shapes in signed mode, EPA from GJK's enclosing tetrahedron (blow_up first
-// when the origin lies on a lower simplex), depth = distance from the origin
-// to the nearest polytope face, points from its barycentric weights
-// (penEPAPosClosest).  Operation for operation the oracle's gjk_query /
-// blow_up / epa_depth (oracle/collide_oracle.c), same capacities.
+// FCL 0.7.0 shape distance: GJKDistance / GJKSignedDistance on float libccd
+// (mpg_ccd_dist.h, the twin of oracle/fcl_gjk_dist.h), the closed forms of
+// GJKSolver_libccd::shapeDistance, and the support mappings they run on.
 // ---------------------------------------------------------------------------
-struct GSV {
-  V3 w, a, b;
-};
+#include "mpg_ccd_dist.h"
 
-template <bool UNI = true>
-__device__ __forceinline__ GSV msupport_pts(const DevWorld& w, cptr<double> HV, const GObj& A, const GObj& B,
-                                            const V3& d) {
-  const CV3 dir = cv3(d.x, d.y, d.z);
-  // the same operations as msupport: v = (R_a la + p_a) - (R_b lb + p_b) in ccd_real
-  const CV3 da = quat_rot(dir, A.rot_inv), db = quat_rot(vscale(dir, ccd_real(-1)), B.rot_inv);
-  const int ga = UNI ? __builtin_amdgcn_readfirstlane(A.geom) : A.geom, ta = UNI ? __builtin_amdgcn_readfirstlane(A.type) : A.type;
-  const int gb = UNI ? __builtin_amdgcn_readfirstlane(B.geom) : B.geom, tb = UNI ? __builtin_amdgcn_readfirstlane(B.type) : B.type;
+// __ccdSupport of (uniform shape a) - (uniform shape b), both points kept
+__device__ __forceinline__ ccdx::Sup csup(const DevWorld& w, cptr<double> HV, const GObj& a, const GObj& b,
+                                         const CV3& dir) {
+  const CV3 da = quat_rot(dir, a.rot_inv), db = quat_rot(vscale(dir, ccd_real(-1)), b.rot_inv);
+  const int ga = __builtin_amdgcn_readfirstlane(a.geom), ta = __builtin_amdgcn_readfirstlane(a.type);
+  const int gb = __builtin_amdgcn_readfirstlane(b.geom), tb = __builtin_amdgcn_readfirstlane(b.type);
   const CV3 la = support_local(w, HV, ga, ta, da), lb = support_local(w, HV, gb, tb, db);
-  const CV3 va = vadd(quat_rot(la, A.rot), A.pos), vb = vadd(quat_rot(lb, B.rot), B.pos);
-  GSV g;
-  g.w = to_v3(vsub(va, vb));
-  g.a = to_v3(va);
-  g.b = to_v3(vb);
-  return g;
+  ccdx::Sup s;
+  s.v1 = vadd(quat_rot(la, a.rot), a.pos);
+  s.v2 = vadd(quat_rot(lb, b.rot), b.pos);
+  s.v = vsub(s.v1, s.v2);
+  return s;
 }
 
-__device__ __forceinline__ void tri_lambda(const V3& a, const V3& b, const V3& c, double lam[3]) {
-  const V3 ab = vsub(b, a), ac = vsub(c, a);
-  lam[0] = lam[1] = lam[2] = 0.0;
-  const double d1 = -d3dot(ab, a), d2 = -d3dot(ac, a);
-  if (d1 <= 0 && d2 <= 0) {
-    lam[0] = 1.0;
-    return;
-  }
-  const double d3 = -d3dot(ab, b), d4 = -d3dot(ac, b);
-  if (d3 >= 0 && d4 <= d3) {
-    lam[1] = 1.0;
-    return;
-  }
-  const double vc = d1 * d4 - d3 * d2;
-  if (vc <= 0 && d1 >= 0 && d3 <= 0) {
-    const double t = d1 / (d1 - d3);
-    lam[0] = 1.0 - t;
-    lam[1] = t;
-    return;
-  }
-  const double d5 = -d3dot(ab, c), d6 = -d3dot(ac, c);
-  if (d6 >= 0 && d5 <= d6) {
-    lam[2] = 1.0;
-    return;
-  }
-  const double vb = d5 * d2 - d1 * d6;
-  if (vb <= 0 && d2 >= 0 && d6 <= 0) {
-    const double t = d2 / (d2 - d6);
-    lam[0] = 1.0 - t;
-    lam[2] = t;
-    return;
-  }
-  const double va = d3 * d6 - d5 * d4;
-  if (va <= 0 && (d4 - d3) >= 0 && (d5 - d6) >= 0) {
-    const double t = (d4 - d3) / ((d4 - d3) + (d5 - d6));
-    lam[1] = 1.0 - t;
-    lam[2] = t;
-    return;
-  }
-  const double den = 1.0 / (va + vb + vc), t1 = vb * den, t2 = vc * den;
-  lam[0] = 1.0 - t1 - t2;
-  lam[1] = t1;
-  lam[2] = t2;
+// boxToGJK support with per-lane half sizes h (an octree leaf box)
+__device__ __forceinline__ CV3 box_support_world(const GObj& a, const ccd_real* h, const CV3& dir) {
+  const CV3 da = quat_rot(dir, a.rot_inv);
+  const CV3 la = CV3{(da.x >= 0 ? ccd_real(1) : ccd_real(-1)) * h[0], (da.y >= 0 ? ccd_real(1) : ccd_real(-1)) * h[1],
+                     (da.z >= 0 ? ccd_real(1) : ccd_real(-1)) * h[2]};
+  return vadd(quat_rot(la, a.rot), a.pos);
 }
 
-// simplex_closest with the supports and the kept vertices' weights
-__device__ __forceinline__ bool simplex_closest_s(GSV S[4], int& n, V3& v, double lam[4]) {
-  if (n == 1) {
-    v = S[0].w;
-    lam[0] = 1.0;
-    return false;
+// (leaf box a) - (uniform shape b)
+__device__ __forceinline__ ccdx::Sup csup_box(const GObj& a, const ccd_real* h, const DevWorld& w, cptr<double> HV,
+                                              const GObj& b, const CV3& dir) {
+  ccdx::Sup s;
+  s.v1 = box_support_world(a, h, dir);
+  const CV3 db = quat_rot(vscale(dir, ccd_real(-1)), b.rot_inv);
+  const int gb = __builtin_amdgcn_readfirstlane(b.geom), tb = __builtin_amdgcn_readfirstlane(b.type);
+  s.v2 = vadd(quat_rot(support_local(w, HV, gb, tb, db), b.rot), b.pos);
+  s.v = vsub(s.v1, s.v2);
+  return s;
+}
+
+__device__ __forceinline__ CV3 tri_support(const GObj& b, const CV3* P, const CV3& tc, const CV3& dir);
+
+// (uniform shape a) - (triangle b: vertices P and centroid tc in the mesh frame)
+__device__ __forceinline__ ccdx::Sup csup_tri(const DevWorld& w, cptr<double> HV, const GObj& a, const GObj& b,
+                                              const CV3* P, const CV3& tc, const CV3& dir) {
+  ccdx::Sup s;
+  const CV3 da = quat_rot(dir, a.rot_inv);
+  const int ga = __builtin_amdgcn_readfirstlane(a.geom), ta = __builtin_amdgcn_readfirstlane(a.type);
+  s.v1 = vadd(quat_rot(support_local(w, HV, ga, ta, da), a.rot), a.pos);
+  s.v2 = tri_support(b, P, tc, vscale(dir, ccd_real(-1)));
+  s.v = vsub(s.v1, s.v2);
+  return s;
+}
+
+// (leaf box a) - (triangle b)
+__device__ __forceinline__ ccdx::Sup csup_box_tri(const GObj& a, const ccd_real* h, const GObj& b, const CV3* P,
+                                                  const CV3& tc, const CV3& dir) {
+  ccdx::Sup s;
+  s.v1 = box_support_world(a, h, dir);
+  s.v2 = tri_support(b, P, tc, vscale(dir, ccd_real(-1)));
+  s.v = vsub(s.v1, s.v2);
+  return s;
+}
+
+// ccdx status -> the pair-index sentinel the distance outputs carry
+constexpr int kDistThrow = MPG_DISTANCE_FCL_THROWS, kDistOverflow = MPG_DISTANCE_EPA_CAPACITY;
+
+// ---- closed-form shape distances (GJKSolver_libccd::shapeDistance's
+// specialisations [ext FCL 0.7.0]; oracle/fcl_gjk_dist.h cf_*, same order)
+__device__ __forceinline__ void cf_tf_point(const SE3& T, const double* p, double* o) {
+#pragma unroll
+  for (int i = 0; i < 3; ++i) o[i] = ((T.R[3 * i] * p[0] + T.R[3 * i + 1] * p[1]) + T.R[3 * i + 2] * p[2]) + T.p[i];
+}
+__device__ __forceinline__ double cf_norm(const double* v) { return std::sqrt((v[0] * v[0] + v[1] * v[1]) + v[2] * v[2]); }
+// X_FO.inverse() * X_FS: the sphere centre in the other shape's frame
+__device__ __forceinline__ void cf_centre_in_frame(const SE3& TS, const SE3& TO, double* c) {
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const double inv_t = -((TO.R[i] * TO.p[0] + TO.R[3 + i] * TO.p[1]) + TO.R[6 + i] * TO.p[2]);
+    c[i] = ((TO.R[i] * TS.p[0] + TO.R[3 + i] * TS.p[1]) + TO.R[6 + i] * TS.p[2]) + inv_t;
   }
-  if (n == 2) {
-    const V3 ab = vsub(S[1].w, S[0].w);
-    const double den = d3dot(ab, ab), t = den > 0 ? -d3dot(S[0].w, ab) / den : 0.0;
-    if (t <= 0) {
-      v = S[0].w;
-      n = 1;
-      lam[0] = 1.0;
-    } else if (t >= 1) {
-      v = S[1].w;
-      S[0] = S[1];
-      n = 1;
-      lam[0] = 1.0;
+}
+
+__device__ double cf_sphere_sphere(double r1, const SE3& T1, double r2, const SE3& T2, double* p1, double* p2) {
+  const double diff[3] = {T1.p[0] - T2.p[0], T1.p[1] - T2.p[1], T1.p[2] - T2.p[2]};
+  const double len = cf_norm(diff);
+  if (len > r1 + r2) {
+    for (int i = 0; i < 3; ++i) {
+      p1[i] = T1.p[i] - diff[i] * (r1 / len);
+      p2[i] = T2.p[i] + diff[i] * (r2 / len);
+    }
+    return len - (r1 + r2);
+  }
+  return -1.0;
+}
+
+__device__ double cf_sphere_capsule(double r1, const SE3& TS, double r2, double lz, const SE3& TC, double* p1,
+                                    double* p2) {
+  const double a[3] = {0.0, 0.0, 0.5 * lz}, b[3] = {0.0, 0.0, -0.5 * lz};
+  double pos1[3], pos2[3], sp[3];
+  cf_tf_point(TC, a, pos1);
+  cf_tf_point(TC, b, pos2);
+  const double* sc = TS.p;
+  const double v[3] = {pos2[0] - pos1[0], pos2[1] - pos1[1], pos2[2] - pos1[2]};
+  const double wv[3] = {sc[0] - pos1[0], sc[1] - pos1[1], sc[2] - pos1[2]};
+  const double c1 = (wv[0] * v[0] + wv[1] * v[1]) + wv[2] * v[2];
+  const double c2 = (v[0] * v[0] + v[1] * v[1]) + v[2] * v[2];
+  if (c1 <= 0) {
+    for (int i = 0; i < 3; ++i) sp[i] = pos1[i];
+  } else if (c2 <= c1) {
+    for (int i = 0; i < 3; ++i) sp[i] = pos2[i];
+  } else {
+    const double bb = c1 / c2;
+    for (int i = 0; i < 3; ++i) sp[i] = pos1[i] + v[i] * bb;
+  }
+  double diff[3] = {sc[0] - sp[0], sc[1] - sp[1], sc[2] - sp[2]};
+  const double distance = cf_norm(diff) - r1 - r2;
+  if (distance <= 0) return -1.0;
+  const double n = cf_norm(diff);
+  for (int i = 0; i < 3; ++i) diff[i] /= n;
+  for (int i = 0; i < 3; ++i) {
+    p1[i] = sc[i] - diff[i] * r1;
+    p2[i] = sp[i] + diff[i] * r2;
+  }
+  return distance;
+}
+
+__device__ double cf_sphere_box(double r, const SE3& TS, const double* side, const SE3& TB, double* pS, double* pB) {
+  double c[3], nq[3];
+  cf_centre_in_frame(TS, TB, c);
+  bool clamped = false;
+  for (int i = 0; i < 3; ++i) {
+    const double h = side[i] / 2;
+    nq[i] = c[i];
+    if (c[i] < -h) {
+      clamped = true;
+      nq[i] = -h;
+    }
+    if (c[i] > h) {
+      clamped = true;
+      nq[i] = h;
+    }
+  }
+  if (clamped) {
+    const double nc[3] = {c[0] - nq[0], c[1] - nq[1], c[2] - nq[2]};
+    const double sq = (nc[0] * nc[0] + nc[1] * nc[1]) + nc[2] * nc[2];
+    if (sq > r * r) {
+      const double d = std::sqrt(sq);
+      double pSb[3];
+      for (int i = 0; i < 3; ++i) pSb[i] = (nc[i] / d) * (d - r) + nq[i];
+      cf_tf_point(TB, nq, pB);
+      cf_tf_point(TB, pSb, pS);
+      return d - r;
+    }
+  }
+  return -1.0;
+}
+
+__device__ double cf_sphere_cylinder(double r, const SE3& TS, double rc, double lz, const SE3& TC, double* pS,
+                                     double* pC) {
+  double c[3], n[3];
+  cf_centre_in_frame(TS, TC, c);
+  const double h = lz / 2;
+  bool clamped = false;
+  n[0] = c[0];
+  n[1] = c[1];
+  n[2] = c[2];
+  if (c[2] > h) {
+    n[2] = h;
+    clamped = true;
+  } else if (c[2] < -h) {
+    n[2] = -h;
+    clamped = true;
+  }
+  const double rd2 = c[0] * c[0] + c[1] * c[1];
+  if (rd2 > rc * rc) {
+    const double scale = rc / std::sqrt(rd2);
+    n[0] = c[0] * scale;
+    n[1] = c[1] * scale;
+    clamped = true;
+  }
+  if (clamped) {
+    const double nc[3] = {c[0] - n[0], c[1] - n[1], c[2] - n[2]};
+    const double sq = (nc[0] * nc[0] + nc[1] * nc[1]) + nc[2] * nc[2];
+    if (sq > r * r) {
+      const double d = std::sqrt(sq);
+      double pSc[3];
+      for (int i = 0; i < 3; ++i) pSc[i] = (nc[i] / d) * (d - r) + n[i];
+      cf_tf_point(TC, n, pC);
+      cf_tf_point(TC, pSc, pS);
+      return d - r;
+    }
+  }
+  return -1.0;
+}
+
+__device__ __forceinline__ double cf_clamp01(double v) { return v < 0.0 ? 0.0 : (v > 1.0 ? 1.0 : v); }
+
+__device__ double cf_capsule_capsule(double r1, double lz1, const SE3& T1, double r2, double lz2, const SE3& T2,
+                                     double* p1, double* p2) {
+  const double eps = 0x1.6a09e667f3bcdp-46, eps2 = eps * eps;  // constants<double>::eps_78() = pow(DBL_EPSILON, 7/8)
+  double P1[3], Q1[3], P2[3], Q2[3];
+  for (int i = 0; i < 3; ++i) {
+    const double h1 = (lz1 / 2) * T1.R[3 * i + 2], h2 = (lz2 / 2) * T2.R[3 * i + 2];
+    P1[i] = T1.p[i] + h1;
+    Q1[i] = T1.p[i] - h1;
+    P2[i] = T2.p[i] + h2;
+    Q2[i] = T2.p[i] - h2;
+  }
+  double d1[3], d2[3], rr[3];
+  for (int i = 0; i < 3; ++i) {
+    d1[i] = Q1[i] - P1[i];
+    d2[i] = Q2[i] - P2[i];
+    rr[i] = P1[i] - P2[i];
+  }
+  const double a = (d1[0] * d1[0] + d1[1] * d1[1]) + d1[2] * d1[2];
+  const double e = (d2[0] * d2[0] + d2[1] * d2[1]) + d2[2] * d2[2];
+  const double f = (d2[0] * rr[0] + d2[1] * rr[1]) + d2[2] * rr[2];
+  double s, t;
+  if (a <= eps2 && e <= eps2) {
+    s = t = 0.0;
+  } else if (a <= eps2) {
+    s = 0.0;
+    t = cf_clamp01(f / e);
+  } else {
+    const double c = (d1[0] * rr[0] + d1[1] * rr[1]) + d1[2] * rr[2];
+    if (e <= eps2) {
+      t = 0.0;
+      s = cf_clamp01(-c / a);
     } else {
-      v = V3{S[0].w.x + t * ab.x, S[0].w.y + t * ab.y, S[0].w.z + t * ab.z};
-      lam[0] = 1.0 - t;
-      lam[1] = t;
-    }
-    return false;
-  }
-  if (n == 3) {
-    bool keep[3];
-    double l3[3];
-    v = tri_closest(S[0].w, S[1].w, S[2].w, keep);
-    tri_lambda(S[0].w, S[1].w, S[2].w, l3);
-    int m = 0;
-    for (int k = 0; k < 3; ++k)
-      if (keep[k]) {
-        S[m] = S[k];
-        lam[m] = l3[k];
-        ++m;
+      const double b = (d1[0] * d2[0] + d1[1] * d2[1]) + d1[2] * d2[2];
+      const double den0 = a * e - b * b, denom = den0 > 0.0 ? den0 : 0.0;
+      s = denom > eps2 ? cf_clamp01((b * f - c * e) / denom) : 0.0;
+      t = (b * s + f) / e;
+      if (t < 0.0) {
+        t = 0.0;
+        s = cf_clamp01(-c / a);
+      } else if (t > 1.0) {
+        t = 1.0;
+        s = cf_clamp01((b - c) / a);
       }
-    n = m;
-    return false;
-  }
-  const int F[4][4] = {{0, 1, 2, 3}, {0, 2, 3, 1}, {0, 3, 1, 2}, {1, 3, 2, 0}};
-  double best = DBL_MAX, bl[3] = {0, 0, 0};
-  V3 bv{0, 0, 0};
-  GSV BP[3];
-  int bn = 0;
-  bool any = false;
-  for (int f = 0; f < 4; ++f) {
-    const V3 a = S[F[f][0]].w, b = S[F[f][1]].w, c = S[F[f][2]].w, d = S[F[f][3]].w;
-    const V3 nrm = vcross(vsub(b, a), vsub(c, a));
-    const double sp = -d3dot(a, nrm), sd = d3dot(vsub(d, a), nrm);
-    if (!(sp * sd < 0 || sd == 0.0)) continue;
-    any = true;
-    bool keep[3];
-    double l3[3];
-    const V3 fv = tri_closest(a, b, c, keep);
-    const double dd = d3dot(fv, fv);
-    if (dd < best) {
-      tri_lambda(a, b, c, l3);
-      best = dd;
-      bv = fv;
-      bn = 0;
-      for (int k = 0; k < 3; ++k)
-        if (keep[k]) {
-          BP[bn] = S[F[f][k]];
-          bl[bn] = l3[k];
-          ++bn;
-        }
     }
   }
-  if (!any) return true;
-  for (int k = 0; k < bn; ++k) {
-    S[k] = BP[k];
-    lam[k] = bl[k];
+  double N1[3], N2[3], v[3];
+  for (int i = 0; i < 3; ++i) {
+    N1[i] = P1[i] + d1[i] * s;
+    N2[i] = P2[i] + d2[i] * t;
+    v[i] = N2[i] - N1[i];
   }
-  n = bn;
-  v = bv;
-  return false;
+  const double seg = std::sqrt((v[0] * v[0] + v[1] * v[1]) + v[2] * v[2]);
+  double vh[3];
+  if (seg > eps) {
+    for (int i = 0; i < 3; ++i) vh[i] = v[i] / seg;
+  } else {
+    double n[3] = {d1[1] * d2[2] - d1[2] * d2[1], d1[2] * d2[0] - d1[0] * d2[2], d1[0] * d2[1] - d1[1] * d2[0]};
+    double nl = cf_norm(n);
+    if (!(nl > eps)) {
+      const double ax[3] = {std::fabs(d1[0]) < std::fabs(d1[1]) ? 1.0 : 0.0,
+                            std::fabs(d1[0]) < std::fabs(d1[1]) ? 0.0 : 1.0, 0.0};
+      n[0] = d1[1] * ax[2] - d1[2] * ax[1];
+      n[1] = d1[2] * ax[0] - d1[0] * ax[2];
+      n[2] = d1[0] * ax[1] - d1[1] * ax[0];
+      nl = cf_norm(n);
+    }
+    for (int i = 0; i < 3; ++i) vh[i] = nl > 0.0 ? n[i] / nl : (i == 2 ? 1.0 : 0.0);
+  }
+  for (int i = 0; i < 3; ++i) {
+    p1[i] = N1[i] + vh[i] * r1;
+    p2[i] = N2[i] - vh[i] * r2;
+  }
+  return seg - r1 - r2;
 }
 
-constexpr int kEpaMaxV = 64, kEpaMaxF = 128;
-struct EpaFace {
-  int v[3];
-  V3 n;
-  double d;
-  int alive;
+// 1 if (ta, tb) has a closed form; d and the points (zeros for -1)
+__device__ bool cf_shape_distance(const DevWorld& w, int ga, int ta, const SE3& Ta, int gb, int tb, const SE3& Tb,
+                                  double& d, V3& q1, V3& q2) {
+  const cptr<double> pa = w.geom_rec + G_STRIDE * ga + G_PARAM, pb = w.geom_rec + G_STRIDE * gb + G_PARAM;
+  double p1[3] = {0, 0, 0}, p2[3] = {0, 0, 0};
+  if (ta == MPG_GEOM_SPHERE && tb == MPG_GEOM_SPHERE) {
+    d = cf_sphere_sphere(pa[0], Ta, pb[0], Tb, p1, p2);
+  } else if (ta == MPG_GEOM_SPHERE && tb == MPG_GEOM_CAPSULE) {
+    d = cf_sphere_capsule(pa[0], Ta, pb[0], pb[1], Tb, p1, p2);
+  } else if (ta == MPG_GEOM_CAPSULE && tb == MPG_GEOM_SPHERE) {
+    d = cf_sphere_capsule(pb[0], Tb, pa[0], pa[1], Ta, p2, p1);
+  } else if (ta == MPG_GEOM_SPHERE && tb == MPG_GEOM_BOX) {
+    const double side[3] = {pb[0], pb[1], pb[2]};
+    d = cf_sphere_box(pa[0], Ta, side, Tb, p1, p2);
+  } else if (ta == MPG_GEOM_BOX && tb == MPG_GEOM_SPHERE) {
+    const double side[3] = {pa[0], pa[1], pa[2]};
+    d = cf_sphere_box(pb[0], Tb, side, Ta, p2, p1);
+  } else if (ta == MPG_GEOM_SPHERE && tb == MPG_GEOM_CYLINDER) {
+    d = cf_sphere_cylinder(pa[0], Ta, pb[0], pb[1], Tb, p1, p2);
+  } else if (ta == MPG_GEOM_CYLINDER && tb == MPG_GEOM_SPHERE) {
+    d = cf_sphere_cylinder(pb[0], Tb, pa[0], pa[1], Ta, p2, p1);
+  } else if (ta == MPG_GEOM_CAPSULE && tb == MPG_GEOM_CAPSULE) {
+    d = cf_capsule_capsule(pa[0], pa[1], Ta, pb[0], pb[1], Tb, p1, p2);
+  } else {
+    return false;
+  }
+  if (d == -1.0) p1[0] = p1[1] = p1[2] = p2[0] = p2[1] = p2[2] = 0.0;
+  q1 = V3{p1[0], p1[1], p1[2]};
+  q2 = V3{p2[0], p2[1], p2[2]};
+  return true;
+}
+
+// Project<S>::projectLine / projectTriangle and sphereTriangleDistance with
+// points (oracle cf_project_line / cf_project_triangle / cf_sphere_triangle)
+struct CfProj {
+  double param[4], sqr_distance;
 };
-
-__device__ __forceinline__ bool epa_face_set(const GSV* V, int i, int j, int k, EpaFace& f) {
-  const V3 n = vcross(vsub(V[j].w, V[i].w), vsub(V[k].w, V[i].w));
-  const double l = std::sqrt(d3dot(n, n));
-  if (!(l > 0.0)) return false;
-  f.n = V3{n.x / l, n.y / l, n.z / l};
-  f.v[0] = i;
-  f.v[1] = j;
-  f.v[2] = k;
-  f.d = d3dot(f.n, V[i].w);
-  f.alive = 1;
-  return true;
-}
-
-__device__ __forceinline__ double epa_finish(const GSV* V, const EpaFace& f, V3& p1, V3& p2) {
-  const V3 a = V[f.v[0]].w, b = V[f.v[1]].w, c = V[f.v[2]].w;
-  const V3 pw{f.d * f.n.x, f.d * f.n.y, f.d * f.n.z};
-  const V3 v0 = vsub(b, a), v1 = vsub(c, a), v2 = vsub(pw, a);
-  const double d00 = d3dot(v0, v0), d01 = d3dot(v0, v1), d11 = d3dot(v1, v1), d20 = d3dot(v2, v0), d21 = d3dot(v2, v1);
-  const double den = d00 * d11 - d01 * d01;
-  const double lb = den != 0.0 ? (d11 * d20 - d01 * d21) / den : 0.0, lc = den != 0.0 ? (d00 * d21 - d01 * d20) / den : 0.0;
-  const double la = 1.0 - lb - lc;
-  const GSV &A = V[f.v[0]], &B = V[f.v[1]], &C = V[f.v[2]];
-  p1 = V3{(la * A.a.x + lb * B.a.x) + lc * C.a.x, (la * A.a.y + lb * B.a.y) + lc * C.a.y, (la * A.a.z + lb * B.a.z) + lc * C.a.z};
-  p2 = V3{(la * A.b.x + lb * B.b.x) + lc * C.b.x, (la * A.b.y + lb * B.b.y) + lc * C.b.y, (la * A.b.z + lb * B.b.z) + lc * C.b.z};
-  return f.d;
-}
-
-template <typename SupFn>
-__device__ double epa_depth(SupFn sup, const GSV S[4], V3& p1, V3& p2) {
-  GSV V[kEpaMaxV];
-  EpaFace F[kEpaMaxF];
-  int nv = 4, nf = 0;
-  for (int k = 0; k < 4; ++k) V[k] = S[k];
-  const int T[4][4] = {{0, 1, 2, 3}, {0, 3, 1, 2}, {0, 2, 3, 1}, {1, 3, 2, 0}};
-  for (int t = 0; t < 4; ++t) {
-    int i = T[t][0], j = T[t][1], k = T[t][2];
-    const int l = T[t][3];
-    const V3 n = vcross(vsub(V[j].w, V[i].w), vsub(V[k].w, V[i].w));
-    if (d3dot(n, vsub(V[l].w, V[i].w)) > 0.0) {
-      const int x = j;
-      j = k;
-      k = x;
+__device__ CfProj cf_project_line(const double* a, const double* b, const double* p) {
+  CfProj r = {{0, 0, 0, 0}, -1.0};
+  const double d[3] = {b[0] - a[0], b[1] - a[1], b[2] - a[2]};
+  const double l = (d[0] * d[0] + d[1] * d[1]) + d[2] * d[2];
+  if (l > 0) {
+    const double pa[3] = {p[0] - a[0], p[1] - a[1], p[2] - a[2]};
+    const double t = (pa[0] * d[0] + pa[1] * d[1]) + pa[2] * d[2];
+    r.param[1] = (t >= l) ? 1 : ((t <= 0) ? 0 : (t / l));
+    r.param[0] = 1 - r.param[1];
+    double v[3];
+    if (t >= l) {
+      for (int i = 0; i < 3; ++i) v[i] = p[i] - b[i];
+    } else if (t <= 0) {
+      for (int i = 0; i < 3; ++i) v[i] = p[i] - a[i];
+    } else {
+      for (int i = 0; i < 3; ++i) v[i] = (a[i] + d[i] * r.param[1]) - p[i];
     }
-    if (!epa_face_set(V, i, j, k, F[nf])) return -1.0;
-    ++nf;
+    r.sqr_distance = (v[0] * v[0] + v[1] * v[1]) + v[2] * v[2];
   }
-  EpaFace fb;
-  for (int it = 0; it < 128; ++it) {
-    int best = -1;
-    for (int f = 0; f < nf; ++f)
-      if (F[f].alive && (best < 0 || F[f].d < F[best].d)) best = f;
-    if (best < 0) return -1.0;
-    fb = F[best];
-    const GSV s = sup(fb.n);
-    if (d3dot(s.w, fb.n) - fb.d <= 1e-10 || nv >= kEpaMaxV) break;
-    bool dup = false;
-    for (int k = 0; k < nv; ++k) dup |= (V[k].w.x == s.w.x && V[k].w.y == s.w.y && V[k].w.z == s.w.z);
-    if (dup) break;
-    const int si = nv;
-    V[nv++] = s;
-    int edges[kEpaMaxF][2], ne = 0;
-    for (int f = 0; f < nf; ++f) {
-      if (!F[f].alive) continue;
-      if (d3dot(F[f].n, vsub(s.w, V[F[f].v[0]].w)) <= 0.0) continue;
-      F[f].alive = 0;
-      for (int e = 0; e < 3; ++e) {
-        const int a = F[f].v[e], b = F[f].v[(e + 1) % 3];
-        int found = -1;
-        for (int x = 0; x < ne; ++x)
-          if (edges[x][0] == b && edges[x][1] == a) {
-            found = x;
-            break;
-          }
-        if (found >= 0) {
-          edges[found][0] = edges[ne - 1][0];
-          edges[found][1] = edges[ne - 1][1];
-          --ne;
-        } else if (ne < kEpaMaxF) {
-          edges[ne][0] = a;
-          edges[ne][1] = b;
-          ++ne;
-        } else {
-          return epa_finish(V, fb, p1, p2);
+  return r;
+}
+__device__ __forceinline__ void cf_cross(double* o, const double* a, const double* b) {
+  o[0] = a[1] * b[2] - a[2] * b[1];
+  o[1] = a[2] * b[0] - a[0] * b[2];
+  o[2] = a[0] * b[1] - a[1] * b[0];
+}
+__device__ CfProj cf_project_triangle(const double* a, const double* b, const double* c, const double* p) {
+  CfProj r = {{0, 0, 0, 0}, -1.0};
+  const double* vt[3] = {a, b, c};
+  double dl[3][3], n[3];
+  for (int i = 0; i < 3; ++i) {
+    dl[0][i] = a[i] - b[i];
+    dl[1][i] = b[i] - c[i];
+    dl[2][i] = c[i] - a[i];
+  }
+  cf_cross(n, dl[0], dl[1]);
+  const double l = (n[0] * n[0] + n[1] * n[1]) + n[2] * n[2];
+  if (l > 0) {
+    double mindist = -1;
+    for (int i = 0; i < 3; ++i) {
+      double vp[3], dn[3];
+      for (int k = 0; k < 3; ++k) vp[k] = vt[i][k] - p[k];
+      cf_cross(dn, dl[i], n);
+      if ((vp[0] * dn[0] + vp[1] * dn[1]) + vp[2] * dn[2] > 0) {
+        const int j = i == 2 ? 0 : i + 1;
+        const CfProj rl = cf_project_line(vt[i], vt[j], p);
+        if (mindist < 0 || rl.sqr_distance < mindist) {
+          mindist = rl.sqr_distance;
+          r.param[i] = rl.param[0];
+          r.param[j] = rl.param[1];
+          r.param[j == 2 ? 0 : j + 1] = 0;
         }
       }
     }
-    int slot = 0;
-    bool full = false;
-    for (int x = 0; x < ne && !full; ++x) {
-      while (slot < nf && F[slot].alive) ++slot;
-      if (slot == nf) {
-        if (nf == kEpaMaxF) {
-          full = true;
-          break;
-        }
-        ++nf;
-      }
-      if (!epa_face_set(V, edges[x][0], edges[x][1], si, F[slot])) F[slot].alive = 0;
+    if (mindist < 0) {
+      const double ap[3] = {a[0] - p[0], a[1] - p[1], a[2] - p[2]};
+      const double d = (ap[0] * n[0] + ap[1] * n[1]) + ap[2] * n[2];
+      const double s = std::sqrt(l);
+      double pp[3], t1[3], t2[3], x[3];
+      for (int k = 0; k < 3; ++k) pp[k] = n[k] * (d / l);
+      mindist = (pp[0] * pp[0] + pp[1] * pp[1]) + pp[2] * pp[2];
+      for (int k = 0; k < 3; ++k) t1[k] = (b[k] - p[k]) - pp[k];
+      cf_cross(x, dl[1], t1);
+      r.param[0] = cf_norm(x) / s;
+      for (int k = 0; k < 3; ++k) t2[k] = (c[k] - p[k]) - pp[k];
+      cf_cross(x, dl[2], t2);
+      r.param[1] = cf_norm(x) / s;
+      r.param[2] = 1 - r.param[0] - r.param[1];
     }
-    if (full) return epa_finish(V, fb, p1, p2);
+    r.sqr_distance = mindist;
   }
-  return epa_finish(V, fb, p1, p2);
+  return r;
+}
+// W: the triangle's world vertices [3][3]
+__device__ double cf_sphere_triangle(double radius, const double* o, const double* W, double* pS, double* pT) {
+  const CfProj r = cf_project_triangle(W, W + 3, W + 6, o);
+  if (r.sqr_distance > radius * radius) {
+    double pp[3], dir[3];
+    for (int k = 0; k < 3; ++k) pp[k] = (W[k] * r.param[0] + W[3 + k] * r.param[1]) + W[6 + k] * r.param[2];
+    for (int k = 0; k < 3; ++k) dir[k] = o[k] - pp[k];
+    const double n = cf_norm(dir);
+    for (int k = 0; k < 3; ++k) dir[k] /= n;
+    for (int k = 0; k < 3; ++k) {
+      pS[k] = o[k] - dir[k] * radius;
+      pT[k] = pp[k];
+    }
+    return std::sqrt(r.sqr_distance) - radius;
+  }
+  return -1.0;
 }
 
-template <typename SupFn>
-__device__ bool blow_up(SupFn sup, GSV S[4], int n) {
-  const double ax[6][3] = {{1, 0, 0}, {-1, 0, 0}, {0, 1, 0}, {0, -1, 0}, {0, 0, 1}, {0, 0, -1}};
-  if (n == 4) n = 3;
-  while (n < 3) {
-    bool grown = false;
-    for (int k = 0; k < 6 && !grown; ++k) {
-      const GSV s = sup(V3{ax[k][0], ax[k][1], ax[k][2]});
-      const V3 e = vsub(s.w, S[0].w);
-      if (n == 1) {
-        if (d3dot(e, e) > 1e-20) {
-          S[n++] = s;
-          grown = true;
-        }
-        continue;
-      }
-      const V3 u = vsub(S[1].w, S[0].w);
-      const V3 c = vcross(u, e);
-      if (d3dot(c, c) > 1e-20 * d3dot(u, u)) {
-        S[n++] = s;
-        grown = true;
-      }
-    }
-    if (!grown) return false;
-  }
-  V3 nr = vcross(vsub(S[1].w, S[0].w), vsub(S[2].w, S[0].w));
-  const double l = std::sqrt(d3dot(nr, nr));
-  if (!(l > 0.0)) return false;
-  nr = V3{nr.x / l, nr.y / l, nr.z / l};
-  const GSV sp = sup(nr), sm = sup(V3{-nr.x, -nr.y, -nr.z});
-  const double hp = d3dot(vsub(sp.w, S[0].w), nr), hm = -d3dot(vsub(sm.w, S[0].w), nr);
-  if (!(hp > 1e-12 || hm > 1e-12)) return false;
-  S[3] = hp >= hm ? sp : sm;
-  return true;
-}
-
-// gjk_distance with the nearest points; SIGNED: -EPA depth for intersecting
-// shapes (0 if they only touch).  Unsigned and intersecting: -1, zero points.
-template <bool SIGNED, typename SupFn>
-__device__ double gjk_query(V3 v, SupFn sup, V3& p1, V3& p2) {
-  if (d3dot(v, v) == 0.0) v.x = 1e-12;
-  GSV S[4];
-  double lam[4] = {0, 0, 0, 0};
-  int n = 0;
-  p1 = V3{0, 0, 0};
-  p2 = V3{0, 0, 0};
-  auto points = [&]() {
-    V3 a{0, 0, 0}, b{0, 0, 0};
-    for (int k = 0; k < n; ++k) {
-      a = V3{a.x + lam[k] * S[k].a.x, a.y + lam[k] * S[k].a.y, a.z + lam[k] * S[k].a.z};
-      b = V3{b.x + lam[k] * S[k].b.x, b.y + lam[k] * S[k].b.y, b.z + lam[k] * S[k].b.z};
-    }
-    p1 = a;
-    p2 = b;
-  };
-  for (int it = 0; it < 128; ++it) {
-    const GSV s = sup(V3{-v.x, -v.y, -v.z});
-    const double vv = d3dot(v, v), vw = d3dot(v, s.w);
-    if (n > 0 && vv - vw <= 1e-12 * vv) break;
-    bool dup = false;
-    for (int k = 0; k < n; ++k) dup |= (S[k].w.x == s.w.x && S[k].w.y == s.w.y && S[k].w.z == s.w.z);
-    if (dup) break;
-    S[n++] = s;
-    if (simplex_closest_s(S, n, v, lam)) {
-      if constexpr (!SIGNED) return -1.0;
-      const double dep = epa_depth(sup, S, p1, p2);
-      return dep >= 0.0 ? -dep : 0.0;
-    }
-    const double nv = d3dot(v, v);
-    if (nv <= 1e-24) {
-      if constexpr (!SIGNED) return -1.0;
-      if (blow_up(sup, S, n)) {
-        const double dep = epa_depth(sup, S, p1, p2);
-        if (dep >= 0.0) return -dep;
-      }
-      points();
-      return 0.0;
-    }
-    if (n > 1 && nv >= vv) break;
-  }
-  points();
-  return std::sqrt(d3dot(v, v));
+// lower-bound pruning slack (oracle mesh_dist_slack): a pair / leaf / triangle
+// is skipped only when its bounding-volume lower bound is above the running
+// minimum by more than the float support rounding of libccd's GJK objects
+__device__ __forceinline__ double dist_slack(const double* pa, const double* pb) {
+  return 1e-5 * (1.0 + std::fabs(pa[0]) + std::fabs(pa[1]) + std::fabs(pa[2]) + std::fabs(pb[0]) + std::fabs(pb[1]) +
+                 std::fabs(pb[2]));
 }
 
 // fcl::distance(shape, OcTree) [ext FCL 0.7.0 OcTreeShapeDistanceRecurse]:
-// the minimum over the occupied leaves of shapeDistance(leaf box, shape) with
-// the box first (constructBox: box_tf = tf * Translation(centre), boxToGJK);
-// FCL's pruning only skips leaves that cannot lower the minimum and it stops
-// at the first penetrating leaf (-1).  Leaves whose bounding sphere cannot
-// beat the running minimum `best` (the caller's) are skipped the same way.
+// shapeDistance(leaf box, box_tf, shape, tf) per occupied leaf in FCL's DFS
+// order (Box-Sphere closed form, else GJKDistance), strict '<' -> the first
+// minimum; points (leaf box, shape).  Leaves whose bounding sphere cannot be
+// below `bound` (the group's running minimum) by the slack are skipped.
+// Returns the pair's minimum (DBL_MAX if every leaf was skipped) or a
+// kDist* sentinel status in st.
 __device__ double octree_distance(const DevWorld& w, cptr<double> HV, int go, const SE3& TO, const GObj& S,
-                                  const V3& cs, double rs, double best) {
+                                  const SE3& TS, const V3& cs, double rs, double bound, ccd_real tol, V3& pb, V3& ps,
+                                  int& st) {
   const cptr<double> go_rec = w.geom_rec + G_STRIDE * go;
   const int l0 = (int)go_rec[G_PARAM], ln = (int)go_rec[G_PARAM + 1];
+  const bool sphere = S.type == MPG_GEOM_SPHERE;
+  const double rsph = w.geom_rec[G_STRIDE * S.geom + G_PARAM];
+  const double slack = dist_slack(TO.p, TS.p);
   GObj A;
   A.rot = gjk_rot_from_matrix(TO.R);
   A.rot_inv = quat_invert2(A.rot);
   A.geom = go;
   A.type = MPG_GEOM_BOX;
+  double best = DBL_MAX;
+  pb = ps = V3{0, 0, 0};
   for (int l = l0; l < l0 + ln && best != -1.0; ++l) {
     const cptr<double> L = w.oct_leaf + 6 * (size_t)l;
     double c[3], side[3], cw[3];
@@ -4015,14 +4027,41 @@ __device__ double octree_distance(const DevWorld& w, cptr<double> HV, int go, co
     }
     for (int i = 0; i < 3; ++i) cw[i] = ((TO.R[3 * i] * c[0] + TO.R[3 * i + 1] * c[1]) + TO.R[3 * i + 2] * c[2]) + TO.p[i];
     const double dx = cw[0] - cs.x, dy = cw[1] - cs.y, dz = cw[2] - cs.z;
-    const double rl = 0.5 * std::sqrt((side[0] * side[0] + side[1] * side[1]) + side[2] * side[2]);
-    if (std::sqrt(dx * dx + dy * dy + dz * dz) - rs - rl - 1e-9 >= best) continue;
-    GObj A1 = A;
-    A1.pos = cv3(cw[0], cw[1], cw[2]);
-    const ccd_real h[3] = {(ccd_real)(side[0] / 2.0), (ccd_real)(side[1] / 2.0), (ccd_real)(side[2] / 2.0)};
-    const double d = gjk_distance_from(vsub(to_v3(A1.pos), to_v3(center(w, S))),
-                                       [&](const CV3& dir) { return msupport_box(A1, h, w, HV, S, dir); });
-    if (d < best) best = d;
+    const double rl = 0.5 * std::sqrt((side[0] * side[0] + side[1] * side[1]) + side[2] * side[2]) * (1.0 + 1e-9) + 1e-9;
+    if (std::sqrt(dx * dx + dy * dy + dz * dz) - rs - rl > fmin(best, bound) + slack) continue;
+    double d;
+    V3 qb{0, 0, 0}, qs{0, 0, 0};
+    if (sphere) {
+      SE3 TL;
+      for (int k = 0; k < 9; ++k) TL.R[k] = TO.R[k];
+      for (int k = 0; k < 3; ++k) TL.p[k] = cw[k];
+      double a1[3], a2[3];
+      d = cf_sphere_box(rsph, TS, side, TL, a2, a1);
+      if (d != -1.0) {
+        qb = V3{a1[0], a1[1], a1[2]};
+        qs = V3{a2[0], a2[1], a2[2]};
+      }
+    } else {
+      GObj A1 = A;
+      A1.pos = cv3(cw[0], cw[1], cw[2]);
+      const ccd_real h[3] = {(ccd_real)(side[0] / 2.0), (ccd_real)(side[1] / 2.0), (ccd_real)(side[2] / 2.0)};
+      auto sup = [&](const CV3& dir) { return csup_box(A1, h, w, HV, S, dir); };
+      ccd_real df;
+      CV3 c1, c2;
+      const int r = ccdx::gjk_distance<false>(sup, tol, nullptr, df, c1, c2);
+      if (r != ccdx::kOk) {
+        st = r == ccdx::kThrow ? kDistThrow : kDistOverflow;
+        return DBL_MAX;
+      }
+      d = df;
+      qb = to_v3(c1);
+      qs = to_v3(c2);
+    }
+    if (d < best) {
+      best = d;
+      pb = qb;
+      ps = qs;
+    }
   }
   return best;
 }
@@ -4071,13 +4110,9 @@ __device__ __forceinline__ SE3 pose_se3(const DevWorld& w, const double* __restr
 //                shapeTriangleDistance(box, box_tf, ...), box first
 // The traversal only skips what cannot lower the running minimum; here the
 // cluster and triangle boxes are skipped when their lower bound exceeds the
-// running minimum by more than the float support rounding (mesh_dist_slack
-// in the oracle).  One lane per configuration, as distance_kernel.
+// running minimum by more than the float support rounding (dist_slack).  One
+// lane per configuration, as distance_kernel.
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ double mesh_dist_slack(const SE3& A, const SE3& B) {
-  return 1e-5 * (1.0 + std::fabs(A.p[0]) + std::fabs(A.p[1]) + std::fabs(A.p[2]) + std::fabs(B.p[0]) +
-                 std::fabs(B.p[1]) + std::fabs(B.p[2]));
-}
 
 // distance from point c to the box [lo, hi]
 __device__ __forceinline__ double point_box_distance(const double* c, const double* lo, const double* hi) {
@@ -4164,7 +4199,9 @@ __device__ void seg_points(const double* P, const double* A, const double* Q, co
   }
 }
 
-__device__ bool tri_face_case(const double* S, const double* Sv, const double* T, bool& disjoint, double& dist) {
+// Pf: the projection of T's closest vertex on S's face, Qf: that vertex
+__device__ bool tri_face_case(const double* S, const double* Sv, const double* T, bool& disjoint, double& dist,
+                              double* Pf, double* Qf) {
   double Sn[3], V[3], Z[3], Tp[3];
   c3(Sn, Sv, Sv + 3);
   const double Snl = d3(Sn, Sn);
@@ -4190,14 +4227,19 @@ __device__ bool tri_face_case(const double* S, const double* Sv, const double* T
   }
   double D[3];
   const double s = Tp[point] / Snl;
-  for (int k = 0; k < 3; ++k) D[k] = (T[3 * point + k] + Sn[k] * s) - T[3 * point + k];
+  for (int k = 0; k < 3; ++k) {
+    Pf[k] = T[3 * point + k] + Sn[k] * s;
+    Qf[k] = T[3 * point + k];
+    D[k] = Pf[k] - Qf[k];
+  }
   dist = std::sqrt(d3(D, D));
   return true;
 }
 
-// S, T: 3 vertices each, row-major [3][3]
-__device__ double tri_distance(const double* S, const double* T) {
-  double Sv[9], Tv[9], VEC[3], P[3], Q[3], V[3], Z[3];
+// TriangleDistance::triDistance(S, T, P, Q) (oracle tri_distance_pq); S, T:
+// 3 vertices each, row-major [3][3]; P, Q zero when they intersect
+__device__ double tri_distance_pq(const double* S, const double* T, double* P, double* Q) {
+  double Sv[9], Tv[9], VEC[3], Pc[3], Qc[3], V[3], Z[3], minP[3] = {0, 0, 0}, minQ[3] = {0, 0, 0};
   for (int k = 0; k < 3; ++k) {
     Sv[k] = S[3 + k] - S[k];
     Sv[3 + k] = S[6 + k] - S[3 + k];
@@ -4205,23 +4247,35 @@ __device__ double tri_distance(const double* S, const double* T) {
     Tv[k] = T[3 + k] - T[k];
     Tv[3 + k] = T[6 + k] - T[3 + k];
     Tv[6 + k] = T[k] - T[6 + k];
+    P[k] = 0.0;
+    Q[k] = 0.0;
   }
   bool shown_disjoint = false;
   for (int k = 0; k < 3; ++k) V[k] = S[k] - T[k];
   double mindd = d3(V, V) + 1;
   for (int i = 0; i < 3; ++i)
     for (int j = 0; j < 3; ++j) {
-      seg_points(S + 3 * i, Sv + 3 * i, T + 3 * j, Tv + 3 * j, VEC, P, Q);
-      for (int k = 0; k < 3; ++k) V[k] = Q[k] - P[k];
+      seg_points(S + 3 * i, Sv + 3 * i, T + 3 * j, Tv + 3 * j, VEC, Pc, Qc);
+      for (int k = 0; k < 3; ++k) V[k] = Qc[k] - Pc[k];
       const double dd = d3(V, V);
       if (dd <= mindd) {
+        for (int k = 0; k < 3; ++k) {
+          minP[k] = Pc[k];
+          minQ[k] = Qc[k];
+        }
         mindd = dd;
         const int i2 = (i + 2) % 3, j2 = (j + 2) % 3;
-        for (int k = 0; k < 3; ++k) Z[k] = S[3 * i2 + k] - P[k];
+        for (int k = 0; k < 3; ++k) Z[k] = S[3 * i2 + k] - Pc[k];
         double a = d3(Z, VEC);
-        for (int k = 0; k < 3; ++k) Z[k] = T[3 * j2 + k] - Q[k];
+        for (int k = 0; k < 3; ++k) Z[k] = T[3 * j2 + k] - Qc[k];
         double b = d3(Z, VEC);
-        if (a <= 0 && b >= 0) return std::sqrt(dd);
+        if (a <= 0 && b >= 0) {
+          for (int k = 0; k < 3; ++k) {
+            P[k] = Pc[k];
+            Q[k] = Qc[k];
+          }
+          return std::sqrt(dd);
+        }
         const double p = d3(V, VEC);
         if (a < 0) a = 0;
         if (b > 0) b = 0;
@@ -4229,9 +4283,16 @@ __device__ double tri_distance(const double* S, const double* T) {
       }
     }
   double d;
-  if (tri_face_case(S, Sv, T, shown_disjoint, d)) return d;
-  if (tri_face_case(T, Tv, S, shown_disjoint, d)) return d;
-  return shown_disjoint ? std::sqrt(mindd) : 0.0;
+  if (tri_face_case(S, Sv, T, shown_disjoint, d, P, Q)) return d;
+  if (tri_face_case(T, Tv, S, shown_disjoint, d, Q, P)) return d;
+  if (shown_disjoint) {
+    for (int k = 0; k < 3; ++k) {
+      P[k] = minP[k];
+      Q[k] = minQ[k];
+    }
+    return std::sqrt(mindd);
+  }
+  return 0.0;
 }
 
 __device__ __forceinline__ GObj mesh_frame_obj(int gm, const SE3& TM) {
@@ -4251,44 +4312,85 @@ __device__ __forceinline__ void to_frame(const SE3& T, const double* p, double* 
   for (int i = 0; i < 3; ++i) o[i] = (T.R[i] * d[0] + T.R[3 + i] * d[1]) + T.R[6 + i] * d[2];
 }
 
-// min over triangles of GJK(shape S, triangle), or something >= best when no
-// triangle can beat the running minimum `best`
+// mesh-shape (MeshShapeDistanceTraversalNodeOBBRSS leaf): the minimum over
+// the triangles of shapeTriangleDistance(shape, tf, P1, P2, P3, tf_mesh)
+// (sphereTriangleDistance for spheres, else GJKDistance with the shape first),
+// points (mesh, shape).  Triangles are met in cluster order; ties go to the
+// lower triangle index, as the oracle's index-order scan with strict '<'.
+// Clusters / triangles whose lower bound is above min(own minimum, bound) by
+// the slack are skipped.  DBL_MAX when everything was skipped.
 __device__ double mesh_shape_distance_lane(const DevWorld& w, cptr<double> HV, int gm, const SE3& TM, const GObj& S,
-                                           const SE3& TS, double best) {
+                                           const SE3& TS, double bound, ccd_real tol, V3& pm, V3& ps, int& st) {
   const cptr<double> grs = w.geom_rec + G_STRIDE * S.geom;
   double cs[3], csm[3];
 #pragma unroll
   for (int i = 0; i < 3; ++i)
     cs[i] = ((TS.R[3 * i] * grs[G_OBB_C] + TS.R[3 * i + 1] * grs[G_OBB_C + 1]) + TS.R[3 * i + 2] * grs[G_OBB_C + 2]) + TS.p[i];
   to_frame(TM, cs, csm);
-  const double rs = grs[G_RADIUS], slack = mesh_dist_slack(TM, TS);
+  const double rs = grs[G_RADIUS], slack = dist_slack(TM.p, TS.p);
+  const bool sphere = S.type == MPG_GEOM_SPHERE;
   const GObj B = mesh_frame_obj(gm, TM);
-  const CV3 ca = center(w, S);
   const int c0 = w.mesh_tree[2 * gm], c1 = c0 + w.mesh_tree[2 * gm + 1];
+  double best = DBL_MAX;
+  int best_id = INT_MAX;
+  pm = ps = V3{0, 0, 0};
   for (int cl = c0; cl < c1 && best != -1.0; ++cl) {
     const cptr<double> bx = w.mesh_node + 6 * (size_t)cl;
     const double lo[3] = {bx[0], bx[1], bx[2]}, hi[3] = {bx[3], bx[4], bx[5]};
-    if (point_box_distance(csm, lo, hi) - rs > best + slack) continue;
+    if (point_box_distance(csm, lo, hi) - rs > fmin(best, bound) + slack) continue;
     const int t1 = w.mesh_link[2 * cl] + w.mesh_link[2 * cl + 1];
     for (int t = w.mesh_link[2 * cl]; t < t1 && best != -1.0; ++t) {
       const cptr<double> rec = w.mesh_tri + TR_STRIDE * (size_t)t;
       const double tlo[3] = {rec[TR_LO], rec[TR_LO + 1], rec[TR_LO + 2]}, thi[3] = {rec[TR_HI], rec[TR_HI + 1], rec[TR_HI + 2]};
-      if (point_box_distance(csm, tlo, thi) - rs > best + slack) continue;
+      if (point_box_distance(csm, tlo, thi) - rs > fmin(best, bound) + slack) continue;
+      const int id = (int)rec[TR_ID];
       double P[9];
 #pragma unroll
       for (int k = 0; k < 9; ++k) P[k] = rec[TR_P + k];
-      const CV3 tc = cv3((P[0] + P[3] + P[6]) / 3, (P[1] + P[4] + P[7]) / 3, (P[2] + P[5] + P[8]) / 3);
-      const CV3 TP[3] = {cv3(P[0], P[1], P[2]), cv3(P[3], P[4], P[5]), cv3(P[6], P[7], P[8])};
-      const double d = gjk_distance_from(vsub(to_v3(ca), to_v3(vadd(quat_rot(tc, B.rot), B.pos))),
-                                         [&](const CV3& dir) { return msupport_tri(w, HV, S, B, TP, tc, dir); });
-      if (d < best) best = d;
+      double d;
+      V3 qm{0, 0, 0}, qs{0, 0, 0};
+      if (sphere) {
+        double W[9], a1[3], a2[3];
+        for (int v = 0; v < 3; ++v)
+          for (int i = 0; i < 3; ++i)
+            W[3 * v + i] = ((TM.R[3 * i] * P[3 * v] + TM.R[3 * i + 1] * P[3 * v + 1]) + TM.R[3 * i + 2] * P[3 * v + 2]) + TM.p[i];
+        d = cf_sphere_triangle(grs[G_PARAM], TS.p, W, a1, a2);
+        if (d != -1.0) {
+          qs = V3{a1[0], a1[1], a1[2]};
+          qm = V3{a2[0], a2[1], a2[2]};
+        }
+      } else {
+        const CV3 tc = cv3((P[0] + P[3] + P[6]) / 3, (P[1] + P[4] + P[7]) / 3, (P[2] + P[5] + P[8]) / 3);
+        const CV3 TP[3] = {cv3(P[0], P[1], P[2]), cv3(P[3], P[4], P[5]), cv3(P[6], P[7], P[8])};
+        auto sup = [&](const CV3& dir) { return csup_tri(w, HV, S, B, TP, tc, dir); };
+        ccd_real df;
+        CV3 c1, c2;
+        const int r = ccdx::gjk_distance<false>(sup, tol, nullptr, df, c1, c2);
+        if (r != ccdx::kOk) {
+          st = r == ccdx::kThrow ? kDistThrow : kDistOverflow;
+          return DBL_MAX;
+        }
+        d = df;
+        qs = to_v3(c1);
+        qm = to_v3(c2);
+      }
+      if (d < best || (d == best && id < best_id)) {
+        best = d;
+        best_id = id;
+        pm = qm;
+        ps = qs;
+      }
     }
   }
   return best;
 }
 
-// min of triDistance over (triangle of A, triangle of B in A's frame)
-__device__ double mesh_mesh_distance_lane(const DevWorld& w, int ga, const SE3& TA, int gb, const SE3& TB, double best) {
+// mesh-mesh (MeshDistanceTraversalNodeOBBRSS): the minimum of triDistance
+// over the triangle pairs, B's triangles in A's frame; 0 once a pair
+// intersects (zero points); points (A, B) in A's frame -> world.  Ties go to
+// the lexicographically lower (A index, B index), the oracle's scan order.
+__device__ double mesh_mesh_distance_lane(const DevWorld& w, int ga, const SE3& TA, int gb, const SE3& TB, double bound,
+                                          V3& pa, V3& pb) {
   double R[9], T[3];
   const double dt[3] = {TB.p[0] - TA.p[0], TB.p[1] - TA.p[1], TB.p[2] - TA.p[2]};
 #pragma unroll
@@ -4297,9 +4399,11 @@ __device__ double mesh_mesh_distance_lane(const DevWorld& w, int ga, const SE3& 
     for (int j = 0; j < 3; ++j) R[3 * i + j] = (TA.R[i] * TB.R[j] + TA.R[3 + i] * TB.R[3 + j]) + TA.R[6 + i] * TB.R[6 + j];
     T[i] = (TA.R[i] * dt[0] + TA.R[3 + i] * dt[1]) + TA.R[6 + i] * dt[2];
   }
-  const double slack = mesh_dist_slack(TA, TB);
+  const double slack = dist_slack(TA.p, TB.p);
   const int a0 = w.mesh_tree[2 * ga], a1 = a0 + w.mesh_tree[2 * ga + 1];
   const int b0 = w.mesh_tree[2 * gb], b1 = b0 + w.mesh_tree[2 * gb + 1];
+  double best = DBL_MAX, bP[3] = {0, 0, 0}, bQ[3] = {0, 0, 0};
+  long long best_key = LLONG_MAX;
   for (int cb = b0; cb < b1 && best != 0.0; ++cb) {
     const cptr<double> bb = w.mesh_node + 6 * (size_t)cb;
     double cc[3], cca[3], e2 = 0.0;
@@ -4314,7 +4418,7 @@ __device__ double mesh_mesh_distance_lane(const DevWorld& w, int ga, const SE3& 
     for (int ca = a0; ca < a1 && best != 0.0; ++ca) {
       const cptr<double> ba = w.mesh_node + 6 * (size_t)ca;
       const double lo[3] = {ba[0], ba[1], ba[2]}, hi[3] = {ba[3], ba[4], ba[5]};
-      if (point_box_distance(cca, lo, hi) - rb > best + slack) continue;
+      if (point_box_distance(cca, lo, hi) - rb > fmin(best, bound) + slack) continue;
       const int tb1 = w.mesh_link[2 * cb] + w.mesh_link[2 * cb + 1];
       for (int tb = w.mesh_link[2 * cb]; tb < tb1 && best != 0.0; ++tb) {
         const cptr<double> rq = w.mesh_tri + TR_STRIDE * (size_t)tb;
@@ -4332,34 +4436,52 @@ __device__ double mesh_mesh_distance_lane(const DevWorld& w, int ga, const SE3& 
           qr = fmax(qr, dx * dx + dy * dy + dz * dz);
         }
         qr = std::sqrt(qr) * (1.0 + 1e-9) + 1e-9;
-        if (point_box_distance(qc, lo, hi) - qr > best + slack) continue;
+        if (point_box_distance(qc, lo, hi) - qr > fmin(best, bound) + slack) continue;
+        const long long idb = (long long)rq[TR_ID];
         const int ta1 = w.mesh_link[2 * ca] + w.mesh_link[2 * ca + 1];
         for (int ta = w.mesh_link[2 * ca]; ta < ta1; ++ta) {
           const cptr<double> rp = w.mesh_tri + TR_STRIDE * (size_t)ta;
           const double tlo[3] = {rp[TR_LO], rp[TR_LO + 1], rp[TR_LO + 2]}, thi[3] = {rp[TR_HI], rp[TR_HI + 1], rp[TR_HI + 2]};
-          if (point_box_distance(qc, tlo, thi) - qr > best + slack) continue;
-          double P[9];
+          if (point_box_distance(qc, tlo, thi) - qr > fmin(best, bound) + slack) continue;
+          double P[9], Pp[3], Qq[3];
 #pragma unroll
           for (int k = 0; k < 9; ++k) P[k] = rp[TR_P + k];
-          const double d = tri_distance(P, Q);
-          if (d < best) best = d;
+          const double d = tri_distance_pq(P, Q, Pp, Qq);
+          const long long key = ((long long)rp[TR_ID] << 32) | idb;
+          if (d < best || (d == best && key < best_key)) {
+            best = d;
+            best_key = key;
+            for (int k = 0; k < 3; ++k) {
+              bP[k] = Pp[k];
+              bQ[k] = Qq[k];
+            }
+          }
           if (best == 0.0) break;
         }
       }
     }
   }
+  double wa[3], wb[3];
+  cf_tf_point(TA, bP, wa);
+  cf_tf_point(TA, bQ, wb);
+  pa = V3{wa[0], wa[1], wa[2]};
+  pb = V3{wb[0], wb[1], wb[2]};
   return best;
 }
 
-// min over (occupied leaf box, triangle) of GJK(box, triangle)
-__device__ double mesh_octree_distance_lane(const DevWorld& w, int gm, const SE3& TM, int go, const SE3& TO, double best) {
+// mesh-OcTree (OcTreeMeshDistanceRecurse): the minimum over (occupied leaf,
+// triangle) of shapeTriangleDistance(Box(leaf), box_tf, triangle) (GJK, leaf
+// box first); points (box, triangle); ties to the earlier leaf, then the
+// lower triangle index, as the oracle's leaf-major scan
+__device__ double mesh_octree_distance_lane(const DevWorld& w, int gm, const SE3& TM, int go, const SE3& TO, double bound,
+                                            ccd_real tol, V3& pbox, V3& ptri, int& st) {
   const cptr<double> grm = w.geom_rec + G_STRIDE * gm, go_rec = w.geom_rec + G_STRIDE * go;
   const int l0 = (int)go_rec[G_PARAM], ln = (int)go_rec[G_PARAM + 1];
   double mcw[3];
 #pragma unroll
   for (int i = 0; i < 3; ++i)
     mcw[i] = ((TM.R[3 * i] * grm[G_OBB_C] + TM.R[3 * i + 1] * grm[G_OBB_C + 1]) + TM.R[3 * i + 2] * grm[G_OBB_C + 2]) + TM.p[i];
-  const double rm = grm[G_RADIUS], slack = mesh_dist_slack(TM, TO);
+  const double rm = grm[G_RADIUS], slack = dist_slack(TM.p, TO.p);
   const GObj B = mesh_frame_obj(gm, TM);
   GObj A;
   A.rot = gjk_rot_from_matrix(TO.R);
@@ -4367,6 +4489,9 @@ __device__ double mesh_octree_distance_lane(const DevWorld& w, int gm, const SE3
   A.geom = go;
   A.type = MPG_GEOM_BOX;
   const int c0 = w.mesh_tree[2 * gm], c1 = c0 + w.mesh_tree[2 * gm + 1];
+  double best = DBL_MAX;
+  int best_id = INT_MAX;
+  pbox = ptri = V3{0, 0, 0};
   for (int l = l0; l < l0 + ln && best != -1.0; ++l) {
     const cptr<double> L = w.oct_leaf + 6 * (size_t)l;
     double c[3], side[3], cw[3], cm[3];
@@ -4379,54 +4504,84 @@ __device__ double mesh_octree_distance_lane(const DevWorld& w, int gm, const SE3
     for (int i = 0; i < 3; ++i) cw[i] = ((TO.R[3 * i] * c[0] + TO.R[3 * i + 1] * c[1]) + TO.R[3 * i + 2] * c[2]) + TO.p[i];
     const double rl = 0.5 * std::sqrt((side[0] * side[0] + side[1] * side[1]) + side[2] * side[2]) * (1.0 + 1e-9) + 1e-9;
     const double dx = cw[0] - mcw[0], dy = cw[1] - mcw[1], dz = cw[2] - mcw[2];
-    if (std::sqrt(dx * dx + dy * dy + dz * dz) - rl - rm > best + slack) continue;
+    if (std::sqrt(dx * dx + dy * dy + dz * dz) - rl - rm > fmin(best, bound) + slack) continue;
     to_frame(TM, cw, cm);
     GObj A1 = A;
     A1.pos = cv3(cw[0], cw[1], cw[2]);
     const ccd_real h[3] = {(ccd_real)(side[0] / 2.0), (ccd_real)(side[1] / 2.0), (ccd_real)(side[2] / 2.0)};
+    const double leaf_best = best;  // a later leaf wins only when strictly below the earlier leaves
     for (int cl = c0; cl < c1 && best != -1.0; ++cl) {
       const cptr<double> bx = w.mesh_node + 6 * (size_t)cl;
       const double lo[3] = {bx[0], bx[1], bx[2]}, hi[3] = {bx[3], bx[4], bx[5]};
-      if (point_box_distance(cm, lo, hi) - rl > best + slack) continue;
+      if (point_box_distance(cm, lo, hi) - rl > fmin(best, bound) + slack) continue;
       const int t1 = w.mesh_link[2 * cl] + w.mesh_link[2 * cl + 1];
       for (int t = w.mesh_link[2 * cl]; t < t1 && best != -1.0; ++t) {
         const cptr<double> rec = w.mesh_tri + TR_STRIDE * (size_t)t;
         const double tlo[3] = {rec[TR_LO], rec[TR_LO + 1], rec[TR_LO + 2]}, thi[3] = {rec[TR_HI], rec[TR_HI + 1], rec[TR_HI + 2]};
-        if (point_box_distance(cm, tlo, thi) - rl > best + slack) continue;
+        if (point_box_distance(cm, tlo, thi) - rl > fmin(best, bound) + slack) continue;
+        const int id = (int)rec[TR_ID];
         double P[9];
 #pragma unroll
         for (int k = 0; k < 9; ++k) P[k] = rec[TR_P + k];
         const CV3 tc = cv3((P[0] + P[3] + P[6]) / 3, (P[1] + P[4] + P[7]) / 3, (P[2] + P[5] + P[8]) / 3);
         const CV3 TP[3] = {cv3(P[0], P[1], P[2]), cv3(P[3], P[4], P[5]), cv3(P[6], P[7], P[8])};
-        const double d = gjk_distance_from(vsub(to_v3(A1.pos), to_v3(vadd(quat_rot(tc, B.rot), B.pos))),
-                                           [&](const CV3& dir) { return msupport_box_tri(A1, h, B, TP, tc, dir); });
-        if (d < best) best = d;
+        auto sup = [&](const CV3& dir) { return csup_box_tri(A1, h, B, TP, tc, dir); };
+        ccd_real df;
+        CV3 q1, q2;
+        const int r = ccdx::gjk_distance<false>(sup, tol, nullptr, df, q1, q2);
+        if (r != ccdx::kOk) {
+          st = r == ccdx::kThrow ? kDistThrow : kDistOverflow;
+          return DBL_MAX;
+        }
+        const double d = df;
+        // within this leaf: the lower triangle index among equals; against
+        // earlier leaves: strictly below
+        if (d < leaf_best && (d < best || (d == best && id < best_id))) {
+          best = d;
+          best_id = id;
+          pbox = to_v3(q1);
+          ptri = to_v3(q2);
+        }
       }
     }
   }
   return best;
 }
 
-// MODE 0: distances only; MPG_DIST_POINTS: also the nearest points of each
-// group's minimum pair (pts [n][6]); | MPG_DIST_SIGNED: signed distances
-// (the host refuses signed requests on worlds with point-cloud / BVH-mesh pairs)
-constexpr int MPG_DIST_POINTS = 1, MPG_DIST_SIGNED = 2;
+// (MODE bit) PTS: write the nearest points; SIGNED: enable_signed_distance;
+// NP: enable_nearest_points (mesh-mesh points, the (shape, mesh) swap)
+constexpr int MPG_DIST_POINTS = 1, MPG_DIST_SIGNED = 2, MPG_DIST_NP = 4;
+
+// Per configuration, every non-allowed pair in order with the group's strict
+// '<' (planning_world.cpp:513): fcl::distance with DistanceRequest's options
+// (oracle/collide_oracle.c pair_distance: which algorithm each pair kind runs
+// and which point is which).  Shape pairs whose bounding spheres are apart
+// by more than the running minimum plus the slack are skipped (their GJK
+// value cannot be below it).  A configuration on which FCL throws
+// (p = kDistThrow) or whose EPA outgrows the polytope arrays (p =
+// kDistOverflow) gets NaN distances in both groups.
 template <int MODE>
 __global__ __launch_bounds__(128) void distance_kernel(DevWorld w, const double* __restrict__ poses, long long n,
-                                                       int n_self, double* __restrict__ d_self,
+                                                       int n_self, ccd_real tol, double* __restrict__ d_self,
                                                        int32_t* __restrict__ p_self, double* __restrict__ d_others,
                                                        int32_t* __restrict__ p_others, double* __restrict__ pts_self,
                                                        double* __restrict__ pts_others) {
   constexpr bool SIGNED = (MODE & MPG_DIST_SIGNED) != 0;
-  constexpr bool PTS = MODE != 0;
+  constexpr bool PTS = (MODE & MPG_DIST_POINTS) != 0;
+  constexpr bool NP = (MODE & MPG_DIST_NP) != 0;
   const long long cfg0 = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const bool live = cfg0 < n;
   const long long cfg = live ? cfg0 : n - 1;
   const cptr<double> HV = w.hull;
+  struct NoPolytope {};
+  std::conditional_t<SIGNED, ccdx::Polytope, NoPolytope> polytope;
+  ccdx::Polytope* ptp = nullptr;
+  if constexpr (SIGNED) ptp = &polytope;
   double best[2] = {DBL_MAX, DBL_MAX};
   int bp[2] = {-1, -1};
   V3 bpt[2][2] = {{{0, 0, 0}, {0, 0, 0}}, {{0, 0, 0}, {0, 0, 0}}};
-  for (int p = 0; p < w.n_pairs; ++p) {
+  int st = 0;
+  for (int p = 0; p < w.n_pairs && !st; ++p) {
     if (w.pair_allowed[p]) continue;  // ACM before distance (planning_world.cpp:509-510)
     const int g = p < n_self ? 0 : 1;
     const int a = w.pair_a[p], b = w.pair_b[p];
@@ -4434,59 +4589,69 @@ __global__ __launch_bounds__(128) void distance_kernel(DevWorld w, const double*
     const GObj A = pose_obj(w, poses, n, cfg, a, ca);
     const GObj B = pose_obj(w, poses, n, cfg, b, cb);
     const double ra = w.geom_rec[G_STRIDE * A.geom + G_RADIUS], rb = w.geom_rec[G_STRIDE * B.geom + G_RADIUS];
-    if (w.pair_cf[p] == CF_MESH) {
-      if (!live || best[g] == -1.0) continue;
+    double d = DBL_MAX;
+    V3 q1{0, 0, 0}, q2{0, 0, 0};
+    if (w.pair_cf[p] == CF_MESH) {  // mesh pairs report unsigned values, never below -1
+      if (!live || best[g] <= -1.0) continue;
       const SE3 TA = pose_se3(w, poses, n, cfg, a), TB = pose_se3(w, poses, n, cfg, b);
-      double d;
-      if (A.type == MPG_GEOM_MESH && B.type == MPG_GEOM_MESH) d = mesh_mesh_distance_lane(w, A.geom, TA, B.geom, TB, best[g]);
-      else if (A.type == MPG_GEOM_OCTREE) d = mesh_octree_distance_lane(w, B.geom, TB, A.geom, TA, best[g]);
-      else if (B.type == MPG_GEOM_OCTREE) d = mesh_octree_distance_lane(w, A.geom, TA, B.geom, TB, best[g]);
-      else if (A.type == MPG_GEOM_MESH) d = mesh_shape_distance_lane(w, HV, A.geom, TA, B, TB, best[g]);
-      else d = mesh_shape_distance_lane(w, HV, B.geom, TB, A, TA, best[g]);
-      if (d < best[g]) {
-        best[g] = d;
-        bp[g] = p;
-        if constexpr (PTS) bpt[g][0] = bpt[g][1] = V3{0, 0, 0};
+      if (A.type == MPG_GEOM_MESH && B.type == MPG_GEOM_MESH) {
+        d = mesh_mesh_distance_lane(w, A.geom, TA, B.geom, TB, best[g], q1, q2);
+        if (!NP) q1 = q2 = V3{0, 0, 0};
+      } else if (A.type == MPG_GEOM_OCTREE) {
+        d = mesh_octree_distance_lane(w, B.geom, TB, A.geom, TA, best[g], tol, q1, q2, st);
+      } else if (B.type == MPG_GEOM_OCTREE) {
+        d = mesh_octree_distance_lane(w, A.geom, TA, B.geom, TB, best[g], tol, q1, q2, st);
+      } else if (A.type == MPG_GEOM_MESH) {
+        d = mesh_shape_distance_lane(w, HV, A.geom, TA, B, TB, best[g], tol, q1, q2, st);
+      } else {
+        V3 pm, ps;
+        d = mesh_shape_distance_lane(w, HV, B.geom, TB, A, TA, best[g], tol, pm, ps, st);
+        q1 = NP ? ps : pm;  // distance() swaps the points back with enable_nearest_points
+        q2 = NP ? pm : ps;
       }
-      continue;
-    }
-    if (w.pair_cf[p] == CF_OCTREE) {  // the octree is the pair's static side (b, or a through the C ABI)
-      if (!live || best[g] == -1.0) continue;
-      const bool oa = A.type == MPG_GEOM_OCTREE;  // distance is symmetric: leaf box first either way
+    } else if (w.pair_cf[p] == CF_OCTREE) {  // leaf box first whatever the order; unsigned
+      if (!live || best[g] <= -1.0) continue;
+      const bool oa = A.type == MPG_GEOM_OCTREE;
       const SE3 TO = load_se3(w.static_T + 12 * ((oa ? a : b) - w.n_moving));
-      const double d = oa ? octree_distance(w, HV, A.geom, TO, B, cb, rb, best[g])
-                          : octree_distance(w, HV, B.geom, TO, A, ca, ra, best[g]);
-      if (d < best[g]) {
-        best[g] = d;
-        bp[g] = p;
-        if constexpr (PTS) bpt[g][0] = bpt[g][1] = V3{0, 0, 0};
+      const SE3 TS = pose_se3(w, poses, n, cfg, oa ? b : a);
+      d = oa ? octree_distance(w, HV, A.geom, TO, B, TS, cb, rb, best[g], tol, q1, q2, st)
+             : octree_distance(w, HV, B.geom, TO, A, TS, ca, ra, best[g], tol, q1, q2, st);
+    } else {
+      if (!live) continue;
+      const V3 dc = vsub(cb, ca);
+      const double lb = std::sqrt(d3dot(dc, dc)) - ra - rb - 1e-9;
+      if (lb > best[g] + dist_slack(&ca.x, &cb.x)) continue;
+      bool done = false;
+      if constexpr (!SIGNED) {
+        const SE3 TA = pose_se3(w, poses, n, cfg, a), TB = pose_se3(w, poses, n, cfg, b);
+        done = cf_shape_distance(w, A.geom, A.type, TA, B.geom, B.type, TB, d, q1, q2);
       }
-      continue;
+      if (!done) {
+        auto sup = [&](const CV3& dir) { return csup(w, HV, A, B, dir); };
+        ccd_real df;
+        CV3 c1, c2;
+        const int r = ccdx::gjk_distance<SIGNED>(sup, tol, ptp, df, c1, c2);
+        if (r != ccdx::kOk) st = r == ccdx::kThrow ? kDistThrow : kDistOverflow;
+        d = df;
+        q1 = to_v3(c1);
+        q2 = to_v3(c2);
+      }
     }
-    const V3 dc = vsub(cb, ca);
-    // bounding spheres: the pair cannot beat the running minimum (signed too:
-    // a penetration is never deeper than the bounding spheres' overlap)
-    const double lb = std::sqrt(d3dot(dc, dc)) - ra - rb - 1e-9;
-    if (!live || (!SIGNED && best[g] == -1.0) || lb >= best[g]) continue;
-    if constexpr (PTS) {
-      V3 q1, q2;
-      const double d = gjk_query<SIGNED>(vsub(to_v3(center(w, A)), to_v3(center(w, B))),
-                                         [&](const V3& dir) { return msupport_pts(w, HV, A, B, dir); }, q1, q2);
-      if (d < best[g]) {
-        best[g] = d;
-        bp[g] = p;
+    if (st) break;
+    if (d < best[g]) {
+      best[g] = d;
+      bp[g] = p;
+      if constexpr (PTS) {
         bpt[g][0] = q1;
         bpt[g][1] = q2;
-      }
-    } else {
-      const double d = gjk_distance(w, HV, A, B);
-      if (d < best[g]) {
-        best[g] = d;
-        bp[g] = p;
       }
     }
   }
   if (!live) return;
+  if (st) {
+    best[0] = best[1] = __longlong_as_double(0x7ff8000000000000ll);
+    bp[0] = bp[1] = st;
+  }
   d_self[cfg] = best[0];
   p_self[cfg] = bp[0];
   d_others[cfg] = best[1];
@@ -5754,6 +5919,13 @@ __device__ bool mesh_octree_first_contact(const DevWorld& w, int gm, const SE3& 
   const int c0 = w.mesh_tree[2 * gm], c1 = c0 + w.mesh_tree[2 * gm + 1];
   const cptr<double> gor = w.geom_rec + G_STRIDE * go;
   const int l0 = (int)gor[G_PARAM], ln = (int)gor[G_PARAM + 1];
+  // the first hit in OcTreeMeshIntersectRecurse's visit order: the reachable
+  // (leaf, triangle) hit whose descent key (fcl_gate_octree_mesh) is smallest
+  uint64_t best[kOctKeyWords];
+  for (int k = 0; k < kOctKeyWords; ++k) best[k] = ~0ull;
+  bool found = false;
+  double bd = 0.0;
+  V3 bn{0, 0, 0}, bp{0, 0, 0};
   for (int l = l0; l < l0 + ln; ++l) {
     const cptr<double> L = w.oct_leaf + 6 * (size_t)l;
     bool out = false;
@@ -5773,9 +5945,6 @@ __device__ bool mesh_octree_first_contact(const DevWorld& w, int gm, const SE3& 
     }
     A.pos = cv3(cw[0], cw[1], cw[2]);
     const ccd_real h[3] = {(ccd_real)(side[0] / 2.0), (ccd_real)(side[1] / 2.0), (ccd_real)(side[2] / 2.0)};
-    int best = INT_MAX;
-    double bd = 0.0;
-    V3 bn{0, 0, 0}, bp{0, 0, 0};
     for (int cl = c0; cl < c1; ++cl) {
       const cptr<double> bx = w.mesh_node + 6 * (size_t)cl;
       bool away = false;
@@ -5785,31 +5954,34 @@ __device__ bool mesh_octree_first_contact(const DevWorld& w, int gm, const SE3& 
       for (int t = w.mesh_link[2 * cl]; t < t1; ++t) {
         const cptr<double> rec = w.mesh_tri + TR_STRIDE * (size_t)t;
         const int id = (int)rec[TR_ID];
-        if (id >= best) continue;
         bool o2 = false;
         for (int i = 0; i < 3; ++i) o2 |= rec[TR_LO + i] > cm[i] + hm[i] || rec[TR_HI + i] < cm[i] - hm[i];
         if (o2) continue;
         double dp = 0.0;
         V3 n{0, 0, 0}, p{0, 0, 0};
-        if (tri_mpr_penetration(w, w.hull, A, h, B, rec, dp, n, p)) {
-          best = id;
+        if (!tri_mpr_penetration(w, w.hull, A, h, B, rec, dp, n, p)) continue;
+        uint64_t key[kOctKeyWords] = {0ull, 0ull, 0ull, 0ull, 0ull};
+        if (!fcl_gate_octree_mesh(w, go, TO, gm, TM, l, id, key)) continue;
+        bool less = false;
+        for (int k = 0; k < kOctKeyWords; ++k)
+          if (key[k] != best[k]) {
+            less = key[k] < best[k];
+            break;
+          }
+        if (!found || less) {
+          for (int k = 0; k < kOctKeyWords; ++k) best[k] = key[k];
+          found = true;
           bd = dp;
           bn = n;
           bp = p;
         }
       }
     }
-    if (best != INT_MAX) {
-      depth = bd;
-      nd = bn;
-      ps = bp;
-      return true;
-    }
   }
-  depth = 0.0;
-  nd = v3(0, 0, 0);
-  ps = v3(0, 0, 0);
-  return false;
+  depth = found ? bd : 0.0;
+  nd = found ? bn : v3(0, 0, 0);
+  ps = found ? bp : v3(0, 0, 0);
+  return found;
 }
 
 __device__ bool mesh_first_contact(const DevWorld& w, cptr<double> HV, int ga, const SE3& TA, int gb, const SE3& TB,
@@ -7212,6 +7384,40 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
   }
   std::vector<double> oct_leaf(6 * (size_t)std::max<int64_t>(d->n_octree_leaves, 1), 0.0);
   if (d->n_octree_leaves > 0) std::copy(d->octree_leaf, d->octree_leaf + 6 * d->n_octree_leaves, oct_leaf.begin());
+  // each leaf's path down FCL's octree: getRootBV (delta = 2^16 resolution /
+  // 2) halved by computeChildBV until the leaf box (the leaves were cut that
+  // way: host octree.cpp collect, octomap's 16 levels)
+  std::vector<uint64_t> oct_path(std::max<int64_t>(d->n_octree_leaves, 1), 0);
+  std::vector<int> oct_depth(std::max<int64_t>(d->n_octree_leaves, 1), 0);
+  for (int g = 0; g < d->n_geoms; ++g) {
+    if (d->geom_type[g] != MPG_GEOM_OCTREE) continue;
+    const int64_t l0 = (int64_t)d->geom_param[4 * g], ln = (int64_t)d->geom_param[4 * g + 1];
+    const double delta = (double)(1 << 16) * d->geom_param[4 * g + 2] / 2;
+    for (int64_t l = l0; l < l0 + ln; ++l) {
+      const double* L = d->octree_leaf + 6 * l;
+      double lo[3] = {-delta, -delta, -delta}, hi[3] = {delta, delta, delta};
+      uint64_t code = 0;
+      int depth = 0;
+      while (!(lo[0] == L[0] && lo[1] == L[1] && lo[2] == L[2] && hi[0] == L[3] && hi[1] == L[4] && hi[2] == L[5])) {
+        if (++depth > 16)
+          return set_error(MPG_E_INVALID, "octree geometry " + std::to_string(g) + ": leaf " + std::to_string(l - l0) +
+                                              " is not a box of FCL's root-BV halving (getRootBV / computeChildBV)");
+        int ci = 0;
+        for (int k = 0; k < 3; ++k) {
+          const double mid = (lo[k] + hi[k]) * 0.5;
+          if (L[k] >= mid) {
+            ci |= 1 << k;
+            lo[k] = mid;
+          } else {
+            hi[k] = mid;
+          }
+        }
+        code = (code << 3) | (uint64_t)ci;
+      }
+      oct_path[l] = code;
+      oct_depth[l] = depth;
+    }
+  }
   std::vector<double> oct_grid((size_t)OG_STRIDE * std::max(d->n_geoms, 1), 0.0);
   std::vector<int> oct_cells, oct_list;
   for (int g = 0; g < d->n_geoms; ++g) {
@@ -7551,6 +7757,8 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
   const size_t o_ogr = bb.add(oct_grid.data(), oct_grid.size());
   const size_t o_oce = bb.add(oct_cells.data(), oct_cells.size());
   const size_t o_oli = bb.add(oct_list.data(), oct_list.size());
+  const size_t o_opa = bb.add(oct_path.data(), oct_path.size());
+  const size_t o_ode = bb.add(oct_depth.data(), oct_depth.size());
 
   mpg_world* w = new mpg_world();
   w->device = device;
@@ -7685,6 +7893,8 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
   bp.mobj = F(o_bmb);
   bp.sobj = F(o_bsb);
   dw.oct_leaf = to_cptr<double>(base + o_olf);
+  dw.oct_path = to_cptr<uint64_t>(base + o_opa);
+  dw.oct_depth = to_cptr<int>(base + o_ode);
   dw.mesh_tri = to_cptr<double>(base + o_mtr);
   dw.mesh_node = to_cptr<double>(base + o_mnd);
   dw.mesh_link = to_cptr<int>(base + o_mln);
@@ -8275,18 +8485,30 @@ int mpg_distance_batch(mpg_world* w, const double* q, int64_t n, int32_t n_self_
 int mpg_distance_batch_ex(mpg_world* w, const double* q, int64_t n, int32_t n_self_pairs, int32_t flags,
                           double* d_self, int32_t* p_self, double* pts_self, double* d_others, int32_t* p_others,
                           double* pts_others, int mem, void* stream) {
+  mpg_distance_request req;
+  req.flags = flags;
+  req.distance_tolerance = 1e-6;
+  return mpg_distance_batch_req(w, q, n, n_self_pairs, &req, d_self, p_self, pts_self, d_others, p_others, pts_others,
+                                mem, stream);
+}
+
+int mpg_distance_batch_req(mpg_world* w, const double* q, int64_t n, int32_t n_self_pairs,
+                           const mpg_distance_request* req, double* d_self, int32_t* p_self, double* pts_self,
+                           double* d_others, int32_t* p_others, double* pts_others, int mem, void* stream) {
   if (!w) return set_error(MPG_E_INVALID, "world is NULL");
+  if (!req) return set_error(MPG_E_INVALID, "request is NULL");
   if (n < 0) return set_error(MPG_E_INVALID, "n < 0");
   if (n_self_pairs < 0 || n_self_pairs > w->dw.n_pairs) return set_error(MPG_E_INVALID, "bad n_self_pairs");
   if (n > 0 && ((!q && w->dw.dof > 0) || !d_self || !p_self || !d_others || !p_others))
     return set_error(MPG_E_INVALID, "NULL buffer");
   if (mem != MPG_MEM_HOST && mem != MPG_MEM_DEVICE) return set_error(MPG_E_INVALID, "bad mem kind");
+  const int32_t flags = req->flags;
   if (flags & ~(MPG_DISTANCE_SIGNED | MPG_DISTANCE_NEAREST_POINTS)) return set_error(MPG_E_INVALID, "bad flags");
-  if (flags && (w->has_mesh || w->has_octree))
-    return set_error(MPG_E_UNSUPPORTED,
-                     "signed distance / requested nearest points of point-cloud or BVH-mesh pairs are not implemented");
+  if (!(req->distance_tolerance >= 0.0)) return set_error(MPG_E_INVALID, "bad distance_tolerance");
+  const ccd_real tol = (ccd_real)req->distance_tolerance;  // GJKSolver_libccd::distance_tolerance -> ccd.dist_tolerance
   const bool want_pts = pts_self || pts_others;
-  const int mode = (want_pts || flags ? MPG_DIST_POINTS : 0) | (flags & MPG_DISTANCE_SIGNED ? MPG_DIST_SIGNED : 0);
+  const int mode = (want_pts || flags ? MPG_DIST_POINTS : 0) | (flags & MPG_DISTANCE_SIGNED ? MPG_DIST_SIGNED : 0) |
+                   (flags & MPG_DISTANCE_NEAREST_POINTS ? MPG_DIST_NP : 0);
   if (n == 0) return MPG_OK;
   HIP_TRY(hipSetDevice(w->device));
   hipStream_t s = static_cast<hipStream_t>(stream);
@@ -8328,13 +8550,18 @@ int mpg_distance_batch_ex(mpg_world* w, const double* q, int64_t n, int32_t n_se
   hipLaunchKernelGGL((pose_kernel<false>), dim3(grid), dim3(128), 0, s, w->dw, qin, (long long)n, D.poses, D.save64);
   HIP_TRY(hipGetLastError());
   auto launch = [&](auto kern) {
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(128), 0, s, w->dw, D.poses, (long long)n, n_self_pairs, ds, ps, dd, po,
-                       qs, qo);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(128), 0, s, w->dw, D.poses, (long long)n, n_self_pairs, tol, ds, ps, dd,
+                       po, qs, qo);
     return hipGetLastError();
   };
-  if (mode == 0) HIP_TRY(launch(distance_kernel<0>));
-  else if (mode == MPG_DIST_POINTS) HIP_TRY(launch(distance_kernel<MPG_DIST_POINTS>));
-  else HIP_TRY(launch(distance_kernel<MPG_DIST_POINTS | MPG_DIST_SIGNED>));
+  constexpr int P = MPG_DIST_POINTS, SG = MPG_DIST_SIGNED, NPF = MPG_DIST_NP;
+  switch (mode) {
+    case 0: HIP_TRY(launch(distance_kernel<0>)); break;
+    case P: HIP_TRY(launch(distance_kernel<P>)); break;
+    case P | NPF: HIP_TRY(launch(distance_kernel<P | NPF>)); break;
+    case P | SG: HIP_TRY(launch(distance_kernel<P | SG>)); break;
+    default: HIP_TRY(launch(distance_kernel<P | SG | NPF>)); break;
+  }
   if (mem == MPG_MEM_HOST) {
     HIP_TRY(hipMemcpyAsync(d_self, ds, sizeof(double) * n, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipMemcpyAsync(d_others, dd, sizeof(double) * n, hipMemcpyDeviceToHost, s));
@@ -8343,6 +8570,15 @@ int mpg_distance_batch_ex(mpg_world* w, const double* q, int64_t n, int32_t n_se
     if (mode && pts_self) HIP_TRY(hipMemcpyAsync(pts_self, qs, sizeof(double) * 6 * n, hipMemcpyDeviceToHost, s));
     if (mode && pts_others) HIP_TRY(hipMemcpyAsync(pts_others, qo, sizeof(double) * 6 * n, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
+    for (int64_t i = 0; i < n; ++i) {
+      if (p_self[i] == MPG_DISTANCE_FCL_THROWS)
+        return set_error(MPG_E_FAILED, "configuration " + std::to_string(i) +
+                                           ": FCL's libccd EPA throws here (FCL_THROW_FAILED_AT_THIS_CONFIGURATION)");
+      if (p_self[i] == MPG_DISTANCE_EPA_CAPACITY)
+        return set_error(MPG_E_UNSUPPORTED, "configuration " + std::to_string(i) +
+                                                ": EPA polytope beyond the device capacity (" +
+                                                std::to_string(ccdx::kPtV) + " vertices)");
+    }
   }
   return MPG_OK;
 }

@@ -345,7 +345,8 @@ class OracleWorld:
         w.mesh_tri = ia(np.concatenate(tris) if tris else [])
         w.conv_nbr = ia(nbr_all)
         w.bvh = None
-        lib().orc_bvh_build(ctypes.byref(w))  # FCL BVHModel<OBBRSS> trees + shape OBBs
+        if lib().orc_bvh_build(ctypes.byref(w)):  # FCL BVHModel<OBBRSS> trees, octree nodes, shape OBBs
+            raise ValueError("octree leaves off FCL's root-BV halving grid")
         self._w = w
         self.geoms = geoms
         self.dof = len(mg)
@@ -439,12 +440,14 @@ class OracleWorld:
             raise RuntimeError("orc_distance_batch failed")
         return ds, ps, do, po
 
-    def distance_batch_ex(self, q: np.ndarray, signed: bool = False, nearest_points: bool = False):
+    def distance_batch_ex(self, q: np.ndarray, signed: bool = False, nearest_points: bool = False,
+                          distance_tolerance: float = 1e-6):
         """distance_batch with DistanceRequest(enable_signed_distance,
-        enable_nearest_points): (d_self, pair_self, pts_self[n, 6], d_others,
-        pair_others, pts_others[n, 6]); pts = (p1, p2) of the group's minimum
-        pair, world frame.  Point-cloud / BVH-mesh pairs with either option:
-        NotImplementedError (the device refuses them the same way)."""
+        enable_nearest_points, distance_tolerance): (d_self, pair_self,
+        pts_self[n, 6], d_others, pair_others, pts_others[n, 6]); pts =
+        DistanceResult::nearest_points of the group's minimum pair, world frame
+        (oracle/collide_oracle.c pair_distance says which point is which).
+        RuntimeError where FCL throws (FCL_THROW_FAILED_AT_THIS_CONFIGURATION)."""
         q = np.ascontiguousarray(q, dtype=np.float64).reshape(-1, self.dof)
         n = q.shape[0]
         ds, do = np.zeros(n), np.zeros(n)
@@ -453,13 +456,22 @@ class OracleWorld:
         mode = (1 if signed else 0) | (2 if nearest_points else 0)
         rc = lib().orc_distance_batch_ex(ctypes.byref(self._w), q.ctypes.data_as(_DP), ctypes.c_long(n),
                                          ctypes.c_int(self.n_self_pairs), ctypes.c_int(mode),
+                                         ctypes.c_double(distance_tolerance),
                                          ds.ctypes.data_as(_DP), ps.ctypes.data_as(_IP), qs.ctypes.data_as(_DP),
                                          do.ctypes.data_as(_DP), po.ctypes.data_as(_IP), qo.ctypes.data_as(_DP))
-        if rc == -2:
-            raise NotImplementedError("signed distance / nearest points of point-cloud or BVH-mesh pairs")
+        if rc == -3:
+            raise RuntimeError("FCL throws on this configuration (libccd EPA: FCL_THROW_FAILED_AT_THIS_CONFIGURATION)")
         if rc != 0:
             raise RuntimeError("orc_distance_batch_ex failed")
         return ds, ps, qs, do, po, qo
+
+    @staticmethod
+    def epa_stats():
+        """(largest EPA polytope in vertices, convexity-guard stops) over the
+        distance calls since the last read (oracle/fcl_gjk_dist.h)."""
+        g = ctypes.c_int(0)
+        m = lib().orc_epa_stats(ctypes.byref(g))
+        return int(m), int(g.value)
 
     def contact_batch(self, q: np.ndarray):
         """fcl::collide with CollisionRequest(enable_contact=True) on every pair:

@@ -1579,425 +1579,9 @@ static int closed_form_contact(const orc_world *w, int ga, const real *Ta, int g
     return h;
 }
 
-/* ------------------------------------------------ GJK distance
- * PlanningWorld::distance* (src/planning_world.cpp:493-720) calls
- * fcl::distance -> GJKSolver_libccd::shapeDistance -> libccd GJK distance
- * [ext FCL 0.7.0 / libccd 2.1], which returns -1 for penetrating shapes
- * (DistanceRequest() has enable_signed_distance = false).  The north star
- * asks for distances within 1e-5 of the CPU path, not bit equality: this is
- * a plain GJK (Johnson sub-distance via Ericson's closest-point regions) run
- * to 1e-12 relative convergence on the same FCL support mappings, so it
- * lands on the true Euclidean distance; the device runs the same algorithm
- * (mplib_amd/csrc/mpg_kernels.hip gjk_distance). */
-static double d3dot(const double *a, const double *b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
-static void d3sub(double *o, const double *a, const double *b) { o[0] = a[0] - b[0]; o[1] = a[1] - b[1]; o[2] = a[2] - b[2]; }
-static void d3cross(double *o, const double *a, const double *b) {
-    o[0] = a[1] * b[2] - a[2] * b[1]; o[1] = a[2] * b[0] - a[0] * b[2]; o[2] = a[0] * b[1] - a[1] * b[0];
-}
-
-/* closest point of triangle (a, b, c) to the origin; keep[] marks the
- * vertices of the reached feature (Ericson, Real-Time Collision Detection 5.1.5) */
-static void tri_closest(const double *a, const double *b, const double *c, double *v, int keep[3]) {
-    double ab[3], ac[3], bc[3];
-    d3sub(ab, b, a); d3sub(ac, c, a);
-    const double d1 = -d3dot(ab, a), d2 = -d3dot(ac, a);
-    keep[0] = keep[1] = keep[2] = 0;
-    if (d1 <= 0 && d2 <= 0) { memcpy(v, a, 24); keep[0] = 1; return; }
-    const double d3 = -d3dot(ab, b), d4 = -d3dot(ac, b);
-    if (d3 >= 0 && d4 <= d3) { memcpy(v, b, 24); keep[1] = 1; return; }
-    const double vc = d1 * d4 - d3 * d2;
-    if (vc <= 0 && d1 >= 0 && d3 <= 0) {
-        const double t = d1 / (d1 - d3);
-        for (int i = 0; i < 3; ++i) v[i] = a[i] + t * ab[i];
-        keep[0] = keep[1] = 1; return;
-    }
-    const double d5 = -d3dot(ab, c), d6 = -d3dot(ac, c);
-    if (d6 >= 0 && d5 <= d6) { memcpy(v, c, 24); keep[2] = 1; return; }
-    const double vb = d5 * d2 - d1 * d6;
-    if (vb <= 0 && d2 >= 0 && d6 <= 0) {
-        const double t = d2 / (d2 - d6);
-        for (int i = 0; i < 3; ++i) v[i] = a[i] + t * ac[i];
-        keep[0] = keep[2] = 1; return;
-    }
-    const double va = d3 * d6 - d5 * d4;
-    if (va <= 0 && (d4 - d3) >= 0 && (d5 - d6) >= 0) {
-        const double t = (d4 - d3) / ((d4 - d3) + (d5 - d6));
-        d3sub(bc, c, b);
-        for (int i = 0; i < 3; ++i) v[i] = b[i] + t * bc[i];
-        keep[1] = keep[2] = 1; return;
-    }
-    const double den = 1.0 / (va + vb + vc), t1 = vb * den, t2 = vc * den;
-    for (int i = 0; i < 3; ++i) v[i] = a[i] + ab[i] * t1 + ac[i] * t2;
-    keep[0] = keep[1] = keep[2] = 1;
-}
-
-/* simplex P[0..n) -> closest point v, reduced simplex; 1 if it encloses the origin */
-static int simplex_closest(double P[4][3], int *n, double *v) {
-    if (*n == 1) { memcpy(v, P[0], 24); return 0; }
-    if (*n == 2) {
-        double ab[3];
-        d3sub(ab, P[1], P[0]);
-        const double den = d3dot(ab, ab), t = den > 0 ? -d3dot(P[0], ab) / den : 0.0;
-        if (t <= 0) { memcpy(v, P[0], 24); *n = 1; return 0; }
-        if (t >= 1) { memcpy(v, P[1], 24); memcpy(P[0], P[1], 24); *n = 1; return 0; }
-        for (int i = 0; i < 3; ++i) v[i] = P[0][i] + t * ab[i];
-        return 0;
-    }
-    if (*n == 3) {
-        int keep[3];
-        tri_closest(P[0], P[1], P[2], v, keep);
-        int m = 0;
-        for (int k = 0; k < 3; ++k) if (keep[k]) { if (m != k) memcpy(P[m], P[k], 24); ++m; }
-        *n = m;
-        return 0;
-    }
-    /* tetrahedron: faces whose plane separates the origin from the 4th vertex */
-    static const int F[4][4] = {{0, 1, 2, 3}, {0, 2, 3, 1}, {0, 3, 1, 2}, {1, 3, 2, 0}};
-    double best = DBL_MAX, bv[3] = {0, 0, 0}, BP[3][3];
-    int bn = -1, any = 0;
-    for (int f = 0; f < 4; ++f) {
-        const double *a = P[F[f][0]], *b = P[F[f][1]], *c = P[F[f][2]], *d = P[F[f][3]];
-        double ab[3], ac[3], nrm[3], ad[3];
-        d3sub(ab, b, a); d3sub(ac, c, a); d3cross(nrm, ab, ac); d3sub(ad, d, a);
-        const double sp = -d3dot(a, nrm), sd = d3dot(ad, nrm);
-        if (!(sp * sd < 0 || sd == 0.0)) continue;
-        any = 1;
-        double fv[3];
-        int keep[3];
-        tri_closest(a, b, c, fv, keep);
-        const double dd = d3dot(fv, fv);
-        if (dd < best) {
-            best = dd; memcpy(bv, fv, 24); bn = 0;
-            const double *abc[3] = {a, b, c};
-            for (int k = 0; k < 3; ++k) if (keep[k]) memcpy(BP[bn++], abc[k], 24);
-        }
-    }
-    if (!any) return 1;
-    for (int k = 0; k < bn; ++k) memcpy(P[k], BP[k], 24);
-    *n = bn;
-    memcpy(v, bv, 24);
-    return 0;
-}
-
-static double gjk_distance(const gjk_obj *o1, const gjk_obj *o2) {
-    ccd_vec3_t c1, c2;
-    gjk_center(o1, &c1);
-    gjk_center(o2, &c2);
-    double v[3] = {c1.v[0] - c2.v[0], c1.v[1] - c2.v[1], c1.v[2] - c2.v[2]};
-    if (d3dot(v, v) == 0.0) v[0] = 1e-12;
-    double P[4][3];
-    int n = 0;
-    for (int it = 0; it < 128; ++it) {
-        ccd_vec3_t dir;
-        ccd_support_t sp;
-        ccdVec3Set(&dir, -v[0], -v[1], -v[2]);
-        ccd_support(o1, o2, &dir, &sp);
-        const double w[3] = {sp.v.v[0], sp.v.v[1], sp.v.v[2]};
-        const double vv = d3dot(v, v), vw = d3dot(v, w);
-        if (n > 0 && vv - vw <= 1e-12 * vv) break;
-        int dup = 0;
-        for (int k = 0; k < n; ++k) dup |= (P[k][0] == w[0] && P[k][1] == w[1] && P[k][2] == w[2]);
-        if (dup) break;
-        memcpy(P[n++], w, 24);
-        if (simplex_closest(P, &n, v)) return -1.0;
-        const double nv = d3dot(v, v);
-        if (nv <= 1e-24) return -1.0;
-        if (n > 1 && nv >= vv) break;
-    }
-    return sqrt(d3dot(v, v));
-}
-
-/* ------------------------------------------- nearest points, signed distance
- * FCL 0.7.0's distance leaf (ShapeDistanceTraversalNode::leafTesting [ext])
- * asks GJKSolver_libccd for the distance AND the closest points of the two
- * shapes, in the world frame (libccd_extension ccdGJKDist2 ->
- * extractClosestPoints: the barycentric weights of the origin's projection on
- * the final simplex applied to the supports of each shape), and with
- * DistanceRequest(enable_signed_distance=True) runs ccdGJKSignedDist: GJK, and
- * for intersecting shapes EPA, depth = -(distance from the origin to the
- * Minkowski difference boundary), points from penEPAPosClosest (the same
- * barycentric reconstruction on the nearest polytope face).
- * Restated here on the same float supports as gjk_distance: gjk_query runs
- * gjk_distance's iteration with identical arithmetic for v (so its distance is
- * gjk_distance's, bit for bit) and carries each simplex vertex's two supports
- * and barycentric weights; epa_depth is a textbook EPA in fp64 from GJK's
- * enclosing tetrahedron, run to 1e-10 m (FCL's float EPA stops at libccd's
- * epa_tolerance 1e-4: the depths agree within that).  Device twin:
- * mplib_amd/csrc/mpg_kernels.hip gjk_query / epa_depth. */
-typedef struct { double w[3], a[3], b[3]; } gsv;
-
-static void tri_closest_l(const double *a, const double *b, const double *c, double *v, int keep[3], double lam[3]) {
-    tri_closest(a, b, c, v, keep);
-    /* the weights of the feature tri_closest reached (same case analysis) */
-    double ab[3], ac[3];
-    d3sub(ab, b, a); d3sub(ac, c, a);
-    lam[0] = lam[1] = lam[2] = 0.0;
-    const double d1 = -d3dot(ab, a), d2 = -d3dot(ac, a);
-    if (d1 <= 0 && d2 <= 0) { lam[0] = 1.0; return; }
-    const double d3 = -d3dot(ab, b), d4 = -d3dot(ac, b);
-    if (d3 >= 0 && d4 <= d3) { lam[1] = 1.0; return; }
-    const double vc = d1 * d4 - d3 * d2;
-    if (vc <= 0 && d1 >= 0 && d3 <= 0) { const double t = d1 / (d1 - d3); lam[0] = 1.0 - t; lam[1] = t; return; }
-    const double d5 = -d3dot(ab, c), d6 = -d3dot(ac, c);
-    if (d6 >= 0 && d5 <= d6) { lam[2] = 1.0; return; }
-    const double vb = d5 * d2 - d1 * d6;
-    if (vb <= 0 && d2 >= 0 && d6 <= 0) { const double t = d2 / (d2 - d6); lam[0] = 1.0 - t; lam[2] = t; return; }
-    const double va = d3 * d6 - d5 * d4;
-    if (va <= 0 && (d4 - d3) >= 0 && (d5 - d6) >= 0) {
-        const double t = (d4 - d3) / ((d4 - d3) + (d5 - d6));
-        lam[1] = 1.0 - t; lam[2] = t; return;
-    }
-    const double den = 1.0 / (va + vb + vc), t1 = vb * den, t2 = vc * den;
-    lam[0] = 1.0 - t1 - t2; lam[1] = t1; lam[2] = t2;
-}
-
-/* simplex_closest with the supports carried along; lam: weights of the kept vertices */
-static int simplex_closest_s(gsv S[4], int *n, double *v, double lam[4]) {
-    if (*n == 1) { memcpy(v, S[0].w, 24); lam[0] = 1.0; return 0; }
-    if (*n == 2) {
-        double ab[3];
-        d3sub(ab, S[1].w, S[0].w);
-        const double den = d3dot(ab, ab), t = den > 0 ? -d3dot(S[0].w, ab) / den : 0.0;
-        if (t <= 0) { memcpy(v, S[0].w, 24); *n = 1; lam[0] = 1.0; return 0; }
-        if (t >= 1) { memcpy(v, S[1].w, 24); S[0] = S[1]; *n = 1; lam[0] = 1.0; return 0; }
-        for (int i = 0; i < 3; ++i) v[i] = S[0].w[i] + t * ab[i];
-        lam[0] = 1.0 - t; lam[1] = t;
-        return 0;
-    }
-    if (*n == 3) {
-        int keep[3];
-        double l3[3];
-        tri_closest_l(S[0].w, S[1].w, S[2].w, v, keep, l3);
-        int m = 0;
-        for (int k = 0; k < 3; ++k) if (keep[k]) { if (m != k) S[m] = S[k]; lam[m] = l3[k]; ++m; }
-        *n = m;
-        return 0;
-    }
-    static const int F[4][4] = {{0, 1, 2, 3}, {0, 2, 3, 1}, {0, 3, 1, 2}, {1, 3, 2, 0}};
-    double best = DBL_MAX, bv[3] = {0, 0, 0}, bl[3] = {0, 0, 0};
-    gsv BP[3];
-    int bn = -1, any = 0;
-    for (int f = 0; f < 4; ++f) {
-        const double *a = S[F[f][0]].w, *b = S[F[f][1]].w, *c = S[F[f][2]].w, *d = S[F[f][3]].w;
-        double ab[3], ac[3], nrm[3], ad[3];
-        d3sub(ab, b, a); d3sub(ac, c, a); d3cross(nrm, ab, ac); d3sub(ad, d, a);
-        const double sp = -d3dot(a, nrm), sd = d3dot(ad, nrm);
-        if (!(sp * sd < 0 || sd == 0.0)) continue;
-        any = 1;
-        double fv[3], l3[3];
-        int keep[3];
-        tri_closest_l(a, b, c, fv, keep, l3);
-        const double dd = d3dot(fv, fv);
-        if (dd < best) {
-            best = dd; memcpy(bv, fv, 24); bn = 0;
-            for (int k = 0; k < 3; ++k) if (keep[k]) { BP[bn] = S[F[f][k]]; bl[bn] = l3[k]; ++bn; }
-        }
-    }
-    if (!any) return 1;
-    for (int k = 0; k < bn; ++k) { S[k] = BP[k]; lam[k] = bl[k]; }
-    *n = bn;
-    memcpy(v, bv, 24);
-    return 0;
-}
-
-static void gsv_support(const gjk_obj *o1, const gjk_obj *o2, const double *d, gsv *out) {
-    ccd_vec3_t dir;
-    ccd_support_t sp;
-    ccdVec3Set(&dir, d[0], d[1], d[2]);
-    ccd_support(o1, o2, &dir, &sp);
-    for (int i = 0; i < 3; ++i) { out->w[i] = sp.v.v[i]; out->a[i] = sp.v1.v[i]; out->b[i] = sp.v2.v[i]; }
-}
-
-/* EPA from the enclosing tetrahedron S[0..3]: depth (>= 0) and the witness
- * points on each shape (world frame). */
-#define EPA_MAXV 64
-#define EPA_MAXF 128
-typedef struct { int v[3]; double n[3], d; int alive; } epa_face;
-
-static int epa_face_set(const gsv *V, int i, int j, int k, epa_face *f) {
-    double e1[3], e2[3], n[3];
-    d3sub(e1, V[j].w, V[i].w); d3sub(e2, V[k].w, V[i].w); d3cross(n, e1, e2);
-    const double l = sqrt(d3dot(n, n));
-    if (!(l > 0.0)) return 0;
-    for (int c = 0; c < 3; ++c) f->n[c] = n[c] / l;
-    f->v[0] = i; f->v[1] = j; f->v[2] = k;
-    f->d = d3dot(f->n, V[i].w);
-    f->alive = 1;
-    return 1;
-}
-
-static double epa_finish(const gsv *V, const epa_face *f, double *p1, double *p2);
-
-static double epa_depth(const gjk_obj *o1, const gjk_obj *o2, const gsv S[4], double *p1, double *p2) {
-    gsv V[EPA_MAXV];
-    epa_face F[EPA_MAXF];
-    int nv = 4, nf = 0;
-    for (int k = 0; k < 4; ++k) V[k] = S[k];
-    static const int T[4][4] = {{0, 1, 2, 3}, {0, 3, 1, 2}, {0, 2, 3, 1}, {1, 3, 2, 0}};
-    for (int t = 0; t < 4; ++t) {
-        int i = T[t][0], j = T[t][1], k = T[t][2];
-        const int l = T[t][3];
-        double e1[3], e2[3], n[3], dl[3];
-        d3sub(e1, V[j].w, V[i].w); d3sub(e2, V[k].w, V[i].w); d3cross(n, e1, e2); d3sub(dl, V[l].w, V[i].w);
-        if (d3dot(n, dl) > 0.0) { const int x = j; j = k; k = x; } /* outward: away from the 4th vertex */
-        if (!epa_face_set(V, i, j, k, &F[nf])) return -1.0;
-        ++nf;
-    }
-    epa_face fb; /* the nearest face of the current polytope */
-    for (int it = 0; it < 128; ++it) {
-        int best = -1;
-        for (int f = 0; f < nf; ++f)
-            if (F[f].alive && (best < 0 || F[f].d < F[best].d)) best = f;
-        if (best < 0) return -1.0;
-        fb = F[best];
-        gsv s;
-        gsv_support(o1, o2, fb.n, &s);
-        if (d3dot(s.w, fb.n) - fb.d <= 1e-10 || nv >= EPA_MAXV) break;
-        int dup = 0;
-        for (int k = 0; k < nv; ++k) dup |= (V[k].w[0] == s.w[0] && V[k].w[1] == s.w[1] && V[k].w[2] == s.w[2]);
-        if (dup) break;
-        const int si = nv;
-        V[nv++] = s;
-        /* faces that see the new vertex go; their unshared edges form the horizon */
-        int edges[EPA_MAXF][2], ne = 0;
-        for (int f = 0; f < nf; ++f) {
-            if (!F[f].alive) continue;
-            double ds[3];
-            d3sub(ds, s.w, V[F[f].v[0]].w);
-            if (d3dot(F[f].n, ds) <= 0.0) continue;
-            F[f].alive = 0;
-            for (int e = 0; e < 3; ++e) {
-                const int a = F[f].v[e], b = F[f].v[(e + 1) % 3];
-                int found = -1;
-                for (int x = 0; x < ne; ++x) if (edges[x][0] == b && edges[x][1] == a) { found = x; break; }
-                if (found >= 0) { edges[found][0] = edges[ne - 1][0]; edges[found][1] = edges[ne - 1][1]; --ne; }
-                else if (ne < EPA_MAXF) { edges[ne][0] = a; edges[ne][1] = b; ++ne; }
-                else return epa_finish(V, &fb, p1, p2); /* horizon beyond capacity: stop here */
-            }
-        }
-        /* new faces take the dead slots first (in index order), then the end */
-        int slot = 0, full = 0;
-        for (int x = 0; x < ne && !full; ++x) {
-            while (slot < nf && F[slot].alive) ++slot;
-            if (slot == nf) {
-                if (nf == EPA_MAXF) { full = 1; break; }
-                ++nf;
-            }
-            if (!epa_face_set(V, edges[x][0], edges[x][1], si, &F[slot])) F[slot].alive = 0;
-        }
-        if (full) return epa_finish(V, &fb, p1, p2);
-    }
-    return epa_finish(V, &fb, p1, p2);
-}
-
-/* the nearest face f: witness = d n, its barycentric weights on the face
- * applied to each shape's supports */
-static double epa_finish(const gsv *V, const epa_face *f, double *p1, double *p2) {
-    const double *a = V[f->v[0]].w, *b = V[f->v[1]].w, *c = V[f->v[2]].w;
-    double pw[3] = {f->d * f->n[0], f->d * f->n[1], f->d * f->n[2]}, v0[3], v1[3], v2[3];
-    d3sub(v0, b, a); d3sub(v1, c, a); d3sub(v2, pw, a);
-    const double d00 = d3dot(v0, v0), d01 = d3dot(v0, v1), d11 = d3dot(v1, v1), d20 = d3dot(v2, v0), d21 = d3dot(v2, v1);
-    const double den = d00 * d11 - d01 * d01;
-    double lb = den != 0.0 ? (d11 * d20 - d01 * d21) / den : 0.0, lc = den != 0.0 ? (d00 * d21 - d01 * d20) / den : 0.0;
-    const double la = 1.0 - lb - lc;
-    for (int i = 0; i < 3; ++i) {
-        p1[i] = (la * V[f->v[0]].a[i] + lb * V[f->v[1]].a[i]) + lc * V[f->v[2]].a[i];
-        p2[i] = (la * V[f->v[0]].b[i] + lb * V[f->v[1]].b[i]) + lc * V[f->v[2]].b[i];
-    }
-    return f->d;
-}
-
-/* S[0..n) with the origin on it (n < 4, or a flat tetrahedron) -> a
- * tetrahedron of Minkowski-difference supports that contains the origin:
- * extra supports along directions off the simplex (libccd's
- * simplexToPolytope2/3 idea: axes, then the triangle's normal, both sides,
- * the farther one).  0 if the difference is flat there (shapes touching). */
-static int blow_up(const gjk_obj *o1, const gjk_obj *o2, gsv S[4], int n) {
-    static const double ax[6][3] = {{1, 0, 0}, {-1, 0, 0}, {0, 1, 0}, {0, -1, 0}, {0, 0, 1}, {0, 0, -1}};
-    if (n == 4) n = 3; /* a flat tetrahedron: rebuild from its first triangle */
-    while (n < 3) {
-        int grown = 0;
-        for (int k = 0; k < 6 && !grown; ++k) {
-            gsv s;
-            gsv_support(o1, o2, ax[k], &s);
-            double e[3], u[3], c[3];
-            d3sub(e, s.w, S[0].w);
-            if (n == 1) { if (d3dot(e, e) > 1e-20) { S[n++] = s; grown = 1; } continue; }
-            d3sub(u, S[1].w, S[0].w);
-            d3cross(c, u, e);
-            if (d3dot(c, c) > 1e-20 * d3dot(u, u)) { S[n++] = s; grown = 1; }
-        }
-        if (!grown) return 0;
-    }
-    double e1[3], e2[3], nr[3];
-    d3sub(e1, S[1].w, S[0].w); d3sub(e2, S[2].w, S[0].w); d3cross(nr, e1, e2);
-    const double l = sqrt(d3dot(nr, nr));
-    if (!(l > 0.0)) return 0;
-    for (int i = 0; i < 3; ++i) nr[i] /= l;
-    const double nn[3] = {-nr[0], -nr[1], -nr[2]};
-    gsv sp, sm;
-    gsv_support(o1, o2, nr, &sp);
-    gsv_support(o1, o2, nn, &sm);
-    double dp[3], dm[3];
-    d3sub(dp, sp.w, S[0].w); d3sub(dm, sm.w, S[0].w);
-    const double hp = d3dot(dp, nr), hm = -d3dot(dm, nr);
-    if (!(hp > 1e-12 || hm > 1e-12)) return 0;
-    S[3] = hp >= hm ? sp : sm;
-    return 1;
-}
-
-/* gjk_distance with the nearest points (world frame) and, when sgn, the
- * signed distance of intersecting shapes (-EPA depth; 0 when the origin lies
- * on the simplex).  Unsigned and intersecting: -1 and zero points, as
- * ccdGJKDist2 leaves them. */
-static double gjk_query(const gjk_obj *o1, const gjk_obj *o2, int sgn, double *p1, double *p2) {
-    ccd_vec3_t c1, c2;
-    gjk_center(o1, &c1);
-    gjk_center(o2, &c2);
-    double v[3] = {c1.v[0] - c2.v[0], c1.v[1] - c2.v[1], c1.v[2] - c2.v[2]};
-    if (d3dot(v, v) == 0.0) v[0] = 1e-12;
-    gsv S[4];
-    double lam[4] = {0, 0, 0, 0};
-    int n = 0;
-    memset(p1, 0, 24); memset(p2, 0, 24);
-    for (int it = 0; it < 128; ++it) {
-        gsv s;
-        const double nd[3] = {-v[0], -v[1], -v[2]};
-        gsv_support(o1, o2, nd, &s);
-        const double vv = d3dot(v, v), vw = d3dot(v, s.w);
-        if (n > 0 && vv - vw <= 1e-12 * vv) break;
-        int dup = 0;
-        for (int k = 0; k < n; ++k) dup |= (S[k].w[0] == s.w[0] && S[k].w[1] == s.w[1] && S[k].w[2] == s.w[2]);
-        if (dup) break;
-        S[n++] = s;
-        if (simplex_closest_s(S, &n, v, lam)) {
-            if (!sgn) return -1.0;
-            const double dep = epa_depth(o1, o2, S, p1, p2);
-            return dep >= 0.0 ? -dep : 0.0;
-        }
-        const double nv = d3dot(v, v);
-        if (nv <= 1e-24) {
-            if (!sgn) return -1.0;
-            /* the origin lies on the simplex: grow it to a tetrahedron around
-             * the origin, then EPA (0 when the shapes only touch) */
-            if (blow_up(o1, o2, S, n)) {
-                const double dep = epa_depth(o1, o2, S, p1, p2);
-                if (dep >= 0.0) return -dep;
-            }
-            for (int i = 0; i < 3; ++i) {
-                p1[i] = 0.0; p2[i] = 0.0;
-                for (int k = 0; k < n; ++k) { p1[i] += lam[k] * S[k].a[i]; p2[i] += lam[k] * S[k].b[i]; }
-            }
-            return 0.0;
-        }
-        if (n > 1 && nv >= vv) break;
-    }
-    for (int i = 0; i < 3; ++i) {
-        p1[i] = 0.0; p2[i] = 0.0;
-        for (int k = 0; k < n; ++k) { p1[i] += lam[k] * S[k].a[i]; p2[i] += lam[k] * S[k].b[i]; }
-    }
-    return sqrt(d3dot(v, v));
-}
+/* FCL 0.7.0 GJK shape distance on float libccd, closed-form shape distances
+ * (fcl_gjk_dist.h: GJKDistance / GJKSignedDistance, ShapeDistanceLibccdImpl) */
+#include "fcl_gjk_dist.h"
 
 /* ------------------------------------------------------- world collide */
 static void make_obj(const orc_world *w, int geom, const real *T, gjk_obj *o, orc_stats *st) {
@@ -2368,9 +1952,17 @@ typedef struct {
     int first_child, first_prim, num_prim; /* first_child < 0: leaf of triangle -(first_child + 1) */
 } bvh_node;
 typedef struct { int n_nodes; bvh_node *nodes; int *prim; } bvh_tree;
+/* an fcl::OcTree rebuilt from its occupied leaves (octree_build) */
+typedef struct {
+    double lo[3], hi[3]; /* AABB from getRootBV / computeChildBV */
+    int child[8];        /* node index, -1: no such child (nodeChildExists false) */
+    int leaf;            /* occupied leaf index, -1 for inner nodes */
+} oct_node;
+typedef struct { int n_nodes; oct_node *nodes; } oct_tree;
 typedef struct {
     bvh_tree *tree;     /* [n_geom] (n_nodes 0 for non-mesh geometries) */
     double (*sobb)[15]; /* [n_geom] computeBV<OBB>(shape, identity): axis 9, To 3, extent 3 */
+    oct_tree *oct;      /* [n_geom] (n_nodes 0 for non-octree geometries) */
 } orc_bvh;
 
 /* eigen_old (fcl/math/geometry-inl.h): Jacobi rotations of a symmetric 3x3;
@@ -2577,12 +2169,74 @@ static void shape_obb(const orc_world *w, int g, double *o) {
     }
 }
 
+/* computeChildBV (octree_solver-inl.h [ext FCL 0.7.0]) */
+static void oct_child_bv(const double *lo, const double *hi, int i, double *clo, double *chi) {
+    for (int k = 0; k < 3; ++k) {
+        const double mid = (lo[k] + hi[k]) * 0.5;
+        if (i & (1 << k)) { clo[k] = mid; chi[k] = hi[k]; }
+        else { clo[k] = lo[k]; chi[k] = mid; }
+    }
+}
+
+/* The tree behind an OcTree geometry's occupied leaves: FCL's getRootBV
+ * (delta = (1 << 16) * resolution / 2, octomap's 16 levels) halved by
+ * computeChildBV down to each leaf box.  MPlib's point clouds only hold
+ * hits, so every node on a leaf's path is occupied (octomap keeps a parent
+ * at its children's maximum log-odds) and the nodes that exist are exactly
+ * the ancestors of occupied leaves.  0, or -1 for a leaf off that grid. */
+static int octree_build(const orc_world *w, int g, oct_tree *O) {
+    const int l0 = (int)w->geom_param[4 * g], ln = (int)w->geom_param[4 * g + 1];
+    const double delta = (double)(1 << 16) * w->geom_param[4 * g + 2] / 2;
+    int cap = 64;
+    O->nodes = malloc(sizeof(oct_node) * (size_t)cap);
+    O->n_nodes = 1;
+    oct_node *r = &O->nodes[0];
+    for (int k = 0; k < 3; ++k) { r->lo[k] = -delta; r->hi[k] = delta; }
+    for (int i = 0; i < 8; ++i) r->child[i] = -1;
+    r->leaf = -1;
+    for (int l = l0; l < l0 + ln; ++l) {
+        const real *L = w->oct_leaf + 6 * (size_t)l;
+        int cur = 0, depth = 0;
+        for (;;) {
+            oct_node *c = &O->nodes[cur];
+            if (c->lo[0] == L[0] && c->lo[1] == L[1] && c->lo[2] == L[2] && c->hi[0] == L[3] && c->hi[1] == L[4] &&
+                c->hi[2] == L[5]) {
+                c->leaf = l;
+                break;
+            }
+            if (++depth > 16) return -1;
+            int i = 0;
+            for (int k = 0; k < 3; ++k)
+                if (L[k] >= (c->lo[k] + c->hi[k]) * 0.5) i |= 1 << k;
+            if (c->child[i] < 0) {
+                if (O->n_nodes == cap) {
+                    cap *= 2;
+                    O->nodes = realloc(O->nodes, sizeof(oct_node) * (size_t)cap);
+                    c = &O->nodes[cur];
+                }
+                const int nn = O->n_nodes++;
+                oct_node *m = &O->nodes[nn];
+                oct_child_bv(c->lo, c->hi, i, m->lo, m->hi);
+                for (int j = 0; j < 8; ++j) m->child[j] = -1;
+                m->leaf = -1;
+                c->child[i] = nn;
+            }
+            cur = c->child[i];
+        }
+    }
+    return 0;
+}
+
 int orc_bvh_build(orc_world *w) {
     orc_bvh *B = calloc(1, sizeof *B);
     B->tree = calloc((size_t)w->n_geom, sizeof(bvh_tree));
     B->sobb = calloc((size_t)w->n_geom, sizeof *B->sobb);
+    B->oct = calloc((size_t)w->n_geom, sizeof(oct_tree));
+    int rc = 0;
     for (int g = 0; g < w->n_geom; ++g) {
         shape_obb(w, g, B->sobb[g]);
+        if (w->geom_type[g] == GEOM_OCTREE && octree_build(w, g, &B->oct[g])) rc = -1;
+
         if (w->geom_type[g] != GEOM_MESH) continue;
         const int t0 = (int)w->geom_param[4 * g], tn = (int)w->geom_param[4 * g + 1];
         if (tn <= 0) continue;
@@ -2594,14 +2248,14 @@ int orc_bvh_build(orc_world *w) {
         bvh_recurse(T, w->verts + 3 * (size_t)w->geom_vstart[g], w->mesh_tri + 3 * (size_t)t0, 0, 0, tn);
     }
     w->bvh = B;
-    return 0;
+    return rc;
 }
 
 void orc_bvh_free(orc_world *w) {
     orc_bvh *B = w->bvh;
     if (!B) return;
-    for (int g = 0; g < w->n_geom; ++g) { free(B->tree[g].nodes); free(B->tree[g].prim); }
-    free(B->tree); free(B->sobb); free(B);
+    for (int g = 0; g < w->n_geom; ++g) { free(B->tree[g].nodes); free(B->tree[g].prim); free(B->oct[g].nodes); }
+    free(B->tree); free(B->sobb); free(B->oct); free(B);
     w->bvh = NULL;
 }
 
@@ -2839,54 +2493,87 @@ static void leaf_box_obj(const real side[3], const real TL[12], gjk_obj *box) {
 
 /* fcl::collide(mesh, OcTree) in either order [ext FCL 0.7.0
  * OcTreeSolver::OcTreeMeshIntersectRecurse; MeshOcTreeIntersect calls it with
- * the tree first]: the leaf test is shapeTriangleIntersect(Box(leaf), box_tf,
- * P1, P2, P3, tf_mesh) -- libccd MPR with the leaf box first and the triangle
- * GJK object second (there is no box-triangle closed form in
- * GJKSolver_libccd).  The traversal only prunes disjoint bounding volumes, so
- * the answer is "some (occupied leaf, triangle) pair's MPR reports a hit";
- * here every pair whose bounding spheres lie within libccd's false-hit reach
- * is run (as mesh_shape_intersect does for shapes). */
-static int mesh_octree_intersect(const orc_world *w, int gm, const real *TM, int go, const real *TO, orc_stats *st) {
-    const int t0 = (int)w->geom_param[4 * gm], tn = (int)w->geom_param[4 * gm + 1];
-    const int l0 = (int)w->geom_param[4 * go], ln = (int)w->geom_param[4 * go + 1];
-    if (tn <= 0 || ln <= 0) return 0;
-    real (*Wt)[9] = malloc(sizeof(real) * 9 * (size_t)tn);
-    real (*S)[4] = malloc(sizeof(real) * 4 * (size_t)tn);
-    mesh_world_tris(w, gm, TM, Wt, S);
-    real lo[3], hi[3];  /* the mesh's world AABB -> one sphere around it */
-    for (int k = 0; k < 3; ++k) { lo[k] = DBL_MAX; hi[k] = -DBL_MAX; }
-    for (int t = 0; t < tn; ++t)
-        for (int v = 0; v < 3; ++v)
-            for (int k = 0; k < 3; ++k) { lo[k] = fmin(lo[k], Wt[t][3 * v + k]); hi[k] = fmax(hi[k], Wt[t][3 * v + k]); }
-    real mc[3], dm[3];
-    for (int k = 0; k < 3; ++k) { mc[k] = (lo[k] + hi[k]) * 0.5; dm[k] = hi[k] - lo[k]; }
-    const real mr = 0.5 * sqrt(dot3(dm, dm)) * (1.0 + 1e-9) + 1e-9;
-    const real pad = 1.001 * sqrt(sqrt((double)CCD_EPS)) + 1e-5 * (1.0 + fabs(TO[9]) + fabs(TO[10]) + fabs(TO[11]) +
-                                                                 fabs(TM[9]) + fabs(TM[10]) + fabs(TM[11]));
+ * the tree first]: the octree's nodes (octree_build) and the mesh's
+ * BVHModel<OBBRSS> nodes are walked together.  Every node pair is tested with
+ * OBB::overlap of the two world OBBs -- convertBV(AABB, tf_tree): To = tf *
+ * centre, axis = R, extent = half sizes; convertBV(OBBRSS, tf_mesh): To = tf *
+ * To, axis = R axis -- and a pair that fails ends that branch.  The octree
+ * node is descended (its existing children 0..7) when the mesh node is a leaf
+ * or the octree node has children and AABB::size() (full width squared) >
+ * OBB::size() (half extents squared); else the mesh node (left, then right).
+ * A (leaf, leaf) pair runs shapeTriangleIntersect(Box(leaf), box_tf, P1, P2,
+ * P3, tf_mesh): libccd MPR with the leaf box first (mpr_penetration with
+ * contacts).  The first pair that hits ends the walk (num_max_contacts 1). */
+typedef struct {
+    const orc_world *w;
+    const oct_tree *O;
+    const bvh_tree *T;
+    int gm, contact;
+    const real *TO, *TM;
     gjk_obj frame;
-    memset(&frame, 0, sizeof frame);
-    shape_to_gjk(TM, &frame);
-    frame.stats = st;
-    int hit = 0;
-    for (int l = l0; l < l0 + ln && !hit; ++l) {
+    orc_stats *st;
+    real *depth, *normal, *pos;
+} om_ctx;
+
+static int octmesh_overlap(const om_ctx *c, const oct_node *a, const bvh_node *b) {
+    const real *TO = c->TO, *TM = c->TM;
+    double ctr[3], To1[3], ext1[3], To2[3], ax2[9], t[3], T[3], R[9];
+    for (int k = 0; k < 3; ++k) { ctr[k] = (a->lo[k] + a->hi[k]) * 0.5; ext1[k] = (a->hi[k] - a->lo[k]) * 0.5; }
+    tf_point(TO, ctr, To1);
+    tf_point(TM, b->To, To2);
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j)
+            ax2[3 * i + j] = (TM[3 * i] * b->axis[j] + TM[3 * i + 1] * b->axis[3 + j]) + TM[3 * i + 2] * b->axis[6 + j];
+    for (int k = 0; k < 3; ++k) t[k] = To2[k] - To1[k];
+    for (int i = 0; i < 3; ++i) T[i] = (TO[i] * t[0] + TO[3 + i] * t[1]) + TO[6 + i] * t[2];
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) R[3 * i + j] = (TO[i] * ax2[j] + TO[3 + i] * ax2[3 + j]) + TO[6 + i] * ax2[6 + j];
+    return !obb_disjoint(R, T, ext1, b->ext);
+}
+
+static int octmesh_rec(om_ctx *c, int n1, int n2) {
+    const oct_node *a = &c->O->nodes[n1];
+    const bvh_node *b = &c->T->nodes[n2];
+    int leaf1 = 1;
+    for (int i = 0; i < 8; ++i) leaf1 &= a->child[i] < 0;
+    const int leaf2 = b->first_child < 0;
+    if (!octmesh_overlap(c, a, b)) return 0;
+    if (leaf1 && leaf2) {
         real side[3], TL[12];
-        octree_leaf_box(w, l, TO, side, TL);
-        const real rl = 0.5 * sqrt(dot3(side, side)) * (1.0 + 1e-9) + 1e-9;
-        const real dc[3] = {TL[9] - mc[0], TL[10] - mc[1], TL[11] - mc[2]};
-        if (sqrt(dot3(dc, dc)) > rl + mr + pad) continue;
+        octree_leaf_box(c->w, a->leaf, c->TO, side, TL);
         gjk_obj box, tri;
         leaf_box_obj(side, TL, &box);
-        box.stats = st;
-        for (int t = 0; t < tn; ++t) {
-            const real d[3] = {TL[9] - S[t][0], TL[10] - S[t][1], TL[11] - S[t][2]};
-            if (sqrt(dot3(d, d)) > rl + S[t][3] + pad) continue;
-            tri_gjk_obj(w, gm, &frame, t0 + t, &tri);
-            if (mpr_intersect(&box, &tri, 1e-6)) { hit = 1; break; }
-        }
+        box.stats = c->st;
+        tri_gjk_obj(c->w, c->gm, &c->frame, (int)c->w->geom_param[4 * c->gm] + (-(b->first_child + 1)), &tri);
+        return c->contact ? mpr_penetration(&box, &tri, 1e-6, c->depth, c->normal, c->pos)
+                          : mpr_intersect(&box, &tri, 1e-6);
     }
-    free(Wt);
-    free(S);
-    return hit;
+    const double d[3] = {a->hi[0] - a->lo[0], a->hi[1] - a->lo[1], a->hi[2] - a->lo[2]};
+    const double s1 = (d[0] * d[0] + d[1] * d[1]) + d[2] * d[2];
+    if (leaf2 || (!leaf1 && s1 > obb_size(b))) {
+        for (int i = 0; i < 8; ++i)
+            if (a->child[i] >= 0 && octmesh_rec(c, a->child[i], n2)) return 1;
+        return 0;
+    }
+    if (octmesh_rec(c, n1, b->first_child)) return 1;
+    return octmesh_rec(c, n1, b->first_child + 1);
+}
+
+static int mesh_octree_run(const orc_world *w, int gm, const real *TM, int go, const real *TO, orc_stats *st,
+                           int contact, real *depth, real *normal, real *pos) {
+    const orc_bvh *B = w->bvh;
+    om_ctx c;
+    memset(&c, 0, sizeof c);
+    c.w = w; c.O = &B->oct[go]; c.T = &B->tree[gm]; c.gm = gm; c.contact = contact;
+    c.TO = TO; c.TM = TM; c.st = st; c.depth = depth; c.normal = normal; c.pos = pos;
+    if (c.O->n_nodes == 0 || c.T->n_nodes == 0 || w->geom_param[4 * go + 1] <= 0) return 0;
+    shape_to_gjk(TM, &c.frame);
+    c.frame.stats = st;
+    return octmesh_rec(&c, 0, 0);
+}
+
+static int mesh_octree_intersect(const orc_world *w, int gm, const real *TM, int go, const real *TO, orc_stats *st) {
+    return mesh_octree_run(w, gm, TM, go, TO, st, 0, NULL, NULL, NULL);
 }
 
 /* 1/0 for a mesh pair, -1 when neither side is a mesh */
@@ -3079,44 +2766,8 @@ static int mesh_shape_contact(const orc_world *w, int gm, const real *TM, int gs
 
 static int mesh_octree_contact(const orc_world *w, int gm, const real *TM, int go, const real *TO, real *depth,
                                real *normal, real *pos) {
-    const int t0 = (int)w->geom_param[4 * gm], tn = (int)w->geom_param[4 * gm + 1];
-    const int l0 = (int)w->geom_param[4 * go], ln = (int)w->geom_param[4 * go + 1];
     zero_contact(depth, normal, pos);
-    if (tn <= 0 || ln <= 0) return 0;
-    real (*Wt)[9] = malloc(sizeof(real) * 9 * (size_t)tn);
-    real (*S)[4] = malloc(sizeof(real) * 4 * (size_t)tn);
-    mesh_world_tris(w, gm, TM, Wt, S);
-    real lo[3], hi[3];
-    for (int k = 0; k < 3; ++k) { lo[k] = DBL_MAX; hi[k] = -DBL_MAX; }
-    for (int t = 0; t < tn; ++t)
-        for (int v = 0; v < 3; ++v)
-            for (int k = 0; k < 3; ++k) { lo[k] = fmin(lo[k], Wt[t][3 * v + k]); hi[k] = fmax(hi[k], Wt[t][3 * v + k]); }
-    real mc[3], dm[3];
-    for (int k = 0; k < 3; ++k) { mc[k] = (lo[k] + hi[k]) * 0.5; dm[k] = hi[k] - lo[k]; }
-    const real mr = 0.5 * sqrt(dot3(dm, dm)) * (1.0 + 1e-9) + 1e-9;
-    const real pad = 1.001 * sqrt(sqrt((double)CCD_EPS)) + 1e-5 * (1.0 + fabs(TO[9]) + fabs(TO[10]) + fabs(TO[11]) +
-                                                                 fabs(TM[9]) + fabs(TM[10]) + fabs(TM[11]));
-    gjk_obj frame;
-    memset(&frame, 0, sizeof frame);
-    shape_to_gjk(TM, &frame);
-    int hit = 0;
-    for (int l = l0; l < l0 + ln && !hit; ++l) {
-        real side[3], TL[12];
-        octree_leaf_box(w, l, TO, side, TL);
-        const real rl = 0.5 * sqrt(dot3(side, side)) * (1.0 + 1e-9) + 1e-9;
-        const real dc[3] = {TL[9] - mc[0], TL[10] - mc[1], TL[11] - mc[2]};
-        if (sqrt(dot3(dc, dc)) > rl + mr + pad) continue;
-        gjk_obj box, tri;
-        leaf_box_obj(side, TL, &box);
-        for (int t = 0; t < tn; ++t) {
-            const real d[3] = {TL[9] - S[t][0], TL[10] - S[t][1], TL[11] - S[t][2]};
-            if (sqrt(dot3(d, d)) > rl + S[t][3] + pad) continue;
-            tri_gjk_obj(w, gm, &frame, t0 + t, &tri);
-            if (mpr_penetration(&box, &tri, 1e-6, depth, normal, pos)) { hit = 1; break; }
-        }
-    }
-    free(Wt);
-    free(S);
+    const int hit = mesh_octree_run(w, gm, TM, go, TO, NULL, 1, depth, normal, pos);
     if (!hit) zero_contact(depth, normal, pos);
     return hit;
 }
@@ -3200,36 +2851,38 @@ static void *worker(void *arg) {
     return NULL;
 }
 
-/* PlanningWorld::distanceSelf / distanceOthers per configuration: pairs
- * [0, n_self) are the self group, the rest the others group; ACM-allowed
- * pairs are skipped before any distance (src/planning_world.cpp:509-510);
- * strict '<' keeps the first minimum.  best = DBL_MAX / pair -1 when a group
- * has no pair. */
-/* fcl::distance(shape, OcTree) [ext FCL 0.7.0 OcTreeSolver::
- * OcTreeShapeDistanceRecurse]: every occupied leaf as a box (constructBox:
- * box_tf = tf * Translation(centre), boxToGJK), shapeDistance(box, shape);
- * its internal-node pruning only skips leaves that cannot lower the running
- * minimum, and it stops at the first penetrating leaf (-1, isSatisfied), so
- * the result is the minimum over all leaves.  Box first, as FCL calls it. */
-static double octree_distance(const orc_world *w, int go, const real *TO, const gjk_obj *shape) {
-    const int l0 = (int)w->geom_param[4 * go], ln = (int)w->geom_param[4 * go + 1];
-    double best = DBL_MAX;
-    for (int l = l0; l < l0 + ln && best != -1.0; ++l) {
-        const real *L = w->oct_leaf + 6 * (size_t)l;
-        real c[3], side[3], TL[12];
-        for (int k = 0; k < 3; ++k) { c[k] = (L[k] + L[3 + k]) * 0.5; side[k] = L[3 + k] - L[k]; }
-        for (int k = 0; k < 9; ++k) TL[k] = TO[k];
-        for (int i = 0; i < 3; ++i) TL[9 + i] = ((TO[3 * i] * c[0] + TO[3 * i + 1] * c[1]) + TO[3 * i + 2] * c[2]) + TO[9 + i];
-        gjk_obj box;
-        memset(&box, 0, sizeof box);
-        shape_to_gjk(TL, &box);
-        box.type = GEOM_BOX;
-        for (int k = 0; k < 3; ++k) box.dim[k] = side[k] / 2.0; /* boxToGJK */
-        const double d = gjk_distance(&box, shape);
-        if (d < best) best = d;
-    }
-    return best;
-}
+/* ------------------------------------------------------------- distance
+ * fcl::distance(o1, o2, DistanceRequest, result) as PlanningWorld::distance*
+ * calls it (src/planning_world.cpp:493-720) [ext FCL 0.7.0 distance-inl.h,
+ * distance_func_matrix-inl.h, the distance traversal nodes,
+ * octree_solver-inl.h]:
+ *   shape-shape   ShapeDistanceTraversalNode::leafTesting: with
+ *                 enable_signed_distance shapeSignedDistance (GJKSignedDistance
+ *                 for every pair), else shapeDistance (the closed forms of
+ *                 fcl_gjk_dist.h, else GJKDistance); the closest points always
+ *   shape-OcTree  OcTreeShapeDistanceRecurse: shapeDistance(Box(leaf), box_tf,
+ *                 shape) per occupied leaf (Box-Sphere closed form, else GJK),
+ *                 the tree first whatever the argument order: points (leaf
+ *                 box, shape)
+ *   mesh-shape    MeshShapeDistanceTraversalNodeOBBRSS leaf:
+ *                 shapeTriangleDistance(shape, tf, P1, P2, P3, tf_mesh)
+ *                 (sphereTriangleDistance for spheres, else GJK), points
+ *                 (mesh, shape); distance() swaps them for a (shape, mesh)
+ *                 call with enable_nearest_points
+ *   mesh-mesh     MeshDistanceTraversalNodeOBBRSS: triDistance, points only
+ *                 with enable_nearest_points (o1's frame -> world)
+ *   mesh-OcTree   OcTreeMeshDistanceRecurse: shapeTriangleDistance(Box(leaf),
+ *                 box_tf, triangle) (GJK), points (leaf box, triangle)
+ * Mesh and octree pairs ignore enable_signed_distance (their leaves call the
+ * unsigned shapeDistance / triDistance) and report -1 once a leaf test
+ * penetrates.  Their BV traversals (RSS / AABB lower bounds, canStop with
+ * rel_err = abs_err = 0) skip only what cannot be strictly below the
+ * running minimum, so the value is the minimum over all leaf tests; here the
+ * leaves are scanned in order (octree leaves in FCL's DFS order, triangles
+ * by index) with strict '<', which decides between exactly equal minima
+ * (and so their points) possibly differently from FCL's RSS-ordered walk.
+ * Leaves are skipped behind bounding spheres only when their lower bound is
+ * above the running minimum by more than mesh_dist_slack. */
 
 /* PQP TriDist as FCL 0.7.0 TriangleDistance::segPoints / triDistance
  * restate it [ext fcl/narrowphase/detail/primitive_shape_algorithm/
@@ -3288,8 +2941,10 @@ static void seg_points(const real *P, const real *A, const real *Q, const real *
 
 /* one triangle's normal as a separating direction: the closest vertex of
  * the other triangle, if its projection falls inside this face, gives the
- * distance (PQP TriDist case 1) */
-static int tri_face_case(const real S[3][3], const real Sv[3][3], const real T[3][3], int *disjoint, real *dist) {
+ * distance (PQP TriDist case 1): Pf = that projection on S's face, Qf = the
+ * vertex of T */
+static int tri_face_case(const real S[3][3], const real Sv[3][3], const real T[3][3], int *disjoint, real *dist,
+                         real *Pf, real *Qf) {
     real Sn[3], V[3], Z[3], Tp[3];
     cross3(Sn, Sv[0], Sv[1]);
     const real Snl = dot3(Sn, Sn);
@@ -3313,35 +2968,44 @@ static int tri_face_case(const real S[3][3], const real Sv[3][3], const real T[3
         cross3(Z, Sn, Sv[e]);
         if (!(dot3(V, Z) > 0)) return 0;
     }
-    real Pp[3], D[3];
+    real D[3];
     const real s = Tp[point] / Snl;
-    for (int k = 0; k < 3; ++k) { Pp[k] = T[point][k] + Sn[k] * s; D[k] = Pp[k] - T[point][k]; }
+    for (int k = 0; k < 3; ++k) { Pf[k] = T[point][k] + Sn[k] * s; Qf[k] = T[point][k]; D[k] = Pf[k] - Qf[k]; }
     *dist = sqrt(dot3(D, D));
     return 1;
 }
 
-/* TriangleDistance::triDistance(S, T): 0 for intersecting triangles */
-static real tri_distance(const real S[3][3], const real T[3][3]) {
-    real Sv[3][3], Tv[3][3], VEC[3], P[3], Q[3], V[3], Z[3];
+/* TriangleDistance::triDistance(S, T, P, Q): 0 for intersecting triangles
+ * (P, Q then left as FCL leaves them unset: zeros here) */
+static real tri_distance_pq(const real S[3][3], const real T[3][3], real *P, real *Q) {
+    real Sv[3][3], Tv[3][3], VEC[3], Pc[3], Qc[3], V[3], Z[3], minP[3] = {0, 0, 0}, minQ[3] = {0, 0, 0};
     for (int k = 0; k < 3; ++k) {
         Sv[0][k] = S[1][k] - S[0][k]; Sv[1][k] = S[2][k] - S[1][k]; Sv[2][k] = S[0][k] - S[2][k];
         Tv[0][k] = T[1][k] - T[0][k]; Tv[1][k] = T[2][k] - T[1][k]; Tv[2][k] = T[0][k] - T[2][k];
+        P[k] = 0.0;
+        Q[k] = 0.0;
     }
     int shown_disjoint = 0;
     for (int k = 0; k < 3; ++k) V[k] = S[0][k] - T[0][k];
     real mindd = dot3(V, V) + 1;
     for (int i = 0; i < 3; ++i)
         for (int j = 0; j < 3; ++j) {
-            seg_points(S[i], Sv[i], T[j], Tv[j], VEC, P, Q);
-            for (int k = 0; k < 3; ++k) V[k] = Q[k] - P[k];
+            seg_points(S[i], Sv[i], T[j], Tv[j], VEC, Pc, Qc);
+            for (int k = 0; k < 3; ++k) V[k] = Qc[k] - Pc[k];
             const real dd = dot3(V, V);
             if (dd <= mindd) {
+                memcpy(minP, Pc, sizeof minP);
+                memcpy(minQ, Qc, sizeof minQ);
                 mindd = dd;
-                for (int k = 0; k < 3; ++k) Z[k] = S[(i + 2) % 3][k] - P[k];
+                for (int k = 0; k < 3; ++k) Z[k] = S[(i + 2) % 3][k] - Pc[k];
                 real a = dot3(Z, VEC);
-                for (int k = 0; k < 3; ++k) Z[k] = T[(j + 2) % 3][k] - Q[k];
+                for (int k = 0; k < 3; ++k) Z[k] = T[(j + 2) % 3][k] - Qc[k];
                 real b = dot3(Z, VEC);
-                if (a <= 0 && b >= 0) return sqrt(dd);
+                if (a <= 0 && b >= 0) {
+                    memcpy(P, Pc, sizeof Pc);
+                    memcpy(Q, Qc, sizeof Qc);
+                    return sqrt(dd);
+                }
                 const real p = dot3(V, VEC);
                 if (a < 0) a = 0;
                 if (b > 0) b = 0;
@@ -3349,28 +3013,33 @@ static real tri_distance(const real S[3][3], const real T[3][3]) {
             }
         }
     real d;
-    if (tri_face_case(S, Sv, T, &shown_disjoint, &d)) return d;
-    if (tri_face_case(T, Tv, S, &shown_disjoint, &d)) return d;
-    return shown_disjoint ? sqrt(mindd) : 0.0;
+    if (tri_face_case(S, Sv, T, &shown_disjoint, &d, P, Q)) return d;
+    if (tri_face_case(T, Tv, S, &shown_disjoint, &d, Q, P)) return d;
+    if (shown_disjoint) {
+        memcpy(P, minP, sizeof minP);
+        memcpy(Q, minQ, sizeof minQ);
+        return sqrt(mindd);
+    }
+    return 0.0;
 }
 
-/* lower-bound pruning slack for the mesh distance loops: a skipped triangle
- * (pair) is farther than the running minimum by more than the float support
- * rounding of libccd's GJK objects */
+static real tri_distance(const real S[3][3], const real T[3][3]) {
+    real P[3], Q[3];
+    return tri_distance_pq(S, T, P, Q);
+}
+
+/* lower-bound pruning slack for the mesh / octree distance loops: a skipped
+ * leaf test is farther than the running minimum by more than the float
+ * support rounding of libccd's GJK objects */
 static real mesh_dist_slack(const real *Ta, const real *Tb) {
     return 1e-5 * (1.0 + fabs(Ta[9]) + fabs(Ta[10]) + fabs(Ta[11]) + fabs(Tb[9]) + fabs(Tb[10]) + fabs(Tb[11]));
 }
 
-/* fcl::distance(mesh, shape) / (shape, mesh) [ext FCL 0.7.0
- * MeshShapeDistanceTraversalNodeOBBRSS]: the minimum over the triangles of
- * shapeTriangleDistance(shape, tf, P1, P2, P3, tf_mesh) (libccd GJK distance
- * on the triangle GJK object; -1 when they intersect); the BV traversal
- * only skips triangles that cannot lower the running minimum. */
-static real mesh_shape_distance(const orc_world *w, int gm, const real *TM, int gs, const real *TS) {
-    const int t0 = (int)w->geom_param[4 * gm], tn = (int)w->geom_param[4 * gm + 1];
+/* the shape's bounding sphere about its origin (mesh / octree loops) */
+static real shape_bradius(const orc_world *w, int gs) {
     const int ts = w->geom_type[gs];
     const real *ps = w->geom_param + 4 * gs;
-    real rs = 0.0;  /* the shape's bounding sphere about its origin (as mesh_shape_intersect) */
+    real rs = 0.0;
     if (ts == GEOM_CONVEX) {
         const real *V = w->verts + 3 * (size_t)w->geom_vstart[gs];
         for (int i = 0; i < w->geom_nv[gs]; ++i) rs = fmax(rs, dot3(V + 3 * i, V + 3 * i));
@@ -3378,7 +3047,58 @@ static real mesh_shape_distance(const orc_world *w, int gm, const real *TM, int 
     } else if (ts == GEOM_BOX) rs = 0.5 * sqrt(dot3(ps, ps));
     else if (ts == GEOM_SPHERE) rs = ps[0];
     else rs = sqrt(ps[0] * ps[0] + 0.25 * ps[1] * ps[1]) + (ts == GEOM_CAPSULE ? ps[0] : 0.0);
-    rs = rs * (1.0 + 1e-9) + 1e-9;
+    return rs * (1.0 + 1e-9) + 1e-9;
+}
+
+/* shapeDistance(Box(leaf), box_tf, shape, tf) (ShapeDistanceLibccdImpl<Box,
+ * Shape>): the Box-Sphere closed form (sphereBoxDistance, points swapped),
+ * else GJKDistance; points (box, shape).  0 or LX_THROW. */
+static int box_shape_distance(const orc_world *w, const real side[3], const real TL[12], int gs, const real *TS,
+                              double tol, double *d, double *pb, double *ps) {
+    for (int k = 0; k < 3; ++k) { pb[k] = 0.0; ps[k] = 0.0; }
+    if (w->geom_type[gs] == GEOM_SPHERE) {
+        *d = cf_sphere_box(w->geom_param[4 * gs], TS, side, TL, ps, pb);
+        if (*d == -1.0) for (int k = 0; k < 3; ++k) { pb[k] = 0.0; ps[k] = 0.0; }
+        return 0;
+    }
+    gjk_obj box, s;
+    leaf_box_obj(side, TL, &box);
+    make_obj(w, gs, TS, &s, NULL);
+    return fcl_gjk_distance(&box, &s, 0, tol, d, pb, ps);
+}
+
+/* OcTreeShapeDistanceRecurse: the first minimum over the occupied leaves in
+ * DFS order; points (box, shape) */
+static int octree_distance(const orc_world *w, int go, const real *TO, int gs, const real *TS, double tol, double *best,
+                           double *pb, double *ps) {
+    const int l0 = (int)w->geom_param[4 * go], ln = (int)w->geom_param[4 * go + 1];
+    const real rs = shape_bradius(w, gs), slack = mesh_dist_slack(TO, TS);
+    *best = DBL_MAX;
+    for (int k = 0; k < 3; ++k) { pb[k] = 0.0; ps[k] = 0.0; }
+    for (int l = l0; l < l0 + ln && *best != -1.0; ++l) {
+        real side[3], TL[12];
+        octree_leaf_box(w, l, TO, side, TL);
+        const real rl = 0.5 * sqrt(dot3(side, side)) * (1.0 + 1e-9) + 1e-9;
+        const real dc[3] = {TL[9] - TS[9], TL[10] - TS[10], TL[11] - TS[11]};
+        if (*best != DBL_MAX && sqrt(dot3(dc, dc)) - rl - rs > *best + slack) continue;
+        double d, qb[3], qs[3];
+        if (box_shape_distance(w, side, TL, gs, TS, tol, &d, qb, qs)) return LX_THROW;
+        if (d < *best) {
+            *best = d;
+            memcpy(pb, qb, sizeof qb);
+            memcpy(ps, qs, sizeof qs);
+        }
+    }
+    return 0;
+}
+
+/* mesh-shape: the minimum over the triangles of shapeTriangleDistance(shape,
+ * tf, P1, P2, P3, tf_mesh); points (mesh, shape) */
+static int mesh_shape_distance(const orc_world *w, int gm, const real *TM, int gs, const real *TS, double tol,
+                               double *best, double *pm, double *ps) {
+    const int t0 = (int)w->geom_param[4 * gm], tn = (int)w->geom_param[4 * gm + 1];
+    const int ts = w->geom_type[gs];
+    const real rs = shape_bradius(w, gs);
     real (*Wt)[9] = malloc(sizeof(real) * 9 * (size_t)(tn > 0 ? tn : 1));
     real (*S)[4] = malloc(sizeof(real) * 4 * (size_t)(tn > 0 ? tn : 1));
     mesh_world_tris(w, gm, TM, Wt, S);
@@ -3387,24 +3107,36 @@ static real mesh_shape_distance(const orc_world *w, int gm, const real *TM, int 
     make_obj(w, gs, TS, &shape, NULL);
     memset(&frame, 0, sizeof frame);
     shape_to_gjk(TM, &frame);
-    real best = DBL_MAX;
-    for (int t = 0; t < tn && best != -1.0; ++t) {
-        const real d[3] = {S[t][0] - TS[9], S[t][1] - TS[10], S[t][2] - TS[11]};
-        if (sqrt(dot3(d, d)) - S[t][3] - rs > best + slack) continue;
-        tri_gjk_obj(w, gm, &frame, t0 + t, &tri);
-        const real dt = gjk_distance(&shape, &tri);
-        if (dt < best) best = dt;
+    *best = DBL_MAX;
+    for (int k = 0; k < 3; ++k) { pm[k] = 0.0; ps[k] = 0.0; }
+    int rc = 0;
+    for (int t = 0; t < tn && *best != -1.0; ++t) {
+        const real dv[3] = {S[t][0] - TS[9], S[t][1] - TS[10], S[t][2] - TS[11]};
+        if (*best != DBL_MAX && sqrt(dot3(dv, dv)) - S[t][3] - rs > *best + slack) continue;
+        double d, qs[3] = {0, 0, 0}, qm[3] = {0, 0, 0};
+        if (ts == GEOM_SPHERE) {
+            d = cf_sphere_triangle(w->geom_param[4 * gs], TS, Wt[t], Wt[t] + 3, Wt[t] + 6, qs, qm);
+            if (d == -1.0) for (int k = 0; k < 3; ++k) { qs[k] = 0.0; qm[k] = 0.0; }
+        } else {
+            tri_gjk_obj(w, gm, &frame, t0 + t, &tri);
+            if (fcl_gjk_distance(&shape, &tri, 0, tol, &d, qs, qm)) { rc = LX_THROW; break; }
+        }
+        if (d < *best) {
+            *best = d;
+            memcpy(pm, qm, sizeof qm);
+            memcpy(ps, qs, sizeof qs);
+        }
     }
     free(Wt);
     free(S);
-    return best;
+    return rc;
 }
 
-/* fcl::distance(mesh, mesh) [ext FCL 0.7.0 MeshDistanceTraversalNodeOBBRSS
- * leafTesting]: the minimum of triDistance over the triangle pairs, B's
+/* mesh-mesh: the minimum of triDistance over the triangle pairs, B's
  * triangles mapped into A's frame (R = R1^T R2, T = R1^T (t2 - t1)); 0 when
- * some pair intersects. */
-static real mesh_mesh_distance(const orc_world *w, int ga, const real *TA, int gb, const real *TB) {
+ * some pair intersects; points (A, B) in A's frame -> world */
+static real mesh_mesh_distance(const orc_world *w, int ga, const real *TA, int gb, const real *TB, double *pa,
+                               double *pb) {
     const int a0 = (int)w->geom_param[4 * ga], an = (int)w->geom_param[4 * ga + 1];
     const int b0 = (int)w->geom_param[4 * gb], bn = (int)w->geom_param[4 * gb + 1];
     real R[9], T[3], dt[3];
@@ -3424,7 +3156,7 @@ static real mesh_mesh_distance(const orc_world *w, int ga, const real *TA, int g
         bsphere(Qp, 3, SB[j], &SB[j][3]);
     }
     const real slack = mesh_dist_slack(TA, TB);
-    real best = DBL_MAX;
+    real best = DBL_MAX, bP[3] = {0, 0, 0}, bQ[3] = {0, 0, 0};
     for (int i = 0; i < an && best != 0.0; ++i) {
         const real *P[3];
         mesh_tri_points(w, ga, a0 + i, P);
@@ -3433,23 +3165,30 @@ static real mesh_mesh_distance(const orc_world *w, int ga, const real *TA, int g
         for (int k = 0; k < 3; ++k)
             for (int m = 0; m < 3; ++m) Sa[k][m] = P[k][m];
         for (int j = 0; j < bn; ++j) {
-            const real d[3] = {c[0] - SB[j][0], c[1] - SB[j][1], c[2] - SB[j][2]};
-            if (sqrt(dot3(d, d)) - r - SB[j][3] > best + slack) continue;
-            const real dd = tri_distance(Sa, (const real (*)[3])QB[j]);
-            if (dd < best) best = dd;
+            const real dv[3] = {c[0] - SB[j][0], c[1] - SB[j][1], c[2] - SB[j][2]};
+            if (sqrt(dot3(dv, dv)) - r - SB[j][3] > best + slack) continue;
+            real Pp[3], Qq[3];
+            const real dd = tri_distance_pq(Sa, (const real (*)[3])QB[j], Pp, Qq);
+            if (dd < best) {
+                best = dd;
+                memcpy(bP, Pp, sizeof Pp);
+                memcpy(bQ, Qq, sizeof Qq);
+            }
             if (best == 0.0) break;
         }
     }
+    tf_point(TA, bP, pa);
+    tf_point(TA, bQ, pb);
     free(QB);
     free(SB);
     return best;
 }
 
-/* fcl::distance(mesh, OcTree) in either order [ext FCL 0.7.0
- * OcTreeSolver::OcTreeMeshDistanceRecurse]: the minimum over (occupied
- * leaf, triangle) of shapeTriangleDistance(Box(leaf), box_tf, P1, P2, P3,
- * tf_mesh), leaf box first; -1 once a pair intersects. */
-static real mesh_octree_distance(const orc_world *w, int gm, const real *TM, int go, const real *TO) {
+/* mesh-OcTree: the minimum over (occupied leaf, triangle) of
+ * shapeTriangleDistance(Box(leaf), box_tf, P1, P2, P3, tf_mesh) (GJK, leaf
+ * box first); points (box, triangle) */
+static int mesh_octree_distance(const orc_world *w, int gm, const real *TM, int go, const real *TO, double tol,
+                                double *best, double *pbox, double *ptri) {
     const int t0 = (int)w->geom_param[4 * gm], tn = (int)w->geom_param[4 * gm + 1];
     const int l0 = (int)w->geom_param[4 * go], ln = (int)w->geom_param[4 * go + 1];
     real (*Wt)[9] = malloc(sizeof(real) * 9 * (size_t)(tn > 0 ? tn : 1));
@@ -3459,85 +3198,85 @@ static real mesh_octree_distance(const orc_world *w, int gm, const real *TM, int
     gjk_obj frame, tri, box;
     memset(&frame, 0, sizeof frame);
     shape_to_gjk(TM, &frame);
-    real best = DBL_MAX;
-    for (int l = l0; l < l0 + ln && best != -1.0; ++l) {
+    *best = DBL_MAX;
+    for (int k = 0; k < 3; ++k) { pbox[k] = 0.0; ptri[k] = 0.0; }
+    int rc = 0;
+    for (int l = l0; l < l0 + ln && *best != -1.0 && !rc; ++l) {
         real side[3], TL[12];
         octree_leaf_box(w, l, TO, side, TL);
         const real rl = 0.5 * sqrt(dot3(side, side)) * (1.0 + 1e-9) + 1e-9;
         leaf_box_obj(side, TL, &box);
-        for (int t = 0; t < tn && best != -1.0; ++t) {
-            const real d[3] = {TL[9] - S[t][0], TL[10] - S[t][1], TL[11] - S[t][2]};
-            if (sqrt(dot3(d, d)) - rl - S[t][3] > best + slack) continue;
+        for (int t = 0; t < tn && *best != -1.0; ++t) {
+            const real dv[3] = {TL[9] - S[t][0], TL[10] - S[t][1], TL[11] - S[t][2]};
+            if (*best != DBL_MAX && sqrt(dot3(dv, dv)) - rl - S[t][3] > *best + slack) continue;
             tri_gjk_obj(w, gm, &frame, t0 + t, &tri);
-            const real dt = gjk_distance(&box, &tri);
-            if (dt < best) best = dt;
+            double d, qb[3], qt[3];
+            if (fcl_gjk_distance(&box, &tri, 0, tol, &d, qb, qt)) { rc = LX_THROW; break; }
+            if (d < *best) {
+                *best = d;
+                memcpy(pbox, qb, sizeof qb);
+                memcpy(ptri, qt, sizeof qt);
+            }
         }
     }
     free(Wt);
     free(S);
-    return best;
+    return rc;
 }
 
-/* fcl::distance on a pair with a BVH mesh side; -2 when neither is a mesh */
-static real mesh_distance(const orc_world *w, int ga, const real *Ta, int gb, const real *Tb) {
+/* fcl::distance(o1 = geometry ga at Ta, o2 = geometry gb at Tb) with
+ * DistanceRequest's options (mode bit 0: enable_signed_distance, bit 1:
+ * enable_nearest_points, dist_tol: distance_tolerance): the distance and
+ * DistanceResult::nearest_points as FCL leaves them (pts[0..3) = [0],
+ * [3..6) = [1]).  0, or LX_THROW where FCL throws. */
+static int pair_distance(const orc_world *w, int ga, const real *Ta, int gb, const real *Tb, int mode, double dist_tol,
+                         double *d, double pts[6]) {
     const int ta = w->geom_type[ga], tb = w->geom_type[gb];
-    if (ta != GEOM_MESH && tb != GEOM_MESH) return -2.0;
-    if (ta == GEOM_MESH && tb == GEOM_MESH) return mesh_mesh_distance(w, ga, Ta, gb, Tb);
-    if (ta == GEOM_OCTREE) return mesh_octree_distance(w, gb, Tb, ga, Ta);
-    if (tb == GEOM_OCTREE) return mesh_octree_distance(w, ga, Ta, gb, Tb);
-    return ta == GEOM_MESH ? mesh_shape_distance(w, ga, Ta, gb, Tb) : mesh_shape_distance(w, gb, Tb, ga, Ta);
-}
-
-int orc_distance_batch(const orc_world *w, const double *q, long n, int n_self, double *d_self, int *p_self,
-                       double *d_others, int *p_others) {
-    real *oMi = malloc(sizeof(real) * 12 * (size_t)(w->nj + 1));
-    real *link_T = malloc(sizeof(real) * 12 * (size_t)(w->n_links + 1));
-    real *obj_T = malloc(sizeof(real) * 12 * (size_t)(w->n_obj + 1));
-    real *att_T = malloc(sizeof(real) * 12 * (size_t)(w->n_att + 1));
-    for (long c = 0; c < n; ++c) {
-        fk_links(w, q + (size_t)c * w->dof, oMi, link_T, NULL);
-        for (int i = 0; i < w->n_obj; ++i) se3_mul(link_T + 12 * w->obj_link[i], w->obj_origin + 12 * i, obj_T + 12 * i);
-        for (int i = 0; i < w->n_att; ++i) se3_mul(link_T + 12 * w->att_link[i], w->att_pose + 12 * i, att_T + 12 * i);
-        double best[2] = {DBL_MAX, DBL_MAX};
-        int bp[2] = {-1, -1};
-        for (int p = 0; p < w->n_pairs; ++p) {
-            if (w->p_allowed[p]) continue;
-            const int g = p < n_self ? 0 : 1;
-            if (best[g] == -1.0) continue;  /* nothing is below -1 */
-            int ks[2] = {w->pa_kind[p], w->pb_kind[p]}, is[2] = {w->pa_idx[p], w->pb_idx[p]};
-            gjk_obj o[2];
-            const real *Ts[2];
-            int gs[2];
-            for (int s = 0; s < 2; ++s) {
-                const real *T;
-                int gg;
-                if (ks[s] == KIND_ROBOT) { T = obj_T + 12 * is[s]; gg = w->obj_geom[is[s]]; }
-                else if (ks[s] == KIND_ATTACHED) { T = att_T + 12 * is[s]; gg = w->att_geom[is[s]]; }
-                else { T = w->scene_tf + 12 * is[s]; gg = w->scene_geom[is[s]]; }
-                Ts[s] = T; gs[s] = gg;
-                if (w->geom_type[gg] != GEOM_OCTREE && w->geom_type[gg] != GEOM_MESH) make_obj(w, gg, T, &o[s], NULL);
-            }
-            const int oi = w->geom_type[gs[0]] == GEOM_OCTREE ? 0 : w->geom_type[gs[1]] == GEOM_OCTREE ? 1 : -1;
-            double d = mesh_distance(w, gs[0], Ts[0], gs[1], Ts[1]);
-            if (d == -2.0) d = oi < 0 ? gjk_distance(&o[0], &o[1]) : octree_distance(w, gs[oi], Ts[oi], &o[1 - oi]);
-            if (d < best[g]) { best[g] = d; bp[g] = p; }
-        }
-        d_self[c] = best[0]; p_self[c] = bp[0]; d_others[c] = best[1]; p_others[c] = bp[1];
+    const int sgn = mode & 1, np = (mode >> 1) & 1;
+    memset(pts, 0, 6 * sizeof(double));
+    if (ta == GEOM_MESH && tb == GEOM_MESH) {
+        double pa[3], pb[3];
+        *d = mesh_mesh_distance(w, ga, Ta, gb, Tb, pa, pb);
+        if (np) { memcpy(pts, pa, sizeof pa); memcpy(pts + 3, pb, sizeof pb); }
+        return 0;
     }
-    free(oMi); free(link_T); free(obj_T); free(att_T);
-    return 0;
+    if ((ta == GEOM_MESH && tb == GEOM_OCTREE) || (ta == GEOM_OCTREE && tb == GEOM_MESH)) {
+        const int am = ta == GEOM_MESH;
+        return mesh_octree_distance(w, am ? ga : gb, am ? Ta : Tb, am ? gb : ga, am ? Tb : Ta, dist_tol, d, pts, pts + 3);
+    }
+    if (ta == GEOM_MESH || tb == GEOM_MESH) {
+        const int am = ta == GEOM_MESH;
+        double pm[3], ps[3];
+        const int rc = mesh_shape_distance(w, am ? ga : gb, am ? Ta : Tb, am ? gb : ga, am ? Tb : Ta, dist_tol, d, pm, ps);
+        const int swap = !am && np; /* (shape, mesh): distance() swaps the points back with enable_nearest_points */
+        memcpy(pts, swap ? ps : pm, 3 * sizeof(double));
+        memcpy(pts + 3, swap ? pm : ps, 3 * sizeof(double));
+        return rc;
+    }
+    if (ta == GEOM_OCTREE || tb == GEOM_OCTREE) {
+        const int ao = ta == GEOM_OCTREE;
+        return octree_distance(w, ao ? ga : gb, ao ? Ta : Tb, ao ? gb : ga, ao ? Tb : Ta, dist_tol, d, pts, pts + 3);
+    }
+    if (!sgn && cf_shape_distance(ta, w->geom_param + 4 * ga, Ta, tb, w->geom_param + 4 * gb, Tb, d, pts, pts + 3)) {
+        if (*d == -1.0) memset(pts, 0, 6 * sizeof(double));
+        return 0;
+    }
+    gjk_obj a, b;
+    make_obj(w, ga, Ta, &a, NULL);
+    make_obj(w, gb, Tb, &b, NULL);
+    return fcl_gjk_distance(&a, &b, sgn, dist_tol, d, pts, pts + 3);
 }
 
-/* orc_distance_batch with DistanceRequest's options (mode bit 0:
- * enable_signed_distance, bit 1: enable_nearest_points) and the nearest points
- * of each group's minimum pair, pts[c*6..] = (p1, p2) in the world frame
- * (zeros when the minimum is an unsigned penetration, -1).  Shape-shape pairs
- * always carry their GJK points (FCL's shape leaf computes them whatever the
- * request); point-cloud and BVH-mesh pairs report zeros, and return -2
- * (unsupported) when the request asks for signed distances or nearest points. */
-int orc_distance_batch_ex(const orc_world *w, const double *q, long n, int n_self, int mode, double *d_self, int *p_self,
-                          double *pts_self, double *d_others, int *p_others, double *pts_others) {
-    const int sgn = mode & 1;
+/* PlanningWorld::distanceSelf / distanceOthers per configuration, with
+ * DistanceRequest's options: pairs [0, n_self) are the self group, the rest
+ * the others group; ACM-allowed pairs are skipped before any distance
+ * (src/planning_world.cpp:509-510); strict '<' keeps the first minimum
+ * (:513).  best = DBL_MAX / pair -1 when a group has no pair.  pts_* (may be
+ * NULL): the minimum pair's nearest_points [n][6].  Returns 0, or LX_THROW
+ * (a configuration on which FCL throws). */
+int orc_distance_batch_ex(const orc_world *w, const double *q, long n, int n_self, int mode, double dist_tol,
+                          double *d_self, int *p_self, double *pts_self, double *d_others, int *p_others,
+                          double *pts_others) {
     real *oMi = malloc(sizeof(real) * 12 * (size_t)(w->nj + 1));
     real *link_T = malloc(sizeof(real) * 12 * (size_t)(w->n_links + 1));
     real *obj_T = malloc(sizeof(real) * 12 * (size_t)(w->n_obj + 1));
@@ -3550,35 +3289,20 @@ int orc_distance_batch_ex(const orc_world *w, const double *q, long n, int n_sel
         double best[2] = {DBL_MAX, DBL_MAX}, bpt[2][6];
         int bp[2] = {-1, -1};
         memset(bpt, 0, sizeof bpt);
-        for (int p = 0; p < w->n_pairs; ++p) {
+        for (int p = 0; p < w->n_pairs && !rc; ++p) {
             if (w->p_allowed[p]) continue;
             const int g = p < n_self ? 0 : 1;
-            if (!sgn && best[g] == -1.0) continue; /* nothing is below -1 */
-            int ks[2] = {w->pa_kind[p], w->pb_kind[p]}, is[2] = {w->pa_idx[p], w->pb_idx[p]};
-            gjk_obj o[2];
+            const int ks[2] = {w->pa_kind[p], w->pb_kind[p]}, is[2] = {w->pa_idx[p], w->pb_idx[p]};
             const real *Ts[2];
             int gs[2];
             for (int k = 0; k < 2; ++k) {
-                const real *T;
-                int gg;
-                if (ks[k] == KIND_ROBOT) { T = obj_T + 12 * is[k]; gg = w->obj_geom[is[k]]; }
-                else if (ks[k] == KIND_ATTACHED) { T = att_T + 12 * is[k]; gg = w->att_geom[is[k]]; }
-                else { T = w->scene_tf + 12 * is[k]; gg = w->scene_geom[is[k]]; }
-                Ts[k] = T; gs[k] = gg;
-                if (w->geom_type[gg] != GEOM_OCTREE && w->geom_type[gg] != GEOM_MESH) make_obj(w, gg, T, &o[k], NULL);
+                if (ks[k] == KIND_ROBOT) { Ts[k] = obj_T + 12 * is[k]; gs[k] = w->obj_geom[is[k]]; }
+                else if (ks[k] == KIND_ATTACHED) { Ts[k] = att_T + 12 * is[k]; gs[k] = w->att_geom[is[k]]; }
+                else { Ts[k] = w->scene_tf + 12 * is[k]; gs[k] = w->scene_geom[is[k]]; }
             }
-            const int special = w->geom_type[gs[0]] == GEOM_OCTREE || w->geom_type[gs[1]] == GEOM_OCTREE ||
-                                w->geom_type[gs[0]] == GEOM_MESH || w->geom_type[gs[1]] == GEOM_MESH;
-            double d, pt[6] = {0, 0, 0, 0, 0, 0};
-            if (special) {
-                if (mode) { rc = -2; break; }
-                const int oi = w->geom_type[gs[0]] == GEOM_OCTREE ? 0 : w->geom_type[gs[1]] == GEOM_OCTREE ? 1 : -1;
-                d = mesh_distance(w, gs[0], Ts[0], gs[1], Ts[1]);
-                if (d == -2.0) d = octree_distance(w, gs[oi], Ts[oi], &o[1 - oi]);
-            } else {
-                d = gjk_query(&o[0], &o[1], sgn, pt, pt + 3);
-            }
-            if (d < best[g]) { best[g] = d; bp[g] = p; memcpy(bpt[g], pt, sizeof pt); }
+            double d, pt[6];
+            rc = pair_distance(w, gs[0], Ts[0], gs[1], Ts[1], mode, dist_tol, &d, pt);
+            if (!rc && d < best[g]) { best[g] = d; bp[g] = p; memcpy(bpt[g], pt, sizeof pt); }
         }
         d_self[c] = best[0]; p_self[c] = bp[0]; d_others[c] = best[1]; p_others[c] = bp[1];
         if (pts_self) memcpy(pts_self + 6 * c, bpt[0], sizeof bpt[0]);
@@ -3588,15 +3312,19 @@ int orc_distance_batch_ex(const orc_world *w, const double *q, long n, int n_sel
     return rc;
 }
 
-/* fcl::distance(geometry ga at Ta, geometry gb at Tb) of two shapes with
- * DistanceRequest's options: distance (signed when mode & 1) and the nearest
- * points pts[0..6) = (p1, p2) in the world frame. */
+/* DistanceRequest() (unsigned, tolerance 1e-6), no points */
+int orc_distance_batch(const orc_world *w, const double *q, long n, int n_self, double *d_self, int *p_self,
+                       double *d_others, int *p_others) {
+    return orc_distance_batch_ex(w, q, n, n_self, 0, 1e-6, d_self, p_self, NULL, d_others, p_others, NULL);
+}
+
+/* fcl::distance(geometry ga at Ta, geometry gb at Tb) with DistanceRequest's
+ * options; pts[0..6) = nearest_points.  *status: 0 or LX_THROW. */
 double orc_distance_pair_ex(const orc_world *w, int ga, const double *Ta, int gb, const double *Tb, int mode,
-                            double *pts) {
-    gjk_obj a, b;
-    make_obj(w, ga, Ta, &a, NULL);
-    make_obj(w, gb, Tb, &b, NULL);
-    return gjk_query(&a, &b, mode & 1, pts, pts + 3);
+                            double dist_tol, double *pts, int *status) {
+    double d = 0.0;
+    *status = pair_distance(w, ga, Ta, gb, Tb, mode, dist_tol, &d, pts);
+    return d;
 }
 
 /* Batch entry point.  flags[n], masks[n*W]; stats (may be NULL) receives
@@ -3721,19 +3449,11 @@ int orc_contact_batch(const orc_world *w, const double *q, long n, uint8_t *hit,
     return 0;
 }
 
+/* fcl::distance(geometry ga at Ta, geometry gb at Tb, DistanceRequest()) */
 double orc_distance_pair(const orc_world *w, int ga, const double *Ta, int gb, const double *Tb) {
-    const double dm = mesh_distance(w, ga, Ta, gb, Tb);
-    if (dm != -2.0) return dm;
-    if (w->geom_type[gb] == GEOM_OCTREE || w->geom_type[ga] == GEOM_OCTREE) {
-        const int oi = w->geom_type[ga] == GEOM_OCTREE ? 0 : 1;
-        gjk_obj s;
-        make_obj(w, oi ? ga : gb, oi ? Ta : Tb, &s, NULL);
-        return octree_distance(w, oi ? gb : ga, oi ? Tb : Ta, &s);
-    }
-    gjk_obj a, b;
-    make_obj(w, ga, Ta, &a, NULL);
-    make_obj(w, gb, Tb, &b, NULL);
-    return gjk_distance(&a, &b);
+    double d = 0.0, pts[6];
+    if (pair_distance(w, ga, Ta, gb, Tb, 0, 1e-6, &d, pts)) return NAN;
+    return d;
 }
 
 int orc_collide_pair(const orc_world *w, int ga, const double *Ta, int gb, const double *Tb) {

@@ -127,8 +127,15 @@ def test_boundary_text_matches_the_code():
     kernels compute (mpg_kernels.hip mesh_shape_first_contact /
     mesh_mesh_first_contact), not the round-3 triangle-index order."""
     hdr = open(os.path.join(ROOT, "include", "mpgpu.h")).read()
-    for stale in ("triangle index order", "is not restated"):
+    design = open(os.path.join(ROOT, "DESIGN.md")).read()
+    # round 3 contact order; round 4 distance (this repo's fp64 EPA, mesh and
+    # point-cloud options refused) -- replaced by FCL's traversal order and the
+    # libccd float restatement (oracle/fcl_gjk_dist.h, csrc/mpg_ccd_dist.h)
+    for stale in ("triangle index order", "is not restated", "fp64 to 1e-10", "at most 64 vertices"):
         assert stale not in hdr, stale
+    for stale in ("GJK + fp64 EPA", "not restated)", "keep the ungated", "OBBRSS gate on single triangles is not"):
+        assert stale not in design, stale
+    assert "MPG_DISTANCE_EPA_CAPACITY" in hdr and "convexity guard" in hdr
 
 
 def test_last_error_copy():

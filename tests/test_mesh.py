@@ -529,9 +529,20 @@ def test_mesh_contacts_match_oracle(convex):
 @pytest.mark.gpu
 @pytest.mark.parametrize("cloud", ["floor", "blue"])
 def test_mesh_robot_point_cloud_contacts_match_oracle(cloud):
-    """enable_contact=True between BVH mesh links and a point cloud: the
-    first occupied leaf with a hit, MPR penetration of (leaf box, lowest
-    such triangle), within 1e-9 of the oracle."""
+    """enable_contact=True between BVH mesh links and a point cloud: MPR
+    penetration of the first (leaf box, triangle) hit in
+    OcTreeMeshIntersectRecurse's visit order, within 1e-9 of the oracle."""
+    w, o = _cloud_mesh_worlds(cloud)
+    q = np.vstack([Wd.sample_q(o.art, 600, 78), [scenes.FLOOR_COLLIDING]])
+    _, mo = o.collide_batch(q, nthreads=min(16, os.cpu_count() or 1))
+    pc = [k for k, (a, b) in enumerate(o.pair_names()) if b == "scene_pcd"]
+    sel = np.nonzero(np.any(np.stack([(mo[:, k >> 5] >> (k & 31)) & 1 for k in pc], 1), 1))[0]
+    assert len(sel) >= 1
+    hit = _check_scalar_contacts(w, o, q[sel[:12]])
+    assert hit[:, pc].sum() >= 1
+
+
+def _cloud_mesh_worlds(cloud):
     art = scenes.panda(convex=False)
     if cloud == "floor":
         w = pymp.planning_world.PlanningWorld([art], ["panda"], [], [])
@@ -543,13 +554,52 @@ def test_mesh_robot_point_cloud_contacts_match_oracle(cloud):
     o = oracle.OracleWorld(Wd.panda_articulation(False),
                            scene=scene + [("scene_pcd", M.OcTreeGeom(scenes.cloud_points(cloud), 1e-3), M.IDENT)],
                            allowed=allowed)
-    q = np.vstack([Wd.sample_q(o.art, 600, 78), [scenes.FLOOR_COLLIDING]])
-    _, mo = o.collide_batch(q, nthreads=min(16, os.cpu_count() or 1))
+    return w, o
+
+
+def _near_cloud_contact(o, n_seg, seed):
+    """Configurations straddling first contact with the cloud: segments from
+    a state with no cloud pair hit to one with a hit, bisected 14 times on the
+    oracle's cloud bits, then jittered by 1e-5 rad around the boundary."""
     pc = [k for k, (a, b) in enumerate(o.pair_names()) if b == "scene_pcd"]
-    sel = np.nonzero(np.any(np.stack([(mo[:, k >> 5] >> (k & 31)) & 1 for k in pc], 1), 1))[0]
-    assert len(sel) >= 1
-    hit = _check_scalar_contacts(w, o, q[sel[:12]])
-    assert hit[:, pc].sum() >= 1
+
+    def cloud_hit(q):
+        _, m = o.collide_batch(q, nthreads=min(16, os.cpu_count() or 1))
+        return np.any(np.stack([(m[:, k >> 5] >> (k & 31)) & 1 for k in pc], 1), 1)
+
+    q = Wd.sample_q(o.art, 4000, seed)
+    h = cloud_hit(q)
+    ins, outs = q[h], q[~h]
+    n = min(n_seg, len(ins), len(outs))
+    assert n >= 8
+    lo, hi = outs[:n].copy(), ins[:n].copy()
+    for _ in range(14):
+        mid = (lo + hi) / 2
+        hm = cloud_hit(mid)
+        hi[hm], lo[~hm] = mid[hm], mid[~hm]
+    rng = np.random.default_rng(seed + 1)
+    return np.vstack([lo, hi] + [hi + rng.normal(0, 1e-5, hi.shape) for _ in range(6)]), pc
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cloud", ["floor", "blue"])
+def test_mesh_robot_point_cloud_near_contact(cloud):
+    """BVH mesh links grazing a point cloud, where OcTreeMeshIntersectRecurse's
+    BV tests decide which (leaf, triangle) pairs reach MPR: flags and pair bits
+    on both batch paths bit-exact with the oracle's traversal, and the first
+    contact in its visit order (depth / normal / position within 1e-9)."""
+    w, o = _cloud_mesh_worlds(cloud)
+    q, pc = _near_cloud_contact(o, 48, 91)
+    fo, mo = o.collide_batch(q, nthreads=min(16, os.cpu_count() or 1))
+    hits = np.any(np.stack([(mo[:, k >> 5] >> (k & 31)) & 1 for k in pc], 1), 1)
+    assert 0 < hits.sum() < len(q)
+    for small in (0, 1 << 20):
+        w.set_small_batch_max(small)
+        f, m = w.collide_batch(q)
+        np.testing.assert_array_equal(f, fo)
+        np.testing.assert_array_equal(m, mo)
+    sel = np.nonzero(hits)[0]
+    _check_scalar_contacts(w, o, q[sel[::max(1, len(sel) // 24)]])
 
 
 @pytest.mark.gpu

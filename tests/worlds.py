@@ -247,16 +247,23 @@ def distance_pair(ow: oracle.OracleWorld, ga: int, Ta, gb: int, Tb) -> float:
                                                 b.ctypes.data_as(DP)))
 
 
-def distance_pair_ex(ow: oracle.OracleWorld, ga: int, Ta, gb: int, Tb, signed: bool = False):
-    """The oracle's fcl::distance of two posed shapes with the nearest points:
-    (distance, p1, p2); signed: enable_signed_distance (EPA depth)."""
+def distance_pair_ex(ow: oracle.OracleWorld, ga: int, Ta, gb: int, Tb, signed: bool = False,
+                     nearest_points: bool = False, distance_tolerance: float = 1e-6):
+    """The oracle's fcl::distance of two posed geometries with
+    DistanceRequest(nearest_points, signed, distance_tolerance): (distance,
+    nearest_points[0], nearest_points[1]); RuntimeError where FCL throws."""
     import ctypes
     DP = ctypes.POINTER(ctypes.c_double)
     flat = lambda T: np.ascontiguousarray(T if np.ndim(T) == 1 else oracle._se3_flat(T), dtype=np.float64)  # noqa: E731
     a, b = flat(Ta), flat(Tb)
     pts = np.zeros(6)
+    st = ctypes.c_int(0)
+    mode = (1 if signed else 0) | (2 if nearest_points else 0)
     d = float(oracle.lib().orc_distance_pair_ex(ctypes.byref(ow._w), ga, a.ctypes.data_as(DP), gb,
-                                                b.ctypes.data_as(DP), 1 if signed else 0, pts.ctypes.data_as(DP)))
+                                                b.ctypes.data_as(DP), mode, ctypes.c_double(distance_tolerance),
+                                                pts.ctypes.data_as(DP), ctypes.byref(st)))
+    if st.value:
+        raise RuntimeError("FCL throws on this configuration")
     return d, pts[:3], pts[3:]
 
 
