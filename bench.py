@@ -165,7 +165,7 @@ def main():
         for i, k in enumerate(STAGES):
             st[k]["ms_per_launch"] = float(t[2 + i])
 
-    gather_ms = None
+    gather_ms = gather_dist_ms = None
     if args.gather and dist.is_initialized() and backend == "nccl":
         # every rank's flags + pair masks to every rank, device to device
         # (RCCL all-gather over xGMI; mplib_amd.dist.collide_sharded_device's
@@ -181,9 +181,29 @@ def main():
             dist.all_gather_into_tensor(all_f, flags)
             dist.all_gather_into_tensor(all_m, masks)
         torch.cuda.synchronize()
-        t = torch.tensor([(time.perf_counter() - g0) * 1e3 / args.steps], dtype=torch.float64, device=q.device)
+        g1 = time.perf_counter()
+        # the distance results (PlanningWorld::distanceSelf / distanceOthers
+        # minima + pair indices, mplib_amd.dist.distance_sharded_device): one
+        # device pass over this rank's batch, then the same all-gather timed
+        dres = {"d_self": torch.empty(n, dtype=torch.float64, device=q.device),
+                "p_self": torch.empty(n, dtype=torch.int32, device=q.device),
+                "d_others": torch.empty(n, dtype=torch.float64, device=q.device),
+                "p_others": torch.empty(n, dtype=torch.int32, device=q.device)}
+        w.distance_batch_device(q.data_ptr(), n, dres["d_self"].data_ptr(), dres["p_self"].data_ptr(),
+                                dres["d_others"].data_ptr(), dres["p_others"].data_ptr(), 0, 0,
+                                torch.cuda.current_stream(q.device).cuda_stream, None)
+        dall = {k: torch.empty((n * world,), dtype=v.dtype, device=q.device) for k, v in dres.items()}
+        torch.cuda.synchronize()
+        dist.barrier()
+        g2 = time.perf_counter()
+        for _ in range(args.steps):
+            for k in dres:
+                dist.all_gather_into_tensor(dall[k], dres[k])
+        torch.cuda.synchronize()
+        t = torch.tensor([(g1 - g0) * 1e3 / args.steps, (time.perf_counter() - g2) * 1e3 / args.steps],
+                         dtype=torch.float64, device=q.device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        gather_ms = float(t[0])
+        gather_ms, gather_dist_ms = float(t[0]), float(t[1])
 
     total = n * world * args.steps
     value = total / elapsed
@@ -262,6 +282,8 @@ def main():
     if gather_ms is not None:
         result["gather_ms"] = gather_ms
         result["gather_bytes_per_rank"] = n * (1 + 4 * W)
+        result["gather_distance_ms"] = gather_dist_ms
+        result["gather_distance_bytes_per_rank"] = n * 24
 
     if rank == 0 and world == 1 and args.cpu_sample > 0:
         k = args.cpu_sample if cfg != 7 else min(args.cpu_sample, 1 << 13)  # the mesh oracle is ~100x slower

@@ -209,6 +209,18 @@ int mpg_collide_batch(mpg_world *world, const double *q, int64_t n, uint8_t *fla
                       uint32_t *pair_mask, int mem, void *stream);
 
 /*
+ * One host batch over several GPUs: worlds[k] (each from mpg_world_create of
+ * the same descriptor, on its own device) checks the k-th contiguous shard of
+ * q (the first n % n_worlds shards one row longer), all shards concurrently
+ * from host threads, results written in place -- isValid is a pure function
+ * of the state (src/ompl_planner.h:59-62), so no collective is involved.
+ * Host buffers only; the first failing world's status is returned.  The
+ * in-process counterpart of mplib_amd.dist (one process per GPU).
+ */
+int mpg_collide_batch_multi(mpg_world *const *worlds, int32_t n_worlds, const double *q, int64_t n,
+                            uint8_t *flags, uint32_t *pair_mask);
+
+/*
  * Host-buffer calls (mem == MPG_MEM_HOST) of at most `n` configurations take
  * the latency path: one launch with one wave per (pair, 64-configuration tile)
  * and one synchronisation, instead of the throughput pipeline (6 launches).

@@ -68,6 +68,8 @@ SIGNATURES = {
                                           ctypes.c_uint64, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int]),
     "mpg_collide_batch": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p,
                                          ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]),
+    "mpg_collide_batch_multi": (ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p), ctypes.c_int32, ctypes.c_void_p,
+                                               ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p]),
     "mpg_collide_link_poses": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p,
                                               ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]),
     "mpg_check_motion_batch": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,

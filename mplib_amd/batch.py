@@ -180,3 +180,21 @@ def device_sincos(x, device: int = 0):
     C.check(C.lib().mpg_debug_sincos(xa.ctypes.data_as(ctypes.c_void_p), xa.size, s.ctypes.data_as(ctypes.c_void_p),
                                      c.ctypes.data_as(ctypes.c_void_p), device), "mpg_debug_sincos")
     return s, c
+
+
+def collide_batch_multi(worlds, q):
+    """One host batch over several DeviceWorlds (built from the same
+    descriptor, one per GPU): mpg_collide_batch_multi checks contiguous shards
+    concurrently.  Returns (flags[n] u8, pair_mask[n, W] u32)."""
+    worlds = list(worlds)
+    if not worlds:
+        raise ValueError("no worlds")
+    w0 = worlds[0]
+    q = np.ascontiguousarray(q, dtype=np.float64).reshape(-1, w0.dof)
+    n = q.shape[0]
+    flags = np.zeros(n, np.uint8)
+    masks = np.zeros((n, w0.mask_words), np.uint32)
+    hs = (ctypes.c_void_p * len(worlds))(*[w.handle for w in worlds])
+    C.check(C.lib().mpg_collide_batch_multi(hs, len(worlds), q.ctypes.data, n, flags.ctypes.data, masks.ctypes.data),
+            "mpg_collide_batch_multi")
+    return flags, masks

@@ -600,6 +600,9 @@ class PlanningWorld {
   const std::vector<PairInfo>& pair_table();
   void collide_batch(const double* q, int64_t n, uint8_t* flags, uint32_t* masks);
   void collide_batch_device(const void* q, int64_t n, void* flags, void* masks, void* stream);
+  // distance_batch_ex on device buffers (MPG_MEM_DEVICE, enqueued on stream)
+  void distance_batch_device(const void* q, int64_t n, const DistanceRequest& r, void* d_self, void* p_self,
+                             void* pts_self, void* d_others, void* p_others, void* pts_others, void* stream);
   int mask_words();
   mpg_world* device_world();  // rebuilds the snapshot if the world changed
   // batched OMPL motion validation over the planner's state space

@@ -4,6 +4,7 @@
 // collision/validity path, plus the batched entry points.  Every evaluation
 // goes to the HIP library (include/mpgpu.h); there is no CPU path.
 #include <pybind11/numpy.h>
+#include <optional>
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
@@ -775,6 +776,21 @@ PYBIND11_MODULE(pymp, m_all) {
            py::arg("states_ptr"), py::arg("n"), py::arg("flags_ptr"), py::arg("masks_ptr") = 0,
            py::arg("stream") = 0,
            "Enqueue the batched check on device buffers (float64 [n, dim], uint8 [n], uint32 [n, W]).")
+      .def("distance_batch_device",
+           [](PW& w, uintptr_t q, int64_t n, uintptr_t d_self, uintptr_t p_self, uintptr_t d_others,
+              uintptr_t p_others, uintptr_t pts_self, uintptr_t pts_others, uintptr_t stream,
+              std::optional<DistanceRequest> request) {
+             const DistanceRequest r = request ? *request : DistanceRequest();
+             w.distance_batch_device(reinterpret_cast<const void*>(q), n, r, reinterpret_cast<void*>(d_self),
+                                     reinterpret_cast<void*>(p_self), reinterpret_cast<void*>(pts_self),
+                                     reinterpret_cast<void*>(d_others), reinterpret_cast<void*>(p_others),
+                                     reinterpret_cast<void*>(pts_others), reinterpret_cast<void*>(stream));
+           },
+           py::arg("states_ptr"), py::arg("n"), py::arg("d_self_ptr"), py::arg("p_self_ptr"),
+           py::arg("d_others_ptr"), py::arg("p_others_ptr"), py::arg("pts_self_ptr") = 0,
+           py::arg("pts_others_ptr") = 0, py::arg("stream") = 0, py::arg("request") = py::none(),
+           "Enqueue distance_batch on device buffers (float64 [n, dim] -> float64 [n], int32 [n] per group, "
+           "optional float64 [n, 6] nearest points).")
       .def("check_motion_batch",
            [](PW& w, py::array_t<double, py::array::c_style | py::array::forcecast> q_from,
               py::array_t<double, py::array::c_style | py::array::forcecast> q_to, double fraction, double lvs) {

@@ -718,6 +718,21 @@ void PlanningWorld::distance_batch_ex(const double* q, int64_t n, const Distance
                "mpg_distance_batch_req");
 }
 
+void PlanningWorld::distance_batch_device(const void* q, int64_t n, const DistanceRequest& r, void* d_self,
+                                          void* p_self, void* pts_self, void* d_others, void* p_others,
+                                          void* pts_others, void* stream) {
+  r.check_supported();
+  const int ns = n_self_pairs();
+  ensure_snapshot(CollisionRequest());
+  const mpg_distance_request req = r.to_c();
+  check_status(mpg_distance_batch_req(world_->get(), static_cast<const double*>(q), n, ns, &req,
+                                      static_cast<double*>(d_self), static_cast<int32_t*>(p_self),
+                                      static_cast<double*>(pts_self), static_cast<double*>(d_others),
+                                      static_cast<int32_t*>(p_others), static_cast<double*>(pts_others),
+                                      MPG_MEM_DEVICE, stream),
+               "mpg_distance_batch_req");
+}
+
 namespace {
 // the WorldDistanceResult of a group's minimum pair p (DistanceResult with
 // its nearest points, planning_world.cpp:512-525)

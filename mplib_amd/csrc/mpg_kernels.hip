@@ -37,6 +37,7 @@
 #include <map>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/mpgpu.h"
@@ -8394,6 +8395,45 @@ int mpg_set_small_batch_max(mpg_world* w, int64_t n) {
 int mpg_collide_batch(mpg_world* w, const double* q, int64_t n, uint8_t* flags, uint32_t* pair_mask, int mem,
                       void* stream) {
   return collide_common<false>(w, q, n, flags, pair_mask, mem, stream);
+}
+
+int mpg_collide_batch_multi(mpg_world* const* worlds, int32_t n_worlds, const double* q, int64_t n, uint8_t* flags,
+                            uint32_t* pair_mask) {
+  if (n_worlds <= 0 || !worlds) return set_error(MPG_E_INVALID, "no worlds");
+  if (n < 0) return set_error(MPG_E_INVALID, "n < 0");
+  if (n > 0 && (!q || !flags)) return set_error(MPG_E_INVALID, "q / flags is NULL");
+  mpg_world_info i0{};
+  for (int k = 0; k < n_worlds; ++k) {
+    mpg_world_info ik{};
+    if (!worlds[k]) return set_error(MPG_E_INVALID, "world " + std::to_string(k) + " is NULL");
+    mpg_world_get_info(worlds[k], &ik);
+    if (k == 0) {
+      i0 = ik;
+    } else if (ik.dof != i0.dof || ik.n_pairs != i0.n_pairs || ik.mask_words != i0.mask_words ||
+               ik.n_links != i0.n_links || ik.snapshot_bytes != i0.snapshot_bytes) {
+      return set_error(MPG_E_INVALID, "world " + std::to_string(k) + " was not built from world 0's descriptor");
+    }
+    for (int j = 0; j < k; ++j)
+      if (worlds[j] == worlds[k]) return set_error(MPG_E_INVALID, "a world is listed twice");
+  }
+  // contiguous shards, the first n % n_worlds one row longer (mplib_amd.dist.shard_range)
+  const int64_t base = n / n_worlds, rem = n % n_worlds;
+  std::vector<int> rc(n_worlds, MPG_OK);
+  std::vector<std::string> err(n_worlds);
+  auto run = [&](int k) {
+    const int64_t start = k * base + std::min<int64_t>(k, rem), count = base + (k < rem ? 1 : 0);
+    if (count == 0) return;
+    rc[k] = mpg_collide_batch(worlds[k], q + (size_t)start * i0.dof, count, flags + start,
+                              pair_mask ? pair_mask + (size_t)start * i0.mask_words : nullptr, MPG_MEM_HOST, nullptr);
+    if (rc[k]) err[k] = g_last_error;  // the worker thread's error text
+  };
+  std::vector<std::thread> th;
+  for (int k = 1; k < n_worlds; ++k) th.emplace_back(run, k);
+  run(0);
+  for (auto& t : th) t.join();
+  for (int k = 0; k < n_worlds; ++k)
+    if (rc[k]) return set_error(rc[k], "world " + std::to_string(k) + ": " + err[k]);
+  return MPG_OK;
 }
 
 int mpg_collide_link_poses(mpg_world* w, const double* link_pose, int64_t n, uint8_t* flags, uint32_t* pair_mask,

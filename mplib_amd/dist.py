@@ -9,7 +9,10 @@ CPU in the tests).  ``collide_sharded_device`` is the same split with the
 batch, the results and the gather all resident on the GPU (no host copy):
 each rank launches its slice of a device tensor through
 ``collide_batch_device`` and RCCL all-gathers flags and pair masks into
-device tensors.
+device tensors.  ``distance_sharded_device`` does the same for
+PlanningWorld::distanceSelf / distanceOthers (src/planning_world.cpp:493-720):
+each rank's ``distance_batch_device`` slice, then the per-group minima and
+their pair indices all-gathered.
 """
 from __future__ import annotations
 
@@ -65,6 +68,25 @@ def collide_sharded(compute, states: np.ndarray, group=None, gather: bool = True
     return all_flags, all_masks, (start, count)
 
 
+def _gather_rows(parts, n, cap, group):
+    """all_gather_into_tensor of each [cap, ...] tensor in parts over the group,
+    the padding rows of the short shards dropped: [n, ...] each."""
+    import torch
+    import torch.distributed as dist
+
+    world = dist.get_world_size(group)
+    out = []
+    for t in parts:
+        full = torch.empty((world * cap,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+        dist.all_gather_into_tensor(full, t, group=group)
+        out.append(full)
+    if world * cap != n:
+        keep = torch.cat([torch.arange(r * cap, r * cap + shard_range(n, r, world)[1], device=parts[0].device)
+                          for r in range(world)])
+        out = [t.index_select(0, keep) for t in out]
+    return out
+
+
 def collide_sharded_device(compute, states, group=None, gather: bool = True, mask_words: Optional[int] = None):
     """Device-resident sharded check.
 
@@ -103,12 +125,56 @@ def collide_sharded_device(compute, states, group=None, gather: bool = True, mas
     run(states[start:start + count], flags[:count], masks[:count])
     if not gather or world == 1:
         return flags[:count], masks[:count], (start, count)
-    all_f = torch.empty(world * cap, dtype=torch.uint8, device=dev)
-    all_m = torch.empty((world * cap, W), dtype=torch.int32, device=dev)
-    dist.all_gather_into_tensor(all_f, flags, group=group)
-    dist.all_gather_into_tensor(all_m, masks, group=group)
-    if world * cap != n:  # drop the padding rows of the short shards
-        keep = torch.cat([torch.arange(r * cap, r * cap + shard_range(n, r, world)[1], device=dev)
-                          for r in range(world)])
-        all_f, all_m = all_f.index_select(0, keep), all_m.index_select(0, keep)
+    all_f, all_m = _gather_rows([flags, masks], n, cap, group)
     return all_f, all_m, (start, count)
+
+
+def distance_sharded_device(compute, states, group=None, gather: bool = True, request=None,
+                            nearest_points: bool = False):
+    """Device-resident sharded distanceSelf / distanceOthers.
+
+    states:  torch float64 tensor [n, dim] on this rank's device, the same
+             batch on every rank.
+    compute: a PlanningWorld (``distance_batch_device`` on torch's current
+             stream, with ``request``: a DistanceRequest or None) or a callable
+             ``(states_slice, d_self, p_self, d_others, p_others, pts_self,
+             pts_others)`` filling the given tensors (pts_* None unless
+             nearest_points).
+    Returns a dict of tensors -- d_self / d_others float64 [n] (DBL_MAX for an
+    empty group), p_self / p_others int32 [n] (the minimum's pair index, -1
+    for none), and with nearest_points pts_self / pts_others float64 [n, 6] --
+    for the whole batch when ``gather`` (RCCL all-gather on GPUs) else for the
+    shard, and the shard's (start, count).
+    """
+    import torch
+    import torch.distributed as dist
+
+    rank, world = dist.get_rank(group), dist.get_world_size(group)
+    if states.dtype != torch.float64 or states.dim() != 2:
+        raise ValueError("states must be a float64 tensor [n, dim]")
+    states = states.contiguous()
+    n, dev = states.shape[0], states.device
+    start, count = shard_range(n, rank, world)
+    cap = -(-n // world) if world > 1 else n
+    out = {"d_self": torch.zeros(cap, dtype=torch.float64, device=dev),
+           "p_self": torch.full((cap,), -1, dtype=torch.int32, device=dev),
+           "d_others": torch.zeros(cap, dtype=torch.float64, device=dev),
+           "p_others": torch.full((cap,), -1, dtype=torch.int32, device=dev)}
+    if nearest_points:
+        out["pts_self"] = torch.zeros((cap, 6), dtype=torch.float64, device=dev)
+        out["pts_others"] = torch.zeros((cap, 6), dtype=torch.float64, device=dev)
+    sl = {k: v[:count] for k, v in out.items()}
+    q = states[start:start + count]
+    if hasattr(compute, "distance_batch_device"):
+        if count:
+            ptr = lambda k: sl[k].data_ptr() if k in sl else 0  # noqa: E731
+            compute.distance_batch_device(q.data_ptr(), count, ptr("d_self"), ptr("p_self"), ptr("d_others"),
+                                          ptr("p_others"), ptr("pts_self"), ptr("pts_others"),
+                                          torch.cuda.current_stream(dev).cuda_stream, request)
+    else:
+        compute(q, sl["d_self"], sl["p_self"], sl["d_others"], sl["p_others"], sl.get("pts_self"),
+                sl.get("pts_others"))
+    if not gather or world == 1:
+        return sl, (start, count)
+    keys = list(out)
+    return dict(zip(keys, _gather_rows([out[k] for k in keys], n, cap, group))), (start, count)

@@ -183,3 +183,16 @@ def test_lib_hash_keys_the_code_object_only(tmp_path):
     p2 = tmp_path / "b.so"
     p2.write_bytes(bytes(inside))
     assert B.build_hash(str(p2)) != key
+
+
+def test_collide_batch_multi_rejects_bad_arguments():
+    """mpg_collide_batch_multi validates before touching a device: no worlds,
+    a NULL world, a negative count."""
+    L = C.lib()
+    none = (ctypes.c_void_p * 1)(None)
+    q = np.zeros(7)
+    f = np.zeros(1, np.uint8)
+    assert L.mpg_collide_batch_multi(none, 0, q.ctypes.data, 1, f.ctypes.data, None) == C.MPG_E_INVALID
+    assert L.mpg_collide_batch_multi(none, 1, q.ctypes.data, 1, f.ctypes.data, None) == C.MPG_E_INVALID
+    assert "NULL" in L.mpg_last_error().decode()
+    assert L.mpg_collide_batch_multi(none, 1, q.ctypes.data, -1, f.ctypes.data, None) == C.MPG_E_INVALID

@@ -100,3 +100,52 @@ def test_collide_sharded_device_gloo_world2(tmp_path, n):
         s, c = int(d["start"]), int(d["count"])
         np.testing.assert_array_equal(d["shard_flags"], fo[s:s + c])
     assert 0.0 < fo.mean() < 1.0
+
+
+def _worker_distance(rank, world, port, q, out_dir):
+    """distance_sharded_device's split + gather (gloo, CPU tensors); the
+    per-rank compute is the oracle's distance_batch_ex with nearest points."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    import torch
+    import torch.distributed as dist
+    import worlds as Wd
+    from mplib_amd.dist import distance_sharded_device
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    ow = Wd.oracle_world(3)
+
+    def compute(qs, ds, ps, do, po, pts_s, pts_o):
+        r = ow.distance_batch_ex(qs.numpy(), signed=True)
+        for t, v in zip((ds, ps, pts_s, do, po, pts_o), r):
+            t.copy_(torch.from_numpy(np.asarray(v)))
+
+    out, (s, c) = distance_sharded_device(compute, torch.from_numpy(q), nearest_points=True)
+    sh, _ = distance_sharded_device(compute, torch.from_numpy(q), gather=False, nearest_points=True)
+    np.savez(os.path.join(out_dir, f"x{rank}.npz"), start=s, count=c, shard_d=sh["d_self"].numpy(),
+             **{k: v.numpy() for k, v in out.items()})
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_distance_sharded_device_gloo_world2(tmp_path):
+    """The distance results (per-group minima, pair indices, nearest points)
+    split over two ranks and all-gathered equal the unsharded batch."""
+    mp = pytest.importorskip("torch.multiprocessing")
+    import worlds as Wd
+    ow = Wd.oracle_world(3)
+    q = Wd.sample_q(ow.art, 301, 43)  # ragged shards
+    mp.start_processes(_worker_distance, args=(2, _free_port(), q, str(tmp_path)), nprocs=2, join=True,
+                       start_method="spawn")
+    ds, ps, qs, do, po, qo = ow.distance_batch_ex(q, signed=True)
+    for r in range(2):
+        d = np.load(tmp_path / f"x{r}.npz")
+        np.testing.assert_array_equal(d["d_self"], ds)
+        np.testing.assert_array_equal(d["p_self"], ps)
+        np.testing.assert_array_equal(d["d_others"], do)
+        np.testing.assert_array_equal(d["p_others"], po)
+        np.testing.assert_array_equal(d["pts_self"], qs)
+        np.testing.assert_array_equal(d["pts_others"], qo)
+        s, c = int(d["start"]), int(d["count"])
+        np.testing.assert_array_equal(d["shard_d"], ds[s:s + c])
+    assert (np.minimum(ds, do) < 0).any()

@@ -989,3 +989,50 @@ def test_dof0_world_with_moving_links(n):
     assert fo[0] == 1
     np.testing.assert_array_equal(fl, np.repeat(fo, n))
     np.testing.assert_array_equal(pm, np.repeat(mo, n, axis=0))
+
+
+def test_collide_batch_multi_one_device():
+    """mpg_collide_batch_multi: one world, and two worlds of the same
+    descriptor on the one device of this box (the shards run concurrently
+    from two host threads), equal the single-world batch bit for bit; worlds
+    of different descriptors are refused."""
+    from mplib_amd.batch import collide_batch_multi
+    q = Wd.sample_q(ow(3).art, 50001, 515)  # odd: ragged shards
+    f, m = dw(3).collide_batch(q)
+    for ws in ([dw(3)], [dw(3), DeviceWorld(Wd.desc_arrays(ow(3)))]):
+        f2, m2 = collide_batch_multi(ws, q)
+        np.testing.assert_array_equal(f2, f)
+        np.testing.assert_array_equal(m2, m)
+    fo, mo = ow(3).collide_batch(q[:3000], nthreads=NTHREADS)
+    np.testing.assert_array_equal(f[:3000], fo)
+    with pytest.raises(ValueError, match="descriptor"):
+        collide_batch_multi([dw(3), dw(2)], q[:10])
+
+
+def test_distance_batch_device_matches_host_path():
+    """PlanningWorld.distance_batch_device (device buffers, torch's stream):
+    the host path's minima, pair indices and nearest points, and
+    mplib_amd.dist.distance_sharded_device (world size 1) the same."""
+    torch = pytest.importorskip("torch")
+    import torch.distributed as dist
+    from mplib_amd import pymp, scenes
+    from mplib_amd.dist import distance_sharded_device
+    w, art = scenes.world(3)
+    q = scenes.sample_states(art, 3000, 616)
+    req = pymp.fcl.DistanceRequest(enable_signed_distance=True)
+    ds, ps, do, po, qs, qo = w.distance_batch(q, request=req)
+    qt = torch.from_numpy(q).cuda()
+    if not dist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29533")
+        dist.init_process_group("gloo", rank=0, world_size=1)
+    out, (s, c) = distance_sharded_device(w, qt, request=req, nearest_points=True)
+    torch.cuda.synchronize()
+    assert (s, c) == (0, len(q))
+    np.testing.assert_array_equal(out["d_self"].cpu().numpy(), ds)
+    np.testing.assert_array_equal(out["p_self"].cpu().numpy(), ps)
+    np.testing.assert_array_equal(out["d_others"].cpu().numpy(), do)
+    np.testing.assert_array_equal(out["p_others"].cpu().numpy(), po)
+    np.testing.assert_array_equal(out["pts_self"].cpu().numpy(), qs)
+    np.testing.assert_array_equal(out["pts_others"].cpu().numpy(), qo)
+    dist.destroy_process_group()
