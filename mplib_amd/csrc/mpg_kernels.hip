@@ -1007,10 +1007,15 @@ __global__ __launch_bounds__(BLOCK) void cull_kernel(DevWorld w, const double* _
   }
 
   uint32_t head = 0, tail = 0;  // wave-uniform queue cursors
+  uint32_t dbg_keep = 0u;       // diagnostics (11): the bounding tests' bits, kept alive
   // queue the entries [eb, eb + 32) some lane kept (kb: this lane's bits);
   // drain 64 queued (pair, lane) entries through the SAT at a time
   auto push = [&](int eb, uint32_t kb) {
     if (!live) kb = 0u;
+    if (w.dbg(11)) {
+      dbg_keep += kb;
+      return;
+    }
     if (w.dbg(2)) {
       for (int i = 0; i < 32; ++i) {
         if (!((kb >> i) & 1u)) continue;
@@ -1084,6 +1089,7 @@ __global__ __launch_bounds__(BLOCK) void cull_kernel(DevWorld w, const double* _
     for (int seg = 0; seg < (FROM_POSES ? 2 : 1); ++seg) {
       const int s0 = seg ? w.sched_keep[m] : e0, s1 = seg ? em : w.sched_keep[m];
       const int p0 = seg ? w.sched_pr1[m] : w.sched_pr0[m];
+      if (w.dbg(12)) continue;  // diagnostics: without the static bounding tests
       for (int eb = s0; eb < s1; eb += 32) {
         const int ee = min(s1, eb + 32);
         uint32_t kb = 0u;
@@ -1112,8 +1118,8 @@ __global__ __launch_bounds__(BLOCK) void cull_kernel(DevWorld w, const double* _
   if (tail != head) sat_drain<BLOCK>(w, cen, rq, cap, cfg0, survw, queue, head, tail - head, wbase, lane);
   if (forced)
     for (int k = 0; k < w.W; ++k) survw[k * BLOCK + tid] = (uint32_t)w.all_mask[k];
-  if (w.dbg(8)) {  // ablation: bounding tests + SAT only
-    if (live && survw[tid] == 12345u) flags[cfg] = 2;
+  if (w.dbg(8) || w.dbg(11)) {  // ablation: bounding tests + SAT only (11: without the queue and SAT)
+    if (live && (survw[tid] == 12345u || dbg_keep == 12345u)) flags[cfg] = 2;
     return;
   }
   // survivor words -> surv, and this wave's candidate count per pair ->
