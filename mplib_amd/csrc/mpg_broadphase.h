@@ -65,7 +65,19 @@ struct BpView {
   cptr<float> moff;      // [n_moving*12]
   cptr<float> mobj;      // [n_moving*BM_STRIDE]
   cptr<float> sobj;      // [n_static*BS_STRIDE]
+  // the fp32 FK program (bp_fk): per joint its motion kind (BpKind) and
+  // placement with a constant (non-move-group) motion folded in; the moving
+  // objects grouped by their link's parent joint (0 = universe) with
+  // link placement * moving offset folded into one transform
+  cptr<int> jkind;       // [nj]
+  cptr<int> jobj_start;  // [nj+2]
+  cptr<int> jobj_order;  // [n_moving]
+  cptr<float> oplace;    // [n_moving*12]
 };
+
+// motion kinds of the fp32 FK: a fixed (or constant) joint, a revolute or
+// prismatic joint about a principal axis (x, y, z), or about any unit axis
+enum BpKind { BK_FIXED = 0, BK_REV_X = 1, BK_REV_AXIS = 4, BK_PRI_X = 5, BK_PRI_AXIS = 8 };
 
 struct F34 {
   float R[9];  // row-major
@@ -112,25 +124,13 @@ MPG_INLINE void f_quat_to_mat(float w, float x, float y, float z, float* m) {
   m[8] = 1.f - (txx + tyy);
 }
 
-// rotation -> unit quaternion (x, y, z, w); Shepperd's method, branch-free selects
-MPG_INLINE void f_mat_to_quat(const float* m, float* q) {
-  const float t0 = m[0] + m[4] + m[8];
-  const float d0 = 1.f + t0, d1 = 1.f + m[0] - m[4] - m[8], d2 = 1.f - m[0] + m[4] - m[8],
-              d3 = 1.f - m[0] - m[4] + m[8];
-  int k = 0;
-  float best = d0;
-  if (d1 > best) { best = d1; k = 1; }
-  if (d2 > best) { best = d2; k = 2; }
-  if (d3 > best) { best = d3; k = 3; }
-  const float s = 0.5f / sqrtf(best);
-  const float h = 0.5f * sqrtf(best);
-  const float a = (m[7] - m[5]) * s, b = (m[2] - m[6]) * s, c = (m[3] - m[1]) * s;  // w*4 components
-  const float e = (m[1] + m[3]) * s, f = (m[2] + m[6]) * s, g = (m[5] + m[7]) * s;
-  // k = 0: w = h, (a, b, c); k = 1: x = h, w = a, y = e, z = f; ...
-  q[0] = k == 0 ? a : k == 1 ? h : k == 2 ? e : f;
-  q[1] = k == 0 ? b : k == 1 ? e : k == 2 ? h : g;
-  q[2] = k == 0 ? c : k == 1 ? f : k == 2 ? g : h;
-  q[3] = k == 0 ? h : k == 1 ? a : k == 2 ? b : c;
+// the third column of a row-major rotation from the first two (c2 = c0 x c1):
+// phase A keeps two columns per object for the SAT stage
+MPG_INLINE void f_complete_rotation(float* m) {
+  MPG_FP32_CONTRACT
+  m[2] = m[3] * m[7] - m[6] * m[4];
+  m[5] = m[6] * m[1] - m[0] * m[7];
+  m[8] = m[0] * m[4] - m[3] * m[1];
 }
 
 // revolute angles are reduced in fp64 before the fp32 sincos so large user
@@ -169,61 +169,107 @@ MPG_INLINE F34 f_joint_motion(int type, P axis, double v) {
 }
 
 // fp32 FK over the whole tree; calls sink(m, T) with every moving object's
-// world transform (link pose * collision origin).  Joint frames that a later
-// non-consecutive child needs are kept in registers for the first
-// kRegSaves slots and spilled to `save` ([slot - kRegSaves][12] x stride)
-// beyond that.
+// world transform (link pose * collision origin).  Per joint: A = parent *
+// placement (one 3x4 product), then the motion applied in place -- a
+// principal-axis rotation mixes two columns of A.R, a principal-axis
+// translation adds one column to A.p, constant joints were folded into the
+// placement on the host -- and per moving object one product with its folded
+// link placement * offset.  Joint frames that a later non-consecutive child
+// needs are kept in registers for the first kRegSaves slots and spilled to
+// `save` ([slot - kRegSaves][12] x stride) beyond that.
 constexpr int kRegSaves = 2;
+
+// A * R_k(a) for a principal axis k: the columns (U, W) spanning the rotated
+// plane become U' = c U + s W, W' = c W - s U
+template <int U, int W>
+MPG_INLINE void f_rotate_cols(F34& A, float c, float s) {
+  MPG_FP32_CONTRACT
+#pragma unroll
+  for (int r = 0; r < 3; ++r) {
+    const float u = A.R[3 * r + U], w = A.R[3 * r + W];
+    A.R[3 * r + U] = c * u + s * w;
+    A.R[3 * r + W] = c * w - s * u;
+  }
+}
 
 template <class Sink>
 MPG_INLINE void bp_fk(const BpView& b, const double* __restrict__ qrow, float* save, int stride, Sink&& sink) {
+  MPG_FP32_CONTRACT
   F34 cur, r0, r1;
+  for (int o = b.jobj_start[0]; o < b.jobj_start[1]; ++o) {  // objects on the universe
+    const int m = b.jobj_order[o];
+    sink(m, f34_load(b.oplace + 12 * m));
+  }
 #pragma unroll 1
-  for (int j = 0; j <= b.nj; ++j) {
-    if (j > 0) {
-      const int jj = j - 1;
-      const int src = b.joint_q_source[jj];
-      const double v = src >= 0 ? qrow[src] : b.joint_q_const[jj];
-      const int jt = b.joint_type[jj];
-      const F34 li = f34_mul(f34_load(b.jplace + 12 * jj), f_joint_motion(jt, b.jaxis + 3 * jj, v));
-      const int s = b.jsrc[jj];
-      if (s < 0) {
-        cur = li;
-      } else if (s == 0) {
-        cur = f34_mul(cur, li);
-      } else if (s == 1) {
-        cur = f34_mul(r0, li);
-      } else if (s == 2) {
-        cur = f34_mul(r1, li);
+  for (int jj = 0; jj < b.nj; ++jj) {
+    const int kind = b.jkind[jj];
+    const F34 Pl = f34_load(b.jplace + 12 * jj);
+    const int s = b.jsrc[jj];
+    F34 A;
+    if (s < 0) {
+      A = Pl;
+    } else if (s == 0) {
+      A = f34_mul(cur, Pl);
+    } else if (s == 1) {
+      A = f34_mul(r0, Pl);
+    } else if (s == 2) {
+      A = f34_mul(r1, Pl);
+    } else {
+      F34 P;
+      const float* sp = save + (size_t)(s - 1 - kRegSaves) * 12 * stride;
+#pragma unroll
+      for (int i = 0; i < 9; ++i) P.R[i] = sp[i * stride];
+#pragma unroll
+      for (int i = 0; i < 3; ++i) P.p[i] = sp[(9 + i) * stride];
+      A = f34_mul(P, Pl);
+    }
+    if (kind != BK_FIXED) {
+      const double v = qrow[b.joint_q_source[jj]];
+      if (kind < BK_PRI_X) {
+        // revolute angles are reduced in fp64 before the fp32 sincos so large
+        // user values (continuous joints) keep full fp32 accuracy
+        const double k = rint(v * 0.15915494309189535);
+        const float a = (float)(v - k * 6.283185307179586);
+        float sn, cs;
+        sincosf(a, &sn, &cs);
+        if (kind == BK_REV_AXIS) {
+          A = f34_mul(A, f_joint_motion(MPG_JOINT_REVOLUTE_UNALIGNED, b.jaxis + 3 * jj, (double)a));
+        } else if (kind == BK_REV_X) {
+          f_rotate_cols<1, 2>(A, cs, sn);
+        } else if (kind == BK_REV_X + 1) {
+          f_rotate_cols<2, 0>(A, cs, sn);
+        } else {
+          f_rotate_cols<0, 1>(A, cs, sn);
+        }
       } else {
-        F34 P;
-        const float* sp = save + (size_t)(s - 1 - kRegSaves) * 12 * stride;
+        const float f = (float)v;
+        if (kind == BK_PRI_AXIS) {
+          const float ax[3] = {b.jaxis[3 * jj] * f, b.jaxis[3 * jj + 1] * f, b.jaxis[3 * jj + 2] * f};
 #pragma unroll
-        for (int i = 0; i < 9; ++i) P.R[i] = sp[i * stride];
+          for (int r = 0; r < 3; ++r) A.p[r] += A.R[3 * r] * ax[0] + A.R[3 * r + 1] * ax[1] + A.R[3 * r + 2] * ax[2];
+        } else {
 #pragma unroll
-        for (int i = 0; i < 3; ++i) P.p[i] = sp[(9 + i) * stride];
-        cur = f34_mul(P, li);
-      }
-      const int sv = b.jsave[jj];
-      if (sv == 0) {
-        r0 = cur;
-      } else if (sv == 1) {
-        r1 = cur;
-      } else if (sv >= kRegSaves) {
-        float* sp = save + (size_t)(sv - kRegSaves) * 12 * stride;
-#pragma unroll
-        for (int i = 0; i < 9; ++i) sp[i * stride] = cur.R[i];
-#pragma unroll
-        for (int i = 0; i < 3; ++i) sp[(9 + i) * stride] = cur.p[i];
+          for (int r = 0; r < 3; ++r)
+            A.p[r] += (kind == BK_PRI_X ? A.R[3 * r] : kind == BK_PRI_X + 1 ? A.R[3 * r + 1] : A.R[3 * r + 2]) * f;
+        }
       }
     }
-    for (int k = b.link_start[j]; k < b.link_start[j + 1]; ++k) {
-      const int l = b.link_order[k];
-      const F34 L = j == 0 ? f34_load(b.lplace + 12 * l) : f34_mul(cur, f34_load(b.lplace + 12 * l));
-      for (int o = b.obj_start[l]; o < b.obj_start[l + 1]; ++o) {
-        const int m = b.obj_order[o];
-        sink(m, f34_mul(L, f34_load(b.moff + 12 * m)));
-      }
+    cur = A;
+    const int sv = b.jsave[jj];
+    if (sv == 0) {
+      r0 = cur;
+    } else if (sv == 1) {
+      r1 = cur;
+    } else if (sv >= kRegSaves) {
+      float* sp = save + (size_t)(sv - kRegSaves) * 12 * stride;
+#pragma unroll
+      for (int i = 0; i < 9; ++i) sp[i * stride] = cur.R[i];
+#pragma unroll
+      for (int i = 0; i < 3; ++i) sp[(9 + i) * stride] = cur.p[i];
+    }
+    for (int o = b.jobj_start[jj + 1]; o < b.jobj_start[jj + 2]; ++o) {
+      const int m = b.jobj_order[o];
+      sink(m, f34_mul(cur, f34_load(b.oplace + 12 * m)));
     }
   }
 }
@@ -343,9 +389,36 @@ inline uint32_t fsphere_obb_keep2(const float* c, float r, P rec, float margin) 
 // ---------------------------------------------------------------------------
 struct BpProgram {
   int n_saves = 0;
-  std::vector<int> jsrc, jsave, link_start, link_order, obj_start, obj_order;
-  std::vector<float> jaxis, jplace, lplace, moff, mobj, sobj;
+  std::vector<int> jsrc, jsave, link_start, link_order, obj_start, obj_order, jkind, jobj_start, jobj_order;
+  std::vector<float> jaxis, jplace, lplace, moff, mobj, sobj, oplace;
 };
+
+// row-major 3x4 product in fp64 (host program folding)
+inline void se3d_mul(const double* A, const double* B, double* C) {
+  double T[12];
+  for (int i = 0; i < 3; ++i) {
+    for (int j = 0; j < 3; ++j) T[3 * i + j] = A[3 * i] * B[j] + A[3 * i + 1] * B[3 + j] + A[3 * i + 2] * B[6 + j];
+    T[9 + i] = A[3 * i] * B[9] + A[3 * i + 1] * B[10] + A[3 * i + 2] * B[11] + A[9 + i];
+  }
+  for (int k = 0; k < 12; ++k) C[k] = T[k];
+}
+
+// a joint's motion at value v in fp64 (pinocchio's joint models)
+inline void joint_motion_d(int type, const double* axis, double v, double* M) {
+  for (int k = 0; k < 12; ++k) M[k] = (k == 0 || k == 4 || k == 8) ? 1.0 : 0.0;
+  if (type <= MPG_JOINT_REVOLUTE_UNALIGNED || type >= MPG_JOINT_RUBX) {
+    const double s = std::sin(v), c = std::cos(v);
+    const int t = type >= MPG_JOINT_RUBX ? type - MPG_JOINT_RUBX : type;
+    const double x = t == 0 ? 1.0 : t == 3 ? axis[0] : 0.0, y = t == 1 ? 1.0 : t == 3 ? axis[1] : 0.0,
+                 z = t == 2 ? 1.0 : t == 3 ? axis[2] : 0.0, u = 1.0 - c;
+    const double R[9] = {c + x * x * u,     x * y * u - z * s, x * z * u + y * s, y * x * u + z * s, c + y * y * u,
+                         y * z * u - x * s, z * x * u - y * s, z * y * u + x * s, c + z * z * u};
+    for (int k = 0; k < 9; ++k) M[k] = R[k];
+  } else {
+    const int t = type - MPG_JOINT_PX;
+    for (int k = 0; k < 3; ++k) M[9 + k] = (t == 3 ? axis[k] : (t == k ? 1.0 : 0.0)) * v;
+  }
+}
 
 inline float widen(double v) {  // |v| rounded away from zero, plus a hair
   const float f = (float)std::fabs(v);
@@ -373,7 +446,23 @@ inline void bp_build(const mpg_world_desc* d, const std::vector<double>& obb, Bp
     P.jsave[j - 1] = slot_of[j];
   }
   for (int i = 0; i < 3 * nj; ++i) P.jaxis.push_back((float)d->joint_axis[i]);
-  for (int i = 0; i < 12 * nj; ++i) P.jplace.push_back((float)d->joint_placement[i]);
+  P.jkind.assign(std::max(nj, 1), BK_FIXED);
+  for (int j = 0; j < nj; ++j) {
+    const int t = d->joint_type[j];
+    double Pl[12];
+    for (int k = 0; k < 12; ++k) Pl[k] = d->joint_placement[12 * j + k];
+    if (d->joint_q_source[j] < 0) {  // constant motion: folded into the placement
+      double M[12];
+      joint_motion_d(t, d->joint_axis + 3 * j, d->joint_q_const[j], M);
+      se3d_mul(Pl, M, Pl);
+    } else if (t <= MPG_JOINT_REVOLUTE_UNALIGNED || t >= MPG_JOINT_RUBX) {
+      const int a = t >= MPG_JOINT_RUBX ? t - MPG_JOINT_RUBX : t;
+      P.jkind[j] = BK_REV_X + a;
+    } else {
+      P.jkind[j] = BK_PRI_X + (t - MPG_JOINT_PX);
+    }
+    for (int k = 0; k < 12; ++k) P.jplace.push_back((float)Pl[k]);
+  }
   for (int i = 0; i < 12 * nl; ++i) P.lplace.push_back((float)d->link_placement[i]);
   for (int i = 0; i < 12 * nm; ++i) P.moff.push_back((float)d->moving_offset[i]);
   P.link_start.assign(nj + 2, 0);
@@ -390,6 +479,20 @@ inline void bp_build(const mpg_world_desc* d, const std::vector<double>& obb, Bp
       if (d->moving_link[m] == l) P.obj_order.push_back(m);
   }
   P.obj_start[nl] = (int)P.obj_order.size();
+  // objects by their link's parent joint, link placement * offset folded
+  P.jobj_start.assign(nj + 2, 0);
+  P.oplace.assign((size_t)12 * std::max(nm, 1), 0.f);
+  for (int j = 0; j <= nj; ++j) {
+    P.jobj_start[j] = (int)P.jobj_order.size();
+    for (int m = 0; m < nm; ++m)
+      if (d->link_parent[d->moving_link[m]] == j) P.jobj_order.push_back(m);
+  }
+  P.jobj_start[nj + 1] = (int)P.jobj_order.size();
+  for (int m = 0; m < nm; ++m) {
+    double O[12];
+    se3d_mul(d->link_placement + 12 * d->moving_link[m], d->moving_offset + 12 * m, O);
+    for (int k = 0; k < 12; ++k) P.oplace[12 * m + k] = (float)O[k];
+  }
   P.mobj.assign((size_t)BM_STRIDE * std::max(nm, 1), 0.f);
   for (int m = 0; m < nm; ++m) {
     const double* g = obb.data() + 7 * d->moving_geom[m];
@@ -433,6 +536,10 @@ inline BpView bp_view(const mpg_world_desc* d, const BpProgram& P) {
   b.moff = to_cptr<float>(P.moff.data());
   b.mobj = to_cptr<float>(P.mobj.data());
   b.sobj = to_cptr<float>(P.sobj.data());
+  b.jkind = to_cptr<int>(P.jkind.data());
+  b.jobj_start = to_cptr<int>(P.jobj_start.data());
+  b.jobj_order = to_cptr<int>(P.jobj_order.data());
+  b.oplace = to_cptr<float>(P.oplace.data());
   return b;
 }
 

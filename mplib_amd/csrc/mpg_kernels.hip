@@ -870,7 +870,9 @@ __device__ __forceinline__ uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi
 // Phase A: one lane per configuration (mpg_broadphase.h).
 //   1. fp32 FK over the tree -> per moving object its world OBB centre in LDS
 //      ([object][3][lane]) and its rotation quaternion in the workspace
-//      (rq[object][4][cfg], read back only by the SAT stage);
+//      (rq[object][6][cfg]: the first two columns of its rotation, read
+//      back only by the SAT stage, which completes the third by a cross
+//      product);
 //   2. pairs are walked grouped by their moving object (host-built schedule,
 //      ACM-allowed pairs dropped): the object's centre is loaded once, then
 //      a cheap bounding test per partner (sphere-OBB against static objects,
@@ -909,8 +911,15 @@ __device__ __forceinline__ FObb bp_obb(const DevWorld& w, const float* __restric
                                        long long cap, int id, int t, long long cfg) {
   FObb o;
   if (id < w.n_moving) {
-    const float* q = rq + (size_t)id * 4 * cap + cfg;
-    f_quat_to_mat(q[3 * cap], q[0], q[cap], q[2 * cap], o.R);
+    const float* q = rq + (size_t)id * 6 * cap + cfg;
+    // columns 0 and 1 of R; column 2 = column 0 x column 1
+    o.R[0] = q[0];
+    o.R[3] = q[cap];
+    o.R[6] = q[2 * cap];
+    o.R[1] = q[3 * cap];
+    o.R[4] = q[4 * cap];
+    o.R[7] = q[5 * cap];
+    f_complete_rotation(o.R);
     const float* c = cen + (size_t)id * 3 * BLOCK + t;
     o.c[0] = c[0];
     o.c[1] = c[BLOCK];
@@ -970,14 +979,17 @@ __global__ __launch_bounds__(BLOCK) void cull_kernel(DevWorld w, const double* _
       for (int k = 0; k < w.W; ++k) masks[cfg * w.W + k] = 0u;
   }
   for (int k = 0; k < w.W; ++k) survw[k * BLOCK + tid] = 0u;
+  if (w.dbg(14)) return;  // diagnostics: the launch and the output zeroing alone
 
   auto put = [&](int m, const F34& T) {
-    float q[4];
-    f_mat_to_quat(T.R, q);
-    if (live) {
-      float* r = rq + (size_t)m * 4 * cap + cfg;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) r[k * cap] = q[k];
+    if (live && !w.dbg(13)) {  // 13: diagnostics, FK without the rq stores
+      float* r = rq + (size_t)m * 6 * cap + cfg;
+      r[0] = T.R[0];
+      r[cap] = T.R[3];
+      r[2 * cap] = T.R[6];
+      r[3 * cap] = T.R[1];
+      r[4 * cap] = T.R[4];
+      r[5 * cap] = T.R[7];
     }
     float* r = cen + (size_t)m * 3 * BLOCK + tid;
     const cptr<float> g = w.bp.mobj + BM_STRIDE * m;
@@ -1001,7 +1013,7 @@ __global__ __launch_bounds__(BLOCK) void cull_kernel(DevWorld w, const double* _
       for (int j = 0; j < w.nj; ++j)
         if (w.prism_bound[j] >= 0.0) forced |= !(std::fabs(in[c * w.dof + w.joint_q_source[j]]) <= w.prism_bound[j]);
   }
-  if (w.dbg(1)) {
+  if (w.dbg(1) || w.dbg(13)) {
     if (live && cen[tid] == 12345.f) flags[cfg] = 2;  // keep the records alive
     return;
   }
@@ -6243,7 +6255,7 @@ struct mpg_world {
     uint32_t* seg_start = nullptr;  // [n_pairs]
     uint32_t* prefix = nullptr;     // [n_pairs + 2] task prefix + task counter
     uint32_t* cand = nullptr;       // [n_pairs * cap] worst case
-    float* rq = nullptr;            // [n_moving * 4 * cap] phase-A rotations for the SAT stage
+    float* rq = nullptr;            // [n_moving * 6 * cap] phase-A rotations (two columns) for the SAT stage
     double* sc = nullptr;           // [cap * dof * 2] exact joint (sin, cos) for phase B
     long long cap = 0;
     uint64_t last = 0;              // LRU tick (get_workspace)
@@ -6977,7 +6989,7 @@ int get_workspace(mpg_world* w, hipStream_t s, long long want, mpg_world::Worksp
     HIP_TRY(hipMalloc(&ws.seg_start, sizeof(uint32_t) * np));
     HIP_TRY(hipMalloc(&ws.prefix, sizeof(uint32_t) * (np + 4)));
     HIP_TRY(hipMalloc(&ws.cand, sizeof(uint32_t) * np * want));
-    HIP_TRY(hipMalloc(&ws.rq, sizeof(float) * 4 * std::max(w->dw.n_moving, 1) * want));
+    HIP_TRY(hipMalloc(&ws.rq, sizeof(float) * 6 * std::max(w->dw.n_moving, 1) * want));
     HIP_TRY(hipMalloc(&ws.sc, sizeof(double) * 2 * std::max(w->dw.dof, 1) * want));
     ws.cap = want;
   }
@@ -7750,6 +7762,11 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
   const size_t o_bmo = bb.add(bpp.moff.data(), bpp.moff.size());
   const size_t o_bmb = bb.add(bpp.mobj.data(), bpp.mobj.size());
   const size_t o_bsb = bb.add(bpp.sobj.data(), bpp.sobj.size());
+  if (bpp.jobj_order.empty()) bpp.jobj_order.push_back(0);
+  const size_t o_bjk = bb.add(bpp.jkind.data(), bpp.jkind.size());
+  const size_t o_bjo = bb.add(bpp.jobj_start.data(), bpp.jobj_start.size());
+  const size_t o_bjr = bb.add(bpp.jobj_order.data(), bpp.jobj_order.size());
+  const size_t o_bop = bb.add(bpp.oplace.data(), bpp.oplace.size());
   const size_t o_olf = bb.add(oct_leaf.data(), oct_leaf.size());
   const size_t o_mtr = bb.add(mesh_tri.data(), mesh_tri.size());
   const size_t o_mnd = bb.add(mesh_node.data(), mesh_node.size());
@@ -7899,6 +7916,10 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
   bp.moff = F(o_bmo);
   bp.mobj = F(o_bmb);
   bp.sobj = F(o_bsb);
+  bp.jkind = I(o_bjk);
+  bp.jobj_start = I(o_bjo);
+  bp.jobj_order = I(o_bjr);
+  bp.oplace = F(o_bop);
   dw.oct_leaf = to_cptr<double>(base + o_olf);
   dw.oct_path = to_cptr<uint64_t>(base + o_opa);
   dw.oct_depth = to_cptr<int>(base + o_ode);

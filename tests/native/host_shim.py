@@ -8,13 +8,18 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 _lib = None
 
 
+def _build(src, stem):
+    """Compile src into a per-process file: pytest-xdist workers build the
+    same shim at once, and a shared output path could be loaded half-written."""
+    out = os.path.join(tempfile.gettempdir(), "%s_%d_%d.so" % (stem, os.getuid(), os.getpid()))
+    subprocess.check_call(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-fPIC", "-shared", "-o", out, src])
+    return ctypes.CDLL(out)
+
+
 def lib():
     global _lib
     if _lib is None:
-        out = os.path.join(tempfile.gettempdir(), "mplib_amd_host_fk_%d.so" % os.getuid())
-        src = os.path.join(_HERE, "host_fk.cpp")
-        subprocess.check_call(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-fPIC", "-shared", "-o", out, src])
-        _lib = ctypes.CDLL(out)
+        _lib = _build(os.path.join(_HERE, "host_fk.cpp"), "mplib_amd_host_fk")
     return _lib
 
 
@@ -25,8 +30,5 @@ def walk_lib():
     """tests/native/walk_cells.cpp: mpg_hullcells.h's walk-hull tables on the host."""
     global _walk
     if _walk is None:
-        out = os.path.join(tempfile.gettempdir(), "mplib_amd_walk_cells_%d.so" % os.getuid())
-        src = os.path.join(_HERE, "walk_cells.cpp")
-        subprocess.check_call(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-fPIC", "-shared", "-o", out, src])
-        _walk = ctypes.CDLL(out)
+        _walk = _build(os.path.join(_HERE, "walk_cells.cpp"), "mplib_amd_walk_cells")
     return _walk

@@ -5,7 +5,8 @@
 # MPG_DEBUG_CULL modes
 #   0 full, 1 FK + records, 2 no SAT (sphere survivors kept), 8 bounding
 #   tests + SAT, 9 all but sincos, 11 bounding tests only (no queue / SAT),
-#   12 full without the static-partner bounding tests
+#   12 full without the static-partner bounding tests, 13 FK without the
+#   rq stores, 14 launch + output zeroing only
 # usage: bash tools/cull_iso.sh <out dir> [bench args]
 set -o pipefail
 OUT=${1:-gpurun_out/cull_iso}; shift
