@@ -90,20 +90,23 @@ struct DevWorld {
   cptr<int> link_chain_len;    // [n_links]
   cptr<int> chain_joints;
   BpView bp;  // fp32 broad-phase program (mpg_broadphase.h)
-  // phase-A pair schedule: entries [sched_start[m], sched_start[m+1]) are the
-  // non-allowed pairs whose lower moving object is m: (pair index, partner)
+  // phase-A pair schedule (entry e: pair sched_pair[e]).  Moving-moving
+  // pairs by their lower object m: entries [sched_start[m], sched_start[m+1])
+  // with the partner in sched_other.  Moving-static pairs static-major:
+  // entries [st_start[g*(n_static+1) + s], st_start[g*(n_static+1) + s + 1])
+  // pair static s with the moving objects st_m (bounding radius st_r); group
+  // g = 0 those the object's reach ball can bring near, g = 1 the rest
+  // (link-pose input only)
   cptr<int> sched_start;  // [n_moving+1]
   cptr<int> sched_pair;
   cptr<int> sched_other;
-  cptr<int> sched_mid;      // [n_moving] first moving-partner entry of the object (static partners before it)
-  cptr<int> sched_keep;     // [n_moving] end of the static partners its reach ball can bring near (the rest: link-pose input only)
+  cptr<int> st_start;     // [2 * (n_static + 1)]
+  cptr<int> st_m;         // [entries]
+  cptr<float> st_r;       // [entries]
   int n_prism;              // prismatic move-group joints with a value bound (a configuration beyond it: every pair)
   cptr<double> prism_bound; // [nj] |q| bound of such a joint, 0 = none
   double pose_bound;        // link-pose input: |position| bound of every link (beyond it: every pair)
   cptr<int> all_mask;       // [W] bits of every non-allowed pair
-  cptr<float> sched_srec;   // static partners' OBB records inline, in interleaved pairs [pair][BS_STRIDE][2]
-  cptr<int> sched_pr0;      // [n_moving] first record pair of the object's near static partners
-  cptr<int> sched_pr1;      // [n_moving] first record pair of its never-near static partners
   // octrees: leaf boxes [L][6] (octree frame), per geometry a uniform grid
   // record (OG_*), cell -> leaf lists (CSR)
   cptr<double> oct_leaf;

@@ -1087,33 +1087,46 @@ __global__ __launch_bounds__(BLOCK) void cull_kernel(DevWorld w, const double* _
       }
     }
   };
+  // moving-static pairs, static-major: the static's OBB record is loaded
+  // once (scalar registers) for all its entries, each entry a moving object's
+  // bounding sphere (centre from LDS); group 1 (objects whose reach ball
+  // never comes near the static) only for link-pose input, which does not
+  // assume the kinematics
+  const int ns = w.n_static;
+  for (int g = 0; g < (FROM_POSES ? 2 : 1) && !w.dbg(12); ++g) {  // 12: diagnostics, without these tests
+    const int E0 = w.st_start[g * (ns + 1)], E1 = w.st_start[g * (ns + 1) + ns];
+    if (E0 == E1) continue;
+    int eb = E0;
+    uint32_t kb = 0u;
+    for (int sid = 0; sid < ns; ++sid) {
+      const int e0 = w.st_start[g * (ns + 1) + sid], e1 = w.st_start[g * (ns + 1) + sid + 1];
+      if (e0 == e1) continue;
+      const cptr<float> rec = w.bp.sobj + BS_STRIDE * sid;
+      float sr[BS_STRIDE];
+#pragma unroll
+      for (int k = 0; k < BS_STRIDE; ++k) sr[k] = rec[k];
+#pragma unroll 2
+      for (int e = e0; e < e1; ++e) {
+        if (e - eb == 32) {
+          push(eb, kb);
+          eb = e;
+          kb = 0u;
+        }
+        const float* rm = cen + (size_t)w.st_m[e] * 3 * BLOCK + tid;
+        const float cm[3] = {rm[0], rm[BLOCK], rm[2 * BLOCK]};
+        kb |= (uint32_t)!fsphere_obb_separated(cm, w.st_r[e], sr, w.bp_margin) << (e - eb);
+      }
+    }
+    push(eb, kb);
+  }
+  // moving-moving pairs: bounding spheres (both centres from LDS)
   for (int m = 0; m < w.n_moving; ++m) {
-    // link-pose input: every static partner, also those the reach balls
-    // rule out (they assume kinematics)
-    const int e0 = w.sched_start[m], em = w.sched_mid[m], e1 = w.sched_start[m + 1];
+    const int e0 = w.sched_start[m], e1 = w.sched_start[m + 1];
     if (e0 == e1) continue;
     const float* rm = cen + (size_t)m * 3 * BLOCK + tid;
     const float cm[3] = {rm[0], rm[BLOCK], rm[2 * BLOCK]};
     const float r_m = w.bp.mobj[BM_STRIDE * m + BM_R];
-    // static partners, two per test: the partners' OBB records are inline in
-    // the schedule, interleaved in pairs (fsphere_obb_keep2: packed fp32 math
-    // on whole scalar-register pairs, no partner-index indirection)
-    for (int seg = 0; seg < (FROM_POSES ? 2 : 1); ++seg) {
-      const int s0 = seg ? w.sched_keep[m] : e0, s1 = seg ? em : w.sched_keep[m];
-      const int p0 = seg ? w.sched_pr1[m] : w.sched_pr0[m];
-      if (w.dbg(12)) continue;  // diagnostics: without the static bounding tests
-      for (int eb = s0; eb < s1; eb += 32) {
-        const int ee = min(s1, eb + 32);
-        uint32_t kb = 0u;
-        int pr = p0 + ((eb - s0) >> 1);
-#pragma unroll 2
-        for (int e = eb; e < ee; e += 2, ++pr)
-          kb |= fsphere_obb_keep2(cm, r_m, w.sched_srec + 2 * BS_STRIDE * pr, w.bp_margin) << (e - eb);
-        push(eb, kb);
-      }
-    }
-    // moving partners: bounding spheres (the partner's centre from LDS)
-    for (int eb = em; eb < e1; eb += 32) {
+    for (int eb = e0; eb < e1; eb += 32) {
       const int ee = min(e1, eb + 32);
       uint32_t kb = 0u;
 #pragma unroll 4
@@ -1136,22 +1149,46 @@ __global__ __launch_bounds__(BLOCK) void cull_kernel(DevWorld w, const double* _
   }
   // survivor words -> surv, and this wave's candidate count per pair ->
   // cnt[pair][tile] (the bucketing's tile counts; cnt is zeroed before the
-  // launch, pairs without a survivor in the tile are skipped): one step per
-  // distinct surviving pair of the wave
+  // launch, pairs without a survivor in the tile are skipped).  The counts
+  // are a per-wave histogram in the idle queue area: 8-bit counters (<= 64
+  // each), four per word, every lane adding its own survivors, then each lane
+  // writes the counts of pairs lane, lane + 64, ...  Worlds with more pairs
+  // than the area holds (W > kQueue / 8) take one ballot per distinct pair.
   bool any = false;
   const long long tile = (cfg0 >> 6) + (tid >> 6);
-  for (int k = 0; k < w.W; ++k) {
-    uint32_t x = live ? survw[k * BLOCK + tid] : 0u;
-    if (live) surv[(long long)k * cap + cfg] = x;
-    any |= x != 0u;
-    for (;;) {
-      const unsigned long long m = __ballot(x != 0u);
-      if (m == 0) break;
-      const uint32_t xl = __builtin_amdgcn_readlane(x, __builtin_ctzll(m));
-      const int b = __builtin_ctz(xl);
-      const unsigned long long bb = __ballot((x >> b) & 1u);
-      x &= ~(1u << b);
-      if (lane == 0) cnt[(long long)(k * 32 + b) * n_tiles + tile] = (uint32_t)__popcll(bb);
+  if (w.W * 8 <= kQueue) {
+    uint32_t* hist = queue;
+    for (int i = (int)lane; i < w.W * 8; i += 64) hist[i] = 0u;
+    wave_lds_sync();
+    for (int k = 0; k < w.W; ++k) {
+      uint32_t x = live ? survw[k * BLOCK + tid] : 0u;
+      if (live) surv[(long long)k * cap + cfg] = x;
+      any |= x != 0u;
+      while (x) {
+        const int p = k * 32 + __builtin_ctz(x);
+        x &= x - 1u;
+        atomicAdd(&hist[p >> 2], 1u << (8 * (p & 3)));
+      }
+    }
+    wave_lds_sync();
+    for (int p = (int)lane; p < w.W * 32; p += 64) {
+      const uint32_t c = (hist[p >> 2] >> (8 * (p & 3))) & 0xffu;
+      if (c) cnt[(long long)p * n_tiles + tile] = c;
+    }
+  } else {
+    for (int k = 0; k < w.W; ++k) {
+      uint32_t x = live ? survw[k * BLOCK + tid] : 0u;
+      if (live) surv[(long long)k * cap + cfg] = x;
+      any |= x != 0u;
+      for (;;) {
+        const unsigned long long m = __ballot(x != 0u);
+        if (m == 0) break;
+        const uint32_t xl = __builtin_amdgcn_readlane(x, __builtin_ctzll(m));
+        const int b = __builtin_ctz(xl);
+        const unsigned long long bb = __ballot((x >> b) & 1u);
+        x &= ~(1u << b);
+        if (lane == 0) cnt[(long long)(k * 32 + b) * n_tiles + tile] = (uint32_t)__popcll(bb);
+      }
     }
   }
   if (FROM_POSES || w.dbg(9)) return;  // 9: ablation without the sincos pass
@@ -7645,58 +7682,49 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
   std::vector<int> all_mask(std::max(W, 1), 0);
   for (int p = 0; p < d->n_pairs; ++p)
     if (!allowed[p]) all_mask[p >> 5] |= (int)(1u << (p & 31));
-  // per moving object: its static partners first (their OBB record inline in
-  // the entry; those that can be near before those that never are), then its
-  // moving partners
-  std::vector<int> sched_start(d->n_moving + 1, 0), sched_mid(std::max(d->n_moving, 1), 0),
-      sched_keep(std::max(d->n_moving, 1), 0), sched_pr0(std::max(d->n_moving, 1), 0),
-      sched_pr1(std::max(d->n_moving, 1), 0), sched_pair, sched_other;
-  std::vector<float> sched_srec;  // static records in pairs, interleaved (2 * BS_STRIDE floats per pair)
-  // a record no sphere can reach: the odd entry of a segment's last pair
-  std::vector<float> far_rec(BS_STRIDE, 0.f);
-  for (int k = 0; k < 3; ++k) far_rec[BS_C + k] = 1e15f;
-  for (int k = 0; k < 3; ++k) far_rec[BS_R + 4 * k] = 1.f;
-  std::vector<const float*> seg_recs;
-  auto flush_pairs = [&]() {  // seg_recs -> interleaved pairs
-    for (size_t i = 0; i < seg_recs.size(); i += 2) {
-      const float* ra = seg_recs[i];
-      const float* rb = i + 1 < seg_recs.size() ? seg_recs[i + 1] : far_rec.data();
-      for (int k = 0; k < BS_STRIDE; ++k) {
-        sched_srec.push_back(ra[k]);
-        sched_srec.push_back(rb[k]);
-      }
-    }
-    seg_recs.clear();
-  };
+  // moving-moving pairs by their lower moving object, then the moving-static
+  // pairs static-major (one static record serves all its entries), those the
+  // object's reach ball can bring near (group 0) before the rest (group 1)
+  const int ns = d->n_static;
+  std::vector<int> sched_start(d->n_moving + 1, 0), sched_pair, sched_other, st_start(2 * (ns + 1), 0), st_m;
+  std::vector<float> st_r;
   for (int m = 0; m < d->n_moving; ++m) {
     sched_start[m] = (int)sched_pair.size();
-    for (int pass = 0; pass < 3; ++pass) {  // statics that can be near, statics never near, movers
-      flush_pairs();
-      if (pass == 0) sched_pr0[m] = (int)(sched_srec.size() / (2 * BS_STRIDE));
-      if (pass == 1) {
-        sched_keep[m] = (int)sched_pair.size();
-        sched_pr1[m] = (int)(sched_srec.size() / (2 * BS_STRIDE));
-      }
-      if (pass == 2) sched_mid[m] = (int)sched_pair.size();
-      for (int p = 0; p < d->n_pairs; ++p) {
-        if (allowed[p]) continue;
-        const int a = d->pair_a[p], b = d->pair_b[p];
-        const int lo = std::min(a, b), hi = std::max(a, b);  // static ids are >= n_moving
-        if (lo != m || (hi >= d->n_moving) != (pass < 2)) continue;
-        if (pass < 2 && never_near(m, hi - d->n_moving) != (pass == 1)) continue;
-        sched_pair.push_back(p);
-        sched_other.push_back(hi);
-        if (pass < 2) seg_recs.push_back(bpp.sobj.data() + (size_t)BS_STRIDE * (hi - d->n_moving));
-      }
+    for (int p = 0; p < d->n_pairs; ++p) {
+      if (allowed[p]) continue;
+      const int a = d->pair_a[p], b = d->pair_b[p];
+      const int lo = std::min(a, b), hi = std::max(a, b);  // static ids are >= n_moving
+      if (lo != m || hi >= d->n_moving) continue;
+      sched_pair.push_back(p);
+      sched_other.push_back(hi);
+      st_m.push_back(0);
+      st_r.push_back(0.f);
     }
   }
   sched_start[d->n_moving] = (int)sched_pair.size();
+  for (int g = 0; g < 2; ++g) {
+    for (int sid = 0; sid < ns; ++sid) {
+      st_start[g * (ns + 1) + sid] = (int)sched_pair.size();
+      for (int m = 0; m < d->n_moving; ++m)
+        for (int p = 0; p < d->n_pairs; ++p) {
+          if (allowed[p]) continue;
+          const int a = d->pair_a[p], b = d->pair_b[p];
+          if (std::min(a, b) != m || std::max(a, b) != d->n_moving + sid) continue;
+          if (never_near(m, sid) != (g == 1)) continue;
+          sched_pair.push_back(p);
+          sched_other.push_back(d->n_moving + sid);
+          st_m.push_back(m);
+          st_r.push_back(bpp.mobj[BM_STRIDE * m + BM_R]);
+        }
+    }
+    st_start[g * (ns + 1) + ns] = (int)sched_pair.size();
+  }
   if (sched_pair.empty()) {
     sched_pair.push_back(0);
     sched_other.push_back(0);
+    st_m.push_back(0);
+    st_r.push_back(0.f);
   }
-  flush_pairs();
-  if (sched_srec.empty()) sched_srec.assign(2 * BS_STRIDE, 0.f);
 
   BlobBuilder bb;
   const size_t o_jt = bb.add(d->joint_type, d->n_joints);
@@ -7743,13 +7771,11 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
   const size_t o_ss = bb.add(sched_start.data(), sched_start.size());
   const size_t o_sp = bb.add(sched_pair.data(), sched_pair.size());
   const size_t o_so = bb.add(sched_other.data(), sched_other.size());
-  const size_t o_sm = bb.add(sched_mid.data(), sched_mid.size());
-  const size_t o_sk = bb.add(sched_keep.data(), sched_keep.size());
-  const size_t o_spr0 = bb.add(sched_pr0.data(), sched_pr0.size());
-  const size_t o_spr1 = bb.add(sched_pr1.data(), sched_pr1.size());
+  const size_t o_sts = bb.add(st_start.data(), st_start.size());
+  const size_t o_stm = bb.add(st_m.data(), st_m.size());
+  const size_t o_str = bb.add(st_r.data(), st_r.size());
   const size_t o_pbd = bb.add(prism_bound.data(), prism_bound.size());
   const size_t o_amk = bb.add(all_mask.data(), all_mask.size());
-  const size_t o_ssr = bb.add(sched_srec.data(), sched_srec.size());
   const size_t o_bjs = bb.add(bpp.jsrc.data(), bpp.jsrc.size());
   const size_t o_bjv = bb.add(bpp.jsave.data(), bpp.jsave.size());
   const size_t o_bja = bb.add(bpp.jaxis.data(), bpp.jaxis.size());
@@ -7888,11 +7914,9 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
   dw.sched_start = I(o_ss);
   dw.sched_pair = I(o_sp);
   dw.sched_other = I(o_so);
-  dw.sched_mid = I(o_sm);
-  dw.sched_keep = I(o_sk);
-  dw.sched_pr0 = I(o_spr0);
-  dw.sched_pr1 = I(o_spr1);
-  dw.sched_srec = to_cptr<float>(base + o_ssr);
+  dw.st_start = I(o_sts);
+  dw.st_m = I(o_stm);
+  dw.st_r = to_cptr<float>(base + o_str);
   auto F = [&](size_t o) { return to_cptr<float>(base + o); };
   BpView& bp = dw.bp;
   bp.nj = d->n_joints;
