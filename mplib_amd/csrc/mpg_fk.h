@@ -107,6 +107,11 @@ struct DevWorld {
   cptr<double> prism_bound; // [nj] |q| bound of such a joint, 0 = none
   double pose_bound;        // link-pose input: |position| bound of every link (beyond it: every pair)
   cptr<int> all_mask;       // [W] bits of every non-allowed pair
+  // visited sets of walk hulls above kMaxWalkVerts vertices (wave_walk):
+  // big_slots slots of big_words words, all zero while free; big_busy[slot]
+  unsigned long long* big_vis;
+  int* big_busy;
+  int big_slots, big_words;
   // octrees: leaf boxes [L][6] (octree frame), per geometry a uniform grid
   // record (OG_*), cell -> leaf lists (CSR)
   cptr<double> oct_leaf;

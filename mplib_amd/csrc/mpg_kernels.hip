@@ -160,13 +160,39 @@ __device__ __forceinline__ double lane_bcast(double v, int L) {
 // (rank among nact), from vertex 0 or resumed from a prefix record (pre:
 // mpg_hullcells.h WalkPrefix, the state where the host's replay stopped).
 // Returns the final vertex index (uniform).
+// A hull above kMaxWalkVerts vertices keeps its visited set in one slot of the
+// world's global pool (big_vis, zero while free): the wave's first active lane
+// claims a free slot (big_busy 0 -> 1), the wave clears the slot's words after
+// the climb and releases it.  Holders never wait, so a wave that finds every
+// slot taken only spins until one of them finishes.
+__device__ __forceinline__ int big_vis_acquire(const DevWorld& w, int rank) {
+  int slot = 0;
+  if (rank == 0) {
+    const int n = w.big_slots;
+    int k = (int)((blockIdx.x * 8u + (threadIdx.x >> 6)) % (unsigned)n);
+    while (atomicCAS(&w.big_busy[k], 0, 1) != 0) k = k + 1 == n ? 0 : k + 1;
+    slot = k;
+  }
+  // rank 0 is the first active lane
+  return __builtin_amdgcn_readfirstlane(slot);
+}
+
 __device__ __forceinline__ int wave_walk(const DevWorld& w, cptr<double> HV, int geom, const V3& d, int rank,
                                          int nact, cptr<int> pre) {
   WalkScratch& S = walk_scratch();
   const cptr<int> hd = w.hull_nbr + 2 * w.geom_nbr[geom];
   const int nwords = (w.geom_nvert[geom] + 63) >> 6;
-  for (int j = rank; j < nwords; j += nact)
-    S.vis[j] = pre ? (uint64_t)(uint32_t)pre[4 + 2 * j] | ((uint64_t)(uint32_t)pre[5 + 2 * j] << 32) : (j == 0 ? 1ull : 0ull);
+  const bool big = nwords > kWalkWords;  // no cell tables either: pre == nullptr
+  const int slot = big ? big_vis_acquire(w, rank) : -1;
+  // the visited set: the wave's LDS bitset or the pool slot, one flat pointer
+  unsigned long long* vis = big ? w.big_vis + (size_t)slot * w.big_words : (unsigned long long*)S.vis;
+  if (big) {
+    if (rank == 0) atomicOr(&vis[0], 1ull);  // vertex 0: the start (the slot is zero)
+    __threadfence();
+  } else {
+    for (int j = rank; j < nwords; j += nact)
+      S.vis[j] = pre ? (uint64_t)(uint32_t)pre[4 + 2 * j] | ((uint64_t)(uint32_t)pre[5 + 2 * j] << 32) : (j == 0 ? 1ull : 0ull);
+  }
   wave_lds_sync();
   int bi = pre ? pre[0] : 0, pv = pre ? pre[1] : 0, k0 = pre ? pre[2] : 0;
   bool keep = pre ? pre[3] != 0 : false, first = true;
@@ -183,8 +209,8 @@ __device__ __forceinline__ int wave_walk(const DevWorld& w, cptr<double> HV, int
         const cptr<double> e = w.nbr_ent + 4 * (size_t)(start + c0 + rank);
         const int vi = (int)e[3];
         const uint64_t bit = 1ull << (vi & 63);
-        const bool seen = (S.vis[vi >> 6] & bit) != 0ull;
-        if (!seen) atomicOr((unsigned long long*)&S.vis[vi >> 6], (unsigned long long)bit);
+        // test-and-set (a neighbour list has no repeats)
+        const bool seen = (atomicOr(&vis[vi >> 6], (unsigned long long)bit) & bit) != 0ull;
         S.vi[rank] = seen ? -1 : vi;
         S.dd[rank] = seen ? 0.0 : (d.x * e[0] + d.y * e[1]) + d.z * e[2];
       }
@@ -203,6 +229,12 @@ __device__ __forceinline__ int wave_walk(const DevWorld& w, cptr<double> HV, int
     bi = __builtin_amdgcn_readfirstlane(bi);
     keep = moved;
   } while (keep);
+  if (big) {  // leave the slot zero, then free it
+    for (int j = rank; j < nwords; j += nact) atomicExch(&vis[j], 0ull);
+    __threadfence();
+    wave_lds_sync();
+    if (rank == 0) atomicExch(&w.big_busy[slot], 0);
+  }
   return bi;
 }
 
@@ -884,9 +916,6 @@ __device__ __forceinline__ uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi
 //      written to surv[word][cfg] at the end (no global atomics).
 // Also zeroes this configuration's outputs for phase B.
 // ---------------------------------------------------------------------------
-#ifndef MPG_NARROW_WAVES
-#define MPG_NARROW_WAVES
-#endif
 #ifndef MPG_TASK
 #define MPG_TASK 128
 #endif
@@ -2558,7 +2587,10 @@ __device__ __forceinline__ void unstage_obj(float (*stg)[64], int c0, uint32_t s
 }
 
 template <bool FROM_POSES>
-__global__ __launch_bounds__(256) MPG_NARROW_WAVES void narrow_kernel(DevWorld w, const double* __restrict__ in,
+// 3 waves per SIMD: the kernel sits at the 168-VGPR edge of that occupancy
+// (a few registers more, e.g. an inlined rare path, would drop it to 2 and
+// cost ~40 % of its throughput)
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void narrow_kernel(DevWorld w, const double* __restrict__ in,
                                                     const uint32_t* __restrict__ seg_len,
                                                     const uint32_t* __restrict__ seg_start,
                                                     const uint32_t* __restrict__ prefix,
@@ -7315,6 +7347,7 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
   std::vector<double> cell_rec, cell_ovf, wcell_rec, wcell_ovf, wcell_aux, nbr_ent;
   const int walk_subk =
       std::getenv("MPG_WALK_SUBK") ? std::max(1, std::min(8, std::atoi(std::getenv("MPG_WALK_SUBK")))) : kSubK;
+  int big_words = 0;  // walk hulls above kMaxWalkVerts: the widest visited set
   for (int g = 0; g < d->n_geoms; ++g) {
     if (d->geom_type[g] != MPG_GEOM_CONVEX) continue;
     const double* Vg = d->vertices + 3 * (size_t)d->geom_vertex_start[g];
@@ -7327,11 +7360,8 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
     if (std::getenv("MPG_DEBUG_NO_WALK")) walk = false;
 #endif
     if (walk) {
-      if (nvg > kMaxWalkVerts)
-        return set_error(MPG_E_UNSUPPORTED, "convex hull with more than " + std::to_string(kMaxWalkVerts) +
-                                                " vertices and watertight faces (FCL's neighbour-walk support) "
-                                                "is not supported on the device");
       geom_nbr[g] = (int)(hull_nbr.size() / 2);
+      if (nvg > kMaxWalkVerts) big_words = std::max(big_words, (nvg + 63) / 64);  // pooled visited set
       for (int i = 0; i < nvg; ++i) {
         const int st = enc[i], cnt = enc[st];
         hull_nbr.push_back((int)(nbr_ent.size() / 4));
@@ -7855,6 +7885,17 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
 #ifdef MPG_DIAG  // ablation builds only (changes results)
   if (const char* e = std::getenv("MPG_DEBUG_CULL")) dw.debug_mode = std::atoi(e);
 #endif
+  dw.big_vis = nullptr;
+  dw.big_busy = nullptr;
+  dw.big_slots = 0;
+  dw.big_words = big_words;
+  if (big_words > 0) {  // one visited set per resident wave at most (256 CUs x 32 waves)
+    dw.big_slots = 8192;
+    HIP_TRY(hipMalloc(&dw.big_vis, sizeof(unsigned long long) * (size_t)dw.big_slots * big_words));
+    HIP_TRY(hipMemset(dw.big_vis, 0, sizeof(unsigned long long) * (size_t)dw.big_slots * big_words));
+    HIP_TRY(hipMalloc(&dw.big_busy, sizeof(int) * (size_t)dw.big_slots));
+    HIP_TRY(hipMemset(dw.big_busy, 0, sizeof(int) * (size_t)dw.big_slots));
+  }
   dw.stats = nullptr;
   if (std::getenv("MPG_STATS") && std::atoi(std::getenv("MPG_STATS")) > 0) {
     HIP_TRY(hipMalloc(&dw.stats, 48 * sizeof(unsigned long long)));
@@ -7998,6 +8039,8 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
 int mpg_world_destroy(mpg_world* w) {
   if (!w) return MPG_OK;
   hipSetDevice(w->device);
+  if (w->dw.big_vis) hipFree(w->dw.big_vis);
+  if (w->dw.big_busy) hipFree(w->dw.big_busy);
   if (w->dw.stats) {
     unsigned long long st[48];
     hipDeviceSynchronize();

@@ -961,6 +961,30 @@ def test_big_walk_hulls_match_oracle(monkeypatch):
                     np.testing.assert_array_equal(m, mo[i:i + k])
 
 
+def test_huge_walk_hull_matches_oracle(monkeypatch):
+    """a watertight hull above 4096 vertices (a 6322-vertex UV
+    sphere) is accepted -- its neighbour walk keeps the visited set in a
+    pooled global slot instead of the per-wave LDS bitset -- and every flag
+    and pair bit equals the oracle's walk on both batch paths and the
+    latency server's batches of 1 and 16 states."""
+    monkeypatch.setenv("MPG_SMALL_SERVER", "1")
+    o = Wd.huge_hull_world()
+    assert len(o.scene[0][1].vertices) > 4096
+    d = DeviceWorld(Wd.desc_arrays(o))
+    q = Wd.sample_q(o.art, 4000, 808)
+    f, m = d.collide_batch(q)
+    fo, mo = o.collide_batch(q, nthreads=NTHREADS)
+    k = [i for i, pn in enumerate(o.pair_names()) if pn[1] == "huge_ball"]
+    assert sum(int(((mo[:, p >> 5] >> (p & 31)) & 1).sum()) for p in k) > 20
+    np.testing.assert_array_equal(f, fo)
+    np.testing.assert_array_equal(m, mo)
+    for bs in (1, 16):
+        for i in range(0, 160, bs):
+            f, m = d.collide_batch(q[i:i + bs])
+            np.testing.assert_array_equal(f, fo[i:i + bs])
+            np.testing.assert_array_equal(m, mo[i:i + bs])
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("n", [5, 300, 5000])
 def test_dof0_world_with_moving_links(n):

@@ -69,22 +69,3 @@ def test_cone_with_long_cell_lists():
                    rng.standard_normal((5000, 3)) * [0.05, 0.05, 1.0] - [0, 0, 2.0]])
     st = check(g, d.astype(np.float32).astype(np.float64))
     assert st[5] == 0, f"{st[5]} of {st[0]} directions disagree with the walk"
-
-
-@pytest.mark.gpu
-def test_hull_above_walk_limit_is_refused():
-    """A watertight hull above kMaxWalkVerts (4096) vertices cannot get walk
-    tables: world creation refuses it with NotImplementedError (DESIGN.md
-    section 9), never a silent linear-support answer."""
-    from scipy.spatial import ConvexHull
-    from mplib_amd import pymp, scenes
-    rng = np.random.default_rng(0)
-    p = rng.normal(size=(5000, 3))
-    p = 0.1 * p / np.linalg.norm(p, axis=1)[:, None]
-    h = ConvexHull(p)
-    assert len(h.vertices) > 4096
-    w, _ = scenes.world(2)
-    w.add_normal_object("ball", pymp.fcl.CollisionObject(pymp.fcl.Convex(p, h.simplices.astype(np.int32), True),
-                                                          [0.6, 0.0, 0.4], [1, 0, 0, 0]))
-    with pytest.raises(NotImplementedError, match="4096"):
-        w.collide()

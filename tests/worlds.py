@@ -302,6 +302,16 @@ def uv_sphere_hull(stacks: int = 24, slices: int = 32, r: float = 0.1):
     return M.ConvexGeom(np.asarray(V, np.float64), F)
 
 
+def huge_hull_world() -> oracle.OracleWorld:
+    """Panda + a 6322-vertex UV sphere: an FCL neighbour-walk hull above the
+    device's 4096-vertex LDS visited set (wave_walk's pooled global set)."""
+    art = panda_articulation()
+    rng = np.random.default_rng(98)
+    w, x, y, z = random_quat(rng)
+    return oracle.OracleWorld(art, scene=[("huge_ball", uv_sphere_hull(80, 80, 0.12),
+                                           (M.quat_to_mat(w, x, y, z), [0.4, -0.2, 0.45]))])
+
+
 def big_hull_world() -> oracle.OracleWorld:
     """Panda + a 302-vertex cone + a 770-vertex sphere (FCL neighbour-walk
     hulls beyond the round-2 device limits), at fixed random poses."""
