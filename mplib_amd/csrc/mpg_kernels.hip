@@ -3336,10 +3336,16 @@ __global__ __launch_bounds__(kSrvThreads) void lat_server_kernel(DevWorld w, Srv
       for (;;) {
         const unsigned long long sq = sys_load(&ctl->seq);
         if (sq != last) {
-          // pairs with the host's release store of seq: the row loads below
-          // (this thread's, and the workgroup's after the barrier) are
-          // ordered after it by the memory model, not only by s_waitcnt
-          cmd = __hip_atomic_load(&ctl->seq, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+          // The host stores the rows, then seq with release (x86: in order).
+          // The rows are read below with system-coherent loads (sys_load: sc0
+          // sc1, past L1 and L2), issued only after this value returned (the
+          // branch waits on it), so they see the host's row stores.  The
+          // compiler fence keeps them after this load in the program; a
+          // system-scope acquire would add an L2 invalidate per batch, which
+          // measured +1.8 us on the one-state round trip
+          // (profiles/r05a/server_acquire.txt) and protects nothing here.
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+          cmd = sq;
           break;
         }
         if (sys_load(&ctl->quit) != 0ull) break;
