@@ -124,13 +124,25 @@ MPG_INLINE void f_quat_to_mat(float w, float x, float y, float z, float* m) {
   m[8] = 1.f - (txx + tyy);
 }
 
-// the third column of a row-major rotation from the first two (c2 = c0 x c1):
-// phase A keeps two columns per object for the SAT stage
-MPG_INLINE void f_complete_rotation(float* m) {
-  MPG_FP32_CONTRACT
-  m[2] = m[3] * m[7] - m[6] * m[4];
-  m[5] = m[6] * m[1] - m[0] * m[7];
-  m[8] = m[0] * m[4] - m[3] * m[1];
+// rotation -> unit quaternion (x, y, z, w); Shepperd's method, branch-free selects
+MPG_INLINE void f_mat_to_quat(const float* m, float* q) {
+  const float t0 = m[0] + m[4] + m[8];
+  const float d0 = 1.f + t0, d1 = 1.f + m[0] - m[4] - m[8], d2 = 1.f - m[0] + m[4] - m[8],
+              d3 = 1.f - m[0] - m[4] + m[8];
+  int k = 0;
+  float best = d0;
+  if (d1 > best) { best = d1; k = 1; }
+  if (d2 > best) { best = d2; k = 2; }
+  if (d3 > best) { best = d3; k = 3; }
+  const float s = 0.5f / sqrtf(best);
+  const float h = 0.5f * sqrtf(best);
+  const float a = (m[7] - m[5]) * s, b = (m[2] - m[6]) * s, c = (m[3] - m[1]) * s;  // w*4 components
+  const float e = (m[1] + m[3]) * s, f = (m[2] + m[6]) * s, g = (m[5] + m[7]) * s;
+  // k = 0: w = h, (a, b, c); k = 1: x = h, w = a, y = e, z = f; ...
+  q[0] = k == 0 ? a : k == 1 ? h : k == 2 ? e : f;
+  q[1] = k == 0 ? b : k == 1 ? e : k == 2 ? h : g;
+  q[2] = k == 0 ? c : k == 1 ? f : k == 2 ? g : h;
+  q[3] = k == 0 ? h : k == 1 ? a : k == 2 ? b : c;
 }
 
 // revolute angles are reduced in fp64 before the fp32 sincos so large user

@@ -902,9 +902,8 @@ __device__ __forceinline__ uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi
 // Phase A: one lane per configuration (mpg_broadphase.h).
 //   1. fp32 FK over the tree -> per moving object its world OBB centre in LDS
 //      ([object][3][lane]) and its rotation quaternion in the workspace
-//      (rq[object][6][cfg]: the first two columns of its rotation, read
-//      back only by the SAT stage, which completes the third by a cross
-//      product);
+//      (rq[object][4][cfg]: its rotation as a quaternion, read back only by
+//      the SAT stage);
 //   2. pairs are walked grouped by their moving object (host-built schedule,
 //      ACM-allowed pairs dropped): the object's centre is loaded once, then
 //      a cheap bounding test per partner (sphere-OBB against static objects,
@@ -940,15 +939,8 @@ __device__ __forceinline__ FObb bp_obb(const DevWorld& w, const float* __restric
                                        long long cap, int id, int t, long long cfg) {
   FObb o;
   if (id < w.n_moving) {
-    const float* q = rq + (size_t)id * 6 * cap + cfg;
-    // columns 0 and 1 of R; column 2 = column 0 x column 1
-    o.R[0] = q[0];
-    o.R[3] = q[cap];
-    o.R[6] = q[2 * cap];
-    o.R[1] = q[3 * cap];
-    o.R[4] = q[4 * cap];
-    o.R[7] = q[5 * cap];
-    f_complete_rotation(o.R);
+    const float* q = rq + (size_t)id * 4 * cap + cfg;
+    f_quat_to_mat(q[3 * cap], q[0], q[cap], q[2 * cap], o.R);
     const float* c = cen + (size_t)id * 3 * BLOCK + t;
     o.c[0] = c[0];
     o.c[1] = c[BLOCK];
@@ -1012,13 +1004,11 @@ __global__ __launch_bounds__(BLOCK) void cull_kernel(DevWorld w, const double* _
 
   auto put = [&](int m, const F34& T) {
     if (live && !w.dbg(13)) {  // 13: diagnostics, FK without the rq stores
-      float* r = rq + (size_t)m * 6 * cap + cfg;
-      r[0] = T.R[0];
-      r[cap] = T.R[3];
-      r[2 * cap] = T.R[6];
-      r[3 * cap] = T.R[1];
-      r[4 * cap] = T.R[4];
-      r[5 * cap] = T.R[7];
+      float q[4];
+      f_mat_to_quat(T.R, q);
+      float* r = rq + (size_t)m * 4 * cap + cfg;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) r[k * cap] = q[k];
     }
     float* r = cen + (size_t)m * 3 * BLOCK + tid;
     const cptr<float> g = w.bp.mobj + BM_STRIDE * m;
@@ -6330,7 +6320,7 @@ struct mpg_world {
     uint32_t* seg_start = nullptr;  // [n_pairs]
     uint32_t* prefix = nullptr;     // [n_pairs + 2] task prefix + task counter
     uint32_t* cand = nullptr;       // [n_pairs * cap] worst case
-    float* rq = nullptr;            // [n_moving * 6 * cap] phase-A rotations (two columns) for the SAT stage
+    float* rq = nullptr;            // [n_moving * 4 * cap] phase-A rotations (quaternions) for the SAT stage
     double* sc = nullptr;           // [cap * dof * 2] exact joint (sin, cos) for phase B
     long long cap = 0;
     uint64_t last = 0;              // LRU tick (get_workspace)
@@ -7064,7 +7054,7 @@ int get_workspace(mpg_world* w, hipStream_t s, long long want, mpg_world::Worksp
     HIP_TRY(hipMalloc(&ws.seg_start, sizeof(uint32_t) * np));
     HIP_TRY(hipMalloc(&ws.prefix, sizeof(uint32_t) * (np + 4)));
     HIP_TRY(hipMalloc(&ws.cand, sizeof(uint32_t) * np * want));
-    HIP_TRY(hipMalloc(&ws.rq, sizeof(float) * 6 * std::max(w->dw.n_moving, 1) * want));
+    HIP_TRY(hipMalloc(&ws.rq, sizeof(float) * 4 * std::max(w->dw.n_moving, 1) * want));
     HIP_TRY(hipMalloc(&ws.sc, sizeof(double) * 2 * std::max(w->dw.dof, 1) * want));
     ws.cap = want;
   }

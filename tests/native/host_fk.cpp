@@ -21,8 +21,8 @@ int host_fk(int nj, const int* jt, const int* jp, const int* jqs, const double* 
   return 0;
 }
 // fp32 broad-phase FK (mpg_broadphase.h bp_fk): every moving object's world
-// transform as float R[9] + p[3], plus the rotation the SAT stage rebuilds
-// from the two stored columns (rq[9], f_complete_rotation)
+// transform as float R[9] + p[3], plus the quaternion round trip of R that
+// the SAT stage uses (rq[9])
 int host_bp_objects(int nj, const int* jt, const int* jp, const int* jqs, const double* jqc, const double* jax,
                     const double* jpl, int dof, int n_links, const int* lp, const double* lpl, int n_moving,
                     const int* mlink, const double* moff, const double* q, long n, float* out, float* rq) {
@@ -42,9 +42,9 @@ int host_bp_objects(int nj, const int* jt, const int* jp, const int* jqs, const 
       float* o = out + (i * n_moving + m) * 12;
       for (int k = 0; k < 9; ++k) o[k] = T.R[k];
       for (int k = 0; k < 3; ++k) o[9 + k] = T.p[k];
-      float* r = rq + (i * n_moving + m) * 9;
-      for (int k = 0; k < 9; ++k) r[k] = T.R[k];
-      mpg::f_complete_rotation(r);
+      float qq[4];
+      mpg::f_mat_to_quat(T.R, qq);
+      mpg::f_quat_to_mat(qq[3], qq[0], qq[1], qq[2], rq + (i * n_moving + m) * 9);
     });
   }
   return 0;
