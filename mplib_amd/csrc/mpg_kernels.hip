@@ -259,7 +259,11 @@ __device__ __forceinline__ bool neighbour_beats(const DevWorld& w, cptr<double> 
 // tie at the maximum, or an uncertified fine cell) pend = true with the
 // linear list's first maximum in hand, for walk_resolve_wave.
 __device__ __forceinline__ V3 walk_cell_fast(const DevWorld& w, cptr<double> HV, int geom, cptr<double> R, int sub,
-                                             int fine, int fine2, const V3& d, bool& pend, int& pre) {
+                                             int fine, int fine2, const V3& d, bool& pend, int& pre,
+                                             unsigned long long t_cell = 0) {
+#ifdef MPG_STATS  // phase stamps (s_memtime after the value each phase produces)
+  unsigned long long t_rec = 0, t_ovf = 0;
+#endif
   const long long no = (long long)R[9];
   const int n = (int)(no & ((1 << kCellCountBits) - 1));
   const cptr<double> ovf = w.wcell_ovf + 4 * (size_t)(no >> kCellCountBits);
@@ -275,6 +279,10 @@ __device__ __forceinline__ V3 walk_cell_fast(const DevWorld& w, cptr<double> HV,
       g = k;
     }
   }
+#ifdef MPG_STATS
+  asm volatile("" ::"v"(best));
+  t_rec = __builtin_amdgcn_s_memtime();
+#endif
   int nmax = 0;  // ... and how many entries reach it (a tie when > 1)
   // the overflow entries kOvfBatch at a time: their loads issued together
   // (one memory round per batch, not per entry), then compared in list order
@@ -300,6 +308,10 @@ __device__ __forceinline__ V3 walk_cell_fast(const DevWorld& w, cptr<double> HV,
       }
     }
   }
+#ifdef MPG_STATS
+  asm volatile("" ::"v"(best));
+  t_ovf = __builtin_amdgcn_s_memtime();
+#endif
   // the inline entries, compared with the final maximum (short lists repeat
   // their first entry: count only k < n)
 #pragma unroll
@@ -318,6 +330,16 @@ __device__ __forceinline__ V3 walk_cell_fast(const DevWorld& w, cptr<double> HV,
     pre = endp <= -2 ? -2 - endp : -1;
   }
 #ifdef MPG_STATS
+  if (w.stats && t_cell) {  // support phases, first active lane: cell lookup -> record + inline dots ->
+    asm volatile("" ::"v"(pend));  // overflow entries -> tie / trap checks
+    const unsigned long long t_end = __builtin_amdgcn_s_memtime();
+    if ((uint32_t)__lane_id() == (uint32_t)__builtin_ctzll(__ballot(true))) {
+      atomicAdd(&w.stats[49], t_rec - t_cell);
+      atomicAdd(&w.stats[50], t_ovf - t_rec);
+      atomicAdd(&w.stats[51], t_end - t_ovf);
+      atomicAdd(&w.stats[52], 1ull);
+    }
+  }
   if (w.stats) {
     atomicAdd(&w.stats[10], 1ull);
     if (!pend) atomicAdd(&w.stats[11], 1ull);
@@ -431,10 +453,20 @@ __device__ __forceinline__ V3 convex_support_fast(const DevWorld& w, cptr<double
   if (w.geom_nbr[geom] >= 0) {  // neighbour-walk hull (wave-uniform branch)
     int sub = 0, fine = 0, fine2 = 0;
     pend = true;
+#ifdef MPG_STATS
+    const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+#endif
     cell = cb >= 0 ? hull_cell_sub(d.x, d.y, d.z, w.walk_subk, &sub, &fine, &fine2) : -1;
+    unsigned long long t_cell = 0;
+#ifdef MPG_STATS
+    asm volatile("" ::"v"(cell), "v"(sub), "v"(fine));
+    t_cell = __builtin_amdgcn_s_memtime();
+    if (w.stats && (uint32_t)__lane_id() == (uint32_t)__builtin_ctzll(__ballot(true))) atomicAdd(&w.stats[48], t_cell - t0);
+#endif
     V3 p = v3(0.0, 0.0, 0.0);
     if (cell >= 0)
-      p = walk_cell_fast(w, HV, geom, w.wcell_rec + kCellRec * (size_t)(cb + cell), sub, fine, fine2, d, pend, pre);
+      p = walk_cell_fast(w, HV, geom, w.wcell_rec + kCellRec * (size_t)(cb + cell), sub, fine, fine2, d, pend, pre,
+                         t_cell);
     return p;
   }
   const int c = cb >= 0 ? hull_cell(d.x, d.y, d.z) : -1;
@@ -581,6 +613,34 @@ __device__ __forceinline__ CV3 msupport(const DevWorld& w, cptr<double> HV, cons
     }
   }
   return vsub(vadd(quat_rot(la, a.rot), a.pos), vadd(quat_rot(lb, b.rot), b.pos));
+}
+
+// msupport on two half-waves: every lane of one half carries the same MPR
+// state as its partner lane ^ 32 of the other; lanes of side 0 evaluate a's
+// support, side 1 b's (at once, instead of one after the other on one lane),
+// then the halves swap their world points.  The arithmetic of each support is
+// msupport's, so the result is the same bits.  Geometry per lane (the halves
+// hold different shapes).
+__device__ __forceinline__ CV3 msupport_split(const DevWorld& w, cptr<double> HV, const GObj& a, const GObj& b,
+                                              const CV3& dir, bool side) {
+  const GObj o = side ? b : a;
+  const CV3 dl = quat_rot(side ? vscale(dir, ccd_real(-1)) : dir, o.rot_inv);
+  bool pend = false;
+  int cell = -1, pre = -1;
+  CV3 l;
+  if (o.type == MPG_GEOM_CONVEX) {
+    const V3 p = convex_support_fast(w, HV, o.geom, to_v3(dl), pend, cell, pre);
+    l = cv3(p.x, p.y, p.z);
+  } else {
+    l = support_local(w, HV, o.geom, o.type, dl);
+  }
+  if (__builtin_expect(__ballot(pend) != 0ull, 0)) {
+    const V3 p = walk_resolve_wave(w, HV, o.geom, to_v3(dl), cell, pend, pre, v3(l.x, l.y, l.z));
+    l = cv3(p.x, p.y, p.z);
+  }
+  const CV3 mine = vadd(quat_rot(l, o.rot), o.pos);
+  const CV3 other = CV3{__shfl_xor(mine.x, 32), __shfl_xor(mine.y, 32), __shfl_xor(mine.z, 32)};
+  return side ? vsub(other, mine) : vsub(mine, other);
 }
 
 // ---------------------------------------------------------------------------
@@ -3460,16 +3520,21 @@ __global__ __launch_bounds__(kSrvThreads) void lat_server_kernel(DevWorld w, Srv
       if (NEAR[p]) NLIST[atomicAdd(&s_nl, 1)] = p;
     __syncthreads();
     stamp(3);
-    // narrow: one near pair per wave at a time, lanes = states
+    // narrow: one near pair per wave at a time, lanes = states.  With at most
+    // 32 states both half-waves run every state's MPR (lane and lane ^ 32
+    // carry the same state) and split each support: one half a's, the other
+    // b's (msupport_split), which halves the support's dependent chain
     const int wv = t >> 6, lane = t & 63, nl = s_nl;
+    const bool split = n <= 32;
+    const int sl = split ? (lane & 31) : lane;  // the state this lane carries
     for (int k = wv; k < nl; k += kSrvThreads / 64) {
       const int p = __builtin_amdgcn_readfirstlane(NLIST[k]);
       const double* E = PT + (size_t)kSrvPT * p;
       const int cf = __builtin_amdgcn_readfirstlane((int)E[1]);
       const int ga = __builtin_amdgcn_readfirstlane((int)E[2]), gb = __builtin_amdgcn_readfirstlane((int)E[3]);
       const int a = __builtin_amdgcn_readfirstlane((int)E[4]), b = __builtin_amdgcn_readfirstlane((int)E[5]);
-      const bool near = lane < n && ((NEAR[p] >> lane) & 1u);
-      const int c = lane < n ? lane : 0;
+      const bool near = sl < n && ((NEAR[p] >> sl) & 1u);
+      const int c = sl < n ? sl : 0;
       const SE3 TA = a < M ? load_se3(TT + ((size_t)c * M + a) * 12) : load_se3(w.static_T + 12 * (a - M));
       const SE3 TB = b < M ? load_se3(TT + ((size_t)c * M + b) * 12) : load_se3(w.static_T + 12 * (b - M));
       bool hit = false;
@@ -3494,7 +3559,7 @@ __global__ __launch_bounds__(kSrvThreads) void lat_server_kernel(DevWorld w, Srv
         while (__ballot(st != MPR_DONE) != 0) {
           const unsigned long long c0 = w.stats ? __builtin_amdgcn_s_memtime() : 0ull;
           if (st != MPR_DONE) {
-            const CV3 sp = msupport(w, HV, A, B, dir);
+            const CV3 sp = split ? msupport_split(w, HV, A, B, dir, lane >= 32) : msupport(w, HV, A, B, dir);
             const unsigned long long c1 = w.stats ? __builtin_amdgcn_s_memtime() : 0ull;
             const int res = mpr_advance(w.mpr_tol, sp, st, v0, v1, v2, v3, dir);
             if (res != 0) {
@@ -3515,7 +3580,7 @@ __global__ __launch_bounds__(kSrvThreads) void lat_server_kernel(DevWorld w, Srv
           atomicMax(&w.stats[23], n_it);
         }
       }
-      if (hit) atomicOr(&HM[c * W + (p >> 5)], 1u << (p & 31));
+      if (hit && (!split || lane < 32)) atomicOr(&HM[c * W + (p >> 5)], 1u << (p & 31));
     }
     __syncthreads();
     stamp(4);
@@ -7894,8 +7959,8 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
   }
   dw.stats = nullptr;
   if (std::getenv("MPG_STATS") && std::atoi(std::getenv("MPG_STATS")) > 0) {
-    HIP_TRY(hipMalloc(&dw.stats, 48 * sizeof(unsigned long long)));
-    HIP_TRY(hipMemset(dw.stats, 0, 48 * sizeof(unsigned long long)));
+    HIP_TRY(hipMalloc(&dw.stats, 64 * sizeof(unsigned long long)));
+    HIP_TRY(hipMemset(dw.stats, 0, 64 * sizeof(unsigned long long)));
   }
   dw.joint_type = to_cptr<int>(base + o_jt);
   dw.joint_parent = to_cptr<int>(base + o_jp);
@@ -8038,7 +8103,7 @@ int mpg_world_destroy(mpg_world* w) {
   if (w->dw.big_vis) hipFree(w->dw.big_vis);
   if (w->dw.big_busy) hipFree(w->dw.big_busy);
   if (w->dw.stats) {
-    unsigned long long st[48];
+    unsigned long long st[64];
     hipDeviceSynchronize();
     hipMemcpy(st, w->dw.stats, sizeof(st), hipMemcpyDeviceToHost);
     std::fprintf(stderr,
@@ -8053,6 +8118,11 @@ int mpg_world_destroy(mpg_world* w) {
     if (st[20])
       std::fprintf(stderr, "[mpg stats] latency server MPR steps: %llu (max %llu per pair), shader clocks per step: "
                    "support %.0f, advance %.0f\n", st[20], st[23], (double)st[21] / st[20], (double)st[22] / st[20]);
+    if (st[52])
+      std::fprintf(stderr, "[mpg stats] walk-hull support phases, shader clocks per hull support (%llu): cell lookup "
+                   "%.0f, record load + inline dots %.0f, overflow entries %.0f, tie / trap checks %.0f\n",
+                   st[52], (double)st[48] / st[52], (double)st[49] / st[52], (double)st[50] / st[52],
+                   (double)st[51] / st[52]);
     std::fprintf(stderr, "[mpg stats] small_kernel slowest narrow test: pair %llu, %.2f us\n",
                  (unsigned long long)(st[31] & 4095), (st[31] >> 12) / 100.0);
     std::fprintf(stderr, "[mpg stats] walk hulls: supports %llu, trap-free fast %llu, verified %llu, full walks %llu, "
