@@ -5650,18 +5650,20 @@ __device__ bool closed_form_contact(int cf, const DevWorld& w, int ga, const SE3
 // Contacts on BVH-mesh pairs (CollisionRequest(enable_contact=True)), one lane
 // per reported (configuration, pair), the lane alone -- the same restatement
 // as oracle/collide_oracle.c mesh_contact [ext FCL 0.7.0, parity unpinned]:
-// the first intersecting triangle (pair) in triangle index order (FCL's own
-// order follows its OBBRSS traversal, not restated), then
+// the first hit in FCL's traversal order (the reachable hit whose descent key
+// -- fcl_gate_shape's leaf position, fcl_gate_mesh's left / right choices,
+// fcl_gate_octree_mesh's octree children and mesh choices -- is smallest),
+// then
 //   mesh-mesh    intersect_Triangle's contact branch (computeDeepestPoints
 //                of each triangle against the other's plane), o1's frame ->
 //                world;
 //   shape-mesh   sphereTriangleIntersect's contact for spheres, libccd MPR
 //                penetration of (shape, triangle GJK object) otherwise; the
 //                mesh-first order negates the normal;
-//   mesh-OcTree  the first occupied leaf in traversal order with a hit, MPR
-//                penetration of (leaf box, lowest such triangle).
-// The AABB prefilters only skip separated triangles, so the first hit in
-// index order is the oracle's (which prunes with bounding spheres).
+//   mesh-OcTree  MPR penetration of (leaf box, triangle) of the first hit in
+//                OcTreeMeshIntersectRecurse's visit order.
+// The AABB prefilters only skip separated triangles and the gates replay
+// FCL's descent, so the first hit is the one the oracle's recursion finds.
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ void tri_plane(const double* v1, const double* v2, const double* v3, double* n, double& t) {
   double a[3], b[3];
@@ -7486,7 +7488,7 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
         r[TR_LO + k] = std::min(r[TR_P + k], std::min(r[TR_P + 3 + k], r[TR_P + 6 + k]));
         r[TR_HI + k] = std::max(r[TR_P + k], std::max(r[TR_P + 3 + k], r[TR_P + 6 + k]));
       }
-      r[TR_ID] = (double)t;  // the triangle's index in the mesh (contacts: first in index order)
+      r[TR_ID] = (double)t;  // the triangle's index in the mesh (its leaf position: tri_pos)
     }
     std::vector<int> order((size_t)tn);
     for (int64_t t = 0; t < tn; ++t) order[t] = (int)t;

@@ -2608,14 +2608,10 @@ static int mesh_intersect(const orc_world *w, int ga, const real *Ta, int gb, co
  *   mesh-OcTree OcTreeMeshIntersectRecurse with contacts: MPR penetration of
  *               (leaf box, triangle); the tree is the contact's o1.
  * num_max_contacts = 1 keeps the first leaf test that emits a contact in
- * FCL's traversal order.  For meshes that order follows FCL's OBBRSS tree,
- * which is not restated: here the first is the lowest triangle index
- * (mesh-mesh: the lexicographically lowest (triangle of o1, triangle of o2);
- * octree pairs: the first occupied leaf in traversal order, then the lowest
- * triangle).  With several intersecting triangle (pairs) the contact
- * reported can be a different one of them than FCL's; the collision flag is
- * the same.  A triangle pair whose deepest-point sets are both empty
- * (degenerate triangles) is reported with a zero contact. */
+ * FCL's traversal order: the recursions above (bvh_shape_walk,
+ * bvh_mesh_walk, octmesh_rec) stop at that test.  A triangle pair whose
+ * deepest-point sets are both empty (degenerate triangles) is reported with a
+ * zero contact. */
 static real plane_dist(const real *n, real t, const real *v) { return dot3(n, v) - t; }
 
 /* buildTrianglePlane: unit normal (v2 - v1) x (v3 - v1) and offset n . v1 */

@@ -136,6 +136,11 @@ def test_boundary_text_matches_the_code():
     for stale in ("GJK + fp64 EPA", "not restated)", "keep the ungated", "OBBRSS gate on single triangles is not"):
         assert stale not in design, stale
     assert "MPG_DISTANCE_EPA_CAPACITY" in hdr and "convexity guard" in hdr
+    # and the source comments next to the code (kernel, oracle)
+    for rel in ("mplib_amd/csrc/mpg_kernels.hip", "oracle/collide_oracle.c"):
+        src = open(os.path.join(ROOT, rel)).read()
+        for stale in ("triangle index order", "lowest triangle index", "first in index order"):
+            assert stale not in src, (rel, stale)
 
 
 def test_last_error_copy():
