@@ -73,6 +73,8 @@ struct BpView {
   cptr<int> jobj_start;  // [nj+2]
   cptr<int> jobj_order;  // [n_moving]
   cptr<float> oplace;    // [n_moving*12]
+  cptr<float> oquat;     // [n_moving*4] rotation of oplace as a quaternion (x, y, z, w)
+  cptr<float> ocen;      // [n_moving*3] the object's OBB centre in its joint frame (oplace * local centre)
 };
 
 // motion kinds of the fp32 FK: a fixed (or constant) joint, a revolute or
@@ -145,6 +147,16 @@ MPG_INLINE void f_mat_to_quat(const float* m, float* q) {
   q[3] = k == 0 ? h : k == 1 ? a : k == 2 ? b : c;
 }
 
+// Hamilton product a * b of unit quaternions (x, y, z, w): the rotation
+// R(a) R(b)
+MPG_INLINE void f_quat_mul(const float* a, const float* b, float* q) {
+  MPG_FP32_CONTRACT
+  q[0] = a[3] * b[0] + a[0] * b[3] + a[1] * b[2] - a[2] * b[1];
+  q[1] = a[3] * b[1] - a[0] * b[2] + a[1] * b[3] + a[2] * b[0];
+  q[2] = a[3] * b[2] + a[0] * b[1] - a[1] * b[0] + a[2] * b[3];
+  q[3] = a[3] * b[3] - a[0] * b[0] - a[1] * b[1] - a[2] * b[2];
+}
+
 // revolute angles are reduced in fp64 before the fp32 sincos so large user
 // values (continuous joints) keep full fp32 accuracy
 template <class P>
@@ -180,8 +192,10 @@ MPG_INLINE F34 f_joint_motion(int type, P axis, double v) {
   return M;
 }
 
-// fp32 FK over the whole tree; calls sink(m, T) with every moving object's
-// world transform (link pose * collision origin).  Per joint: A = parent *
+// fp32 FK over the whole tree; calls sink(m, J, jq) for every moving object
+// with its joint's world frame J and J's rotation as a quaternion jq (one
+// conversion per joint with objects): the object's pose is J * oplace[m],
+// its rotation jq * oquat[m], its OBB centre J * ocen[m].  Per joint: A = parent *
 // placement (one 3x4 product), then the motion applied in place -- a
 // principal-axis rotation mixes two columns of A.R, a principal-axis
 // translation adds one column to A.p, constant joints were folded into the
@@ -208,9 +222,13 @@ template <class Sink>
 MPG_INLINE void bp_fk(const BpView& b, const double* __restrict__ qrow, float* save, int stride, Sink&& sink) {
   MPG_FP32_CONTRACT
   F34 cur, r0, r1;
-  for (int o = b.jobj_start[0]; o < b.jobj_start[1]; ++o) {  // objects on the universe
-    const int m = b.jobj_order[o];
-    sink(m, f34_load(b.oplace + 12 * m));
+  if (b.jobj_start[0] < b.jobj_start[1]) {  // objects on the universe
+    F34 I;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) I.R[k] = (k % 4 == 0) ? 1.f : 0.f;
+    I.p[0] = I.p[1] = I.p[2] = 0.f;
+    const float iq[4] = {0.f, 0.f, 0.f, 1.f};
+    for (int o = b.jobj_start[0]; o < b.jobj_start[1]; ++o) sink(b.jobj_order[o], I, iq);
   }
 #pragma unroll 1
   for (int jj = 0; jj < b.nj; ++jj) {
@@ -279,9 +297,11 @@ MPG_INLINE void bp_fk(const BpView& b, const double* __restrict__ qrow, float* s
 #pragma unroll
       for (int i = 0; i < 3; ++i) sp[(9 + i) * stride] = cur.p[i];
     }
-    for (int o = b.jobj_start[jj + 1]; o < b.jobj_start[jj + 2]; ++o) {
-      const int m = b.jobj_order[o];
-      sink(m, f34_mul(cur, f34_load(b.oplace + 12 * m)));
+    const int o0 = b.jobj_start[jj + 1], o1 = b.jobj_start[jj + 2];
+    if (o0 < o1) {
+      float jq[4];
+      f_mat_to_quat(cur.R, jq);
+      for (int o = o0; o < o1; ++o) sink(b.jobj_order[o], cur, jq);
     }
   }
 }
@@ -402,7 +422,7 @@ inline uint32_t fsphere_obb_keep2(const float* c, float r, P rec, float margin) 
 struct BpProgram {
   int n_saves = 0;
   std::vector<int> jsrc, jsave, link_start, link_order, obj_start, obj_order, jkind, jobj_start, jobj_order;
-  std::vector<float> jaxis, jplace, lplace, moff, mobj, sobj, oplace;
+  std::vector<float> jaxis, jplace, lplace, moff, mobj, sobj, oplace, oquat, ocen;
 };
 
 // row-major 3x4 product in fp64 (host program folding)
@@ -413,6 +433,25 @@ inline void se3d_mul(const double* A, const double* B, double* C) {
     T[9 + i] = A[3 * i] * B[9] + A[3 * i + 1] * B[10] + A[3 * i + 2] * B[11] + A[9 + i];
   }
   for (int k = 0; k < 12; ++k) C[k] = T[k];
+}
+
+// unit quaternion (x, y, z, w) of a row-major rotation, fp64 (Shepperd)
+inline void mat_to_quat_d(const double* m, double* q) {
+  const double d[4] = {1.0 + m[0] + m[4] + m[8], 1.0 + m[0] - m[4] - m[8], 1.0 - m[0] + m[4] - m[8],
+                       1.0 - m[0] - m[4] + m[8]};
+  int k = 0;
+  for (int i = 1; i < 4; ++i)
+    if (d[i] > d[k]) k = i;
+  const double h = 0.5 * std::sqrt(d[k]), s = 0.25 / h;
+  if (k == 0) {
+    q[3] = h; q[0] = (m[7] - m[5]) * s; q[1] = (m[2] - m[6]) * s; q[2] = (m[3] - m[1]) * s;
+  } else if (k == 1) {
+    q[0] = h; q[3] = (m[7] - m[5]) * s; q[1] = (m[1] + m[3]) * s; q[2] = (m[2] + m[6]) * s;
+  } else if (k == 2) {
+    q[1] = h; q[3] = (m[2] - m[6]) * s; q[0] = (m[1] + m[3]) * s; q[2] = (m[5] + m[7]) * s;
+  } else {
+    q[2] = h; q[3] = (m[3] - m[1]) * s; q[0] = (m[2] + m[6]) * s; q[1] = (m[5] + m[7]) * s;
+  }
 }
 
 // a joint's motion at value v in fp64 (pinocchio's joint models)
@@ -500,10 +539,18 @@ inline void bp_build(const mpg_world_desc* d, const std::vector<double>& obb, Bp
       if (d->link_parent[d->moving_link[m]] == j) P.jobj_order.push_back(m);
   }
   P.jobj_start[nj + 1] = (int)P.jobj_order.size();
+  P.oquat.assign((size_t)4 * std::max(nm, 1), 0.f);
+  P.ocen.assign((size_t)3 * std::max(nm, 1), 0.f);
   for (int m = 0; m < nm; ++m) {
     double O[12];
     se3d_mul(d->link_placement + 12 * d->moving_link[m], d->moving_offset + 12 * m, O);
     for (int k = 0; k < 12; ++k) P.oplace[12 * m + k] = (float)O[k];
+    double q[4];
+    mat_to_quat_d(O, q);
+    for (int k = 0; k < 4; ++k) P.oquat[4 * m + k] = (float)q[k];
+    const double* g = obb.data() + 7 * d->moving_geom[m];  // local OBB centre
+    for (int i = 0; i < 3; ++i)
+      P.ocen[3 * m + i] = (float)(O[3 * i] * g[0] + O[3 * i + 1] * g[1] + O[3 * i + 2] * g[2] + O[9 + i]);
   }
   P.mobj.assign((size_t)BM_STRIDE * std::max(nm, 1), 0.f);
   for (int m = 0; m < nm; ++m) {
@@ -552,6 +599,8 @@ inline BpView bp_view(const mpg_world_desc* d, const BpProgram& P) {
   b.jobj_start = to_cptr<int>(P.jobj_start.data());
   b.jobj_order = to_cptr<int>(P.jobj_order.data());
   b.oplace = to_cptr<float>(P.oplace.data());
+  b.oquat = to_cptr<float>(P.oquat.data());
+  b.ocen = to_cptr<float>(P.ocen.data());
   return b;
 }
 

@@ -1062,19 +1062,37 @@ __global__ __launch_bounds__(BLOCK) void cull_kernel(DevWorld w, const double* _
   for (int k = 0; k < w.W; ++k) survw[k * BLOCK + tid] = 0u;
   if (w.dbg(14)) return;  // diagnostics: the launch and the output zeroing alone
 
-  auto put = [&](int m, const F34& T) {
+  // object m's rotation (quaternion q) to rq, its OBB centre to cen
+  auto store_obj = [&](int m, const float* q, const float* c) {
     if (live && !w.dbg(13)) {  // 13: diagnostics, FK without the rq stores
-      float q[4];
-      f_mat_to_quat(T.R, q);
       float* r = rq + (size_t)m * 4 * cap + cfg;
 #pragma unroll
       for (int k = 0; k < 4; ++k) r[k * cap] = q[k];
     }
     float* r = cen + (size_t)m * 3 * BLOCK + tid;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) r[i * BLOCK] = c[i];
+  };
+  // link-pose input: the object's world transform
+  auto put = [&](int m, const F34& T) {
+    float q[4], c[3];
+    f_mat_to_quat(T.R, q);
     const cptr<float> g = w.bp.mobj + BM_STRIDE * m;
 #pragma unroll
     for (int i = 0; i < 3; ++i)
-      r[i * BLOCK] = T.R[3 * i] * g[BM_C] + T.R[3 * i + 1] * g[BM_C + 1] + T.R[3 * i + 2] * g[BM_C + 2] + T.p[i];
+      c[i] = T.R[3 * i] * g[BM_C] + T.R[3 * i + 1] * g[BM_C + 1] + T.R[3 * i + 2] * g[BM_C + 2] + T.p[i];
+    store_obj(m, q, c);
+  };
+  // joint-value input: the object's joint frame J (and its quaternion jq)
+  auto put_j = [&](int m, const F34& J, const float* jq) {
+    MPG_FP32_CONTRACT
+    float q[4], c[3];
+    const cptr<float> oq = w.bp.oquat + 4 * m, oc = w.bp.ocen + 3 * m;
+    const float o[4] = {oq[0], oq[1], oq[2], oq[3]};
+    f_quat_mul(jq, o, q);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) c[i] = J.R[3 * i] * oc[0] + J.R[3 * i + 1] * oc[1] + J.R[3 * i + 2] * oc[2] + J.p[i];
+    store_obj(m, q, c);
   };
   // a configuration outside the bounds the cull's margins assume (a prismatic
   // value beyond its travel bound, or a given link pose beyond the chain's
@@ -1087,7 +1105,7 @@ __global__ __launch_bounds__(BLOCK) void cull_kernel(DevWorld w, const double* _
       forced |= !(std::fabs(pl[0]) <= w.pose_bound && std::fabs(pl[1]) <= w.pose_bound && std::fabs(pl[2]) <= w.pose_bound);
     }
   } else {
-    bp_fk(w.bp, in + c * w.dof, save + tid, BLOCK, put);
+    bp_fk(w.bp, in + c * w.dof, save + tid, BLOCK, put_j);
     if (w.n_prism)
       for (int j = 0; j < w.nj; ++j)
         if (w.prism_bound[j] >= 0.0) forced |= !(std::fabs(in[c * w.dof + w.joint_q_source[j]]) <= w.prism_bound[j]);
@@ -7886,6 +7904,8 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
   const size_t o_bjo = bb.add(bpp.jobj_start.data(), bpp.jobj_start.size());
   const size_t o_bjr = bb.add(bpp.jobj_order.data(), bpp.jobj_order.size());
   const size_t o_bop = bb.add(bpp.oplace.data(), bpp.oplace.size());
+  const size_t o_boq = bb.add(bpp.oquat.data(), bpp.oquat.size());
+  const size_t o_boc = bb.add(bpp.ocen.data(), bpp.ocen.size());
   const size_t o_olf = bb.add(oct_leaf.data(), oct_leaf.size());
   const size_t o_mtr = bb.add(mesh_tri.data(), mesh_tri.size());
   const size_t o_mnd = bb.add(mesh_node.data(), mesh_node.size());
@@ -8048,6 +8068,8 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
   bp.jobj_start = I(o_bjo);
   bp.jobj_order = I(o_bjr);
   bp.oplace = F(o_bop);
+  bp.oquat = F(o_boq);
+  bp.ocen = F(o_boc);
   dw.oct_leaf = to_cptr<double>(base + o_olf);
   dw.oct_path = to_cptr<uint64_t>(base + o_opa);
   dw.oct_depth = to_cptr<int>(base + o_ode);

@@ -1,7 +1,9 @@
 // Test shim: compiles the product's FK/math headers (mplib_amd/csrc/mpg_fk.h)
 // for the host with g++ -ffp-contract=off so tests can compare them with the
 // oracle on a machine without a GPU.  Not part of the product.
+#include <algorithm>
 #include <cfloat>
+#include <cmath>
 
 #include "../../mplib_amd/csrc/mpg_fk.h"
 
@@ -20,6 +22,8 @@ int host_fk(int nj, const int* jt, const int* jp, const int* jqs, const double* 
   }
   return 0;
 }
+static float g_cen_dev = 0.f;  // largest |J * ocen - T.p| seen by host_bp_objects
+float host_bp_cen_dev() { return g_cen_dev; }
 // fp32 broad-phase FK (mpg_broadphase.h bp_fk): every moving object's world
 // transform as float R[9] + p[3], plus the quaternion round trip of R that
 // the SAT stage uses (rq[9])
@@ -38,12 +42,23 @@ int host_bp_objects(int nj, const int* jt, const int* jp, const int* jqs, const 
   const mpg::BpView b = mpg::bp_view(&d, P);
   std::vector<float> save(12 * (P.n_saves + 1));
   for (long i = 0; i < n; ++i) {
-    mpg::bp_fk(b, q + i * dof, save.data(), 1, [&](int m, const mpg::F34& T) {
+    mpg::bp_fk(b, q + i * dof, save.data(), 1, [&](int m, const mpg::F34& J, const float* jq) {
+      // the object's pose J * oplace (checked against the fp64 FK) and the
+      // rotation the SAT stage rebuilds from jq * oquat
+      const mpg::F34 T = mpg::f34_mul(J, mpg::f34_load(b.oplace + 12 * m));
       float* o = out + (i * n_moving + m) * 12;
       for (int k = 0; k < 9; ++k) o[k] = T.R[k];
       for (int k = 0; k < 3; ++k) o[9 + k] = T.p[k];
+      // the OBB centre the cull stores, J * ocen (here the local centre is 0,
+      // so it must be T's position)
+      for (int k = 0; k < 3; ++k) {
+        const float c = J.R[3 * k] * b.ocen[3 * m] + J.R[3 * k + 1] * b.ocen[3 * m + 1] +
+                        J.R[3 * k + 2] * b.ocen[3 * m + 2] + J.p[k];
+        g_cen_dev = std::max(g_cen_dev, std::fabs(c - T.p[k]));
+      }
+      const float oq[4] = {b.oquat[4 * m], b.oquat[4 * m + 1], b.oquat[4 * m + 2], b.oquat[4 * m + 3]};
       float qq[4];
-      mpg::f_mat_to_quat(T.R, qq);
+      mpg::f_quat_mul(jq, oq, qq);
       mpg::f_quat_to_mat(qq[3], qq[0], qq[1], qq[2], rq + (i * n_moving + m) * 9);
     });
   }

@@ -66,6 +66,16 @@ def test_fp32_poses_within_margin_uniform():
     assert dp + 0.3 * 3 ** 0.5 * dRq < MARGIN / 10
 
 
+def test_fp32_object_centres_match_poses():
+    """The cull stores each object's OBB centre as J * ocen (its joint frame
+    times the host-folded centre); with a zero local centre that is the
+    object's position, which must agree with J * oplace to fp32 rounding."""
+    ow = Wd.oracle_world(3)
+    bp_objects(Wd.desc_arrays(ow), Wd.sample_q(ow.art, 20000, 13))
+    lib().host_bp_cen_dev.restype = ctypes.c_float
+    assert lib().host_bp_cen_dev() < 1e-5
+
+
 def test_fp32_poses_within_margin_extreme():
     ow = Wd.oracle_world(3)
     rng = np.random.default_rng(12)
