@@ -79,7 +79,9 @@ struct BpView {
 
 // motion kinds of the fp32 FK: a fixed (or constant) joint, a revolute or
 // prismatic joint about a principal axis (x, y, z), or about any unit axis
-enum BpKind { BK_FIXED = 0, BK_REV_X = 1, BK_REV_AXIS = 4, BK_PRI_X = 5, BK_PRI_AXIS = 8 };
+// (BK_SKIP: a constant joint no other joint hangs from, its objects folded
+// into its parent's)
+enum BpKind { BK_FIXED = 0, BK_REV_X = 1, BK_REV_AXIS = 4, BK_PRI_X = 5, BK_PRI_AXIS = 8, BK_SKIP = 9 };
 
 struct F34 {
   float R[9];  // row-major
@@ -233,6 +235,7 @@ MPG_INLINE void bp_fk(const BpView& b, const double* __restrict__ qrow, float* s
 #pragma unroll 1
   for (int jj = 0; jj < b.nj; ++jj) {
     const int kind = b.jkind[jj];
+    if (kind == BK_SKIP) continue;
     const F34 Pl = f34_load(b.jplace + 12 * jj);
     const int s = b.jsrc[jj];
     F34 A;
@@ -498,6 +501,7 @@ inline void bp_build(const mpg_world_desc* d, const std::vector<double>& obb, Bp
   }
   for (int i = 0; i < 3 * nj; ++i) P.jaxis.push_back((float)d->joint_axis[i]);
   P.jkind.assign(std::max(nj, 1), BK_FIXED);
+  std::vector<double> jpl_d((size_t)12 * std::max(nj, 1), 0.0);  // the placements in fp64
   for (int j = 0; j < nj; ++j) {
     const int t = d->joint_type[j];
     double Pl[12];
@@ -513,7 +517,17 @@ inline void bp_build(const mpg_world_desc* d, const std::vector<double>& obb, Bp
       P.jkind[j] = BK_PRI_X + (t - MPG_JOINT_PX);
     }
     for (int k = 0; k < 12; ++k) P.jplace.push_back((float)Pl[k]);
+    for (int k = 0; k < 12; ++k) jpl_d[12 * j + k] = Pl[k];
   }
+  // constant joints that no joint hangs from (leaves first, so chains of
+  // them fold too): skipped, their objects ride on the parent's frame
+  std::vector<int> live_children(nj + 1, 0);
+  for (int j = 1; j <= nj; ++j) ++live_children[d->joint_parent[j - 1]];
+  for (int j = nj; j >= 1; --j)
+    if (P.jkind[j - 1] == BK_FIXED && live_children[j] == 0) {
+      P.jkind[j - 1] = BK_SKIP;
+      --live_children[d->joint_parent[j - 1]];
+    }
   for (int i = 0; i < 12 * nl; ++i) P.lplace.push_back((float)d->link_placement[i]);
   for (int i = 0; i < 12 * nm; ++i) P.moff.push_back((float)d->moving_offset[i]);
   P.link_start.assign(nj + 2, 0);
@@ -530,20 +544,33 @@ inline void bp_build(const mpg_world_desc* d, const std::vector<double>& obb, Bp
       if (d->moving_link[m] == l) P.obj_order.push_back(m);
   }
   P.obj_start[nl] = (int)P.obj_order.size();
-  // objects by their link's parent joint, link placement * offset folded
+  // objects by the joint whose frame carries them (their link's parent joint,
+  // or its first ancestor that is not skipped), every placement from there
+  // to the collision origin folded into one transform
+  std::vector<int> ojoint(std::max(nm, 1), 0);
+  std::vector<double> ofold((size_t)12 * std::max(nm, 1), 0.0);
+  for (int m = 0; m < nm; ++m) {
+    double* O = ofold.data() + 12 * m;
+    se3d_mul(d->link_placement + 12 * d->moving_link[m], d->moving_offset + 12 * m, O);
+    int j = d->link_parent[d->moving_link[m]];
+    while (j > 0 && P.jkind[j - 1] == BK_SKIP) {
+      se3d_mul(jpl_d.data() + 12 * (j - 1), O, O);
+      j = d->joint_parent[j - 1];
+    }
+    ojoint[m] = j;
+  }
   P.jobj_start.assign(nj + 2, 0);
   P.oplace.assign((size_t)12 * std::max(nm, 1), 0.f);
   for (int j = 0; j <= nj; ++j) {
     P.jobj_start[j] = (int)P.jobj_order.size();
     for (int m = 0; m < nm; ++m)
-      if (d->link_parent[d->moving_link[m]] == j) P.jobj_order.push_back(m);
+      if (ojoint[m] == j) P.jobj_order.push_back(m);
   }
   P.jobj_start[nj + 1] = (int)P.jobj_order.size();
   P.oquat.assign((size_t)4 * std::max(nm, 1), 0.f);
   P.ocen.assign((size_t)3 * std::max(nm, 1), 0.f);
   for (int m = 0; m < nm; ++m) {
-    double O[12];
-    se3d_mul(d->link_placement + 12 * d->moving_link[m], d->moving_offset + 12 * m, O);
+    const double* O = ofold.data() + 12 * m;
     for (int k = 0; k < 12; ++k) P.oplace[12 * m + k] = (float)O[k];
     double q[4];
     mat_to_quat_d(O, q);
