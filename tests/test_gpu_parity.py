@@ -985,6 +985,44 @@ def test_huge_walk_hull_matches_oracle(monkeypatch):
             np.testing.assert_array_equal(m, mo[i:i + bs])
 
 
+def test_huge_walk_hull_distance_and_contacts():
+    """The 6322-vertex sphere of test_huge_walk_hull_matches_oracle through
+    the PlanningWorld API: batched distances (GJK on its neighbour-walk
+    support, pooled visited sets) equal the oracle's, and contacts of the
+    colliding states (MPR penetration) within 1e-9."""
+    o = Wd.huge_hull_world()
+    V = np.asarray(o.scene[0][1].vertices, np.float64)
+    F = np.asarray(o.scene[0][1].faces, np.int32)
+    pos = o.scene[0][2][1]
+    wxyz = Wd.random_quat(np.random.default_rng(98))  # the pose huge_hull_world draws
+    w, _ = scenes.world(2)
+    w.add_normal_object("huge_ball", pymp.fcl.CollisionObject(pymp.fcl.Convex(V, F, True), list(pos), list(wxyz)))
+    names = [(i[3], i[4]) for i in w.get_collision_pair_info()]
+    assert names == o.pair_names()
+    q = Wd.sample_q(o.art, 400, 818)
+    f, m = w.collide_batch(q)
+    fo, mo = o.collide_batch(q, nthreads=NTHREADS)
+    np.testing.assert_array_equal(f, fo)
+    np.testing.assert_array_equal(m, mo)
+    ds, ps, do, po = w.distance_batch(q)
+    rs, rps, ro, rpo = o.distance_batch(q)
+    for d, r in ((ds, rs), (do, ro)):
+        np.testing.assert_array_equal(d == -1.0, r == -1.0)
+        np.testing.assert_allclose(d, r, rtol=0, atol=1e-9)
+    k = [i for i, pn in enumerate(names) if pn[1] == "huge_ball"]
+    hitq = np.nonzero(np.any(np.stack([(mo[:, p >> 5] >> (p & 31)) & 1 for p in k], 1), 1))[0]
+    assert len(hitq) > 5
+    hit, rd, rn, rp = o.contact_batch(q[hitq[:12]])
+    req = pymp.fcl.CollisionRequest(enable_contact=True)
+    for i, qi in enumerate(q[hitq[:12]]):
+        w.set_qpos_all(list(qi))
+        got = {(c.link_name1, c.link_name2): c.res.get_contacts()[0] for c in w.collide_full(req)}
+        for p in np.nonzero(hit[i])[0]:
+            c = got[names[p]]
+            assert abs(c.penetration_depth - rd[i, p]) < 1e-9
+            np.testing.assert_allclose(c.normal, rn[i, p], atol=1e-9)
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("n", [5, 300, 5000])
 def test_dof0_world_with_moving_links(n):
