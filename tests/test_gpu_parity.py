@@ -772,7 +772,7 @@ def test_bench_gpus2_self_launch_gloo_one_gpu():
 def test_bench_one_rank_nccl_gather():
     """RCCL on hardware: one rank launched by torch.distributed.run with the
     nccl backend (RCCL) initialises its communicator and times the all-gather
-    of flags + pair masks (--gather)."""
+    of flags + pair masks and of the distance results (--gather)."""
     import json
     import socket
     import subprocess
@@ -791,6 +791,8 @@ def test_bench_one_rank_nccl_gather():
     r = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][-1])
     assert r["n_gpus"] == 1 and r["value"] > 0 and r["gather_ms"] > 0
     assert r["gather_bytes_per_rank"] == 65536 * (1 + 4 * r["config"]["mask_words"])
+    # and the distance results (minima + pair indices of both groups)
+    assert r["gather_distance_ms"] > 0 and r["gather_distance_bytes_per_rank"] == 65536 * 24
 
 
 # --------------------------------------------------------------- point clouds
