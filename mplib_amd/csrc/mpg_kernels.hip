@@ -8488,7 +8488,12 @@ template <bool FROM_POSES>
 int launch_collide_overlapped(mpg_world* w, const double* in, long long n, uint8_t* flags, uint32_t* masks,
                               hipStream_t s) {
   StreamPin pin(w, s);
-  if (w->overlap_min <= 0 || n < w->overlap_min) return launch_collide<FROM_POSES>(w, in, n, flags, masks, s);
+  // one chunk or less runs on the caller's stream alone: its two halves'
+  // cull and narrow kernels each fill the chip and are latency-bound, so on a
+  // second stream they only time-share the CUs (cfg3, 2^20: single stream
+  // +0.7-1.3 %; cfg4, 4 chunks: overlapped +16 %, profiles/r05a/overlap_ab.txt)
+  if (w->overlap_min <= 0 || n < w->overlap_min || n <= w->max_chunk)
+    return launch_collide<FROM_POSES>(w, in, n, flags, masks, s);
   // one side stream and fork/join event pair per caller stream: callers on
   // different streams (one host thread each, include/mpgpu.h) never record
   // into or wait on each other's events, and each side stream has its own

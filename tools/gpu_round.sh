@@ -18,7 +18,7 @@ for step in "$@"; do
     timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { cat gpurun_out/smoke.log; exit 1; }
     tail -1 gpurun_out/smoke.log ;;
   prof)
-    NCFG=524288 bash tools/profile.sh $TAG || exit 1
+    NCFG=1048576 bash tools/profile.sh $TAG || exit 1
     cp gpurun_out/prof_$TAG/pmc_summary.json profiles/pmc_cfg3.json
     NCFG=65536 bash tools/profile.sh ${TAG}_cfg2 --cfg 2 || exit 1
     cp gpurun_out/prof_${TAG}_cfg2/pmc_summary.json profiles/pmc_cfg2.json
