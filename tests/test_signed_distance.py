@@ -3,10 +3,17 @@ oracle: FCL 0.7.0's shape distance leaf returns the world-frame
 nearest points of the two shapes with every distance (libccd ccdGJKDist2 ->
 extractClosestPoints), and with enable_signed_distance the depth of
 intersecting shapes from EPA (ccdGJKSignedDist -> penEPAPosClosest), as
--depth.  Known answers from plain geometry, and random hulls against an
-independent computation (scipy's convex hull of the Minkowski difference:
-the penetration depth is the distance from the origin to its nearest facet;
-the separation distance is the QP of test_oracle)."""
+-depth -- restated from FCL 0.7.0 / libccd 2.1 in float (oracle/fcl_gjk_dist.h;
+the device's twin is bit-equal, GPU tests below).  Known answers from plain
+geometry, and random hulls against an independent computation (scipy's convex
+hull of the Minkowski difference: the penetration depth is the distance from
+the origin to its nearest facet; the separation distance is the QP of
+test_oracle).  Tolerances are FCL's own: polytopes (boxes, hulls) end on an
+exact facet / feature, so only float rounding remains (1e-6 at these sizes);
+_ccdDist converges to dist_tolerance (1e-6) in the distance and to about its
+square root in the nearest points of curved shapes (1e-4); EPA on a curved
+shape stops once a support improves by less than epa_tolerance (1e-4, sqrt
+comparisons), which leaves the sphere-into-box depth within 2e-3."""
 import numpy as np
 import pytest
 
