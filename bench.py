@@ -36,6 +36,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+PCIE_PEAK_GBPS = 63.0  # MI355X_MICROARCH.md: host link PCIe Gen5 x16, 63 GB/s spec
 # VALU issue: a wave issues one VALU instruction per 2 cycles on its SIMD
 # (MI355X_MICROARCH.md "Wave scheduling"); 1024 SIMDs at 2.4 GHz.  FP64 VALU
 # instructions run at half the FP32 rate (78.6 TF vs 157.3 TF vector, spec):
@@ -65,6 +66,9 @@ def parse():
     p.add_argument("--cpu-threads", type=int, default=0,
                    help="threads of the all-core CPU baseline (0: the box's share, OMP_NUM_THREADS or nproc)")
     p.add_argument("--gather", action="store_true", help="also time an all-gather of the results to every rank")
+    p.add_argument("--host", action="store_true",
+                   help="the batch in host memory: numpy in, numpy out through PlanningWorld.collide_batch "
+                        "(mpg_collide_batch with MPG_MEM_HOST, PCIe both ways inside the timed step)")
     return p.parse_args()
 
 
@@ -123,6 +127,8 @@ def main():
     n_pairs = len(w.get_collision_pair_info())
     # this rank's shard of synthetic uniform states (rank 0 = the BASELINE seed)
     q_host = scenes.sample_states(art, n, scenes.CFG_SEED[cfg] + 1000 * rank)
+    if args.host:
+        return host_main(args, world, rank, local, backend, cfg, n, w, q_host, dim, W, n_pairs)
     q = torch.from_numpy(q_host).to(f"cuda:{local}")
     flags = torch.empty(n, dtype=torch.uint8, device=q.device)
     masks = torch.empty((n, W), dtype=torch.int32, device=q.device)
@@ -207,6 +213,139 @@ def main():
 
     total = n * world * args.steps
     value = total / elapsed
+    roofline, valu = rooflines(st, cfg, dim, W)
+
+    result = {
+        "metric": "configs/sec full collide() Panda-7DoF+10 boxes" if cfg == 3 else f"configs/sec collide() cfg{cfg}",
+
+        "value": value,
+        "unit": "configs/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        # cfg4 is quoted on a fixed 2^22 batch split over the ranks
+        "scaling": "strong" if cfg == 4 and not args.per_gpu else "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (uniform in URDF joint limits)",
+        "config": {"workload": f"cfg{cfg} {scenes.CFG_NAME[cfg]}: {n} configs/GPU/step, {n_pairs} pairs, "
+                               f"full self+world collide() with ACM filter",
+                   "configs_per_gpu": n, "pairs": n_pairs, "mask_words": W, "parallelism": f"dp{world} (config shards, no "
+                                                                          "data-path collective)"},
+        "roofline": roofline,
+        "valu_roofline": valu,
+        "lib_hash": lib_hash(),
+        "stages": {k: {"ms_per_step": st[k]["ms_per_launch"] * st[k]["launches_per_step"],
+                       "units_per_launch": st[k]["units_per_launch"]} for k in STAGES},
+        "step_ms_events": step_ms,
+    }
+    if gather_ms is not None:
+        result["gather_ms"] = gather_ms
+        result["gather_bytes_per_rank"] = n * (1 + 4 * W)
+        result["gather_distance_ms"] = gather_dist_ms
+        result["gather_distance_bytes_per_rank"] = n * 24
+
+    if rank == 0 and world == 1 and args.cpu_sample > 0:
+        k = args.cpu_sample if cfg != 7 else min(args.cpu_sample, 1 << 13)  # the mesh oracle is ~100x slower
+        threads = args.cpu_threads or box_threads()
+        result["cpu_baseline"] = cpu_baseline(cfg, q_host[:k], flags, masks, threads)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if dist.is_initialized():
+        dist.destroy_process_group()
+
+
+def host_main(args, world, rank, local, backend, cfg, n, w, q_host, dim, W, n_pairs):
+    """--host: the same workload with the batch in host memory, as a caller of
+    the reference's API holds it: numpy in, numpy out through
+    PlanningWorld.collide_batch -> mpg_collide_batch(MPG_MEM_HOST), the
+    pipelined host path (input chunks over PCIe while earlier chunks compute,
+    only the colliding configurations' mask rows back).  A step = one call,
+    both PCIe directions and the allocation of the returned arrays included."""
+    import torch
+    import torch.distributed as dist
+    for _ in range(args.warmup):
+        w.collide_batch(q_host)
+    if dist.is_initialized():
+        dist.barrier()
+    torch.cuda.synchronize()
+    per_call = []
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        t1 = time.perf_counter()
+        flags, masks = w.collide_batch(q_host)
+        per_call.append(time.perf_counter() - t1)
+    torch.cuda.synchronize()
+    if dist.is_initialized():
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    # the per-stage kernel times (HIP events on the launch streams) from a
+    # few more calls, outside the timed region: the events cost host time in
+    # the launching thread, which the pipeline would show
+    w.profile_enable(True)
+    w.profile_read()
+    for _ in range(max(1, min(args.steps, 5))):
+        w.collide_batch(q_host)
+    prof = w.profile_read()
+    w.profile_enable(False)
+    prof_steps = max(1, min(args.steps, 5))
+    st = {k: {"ms_per_launch": v[0] / max(v[1], 1), "launches_per_step": v[1] / prof_steps,
+              "units_per_launch": v[2] / max(v[1], 1)} for k, v in prof.items()}
+    if dist.is_initialized():
+        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}" if backend == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t[0])
+    rate = float(flags.mean())
+    # bytes that cross PCIe per step: the q rows in, the flags and the packed
+    # mask rows of the colliding configurations out
+    pcie_bytes = n * (8 * dim) + n + n * rate * 4 * W
+    step_s = elapsed / args.steps
+    roofline, valu = rooflines(st, cfg, dim, W)
+    result = {
+        "metric": ("configs/sec full collide() Panda-7DoF+10 boxes" if cfg == 3 else f"configs/sec collide() cfg{cfg}")
+        + ", host buffers (numpy in/out, PCIe included)",
+        "value": n * world * args.steps / elapsed, "unit": "configs/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": step_s * 1e3, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "f64", "data": "synthetic (uniform in URDF joint limits)",
+        "config": {"workload": f"cfg{cfg} {scenes_name(cfg)}: {n} configs/GPU/step in host memory, {n_pairs} pairs, "
+                               f"full self+world collide() with ACM filter",
+                   "configs_per_gpu": n, "pairs": n_pairs, "mask_words": W, "memory": "host (pageable numpy)",
+                   "parallelism": f"dp{world}"},
+        "call_ms_median": float(np.median(per_call) * 1e3),
+        "collision_rate": rate,
+        "pcie": {"bound": "pcie", "achieved": pcie_bytes / step_s / 1e9, "peak": PCIE_PEAK_GBPS, "unit": "GB/s",
+                 "frac": pcie_bytes / step_s / 1e9 / PCIE_PEAK_GBPS, "bytes_per_step": pcie_bytes,
+                 "bytes_per_config": pcie_bytes / n,
+                 "note": "q rows in (8*dof B) + flags (1 B) + packed mask rows of colliding configurations "
+                         "(4W B each) out; peak = PCIe Gen5 x16 spec (MI355X_MICROARCH.md), one link shared by "
+                         "both directions on this box (profiles/r06a/host_probe.json)"},
+        "roofline": roofline,
+        "valu_roofline": valu,
+        "lib_hash": lib_hash(),
+        "stages": {k: {"ms_per_step": st[k]["ms_per_launch"] * st[k]["launches_per_step"],
+                       "units_per_launch": st[k]["units_per_launch"]} for k in STAGES},
+    }
+    if rank == 0 and world == 1 and args.cpu_sample > 0:
+        k = args.cpu_sample if cfg != 7 else min(args.cpu_sample, 1 << 13)
+        threads = args.cpu_threads or box_threads()
+        result["cpu_baseline"] = cpu_baseline(cfg, q_host[:k], flags, masks, threads)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if dist.is_initialized():
+        dist.destroy_process_group()
+
+
+def scenes_name(cfg):
+    from mplib_amd import scenes
+    return scenes.CFG_NAME[cfg]
+
+
+def rooflines(st, cfg, dim, W):
+    """(roofline, valu_roofline) of the dominant kernel from the per-stage
+    profile `st` (HIP events on the launch stream) and, when it was collected
+    with this library build, profiles/pmc_cfg<cfg>.json."""
     # roofline of the dominant kernel (DESIGN.md "Measurement"): achieved =
     # SURVEY.md 8(d)'s algorithmic bytes per configuration (q row 8*dof + flag 1
     # + pair mask 4W: 77 B for cfg3) x the configurations one launch covers,
@@ -243,56 +382,18 @@ def main():
                                       if k.get("SQ_ACTIVE_INST_VALU") else None),
                     "wait_frac": (k["SQ_WAIT_ANY"] / k["SQ_WAVE_CYCLES"] if k.get("SQ_WAVE_CYCLES") else None),
                     "note": "VALU instructions x 2 issue cycles (fp64 counted twice) per SIMD over the measured "
-                            "clock x the kernel's live duration (frac; the two halves' kernels overlap on two "
-                            "streams) and over its active cycles when it runs alone in the PMC pass (frac_alone); "
+                            "clock x the kernel's live duration (frac) and over its active cycles when it runs "
+                            "alone in the PMC pass (frac_alone); "
                             "PMC counts from " + pm.get("source", "?")}
 
-    result = {
-        "metric": "configs/sec full collide() Panda-7DoF+10 boxes" if cfg == 3 else f"configs/sec collide() cfg{cfg}",
-
-        "value": value,
-        "unit": "configs/s",
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": elapsed / args.steps * 1e3,
-        "higher_is_better": True,
-        # cfg4 is quoted on a fixed 2^22 batch split over the ranks
-        "scaling": "strong" if cfg == 4 and not args.per_gpu else "weak",
-        "vs_baseline": None,
-        "dtype": "f64",
-        "data": "synthetic (uniform in URDF joint limits)",
-        "config": {"workload": f"cfg{cfg} {scenes.CFG_NAME[cfg]}: {n} configs/GPU/step, {n_pairs} pairs, "
-                               f"full self+world collide() with ACM filter",
-                   "configs_per_gpu": n, "pairs": n_pairs, "mask_words": W, "parallelism": f"dp{world} (config shards, no "
-                                                                          "data-path collective)"},
-        "roofline": {"bound": "hbm", "achieved": achieved_gbps, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                     "frac": achieved_gbps / HBM_PEAK_GBPS, "traffic": traffic,
-                     "kernel": KERNEL_NAME[dom], "kernel_ms": st[dom]["ms_per_launch"],
-                     "units_per_launch": cfg_per_launch, "unit_kind": "configs",
-                     "algorithmic_bytes_per_unit": bytes_per_config,
-                     "note": "SURVEY.md 8(d) bytes per configuration; the path is VALU and latency bound, not HBM "
-                             "bound (DESIGN.md), see valu_roofline"},
-        "valu_roofline": valu,
-        "lib_hash": lib_hash(),
-        "stages": {k: {"ms_per_step": st[k]["ms_per_launch"] * st[k]["launches_per_step"],
-                       "units_per_launch": st[k]["units_per_launch"]} for k in STAGES},
-        "step_ms_events": step_ms,
-    }
-    if gather_ms is not None:
-        result["gather_ms"] = gather_ms
-        result["gather_bytes_per_rank"] = n * (1 + 4 * W)
-        result["gather_distance_ms"] = gather_dist_ms
-        result["gather_distance_bytes_per_rank"] = n * 24
-
-    if rank == 0 and world == 1 and args.cpu_sample > 0:
-        k = args.cpu_sample if cfg != 7 else min(args.cpu_sample, 1 << 13)  # the mesh oracle is ~100x slower
-        threads = args.cpu_threads or box_threads()
-        result["cpu_baseline"] = cpu_baseline(cfg, q_host[:k], flags, masks, threads)
-    if rank == 0:
-        print(json.dumps(result), flush=True)
-    if dist.is_initialized():
-        dist.destroy_process_group()
+    roofline = {"bound": "hbm", "achieved": achieved_gbps, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                "frac": achieved_gbps / HBM_PEAK_GBPS, "traffic": traffic,
+                "kernel": KERNEL_NAME[dom], "kernel_ms": st[dom]["ms_per_launch"],
+                "units_per_launch": cfg_per_launch, "unit_kind": "configs",
+                "algorithmic_bytes_per_unit": bytes_per_config,
+                "note": "SURVEY.md 8(d) bytes per configuration; the path is VALU and latency bound, not HBM "
+                        "bound (DESIGN.md), see valu_roofline"}
+    return roofline, valu
 
 
 def dryrun_main(args, world, rank, launched):
@@ -487,8 +588,8 @@ def cpu_baseline(cfg, q_sample, flags, masks, threads):
     t0 = time.perf_counter()
     fo, mo = ow.collide_batch(q_sample, nthreads=threads)
     dt = time.perf_counter() - t0
-    parity = bool(np.array_equal(fo, flags[:k].cpu().numpy()) and
-                  np.array_equal(mo, masks[:k].cpu().numpy().view(np.uint32)))
+    as_np = lambda x: x.cpu().numpy() if hasattr(x, "cpu") else np.asarray(x)  # noqa: E731
+    parity = bool(np.array_equal(fo, as_np(flags[:k])) and np.array_equal(mo, as_np(masks[:k]).view(np.uint32)))
     return {"value": k / dt, "unit": "configs/s", "cores": threads, "kind": "port",
             "single_core": {"value": k1 / dt1, "unit": "configs/s", "cores": 1,
                             "sample": f"first {k1} configs, {dt1:.1f} s"},

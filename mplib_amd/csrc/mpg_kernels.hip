@@ -35,6 +35,7 @@
 #include <cstring>
 #include <limits>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -43,6 +44,7 @@
 #include "../../include/mpgpu.h"
 #include "mpg_math.h"
 #include "mpg_fk.h"
+#include "mpg_hostpipe.h"
 
 using namespace mpg;
 
@@ -4787,7 +4789,12 @@ __global__ __launch_bounds__(128) void distance_kernel(DevWorld w, const double*
       if (!live) continue;
       const V3 dc = vsub(cb, ca);
       const double lb = std::sqrt(d3dot(dc, dc)) - ra - rb - 1e-9;
-      if (lb > best[g] + dist_slack(&ca.x, &cb.x)) continue;
+      const double slack = dist_slack(&ca.x, &cb.x);
+      // with signed distances a pair is skipped only when its shapes are
+      // apart: an intersecting pair reaches EPA, which can throw
+      // (FCL_THROW_FAILED_AT_THIS_CONFIGURATION) however deep the running
+      // minimum already is, and FCL runs every pair (planning_world.cpp:509-537)
+      if (lb > best[g] + slack && (!SIGNED || lb > slack)) continue;
       bool done = false;
       if constexpr (!SIGNED) {
         const SE3 TA = pose_se3(w, poses, n, cfg, a), TB = pose_se3(w, poses, n, cfg, b);
@@ -6375,6 +6382,85 @@ __global__ __launch_bounds__(256) void pair_count_kernel(const uint32_t* __restr
     if (c_lds[p]) atomicAdd(&counts[p], (unsigned long long)c_lds[p]);
 }
 
+// ---------------------------------------------------------------------------
+// Host-buffer pipeline (collide_host_pipelined): the pair-mask rows of the
+// colliding configurations only, packed in configuration order and written
+// straight into pinned host memory.  flags[i] != 0 exactly when row i has a
+// bit (collide() == !collideFull().empty(), planning_world.h:248-250), so the
+// host rebuilds the full [m, W] mask from the flags and the packed rows.
+// Block b covers configurations [b * kPackCfg, (b + 1) * kPackCfg).
+// ---------------------------------------------------------------------------
+constexpr int kPackCfg = 4096;
+
+__device__ __forceinline__ int block_sum256(int v, int* red) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  const int s = red[0] + red[1] + red[2] + red[3];
+  __syncthreads();
+  return s;
+}
+
+__global__ __launch_bounds__(256) void flag_count_kernel(const uint8_t* __restrict__ fl, long long m,
+                                                         uint32_t* __restrict__ bcnt, uint32_t* __restrict__ bcnt_host) {
+  __shared__ int red[4];
+  const long long base = (long long)blockIdx.x * kPackCfg;
+  int c = 0;
+  for (int r = 0; r < kPackCfg / 256; ++r) {
+    const long long i = base + r * 256 + threadIdx.x;
+    c += (i < m && fl[i]) ? 1 : 0;
+  }
+  c = block_sum256(c, red);
+  if (threadIdx.x == 0) {
+    bcnt[blockIdx.x] = (uint32_t)c;
+    bcnt_host[blockIdx.x] = (uint32_t)c;
+  }
+}
+
+// STAGED: the block's packed rows go through LDS (256 * W words), so each
+// store instruction writes consecutive words of host memory; otherwise each
+// colliding lane writes its own row (wide masks only)
+// The flags go to host memory too (fl_out); W = 0: flags only.
+template <bool STAGED>
+__global__ __launch_bounds__(256) void mask_pack_kernel(const uint8_t* __restrict__ fl, const uint32_t* __restrict__ mk,
+                                                        long long m, int W, const uint32_t* __restrict__ bcnt,
+                                                        uint32_t* __restrict__ out, uint8_t* __restrict__ fl_out) {
+  extern __shared__ uint32_t pk_lds[];
+  __shared__ int red[4];
+  __shared__ int wcnt[4];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  int off = 0;
+  for (int b = tid; b < (int)blockIdx.x; b += 256) off += (int)bcnt[b];
+  long long run = block_sum256(off, red);
+  const long long base = (long long)blockIdx.x * kPackCfg;
+  for (int r = 0; r < kPackCfg / 256; ++r) {
+    const long long i = base + r * 256 + tid;
+    if (base + r * 256 >= m) break;  // block-uniform
+    const bool f = i < m && fl[i];
+    if (i < m) fl_out[i] = f ? 1 : 0;
+    if (W == 0) continue;  // block-uniform
+    const unsigned long long bal = __ballot(f);
+    const int lpos = __popcll(bal & ((1ull << lane) - 1ull));
+    if (lane == 0) wcnt[wv] = __popcll(bal);
+    __syncthreads();
+    int woff = 0;
+    for (int k = 0; k < wv; ++k) woff += wcnt[k];
+    const int total = wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
+    if constexpr (STAGED) {
+      if (f)
+        for (int k = 0; k < W; ++k) pk_lds[(woff + lpos) * W + k] = mk[i * W + k];
+      __syncthreads();
+      uint32_t* o = out + run * W;
+      for (int d = tid; d < total * W; d += 256) o[d] = pk_lds[d];
+    } else {
+      if (f)
+        for (int k = 0; k < W; ++k) out[(run + woff + lpos) * W + k] = mk[i * W + k];
+    }
+    run += total;
+    __syncthreads();
+  }
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------------------
@@ -6531,6 +6617,38 @@ struct mpg_world {
   double srv_stat[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   size_t small_cap = 0;   // configurations (hit bytes per pair)
   size_t small_qcap = 0;  // input doubles (h_q, d_qs)
+  // host-buffer batches above small_max (collide_host_pipelined): chunks
+  // through a ring of slots -- the input of one chunk crosses PCIe while the
+  // previous one computes and the one before is unpacked on the host.
+  // Grow-only, guarded by host_mu.
+  static constexpr int kRing = 3;
+  struct Ring {
+    double* d_in[kRing] = {};
+    uint8_t* d_fl[kRing] = {};
+    uint32_t* d_mk[kRing] = {};
+    uint32_t* d_bcnt[kRing] = {};  // colliding configurations per kPackCfg block
+    uint8_t* h_fl[kRing] = {};     // pinned, host-mapped: the chunk's flags (mask_pack_kernel)
+    uint32_t* h_mk[kRing] = {};    // pinned, host-mapped: packed mask rows (mask_pack_kernel)
+    uint32_t* h_mk_d[kRing] = {};  // h_mk as the device sees it
+    uint32_t* h_bcnt[kRing] = {};  // pinned, host-mapped copy of d_bcnt (where each block's packed rows start)
+    uint8_t* h_fl_d[kRing] = {};   // device aliases of h_fl, h_bcnt
+    uint32_t* h_bcnt_d[kRing] = {};
+    hipEvent_t e_in[kRing] = {}, e_done[kRing] = {};
+    hipStream_t h2d = nullptr;     // input copies
+    hipStream_t side = nullptr;    // odd chunks compute here (one chunk's narrow tail overlaps the next's cull)
+    size_t cap = 0;                // configurations per slot
+    size_t in_cap = 0;             // input doubles per slot
+  } ring;
+  // chunk sizes: profiles/r06a/host_ab*.txt (2^18 / 2^19 chunks, head and
+  // tail sizes within +-3 % of each other on cfg3 2^20; this is the best seen)
+  long long ring_chunk = 1 << 19;  // largest chunk (env MPG_HOST_CHUNK)
+  int ring_streams = 2;            // compute streams of the pipeline (env MPG_HOST_STREAMS: 1 or 2)
+  int host_threads = 8;            // threads unpacking a finished chunk (env MPG_HOST_THREADS)
+  long long ring_head = 1 << 17, ring_tail = 1 << 16;  // smaller first / last chunk (env MPG_HOST_HEAD / _TAIL)
+  std::unique_ptr<mpg_hostpipe::Pool> pool;
+  // MPG_STATS: host pipeline phase sums (us): calls, input copy, issue,
+  // result wait, unpack, whole call
+  double hp_stat[6] = {0, 0, 0, 0, 0, 0};
 };
 
 namespace {
@@ -7291,6 +7409,67 @@ int ensure_staging(mpg_world* w, size_t ncfg, size_t nout) {
     HIP_TRY(hipMalloc(&w->d_out, sizeof(double) * nout));
     w->cap_out = nout;
   }
+  return MPG_OK;
+}
+
+// the host pipeline's slot buffers (not its stream and events)
+void free_ring(mpg_world* w) {
+  auto& R = w->ring;
+  for (int j = 0; j < mpg_world::kRing; ++j) {
+    if (R.d_in[j]) hipFree(R.d_in[j]);
+    if (R.d_fl[j]) hipFree(R.d_fl[j]);
+    if (R.d_mk[j]) hipFree(R.d_mk[j]);
+    if (R.d_bcnt[j]) hipFree(R.d_bcnt[j]);
+    if (R.h_fl[j]) hipHostFree(R.h_fl[j]);
+    if (R.h_mk[j]) hipHostFree(R.h_mk[j]);
+    if (R.h_bcnt[j]) hipHostFree(R.h_bcnt[j]);
+    R.h_bcnt[j] = nullptr;
+    R.h_fl_d[j] = nullptr;
+    R.h_bcnt_d[j] = nullptr;
+    R.d_in[j] = nullptr;
+    R.d_fl[j] = nullptr;
+    R.d_mk[j] = nullptr;
+    R.d_bcnt[j] = nullptr;
+    R.h_fl[j] = nullptr;
+    R.h_mk[j] = nullptr;
+    R.h_mk_d[j] = nullptr;
+  }
+  R.cap = 0;
+  R.in_cap = 0;
+}
+
+// slots of `cap` configurations with `row` input doubles each (grow-only)
+int ensure_ring(mpg_world* w, size_t cap, size_t row) {
+  auto& R = w->ring;
+  if (!R.h2d) {
+    HIP_TRY(hipStreamCreateWithFlags(&R.h2d, hipStreamNonBlocking));
+    HIP_TRY(hipStreamCreateWithFlags(&R.side, hipStreamNonBlocking));
+    for (int j = 0; j < mpg_world::kRing; ++j) {
+      HIP_TRY(hipEventCreateWithFlags(&R.e_in[j], hipEventDisableTiming));
+      HIP_TRY(hipEventCreateWithFlags(&R.e_done[j], hipEventDisableTiming));
+    }
+  }
+  const size_t in = cap * std::max<size_t>(row, 1);
+  if (cap <= R.cap && in <= R.in_cap) return MPG_OK;
+  cap = std::max(cap, R.cap);
+  const size_t in_cap = std::max(in, R.in_cap);
+  free_ring(w);
+  const size_t W = (size_t)std::max(w->dw.W, 1);
+  for (int j = 0; j < mpg_world::kRing; ++j) {
+    HIP_TRY(hipMalloc(&R.d_in[j], sizeof(double) * in_cap));
+    HIP_TRY(hipMalloc(&R.d_fl[j], cap));
+    HIP_TRY(hipMalloc(&R.d_mk[j], sizeof(uint32_t) * W * cap));
+    HIP_TRY(hipMalloc(&R.d_bcnt[j], sizeof(uint32_t) * ((cap + kPackCfg - 1) / kPackCfg)));
+    HIP_TRY(hipHostMalloc((void**)&R.h_fl[j], cap, hipHostMallocMapped));
+    HIP_TRY(hipHostGetDevicePointer((void**)&R.h_fl_d[j], R.h_fl[j], 0));
+    HIP_TRY(hipHostMalloc((void**)&R.h_mk[j], sizeof(uint32_t) * W * cap, hipHostMallocMapped));
+    HIP_TRY(hipHostGetDevicePointer((void**)&R.h_mk_d[j], R.h_mk[j], 0));
+    HIP_TRY(hipHostMalloc((void**)&R.h_bcnt[j], sizeof(uint32_t) * ((cap + kPackCfg - 1) / kPackCfg),
+                          hipHostMallocMapped));
+    HIP_TRY(hipHostGetDevicePointer((void**)&R.h_bcnt_d[j], R.h_bcnt[j], 0));
+  }
+  R.cap = cap;
+  R.in_cap = in_cap;
   return MPG_OK;
 }
 
@@ -8099,6 +8278,12 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
   if (const char* e = std::getenv("MPG_SMALL_BATCH_MAX")) w->small_max = std::atoll(e);
   if (const char* e = std::getenv("MPG_SMALL_ZEROCOPY")) w->small_zero_copy = std::atoi(e) != 0;
   if (const char* e = std::getenv("MPG_OVERLAP_MIN")) w->overlap_min = std::atoll(e);
+  if (const char* e = std::getenv("MPG_HOST_STREAMS")) w->ring_streams = std::atoi(e) > 1 ? 2 : 1;
+  if (const char* e = std::getenv("MPG_HOST_THREADS")) w->host_threads = std::max(1, std::min(64, std::atoi(e)));
+  if (const char* e = std::getenv("MPG_HOST_HEAD")) w->ring_head = std::max(0ll, std::atoll(e));
+  if (const char* e = std::getenv("MPG_HOST_TAIL")) w->ring_tail = std::max(0ll, std::atoll(e));
+  if (const char* e = std::getenv("MPG_HOST_CHUNK"))
+    w->ring_chunk = std::max(64ll, std::min((long long)w->max_chunk, (std::atoll(e) + 63) / 64 * 64));
   if (const char* e = std::getenv("MPG_SMALL_INLINE_SC")) w->small_inline_sc = std::atoll(e);
   if (const char* e = std::getenv("MPG_OVERLAP_PARTS")) w->overlap_parts = std::atoi(e);
   if (const char* e = std::getenv("MPG_SMALL_HOST_SC")) w->small_host_sc = std::atoll(e);
@@ -8164,6 +8349,11 @@ int mpg_world_destroy(mpg_world* w) {
                  "narrow %.2f, publish %.2f; host post->done %.2f\n", w->srv_stat[5], w->srv_stat[0] / w->srv_stat[5],
                  w->srv_stat[1] / w->srv_stat[5], w->srv_stat[2] / w->srv_stat[5], w->srv_stat[3] / w->srv_stat[5],
                  w->srv_stat[4] / w->srv_stat[5], w->srv_stat[6] / w->srv_stat[5]);
+  if (w->srv_stats && w->hp_stat[0] > 0)
+    std::fprintf(stderr, "[mpg stats] host pipeline, mean us over %.0f calls: input copies %.1f, issue %.1f, "
+                 "result wait %.1f, unpack %.1f; whole call %.1f\n", w->hp_stat[0], w->hp_stat[1] / w->hp_stat[0],
+                 w->hp_stat[2] / w->hp_stat[0], w->hp_stat[3] / w->hp_stat[0], w->hp_stat[4] / w->hp_stat[0],
+                 w->hp_stat[5] / w->hp_stat[0]);
   if (w->srv_h) {  // the server leaves at its next poll
     __atomic_store_n(&w->srv_h->quit, 1ull, __ATOMIC_RELEASE);
     hipStreamSynchronize(w->srv_stream);
@@ -8186,6 +8376,16 @@ int mpg_world_destroy(mpg_world* w) {
   hipFree(w->d_flags);
   hipFree(w->d_masks);
   hipFree(w->d_out);
+  free_ring(w);
+  w->pool.reset();
+  if (w->ring.h2d) {
+    hipStreamDestroy(w->ring.h2d);
+    hipStreamDestroy(w->ring.side);
+    for (int j = 0; j < mpg_world::kRing; ++j) {
+      hipEventDestroy(w->ring.e_in[j]);
+      hipEventDestroy(w->ring.e_done[j]);
+    }
+  }
   for (auto& mk : w->marks) {
     hipEventDestroy(mk.a);
     hipEventDestroy(mk.b);
@@ -8531,6 +8731,128 @@ int launch_collide_overlapped(mpg_world* w, const double* in, long long n, uint8
   return MPG_OK;
 }
 
+// Host buffers above the latency path's sizes (mpg_hostpipe.h): per chunk,
+// the rows are copied from the caller's (pageable) buffer on the ring's copy
+// stream by the feeder thread; the compute stream waits for them, runs the
+// collide pipeline into the slot's device outputs, packs the colliding
+// configurations' mask rows straight into pinned host memory and copies the
+// flags back; the issuing thread unpacks a finished chunk into the caller's
+// buffers while the next chunks are in flight.  PCIe carries the rows in
+// (8 * row B per configuration) and 1 + 4W B per colliding configuration
+// back instead of 1 + 4W B per configuration.  Caller holds host_mu.
+template <bool FROM_POSES>
+struct HostPipeOps {
+  mpg_world* w;
+  const double* q;
+  uint8_t* flags;
+  uint32_t* pair_mask;
+  hipStream_t s;
+  size_t row;
+  // the first error text of the feeder / issuer threads (g_last_error is per
+  // thread); finish() runs on the caller's thread and sets g_last_error itself
+  std::mutex err_mu;
+  std::string thread_err;
+  bool fin_failed = false;
+
+  int thread_fail(int rc, const std::string& msg) {
+    std::lock_guard<std::mutex> lk(err_mu);
+    if (thread_err.empty()) thread_err = msg;
+    return rc;
+  }
+  int bind_thread() {
+    if (hipSetDevice(w->device) != hipSuccess) return thread_fail(MPG_E_HIP, "hipSetDevice failed in a pipeline thread");
+    return MPG_OK;
+  }
+  double t_in = 0, t_issue = 0, t_wait = 0, t_unpack = 0;
+  static double us_since(std::chrono::steady_clock::time_point t0) {
+    return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+  }
+  int h2d(int64_t, int j, int64_t start, int64_t m) {
+    auto& R = w->ring;
+    const auto t0 = std::chrono::steady_clock::now();
+    hipError_t e = hipSuccess;
+    if (row) e = hipMemcpyAsync(R.d_in[j], q + (size_t)start * row, sizeof(double) * (size_t)m * row,
+                                hipMemcpyHostToDevice, R.h2d);
+    if (e == hipSuccess) e = hipEventRecord(R.e_in[j], R.h2d);
+    t_in += us_since(t0);
+    if (e != hipSuccess) return thread_fail(MPG_E_HIP, std::string("host pipeline input copy failed: ") + hipGetErrorString(e));
+    return MPG_OK;
+  }
+  int issue(int64_t k, int j, int64_t start, int64_t m) {
+    const int rc = issue_chunk(k, j, start, m);
+    return rc ? thread_fail(rc, g_last_error) : MPG_OK;  // g_last_error of this (issuer) thread
+  }
+  int issue_chunk(int64_t k, int j, int64_t, int64_t m) {
+    auto& R = w->ring;
+    const auto t0 = std::chrono::steady_clock::now();
+    const hipStream_t cs = (w->ring_streams > 1 && (k & 1)) ? R.side : s;
+    HIP_TRY(hipStreamWaitEvent(cs, R.e_in[j], 0));
+    const int rc = launch_collide<FROM_POSES>(w, R.d_in[j], m, R.d_fl[j], R.d_mk[j], cs);
+    if (rc) return rc;
+    // results straight into pinned host memory: the flags, and with masks the
+    // block counts and the packed rows (no copy launches)
+    const int Wp = pair_mask ? w->dw.W : 0;
+    const unsigned nb = (unsigned)((m + kPackCfg - 1) / kPackCfg);
+    if (Wp > 0) {
+      hipLaunchKernelGGL(flag_count_kernel, dim3(nb), dim3(256), 0, cs, R.d_fl[j], (long long)m, R.d_bcnt[j],
+                         R.h_bcnt_d[j]);
+      HIP_TRY(hipGetLastError());
+    }
+    const size_t lds = sizeof(uint32_t) * 256 * (size_t)Wp;
+    if (lds <= 64 * 1024)
+      hipLaunchKernelGGL(mask_pack_kernel<true>, dim3(nb), dim3(256), lds, cs, R.d_fl[j], R.d_mk[j], (long long)m, Wp,
+                         R.d_bcnt[j], R.h_mk_d[j], R.h_fl_d[j]);
+    else
+      hipLaunchKernelGGL(mask_pack_kernel<false>, dim3(nb), dim3(256), 0, cs, R.d_fl[j], R.d_mk[j], (long long)m, Wp,
+                         R.d_bcnt[j], R.h_mk_d[j], R.h_fl_d[j]);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(R.e_done[j], cs));
+    t_issue += us_since(t0);
+    return MPG_OK;
+  }
+  int finish(int64_t, int j, int64_t start, int64_t m) {
+    auto& R = w->ring;
+    const auto t0 = std::chrono::steady_clock::now();
+    const hipError_t e = hipEventSynchronize(R.e_done[j]);
+    if (e != hipSuccess) {
+      fin_failed = true;
+      return set_error(MPG_E_HIP, std::string("host pipeline: ") + hipGetErrorString(e));
+    }
+    const auto t1 = std::chrono::steady_clock::now();
+    t_wait += std::chrono::duration<double, std::micro>(t1 - t0).count();
+    mpg_hostpipe::unpack_chunk(w->pool.get(), R.h_fl[j], R.h_mk[j], R.h_bcnt[j], kPackCfg, m, w->dw.W, flags + start,
+                               pair_mask && w->dw.W > 0 ? pair_mask + (size_t)start * w->dw.W : nullptr);
+    t_unpack += us_since(t1);
+    return MPG_OK;
+  }
+  void drain() {
+    hipStreamSynchronize(w->ring.h2d);
+    hipStreamSynchronize(w->ring.side);
+    hipStreamSynchronize(s);
+  }
+};
+
+template <bool FROM_POSES>
+int collide_host_pipelined(mpg_world* w, const double* q, int64_t n, uint8_t* flags, uint32_t* pair_mask,
+                           hipStream_t s) {
+  const mpg_hostpipe::Plan p =
+      mpg_hostpipe::plan(n, w->ring_chunk, 1 << 15, mpg_world::kRing, w->ring_head, w->ring_tail);
+  const size_t row = FROM_POSES ? (size_t)w->dw.n_links * 7 : (size_t)w->dw.dof;
+  int rc = ensure_ring(w, (size_t)p.chunk, row);
+  if (rc) return rc;
+  if (!w->pool && w->host_threads > 1 && p.chunk >= 2 * kPackCfg)
+    w->pool.reset(new mpg_hostpipe::Pool(w->host_threads - 1));
+  HostPipeOps<FROM_POSES> ops{w, q, flags, pair_mask, s, row};
+  const auto t0 = std::chrono::steady_clock::now();
+  rc = mpg_hostpipe::run(p, n, ops);
+  if (w->srv_stats) {
+    const double v[6] = {1.0, ops.t_in, ops.t_issue, ops.t_wait, ops.t_unpack, HostPipeOps<FROM_POSES>::us_since(t0)};
+    for (int k = 0; k < 6; ++k) w->hp_stat[k] += v[k];
+  }
+  if (rc && !ops.fin_failed) return set_error(rc, ops.thread_err);
+  return rc;
+}
+
 template <bool FROM_POSES>
 int collide_common(mpg_world* w, const double* q, int64_t n, uint8_t* flags, uint32_t* pair_mask, int mem,
                    void* stream) {
@@ -8545,19 +8867,9 @@ int collide_common(mpg_world* w, const double* q, int64_t n, uint8_t* flags, uin
   if (mem != MPG_MEM_HOST) return set_error(MPG_E_INVALID, "bad mem kind");
   std::lock_guard<std::mutex> lk(w->host_mu);
   if (!s && w->own_stream) s = w->own_stream;
-  if (n > 0 && n <= w->small_max) return collide_small<FROM_POSES>(w, q, n, flags, pair_mask, s);
-  int rc = ensure_staging(w, (size_t)n, std::max<size_t>(1, (size_t)n * row));
-  if (rc) return rc;
   if (n == 0) return MPG_OK;
-  double* din = FROM_POSES ? w->d_out : w->d_q;
-  if (row) HIP_TRY(hipMemcpyAsync(din, q, sizeof(double) * n * row, hipMemcpyHostToDevice, s));
-  rc = launch_collide_overlapped<FROM_POSES>(w, din, n, w->d_flags, w->d_masks, s);
-  if (rc) return rc;
-  HIP_TRY(hipMemcpyAsync(flags, w->d_flags, n, hipMemcpyDeviceToHost, s));
-  if (pair_mask)
-    HIP_TRY(hipMemcpyAsync(pair_mask, w->d_masks, sizeof(uint32_t) * n * w->dw.W, hipMemcpyDeviceToHost, s));
-  HIP_TRY(hipStreamSynchronize(s));
-  return MPG_OK;
+  if (n <= w->small_max) return collide_small<FROM_POSES>(w, q, n, flags, pair_mask, s);
+  return collide_host_pipelined<FROM_POSES>(w, q, n, flags, pair_mask, s);
 }
 }  // namespace
 
