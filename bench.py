@@ -17,6 +17,8 @@ convex=False), --cfg 5 (RRTConnect plan() end to end: a step is one plan()).
 
 Usage:  python bench.py [--gpus N] [--steps K] [--warmup W] [--cpu-sample S] [--cfg C]
         torchrun --nproc-per-node N bench.py --gpus N ...
+        python bench.py --host ...          (the batch in host memory: numpy in / numpy out, PCIe timed)
+        python bench.py --capi-multi N ...  (one process, N GPUs through mpg_collide_batch_multi_device)
 `python bench.py --gpus N` (N > 1) without a launcher starts the N ranks
 itself (torch.distributed.run as a child process, one process per GPU, RCCL);
 under a launcher whose WORLD_SIZE differs from --gpus it exits non-zero.
@@ -66,6 +68,10 @@ def parse():
     p.add_argument("--cpu-threads", type=int, default=0,
                    help="threads of the all-core CPU baseline (0: the box's share, OMP_NUM_THREADS or nproc)")
     p.add_argument("--gather", action="store_true", help="also time an all-gather of the results to every rank")
+    p.add_argument("--capi-multi", type=int, default=0, metavar="N",
+                   help="one process drives N GPUs through the C entry mpg_collide_batch_multi_device "
+                        "(device-resident shards, one host thread per GPU; --gather adds the peer-copy gather "
+                        "into GPU 0); not under a launcher")
     p.add_argument("--host", action="store_true",
                    help="the batch in host memory: numpy in, numpy out through PlanningWorld.collide_batch "
                         "(mpg_collide_batch with MPG_MEM_HOST, PCIe both ways inside the timed step)")
@@ -90,6 +96,10 @@ def launch_ranks(n: int) -> int:
 def main():
     args = parse()
     launched = "WORLD_SIZE" in os.environ
+    if args.capi_multi:
+        if launched or args.gpus != 1:
+            sys.exit("bench.py: --capi-multi N runs in one process (no launcher, no --gpus)")
+        return capi_multi_main(args)
     if not launched and args.gpus > 1:
         sys.exit(launch_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -255,6 +265,93 @@ def main():
         print(json.dumps(result), flush=True)
     if dist.is_initialized():
         dist.destroy_process_group()
+
+
+def capi_multi_main(args):
+    """--capi-multi N: the in-process multi-GPU route a C++ caller of the C
+    ABI takes (include/mpgpu.h mpg_collide_batch_multi_device): N worlds, one
+    per GPU, each GPU's shard (the BASELINE size per GPU, weak scaling; cfg4
+    the fixed 2^22 batch split) resident in its HBM, one host thread per GPU
+    enqueueing its shard on its own stream; a step = one call + the
+    synchronisation of every GPU.  --gather: every shard's flags and mask rows
+    also copied into GPU 0 (peer copies over xGMI) inside the step."""
+    import torch
+    from mplib_amd import scenes
+    from mplib_amd.batch import collide_batch_multi_device
+
+    N, cfg = args.capi_multi, args.cfg
+    if torch.cuda.device_count() < N:
+        sys.exit(f"bench.py: --capi-multi {N} but {torch.cuda.device_count()} GPUs")
+    n = args.per_gpu or (scenes.CFG_N[cfg] if cfg != 4 else (1 << 22) // N)
+    worlds, qs, fl, mk, streams = [], [], [], [], []
+    for k in range(N):
+        os.environ["MPLIB_AMD_DEVICE"] = str(k)  # the snapshot is built on GPU k
+        w, art = scenes.world(cfg)
+        w.device_handle()
+        dev = torch.device("cuda", k)
+        worlds.append(w)
+        qs.append(torch.from_numpy(scenes.sample_states(art, n, scenes.CFG_SEED[cfg] + 1000 * k)).to(dev))
+        fl.append(torch.empty(n, dtype=torch.uint8, device=dev))
+        mk.append(torch.empty((n, w.get_mask_words()), dtype=torch.int32, device=dev))
+        streams.append(torch.cuda.Stream(device=dev))
+    W, dim, n_pairs = worlds[0].get_mask_words(), worlds[0].get_state_dim(), len(worlds[0].get_collision_pair_info())
+    gf = gm = None
+    if args.gather:
+        gf = torch.empty(n * N, dtype=torch.uint8, device="cuda:0")
+        gm = torch.empty((n * N, W), dtype=torch.int32, device="cuda:0")
+    sptr = [s.cuda_stream for s in streams]
+
+    def step():
+        collide_batch_multi_device(worlds, qs, fl, mk, sptr, gf, gm)
+
+    def sync_all():
+        for k in range(N):
+            torch.cuda.synchronize(k)
+
+    for _ in range(args.warmup):
+        step()
+    sync_all()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    sync_all()
+    elapsed = time.perf_counter() - t0
+    worlds[0].profile_enable(True)
+    worlds[0].profile_read()
+    prof_steps = max(1, min(args.steps, 5))
+    for _ in range(prof_steps):
+        step()
+    sync_all()
+    prof = worlds[0].profile_read()
+    worlds[0].profile_enable(False)
+    st = {k: {"ms_per_launch": v[0] / max(v[1], 1), "launches_per_step": v[1] / prof_steps,
+              "units_per_launch": v[2] / max(v[1], 1)} for k, v in prof.items()}
+    roofline, valu = rooflines(st, cfg, dim, W)
+    ok = True
+    if N > 1 or args.gather:  # shard 0 against a plain single-world call on the same data
+        f0 = torch.empty_like(fl[0])
+        m0 = torch.empty_like(mk[0])
+        worlds[0].collide_batch_device(qs[0].data_ptr(), n, f0.data_ptr(), m0.data_ptr(),
+                                       torch.cuda.current_stream(0).cuda_stream)
+        sync_all()
+        ok = bool(torch.equal(f0, fl[0]) and torch.equal(m0, mk[0]))
+        if args.gather:
+            ok &= bool(torch.equal(gf[:n], fl[0]) and torch.equal(gm[:n], mk[0]))
+    result = {
+        "metric": "configs/sec full collide() Panda-7DoF+10 boxes" if cfg == 3 else f"configs/sec collide() cfg{cfg}",
+        "value": n * N * args.steps / elapsed, "unit": "configs/s", "n_gpus": N, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+        "scaling": "strong" if cfg == 4 and not args.per_gpu else "weak", "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic (uniform in URDF joint limits)",
+        "config": {"workload": f"cfg{cfg} {scenes.CFG_NAME[cfg]}: {n} configs/GPU/step, {n_pairs} pairs, "
+                               f"full self+world collide() with ACM filter",
+                   "configs_per_gpu": n, "pairs": n_pairs, "mask_words": W,
+                   "parallelism": f"capi-multi x{N}: one process, one host thread per GPU "
+                                  f"(mpg_collide_batch_multi_device){', gather into GPU 0' if args.gather else ''}"},
+        "shard0_matches_single_world_call": ok,
+        "roofline": roofline, "valu_roofline": valu, "lib_hash": lib_hash(),
+    }
+    print(json.dumps(result), flush=True)
 
 
 def host_main(args, world, rank, local, backend, cfg, n, w, q_host, dim, W, n_pairs):

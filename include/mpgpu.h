@@ -34,11 +34,17 @@
  * device pointer on the world's device and the work is enqueued on `stream`
  * (a hipStream_t, NULL = default stream) without synchronising.  With
  * MPG_MEM_HOST the call copies through internal device staging buffers and
- * returns after the results are back on the host.
+ * returns after the results are back on the host; batches above the latency
+ * path's size (mpg_set_small_batch_max) run as chunks through a pinned ring:
+ * the input of one chunk crosses PCIe while earlier chunks compute and are
+ * unpacked (internal threads and streams; the call is still synchronous).
  *
  * Threading: a world is immutable after creation; concurrent calls on one
  * world from several host threads are allowed when each uses its own stream
  * and MPG_MEM_DEVICE.  MPG_MEM_HOST calls on one world are serialised.
+ * mpg_distance_batch* and mpg_check_motion_batch use scratch owned by the
+ * world: their MPG_MEM_DEVICE calls from several streams are ordered on the
+ * device (each waits for the previous call's work), never overlapped.
  */
 #ifndef MPGPU_H
 #define MPGPU_H
@@ -219,6 +225,33 @@ int mpg_collide_batch(mpg_world *world, const double *q, int64_t n, uint8_t *fla
  */
 int mpg_collide_batch_multi(mpg_world *const *worlds, int32_t n_worlds, const double *q, int64_t n,
                             uint8_t *flags, uint32_t *pair_mask);
+
+/*
+ * The shard of a batch of n configurations that part k of n_parts checks:
+ * contiguous, the first n % n_parts shards one row longer (the split of
+ * mpg_collide_batch_multi and of mplib_amd.dist.shard_range).  Host only.
+ */
+int mpg_shard_range(int64_t n, int32_t k, int32_t n_parts, int64_t *start, int64_t *count);
+
+/*
+ * Device-resident multi-GPU batch: shard k is already on worlds[k]'s device
+ * -- q[k] [counts[k] * dof], flags[k] [counts[k]], pair_mask[k]
+ * [counts[k] * mask_words] (pair_mask or pair_mask[k] NULL: flags only) --
+ * and is enqueued on streams[k] (a hipStream_t of that device; streams or
+ * streams[k] NULL: its default stream), one host thread per world; no host
+ * round trip, no synchronisation (as MPG_MEM_DEVICE calls).
+ * gather_flags / gather_masks (device pointers on worlds[0]'s device, NULL:
+ * no gather): every shard's flags / mask rows are also copied there, shard k
+ * at row counts[0] + ... + counts[k-1], device to device (peer copies over
+ * xGMI on streams[k]); streams[0] then waits for all of them, so work queued
+ * on streams[0] after the call sees the whole batch.  The worlds must come
+ * from the same descriptor (checked by the snapshot's hash) and be distinct.
+ * isValid is a pure function of the state (src/ompl_planner.h:59-62): no
+ * collective is involved in the check itself.
+ */
+int mpg_collide_batch_multi_device(mpg_world *const *worlds, int32_t n_worlds, const double *const *q,
+                                   const int64_t *counts, uint8_t *const *flags, uint32_t *const *pair_mask,
+                                   void *const *streams, uint8_t *gather_flags, uint32_t *gather_masks);
 
 /*
  * Host-buffer calls (mem == MPG_MEM_HOST) of at most `n` configurations take

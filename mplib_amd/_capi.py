@@ -70,6 +70,13 @@ SIGNATURES = {
                                          ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]),
     "mpg_collide_batch_multi": (ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p), ctypes.c_int32, ctypes.c_void_p,
                                                ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p]),
+    "mpg_shard_range": (ctypes.c_int, [ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, ctypes.POINTER(ctypes.c_int64),
+                                       ctypes.POINTER(ctypes.c_int64)]),
+    "mpg_collide_batch_multi_device": (ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p), ctypes.c_int32,
+                                                      ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_int64),
+                                                      ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_void_p),
+                                                      ctypes.POINTER(ctypes.c_void_p), ctypes.c_void_p,
+                                                      ctypes.c_void_p]),
     "mpg_collide_link_poses": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p,
                                               ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]),
     "mpg_check_motion_batch": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,

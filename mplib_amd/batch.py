@@ -198,3 +198,35 @@ def collide_batch_multi(worlds, q):
     C.check(C.lib().mpg_collide_batch_multi(hs, len(worlds), q.ctypes.data, n, flags.ctypes.data, masks.ctypes.data),
             "mpg_collide_batch_multi")
     return flags, masks
+
+
+def shard_range_c(n: int, k: int, parts: int):
+    """mpg_shard_range: (start, count) of part k of n configurations."""
+    start, count = ctypes.c_int64(), ctypes.c_int64()
+    C.check(C.lib().mpg_shard_range(int(n), int(k), int(parts), ctypes.byref(start), ctypes.byref(count)),
+            "mpg_shard_range")
+    return start.value, count.value
+
+
+def collide_batch_multi_device(worlds, qs, flags, masks=None, streams=None, gather_flags=None, gather_masks=None):
+    """mpg_collide_batch_multi_device: shard k already on worlds[k]'s device
+    (torch tensors or raw device pointers via .data_ptr()): qs[k] [count, dof]
+    float64, flags[k] [count] uint8, masks[k] [count, W] int32/uint32 or None;
+    streams[k] a stream handle (int) or None.  gather_flags / gather_masks:
+    tensors on worlds[0]'s device receiving every shard in order.  Enqueues
+    only (no synchronisation)."""
+    worlds = list(worlds)
+    k = len(worlds)
+    handle = lambda w: w.handle if hasattr(w, "handle") else w.device_handle()  # noqa: E731  (DeviceWorld / PlanningWorld)
+    if not (len(qs) == len(flags) == k) or (masks is not None and len(masks) != k):
+        raise ValueError("one q / flags (/ masks) buffer per world")
+    P = ctypes.c_void_p
+    ptr = lambda t: P(t.data_ptr() if t is not None else 0)  # noqa: E731
+    hs = (P * k)(*[handle(w) for w in worlds])
+    qa = (P * k)(*[ptr(t) for t in qs])
+    fa = (P * k)(*[ptr(t) for t in flags])
+    ma = (P * k)(*[ptr(t) for t in masks]) if masks is not None else None
+    sa = (P * k)(*[P(int(s or 0)) for s in streams]) if streams is not None else None
+    counts = (ctypes.c_int64 * k)(*[int(t.shape[0]) for t in qs])
+    C.check(C.lib().mpg_collide_batch_multi_device(hs, k, qa, counts, fa, ma, sa, ptr(gather_flags),
+                                                   ptr(gather_masks)), "mpg_collide_batch_multi_device")

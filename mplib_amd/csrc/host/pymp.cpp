@@ -790,7 +790,10 @@ PYBIND11_MODULE(pymp, m_all) {
            py::arg("d_others_ptr"), py::arg("p_others_ptr"), py::arg("pts_self_ptr") = 0,
            py::arg("pts_others_ptr") = 0, py::arg("stream") = 0, py::arg("request") = py::none(),
            "Enqueue distance_batch on device buffers (float64 [n, dim] -> float64 [n], int32 [n] per group, "
-           "optional float64 [n, 6] nearest points).")
+           "optional float64 [n, 6] nearest points).  No error is raised for a configuration where FCL throws: "
+           "it gets NaN distances and pair index -2 (MPG_DISTANCE_FCL_THROWS) in both groups, or -3 "
+           "(MPG_DISTANCE_EPA_CAPACITY) when the EPA polytope outgrew the device; check p < -1 before indexing "
+           "the pair table (mplib_amd.dist.distance_sharded_device does).")
       .def("check_motion_batch",
            [](PW& w, py::array_t<double, py::array::c_style | py::array::forcecast> q_from,
               py::array_t<double, py::array::c_style | py::array::forcecast> q_to, double fraction, double lvs) {
@@ -839,6 +842,11 @@ PYBIND11_MODULE(pymp, m_all) {
            },
            "{stage: (milliseconds, launches, units)} accumulated since the last read; units are configurations "
            "(cull, bucket) or narrow-phase candidates (narrow).")
+      .def("device_handle",
+           [](PW& w) { return reinterpret_cast<uintptr_t>(w.device_world()); },
+           "The mpg_world* of the current snapshot (include/mpgpu.h), e.g. for mpg_collide_batch_multi_device; valid "
+           "until the world changes (a mutation rebuilds the snapshot).  The device is MPLIB_AMD_DEVICE / LOCAL_RANK "
+           "(default 0) when the snapshot is built.")
       .def("latency_server_stats",
            [](PW& w) {
              int64_t served = 0, starts = 0, fallbacks = 0;

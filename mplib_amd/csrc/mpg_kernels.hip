@@ -6473,6 +6473,8 @@ struct mpg_world {
   std::vector<int> geom_type_h;  // host copy of the geometry kinds (diagnostics)
   void* blob = nullptr;
   size_t blob_bytes = 0;
+  uint64_t snapshot_hash = 0;  // FNV-1a of the snapshot blob (mpg_collide_batch_multi's same-scene check)
+  hipEvent_t gather_ev = nullptr;  // mpg_collide_batch_multi_device: this shard's gather copies are queued
   int block = 128;
   size_t lds_bytes = 0;
   // staging for MPG_MEM_HOST
@@ -6517,6 +6519,7 @@ struct mpg_world {
     size_t states_cap = 0;
     uint8_t* flags = nullptr;
     size_t flags_cap = 0;
+    hipEvent_t last = nullptr;  // the previous call's work (scratch order across streams)
   } motion;
   std::mutex motion_mu;
   bool has_closed_form = false;  // a non-allowed pair uses an FCL closed form
@@ -6538,6 +6541,7 @@ struct mpg_world {
     size_t out_cap = 0;
     double* pts = nullptr;  // device-buffer calls: points nobody asked for
     size_t pts_cap = 0;
+    hipEvent_t last = nullptr;  // the previous call's work (scratch order across streams)
   } dist;
   // host-buffer contact calls: grow-only device staging (guarded by host_mu)
   struct ContactStage {
@@ -7438,6 +7442,30 @@ void free_ring(mpg_world* w) {
   R.in_cap = 0;
 }
 
+// World-owned scratch (distance, motion validation) used by calls on any
+// stream: a call's work waits for the previous call's (`last`, whatever its
+// stream), and a buffer is freed to grow only after that work has finished,
+// so two host threads on two streams never run over the same buffers at once
+// (calls on one world are serialised on the device; their enqueueing already
+// is, by the world's mutex).  Caller holds the scratch's mutex.
+int scratch_begin(hipEvent_t& last, hipStream_t s) {
+  if (!last) HIP_TRY(hipEventCreateWithFlags(&last, hipEventDisableTiming));
+  else HIP_TRY(hipStreamWaitEvent(s, last, 0));
+  return MPG_OK;
+}
+int scratch_grow(hipEvent_t last, void** p, size_t& cap, size_t want) {
+  if (cap >= want) return MPG_OK;
+  if (*p) {
+    if (last) HIP_TRY(hipEventSynchronize(last));
+    HIP_TRY(hipFree(*p));
+  }
+  *p = nullptr;
+  cap = 0;
+  HIP_TRY(hipMalloc(p, want));
+  cap = want;
+  return MPG_OK;
+}
+
 // slots of `cap` configurations with `row` input doubles each (grow-only)
 int ensure_ring(mpg_world* w, size_t cap, size_t row) {
   auto& R = w->ring;
@@ -8109,6 +8137,11 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
   w->block = block;
   w->lds_bytes = lds;
   w->blob_bytes = bb.bytes.size();
+  {  // FNV-1a over the snapshot: worlds built from the same descriptor agree
+    uint64_t h = 1469598103934665603ull;
+    for (const char c : bb.bytes) h = (h ^ (uint8_t)c) * 1099511628211ull;
+    w->snapshot_hash = h;
+  }
   hipError_t e = hipMalloc(&w->blob, w->blob_bytes);
   if (e != hipSuccess) {
     delete w;
@@ -8396,6 +8429,9 @@ int mpg_world_destroy(mpg_world* w) {
   hipFree(w->dist.q);
   hipFree(w->dist.out);
   hipFree(w->dist.pts);
+  if (w->dist.last) hipEventDestroy(w->dist.last);
+  if (w->gather_ev) hipEventDestroy(w->gather_ev);
+  if (w->motion.last) hipEventDestroy(w->motion.last);
   hipFree(w->contact.in);
   hipFree(w->contact.out);
   hipFree(w->contact.fl);
@@ -8911,18 +8947,18 @@ int mpg_collide_batch_multi(mpg_world* const* worlds, int32_t n_worlds, const do
     if (k == 0) {
       i0 = ik;
     } else if (ik.dof != i0.dof || ik.n_pairs != i0.n_pairs || ik.mask_words != i0.mask_words ||
-               ik.n_links != i0.n_links || ik.snapshot_bytes != i0.snapshot_bytes) {
+               ik.n_links != i0.n_links || ik.snapshot_bytes != i0.snapshot_bytes ||
+               worlds[k]->snapshot_hash != worlds[0]->snapshot_hash) {
       return set_error(MPG_E_INVALID, "world " + std::to_string(k) + " was not built from world 0's descriptor");
     }
     for (int j = 0; j < k; ++j)
       if (worlds[j] == worlds[k]) return set_error(MPG_E_INVALID, "a world is listed twice");
   }
-  // contiguous shards, the first n % n_worlds one row longer (mplib_amd.dist.shard_range)
-  const int64_t base = n / n_worlds, rem = n % n_worlds;
   std::vector<int> rc(n_worlds, MPG_OK);
   std::vector<std::string> err(n_worlds);
   auto run = [&](int k) {
-    const int64_t start = k * base + std::min<int64_t>(k, rem), count = base + (k < rem ? 1 : 0);
+    int64_t start = 0, count = 0;
+    mpg_shard_range(n, k, n_worlds, &start, &count);
     if (count == 0) return;
     rc[k] = mpg_collide_batch(worlds[k], q + (size_t)start * i0.dof, count, flags + start,
                               pair_mask ? pair_mask + (size_t)start * i0.mask_words : nullptr, MPG_MEM_HOST, nullptr);
@@ -8934,6 +8970,98 @@ int mpg_collide_batch_multi(mpg_world* const* worlds, int32_t n_worlds, const do
   for (auto& t : th) t.join();
   for (int k = 0; k < n_worlds; ++k)
     if (rc[k]) return set_error(rc[k], "world " + std::to_string(k) + ": " + err[k]);
+  return MPG_OK;
+}
+
+int mpg_shard_range(int64_t n, int32_t k, int32_t n_parts, int64_t* start, int64_t* count) {
+  if (n < 0 || n_parts <= 0 || k < 0 || k >= n_parts || !start || !count)
+    return set_error(MPG_E_INVALID, "mpg_shard_range: bad arguments");
+  // contiguous shards, the first n % n_parts one row longer (mplib_amd.dist.shard_range)
+  const int64_t base = n / n_parts, rem = n % n_parts;
+  *start = k * base + std::min<int64_t>(k, rem);
+  *count = base + (k < rem ? 1 : 0);
+  return MPG_OK;
+}
+
+int mpg_collide_batch_multi_device(mpg_world* const* worlds, int32_t n_worlds, const double* const* q,
+                                   const int64_t* counts, uint8_t* const* flags, uint32_t* const* pair_mask,
+                                   void* const* streams, uint8_t* gather_flags, uint32_t* gather_masks) {
+  if (n_worlds <= 0 || !worlds) return set_error(MPG_E_INVALID, "no worlds");
+  if (!counts || !q || !flags) return set_error(MPG_E_INVALID, "counts / q / flags array is NULL");
+  if (gather_masks && !pair_mask) return set_error(MPG_E_INVALID, "gather_masks needs pair_mask");
+  for (int k = 0; k < n_worlds; ++k) {
+    if (!worlds[k]) return set_error(MPG_E_INVALID, "world " + std::to_string(k) + " is NULL");
+    if (counts[k] < 0) return set_error(MPG_E_INVALID, "counts[" + std::to_string(k) + "] < 0");
+    for (int j = 0; j < k; ++j)
+      if (worlds[j] == worlds[k]) return set_error(MPG_E_INVALID, "a world is listed twice");
+  }
+  const mpg_world* w0 = worlds[0];
+  for (int k = 0; k < n_worlds; ++k) {
+    const mpg_world* wk = worlds[k];
+    if (wk->dw.dof != w0->dw.dof || wk->dw.n_pairs != w0->dw.n_pairs || wk->dw.W != w0->dw.W ||
+        wk->blob_bytes != w0->blob_bytes || wk->snapshot_hash != w0->snapshot_hash)
+      return set_error(MPG_E_INVALID, "world " + std::to_string(k) + " was not built from world 0's descriptor");
+    if (counts[k] > 0 && ((!q[k] && wk->dw.dof > 0) || !flags[k]))
+      return set_error(MPG_E_INVALID, "shard " + std::to_string(k) + ": q / flags is NULL");
+    if (counts[k] > 0 && gather_masks && !pair_mask[k])
+      return set_error(MPG_E_INVALID, "shard " + std::to_string(k) + ": gather_masks needs its pair_mask");
+  }
+  const int W = w0->dw.W;
+  std::vector<int64_t> off(n_worlds + 1, 0);
+  for (int k = 0; k < n_worlds; ++k) off[k + 1] = off[k] + counts[k];
+  const bool gather = gather_flags || gather_masks;
+  if (gather) {  // direct peer copies over xGMI from every other device into device 0
+    HIP_TRY(hipSetDevice(w0->device));
+    for (int k = 1; k < n_worlds; ++k) {
+      if (worlds[k]->device == w0->device) continue;
+      int can = 0;
+      HIP_TRY(hipDeviceCanAccessPeer(&can, w0->device, worlds[k]->device));
+      if (!can) continue;  // hipMemcpyPeerAsync still works, staged by the runtime
+      const hipError_t e = hipDeviceEnablePeerAccess(worlds[k]->device, 0);
+      if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled)
+        return set_error(MPG_E_HIP, std::string("hipDeviceEnablePeerAccess: ") + hipGetErrorString(e));
+      (void)hipGetLastError();
+    }
+  }
+  std::vector<int> rc(n_worlds, MPG_OK);
+  std::vector<std::string> err(n_worlds);
+  auto run = [&](int k) {
+    mpg_world* w = worlds[k];
+    hipStream_t s = streams ? static_cast<hipStream_t>(streams[k]) : nullptr;
+    uint32_t* mk = pair_mask ? pair_mask[k] : nullptr;
+    auto fail = [&](int code, const std::string& m) {
+      rc[k] = code;
+      err[k] = m;
+    };
+    if (hipSetDevice(w->device) != hipSuccess) return fail(MPG_E_HIP, "hipSetDevice failed");
+    if (counts[k] > 0) {
+      const int r = mpg_collide_batch(w, q[k], counts[k], flags[k], mk, MPG_MEM_DEVICE, s);
+      if (r) return fail(r, g_last_error);
+    }
+    if (!gather) return;
+    hipError_t e = hipSuccess;
+    if (counts[k] > 0 && gather_flags)
+      e = hipMemcpyPeerAsync(gather_flags + off[k], w0->device, flags[k], w->device, (size_t)counts[k], s);
+    if (e == hipSuccess && counts[k] > 0 && gather_masks)
+      e = hipMemcpyPeerAsync(gather_masks + off[k] * W, w0->device, mk, w->device,
+                             sizeof(uint32_t) * (size_t)counts[k] * W, s);
+    if (e == hipSuccess && k > 0) {
+      if (!w->gather_ev) e = hipEventCreateWithFlags(&w->gather_ev, hipEventDisableTiming);
+      if (e == hipSuccess) e = hipEventRecord(w->gather_ev, s);
+    }
+    if (e != hipSuccess) return fail(MPG_E_HIP, std::string("gather: ") + hipGetErrorString(e));
+  };
+  std::vector<std::thread> th;
+  for (int k = 1; k < n_worlds; ++k) th.emplace_back(run, k);
+  run(0);
+  for (auto& t : th) t.join();
+  for (int k = 0; k < n_worlds; ++k)
+    if (rc[k]) return set_error(rc[k], "world " + std::to_string(k) + ": " + err[k]);
+  if (gather) {  // streams[0] orders after every shard's copies
+    HIP_TRY(hipSetDevice(w0->device));
+    hipStream_t s0 = streams ? static_cast<hipStream_t>(streams[0]) : nullptr;
+    for (int k = 1; k < n_worlds; ++k) HIP_TRY(hipStreamWaitEvent(s0, worlds[k]->gather_ev, 0));
+  }
   return MPG_OK;
 }
 
@@ -8957,16 +9085,10 @@ int mpg_check_motion_batch(mpg_world* w, const double* q_from, const double* q_t
   std::lock_guard<std::mutex> lk(w->motion_mu);
   const int dof = w->dw.dof;
   const size_t eb = sizeof(double) * (size_t)n * dof;
-  auto grow = [&](void** p, size_t& cap, size_t want) -> int {
-    if (cap >= want) return MPG_OK;
-    if (*p) HIP_TRY(hipFree(*p));
-    *p = nullptr;
-    HIP_TRY(hipMalloc(p, want));
-    cap = want;
-    return MPG_OK;
-  };
   auto& M = w->motion;
-  int rc;
+  auto grow = [&](void** p, size_t& cap, size_t want) { return scratch_grow(M.last, p, cap, want); };
+  int rc = scratch_begin(M.last, s);
+  if (rc) return rc;
   if ((rc = grow((void**)&M.edges, M.edges_cap, 2 * eb))) return rc;
   if ((rc = grow((void**)&M.segs, M.segs_cap, sizeof(int32_t) * n))) return rc;
   if ((rc = grow((void**)&M.offs, M.offs_cap, sizeof(long long) * n))) return rc;
@@ -9014,6 +9136,7 @@ int mpg_check_motion_batch(mpg_world* w, const double* q_from, const double* q_t
   } else if (segments) {
     HIP_TRY(hipMemcpyAsync(segments, M.segs, sizeof(int32_t) * n, hipMemcpyDeviceToDevice, s));
   }
+  HIP_TRY(hipEventRecord(M.last, s));
   return MPG_OK;
 }
 
@@ -9054,16 +9177,10 @@ int mpg_distance_batch_req(mpg_world* w, const double* q, int64_t n, int32_t n_s
   HIP_TRY(hipSetDevice(w->device));
   hipStream_t s = static_cast<hipStream_t>(stream);
   std::lock_guard<std::mutex> lk(w->dist_mu);
-  auto grow = [&](void** p, size_t& cap, size_t want) -> int {
-    if (cap >= want) return MPG_OK;
-    if (*p) HIP_TRY(hipFree(*p));
-    *p = nullptr;
-    HIP_TRY(hipMalloc(p, want));
-    cap = want;
-    return MPG_OK;
-  };
   auto& D = w->dist;
-  int rc;
+  auto grow = [&](void** p, size_t& cap, size_t want) { return scratch_grow(D.last, p, cap, want); };
+  int rc = scratch_begin(D.last, s);
+  if (rc) return rc;
   const size_t nm = std::max(w->dw.n_moving, 1), ns = std::max(w->dw.bp.n_saves, 1);
   if ((rc = grow((void**)&D.poses, D.poses_cap, sizeof(double) * kPoseStride * nm * n))) return rc;
   if ((rc = grow((void**)&D.save64, D.save_cap, sizeof(double) * 12 * ns * n))) return rc;
@@ -9103,6 +9220,7 @@ int mpg_distance_batch_req(mpg_world* w, const double* q, int64_t n, int32_t n_s
     case P | SG: HIP_TRY(launch(distance_kernel<P | SG>)); break;
     default: HIP_TRY(launch(distance_kernel<P | SG | NPF>)); break;
   }
+  HIP_TRY(hipEventRecord(D.last, s));
   if (mem == MPG_MEM_HOST) {
     HIP_TRY(hipMemcpyAsync(d_self, ds, sizeof(double) * n, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipMemcpyAsync(d_others, dd, sizeof(double) * n, hipMemcpyDeviceToHost, s));

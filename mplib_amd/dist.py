@@ -145,6 +145,12 @@ def distance_sharded_device(compute, states, group=None, gather: bool = True, re
     for none), and with nearest_points pts_self / pts_others float64 [n, 6] --
     for the whole batch when ``gather`` (RCCL all-gather on GPUs) else for the
     shard, and the shard's (start, count).
+    Configurations where FCL throws (signed distance: libccd's EPA,
+    FCL_THROW_FAILED_AT_THIS_CONFIGURATION) come back from the device as NaN
+    distances with p = -2 (MPG_DISTANCE_FCL_THROWS), and p = -3 when the EPA
+    polytope outgrew the device's capacity (MPG_DISTANCE_EPA_CAPACITY); this
+    helper raises RuntimeError for either (after the gather, on every rank),
+    as the host-buffer API does, so no negative index reaches a pair table.
     """
     import torch
     import torch.distributed as dist
@@ -175,6 +181,26 @@ def distance_sharded_device(compute, states, group=None, gather: bool = True, re
         compute(q, sl["d_self"], sl["p_self"], sl["d_others"], sl["p_others"], sl.get("pts_self"),
                 sl.get("pts_others"))
     if not gather or world == 1:
+        _raise_on_sentinels(sl["p_self"], start)
         return sl, (start, count)
     keys = list(out)
-    return dict(zip(keys, _gather_rows([out[k] for k in keys], n, cap, group))), (start, count)
+    res = dict(zip(keys, _gather_rows([out[k] for k in keys], n, cap, group)))
+    _raise_on_sentinels(res["p_self"], 0)
+    return res, (start, count)
+
+
+MPG_DISTANCE_FCL_THROWS, MPG_DISTANCE_EPA_CAPACITY = -2, -3  # include/mpgpu.h
+
+
+def _raise_on_sentinels(p_self, offset: int):
+    """The device marks a failed configuration in both groups' pair index
+    (mpg_distance_batch_req); one small device reduction finds the first."""
+    bad = (p_self < -1).nonzero()
+    if bad.numel() == 0:
+        return
+    i = int(bad[0, 0])
+    code = int(p_self[i])
+    if code == MPG_DISTANCE_FCL_THROWS:
+        raise RuntimeError(f"configuration {offset + i}: FCL's libccd EPA throws here "
+                           "(FCL_THROW_FAILED_AT_THIS_CONFIGURATION)")
+    raise RuntimeError(f"configuration {offset + i}: EPA polytope beyond the device capacity (code {code})")

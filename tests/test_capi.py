@@ -136,6 +136,11 @@ def test_boundary_text_matches_the_code():
     for stale in ("GJK + fp64 EPA", "not restated)", "keep the ungated", "OBBRSS gate on single triangles is not"):
         assert stale not in design, stale
     assert "MPG_DISTANCE_EPA_CAPACITY" in hdr and "convexity guard" in hdr
+    # bench.py's notes describe the code that runs (a batch of
+    # at most one chunk runs on one stream since round 5)
+    bench = open(os.path.join(ROOT, "bench.py")).read()
+    for stale in ("overlap on two streams", "two halves' kernels"):
+        assert stale not in bench, stale
     # and the source comments next to the code (kernel, oracle)
     for rel in ("mplib_amd/csrc/mpg_kernels.hip", "oracle/collide_oracle.c"):
         src = open(os.path.join(ROOT, rel)).read()
@@ -201,3 +206,43 @@ def test_collide_batch_multi_rejects_bad_arguments():
     assert L.mpg_collide_batch_multi(none, 1, q.ctypes.data, 1, f.ctypes.data, None) == C.MPG_E_INVALID
     assert "NULL" in L.mpg_last_error().decode()
     assert L.mpg_collide_batch_multi(none, 1, q.ctypes.data, -1, f.ctypes.data, None) == C.MPG_E_INVALID
+
+
+def test_shard_range_matches_the_python_split():
+    """mpg_shard_range (the split of both multi-GPU C entries) equals
+    mplib_amd.dist.shard_range: contiguous, covering, the first n % parts
+    shards one row longer; bad arguments refused."""
+    from mplib_amd.batch import shard_range_c
+    from mplib_amd.dist import shard_range
+    for n in (0, 1, 7, 8, 9, 1000, 1 << 20, (1 << 22) + 5):
+        for parts in (1, 2, 3, 7, 8):
+            got = [shard_range_c(n, k, parts) for k in range(parts)]
+            assert got == [shard_range(n, k, parts) for k in range(parts)]
+            assert got[0][0] == 0 and sum(c for _, c in got) == n
+            assert all(got[k][0] + got[k][1] == got[k + 1][0] for k in range(parts - 1))
+    L = C.lib()
+    s, c = ctypes.c_int64(), ctypes.c_int64()
+    for args in ((10, 2, 2), (10, -1, 2), (10, 0, 0), (-1, 0, 1)):
+        assert L.mpg_shard_range(*args, ctypes.byref(s), ctypes.byref(c)) == C.MPG_E_INVALID
+    assert L.mpg_shard_range(10, 0, 1, None, ctypes.byref(c)) == C.MPG_E_INVALID
+
+
+def test_collide_batch_multi_device_rejects_bad_arguments():
+    """mpg_collide_batch_multi_device validates before touching a device."""
+    L = C.lib()
+    P = ctypes.c_void_p
+    none = (P * 1)(None)
+    counts = (ctypes.c_int64 * 1)(4)
+    neg = (ctypes.c_int64 * 1)(-1)
+    ptrs = (P * 1)(P(16))
+    f = L.mpg_collide_batch_multi_device
+    assert f(none, 0, ptrs, counts, ptrs, None, None, None, None) == C.MPG_E_INVALID
+    assert f(None, 1, ptrs, counts, ptrs, None, None, None, None) == C.MPG_E_INVALID
+    assert f(none, 1, ptrs, counts, ptrs, None, None, None, None) == C.MPG_E_INVALID  # NULL world
+    assert "NULL" in L.mpg_last_error().decode()
+    assert f(none, 1, None, counts, ptrs, None, None, None, None) == C.MPG_E_INVALID
+    assert f(none, 1, ptrs, None, ptrs, None, None, None, None) == C.MPG_E_INVALID
+    assert f(none, 1, ptrs, neg, ptrs, None, None, None, None) == C.MPG_E_INVALID
+    # mask gather without mask buffers
+    assert f(none, 1, ptrs, counts, ptrs, None, None, None, P(16)) == C.MPG_E_INVALID
+    assert "gather_masks" in L.mpg_last_error().decode()

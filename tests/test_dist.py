@@ -149,3 +149,37 @@ def test_distance_sharded_device_gloo_world2(tmp_path):
         s, c = int(d["start"]), int(d["count"])
         np.testing.assert_array_equal(d["shard_d"], ds[s:s + c])
     assert (np.minimum(ds, do) < 0).any()
+
+
+def test_distance_sharded_device_raises_on_fcl_throw_sentinels(tmp_path):
+    """the device marks a configuration where FCL throws with p =
+    -2 (MPG_DISTANCE_FCL_THROWS) and NaN distances, p = -3 past the EPA
+    capacity; distance_sharded_device raises instead of handing back a
+    negative pair index (one rank, gloo)."""
+    torch = pytest.importorskip("torch")
+    import torch.distributed as dist
+    from mplib_amd.dist import distance_sharded_device
+    dist.init_process_group("gloo", init_method=f"file://{tmp_path}/pg", rank=0, world_size=1)
+    try:
+        for code, what in ((-2, "throws"), (-3, "capacity")):
+            def compute(q, ds, ps, do, po, pts_s, pts_o, code=code):
+                ds.fill_(0.5)
+                do.fill_(0.25)
+                ps.fill_(3)
+                po.fill_(7)
+                ps[5] = code
+                po[5] = code
+                ds[5] = float("nan")
+                do[5] = float("nan")
+            with pytest.raises(RuntimeError, match=f"configuration 5: .*{what}"):
+                distance_sharded_device(compute, torch.zeros((9, 7), dtype=torch.float64))
+
+        def clean(q, ds, ps, do, po, pts_s, pts_o):
+            ds.fill_(0.5)
+            do.fill_(0.25)
+            ps.fill_(-1)
+            po.fill_(2)
+        out, (s, c) = distance_sharded_device(clean, torch.zeros((9, 7), dtype=torch.float64))
+        assert (s, c) == (0, 9) and int(out["p_self"][0]) == -1
+    finally:
+        dist.destroy_process_group()

@@ -1072,6 +1072,17 @@ def test_collide_batch_multi_one_device():
     np.testing.assert_array_equal(f[:3000], fo)
     with pytest.raises(ValueError, match="descriptor"):
         collide_batch_multi([dw(3), dw(2)], q[:10])
+    # same counts, another scene (red_cube moved 1 cm): refused by
+    # the snapshot hash, not only by the counts
+    import oracle
+    scene = Wd.boxes_scene()
+    name, geom, pose = scene[1]
+    scene[1] = (name, geom, (pose[0], [pose[1][0] + 0.01, pose[1][1], pose[1][2]]))
+    other = DeviceWorld(Wd.desc_arrays(oracle.OracleWorld(Wd.panda_articulation(), scene=scene,
+                                                          allowed=[("panda_link0", "table")])))
+    assert other.mask_words == dw(3).mask_words
+    with pytest.raises(ValueError, match="descriptor"):
+        collide_batch_multi([dw(3), other], q[:10])
 
 
 def test_distance_batch_device_matches_host_path():
@@ -1101,3 +1112,38 @@ def test_distance_batch_device_matches_host_path():
     np.testing.assert_array_equal(out["pts_self"].cpu().numpy(), qs)
     np.testing.assert_array_equal(out["pts_others"].cpu().numpy(), qo)
     dist.destroy_process_group()
+
+
+def test_collide_batch_multi_device_one_device():
+    """mpg_collide_batch_multi_device: a one-world list, and two
+    worlds of the same descriptor on the one device of this box with their
+    own streams and ragged shards, device-resident, gathered into one device
+    buffer: equal the single-world batch bit for bit."""
+    torch = pytest.importorskip("torch")
+    from mplib_amd.batch import collide_batch_multi_device, shard_range_c
+    q = Wd.sample_q(ow(3).art, 40001, 717)
+    f, m = dw(3).collide_batch(q)
+    qt = torch.from_numpy(q).cuda()
+    W = dw(3).mask_words
+    for ws in ([dw(3)], [dw(3), DeviceWorld(Wd.desc_arrays(ow(3)))]):
+        k = len(ws)
+        parts = [shard_range_c(len(q), i, k) for i in range(k)]
+        qs = [qt[s:s + c] for s, c in parts]
+        fl = [torch.full((c,), 7, dtype=torch.uint8, device="cuda") for _, c in parts]
+        mk = [torch.full((c, W), -1, dtype=torch.int32, device="cuda") for _, c in parts]
+        streams = [torch.cuda.Stream() for _ in ws]
+        gf = torch.zeros(len(q), dtype=torch.uint8, device="cuda")
+        gm = torch.zeros((len(q), W), dtype=torch.int32, device="cuda")
+        collide_batch_multi_device(ws, qs, fl, mk, [s.cuda_stream for s in streams], gf, gm)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(torch.cat(fl).cpu().numpy(), f)
+        np.testing.assert_array_equal(torch.cat(mk).cpu().numpy().view(np.uint32), m)
+        np.testing.assert_array_equal(gf.cpu().numpy(), f)
+        np.testing.assert_array_equal(gm.cpu().numpy().view(np.uint32), m)
+        for w, s in zip(ws, streams):
+            w.release_stream(s.cuda_stream)
+    # flags only, default streams, no gather
+    fl = [torch.zeros(len(q), dtype=torch.uint8, device="cuda")]
+    collide_batch_multi_device([dw(3)], [qt], fl)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(fl[0].cpu().numpy(), f)

@@ -5,6 +5,7 @@
 #   prof  : rocprofv3 kernel-trace/stats + PMC passes for cfg3, cfg2, cfg4
 #           (tools/profile.sh; each config's PMC record keyed to this build)
 #   bench : bench lines for cfg3 (default), cfg2, cfg4, cfg5
+#   extra : bench.py --host and --capi-multi 1 --gather
 # Every step has its own time limit; the first failure ends the call.
 set -o pipefail
 TAG=${1:-r04}; shift
@@ -31,6 +32,11 @@ for step in "$@"; do
       timeout -k 10 300 python bench.py --cfg $c > gpurun_out/bench_${TAG}_cfg$c.json 2> gpurun_out/bench_${TAG}_cfg$c.err || { tail gpurun_out/bench_${TAG}_cfg$c.err; exit 1; }
       head -c 300 gpurun_out/bench_${TAG}_cfg$c.json; echo
     done ;;
+  extra)  # round 6: host-buffer line, the in-process multi-GPU C route (one GPU here)
+    timeout -k 10 300 python bench.py --host > gpurun_out/bench_${TAG}_host.json 2> gpurun_out/bench_${TAG}_host.err || { tail gpurun_out/bench_${TAG}_host.err; exit 1; }
+    head -c 400 gpurun_out/bench_${TAG}_host.json; echo
+    timeout -k 10 300 python bench.py --capi-multi 1 --gather > gpurun_out/bench_${TAG}_capi1.json 2> gpurun_out/bench_${TAG}_capi1.err || { tail gpurun_out/bench_${TAG}_capi1.err; exit 1; }
+    head -c 400 gpurun_out/bench_${TAG}_capi1.json; echo ;;
   *) echo "unknown step $step"; exit 2 ;;
   esac
 done
