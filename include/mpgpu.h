@@ -360,10 +360,11 @@ int mpg_distance_batch(mpg_world *world, const double *q, int64_t n, int32_t n_s
  *   mesh-OcTree   always, (leaf box point, triangle point).
  * Where FCL throws (its EPA's FCL_THROW_FAILED_AT_THIS_CONFIGURATION) the
  * configuration's p_self = p_others = MPG_DISTANCE_FCL_THROWS and both
- * distances are NaN; MPG_MEM_HOST calls then return MPG_E_FAILED.  A device
- * EPA that outgrows its polytope (96 vertices) marks the configuration
- * MPG_DISTANCE_EPA_CAPACITY (MPG_MEM_HOST: MPG_E_UNSUPPORTED) -- never a
- * silently different value.
+ * distances are NaN; MPG_MEM_HOST calls then return MPG_E_FAILED.  An EPA
+ * that outgrows the lane's private polytope (96 vertices) is run again from
+ * the start with a 2048-vertex polytope from a per-world pool; only past
+ * that is the configuration marked MPG_DISTANCE_EPA_CAPACITY (MPG_MEM_HOST:
+ * MPG_E_UNSUPPORTED) -- never a silently different value.
  */
 #define MPG_DISTANCE_SIGNED 1
 #define MPG_DISTANCE_NEAREST_POINTS 2

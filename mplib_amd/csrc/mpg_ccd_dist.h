@@ -20,13 +20,14 @@
 // reused, list order is the link order, as ccdListAppend / ccdListDel keep
 // it).  Capacities: kPtV vertices (one per EPA iteration), kPtE edges, kPtF
 // faces (the oracle, unbounded, needs at most 29 vertices on the cfg3 / cfg4
-// test batches); a query that needs more sets Polytope::overflow and the call
-// fails loudly.
+// test batches); a query that needs more sets the polytope's overflow flag
+// and its configuration is run again with kBigPtV vertices (a global-memory
+// pool); past those the call fails loudly (MPG_DISTANCE_EPA_CAPACITY).
 #pragma once
 
 namespace ccdx {
 
-constexpr int kPtV = 96, kPtE = 288, kPtF = 192, kPtStack = 192;
+constexpr int kPtV = 96;  // the private polytope's vertices (edges 3x, faces 2x)
 constexpr ccd_real kEpaTol = ccd_real(0.0001);  // CCD_INIT epa_tolerance
 constexpr unsigned kMaxIter = 1000u;            // GJKSolver_libccd::max_distance_iterations
 constexpr int kVertex = 1, kEdge = 2, kFace = 3;
@@ -380,28 +381,37 @@ struct PtFace {
   CV3 wit;
   uint8_t mark;
 };
-struct Polytope {
-  Sup vs[kPtV];
-  ccd_real vdist[kPtV];
-  int16_t vnew[kPtV];
+// V vertices, 3V edges, 2V faces: the kernels' private polytope is
+// Polytope (V = kPtV); a query that outgrows it is run again with a
+// BigPolytope in a global-memory pool (distance_redo_kernel)
+template <int V>
+struct PolytopeT {
+  static constexpr int kV = V, kE = 3 * V, kF = 2 * V, kStk = 2 * V;
+  Sup vs[kV];
+  ccd_real vdist[kV];
+  int16_t vnew[kV];
   int nv;
-  PtEdge es[kPtE];
-  PtFace fs[kPtF];
+  PtEdge es[kE];
+  PtFace fs[kF];
   int ehead, etail, efree, fhead, ftail, ffree;
   int near_type, near_idx;  // near_idx < 0: NULL
   ccd_real near_dist;
   bool overflow;
-  int16_t stk_f[kPtStack];
-  uint8_t stk_e[kPtStack];
-  int16_t border[kPtE];
+  int16_t stk_f[kStk];
+  uint8_t stk_e[kStk];
+  int16_t border[kE];
 };
+using Polytope = PolytopeT<kPtV>;
+constexpr int kBigPtV = 2048;
+using BigPolytope = PolytopeT<kBigPtV>;
 
-__device__ void pt_init(Polytope& pt) {
+template <class PT>
+__device__ void pt_init(PT& pt) {
   pt.nv = 0;
   pt.ehead = pt.etail = -1;
   pt.fhead = pt.ftail = -1;
-  for (int i = 0; i < kPtE; ++i) pt.es[i].next = (int16_t)(i + 1 < kPtE ? i + 1 : -1);
-  for (int i = 0; i < kPtF; ++i) pt.fs[i].next = (int16_t)(i + 1 < kPtF ? i + 1 : -1);
+  for (int i = 0; i < PT::kE; ++i) pt.es[i].next = (int16_t)(i + 1 < PT::kE ? i + 1 : -1);
+  for (int i = 0; i < PT::kF; ++i) pt.fs[i].next = (int16_t)(i + 1 < PT::kF ? i + 1 : -1);
   pt.efree = 0;
   pt.ffree = 0;
   pt.near_type = 3;
@@ -410,7 +420,8 @@ __device__ void pt_init(Polytope& pt) {
   pt.overflow = false;
 }
 
-__device__ __forceinline__ void near_update(Polytope& pt, int type, int idx, ccd_real d) {
+template <class PT>
+__device__ __forceinline__ void near_update(PT& pt, int type, int idx, ccd_real d) {
   if (eq(pt.near_dist, d)) {
     if (type < pt.near_type) {
       pt.near_type = type;
@@ -424,15 +435,18 @@ __device__ __forceinline__ void near_update(Polytope& pt, int type, int idx, ccd
   }
 }
 
-__device__ __forceinline__ ccd_real el_dist(const Polytope& pt, int type, int idx) {
+template <class PT>
+__device__ __forceinline__ ccd_real el_dist(const PT& pt, int type, int idx) {
   return type == kVertex ? pt.vdist[idx] : type == kEdge ? pt.es[idx].dist : pt.fs[idx].dist;
 }
-__device__ __forceinline__ CV3 el_wit(const Polytope& pt, int type, int idx) {
+template <class PT>
+__device__ __forceinline__ CV3 el_wit(const PT& pt, int type, int idx) {
   return type == kVertex ? pt.vs[idx].v : type == kEdge ? pt.es[idx].wit : pt.fs[idx].wit;
 }
 
 // ccdPtNearest (renew: vertices, edges, faces, each in list order)
-__device__ void pt_nearest(Polytope& pt) {
+template <class PT>
+__device__ void pt_nearest(PT& pt) {
   if (pt.near_idx >= 0) return;
   pt.near_dist = FLT_MAX;
   pt.near_type = 3;
@@ -442,8 +456,9 @@ __device__ void pt_nearest(Polytope& pt) {
   for (int f = pt.fhead; f >= 0; f = pt.fs[f].next) near_update(pt, kFace, f, pt.fs[f].dist);
 }
 
-__device__ int add_vertex(Polytope& pt, const Sup& v) {
-  if (pt.nv >= kPtV) {
+template <class PT>
+__device__ int add_vertex(PT& pt, const Sup& v) {
+  if (pt.nv >= PT::kV) {
     pt.overflow = true;
     return -1;
   }
@@ -454,7 +469,8 @@ __device__ int add_vertex(Polytope& pt, const Sup& v) {
   return i;
 }
 
-__device__ int add_edge(Polytope& pt, int v1, int v2) {
+template <class PT>
+__device__ int add_edge(PT& pt, int v1, int v2) {
   if (pt.efree < 0 || v1 < 0 || v2 < 0) {
     pt.overflow = true;
     return -1;
@@ -477,14 +493,16 @@ __device__ int add_edge(Polytope& pt, int v1, int v2) {
 }
 
 // ccdPtFaceVec3 / getFaceVertices order
-__device__ __forceinline__ void face_vertices(const Polytope& pt, int f, int out[3]) {
+template <class PT>
+__device__ __forceinline__ void face_vertices(const PT& pt, int f, int out[3]) {
   const PtEdge &e0 = pt.es[pt.fs[f].e[0]], &e1 = pt.es[pt.fs[f].e[1]];
   out[0] = e0.v[0];
   out[1] = e0.v[1];
   out[2] = (e1.v[0] != out[0] && e1.v[0] != out[1]) ? e1.v[0] : e1.v[1];
 }
 
-__device__ int add_face(Polytope& pt, int e1, int e2, int e3) {
+template <class PT>
+__device__ int add_face(PT& pt, int e1, int e2, int e3) {
   if (pt.ffree < 0 || e1 < 0 || e2 < 0 || e3 < 0) {
     pt.overflow = true;
     return -1;
@@ -513,7 +531,8 @@ __device__ int add_face(Polytope& pt, int e1, int e2, int e3) {
   return f;
 }
 
-__device__ void del_face(Polytope& pt, int f) {
+template <class PT>
+__device__ void del_face(PT& pt, int f) {
   PtFace& F = pt.fs[f];
   for (int i = 0; i < 3; ++i) {
     PtEdge& E = pt.es[F.e[i]];
@@ -529,7 +548,8 @@ __device__ void del_face(Polytope& pt, int f) {
   pt.ffree = f;
 }
 
-__device__ void del_edge(Polytope& pt, int e) {
+template <class PT>
+__device__ void del_edge(PT& pt, int e) {
   PtEdge& E = pt.es[e];
   if (E.prev >= 0) pt.es[E.prev].next = E.next;
   else pt.ehead = E.next;
@@ -541,8 +561,8 @@ __device__ void del_edge(Polytope& pt, int e) {
 }
 
 // simplexToPolytope3: -1 = touching (nearest = the triangle)
-template <class SupF>
-__device__ int to_polytope3(SupF& sup, const Simplex& s, Polytope& pt) {
+template <class SupF, class PT>
+__device__ int to_polytope3(SupF& sup, const Simplex& s, PT& pt) {
   const Sup &a = s.ps[0], &b = s.ps[1], &c = s.ps[2];
   CV3 dir = vcross(vsub(b.v, a.v), vsub(c.v, a.v));
   const Sup d = sup(dir);
@@ -584,8 +604,8 @@ __device__ int to_polytope3(SupF& sup, const Simplex& s, Polytope& pt) {
 
 // simplexToPolytope4 (the degeneracy checks rewrite the simplex in place,
 // as libccd's aliased a..d pointers see it)
-template <class SupF>
-__device__ int to_polytope4(SupF& sup, Simplex& s, Polytope& pt) {
+template <class SupF, class PT>
+__device__ int to_polytope4(SupF& sup, Simplex& s, PT& pt) {
   bool use3 = false;
   if (iszero(tri_dist2<false>(s.ps[0].v, s.ps[1].v, s.ps[2].v, s.ps[3].v, nullptr))) use3 = true;
   if (iszero(tri_dist2<false>(s.ps[0].v, s.ps[2].v, s.ps[3].v, s.ps[1].v, nullptr))) {
@@ -624,8 +644,8 @@ __device__ int to_polytope4(SupF& sup, Simplex& s, Polytope& pt) {
 
 // the 2-simplex (origin on segment AB): a tetrahedron, or -1 (touching:
 // nearest = the segment's edge)
-template <class SupF>
-__device__ int segment_to_tetrahedron(SupF& sup, Simplex& s, Polytope& pt) {
+template <class SupF, class PT>
+__device__ int segment_to_tetrahedron(SupF& sup, Simplex& s, PT& pt) {
   const Sup A = s.ps[0], B = s.ps[1];
   const CV3 AB = vsub(B.v, A.v);
   int k = 0;
@@ -664,7 +684,8 @@ __device__ int segment_to_tetrahedron(SupF& sup, Simplex& s, Polytope& pt) {
 }
 
 // faceNormalPointingOutward (not normalised)
-__device__ CV3 face_normal_out(const Polytope& pt, int f) {
+template <class PT>
+__device__ CV3 face_normal_out(const PT& pt, int f) {
   const PtEdge &e0 = pt.es[pt.fs[f].e[0]], &e1 = pt.es[pt.fs[f].e[1]];
   const CV3 E1 = vsub(pt.vs[e0.v[1]].v, pt.vs[e0.v[0]].v), E2 = vsub(pt.vs[e1.v[1]].v, pt.vs[e1.v[0]].v);
   CV3 dir = vcross(E1, E2);
@@ -689,7 +710,8 @@ __device__ CV3 face_normal_out(const Polytope& pt, int f) {
   return dir;
 }
 
-__device__ __forceinline__ bool outside_face(const Polytope& pt, int f, const CV3& p) {
+template <class PT>
+__device__ __forceinline__ bool outside_face(const PT& pt, int f, const CV3& p) {
   const CV3 n = face_normal_out(pt, f);
   return vdot(n, vsub(p, pt.vs[pt.es[pt.fs[f].e[0]].v[0]].v)) > ccd_real(0);
 }
@@ -699,7 +721,8 @@ __device__ __forceinline__ bool outside_face(const Polytope& pt, int f, const CV
 // no-op, the parent being marked visible already), border edges kept in the
 // order it meets them; delete the visible faces and the internal edges, add
 // the vertex, one edge per silhouette vertex and one face per border edge
-__device__ int expand(Polytope& pt, int el_type, int el_idx, const Sup& newv) {
+template <class PT>
+__device__ int expand(PT& pt, int el_type, int el_idx, const Sup& newv) {
   int start;
   if (el_type == kVertex) return kThrow;
   if (el_type == kFace) {
@@ -728,7 +751,7 @@ __device__ int expand(Polytope& pt, int el_type, int el_idx, const Sup& newv) {
       if (outside_face(pt, g, newv.v)) {
         pt.fs[g].mark = 1;
         if (!E.mark) E.mark = 1;
-        if (sp >= kPtStack) {
+        if (sp >= PT::kStk) {
           pt.overflow = true;
           return kOverflow;
         }
@@ -772,7 +795,8 @@ __device__ int expand(Polytope& pt, int el_type, int el_idx, const Sup& newv) {
 }
 
 // supportEPADirection
-__device__ int epa_direction(const Polytope& pt, int type, int idx, CV3& dir) {
+template <class PT>
+__device__ int epa_direction(const PT& pt, int type, int idx, CV3& dir) {
   if (iszero(el_dist(pt, type, idx))) {
     if (type != kFace) return kThrow;
     dir = face_normal_out(pt, idx);
@@ -784,8 +808,8 @@ __device__ int epa_direction(const Polytope& pt, int type, int idx, CV3& dir) {
 }
 
 // nextSupport: 0 = expand, 1 = converged, kThrow (as the status, negated)
-template <class SupF>
-__device__ int next_support(const Polytope& pt, SupF& sup, int type, int idx, Sup& out) {
+template <class SupF, class PT>
+__device__ int next_support(const PT& pt, SupF& sup, int type, int idx, Sup& out) {
   if (type == kVertex) return 1;
   CV3 dir;
   if (epa_direction(pt, type, idx, dir)) return -kThrow;
@@ -805,7 +829,8 @@ __device__ int next_support(const Polytope& pt, SupF& sup, int type, int idx, Su
 }
 
 // validateNearestFeatureOfPolytopeBeingEdge
-__device__ int validate_edge(Polytope& pt) {
+template <class PT>
+__device__ int validate_edge(PT& pt) {
   const PtEdge& E = pt.es[pt.near_idx];
   const ccd_real kEps = ccd_real(2) * kCcdEps;
   const CV3 v0 = pt.vs[E.v[0]].v;
@@ -825,8 +850,8 @@ __device__ int validate_edge(Polytope& pt) {
 }
 
 // __ccdEPA; on kOk the nearest element is (pt.near_type, pt.near_idx)
-template <class SupF>
-__device__ int epa(SupF& sup, Simplex& s, Polytope& pt) {
+template <class SupF, class PT>
+__device__ int epa(SupF& sup, Simplex& s, PT& pt) {
   int ret;
   const int size = sx_size(s);
   if (size == 4) {
@@ -856,7 +881,8 @@ __device__ int epa(SupF& sup, Simplex& s, Polytope& pt) {
 }
 
 // penEPAPosClosest
-__device__ void pen_epa_pos_closest(const Polytope& pt, CV3& p1, CV3& p2) {
+template <class PT>
+__device__ void pen_epa_pos_closest(const PT& pt, CV3& p1, CV3& p2) {
   const int type = pt.near_type, idx = pt.near_idx;
   if (type == kVertex) {
     p1 = pt.vs[idx].v1;
@@ -881,8 +907,8 @@ __device__ void pen_epa_pos_closest(const Polytope& pt, CV3& p1, CV3& p2) {
 // GJKDistanceImpl with ccdGJKDist2 (SIGNED = false) or ccdGJKSignedDist:
 // points start at zero; status kOk / kThrow / kOverflow.  pt: the caller's
 // private polytope (signed queries only).
-template <bool SIGNED, class SupF>
-__device__ int gjk_distance(SupF& sup, ccd_real tol, Polytope* pt, ccd_real& d, CV3& p1, CV3& p2) {
+template <bool SIGNED, class SupF, class PT>
+__device__ int gjk_distance(SupF& sup, ccd_real tol, PT* pt, ccd_real& d, CV3& p1, CV3& p2) {
   p1 = CV3{0, 0, 0};
   p2 = CV3{0, 0, 0};
   Simplex s;

@@ -4217,7 +4217,7 @@ __device__ double octree_distance(const DevWorld& w, cptr<double> HV, int go, co
       auto sup = [&](const CV3& dir) { return csup_box(A1, h, w, HV, S, dir); };
       ccd_real df;
       CV3 c1, c2;
-      const int r = ccdx::gjk_distance<false>(sup, tol, nullptr, df, c1, c2);
+      const int r = ccdx::gjk_distance<false>(sup, tol, (ccdx::Polytope*)nullptr, df, c1, c2);
       if (r != ccdx::kOk) {
         st = r == ccdx::kThrow ? kDistThrow : kDistOverflow;
         return DBL_MAX;
@@ -4534,7 +4534,7 @@ __device__ double mesh_shape_distance_lane(const DevWorld& w, cptr<double> HV, i
         auto sup = [&](const CV3& dir) { return csup_tri(w, HV, S, B, TP, tc, dir); };
         ccd_real df;
         CV3 c1, c2;
-        const int r = ccdx::gjk_distance<false>(sup, tol, nullptr, df, c1, c2);
+        const int r = ccdx::gjk_distance<false>(sup, tol, (ccdx::Polytope*)nullptr, df, c1, c2);
         if (r != ccdx::kOk) {
           st = r == ccdx::kThrow ? kDistThrow : kDistOverflow;
           return DBL_MAX;
@@ -4697,7 +4697,7 @@ __device__ double mesh_octree_distance_lane(const DevWorld& w, int gm, const SE3
         auto sup = [&](const CV3& dir) { return csup_box_tri(A1, h, B, TP, tc, dir); };
         ccd_real df;
         CV3 q1, q2;
-        const int r = ccdx::gjk_distance<false>(sup, tol, nullptr, df, q1, q2);
+        const int r = ccdx::gjk_distance<false>(sup, tol, (ccdx::Polytope*)nullptr, df, q1, q2);
         if (r != ccdx::kOk) {
           st = r == ccdx::kThrow ? kDistThrow : kDistOverflow;
           return DBL_MAX;
@@ -4720,6 +4720,7 @@ __device__ double mesh_octree_distance_lane(const DevWorld& w, int gm, const SE3
 // (MODE bit) PTS: write the nearest points; SIGNED: enable_signed_distance;
 // NP: enable_nearest_points (mesh-mesh points, the (shape, mesh) swap)
 constexpr int MPG_DIST_POINTS = 1, MPG_DIST_SIGNED = 2, MPG_DIST_NP = 4;
+constexpr int kBigPool = 16;  // big EPA polytopes per world (distance_redo_kernel)
 
 // Per configuration, every non-allowed pair in order with the group's strict
 // '<' (planning_world.cpp:513): fcl::distance with DistanceRequest's options
@@ -4729,23 +4730,18 @@ constexpr int MPG_DIST_POINTS = 1, MPG_DIST_SIGNED = 2, MPG_DIST_NP = 4;
 // value cannot be below it).  A configuration on which FCL throws
 // (p = kDistThrow) or whose EPA outgrows the polytope arrays (p =
 // kDistOverflow) gets NaN distances in both groups.
-template <int MODE>
-__global__ __launch_bounds__(128) void distance_kernel(DevWorld w, const double* __restrict__ poses, long long n,
-                                                       int n_self, ccd_real tol, double* __restrict__ d_self,
-                                                       int32_t* __restrict__ p_self, double* __restrict__ d_others,
-                                                       int32_t* __restrict__ p_others, double* __restrict__ pts_self,
-                                                       double* __restrict__ pts_others) {
+// PT: the signed instances' EPA polytope type; ptp its storage (private in
+// distance_kernel, a global pool slot in distance_redo_kernel).
+template <int MODE, class PT>
+__device__ __forceinline__ void distance_config(const DevWorld& w, const double* __restrict__ poses, long long n,
+                                                long long cfg, bool live, int n_self, ccd_real tol, PT* ptp,
+                                                double* __restrict__ d_self, int32_t* __restrict__ p_self,
+                                                double* __restrict__ d_others, int32_t* __restrict__ p_others,
+                                                double* __restrict__ pts_self, double* __restrict__ pts_others) {
   constexpr bool SIGNED = (MODE & MPG_DIST_SIGNED) != 0;
   constexpr bool PTS = (MODE & MPG_DIST_POINTS) != 0;
   constexpr bool NP = (MODE & MPG_DIST_NP) != 0;
-  const long long cfg0 = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  const bool live = cfg0 < n;
-  const long long cfg = live ? cfg0 : n - 1;
   const cptr<double> HV = w.hull;
-  struct NoPolytope {};
-  std::conditional_t<SIGNED, ccdx::Polytope, NoPolytope> polytope;
-  ccdx::Polytope* ptp = nullptr;
-  if constexpr (SIGNED) ptp = &polytope;
   double best[2] = {DBL_MAX, DBL_MAX};
   int bp[2] = {-1, -1};
   V3 bpt[2][2] = {{{0, 0, 0}, {0, 0, 0}}, {{0, 0, 0}, {0, 0, 0}}};
@@ -4841,6 +4837,51 @@ __global__ __launch_bounds__(128) void distance_kernel(DevWorld w, const double*
       o[5] = bpt[g][1].z;
     }
   }
+}
+
+template <int MODE>
+__global__ __launch_bounds__(128) void distance_kernel(DevWorld w, const double* __restrict__ poses, long long n,
+                                                       int n_self, ccd_real tol, double* __restrict__ d_self,
+                                                       int32_t* __restrict__ p_self, double* __restrict__ d_others,
+                                                       int32_t* __restrict__ p_others, double* __restrict__ pts_self,
+                                                       double* __restrict__ pts_others) {
+  constexpr bool SIGNED = (MODE & MPG_DIST_SIGNED) != 0;
+  const long long cfg0 = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool live = cfg0 < n;
+  const long long cfg = live ? cfg0 : n - 1;
+  struct NoPolytope {};
+  std::conditional_t<SIGNED, ccdx::Polytope, NoPolytope> polytope;
+  ccdx::Polytope* ptp = nullptr;
+  if constexpr (SIGNED) ptp = &polytope;
+  distance_config<MODE>(w, poses, n, cfg, live, n_self, tol, ptp, d_self, p_self, d_others, p_others, pts_self,
+                        pts_others);
+}
+
+// Signed instances only: the configurations distance_kernel left at
+// kDistOverflow (an EPA past kPtV vertices; rare -- 29 at most on the parity
+// batches, 124 for a sphere deep in a sphere) are listed (overflow_list_kernel:
+// list[0] = count, ids after it; the count zeroed by the host), then evaluated
+// again from the start by kBigPool lanes, lane k with the k-th kBigPtV-vertex
+// polytope of `pool`, taking every kBigPool-th listed configuration.
+__global__ __launch_bounds__(256) void overflow_list_kernel(const int32_t* __restrict__ p_self, long long n,
+                                                            unsigned* __restrict__ list) {
+  const long long cfg = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (cfg < n && p_self[cfg] == kDistOverflow) list[1 + atomicAdd(&list[0], 1u)] = (unsigned)cfg;
+}
+
+template <int MODE>
+__global__ __launch_bounds__(64) void distance_redo_kernel(DevWorld w, const double* __restrict__ poses, long long n,
+                                                           int n_self, ccd_real tol, double* __restrict__ d_self,
+                                                           int32_t* __restrict__ p_self, double* __restrict__ d_others,
+                                                           int32_t* __restrict__ p_others,
+                                                           double* __restrict__ pts_self,
+                                                           double* __restrict__ pts_others,
+                                                           ccdx::BigPolytope* __restrict__ pool,
+                                                           const unsigned* __restrict__ list) {
+  const unsigned k = threadIdx.x, count = list[0];
+  for (unsigned i = k; i < count; i += kBigPool)
+    distance_config<MODE>(w, poses, n, (long long)list[1 + i], true, n_self, tol, pool + k, d_self, p_self, d_others,
+                          p_others, pts_self, pts_others);
 }
 
 // ---------------------------------------------------------------------------
@@ -6542,6 +6583,10 @@ struct mpg_world {
     double* pts = nullptr;  // device-buffer calls: points nobody asked for
     size_t pts_cap = 0;
     hipEvent_t last = nullptr;  // the previous call's work (scratch order across streams)
+    ccdx::BigPolytope* big = nullptr;  // kBigPool EPA polytopes (distance_redo_kernel)
+    size_t big_cap = 0;
+    unsigned* list = nullptr;  // overflowed configurations: [count, ids...]
+    size_t list_cap = 0;
   } dist;
   // host-buffer contact calls: grow-only device staging (guarded by host_mu)
   struct ContactStage {
@@ -8430,6 +8475,8 @@ int mpg_world_destroy(mpg_world* w) {
   hipFree(w->dist.out);
   hipFree(w->dist.pts);
   if (w->dist.last) hipEventDestroy(w->dist.last);
+  hipFree(w->dist.big);
+  hipFree(w->dist.list);
   if (w->gather_ev) hipEventDestroy(w->gather_ev);
   if (w->motion.last) hipEventDestroy(w->motion.last);
   hipFree(w->contact.in);
@@ -9220,6 +9267,21 @@ int mpg_distance_batch_req(mpg_world* w, const double* q, int64_t n, int32_t n_s
     case P | SG: HIP_TRY(launch(distance_kernel<P | SG>)); break;
     default: HIP_TRY(launch(distance_kernel<P | SG | NPF>)); break;
   }
+  if (mode & SG) {  // EPAs past the private polytope: again with a big one from the pool
+    if ((rc = grow((void**)&D.big, D.big_cap, sizeof(ccdx::BigPolytope) * kBigPool))) return rc;
+    if ((rc = grow((void**)&D.list, D.list_cap, sizeof(unsigned) * (n + 1)))) return rc;
+    HIP_TRY(hipMemsetAsync(D.list, 0, sizeof(unsigned), s));
+    hipLaunchKernelGGL(overflow_list_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, ps, (long long)n,
+                       D.list);
+    HIP_TRY(hipGetLastError());
+    auto redo = [&](auto kern) {
+      hipLaunchKernelGGL(kern, dim3(1), dim3(kBigPool), 0, s, w->dw, D.poses, (long long)n, n_self_pairs, tol, ds, ps,
+                         dd, po, qs, qo, D.big, D.list);
+      return hipGetLastError();
+    };
+    if (mode & NPF) HIP_TRY(redo(distance_redo_kernel<P | SG | NPF>));
+    else HIP_TRY(redo(distance_redo_kernel<P | SG>));
+  }
   HIP_TRY(hipEventRecord(D.last, s));
   if (mem == MPG_MEM_HOST) {
     HIP_TRY(hipMemcpyAsync(d_self, ds, sizeof(double) * n, hipMemcpyDeviceToHost, s));
@@ -9236,7 +9298,7 @@ int mpg_distance_batch_req(mpg_world* w, const double* q, int64_t n, int32_t n_s
       if (p_self[i] == MPG_DISTANCE_EPA_CAPACITY)
         return set_error(MPG_E_UNSUPPORTED, "configuration " + std::to_string(i) +
                                                 ": EPA polytope beyond the device capacity (" +
-                                                std::to_string(ccdx::kPtV) + " vertices)");
+                                                std::to_string(ccdx::kBigPtV) + " vertices)");
     }
   }
   return MPG_OK;
