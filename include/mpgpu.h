@@ -186,7 +186,20 @@ typedef struct mpg_world_desc {
    *     narrow phase), so no input changes a result.                         */
   const double *joint_lower;      /* [n_joints] or NULL                     */
   const double *joint_upper;      /* [n_joints] or NULL                     */
+
+  /* --- CollisionRequest::gjk_solver_type (python/pybind_fcl.hpp:264, 276):
+   *     MPG_GJK_LIBCCD (0, the default, libccd MPR in float) or MPG_GJK_INDEP
+   *     (FCL's own GJK in double, GJKSolver_indep::shapeIntersect) for every
+   *     shape pair without an FCL closed form.  GST_INDEP worlds take shape
+   *     geometry only (MPG_GEOM_OCTREE / MPG_GEOM_MESH in a non-allowed pair:
+   *     MPG_E_UNSUPPORTED) and the collide entry points only (contacts:
+   *     MPG_E_UNSUPPORTED; the distance calls keep libccd, as
+   *     DistanceRequest's own default does).                               */
+  int32_t gjk_solver;
 } mpg_world_desc;
+
+#define MPG_GJK_LIBCCD 0
+#define MPG_GJK_INDEP 1
 
 typedef struct mpg_world mpg_world;
 

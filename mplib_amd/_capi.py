@@ -20,6 +20,7 @@ STAGES = ("cull", "bucket", "narrow")  # MPG_STAGE_* order
 (JOINT_RX, JOINT_RY, JOINT_RZ, JOINT_REVOLUTE_UNALIGNED, JOINT_PX, JOINT_PY, JOINT_PZ,
  JOINT_PRISMATIC_UNALIGNED, JOINT_RUBX, JOINT_RUBY, JOINT_RUBZ, JOINT_RUB_UNALIGNED) = range(12)
 GEOM_CONVEX, GEOM_BOX, GEOM_SPHERE, GEOM_CAPSULE, GEOM_CYLINDER = range(5)
+GJK_LIBCCD, GJK_INDEP = 0, 1
 
 _I32P = ctypes.POINTER(ctypes.c_int32)
 _F64P = ctypes.POINTER(ctypes.c_double)
@@ -46,6 +47,7 @@ class WorldDesc(ctypes.Structure):
         ("n_mesh_triangles", ctypes.c_int64), ("mesh_triangle", _I32P),
         ("n_convex_face_ints", ctypes.c_int64), ("convex_face", _I32P),
         ("joint_lower", _F64P), ("joint_upper", _F64P),
+        ("gjk_solver", ctypes.c_int32),
     ]
 
 

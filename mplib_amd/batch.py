@@ -32,7 +32,8 @@ _DESC_F64_FIELDS = ["joint_axis", "joint_placement", "joint_q_const", "link_plac
 class DeviceWorld:
     """An ``mpg_world`` snapshot on one device."""
 
-    def __init__(self, arrays: Dict[str, np.ndarray], device: int = 0, gjk_tolerance: float = 1e-6):
+    def __init__(self, arrays: Dict[str, np.ndarray], device: int = 0, gjk_tolerance: float = 1e-6,
+                 gjk_solver: int = C.GJK_LIBCCD):
         L = C.lib()
         self._keep = []
 
@@ -69,6 +70,7 @@ class DeviceWorld:
         self._keep.append(al)
         d.pair_allowed = al.ctypes.data_as(C._U8P)
         d.gjk_tolerance = gjk_tolerance
+        d.gjk_solver = int(gjk_solver)
         leaves = np.ascontiguousarray(np.asarray(arrays.get("octree_leaf", np.zeros(0)), dtype=np.float64).reshape(-1))
         d.n_octree_leaves = leaves.size // 6
         if leaves.size == 0:

@@ -261,6 +261,7 @@ struct DescBuilder {
   std::vector<int32_t> pair_a, pair_b;
   std::vector<uint8_t> pair_allowed;
   double gjk_tolerance = 1e-6;
+  int gjk_solver = MPG_GJK_LIBCCD;  // CollisionRequest::gjk_solver_type
   std::vector<const CollisionGeometry*> geoms;  // identity for geometry dedup
 
   int add_geometry(const CollisionGeometry* g);

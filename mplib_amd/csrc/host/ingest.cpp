@@ -332,8 +332,11 @@ std::shared_ptr<BVHModel> load_mesh_as_bvh(const std::string& path, const Vec3& 
 // ---------------------------------------------------------------------------
 void CollisionRequest::check_supported() const {
   if (num_max_contacts == 0) throw std::invalid_argument("CollisionRequest.num_max_contacts must be >= 1");
-  if (gjk_solver_type != GST_LIBCCD)
-    throw std::logic_error("NotImplemented: only gjk_solver_type=GST_LIBCCD is implemented on the device");
+  // GST_INDEP: FCL's own GJK on the device for collision; its EPA contacts are
+  // not restated
+  if (gjk_solver_type == GST_INDEP && enable_contact)
+    throw std::logic_error("NotImplemented: enable_contact=True with gjk_solver_type=GST_INDEP (FCL's EPA) is not "
+                           "implemented on the device");
   if (enable_cost) throw std::logic_error("NotImplemented: enable_cost=True is not implemented on the device");
   if (!(gjk_tolerance > 0)) throw std::invalid_argument("gjk_tolerance must be > 0");
 }
@@ -452,6 +455,7 @@ mpg_world_desc DescBuilder::desc() const {
   d.pair_b = pair_b.data();
   d.pair_allowed = pair_allowed.data();
   d.gjk_tolerance = gjk_tolerance;
+  d.gjk_solver = gjk_solver;
   d.n_octree_leaves = (int64_t)(octree_leaf.size() / 6);
   d.octree_leaf = octree_leaf.data();
   d.n_mesh_triangles = (int64_t)(mesh_triangle.size() / 3);

@@ -495,10 +495,12 @@ const std::vector<ObjPtr>& FCLModel::get_collision_objects() const {
 std::vector<uint32_t> FCLModel::run_pairs(const CollisionRequest& req, std::vector<double>* depth,
                                           std::vector<double>* normal, std::vector<double>* pos) const {
   req.check_supported();
-  const uint64_t key = structure_version_ * 1000003ull + (uint64_t)std::llround(req.gjk_tolerance * 1e15);
+  const uint64_t key = (structure_version_ * 1000003ull + (uint64_t)std::llround(req.gjk_tolerance * 1e15)) * 2ull +
+                       (req.gjk_solver_type == GST_INDEP ? 1ull : 0ull);
   if (!world_ || world_key_ != key) {
     DescBuilder d;
     d.gjk_tolerance = req.gjk_tolerance;
+    d.gjk_solver = req.gjk_solver_type == GST_INDEP ? MPG_GJK_INDEP : MPG_GJK_LIBCCD;
     for (size_t l = 0; l < user_link_names_.size(); ++l) {
       d.link_parent.push_back(0);
       push_se3(d.link_placement, identity_se3());

@@ -348,6 +348,7 @@ PYBIND11_MODULE(pymp, m_all) {
         req.check_supported();
         DescBuilder d;
         d.gjk_tolerance = req.gjk_tolerance;
+        d.gjk_solver = req.gjk_solver_type == GST_INDEP ? MPG_GJK_INDEP : MPG_GJK_LIBCCD;
         d.link_parent.push_back(0);
         SE3 I;
         mpg::se3_identity(I);

@@ -362,6 +362,7 @@ uint64_t PlanningWorld::snapshot_key(const CollisionRequest& r) const {
   mix(structure_version_);
   mix(acm_->version());
   mixd(r.gjk_tolerance);
+  mix((uint64_t)r.gjk_solver_type);
   for (auto& kv : arts_) {
     mix(kv.second->structure_version());
     mix(kv.second->get_fcl_model()->structure_version());
@@ -398,6 +399,7 @@ void PlanningWorld::ensure_snapshot(const CollisionRequest& r, bool need_device)
   desc_ = std::make_unique<DescBuilder>();
   DescBuilder& d = *desc_;
   d.gjk_tolerance = r.gjk_tolerance;
+  d.gjk_solver = r.gjk_solver_type == GST_INDEP ? MPG_GJK_INDEP : MPG_GJK_LIBCCD;
   pairs_.clear();
   full_src_.clear();
   full_lo_.clear();
@@ -781,6 +783,7 @@ WorldDistanceResult PlanningWorld::distance_full(const DistanceRequest& r) {
   return r1.min_distance < r2.min_distance ? r1 : r2;  // planning_world.cpp:718-719
 }
 // the reference ignores the request here (planning_world.h:271-273)
+// the reference ignores the request here (planning_world.h:271-273: distanceFull())
 double PlanningWorld::distance(const DistanceRequest&) { return distance_full().min_distance; }
 
 void PlanningWorld::profile_enable(bool on) { check_status(mpg_profile_enable(device_world(), on ? 1 : 0), "mpg_profile_enable"); }

@@ -526,6 +526,8 @@ __device__ __forceinline__ CV3 support_local(const DevWorld& w, cptr<double> HV,
   return v;
 }
 
+#include "mpg_gjk_indep.h"
+
 // True extreme point of a shape along dir in its own frame, fp64 (every
 // vertex for hulls, whatever FCL's walk would return): conservative range
 // tests only, never an output bit.
@@ -699,12 +701,13 @@ __device__ __forceinline__ GObj moving_obj(const DevWorld& w, const double* __re
 // ---------------------------------------------------------------------------
 enum : int {
   CF_NONE = 0, CF_BOX_BOX = 1, CF_SPHERE_SPHERE = 2, CF_SPHERE_BOX = 3, CF_BOX_SPHERE = 4, CF_OCTREE = 5,
-  CF_SPHERE_CAPSULE = 6, CF_CAPSULE_SPHERE = 7, CF_SPHERE_CYLINDER = 8, CF_CYLINDER_SPHERE = 9, CF_MESH = 10
+  CF_SPHERE_CAPSULE = 6, CF_CAPSULE_SPHERE = 7, CF_SPHERE_CYLINDER = 8, CF_CYLINDER_SPHERE = 9, CF_MESH = 10,
+  CF_GJK = 11  // GST_INDEP worlds: FCL's own GJK (mpg_gjk_indep.h) in place of libccd MPR
 };
 // narrow-phase classes of the candidate lists: each its own kernel instance
-enum : int { CLS_CLOSED = 0, CLS_OCTREE = 1, CLS_MESH = 2 };
+enum : int { CLS_CLOSED = 0, CLS_OCTREE = 1, CLS_MESH = 2, CLS_GJK = 3 };
 __host__ __device__ __forceinline__ int cf_class(int cf) {
-  return cf == CF_OCTREE ? CLS_OCTREE : cf == CF_MESH ? CLS_MESH : CLS_CLOSED;
+  return cf == CF_OCTREE ? CLS_OCTREE : cf == CF_MESH ? CLS_MESH : cf == CF_GJK ? CLS_GJK : CLS_CLOSED;
 }
 
 // detail::boxBox2 (box_box-inl.h, from ODE dBoxBox): return_code != 0
@@ -1526,7 +1529,8 @@ __device__ __forceinline__ unsigned long long walk_wave_eval(const DevWorld& w, 
 template <int CLS>
 __device__ __forceinline__ bool pair_closed_form(int cf, const DevWorld& w, int ga, const SE3& TA, int gb,
                                                  const SE3& TB) {
-  if (CLS == CLS_CLOSED) return closed_form(cf, w, ga, TA, gb, TB);
+  if constexpr (CLS == CLS_CLOSED) return closed_form(cf, w, ga, TA, gb, TB);
+  if constexpr (CLS == CLS_GJK) return gjk_indep_intersect(w, ga, TA, gb, TB);
   return false;  // octree / mesh pairs: evaluated wave-wide (walk_wave_eval)
 }
 
@@ -1564,7 +1568,7 @@ __global__ __launch_bounds__(256, CLS == CLS_OCTREE ? 2 : 1) void closed_form_ke
     const uint32_t* __restrict__ cl = cand + seg_start[p];
     for (uint32_t base = t0; base < t1; base += 64) {
       const uint32_t idx = base + lane;
-      if (CLS != CLS_CLOSED) {  // octree / mesh walks: the wave walks each candidate together
+      if constexpr (CLS == CLS_OCTREE || CLS == CLS_MESH) {  // the wave walks each candidate together
         const bool active = idx < t1;
         const long long c = active ? cl[idx] : 0;
         SE3 TA = {}, TB = {};
@@ -3197,14 +3201,14 @@ __global__ __launch_bounds__(256) void small_kernel(DevWorld w, const double* __
     }
     const double rr = rsum + w.small_margin;
     bool near = live && d2 <= rr * rr && !w.dbg(3) && !(w.dbg(7) && d2 >= 0.0);
-    if (CLS == CLS_CLOSED && __ballot(near) != 0ull) {  // the boxes next (MPR / closed-form pairs)
+    if ((CLS == CLS_CLOSED || CLS == CLS_GJK) && __ballot(near) != 0ull) {  // the boxes next (MPR / closed forms)
       const cptr<double> ra = w.geom_rec + G_STRIDE * ga, rb = w.geom_rec + G_STRIDE * gb;
       const double ea[3] = {ra[G_OBB_E], ra[G_OBB_E + 1], ra[G_OBB_E + 2]};
       const double eb[3] = {rb[G_OBB_E], rb[G_OBB_E + 1], rb[G_OBB_E + 2]};
       if (near && dobb_separated(TA.R, wc[0], ea, TB.R, wc[1], eb, w.small_margin)) near = false;
     }
     tmark(3, tlast);  // bounding spheres
-    if (CLS != CLS_CLOSED) {
+    if constexpr (CLS == CLS_OCTREE || CLS == CLS_MESH) {
       hit = (walk_wave_eval<CLS>(w, HV, ga, TA, gb, TB, near) >> lane) & 1ull;
     } else if (cf != CF_NONE) {
       if (near && pair_closed_form<CLS>(cf, w, ga, TA, gb, TB)) hit = 1;
@@ -6570,6 +6574,7 @@ struct mpg_world {
   bool any_octree = false;       // some pair involves an octree
   bool has_mesh = false;         // a non-allowed pair involves a BVH mesh
   bool any_mesh = false;         // some pair involves a BVH mesh
+  bool any_gjk = false;          // GST_INDEP world: some pair runs FCL's own GJK (CF_GJK)
   // batched distance buffers (grow-only)
   struct Dist {
     double* poses = nullptr;
@@ -6779,6 +6784,8 @@ int closed_form_kind(const mpg_world_desc* d, int a, int b) {
 
 int validate(const mpg_world_desc* d) {
   if (!d) return set_error(MPG_E_INVALID, "desc is NULL");
+  if (d->gjk_solver != MPG_GJK_LIBCCD && d->gjk_solver != MPG_GJK_INDEP)
+    return set_error(MPG_E_INVALID, "gjk_solver must be MPG_GJK_LIBCCD or MPG_GJK_INDEP");
   if (d->n_joints < 0 || d->n_joints > kMaxJoints) return set_error(MPG_E_INVALID, "n_joints out of range [0, 32]");
   if (d->dof < 0) return set_error(MPG_E_INVALID, "dof < 0");
   if (d->n_links < 0 || d->n_geoms < 0 || d->n_moving < 0 || d->n_static < 0 || d->n_pairs < 0)
@@ -6857,6 +6864,12 @@ int validate(const mpg_world_desc* d) {
     // FCL 0.7.0 GJKSolver_libccd: box-box, sphere-sphere, sphere-box,
     // sphere-capsule and sphere-cylinder have closed forms (all on the
     // device, closed_form_kind); every other shape pair is MPR
+    if (d->gjk_solver == MPG_GJK_INDEP && !(d->pair_allowed && d->pair_allowed[p])) {
+      const int ta = obj_geom_type(d, a), tb = obj_geom_type(d, b);
+      if (ta == MPG_GEOM_MESH || tb == MPG_GEOM_MESH || ta == MPG_GEOM_OCTREE || tb == MPG_GEOM_OCTREE)
+        return set_error(MPG_E_UNSUPPORTED,
+                         "gjk_solver MPG_GJK_INDEP with an OcTree or BVH mesh in a pair is not implemented");
+    }
   }
   if (!finite_all(d->joint_placement, 12 * (size_t)d->n_joints) || !finite_all(d->link_placement, 12 * (size_t)d->n_links) ||
       !finite_all(d->vertices, 3 * (size_t)d->n_vertices))
@@ -7425,6 +7438,11 @@ int launch_collide(mpg_world* w, const double* in, long long n, uint8_t* flags, 
                          w->dw, qin, ws->seg_len, ws->seg_start, ws->prefix, ws->cand, fl, mk, ws->sc);
       HIP_TRY(hipGetLastError());
     }
+    if (w->any_gjk) {
+      hipLaunchKernelGGL((closed_form_kernel<FROM_POSES, CLS_GJK>), dim3(w->narrow_blocks), dim3(256), 0, stream,
+                         w->dw, qin, ws->seg_len, ws->seg_start, ws->prefix, ws->cand, fl, mk, ws->sc);
+      HIP_TRY(hipGetLastError());
+    }
     if (co) {  // penetration info of the reported pairs (enable_contact)
       const size_t P = (size_t)w->dw.n_pairs;
       HIP_TRY(hipMemsetAsync(co->depth + off * P, 0, sizeof(double) * m * P, stream));
@@ -7895,7 +7913,12 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
   std::vector<int> allowed(std::max(d->n_pairs, 1), 0);
   for (int p = 0; p < d->n_pairs; ++p) allowed[p] = d->pair_allowed ? (d->pair_allowed[p] != 0) : 0;
   std::vector<int> pair_cf(std::max(d->n_pairs, 1), 0);
-  for (int p = 0; p < d->n_pairs; ++p) pair_cf[p] = closed_form_kind(d, d->pair_a[p], d->pair_b[p]);
+  for (int p = 0; p < d->n_pairs; ++p) {
+    pair_cf[p] = closed_form_kind(d, d->pair_a[p], d->pair_b[p]);
+    // GST_INDEP: the shape pairs without a closed form run FCL's own GJK
+    // (GJKSolver_indep keeps the same closed forms as GJKSolver_libccd)
+    if (d->gjk_solver == MPG_GJK_INDEP && pair_cf[p] == CF_NONE) pair_cf[p] = CF_GJK;
+  }
   // latency pair records (LR_*): one round of loads per wave instead of a
   // chain of dependent snapshot lookups (pair -> object -> link -> chain ->
   // joints -> geometry)
@@ -8286,6 +8309,7 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
     w->any_octree |= pair_cf[p] == CF_OCTREE;
     w->has_mesh |= pair_cf[p] == CF_MESH && !allowed[p];
     w->any_mesh |= pair_cf[p] == CF_MESH;
+    w->any_gjk |= pair_cf[p] == CF_GJK;
   }
   dw.static_T = to_cptr<double>(base + o_sT);
   dw.link_chain_start = to_cptr<int>(base + o_cs);
@@ -8376,7 +8400,7 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
   if (const char* e = std::getenv("MPG_SMALL_SERVER_WG")) w->srv_g = std::min(kSrvMaxG, std::max(1, std::atoi(e)));
   if (const char* e = std::getenv("MPG_SMALL_SERVER_MAX")) w->srv_max_n = std::min(kSrvN, std::max(1, std::atoi(e)));
   w->srv_lds = srv_lds_bytes(d->n_moving, d->n_pairs, d->dof, w->dw.W, d->n_joints, d->n_static);
-  w->srv_ok = lat_rec_ok && !w->any_octree && !w->any_mesh && d->dof > 0 && d->dof <= kLatScDof &&
+  w->srv_ok = lat_rec_ok && !w->any_octree && !w->any_mesh && !w->any_gjk && d->dof > 0 && d->dof <= kLatScDof &&
               d->n_pairs > 0 && w->dw.W <= kSrvMaxW && w->srv_lds <= 144 * 1024;  // + ~11 KB static LDS
   const char* own = std::getenv("MPG_OWN_STREAM");
   if (!own || std::atoi(own) != 0) HIP_TRY(hipStreamCreateWithFlags(&w->own_stream, hipStreamNonBlocking));
@@ -8750,6 +8774,9 @@ int collide_small(mpg_world* w, const double* q, int64_t n, uint8_t* flags, uint
   if (w->any_mesh)
     HIP_TRY(pick(small_kernel<FROM_POSES, CLS_MESH, 0>, small_kernel<FROM_POSES, CLS_MESH, 1>,
                  small_kernel<FROM_POSES, CLS_MESH, 2>, small_kernel<FROM_POSES, CLS_MESH, 3>));
+  if (w->any_gjk)
+    HIP_TRY(pick(small_kernel<FROM_POSES, CLS_GJK, 0>, small_kernel<FROM_POSES, CLS_GJK, 1>,
+                 small_kernel<FROM_POSES, CLS_GJK, 2>, small_kernel<FROM_POSES, CLS_GJK, 3>));
   t_small.stop();
   HIP_TRY(hipStreamSynchronize(s));
   const uint8_t* h = w->h_hits;
@@ -9314,6 +9341,8 @@ int mpg_collide_contacts(mpg_world* w, const double* input, int64_t n, int input
   if (n > 0 && ((!input && row > 0) || !flags || !pair_mask || !depth || !normal || !pos))
     return set_error(MPG_E_INVALID, "NULL buffer");
   if (mem != MPG_MEM_HOST && mem != MPG_MEM_DEVICE) return set_error(MPG_E_INVALID, "bad mem kind");
+  if (w->any_gjk)
+    return set_error(MPG_E_UNSUPPORTED, "contacts with gjk_solver MPG_GJK_INDEP (FCL's EPA) are not implemented");
   if (w->octree_first)  // contact_kernel reports the (shape, octree) order PlanningWorld uses
     return set_error(MPG_E_UNSUPPORTED, "contacts for a pair whose first object is an OcTree are not implemented");
   if (n == 0) return MPG_OK;

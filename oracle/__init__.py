@@ -167,6 +167,7 @@ class _World(ctypes.Structure):
         ("mesh_tri", _IP),
         ("conv_nbr", _IP),
         ("bvh", ctypes.c_void_p),
+        ("gjk_solver", ctypes.c_int),
     ]
 
 
@@ -200,7 +201,10 @@ class OracleWorld:
 
     def __init__(self, art: M.Articulation, scene: Sequence[Tuple[str, object, tuple]] = (),
                  attached: Sequence[Tuple[str, int, object, tuple]] = (),
-                 allowed: Sequence[Tuple[str, str]] = ()):
+                 allowed: Sequence[Tuple[str, str]] = (), gjk_solver: str = "libccd"):
+        if gjk_solver not in ("libccd", "indep"):
+            raise ValueError(gjk_solver)
+        self.gjk_solver = gjk_solver      # CollisionRequest::gjk_solver_type (GST_LIBCCD / GST_INDEP)
         self.art = art
         self.scene = list(scene)          # (name, geom, SE3)
         self.attached = list(attached)    # (name, user link index, geom, SE3 pose)
@@ -345,6 +349,7 @@ class OracleWorld:
         w.mesh_tri = ia(np.concatenate(tris) if tris else [])
         w.conv_nbr = ia(nbr_all)
         w.bvh = None
+        w.gjk_solver = 1 if getattr(self, "gjk_solver", "libccd") == "indep" else 0
         if lib().orc_bvh_build(ctypes.byref(w)):  # FCL BVHModel<OBBRSS> trees, octree nodes, shape OBBs
             raise ValueError("octree leaves off FCL's root-BV halving grid")
         self._w = w

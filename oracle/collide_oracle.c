@@ -123,6 +123,9 @@ typedef struct {
     /* FCL BVHModel<OBBRSS> trees of the mesh geometries and the OBBs FCL's
      * computeBV gives every shape (orc_bvh_build; NULL until built) */
     void *bvh;
+    /* CollisionRequest::gjk_solver_type: 0 = GST_LIBCCD (MPR), 1 = GST_INDEP
+     * (FCL's own GJK, fcl_gjk_indep.h; shape pairs only) */
+    int gjk_solver;
 } orc_world;
 
 typedef struct {
@@ -448,13 +451,11 @@ static void shape_to_gjk(const real *T, gjk_obj *o) {
     ccdQuatInvert2(&o->rot_inv, &o->rot);
 }
 
-static void support_convex(const gjk_obj *c, const ccd_vec3_t *dir_, ccd_vec3_t *v) {
-    ccd_vec3_t dir;
-    ccdVec3Copy(&dir, dir_);
-    ccdQuatRotVec(&dir, &c->rot_inv);
-    /* Convex::findExtremeVertex: argmax of dir . vertex, first maximum wins */
-    const real *p = c->verts;
-    const real dC[3] = {dir.v[0], dir.v[1], dir.v[2]}; /* Vector3<S> dir_C{S(dir.v[0]), ...} */
+/* Convex::findExtremeVertex [ext FCL 0.7.0 fcl/geometry/shape/convex-inl.h]:
+ * the index of the vertex FCL returns for direction dC (hull frame, double).
+ * Shared by libccd's supportConvex (below) and GJKSolver_indep's getSupport
+ * (fcl_gjk_indep.h). */
+static int convex_find_extreme(const real *p, int nv, const int *nbr, const real dC[3], orc_stats *stats) {
     real maxdot = -DBL_MAX;
     int best = 0;
 #ifndef ORC_FCL_LINEAR
@@ -468,18 +469,18 @@ static void support_convex(const gjk_obj *c, const ccd_vec3_t *dir_, ccd_vec3_t 
      * planes), so the climb can stop at a local maximum: a different support
      * point than the linear scan (ORC_FCL_LINEAR variant) for ~1e-4 of
      * directions. */
-    if (c->nbr && c->nv > 32) {
+    if (nbr && nv > 32) {
         unsigned char stack_vis[4096];
-        unsigned char *visited = c->nv <= 4096 ? stack_vis : (unsigned char *)malloc((size_t)c->nv);
-        memset(visited, 0, (size_t)c->nv);
+        unsigned char *visited = nv <= 4096 ? stack_vis : (unsigned char *)malloc((size_t)nv);
+        memset(visited, 0, (size_t)nv);
         maxdot = (dC[0] * p[0] + dC[1] * p[1]) + dC[2] * p[2];
         visited[0] = 1;
         int keep = 1;
         while (keep) {
             keep = 0;
-            const int start = c->nbr[best], cnt = c->nbr[start];
+            const int start = nbr[best], cnt = nbr[start];
             for (int k = start + 1; k <= start + cnt; ++k) {
-                const int vi = c->nbr[k];
+                const int vi = nbr[k];
                 if (visited[vi]) continue;
                 visited[vi] = 1;
                 real d = (dC[0] * p[3 * vi] + dC[1] * p[3 * vi + 1]) + dC[2] * p[3 * vi + 2];
@@ -487,18 +488,25 @@ static void support_convex(const gjk_obj *c, const ccd_vec3_t *dir_, ccd_vec3_t 
             }
         }
         if (visited != stack_vis) free(visited);
-        if (c->stats) c->stats->vertex_dots += c->nv;
-        ccdVec3Set(v, p[3 * best], p[3 * best + 1], p[3 * best + 2]);
-        ccdQuatRotVec(v, &c->rot);
-        ccdVec3Add(v, &c->pos);
-        return;
+        if (stats) stats->vertex_dots += nv;
+        return best;
     }
 #endif
-    for (int i = 0; i < c->nv; ++i) {
+    for (int i = 0; i < nv; ++i) {
         real dot = (dC[0] * p[3 * i] + dC[1] * p[3 * i + 1]) + dC[2] * p[3 * i + 2];
         if (dot > maxdot) { maxdot = dot; best = i; }
     }
-    if (c->stats) c->stats->vertex_dots += c->nv;
+    if (stats) stats->vertex_dots += nv;
+    return best;
+}
+
+static void support_convex(const gjk_obj *c, const ccd_vec3_t *dir_, ccd_vec3_t *v) {
+    ccd_vec3_t dir;
+    ccdVec3Copy(&dir, dir_);
+    ccdQuatRotVec(&dir, &c->rot_inv);
+    const real *p = c->verts;
+    const real dC[3] = {dir.v[0], dir.v[1], dir.v[2]}; /* Vector3<S> dir_C{S(dir.v[0]), ...} */
+    const int best = convex_find_extreme(p, c->nv, c->nbr, dC, c->stats);
     ccdVec3Set(v, p[3 * best], p[3 * best + 1], p[3 * best + 2]);
     ccdQuatRotVec(v, &c->rot);
     ccdVec3Add(v, &c->pos);
@@ -2768,6 +2776,8 @@ static int mesh_octree_contact(const orc_world *w, int gm, const real *TM, int g
     return hit;
 }
 
+#include "fcl_gjk_indep.h"
+
 /* the contact of a pair with a mesh side; -1 when neither side is a mesh */
 static int mesh_contact(const orc_world *w, int ga, const real *Ta, int gb, const real *Tb, real *depth, real *normal,
                         real *pos) {
@@ -2811,7 +2821,9 @@ static int collide_one(const orc_world *w, const real *q, uint32_t *mask, int W,
         else if (w->geom_type[gs[1]] == GEOM_OCTREE) hit = octree_intersect(w, gs[1], Ts[1], gs[0], Ts[0], st);
         else if (w->geom_type[gs[0]] == GEOM_OCTREE) hit = octree_intersect(w, gs[0], Ts[0], gs[1], Ts[1], st);
         else hit = closed_form_intersect(w, gs[0], Ts[0], gs[1], Ts[1]);
-        if (hit < 0) {
+        if (hit < 0 && w->gjk_solver == 1) {
+            hit = gjk_indep_intersect(w, gs[0], Ts[0], gs[1], Ts[1], 1e-6);
+        } else if (hit < 0) {
             for (int s = 0; s < 2; ++s) make_obj(w, gs[s], Ts[s], objs[s], st);
             hit = mpr_intersect(&a, &b, 1e-6);
         }
@@ -3328,6 +3340,9 @@ double orc_distance_pair_ex(const orc_world *w, int ga, const double *Ta, int gb
 int orc_collide_batch(const orc_world *w, const double *q, long n, uint8_t *flags, uint32_t *masks, int W,
                       int nthreads, orc_stats *stats) {
     if (w->nq_user > 64 || w->nq_pin > 64) return -1;
+    if (w->gjk_solver == 1) /* GST_INDEP: shape pairs only (the device refuses the rest too) */
+        for (int g = 0; g < w->n_geom; ++g)
+            if (w->geom_type[g] == GEOM_MESH || w->geom_type[g] == GEOM_OCTREE) return -2;
     if (nthreads < 1) nthreads = 1;
     if (nthreads > 256) nthreads = 256;
     job_t jobs[256];
@@ -3459,6 +3474,7 @@ int orc_collide_pair(const orc_world *w, int ga, const double *Ta, int gb, const
     if (w->geom_type[ga] == GEOM_OCTREE) return octree_intersect(w, ga, Ta, gb, Tb, NULL);
     const int cf = closed_form_intersect(w, ga, Ta, gb, Tb);
     if (cf >= 0) return cf;
+    if (w->gjk_solver == 1) return gjk_indep_intersect(w, ga, Ta, gb, Tb, 1e-6);
     gjk_obj a, b;
     make_obj(w, ga, Ta, &a, NULL);
     make_obj(w, gb, Tb, &b, NULL);
