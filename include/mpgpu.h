@@ -94,7 +94,8 @@ extern "C" {
 #define MPG_GEOM_CAPSULE 3  /* fcl::Capsule  : param = radius, lz            */
 #define MPG_GEOM_CYLINDER 4 /* fcl::Cylinder : param = radius, lz            */
 #define MPG_GEOM_OCTREE 5   /* fcl::OcTree   : param = first leaf, leaf count,
-                               resolution; static objects only          */
+                               resolution; static, on a link or attached
+                               (not paired with another OcTree)         */
 #define MPG_GEOM_MESH 6     /* fcl::BVHModel<OBBRSS> (non-convex mesh):
                                vertices, param = first triangle, triangle
                                count (mesh_triangle)                     */

