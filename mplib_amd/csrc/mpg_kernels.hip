@@ -677,11 +677,7 @@ __device__ __forceinline__ SE3 moving_tf_row(const DevWorld& w, const double* __
 template <bool FROM_POSES, bool USE_SC = true>
 __device__ __forceinline__ SE3 moving_tf(const DevWorld& w, const double* __restrict__ in,
                                          const double* __restrict__ sc, long long cfg, int id) {
-#ifdef MPG_SC_INLINE  // A/B (round 6): sincos recomputed by the consumers, no sc rows
-  return moving_tf_row<FROM_POSES>(w, in, nullptr, cfg, id);
-#else
   return moving_tf_row<FROM_POSES>(w, in, USE_SC ? sc + cfg * w.dof * 2 : nullptr, cfg, id);
-#endif
 }
 
 // Moving object -> FCL GJK object (shapeToGJK on link pose * offset).
@@ -1298,9 +1294,6 @@ __global__ __launch_bounds__(BLOCK) void cull_kernel(DevWorld w, const double* _
     }
   }
   if (FROM_POSES || w.dbg(9)) return;  // 9: ablation without the sincos pass
-#ifdef MPG_SC_INLINE
-  return;
-#endif
   // Exact fp64 sin/cos of every revolute move-group joint for the narrow
   // phase's chain FK (the glibc sincos restatement), only for configurations
   // with a candidate pair (about a quarter of them): compacted across the
