@@ -99,6 +99,17 @@ extern "C" {
 #define MPG_GEOM_MESH 6     /* fcl::BVHModel<OBBRSS> (non-convex mesh):
                                vertices, param = first triangle, triangle
                                count (mesh_triangle)                     */
+#define MPG_GEOM_ELLIPSOID 7 /* fcl::Ellipsoid : param = radii a, b, c
+                                (python/pybind_fcl.hpp:137-141); libccd
+                                supportEllipsoid, MPR with every partner */
+#define MPG_GEOM_CONE 8      /* fcl::Cone : param = radius, lz, apex at
+                                +lz/2 (python/pybind_fcl.hpp:95-98); libccd
+                                supportCone, MPR with every partner       */
+#define MPG_GEOM_TRIANGLE 9  /* fcl::TriangleP : vertices a, b, c (vertex
+                                count 3, python/pybind_fcl.hpp:168-175);
+                                libccd supportTriangle / centerTriangle,
+                                MPR with every shape (not paired with an
+                                OcTree or BVH mesh)                        */
 
 /*
  * World descriptor.  SE3 values are 12 doubles: a row-major 3x3 rotation

@@ -19,7 +19,7 @@ STAGES = ("cull", "bucket", "narrow")  # MPG_STAGE_* order
 
 (JOINT_RX, JOINT_RY, JOINT_RZ, JOINT_REVOLUTE_UNALIGNED, JOINT_PX, JOINT_PY, JOINT_PZ,
  JOINT_PRISMATIC_UNALIGNED, JOINT_RUBX, JOINT_RUBY, JOINT_RUBZ, JOINT_RUB_UNALIGNED) = range(12)
-GEOM_CONVEX, GEOM_BOX, GEOM_SPHERE, GEOM_CAPSULE, GEOM_CYLINDER = range(5)
+GEOM_CONVEX, GEOM_BOX, GEOM_SPHERE, GEOM_CAPSULE, GEOM_CYLINDER, GEOM_OCTREE, GEOM_MESH, GEOM_ELLIPSOID, GEOM_CONE = range(9)
 GJK_LIBCCD, GJK_INDEP = 0, 1
 
 _I32P = ctypes.POINTER(ctypes.c_int32)

@@ -6,7 +6,9 @@
 // device library cannot run, calls raise.
 #pragma once
 
+#include <algorithm>
 #include <array>
+#include <cmath>
 #include <cstdint>
 #include <functional>
 #include <map>
@@ -33,6 +35,12 @@ using Vec7 = std::array<double, 7>;  // (px, py, pz, qw, qx, qy, qz)
 struct CollisionGeometry {
   int type = -1;  // MPG_GEOM_*, or -1 for geometry the device does not support
   std::string kind;
+  // fcl::CollisionGeometry's bookkeeping (python/pybind_fcl.hpp:67-82):
+  // computeLocalAABB sets aabb_center / aabb_radius (CollisionObject's
+  // constructor calls it); cost_density against the occupancy thresholds
+  Vec3 aabb_center{0, 0, 0};
+  double aabb_radius = 0.0;
+  double cost_density = 1.0, threshold_occupied = 1.0, threshold_free = 0.0;
   virtual ~CollisionGeometry() = default;
 };
 struct Box : CollisionGeometry {
@@ -50,6 +58,48 @@ struct Capsule : CollisionGeometry {
 struct Cylinder : CollisionGeometry {
   double radius, lz;
   Cylinder(double r, double l) : radius(r), lz(l) { type = MPG_GEOM_CYLINDER; kind = "Cylinder"; }
+};
+struct Ellipsoid : CollisionGeometry {
+  Vec3 radii;
+  explicit Ellipsoid(const Vec3& r) : radii(r) { type = MPG_GEOM_ELLIPSOID; kind = "Ellipsoid"; }
+};
+struct Cone : CollisionGeometry {
+  double radius, lz;
+  Cone(double r, double l) : radius(r), lz(l) { type = MPG_GEOM_CONE; kind = "Cone"; }
+};
+struct TriangleP : CollisionGeometry {
+  Vec3 a, b, c;
+  TriangleP(const Vec3& a_, const Vec3& b_, const Vec3& c_) : a(a_), b(b_), c(c_) {
+    type = MPG_GEOM_TRIANGLE;
+    kind = "TriangleP";
+  }
+};
+// fcl::Halfspace / fcl::Plane (python/pybind_fcl.hpp:143-161): n . x <= d /
+// n . x = d, the normal made unit by the constructor (unitNormalTest).  No
+// device evaluation (type -1): the reference's own scene conversion leaves
+// them out over wrong FCL halfspace checks (mplib/sapien_utils/conversion.py:384-396)
+struct PlaneLike : CollisionGeometry {
+  Vec3 n;
+  double d;
+  PlaneLike(const Vec3& n_, double d_, const char* k) : n(n_), d(d_) {
+    kind = k;
+    const double l = std::sqrt(n[0] * n[0] + n[1] * n[1] + n[2] * n[2]);
+    if (l > 0) {
+      const double inv = 1.0 / l;
+      for (double& x : n) x *= inv;
+      d *= inv;
+    } else {
+      n = {1.0, 0.0, 0.0};
+      d = 0.0;
+    }
+  }
+  double signed_distance(const Vec3& p) const { return n[0] * p[0] + n[1] * p[1] + n[2] * p[2] - d; }
+};
+struct Halfspace : PlaneLike {
+  Halfspace(const Vec3& n_, double d_) : PlaneLike(n_, d_, "Halfspace") {}
+};
+struct Plane : PlaneLike {
+  Plane(const Vec3& n_, double d_) : PlaneLike(n_, d_, "Plane") {}
 };
 struct Convex : CollisionGeometry {
   std::vector<Vec3> vertices;
@@ -110,11 +160,27 @@ struct UnsupportedGeometry : CollisionGeometry {
 
 using GeomPtr = std::shared_ptr<CollisionGeometry>;
 
+// FCL 0.7.0's mass properties and local bounding box of a geometry
+// (geomprops.cpp): computeLocalAABB, computeVolume, computeCOM,
+// computeMomentofInertia[RelatedToCOM]
+struct LocalAABB {
+  Vec3 min, max;
+};
+LocalAABB local_aabb(const CollisionGeometry& g);
+void compute_local_aabb(CollisionGeometry& g);
+double compute_volume(const CollisionGeometry& g);
+Vec3 compute_com(const CollisionGeometry& g);
+std::array<double, 9> compute_moment_of_inertia(const CollisionGeometry& g);
+std::array<double, 9> compute_moment_of_inertia_com(const CollisionGeometry& g);
+
 struct CollisionObject {
   GeomPtr geom;
   SE3 tf;
   uint64_t version = 0;
-  CollisionObject(GeomPtr g, const SE3& t) : geom(std::move(g)), tf(t) {}
+  // fcl::CollisionObject's constructor calls cgeom->computeLocalAABB()
+  CollisionObject(GeomPtr g, const SE3& t) : geom(std::move(g)), tf(t) {
+    if (geom) compute_local_aabb(*geom);
+  }
   void set_transform(const SE3& t) {
     tf = t;
     ++version;
@@ -164,11 +230,47 @@ struct Contact {
   double penetration_depth = 0;
 };
 
+// fcl::ContactPoint / fcl::CostSource (python/pybind_fcl.hpp:340-359)
+struct ContactPoint {
+  Vec3 normal{0, 0, 0}, pos{0, 0, 0};
+  double penetration_depth = 0;
+};
+struct CostSource {
+  Vec3 aabb_min{0, 0, 0}, aabb_max{0, 0, 0};
+  double cost_density = 0, total_cost = 0;
+  // CostSource(aabb_min, aabb_max, cost_density): total_cost = density x box volume
+  CostSource() = default;
+  CostSource(const Vec3& lo, const Vec3& hi, double d) : aabb_min(lo), aabb_max(hi), cost_density(d) {
+    total_cost = d * (hi[0] - lo[0]) * (hi[1] - lo[1]) * (hi[2] - lo[2]);
+  }
+  // the std::set order of CollisionResult::cost_sources: larger total cost
+  // first, then aabb_min, aabb_max (lexicographic), cost_density
+  bool operator<(const CostSource& o) const {
+    if (total_cost != o.total_cost) return total_cost > o.total_cost;
+    if (aabb_min != o.aabb_min) return aabb_min < o.aabb_min;
+    if (aabb_max != o.aabb_max) return aabb_max < o.aabb_max;
+    return cost_density < o.cost_density;
+  }
+};
+
 struct CollisionResult {
   std::vector<Contact> contacts;
+  std::vector<CostSource> cost_sources;  // kept sorted (CostSource::operator<), no duplicates
   bool is_collision() const { return !contacts.empty(); }
   size_t num_contacts() const { return contacts.size(); }
-  void clear() { contacts.clear(); }
+  size_t num_cost_sources() const { return cost_sources.size(); }
+  void add_contact(const Contact& c) { contacts.push_back(c); }
+  // CollisionResult::addCostSource: insert into the ordered set, then drop
+  // the last entries beyond num_max
+  void add_cost_source(const CostSource& c, size_t num_max) {
+    auto it = std::lower_bound(cost_sources.begin(), cost_sources.end(), c);
+    if (it == cost_sources.end() || c < *it) cost_sources.insert(it, c);
+    while (cost_sources.size() > num_max) cost_sources.pop_back();
+  }
+  void clear() {
+    contacts.clear();
+    cost_sources.clear();
+  }
 };
 
 // ---------------------------------------------------------------------------
@@ -576,6 +678,8 @@ class PlanningWorld {
   void set_qpos(const std::string& n, const std::vector<double>& q) const;
   void set_qpos_all(const std::vector<double>& state) const;
   AcmPtr get_allowed_collision_matrix() const { return acm_; }
+  // PlanningWorldTpl::printAttachedBodyPose (src/planning_world.cpp:237-241)
+  void print_attached_body_pose() const;
 
   bool collide(const CollisionRequest& r = CollisionRequest());
   std::vector<WorldCollisionResult> self_collide(const CollisionRequest& r = CollisionRequest());

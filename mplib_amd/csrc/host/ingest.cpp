@@ -387,6 +387,17 @@ int DescBuilder::add_geometry(const CollisionGeometry* g) {
   } else if (auto cy = dynamic_cast<const Cylinder*>(g)) {
     prm[0] = cy->radius;
     prm[1] = cy->lz;
+  } else if (auto tp = dynamic_cast<const TriangleP*>(g)) {
+    vs = (int)(vertices.size() / 3);
+    nv = 3;
+    for (const Vec3* v : {&tp->a, &tp->b, &tp->c}) vertices.insert(vertices.end(), v->begin(), v->end());
+  } else if (auto co = dynamic_cast<const Cone*>(g)) {
+    prm[0] = co->radius;
+    prm[1] = co->lz;
+  } else if (auto el = dynamic_cast<const Ellipsoid*>(g)) {
+    prm[0] = el->radii[0];
+    prm[1] = el->radii[1];
+    prm[2] = el->radii[2];
   } else if (auto oc = dynamic_cast<const OcTree*>(g)) {
     prm[0] = (double)(octree_leaf.size() / 6);
     prm[1] = (double)oc->leaves.size();

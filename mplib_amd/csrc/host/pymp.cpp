@@ -49,6 +49,19 @@ py::array_t<double> mat4(const SE3& T) {  // homogeneous matrix of an Isometry3d
   return a;
 }
 
+py::array_t<double> mat33(const std::array<double, 9>& M) {
+  py::array_t<double> a({3, 3});
+  auto m = a.mutable_unchecked<2>();
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) m(i, j) = M[3 * i + j];
+  return a;
+}
+
+// fcl::Triangle: three vertex indices
+struct Triangle {
+  std::array<size_t, 3> v{0, 0, 0};
+};
+
 py::array_t<double> vec(const double* p, int n) {
   py::array_t<double> a(n);
   auto m = a.mutable_unchecked<1>();
@@ -95,8 +108,33 @@ PYBIND11_MODULE(pymp, m_all) {
 
   // ------------------------------------------------------------------ fcl
   auto m = m_all.def_submodule("fcl");
+  // fcl.Triangle (python/pybind_fcl.hpp:59-65): three vertex indices
+  py::class_<Triangle, std::shared_ptr<Triangle>>(m, "Triangle")
+      .def(py::init<>())
+      .def(py::init([](unsigned long a, unsigned long b, unsigned long c) { return Triangle{{a, b, c}}; }))
+      .def("set", [](Triangle& t, int a, int b, int c) { t.v = {(size_t)a, (size_t)b, (size_t)c}; })
+      .def("get", [](const Triangle& t, int i) { return t.v.at(i); })
+      .def("__getitem__", [](const Triangle& t, int i) { return t.v.at(i); });
+
+  // fcl.CollisionGeometry (python/pybind_fcl.hpp:68-82); the methods are
+  // FCL 0.7.0's, restated in geomprops.cpp
   py::class_<CollisionGeometry, std::shared_ptr<CollisionGeometry>>(m, "CollisionGeometry")
-      .def_readonly("kind", &CollisionGeometry::kind);
+      .def_readonly("kind", &CollisionGeometry::kind)
+      .def("computeLocalAABB", [](CollisionGeometry& g) { compute_local_aabb(g); })
+      .def("isOccupied", [](const CollisionGeometry& g) { return g.cost_density >= g.threshold_occupied; })
+      .def("isFree", [](const CollisionGeometry& g) { return g.cost_density <= g.threshold_free; })
+      .def("isUncertain",
+           [](const CollisionGeometry& g) {
+             return !(g.cost_density >= g.threshold_occupied) && !(g.cost_density <= g.threshold_free);
+           })
+      .def("computeCOM", [](const CollisionGeometry& g) { return compute_com(g); })
+      .def("computeMomentofInertia", [](const CollisionGeometry& g) { return mat33(compute_moment_of_inertia(g)); })
+      .def("computeVolume", [](const CollisionGeometry& g) { return compute_volume(g); })
+      .def("computeMomentofInertiaRelatedToCOM",
+           [](const CollisionGeometry& g) { return mat33(compute_moment_of_inertia_com(g)); })
+      .def_readwrite("aabb_center", &CollisionGeometry::aabb_center)
+      .def_readwrite("aabb_radius", &CollisionGeometry::aabb_radius)
+      .def_readwrite("cost_density", &CollisionGeometry::cost_density);
   py::class_<Box, CollisionGeometry, std::shared_ptr<Box>>(m, "Box")
       .def(py::init([](const std::vector<double>& s) { return std::make_shared<Box>(vec3_arg(s)); }), py::arg("side"))
       .def(py::init([](double x, double y, double z) { return std::make_shared<Box>(Vec3{x, y, z}); }), py::arg("x"),
@@ -113,6 +151,42 @@ PYBIND11_MODULE(pymp, m_all) {
       .def(py::init<double, double>(), py::arg("radius"), py::arg("lz"))
       .def_readwrite("radius", &Cylinder::radius)
       .def_readwrite("lz", &Cylinder::lz);
+  py::class_<Cone, CollisionGeometry, std::shared_ptr<Cone>>(m, "Cone")
+      .def(py::init<double, double>(), py::arg("radius"), py::arg("lz"))
+      .def_readwrite("radius", &Cone::radius)
+      .def_readwrite("lz", &Cone::lz);
+  py::class_<Ellipsoid, CollisionGeometry, std::shared_ptr<Ellipsoid>>(m, "Ellipsoid")
+      .def(py::init([](double a, double b, double c) { return std::make_shared<Ellipsoid>(Vec3{a, b, c}); }),
+           py::arg("a"), py::arg("b"), py::arg("c"))
+      .def(py::init([](const std::vector<double>& r) { return std::make_shared<Ellipsoid>(vec3_arg(r)); }),
+           py::arg("radii"))
+      .def_readwrite("radii", &Ellipsoid::radii);
+  py::class_<TriangleP, CollisionGeometry, std::shared_ptr<TriangleP>>(m, "TriangleP")
+      .def(py::init([](const std::vector<double>& a, const std::vector<double>& b, const std::vector<double>& c) {
+             return std::make_shared<TriangleP>(vec3_arg(a), vec3_arg(b), vec3_arg(c));
+           }),
+           py::arg("a"), py::arg("b"), py::arg("c"))
+      .def_readwrite("a", &TriangleP::a)
+      .def_readwrite("b", &TriangleP::b)
+      .def_readwrite("c", &TriangleP::c);
+  // Halfspace / Plane: the types and their geometry; colliding them raises
+  // NotImplementedError (host.hpp PlaneLike)
+  auto plane_like = [&](auto cls) {
+    using T = typename decltype(cls)::type;
+    cls.def(py::init([](const std::vector<double>& n, double d) { return std::make_shared<T>(vec3_arg(n), d); }),
+            py::arg("n"), py::arg("d"))
+        .def(py::init([](double a, double b, double c, double d) { return std::make_shared<T>(Vec3{a, b, c}, d); }),
+             py::arg("a"), py::arg("b"), py::arg("c"), py::arg("d"))
+        .def_readwrite("n", &T::n)
+        .def_readwrite("d", &T::d)
+        .def("signed_distance", [](const T& h, const std::vector<double>& p) { return h.signed_distance(vec3_arg(p)); },
+             py::arg("p"))
+        .def("distance",
+             [](const T& h, const std::vector<double>& p) { return std::fabs(h.signed_distance(vec3_arg(p))); },
+             py::arg("p"));
+  };
+  plane_like(py::class_<Halfspace, CollisionGeometry, std::shared_ptr<Halfspace>>(m, "Halfspace"));
+  plane_like(py::class_<Plane, CollisionGeometry, std::shared_ptr<Plane>>(m, "Plane"));
   py::class_<Convex, CollisionGeometry, std::shared_ptr<Convex>>(m, "Convex")
       .def(py::init([](py::array_t<double, py::array::c_style | py::array::forcecast> v,
                        py::array_t<int, py::array::c_style | py::array::forcecast> f, bool throw_if_invalid) {
@@ -144,6 +218,7 @@ PYBIND11_MODULE(pymp, m_all) {
                for (int k = 0; k < 3; ++k) x(i, k) = c.vertices[i][k];
              return a;
            })
+      .def("compute_volume", [](const Convex& c) { return compute_volume(c); })
       .def("get_interior_point", [](const Convex& c) {
         auto p = c.interior_point();
         return vec(p.data(), 3);
@@ -181,6 +256,13 @@ PYBIND11_MODULE(pymp, m_all) {
       .def(
           "addSubModel", [=](BVHModel& b, py::array_t<double> v) { b.add_sub_model(vert_arg(v), {}); },
           py::arg("vertices"))
+      .def(
+          "addSubModel", [=](BVHModel& b, py::array_t<double> v, const std::vector<Triangle>& f) {
+            std::vector<std::array<int, 3>> t;
+            for (auto& x : f) t.push_back({(int)x.v[0], (int)x.v[1], (int)x.v[2]});
+            b.add_sub_model(vert_arg(v), t);
+          },
+          py::arg("vertices"), py::arg("faces"))
       .def(
           "addSubModel", [=](BVHModel& b, py::array_t<double> v, py::array_t<int> f) {
             b.add_sub_model(vert_arg(v), tri_arg(f));
@@ -270,9 +352,52 @@ PYBIND11_MODULE(pymp, m_all) {
 
   py::class_<Contact, std::shared_ptr<Contact>>(m, "Contact")
       .def(py::init<>())
+      .def(py::init([](const GeomPtr& o1, const GeomPtr& o2, int b1, int b2) {
+             Contact c;
+             c.o1 = o1;
+             c.o2 = o2;
+             c.b1 = b1;
+             c.b2 = b2;
+             return c;
+           }),
+           py::arg("o1"), py::arg("o2"), py::arg("b1"), py::arg("b2"))
+      .def(py::init([](const GeomPtr& o1, const GeomPtr& o2, int b1, int b2, const std::vector<double>& pos,
+                       const std::vector<double>& normal, double depth) {
+             Contact c;
+             c.o1 = o1;
+             c.o2 = o2;
+             c.b1 = b1;
+             c.b2 = b2;
+             c.pos = vec3_arg(pos);
+             c.normal = vec3_arg(normal);
+             c.penetration_depth = depth;
+             return c;
+           }),
+           py::arg("o1"), py::arg("o2"), py::arg("b1"), py::arg("b2"), py::arg("pos"), py::arg("normal"),
+           py::arg("depth"))
       .def_readonly("normal", &Contact::normal)
       .def_readonly("pos", &Contact::pos)
       .def_readonly("penetration_depth", &Contact::penetration_depth);
+
+  py::class_<ContactPoint, std::shared_ptr<ContactPoint>>(m, "ContactPoint")
+      .def(py::init<>())
+      .def(py::init([](const std::vector<double>& normal, const std::vector<double>& pos, double depth) {
+             return ContactPoint{vec3_arg(normal), vec3_arg(pos), depth};
+           }),
+           py::arg("normal"), py::arg("pos"), py::arg("penetration_depth"))
+      .def_readonly("normal", &ContactPoint::normal)
+      .def_readonly("pos", &ContactPoint::pos)
+      .def_readonly("penetration_depth", &ContactPoint::penetration_depth);
+  py::class_<CostSource, std::shared_ptr<CostSource>>(m, "CostSource")
+      .def(py::init<>())
+      .def(py::init([](const std::vector<double>& lo, const std::vector<double>& hi, double d) {
+             return CostSource(vec3_arg(lo), vec3_arg(hi), d);
+           }),
+           py::arg("aabb_min"), py::arg("aabb_max"), py::arg("cost_density"))
+      .def_readonly("aabb_min", &CostSource::aabb_min)
+      .def_readonly("aabb_max", &CostSource::aabb_max)
+      .def_readonly("cost_density", &CostSource::cost_density)
+      .def_readonly("total_cost", &CostSource::total_cost);
 
   py::class_<DistanceRequest, std::shared_ptr<DistanceRequest>>(m, "DistanceRequest")
       .def(py::init([](bool np_, bool sd, double rel, double abs_, double tol, GJKSolverType t) {
@@ -302,6 +427,10 @@ PYBIND11_MODULE(pymp, m_all) {
 
   py::class_<CollisionResult, std::shared_ptr<CollisionResult>>(m, "CollisionResult")
       .def(py::init<>())
+      .def("add_contact", &CollisionResult::add_contact, py::arg("c"))
+      .def("add_cost_source", &CollisionResult::add_cost_source, py::arg("c"), py::arg("num_max_cost_sources"))
+      .def("num_cost_sources", &CollisionResult::num_cost_sources)
+      .def("get_cost_sources", [](const CollisionResult& r) { return r.cost_sources; })
       .def("is_collision", &CollisionResult::is_collision)
       .def("num_contacts", &CollisionResult::num_contacts)
       .def("get_contacts", [](const CollisionResult& r) { return r.contacts; })
@@ -424,6 +553,106 @@ PYBIND11_MODULE(pymp, m_all) {
         return r;
       },
       py::arg("o1"), py::arg("o2"), py::arg("request") = DistanceRequest());
+
+  // fcl.collide / fcl.distance(articulation, o2, request)
+  // (python/pybind_fcl.hpp:371-436): every collision object of the
+  // articulation's FCLModel (at its current poses) against o2, as one device
+  // world -- the objects ride on one identity link pose, o2 is static
+  auto art_world = [](const ArtPtr& art, const ObjPtr& o2, DescBuilder& d) {
+    const auto& objs = art->get_fcl_model()->get_collision_objects();
+    d.link_parent.push_back(0);
+    SE3 I;
+    mpg::se3_identity(I);
+    push_se3(d.link_placement, I);
+    for (auto& o : objs) {
+      d.moving_link.push_back(0);
+      d.moving_geom.push_back(d.add_geometry(o->geom.get()));
+      push_se3(d.moving_offset, o->tf);
+    }
+    d.static_geom.push_back(d.add_geometry(o2->geom.get()));
+    push_se3(d.static_transform, o2->tf);
+    for (size_t i = 0; i < objs.size(); ++i) {
+      d.pair_a.push_back((int)i);
+      d.pair_b.push_back((int)objs.size());
+      d.pair_allowed.push_back(0);
+    }
+    return objs.size();
+  };
+  m.def(
+      "collide",
+      [=](const ArtPtr& art, const ObjPtr& o2, const CollisionRequest& req) {
+        req.check_supported();
+        DescBuilder d;
+        d.gjk_tolerance = req.gjk_tolerance;
+        d.gjk_solver = req.gjk_solver_type == GST_INDEP ? MPG_GJK_INDEP : MPG_GJK_LIBCCD;
+        const size_t n = art_world(art, o2, d);
+        std::vector<WorldCollisionResult> ret;
+        if (n == 0) return ret;
+        DeviceWorld w(d, default_device());
+        const double pose[7] = {0, 0, 0, 1, 0, 0, 0};
+        uint8_t flag = 0;
+        std::vector<uint32_t> mask((n + 31) / 32, 0);
+        std::vector<double> depth(n, 0.0), normal(3 * n, 0.0), pos(3 * n, 0.0);
+        if (req.enable_contact)
+          check_status(mpg_collide_contacts(w.get(), pose, 1, MPG_INPUT_LINK_POSES, &flag, mask.data(), depth.data(),
+                                            normal.data(), pos.data(), MPG_MEM_HOST, nullptr),
+                       "mpg_collide_contacts");
+        else
+          check_status(mpg_collide_link_poses(w.get(), pose, 1, &flag, mask.data(), MPG_MEM_HOST, nullptr),
+                       "mpg_collide_link_poses");
+        const auto& objs = art->get_fcl_model()->get_collision_objects();
+        const auto& names = art->get_fcl_model()->get_collision_link_names();
+        for (size_t i = 0; i < n; ++i) {
+          if (!((mask[i >> 5] >> (i & 31)) & 1u)) continue;
+          WorldCollisionResult r;
+          Contact c;
+          c.o1 = objs[i]->geom;
+          c.o2 = o2->geom;
+          if (req.enable_contact) fill_contacts(mask.data(), n, depth, normal, pos, i, c);
+          r.res.contacts.push_back(c);
+          r.collision_type = "articulation_sceneobject";
+          r.object_name1 = art->get_name();
+          r.object_name2 = "__object__";
+          r.link_name1 = names[i];
+          r.link_name2 = "__object__";
+          ret.push_back(std::move(r));
+        }
+        return ret;
+      },
+      py::arg("articulation"), py::arg("o2"), py::arg("request") = CollisionRequest());
+  m.def(
+      "distance",
+      [=](const ArtPtr& art, const ObjPtr& o2, const DistanceRequest& req) {
+        req.check_supported();
+        DescBuilder d;
+        const size_t n = art_world(art, o2, d);
+        WorldDistanceResult ret;
+        if (n == 0) return ret;
+        DeviceWorld w(d, default_device());
+        // the pairs are the world's "others" group: minimum and first argmin
+        // (FCL's loop keeps the first strictly smaller distance)
+        double ds = 0, dd = 0, qs[6], qo[6];
+        int32_t ps = -1, po = -1;
+        const mpg_distance_request creq = req.to_c();
+        check_status(mpg_distance_batch_req(w.get(), nullptr, 1, 0, &creq, &ds, &ps, qs, &dd, &po, qo, MPG_MEM_HOST,
+                                            nullptr),
+                     "mpg_distance_batch_req");
+        if (po < 0) return ret;
+        const auto& names = art->get_fcl_model()->get_collision_link_names();
+        ret.res.min_distance = dd;
+        for (int k = 0; k < 3; ++k) {
+          ret.res.nearest_points[0][k] = qo[k];
+          ret.res.nearest_points[1][k] = qo[3 + k];
+        }
+        ret.min_distance = dd;
+        ret.distance_type = "articulation_sceneobject";
+        ret.object_name1 = art->get_name();
+        ret.object_name2 = "__object__";
+        ret.link_name1 = names[po];
+        ret.link_name2 = "__object__";
+        return ret;
+      },
+      py::arg("articulation"), py::arg("o2"), py::arg("request") = DistanceRequest());
 
   // ------------------------------------------------------------ pinocchio
   auto mp = m_all.def_submodule("pinocchio");
@@ -620,6 +849,7 @@ PYBIND11_MODULE(pymp, m_all) {
       .def("remove_articulation", &PW::remove_articulation, py::arg("name"))
       .def("is_articulation_planned", &PW::is_articulation_planned, py::arg("name"))
       .def("set_articulation_planned", &PW::set_articulation_planned, py::arg("name"), py::arg("planned"))
+      .def("print_attached_body_pose", &PW::print_attached_body_pose)
       .def("get_normal_object_names", &PW::get_normal_object_names)
       .def("get_normal_object", &PW::get_normal_object, py::arg("name"))
       .def("has_normal_object", &PW::has_normal_object, py::arg("name"))

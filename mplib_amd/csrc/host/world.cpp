@@ -12,6 +12,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <iostream>
 #include <set>
 #include <sstream>
 
@@ -229,6 +230,39 @@ bool PlanningWorld::remove_normal_object(const std::string& n) {
 }
 SE3 AttachedBody::global_pose() const {
   return mpg::se3_mul(se3_from_pose7(articulation->get_pinocchio_model()->get_link_pose(link_id)), pose);
+}
+
+// Eigen's operator<< for a matrix: the stream's precision, every coefficient
+// right-aligned to the widest one, " " between columns, "\n" between rows
+void PlanningWorld::print_attached_body_pose() const {
+  for (const auto& [name, body] : attached_) {
+    const SE3 T = body->global_pose();
+    double M[16];
+    for (int i = 0; i < 3; ++i) {
+      for (int j = 0; j < 3; ++j) M[4 * i + j] = T.R[3 * i + j];
+      M[4 * i + 3] = T.p[i];
+    }
+    M[12] = M[13] = M[14] = 0.0;
+    M[15] = 1.0;
+    std::string cell[16];
+    size_t width = 0;
+    for (int k = 0; k < 16; ++k) {
+      std::ostringstream o;
+      o << M[k];
+      cell[k] = o.str();
+      width = std::max(width, cell[k].size());
+    }
+    std::ostringstream out;
+    out << name << " global pose:\n";
+    for (int i = 0; i < 4; ++i) {
+      for (int j = 0; j < 4; ++j) {
+        if (j) out << ' ';
+        out << std::string(width - cell[4 * i + j].size(), ' ') << cell[4 * i + j];
+      }
+      if (i < 3) out << '\n';
+    }
+    std::cout << out.str() << std::endl;
+  }
 }
 
 AttachedPtr PlanningWorld::get_attached_object(const std::string& n) const {

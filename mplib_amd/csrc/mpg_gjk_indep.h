@@ -134,6 +134,13 @@ __device__ Proj tetrahedron(const V3& a, const V3& b, const V3& c, const V3& d) 
 __device__ __forceinline__ V3 shape_support(const DevWorld& w, cptr<double> HV, int geom, int type, const V3& d) {
   const cptr<double> prm = w.geom_rec + G_STRIDE * geom + G_PARAM;
   if (type == MPG_GEOM_CONVEX) return convex_support_local(w, HV, geom, d);
+  if (type == MPG_GEOM_TRIANGLE) {  // the first of the larger dot products a / b / c
+    const cptr<double> G = HV + 12 * (size_t)w.geom_gstart[geom];
+    const V3 a = v3(G[0], G[4], G[8]), b = v3(G[1], G[5], G[9]), c = v3(G[2], G[6], G[10]);
+    const double dota = vdot(d, a), dotb = vdot(d, b), dotc = vdot(d, c);
+    if (dota > dotb) return dotc > dota ? c : a;
+    return dotc > dotb ? c : b;
+  }
   if (type == MPG_GEOM_BOX)
     return v3((d.x > 0) ? (prm[0] / 2) : (-prm[0] / 2), (d.y > 0) ? (prm[1] / 2) : (-prm[1] / 2),
               (d.z > 0) ? (prm[2] / 2) : (-prm[2] / 2));
@@ -143,6 +150,25 @@ __device__ __forceinline__ V3 shape_support(const DevWorld& w, cptr<double> HV, 
     const V3 v = vscale(d, prm[0]);
     const V3 pos1 = vadd(v3(0, 0, half_h), v), pos2 = vadd(v3(0, 0, -half_h), v);
     return vdot(d, pos1) > vdot(d, pos2) ? pos1 : pos2;
+  }
+  if (type == MPG_GEOM_CONE) {
+    double zdist = d.x * d.x + d.y * d.y;
+    double len = zdist + d.z * d.z;
+    zdist = std::sqrt(zdist);
+    len = std::sqrt(len);
+    const double radius = prm[0];
+    const double sin_a = radius / std::sqrt(radius * radius + 4 * half_h * half_h);
+    if (d.z > len * sin_a) return v3(0, 0, half_h);
+    if (zdist > 0) {
+      const double rad = radius / zdist;
+      return v3(rad * d.x, rad * d.y, -half_h);
+    }
+    return v3(0, 0, -half_h);
+  }
+  if (type == MPG_GEOM_ELLIPSOID) {  // v / sqrt(v . d), one division per coefficient (Eigen's quotient)
+    const V3 v = v3(prm[0] * prm[0] * d.x, prm[1] * prm[1] * d.y, prm[2] * prm[2] * d.z);
+    const double dd = std::sqrt(vdot(v, d));
+    return v3(v.x / dd, v.y / dd, v.z / dd);
   }
   // cylinder
   const double zdist = std::sqrt(d.x * d.x + d.y * d.y);

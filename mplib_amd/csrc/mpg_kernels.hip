@@ -512,6 +512,38 @@ __device__ __forceinline__ CV3 support_local(const DevWorld& w, cptr<double> HV,
     p1 = vadd(p1, n);
     p2 = vadd(p2, n);
     v = dir.z > 0 ? p1 : p2;
+  } else if (type == MPG_GEOM_CONE) {  // supportCone (coneToGJK: height = lz / 2)
+    const ccd_real r = (ccd_real)rec[G_PARAM], h = (ccd_real)(rec[G_PARAM + 1] / 2.0);
+    ccd_real zdist = dir.x * dir.x + dir.y * dir.y;
+    ccd_real len = zdist + dir.z * dir.z;
+    zdist = std::sqrt(zdist);
+    len = std::sqrt(len);
+    const ccd_real sin_a = r / std::sqrt(r * r + 4 * h * h);
+    if (dir.z > len * sin_a) {
+      v = CV3{0, 0, h};
+    } else if (zdist > 0) {
+      const ccd_real rad = r / zdist;
+      v = CV3{rad * dir.x, rad * dir.y, -h};
+    } else {
+      v = CV3{0, 0, -h};
+    }
+  } else if (type == MPG_GEOM_TRIANGLE) {  // supportTriangle: first maximum of dir . (p - c), ccd_real
+    const cptr<double> G = HV + 12 * (size_t)w.geom_gstart[geom];
+    const CV3 c = cv3(rec[G_INTERIOR], rec[G_INTERIOR + 1], rec[G_INTERIOR + 2]);
+    ccd_real maxdot = -FLT_MAX;
+    v = cv3(G[0], G[4], G[8]);
+    for (int i = 0; i < 3; ++i) {
+      const CV3 p = cv3(G[i], G[4 + i], G[8 + i]);
+      const ccd_real dot = vdot(dir, vsub(p, c));
+      if (dot > maxdot) {
+        v = p;
+        maxdot = dot;
+      }
+    }
+  } else if (type == MPG_GEOM_ELLIPSOID) {  // supportEllipsoid
+    const ccd_real a = (ccd_real)rec[G_PARAM], b = (ccd_real)rec[G_PARAM + 1], c = (ccd_real)rec[G_PARAM + 2];
+    const CV3 p = CV3{(a * a) * dir.x, (b * b) * dir.y, (c * c) * dir.z};
+    v = vscale(p, ccd_real(1) / std::sqrt(vdot(p, dir)));
   } else {  // cylinder
     const ccd_real r = (ccd_real)rec[G_PARAM], h = (ccd_real)(rec[G_PARAM + 1] / 2.0);
     ccd_real zdist = dir.x * dir.x + dir.y * dir.y;
@@ -533,13 +565,24 @@ __device__ __forceinline__ CV3 support_local(const DevWorld& w, cptr<double> HV,
 // tests only, never an output bit.
 __device__ __forceinline__ V3 support_local_exact(const DevWorld& w, cptr<double> HV, int geom, int type, const V3& dir) {
   const cptr<double> rec = w.geom_rec + G_STRIDE * geom;
-  if (type == MPG_GEOM_CONVEX) return convex_full_scan(w, HV, geom, dir);
+  if (type == MPG_GEOM_CONVEX || type == MPG_GEOM_TRIANGLE) return convex_full_scan(w, HV, geom, dir);
   if (type == MPG_GEOM_BOX)
     return v3((dir.x >= 0 ? 1.0 : -1.0) * rec[G_PARAM] / 2.0, (dir.y >= 0 ? 1.0 : -1.0) * rec[G_PARAM + 1] / 2.0,
               (dir.z >= 0 ? 1.0 : -1.0) * rec[G_PARAM + 2] / 2.0);
   if (type == MPG_GEOM_SPHERE) return vscale(vscale(dir, rec[G_PARAM]), 1.0 / std::sqrt(vdot(dir, dir)));
+  if (type == MPG_GEOM_ELLIPSOID) {
+    const V3 p = v3(rec[G_PARAM] * rec[G_PARAM] * dir.x, rec[G_PARAM + 1] * rec[G_PARAM + 1] * dir.y,
+                    rec[G_PARAM + 2] * rec[G_PARAM + 2] * dir.z);
+    return vscale(p, 1.0 / std::sqrt(vdot(p, dir)));
+  }
   const double r = rec[G_PARAM], h = rec[G_PARAM + 1] / 2.0;
   if (type == MPG_GEOM_CAPSULE) return vadd(v3(0.0, 0.0, dir.z > 0 ? h : -h), vscale(vnormalize(dir), r));
+  if (type == MPG_GEOM_CONE) {  // the better of the apex and the base rim point along dir
+    const double zd = std::sqrt(dir.x * dir.x + dir.y * dir.y);
+    const double rad = zd > 0.0 ? r / zd : 0.0;
+    const V3 rim = v3(rad * dir.x, rad * dir.y, -h);
+    return dir.z * h > vdot(dir, rim) ? v3(0.0, 0.0, h) : rim;
+  }
   const double zd = std::sqrt(dir.x * dir.x + dir.y * dir.y);  // cylinder
   const double rad = zd > 0.0 ? r / zd : 0.0;
   return v3(rad * dir.x, rad * dir.y, (dir.z > 0 ? 1.0 : -1.0) * h);
@@ -558,7 +601,8 @@ __device__ __forceinline__ CV3 support(const DevWorld& w, cptr<double> HV, const
 // centerConvex (interior point ccdVec3Set, rotated, translated) / centerShape
 template <bool UNI = true>
 __device__ __forceinline__ CV3 center(const DevWorld& w, const GObj& o) {
-  if ((UNI ? __builtin_amdgcn_readfirstlane(o.type) : o.type) == MPG_GEOM_CONVEX) {
+  const int t = UNI ? __builtin_amdgcn_readfirstlane(o.type) : o.type;
+  if (t == MPG_GEOM_CONVEX || t == MPG_GEOM_TRIANGLE) {  // centerConvex / centerTriangle
     const cptr<double> rec = w.geom_rec + G_STRIDE * (UNI ? __builtin_amdgcn_readfirstlane(o.geom) : o.geom);
     return vadd(quat_rot(cv3(rec[G_INTERIOR], rec[G_INTERIOR + 1], rec[G_INTERIOR + 2]), o.rot), o.pos);
   }
@@ -6803,7 +6847,17 @@ int validate(const mpg_world_desc* d) {
     if (d->link_parent[l] < 0 || d->link_parent[l] > d->n_joints) return set_error(MPG_E_INVALID, "bad link_parent");
   for (int g = 0; g < d->n_geoms; ++g) {
     const int t = d->geom_type[g];
-    if (t < MPG_GEOM_CONVEX || t > MPG_GEOM_MESH) return set_error(MPG_E_UNSUPPORTED, "unsupported geometry type");
+    if (t < MPG_GEOM_CONVEX || t > MPG_GEOM_TRIANGLE) return set_error(MPG_E_UNSUPPORTED, "unsupported geometry type");
+    if (t == MPG_GEOM_TRIANGLE && (d->geom_vertex_count[g] != 3 || d->geom_vertex_start[g] < 0 ||
+                                   (int64_t)d->geom_vertex_start[g] + 3 > d->n_vertices))
+      return set_error(MPG_E_INVALID, "a TriangleP needs 3 vertices inside the vertex array");
+    if (t == MPG_GEOM_ELLIPSOID || t == MPG_GEOM_CONE) {
+      const double* p = d->geom_param + 4 * g;
+      const int np = t == MPG_GEOM_ELLIPSOID ? 3 : 2;
+      for (int k = 0; k < np; ++k)
+        if (!(p[k] > 0.0 && std::isfinite(p[k])))
+          return set_error(MPG_E_INVALID, "ellipsoid radii / cone radius and lz must be positive and finite");
+    }
     if (t == MPG_GEOM_CONVEX || t == MPG_GEOM_MESH) {
       if (d->geom_vertex_count[g] <= 0 || d->geom_vertex_start[g] < 0 ||
           (int64_t)d->geom_vertex_start[g] + d->geom_vertex_count[g] > d->n_vertices)
@@ -6870,6 +6924,12 @@ int validate(const mpg_world_desc* d) {
     // FCL 0.7.0 GJKSolver_libccd: box-box, sphere-sphere, sphere-box,
     // sphere-capsule and sphere-cylinder have closed forms (all on the
     // device, closed_form_kind); every other shape pair is MPR
+    if (!(d->pair_allowed && d->pair_allowed[p])) {
+      const int ta = obj_geom_type(d, a), tb = obj_geom_type(d, b);
+      const bool tri = ta == MPG_GEOM_TRIANGLE || tb == MPG_GEOM_TRIANGLE;
+      if (tri && (ta == MPG_GEOM_MESH || tb == MPG_GEOM_MESH || ta == MPG_GEOM_OCTREE || tb == MPG_GEOM_OCTREE))
+        return set_error(MPG_E_UNSUPPORTED, "a TriangleP paired with an OcTree or BVH mesh is not implemented");
+    }
     if (d->gjk_solver == MPG_GJK_INDEP && !(d->pair_allowed && d->pair_allowed[p])) {
       const int ta = obj_geom_type(d, a), tb = obj_geom_type(d, b);
       if (ta == MPG_GEOM_MESH || tb == MPG_GEOM_MESH || ta == MPG_GEOM_OCTREE || tb == MPG_GEOM_OCTREE)
@@ -6917,6 +6977,18 @@ void geom_record(const mpg_world_desc* d, int g, double* rec) {
       hi[k] = d->geom_param[4 * g];
       lo[k] = -hi[k];
     }
+  } else if (t == MPG_GEOM_TRIANGLE) {  // triCreateGJKObject: centre ((a + b) + c) / 3
+    const double* V = d->vertices + 3 * (size_t)d->geom_vertex_start[g];
+    for (int k = 0; k < 3; ++k) {
+      rec[G_INTERIOR + k] = (V[k] + V[3 + k] + V[6 + k]) / 3;
+      lo[k] = std::min(V[k], std::min(V[3 + k], V[6 + k]));
+      hi[k] = std::max(V[k], std::max(V[3 + k], V[6 + k]));
+    }
+  } else if (t == MPG_GEOM_ELLIPSOID) {
+    for (int k = 0; k < 3; ++k) {
+      hi[k] = d->geom_param[4 * g + k];
+      lo[k] = -hi[k];
+    }
   } else if (t == MPG_GEOM_OCTREE) {  // union of the occupied leaf boxes (octree frame)
     const int64_t l0 = (int64_t)d->geom_param[4 * g], ln = (int64_t)d->geom_param[4 * g + 1];
     for (int k = 0; k < 3; ++k) {
@@ -6928,7 +7000,7 @@ void geom_record(const mpg_world_desc* d, int g, double* rec) {
         lo[k] = std::min(lo[k], d->octree_leaf[6 * i + k]);
         hi[k] = std::max(hi[k], d->octree_leaf[6 * i + 3 + k]);
       }
-  } else {  // capsule / cylinder along z
+  } else {  // capsule / cylinder / cone along z
     const double r = d->geom_param[4 * g], hz = d->geom_param[4 * g + 1] / 2.0 + (t == MPG_GEOM_CAPSULE ? r : 0.0);
     lo[0] = lo[1] = -r;
     hi[0] = hi[1] = r;
@@ -6945,7 +7017,7 @@ void geom_record(const mpg_world_desc* d, int g, double* rec) {
     rec[G_AABB_E + k] = (hi[k] - lo[k]) * 0.5;
     r2 += rec[G_OBB_E + k] * rec[G_OBB_E + k];
   }
-  if (t == MPG_GEOM_CONVEX || t == MPG_GEOM_MESH) {  // bounding sphere about the box centre: farthest vertex
+  if (t == MPG_GEOM_CONVEX || t == MPG_GEOM_MESH || t == MPG_GEOM_TRIANGLE) {  // bounding sphere about the box centre: farthest vertex
     const double* V = d->vertices + 3 * (size_t)d->geom_vertex_start[g];
     r2 = 0.0;
     for (int i = 0; i < d->geom_vertex_count[g]; ++i) {
@@ -7146,7 +7218,8 @@ void fcl_bvh_node(FclBvh& B, const double* V, const int32_t* tri, std::vector<in
 }
 
 // computeBV<OBB>(shape, identity): box I / side/2; sphere I / r; capsule
-// I / (r, r, lz/2 + r); cylinder I / (r, r, lz/2); convex: fitn over the
+// I / (r, r, lz/2 + r); cylinder and cone I / (r, r, lz/2); ellipsoid I /
+// radii; convex: fitn over the
 // vertices (covariance of the points)
 void fcl_shape_obb(const mpg_world_desc* d, int g, double* o) {
   std::fill(o, o + FB_STRIDE, 0.0);
@@ -7164,8 +7237,12 @@ void fcl_shape_obb(const mpg_world_desc* d, int g, double* o) {
       o[FB_EXT + 2] = p[1] / 2 + p[0];
       break;
     case MPG_GEOM_CYLINDER:
+    case MPG_GEOM_CONE:
       o[FB_EXT] = o[FB_EXT + 1] = p[0];
       o[FB_EXT + 2] = p[1] / 2;
+      break;
+    case MPG_GEOM_ELLIPSOID:
+      for (int k = 0; k < 3; ++k) o[FB_EXT + k] = p[k];
       break;
     case MPG_GEOM_CONVEX: {
       const double* V = d->vertices + 3 * (size_t)d->geom_vertex_start[g];
@@ -7749,6 +7826,14 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
           const int i = 4 * q + l < nv ? 4 * q + l : 0;
           hull.push_back(V[3 * i + k]);
         }
+  }
+  for (int g = 0; g < d->n_geoms; ++g) {  // TriangleP: its three vertices as one group (supportTriangle reads them)
+    if (d->geom_type[g] != MPG_GEOM_TRIANGLE) continue;
+    const double* V = d->vertices + 3 * (size_t)d->geom_vertex_start[g];
+    gstart[g] = (int)(hull.size() / 12);
+    ngroups[g] = 1;
+    for (int k = 0; k < 3; ++k)
+      for (int l = 0; l < 4; ++l) hull.push_back(V[3 * (l < 3 ? l : 0) + k]);
   }
   if (hull.empty()) hull.assign(12, 0.0);
   if (cell_rec.empty()) cell_rec.assign(kCellRec, 0.0);

@@ -269,8 +269,23 @@ class OracleWorld:
                 ginterior += [0.0] * 3
                 leaves.append(np.asarray(g.leaves, dtype=np.float64).reshape(-1))
                 nleaves += len(g.leaves)
-            elif isinstance(g, (M.CapsuleGeom, M.CylinderGeom)):
-                gtype.append(M.GEOM_CAPSULE if isinstance(g, M.CapsuleGeom) else M.GEOM_CYLINDER)
+            elif isinstance(g, M.TrianglePGeom):
+                gtype.append(M.GEOM_TRIANGLE_P)
+                gvstart.append(nverts)
+                gnv.append(3)
+                nverts += 3
+                verts.append(g.vertices.reshape(-1))
+                gparam += [0.0] * 4
+                ginterior += [0.0] * 3
+            elif isinstance(g, M.EllipsoidGeom):
+                gtype.append(M.GEOM_ELLIPSOID)
+                gvstart.append(0)
+                gnv.append(0)
+                gparam += [float(g.radii[0]), float(g.radii[1]), float(g.radii[2]), 0.0]
+                ginterior += [0.0] * 3
+            elif isinstance(g, (M.CapsuleGeom, M.CylinderGeom, M.ConeGeom)):
+                gtype.append(M.GEOM_CAPSULE if isinstance(g, M.CapsuleGeom) else
+                             M.GEOM_CONE if isinstance(g, M.ConeGeom) else M.GEOM_CYLINDER)
                 gvstart.append(0)
                 gnv.append(0)
                 gparam += [float(g.radius), float(g.lz), 0.0, 0.0]

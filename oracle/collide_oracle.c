@@ -69,6 +69,7 @@ typedef double ccd_real_t;
 
 /* ---------------------------------------------------------------- world */
 enum { GEOM_CONVEX = 0, GEOM_BOX = 1, GEOM_SPHERE = 2, GEOM_CAPSULE = 3, GEOM_CYLINDER = 4, GEOM_OCTREE = 5, GEOM_MESH = 6,
+       GEOM_ELLIPSOID = 7, GEOM_CONE = 8, GEOM_TRIANGLE_P = 9 /* fcl::TriangleP: 3 vertices */,
        GEOM_TRIANGLE = 100 /* one mesh triangle as a GJK object (internal) */ };
 enum { JT_RX, JT_RY, JT_RZ, JT_RU, JT_PX, JT_PY, JT_PZ, JT_PU, JT_RUBX, JT_RUBY, JT_RUBZ, JT_RUBU };
 enum { KIND_ROBOT = 0, KIND_ATTACHED = 1, KIND_SCENE = 2 };
@@ -437,7 +438,8 @@ typedef struct {
     const real *interior;
     const int *nbr;    /* convex: FCL neighbors_ encoding (ORC_FCL_WALK variant) */
     ccd_real_t dim[3];       /* box half sizes */
-    ccd_real_t radius, height; /* sphere / capsule / cylinder */
+    ccd_real_t radius, height; /* sphere / capsule / cylinder / cone */
+    ccd_real_t radii[3];       /* ellipsoid (ellipsoidToGJK) */
     ccd_vec3_t tp[3], tc; /* triangle (triCreateGJKObject): vertices, centroid */
     orc_stats *stats;
 } gjk_obj;
@@ -568,6 +570,48 @@ static void support_cylinder(const gjk_obj *c, const ccd_vec3_t *dir_, ccd_vec3_
     ccdVec3Add(v, &c->pos);
 }
 
+/* supportCone (FCL 0.7.0 gjk_libccd-inl.h [ext, restated]): the apex when
+ * the direction lies inside the apex cone (dir_z > |dir| sin a, sin a =
+ * r / sqrt(r^2 + 4 h^2), h = lz / 2), else the base rim point along the
+ * direction's xy part, else the base centre; ccd_real arithmetic */
+static void support_cone(const gjk_obj *c, const ccd_vec3_t *dir_, ccd_vec3_t *v) {
+    ccd_vec3_t dir;
+    ccd_real_t zdist, len, rad, sin_a;
+    ccdVec3Copy(&dir, dir_);
+    ccdQuatRotVec(&dir, &c->rot_inv);
+    zdist = dir.v[0] * dir.v[0] + dir.v[1] * dir.v[1];
+    len = zdist + dir.v[2] * dir.v[2];
+    zdist = CCD_SQRT(zdist);
+    len = CCD_SQRT(len);
+    sin_a = c->radius / CCD_SQRT(c->radius * c->radius + 4 * c->height * c->height);
+    if (dir.v[2] > len * sin_a)
+        ccdVec3Set(v, 0.0, 0.0, c->height);
+    else if (zdist > 0) {
+        rad = c->radius / zdist;
+        ccdVec3Set(v, rad * dir.v[0], rad * dir.v[1], -c->height);
+    } else
+        ccdVec3Set(v, 0.0, 0.0, -c->height);
+    ccdQuatRotVec(v, &c->rot);
+    ccdVec3Add(v, &c->pos);
+}
+
+/* supportEllipsoid (FCL 0.7.0 gjk_libccd-inl.h [ext, restated]): p =
+ * (a^2 d_x, b^2 d_y, c^2 d_z) scaled by 1 / sqrt(p . d), d in the ellipsoid
+ * frame; ccd_real arithmetic */
+static void support_ellipsoid(const gjk_obj *o, const ccd_vec3_t *dir_, ccd_vec3_t *v) {
+    ccd_vec3_t dir;
+    ccd_real_t a2, b2, c2;
+    ccdVec3Copy(&dir, dir_);
+    ccdQuatRotVec(&dir, &o->rot_inv);
+    a2 = o->radii[0] * o->radii[0];
+    b2 = o->radii[1] * o->radii[1];
+    c2 = o->radii[2] * o->radii[2];
+    ccdVec3Set(v, a2 * dir.v[0], b2 * dir.v[1], c2 * dir.v[2]);
+    ccdVec3Scale(v, CCD_ONE / CCD_SQRT(ccdVec3Dot(v, &dir)));
+    ccdQuatRotVec(v, &o->rot);
+    ccdVec3Add(v, &o->pos);
+}
+
 /* supportTriangle (FCL gjk_libccd-inl.h): argmax of dir . (p_i - c), first
  * maximum wins, then the vertex itself is transformed */
 static void support_triangle(const gjk_obj *t, const ccd_vec3_t *dir_, ccd_vec3_t *v) {
@@ -594,6 +638,8 @@ static void gjk_support(const gjk_obj *o, const ccd_vec3_t *dir, ccd_vec3_t *v) 
     case GEOM_BOX: support_box(o, dir, v); break;
     case GEOM_SPHERE: support_sphere(o, dir, v); break;
     case GEOM_CAPSULE: support_capsule(o, dir, v); break;
+    case GEOM_CONE: support_cone(o, dir, v); break;
+    case GEOM_ELLIPSOID: support_ellipsoid(o, dir, v); break;
     default: support_cylinder(o, dir, v); break;
     }
 }
@@ -1610,6 +1656,15 @@ static void make_obj(const orc_world *w, int geom, const real *T, gjk_obj *o, or
     case GEOM_SPHERE: o->radius = prm[0]; break;
     case GEOM_CAPSULE: o->radius = prm[0]; o->height = prm[1] / 2.0; break;
     case GEOM_CYLINDER: o->radius = prm[0]; o->height = prm[1] / 2.0; break;
+    case GEOM_CONE: o->radius = prm[0]; o->height = prm[1] / 2.0; break; /* coneToGJK */
+    case GEOM_ELLIPSOID: o->radii[0] = prm[0]; o->radii[1] = prm[1]; o->radii[2] = prm[2]; break;
+    case GEOM_TRIANGLE_P: { /* GJKInitializer<TriangleP>: triCreateGJKObject(a, b, c, tf) */
+        const real *V = w->verts + 3 * (size_t)w->geom_vstart[geom];
+        o->type = GEOM_TRIANGLE;
+        for (int i = 0; i < 3; ++i) ccdVec3Set(&o->tp[i], V[3 * i], V[3 * i + 1], V[3 * i + 2]);
+        ccdVec3Set(&o->tc, (V[0] + V[3] + V[6]) / 3, (V[1] + V[4] + V[7]) / 3, (V[2] + V[5] + V[8]) / 3);
+        break;
+    }
     }
 }
 
@@ -1683,7 +1738,9 @@ static int octree_intersect(const orc_world *w, int go, const real *TO, int gs, 
         for (int k = 0; k < 3; ++k) { hi[k] = 0.5 * ps[k]; lo[k] = -hi[k]; }
     } else if (ts == GEOM_SPHERE) {
         for (int k = 0; k < 3; ++k) { hi[k] = ps[0]; lo[k] = -hi[k]; }
-    } else {
+    } else if (ts == GEOM_ELLIPSOID) { /* computeBV<OBB, Ellipsoid>: extent = radii */
+        for (int k = 0; k < 3; ++k) { hi[k] = ps[k]; lo[k] = -hi[k]; }
+    } else { /* capsule / cylinder / cone (cone extent r, r, lz / 2) */
         const real r = ps[0], hz = 0.5 * ps[1] + (ts == GEOM_CAPSULE ? r : 0.0);
         lo[0] = lo[1] = -r; hi[0] = hi[1] = r; lo[2] = -hz; hi[2] = hz;
     }
@@ -1747,7 +1804,9 @@ static int octree_contact(const orc_world *w, int go, const real *TO, int gs, co
         for (int k = 0; k < 3; ++k) { hi[k] = 0.5 * ps[k]; lo[k] = -hi[k]; }
     } else if (ts == GEOM_SPHERE) {
         for (int k = 0; k < 3; ++k) { hi[k] = ps[0]; lo[k] = -hi[k]; }
-    } else {
+    } else if (ts == GEOM_ELLIPSOID) { /* computeBV<OBB, Ellipsoid>: extent = radii */
+        for (int k = 0; k < 3; ++k) { hi[k] = ps[k]; lo[k] = -hi[k]; }
+    } else { /* capsule / cylinder / cone (cone extent r, r, lz / 2) */
         const real r = ps[0], hz = 0.5 * ps[1] + (ts == GEOM_CAPSULE ? r : 0.0);
         lo[0] = lo[1] = -r; hi[0] = hi[1] = r; lo[2] = -hz; hi[2] = hz;
     }
@@ -2172,6 +2231,8 @@ static void shape_obb(const orc_world *w, int g, double *o) {
     case GEOM_SPHERE: o[12] = o[13] = o[14] = p[0]; break;
     case GEOM_CAPSULE: o[12] = o[13] = p[0]; o[14] = p[1] / 2 + p[0]; break;
     case GEOM_CYLINDER: o[12] = o[13] = p[0]; o[14] = p[1] / 2; break;
+    case GEOM_CONE: o[12] = o[13] = p[0]; o[14] = p[1] / 2; break;
+    case GEOM_ELLIPSOID: o[12] = p[0]; o[13] = p[1]; o[14] = p[2]; break;
     case GEOM_CONVEX: fit_points(w->verts + 3 * (size_t)w->geom_vstart[g], w->geom_nv[g], o, o + 9, o + 12); break;
     default: break;
     }
@@ -3054,6 +3115,7 @@ static real shape_bradius(const orc_world *w, int gs) {
         rs = sqrt(rs);
     } else if (ts == GEOM_BOX) rs = 0.5 * sqrt(dot3(ps, ps));
     else if (ts == GEOM_SPHERE) rs = ps[0];
+    else if (ts == GEOM_ELLIPSOID) rs = fmax(ps[0], fmax(ps[1], ps[2]));
     else rs = sqrt(ps[0] * ps[0] + 0.25 * ps[1] * ps[1]) + (ts == GEOM_CAPSULE ? ps[0] : 0.0);
     return rs * (1.0 + 1e-9) + 1e-9;
 }

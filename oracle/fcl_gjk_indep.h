@@ -21,7 +21,11 @@
  * getSupport (gjk-inl.h): box (d_i > 0 ? side_i / 2 : -side_i / 2); sphere
  * d * r; capsule pos1/pos2 = (0, 0, +-lz/2) + d * r, the larger d . pos;
  * cylinder zdist = sqrt(d0^2 + d1^2), zdist == 0 -> (0, 0, +-lz/2) else
- * (r/zdist d0, r/zdist d1, +-lz/2); convex Convex::findExtremeVertex (the
+ * (r/zdist d0, r/zdist d1, +-lz/2); cone: the apex (0, 0, lz/2) when
+ * d2 > |d| sin a (sin a = r / sqrt(r^2 + 4 (lz/2)^2)), else the rim point
+ * (r/zdist d0, r/zdist d1, -lz/2), else (0, 0, -lz/2); ellipsoid v / sqrt(v . d)
+ * with v = (a^2 d0, b^2 d1, c^2 d2); triangle (TriangleP) the first of the
+ * larger d . a / d . b / d . c; convex Convex::findExtremeVertex (the
  * neighbour walk on watertight hulls of more than 32 vertices, else the
  * first maximum) -- convex_find_extreme above.
  * Eigen's 3-term sums are taken in the oracle's default order
@@ -204,6 +208,33 @@ static gv3 gjk_shape_support(const gshape *sh, gv3 d) {
         const real dd = sh->prm[0] / zdist;
         return gv(dd * d.v[0], dd * d.v[1], (d.v[2] > 0) ? half_h : -half_h);
     }
+    case GEOM_CONE: {
+        real zdist = d.v[0] * d.v[0] + d.v[1] * d.v[1];
+        real len = zdist + d.v[2] * d.v[2];
+        zdist = sqrt(zdist);
+        len = sqrt(len);
+        const real half_h = sh->prm[1] * 0.5, radius = sh->prm[0];
+        const real sin_a = radius / sqrt(radius * radius + 4 * half_h * half_h);
+        if (d.v[2] > len * sin_a) return gv(0, 0, half_h);
+        if (zdist > 0) {
+            const real rad = radius / zdist;
+            return gv(rad * d.v[0], rad * d.v[1], -half_h);
+        }
+        return gv(0, 0, -half_h);
+    }
+    case GEOM_TRIANGLE_P: { /* the first of the larger dot products a / b / c */
+        const gv3 a = gv(sh->verts[0], sh->verts[1], sh->verts[2]), b = gv(sh->verts[3], sh->verts[4], sh->verts[5]),
+                  c = gv(sh->verts[6], sh->verts[7], sh->verts[8]);
+        const real dota = gdot(d, a), dotb = gdot(d, b), dotc = gdot(d, c);
+        if (dota > dotb) return dotc > dota ? c : a;
+        return dotc > dotb ? c : b;
+    }
+    case GEOM_ELLIPSOID: { /* v / sqrt(v . d): Eigen's quotient, one division per coefficient */
+        const real a2 = sh->prm[0] * sh->prm[0], b2 = sh->prm[1] * sh->prm[1], c2 = sh->prm[2] * sh->prm[2];
+        const gv3 v = gv(a2 * d.v[0], b2 * d.v[1], c2 * d.v[2]);
+        const real dd = sqrt(gdot(v, d));
+        return gv(v.v[0] / dd, v.v[1] / dd, v.v[2] / dd);
+    }
     default: { /* GEOM_CONVEX */
         const real dC[3] = {d.v[0], d.v[1], d.v[2]};
         const int k = convex_find_extreme(sh->verts, sh->nv, sh->nbr, dC, NULL);
@@ -332,6 +363,7 @@ static void gshape_of(const orc_world *w, int geom, gshape *sh) {
     sh->verts = NULL;
     sh->nv = 0;
     sh->nbr = NULL;
+    if (sh->type == GEOM_TRIANGLE_P) sh->verts = w->verts + 3 * (size_t)w->geom_vstart[geom];
     if (sh->type == GEOM_CONVEX) {
         sh->verts = w->verts + 3 * (size_t)w->geom_vstart[geom];
         sh->nv = w->geom_nv[geom];

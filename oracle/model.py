@@ -416,6 +416,39 @@ class CylinderGeom:
     lz: float
 
 
+GEOM_ELLIPSOID, GEOM_CONE = 7, 8
+
+
+@dataclass
+class EllipsoidGeom:
+    """fcl::Ellipsoid (python/pybind_fcl.hpp:137-141): semi-axes a, b, c."""
+    radii: Tuple[float, float, float]
+
+
+@dataclass
+class ConeGeom:
+    """fcl::Cone (python/pybind_fcl.hpp:95-98): base radius, height lz along
+    z, centred on its origin (apex at +lz/2)."""
+    radius: float
+    lz: float
+
+
+GEOM_TRIANGLE_P = 9
+
+
+@dataclass
+class TrianglePGeom:
+    """fcl::TriangleP (python/pybind_fcl.hpp:168-175): one triangle a, b, c
+    as a shape (libccd supportTriangle / centerTriangle about its centroid)."""
+    a: Tuple[float, float, float]
+    b: Tuple[float, float, float]
+    c: Tuple[float, float, float]
+
+    @property
+    def vertices(self) -> np.ndarray:
+        return np.array([self.a, self.b, self.c], dtype=np.float64)
+
+
 GEOM_OCTREE = 5
 
 

@@ -59,18 +59,23 @@ def test_invalid_descriptor_rejected(field, value, msg):
 
 
 def test_unsupported_geometry_rejected():
-    """An OcTree as a robot link / attached body (the reference only builds
-    point clouds as world objects) is refused at world creation, never
-    approximated."""
+    """An OcTree may ride on a link or an attached body (round 6), but a
+    non-allowed pair of two OcTrees (FCL's OcTreeIntersect) is refused at
+    world creation, never approximated; so is an unknown geometry kind."""
     ow = Wd.oracle_world(3)
     a = _desc(ow)
     a["geom_type"] = list(a["geom_type"])
     a["geom_param"] = list(a["geom_param"])
-    g = a["moving_geom"][0]
-    a["geom_type"][g] = 5  # MPG_GEOM_OCTREE with an empty leaf range
-    a["geom_param"][4 * g:4 * g + 3] = [0.0, 0.0, 0.01]
+    for g in (a["moving_geom"][1], a["static_geom"][0]):  # panda_link1 and the table
+        a["geom_type"][g] = 5  # MPG_GEOM_OCTREE with an empty leaf range
+        a["geom_param"][4 * g:4 * g + 3] = [0.0, 0.0, 0.01]
     with pytest.raises(NotImplementedError, match="OcTree"):
         _create(a)
+    b = _desc(ow)
+    b["geom_type"] = list(b["geom_type"])
+    b["geom_type"][b["static_geom"][0]] = 9
+    with pytest.raises(NotImplementedError, match="unsupported geometry type"):
+        _create(b)
 
 
 def test_capsule_pairs_accepted():

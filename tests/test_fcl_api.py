@@ -1,0 +1,187 @@
+"""The rest of the reference's fcl binding surface (python/pybind_fcl.hpp):
+Triangle, CollisionGeometry's bookkeeping and mass properties, Convex
+compute_volume, Contact / ContactPoint / CostSource constructors,
+CollisionResult's contact and cost-source lists, fcl.collide / fcl.distance
+with an articulation, and PlanningWorld.print_attached_body_pose
+(python/pybind_planning_world.hpp:102).  The mass properties restate FCL
+0.7.0 [ext] and are pinned here by the closed-form volumes and inertias of
+the solids (none of this is on the collision path)."""
+import numpy as np
+import pytest
+
+from mplib_amd import pymp
+
+fcl = pymp.fcl
+
+
+def _cube_convex(side=1.0, off=(0.0, 0.0, 0.0)):
+    h = side / 2
+    V = np.array([[x, y, z] for x in (-h, h) for y in (-h, h) for z in (-h, h)], np.float64) + np.asarray(off)
+    F = np.array([(0, 1, 3), (0, 3, 2), (4, 6, 7), (4, 7, 5), (0, 4, 5), (0, 5, 1), (2, 3, 7), (2, 7, 6), (0, 2, 6),
+                  (0, 6, 4), (1, 5, 7), (1, 7, 3)], np.int32)
+    return V, F
+
+
+def test_triangle():
+    t = fcl.Triangle(1, 2, 3)
+    assert (t[0], t[1], t[2]) == (1, 2, 3) and t.get(1) == 2
+    t.set(4, 5, 6)
+    assert [t[i] for i in range(3)] == [4, 5, 6]
+    assert fcl.Triangle()[0] == 0
+    b = fcl.BVHModel()
+    b.beginModel()
+    V, F = _cube_convex()
+    b.addSubModel(V, [fcl.Triangle(*map(int, f)) for f in F])
+    b.endModel()
+    np.testing.assert_array_equal(b.get_faces(), F)
+
+
+@pytest.mark.parametrize("name", ["box", "sphere", "capsule", "cylinder", "cone", "ellipsoid"])
+def test_shape_volume_com_inertia(name):
+    """FCL's closed forms against the solids' textbook values (unit
+    density: the inertia tensor's mass is the volume)."""
+    pi = np.pi
+    if name == "box":
+        g, V = fcl.Box(0.2, 0.3, 0.4), 0.024
+        I = V / 12 * np.array([0.09 + 0.16, 0.04 + 0.16, 0.04 + 0.09])
+        lo = [0.1, 0.15, 0.2]
+    elif name == "sphere":
+        g, V = fcl.Sphere(0.3), 4 / 3 * pi * 0.027
+        I = np.full(3, 0.4 * V * 0.09)
+        lo = [0.3] * 3
+    elif name == "capsule":
+        r, lz = 0.1, 0.4
+        g = fcl.Capsule(r, lz)
+        vc, vs = pi * r * r * lz, 4 / 3 * pi * r ** 3
+        V = vc + vs
+        ix = vc * (lz * lz / 12 + r * r / 4) + vs * (0.4 * r * r + lz * lz / 4 + 3 * r * lz / 8)
+        I = np.array([ix, ix, (0.5 * vc + 0.4 * vs) * r * r])
+        lo = [r, r, lz / 2 + r]
+    elif name == "cylinder":
+        r, lz = 0.1, 0.4
+        g, V = fcl.Cylinder(r, lz), pi * r * r * lz
+        I = np.array([V * (3 * r * r + lz * lz) / 12] * 2 + [V * r * r / 2])
+        lo = [r, r, lz / 2]
+    elif name == "cone":
+        r, lz = 0.1, 0.4
+        g, V = fcl.Cone(r, lz), pi * r * r * lz / 3
+        I = np.array([V * (0.1 * lz * lz + 3 * r * r / 20)] * 2 + [0.3 * V * r * r])
+        lo = [r, r, lz / 2]
+    else:
+        g, V = fcl.Ellipsoid(0.1, 0.2, 0.3), 4 / 3 * pi * 0.006
+        I = 0.2 * V * np.array([0.04 + 0.09, 0.01 + 0.09, 0.01 + 0.04])
+        lo = [0.1, 0.2, 0.3]
+    assert g.computeVolume() == pytest.approx(V, rel=1e-12)
+    np.testing.assert_allclose(np.diag(g.computeMomentofInertia()), I, rtol=1e-12)
+    com = np.asarray(g.computeCOM())
+    np.testing.assert_allclose(com, [0, 0, -0.1] if name == "cone" else [0, 0, 0], atol=1e-15)
+    Ic = np.asarray(g.computeMomentofInertiaRelatedToCOM())
+    np.testing.assert_allclose(np.diag(Ic), I - V * np.array([com[2] ** 2, com[2] ** 2, 0.0]), rtol=1e-12)
+    # computeLocalAABB runs in CollisionObject's constructor
+    assert g.aabb_radius == 0.0
+    fcl.CollisionObject(g, [1.0, 2.0, 3.0], [1, 0, 0, 0])
+    np.testing.assert_allclose(g.aabb_center, 0.0, atol=1e-15)
+    assert g.aabb_radius == pytest.approx(np.linalg.norm(lo), rel=1e-15)
+
+
+def test_convex_and_mesh_mass_properties():
+    """Signed-tetrahedron sums: an offset unit cube has volume 1, its centre
+    as COM, inertia 1/6 about the COM, and the parallel-axis term about the
+    origin; the BVH of the same triangles agrees."""
+    off = (0.3, -0.2, 0.5)
+    V, F = _cube_convex(1.0, off)
+    c = fcl.Convex(V, F)
+    b = fcl.BVHModel()
+    b.beginModel()
+    b.addSubModel(V, F)
+    b.endModel()
+    d = np.asarray(off)
+    Io = np.eye(3) / 6 + (d @ d) * np.eye(3) - np.outer(d, d)
+    for g in (c, b):
+        assert g.computeVolume() == pytest.approx(1.0, rel=1e-12)
+        np.testing.assert_allclose(g.computeCOM(), off, atol=1e-12)
+        np.testing.assert_allclose(g.computeMomentofInertia(), Io, atol=1e-12)
+        np.testing.assert_allclose(g.computeMomentofInertiaRelatedToCOM(), np.eye(3) / 6, atol=1e-12)
+    assert c.compute_volume() == pytest.approx(1.0, rel=1e-12)
+    g = fcl.CollisionObject(c, [0, 0, 0], [1, 0, 0, 0]).get_collision_geometry()
+    np.testing.assert_allclose(g.aabb_center, off, atol=1e-15)
+    assert g.aabb_radius == pytest.approx(np.sqrt(0.75), rel=1e-15)
+    fcl.CollisionObject(b)
+    assert b.aabb_radius == pytest.approx(np.sqrt(0.75), rel=1e-15)
+
+
+def test_occupancy_and_octree_box():
+    g = fcl.Box(1.0, 1.0, 1.0)
+    assert g.cost_density == 1.0 and g.isOccupied() and not g.isFree() and not g.isUncertain()
+    g.cost_density = 0.5
+    assert not g.isOccupied() and not g.isFree() and g.isUncertain()
+    g.cost_density = 0.0
+    assert g.isFree()
+    t = fcl.OcTree(0.01)
+    t.computeLocalAABB()
+    d = (1 << 16) * 0.01 / 2  # OcTree::getRootBV: (1 << depth) * resolution / 2
+    assert t.aabb_radius == pytest.approx(d * np.sqrt(3)) and t.computeVolume() == 0.0
+
+
+def test_contacts_and_cost_sources():
+    a, b = fcl.Box(1.0, 1.0, 1.0), fcl.Sphere(0.5)
+    c = fcl.Contact(a, b, 1, 2, [0.1, 0.2, 0.3], [0.0, 0.0, 1.0], 0.05)
+    np.testing.assert_array_equal(c.pos, [0.1, 0.2, 0.3])
+    assert c.penetration_depth == 0.05
+    p = fcl.ContactPoint([0.0, 1.0, 0.0], [1.0, 2.0, 3.0], 0.25)
+    np.testing.assert_array_equal(p.normal, [0, 1, 0])
+    assert p.penetration_depth == 0.25
+    r = fcl.CollisionResult()
+    assert not r.is_collision()
+    r.add_contact(fcl.Contact(a, b, -1, -1))
+    r.add_contact(c)
+    assert r.is_collision() and r.num_contacts() == 2 and r.get_contact(1).penetration_depth == 0.05
+    s1 = fcl.CostSource([0, 0, 0], [1, 1, 1], 2.0)    # total 2
+    s2 = fcl.CostSource([0, 0, 0], [2, 1, 1], 0.5)    # total 1
+    s3 = fcl.CostSource([1, 0, 0], [2, 3, 1], 1.0)    # total 3
+    assert s3.total_cost == 3.0
+    for s in (s2, s1, s3, s1):  # a duplicate is not inserted twice
+        r.add_cost_source(s, 2)
+    assert r.num_cost_sources() == 2
+    assert [x.total_cost for x in r.get_cost_sources()] == [3.0, 2.0]  # largest first, beyond 2 dropped
+    r.clear()
+    assert r.num_contacts() == 0 and r.num_cost_sources() == 0
+
+
+# ------------------------------------------------------------------ GPU
+@pytest.mark.gpu
+def test_fcl_collide_and_distance_with_articulation():
+    """fcl.collide(articulation, o2) reports each link colliding with o2
+    (articulation_sceneobject, "__object__") exactly like the world's
+    collide_with_others on a one-obstacle world; fcl.distance(articulation,
+    o2) is the minimum over the links."""
+    from mplib_amd import scenes
+    w, art = scenes.world(2)
+    a = w.get_articulation(w.get_articulation_names()[0])
+    box = fcl.CollisionObject(fcl.Box(0.2, 0.2, 0.2), [0.45, 0.0, 0.45], [1, 0, 0, 0])
+    w.add_normal_object("blk", box)
+    q = scenes.sample_states(art, 40, 41)
+    hits = 0
+    for i in range(len(q)):
+        w.set_qpos_all(list(q[i]))
+        got = fcl.collide(a, box)
+        want = sorted(r.link_name1 for r in w.collide_with_others() if r.link_name2 == "blk")
+        assert sorted(r.link_name1 for r in got) == want, i
+        assert all(r.collision_type == "articulation_sceneobject" and r.object_name2 == "__object__" for r in got)
+        hits += len(got)
+        dres, dw = fcl.distance(a, box), w.distance_with_others()  # the only scene object
+        assert dres.min_distance == pytest.approx(dw.min_distance, abs=1e-12)
+        assert dres.link_name1 == dw.link_name1
+        assert dres.distance_type == "articulation_sceneobject" and dres.link_name2 == "__object__"
+    assert hits > 0
+
+
+@pytest.mark.gpu
+def test_print_attached_body_pose(capfd):
+    from mplib_amd import scenes
+    w, art = scenes.world(2)
+    w.attach_box([0.04, 0.04, 0.1], "panda", 8, [0.0, 0.0, 0.1, 1.0, 0.0, 0.0, 0.0])
+    w.set_qpos_all(list(scenes.sample_states(art, 1, 0)[0]))
+    w.print_attached_body_pose()
+    out = capfd.readouterr().out
+    assert "global pose:" in out and len(out.strip().splitlines()) == 5

@@ -176,11 +176,23 @@ def desc_arrays(ow: oracle.OracleWorld) -> dict:
             gvs.append(0)
             gnv.append(0)
             gparam += [float(g.radius), 0.0, 0.0, 0.0]
-        elif isinstance(g, (M.CapsuleGeom, M.CylinderGeom)):
-            gtype.append(3 if isinstance(g, M.CapsuleGeom) else 4)
+        elif isinstance(g, (M.CapsuleGeom, M.CylinderGeom, M.ConeGeom)):
+            gtype.append(3 if isinstance(g, M.CapsuleGeom) else M.GEOM_CONE if isinstance(g, M.ConeGeom) else 4)
             gvs.append(0)
             gnv.append(0)
             gparam += [float(g.radius), float(g.lz), 0.0, 0.0]
+        elif isinstance(g, M.TrianglePGeom):
+            gtype.append(M.GEOM_TRIANGLE_P)
+            gvs.append(nv)
+            gnv.append(3)
+            nv += 3
+            verts.append(g.vertices.reshape(-1))
+            gparam += [0.0] * 4
+        elif isinstance(g, M.EllipsoidGeom):
+            gtype.append(M.GEOM_ELLIPSOID)
+            gvs.append(0)
+            gnv.append(0)
+            gparam += [float(g.radii[0]), float(g.radii[1]), float(g.radii[2]), 0.0]
         else:
             gtype.append(1)
             gvs.append(0)
