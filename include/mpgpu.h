@@ -370,7 +370,8 @@ int mpg_distance_batch(mpg_world *world, const double *q, int64_t n, int32_t n_s
  * DistanceRequest (python/pybind_fcl.hpp:310-316) as PlanningWorldTpl::
  * distance* passes it to fcl::distance (src/planning_world.cpp:512, 537):
  *   flags: MPG_DISTANCE_SIGNED (enable_signed_distance),
- *          MPG_DISTANCE_NEAREST_POINTS (enable_nearest_points);
+ *          MPG_DISTANCE_NEAREST_POINTS (enable_nearest_points),
+ *          MPG_DISTANCE_GJK_INDEP (gjk_solver_type = GST_INDEP);
  *   distance_tolerance: GJKSolver_libccd::distance_tolerance, libccd's
  *          dist_tolerance (default 1e-6).
  * pts_self / pts_others ([n*6], may be NULL): DistanceResult::nearest_points
@@ -393,6 +394,12 @@ int mpg_distance_batch(mpg_world *world, const double *q, int64_t n, int32_t n_s
  */
 #define MPG_DISTANCE_SIGNED 1
 #define MPG_DISTANCE_NEAREST_POINTS 2
+#define MPG_DISTANCE_GJK_INDEP 4 /* gjk_solver_type = GST_INDEP: FCL's own GJK
+                                    in double (ShapeDistanceIndepImpl, its
+                                    gjk_tolerance = distance_tolerance) for
+                                    the shape pairs without a closed form;
+                                    unsigned only, no OcTree / BVH mesh pair
+                                    (MPG_E_UNSUPPORTED)                   */
 #define MPG_DISTANCE_FCL_THROWS (-2)
 #define MPG_DISTANCE_EPA_CAPACITY (-3)
 typedef struct mpg_distance_request {

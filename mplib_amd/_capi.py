@@ -51,6 +51,15 @@ class WorldDesc(ctypes.Structure):
     ]
 
 
+MPG_DISTANCE_SIGNED, MPG_DISTANCE_NEAREST_POINTS, MPG_DISTANCE_GJK_INDEP = 1, 2, 4
+
+
+class DistanceRequest(ctypes.Structure):
+    """mpg_distance_request (include/mpgpu.h): DistanceRequest's flags and
+    distance_tolerance."""
+    _fields_ = [("flags", ctypes.c_int32), ("distance_tolerance", ctypes.c_double)]
+
+
 class WorldInfo(ctypes.Structure):
     _fields_ = [("n_pairs", ctypes.c_int32), ("mask_words", ctypes.c_int32), ("dof", ctypes.c_int32),
                 ("n_links", ctypes.c_int32), ("device", ctypes.c_int32), ("block_size", ctypes.c_int32),

@@ -211,7 +211,7 @@ struct DistanceRequest {
   bool enable_signed_distance = false;
   double rel_err = 0.0, abs_err = 0.0, distance_tolerance = 1e-6;
   GJKSolverType gjk_solver_type = GST_LIBCCD;
-  // GST_INDEP is not implemented on the device (raises)
+  // GST_INDEP: FCL's own GJK, unsigned only (enable_signed_distance raises)
   void check_supported() const;
   // MPG_DISTANCE_* flags of the C ABI
   int32_t flags() const;

@@ -710,13 +710,18 @@ void PlanningWorld::check_motion_batch(const double* from, const double* to, int
                "mpg_check_motion_batch");
 }
 
+// GST_INDEP: FCL's own GJK for unsigned distances; its EPA (signed) is not
+// restated.  OcTree / BVH mesh pairs with GST_INDEP are refused by the device
+// call (MPG_E_UNSUPPORTED -> NotImplementedError).
 void DistanceRequest::check_supported() const {
-  if (gjk_solver_type != GST_LIBCCD)
-    throw std::logic_error("NotImplemented: only GJKSolverType.GST_LIBCCD is implemented on the device");
+  if (gjk_solver_type == GST_INDEP && enable_signed_distance)
+    throw std::logic_error("NotImplemented: enable_signed_distance=True with gjk_solver_type=GST_INDEP (FCL's EPA) "
+                           "is not implemented on the device");
 }
 
 int32_t DistanceRequest::flags() const {
-  return (enable_signed_distance ? MPG_DISTANCE_SIGNED : 0) | (enable_nearest_points ? MPG_DISTANCE_NEAREST_POINTS : 0);
+  return (enable_signed_distance ? MPG_DISTANCE_SIGNED : 0) | (enable_nearest_points ? MPG_DISTANCE_NEAREST_POINTS : 0) |
+         (gjk_solver_type == GST_INDEP ? MPG_DISTANCE_GJK_INDEP : 0);
 }
 
 mpg_distance_request DistanceRequest::to_c() const {

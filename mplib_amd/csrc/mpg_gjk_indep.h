@@ -189,40 +189,71 @@ __device__ __forceinline__ V3 matv(const double* M, const V3& d) {
             (M[6] * d.x + M[7] * d.y) + M[8] * d.z);
 }
 
-// GJK::getSupport: d.normalized() (each coefficient over sqrt(|d|^2)), then
-// support0(d) - toshape0 * getSupport(s2, toshape1 * -d)
-__device__ __forceinline__ V3 support(const DevWorld& w, cptr<double> HV, const Mink& m, const V3& d_in) {
-  V3 d = d_in;
+// GJK::getSupport: d.normalized() (each coefficient over sqrt(|d|^2))
+__device__ __forceinline__ V3 normalized(const V3& d_in) {
   const double n2 = vdot(d_in, d_in);
-  if (n2 > 0) {
-    const double s = std::sqrt(n2);
-    d = v3(d_in.x / s, d_in.y / s, d_in.z / s);
-  }
-  const V3 s0 = shape_support(w, HV, m.ga, m.ta, d);
-  const V3 l1 = shape_support(w, HV, m.gb, m.tb, matv(m.ts1, vscale(d, -1.0)));
-  return vsub(s0, vadd(matv(m.r0, l1), m.t0));
+  if (!(n2 > 0)) return d_in;
+  const double s = std::sqrt(n2);
+  return v3(d_in.x / s, d_in.y / s, d_in.z / s);
 }
 
-// GJK<S>::evaluate(shape, guess = (-1, 0, 0)) == Inside
-__device__ bool evaluate(const DevWorld& w, cptr<double> HV, const Mink& m, double tol) {
+// MinkowskiDiff::support0(d) / support1(-d) for a normalised d
+__device__ __forceinline__ V3 support0(const DevWorld& w, cptr<double> HV, const Mink& m, const V3& d) {
+  return shape_support(w, HV, m.ga, m.ta, d);
+}
+__device__ __forceinline__ V3 support1_neg(const DevWorld& w, cptr<double> HV, const Mink& m, const V3& d) {
+  return vadd(matv(m.r0, shape_support(w, HV, m.gb, m.tb, matv(m.ts1, vscale(d, -1.0)))), m.t0);
+}
+
+// support0(d) - toshape0 * getSupport(s2, toshape1 * -d), d normalised
+__device__ __forceinline__ V3 support_n(const DevWorld& w, cptr<double> HV, const Mink& m, const V3& d) {
+  return vsub(support0(w, HV, m, d), support1_neg(w, HV, m, d));
+}
+
+enum : int { kGjkValid = 0, kGjkInside = 1, kGjkFailed = 2 };
+
+// the simplex GJK<S>::evaluate leaves (getSimplex()): directions and weights
+struct Simplex {
+  int rank;
+  V3 d[4];
+  double p[4];
+};
+
+// GJK<S>::evaluate(shape, guess = (-1, 0, 0)) -> status; with SIMPLEX the
+// final simplex (simplices[current]) into *out
+template <bool SIMPLEX>
+__device__ int evaluate(const DevWorld& w, cptr<double> HV, const Mink& m, double tol, Simplex* out) {
   constexpr unsigned kMaxIter = 128u;  // GJKSolver_indep::gjk_max_iterations
   V3 sw[4];  // the current simplex's support points
+  V3 sd[4];  // ... their directions (SIMPLEX)
+  double sp[4];  // ... and weights (SIMPLEX)
   int rank = 0;
   unsigned iterations = 0;
   double alpha = 0;
   V3 lastw[4];
   unsigned clastw = 0;
-  bool inside = false;
-  sw[rank++] = support(w, HV, m, vscale(v3(-1.0, 0.0, 0.0), -1.0));  // -ray, ray = guess = (-1, 0, 0)
+  int status = kGjkValid;
+  {
+    const V3 d0 = normalized(vscale(v3(-1.0, 0.0, 0.0), -1.0));  // -ray, ray = guess = (-1, 0, 0)
+    if constexpr (SIMPLEX) {
+      sd[0] = d0;
+      sp[0] = 1;
+    }
+    sw[rank++] = support_n(w, HV, m, d0);
+  }
   V3 ray = sw[0];
   lastw[0] = lastw[1] = lastw[2] = lastw[3] = ray;
   for (;;) {
     const double rl = std::sqrt(vdot(ray, ray));
     if (rl < tol) {
-      inside = true;
+      status = kGjkInside;
       break;
     }
-    sw[rank++] = support(w, HV, m, vscale(ray, -1.0));
+    {
+      const V3 dn = normalized(vscale(ray, -1.0));
+      if constexpr (SIMPLEX) sd[rank] = dn;
+      sw[rank++] = support_n(w, HV, m, dn);
+    }
     const V3 wv = sw[rank - 1];
     bool found = false;
 #pragma unroll
@@ -230,43 +261,75 @@ __device__ bool evaluate(const DevWorld& w, cptr<double> HV, const Mink& m, doub
       const V3 e = vsub(wv, lastw[i]);
       if (vdot(e, e) < tol) found = true;
     }
-    if (found) break;  // (removeVertex: the simplex is not read again)
+    if (found) {  // removeVertex
+      --rank;
+      break;
+    }
     clastw = (clastw + 1) & 3;
     lastw[clastw] = wv;
     const double omega = vdot(ray, wv) / rl;
     alpha = alpha > omega ? alpha : omega;
-    if ((rl - alpha) - tol * rl <= 0) break;
+    if ((rl - alpha) - tol * rl <= 0) {
+      --rank;
+      break;
+    }
     Proj pr = proj0();
     if (rank == 2) pr = line(sw[0], sw[1]);
     else if (rank == 3) pr = triangle(sw[0], sw[1], sw[2]);
     else pr = tetrahedron(sw[0], sw[1], sw[2], sw[3]);
-    if (!(pr.sqd >= 0)) break;
-    V3 nw[4];
+    if (!(pr.sqd >= 0)) {
+      --rank;
+      break;
+    }
+    V3 nw[4], nd[4];
+    double np[4];
     int nr = 0;
     ray = v3(0, 0, 0);
 #pragma unroll
     for (int i = 0; i < 4; ++i)
       if (i < rank && (pr.enc & (1u << i))) {
+        if constexpr (SIMPLEX) {
+          nd[nr] = sd[i];
+          np[nr] = pr.p[i];
+        }
         nw[nr++] = sw[i];
         ray = vadd(ray, vscale(sw[i], pr.p[i]));
       }
 #pragma unroll
-    for (int i = 0; i < 4; ++i) sw[i] = nw[i];
+    for (int i = 0; i < 4; ++i) {
+      sw[i] = nw[i];
+      if constexpr (SIMPLEX) {
+        sd[i] = nd[i];
+        sp[i] = np[i];
+      }
+    }
     rank = nr;
     const bool in15 = pr.enc == 15;
-    if (++iterations >= kMaxIter) break;  // Failed (an Inside of this very step included)
+    if (++iterations >= kMaxIter) {  // Failed (an Inside of this very step included)
+      status = kGjkFailed;
+      break;
+    }
     if (in15) {
-      inside = true;
+      status = kGjkInside;
       break;
     }
   }
-  return inside;
+  if constexpr (SIMPLEX) {
+    out->rank = rank;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      out->d[i] = sd[i];
+      out->p[i] = sp[i];
+    }
+  }
+  return status;
 }
 
 }  // namespace gjki
 
-// GJKSolver_indep::shapeIntersect (generic): true = collision
-__device__ bool gjk_indep_intersect(const DevWorld& w, int ga, const SE3& T1, int gb, const SE3& T2) {
+// MinkowskiDiff of (ga at T1, gb at T2) in shape 1's frame: toshape1 =
+// R2^T R1, toshape0 = tf1^-1 tf2
+__device__ __forceinline__ gjki::Mink gjk_indep_mink(const DevWorld& w, int ga, const SE3& T1, int gb, const SE3& T2) {
   gjki::Mink m;
   m.ga = ga;
   m.gb = gb;
@@ -286,5 +349,37 @@ __device__ bool gjk_indep_intersect(const DevWorld& w, int ga, const SE3& T1, in
     t0[i] = ((T1.R[i] * T2.p[0] + T1.R[3 + i] * T2.p[1]) + T1.R[6 + i] * T2.p[2]) + inv_t;
   }
   m.t0 = v3(t0[0], t0[1], t0[2]);
-  return gjki::evaluate(w, w.hull, m, w.mpr_tol);
+  return m;
+}
+
+// GJKSolver_indep::shapeDistance (generic, ShapeDistanceIndepImpl): GJK with
+// gjk_tolerance = the request's distance_tolerance; Valid -> w0 = sum p_i
+// support0(d_i), w1 = sum p_i support1(-d_i), distance |w0 - w1|, points
+// tf1 * w0 and tf1 * w1; otherwise -1 and zero points
+// (oracle/fcl_gjk_indep.h gjk_indep_distance)
+__device__ double gjk_indep_distance(const DevWorld& w, cptr<double> HV, int ga, const SE3& T1, int gb, const SE3& T2,
+                                     double tol, V3& p1, V3& p2) {
+  const gjki::Mink m = gjk_indep_mink(w, ga, T1, gb, T2);
+  gjki::Simplex s;
+  p1 = p2 = v3(0, 0, 0);
+  if (gjki::evaluate<true>(w, HV, m, tol, &s) != gjki::kGjkValid) return -1.0;
+  V3 w0 = v3(0, 0, 0), w1 = v3(0, 0, 0);
+  for (int i = 0; i < s.rank; ++i) {
+    w0 = vadd(w0, vscale(gjki::support0(w, HV, m, s.d[i]), s.p[i]));
+    w1 = vadd(w1, vscale(gjki::support1_neg(w, HV, m, s.d[i]), s.p[i]));
+  }
+  const V3 dv = vsub(w0, w1);
+  p1 = v3(((T1.R[0] * w0.x + T1.R[1] * w0.y) + T1.R[2] * w0.z) + T1.p[0],
+          ((T1.R[3] * w0.x + T1.R[4] * w0.y) + T1.R[5] * w0.z) + T1.p[1],
+          ((T1.R[6] * w0.x + T1.R[7] * w0.y) + T1.R[8] * w0.z) + T1.p[2]);
+  p2 = v3(((T1.R[0] * w1.x + T1.R[1] * w1.y) + T1.R[2] * w1.z) + T1.p[0],
+          ((T1.R[3] * w1.x + T1.R[4] * w1.y) + T1.R[5] * w1.z) + T1.p[1],
+          ((T1.R[6] * w1.x + T1.R[7] * w1.y) + T1.R[8] * w1.z) + T1.p[2]);
+  return std::sqrt(vdot(dv, dv));
+}
+
+// GJKSolver_indep::shapeIntersect (generic): true = collision
+__device__ bool gjk_indep_intersect(const DevWorld& w, int ga, const SE3& T1, int gb, const SE3& T2) {
+  const gjki::Mink m = gjk_indep_mink(w, ga, T1, gb, T2);
+  return gjki::evaluate<false>(w, w.hull, m, w.mpr_tol, nullptr) == gjki::kGjkInside;
 }

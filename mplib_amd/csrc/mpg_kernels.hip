@@ -4767,7 +4767,8 @@ __device__ double mesh_octree_distance_lane(const DevWorld& w, int gm, const SE3
 
 // (MODE bit) PTS: write the nearest points; SIGNED: enable_signed_distance;
 // NP: enable_nearest_points (mesh-mesh points, the (shape, mesh) swap)
-constexpr int MPG_DIST_POINTS = 1, MPG_DIST_SIGNED = 2, MPG_DIST_NP = 4;
+// INDEP: DistanceRequest(gjk_solver_type=GST_INDEP), unsigned shape pairs only
+constexpr int MPG_DIST_POINTS = 1, MPG_DIST_SIGNED = 2, MPG_DIST_NP = 4, MPG_DIST_INDEP = 8;
 constexpr int kBigPool = 16;  // big EPA polytopes per world (distance_redo_kernel)
 
 // Per configuration, every non-allowed pair in order with the group's strict
@@ -4782,13 +4783,15 @@ constexpr int kBigPool = 16;  // big EPA polytopes per world (distance_redo_kern
 // distance_kernel, a global pool slot in distance_redo_kernel).
 template <int MODE, class PT>
 __device__ __forceinline__ void distance_config(const DevWorld& w, const double* __restrict__ poses, long long n,
-                                                long long cfg, bool live, int n_self, ccd_real tol, PT* ptp,
-                                                double* __restrict__ d_self, int32_t* __restrict__ p_self,
+                                                long long cfg, bool live, int n_self, ccd_real tol, double dtol,
+                                                PT* ptp, double* __restrict__ d_self, int32_t* __restrict__ p_self,
                                                 double* __restrict__ d_others, int32_t* __restrict__ p_others,
                                                 double* __restrict__ pts_self, double* __restrict__ pts_others) {
   constexpr bool SIGNED = (MODE & MPG_DIST_SIGNED) != 0;
   constexpr bool PTS = (MODE & MPG_DIST_POINTS) != 0;
   constexpr bool NP = (MODE & MPG_DIST_NP) != 0;
+  constexpr bool INDEP = (MODE & MPG_DIST_INDEP) != 0;
+  static_assert(!(INDEP && SIGNED), "GST_INDEP signed distance (FCL's EPA) is not restated");
   const cptr<double> HV = w.hull;
   double best[2] = {DBL_MAX, DBL_MAX};
   int bp[2] = {-1, -1};
@@ -4843,6 +4846,10 @@ __device__ __forceinline__ void distance_config(const DevWorld& w, const double*
       if constexpr (!SIGNED) {
         const SE3 TA = pose_se3(w, poses, n, cfg, a), TB = pose_se3(w, poses, n, cfg, b);
         done = cf_shape_distance(w, A.geom, A.type, TA, B.geom, B.type, TB, d, q1, q2);
+        if constexpr (INDEP) {  // FCL's own GJK in double (the same closed forms first)
+          if (!done) d = gjk_indep_distance(w, HV, A.geom, TA, B.geom, TB, dtol, q1, q2);
+          done = true;
+        }
       }
       if (!done) {
         auto sup = [&](const CV3& dir) { return csup(w, HV, A, B, dir); };
@@ -4889,10 +4896,10 @@ __device__ __forceinline__ void distance_config(const DevWorld& w, const double*
 
 template <int MODE>
 __global__ __launch_bounds__(128) void distance_kernel(DevWorld w, const double* __restrict__ poses, long long n,
-                                                       int n_self, ccd_real tol, double* __restrict__ d_self,
-                                                       int32_t* __restrict__ p_self, double* __restrict__ d_others,
-                                                       int32_t* __restrict__ p_others, double* __restrict__ pts_self,
-                                                       double* __restrict__ pts_others) {
+                                                       int n_self, ccd_real tol, double dtol,
+                                                       double* __restrict__ d_self, int32_t* __restrict__ p_self,
+                                                       double* __restrict__ d_others, int32_t* __restrict__ p_others,
+                                                       double* __restrict__ pts_self, double* __restrict__ pts_others) {
   constexpr bool SIGNED = (MODE & MPG_DIST_SIGNED) != 0;
   const long long cfg0 = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const bool live = cfg0 < n;
@@ -4901,7 +4908,7 @@ __global__ __launch_bounds__(128) void distance_kernel(DevWorld w, const double*
   std::conditional_t<SIGNED, ccdx::Polytope, NoPolytope> polytope;
   ccdx::Polytope* ptp = nullptr;
   if constexpr (SIGNED) ptp = &polytope;
-  distance_config<MODE>(w, poses, n, cfg, live, n_self, tol, ptp, d_self, p_self, d_others, p_others, pts_self,
+  distance_config<MODE>(w, poses, n, cfg, live, n_self, tol, dtol, ptp, d_self, p_self, d_others, p_others, pts_self,
                         pts_others);
 }
 
@@ -4919,7 +4926,8 @@ __global__ __launch_bounds__(256) void overflow_list_kernel(const int32_t* __res
 
 template <int MODE>
 __global__ __launch_bounds__(64) void distance_redo_kernel(DevWorld w, const double* __restrict__ poses, long long n,
-                                                           int n_self, ccd_real tol, double* __restrict__ d_self,
+                                                           int n_self, ccd_real tol, double dtol,
+                                                           double* __restrict__ d_self,
                                                            int32_t* __restrict__ p_self, double* __restrict__ d_others,
                                                            int32_t* __restrict__ p_others,
                                                            double* __restrict__ pts_self,
@@ -4928,8 +4936,8 @@ __global__ __launch_bounds__(64) void distance_redo_kernel(DevWorld w, const dou
                                                            const unsigned* __restrict__ list) {
   const unsigned k = threadIdx.x, count = list[0];
   for (unsigned i = k; i < count; i += kBigPool)
-    distance_config<MODE>(w, poses, n, (long long)list[1 + i], true, n_self, tol, pool + k, d_self, p_self, d_others,
-                          p_others, pts_self, pts_others);
+    distance_config<MODE>(w, poses, n, (long long)list[1 + i], true, n_self, tol, dtol, pool + k, d_self, p_self,
+                          d_others, p_others, pts_self, pts_others);
 }
 
 // ---------------------------------------------------------------------------
@@ -9332,12 +9340,20 @@ int mpg_distance_batch_req(mpg_world* w, const double* q, int64_t n, int32_t n_s
     return set_error(MPG_E_INVALID, "NULL buffer");
   if (mem != MPG_MEM_HOST && mem != MPG_MEM_DEVICE) return set_error(MPG_E_INVALID, "bad mem kind");
   const int32_t flags = req->flags;
-  if (flags & ~(MPG_DISTANCE_SIGNED | MPG_DISTANCE_NEAREST_POINTS)) return set_error(MPG_E_INVALID, "bad flags");
+  if (flags & ~(MPG_DISTANCE_SIGNED | MPG_DISTANCE_NEAREST_POINTS | MPG_DISTANCE_GJK_INDEP))
+    return set_error(MPG_E_INVALID, "bad flags");
   if (!(req->distance_tolerance >= 0.0)) return set_error(MPG_E_INVALID, "bad distance_tolerance");
+  const bool indep = (flags & MPG_DISTANCE_GJK_INDEP) != 0;
+  if (indep && (flags & MPG_DISTANCE_SIGNED))
+    return set_error(MPG_E_UNSUPPORTED, "signed distance with GST_INDEP (FCL's EPA) is not implemented");
+  if (indep && (w->has_mesh || w->has_octree))
+    return set_error(MPG_E_UNSUPPORTED, "distance with GST_INDEP for an OcTree or BVH mesh pair is not implemented");
   const ccd_real tol = (ccd_real)req->distance_tolerance;  // GJKSolver_libccd::distance_tolerance -> ccd.dist_tolerance
+  const double dtol = req->distance_tolerance;              // GJKSolver_indep::gjk_tolerance (distance-inl.h)
   const bool want_pts = pts_self || pts_others;
-  const int mode = (want_pts || flags ? MPG_DIST_POINTS : 0) | (flags & MPG_DISTANCE_SIGNED ? MPG_DIST_SIGNED : 0) |
-                   (flags & MPG_DISTANCE_NEAREST_POINTS ? MPG_DIST_NP : 0);
+  const int mode = (want_pts || (flags & (MPG_DISTANCE_SIGNED | MPG_DISTANCE_NEAREST_POINTS)) ? MPG_DIST_POINTS : 0) |
+                   (flags & MPG_DISTANCE_SIGNED ? MPG_DIST_SIGNED : 0) |
+                   (flags & MPG_DISTANCE_NEAREST_POINTS ? MPG_DIST_NP : 0) | (indep ? MPG_DIST_INDEP : 0);
   if (n == 0) return MPG_OK;
   HIP_TRY(hipSetDevice(w->device));
   hipStream_t s = static_cast<hipStream_t>(stream);
@@ -9373,17 +9389,20 @@ int mpg_distance_batch_req(mpg_world* w, const double* q, int64_t n, int32_t n_s
   hipLaunchKernelGGL((pose_kernel<false>), dim3(grid), dim3(128), 0, s, w->dw, qin, (long long)n, D.poses, D.save64);
   HIP_TRY(hipGetLastError());
   auto launch = [&](auto kern) {
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(128), 0, s, w->dw, D.poses, (long long)n, n_self_pairs, tol, ds, ps, dd,
-                       po, qs, qo);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(128), 0, s, w->dw, D.poses, (long long)n, n_self_pairs, tol, dtol, ds,
+                       ps, dd, po, qs, qo);
     return hipGetLastError();
   };
-  constexpr int P = MPG_DIST_POINTS, SG = MPG_DIST_SIGNED, NPF = MPG_DIST_NP;
+  constexpr int P = MPG_DIST_POINTS, SG = MPG_DIST_SIGNED, NPF = MPG_DIST_NP, IN = MPG_DIST_INDEP;
   switch (mode) {
     case 0: HIP_TRY(launch(distance_kernel<0>)); break;
     case P: HIP_TRY(launch(distance_kernel<P>)); break;
     case P | NPF: HIP_TRY(launch(distance_kernel<P | NPF>)); break;
     case P | SG: HIP_TRY(launch(distance_kernel<P | SG>)); break;
-    default: HIP_TRY(launch(distance_kernel<P | SG | NPF>)); break;
+    case P | SG | NPF: HIP_TRY(launch(distance_kernel<P | SG | NPF>)); break;
+    case IN: HIP_TRY(launch(distance_kernel<IN>)); break;
+    case P | IN: HIP_TRY(launch(distance_kernel<P | IN>)); break;
+    default: HIP_TRY(launch(distance_kernel<P | NPF | IN>)); break;
   }
   if (mode & SG) {  // EPAs past the private polytope: again with a big one from the pool
     if ((rc = grow((void**)&D.big, D.big_cap, sizeof(ccdx::BigPolytope) * kBigPool))) return rc;
@@ -9393,8 +9412,8 @@ int mpg_distance_batch_req(mpg_world* w, const double* q, int64_t n, int32_t n_s
                        D.list);
     HIP_TRY(hipGetLastError());
     auto redo = [&](auto kern) {
-      hipLaunchKernelGGL(kern, dim3(1), dim3(kBigPool), 0, s, w->dw, D.poses, (long long)n, n_self_pairs, tol, ds, ps,
-                         dd, po, qs, qo, D.big, D.list);
+      hipLaunchKernelGGL(kern, dim3(1), dim3(kBigPool), 0, s, w->dw, D.poses, (long long)n, n_self_pairs, tol, dtol,
+                         ds, ps, dd, po, qs, qo, D.big, D.list);
       return hipGetLastError();
     };
     if (mode & NPF) HIP_TRY(redo(distance_redo_kernel<P | SG | NPF>));

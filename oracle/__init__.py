@@ -461,19 +461,21 @@ class OracleWorld:
         return ds, ps, do, po
 
     def distance_batch_ex(self, q: np.ndarray, signed: bool = False, nearest_points: bool = False,
-                          distance_tolerance: float = 1e-6):
+                          distance_tolerance: float = 1e-6, indep: bool = False):
         """distance_batch with DistanceRequest(enable_signed_distance,
         enable_nearest_points, distance_tolerance): (d_self, pair_self,
         pts_self[n, 6], d_others, pair_others, pts_others[n, 6]); pts =
         DistanceResult::nearest_points of the group's minimum pair, world frame
         (oracle/collide_oracle.c pair_distance says which point is which).
-        RuntimeError where FCL throws (FCL_THROW_FAILED_AT_THIS_CONFIGURATION)."""
+        RuntimeError where FCL throws (FCL_THROW_FAILED_AT_THIS_CONFIGURATION).
+        indep: DistanceRequest(gjk_solver_type=GST_INDEP) -- FCL's own GJK
+        (fcl_gjk_indep.h gjk_indep_distance), unsigned shape pairs only."""
         q = np.ascontiguousarray(q, dtype=np.float64).reshape(-1, self.dof)
         n = q.shape[0]
         ds, do = np.zeros(n), np.zeros(n)
         ps, po = np.zeros(n, np.int32), np.zeros(n, np.int32)
         qs, qo = np.zeros((n, 6)), np.zeros((n, 6))
-        mode = (1 if signed else 0) | (2 if nearest_points else 0)
+        mode = (1 if signed else 0) | (2 if nearest_points else 0) | (4 if indep else 0)
         rc = lib().orc_distance_batch_ex(ctypes.byref(self._w), q.ctypes.data_as(_DP), ctypes.c_long(n),
                                          ctypes.c_int(self.n_self_pairs), ctypes.c_int(mode),
                                          ctypes.c_double(distance_tolerance),

@@ -3302,8 +3302,16 @@ static int mesh_octree_distance(const orc_world *w, int gm, const real *TM, int 
 static int pair_distance(const orc_world *w, int ga, const real *Ta, int gb, const real *Tb, int mode, double dist_tol,
                          double *d, double pts[6]) {
     const int ta = w->geom_type[ga], tb = w->geom_type[gb];
-    const int sgn = mode & 1, np = (mode >> 1) & 1;
+    const int sgn = mode & 1, np = (mode >> 1) & 1, indep = (mode >> 2) & 1;
     memset(pts, 0, 6 * sizeof(double));
+    if (indep) { /* GST_INDEP: shape pairs only, unsigned (the callers refuse the rest) */
+        if (sgn || ta == GEOM_MESH || tb == GEOM_MESH || ta == GEOM_OCTREE || tb == GEOM_OCTREE) return -2;
+        if (cf_shape_distance(ta, w->geom_param + 4 * ga, Ta, tb, w->geom_param + 4 * gb, Tb, d, pts, pts + 3)) {
+            if (*d == -1.0) memset(pts, 0, 6 * sizeof(double));
+            return 0;
+        }
+        return gjk_indep_distance(w, ga, Ta, gb, Tb, dist_tol, d, pts, pts + 3);
+    }
     if (ta == GEOM_MESH && tb == GEOM_MESH) {
         double pa[3], pb[3];
         *d = mesh_mesh_distance(w, ga, Ta, gb, Tb, pa, pb);

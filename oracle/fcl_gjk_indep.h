@@ -283,8 +283,11 @@ static void gjk_append(gjk_state *g, gsimplex *s, gv3 v) {
 
 static void gjk_remove(gjk_state *g, gsimplex *s) { g->free_v[g->nfree++] = s->c[--s->rank]; }
 
-/* GJK<S>::evaluate -> status */
-static int gjk_evaluate(const gmink *shape, gv3 guess, real tolerance, unsigned max_iterations) {
+/* the simplex GJK<S>::evaluate leaves (getSimplex()): directions and weights */
+typedef struct { int rank; gv3 d[4]; real p[4]; } gsimplex_out;
+
+/* GJK<S>::evaluate -> status; *out (may be NULL) = simplices[current] at exit */
+static int gjk_evaluate(const gmink *shape, gv3 guess, real tolerance, unsigned max_iterations, gsimplex_out *out) {
     gjk_state g;
     unsigned iterations = 0;
     real alpha = 0;
@@ -354,6 +357,14 @@ static int gjk_evaluate(const gmink *shape, gv3 guess, real tolerance, unsigned 
         }
         status = ((++iterations) < max_iterations) ? status : GJK_FAILED;
     } while (status == GJK_VALID);
+    if (out) {
+        const gsimplex *fin = &g.simplices[current];
+        out->rank = fin->rank;
+        for (int i = 0; i < fin->rank; ++i) {
+            out->d[i] = fin->c[i]->d;
+            out->p[i] = fin->p[i];
+        }
+    }
     return status;
 }
 
@@ -371,8 +382,7 @@ static void gshape_of(const orc_world *w, int geom, gshape *sh) {
     }
 }
 
-/* GJKSolver_indep::shapeIntersect (generic): 1 = collision */
-static int gjk_indep_intersect(const orc_world *w, int ga, const real *T1, int gb, const real *T2, real tolerance) {
+static void gmink_of(const orc_world *w, int ga, const real *T1, int gb, const real *T2, gmink *mp) {
     gmink m;
     gshape_of(w, ga, &m.s[0]);
     gshape_of(w, gb, &m.s[1]);
@@ -388,7 +398,46 @@ static int gjk_indep_intersect(const orc_world *w, int ga, const real *T1, int g
         const real inv_t = -((T1[i] * T1[9] + T1[3 + i] * T1[10]) + T1[6 + i] * T1[11]);
         m.toshape0_t[i] = ((T1[i] * T2[9] + T1[3 + i] * T2[10]) + T1[6 + i] * T2[11]) + inv_t;
     }
-    return gjk_evaluate(&m, gv(-1.0, 0.0, 0.0), tolerance, 128u) == GJK_INSIDE;
+    *mp = m;
+}
+
+/* GJKSolver_indep::shapeIntersect (generic): 1 = collision */
+static int gjk_indep_intersect(const orc_world *w, int ga, const real *T1, int gb, const real *T2, real tolerance) {
+    gmink m;
+    gmink_of(w, ga, T1, gb, T2, &m);
+    return gjk_evaluate(&m, gv(-1.0, 0.0, 0.0), tolerance, 128u, NULL) == GJK_INSIDE;
+}
+
+/* GJKSolver_indep::shapeDistance (generic, ShapeDistanceIndepImpl): GJK with
+ * gjk_tolerance = the request's distance_tolerance; Valid -> w0 = sum p_i
+ * support0(d_i), w1 = sum p_i support1(-d_i) (shape 1's frame), distance
+ * |w0 - w1|, points tf1 * w0, tf1 * w1; otherwise distance -1 and the points
+ * left as the traversal initialised them (zero).  Returns 0. */
+static int gjk_indep_distance(const orc_world *w, int ga, const real *T1, int gb, const real *T2, real tolerance,
+                              double *dist, double p1[3], double p2[3]) {
+    gmink m;
+    gsimplex_out s;
+    gmink_of(w, ga, T1, gb, T2, &m);
+    memset(p1, 0, 3 * sizeof(double));
+    memset(p2, 0, 3 * sizeof(double));
+    if (gjk_evaluate(&m, gv(-1.0, 0.0, 0.0), tolerance, 128u, &s) != GJK_VALID) {
+        *dist = -1.0;
+        return 0;
+    }
+    gv3 w0 = gv(0, 0, 0), w1 = gv(0, 0, 0);
+    for (int i = 0; i < s.rank; ++i) {
+        const gv3 a = gjk_shape_support(&m.s[0], s.d[i]);
+        const gv3 l1 = gjk_shape_support(&m.s[1], gmatv(m.toshape1, gscale(s.d[i], -1.0)));
+        const gv3 b = gadd(gmatv(m.toshape0_R, l1), gv(m.toshape0_t[0], m.toshape0_t[1], m.toshape0_t[2]));
+        w0 = gadd(w0, gscale(a, s.p[i]));
+        w1 = gadd(w1, gscale(b, s.p[i]));
+    }
+    *dist = sqrt(gnorm2(gsub(w0, w1)));
+    for (int i = 0; i < 3; ++i) {
+        p1[i] = ((T1[3 * i] * w0.v[0] + T1[3 * i + 1] * w0.v[1]) + T1[3 * i + 2] * w0.v[2]) + T1[9 + i];
+        p2[i] = ((T1[3 * i] * w1.v[0] + T1[3 * i + 1] * w1.v[1]) + T1[3 * i + 2] * w1.v[2]) + T1[9 + i];
+    }
+    return 0;
 }
 
 #endif

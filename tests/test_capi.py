@@ -73,7 +73,7 @@ def test_unsupported_geometry_rejected():
         _create(a)
     b = _desc(ow)
     b["geom_type"] = list(b["geom_type"])
-    b["geom_type"][b["static_geom"][0]] = 9
+    b["geom_type"][b["static_geom"][0]] = 42
     with pytest.raises(NotImplementedError, match="unsupported geometry type"):
         _create(b)
 

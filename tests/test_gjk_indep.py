@@ -146,6 +146,44 @@ def test_gjk_indep_world_against_libccd():
         assert min(ds[0], do[0]) < 0.0187, (i, names[p])
 
 
+def test_gjk_indep_distance_known_answers():
+    """DistanceRequest(gjk_solver_type=GST_INDEP): FCL's own GJK in double
+    (ShapeDistanceIndepImpl) -- polytope gaps exact to rounding where
+    libccd's float GJK is off by ~1e-7, curved sides within GJK's tolerance
+    band, the nearest points |p1 - p2| = d apart, -1 and zero points for
+    penetration; closed-form pairs unchanged."""
+    import oracle
+    from oracle import model as M
+    w, (gc, gb, ge, gs) = _pair_world([_cube(), M.BoxGeom((1.0, 1.0, 1.0)), M.EllipsoidGeom((0.3, 0.2, 0.1)),
+                                       M.SphereGeom(0.2)])
+    P = ctypes.POINTER(ctypes.c_double)
+
+    def dist(ga, Ta, gb_, Tb, indep):
+        pts, st = np.zeros(6), ctypes.c_int(0)
+        d = oracle.lib().orc_distance_pair_ex(ctypes.byref(w._w), ga, np.ascontiguousarray(Ta).ctypes.data_as(P), gb_,
+                                              np.ascontiguousarray(Tb).ctypes.data_as(P), 4 if indep else 0,
+                                              ctypes.c_double(1e-6), pts.ctypes.data_as(P), ctypes.byref(st))
+        assert st.value == 0
+        return d, pts
+    # polytopes: exact to rounding; the ellipsoid's curved side within GJK's
+    # termination band (rl - alpha <= tolerance * rl)
+    for ga, Ta, gb_, Tb, gap, eps in [(gc, _T(), gc, _T(p=(1.3, 0.2, 0.1)), 0.3, 1e-12),
+                                      (gc, _T(), gb, _T(p=(0.0, 1.25, 0.0)), 0.25, 1e-12),
+                                      (ge, _T(), gb, _T(p=(0.9, 0.0, 0.0)), 0.1, 1e-6 * 0.1),
+                                      (gc, _T(), gc, _T(q=(np.cos(0.2), 0.0, 0.0, np.sin(0.2)), p=(1.8, 0.0, 0.0)),
+                                       None, None)]:
+        d, pts = dist(ga, Ta, gb_, Tb, True)
+        dl, _ = dist(ga, Ta, gb_, Tb, False)
+        assert abs(d - dl) < 1e-6
+        if gap is not None:
+            assert abs(d - gap) <= eps, (d, gap)
+        assert abs(np.linalg.norm(pts[:3] - pts[3:]) - d) < 1e-12
+    d, pts = dist(gc, _T(), gc, _T(p=(0.9, 0.0, 0.0)), True)
+    assert d == -1.0 and not pts.any()
+    # sphere - box keeps its closed form: identical to the libccd request's value
+    assert dist(gs, _T(), gb, _T(p=(0.0, 0.0, 0.9)), True)[0] == dist(gs, _T(), gb, _T(p=(0.0, 0.0, 0.9)), False)[0]
+
+
 # ------------------------------------------------------------------ GPU
 def _indep_worlds(cfg):
     import oracle
@@ -176,6 +214,45 @@ def test_device_gjk_indep_matches_oracle(cfg):
     f2, m2 = dw.collide_batch(q[:512])  # <= 1024: one small_kernel launch per class
     np.testing.assert_array_equal(f2, fo[:512])
     np.testing.assert_array_equal(m2, mo[:512])
+    dw.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg", [3, 4])
+def test_device_gjk_indep_distance_matches_oracle(cfg):
+    """GST_INDEP distances (mpg_distance_batch_req with
+    MPG_DISTANCE_GJK_INDEP) on 2000 configurations: every distance, argmin
+    pair and nearest point equal to the oracle's FCL-GJK restatement; they
+    differ from the libccd request's values only at float precision."""
+    import ctypes as ct
+    from mplib_amd import _capi as C
+    from mplib_amd import scenes
+    ow, dw = _indep_worlds(cfg)
+    _, art = scenes.world(cfg)
+    q = scenes.sample_states(art, 2000, 950 + cfg)
+    n = len(q)
+    ns = ow.n_self_pairs
+    for np_flag in (False, True):
+        rs, rps, rqs, ro, rpo, rqo = ow.distance_batch_ex(q, nearest_points=np_flag, indep=True)
+        req = C.DistanceRequest(flags=C.MPG_DISTANCE_GJK_INDEP | (C.MPG_DISTANCE_NEAREST_POINTS if np_flag else 0),
+                                distance_tolerance=1e-6)
+        ds, do = np.zeros(n), np.zeros(n)
+        ps, po = np.zeros(n, np.int32), np.zeros(n, np.int32)
+        qs, qo = np.zeros((n, 6)), np.zeros((n, 6))
+        v = lambda a: a.ctypes.data_as(ct.c_void_p)  # noqa: E731
+        C.check(C.lib().mpg_distance_batch_req(dw.handle, v(np.ascontiguousarray(q)), n, ns, ct.byref(req), v(ds),
+                                               v(ps), v(qs), v(do), v(po), v(qo), C.MPG_MEM_HOST, None),
+                "mpg_distance_batch_req")
+        np.testing.assert_array_equal(ds, rs)
+        np.testing.assert_array_equal(do, ro)
+        np.testing.assert_array_equal(ps, rps)
+        np.testing.assert_array_equal(po, rpo)
+        np.testing.assert_array_equal(qs, rqs)
+        np.testing.assert_array_equal(qo, rqo)
+    ls, _, _, lo, _, _ = ow.distance_batch_ex(q)
+    for a, b in ((ds, ls), (do, lo)):
+        np.testing.assert_array_equal(a == -1.0, b == -1.0)
+        assert np.abs(a - b).max() < 1e-5
     dw.close()
 
 

@@ -472,8 +472,9 @@ def test_scalar_distance_api():
         assert abs(o.min_distance - ro[i]) < 1e-9 and (o.link_name1, o.link_name2) == names[rpo[i]]
         assert s.distance_type == "self" and o.distance_type == "articulation_sceneobject"
         assert full.min_distance == min(s.min_distance, o.min_distance) == w.distance()
-    with pytest.raises(NotImplementedError):  # FCL's own GJK/EPA solver is not restated
-        w.self_distance(pymp.fcl.DistanceRequest(gjk_solver_type=pymp.fcl.GJKSolverType.GST_INDEP))
+    with pytest.raises(NotImplementedError):  # FCL's own EPA (GST_INDEP signed) is not restated
+        w.self_distance(pymp.fcl.DistanceRequest(enable_signed_distance=True,
+                                                 gjk_solver_type=pymp.fcl.GJKSolverType.GST_INDEP))
 
 
 def test_fcl_distance_free_function():

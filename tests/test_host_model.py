@@ -96,12 +96,14 @@ def test_unsupported_requests_raise():
     w, _ = scenes.world(2)
     with pytest.raises(NotImplementedError):
         w.collide(pymp.fcl.CollisionRequest(enable_cost=True))
-    # GST_INDEP collides on the device since round 6 (tests/test_gjk_indep.py);
-    # its EPA contacts and distances are not restated
+    # GST_INDEP collides and measures unsigned distances on the device since
+    # round 6 (tests/test_gjk_indep.py); its EPA (contacts, signed distances)
+    # is not restated
     with pytest.raises(NotImplementedError):
         w.collide(pymp.fcl.CollisionRequest(enable_contact=True, gjk_solver_type=pymp.fcl.GJKSolverType.GST_INDEP))
     with pytest.raises(NotImplementedError):
-        w.distance_full(pymp.fcl.DistanceRequest(gjk_solver_type=pymp.fcl.GJKSolverType.GST_INDEP))
+        w.distance_full(pymp.fcl.DistanceRequest(enable_signed_distance=True,
+                                                 gjk_solver_type=pymp.fcl.GJKSolverType.GST_INDEP))
 
 
 def test_set_qpos_validation(art):
