@@ -184,6 +184,33 @@ def test_gjk_indep_distance_known_answers():
     assert dist(gs, _T(), gb, _T(p=(0.0, 0.0, 0.9)), True)[0] == dist(gs, _T(), gb, _T(p=(0.0, 0.0, 0.9)), False)[0]
 
 
+def test_gjk_indep_world_distance_is_exact():
+    """cfg4 (hull obstacles), the others group's minimum with GST_INDEP
+    against an exact QP distance of the two posed hulls: FCL's double GJK
+    agrees to 1e-12 where libccd's float GJK is off by up to ~1.5 mm."""
+    import oracle
+    from mplib_amd import scenes
+    from test_oracle import _qp_distance
+    base = Wd.oracle_world(4)
+    ow = oracle.OracleWorld(base.art, scene=base.scene, gjk_solver="indep")
+    _, art = scenes.world(4)
+    q = scenes.sample_states(art, 200, 954)
+    _, _, _, ro, rpo, _ = ow.distance_batch_ex(q, indep=True)
+    _, _, _, lo, _, _ = ow.distance_batch_ex(q)
+    _, objT = ow.fk_batch(q)
+    ok = np.nonzero(ro > 0)[0]
+    worst = ok[np.argsort(np.abs(ro - lo)[ok])[-3:]]  # where the two solvers differ most
+    for i in worst:
+        _, ia, _, ib, _, _ = ow.pairs[rpo[i]]
+        T = objT[i, ia]
+        VA = np.asarray(ow.art.objects[ia].geom.vertices) @ T[:9].reshape(3, 3).T + T[9:]
+        _, gb, (Rb, tb) = ow.scene[ib]
+        VB = np.asarray(gb.vertices) @ np.asarray(Rb).reshape(3, 3).T + np.asarray(tb)
+        d = _qp_distance(VA, VB)
+        assert abs(ro[i] - d) < 1e-9, (i, ro[i], d)
+    assert np.abs(ro - lo)[ok].max() > 1e-5  # the float solver's error the double one avoids
+
+
 # ------------------------------------------------------------------ GPU
 def _indep_worlds(cfg):
     import oracle
@@ -222,8 +249,7 @@ def test_device_gjk_indep_matches_oracle(cfg):
 def test_device_gjk_indep_distance_matches_oracle(cfg):
     """GST_INDEP distances (mpg_distance_batch_req with
     MPG_DISTANCE_GJK_INDEP) on 2000 configurations: every distance, argmin
-    pair and nearest point equal to the oracle's FCL-GJK restatement; they
-    differ from the libccd request's values only at float precision."""
+    pair and nearest point equal to the oracle's FCL-GJK restatement."""
     import ctypes as ct
     from mplib_amd import _capi as C
     from mplib_amd import scenes
@@ -251,8 +277,15 @@ def test_device_gjk_indep_distance_matches_oracle(cfg):
         np.testing.assert_array_equal(qo, rqo)
     ls, _, _, lo, _, _ = ow.distance_batch_ex(q)
     for a, b in ((ds, ls), (do, lo)):
-        np.testing.assert_array_equal(a == -1.0, b == -1.0)
-        assert np.abs(a - b).max() < 1e-5
+        # penetration (-1) can differ only for shapes within libccd's float
+        # false-hit reach (1.86 cm, as collide's MPR; measured: 0.2-1.3 mm)
+        odd = (a == -1.0) != (b == -1.0)
+        assert (np.maximum(a, b)[odd] < 0.0187).all()
+        # libccd's float GJK distance is off by up to ~1.5 mm on these hull
+        # pairs (FCL's own GJK matches an exact QP to 1e-15:
+        # test_gjk_indep_world_distance_is_exact)
+        both = ~odd & (a != -1.0)
+        assert np.abs(a - b)[both].max() < 2e-3
     dw.close()
 
 
