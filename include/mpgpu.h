@@ -94,8 +94,9 @@ extern "C" {
 #define MPG_GEOM_CAPSULE 3  /* fcl::Capsule  : param = radius, lz            */
 #define MPG_GEOM_CYLINDER 4 /* fcl::Cylinder : param = radius, lz            */
 #define MPG_GEOM_OCTREE 5   /* fcl::OcTree   : param = first leaf, leaf count,
-                               resolution; static, on a link or attached
-                               (not paired with another OcTree)         */
+                               resolution; static, on a link or attached;
+                               a pair of two OcTrees collides (leaf OBBs),
+                               its contacts / distance are refused      */
 #define MPG_GEOM_MESH 6     /* fcl::BVHModel<OBBRSS> (non-convex mesh):
                                vertices, param = first triangle, triangle
                                count (mesh_triangle)                     */

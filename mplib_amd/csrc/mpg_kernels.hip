@@ -1948,6 +1948,89 @@ __device__ __forceinline__ bool octree_wave(const DevWorld& w, cptr<double> HV, 
   return octree_range_any(w, go, blo, bhi, leaf_hit);
 }
 
+// fcl OcTreeSolver::OcTreeIntersectRecurse [ext FCL 0.7.0] without contacts
+// or costs, reduced to its result: some occupied leaf of tree 1 (the pair's
+// o1) whose OBB overlaps some occupied leaf's OBB of tree 2 -- no box test
+// (oracle octree_octree_intersect).  The wave takes tree 1's leaves 64 at a
+// time, one per lane; a lane lists tree 2's leaves in the grid cells under
+// the box obbDisjoint's tree-2 axis tests leave open (centre R2^T (c1 - p2),
+// half extents sum_i (|R_ik| + 1e-6) a_i, padded far above rounding) and
+// runs obbDisjoint(R1^T R2, R1^T (c2 - c1), a1, a2) on each.  Wave-uniform
+// inputs.
+__device__ bool octree_octree_wave(const DevWorld& w, int g1, const SE3& T1, int g2, const SE3& T2) {
+  const cptr<double> r1 = w.geom_rec + G_STRIDE * g1;
+  const long long l0 = (long long)r1[G_PARAM], l1 = l0 + (long long)r1[G_PARAM + 1];
+  double R[9];
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) R[3 * i + j] = (T1.R[i] * T2.R[j] + T1.R[3 + i] * T2.R[3 + j]) + T1.R[6 + i] * T2.R[6 + j];
+  const cptr<double> og = w.oct_grid + OG_STRIDE * g2;
+  const double inv = og[OG_INV];
+  const int dims[3] = {(int)og[OG_DIMS], (int)og[OG_DIMS + 1], (int)og[OG_DIMS + 2]};
+  const int cell0 = (int)og[OG_CELL0];
+  for (long long base = l0; base < l1; base += 64) {
+    const long long la = base + (long long)lane_id();
+    bool hit = false;
+    if (la < l1) {
+      const cptr<double> L = w.oct_leaf + 6 * (size_t)la;
+      double a[3], cw[3];
+      {
+        double c[3];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+          c[k] = (L[k] + L[3 + k]) * 0.5;
+          a[k] = (L[3 + k] - L[k]) * 0.5;
+        }
+#pragma unroll
+        for (int i = 0; i < 3; ++i) cw[i] = ((T1.R[3 * i] * c[0] + T1.R[3 * i + 1] * c[1]) + T1.R[3 * i + 2] * c[2]) + T1.p[i];
+      }
+      const double dq[3] = {cw[0] - T2.p[0], cw[1] - T2.p[1], cw[2] - T2.p[2]};
+      double blo[3], bhi[3];
+      int c0[3], c1[3];
+      bool empty = false;
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        const double q = (T2.R[k] * dq[0] + T2.R[3 + k] * dq[1]) + T2.R[6 + k] * dq[2];
+        const double h = ((std::fabs(R[k]) + 1e-6) * a[0] + (std::fabs(R[3 + k]) + 1e-6) * a[1] +
+                          (std::fabs(R[6 + k]) + 1e-6) * a[2]) * (1.0 + 1e-9) + 1e-9 * (1.0 + std::fabs(q));
+        blo[k] = q - h;
+        bhi[k] = q + h;
+        const double f0 = std::floor((blo[k] - og[OG_ORIGIN + k]) * inv);
+        const double f1 = std::floor((bhi[k] - og[OG_ORIGIN + k]) * inv);
+        empty |= f1 < 0.0 || f0 >= (double)dims[k];
+        c0[k] = f0 < 0.0 ? 0 : (int)fmin(f0, (double)(dims[k] - 1));
+        c1[k] = f1 >= (double)dims[k] ? dims[k] - 1 : (f1 < 0.0 ? 0 : (int)f1);
+      }
+      for (int x = c0[0]; !empty && !hit && x <= c1[0]; ++x)
+        for (int y = c0[1]; !hit && y <= c1[1]; ++y)
+          for (int z = c0[2]; !hit && z <= c1[2]; ++z) {
+            const int cell = cell0 + (x * dims[1] + y) * dims[2] + z;
+            for (int k = w.oct_cells[cell], ke = w.oct_cells[cell + 1]; k < ke && !hit; ++k) {
+              const cptr<double> K = w.oct_leaf + 6 * (size_t)w.oct_list[k];
+              bool out = false;
+#pragma unroll
+              for (int i = 0; i < 3; ++i) out |= K[i] > bhi[i] || K[3 + i] < blo[i];
+              if (out) continue;
+              double b[3], d[3], t[3], T[3];
+#pragma unroll
+              for (int i = 0; i < 3; ++i) {
+                d[i] = (K[i] + K[3 + i]) * 0.5;
+                b[i] = (K[3 + i] - K[i]) * 0.5;
+              }
+#pragma unroll
+              for (int i = 0; i < 3; ++i)
+                t[i] = (((T2.R[3 * i] * d[0] + T2.R[3 * i + 1] * d[1]) + T2.R[3 * i + 2] * d[2]) + T2.p[i]) - cw[i];
+#pragma unroll
+              for (int i = 0; i < 3; ++i) T[i] = (T1.R[i] * t[0] + T1.R[3 + i] * t[1]) + T1.R[6 + i] * t[2];
+              hit = !obb_disjoint(R, T, a, b);
+            }
+          }
+    }
+    if (__ballot(hit) != 0) return true;
+  }
+  return false;
+}
 
 // ---------------------------------------------------------------------------
 // BVH meshes (fcl::BVHModel<OBBRSS>, load_mesh_as_BVH src/urdf_utils.cpp:
@@ -2641,7 +2724,9 @@ __device__ __forceinline__ unsigned long long walk_wave_eval(const DevWorld& w, 
       const int k = __builtin_ctzll(todo);
       todo &= todo - 1;
       const SE3 A = bcast_se3(TA, k), B = bcast_se3(TB, k);
-      const bool h = tga == MPG_GEOM_OCTREE ? octree_wave(w, HV, ga, A, gb, B) : octree_wave(w, HV, gb, B, ga, A);
+      const bool h = tga == MPG_GEOM_OCTREE && tgb == MPG_GEOM_OCTREE ? octree_octree_wave(w, ga, A, gb, B)
+                     : tga == MPG_GEOM_OCTREE                         ? octree_wave(w, HV, ga, A, gb, B)
+                                                                      : octree_wave(w, HV, gb, B, ga, A);
       if (h) hits |= 1ull << k;
     }
     return hits;
@@ -6629,6 +6714,7 @@ struct mpg_world {
   bool has_mesh = false;         // a non-allowed pair involves a BVH mesh
   bool any_mesh = false;         // some pair involves a BVH mesh
   bool any_gjk = false;          // GST_INDEP world: some pair runs FCL's own GJK (CF_GJK)
+  bool has_octree2 = false;      // a non-allowed pair of two OcTrees
   // batched distance buffers (grow-only)
   struct Dist {
     double* poses = nullptr;
@@ -6924,11 +7010,8 @@ int validate(const mpg_world_desc* d) {
     if (a < 0 || a >= nobj || b < 0 || b >= nobj) return set_error(MPG_E_INVALID, "pair object id out of range");
     if (a >= d->n_moving && b >= d->n_moving) return set_error(MPG_E_INVALID, "static-static pair");
     // an OcTree may ride on a link or an attached body (attachObject takes any
-    // FCL geometry, planning_world.cpp:174-191); octree x octree
-    // (OcTreeIntersect) is not restated
-    if (!(d->pair_allowed && d->pair_allowed[p]) && obj_geom_type(d, a) == MPG_GEOM_OCTREE &&
-        obj_geom_type(d, b) == MPG_GEOM_OCTREE)
-      return set_error(MPG_E_UNSUPPORTED, "a pair of two OcTrees is not implemented");
+    // FCL geometry, planning_world.cpp:174-191), and meet another OcTree
+    // (octree_octree_wave; its contacts and distance are refused per call)
     // FCL 0.7.0 GJKSolver_libccd: box-box, sphere-sphere, sphere-box,
     // sphere-capsule and sphere-cylinder have closed forms (all on the
     // device, closed_form_kind); every other shape pair is MPR
@@ -8409,6 +8492,8 @@ int mpg_world_create(const mpg_world_desc* d, int device, mpg_world** out) {
     w->has_mesh |= pair_cf[p] == CF_MESH && !allowed[p];
     w->any_mesh |= pair_cf[p] == CF_MESH;
     w->any_gjk |= pair_cf[p] == CF_GJK;
+    w->has_octree2 |= !allowed[p] && obj_geom_type(d, d->pair_a[p]) == MPG_GEOM_OCTREE &&
+                      obj_geom_type(d, d->pair_b[p]) == MPG_GEOM_OCTREE;
   }
   dw.static_T = to_cptr<double>(base + o_sT);
   dw.link_chain_start = to_cptr<int>(base + o_cs);
@@ -9343,6 +9428,8 @@ int mpg_distance_batch_req(mpg_world* w, const double* q, int64_t n, int32_t n_s
   if (flags & ~(MPG_DISTANCE_SIGNED | MPG_DISTANCE_NEAREST_POINTS | MPG_DISTANCE_GJK_INDEP))
     return set_error(MPG_E_INVALID, "bad flags");
   if (!(req->distance_tolerance >= 0.0)) return set_error(MPG_E_INVALID, "bad distance_tolerance");
+  if (w->has_octree2)
+    return set_error(MPG_E_UNSUPPORTED, "distance for a pair of two OcTrees (OcTreeDistanceRecurse) is not implemented");
   const bool indep = (flags & MPG_DISTANCE_GJK_INDEP) != 0;
   if (indep && (flags & MPG_DISTANCE_SIGNED))
     return set_error(MPG_E_UNSUPPORTED, "signed distance with GST_INDEP (FCL's EPA) is not implemented");
@@ -9453,6 +9540,8 @@ int mpg_collide_contacts(mpg_world* w, const double* input, int64_t n, int input
   if (mem != MPG_MEM_HOST && mem != MPG_MEM_DEVICE) return set_error(MPG_E_INVALID, "bad mem kind");
   if (w->any_gjk)
     return set_error(MPG_E_UNSUPPORTED, "contacts with gjk_solver MPG_GJK_INDEP (FCL's EPA) are not implemented");
+  if (w->has_octree2)
+    return set_error(MPG_E_UNSUPPORTED, "contacts for a pair of two OcTrees are not implemented");
   if (w->octree_first)  // contact_kernel reports the (shape, octree) order PlanningWorld uses
     return set_error(MPG_E_UNSUPPORTED, "contacts for a pair whose first object is an OcTree are not implemented");
   if (n == 0) return MPG_OK;

@@ -1778,6 +1778,62 @@ static int octree_intersect(const orc_world *w, int go, const real *TO, int gs, 
     return 0;
 }
 
+/* fcl::collide(OcTree, OcTree) -> OcTreeSolver::OcTreeIntersectRecurse
+ * [ext FCL 0.7.0] without contacts or costs: a pair of occupied leaves
+ * collides as soon as their OBBs overlap (convertBV(leaf AABB, tf): axes
+ * R, centre tf * c, extent (max - min) * 0.5; OBB::overlap = !obbDisjoint(
+ * R1^T R2, R1^T (c2 - c1), a1, a2)) -- no box test.  An inner node's box
+ * contains its leaves' (obbDisjoint's widening shrinks with the extents),
+ * and an inner node is occupied when a leaf under it is, so the recursion's
+ * pruning never hides a leaf pair this test accepts. */
+/* the union box of an octree's leaves in its frame (an inner node's box in
+ * spirit: every leaf OBB lies inside it) -- only to skip work below */
+static void octree_union(const orc_world *w, int g, real c[3], real e[3]) {
+    const int l0 = (int)w->geom_param[4 * g], ln = (int)w->geom_param[4 * g + 1];
+    real lo[3] = {1e300, 1e300, 1e300}, hi[3] = {-1e300, -1e300, -1e300};
+    for (int l = l0; l < l0 + ln; ++l)
+        for (int k = 0; k < 3; ++k) {
+            lo[k] = fmin(lo[k], w->oct_leaf[6 * (size_t)l + k]);
+            hi[k] = fmax(hi[k], w->oct_leaf[6 * (size_t)l + 3 + k]);
+        }
+    for (int k = 0; k < 3; ++k) { c[k] = (lo[k] + hi[k]) * 0.5; e[k] = (hi[k] - lo[k]) * 0.5 * (1 + 1e-9) + 1e-9; }
+}
+
+static int octree_octree_intersect(const orc_world *w, int g1, const real *T1, int g2, const real *T2) {
+    const int a0 = (int)w->geom_param[4 * g1], an = (int)w->geom_param[4 * g1 + 1];
+    const int b0 = (int)w->geom_param[4 * g2], bn = (int)w->geom_param[4 * g2 + 1];
+    real B[9], uc[3], ue[3], ucw[3];
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) B[3 * i + j] = (T1[i] * T2[j] + T1[3 + i] * T2[3 + j]) + T1[6 + i] * T2[6 + j];
+    octree_union(w, g2, uc, ue);
+    for (int i = 0; i < 3; ++i) ucw[i] = ((T2[3 * i] * uc[0] + T2[3 * i + 1] * uc[1]) + T2[3 * i + 2] * uc[2]) + T2[9 + i];
+    for (int la = a0; la < a0 + an; ++la) {
+        const real *L = w->oct_leaf + 6 * (size_t)la;
+        real c[3], a[3], cw[3];
+        for (int k = 0; k < 3; ++k) { c[k] = (L[k] + L[3 + k]) * 0.5; a[k] = (L[3 + k] - L[k]) * 0.5; }
+        for (int i = 0; i < 3; ++i) cw[i] = ((T1[3 * i] * c[0] + T1[3 * i + 1] * c[1]) + T1[3 * i + 2] * c[2]) + T1[9 + i];
+        {   /* tree 2's union box apart from this leaf (with the test's own
+             * widening): no leaf of tree 2 can overlap it */
+            real t[3], T[3], ea[3];
+            for (int i = 0; i < 3; ++i) t[i] = ucw[i] - cw[i];
+            for (int i = 0; i < 3; ++i) T[i] = (T1[i] * t[0] + T1[3 + i] * t[1]) + T1[6 + i] * t[2];
+            for (int k = 0; k < 3; ++k) ea[k] = a[k] * (1 + 1e-9) + 1e-9;
+            if (obb_disjoint(B, T, ea, ue)) continue;
+        }
+        for (int lb = b0; lb < b0 + bn; ++lb) {
+            const real *K = w->oct_leaf + 6 * (size_t)lb;
+            real d[3], b[3], dw[3], t[3], T[3];
+            for (int k = 0; k < 3; ++k) { d[k] = (K[k] + K[3 + k]) * 0.5; b[k] = (K[3 + k] - K[k]) * 0.5; }
+            for (int i = 0; i < 3; ++i)
+                dw[i] = ((T2[3 * i] * d[0] + T2[3 * i + 1] * d[1]) + T2[3 * i + 2] * d[2]) + T2[9 + i];
+            for (int i = 0; i < 3; ++i) t[i] = dw[i] - cw[i];
+            for (int i = 0; i < 3; ++i) T[i] = (T1[i] * t[0] + T1[3 + i] * t[1]) + T1[6 + i] * t[2];
+            if (!obb_disjoint(B, T, a, b)) return 1;
+        }
+    }
+    return 0;
+}
+
 /* CollisionRequest(enable_contact=True) on a (shape, OcTree) pair
  * [ext FCL 0.7.0 OcTreeShapeIntersectRecurse with contacts]: the traversal
  * stops at the first occupied leaf (children in order) whose OBB overlaps
@@ -2879,6 +2935,8 @@ static int collide_one(const orc_world *w, const real *q, uint32_t *mask, int W,
         }
         int hit = mesh_intersect(w, gs[0], Ts[0], gs[1], Ts[1], st);
         if (hit >= 0) {}
+        else if (w->geom_type[gs[0]] == GEOM_OCTREE && w->geom_type[gs[1]] == GEOM_OCTREE)
+            hit = octree_octree_intersect(w, gs[0], Ts[0], gs[1], Ts[1]);
         else if (w->geom_type[gs[1]] == GEOM_OCTREE) hit = octree_intersect(w, gs[1], Ts[1], gs[0], Ts[0], st);
         else if (w->geom_type[gs[0]] == GEOM_OCTREE) hit = octree_intersect(w, gs[0], Ts[0], gs[1], Ts[1], st);
         else hit = closed_form_intersect(w, gs[0], Ts[0], gs[1], Ts[1]);
@@ -3540,6 +3598,7 @@ double orc_distance_pair(const orc_world *w, int ga, const double *Ta, int gb, c
 int orc_collide_pair(const orc_world *w, int ga, const double *Ta, int gb, const double *Tb) {
     const int mh = mesh_intersect(w, ga, Ta, gb, Tb, NULL);
     if (mh >= 0) return mh;
+    if (w->geom_type[ga] == GEOM_OCTREE && w->geom_type[gb] == GEOM_OCTREE) return octree_octree_intersect(w, ga, Ta, gb, Tb);
     if (w->geom_type[gb] == GEOM_OCTREE) return octree_intersect(w, gb, Tb, ga, Ta, NULL);
     if (w->geom_type[ga] == GEOM_OCTREE) return octree_intersect(w, ga, Ta, gb, Tb, NULL);
     const int cf = closed_form_intersect(w, ga, Ta, gb, Tb);

@@ -59,18 +59,10 @@ def test_invalid_descriptor_rejected(field, value, msg):
 
 
 def test_unsupported_geometry_rejected():
-    """An OcTree may ride on a link or an attached body (round 6), but a
-    non-allowed pair of two OcTrees (FCL's OcTreeIntersect) is refused at
-    world creation, never approximated; so is an unknown geometry kind."""
+    """An unknown geometry kind is refused at world creation, never
+    approximated (OcTrees on links, attached bodies and against each other
+    are accepted since round 6)."""
     ow = Wd.oracle_world(3)
-    a = _desc(ow)
-    a["geom_type"] = list(a["geom_type"])
-    a["geom_param"] = list(a["geom_param"])
-    for g in (a["moving_geom"][1], a["static_geom"][0]):  # panda_link1 and the table
-        a["geom_type"][g] = 5  # MPG_GEOM_OCTREE with an empty leaf range
-        a["geom_param"][4 * g:4 * g + 3] = [0.0, 0.0, 0.01]
-    with pytest.raises(NotImplementedError, match="OcTree"):
-        _create(a)
     b = _desc(ow)
     b["geom_type"] = list(b["geom_type"])
     b["geom_type"][b["static_geom"][0]] = 42
