@@ -371,6 +371,12 @@ int DescBuilder::add_geometry(const CollisionGeometry* g) {
     if (geoms[i] == g) return (int)i;
   if (g->type < 0)
     throw std::logic_error("NotImplemented: geometry '" + g->kind + "' is not supported by the device collider");
+  // FCL's shape traversal reports a pair only when both geometries are
+  // occupied (cost_density >= threshold_occupied, ShapeCollisionTraversalNode::
+  // leafTesting); the device assumes that (every geometry's default)
+  if (!(g->cost_density >= g->threshold_occupied))
+    throw std::logic_error("NotImplemented: geometry '" + g->kind +
+                           "' with cost_density below its occupancy threshold (FCL's free / uncertain geometry)");
   geoms.push_back(g);
   geom_type.push_back(g->type);
   double prm[4] = {0, 0, 0, 0};

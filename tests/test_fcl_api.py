@@ -117,6 +117,10 @@ def test_occupancy_and_octree_box():
     assert not g.isOccupied() and not g.isFree() and g.isUncertain()
     g.cost_density = 0.0
     assert g.isFree()
+    # FCL skips pairs whose geometry is not occupied; the device refuses them
+    other = fcl.CollisionObject(fcl.Box(1.0, 1.0, 1.0), [0, 0, 0], [1, 0, 0, 0])
+    with pytest.raises(NotImplementedError, match="cost_density"):
+        fcl.collide(fcl.CollisionObject(g, [0, 0, 0], [1, 0, 0, 0]), other)
     t = fcl.OcTree(0.01)
     t.computeLocalAABB()
     d = (1 << 16) * 0.01 / 2  # OcTree::getRootBV: (1 << depth) * resolution / 2
