@@ -420,6 +420,23 @@ class PinocchioModel {
   std::vector<std::string> get_chain_joint_name(const std::string& ee) const;
   std::vector<size_t> supports(int joint) const;
   int body_frame(const std::string& name) const;
+
+  // Jacobians and closed-loop IK on the host (kinjac.cpp; pinocchio_model.cpp:335-496)
+  std::vector<double> qpos_user2pin(const std::vector<double>& q) const;
+  std::vector<double> qpos_pin2user(const std::vector<double>& q) const;
+  std::vector<SE3> joint_frames(const std::vector<double>& qpin) const;  // oMi, [0] = universe
+  void compute_full_jacobian(const std::vector<double>& qpos);
+  std::vector<double> get_link_jacobian(size_t index, bool local) const;  // 6 x nv, row-major
+  std::vector<double> compute_single_link_local_jacobian(const std::vector<double>& qpos, size_t index);
+  struct IKResult {
+    std::vector<double> q;
+    bool success = false;
+    std::array<double, 6> err{};
+  };
+  // computeIKCLIK (mask, no limits) / computeIKCLIKJL (q_min / q_max, no mask)
+  IKResult ik_clik(size_t index, const Vec7& pose, const std::vector<double>& q_init, const std::vector<bool>* mask,
+                   const std::vector<double>* q_min, const std::vector<double>* q_max, double eps, int max_iter,
+                   double dt, double damp) const;
   int nq() const { return nq_; }
   int nv() const { return nv_; }
 
@@ -439,6 +456,12 @@ class PinocchioModel {
   void add_fixed(int parent_frame, const SE3& jp, const std::string& jname, const std::string& body);
   void dfs(const UrdfModel& urdf, const std::string& link);
   void ensure_fk_world() const;
+  std::vector<size_t> support_columns(int joint) const;
+  std::vector<double> user_columns(const std::vector<double>& Jpin) const;
+  std::vector<double> joint_local_jacobian(const std::vector<SE3>& oMi, int joint) const;
+  std::vector<SE3> jac_oMi_;        // compute_full_jacobian's joint frames
+  std::vector<double> jac_world_;   // ... and WORLD Jacobian, pinocchio columns
+  bool jac_valid_ = false;
 
   std::vector<PinJoint> joints_;  // [0] = universe
   std::vector<PinFrame> frames_;

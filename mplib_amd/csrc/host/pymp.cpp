@@ -57,6 +57,15 @@ py::array_t<double> mat33(const std::array<double, 9>& M) {
   return a;
 }
 
+py::array_t<double> mat6x(const std::vector<double>& J) {  // 6 x n row-major -> ndarray
+  const ssize_t n = (ssize_t)(J.size() / 6);
+  py::array_t<double> a({(ssize_t)6, n});
+  auto m = a.mutable_unchecked<2>();
+  for (ssize_t r = 0; r < 6; ++r)
+    for (ssize_t c = 0; c < n; ++c) m(r, c) = J[(size_t)r * n + c];
+  return a;
+}
+
 // fcl::Triangle: three vertex indices
 struct Triangle {
   std::array<size_t, 3> v{0, 0, 0};
@@ -677,6 +686,33 @@ PYBIND11_MODULE(pymp, m_all) {
            },
            py::arg("index"))
       .def("get_random_configuration", &PinocchioModel::get_random_configuration)
+      // Jacobians and CLIK IK (python/pybind_pinocchio.hpp:47-58), host side (kinjac.cpp)
+      .def("compute_full_jacobian", &PinocchioModel::compute_full_jacobian, py::arg("qpos"))
+      .def("get_link_jacobian",
+           [](const PinocchioModel& p, size_t i, bool local) { return mat6x(p.get_link_jacobian(i, local)); },
+           py::arg("index"), py::arg("local") = false)
+      .def("compute_single_link_local_jacobian",
+           [](PinocchioModel& p, const std::vector<double>& q, size_t i) {
+             return mat6x(p.compute_single_link_local_jacobian(q, i));
+           },
+           py::arg("qpos"), py::arg("index"))
+      .def("compute_IK_CLIK",
+           [](const PinocchioModel& p, size_t i, const std::vector<double>& pose, const std::vector<double>& q_init,
+              const std::vector<bool>& mask, double eps, int max_iter, double dt, double damp) {
+             const auto r = p.ik_clik(i, vec7_arg(pose), q_init, &mask, nullptr, nullptr, eps, max_iter, dt, damp);
+             return py::make_tuple(vec(r.q.data(), (int)r.q.size()), r.success, vec(r.err.data(), 6));
+           },
+           py::arg("index"), py::arg("pose"), py::arg("q_init"), py::arg("mask") = std::vector<bool>(),
+           py::arg("eps") = 1e-5, py::arg("maxIter") = 1000, py::arg("dt") = 1e-1, py::arg("damp") = 1e-12)
+      .def("compute_IK_CLIK_JL",
+           [](const PinocchioModel& p, size_t i, const std::vector<double>& pose, const std::vector<double>& q_init,
+              const std::vector<double>& q_min, const std::vector<double>& q_max, double eps, int max_iter, double dt,
+              double damp) {
+             const auto r = p.ik_clik(i, vec7_arg(pose), q_init, nullptr, &q_min, &q_max, eps, max_iter, dt, damp);
+             return py::make_tuple(vec(r.q.data(), (int)r.q.size()), r.success, vec(r.err.data(), 6));
+           },
+           py::arg("index"), py::arg("pose"), py::arg("q_init"), py::arg("q_min"), py::arg("q_max"),
+           py::arg("eps") = 1e-5, py::arg("maxIter") = 1000, py::arg("dt") = 1e-1, py::arg("damp") = 1e-12)
       .def("get_joint_names", &PinocchioModel::get_joint_names, py::arg("user") = true)
       .def("get_link_names", &PinocchioModel::get_link_names, py::arg("user") = true)
       .def("get_leaf_links", &PinocchioModel::get_leaf_links)
