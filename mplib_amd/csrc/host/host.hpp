@@ -16,6 +16,7 @@
 #include <optional>
 #include <stdexcept>
 #include <string>
+#include <tuple>
 #include <unordered_map>
 #include <utility>
 #include <vector>
@@ -421,6 +422,9 @@ class PinocchioModel {
   std::vector<size_t> supports(int joint) const;
   int body_frame(const std::string& name) const;
 
+  // PinocchioModelTpl::printFrames (pinocchio_model.cpp:165-185): the model's
+  // sizes, then "Frame i name parent_joint TYPE" per frame (kinjac.cpp)
+  void print_frames() const;
   // Jacobians and closed-loop IK on the host (kinjac.cpp; pinocchio_model.cpp:335-496)
   std::vector<double> qpos_user2pin(const std::vector<double>& q) const;
   std::vector<double> qpos_pin2user(const std::vector<double>& q) const;
@@ -482,6 +486,34 @@ class PinocchioModel {
 // ---------------------------------------------------------------------------
 // FCL model (reference src/fcl_model.{h,cpp})
 // ---------------------------------------------------------------------------
+// KDLModel (python/pybind_kdl.hpp, src/kdl_model.cpp): chain / tree IK over
+// the URDF's kinematic tree (kinjac.cpp); q vectors in joint_names order
+class KDLModel {
+ public:
+  KDLModel(const std::string& urdf, const std::vector<std::string>& joint_names,
+           const std::vector<std::string>& link_names, bool verbose);
+  const std::string& get_tree_root_name() const { return root_; }
+  // kind 0: ChainIkSolverPos_NR, 1: ..._NR_JL (qmin / qmax), 2: ..._LMA
+  std::tuple<std::vector<double>, int> chain_ik(size_t index, const std::vector<double>& q0, const Vec7& pose,
+                                                int kind, const std::vector<double>* qmin = nullptr,
+                                                const std::vector<double>* qmax = nullptr) const;
+  std::tuple<std::vector<double>, int> tree_ik_nr_jl(const std::vector<std::string>& endpoints,
+                                                     const std::vector<double>& q0, const std::vector<Vec7>& poses,
+                                                     const std::vector<double>& qmin,
+                                                     const std::vector<double>& qmax) const;
+
+ private:
+  std::vector<int> chain(size_t index) const;  // joint ids root -> link
+  std::vector<SE3> frames_at(const std::vector<double>& q_user) const;
+  SE3 tip(const std::vector<SE3>& oMi, size_t index) const;
+  std::vector<double> jacobian(const std::vector<SE3>& oMi, const SE3& T, const std::vector<int>& cols) const;
+  std::vector<std::string> user_joint_names_, user_link_names_;
+  std::map<std::string, int> user_idx_;
+  std::vector<int> pin_user_;  // pinocchio joint -> user slot, -1 if unnamed
+  std::shared_ptr<PinocchioModel> pin_;
+  std::string root_;
+};
+
 class FCLModel {
  public:
   FCLModel(const UrdfModel& urdf, bool verbose, bool convex);

@@ -10,9 +10,26 @@
 // damped least-squares step v = -J^T (J J^T + damp I)^-1 err.  Host only: the
 // IK is a caller of the collision path (planner.py:292-326), not part of it;
 // the results are floating-point (parity with pinocchio unpinned, tests check
-// the Jacobian against finite differences of the device FK and the IK
+// the Jacobian against finite differences of the oracle FK and the IK
 // against its own targets).
+//
+// KDLModel (python/pybind_kdl.hpp, src/kdl_model.cpp): the chain / tree IK
+// entry points with orocos KDL 1.5's solver semantics [ext, not under
+// /root/reference]: ChainIkSolverPos_NR (full Newton steps q += J^+ diff(f,
+// goal), maxiter 100, eps 1e-6), ..._NR_JL (the same, clamped to the limits
+// after each step), ChainIkSolverPos_LMA (Levenberg-Marquardt on the
+// L-weighted twist, L = (1, 1, 1, .01, .01, .01), eps 1e-5, maxiter 500,
+// eps_joints 1e-15, lambda schedule of KDL's implementation) and
+// TreeIkSolverPos_NR_JL (all endpoints' twists stacked, damped least
+// squares with lambda 1e-6, maxiter 1000, eps 1e-6).  Twists are KDL's: the
+// position error and the base-frame rotation vector of R_cur^T R_goal
+// (KDL::diff), Jacobians with the reference point at the tip.  Return codes
+// are KDL's (0 ok, -5 max iterations, -100 / -101 LMA's gradient /
+// increment too small).  The iteration paths are not KDL's bit for bit (its
+// SVD is not restated); answers are checked against their targets.
 #include <cmath>
+#include <iostream>
+#include <sstream>
 #include <tuple>
 
 #include "host.hpp"
@@ -148,6 +165,20 @@ SE3 pose_se3(const Vec7& pose) {  // (x, y, z, qw, qx, qy, qz) -> SE3
 }
 
 }  // namespace
+
+void PinocchioModel::print_frames() const {
+  std::ostringstream o;
+  const size_t nj = joints_.size();
+  o << "Joint dim " << nj << " " << nv_ << " " << nj << " " << nj << "\n";
+  o << "Joint Tangent dim " << nq_ << " " << nj << " " << nj << "\n";
+  o << "Joint Limit " << nq_ << " " << nq_ << "\n";
+  for (size_t i = 0; i < frames_.size(); ++i) {
+    const PinFrame& f = frames_[i];
+    const char* t = f.type == PinFrame::JOINT ? "JOINT" : f.type == PinFrame::FIXED_JOINT ? "FIXED_JOINT" : "BODY";
+    o << "Frame " << i << " " << f.name << " " << f.parent << " " << t << "\n";
+  }
+  std::cout << o.str() << std::flush;
+}
 
 std::vector<double> PinocchioModel::qpos_user2pin(const std::vector<double>& q) const {
   if ((int)q.size() != nv_) throw std::runtime_error("Qpos user2pinocchio failed");
@@ -386,6 +417,281 @@ PinocchioModel::IKResult PinocchioModel::ik_clik(size_t index, const Vec7& pose,
   }
   r.q = qpos_pin2user(q);
   return r;
+}
+
+
+// ------------------------------------------------------------------ KDL
+namespace {
+
+// KDL::diff(F_cur, F_goal): (p_goal - p_cur, R_cur * rotvec(R_cur^T R_goal))
+std::array<double, 6> kdl_diff(const SE3& cur, const SE3& goal) {
+  std::array<double, 6> t;
+  for (int k = 0; k < 3; ++k) t[k] = goal.p[k] - cur.p[k];
+  double Rr[9];
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j)
+      Rr[3 * i + j] = (cur.R[i] * goal.R[j] + cur.R[3 + i] * goal.R[3 + j]) + cur.R[6 + i] * goal.R[6 + j];
+  double w[3], th, ww[3];
+  log3(Rr, w, th);
+  matv(cur.R, w, ww);
+  for (int k = 0; k < 3; ++k) t[3 + k] = ww[k];
+  return t;
+}
+
+// solve A x = b for a symmetric positive definite m x m A (Cholesky, row-major)
+std::vector<double> chol_solve(std::vector<double> A, int m, std::vector<double> b) {
+  for (int j = 0; j < m; ++j) {
+    double d = A[(size_t)j * m + j];
+    for (int k = 0; k < j; ++k) d -= A[(size_t)j * m + k] * A[(size_t)j * m + k];
+    if (!(d > 0)) throw std::runtime_error("KDL IK: singular system");
+    const double l = std::sqrt(d);
+    A[(size_t)j * m + j] = l;
+    for (int i = j + 1; i < m; ++i) {
+      double t = A[(size_t)i * m + j];
+      for (int k = 0; k < j; ++k) t -= A[(size_t)i * m + k] * A[(size_t)j * m + k];
+      A[(size_t)i * m + j] = t / l;
+    }
+  }
+  for (int i = 0; i < m; ++i) {
+    double t = b[i];
+    for (int k = 0; k < i; ++k) t -= A[(size_t)i * m + k] * b[k];
+    b[i] = t / A[(size_t)i * m + i];
+  }
+  for (int i = m - 1; i >= 0; --i) {
+    double t = b[i];
+    for (int k = i + 1; k < m; ++k) t -= A[(size_t)k * m + i] * b[k];
+    b[i] = t / A[(size_t)i * m + i];
+  }
+  return b;
+}
+
+// (A^T A + lambda I) x = A^T b, A m x n row-major (Levenberg-Marquardt step)
+std::vector<double> damped_ls(const std::vector<double>& A, int m, int n, const std::vector<double>& b, double lambda) {
+  std::vector<double> N((size_t)n * n, 0.0), r(n, 0.0);
+  for (int i = 0; i < n; ++i) {
+    for (int j = 0; j < n; ++j) {
+      double s = 0.0;
+      for (int k = 0; k < m; ++k) s += A[(size_t)k * n + i] * A[(size_t)k * n + j];
+      N[(size_t)i * n + j] = s + (i == j ? lambda : 0.0);
+    }
+    for (int k = 0; k < m; ++k) r[i] += A[(size_t)k * n + i] * b[k];
+  }
+  return chol_solve(std::move(N), n, std::move(r));
+}
+
+// J^T (J J^T + l2 I)^-1 b, J m x n row-major: the minimum-norm step
+// (ChainIkSolverVel_pinv with l2 -> 0, TreeIkSolverVel_wdls with l2 = lambda^2)
+std::vector<double> min_norm_step(const std::vector<double>& J, int m, int n, const std::vector<double>& b, double l2) {
+  std::vector<double> G((size_t)m * m, 0.0);
+  for (int a = 0; a < m; ++a)
+    for (int c = 0; c < m; ++c) {
+      double s = 0.0;
+      for (int k = 0; k < n; ++k) s += J[(size_t)a * n + k] * J[(size_t)c * n + k];
+      G[(size_t)a * m + c] = s + (a == c ? l2 : 0.0);
+    }
+  const std::vector<double> z = chol_solve(std::move(G), m, b);
+  std::vector<double> x(n, 0.0);
+  for (int j = 0; j < n; ++j)
+    for (int a = 0; a < m; ++a) x[j] += J[(size_t)a * n + j] * z[a];
+  return x;
+}
+
+}  // namespace
+
+KDLModel::KDLModel(const std::string& urdf, const std::vector<std::string>& joint_names,
+                   const std::vector<std::string>& link_names, bool verbose)
+    : user_joint_names_(joint_names), user_link_names_(link_names) {
+  const UrdfModel m = parse_urdf_file(urdf);
+  root_ = m.root;
+  pin_ = std::make_shared<PinocchioModel>(m, Vec3{0, 0, -9.81}, verbose);
+  for (size_t i = 0; i < joint_names.size(); ++i) user_idx_[joint_names[i]] = (int)i;
+  // pinocchio joint -> user slot (by name); joints the user did not name stay at 0
+  const auto& J = pin_->joints();
+  pin_user_.assign(J.size(), -1);
+  for (size_t j = 1; j < J.size(); ++j) {
+    auto it = user_idx_.find(J[j].name);
+    if (it != user_idx_.end()) pin_user_[j] = it->second;
+  }
+}
+
+std::vector<int> KDLModel::chain(size_t index) const {
+  if (index >= user_link_names_.size()) throw std::runtime_error("link index out of bound");
+  const int f = pin_->body_frame(user_link_names_[index]);
+  if (f < 0) throw std::runtime_error("unknown link " + user_link_names_[index]);
+  std::vector<int> c;
+  for (int j = pin_->frames()[f].parent; j > 0; j = pin_->joints()[j].parent) c.push_back(j);
+  std::reverse(c.begin(), c.end());
+  for (int j : c)
+    if (pin_user_[j] < 0) throw std::out_of_range("joint " + pin_->joints()[j].name + " is not in joint_names");
+  return c;
+}
+
+std::vector<SE3> KDLModel::frames_at(const std::vector<double>& q_user) const {
+  const auto& J = pin_->joints();
+  std::vector<double> qpin(pin_->nq(), 0.0);
+  for (size_t j = 1; j < J.size(); ++j) {
+    if (pin_user_[j] < 0 || J[j].nq == 0) continue;
+    const double v = q_user.at(pin_user_[j]);
+    if (J[j].nq == 1) qpin[J[j].idx_q] = v;
+    else {
+      qpin[J[j].idx_q] = std::cos(v);
+      qpin[J[j].idx_q + 1] = std::sin(v);
+    }
+  }
+  return pin_->joint_frames(qpin);
+}
+
+SE3 KDLModel::tip(const std::vector<SE3>& oMi, size_t index) const {
+  const PinFrame& fr = pin_->frames()[pin_->body_frame(user_link_names_[index])];
+  return mpg::se3_mul(oMi[fr.parent], fr.placement);
+}
+
+// KDL's chain Jacobian: reference point at the tip, base-frame axes; columns
+// in `cols` order (joint ids)
+std::vector<double> KDLModel::jacobian(const std::vector<SE3>& oMi, const SE3& T, const std::vector<int>& cols) const {
+  const int n = (int)cols.size();
+  std::vector<double> Jm(6 * (size_t)n, 0.0);
+  for (int c = 0; c < n; ++c) {
+    const PinJoint& pj = pin_->joints()[cols[c]];
+    const Mot S = act(oMi[cols[c]], joint_subspace(pj));  // (v at the base origin, w)
+    double wxp[3];
+    cross3(S.w, T.p, wxp);  // velocity of the tip point: v + w x p
+    for (int k = 0; k < 3; ++k) {
+      Jm[(size_t)k * n + c] = S.v[k] + wxp[k];
+      Jm[(size_t)(3 + k) * n + c] = S.w[k];
+    }
+  }
+  return Jm;
+}
+
+std::tuple<std::vector<double>, int> KDLModel::chain_ik(size_t index, const std::vector<double>& q0, const Vec7& pose,
+                                                      int kind, const std::vector<double>* qmin,
+                                                      const std::vector<double>* qmax) const {
+  const std::vector<int> c = chain(index);
+  const SE3 goal = pose_se3(pose);
+  std::vector<double> q = q0;
+  const int n = (int)c.size();
+  auto err_of = [&](const std::vector<double>& qq) { return kdl_diff(tip(frames_at(qq), index), goal); };
+  if (kind != 2) {  // Newton-Raphson (NR / NR_JL)
+    for (int it = 0; it < 100; ++it) {
+      const std::vector<SE3> oMi = frames_at(q);
+      const auto e = kdl_diff(tip(oMi, index), goal);
+      bool zero = true;
+      for (double x : e) zero &= std::fabs(x) < 1e-6;  // KDL::Equal(twist, Zero, eps)
+      if (zero) return {q, 0};
+      const std::vector<double> dq =
+          min_norm_step(jacobian(oMi, tip(oMi, index), c), 6, n, std::vector<double>(e.begin(), e.end()), 1e-12);
+      for (int k = 0; k < n; ++k) {
+        double& v = q[pin_user_[c[k]]];
+        v += dq[k];
+        if (kind == 1) v = std::min(std::max(v, (*qmin)[pin_user_[c[k]]]), (*qmax)[pin_user_[c[k]]]);
+      }
+    }
+    return {q, -5};
+  }
+  // Levenberg-Marquardt (ChainIkSolverPos_LMA)
+  const double L[6] = {1, 1, 1, 0.01, 0.01, 0.01}, eps = 1e-5, eps_joints = 1e-15;
+  auto weighted = [&](const std::array<double, 6>& e) {
+    std::vector<double> w(6);
+    for (int k = 0; k < 6; ++k) w[k] = L[k] * e[k];
+    return w;
+  };
+  auto norm = [](const std::vector<double>& v) {
+    double s = 0.0;
+    for (double x : v) s += x * x;
+    return std::sqrt(s);
+  };
+  std::vector<double> dp = weighted(err_of(q));
+  double dpn = norm(dp);
+  if (dpn < eps) return {q, 0};
+  auto wjac = [&](const std::vector<double>& qq) {
+    const std::vector<SE3> oMi = frames_at(qq);
+    std::vector<double> Jm = jacobian(oMi, tip(oMi, index), c);
+    for (int r = 0; r < 6; ++r)
+      for (int k = 0; k < n; ++k) Jm[(size_t)r * n + k] *= L[r];
+    return Jm;
+  };
+  std::vector<double> Jw = wjac(q);
+  double lambda = 10.0, v = 2.0;
+  for (int it = 0; it < 500; ++it) {
+    const std::vector<double> diffq = damped_ls(Jw, 6, n, dp, lambda);
+    std::vector<double> grad(n, 0.0);
+    for (int k = 0; k < n; ++k)
+      for (int r = 0; r < 6; ++r) grad[k] += Jw[(size_t)r * n + k] * dp[r];
+    if (norm(diffq) < eps_joints) return {q, -101};
+    if (norm(grad) * norm(grad) < eps_joints * eps_joints) return {q, -100};
+    std::vector<double> qn = q;
+    for (int k = 0; k < n; ++k) qn[pin_user_[c[k]]] += diffq[k];
+    const std::vector<double> dpnew = weighted(err_of(qn));
+    const double dpnn = norm(dpnew);
+    double den = 0.0;
+    for (int k = 0; k < n; ++k) den += diffq[k] * (lambda * diffq[k] + grad[k]);
+    const double rho = (dpn * dpn - dpnn * dpnn) / den;
+    if (rho > 0) {
+      q = qn;
+      dp = dpnew;
+      dpn = dpnn;
+      if (dpn < eps) return {q, 0};
+      Jw = wjac(q);
+      const double t = 2 * rho - 1;
+      lambda = lambda * std::max(1 / 3.0, 1 - t * t * t);
+      v = 2;
+    } else {
+      lambda = lambda * v;
+      v = 2 * v;
+    }
+  }
+  return {q, -5};
+}
+
+std::tuple<std::vector<double>, int> KDLModel::tree_ik_nr_jl(const std::vector<std::string>& endpoints,
+                                                           const std::vector<double>& q0,
+                                                           const std::vector<Vec7>& poses,
+                                                           const std::vector<double>& qmin,
+                                                           const std::vector<double>& qmax) const {
+  if (endpoints.size() != poses.size()) throw std::invalid_argument("endpoints and goal_poses differ in length");
+  // the tree's joints: every named pinocchio joint with one dof
+  std::vector<int> cols;
+  for (size_t j = 1; j < pin_->joints().size(); ++j)
+    if (pin_user_[j] >= 0 && pin_->joints()[j].nv == 1) cols.push_back((int)j);
+  std::vector<int> ends;
+  for (auto& e : endpoints) {
+    auto it = std::find(user_link_names_.begin(), user_link_names_.end(), e);
+    if (it == user_link_names_.end()) throw std::out_of_range("unknown endpoint " + e);
+    ends.push_back((int)(it - user_link_names_.begin()));
+  }
+  std::vector<SE3> goals;
+  for (auto& p : poses) goals.push_back(pose_se3(p));
+  const int n = (int)cols.size(), m = 6 * (int)ends.size();
+  std::vector<double> q = q0;
+  for (int it = 0; it < 1000; ++it) {
+    const std::vector<SE3> oMi = frames_at(q);
+    std::vector<double> Jall((size_t)m * n, 0.0), e(m, 0.0);
+    double en2 = 0.0;
+    for (size_t k = 0; k < ends.size(); ++k) {
+      const SE3 T = tip(oMi, ends[k]);
+      const auto d = kdl_diff(T, goals[k]);
+      for (int r = 0; r < 6; ++r) {
+        e[6 * k + r] = d[r];
+        en2 += d[r] * d[r];
+      }
+      // only the joints supporting this endpoint move it
+      const std::vector<int> sup = chain(ends[k]);
+      const std::vector<double> Jk = jacobian(oMi, T, cols);
+      for (int c = 0; c < n; ++c) {
+        if (std::find(sup.begin(), sup.end(), cols[c]) == sup.end()) continue;
+        for (int r = 0; r < 6; ++r) Jall[(size_t)(6 * k + r) * n + c] = Jk[(size_t)r * n + c];
+      }
+    }
+    if (std::sqrt(en2) < 1e-6) return {q, 0};
+    // TreeIkSolverVel_wdls, lambda 1e-6: J^T (J J^T + lambda^2 I)^-1 e
+    const std::vector<double> dq = min_norm_step(Jall, m, n, e, 1e-12);
+    for (int c = 0; c < n; ++c) {
+      double& v = q[pin_user_[cols[c]]];
+      v = std::min(std::max(v + dq[c], qmin[pin_user_[cols[c]]]), qmax[pin_user_[cols[c]]]);
+    }
+  }
+  return {q, -5};
 }
 
 }  // namespace mpgh

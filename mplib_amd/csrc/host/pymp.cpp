@@ -686,6 +686,7 @@ PYBIND11_MODULE(pymp, m_all) {
            },
            py::arg("index"))
       .def("get_random_configuration", &PinocchioModel::get_random_configuration)
+      .def("print_frames", &PinocchioModel::print_frames)
       // Jacobians and CLIK IK (python/pybind_pinocchio.hpp:47-58), host side (kinjac.cpp)
       .def("compute_full_jacobian", &PinocchioModel::compute_full_jacobian, py::arg("qpos"))
       .def("get_link_jacobian",
@@ -727,6 +728,42 @@ PYBIND11_MODULE(pymp, m_all) {
       .def("get_joint_limits", &PinocchioModel::get_joint_limits, py::arg("user") = true)
       .def("get_chain_joint_name", &PinocchioModel::get_chain_joint_name, py::arg("end_effector"))
       .def("get_chain_joint_index", &PinocchioModel::get_chain_joint_index, py::arg("end_effector"));
+
+  // ------------------------------------------------------------------ kdl
+  auto mk = m_all.def_submodule("kdl");
+  auto kdl_ret = [](const std::tuple<std::vector<double>, int>& r) {
+    const auto& q = std::get<0>(r);
+    return py::make_tuple(vec(q.data(), (int)q.size()), std::get<1>(r));
+  };
+  py::class_<KDLModel, std::shared_ptr<KDLModel>>(mk, "KDLModel")
+      .def(py::init<const std::string&, const std::vector<std::string>&, const std::vector<std::string>&, bool>(),
+           py::arg("urdf_filename"), py::arg("joint_names"), py::arg("link_names"), py::arg("verbose"))
+      .def("get_tree_root_name", &KDLModel::get_tree_root_name)
+      .def("chain_IK_LMA",
+           [=](const KDLModel& k, size_t i, const std::vector<double>& q0, const std::vector<double>& pose) {
+             return kdl_ret(k.chain_ik(i, q0, vec7_arg(pose), 2));
+           },
+           py::arg("index"), py::arg("q_init"), py::arg("goal_pose"))
+      .def("chain_IK_NR",
+           [=](const KDLModel& k, size_t i, const std::vector<double>& q0, const std::vector<double>& pose) {
+             return kdl_ret(k.chain_ik(i, q0, vec7_arg(pose), 0));
+           },
+           py::arg("index"), py::arg("q_init"), py::arg("goal_pose"))
+      .def("chain_IK_NR_JL",
+           [=](const KDLModel& k, size_t i, const std::vector<double>& q0, const std::vector<double>& pose,
+               const std::vector<double>& qmin, const std::vector<double>& qmax) {
+             return kdl_ret(k.chain_ik(i, q0, vec7_arg(pose), 1, &qmin, &qmax));
+           },
+           py::arg("index"), py::arg("q_init"), py::arg("goal_pose"), py::arg("q_min"), py::arg("q_max"))
+      .def("tree_IK_NR_JL",
+           [=](const KDLModel& k, const std::vector<std::string>& ends, const std::vector<double>& q0,
+               const std::vector<std::vector<double>>& poses, const std::vector<double>& qmin,
+               const std::vector<double>& qmax) {
+             std::vector<Vec7> p;
+             for (auto& v : poses) p.push_back(vec7_arg(v));
+             return kdl_ret(k.tree_ik_nr_jl(ends, q0, p, qmin, qmax));
+           },
+           py::arg("endpoints"), py::arg("q_init"), py::arg("goal_poses"), py::arg("q_min"), py::arg("q_max"));
 
   // ---------------------------------------------------------- articulation
   auto ma = m_all.def_submodule("articulation");

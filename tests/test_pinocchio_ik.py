@@ -108,3 +108,65 @@ def test_ik_mask_freezes_joints(models):
     assert q[0] == q0[0]
     with pytest.raises(RuntimeError, match="out of bound"):
         pin.compute_IK_CLIK(99, list(p) + [w, x, y, z], _full(q0))
+
+
+def test_print_frames(models, capfd):
+    pin, _ = models
+    pin.print_frames()
+    out = capfd.readouterr().out.splitlines()
+    assert out[0].startswith("Joint dim ") and any(" panda_hand " in l for l in out if l.startswith("Frame "))
+
+
+# ------------------------------------------------------------------ KDL
+def test_kdl_model_chain_and_tree_ik(models):
+    """KDLModel (python/pybind_kdl.hpp): the tree root, the chain solvers NR /
+    NR_JL / LMA from a perturbed start reach the FK target (return code 0),
+    NR_JL stays inside its limits, and the tree solver meets two endpoints
+    at once.  orocos KDL is absent here: its solver semantics are restated
+    (kinjac.cpp), the answers are checked against their targets."""
+    import os
+    from oracle import model as M
+    from mplib_amd import pymp, scenes
+    _, ow = models
+    joints = ["panda_joint%d" % i for i in range(1, 8)] + ["panda_finger_joint1", "panda_finger_joint2"]
+    links = ["panda_link%d" % i for i in range(8)] + ["panda_hand", "panda_leftfinger", "panda_rightfinger"]
+    kdl = pymp.kdl.KDLModel(os.path.join(scenes.PANDA_DIR, "panda.urdf"), joints, links, False)
+    assert kdl.get_tree_root_name() == "panda_link0"
+    rng = np.random.default_rng(12)
+    lim = ow.art.joint_limits()[:7]
+    lo = np.array(list(lim[:, 0]) + [0.0, 0.0])
+    hi = np.array(list(lim[:, 1]) + [0.04, 0.04])
+    solved = {"nr": 0, "jl": 0, "lma": 0}
+    for _ in range(5):
+        q_goal = rng.uniform(lim[:, 0] * 0.8, lim[:, 1] * 0.8)
+        R, p = _hand_pose(ow, q_goal)
+        w, x, y, z = M.mat_to_quat(list(R.reshape(-1)))
+        pose = list(p) + [w, x, y, z]
+        q0 = np.array(_full(np.clip(q_goal + rng.normal(scale=0.15, size=7), lim[:, 0], lim[:, 1])))
+        for name, (q, rc) in (("nr", kdl.chain_IK_NR(HAND, q0, pose)),
+                              ("jl", kdl.chain_IK_NR_JL(HAND, q0, pose, lo, hi)),
+                              ("lma", kdl.chain_IK_LMA(HAND, q0, pose))):
+            assert q.shape == (9,)
+            assert (q[7:] == q0[7:]).all()  # joints off the chain keep their values
+            if name == "jl":
+                assert (q >= lo - 1e-12).all() and (q <= hi + 1e-12).all()
+            if rc != 0:
+                continue
+            solved[name] += 1
+            R2, p2 = _hand_pose(ow, q[:7])
+            assert np.linalg.norm(p2 - p) < 1e-4 and np.abs(R2 - R).max() < 1e-3, name
+    assert min(solved.values()) >= 3, solved
+    # two endpoints at once: the hand and link 4 of one configuration
+    q_goal = np.array([0.2, -0.3, 0.1, -2.1, 0.2, 1.9, 0.4])
+    _, objT = ow.fk_batch(q_goal.reshape(1, 7))
+    poses = []
+    for k in (4, HAND):
+        T = objT[0, k]
+        w, x, y, z = M.mat_to_quat(list(T[:9]))
+        poses.append(list(T[9:]) + [w, x, y, z])
+    q0 = np.array(_full(q_goal + 0.05))
+    q, rc = kdl.tree_IK_NR_JL(["panda_link4", "panda_hand"], q0, poses, lo, hi)
+    assert rc == 0
+    _, objT2 = ow.fk_batch(q[:7].reshape(1, 7))
+    for k in (4, HAND):
+        assert np.linalg.norm(objT2[0, k, 9:] - objT[0, k, 9:]) < 1e-4
